@@ -1,0 +1,654 @@
+/* oracle/gmapdp_oracle.c -- TEST INFRASTRUCTURE ONLY (see gmapdp_oracle.h).
+ *
+ * Plain-C restatement of the reference's nosimd Dynprog_* path.  Every
+ * function names the reference code it restates (paths relative to
+ * /root/reference/src).  Checked against the reference's own objects by
+ * tests/test_oracle_vs_ref.py and against tests/golden/ vectors.
+ */
+#include <ctype.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "gmapdp_oracle.h"
+
+/* ---- constants (dynprog.h:44-119, dynprog.c:104, scores.h, comp.h) ---- */
+enum { HIGHQ = 0, MEDQ = 1, LOWQ = 2, ENDQ = 3 };
+#define FULLMATCH 3
+#define HALFMATCH 1
+#define AMBIGUOUS 3
+#define MISMATCH_HIGHQ -3
+#define MISMATCH_MEDQ -2
+#define MISMATCH_LOWQ -1
+#define MISMATCH_ENDQ -5
+#define DEFECT_HIGHQ 0.003
+#define DEFECT_MEDQ 0.014
+#define SINGLE_OPEN_HIGHQ -8
+#define SINGLE_OPEN_MEDQ -7
+#define SINGLE_OPEN_LOWQ -6
+#define SINGLE_EXTEND_HIGHQ -3
+#define SINGLE_EXTEND_MEDQ -2
+#define SINGLE_EXTEND_LOWQ -1
+#define NEG_INFINITY_8 (-128)
+#define NEG_INFINITY_32 (-32768)
+#define VERT -2
+#define HORIZ -1
+#define DIAG 0
+#define MATCH 1
+#define MISMATCH -3
+#define QOPEN -3
+#define QINDEL -1
+#define TOPEN -3
+#define TINDEL -1
+#define DYNPROG_MATCH_COMP '*'
+#define AMBIGUOUS_COMP ':'
+#define MISMATCH_COMP ' '
+#define INDEL_COMP '-'
+#define MICROINTRON_LENGTH 9 /* pairpool.c: genome skips >= this become a gap holder */
+#define LAZY_INDEL 1         /* dynprog.c:1791 */
+
+/* Mode_T (mode.h:5) */
+enum { STANDARD, CMET_STRANDED, CMET_NONSTRANDED, ATOI_STRANDED, ATOI_NONSTRANDED, TTOC_STRANDED, TTOC_NONSTRANDED };
+
+/* complement.h:31 COMPLEMENT_LC (IUPAC complement, case preserving) */
+static const char complCode[129] =
+  "???????????????????????????????? ??#$%&')(*+,-./0123456789:;>=<??TVGHEFCDIJMLKNOPQYSAABWXRZ]?[^_`tvghefcdijmlknopqysaabwxrz}|{~?";
+
+static short pairdistance[4][128][128];
+static unsigned char consistent[3][128][128];
+static int use8p_size[4];
+static int g_mode;
+static int g_user_open, g_user_extend, g_user_dynprog_p;
+
+static const char *g_genome = NULL;
+static unsigned int g_genomelength = 0;
+
+/* ---------------------------------------------------------------------------
+ * Score tables: restates Dynprog_init / permute_cases / permute_cases_oneway
+ * (dynprog.c:903-1197).  Note the reference's loop bounds ('z' exclusive for
+ * the second character, 'Z' exclusive for the identity loop) are kept.
+ * ------------------------------------------------------------------------- */
+static int
+stranded_mode (int mode) {
+  return mode == STANDARD || mode == CMET_STRANDED || mode == ATOI_STRANDED || mode == TTOC_STRANDED;
+}
+
+static void
+set_both (int a, int b, short score, int mode) {
+  int la = tolower(a), lb = tolower(b), t;
+  int pairs[4][2] = {{la, lb}, {la, b}, {a, lb}, {a, b}};
+  int k;
+  for (k = 0; k < 4; k++) {
+    if (stranded_mode(mode)) {
+      consistent[0][pairs[k][0]][pairs[k][1]] = 1;
+    } else {
+      consistent[1][pairs[k][0]][pairs[k][1]] = 1;
+      consistent[2][pairs[k][0]][pairs[k][1]] = 1;
+    }
+  }
+  for (k = 0; k < 4; k++) {
+    if (stranded_mode(mode)) {
+      consistent[0][pairs[k][1]][pairs[k][0]] = 1;
+    } else {
+      consistent[1][pairs[k][1]][pairs[k][0]] = 1;
+      consistent[2][pairs[k][1]][pairs[k][0]] = 1;
+    }
+  }
+  for (t = 0; t < 4; t++) {
+    for (k = 0; k < 4; k++) pairdistance[t][pairs[k][0]][pairs[k][1]] = score;
+    for (k = 0; k < 4; k++) pairdistance[t][pairs[k][1]][pairs[k][0]] = score;
+  }
+}
+
+static void
+set_oneway (int a, int b, short score, int genestrand) {
+  int la = tolower(a), lb = tolower(b), t;
+  consistent[genestrand][la][lb] = 1;
+  consistent[genestrand][la][b] = 1;
+  consistent[genestrand][a][lb] = 1;
+  consistent[genestrand][a][b] = 1;
+  for (t = 0; t < 4; t++) {
+    pairdistance[t][la][lb] = score;
+    pairdistance[t][la][b] = score;
+    pairdistance[t][a][lb] = score;
+    pairdistance[t][a][b] = score;
+  }
+}
+
+int
+orc_init (int mode, int user_open, int user_extend, int user_dynprog_p) {
+  int c1, c2;
+  static const struct { char a, b; short s; } exc[] = {
+    {'U','T',FULLMATCH},
+    {'R','A',HALFMATCH},{'R','G',HALFMATCH},{'Y','T',HALFMATCH},{'Y','C',HALFMATCH},
+    {'W','A',HALFMATCH},{'W','T',HALFMATCH},{'S','G',HALFMATCH},{'S','C',HALFMATCH},
+    {'M','A',HALFMATCH},{'M','C',HALFMATCH},{'K','G',HALFMATCH},{'K','T',HALFMATCH},
+    {'H','A',AMBIGUOUS},{'H','T',AMBIGUOUS},{'H','C',AMBIGUOUS},
+    {'B','G',AMBIGUOUS},{'B','C',AMBIGUOUS},{'B','T',AMBIGUOUS},
+    {'V','G',AMBIGUOUS},{'V','A',AMBIGUOUS},{'V','C',AMBIGUOUS},
+    {'D','G',AMBIGUOUS},{'D','A',AMBIGUOUS},{'D','T',AMBIGUOUS},
+    {'N','T',AMBIGUOUS},{'N','C',AMBIGUOUS},{'N','A',AMBIGUOUS},{'N','G',AMBIGUOUS},
+    {'X','T',AMBIGUOUS},{'X','C',AMBIGUOUS},{'X','A',AMBIGUOUS},{'X','G',AMBIGUOUS},
+    {'N','N',AMBIGUOUS},{'X','X',AMBIGUOUS},
+  };
+  size_t k;
+
+  memset(pairdistance, 0, sizeof(pairdistance));
+  memset(consistent, 0, sizeof(consistent));
+  g_mode = mode;
+  g_user_open = user_open;
+  g_user_extend = user_extend;
+  g_user_dynprog_p = user_dynprog_p;
+
+  /* dynprog.c:1022-1025: NEG_INFINITY_8 / mismatch - 1 (C integer division) */
+  use8p_size[HIGHQ] = NEG_INFINITY_8 / MISMATCH_HIGHQ - 1;
+  use8p_size[MEDQ] = NEG_INFINITY_8 / MISMATCH_MEDQ - 1;
+  use8p_size[LOWQ] = NEG_INFINITY_8 / MISMATCH_LOWQ - 1;
+  use8p_size[ENDQ] = NEG_INFINITY_8 / MISMATCH_ENDQ - 1;
+
+  for (c1 = 'A'; c1 <= 'z'; c1++) {
+    for (c2 = 'A'; c2 < 'z'; c2++) {
+      pairdistance[HIGHQ][c1][c2] = MISMATCH_HIGHQ;
+      pairdistance[MEDQ][c1][c2] = MISMATCH_MEDQ;
+      pairdistance[LOWQ][c1][c2] = MISMATCH_LOWQ;
+      pairdistance[ENDQ][c1][c2] = MISMATCH_ENDQ;
+    }
+  }
+  for (c1 = 'A'; c1 < 'Z'; c1++) set_both(c1, c1, FULLMATCH, mode);
+  for (k = 0; k < sizeof(exc) / sizeof(exc[0]); k++) set_both(exc[k].a, exc[k].b, exc[k].s, mode);
+
+  switch (mode) {
+  case STANDARD: break;
+  case CMET_STRANDED: set_oneway('T', 'C', FULLMATCH, 0); break;
+  case CMET_NONSTRANDED: set_oneway('T', 'C', FULLMATCH, 1); set_oneway('A', 'G', FULLMATCH, 2); break;
+  case ATOI_STRANDED: set_oneway('G', 'A', FULLMATCH, 0); break;
+  case ATOI_NONSTRANDED: set_oneway('G', 'A', FULLMATCH, 1); set_oneway('C', 'T', FULLMATCH, 2); break;
+  case TTOC_STRANDED: set_oneway('C', 'T', FULLMATCH, 0); break;
+  case TTOC_NONSTRANDED: set_oneway('C', 'T', FULLMATCH, 1); set_oneway('G', 'A', FULLMATCH, 2); break;
+  default: return -1;
+  }
+  return 0;
+}
+
+int
+orc_pairdistance (int mismatchtype, short *out) {
+  memcpy(out, pairdistance[mismatchtype], sizeof(pairdistance[0]));
+  return 0;
+}
+
+int
+orc_consistent (int genestrand, unsigned char *out) {
+  memcpy(out, consistent[genestrand], sizeof(consistent[0]));
+  return 0;
+}
+
+int
+orc_set_genome (const char *genome, unsigned int length) {
+  g_genome = genome;
+  g_genomelength = length;
+  return 0;
+}
+
+/* ---------------------------------------------------------------------------
+ * Genome access: get_genomic_nt (dynprog_single.c:116, pairpool.c) and
+ * Genome_get_segment_right/left (genome.c:11023/11079).  Univcoord_T is the
+ * 32-bit gmap type, so positions wrap exactly as in the reference.
+ * ------------------------------------------------------------------------- */
+static char
+get_genomic_nt (char *g_alt, int genomicpos, unsigned int chroffset, unsigned int chrhigh, int watsonp) {
+  unsigned int pos;
+  char c;
+  if (watsonp) {
+    pos = chroffset + (unsigned int) genomicpos;
+    if (pos < chroffset || pos >= chrhigh) { *g_alt = '*'; return '*'; }
+    c = g_genome[pos];
+    *g_alt = c;
+    return c;
+  } else {
+    pos = chrhigh - (unsigned int) genomicpos;
+    if (pos < chroffset || pos >= chrhigh) { *g_alt = '*'; return '*'; }
+    c = g_genome[pos];
+    *g_alt = complCode[(int) c];
+    return complCode[(int) c];
+  }
+}
+
+static void
+complement_inplace (char *s, unsigned int length) {
+  unsigned int i, j;
+  char t;
+  if (length == 0) return;
+  for (i = 0, j = length - 1; i < length / 2; i++, j--) {
+    t = complCode[(int) s[i]];
+    s[i] = complCode[(int) s[j]];
+    s[j] = t;
+  }
+  if (i == j) s[i] = complCode[(int) s[i]];
+}
+
+int
+orc_get_segment (int rightp, unsigned int pos, int length_in, unsigned int chrbound, int revcomp,
+                 char *segment, char *segmentalt) {
+  unsigned int length = (unsigned int) length_in, oob, i;
+  if (length == 0) { segment[0] = segmentalt[0] = '\0'; return 0; }
+  if (rightp) {
+    unsigned int left = pos, chrhigh = chrbound;
+    if (left >= chrhigh) {
+      for (i = 0; i < length; i++) segment[i] = segmentalt[i] = '*';
+      segment[length] = segmentalt[length] = '\0';
+      return 0;
+    } else if (left + length >= chrhigh) {
+      oob = left + length - chrhigh;
+      for (i = length - 1; i + oob >= length; i--) segment[i] = '*';
+    } else {
+      oob = 0;
+    }
+    for (i = 0; i < length - oob; i++) segment[i] = g_genome[left + i];
+  } else {
+    unsigned int right = pos, chroffset = chrbound;
+    if (right < chroffset) {
+      for (i = 0; i < length; i++) segment[i] = segmentalt[i] = '*';
+      segment[length] = segmentalt[length] = '\0';
+      return 0;
+    } else if (right < chroffset + length) {
+      oob = chroffset + length - right;
+      for (i = 0; i < oob; i++) segment[i] = '*';
+    } else {
+      oob = 0;
+    }
+    for (i = 0; i < length - oob; i++) segment[oob + i] = g_genome[right - length + oob + i];
+  }
+  segment[length] = '\0';
+  if (revcomp) complement_inplace(segment, length);
+  memcpy(segmentalt, segment, length);
+  segmentalt[length] = '\0';
+  return 0;
+}
+
+/* ---------------------------------------------------------------------------
+ * Pair emission: Pairpool_push / _push_gapholder / _add_queryskip /
+ * _add_genomeskip (pairpool.c:180,375,981,1068).  Pairs are recorded in PUSH
+ * order; the reference list is the reverse of push order (each push
+ * prepends).
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  OrcPair *buf;
+  int n, cap;
+} PairSink;
+
+static void
+sink_push (PairSink *s, int querypos, int genomepos, char cdna, char comp, char genome, char genomealt,
+           int dynprogindex) {
+  OrcPair *p;
+  if (querypos < 0 || genomepos < 0) return; /* pairpool.c:188-190 */
+  if (s->n < s->cap) {
+    p = &s->buf[s->n];
+    p->querypos = querypos; p->genomepos = genomepos; p->queryjump = 0; p->genomejump = 0;
+    p->dynprogindex = dynprogindex; p->cdna = cdna; p->comp = comp; p->genome = genome;
+    p->genomealt = genomealt; p->gapp = 0;
+  }
+  s->n++;
+}
+
+static void
+sink_gapholder (PairSink *s, int queryjump, int genomejump) {
+  OrcPair *p;
+  if (s->n < s->cap) {
+    p = &s->buf[s->n];
+    p->querypos = -1; p->genomepos = -1; p->queryjump = queryjump; p->genomejump = genomejump;
+    p->dynprogindex = 0; p->cdna = ' '; p->comp = ' '; p->genome = ' '; p->genomealt = ' '; p->gapp = 1;
+  }
+  s->n++;
+}
+
+static void
+add_queryskip (PairSink *s, int r, int c, int dist, const char *qseq, int queryoffset, int genomeoffset,
+               int revp, int dpi) {
+  int j, querycoord = r - 1, genomecoord = c - 1, step;
+  if (revp) { querycoord = -querycoord; genomecoord = -genomecoord; step = +1; } else { step = -1; }
+  for (j = 0; j < dist; j++) {
+    sink_push(s, queryoffset + querycoord, genomeoffset + genomecoord, qseq[querycoord], INDEL_COMP, ' ', ' ', dpi);
+    querycoord += step;
+  }
+}
+
+static int
+add_genomeskip (PairSink *s, int r, int c, int dist, int queryoffset, int genomeoffset, int revp,
+                unsigned int chroffset, unsigned int chrhigh, int watsonp, int dpi) {
+  int j, querycoord = r - 1, left = c - dist, right = c - 1, t, genomecoord, step;
+  char c2, c2_alt;
+  if (revp) { querycoord = -querycoord; t = left; left = -right; right = -t; step = +1; } else { step = -1; }
+  if (dist >= MICROINTRON_LENGTH) {
+    sink_gapholder(s, 0, dist);
+    return 0;
+  }
+  genomecoord = revp ? left : right;
+  for (j = 0; j < dist; j++) {
+    c2 = get_genomic_nt(&c2_alt, genomeoffset + genomecoord, chroffset, chrhigh, watsonp);
+    sink_push(s, queryoffset + querycoord, genomeoffset + genomecoord, ' ', INDEL_COMP, c2, c2_alt, dpi);
+    genomecoord += step;
+  }
+  return 1;
+}
+
+/* ---------------------------------------------------------------------------
+ * Dynprog_standard (dynprog.c:1268-1786): banded affine-gap fill, column-major
+ * over genome position c, rows r in [c-uband, c+lband].  The three direction
+ * planes start cleared to DIAG (Directions32_alloc, dynprog.c:488-501).
+ * ------------------------------------------------------------------------- */
+#define IDX(c, r) ((size_t) (c) * (size_t) (rlength + 1) + (size_t) (r))
+
+static inline int
+prefer (int a, int b, int late) { return late ? (a >= b) : (a > b); }
+
+int
+orc_standard_fill (const char *rsequence, const char *gsequence, const char *gsequence_alt,
+                   int rlength, int glength, int mismatchtype, int open, int extend,
+                   int lband, int uband, int jump_late_p, int revp, int saturation,
+                   int upperp, int lowerp, int *matrix, signed char *dirs) {
+  size_t plane = (size_t) (glength + 1) * (size_t) (rlength + 1);
+  signed char *dnogap = dirs, *dE = dirs + plane, *dF = dirs + 2 * plane;
+  int *r_gap, *nogap;
+  int penalty, c_gap, last_nogap, prev_nogap, first_nogap = 0, score, pairscore;
+  int r, c, rlo, rhigh, na1, na2, na2_alt;
+  short (*pd)[128] = pairdistance[mismatchtype];
+
+  memset(matrix, 0, plane * sizeof(int));
+  memset(dirs, DIAG, 3 * plane);
+
+  /* row 0 and column 0 (INFINITE_INITIAL_GAP_PENALTY branch) */
+  penalty = open;
+  for (c = 1; c <= uband && c <= glength; c++) {
+    penalty += extend;
+    matrix[IDX(c, 0)] = penalty;
+    dE[IDX(c, 0)] = HORIZ;
+    dnogap[IDX(c, 0)] = HORIZ;
+  }
+  penalty = open;
+  for (r = 1; r <= lband && r <= rlength; r++) {
+    penalty += extend;
+    matrix[IDX(0, r)] = penalty;
+    dF[IDX(0, r)] = VERT;
+    dnogap[IDX(0, r)] = VERT;
+  }
+
+  r_gap = (int *) malloc((rlength + 1) * sizeof(int));
+  nogap = (int *) malloc((rlength + 1) * sizeof(int));
+  nogap[0] = 0;
+  penalty = open;
+  for (r = 1; r <= lband && r <= rlength; r++) {
+    penalty += extend;
+    r_gap[r] = NEG_INFINITY_32;
+    nogap[r] = penalty;
+  }
+  for (; r <= rlength; r++) {
+    r_gap[r] = NEG_INFINITY_32;
+    nogap[r] = NEG_INFINITY_32;
+  }
+
+  penalty = open + extend;
+  for (c = 1; c <= glength; c++) {
+    na2 = (unsigned char) (revp ? gsequence[1 - c] : gsequence[c - 1]);
+    na2_alt = (unsigned char) (revp ? gsequence_alt[1 - c] : gsequence_alt[c - 1]);
+
+    c_gap = NEG_INFINITY_32;
+    if (c == 1) {
+      rlo = 1;
+      prev_nogap = 0;
+      last_nogap = NEG_INFINITY_32 - open + 1;
+    } else if ((rlo = c - uband) < 1) {
+      rlo = 1;
+      prev_nogap = penalty;
+      penalty += extend;
+      last_nogap = penalty;
+    } else if (rlo == 1) {
+      prev_nogap = penalty;
+      last_nogap = NEG_INFINITY_32;
+    } else {
+      prev_nogap = first_nogap;
+      last_nogap = NEG_INFINITY_32;
+    }
+    if ((rhigh = c + lband) > rlength) rhigh = rlength;
+
+    for (r = rlo; r <= rhigh; r++) {
+      na1 = (unsigned char) (revp ? rsequence[1 - r] : rsequence[r - 1]);
+
+      /* F: vertical gap (query skip), chained down the column */
+      score = last_nogap + open;
+      if (lowerp && prefer(c_gap, score, jump_late_p)) {
+        c_gap += extend;
+        dF[IDX(c, r)] = VERT;
+      } else {
+        c_gap = score + extend;
+      }
+
+      /* E: horizontal gap (genome skip), chained along the row */
+      score = nogap[r] + open;
+      if (upperp && prefer(r_gap[r], score, jump_late_p)) {
+        r_gap[r] += extend;
+        dE[IDX(c, r)] = HORIZ;
+      } else {
+        r_gap[r] = score + extend;
+      }
+
+      /* H */
+      pairscore = pd[na1][na2];
+      if ((score = pd[na1][na2_alt]) > pairscore) pairscore = score;
+      last_nogap = prev_nogap + pairscore;
+      if (upperp && prefer(r_gap[r], last_nogap, jump_late_p)) {
+        last_nogap = r_gap[r];
+        dnogap[IDX(c, r)] = HORIZ;
+      }
+      if (lowerp && prefer(c_gap, last_nogap, jump_late_p)) {
+        last_nogap = c_gap;
+        dnogap[IDX(c, r)] = VERT;
+      }
+
+      prev_nogap = nogap[r];
+      matrix[IDX(c, r)] = nogap[r] = (last_nogap < saturation) ? saturation : last_nogap;
+      if (r == rlo) first_nogap = last_nogap;
+    }
+  }
+
+  free(r_gap);
+  free(nogap);
+  return 0;
+}
+
+/* ---------------------------------------------------------------------------
+ * Dynprog_traceback_std (dynprog.c:1796-1948)
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  int score, nmatches, nmismatches, nopens, nindels;
+} Tally;
+
+static void
+traceback_std (PairSink *s, Tally *t, const signed char *dirs, int rlength, int glength, int r, int c,
+               const char *rsequence, const char *rsequenceuc, const char *gsequence,
+               const char *gsequence_alt, int queryoffset, int genomeoffset, int revp,
+               unsigned int chroffset, unsigned int chrhigh, int watsonp, int genestrand, int dpi) {
+  size_t plane = (size_t) (glength + 1) * (size_t) (rlength + 1);
+  const signed char *dnogap = dirs, *dE = dirs + plane, *dF = dirs + 2 * plane;
+  int dist, querycoord, genomecoord;
+  signed char dir;
+  char c1, c1_uc, c2, c2_alt;
+
+  while (r > 0 && c > 0) {
+    if ((dir = dnogap[IDX(c, r)]) == HORIZ) {
+      dist = 1;
+      while (c > 0 && dE[IDX(c--, r)] != DIAG) dist++;
+      if (add_genomeskip(s, r, c + dist, dist, queryoffset, genomeoffset, revp, chroffset, chrhigh,
+                         watsonp, dpi)) {
+        t->score += TOPEN + dist * TINDEL;
+        t->nopens += 1;
+        t->nindels += dist;
+      }
+    } else if (dir == VERT) {
+      dist = 1;
+      while (r > 0 && dF[IDX(c, r--)] != DIAG) dist++;
+      add_queryskip(s, r + dist, c, dist, rsequence, queryoffset, genomeoffset, revp, dpi);
+      t->score += QOPEN + dist * QINDEL;
+      t->nopens += 1;
+      t->nindels += dist;
+    } else {
+      querycoord = r - 1;
+      genomecoord = c - 1;
+      if (revp) { querycoord = -querycoord; genomecoord = -genomecoord; }
+      c1 = rsequence[querycoord];
+      c1_uc = rsequenceuc[querycoord];
+      c2 = gsequence[genomecoord];
+      c2_alt = gsequence_alt[genomecoord];
+      if (c2 == '*') {
+        /* not pushed past the end of the chromosome */
+      } else if (c1_uc == c2 || c1_uc == c2_alt) {
+        t->score += MATCH; t->nmatches += 1;
+        sink_push(s, queryoffset + querycoord, genomeoffset + genomecoord, c1, DYNPROG_MATCH_COMP, c2, c2_alt, dpi);
+      } else if (consistent[genestrand][(unsigned char) c1_uc][(unsigned char) c2] ||
+                 consistent[genestrand][(unsigned char) c1_uc][(unsigned char) c2_alt]) {
+        t->score += MATCH; t->nmatches += 1;
+        sink_push(s, queryoffset + querycoord, genomeoffset + genomecoord, c1, AMBIGUOUS_COMP, c2, c2_alt, dpi);
+      } else {
+        t->score += MISMATCH; t->nmismatches += 1;
+        sink_push(s, queryoffset + querycoord, genomeoffset + genomecoord, c1, MISMATCH_COMP, c2, c2_alt, dpi);
+      }
+      r--; c--;
+    }
+  }
+
+  if (r == 0 && c == 0) {
+    /* finished with a diagonal step */
+  } else if (c == 0) {
+    dist = r;
+    add_queryskip(s, r, 0 + LAZY_INDEL, dist, rsequence, queryoffset, genomeoffset, revp, dpi);
+    t->score += QOPEN + dist * QINDEL;
+    t->nopens += 1;
+    t->nindels += dist;
+  } else {
+    dist = c;
+    if (add_genomeskip(s, 0 + LAZY_INDEL, c, dist, queryoffset, genomeoffset, revp, chroffset, chrhigh,
+                       watsonp, dpi)) {
+      t->score += TOPEN + dist * TINDEL;
+      t->nopens += 1;
+      t->nindels += dist;
+    }
+  }
+}
+
+/* Dynprog_compute_bands (dynprog.c:1247) */
+static void
+compute_bands (int *lband, int *uband, int rlength, int glength, int extraband, int widebandp) {
+  if (!widebandp) { *lband = extraband; *uband = extraband; }
+  else if (glength >= rlength) { *uband = glength - rlength + extraband; *lband = extraband; }
+  else { *lband = rlength - glength + extraband; *uband = extraband; }
+}
+
+/* ---------------------------------------------------------------------------
+ * Dynprog_single_gap (dynprog_single.c:429-676), nosimd build, homopolymerp
+ * false (the default; dynprog_single.c:535 is out of scope).  Max lengths are
+ * those of Dynprog_new with gmap.c's defaults (dynprog.c:602-627):
+ * max_rlength 660, max_glength 2000.
+ * ------------------------------------------------------------------------- */
+#define ORC_MAX_RLENGTH 660
+#define ORC_MAX_GLENGTH 2000
+
+/* single_gap_simple (dynprog_single.c:346) */
+static int
+single_gap_simple (PairSink *s, Tally *t, const char *rsequence, const char *rsequenceuc, int rlength,
+                   const char *gsequence, const char *gsequence_alt, int roffset, int goffset,
+                   int genestrand, int dpi) {
+  int r, q;
+  char c1, c1_uc, c2, c2_alt;
+  t->score = 0; t->nmatches = t->nmismatches = 0;
+  for (r = 1; r <= rlength; r++) {
+    q = r - 1;
+    c1 = rsequence[q]; c1_uc = rsequenceuc[q]; c2 = gsequence[q]; c2_alt = gsequence_alt[q];
+    if (c2 == '*') {
+    } else if (c1_uc == c2 || c1_uc == c2_alt) {
+      t->score += MATCH; t->nmatches += 1;
+      sink_push(s, roffset + q, goffset + q, c1, DYNPROG_MATCH_COMP, c2, c2_alt, dpi);
+    } else if (consistent[genestrand][(unsigned char) c1_uc][(unsigned char) c2] ||
+               consistent[genestrand][(unsigned char) c1_uc][(unsigned char) c2_alt]) {
+      t->score += MATCH; t->nmatches += 1;
+      sink_push(s, roffset + q, goffset + q, c1, AMBIGUOUS_COMP, c2, c2_alt, dpi);
+    } else {
+      t->score += MISMATCH; t->nmismatches += 1;
+      sink_push(s, roffset + q, goffset + q, c1, MISMATCH_COMP, c2, c2_alt, dpi);
+    }
+  }
+  return t->nmismatches > 1 ? 0 : 1;
+}
+
+static void
+reverse_pairs (OrcPair *p, int n) {
+  int i, j;
+  OrcPair t;
+  for (i = 0, j = n - 1; i < j; i++, j--) { t = p[i]; p[i] = p[j]; p[j] = t; }
+}
+
+int
+orc_single_gap (const char *rsequence, const char *rsequenceuc, int rlength, int glength,
+                int roffset, int goffset, unsigned int chroffset, unsigned int chrhigh,
+                int watsonp, int genestrand, int jump_late_p, int extraband_single, int widebandp,
+                double defect_rate, int dynprogindex, int *scalars, OrcPair *out, int max_pairs) {
+  int mismatchtype, open, extend, lband, uband, n;
+  char *gseq, *gseq_alt;
+  int *matrix;
+  signed char *dirs;
+  PairSink sink = {out, 0, max_pairs};
+  Tally t = {0, 0, 0, 0, 0};
+  int dpi_next = dynprogindex + (dynprogindex > 0 ? +1 : -1);
+
+  if (defect_rate < DEFECT_HIGHQ) mismatchtype = HIGHQ;
+  else if (defect_rate < DEFECT_MEDQ) mismatchtype = MEDQ;
+  else mismatchtype = LOWQ;
+
+  if (g_user_dynprog_p) { open = g_user_open; extend = g_user_extend; }
+  else if (defect_rate < DEFECT_HIGHQ) { open = SINGLE_OPEN_HIGHQ; extend = SINGLE_EXTEND_HIGHQ; }
+  else if (defect_rate < DEFECT_MEDQ) { open = SINGLE_OPEN_MEDQ; extend = SINGLE_EXTEND_MEDQ; }
+  else { open = SINGLE_OPEN_LOWQ; extend = SINGLE_EXTEND_LOWQ; }
+
+  if (rlength <= 0 || glength <= 0 || rlength > ORC_MAX_RLENGTH || glength > ORC_MAX_GLENGTH) {
+    scalars[0] = dpi_next; scalars[1] = NEG_INFINITY_32;
+    scalars[2] = scalars[3] = scalars[4] = scalars[5] = 0;
+    return -1;
+  }
+
+  gseq = (char *) malloc(glength + 1);
+  gseq_alt = (char *) malloc(glength + 1);
+  if (watsonp) orc_get_segment(1, chroffset + (unsigned int) goffset, glength, chrhigh, 0, gseq, gseq_alt);
+  else orc_get_segment(0, chrhigh - (unsigned int) goffset + 1, glength, chroffset, 1, gseq, gseq_alt);
+
+  if (gseq[0] == '\0') {
+    scalars[0] = dynprogindex; scalars[1] = NEG_INFINITY_32;
+    scalars[2] = scalars[3] = scalars[4] = scalars[5] = 0;
+    free(gseq); free(gseq_alt);
+    return -1;
+  }
+  if (glength == rlength) {
+    if (single_gap_simple(&sink, &t, rsequence, rsequenceuc, rlength, gseq, gseq_alt, roffset, goffset,
+                          genestrand, dynprogindex)) {
+      /* list order = reverse of push order; no List_reverse on this path */
+      n = sink.n < max_pairs ? sink.n : max_pairs;
+      reverse_pairs(out, n);
+      scalars[0] = dpi_next; scalars[1] = t.score; scalars[2] = t.nmatches; scalars[3] = t.nmismatches;
+      scalars[4] = 0; scalars[5] = 0;
+      free(gseq); free(gseq_alt);
+      return sink.n > 0 ? sink.n : -1; /* an empty List_T is NULL */
+    }
+    sink.n = 0;
+    t.score = t.nmatches = t.nmismatches = 0;
+  }
+
+  compute_bands(&lband, &uband, rlength, glength, extraband_single, widebandp);
+  matrix = (int *) malloc((size_t) (glength + 1) * (rlength + 1) * sizeof(int));
+  dirs = (signed char *) malloc((size_t) 3 * (glength + 1) * (rlength + 1));
+  orc_standard_fill(rsequence, gseq, gseq_alt, rlength, glength, mismatchtype, open, extend, lband, uband,
+                    jump_late_p, /*revp*/0, /*saturation*/NEG_INFINITY_32, 1, 1, matrix, dirs);
+  traceback_std(&sink, &t, dirs, rlength, glength, rlength, glength, rsequence, rsequenceuc, gseq, gseq_alt,
+                roffset, goffset, /*revp*/0, chroffset, chrhigh, watsonp, genestrand, dynprogindex);
+  /* pushes prepend; List_reverse (dynprog_single.c:675) => list order == push order */
+  scalars[0] = dpi_next;
+  scalars[1] = t.score;
+  scalars[2] = t.nmatches; scalars[3] = t.nmismatches; scalars[4] = t.nopens; scalars[5] = t.nindels;
+  free(matrix); free(dirs); free(gseq); free(gseq_alt);
+  return sink.n > 0 ? sink.n : -1; /* an empty List_T is NULL */
+}

@@ -1,0 +1,68 @@
+/* oracle/gmapdp_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference GMAP 2024-02-22 Dynprog_* path, written in
+ * plain C from a reading of /root/reference/src (never copied).  It is the
+ * checker for the HIP engine: only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it.  The product (libgmapdp.so) never
+ * links or calls it.
+ *
+ * Parity pinning: tests/test_oracle_vs_ref.py compares every entry point
+ * against the reference's own objects (oracle/_ref/librefdp_*.so, built by
+ * oracle/ref.mk) on seeded random problems, and against the committed golden
+ * vectors in tests/golden/ (generated from those objects by
+ * tests/golden/make_golden.py).
+ */
+#ifndef GMAPDP_ORACLE_H
+#define GMAPDP_ORACLE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* One Pair_T of the reference (pairdef.h:8-42), flattened: the fields a
+   Dynprog_* call sets.  Same layout as refharness.c RefPair. */
+typedef struct {
+  int querypos;
+  int genomepos;
+  int queryjump;
+  int genomejump;
+  int dynprogindex;
+  char cdna, comp, genome, genomealt;
+  int gapp;
+} OrcPair;
+
+/* mode: Mode_T of mode.h:5 (0 = STANDARD). */
+int orc_init (int mode, int user_open, int user_extend, int user_dynprog_p);
+
+/* The genome as unpacked characters (A,C,G,T,N), i.e. what
+   Genome_get_char / uncompress_mmap return for each position. */
+int orc_set_genome (const char *genome, unsigned int length);
+
+/* Dynprog_single_gap (dynprog_single.c:429), nosimd semantics.
+   scalars[0..5] = dynprogindex(after), finalscore, nmatches, nmismatches,
+   nopens, nindels.  Returns npairs (list order), or -1 for a NULL list. */
+int orc_single_gap (const char *rsequence, const char *rsequenceuc, int rlength, int glength,
+                    int roffset, int goffset, unsigned int chroffset, unsigned int chrhigh,
+                    int watsonp, int genestrand, int jump_late_p, int extraband_single, int widebandp,
+                    double defect_rate, int dynprogindex, int *scalars, OrcPair *out, int max_pairs);
+
+/* Genome_get_segment_right / _left (genome.c:11023/11079) over the oracle
+   genome (no alternate genome: segmentalt = segment). */
+int orc_get_segment (int rightp, unsigned int pos, int length, unsigned int chrbound, int revcomp,
+                     char *segment, char *segmentalt);
+
+/* Dynprog_standard (dynprog.c:1268) on explicit segments; exported so the
+   fill can be checked cell by cell.  matrix: (glength+1)*(rlength+1) int32,
+   dirs: 3 planes of the same size (nogap, Egap, Fgap), [c][r] layout. */
+int orc_standard_fill (const char *rsequence, const char *gsequence, const char *gsequence_alt,
+                       int rlength, int glength, int mismatchtype, int open, int extend,
+                       int lband, int uband, int jump_late_p, int revp, int saturation,
+                       int upperp, int lowerp, int *matrix, signed char *dirs);
+
+int orc_pairdistance (int mismatchtype, short *out128x128);
+int orc_consistent (int genestrand, unsigned char *out128x128);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,81 @@
+# oracle/ref.mk -- TEST INFRASTRUCTURE ONLY.
+#
+# Compiles the reference GMAP 2024-02-22 C sources *where they lie* under
+# $(REF)/src into oracle/_ref/ (git-ignored; it travels to the GPU box with the
+# gpurun snapshot like any other built .so).  Nothing under /root/reference is
+# copied into the repository and the reference's own build system (autotools)
+# is not run: the source list is GMAP_FILES from src/Makefile.am:226-265 and
+# the per-variant SIMD defines are those of src/Makefile.am:268-319.  The
+# reference ships its own src/config.h, which is used as-is.
+#
+# That shipped config.h was generated on the upstream author's macOS machine:
+# it sets HAVE_BZLIB (no <bzlib.h> here) and PAGESIZE_VIA_SYSCTL (macOS-only
+# <sys/sysctl.h>).  bzip2.c and getline.c use config.h only for HAVE_BZLIB, so
+# they are compiled without -DHAVE_CONFIG_H (their own no-bzip2 configuration).
+# access.c does not compile here in either configuration, so the full `gmap`
+# program is UNBUILDABLE in this image without a regenerated config.h
+# (generated code we do not write).  The Dynprog_* path does not need
+# access.c: the harness library links every other GMAP object with
+# --gc-sections and exports only refh_*, so the unreachable callers of
+# Access_* drop out (tests check the .so has no unresolved GMAP symbols).
+#
+# Products (per variant V in {nosimd, avx2}):
+#   _ref/V/*.o                 reference objects
+#   _ref/librefdp_V.so         reference objects + refharness.c: a flat C API
+#                              over the reference's own Dynprog_* entry points,
+#                              used only by tests/ and the golden generator.
+
+REF      ?= /root/reference
+SRC      := $(REF)/src
+OUT      ?= _ref
+CC       := gcc
+BASEFLAGS := -O3 -fomit-frame-pointer -fPIC -pthread -I$(SRC) \
+             -DTARGET=\"x86_64-pc-linux-gnu\" -DGMAPDB=\"/nonexistent/gmapdb\" -w \
+             -ffunction-sections -fdata-sections
+
+GMAP_C := except.c assert.c mem.c intlist.c uintlist.c list.c littleendian.c bigendian.c \
+  univinterval.c interval.c stopwatch.c semaphore.c access.c filestring.c iit-read-univ.c \
+  iit-read.c md5.c bzip2.c fopen.c sequence.c reader.c genomicpos.c compress.c compress-write.c \
+  gbuffer.c genome.c popcount.c dinucl_bits.c genome_canonical.c genome-write.c bitpack64-read.c \
+  bitpack64-readtwo.c indexdb.c oligo.c block.c chrom.c segmentpos.c chrnum.c uinttable_rh.c \
+  gregion.c match.c matchpool.c diagnostic.c stage1.c diag.c diagpool.c cmet.c atoi.c orderstat.c \
+  oligoindex_hr.c intron.c maxent.c maxent_hr.c pair.c pairpool.c cellpool.c stage2.c doublelist.c \
+  smooth.c splicestringpool.c splicetrie_build.c splicetrie.c boyer-moore.c dynprog.c dynprog_simd.c \
+  dynprog_single.c dynprog_genome.c dynprog_cdna.c dynprog_end.c translation.c pbinom.c \
+  changepoint.c stage3.c request.c result.c output.c inbuffer.c samheader.c printbuffer.c \
+  outbuffer.c chimera.c datadir.c parserange.c getline.c getopt.c getopt1.c gmap.c
+
+# Not buildable with the shipped (macOS) config.h, and not on the Dynprog_* path.
+UNBUILDABLE_C := access.c
+# Compiled without config.h (their only config switch is HAVE_BZLIB).
+NOCONFIG_C := bzip2.c getline.c
+# Driver (main) and output/threading layers: not linked into the harness.
+NOTLINKED_C := gmap.c inbuffer.c outbuffer.c
+HARNESS_C := $(filter-out $(UNBUILDABLE_C) $(NOTLINKED_C),$(GMAP_C))
+
+FLAGS_nosimd :=
+FLAGS_avx2   := -mpopcnt -DHAVE_SSE2=1 -DHAVE_SSSE3=1 -DHAVE_SSE4_1=1 -DHAVE_SSE4_2=1 -DHAVE_AVX2=1 \
+                -msse2 -mssse3 -msse4.1 -msse4.2 -mavx2 -mno-avx512f -mno-avx512cd -mno-avx512vl -mno-avx512bw
+
+VARIANTS := nosimd avx2
+
+define variant_rules
+LIBOBJS_$(1) := $$(patsubst %.c,$(OUT)/$(1)/%.o,$(HARNESS_C))
+
+$(OUT)/$(1)/%.o: $(SRC)/%.c
+	@mkdir -p $$(dir $$@)
+	$$(CC) $(BASEFLAGS) $$(if $$(filter $$(notdir $$<),$(NOCONFIG_C)),,-DHAVE_CONFIG_H) $$(FLAGS_$(1)) -c $$< -o $$@
+
+$(OUT)/$(1)/refharness.o: refharness.c
+	@mkdir -p $$(dir $$@)
+	$$(CC) $(BASEFLAGS) -DHAVE_CONFIG_H $$(FLAGS_$(1)) -I. -c $$< -o $$@
+
+$(OUT)/librefdp_$(1).so: $$(LIBOBJS_$(1)) $(OUT)/$(1)/refharness.o
+	$$(CC) -shared -pthread -Wl,--gc-sections -Wl,--version-script=refharness.map -o $$@ $$^ -lz -lm
+endef
+
+$(foreach v,$(VARIANTS),$(eval $(call variant_rules,$(v))))
+
+all: $(foreach v,$(VARIANTS),$(OUT)/librefdp_$(v).so)
+
+.PHONY: all

@@ -1,0 +1,214 @@
+/* oracle/refharness.c -- TEST INFRASTRUCTURE ONLY (never shipped, never on the
+ * product path).
+ *
+ * A flat, plain-C API over the *reference's own* compiled Dynprog_* objects
+ * (built by oracle/ref.mk into oracle/_ref/librefdp_<variant>.so).  Tests and
+ * tests/golden/make_golden.py call it through ctypes to (1) pin the CPU
+ * restatement in oracle/gmapdp_oracle.c and (2) generate golden vectors.
+ *
+ * Everything below only *calls* reference functions; the algorithm lives in the
+ * reference objects.  Interfaces used (all /root/reference/src):
+ *   Dynprog_init            dynprog.c:1008
+ *   Dynprog_new             dynprog.c:631 (sizes as gmap.c:4898-4903)
+ *   Dynprog_single_gap      dynprog_single.c:429
+ *   Dynprog_end5_gap        dynprog_end.c:1294
+ *   Dynprog_end3_gap        dynprog_end.c:1924
+ *   Genome_from_sequence    genome.c:307
+ *   Pairpool_new/reset      pairpool.c
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "bool.h"
+#include "mem.h"
+#include "list.h"
+#include "pair.h"
+#include "pairdef.h"
+#include "pairpool.h"
+#include "sequence.h"
+#include "genome.h"
+#include "dynprog.h"
+#include "dynprog_single.h"
+#include "dynprog_end.h"
+#include "dynprog_genome.h"
+
+/* Flat pair record (matches oracle/gmapdp_oracle.h RefPair / GmapdpPair
+ * semantics: one record per Pair_T in list order). */
+typedef struct {
+  int querypos;
+  int genomepos;
+  int queryjump;
+  int genomejump;
+  int dynprogindex;
+  char cdna, comp, genome, genomealt;
+  int gapp;
+} RefPair;
+
+static Dynprog_T dynprogM = NULL, dynprogL = NULL, dynprogR = NULL;
+static Pairpool_T pairpool = NULL;
+static Genome_T genome = NULL;
+static Sequence_T genome_seq = NULL;
+static int initialized = 0;
+
+/* gmap.c:259,275-277 and stage3.h:36 defaults */
+#define NULLGAP 600
+#define EXTRAQUERYGAP 20
+#define MAXPEELBACK 60
+#define EXTRAMATERIAL_END 10
+#define EXTRAMATERIAL_PAIRED 8
+
+int
+refh_init (int user_open, int user_extend, int user_dynprog_p) {
+  if (initialized) return 0;
+  Dynprog_init(STANDARD);
+  Dynprog_single_setup(user_open, user_extend, user_dynprog_p ? true : false, /*homopolymerp*/false);
+  Dynprog_end_setup(/*splicesites*/NULL, /*splicetypes*/NULL, /*splicedists*/NULL, /*nsplicesites*/0,
+                    /*trieoffsets_obs*/NULL, /*triecontents_obs*/NULL,
+                    /*trieoffsets_max*/NULL, /*triecontents_max*/NULL,
+                    user_open, user_extend, user_dynprog_p ? true : false);
+  dynprogM = Dynprog_new(NULLGAP, EXTRAQUERYGAP, MAXPEELBACK, EXTRAMATERIAL_END, EXTRAMATERIAL_PAIRED, false);
+  dynprogL = Dynprog_new(NULLGAP, EXTRAQUERYGAP, MAXPEELBACK, EXTRAMATERIAL_END, EXTRAMATERIAL_PAIRED, true);
+  dynprogR = Dynprog_new(NULLGAP, EXTRAQUERYGAP, MAXPEELBACK, EXTRAMATERIAL_END, EXTRAMATERIAL_PAIRED, true);
+  pairpool = Pairpool_new();
+  initialized = 1;
+  return 0;
+}
+
+int
+refh_max_lengths (int *max_rlength, int *max_glength) {
+  *max_rlength = dynprogM->max_rlength;
+  *max_glength = dynprogM->max_glength;
+  return 0;
+}
+
+/* The genome is wrapped the way GMAP wraps a user-supplied segment (-g):
+   Genome_from_sequence (genome.c:307) packs it into .genomecomp blocks. */
+int
+refh_set_genome (const char *seq, int length) {
+  char *copy = (char *) malloc(length + 1);
+  memcpy(copy, seq, length);
+  copy[length] = '\0';
+  genome_seq = Sequence_genomic_new(copy, length, /*copyp*/true);
+  genome = Genome_from_sequence(genome_seq);
+  free(copy);
+  return 0;
+}
+
+static int
+flatten (List_T pairs, RefPair *out, int max_pairs) {
+  int n = 0;
+  List_T p;
+  Pair_T pair;
+  for (p = pairs; p != NULL; p = List_next(p)) {
+    pair = (Pair_T) List_head(p);
+    if (n < max_pairs) {
+      out[n].querypos = pair->querypos;
+      out[n].genomepos = (int) pair->genomepos;
+      out[n].queryjump = pair->queryjump;
+      out[n].genomejump = pair->genomejump;
+      out[n].dynprogindex = pair->dynprogindex;
+      out[n].cdna = pair->cdna;
+      out[n].comp = pair->comp;
+      out[n].genome = pair->genome;
+      out[n].genomealt = pair->genomealt;
+      out[n].gapp = pair->gapp ? 1 : 0;
+    }
+    n++;
+  }
+  return n;
+}
+
+/* scalars[0..5] = dynprogindex(after), finalscore, nmatches, nmismatches, nopens, nindels.
+   Returns number of pairs, or -1 when the reference returned NULL. */
+int
+refh_single_gap (const char *rsequence, const char *rsequenceuc, int rlength, int glength,
+                 int roffset, int goffset, unsigned int chroffset, unsigned int chrhigh,
+                 int watsonp, int genestrand, int jump_late_p, int extraband_single, int widebandp,
+                 double defect_rate, int dynprogindex, int *scalars, RefPair *out, int max_pairs) {
+  List_T pairs;
+  int finalscore = 0, nmatches = 0, nmismatches = 0, nopens = 0, nindels = 0, n;
+
+  Pairpool_reset(pairpool);
+  pairs = Dynprog_single_gap(&dynprogindex, &finalscore, &nmatches, &nmismatches, &nopens, &nindels,
+                             dynprogM, (char *) rsequence, (char *) rsequenceuc, rlength, glength,
+                             roffset, goffset, (Univcoord_T) chroffset, (Univcoord_T) chrhigh,
+                             watsonp ? true : false, genestrand, jump_late_p ? true : false,
+                             genome, genome, pairpool, extraband_single, widebandp ? true : false,
+                             defect_rate);
+  scalars[0] = dynprogindex; scalars[1] = finalscore; scalars[2] = nmatches;
+  scalars[3] = nmismatches; scalars[4] = nopens; scalars[5] = nindels;
+  if (pairs == NULL) return -1;
+  n = flatten(pairs, out, max_pairs);
+  return n;
+}
+
+/* endalign: 0 QUERYEND_GAP, 1 QUERYEND_INDELS, 2 QUERYEND_NOGAPS, 3 BEST_LOCAL (dynprog.h:23) */
+int
+refh_end_gap (int end3p, const char *rsequence, const char *rsequenceuc, int rlength, int glength,
+              int roffset, int goffset, unsigned int chroffset, unsigned int chrhigh,
+              int watsonp, int genestrand, int jump_late_p, int extraband_end,
+              double defect_rate, int endalign, int require_pos_score_p, int dynprogindex,
+              int *scalars, RefPair *out, int max_pairs) {
+  List_T pairs;
+  int finalscore = 0, nmatches = 0, nmismatches = 0, nopens = 0, nindels = 0, n;
+
+  Pairpool_reset(pairpool);
+  if (end3p) {
+    pairs = Dynprog_end3_gap(&dynprogindex, &finalscore, &nmatches, &nmismatches, &nopens, &nindels,
+                             dynprogR, (char *) rsequence, (char *) rsequenceuc, rlength, glength,
+                             roffset, goffset, (Univcoord_T) chroffset, (Univcoord_T) chrhigh,
+                             watsonp ? true : false, genestrand, jump_late_p ? true : false,
+                             genome, genome, pairpool, extraband_end, defect_rate,
+                             (Endalign_T) endalign, require_pos_score_p ? true : false);
+  } else {
+    pairs = Dynprog_end5_gap(&dynprogindex, &finalscore, &nmatches, &nmismatches, &nopens, &nindels,
+                             dynprogL, (char *) rsequence, (char *) rsequenceuc, rlength, glength,
+                             roffset, goffset, (Univcoord_T) chroffset, (Univcoord_T) chrhigh,
+                             watsonp ? true : false, genestrand, jump_late_p ? true : false,
+                             genome, genome, pairpool, extraband_end, defect_rate,
+                             (Endalign_T) endalign, require_pos_score_p ? true : false);
+  }
+  scalars[0] = dynprogindex; scalars[1] = finalscore; scalars[2] = nmatches;
+  scalars[3] = nmismatches; scalars[4] = nopens; scalars[5] = nindels;
+  if (pairs == NULL) return -1;
+  n = flatten(pairs, out, max_pairs);
+  return n;
+}
+
+/* Reference genome-segment extraction (genome.c:11023/11079), for the oracle's
+   unpacking to be checked against. */
+int
+refh_get_segment (int rightp, unsigned int pos, int length, unsigned int chrbound, int revcomp,
+                  char *segment, char *segmentalt) {
+  if (rightp) {
+    Genome_get_segment_right(segment, segmentalt, genome, genome, (Univcoord_T) pos, (Chrpos_T) length,
+                             (Univcoord_T) chrbound, revcomp ? true : false);
+  } else {
+    Genome_get_segment_left(segment, segmentalt, genome, genome, (Univcoord_T) pos, (Chrpos_T) length,
+                            (Univcoord_T) chrbound, revcomp ? true : false);
+  }
+  return 0;
+}
+
+/* Copy of the mismatch-type score table the reference builds (dynprog.c:1008). */
+int
+refh_pairdistance (int mismatchtype, short *out128x128) {
+  int i, j;
+  for (i = 0; i < 128; i++) for (j = 0; j < 128; j++) out128x128[i * 128 + j] = pairdistance_array[mismatchtype][i][j];
+  return 0;
+}
+
+int
+refh_consistent (int genestrand, unsigned char *out128x128) {
+  int i, j;
+  for (i = 0; i < 128; i++) for (j = 0; j < 128; j++) out128x128[i * 128 + j] = consistent_array[genestrand][i][j] ? 1 : 0;
+  return 0;
+}
+
+int
+refh_use8p_size (int *out4) {
+  int i;
+  for (i = 0; i < 4; i++) out4[i] = use8p_size[i];
+  return 0;
+}

@@ -1,0 +1,177 @@
+"""ctypes bindings used by the tests (test infrastructure).
+
+Three implementations share one calling convention for each Dynprog_* entry
+point:
+
+* ``Ref``    -- the reference's own objects (oracle/_ref/librefdp_<v>.so,
+                built from /root/reference by oracle/ref.mk);
+* ``Oracle`` -- the repo's CPU restatement (oracle/libgmapdp_oracle.so);
+* the HIP engine is bound separately through gmapdp (the product package).
+
+Problem generation helpers (seeded, GMAP-shaped sub-problems) live here too.
+"""
+import ctypes as C
+import os
+import random
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "libgmapdp_oracle.so")
+REF_SO = {v: os.path.join(ROOT, "oracle", "_ref", "librefdp_%s.so" % v) for v in ("nosimd", "avx2")}
+
+
+class Pair(C.Structure):
+    _fields_ = [("querypos", C.c_int), ("genomepos", C.c_int), ("queryjump", C.c_int),
+                ("genomejump", C.c_int), ("dynprogindex", C.c_int),
+                ("cdna", C.c_char), ("comp", C.c_char), ("genome", C.c_char), ("genomealt", C.c_char),
+                ("gapp", C.c_int)]
+
+    def key(self):
+        return (self.querypos, self.genomepos, self.queryjump, self.genomejump, self.dynprogindex,
+                self.cdna, self.comp, self.genome, self.genomealt, self.gapp)
+
+
+MAXPAIRS = 8192
+
+
+class _Impl:
+    prefix = None
+
+    def __init__(self, path):
+        self.lib = C.CDLL(path)
+        p = self.prefix
+        f = getattr(self.lib, p + "single_gap")
+        f.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint, C.c_uint,
+                      C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int,
+                      C.POINTER(C.c_int), C.POINTER(Pair), C.c_int]
+        f.restype = C.c_int
+        self._single = f
+        self._pairs = (Pair * MAXPAIRS)()
+        self._scal = (C.c_int * 6)()
+        self._genome_keep = None
+
+    def single_gap(self, q, quc, rlength, glength, roffset, goffset, chroffset, chrhigh, watsonp,
+                   genestrand, jump_late_p, extraband, widebandp, defect_rate, dynprogindex):
+        n = self._single(q, quc, rlength, glength, roffset, goffset, chroffset, chrhigh, watsonp,
+                         genestrand, jump_late_p, extraband, widebandp, defect_rate, dynprogindex,
+                         self._scal, self._pairs, MAXPAIRS)
+        assert n <= MAXPAIRS
+        pairs = None if n < 0 else [self._pairs[i].key() for i in range(n)]
+        return tuple(self._scal), pairs
+
+
+class Ref(_Impl):
+    prefix = "refh_"
+
+    def __init__(self, variant="nosimd"):
+        super().__init__(REF_SO[variant])
+        self.lib.refh_init(0, 0, 0)
+
+    def set_genome(self, g: bytes):
+        self._genome_keep = C.create_string_buffer(g, len(g))
+        self.lib.refh_set_genome(self._genome_keep, len(g))
+
+
+class Oracle(_Impl):
+    prefix = "orc_"
+
+    def __init__(self):
+        super().__init__(ORACLE_SO)
+        self.lib.orc_init(0, 0, 0, 0)
+
+    def set_genome(self, g: bytes):
+        self._genome_keep = C.create_string_buffer(g, len(g))
+        self.lib.orc_set_genome(self._genome_keep, C.c_uint(len(g)))
+
+
+def ref_available(variant="nosimd"):
+    return os.path.exists(REF_SO[variant])
+
+
+# ---------------------------------------------------------------------------
+# Seeded GMAP-shaped problem generators
+# ---------------------------------------------------------------------------
+COMP = {ord("A"): "T", ord("C"): "G", ord("G"): "C", ord("T"): "A", ord("N"): "N"}
+
+
+def random_genome(rng: random.Random, n: int, nfrac=0.002) -> bytes:
+    s = bytearray(rng.choice(b"ACGT") for _ in range(n))
+    for i in range(n):
+        if rng.random() < nfrac:
+            s[i] = ord("N")
+    return bytes(s)
+
+
+def mutate(rng, seg: bytes, sub=0.03, indel=0.01, maxindel=4, lower=0.05, iupac=0.002):
+    out = bytearray()
+    i = 0
+    while i < len(seg):
+        x = rng.random()
+        if x < indel / 2:
+            i += rng.randint(1, maxindel)  # deletion in query
+            continue
+        if x < indel:
+            out.extend(rng.choice(b"ACGT") for _ in range(rng.randint(1, maxindel)))
+        b = seg[i]
+        y = rng.random()
+        if y < sub:
+            b = rng.choice(b"ACGT")
+        elif y < sub + iupac:
+            b = rng.choice(b"RYWSMKHBVDNX")
+        out.append(b)
+        i += 1
+    q = bytes(out)
+    uc = q
+    if lower:
+        q = bytes((c + 32) if (65 <= c <= 90 and rng.random() < lower) else c for c in q)
+    return q, uc
+
+
+def revcomp(s: bytes) -> bytes:
+    return bytes(ord(COMP.get(c, "N")) for c in reversed(s))
+
+
+def single_gap_problem(rng, genome: bytes, maxlen=400, chrhigh=None):
+    """One Dynprog_single_gap-shaped call: query slice ~ genome slice."""
+    glen = len(genome)
+    chrhigh = glen if chrhigh is None else chrhigh
+    watsonp = rng.random() < 0.6
+    glength = max(1, int(rng.expovariate(1 / 110.0))) if rng.random() < 0.9 else rng.randint(1, maxlen)
+    glength = min(glength, maxlen)
+    goffset = rng.randint(-3 if rng.random() < 0.02 else 0, max(0, chrhigh - glength - 1))
+    if rng.random() < 0.03:
+        goffset = max(0, chrhigh - glength + rng.randint(0, 5))  # run past chromosome end
+    if not watsonp:
+        # minus strand reads genome[chrhigh-goffset-glength+1 .. chrhigh-goffset]; GMAP never passes
+        # goffset outside [1, chrhigh+1] there (the reference would read outside the genome).
+        goffset = min(max(goffset, 1), chrhigh + 1)
+    # genome characters as the engine will see them
+    if watsonp:
+        seg = bytes(genome[goffset + i] if 0 <= goffset + i < chrhigh else ord("*") for i in range(glength))
+    else:
+        seg = bytes(ord(COMP.get(genome[chrhigh - goffset - i], "?")) if 0 <= chrhigh - goffset - i < chrhigh
+                    else ord("*") for i in range(glength))
+    seg = seg.replace(b"*", b"A")
+    mode = rng.random()
+    if mode < 0.15:
+        q, uc = bytes(rng.choice(b"ACGT") for _ in range(rng.randint(1, maxlen // 2))), None
+        uc = q
+    elif mode < 0.25:
+        q, uc = mutate(rng, seg, sub=0.0, indel=0.0)  # equal length, maybe simple path
+    else:
+        q, uc = mutate(rng, seg, sub=rng.choice([0.01, 0.03, 0.08]), indel=rng.choice([0.0, 0.01, 0.03]))
+    if len(q) == 0:
+        q = uc = b"A"
+    rlength = len(q)
+    roffset = rng.randint(0, 3000)
+    return dict(q=q, quc=uc, rlength=rlength, glength=glength, roffset=roffset, goffset=goffset,
+                chroffset=0, chrhigh=chrhigh, watsonp=int(watsonp), genestrand=0,
+                jump_late_p=rng.randint(0, 1), extraband=rng.choice([0, 3, 6, 6, 6, 14]),
+                widebandp=int(rng.random() < 0.85),
+                defect_rate=rng.choice([0.001, 0.005, 0.02, 0.05]),
+                dynprogindex=rng.choice([1, 5, -1, -7]))
+
+
+def call_single(impl, p):
+    return impl.single_gap(p["q"], p["quc"], p["rlength"], p["glength"], p["roffset"], p["goffset"],
+                           p["chroffset"], p["chrhigh"], p["watsonp"], p["genestrand"], p["jump_late_p"],
+                           p["extraband"], p["widebandp"], p["defect_rate"], p["dynprogindex"])
