@@ -1,0 +1,219 @@
+"""gmapdp -- Python host binding of libgmapdp.so (the MI355X Dynprog engine).
+
+Mirrors the reference's Dynprog_* operator interface for tests and the bench:
+argument names and meaning follow dynprog_single.c:429 (Dynprog_single_gap),
+results follow its out-parameters and the List_T of Pair_T it returns.
+
+The native library is required: importing this module on a machine without
+the built extension, or calling into it without a HIP device, raises -- there
+is no CPU fallback on the product path.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libgmapdp.so")
+
+WATSON, JUMP_LATE, WIDEBAND = 0x1, 0x2, 0x4
+NEG_INFINITY_32 = -32768
+MAX_RLENGTH, MAX_GLENGTH = 660, 2000
+
+
+class GmapdpError(RuntimeError):
+    pass
+
+
+class SingleProblem(C.Structure):
+    _fields_ = [("qoff", C.c_int32), ("rlength", C.c_int32), ("glength", C.c_int32), ("roffset", C.c_int32),
+                ("goffset", C.c_int32), ("chroffset", C.c_uint32), ("chrhigh", C.c_uint32), ("flags", C.c_int32),
+                ("genestrand", C.c_int32), ("extraband", C.c_int32), ("defect_rate", C.c_double),
+                ("dynprogindex", C.c_int32), ("pad_", C.c_int32)]
+
+
+class Result(C.Structure):
+    _fields_ = [("npairs", C.c_int32), ("pair_offset", C.c_int32), ("traceback_score", C.c_int32),
+                ("nmatches", C.c_int32), ("nmismatches", C.c_int32), ("nopens", C.c_int32),
+                ("nindels", C.c_int32), ("dynprogindex", C.c_int32)]
+
+
+PAIR_DTYPE = np.dtype([("querypos", "<i4"), ("genomepos", "<i4"), ("jump", "<i4"), ("cdna", "S1"),
+                       ("comp", "S1"), ("genome", "S1"), ("genomealt", "S1")])
+RESULT_DTYPE = np.dtype([(n, "<i4") for n, _ in Result._fields_])
+PROBLEM_DTYPE = np.dtype({"names": [n for n, _ in SingleProblem._fields_],
+                          "formats": ["<i4", "<i4", "<i4", "<i4", "<i4", "<u4", "<u4", "<i4", "<i4", "<i4", "<f8",
+                                      "<i4", "<i4"],
+                          "offsets": [SingleProblem.__dict__[n].offset for n, _ in SingleProblem._fields_],
+                          "itemsize": C.sizeof(SingleProblem)})
+
+_lib = None
+
+
+def load_library(path=LIB_PATH):
+    """Load libgmapdp.so; raises GmapdpError if the HIP extension is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise GmapdpError("libgmapdp.so not built (%s); run __graft_entry__.build()" % path)
+    lib = C.CDLL(path)
+    P = C.POINTER
+    sig = {
+        "gmapdp_create": (C.c_int, [P(C.c_void_p), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
+        "gmapdp_destroy": (None, [C.c_void_p]),
+        "gmapdp_genome_words": (C.c_size_t, [C.c_uint64]),
+        "gmapdp_pack_genome": (C.c_int, [C.c_char_p, C.c_uint64, C.c_void_p]),
+        "gmapdp_set_genome": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint64]),
+        "gmapdp_single_gap_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t,
+                                              C.c_void_p, C.c_void_p, C.c_size_t]),
+        "gmapdp_single_pair_capacity": (C.c_size_t, [C.c_void_p, C.c_int]),
+        "gmapdp_plan_single": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, P(C.c_void_p)]),
+        "gmapdp_plan_pair_capacity": (C.c_size_t, [C.c_void_p]),
+        "gmapdp_plan_gpu_problems": (C.c_int, [C.c_void_p]),
+        "gmapdp_plan_dev_index": (C.c_int, [C.c_void_p, C.c_int]),
+        "gmapdp_plan_nlaunches": (C.c_int, [C.c_void_p]),
+        "gmapdp_plan_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_void_p]),
+        "gmapdp_plan_destroy": (None, [C.c_void_p]),
+        "gmapdp_plan_launch_info": (C.c_int, [C.c_void_p, C.c_int, P(C.c_int), P(C.c_int), P(C.c_int),
+                                              P(C.c_size_t)]),
+        "gmapdp_plan_run_launch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                             C.c_void_p, C.c_void_p]),
+        "gmapdp_stream": (C.c_void_p, [C.c_void_p]),
+        "gmapdp_compute_bands": (None, [P(C.c_int), P(C.c_int), C.c_int, C.c_int, C.c_int, C.c_int]),
+        "gmapdp_last_error": (C.c_char_p, [C.c_void_p]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    """Names of the C ABI functions declared in include/gmapdp.h."""
+    hdr = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "gmapdp.h")
+    import re
+    txt = open(hdr).read()
+    return sorted(set(re.findall(r"\b(gmapdp_[a-z_0-9]+)\s*\(", txt)))
+
+
+def pack_genome(seq: bytes) -> np.ndarray:
+    """Compress_create_blocks_comp-format packing (compress-write.c:754)."""
+    lib = load_library()
+    n = lib.gmapdp_genome_words(len(seq))
+    out = np.zeros(n, dtype=np.uint32)
+    rc = lib.gmapdp_pack_genome(seq, len(seq), out.ctypes.data)
+    if rc:
+        raise GmapdpError("gmapdp_pack_genome failed: %d" % rc)
+    return out
+
+
+class Engine:
+    """One Dynprog engine context on one GPU (mirrors a GMAP worker's Dynprog_T)."""
+
+    def __init__(self, device=0, mode=0, user_open=0, user_extend=0, user_dynprog_p=False):
+        self.lib = load_library()
+        h = C.c_void_p()
+        rc = self.lib.gmapdp_create(C.byref(h), device, mode, user_open, user_extend, int(bool(user_dynprog_p)))
+        if rc:
+            raise GmapdpError("gmapdp_create failed (%d): no usable HIP device %d?" % (rc, device))
+        self.h = h
+        self.genome_length = 0
+
+    def close(self):
+        if self.h:
+            self.lib.gmapdp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc:
+            raise GmapdpError("%s failed (%d): %s" % (what, rc, self.lib.gmapdp_last_error(self.h).decode()))
+
+    def set_genome(self, seq: bytes = None, blocks: np.ndarray = None, length: int = None):
+        if blocks is None:
+            blocks = pack_genome(seq)
+            length = len(seq)
+        blocks = np.ascontiguousarray(blocks, dtype=np.uint32)
+        self._check(self.lib.gmapdp_set_genome(self.h, blocks.ctypes.data, blocks.size, length), "gmapdp_set_genome")
+        self.genome_length = length
+
+    # -- batched Dynprog_single_gap ------------------------------------------
+    @staticmethod
+    def build_single_batch(calls):
+        """calls: iterable of dicts with the Dynprog_single_gap arguments
+        (q, quc, rlength, glength, roffset, goffset, chroffset, chrhigh, watsonp, genestrand,
+        jump_late_p, extraband, widebandp, defect_rate, dynprogindex)."""
+        calls = list(calls)
+        probs = np.zeros(len(calls), dtype=PROBLEM_DTYPE)
+        qparts, qucparts, off = [], [], 0
+        for i, p in enumerate(calls):
+            q, quc = p["q"], p["quc"]
+            probs[i]["qoff"] = off
+            probs[i]["rlength"] = p["rlength"]
+            probs[i]["glength"] = p["glength"]
+            probs[i]["roffset"] = p["roffset"]
+            probs[i]["goffset"] = p["goffset"]
+            probs[i]["chroffset"] = p["chroffset"]
+            probs[i]["chrhigh"] = p["chrhigh"]
+            probs[i]["flags"] = ((WATSON if p["watsonp"] else 0) | (JUMP_LATE if p["jump_late_p"] else 0) |
+                                 (WIDEBAND if p["widebandp"] else 0))
+            probs[i]["genestrand"] = p["genestrand"]
+            probs[i]["extraband"] = p["extraband"]
+            probs[i]["defect_rate"] = p["defect_rate"]
+            probs[i]["dynprogindex"] = p["dynprogindex"]
+            qparts.append(q)
+            qucparts.append(quc)
+            off += len(q)
+        qbuf = b"".join(qparts) or b"\0"
+        qucbuf = b"".join(qucparts) or b"\0"
+        return probs, qbuf, qucbuf
+
+    def single_gap_batch_raw(self, probs, qbuf, qucbuf):
+        n = len(probs)
+        results = np.zeros(n, dtype=RESULT_DTYPE)
+        cap = self.lib.gmapdp_single_pair_capacity(probs.ctypes.data, n)
+        pairs = np.zeros(max(cap, 1), dtype=PAIR_DTYPE)
+        rc = self.lib.gmapdp_single_gap_batch(self.h, probs.ctypes.data, n, qbuf, qucbuf, len(qbuf),
+                                              results.ctypes.data, pairs.ctypes.data, cap)
+        self._check(rc, "gmapdp_single_gap_batch")
+        return results, pairs
+
+    def single_gap_batch(self, calls):
+        """Returns, per call, ((dynprogindex, traceback_score, nmatches, nmismatches, nopens, nindels),
+        pairs-or-None) with pairs in the reference's list order as tuples
+        (querypos, genomepos, queryjump, genomejump, dynprogindex, cdna, comp, genome, genomealt, gapp)."""
+        calls = list(calls)
+        probs, qbuf, qucbuf = self.build_single_batch(calls)
+        results, pairs = self.single_gap_batch_raw(probs, qbuf, qucbuf)
+        return decode_results(results, pairs, [p["dynprogindex"] for p in calls])
+
+
+def decode_results(results, pairs, dynprogindices):
+    out = []
+    for i, res in enumerate(results):
+        scal = (int(res["dynprogindex"]), int(res["traceback_score"]), int(res["nmatches"]),
+                int(res["nmismatches"]), int(res["nopens"]), int(res["nindels"]))
+        n = int(res["npairs"])
+        if n == 0:
+            out.append((scal, None))
+            continue
+        dpi = dynprogindices[i]
+        seg = pairs[int(res["pair_offset"]):int(res["pair_offset"]) + n]
+        lst = []
+        for rec in seg:
+            if rec["querypos"] == -1 and rec["genomepos"] == -1:
+                lst.append((-1, -1, 0, int(rec["jump"]), 0, b" ", b" ", b" ", b" ", 1))
+            else:
+                lst.append((int(rec["querypos"]), int(rec["genomepos"]), 0, 0, dpi, rec["cdna"], rec["comp"],
+                            rec["genome"], rec["genomealt"], 0))
+        out.append((scal, lst))
+    return out

@@ -1,0 +1,167 @@
+/* include/gmapdp.h -- C ABI of the MI355X GMAP Dynprog engine (libgmapdp.so).
+ *
+ * This is the drop-in boundary for GMAP's Dynprog_* hot path.  It is a
+ * batched, plain-pointer restatement of the reference entry points; the
+ * reference-signature wrappers (Dynprog_single_gap(...) etc., which take
+ * GMAP's Dynprog_T / Genome_T / Pairpool_T and return List_T of Pair_T) are
+ * declared in include/gmapdp_dynprog.h and documented in INTEGRATION.md.
+ *
+ * Entry point -> reference interface it replaces (paths under the reference
+ * tree's src/):
+ *   gmapdp_create            Dynprog_init (dynprog.c:1008) + Dynprog_single_setup
+ *                            (dynprog_single.c:101) + Dynprog_end_setup (dynprog_end.c)
+ *   gmapdp_destroy           Dynprog_term (dynprog.c:1203)
+ *   gmapdp_pack_genome       Compress_create_blocks_comp (compress-write.c:754): the
+ *                            .genomecomp block format that GMAP mmaps (genome.c:208)
+ *   gmapdp_set_genome        Genome_new / Genome_from_sequence (genome.c:208/307):
+ *                            the packed genome is made resident in HBM
+ *   gmapdp_single_gap_batch  Dynprog_single_gap (dynprog_single.c:429), one call per
+ *                            problem, many problems per launch
+ *   gmapdp_compute_bands     Dynprog_compute_bands (dynprog.c:1247)
+ *
+ * Semantics: every result is bit-identical to the reference's nosimd build
+ * (Dynprog_standard + Dynprog_traceback_std); see DESIGN.md "Parity".
+ *
+ * Errors: functions return 0 on success and a negative GMAPDP_E* code on
+ * failure (no errno).  A per-problem NULL result (the reference returning a
+ * NULL List_T) is reported as npairs == 0 with the reference's score
+ * convention in traceback_score (NEG_INFINITY_32 = -32768 for the size
+ * guard).
+ *
+ * Threading: a gmapdp_ctx is owned by one host thread at a time; create one
+ * per worker (mirrors GMAP's per-thread Dynprog_T, gmap.c:4898-4903).
+ */
+#ifndef GMAPDP_H
+#define GMAPDP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GMAPDP_OK 0
+#define GMAPDP_EINVAL (-1)
+#define GMAPDP_ENODEV (-2)
+#define GMAPDP_ENOMEM (-3)
+#define GMAPDP_ELAUNCH (-4)
+#define GMAPDP_ENOGENOME (-5)
+
+/* Reference limits (Dynprog_new with gmap.c defaults, dynprog.c:602-627). */
+#define GMAPDP_MAX_RLENGTH 660
+#define GMAPDP_MAX_GLENGTH 2000
+#define GMAPDP_NEG_INFINITY_32 (-32768)
+
+typedef struct gmapdp_ctx gmapdp_ctx;
+
+/* One Pair_T (pairdef.h:8-42) as the engine emits it, in the order of the
+ * List_T the reference returns.  A gap holder (Pairpool_push_gapholder,
+ * pairpool.c:375) has querypos == genomepos == -1 and jump == genomejump;
+ * ordinary pairs have jump == 0.  dynprogindex is per problem (all pairs of
+ * one call carry the caller's *dynprogindex, gap holders carry 0). */
+typedef struct {
+  int32_t querypos;
+  int32_t genomepos;
+  int32_t jump;
+  char cdna;
+  char comp;
+  char genome;
+  char genomealt;
+} gmapdp_pair;
+
+/* Problem flags */
+#define GMAPDP_WATSON     0x1  /* watsonp */
+#define GMAPDP_JUMP_LATE  0x2  /* jump_late_p */
+#define GMAPDP_WIDEBAND   0x4  /* widebandp */
+
+/* One Dynprog_single_gap call (dynprog_single.c:429 argument list).  The
+ * query slice is qseq[qoff .. qoff+rlength) (rsequence, case as given) and
+ * qseq_uc[...] (rsequenceuc) in the batch's query arena. */
+typedef struct {
+  int32_t qoff;
+  int32_t rlength;
+  int32_t glength;
+  int32_t roffset;
+  int32_t goffset;
+  uint32_t chroffset;
+  uint32_t chrhigh;
+  int32_t flags;          /* GMAPDP_WATSON | GMAPDP_JUMP_LATE | GMAPDP_WIDEBAND */
+  int32_t genestrand;     /* 0, +1, +2 */
+  int32_t extraband;      /* extraband_single */
+  double defect_rate;
+  int32_t dynprogindex;   /* *dynprogindex on entry */
+  int32_t pad_;
+} gmapdp_single_problem;
+
+/* Per-problem outputs (the reference's out-parameters). */
+typedef struct {
+  int32_t npairs;          /* 0 <=> NULL List_T */
+  int32_t pair_offset;     /* first pair in the batch's pair arena */
+  int32_t traceback_score; /* *finalscore / *traceback_score */
+  int32_t nmatches;
+  int32_t nmismatches;
+  int32_t nopens;
+  int32_t nindels;
+  int32_t dynprogindex;    /* *dynprogindex on exit */
+} gmapdp_result;
+
+/* Create a context on HIP device `device`.  mode = Mode_T (mode.h:5;
+ * 0 = STANDARD).  user_* mirror Dynprog_single_setup. */
+int gmapdp_create (gmapdp_ctx **ctx, int device, int mode,
+                   int user_open, int user_extend, int user_dynprog_p);
+void gmapdp_destroy (gmapdp_ctx *ctx);
+
+/* Words needed for a packed genome of `length` nt ((len+31)/32*3 + 4). */
+size_t gmapdp_genome_words (uint64_t length);
+/* Pack characters into .genomecomp blocks (A=0 C=1 G=2 T=3, 32 nt per
+ * {high, low, flags} triple, non-ACGT flagged).  `blocks` must hold
+ * gmapdp_genome_words(length) words. */
+int gmapdp_pack_genome (const char *seq, uint64_t length, uint32_t *blocks);
+/* Upload packed blocks (e.g. Genome_blocks(genome) of a loaded GMAP
+ * genome) to HBM.  nwords as returned by gmapdp_genome_words. */
+int gmapdp_set_genome (gmapdp_ctx *ctx, const uint32_t *blocks, size_t nwords, uint64_t length);
+
+/* Run n Dynprog_single_gap problems.  Host arrays in, host arrays out
+ * (the engine stages them through pinned device buffers).  `pairs` must
+ * have room for gmapdp_single_pair_capacity(problems, n) records; result
+ * i's pairs are pairs[results[i].pair_offset .. +npairs). */
+int gmapdp_single_gap_batch (gmapdp_ctx *ctx, const gmapdp_single_problem *problems, int n,
+                             const char *qseq, const char *qseq_uc, size_t qbytes,
+                             gmapdp_result *results, gmapdp_pair *pairs, size_t pair_capacity);
+size_t gmapdp_single_pair_capacity (const gmapdp_single_problem *problems, int n);
+
+/* Device-resident path for pipelined callers and throughput measurement.
+ * gmapdp_plan_single resolves penalties, bands and launch classes once on
+ * the host (problems resolved on the host -- the size guard -- are written
+ * to host_results immediately) and uploads the descriptors.
+ * gmapdp_plan_run then launches asynchronously on `stream` (a hipStream_t;
+ * NULL = the context's stream) against device-resident query arenas; GPU
+ * results land in d_results[gmapdp_plan_dev_index(plan, i)] and pairs in
+ * d_pairs (capacity gmapdp_plan_pair_capacity). */
+typedef struct gmapdp_plan gmapdp_plan;
+int gmapdp_plan_single (gmapdp_ctx *ctx, const gmapdp_single_problem *problems, int n,
+                        gmapdp_result *host_results, gmapdp_plan **plan);
+size_t gmapdp_plan_pair_capacity (const gmapdp_plan *plan);
+int gmapdp_plan_gpu_problems (const gmapdp_plan *plan);
+int gmapdp_plan_dev_index (const gmapdp_plan *plan, int i);
+int gmapdp_plan_nlaunches (const gmapdp_plan *plan);
+int gmapdp_plan_run (gmapdp_ctx *ctx, const gmapdp_plan *plan, const char *d_qseq, const char *d_qseq_uc,
+                     gmapdp_result *d_results, gmapdp_pair *d_pairs, void *stream);
+/* Per-launch-class access (one kernel launch per class; for profiling). */
+int gmapdp_plan_launch_info (const gmapdp_plan *plan, int li, int *R, int *dirs_lds, int *count, size_t *lds);
+int gmapdp_plan_run_launch (gmapdp_ctx *ctx, const gmapdp_plan *plan, int li, const char *d_qseq,
+                            const char *d_qseq_uc, gmapdp_result *d_results, gmapdp_pair *d_pairs, void *stream);
+void gmapdp_plan_destroy (gmapdp_plan *plan);
+/* The context's HIP stream (hipStream_t). */
+void *gmapdp_stream (gmapdp_ctx *ctx);
+
+void gmapdp_compute_bands (int *lband, int *uband, int rlength, int glength, int extraband, int widebandp);
+
+/* Last error message for this context (static storage). */
+const char *gmapdp_last_error (gmapdp_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

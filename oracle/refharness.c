@@ -28,6 +28,7 @@
 #include "pairpool.h"
 #include "sequence.h"
 #include "genome.h"
+#include "compress-write.h"
 #include "dynprog.h"
 #include "dynprog_single.h"
 #include "dynprog_end.h"
@@ -143,6 +144,38 @@ refh_single_gap (const char *rsequence, const char *rsequenceuc, int rlength, in
   return n;
 }
 
+/* CPU baseline loop for bench.py: the reference's Dynprog_single_gap over a
+   batch laid out like include/gmapdp.h's gmapdp_single_problem array (the
+   struct is restated here; bench.py passes the same bytes to both).  Returns
+   the total number of pairs produced. */
+typedef struct {
+  int qoff, rlength, glength, roffset, goffset;
+  unsigned int chroffset, chrhigh;
+  int flags, genestrand, extraband;
+  double defect_rate;
+  int dynprogindex, pad_;
+} RefSingleProblem;
+
+long
+refh_single_gap_batch (const RefSingleProblem *probs, int n, const char *qseq, const char *qseq_uc) {
+  long total = 0;
+  int i, dpi, finalscore, nmatches, nmismatches, nopens, nindels;
+  List_T pairs;
+  for (i = 0; i < n; i++) {
+    const RefSingleProblem *p = &probs[i];
+    Pairpool_reset(pairpool);
+    dpi = p->dynprogindex;
+    pairs = Dynprog_single_gap(&dpi, &finalscore, &nmatches, &nmismatches, &nopens, &nindels, dynprogM,
+                               (char *) qseq + p->qoff, (char *) qseq_uc + p->qoff, p->rlength, p->glength,
+                               p->roffset, p->goffset, (Univcoord_T) p->chroffset, (Univcoord_T) p->chrhigh,
+                               (p->flags & 1) ? true : false, p->genestrand, (p->flags & 2) ? true : false,
+                               genome, genome, pairpool, p->extraband, (p->flags & 4) ? true : false,
+                               p->defect_rate);
+    total += List_length(pairs);
+  }
+  return total;
+}
+
 /* endalign: 0 QUERYEND_GAP, 1 QUERYEND_INDELS, 2 QUERYEND_NOGAPS, 3 BEST_LOCAL (dynprog.h:23) */
 int
 refh_end_gap (int end3p, const char *rsequence, const char *rsequenceuc, int rlength, int glength,
@@ -204,6 +237,22 @@ refh_consistent (int genestrand, unsigned char *out128x128) {
   int i, j;
   for (i = 0; i < 128; i++) for (j = 0; j < 128; j++) out128x128[i * 128 + j] = consistent_array[genestrand][i][j] ? 1 : 0;
   return 0;
+}
+
+/* The reference's .genomecomp packing of a user segment
+   (Compress_create_blocks_comp, compress-write.c:754): nwords = (len+31)/32*3 + 4. */
+int
+refh_pack_genome (const char *seq, unsigned int length, unsigned int *out) {
+  Genomecomp_T *blocks;
+  char *copy = (char *) malloc(length + 1);
+  size_t nw = ((size_t) (length + 31) / 32) * 3 + 4, i;
+  memcpy(copy, seq, length);
+  copy[length] = '\0';
+  blocks = Compress_create_blocks_comp(copy, (Univcoord_T) length);
+  for (i = 0; i < nw; i++) out[i] = blocks[i];
+  FREE(blocks);
+  free(copy);
+  return (int) nw;
 }
 
 int

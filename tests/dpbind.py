@@ -171,6 +171,55 @@ def single_gap_problem(rng, genome: bytes, maxlen=400, chrhigh=None):
                 dynprogindex=rng.choice([1, 5, -1, -7]))
 
 
+def edge_single_gap_problem(rng, genome: bytes):
+    """Stress shapes: wide bands (several band words per lane), long segments
+    (directions spilled out of LDS), genome skips >= 9 (gap holders), banded
+    problems whose band misses the corner, and chromosome-boundary segments."""
+    kind = rng.randrange(6)
+    p = single_gap_problem(rng, genome, maxlen=2000)
+    g = genome
+    if kind == 0:    # wide band: R = 2..8
+        p["extraband"] = rng.choice([40, 70, 130, 250])
+    elif kind == 1:  # long segments (max_rlength 660 / max_glength 2000)
+        glength = rng.randint(700, 2000)
+        goffset = rng.randint(1, len(g) - glength - 1)
+        seg = g[goffset:goffset + glength] if p["watsonp"] else revcomp(g[len(g) - goffset - glength + 1:len(g) - goffset + 1])
+        cut = rng.randint(0, max(0, glength - 660))
+        q, uc = mutate(rng, seg[cut:cut + rng.randint(200, 660)], sub=0.03, indel=0.01)
+        q, uc = q[:660], uc[:660]
+        p.update(q=q, quc=uc, rlength=len(q), glength=glength, goffset=goffset, widebandp=1,
+                 extraband=rng.choice([6, 14]))
+    elif kind == 2:  # big deletion inside -> genome skip >= 9 (gap holder) or long E chain
+        seg_len = rng.randint(60, 400)
+        goffset = rng.randint(1, len(g) - seg_len - 1)
+        seg = g[goffset:goffset + seg_len] if p["watsonp"] else revcomp(g[len(g) - goffset - seg_len + 1:len(g) - goffset + 1])
+        a = rng.randint(5, seg_len // 2)
+        d = rng.randint(3, min(60, seg_len - a - 2))
+        q = seg[:a] + seg[a + d:]
+        p.update(q=q, quc=q, rlength=len(q), glength=seg_len, goffset=goffset, widebandp=1,
+                 extraband=rng.choice([3, 6, 14]))
+    elif kind == 3:  # big insertion -> long F chain
+        seg_len = rng.randint(40, 300)
+        goffset = rng.randint(1, len(g) - seg_len - 1)
+        seg = g[goffset:goffset + seg_len] if p["watsonp"] else revcomp(g[len(g) - goffset - seg_len + 1:len(g) - goffset + 1])
+        a = rng.randint(1, seg_len - 1)
+        ins = bytes(rng.choice(b"ACGT") for _ in range(rng.randint(1, 80)))
+        q = seg[:a] + ins + seg[a:]
+        q = q[:660]
+        p.update(q=q, quc=q, rlength=len(q), glength=seg_len, goffset=goffset, widebandp=1,
+                 extraband=rng.choice([3, 6, 14]))
+    elif kind == 4:  # narrow band that may not reach the corner
+        p["widebandp"] = 0
+        p["extraband"] = rng.choice([0, 1, 2, 3])
+    else:            # chromosome boundary
+        glength = rng.randint(5, 200)
+        goffset = len(g) - glength + rng.randint(-3, 10)
+        if not p["watsonp"]:
+            goffset = min(goffset, len(g) + 1)
+        p.update(glength=glength, goffset=goffset)
+    return p
+
+
 def call_single(impl, p):
     return impl.single_gap(p["q"], p["quc"], p["rlength"], p["glength"], p["roffset"], p["goffset"],
                            p["chroffset"], p["chrhigh"], p["watsonp"], p["genestrand"], p["jump_late_p"],

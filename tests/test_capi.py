@@ -1,0 +1,81 @@
+"""CPU tests of the product library's C ABI (no device compute here)."""
+import ctypes as C
+import os
+import random
+
+import numpy as np
+import pytest
+
+import gmapdp
+from dpbind import REF_SO, ref_available
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def test_library_exports_every_header_symbol():
+    lib = gmapdp.load_library()
+    syms = gmapdp.exported_symbols()
+    assert "gmapdp_single_gap_batch" in syms and "gmapdp_plan_run" in syms
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert missing == []
+
+
+def read_fasta(path):
+    seq = []
+    for line in open(path, "rb"):
+        if not line.startswith(b">"):
+            seq.append(line.strip())
+    return b"".join(seq)
+
+
+def test_pack_genome_matches_gmap_build_golden():
+    """tests/setup.genomecomp.ok is gmap_build's .genomecomp for ss.chr17test
+    (reference tests/setup1.test.in:15-26)."""
+    seq = read_fasta(os.path.join(HERE, "golden", "ss.chr17test.fa"))
+    ok = np.fromfile(os.path.join(HERE, "golden", "setup.genomecomp.ok"), dtype="<u4")
+    mine = gmapdp.pack_genome(seq)
+    nb = (len(seq) + 31) // 32
+    assert np.array_equal(mine[:3 * nb], ok[:3 * nb])
+    # gmap_build appends one extra {high, low} pair of all-ones (compress-write.c:640-643)
+    assert np.all(ok[3 * nb:] == 0xFFFFFFFF) and np.all(mine[3 * nb:] == 0xFFFFFFFF)
+
+
+@pytest.mark.skipif(not ref_available("nosimd"), reason="reference objects not built")
+def test_pack_genome_matches_reference_compressor():
+    lib = C.CDLL(REF_SO["nosimd"])
+    rng = random.Random(5)
+    for n in [1, 5, 31, 32, 33, 64, 100, 999, 4097]:
+        s = bytes(rng.choice(b"ACGTacgtNnXx") if rng.random() < 0.2 else rng.choice(b"ACGT") for _ in range(n))
+        ref = np.zeros(gmapdp.load_library().gmapdp_genome_words(n), dtype=np.uint32)
+        lib.refh_pack_genome(s, n, ref.ctypes.data_as(C.c_void_p))
+        assert np.array_equal(ref, gmapdp.pack_genome(s)), n
+
+
+def test_compute_bands():
+    lib = gmapdp.load_library()
+    lb, ub = C.c_int(), C.c_int()
+    # Dynprog_compute_bands (dynprog.c:1247)
+    for r, g, eb, wide, exp in [(10, 20, 3, 1, (3, 13)), (20, 10, 3, 1, (13, 3)), (20, 10, 3, 0, (3, 3)),
+                                (7, 7, 0, 1, (0, 0))]:
+        lib.gmapdp_compute_bands(C.byref(lb), C.byref(ub), r, g, eb, wide)
+        assert (lb.value, ub.value) == exp
+
+
+def test_engine_fails_loudly_without_device():
+    """No CPU fallback on the product path: without a HIP device the engine refuses to start."""
+    try:
+        import torch
+        has_gpu = torch.cuda.is_available()
+    except Exception:
+        has_gpu = False
+    if has_gpu:
+        pytest.skip("a GPU is present")
+    with pytest.raises(gmapdp.GmapdpError):
+        gmapdp.Engine(0)
+
+
+def test_problem_struct_layout():
+    assert C.sizeof(gmapdp.SingleProblem) == 56
+    assert C.sizeof(gmapdp.Result) == 32
+    assert gmapdp.PAIR_DTYPE.itemsize == 16
+    assert gmapdp.PROBLEM_DTYPE.itemsize == 56

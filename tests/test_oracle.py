@@ -1,0 +1,95 @@
+"""CPU tests: the oracle (oracle/gmapdp_oracle.c) is pinned to the reference.
+
+1. against the committed golden vectors (generated from the reference's own
+   nosimd objects by tests/golden/make_golden.py) -- always runs;
+2. against the reference objects themselves on fresh seeded problems --
+   runs where oracle/_ref was built (this container, or any box the built
+   .so files travelled to).
+"""
+import ctypes as C
+import os
+import random
+
+import numpy as np
+import pytest
+
+from dpbind import (Oracle, Ref, call_single, edge_single_gap_problem, random_genome, ref_available,
+                    single_gap_problem, ORACLE_SO, REF_SO)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden", "single_gap_golden.npz")
+
+
+def _golden():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(HERE, "golden", "make_golden.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m.load(GOLDEN)
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    if not os.path.exists(ORACLE_SO):
+        pytest.fail("oracle not built: run __graft_entry__.build() (make -C oracle)")
+    return Oracle()
+
+
+def test_oracle_matches_golden(oracle):
+    g, probs, outs = _golden()
+    oracle.set_genome(g)
+    exp = outs["ref_nosimd"]
+    assert len(probs) == len(exp) == 1600
+    bad = [i for i, p in enumerate(probs) if call_single(oracle, p) != exp[i]]
+    assert bad == [], "oracle differs from reference golden on %d problems (first %s)" % (len(bad), bad[:5])
+
+
+def test_golden_covers_edge_cases():
+    g, probs, outs = _golden()
+    exp = outs["ref_nosimd"]
+    nulls = sum(1 for s, p in exp if p is None)
+    gapholders = sum(1 for s, p in exp if p and any(x[9] == 1 for x in p))
+    wide = sum(1 for p in probs if p["widebandp"] and p["extraband"] >= 40)
+    longg = sum(1 for p in probs if p["glength"] > 700)
+    stars = sum(1 for s, p in exp if p and any(x[7] == b"*" for x in p))
+    assert nulls > 0 and gapholders > 20 and wide > 20 and longg > 20 and stars > 0
+
+
+@pytest.mark.skipif(not ref_available("nosimd"), reason="reference objects (oracle/_ref) not built here")
+def test_oracle_vs_reference_random(oracle):
+    ref = Ref("nosimd")
+    rng = random.Random(99)
+    g = random_genome(rng, 30000)
+    ref.set_genome(g)
+    oracle.set_genome(g)
+    bad = 0
+    for i in range(4000):
+        p = single_gap_problem(rng, g) if i % 4 else edge_single_gap_problem(rng, g)
+        if call_single(ref, p) != call_single(oracle, p):
+            bad += 1
+    assert bad == 0
+
+
+@pytest.mark.skipif(not ref_available("nosimd"), reason="reference objects (oracle/_ref) not built here")
+def test_tables_match_reference(oracle):
+    ref = Ref("nosimd")
+    for t in range(4):
+        a = np.zeros(128 * 128, dtype=np.int16)
+        b = np.zeros(128 * 128, dtype=np.int16)
+        ref.lib.refh_pairdistance(t, a.ctypes.data_as(C.c_void_p))
+        oracle.lib.orc_pairdistance(t, b.ctypes.data_as(C.c_void_p))
+        assert np.array_equal(a, b), "pairdistance type %d" % t
+    a = np.zeros(128 * 128, dtype=np.uint8)
+    b = np.zeros(128 * 128, dtype=np.uint8)
+    ref.lib.refh_consistent(0, a.ctypes.data_as(C.c_void_p))
+    oracle.lib.orc_consistent(0, b.ctypes.data_as(C.c_void_p))
+    assert np.array_equal(a, b)
+
+
+@pytest.mark.skipif(not ref_available("nosimd"), reason="reference objects (oracle/_ref) not built here")
+def test_reference_harness_has_no_unresolved_gmap_symbols():
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--undefined-only", REF_SO["nosimd"]], capture_output=True, text=True).stdout
+    und = [l.split()[-1] for l in out.splitlines() if l.strip()]
+    und = [s for s in und if not s.startswith("_") and "@" not in s and s not in ("gzgetc",)]
+    assert und == [], und
