@@ -185,39 +185,47 @@ def main():
         R, dl, cnt, lds = C.c_int(), C.c_int(), C.c_int(), C.c_size_t()
         lib.gmapdp_plan_launch_info(plan, li, C.byref(R), C.byref(dl), C.byref(cnt), C.byref(lds))
         info.append((R.value, dl.value, cnt.value, lds.value))
-    dominant = max(range(nl), key=lambda i: info[i][2])
-    stream = torch.cuda.current_stream(dev)
+    # the kernel template each launch runs; the dominant kernel is the template with most problems
+    kname = ["single_gap_kernel<R=%d,dirs_lds=%d>" % (i[0], i[1]) for i in info]
+    per_kernel = {}
+    for li in range(nl):
+        per_kernel.setdefault(kname[li], []).append(li)
+    dominant = max(per_kernel, key=lambda k: sum(info[li][2] for li in per_kernel[k]))
+    stream = torch.cuda.Stream(dev)  # a real (non-null) stream: the events below see exactly these launches
 
     def step(ev=None):
         for li in range(nl):
-            if ev is not None and li == dominant:
-                ev[0].record(stream)
+            if ev is not None:
+                ev[li][0].record(stream)
             eng._check(lib.gmapdp_plan_run_launch(eng.h, plan, li, C.c_void_p(d_q.data_ptr()),
                                                   C.c_void_p(d_q.data_ptr()), C.c_void_p(d_res.data_ptr()),
                                                   C.c_void_p(d_pairs.data_ptr()), C.c_void_p(stream.cuda_stream)),
                        "gmapdp_plan_run_launch")
-            if ev is not None and li == dominant:
-                ev[1].record(stream)
+            if ev is not None:
+                ev[li][1].record(stream)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(evs[k])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    with torch.cuda.stream(stream):
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nl)]
+               for _ in range(args.steps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            step(evs[k])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    dom_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    launch_ms = [sum(evs[k][li][0].elapsed_time(evs[k][li][1]) for k in range(args.steps)) / args.steps
+                 for li in range(nl)]
 
     # results of the last pass (for algorithmic byte accounting)
     res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=gmapdp.RESULT_DTYPE)[:ngpu]
@@ -225,23 +233,14 @@ def main():
     gpu_mask = dev_index >= 0
     npairs = np.zeros(nprob, dtype=np.int64)
     npairs[gpu_mask] = res["npairs"][dev_index[gpu_mask]]
-    # bytes of the dominant launch's problems only
-    R0, dl0, cnt0, _ = info[dominant]
-    order_sel = np.zeros(nprob, dtype=bool)
-    Wb = None
-    lb = np.zeros(nprob, dtype=np.int64)
-    # identify problems of the dominant class by recomputing the class key
-    r = probs["rlength"].astype(np.int64)
-    g = probs["glength"].astype(np.int64)
-    W = np.abs(g - r) + 2 * 6 + 1
-    Rk = np.ones(nprob, dtype=np.int64)
-    while True:
-        m = Rk * 64 < W
-        if not m.any():
-            break
-        Rk[m] *= 2
-    dom_sel = gpu_mask & (Rk == R0)
-    dom_bytes = algorithmic_bytes(probs[dom_sel], npairs[dom_sel])
+    dom_launches = per_kernel[dominant]
+    dom_bytes_total = 0
+    for li in dom_launches:
+        members = np.zeros(info[li][2], dtype=np.int32)
+        lib.gmapdp_plan_launch_members(plan, li, members.ctypes.data)
+        dom_bytes_total += algorithmic_bytes(probs[members], npairs[members])
+    dom_ms = sum(launch_ms[li] for li in dom_launches) / len(dom_launches)   # average dispatch duration
+    dom_bytes = dom_bytes_total / len(dom_launches)                          # average bytes per dispatch
     step_bytes = algorithmic_bytes(probs[gpu_mask], npairs[gpu_mask])
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
 
@@ -270,8 +269,9 @@ def main():
         "gcups": banded_cells(probs) * world * args.steps / elapsed / 1e9,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "single_gap_kernel<R=%d,dirs_lds=%d>" % (R0, dl0),
+                     "kernel": dominant, "dispatches_per_step": len(dom_launches),
                      "kernel_ms_per_launch": dom_ms, "algorithmic_bytes_per_launch": dom_bytes,
+                     "launch_ms": launch_ms,
                      "note": "integer VALU/LDS-bound DP; HBM roofline reported as required (DESIGN.md)"},
         "step_algorithmic_bytes": step_bytes,
     }

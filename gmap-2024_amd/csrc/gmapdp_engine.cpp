@@ -144,6 +144,7 @@ struct gmapdp_ctx {
 struct gmapdp_plan_internal {
   std::vector<DevSingle> dev;        // one per GPU problem
   std::vector<int> dev_index;        // problem index -> dev slot (-1: resolved on host)
+  std::vector<int> dev_problem;      // dev slot -> problem index
   struct Launch { int R; bool dirs_lds; size_t lds; int first, count; };
   std::vector<Launch> launches;
   std::vector<int> order;            // dev slots grouped by launch
@@ -301,6 +302,7 @@ static int plan_single(gmapdp_ctx* ctx, const gmapdp_single_problem* pr, int n, 
                        gmapdp_plan_internal& plan) {
   plan.dev.clear();
   plan.dev_index.assign(n, -1);
+  plan.dev_problem.clear();
   plan.launches.clear();
   plan.order.clear();
   size_t pair_off = 0, gdirs_off = 0;
@@ -369,6 +371,7 @@ static int plan_single(gmapdp_ctx* ctx, const gmapdp_single_problem* pr, int n, 
       gdirs_off += ((size_t)(p.glength + 1) * 4 * R * 8 + 255) & ~(size_t)255;
     }
     plan.dev_index[i] = (int)plan.dev.size();
+    plan.dev_problem.push_back(i);
     classes[std::make_tuple(R, dirs_lds ? 1 : 0, lds_bucket(lds))].push_back((int)plan.dev.size());
     plan.dev.push_back(d);
     pair_off += (size_t)p.rlength + (size_t)p.glength + 2;
@@ -537,6 +540,13 @@ int gmapdp_plan_launch_info(const gmapdp_plan* plan, int li, int* R, int* dirs_l
   if (dirs_lds) *dirs_lds = L.dirs_lds ? 1 : 0;
   if (count) *count = L.count;
   if (lds) *lds = L.lds;
+  return GMAPDP_OK;
+}
+
+int gmapdp_plan_launch_members(const gmapdp_plan* plan, int li, int* problem_indices) {
+  if (!plan || li < 0 || li >= (int)plan->in.launches.size() || !problem_indices) return GMAPDP_EINVAL;
+  const auto& L = plan->in.launches[li];
+  for (int k = 0; k < L.count; k++) problem_indices[k] = plan->in.dev_problem[plan->in.order[L.first + k]];
   return GMAPDP_OK;
 }
 

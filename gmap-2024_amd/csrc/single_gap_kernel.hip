@@ -434,14 +434,18 @@ __global__ __launch_bounds__(64) void single_gap_kernel(
         E[i] = kNegInf32;
       }
     }
-    if (lane < 4 * R) {
-      const int t = lane / R, i = lane % R;
-      uint64_t m = 0;
 #pragma unroll
-      for (int ii = 0; ii < R; ii++) {
-        if (ii == i) m = (t == 0) ? mH[ii] : (t == 1) ? mV[ii] : (t == 2) ? mE[ii] : mF[ii];
+    for (int w0 = 0; w0 < 4 * R; w0 += 64) {  // 4R words per column, 64 lanes per pass
+      const int w = w0 + lane;
+      if (w < 4 * R) {
+        const int t = w / R, i = w % R;
+        uint64_t m = 0;
+#pragma unroll
+        for (int ii = 0; ii < R; ii++) {
+          if (ii == i) m = (t == 0) ? mH[ii] : (t == 1) ? mV[ii] : (t == 2) ? mE[ii] : mF[ii];
+        }
+        dirs[((size_t)c * 4 + t) * R + i] = m;
       }
-      dirs[((size_t)c * 4 + t) * R + i] = m;
     }
   }
   if (DIRS_LDS) __syncthreads();

@@ -150,6 +150,8 @@ int gmapdp_plan_run (gmapdp_ctx *ctx, const gmapdp_plan *plan, const char *d_qse
                      gmapdp_result *d_results, gmapdp_pair *d_pairs, void *stream);
 /* Per-launch-class access (one kernel launch per class; for profiling). */
 int gmapdp_plan_launch_info (const gmapdp_plan *plan, int li, int *R, int *dirs_lds, int *count, size_t *lds);
+/* Original problem indices of launch li (count entries, launch order). */
+int gmapdp_plan_launch_members (const gmapdp_plan *plan, int li, int *problem_indices);
 int gmapdp_plan_run_launch (gmapdp_ctx *ctx, const gmapdp_plan *plan, int li, const char *d_qseq,
                             const char *d_qseq_uc, gmapdp_result *d_results, gmapdp_pair *d_pairs, void *stream);
 void gmapdp_plan_destroy (gmapdp_plan *plan);
