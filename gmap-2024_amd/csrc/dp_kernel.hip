@@ -1,0 +1,644 @@
+// dp_kernel.hip -- CDNA4 (gfx950) kernel for GMAP's Dynprog_single_gap,
+// Dynprog_end5_gap and Dynprog_end3_gap (nosimd semantics).
+//
+// One 64-lane wavefront (= one workgroup) owns one DP sub-problem.  Reference
+// semantics restated (paths under the reference tree's src/):
+//   Dynprog_single_gap      dynprog_single.c:429-676 (simple path :346-425)
+//   Dynprog_end5/3_gap      dynprog_end.c:1294-1647 / 1924-2247
+//   find_best_endpoint_*    dynprog_end.c:297-587, traceback_nogaps :649
+//   Dynprog_standard        dynprog.c:1268-1786 (fill: recurrence, band, boundary
+//                           rows/columns, >= vs > tie rule, clamp, revp)
+//   Dynprog_traceback_std   dynprog.c:1796-1948
+//   Pairpool_add_queryskip / _add_genomeskip / _push_gapholder  pairpool.c:981/1068/375
+//   Genome_get_segment_right/_left, get_genomic_nt   genome.c:11023/11079, dynprog_single.c:116
+//
+// Design (not a translation of the reference's column loop):
+//  * Band-major lanes: lane L holds band offsets k = L*R .. L*R+R-1 of the
+//    current genome column c (row r = c - uband + k).  The diagonal input of a
+//    cell is the same band offset one column back (a register), the E
+//    (horizontal) input is band offset k+1 one column back (one DPP
+//    wave_shl:1), and the vertical F chain -- the only intra-column
+//    dependence -- is resolved with a max-plus prefix scan across the wave
+//    (DPP row_shr/row_bcast), using F(r) = ext + max(F(r-1), H'(r-1)+open),
+//    valid because open <= 0 (H' = max(diag+pair, E), the H value before F).
+//  * Ties: "a wins over b" is `a > b - late` with late in {0,1} (>= for jump
+//    late, > otherwise), one compare per decision.
+//  * Direction bits never leave the CU: per column four 64-bit ballots
+//    (nogap=HORIZ, nogap=VERT, Egap=HORIZ, Fgap=VERT) go to LDS (or, for the
+//    rare very long / very wide problems, to an L2-resident scratch).
+//  * End gaps track the best endpoint per lane during the fill and reduce it
+//    across the wave with the reference's scan-order tie rule.
+//  * Traceback is wave-cooperative: each run (diagonal run, E chain, F chain)
+//    is found with one ballot over 64 candidate cells, and its Pair records
+//    are expanded by all 64 lanes and stream-compacted straight to HBM in the
+//    reference's List_T order.
+//  * The genome segment is decoded in-kernel from the HBM-resident packed
+//    .genomecomp blocks (3 x u32 per 32 nt).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gmapdp_internal.h"
+#include "../../include/gmapdp.h"
+
+namespace gmapdp {
+
+constexpr int kSent = -(1 << 28);  // scan identity, far below any reachable score
+
+__device__ __forceinline__ int dpp_wave_shl1(int x, int fill) {
+  // lane i <- lane i+1; lane 63 <- fill
+  return __builtin_amdgcn_update_dpp(fill, x, 0x130, 0xf, 0xf, false);
+}
+__device__ __forceinline__ int dpp_wave_shr1(int x, int fill) {
+  // lane i <- lane i-1; lane 0 <- fill
+  return __builtin_amdgcn_update_dpp(fill, x, 0x138, 0xf, 0xf, false);
+}
+
+// Inclusive max-scan over the 64 lanes (lane order).  Lanes without a source
+// keep their own value (old = x), which is the max identity for that step.
+__device__ __forceinline__ int wave_scan_max(int x) {
+  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x111, 0xf, 0xf, false));  // row_shr:1
+  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x112, 0xf, 0xf, false));  // row_shr:2
+  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x114, 0xf, 0xf, false));  // row_shr:4
+  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x118, 0xf, 0xf, false));  // row_shr:8
+  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return x;
+}
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ int lanes_below(uint64_t m, int lane) {
+  return __popcll(m & ((1ull << lane) - 1ull));
+}
+
+// ---- genome access (.genomecomp: {high nt16-31, low nt0-15, flags} per 32 nt) ----
+__device__ __forceinline__ char decode_nt(const uint32_t* __restrict__ blocks, uint64_t nwords, uint32_t pos) {
+  const uint64_t ptr = (uint64_t)(pos >> 5) * 3u;
+  if (ptr + 2 >= nwords) return 'N';  // beyond the allocation (reference: undefined)
+  const uint32_t bit = pos & 31u;
+  if ((blocks[ptr + 2] >> bit) & 1u) return 'N';
+  const uint32_t w = (bit < 16) ? blocks[ptr + 1] : blocks[ptr];
+  const uint32_t x = (w >> (2u * (bit & 15u))) & 3u;
+  return (char)((0x54474341u >> (8u * x)) & 0xffu);  // "ACGT"
+}
+__device__ __forceinline__ char compl_nt(char c) {
+  // only A C G T N * occur: complement of ACGT via a 4-entry table, N and * unchanged
+  return (c == 'A') ? 'T' : (c == 'C') ? 'G' : (c == 'G') ? 'C' : (c == 'T') ? 'A' : c;
+}
+__device__ __forceinline__ uint8_t gclass(char c) {
+  return (c == 'A') ? kA : (c == 'C') ? kC : (c == 'G') ? kG : (c == 'T') ? kT : (c == '*') ? kStar : kN;
+}
+// get_genomic_nt (dynprog_single.c:116; Univcoord_T is 32-bit)
+__device__ __forceinline__ char genomic_nt(const uint32_t* __restrict__ blocks, uint64_t nwords, int genomicpos,
+                                           uint32_t chroffset, uint32_t chrhigh, bool watson) {
+  const uint32_t pos = watson ? chroffset + (uint32_t)genomicpos : chrhigh - (uint32_t)genomicpos;
+  if (pos < chroffset || pos >= chrhigh) return '*';
+  const char c = decode_nt(blocks, nwords, pos);
+  return watson ? c : compl_nt(c);
+}
+// Character i of Genome_get_segment_right(left=pos, L, chrhigh=bound) or
+// Genome_get_segment_left(right=pos, L, chroffset=bound), optionally
+// reverse-complemented (genome.c:11023-11135).
+__device__ __forceinline__ char segment_nt(const uint32_t* __restrict__ blocks, uint64_t nwords, uint32_t i,
+                                           uint32_t L, uint32_t pos, uint32_t bound, bool leftvariant,
+                                           bool revcomp) {
+  const uint32_t j = revcomp ? L - 1u - i : i;  // index into the forward segment
+  char c;
+  if (!leftvariant) {
+    const uint32_t left = pos, chrhigh = bound;
+    if (left >= chrhigh) return '*';
+    if (left + L >= chrhigh && j + (left + L - chrhigh) >= L) return '*';
+    c = decode_nt(blocks, nwords, left + j);
+  } else {
+    const uint32_t right = pos, chroffset = bound;
+    if (right < chroffset) return '*';
+    if (right < chroffset + L && j < chroffset + L - right) return '*';
+    c = decode_nt(blocks, nwords, right - L + j);
+  }
+  return revcomp ? compl_nt(c) : c;
+}
+
+// ---- LDS carve (must match lds_bytes_dp on the host) ----
+__host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+struct Carve {
+  size_t sc, q, quc, gch, gcls, dirs, total;
+};
+__host__ __device__ inline Carve carve_dp(int rlength, int glength, int R, bool dirs_lds) {
+  Carve cv;
+  size_t off = 0;
+  const size_t srow = (size_t)(rlength + 2);
+  cv.sc = off;   off = align16(off + (size_t)kNClass * srow);  // int8 sc[class][row], rows 0..rlength+1
+  cv.q = off;    off = align16(off + (size_t)(rlength + 1));
+  cv.quc = off;  off = align16(off + (size_t)(rlength + 1));
+  cv.gch = off;  off = align16(off + (size_t)(glength + 1));
+  cv.gcls = off; off = align16(off + (size_t)(glength + 1));
+  cv.dirs = off;
+  if (dirs_lds) off = align16(off + (size_t)(glength + 1) * 4u * (size_t)R * 8u);
+  cv.total = off;
+  return cv;
+}
+
+// direction planes: [c][t][i] 64-bit masks; t: 0 nogap=HORIZ, 1 nogap=VERT, 2 Egap=HORIZ, 3 Fgap=VERT;
+// band offset k lives in word i = k % R at bit k / R.
+template <int R>
+__device__ __forceinline__ uint32_t dir_bit(const uint64_t* dirs, int c, int t, int k, int W) {
+  if (k < 0 || k >= W) return 0u;  // outside the band: cleared to DIAG (dynprog.c:498)
+  const uint64_t m = dirs[((size_t)c * 4 + t) * R + (k % R)];
+  return (uint32_t)(m >> (k / R)) & 1u;
+}
+
+struct Tally {
+  int score, nmatches, nmismatches, nopens, nindels, count;
+  int lead;        // leading INDEL records (dropped by the end gaps)
+  bool seen;       // a non-INDEL record has been emitted
+};
+
+__device__ __forceinline__ void put_pair(gmapdp_pair* __restrict__ out, int idx, int querypos, int genomepos, int jump,
+                                         char cdna, char comp, char genome, char genomealt) {
+  int4 v;
+  v.x = querypos;
+  v.y = genomepos;
+  v.z = jump;
+  v.w = (int)((uint32_t)(uint8_t)cdna | ((uint32_t)(uint8_t)comp << 8) | ((uint32_t)(uint8_t)genome << 16) |
+              ((uint32_t)(uint8_t)genomealt << 24));
+  reinterpret_cast<int4*>(out)[idx] = v;
+}
+
+struct Geo {  // coordinate transform of a problem (revp flips both axes)
+  int roffset, goffset, sgn;
+  __device__ int qpos(int r) const { return roffset + sgn * (r - 1); }
+  __device__ int gpos(int c) const { return goffset + sgn * (c - 1); }
+};
+
+// Diagonal run: cells (r-j, c-j), j in [0, n)  (dynprog.c:1861-1915, traceback_nogaps)
+__device__ __forceinline__ void emit_diag(int lane, int r, int c, int n, const Geo& G, const char* q, const char* quc,
+                                          const char* gch, const uint8_t* __restrict__ cons, gmapdp_pair* out,
+                                          Tally& t) {
+  for (int base = 0; base < n; base += 64) {
+    const int j = base + lane;
+    const bool active = j < n;
+    bool notstar = false, good = false, matchish = false, amb = false;
+    int qp = 0, gp = 0;
+    char c1 = 0, c2 = 0;
+    if (active) {
+      const int rr = r - j, cc = c - j;
+      c1 = q[rr];
+      const char c1u = quc[rr];
+      c2 = gch[cc];
+      notstar = c2 != '*';
+      if (c1u == c2) {
+        matchish = true;
+      } else if (cons[(uint8_t)(c1u & 127) * kNClass + gclass(c2)]) {
+        matchish = true;
+        amb = true;
+      }
+      qp = G.qpos(rr);
+      gp = G.gpos(cc);
+      good = notstar && qp >= 0 && gp >= 0;
+    }
+    const uint64_t mgood = ballot(good);
+    t.nmatches += __popcll(ballot(active && notstar && matchish));
+    t.nmismatches += __popcll(ballot(active && notstar && !matchish));
+    if (good) {
+      put_pair(out, t.count + lanes_below(mgood, lane), qp, gp, 0, c1, matchish ? (amb ? ':' : '*') : ' ', c2, c2);
+    }
+    t.count += __popcll(mgood);
+    if (mgood) t.seen = true;
+  }
+}
+
+// Query skip: Pairpool_add_queryskip(pairs, rs, c, dist, ...) (pairpool.c:981): rows rs, rs-1, ...
+__device__ __forceinline__ void emit_queryskip(int lane, int rs, int c, int dist, const Geo& G, const char* q,
+                                               gmapdp_pair* out, Tally& t) {
+  const int gp = G.gpos(c);
+  for (int base = 0; base < dist; base += 64) {
+    const int j = base + lane;
+    const bool active = j < dist;
+    const int rr = rs - j;
+    const int qp = G.qpos(rr);
+    const bool good = active && qp >= 0 && gp >= 0;
+    const uint64_t mgood = ballot(good);
+    if (good) put_pair(out, t.count + lanes_below(mgood, lane), qp, gp, 0, q[rr], '-', ' ', ' ');
+    const int nw = __popcll(mgood);
+    t.count += nw;
+    if (!t.seen) t.lead += nw;
+  }
+  t.score += kQopen + dist * kQindel;
+  t.nopens += 1;
+  t.nindels += dist;
+}
+
+// Genome skip: Pairpool_add_genomeskip(&add_dashes_p, pairs, r, cs, dist, NULL, ...) (pairpool.c:1068):
+// columns cs, cs-1, ...; dist >= 9 gives one gap holder
+__device__ __forceinline__ void emit_genomeskip(int lane, int r, int cs, int dist, const Geo& G, bool watson,
+                                                uint32_t chroffset, uint32_t chrhigh, const uint32_t* blocks,
+                                                uint64_t nwords, gmapdp_pair* out, Tally& t) {
+  if (dist >= kMicrointronLength) {
+    if (lane == 0) put_pair(out, t.count, -1, -1, dist, ' ', ' ', ' ', ' ');
+    t.count += 1;
+    t.seen = true;
+    return;
+  }
+  const int qp = G.qpos(r);
+  for (int base = 0; base < dist; base += 64) {
+    const int j = base + lane;
+    const bool active = j < dist;
+    const int gp = G.gpos(cs - j);
+    const bool good = active && qp >= 0 && gp >= 0;
+    const uint64_t mgood = ballot(good);
+    if (good) {
+      const char c2 = genomic_nt(blocks, nwords, gp, chroffset, chrhigh, watson);
+      put_pair(out, t.count + lanes_below(mgood, lane), qp, gp, 0, ' ', '-', c2, c2);
+    }
+    const int nw = __popcll(mgood);
+    t.count += nw;
+    if (!t.seen) t.lead += nw;
+  }
+  t.score += kTopen + dist * kTindel;
+  t.nopens += 1;
+  t.nindels += dist;
+}
+
+// 64-bit max across the wave (used once per problem for the best endpoint).
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const uint64_t y = __shfl_xor(x, off, 64);
+    x = y > x ? y : x;
+  }
+  return x;
+}
+
+template <int R, bool DIRS_LDS>
+__global__ __launch_bounds__(64) void dp_kernel(
+    const DevProblem* __restrict__ probs, const int* __restrict__ order,
+    const uint32_t* __restrict__ blocks, uint64_t nwords,
+    const char* __restrict__ qseq, const char* __restrict__ qseq_uc,
+    const int8_t* __restrict__ sctab, const uint8_t* __restrict__ constab,
+    gmapdp_result* __restrict__ results, gmapdp_pair* __restrict__ pairs,
+    uint64_t* __restrict__ gdirs) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x;
+  const int pid = order[blockIdx.x];
+  const DevProblem P = probs[pid];
+  const int rlen = P.rlength, glen = P.glength;
+  const int flags = P.flags;
+  const bool watson = flags & kFWatson;
+  const int late = (flags & kFLate) ? 1 : 0;
+  const bool rev = flags & kFRev;
+  const int kind = P.kind;
+  const Carve cv = carve_dp(rlen, glen, R, DIRS_LDS);
+  int8_t* sc = reinterpret_cast<int8_t*>(smem + cv.sc);
+  char* q = reinterpret_cast<char*>(smem + cv.q);
+  char* quc = reinterpret_cast<char*>(smem + cv.quc);
+  char* gch = reinterpret_cast<char*>(smem + cv.gch);
+  uint8_t* gcl = reinterpret_cast<uint8_t*>(smem + cv.gcls);
+  uint64_t* dirs = DIRS_LDS ? reinterpret_cast<uint64_t*>(smem + cv.dirs)
+                            : reinterpret_cast<uint64_t*>(reinterpret_cast<unsigned char*>(gdirs) + P.dirs_offset);
+  const int8_t* sct = sctab + (size_t)P.mismatchtype * 128 * kNClass;
+  const uint8_t* cons = constab + (size_t)P.genestrand * 128 * kNClass;
+  gmapdp_pair* out = pairs + P.pair_offset;
+  const Geo G{P.roffset, P.goffset, rev ? -1 : 1};
+  const int srow = rlen + 2;
+
+  // ---- stage query (DP row order), per-class score rows and the genome segment in LDS ----
+  const int qstep = rev ? -1 : 1;
+  const bool score_uc = flags & kFScoreUC;
+  for (int i = lane; i < rlen; i += 64) {
+    const char c1 = qseq[P.qbase + qstep * i];
+    const char c1u = qseq_uc[P.qbase + qstep * i];
+    q[i + 1] = c1;
+    quc[i + 1] = c1u;
+    const uint64_t row = *reinterpret_cast<const uint64_t*>(sct + (uint8_t)((score_uc ? c1u : c1) & 127) * kNClass);
+#pragma unroll
+    for (int g = 0; g < 6; g++) sc[g * srow + i + 1] = (int8_t)(row >> (8 * g));
+  }
+  if (lane < 6) {  // rows 0 and rlength+1 are never scored but keep the clamped reads defined
+    sc[lane * srow] = 0;
+    sc[lane * srow + rlen + 1] = 0;
+  }
+  const bool segleft = flags & kFSegLeft, segrc = flags & kFSegRevcomp;
+  for (int i = lane; i < glen; i += 64) {
+    const char c2 = segment_nt(blocks, nwords, (uint32_t)i, (uint32_t)glen, P.segpos, P.segbound, segleft, segrc);
+    const int c = rev ? glen - i : i + 1;  // end5 walks the segment from its right end
+    gch[c] = c2;
+    gcl[c] = gclass(c2);
+  }
+  __syncthreads();
+
+  Tally t = {0, 0, 0, 0, 0, 0, 0, false};
+  const int dpi_next = P.dynprogindex + (P.dynprogindex > 0 ? 1 : -1);
+  const int endalign = P.endalign;
+  const bool is_end = kind != kSingle;
+
+  // ---- single_gap_simple (dynprog_single.c:346, taken when glength == rlength) ----
+  if (kind == kSingle && glen == rlen) {
+    int nmism = 0;
+    for (int base = 0; base < rlen; base += 64) {
+      const int r = base + lane + 1;
+      bool mism = false;
+      if (r <= rlen) {
+        const char c1u = quc[r], c2 = gch[r];
+        mism = (c2 != '*') && (c1u != c2) && !cons[(uint8_t)(c1u & 127) * kNClass + gclass(c2)];
+      }
+      nmism += __popcll(ballot(mism));
+    }
+    if (nmism <= 1) {
+      // pushes r = 1..rlength without List_reverse: list order is r = rlength .. 1, a diagonal run
+      emit_diag(lane, rlen, rlen, rlen, G, q, quc, gch, cons, out, t);
+      if (lane == 0) {
+        gmapdp_result res;
+        res.npairs = t.count;
+        res.pair_offset = P.pair_offset;
+        res.traceback_score = t.nmatches * kMatch + t.nmismatches * kMismatch;
+        res.nmatches = t.nmatches;
+        res.nmismatches = t.nmismatches;
+        res.nopens = 0;
+        res.nindels = 0;
+        res.dynprogindex = dpi_next;
+        results[pid] = res;
+      }
+      return;
+    }
+  }
+
+  const int lband = P.lband, uband = P.uband, open = P.open, ext = P.extend;
+  const int W = lband + uband + 1;
+  int bestr = 0, bestc = 0;
+
+  if (!(is_end && endalign == kQueryendNogaps)) {
+    // ---- banded fill (Dynprog_standard, upperp = lowerp = true, saturation NEG_INFINITY_INT) ----
+    const int sat = kNegInf32;
+    const bool track_all = is_end && (endalign == kQueryendGap || endalign == kBestLocal);
+    const bool track_row = is_end && endalign == kQueryendIndels;
+    const int binit = track_row ? kNegInf32 : 0;
+    int Hs[R], E[R], bv[R], bcol[R];
+#pragma unroll
+    for (int i = 0; i < R; i++) {  // column 0 (dynprog.c:1331-1369)
+      const int k = lane * R + i;
+      const int r = k - uband;
+      int v = kNegInf32;
+      if (k < W && r >= 0 && r <= rlen) v = (r == 0) ? 0 : (r <= lband ? open + r * ext : kNegInf32);
+      Hs[i] = v;
+      E[i] = kNegInf32;
+      bv[i] = binit;
+      bcol[i] = 0;
+    }
+    // Hs holds the stored nogap value (clamped at `sat`) except on band offset 0, whose only reader is
+    // itself as the diagonal of the band-top row, which the reference takes unclamped (first_nogap).
+    for (int c = 1; c <= glen; c++) {
+      const int gi = gcl[c];
+      const int rtop = c - uband;
+      const int rlo = rtop < 1 ? 1 : rtop;
+      const int rhigh = (c + lband) < rlen ? (c + lband) : rlen;
+      // last_nogap entering row rlo (dynprog.c:1411-1449)
+      const int L0 = (c == 1) ? (kNegInf32 - open + 1) : (c <= uband ? open + c * ext : kNegInf32);
+      const int8_t* scg = sc + gi * srow;
+
+      int Ein[R], Hin[R];
+#pragma unroll
+      for (int i = 0; i < R - 1; i++) { Ein[i] = E[i + 1]; Hin[i] = Hs[i + 1]; }
+      Ein[R - 1] = dpp_wave_shl1(E[0], kNegInf32);
+      Hin[R - 1] = dpp_wave_shl1(Hs[0], kNegInf32);
+
+      int Hp[R], En[R], A[R];
+      bool valid[R], eb[R], hb[R];
+#pragma unroll
+      for (int i = 0; i < R; i++) {
+        const int k = lane * R + i;
+        const int r = rtop + k;
+        valid[i] = (k < W) && (r >= rlo) && (r <= rhigh);
+        const int s = scg[min(max(r, 0), rlen + 1)];
+        // Egap (dynprog.c:1518-1524)
+        const int es = Hin[i] + open;
+        eb[i] = Ein[i] > es - late;
+        En[i] = max(Ein[i], es) + ext;
+        const int dg = Hs[i] + s;
+        hb[i] = En[i] > dg - late;
+        Hp[i] = max(En[i], dg);
+        A[i] = valid[i] ? Hp[i] + open - r * ext : kSent;
+      }
+      // F chain: F(r) = r*ext + max(init, max_{rlo<=j<r} (H'(j) + open - j*ext))
+      int pre[R];
+      pre[0] = A[0];
+#pragma unroll
+      for (int i = 1; i < R; i++) pre[i] = max(pre[i - 1], A[i]);
+      const int X = dpp_wave_shr1(wave_scan_max(pre[R - 1]), kSent);
+      const int init = max(kNegInf32, L0 + open) - (rlo - 1) * ext;
+      int F[R], Hun[R];
+      bool vb[R];
+#pragma unroll
+      for (int i = 0; i < R; i++) {
+        const int r = rtop + lane * R + i;
+        const int ex = (i == 0) ? X : max(X, pre[i - 1]);
+        F[i] = r * ext + max(init, ex);
+        vb[i] = F[i] > Hp[i] - late;
+        Hun[i] = max(F[i], Hp[i]);
+      }
+      // Fgap direction needs F(r-1), H(r-1) of this column (dynprog.c:1486-1492)
+      const int Fup = dpp_wave_shr1(F[R - 1], kNegInf32);
+      const int Hup = dpp_wave_shr1(Hun[R - 1], kNegInf32);
+      uint64_t mH[R], mV[R], mE[R], mF[R];
+#pragma unroll
+      for (int i = 0; i < R; i++) {
+        const int k = lane * R + i;
+        const int r = rtop + k;
+        int fprev = (i == 0) ? Fup : F[i - 1];
+        int hprev = (i == 0) ? Hup : Hun[i - 1];
+        if (r == rlo) { fprev = kNegInf32; hprev = L0; }
+        const bool fb = fprev > hprev + open - late;
+        mV[i] = ballot(valid[i] && vb[i]);
+        mH[i] = ballot(valid[i] && hb[i] && !vb[i]);
+        mE[i] = ballot(valid[i] && eb[i]);
+        mF[i] = ballot(valid[i] && fb);
+        const int Hc = max(Hun[i], sat);
+        if (valid[i]) {
+          Hs[i] = (k == 0) ? Hun[i] : Hc;
+          E[i] = En[i];
+          // best endpoint (find_best_endpoint_std / _to_queryend_indels_std): scan-order first/last max
+          if ((track_all || (track_row && r == rlen)) && Hc > bv[i] - late) { bv[i] = Hc; bcol[i] = c; }
+        } else {
+          Hs[i] = (r == 0 && c <= uband) ? open + c * ext : kNegInf32;  // row 0 (dynprog.c:1318-1325)
+          E[i] = kNegInf32;
+        }
+      }
+#pragma unroll
+      for (int w0 = 0; w0 < 4 * R; w0 += 64) {  // 4R words per column, 64 lanes per pass
+        const int w = w0 + lane;
+        if (w < 4 * R) {
+          const int tt = w / R, i = w % R;
+          uint64_t m = 0;
+#pragma unroll
+          for (int ii = 0; ii < R; ii++) {
+            if (ii == i) m = (tt == 0) ? mH[ii] : (tt == 1) ? mV[ii] : (tt == 2) ? mE[ii] : mF[ii];
+          }
+          dirs[((size_t)c * 4 + tt) * R + i] = m;
+        }
+      }
+    }
+    if (is_end) {
+      // reduce the endpoint over the wave: key orders (score, r, c) so that the max key is the
+      // reference's choice (> keeps the first in r-major scan order, >= the last)
+      uint64_t key = 0;
+#pragma unroll
+      for (int i = 0; i < R; i++) {
+        if (bcol[i] > 0) {
+          const int r = bcol[i] - uband + lane * R + i;
+          const uint32_t rk = late ? (uint32_t)r : 4095u - (uint32_t)r;
+          const uint32_t ck = late ? (uint32_t)bcol[i] : 4095u - (uint32_t)bcol[i];
+          const uint64_t kk = ((uint64_t)(uint32_t)(bv[i] + (1 << 30)) << 24) | ((uint64_t)rk << 12) | ck;
+          key = kk > key ? kk : key;
+        }
+      }
+      key = wave_max_u64(key);
+      if (key == 0) {
+        bestr = track_row ? rlen : 0;
+        bestc = 0;
+      } else {
+        const uint32_t rk = (uint32_t)(key >> 12) & 4095u, ck = (uint32_t)key & 4095u;
+        bestr = late ? (int)rk : 4095 - (int)rk;
+        bestc = late ? (int)ck : 4095 - (int)ck;
+      }
+    } else {
+      bestr = rlen;
+      bestc = glen;
+    }
+    if (DIRS_LDS) __syncthreads();
+    else __threadfence_block();
+  } else {
+    bestr = bestc = glen < rlen ? glen : rlen;  // find_best_endpoint_to_queryend_nogaps
+  }
+
+  const bool skip = is_end && endalign != kQueryendNogaps && (flags & kFRequirePos);
+  if (is_end && endalign == kQueryendNogaps) {
+    emit_diag(lane, bestr, bestc, bestr, G, q, quc, gch, cons, out, t);  // traceback_nogaps
+  } else if (!skip) {
+    // ---- wave-cooperative traceback (Dynprog_traceback_std, dynprog.c:1796-1948) ----
+    int r = bestr, c = bestc;
+    while (r > 0 && c > 0) {
+      const int k = r - c + uband;
+      const uint32_t isV = dir_bit<R>(dirs, c, 1, k, W);
+      const uint32_t isH = dir_bit<R>(dirs, c, 0, k, W);
+      if (!isV && isH) {
+        // E chain along row r: columns c, c-1, ... while Egap == HORIZ
+        int n = 0;
+        for (int base = 0;; base += 64) {
+          const int j = base + lane;
+          const bool cont = (c - j >= 1) && dir_bit<R>(dirs, c - j, 2, k + j, W);
+          const uint64_t stop = ~ballot(cont);
+          if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
+        }
+        const int dist = n + 1;
+        const int c_end = (c - n - 1) > 0 ? (c - n - 1) : 0;
+        emit_genomeskip(lane, r, c_end + dist, dist, G, watson, P.chroffset, P.chrhigh, blocks, nwords, out, t);
+        c = c_end;
+      } else if (isV) {
+        // F chain up column c: rows r, r-1, ... while Fgap == VERT
+        int n = 0;
+        for (int base = 0;; base += 64) {
+          const int j = base + lane;
+          const bool cont = (r - j >= 1) && dir_bit<R>(dirs, c, 3, k - j, W);
+          const uint64_t stop = ~ballot(cont);
+          if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
+        }
+        const int dist = n + 1;
+        const int r_end = (r - n - 1) > 0 ? (r - n - 1) : 0;
+        emit_queryskip(lane, r_end + dist, c, dist, G, q, out, t);
+        r = r_end;
+      } else {
+        // diagonal run at fixed band offset k
+        int n = 0;
+        for (int base = 0;; base += 64) {
+          const int j = base + lane;
+          const bool inrange = (c - j >= 1) && (r - j >= 1);
+          const bool cont = (j == 0) || (inrange && !dir_bit<R>(dirs, c - j, 0, k, W) &&
+                                         !dir_bit<R>(dirs, c - j, 1, k, W));
+          const uint64_t stop = ~ballot(cont && inrange);
+          if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
+        }
+        emit_diag(lane, r, c, n, G, q, quc, gch, cons, out, t);
+        r -= n;
+        c -= n;
+      }
+    }
+    if (r == 0 && c == 0) {
+    } else if (c == 0) {
+      emit_queryskip(lane, r, 1, r, G, q, out, t);  // LAZY_INDEL
+    } else {
+      emit_genomeskip(lane, 1, c, c, G, watson, P.chroffset, P.chrhigh, blocks, nwords, out, t);
+    }
+  }
+
+  int score = t.score + t.nmatches * kMatch + t.nmismatches * kMismatch;
+  int first = 0, npairs = t.count;
+  if (is_end) {
+    if ((endalign == kQueryendGap || endalign == kBestLocal) && (t.nmatches + 1) < t.nmismatches) {
+      score = 0;  // dynprog_end.c:1623-1626: list dropped, counters kept
+      npairs = 0;
+    } else {
+      first = t.lead;  // INDEL pairs at the far end removed (dynprog_end.c:1629-1632)
+      npairs = t.count - t.lead;
+      if (kind == kEnd5 && npairs > 1) {
+        // Dynprog_end5_gap returns List_reverse of that list (dynprog_end.c:1646)
+        __threadfence_block();
+        int4* recs = reinterpret_cast<int4*>(out + first);
+        for (int a = lane; a < npairs / 2; a += 64) {
+          const int b = npairs - 1 - a;
+          const int4 x = recs[a], y = recs[b];
+          recs[a] = y;
+          recs[b] = x;
+        }
+      }
+    }
+  }
+  if (lane == 0) {
+    gmapdp_result res;
+    res.npairs = npairs;
+    res.pair_offset = P.pair_offset + first;
+    res.traceback_score = score;
+    res.nmatches = t.nmatches;
+    res.nmismatches = t.nmismatches;
+    res.nopens = t.nopens;
+    res.nindels = t.nindels;
+    res.dynprogindex = dpi_next;
+    results[pid] = res;
+  }
+}
+
+// ---- host-side launch table ----
+template <int R, bool D>
+static void* kptr() { return reinterpret_cast<void*>(&dp_kernel<R, D>); }
+
+size_t lds_bytes_dp(int rlength, int glength, int R, bool dirs_lds) {
+  return carve_dp(rlength, glength, R, dirs_lds).total;
+}
+
+hipError_t launch_dp(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevProblem* probs,
+                     const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
+                     const char* qseq_uc, const int8_t* sctab, const uint8_t* constab, gmapdp_result* results,
+                     gmapdp_pair* pairs, uint64_t* gdirs) {
+  void* fn = nullptr;
+#define GMAPDP_CASE(RR)                                          \
+  case RR:                                                       \
+    fn = dirs_lds ? kptr<RR, true>() : kptr<RR, false>();        \
+    break;
+  switch (R) {
+    GMAPDP_CASE(1)
+    GMAPDP_CASE(2)
+    GMAPDP_CASE(4)
+    GMAPDP_CASE(8)
+    GMAPDP_CASE(16)
+    GMAPDP_CASE(32)
+    GMAPDP_CASE(64)
+    default: return hipErrorInvalidValue;
+  }
+#undef GMAPDP_CASE
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  void* args[] = {(void*)&probs, (void*)&order, (void*)&blocks, (void*)&nwords, (void*)&qseq, (void*)&qseq_uc,
+                  (void*)&sctab, (void*)&constab, (void*)&results, (void*)&pairs, (void*)&gdirs};
+  return hipLaunchKernel(fn, dim3(nblocks), dim3(64), args, lds, stream);
+}
+
+}  // namespace gmapdp

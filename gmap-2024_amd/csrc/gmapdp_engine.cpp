@@ -4,7 +4,9 @@
 // Reference interfaces mirrored (paths under the reference tree's src/):
 //   Dynprog_init / permute_cases  dynprog.c:903-1197  (score + consistency tables)
 //   Dynprog_compute_bands         dynprog.c:1247
-//   Dynprog_single_gap prologue   dynprog_single.c:459-521 (penalties, size guard)
+//   Dynprog_single_gap prologue   dynprog_single.c:459-521 (penalties, size guard, segment)
+//   Dynprog_end5/3_gap prologues  dynprog_end.c:1333-1411 / 1962-2027 (penalties, chopping,
+//                                 NULL cases, segment orientation, bands per endalign)
 //   Compress_create_blocks_comp   compress-write.c:754  (.genomecomp packing)
 #include <hip/hip_runtime.h>
 
@@ -13,19 +15,19 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
-#include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "gmapdp_internal.h"
 #include "../../include/gmapdp.h"
 
 namespace gmapdp {
-size_t lds_bytes_single(int rlength, int glength, int R, bool dirs_lds);
-hipError_t launch_single(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevSingle* probs,
-                         const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
-                         const char* qseq_uc, const int8_t* sctab, const uint8_t* constab, gmapdp_result* results,
-                         gmapdp_pair* pairs, uint64_t* gdirs);
+size_t lds_bytes_dp(int rlength, int glength, int R, bool dirs_lds);
+hipError_t launch_dp(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevProblem* probs,
+                     const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
+                     const char* qseq_uc, const int8_t* sctab, const uint8_t* constab, gmapdp_result* results,
+                     gmapdp_pair* pairs, uint64_t* gdirs);
 
 // ---------------------------------------------------------------------------
 // Score tables.  The reference builds pairdistance_array[4][128][128] and
@@ -51,10 +53,10 @@ static void build_tables(Tables& T, int mode) {
   for (int a = 'A'; a <= 'z'; a++)
     for (int b = 'A'; b < 'z'; b++)
       for (int t = 0; t < 4; t++) T.pd[t][a][b] = (short)kMismatchScore[t];
-  auto mark = [&](int strandset, int a, int b) {
+  auto mark = [&](int a, int b) {
     if (stranded(mode)) {
-      if (strandset) T.cons[0][a][b] = 1;
-    } else if (strandset) {
+      T.cons[0][a][b] = 1;
+    } else {
       T.cons[1][a][b] = 1;
       T.cons[2][a][b] = 1;
     }
@@ -63,7 +65,7 @@ static void build_tables(Tables& T, int mode) {
   auto both = [&](int A, int B, short s) {
     const int a = std::tolower(A), b = std::tolower(B);
     const int v[4][2] = {{a, b}, {a, B}, {A, b}, {A, B}};
-    for (auto& p : v) { mark(1, p[0], p[1]); mark(1, p[1], p[0]); }
+    for (auto& p : v) { mark(p[0], p[1]); mark(p[1], p[0]); }
     for (int t = 0; t < 4; t++)
       for (auto& p : v) { T.pd[t][p[0]][p[1]] = s; T.pd[t][p[1]][p[0]] = s; }
   };
@@ -141,8 +143,9 @@ struct gmapdp_ctx {
   std::string err;
 };
 
-struct gmapdp_plan_internal {
-  std::vector<DevSingle> dev;        // one per GPU problem
+// A batch resolved on the host: GPU problems grouped into launch classes.
+struct PlanCore {
+  std::vector<DevProblem> dev;       // one per GPU problem
   std::vector<int> dev_index;        // problem index -> dev slot (-1: resolved on host)
   std::vector<int> dev_problem;      // dev slot -> problem index
   struct Launch { int R; bool dirs_lds; size_t lds; int first, count; };
@@ -157,6 +160,11 @@ static int fail(gmapdp_ctx* ctx, int code, const char* fmt, hipError_t e) {
   std::snprintf(buf, sizeof(buf), fmt, hipGetErrorString(e));
   if (ctx) ctx->err = buf;
   return code;
+}
+
+static int bad(gmapdp_ctx* ctx, const char* msg) {
+  if (ctx) ctx->err = msg;
+  return GMAPDP_EINVAL;
 }
 
 extern "C" {
@@ -227,33 +235,28 @@ int gmapdp_pack_genome(const char* seq, uint64_t length, uint32_t* blocks) {
   const uint64_t nblocks = (length + 31) / 32;
   const size_t nw = gmapdp_genome_words(length);
   std::memset(blocks, 0, nw * sizeof(uint32_t));
-  if (nblocks) {
-    blocks[3 * nblocks - 3] = blocks[3 * nblocks - 2] = blocks[3 * nblocks - 1] = 0xFFFFFFFFu;
-  }
   for (int i = 0; i < 4; i++) blocks[3 * nblocks + i] = 0xFFFFFFFFu;
   for (uint64_t b = 0; b < nblocks; b++) {
     uint32_t high = 0, low = 0, flags = 0;
     const uint64_t base = b * 32;
     const int n = (int)std::min<uint64_t>(32, length - base);
-    for (int j = 0; j < n; j++) {
+    for (int j = 0; j < 32; j++) {
       uint32_t code;
-      switch (seq[base + j]) {
-        case 'A': case 'a': code = 0; break;
-        case 'C': case 'c': code = 1; break;
-        case 'G': case 'g': code = 2; break;
-        case 'T': case 't': code = 3; break;
-        case 'X': case 'x': code = 3; flags |= 1u << j; break;  // put_compressed_one: 'X' = T code + flag
-        default: code = 0; flags |= 1u << j; break;            // 'N' and anything else: A code + flag
+      if (j >= n) {  // tail of the last block reads as 'X'
+        code = 3;
+        flags |= 1u << j;
+      } else {
+        switch (seq[base + j]) {
+          case 'A': case 'a': code = 0; break;
+          case 'C': case 'c': code = 1; break;
+          case 'G': case 'g': code = 2; break;
+          case 'T': case 't': code = 3; break;
+          case 'X': case 'x': code = 3; flags |= 1u << j; break;  // put_compressed_one: 'X' = T code + flag
+          default: code = 0; flags |= 1u << j; break;            // 'N' and anything else: A code + flag
+        }
       }
       if (j < 16) low |= code << (2 * j);
       else high |= code << (2 * (j - 16));
-    }
-    if (n < 32) {  // tail of the last block reads as 'X' (all bits set)
-      for (int j = n; j < 32; j++) {
-        flags |= 1u << j;
-        if (j < 16) low |= 3u << (2 * j);
-        else high |= 3u << (2 * (j - 16));
-      }
     }
     blocks[3 * b] = high;
     blocks[3 * b + 1] = low;
@@ -279,9 +282,9 @@ int gmapdp_set_genome(gmapdp_ctx* ctx, const uint32_t* blocks, size_t nwords, ui
 }  // extern "C"
 
 // ---------------------------------------------------------------------------
-// Planning: resolve host-side cases (size guard), derive penalties and bands
-// (dynprog_single.c:459-521, dynprog.c:1247), pick the launch class and LDS
-// footprint, and lay out the pair arena.
+// Planning: resolve host-side cases, derive penalties, bands, orientation and
+// segment extraction, pick the launch class and LDS footprint, and lay out
+// the pair arena.
 // ---------------------------------------------------------------------------
 static const size_t kLdsBudget = 64 * 1024;  // per workgroup; keeps >= 2 problems resident per CU
 
@@ -298,86 +301,160 @@ static size_t lds_bucket(size_t lds) {
   return lds;
 }
 
-static int plan_single(gmapdp_ctx* ctx, const gmapdp_single_problem* pr, int n, gmapdp_result* results,
-                       gmapdp_plan_internal& plan) {
-  plan.dev.clear();
-  plan.dev_index.assign(n, -1);
-  plan.dev_problem.clear();
-  plan.launches.clear();
-  plan.order.clear();
-  size_t pair_off = 0, gdirs_off = 0;
-  std::map<std::tuple<int, int, size_t>, std::vector<int>> classes;
-  for (int i = 0; i < n; i++) {
-    const gmapdp_single_problem& p = pr[i];
-    gmapdp_result& res = results[i];
-    const int dpi_next = p.dynprogindex + (p.dynprogindex > 0 ? 1 : -1);
-    res.pair_offset = (int32_t)pair_off;
-    if (p.rlength <= 0 || p.glength <= 0 || p.rlength > GMAPDP_MAX_RLENGTH || p.glength > GMAPDP_MAX_GLENGTH) {
-      // size guard (dynprog_single.c:509-521)
-      res.npairs = 0;
-      res.traceback_score = GMAPDP_NEG_INFINITY_32;
-      res.nmatches = res.nmismatches = res.nopens = res.nindels = 0;
-      res.dynprogindex = dpi_next;
-      continue;
-    }
-    DevSingle d;
-    d.qoff = p.qoff;
-    d.rlength = p.rlength;
-    d.glength = p.glength;
-    d.roffset = p.roffset;
-    d.goffset = p.goffset;
-    d.chroffset = p.chroffset;
-    d.chrhigh = p.chrhigh;
-    const double dr = p.defect_rate;
-    d.mismatchtype = dr < 0.003 ? kHighQ : (dr < 0.014 ? kMedQ : kLowQ);  // DEFECT_HIGHQ / DEFECT_MEDQ
-    if (ctx->user_dynprog_p) {
-      d.open = ctx->user_open;
-      d.extend = ctx->user_extend;
-    } else if (dr < 0.003) {
-      d.open = -8; d.extend = -3;  // SINGLE_OPEN/EXTEND_HIGHQ
-    } else if (dr < 0.014) {
-      d.open = -7; d.extend = -2;
+static void null_result(gmapdp_result& res, int score, int dpi) {
+  res.npairs = 0;
+  res.traceback_score = score;
+  res.nmatches = res.nmismatches = res.nopens = res.nindels = 0;
+  res.dynprogindex = dpi;
+}
+
+static int next_dpi(int dpi) { return dpi + (dpi > 0 ? 1 : -1); }
+
+// Dynprog_single_gap (dynprog_single.c:459-592): returns 1 if the problem runs on the GPU.
+static int convert_single(const gmapdp_ctx* ctx, const gmapdp_single_problem& p, gmapdp_result& res, DevProblem& d) {
+  if (p.rlength <= 0 || p.glength <= 0 || p.rlength > GMAPDP_MAX_RLENGTH || p.glength > GMAPDP_MAX_GLENGTH) {
+    null_result(res, GMAPDP_NEG_INFINITY_32, next_dpi(p.dynprogindex));  // size guard (:509-521)
+    return 0;
+  }
+  std::memset(&d, 0, sizeof(d));
+  d.kind = kSingle;
+  d.qbase = p.qoff;
+  d.rlength = p.rlength;
+  d.glength = p.glength;
+  d.roffset = p.roffset;
+  d.goffset = p.goffset;
+  d.chroffset = p.chroffset;
+  d.chrhigh = p.chrhigh;
+  const double dr = p.defect_rate;
+  d.mismatchtype = dr < 0.003 ? kHighQ : (dr < 0.014 ? kMedQ : kLowQ);  // DEFECT_HIGHQ / DEFECT_MEDQ
+  if (ctx->user_dynprog_p) {
+    d.open = ctx->user_open;
+    d.extend = ctx->user_extend;
+  } else if (dr < 0.003) {
+    d.open = -8; d.extend = -3;  // SINGLE_OPEN/EXTEND_HIGHQ
+  } else if (dr < 0.014) {
+    d.open = -7; d.extend = -2;
+  } else {
+    d.open = -6; d.extend = -1;
+  }
+  const bool watson = p.flags & GMAPDP_WATSON;
+  d.flags = (watson ? kFWatson : 0) | ((p.flags & GMAPDP_JUMP_LATE) ? kFLate : 0);
+  if (watson) {
+    d.segpos = p.chroffset + (uint32_t)p.goffset;  // Genome_get_segment_right(left, chrhigh)
+    d.segbound = p.chrhigh;
+  } else {
+    d.segpos = p.chrhigh - (uint32_t)p.goffset + 1u;  // Genome_get_segment_left(right, chroffset), revcomp
+    d.segbound = p.chroffset;
+    d.flags |= kFSegLeft | kFSegRevcomp;
+  }
+  gmapdp_compute_bands(&d.lband, &d.uband, p.rlength, p.glength, p.extraband, p.flags & GMAPDP_WIDEBAND);
+  d.genestrand = p.genestrand;
+  d.dynprogindex = p.dynprogindex;
+  d.endalign = 0;
+  return 1;
+}
+
+// Dynprog_end5_gap / Dynprog_end3_gap prologues (dynprog_end.c:1333-1411 / 1962-2027).
+static int convert_end(gmapdp_ctx* ctx, const gmapdp_end_problem& p, gmapdp_result& res, DevProblem& d,
+                       int* err) {
+  *err = 0;
+  const bool end3 = p.end3p != 0;
+  const bool nogaps = p.endalign == kQueryendNogaps;
+  if (p.endalign < 0 || p.endalign > 3) {
+    *err = bad(ctx, "endalign out of range");
+    return 0;
+  }
+  int rlength = p.rlength, glength = p.glength;
+  if (rlength <= 0) { null_result(res, 0, p.dynprogindex); return 0; }
+  if (!nogaps && rlength > GMAPDP_MAX_RLENGTH) rlength = GMAPDP_MAX_RLENGTH;
+  if (!end3 && p.goffset < 0) { null_result(res, 0, p.dynprogindex); return 0; }
+  if (glength <= 0) { null_result(res, 0, p.dynprogindex); return 0; }
+  if (!nogaps && glength > GMAPDP_MAX_GLENGTH) glength = GMAPDP_MAX_GLENGTH;
+  if (end3 && p.goffset < 0) {
+    *err = bad(ctx, "Dynprog_end3_gap with goffset < 0 (the reference asserts)");
+    return 0;
+  }
+  std::memset(&d, 0, sizeof(d));
+  d.kind = end3 ? kEnd3 : kEnd5;
+  d.endalign = p.endalign;
+  d.rlength = rlength;
+  d.glength = glength;
+  d.roffset = p.roffset;
+  d.goffset = p.goffset;
+  d.chroffset = p.chroffset;
+  d.chrhigh = p.chrhigh;
+  d.mismatchtype = kEndQ;
+  const double dr = p.defect_rate;
+  if (ctx->user_dynprog_p) {
+    d.open = ctx->user_open;
+    d.extend = ctx->user_extend;
+  } else {
+    d.open = dr < 0.003 ? -10 : (dr < 0.014 ? -8 : -6);  // END_OPEN_HIGHQ/MEDQ/LOWQ
+    d.extend = -2;                                        // END_EXTEND_*
+  }
+  const bool watson = p.flags & GMAPDP_WATSON;
+  const bool jl = p.flags & GMAPDP_JUMP_LATE;
+  d.flags = (watson ? kFWatson : 0) | (p.require_pos_score_p ? kFRequirePos : 0);
+  if (end3) {
+    d.qbase = p.qoff;
+    d.flags |= (jl ? kFLate : 0) | kFScoreUC;  // end3 fills on rsequenceuc (dynprog_end.c:2061)
+    if (watson) {
+      d.segpos = p.chroffset + (uint32_t)p.goffset;
+      d.segbound = p.chrhigh;
     } else {
-      d.open = -6; d.extend = -1;
+      d.segpos = p.chrhigh - (uint32_t)p.goffset + 1u;
+      d.segbound = p.chroffset;
+      d.flags |= kFSegLeft | kFSegRevcomp;
     }
-    if (d.open > 0) {
-      ctx->err = "positive gap-open penalty is not supported by the scan formulation";
-      return GMAPDP_EINVAL;
+  } else {
+    d.qbase = p.qoff + p.rlength - 1;          // rev_rsequence: the slice's last character
+    d.flags |= (jl ? 0 : kFLate) | kFRev;      // fills with !jump_late_p, revp
+    if (watson) {
+      d.segpos = p.chroffset + (uint32_t)p.goffset + 1u;  // Genome_get_segment_left(right, chroffset)
+      d.segbound = p.chroffset;
+      d.flags |= kFSegLeft;
+    } else {
+      d.segpos = p.chrhigh - (uint32_t)p.goffset;  // Genome_get_segment_right(left, chrhigh), revcomp
+      d.segbound = p.chrhigh;
+      d.flags |= kFSegRevcomp;
     }
-    int lb, ub;
-    gmapdp_compute_bands(&lb, &ub, p.rlength, p.glength, p.extraband, p.flags & GMAPDP_WIDEBAND);
-    if (lb < 0 || ub < 0) {
-      ctx->err = "negative band";
-      return GMAPDP_EINVAL;
-    }
-    d.lband = lb;
-    d.uband = ub;
-    d.flags = p.flags;
-    d.genestrand = p.genestrand;
-    d.dynprogindex = p.dynprogindex;
+  }
+  if (!nogaps)
+    gmapdp_compute_bands(&d.lband, &d.uband, rlength, glength, p.extraband,
+                         /*widebandp*/ p.endalign != kQueryendIndels);
+  d.genestrand = p.genestrand;
+  d.dynprogindex = p.dynprogindex;
+  return 1;
+}
+
+static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
+  std::map<std::tuple<int, int, size_t>, std::vector<int>> classes;
+  size_t pair_off = 0, gdirs_off = 0;
+  for (size_t s = 0; s < plan.dev.size(); s++) {
+    DevProblem& d = plan.dev[s];
     d.pair_offset = (int32_t)pair_off;
-    const int W = lb + ub + 1;
-    const int R = pick_R(W);
-    if (R > kMaxR) {
-      ctx->err = "band wider than 4096";
-      return GMAPDP_EINVAL;
-    }
-    size_t lds = lds_bytes_single(p.rlength, p.glength, R, true);
-    bool dirs_lds = lds <= kLdsBudget;
+    pair_off += (size_t)d.rlength + (size_t)d.glength + 2;
+    const bool nofill = d.kind != kSingle && d.endalign == kQueryendNogaps;
+    if (d.open > 0 && !nofill) return bad(ctx, "positive gap-open penalty is not supported by the scan formulation");
+    if (d.lband < 0 || d.uband < 0) return bad(ctx, "negative band");
+    const int W = d.lband + d.uband + 1;
+    const int R = nofill ? 1 : pick_R(W);
+    if (R > kMaxR) return bad(ctx, "band wider than 4096");
+    size_t lds = lds_bytes_dp(d.rlength, d.glength, R, !nofill);
+    bool dirs_lds = !nofill && lds <= kLdsBudget;
     d.dirs_offset = 0;
     if (!dirs_lds) {
-      lds = lds_bytes_single(p.rlength, p.glength, R, false);
-      d.dirs_offset = (int64_t)gdirs_off;
-      gdirs_off += ((size_t)(p.glength + 1) * 4 * R * 8 + 255) & ~(size_t)255;
+      lds = lds_bytes_dp(d.rlength, d.glength, R, false);
+      if (!nofill) {
+        d.dirs_offset = (int64_t)gdirs_off;
+        gdirs_off += ((size_t)(d.glength + 1) * 4 * R * 8 + 255) & ~(size_t)255;
+      }
     }
-    plan.dev_index[i] = (int)plan.dev.size();
-    plan.dev_problem.push_back(i);
-    classes[std::make_tuple(R, dirs_lds ? 1 : 0, lds_bucket(lds))].push_back((int)plan.dev.size());
-    plan.dev.push_back(d);
-    pair_off += (size_t)p.rlength + (size_t)p.glength + 2;
+    if (lds > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
+    classes[std::make_tuple(R, dirs_lds ? 1 : 0, lds_bucket(lds))].push_back((int)s);
   }
   for (auto& kv : classes) {
-    gmapdp_plan_internal::Launch L;
+    PlanCore::Launch L;
     L.R = std::get<0>(kv.first);
     L.dirs_lds = std::get<1>(kv.first) != 0;
     L.lds = std::get<2>(kv.first);
@@ -397,71 +474,88 @@ static int plan_single(gmapdp_ctx* ctx, const gmapdp_single_problem* pr, int n, 
   return GMAPDP_OK;
 }
 
-static int run_plan(gmapdp_ctx* ctx, const gmapdp_plan_internal& plan, const DevSingle* d_probs, const int* d_order,
+// Results: singles first, then ends.
+static int build_plan(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int nsingle,
+                      const gmapdp_end_problem* ends, int nend, gmapdp_result* results, PlanCore& plan) {
+  plan = PlanCore();
+  const int n = nsingle + nend;
+  plan.dev_index.assign(n, -1);
+  for (int i = 0; i < n; i++) {
+    DevProblem d;
+    int gpu, err = 0;
+    if (i < nsingle) gpu = convert_single(ctx, singles[i], results[i], d);
+    else gpu = convert_end(ctx, ends[i - nsingle], results[i], d, &err);
+    if (err) return err;
+    results[i].pair_offset = 0;
+    if (!gpu) continue;
+    plan.dev_index[i] = (int)plan.dev.size();
+    plan.dev_problem.push_back(i);
+    plan.dev.push_back(d);
+  }
+  int rc = classify(ctx, plan);
+  if (rc) return rc;
+  for (size_t s = 0; s < plan.dev.size(); s++) results[plan.dev_problem[s]].pair_offset = plan.dev[s].pair_offset;
+  return GMAPDP_OK;
+}
+
+static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, const DevProblem* d_probs,
+                             const int* d_order, const char* d_q, const char* d_quc, gmapdp_result* d_results,
+                             gmapdp_pair* d_pairs, hipStream_t stream) {
+  const auto& L = plan.launches[li];
+  return launch_dp(L.R, L.dirs_lds, L.count, L.lds, stream, d_probs, d_order + L.first, ctx->d_genome,
+                   ctx->genome_words, d_q, d_quc, ctx->d_sc, ctx->d_cs, d_results, d_pairs,
+                   (uint64_t*)ctx->gdirs.p);
+}
+
+static int run_plan(gmapdp_ctx* ctx, const PlanCore& plan, const DevProblem* d_probs, const int* d_order,
                     const char* d_q, const char* d_quc, gmapdp_result* d_results, gmapdp_pair* d_pairs,
                     hipStream_t stream) {
   if (plan.gdirs_bytes) {
     hipError_t e = ctx->gdirs.ensure(plan.gdirs_bytes);
     if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "direction scratch: %s", e);
   }
-  for (const auto& L : plan.launches) {
-    hipError_t e = launch_single(L.R, L.dirs_lds, L.count, L.lds, stream, d_probs, d_order + L.first, ctx->d_genome,
-                                 ctx->genome_words, d_q, d_quc, ctx->d_sc, ctx->d_cs, d_results, d_pairs,
-                                 (uint64_t*)ctx->gdirs.p);
-    if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "single_gap launch: %s", e);
+  for (size_t li = 0; li < plan.launches.size(); li++) {
+    hipError_t e = launch_one(ctx, plan, (int)li, d_probs, d_order, d_q, d_quc, d_results, d_pairs, stream);
+    if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "dp launch: %s", e);
   }
   return GMAPDP_OK;
 }
 
-extern "C" {
-
-size_t gmapdp_single_pair_capacity(const gmapdp_single_problem* problems, int n) {
-  size_t cap = 0;
-  for (int i = 0; i < n; i++)
-    if (problems[i].rlength > 0 && problems[i].glength > 0) cap += (size_t)problems[i].rlength + problems[i].glength + 2;
-  return cap;
-}
-
-int gmapdp_single_gap_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* problems, int n, const char* qseq,
-                            const char* qseq_uc, size_t qbytes, gmapdp_result* results, gmapdp_pair* pairs,
-                            size_t pair_capacity) {
-  if (!ctx || n < 0 || (n && (!problems || !results))) return GMAPDP_EINVAL;
+// Synchronous host-array batch (both entry-point families).
+static int run_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int nsingle,
+                     const gmapdp_end_problem* ends, int nend, const char* qseq, const char* qseq_uc,
+                     size_t qbytes, gmapdp_result* results, gmapdp_pair* pairs, size_t pair_capacity) {
+  const int n = nsingle + nend;
+  if (!ctx || n < 0 || (n && !results)) return GMAPDP_EINVAL;
   if (!ctx->d_genome) return GMAPDP_ENOGENOME;
   if (n == 0) return GMAPDP_OK;
   (void)hipSetDevice(ctx->device);
-  gmapdp_plan_internal plan;
-  int rc = plan_single(ctx, problems, n, results, plan);
+  PlanCore plan;
+  int rc = build_plan(ctx, singles, nsingle, ends, nend, results, plan);
   if (rc) return rc;
-  if (plan.pair_capacity > pair_capacity) {
-    ctx->err = "pair arena too small";
-    return GMAPDP_EINVAL;
-  }
-  for (int i = 0; i < n; i++) {
-    if (plan.dev_index[i] < 0) continue;
-    if (problems[i].qoff < 0 || (size_t)problems[i].qoff + (size_t)problems[i].rlength > qbytes) {
-      ctx->err = "query slice outside the query arena";
-      return GMAPDP_EINVAL;
-    }
+  if (plan.pair_capacity > pair_capacity) return bad(ctx, "pair arena too small");
+  for (size_t s = 0; s < plan.dev.size(); s++) {
+    const int i = plan.dev_problem[s];
+    const long lo = i < nsingle ? singles[i].qoff : ends[i - nsingle].qoff;
+    const long len = i < nsingle ? singles[i].rlength : ends[i - nsingle].rlength;
+    if (lo < 0 || (size_t)(lo + len) > qbytes) return bad(ctx, "query slice outside the query arena");
   }
   const int ndev = (int)plan.dev.size();
   if (ndev == 0) return GMAPDP_OK;
-  hipError_t e = hipSuccess;
-  if (e == hipSuccess) e = ctx->probs.ensure(sizeof(DevSingle) * ndev);
+  hipError_t e = ctx->probs.ensure(sizeof(DevProblem) * ndev);
   if (e == hipSuccess) e = ctx->order.ensure(sizeof(int) * ndev);
   if (e == hipSuccess) e = ctx->qseq.ensure(qbytes);
   if (e == hipSuccess) e = ctx->qseq_uc.ensure(qbytes);
   if (e == hipSuccess) e = ctx->results.ensure(sizeof(gmapdp_result) * ndev);
   if (e == hipSuccess) e = ctx->pairs.ensure(sizeof(gmapdp_pair) * std::max<size_t>(plan.pair_capacity, 1));
   if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "device buffers: %s", e);
-  // results are written per dev slot; map dev slot -> original index afterwards
-  std::vector<DevSingle> dev = plan.dev;
   hipStream_t s = ctx->stream;
-  e = hipMemcpyAsync(ctx->probs.p, dev.data(), sizeof(DevSingle) * ndev, hipMemcpyHostToDevice, s);
+  e = hipMemcpyAsync(ctx->probs.p, plan.dev.data(), sizeof(DevProblem) * ndev, hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipMemcpyAsync(ctx->order.p, plan.order.data(), sizeof(int) * ndev, hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipMemcpyAsync(ctx->qseq.p, qseq, qbytes, hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipMemcpyAsync(ctx->qseq_uc.p, qseq_uc, qbytes, hipMemcpyHostToDevice, s);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "upload: %s", e);
-  rc = run_plan(ctx, plan, (const DevSingle*)ctx->probs.p, (const int*)ctx->order.p, (const char*)ctx->qseq.p,
+  rc = run_plan(ctx, plan, (const DevProblem*)ctx->probs.p, (const int*)ctx->order.p, (const char*)ctx->qseq.p,
                 (const char*)ctx->qseq_uc.p, (gmapdp_result*)ctx->results.p, (gmapdp_pair*)ctx->pairs.p, s);
   if (rc) return rc;
   std::vector<gmapdp_result> dres(ndev);
@@ -469,12 +563,47 @@ int gmapdp_single_gap_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* proble
   if (e == hipSuccess && pairs && plan.pair_capacity)
     e = hipMemcpyAsync(pairs, ctx->pairs.p, sizeof(gmapdp_pair) * plan.pair_capacity, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "single_gap execution: %s", e);
-  for (int i = 0; i < n; i++) {
-    const int d = plan.dev_index[i];
-    if (d >= 0) results[i] = dres[d];
-  }
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "dp execution: %s", e);
+  for (int d = 0; d < ndev; d++) results[plan.dev_problem[d]] = dres[d];
   return GMAPDP_OK;
+}
+
+static size_t capacity(const gmapdp_single_problem* singles, int nsingle, const gmapdp_end_problem* ends, int nend) {
+  size_t cap = 0;
+  for (int i = 0; i < nsingle; i++)
+    if (singles[i].rlength > 0 && singles[i].glength > 0 && singles[i].rlength <= GMAPDP_MAX_RLENGTH &&
+        singles[i].glength <= GMAPDP_MAX_GLENGTH)
+      cap += (size_t)singles[i].rlength + singles[i].glength + 2;
+  for (int i = 0; i < nend; i++) {
+    const bool nog = ends[i].endalign == kQueryendNogaps;
+    const int r = nog ? ends[i].rlength : std::min(ends[i].rlength, GMAPDP_MAX_RLENGTH);
+    const int g = nog ? ends[i].glength : std::min(ends[i].glength, GMAPDP_MAX_GLENGTH);
+    if (r > 0 && g > 0) cap += (size_t)r + g + 2;
+  }
+  return cap;
+}
+
+extern "C" {
+
+size_t gmapdp_single_pair_capacity(const gmapdp_single_problem* problems, int n) {
+  return capacity(problems, n, nullptr, 0);
+}
+size_t gmapdp_end_pair_capacity(const gmapdp_end_problem* problems, int n) {
+  return capacity(nullptr, 0, problems, n);
+}
+
+int gmapdp_single_gap_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* problems, int n, const char* qseq,
+                            const char* qseq_uc, size_t qbytes, gmapdp_result* results, gmapdp_pair* pairs,
+                            size_t pair_capacity) {
+  if (n > 0 && !problems) return GMAPDP_EINVAL;
+  return run_batch(ctx, problems, n, nullptr, 0, qseq, qseq_uc, qbytes, results, pairs, pair_capacity);
+}
+
+int gmapdp_end_gap_batch(gmapdp_ctx* ctx, const gmapdp_end_problem* problems, int n, const char* qseq,
+                         const char* qseq_uc, size_t qbytes, gmapdp_result* results, gmapdp_pair* pairs,
+                         size_t pair_capacity) {
+  if (n > 0 && !problems) return GMAPDP_EINVAL;
+  return run_batch(ctx, nullptr, 0, problems, n, qseq, qseq_uc, qbytes, results, pairs, pair_capacity);
 }
 
 }  // extern "C"
@@ -484,28 +613,28 @@ int gmapdp_single_gap_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* proble
 // the host, then replayed against device-resident inputs.
 // ---------------------------------------------------------------------------
 struct gmapdp_plan {
-  gmapdp_plan_internal in;
-  DevSingle* d_probs = nullptr;
+  PlanCore in;
+  DevProblem* d_probs = nullptr;
   int* d_order = nullptr;
 };
 
 extern "C" {
 
-int gmapdp_plan_single(gmapdp_ctx* ctx, const gmapdp_single_problem* problems, int n, gmapdp_result* host_results,
-                       gmapdp_plan** out) {
-  if (!ctx || !out || n <= 0 || !problems || !host_results) return GMAPDP_EINVAL;
+int gmapdp_plan_create(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int nsingle,
+                       const gmapdp_end_problem* ends, int nend, gmapdp_result* host_results, gmapdp_plan** out) {
+  if (!ctx || !out || nsingle < 0 || nend < 0 || nsingle + nend <= 0 || !host_results) return GMAPDP_EINVAL;
+  if ((nsingle && !singles) || (nend && !ends)) return GMAPDP_EINVAL;
   (void)hipSetDevice(ctx->device);
   gmapdp_plan* p = new gmapdp_plan();
-  int rc = plan_single(ctx, problems, n, host_results, p->in);
+  int rc = build_plan(ctx, singles, nsingle, ends, nend, host_results, p->in);
   if (rc) {
     delete p;
     return rc;
   }
-  // device results are indexed by dev slot; keep problem order == dev order for this API
   const size_t nd = p->in.dev.size();
-  hipError_t e = hipMalloc(&p->d_probs, sizeof(DevSingle) * std::max<size_t>(nd, 1));
+  hipError_t e = hipMalloc(&p->d_probs, sizeof(DevProblem) * std::max<size_t>(nd, 1));
   if (e == hipSuccess) e = hipMalloc(&p->d_order, sizeof(int) * std::max<size_t>(nd, 1));
-  if (e == hipSuccess && nd) e = hipMemcpy(p->d_probs, p->in.dev.data(), sizeof(DevSingle) * nd, hipMemcpyHostToDevice);
+  if (e == hipSuccess && nd) e = hipMemcpy(p->d_probs, p->in.dev.data(), sizeof(DevProblem) * nd, hipMemcpyHostToDevice);
   if (e == hipSuccess && nd) e = hipMemcpy(p->d_order, p->in.order.data(), sizeof(int) * nd, hipMemcpyHostToDevice);
   if (e == hipSuccess && p->in.gdirs_bytes) e = ctx->gdirs.ensure(p->in.gdirs_bytes);
   if (e != hipSuccess) {
@@ -518,20 +647,17 @@ int gmapdp_plan_single(gmapdp_ctx* ctx, const gmapdp_single_problem* problems, i
   return GMAPDP_OK;
 }
 
+int gmapdp_plan_single(gmapdp_ctx* ctx, const gmapdp_single_problem* problems, int n, gmapdp_result* host_results,
+                       gmapdp_plan** out) {
+  return gmapdp_plan_create(ctx, problems, n, nullptr, 0, host_results, out);
+}
+
 size_t gmapdp_plan_pair_capacity(const gmapdp_plan* plan) { return plan ? plan->in.pair_capacity : 0; }
 int gmapdp_plan_gpu_problems(const gmapdp_plan* plan) { return plan ? (int)plan->in.dev.size() : 0; }
 int gmapdp_plan_dev_index(const gmapdp_plan* plan, int i) {
   return (plan && i >= 0 && i < (int)plan->in.dev_index.size()) ? plan->in.dev_index[i] : -1;
 }
 int gmapdp_plan_nlaunches(const gmapdp_plan* plan) { return plan ? (int)plan->in.launches.size() : 0; }
-
-int gmapdp_plan_run(gmapdp_ctx* ctx, const gmapdp_plan* plan, const char* d_qseq, const char* d_qseq_uc,
-                    gmapdp_result* d_results, gmapdp_pair* d_pairs, void* stream) {
-  if (!ctx || !plan) return GMAPDP_EINVAL;
-  if (!ctx->d_genome) return GMAPDP_ENOGENOME;
-  return run_plan(ctx, plan->in, plan->d_probs, plan->d_order, d_qseq, d_qseq_uc, d_results, d_pairs,
-                  stream ? (hipStream_t)stream : ctx->stream);
-}
 
 int gmapdp_plan_launch_info(const gmapdp_plan* plan, int li, int* R, int* dirs_lds, int* count, size_t* lds) {
   if (!plan || li < 0 || li >= (int)plan->in.launches.size()) return GMAPDP_EINVAL;
@@ -550,15 +676,21 @@ int gmapdp_plan_launch_members(const gmapdp_plan* plan, int li, int* problem_ind
   return GMAPDP_OK;
 }
 
+int gmapdp_plan_run(gmapdp_ctx* ctx, const gmapdp_plan* plan, const char* d_qseq, const char* d_qseq_uc,
+                    gmapdp_result* d_results, gmapdp_pair* d_pairs, void* stream) {
+  if (!ctx || !plan) return GMAPDP_EINVAL;
+  if (!ctx->d_genome) return GMAPDP_ENOGENOME;
+  return run_plan(ctx, plan->in, plan->d_probs, plan->d_order, d_qseq, d_qseq_uc, d_results, d_pairs,
+                  stream ? (hipStream_t)stream : ctx->stream);
+}
+
 int gmapdp_plan_run_launch(gmapdp_ctx* ctx, const gmapdp_plan* plan, int li, const char* d_qseq,
                            const char* d_qseq_uc, gmapdp_result* d_results, gmapdp_pair* d_pairs, void* stream) {
   if (!ctx || !plan || li < 0 || li >= (int)plan->in.launches.size()) return GMAPDP_EINVAL;
   if (!ctx->d_genome) return GMAPDP_ENOGENOME;
-  const auto& L = plan->in.launches[li];
-  hipError_t e = launch_single(L.R, L.dirs_lds, L.count, L.lds, stream ? (hipStream_t)stream : ctx->stream,
-                               plan->d_probs, plan->d_order + L.first, ctx->d_genome, ctx->genome_words, d_qseq,
-                               d_qseq_uc, ctx->d_sc, ctx->d_cs, d_results, d_pairs, (uint64_t*)ctx->gdirs.p);
-  if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "single_gap launch: %s", e);
+  hipError_t e = launch_one(ctx, plan->in, li, plan->d_probs, plan->d_order, d_qseq, d_qseq_uc, d_results, d_pairs,
+                            stream ? (hipStream_t)stream : ctx->stream);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "dp launch: %s", e);
   return GMAPDP_OK;
 }
 

@@ -15,25 +15,43 @@ constexpr int kMaxR = 64;               // band up to 64*64 = 4096 cells wide
 enum GClass : uint8_t { kA = 0, kC = 1, kG = 2, kT = 3, kN = 4, kStar = 5 };
 constexpr int kNClass = 8;              // padded to 8 bytes per score row
 
-// Device-side problem descriptor derived on the host from gmapdp_single_problem
-// (penalties, bands and the launch class are resolved once, in the plan).
-struct DevSingle {
-  int32_t qoff;
-  int32_t rlength;
-  int32_t glength;
-  int32_t roffset;
-  int32_t goffset;
+// Problem kinds (one kernel serves all Dynprog_* fills with a traceback).
+enum Kind : int32_t { kSingle = 0, kEnd5 = 1, kEnd3 = 2 };
+// Endalign_T (dynprog.h:25)
+enum Endalign : int32_t { kQueryendGap = 0, kQueryendIndels = 1, kQueryendNogaps = 2, kBestLocal = 3 };
+
+// DevProblem.flags
+constexpr int32_t kFWatson = 0x1;     // watsonp
+constexpr int32_t kFLate = 0x2;       // tie rule of the fill/endpoint search: >= (jump late) instead of >
+constexpr int32_t kFRequirePos = 0x4; // require_pos_score_p (end gaps)
+constexpr int32_t kFSegLeft = 0x8;    // genome segment via Genome_get_segment_left (else _right)
+constexpr int32_t kFSegRevcomp = 0x10;
+constexpr int32_t kFRev = 0x20;       // revp: DP runs away from the anchor (end5)
+constexpr int32_t kFScoreUC = 0x40;   // the fill scores rsequenceuc (Dynprog_end3_gap) instead of rsequence
+
+// Device-side problem descriptor derived on the host (penalties, bands,
+// orientation and the launch class are resolved once, in the plan).
+struct DevProblem {
+  int32_t qbase;          // arena index of the query character of DP row 1
+  int32_t rlength;        // DP rows (after the reference's chopping)
+  int32_t glength;        // DP columns
+  int32_t roffset;        // querypos of row r = roffset + sgn*(r-1)
+  int32_t goffset;        // genomepos of column c = goffset + sgn*(c-1)
   uint32_t chroffset;
   uint32_t chrhigh;
+  uint32_t segpos;        // left (right variant) or right (left variant) coordinate of the segment
+  uint32_t segbound;      // chrhigh (right variant) or chroffset (left variant)
   int32_t lband;
   int32_t uband;
   int32_t open;
   int32_t extend;
   int32_t mismatchtype;
-  int32_t flags;          // bit0 watson, bit1 jump_late
+  int32_t flags;
   int32_t genestrand;
   int32_t dynprogindex;
   int32_t pair_offset;
+  int32_t kind;
+  int32_t endalign;
   int64_t dirs_offset;    // byte offset into the global direction scratch (global-dirs classes)
 };
 

@@ -32,6 +32,13 @@ class SingleProblem(C.Structure):
                 ("dynprogindex", C.c_int32), ("pad_", C.c_int32)]
 
 
+class EndProblem(C.Structure):
+    _fields_ = [("qoff", C.c_int32), ("rlength", C.c_int32), ("glength", C.c_int32), ("roffset", C.c_int32),
+                ("goffset", C.c_int32), ("chroffset", C.c_uint32), ("chrhigh", C.c_uint32), ("flags", C.c_int32),
+                ("genestrand", C.c_int32), ("extraband", C.c_int32), ("end3p", C.c_int32), ("endalign", C.c_int32),
+                ("require_pos_score_p", C.c_int32), ("dynprogindex", C.c_int32), ("defect_rate", C.c_double)]
+
+
 class Result(C.Structure):
     _fields_ = [("npairs", C.c_int32), ("pair_offset", C.c_int32), ("traceback_score", C.c_int32),
                 ("nmatches", C.c_int32), ("nmismatches", C.c_int32), ("nopens", C.c_int32),
@@ -46,6 +53,11 @@ PROBLEM_DTYPE = np.dtype({"names": [n for n, _ in SingleProblem._fields_],
                                       "<i4", "<i4"],
                           "offsets": [SingleProblem.__dict__[n].offset for n, _ in SingleProblem._fields_],
                           "itemsize": C.sizeof(SingleProblem)})
+END_PROBLEM_DTYPE = np.dtype({"names": [n for n, _ in EndProblem._fields_],
+                              "formats": ["<i4", "<i4", "<i4", "<i4", "<i4", "<u4", "<u4", "<i4", "<i4", "<i4",
+                                          "<i4", "<i4", "<i4", "<i4", "<f8"],
+                              "offsets": [EndProblem.__dict__[n].offset for n, _ in EndProblem._fields_],
+                              "itemsize": C.sizeof(EndProblem)})
 
 _lib = None
 
@@ -68,6 +80,11 @@ def load_library(path=LIB_PATH):
         "gmapdp_single_gap_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t,
                                               C.c_void_p, C.c_void_p, C.c_size_t]),
         "gmapdp_single_pair_capacity": (C.c_size_t, [C.c_void_p, C.c_int]),
+        "gmapdp_end_gap_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t,
+                                           C.c_void_p, C.c_void_p, C.c_size_t]),
+        "gmapdp_end_pair_capacity": (C.c_size_t, [C.c_void_p, C.c_int]),
+        "gmapdp_plan_create": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
+                                         P(C.c_void_p)]),
         "gmapdp_plan_single": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, P(C.c_void_p)]),
         "gmapdp_plan_pair_capacity": (C.c_size_t, [C.c_void_p]),
         "gmapdp_plan_gpu_problems": (C.c_int, [C.c_void_p]),
@@ -195,6 +212,42 @@ class Engine:
         calls = list(calls)
         probs, qbuf, qucbuf = self.build_single_batch(calls)
         results, pairs = self.single_gap_batch_raw(probs, qbuf, qucbuf)
+        return decode_results(results, pairs, [p["dynprogindex"] for p in calls])
+
+
+    # -- batched Dynprog_end5_gap / Dynprog_end3_gap ---------------------------
+    @staticmethod
+    def build_end_batch(calls):
+        """calls: dicts with the Dynprog_end{5,3}_gap arguments (end3p, q, quc, rlength, glength, roffset,
+        goffset, chroffset, chrhigh, watsonp, genestrand, jump_late_p, extraband, defect_rate, endalign,
+        require_pos_score_p, dynprogindex); q/quc is the query slice the reference reads (end5: its
+        rev pointer is the slice's last character)."""
+        calls = list(calls)
+        probs = np.zeros(len(calls), dtype=END_PROBLEM_DTYPE)
+        qparts, qucparts, off = [], [], 0
+        for i, p in enumerate(calls):
+            q, quc = p["q"], p["quc"]
+            probs[i]["qoff"] = off
+            for k in ("rlength", "glength", "roffset", "goffset", "chroffset", "chrhigh", "genestrand",
+                      "end3p", "endalign", "require_pos_score_p", "dynprogindex", "defect_rate"):
+                probs[i][k] = p[k]
+            probs[i]["extraband"] = p["extraband"]
+            probs[i]["flags"] = (WATSON if p["watsonp"] else 0) | (JUMP_LATE if p["jump_late_p"] else 0)
+            qparts.append(q)
+            qucparts.append(quc)
+            off += len(q)
+        return probs, (b"".join(qparts) or b"\0"), (b"".join(qucparts) or b"\0")
+
+    def end_gap_batch(self, calls):
+        calls = list(calls)
+        probs, qbuf, qucbuf = self.build_end_batch(calls)
+        n = len(probs)
+        results = np.zeros(n, dtype=RESULT_DTYPE)
+        cap = self.lib.gmapdp_end_pair_capacity(probs.ctypes.data, n)
+        pairs = np.zeros(max(cap, 1), dtype=PAIR_DTYPE)
+        rc = self.lib.gmapdp_end_gap_batch(self.h, probs.ctypes.data, n, qbuf, qucbuf, len(qbuf),
+                                           results.ctypes.data, pairs.ctypes.data, cap)
+        self._check(rc, "gmapdp_end_gap_batch")
         return decode_results(results, pairs, [p["dynprogindex"] for p in calls])
 
 

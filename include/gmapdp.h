@@ -17,6 +17,9 @@
  *                            the packed genome is made resident in HBM
  *   gmapdp_single_gap_batch  Dynprog_single_gap (dynprog_single.c:429), one call per
  *                            problem, many problems per launch
+ *   gmapdp_end_gap_batch     Dynprog_end5_gap / Dynprog_end3_gap (dynprog_end.c:1294/1924)
+ *   gmapdp_plan_*            the same calls, planned once and replayed on device-resident
+ *                            inputs (mixed single + end batches)
  *   gmapdp_compute_bands     Dynprog_compute_bands (dynprog.c:1247)
  *
  * Semantics: every result is bit-identical to the reference's nosimd build
@@ -94,6 +97,37 @@ typedef struct {
   int32_t pad_;
 } gmapdp_single_problem;
 
+/* Endalign_T (dynprog.h:25) */
+#define GMAPDP_QUERYEND_GAP     0
+#define GMAPDP_QUERYEND_INDELS  1
+#define GMAPDP_QUERYEND_NOGAPS  2
+#define GMAPDP_BEST_LOCAL       3
+
+/* One Dynprog_end5_gap (end3p = 0, dynprog_end.c:1294) or Dynprog_end3_gap
+ * (end3p = 1, dynprog_end.c:1924) call.  The query slice is
+ * qseq[qoff .. qoff+rlength): for end3 the reference's rsequence points at its
+ * first character, for end5 rev_rsequence points at its LAST character (the
+ * DP walks away from the anchor).  roffset/goffset are the reference's
+ * (rev_)roffset/(rev_)goffset.  The engine applies the reference's chopping
+ * to 660 x 2000 (except QUERYEND_NOGAPS). */
+typedef struct {
+  int32_t qoff;
+  int32_t rlength;
+  int32_t glength;
+  int32_t roffset;
+  int32_t goffset;
+  uint32_t chroffset;
+  uint32_t chrhigh;
+  int32_t flags;          /* GMAPDP_WATSON | GMAPDP_JUMP_LATE */
+  int32_t genestrand;
+  int32_t extraband;      /* extraband_end */
+  int32_t end3p;
+  int32_t endalign;       /* GMAPDP_QUERYEND_* / GMAPDP_BEST_LOCAL */
+  int32_t require_pos_score_p;
+  int32_t dynprogindex;
+  double defect_rate;
+} gmapdp_end_problem;
+
 /* Per-problem outputs (the reference's out-parameters). */
 typedef struct {
   int32_t npairs;          /* 0 <=> NULL List_T */
@@ -131,6 +165,15 @@ int gmapdp_single_gap_batch (gmapdp_ctx *ctx, const gmapdp_single_problem *probl
                              gmapdp_result *results, gmapdp_pair *pairs, size_t pair_capacity);
 size_t gmapdp_single_pair_capacity (const gmapdp_single_problem *problems, int n);
 
+/* Run n Dynprog_end5_gap / Dynprog_end3_gap problems (same conventions).
+ * NULL results follow dynprog_end.c: traceback_score 0; dynprogindex is left
+ * unchanged on the early returns (rlength <= 0, end5 goffset < 0,
+ * glength <= 0) and advanced otherwise. */
+int gmapdp_end_gap_batch (gmapdp_ctx *ctx, const gmapdp_end_problem *problems, int n,
+                          const char *qseq, const char *qseq_uc, size_t qbytes,
+                          gmapdp_result *results, gmapdp_pair *pairs, size_t pair_capacity);
+size_t gmapdp_end_pair_capacity (const gmapdp_end_problem *problems, int n);
+
 /* Device-resident path for pipelined callers and throughput measurement.
  * gmapdp_plan_single resolves penalties, bands and launch classes once on
  * the host (problems resolved on the host -- the size guard -- are written
@@ -140,6 +183,10 @@ size_t gmapdp_single_pair_capacity (const gmapdp_single_problem *problems, int n
  * results land in d_results[gmapdp_plan_dev_index(plan, i)] and pairs in
  * d_pairs (capacity gmapdp_plan_pair_capacity). */
 typedef struct gmapdp_plan gmapdp_plan;
+/* Mixed batch: host_results has nsingle + nend entries (singles first). */
+int gmapdp_plan_create (gmapdp_ctx *ctx, const gmapdp_single_problem *singles, int nsingle,
+                        const gmapdp_end_problem *ends, int nend, gmapdp_result *host_results,
+                        gmapdp_plan **plan);
 int gmapdp_plan_single (gmapdp_ctx *ctx, const gmapdp_single_problem *problems, int n,
                         gmapdp_result *host_results, gmapdp_plan **plan);
 size_t gmapdp_plan_pair_capacity (const gmapdp_plan *plan);

@@ -652,3 +652,162 @@ orc_single_gap (const char *rsequence, const char *rsequenceuc, int rlength, int
   free(matrix); free(dirs); free(gseq); free(gseq_alt);
   return sink.n > 0 ? sink.n : -1; /* an empty List_T is NULL */
 }
+
+/* ---------------------------------------------------------------------------
+ * Dynprog_end5_gap / Dynprog_end3_gap (dynprog_end.c:1294-1647 / 1924-2247),
+ * nosimd build: ENDQ scores, END_OPEN/EXTEND penalties (dynprog_end.c:68-74),
+ * find_best_endpoint_std / _to_queryend_indels_std / _nogaps
+ * (dynprog_end.c:297-587), traceback_nogaps (:649), then removal of INDEL
+ * pairs at the far end.  qbuf/qucbuf + qpos is the reference's
+ * (rev_)rsequence pointer: for end5 it points at the LAST query character
+ * and the fill walks backwards (revp).
+ * ------------------------------------------------------------------------- */
+#define END_OPEN_HIGHQ -10
+#define END_OPEN_MEDQ -8
+#define END_OPEN_LOWQ -6
+#define END_EXTEND -2
+enum { QUERYEND_GAP = 0, QUERYEND_INDELS = 1, QUERYEND_NOGAPS = 2, BEST_LOCAL = 3 };
+
+static void
+find_best_endpoint_std (int *finalscore, int *bestr, int *bestc, const int *matrix, int rlength, int glength,
+                        int lband, int uband, int late) {
+  int bestscore = 0, r, c, clo, chigh;
+  *bestr = *bestc = 0;
+  for (r = 1; r <= rlength; r++) {
+    if ((clo = r - lband) < 1) clo = 1;
+    if ((chigh = r + uband) > glength) chigh = glength;
+    for (c = clo; c <= chigh; c++) {
+      if (prefer(matrix[IDX(c, r)], bestscore, late)) { *bestr = r; *bestc = c; bestscore = matrix[IDX(c, r)]; }
+    }
+  }
+  *finalscore = bestscore;
+}
+
+static void
+find_best_endpoint_to_queryend_indels_std (int *finalscore, int *bestr, int *bestc, const int *matrix, int rlength,
+                                           int glength, int lband, int uband, int late) {
+  int bestscore = NEG_INFINITY_32, r, c, clo, chigh;
+  *bestr = r = rlength;
+  *bestc = 0;
+  if ((clo = r - lband) < 1) clo = 1;
+  if ((chigh = r + uband) > glength) chigh = glength;
+  for (c = clo; c <= chigh; c++) {
+    if (prefer(matrix[IDX(c, r)], bestscore, late)) { *bestr = r; *bestc = c; bestscore = matrix[IDX(c, r)]; }
+  }
+  *finalscore = bestscore;
+}
+
+/* traceback_nogaps (dynprog_end.c:649) */
+static void
+traceback_nogaps (PairSink *s, Tally *t, int r, int c, const char *rsequence, const char *rsequenceuc,
+                  const char *gsequence, const char *gsequence_alt, int queryoffset, int genomeoffset,
+                  int genestrand, int revp, int dpi) {
+  int querycoord, genomecoord;
+  char c1, c1_uc, c2, c2_alt;
+  while (r > 0 && c > 0) {
+    querycoord = r - 1;
+    genomecoord = c - 1;
+    if (revp) { querycoord = -querycoord; genomecoord = -genomecoord; }
+    c1 = rsequence[querycoord]; c1_uc = rsequenceuc[querycoord];
+    c2 = gsequence[genomecoord]; c2_alt = gsequence_alt[genomecoord];
+    if (c2 == '*') {
+    } else if (c1_uc == c2 || c1_uc == c2_alt) {
+      t->score += MATCH; t->nmatches += 1;
+      sink_push(s, queryoffset + querycoord, genomeoffset + genomecoord, c1, DYNPROG_MATCH_COMP, c2, c2_alt, dpi);
+    } else if (consistent[genestrand][(unsigned char) c1_uc][(unsigned char) c2] ||
+               consistent[genestrand][(unsigned char) c1_uc][(unsigned char) c2_alt]) {
+      t->score += MATCH; t->nmatches += 1;
+      sink_push(s, queryoffset + querycoord, genomeoffset + genomecoord, c1, AMBIGUOUS_COMP, c2, c2_alt, dpi);
+    } else {
+      t->score += MISMATCH; t->nmismatches += 1;
+      sink_push(s, queryoffset + querycoord, genomeoffset + genomecoord, c1, MISMATCH_COMP, c2, c2_alt, dpi);
+    }
+    r--; c--;
+  }
+}
+
+int
+orc_end_gap (int end3p, const char *qbuf, const char *qucbuf, int qpos, int rlength, int glength,
+             int roffset, int goffset, unsigned int chroffset, unsigned int chrhigh,
+             int watsonp, int genestrand, int jump_late_p, int extraband_end, double defect_rate,
+             int endalign, int require_pos_score_p, int dynprogindex, int *scalars, OrcPair *out, int max_pairs) {
+  const char *rsequence = qbuf + qpos, *rsequenceuc = qucbuf + qpos;
+  int open, extend, lband = 0, uband = 0, bestr = 0, bestc = 0, finalscore = 0, n, i, first, revp = !end3p;
+  int late = end3p ? jump_late_p : !jump_late_p;
+  char *gseq, *gseq_alt;
+  const char *gptr, *gptr_alt;
+  int *matrix = NULL;
+  signed char *dirs = NULL;
+  PairSink sink = {out, 0, max_pairs};
+  Tally t = {0, 0, 0, 0, 0};
+
+  if (g_user_dynprog_p) { open = g_user_open; extend = g_user_extend; }
+  else if (defect_rate < DEFECT_HIGHQ) { open = END_OPEN_HIGHQ; extend = END_EXTEND; }
+  else if (defect_rate < DEFECT_MEDQ) { open = END_OPEN_MEDQ; extend = END_EXTEND; }
+  else { open = END_OPEN_LOWQ; extend = END_EXTEND; }
+
+  scalars[0] = dynprogindex;
+  scalars[1] = scalars[2] = scalars[3] = scalars[4] = scalars[5] = 0;
+  if (rlength <= 0) return -1;
+  if (endalign != QUERYEND_NOGAPS && rlength > ORC_MAX_RLENGTH) rlength = ORC_MAX_RLENGTH;
+  if (!end3p && goffset < 0) return -1;
+  if (glength <= 0) return -1;
+  if (endalign != QUERYEND_NOGAPS && glength > ORC_MAX_GLENGTH) glength = ORC_MAX_GLENGTH;
+
+  gseq = (char *) malloc(glength + 1);
+  gseq_alt = (char *) malloc(glength + 1);
+  if (end3p) {
+    if (watsonp) orc_get_segment(1, chroffset + (unsigned int) goffset, glength, chrhigh, 0, gseq, gseq_alt);
+    else orc_get_segment(0, chrhigh - (unsigned int) goffset + 1, glength, chroffset, 1, gseq, gseq_alt);
+    gptr = gseq; gptr_alt = gseq_alt;
+  } else {
+    if (watsonp) orc_get_segment(0, chroffset + (unsigned int) goffset + 1, glength, chroffset, 0, gseq, gseq_alt);
+    else orc_get_segment(1, chrhigh - (unsigned int) goffset, glength, chrhigh, 1, gseq, gseq_alt);
+    gptr = &gseq[glength - 1]; gptr_alt = &gseq_alt[glength - 1];
+  }
+  if (gseq[0] == '\0') { free(gseq); free(gseq_alt); return -1; }
+
+  if (endalign == QUERYEND_GAP || endalign == BEST_LOCAL || endalign == QUERYEND_INDELS) {
+    compute_bands(&lband, &uband, rlength, glength, extraband_end, endalign != QUERYEND_INDELS);
+    matrix = (int *) malloc((size_t) (glength + 1) * (rlength + 1) * sizeof(int));
+    dirs = (signed char *) malloc((size_t) 3 * (glength + 1) * (rlength + 1));
+    /* end3 scores the upper-cased query, end5 the query as given */
+    orc_standard_fill(end3p ? rsequenceuc : rsequence, gptr, gptr_alt, rlength, glength, ENDQ, open, extend,
+                      lband, uband, late, revp, NEG_INFINITY_32, 1, 1, matrix, dirs);
+    if (endalign == QUERYEND_INDELS)
+      find_best_endpoint_to_queryend_indels_std(&finalscore, &bestr, &bestc, matrix, rlength, glength, lband, uband, late);
+    else
+      find_best_endpoint_std(&finalscore, &bestr, &bestc, matrix, rlength, glength, lband, uband, late);
+  } else if (endalign == QUERYEND_NOGAPS) {
+    bestr = bestc = glength < rlength ? glength : rlength;
+  } else {
+    free(gseq); free(gseq_alt);
+    return -2;
+  }
+
+  if (endalign == QUERYEND_NOGAPS) {
+    traceback_nogaps(&sink, &t, bestr, bestc, rsequence, rsequenceuc, gptr, gptr_alt, roffset, goffset,
+                     genestrand, revp, dynprogindex);
+  } else if (require_pos_score_p) {
+    /* *traceback_score was just zeroed, so this always skips (dynprog_end.c:1572) */
+  } else {
+    traceback_std(&sink, &t, dirs, rlength, glength, bestr, bestc, rsequence, rsequenceuc, gptr, gptr_alt,
+                  roffset, goffset, revp, chroffset, chrhigh, watsonp, genestrand, dynprogindex);
+  }
+  scalars[0] = dynprogindex + (dynprogindex > 0 ? +1 : -1);
+  scalars[1] = t.score; scalars[2] = t.nmatches; scalars[3] = t.nmismatches;
+  scalars[4] = t.nopens; scalars[5] = t.nindels;
+  free(matrix); free(dirs); free(gseq); free(gseq_alt);
+
+  if ((endalign == QUERYEND_GAP || endalign == BEST_LOCAL) && (t.nmatches + 1) < t.nmismatches) {
+    scalars[1] = 0;
+    return -1;
+  }
+  /* push order == List_reverse(pairs); drop INDEL pairs at its head (the far end) */
+  n = sink.n < max_pairs ? sink.n : max_pairs;
+  for (first = 0; first < n && out[first].comp == INDEL_COMP; first++) ;
+  for (i = first; i < n; i++) out[i - first] = out[i];
+  n -= first;
+  if (!end3p) reverse_pairs(out, n); /* end5 returns List_reverse once more */
+  return n > 0 ? n : -1;
+}

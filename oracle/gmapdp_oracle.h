@@ -46,6 +46,16 @@ int orc_single_gap (const char *rsequence, const char *rsequenceuc, int rlength,
                     int watsonp, int genestrand, int jump_late_p, int extraband_single, int widebandp,
                     double defect_rate, int dynprogindex, int *scalars, OrcPair *out, int max_pairs);
 
+/* Dynprog_end5_gap (end3p = 0) / Dynprog_end3_gap (end3p = 1)
+   (dynprog_end.c:1294/1924), nosimd semantics.  The reference's
+   (rev_)rsequence pointer is qbuf + qpos (end5: the LAST query character).
+   endalign: 0 QUERYEND_GAP, 1 QUERYEND_INDELS, 2 QUERYEND_NOGAPS, 3 BEST_LOCAL. */
+int orc_end_gap (int end3p, const char *qbuf, const char *qucbuf, int qpos, int rlength, int glength,
+                 int roffset, int goffset, unsigned int chroffset, unsigned int chrhigh,
+                 int watsonp, int genestrand, int jump_late_p, int extraband_end, double defect_rate,
+                 int endalign, int require_pos_score_p, int dynprogindex, int *scalars, OrcPair *out,
+                 int max_pairs);
+
 /* Genome_get_segment_right / _left (genome.c:11023/11079) over the oracle
    genome (no alternate genome: segmentalt = segment). */
 int orc_get_segment (int rightp, unsigned int pos, int length, unsigned int chrbound, int revcomp,

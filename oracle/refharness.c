@@ -178,13 +178,14 @@ refh_single_gap_batch (const RefSingleProblem *probs, int n, const char *qseq, c
 
 /* endalign: 0 QUERYEND_GAP, 1 QUERYEND_INDELS, 2 QUERYEND_NOGAPS, 3 BEST_LOCAL (dynprog.h:23) */
 int
-refh_end_gap (int end3p, const char *rsequence, const char *rsequenceuc, int rlength, int glength,
+refh_end_gap (int end3p, const char *qbuf, const char *qucbuf, int qpos, int rlength, int glength,
               int roffset, int goffset, unsigned int chroffset, unsigned int chrhigh,
               int watsonp, int genestrand, int jump_late_p, int extraband_end,
               double defect_rate, int endalign, int require_pos_score_p, int dynprogindex,
               int *scalars, RefPair *out, int max_pairs) {
   List_T pairs;
   int finalscore = 0, nmatches = 0, nmismatches = 0, nopens = 0, nindels = 0, n;
+  const char *rsequence = qbuf + qpos, *rsequenceuc = qucbuf + qpos;
 
   Pairpool_reset(pairpool);
   if (end3p) {

@@ -45,6 +45,12 @@ class _Impl:
                       C.POINTER(C.c_int), C.POINTER(Pair), C.c_int]
         f.restype = C.c_int
         self._single = f
+        f = getattr(self.lib, p + "end_gap")
+        f.argtypes = [C.c_int, C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint,
+                      C.c_uint, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int, C.c_int,
+                      C.POINTER(C.c_int), C.POINTER(Pair), C.c_int]
+        f.restype = C.c_int
+        self._end = f
         self._pairs = (Pair * MAXPAIRS)()
         self._scal = (C.c_int * 6)()
         self._genome_keep = None
@@ -54,6 +60,15 @@ class _Impl:
         n = self._single(q, quc, rlength, glength, roffset, goffset, chroffset, chrhigh, watsonp,
                          genestrand, jump_late_p, extraband, widebandp, defect_rate, dynprogindex,
                          self._scal, self._pairs, MAXPAIRS)
+        assert n <= MAXPAIRS
+        pairs = None if n < 0 else [self._pairs[i].key() for i in range(n)]
+        return tuple(self._scal), pairs
+
+    def end_gap(self, end3p, q, quc, qpos, rlength, glength, roffset, goffset, chroffset, chrhigh, watsonp,
+                genestrand, jump_late_p, extraband, defect_rate, endalign, require_pos_score_p, dynprogindex):
+        n = self._end(end3p, q, quc, qpos, rlength, glength, roffset, goffset, chroffset, chrhigh, watsonp,
+                      genestrand, jump_late_p, extraband, defect_rate, endalign, require_pos_score_p,
+                      dynprogindex, self._scal, self._pairs, MAXPAIRS)
         assert n <= MAXPAIRS
         pairs = None if n < 0 else [self._pairs[i].key() for i in range(n)]
         return tuple(self._scal), pairs
@@ -218,6 +233,72 @@ def edge_single_gap_problem(rng, genome: bytes):
             goffset = min(goffset, len(g) + 1)
         p.update(glength=glength, goffset=goffset)
     return p
+
+
+def genomic_char(genome: bytes, p: int, chrhigh: int, watsonp: bool) -> int:
+    """get_genomic_nt with chroffset 0 (dynprog_single.c:116)."""
+    if watsonp:
+        return genome[p] if 0 <= p < chrhigh else ord("*")
+    pos = chrhigh - p
+    return ord(COMP.get(genome[pos], "N")) if 0 <= pos < chrhigh else ord("*")
+
+
+ENDALIGNS = (0, 1, 2, 3)  # QUERYEND_GAP, QUERYEND_INDELS, QUERYEND_NOGAPS, BEST_LOCAL
+
+
+def end_gap_problem(rng, genome: bytes, edge=False):
+    """One Dynprog_end5_gap / Dynprog_end3_gap-shaped call (stage3.c:10244-10600):
+    query = the read end beyond the last anchor, genome = queryjump + extramaterial_end."""
+    chrhigh = len(genome)
+    end3p = rng.random() < 0.5
+    watsonp = rng.random() < 0.6
+    L = max(1, int(rng.gammavariate(1.6, 110))) if not edge else rng.choice([1, 2, 5, rng.randint(300, 800)])
+    glength = L + rng.choice([10, 10, 10, 0, 30, -3]) if rng.random() < 0.9 else rng.randint(1, 2100)
+    glength = max(1, glength)
+    if end3p:
+        goffset = rng.randint(0, chrhigh - 1)
+        if not edge:
+            goffset = rng.randint(0, max(0, chrhigh - glength - 2))
+        if not watsonp:
+            goffset = min(max(goffset, 1), chrhigh)
+        seg = bytes(genomic_char(genome, goffset + i, chrhigh, watsonp) for i in range(min(L, glength)))
+    else:
+        goffset = rng.randint(-2 if edge else 0, chrhigh - 1)
+        if not edge:
+            goffset = rng.randint(min(glength, chrhigh - 1), chrhigh - 1)
+        if not watsonp:
+            goffset = min(goffset, chrhigh - 1)
+        n = min(L, glength)
+        seg = bytes(genomic_char(genome, goffset - n + 1 + i, chrhigh, watsonp) for i in range(n))
+    seg = seg.replace(b"*", b"A") or b"A"
+    kind = rng.random()
+    if kind < 0.1:
+        q = bytes(rng.choice(b"ACGT") for _ in range(L))
+        quc = q
+    else:
+        q, quc = mutate(rng, seg, sub=rng.choice([0.01, 0.03, 0.1, 0.3]), indel=rng.choice([0.0, 0.01, 0.04]))
+        if len(q) < L:  # pad with random sequence (the unaligned part of a real read end)
+            pad = bytes(rng.choice(b"ACGT") for _ in range(L - len(q)))
+            q, quc = (q + pad, quc + pad) if end3p else (pad + q, pad + quc)
+        q, quc = (q[:L], quc[:L]) if end3p else (q[-L:], quc[-L:])
+    rlength = len(q)
+    if edge and rng.random() < 0.2:
+        rlength = 0 if rng.random() < 0.3 else rlength
+    return dict(end3p=int(end3p), q=q, quc=quc, rlength=rlength, glength=glength,
+                roffset=rng.randint(0, 3000) + (rlength if not end3p else 0), goffset=goffset,
+                chroffset=0, chrhigh=chrhigh, watsonp=int(watsonp), genestrand=0,
+                jump_late_p=rng.randint(0, 1), extraband=rng.choice([6, 6, 6, 3, 14]),
+                defect_rate=rng.choice([0.001, 0.005, 0.02, 0.05]),
+                endalign=rng.choice([0, 1, 1, 2, 3]), require_pos_score_p=int(rng.random() < 0.1),
+                dynprogindex=rng.choice([1, 5, -1, -7]))
+
+
+def call_end(impl, p):
+    qpos = 0 if p["end3p"] else max(len(p["q"]) - 1, 0)
+    return impl.end_gap(p["end3p"], p["q"] or b"A", p["quc"] or b"A", qpos, p["rlength"], p["glength"],
+                        p["roffset"], p["goffset"], p["chroffset"], p["chrhigh"], p["watsonp"], p["genestrand"],
+                        p["jump_late_p"], p["extraband"], p["defect_rate"], p["endalign"],
+                        p["require_pos_score_p"], p["dynprogindex"])
 
 
 def call_single(impl, p):

@@ -1,4 +1,4 @@
-"""Generate the committed golden vectors for Dynprog_single_gap.
+"""Generate the committed golden vectors for the Dynprog_* entry points.
 
 Run in the development container (needs /root/reference, built into
 oracle/_ref/ by `make -C oracle ref`):
@@ -7,9 +7,12 @@ oracle/_ref/ by `make -C oracle ref`):
 
 Inputs are seeded GMAP-shaped sub-problems (tests/dpbind.py); expected
 outputs come from the REFERENCE's own compiled objects (nosimd build: the
-Dynprog_standard path; avx2 build: the SIMD path), called through
-oracle/refharness.c.  The output file holds data only: the genome, the
-problem parameters, the query bytes and the reference's outputs.
+Dynprog_standard path), called through oracle/refharness.c.  Each output
+file holds data only: the genome, the problem parameters, the query bytes
+and the reference's outputs.
+
+  single_gap_golden.npz  Dynprog_single_gap   (dynprog_single.c:429)
+  end_gap_golden.npz     Dynprog_end5_gap / Dynprog_end3_gap (dynprog_end.c:1294/1924)
 """
 import os
 import random
@@ -19,17 +22,19 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
-from dpbind import (Ref, call_single, edge_single_gap_problem, random_genome,  # noqa: E402
-                    single_gap_problem)
+from dpbind import (Ref, call_end, call_single, edge_single_gap_problem, end_gap_problem,  # noqa: E402
+                    random_genome, single_gap_problem)
 
-PARAMS = ["rlength", "glength", "roffset", "goffset", "chroffset", "chrhigh", "watsonp", "genestrand",
-          "jump_late_p", "extraband", "widebandp", "dynprogindex"]
+SINGLE_PARAMS = ["rlength", "glength", "roffset", "goffset", "chroffset", "chrhigh", "watsonp", "genestrand",
+                 "jump_late_p", "extraband", "widebandp", "dynprogindex"]
+END_PARAMS = ["end3p", "rlength", "glength", "roffset", "goffset", "chroffset", "chrhigh", "watsonp",
+              "genestrand", "jump_late_p", "extraband", "endalign", "require_pos_score_p", "dynprogindex"]
 PAIR_DT = np.dtype([("querypos", "<i4"), ("genomepos", "<i4"), ("queryjump", "<i4"), ("genomejump", "<i4"),
                     ("dynprogindex", "<i4"), ("cdna", "S1"), ("comp", "S1"), ("genome", "S1"), ("genomealt", "S1"),
                     ("gapp", "<i4")])
 
 
-def problems(seed=2024, n_typical=1200, n_edge=400, genome_len=20000):
+def single_problems(seed=2024, n_typical=1200, n_edge=400, genome_len=20000):
     rng = random.Random(seed)
     g = random_genome(rng, genome_len)
     probs = [single_gap_problem(rng, g) for _ in range(n_typical)]
@@ -37,22 +42,29 @@ def problems(seed=2024, n_typical=1200, n_edge=400, genome_len=20000):
     return g, probs
 
 
-def pack(g, probs, outputs):
-    par = np.array([[p[k] for k in PARAMS] for p in probs], dtype=np.int64)
+def end_problems(seed=2025, n_typical=1200, n_edge=400, genome_len=20000):
+    rng = random.Random(seed)
+    g = random_genome(rng, genome_len)
+    probs = [end_gap_problem(rng, g) for _ in range(n_typical)]
+    probs += [end_gap_problem(rng, g, edge=True) for _ in range(n_edge)]
+    return g, probs
+
+
+def pack(g, probs, outputs, names):
+    par = np.array([[p[k] for k in names] for p in probs], dtype=np.int64)
     defect = np.array([p["defect_rate"] for p in probs], dtype=np.float64)
     qlen = np.array([len(p["q"]) for p in probs], dtype=np.int32)
-    qbuf = np.frombuffer(b"".join(p["q"] for p in probs), dtype=np.uint8)
-    qucbuf = np.frombuffer(b"".join(p["quc"] for p in probs), dtype=np.uint8)
-    d = dict(genome=np.frombuffer(g, dtype=np.uint8), params=par, param_names=np.array(PARAMS), defect=defect,
+    qbuf = np.frombuffer(b"".join(p["q"] for p in probs) or b"\0", dtype=np.uint8)
+    qucbuf = np.frombuffer(b"".join(p["quc"] for p in probs) or b"\0", dtype=np.uint8)
+    d = dict(genome=np.frombuffer(g, dtype=np.uint8), params=par, param_names=np.array(names), defect=defect,
              qlen=qlen, qbuf=qbuf, qucbuf=qucbuf)
     for tag, outs in outputs.items():
         scal = np.array([o[0] for o in outs], dtype=np.int32)
         npairs = np.array([-1 if o[1] is None else len(o[1]) for o in outs], dtype=np.int32)
         flat = [pr for o in outs if o[1] is not None for pr in o[1]]
-        pairs = np.array(flat, dtype=PAIR_DT)
         d[tag + "_scalars"] = scal
         d[tag + "_npairs"] = npairs
-        d[tag + "_pairs"] = pairs
+        d[tag + "_pairs"] = np.array(flat, dtype=PAIR_DT)
     return d
 
 
@@ -92,15 +104,17 @@ def load(path):
 
 
 def main():
-    g, probs = problems()
-    outputs = {}
-    for variant in ("nosimd",):  # avx2 (SIMD semantics): see DESIGN.md, aborts on some edge shapes
-        ref = Ref(variant)
+    # SIMD (avx2) outputs are not generated here: that build aborts ("Bad dir",
+    # dynprog_simd.c:9278) on narrow bands that miss the corner; see DESIGN.md.
+    for name, maker, call, names in (("single_gap_golden.npz", single_problems, call_single, SINGLE_PARAMS),
+                                     ("end_gap_golden.npz", end_problems, call_end, END_PARAMS)):
+        g, probs = maker()
+        ref = Ref("nosimd")
         ref.set_genome(g)
-        outputs["ref_" + variant] = [call_single(ref, p) for p in probs]
-    out = os.path.join(HERE, "single_gap_golden.npz")
-    np.savez_compressed(out, **pack(g, probs, outputs))
-    print("wrote %s: %d problems" % (out, len(probs)))
+        outputs = {"ref_nosimd": [call(ref, p) for p in probs]}
+        out = os.path.join(HERE, name)
+        np.savez_compressed(out, **pack(g, probs, outputs, names))
+        print("wrote %s: %d problems" % (out, len(probs)))
 
 
 if __name__ == "__main__":

@@ -93,3 +93,53 @@ def test_reference_harness_has_no_unresolved_gmap_symbols():
     und = [l.split()[-1] for l in out.splitlines() if l.strip()]
     und = [s for s in und if not s.startswith("_") and "@" not in s and s not in ("gzgetc",)]
     assert und == [], und
+
+
+# ---------------------------------------------------------------------------
+# Dynprog_end5_gap / Dynprog_end3_gap
+# ---------------------------------------------------------------------------
+def _golden_end():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(HERE, "golden", "make_golden.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m.load(os.path.join(HERE, "golden", "end_gap_golden.npz"))
+
+
+def test_oracle_end_gap_matches_golden(oracle):
+    from dpbind import call_end
+    g, probs, outs = _golden_end()
+    oracle.set_genome(g)
+    exp = outs["ref_nosimd"]
+    assert len(probs) == len(exp) == 1600
+    bad = [i for i, p in enumerate(probs) if call_end(oracle, p) != exp[i]]
+    assert bad == [], "oracle differs from reference end-gap golden on %d problems (first %s)" % (len(bad), bad[:5])
+
+
+def test_end_golden_covers_every_branch():
+    g, probs, outs = _golden_end()
+    exp = outs["ref_nosimd"]
+    seen = set()
+    for p, (s, pairs) in zip(probs, exp):
+        seen.add((p["end3p"], p["endalign"], pairs is None))
+    for end3p in (0, 1):
+        for ea in (0, 1, 2, 3):
+            assert (end3p, ea, False) in seen
+    assert sum(1 for p in probs if p["rlength"] > 660) > 0          # chopping
+    assert sum(1 for p in probs if p["require_pos_score_p"]) > 0
+
+
+@pytest.mark.skipif(not ref_available("nosimd"), reason="reference objects (oracle/_ref) not built here")
+def test_oracle_end_gap_vs_reference_random(oracle):
+    from dpbind import call_end, end_gap_problem
+    ref = Ref("nosimd")
+    rng = random.Random(4242)
+    g = random_genome(rng, 30000)
+    ref.set_genome(g)
+    oracle.set_genome(g)
+    bad = 0
+    for i in range(4000):
+        p = end_gap_problem(rng, g, edge=(i % 5 == 0))
+        if call_end(ref, p) != call_end(oracle, p):
+            bad += 1
+    assert bad == 0
