@@ -3,16 +3,17 @@
 Workload (configs[1]: "100k synthetic 2-kb cDNA vs human chr22, 1xMI355X,
 Dynprog_single + Dynprog_end only"): a chr22-length (50,818,468 nt) i.i.d.
 genome (seed 22) packed in the reference's .genomecomp format and resident
-in HBM, and the stream of Dynprog_single_gap sub-problems that GMAP issues
-for 2-kb reads (43.7 calls per read): query slices of the
-genome with 2 % substitutions and occasional 1-3 nt indels, GMAP's default
-extraband 6 / wide band, MEDQ/LOWQ defect rates.  One "step" = one pass of
-the engine over the sub-problems of --reads reads (all inputs already in
-HBM; host->device copies are outside the timed region).
+in HBM, and the stream of sub-problems GMAP issues per 2-kb read (nosimd
+instrumented counts): 43.7 Dynprog_single_gap calls (query
+slices with 2 % substitutions and occasional 1-3 nt indels, extraband 6,
+wide band) plus 7.1 Dynprog_end5_gap + 6.5 Dynprog_end3_gap calls (read ends
+beyond the last anchor, glength = rlength + extramaterial_end 10, mixed
+endalign).  One "step" = one pass of the engine over the sub-problems of
+--reads reads; all inputs are in HBM before the timed region.
 
-value = reads whose sub-problems were processed per second, whole job (all
-ranks).  This is the DP-engine throughput of the path, not end-to-end GMAP
-(stage 1/2/3 orchestration stays on the host; DESIGN.md "Measurement").
+value = reads whose DP sub-problems were processed per second, whole job
+(all ranks).  This is the DP-engine throughput of the path, not end-to-end
+GMAP (stage 1/2/3 orchestration stays on the host; DESIGN.md "Measurement").
 """
 import argparse
 import ctypes as C
@@ -25,121 +26,190 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gmap-2024_amd"))
-sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 CHR22_LEN = 50_818_468
-CALLS_PER_READ = 43.7          # Dynprog_single_gap calls per 2-kb read
+SINGLE_PER_READ = 43.7         # Dynprog_single_gap calls per 2-kb read (nosimd)
+END5_PER_READ = 7.1            # Dynprog_end5_gap
+END3_PER_READ = 6.5            # Dynprog_end3_gap
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 COMPL = np.zeros(256, dtype=np.uint8)
-for a, b in zip(b"ACGTN", b"TGCAN"):
-    COMPL[a] = b
+for _a, _b in zip(b"ACGTN", b"TGCAN"):
+    COMPL[_a] = _b
+ACGT = np.frombuffer(b"ACGT", dtype=np.uint8)
 
 
 def make_genome(seed=22, length=CHR22_LEN):
     rng = np.random.default_rng(seed)
-    return np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, size=length, dtype=np.uint8)]
+    return ACGT[rng.integers(0, 4, size=length, dtype=np.uint8)]
 
 
-def make_problems(genome, nprob, seed):
-    """Vectorised GMAP-shaped single-gap sub-problems (see module docstring)."""
-    import gmapdp
-    rng = np.random.default_rng(seed)
+def genomic_chars(genome, pos, watson):
+    """get_genomic_nt with chroffset 0, chrhigh = len(genome), positions in range."""
     glen = len(genome)
-    g = np.clip(rng.gamma(3.0, 40.0, size=nprob).astype(np.int64), 1, 640)
-    d = np.where(rng.random(nprob) < 0.15, rng.integers(-3, 4, size=nprob), 0)
+    fwd = genome[np.where(watson, pos, 0)]
+    rev = COMPL[genome[np.where(watson, 0, glen - pos)]]
+    return np.where(watson, fwd, rev)
+
+
+def make_single(genome, n, rng):
+    """Vectorised GMAP-shaped Dynprog_single_gap sub-problems."""
+    import gmapdp
+    glen = len(genome)
+    g = np.clip(rng.gamma(3.0, 40.0, size=n).astype(np.int64), 1, 640)
+    d = np.where(rng.random(n) < 0.15, rng.integers(-3, 4, size=n), 0)
     d = np.where(g + d < 1, 0, d)
     r = np.clip(g + d, 1, 660)
     d = r - g
-    watson = rng.random(nprob) < 0.5
-    goff = rng.integers(1, glen - 700, size=nprob)
-    # segment characters as the engine sees them
+    watson = rng.random(n) < 0.5
+    goff = rng.integers(1, glen - 700, size=n)
     seg_off = np.concatenate([[0], np.cumsum(g)])
-    pid = np.repeat(np.arange(nprob), g)
+    pid = np.repeat(np.arange(n), g)
     i = np.arange(seg_off[-1]) - seg_off[pid]
-    gpos = np.where(watson[pid], goff[pid] + i, glen - goff[pid] - i)
-    seg = genome[gpos]
-    seg = np.where(watson[pid], seg, COMPL[seg])
+    seg = genomic_chars(genome, goff[pid] + i, watson[pid])
     # query = segment with one indel of |d| at position a, then 2 % substitutions
     q_off = np.concatenate([[0], np.cumsum(r)])
-    qpid = np.repeat(np.arange(nprob), r)
+    qpid = np.repeat(np.arange(n), r)
     j = np.arange(q_off[-1]) - q_off[qpid]
-    a = (rng.random(nprob) * np.maximum(r - np.maximum(d, 0), 1)).astype(np.int64)
+    a = (rng.random(n) * np.maximum(r - np.maximum(d, 0), 1)).astype(np.int64)
     dd, aa = d[qpid], a[qpid]
     src = np.where((dd < 0) & (j >= aa), j - dd, j)                      # deletion: skip -d bases
     ins = (dd > 0) & (j >= aa) & (j < aa + dd)
     src = np.where((dd > 0) & (j >= aa + dd), j - dd, src)               # insertion: shift back
     src = np.clip(src, 0, g[qpid] - 1)
     q = seg[seg_off[qpid] + src]
-    rnd = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, size=q.size, dtype=np.uint8)]
+    rnd = ACGT[rng.integers(0, 4, size=q.size, dtype=np.uint8)]
     q = np.where(ins | (rng.random(q.size) < 0.02), rnd, q).astype(np.uint8)
-    probs = np.zeros(nprob, dtype=gmapdp.PROBLEM_DTYPE)
+    probs = np.zeros(n, dtype=gmapdp.PROBLEM_DTYPE)
     probs["qoff"] = q_off[:-1]
     probs["rlength"] = r
     probs["glength"] = g
-    probs["roffset"] = rng.integers(0, 1800, size=nprob)
+    probs["roffset"] = rng.integers(0, 1800, size=n)
     probs["goffset"] = goff
     probs["chroffset"] = 0
     probs["chrhigh"] = glen
-    probs["flags"] = (watson.astype(np.int32) * gmapdp.WATSON | (rng.random(nprob) < 0.5) * gmapdp.JUMP_LATE |
+    probs["flags"] = (watson.astype(np.int32) * gmapdp.WATSON | (rng.random(n) < 0.5) * gmapdp.JUMP_LATE |
                       gmapdp.WIDEBAND)
     probs["genestrand"] = 0
     probs["extraband"] = 6
-    probs["defect_rate"] = np.where(rng.random(nprob) < 0.7, 0.02, 0.01)
-    probs["dynprogindex"] = rng.integers(1, 50, size=nprob) * np.where(rng.random(nprob) < 0.5, 1, -1)
+    probs["defect_rate"] = np.where(rng.random(n) < 0.7, 0.02, 0.01)
+    probs["dynprogindex"] = rng.integers(1, 50, size=n) * np.where(rng.random(n) < 0.5, 1, -1)
     return probs, q
 
 
-def algorithmic_bytes(probs, npairs):
-    """HBM bytes the path must move per launch (DESIGN.md "Roofline"): problem
-    descriptor (56 B) + query and upper-cased query (2 x rlength) + the packed
-    genome blocks covering the segment (12 B per 32 nt) + result (32 B) + one
-    16-B Pair record per emitted pair."""
-    g = probs["glength"].astype(np.int64)
-    return int((56 + 2 * probs["rlength"].astype(np.int64) + 12 * ((g + 62) // 32) + 32).sum()
-               + 16 * int(npairs.sum()))
-
-
-def banded_cells(probs):
+def make_end(genome, n5, n3, rng):
+    """Vectorised Dynprog_end5_gap / Dynprog_end3_gap sub-problems: the read end beyond the last
+    anchor (lognormal length, median 60 nt), genome = rlength + extramaterial_end (10)."""
     import gmapdp
-    lib = gmapdp.load_library()
-    lb, ub = C.c_int(), C.c_int()
-    r = probs["rlength"].astype(np.int64)
-    g = probs["glength"].astype(np.int64)
-    # widebandp, extraband 6: W = |g - r| + 13; cells ~ g * W clipped by r (exact count not needed)
-    W = np.abs(g - r) + 2 * probs["extraband"].astype(np.int64) + 1
-    return int(np.minimum(W, r + 1).dot(g))
+    glen = len(genome)
+    n = n5 + n3
+    end3 = np.zeros(n, dtype=bool)
+    end3[n5:] = True
+    L = np.clip(rng.lognormal(np.log(60.0), 1.2, size=n).astype(np.int64), 1, 800)
+    g = L + 10
+    watson = rng.random(n) < 0.5
+    # end3: genomic positions goffset .. goffset+L-1; end5: rev_goffset-L+1 .. rev_goffset
+    goff = np.where(end3, rng.integers(1, glen - 900, size=n), rng.integers(900, glen - 2, size=n))
+    first = np.where(end3, goff, goff - L + 1)
+    q_off = np.concatenate([[0], np.cumsum(L)])
+    qpid = np.repeat(np.arange(n), L)
+    j = np.arange(q_off[-1]) - q_off[qpid]
+    q = genomic_chars(genome, first[qpid] + j, watson[qpid])
+    # 2 % substitutions; 15 % of ends carry an unalignable tail (adapter / poly-A) over their far 30 %
+    tail = rng.random(n) < 0.15
+    far = np.where(end3[qpid], j >= (0.7 * L[qpid]).astype(np.int64), j < (0.3 * L[qpid]).astype(np.int64))
+    noise = (rng.random(q.size) < 0.02) | (tail[qpid] & far)
+    q = np.where(noise, ACGT[rng.integers(0, 4, size=q.size, dtype=np.uint8)], q).astype(np.uint8)
+    probs = np.zeros(n, dtype=gmapdp.END_PROBLEM_DTYPE)
+    probs["qoff"] = q_off[:-1]
+    probs["rlength"] = L
+    probs["glength"] = g
+    probs["roffset"] = np.where(end3, rng.integers(1200, 1900, size=n), L - 1 + rng.integers(0, 100, size=n))
+    probs["goffset"] = goff
+    probs["chroffset"] = 0
+    probs["chrhigh"] = glen
+    probs["flags"] = watson.astype(np.int32) * gmapdp.WATSON | (rng.random(n) < 0.5) * gmapdp.JUMP_LATE
+    probs["genestrand"] = 0
+    probs["extraband"] = 6
+    probs["end3p"] = end3
+    u = rng.random(n)
+    probs["endalign"] = np.where(u < 0.5, 1, np.where(u < 0.85, 0, np.where(u < 0.9, 3, 2)))
+    probs["require_pos_score_p"] = 0
+    probs["dynprogindex"] = rng.integers(1, 50, size=n) * np.where(rng.random(n) < 0.5, 1, -1)
+    probs["defect_rate"] = np.where(rng.random(n) < 0.7, 0.02, 0.01)
+    return probs, q
 
 
-def cpu_baseline(probs, q, genome, budget_s=12.0):
-    """Time the reference itself (oracle/_ref/librefdp_nosimd.so, 1 core) on a
-    bounded prefix of the same problem stream; fall back to the repo's oracle
-    port if the reference objects are absent."""
+def make_workload(genome, reads, seed):
+    rng = np.random.default_rng(seed)
+    ns = int(round(reads * SINGLE_PER_READ))
+    n5 = int(round(reads * END5_PER_READ))
+    n3 = int(round(reads * END3_PER_READ))
+    sp, sq = make_single(genome, ns, rng)
+    ep, eq = make_end(genome, n5, n3, rng)
+    ep["qoff"] += len(sq)  # one query arena: singles then ends
+    return sp, ep, np.concatenate([sq, eq])
+
+
+def algorithmic_bytes(rlength, glength, npairs, desc_bytes):
+    """HBM bytes the path must move (DESIGN.md "Roofline"): problem descriptor + query and
+    upper-cased query (2 x rlength) + packed genome blocks covering the segment (12 B per
+    32 nt) + result (32 B) + one 16-B Pair record per emitted pair."""
+    r = np.asarray(rlength, dtype=np.int64)
+    g = np.asarray(glength, dtype=np.int64)
+    return int((desc_bytes + 2 * r + 12 * ((g + 62) // 32) + 32).sum() + 16 * int(np.asarray(npairs).sum()))
+
+
+def banded_cells(sp, ep):
+    """Banded DP cells of the fills (wide band for single/GAP/BEST_LOCAL, narrow for INDELS)."""
+    r = sp["rlength"].astype(np.int64)
+    g = sp["glength"].astype(np.int64)
+    cells = int(np.minimum(np.abs(g - r) + 2 * sp["extraband"].astype(np.int64) + 1, r + 1).dot(g))
+    r = np.minimum(ep["rlength"].astype(np.int64), 660)
+    g = np.minimum(ep["glength"].astype(np.int64), 2000)
+    eb = ep["extraband"].astype(np.int64)
+    W = np.where(ep["endalign"] == 1, 2 * eb + 1, np.abs(g - r) + 2 * eb + 1)
+    W = np.where(ep["endalign"] == 2, 0, W)
+    return cells + int(np.minimum(W, r + 1).dot(g))
+
+
+def cpu_baseline(sp, ep, q, genome, budget_s=12.0):
+    """Time the reference itself (oracle/_ref/librefdp_nosimd.so, 1 core) on a bounded prefix of
+    the same per-read problem mix; None if the reference objects are absent."""
     ref_so = os.path.join(ROOT, "oracle", "_ref", "librefdp_nosimd.so")
-    qb = q.tobytes()
-    if os.path.exists(ref_so):
-        lib = C.CDLL(ref_so)
-        lib.refh_init(0, 0, 0)
-        gb = genome.tobytes()
-        lib.refh_set_genome(gb, len(gb))
-        fn = lib.refh_single_gap_batch
-        fn.restype = C.c_long
-        fn.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_char_p]
-        kind = "reference"
-    else:
+    if not os.path.exists(ref_so):
         return None
-    n, done, t_total = 256, 0, 0.0
-    while t_total < budget_s and done + n <= len(probs):
-        sub = np.ascontiguousarray(probs[done:done + n])
+    lib = C.CDLL(ref_so)
+    lib.refh_init(0, 0, 0)
+    gb = genome.tobytes()
+    lib.refh_set_genome(gb, len(gb))
+    for name in ("refh_single_gap_batch", "refh_end_gap_batch"):
+        f = getattr(lib, name)
+        f.restype = C.c_long
+        f.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_char_p]
+    qb = q.tobytes()
+    per_read_s = SINGLE_PER_READ / (SINGLE_PER_READ + END5_PER_READ + END3_PER_READ)
+    t_single = t_end = 0.0
+    ns = ne = 0
+    chunk = 256
+    while t_single + t_end < budget_s and ns + chunk <= len(sp) and ne + chunk <= len(ep):
+        a = np.ascontiguousarray(sp[ns:ns + chunk])
         t0 = time.perf_counter()
-        fn(sub.ctypes.data, n, qb, qb)
-        t_total += time.perf_counter() - t0
-        done += n
-        n = min(n * 2, 8192)
-    per_s = done / t_total
-    return {"value": per_s / CALLS_PER_READ, "unit": "reads/s", "cores": 1, "kind": kind,
-            "sample": "%d Dynprog_single_gap problems of the same stream (%.1f s, 1 thread, gmap nosimd "
-                      "objects via oracle/_ref); %.0f problems/s / %.1f calls per read" %
-                      (done, t_total, per_s, CALLS_PER_READ)}
+        lib.refh_single_gap_batch(a.ctypes.data, chunk, qb, qb)
+        t_single += time.perf_counter() - t0
+        ns += chunk
+        m = max(1, int(round(chunk * (1 - per_read_s) / per_read_s)))
+        m = min(m, len(ep) - ne)
+        b = np.ascontiguousarray(ep[ne:ne + m])
+        t0 = time.perf_counter()
+        lib.refh_end_gap_batch(b.ctypes.data, m, qb, qb)
+        t_end += time.perf_counter() - t0
+        ne += m
+        chunk = min(chunk * 2, 8192)
+    sec_per_read = SINGLE_PER_READ * t_single / ns + (END5_PER_READ + END3_PER_READ) * t_end / ne
+    return {"value": 1.0 / sec_per_read, "unit": "reads/s", "cores": 1, "kind": "reference",
+            "sample": "%d Dynprog_single_gap + %d Dynprog_end{5,3}_gap problems of the same stream "
+                      "(%.1f s, 1 thread, gmap nosimd objects via oracle/_ref), weighted %.1f + %.1f calls/read"
+                      % (ns, ne, t_single + t_end, SINGLE_PER_READ, END5_PER_READ + END3_PER_READ)}
 
 
 def main():
@@ -164,16 +234,17 @@ def main():
     dev = torch.device("cuda", local)
 
     genome = make_genome()
-    nprob = int(round(args.reads * CALLS_PER_READ))
-    probs, q = make_problems(genome, nprob, seed=1000 + rank)
+    sp, ep, q = make_workload(genome, args.reads, seed=1000 + rank)
+    ns, ne = len(sp), len(ep)
+    nprob = ns + ne
 
     eng = gmapdp.Engine(local)
     eng.set_genome(genome.tobytes())
     lib = eng.lib
     host_res = np.zeros(nprob, dtype=gmapdp.RESULT_DTYPE)
     plan = C.c_void_p()
-    eng._check(lib.gmapdp_plan_single(eng.h, probs.ctypes.data, nprob, host_res.ctypes.data, C.byref(plan)),
-               "gmapdp_plan_single")
+    eng._check(lib.gmapdp_plan_create(eng.h, sp.ctypes.data, ns, ep.ctypes.data, ne, host_res.ctypes.data,
+                                      C.byref(plan)), "gmapdp_plan_create")
     ngpu = lib.gmapdp_plan_gpu_problems(plan)
     cap = lib.gmapdp_plan_pair_capacity(plan)
     d_q = torch.from_numpy(q).to(dev)
@@ -186,23 +257,45 @@ def main():
         lib.gmapdp_plan_launch_info(plan, li, C.byref(R), C.byref(dl), C.byref(cnt), C.byref(lds))
         info.append((R.value, dl.value, cnt.value, lds.value))
     # the kernel template each launch runs; the dominant kernel is the template with most problems
-    kname = ["single_gap_kernel<R=%d,dirs_lds=%d>" % (i[0], i[1]) for i in info]
+    kname = ["dp_kernel<R=%d,dirs_lds=%d>" % (i[0], i[1]) for i in info]
+    tail = [lib.gmapdp_plan_launch_is_tail(plan, li) == 1 for li in range(nl)]
     per_kernel = {}
     for li in range(nl):
-        per_kernel.setdefault(kname[li], []).append(li)
+        if not tail[li]:
+            per_kernel.setdefault(kname[li], []).append(li)
     dominant = max(per_kernel, key=lambda k: sum(info[li][2] for li in per_kernel[k]))
-    stream = torch.cuda.Stream(dev)  # a real (non-null) stream: the events below see exactly these launches
+    # Same issue order as gmapdp_plan_run: tail classes (long problems, latency-bound) on side
+    # streams, the bulk on the main stream, joined at the end of the step.  Real (non-null)
+    # streams, so the per-launch events on the main stream see exactly the bulk launches.
+    stream = torch.cuda.Stream(dev)
+    sides = [torch.cuda.Stream(dev) for _ in range(3)]
+
+    def launch(li, s):
+        eng._check(lib.gmapdp_plan_run_launch(eng.h, plan, li, C.c_void_p(d_q.data_ptr()),
+                                              C.c_void_p(d_q.data_ptr()), C.c_void_p(d_res.data_ptr()),
+                                              C.c_void_p(d_pairs.data_ptr()), C.c_void_p(s.cuda_stream)),
+                   "gmapdp_plan_run_launch")
 
     def step(ev=None):
+        fork = torch.cuda.Event()
+        fork.record(stream)
+        used = 0
         for li in range(nl):
+            if tail[li]:
+                s = sides[used % len(sides)]
+                s.wait_event(fork)
+                launch(li, s)
+                used += 1
+        for li in range(nl):
+            if tail[li]:
+                continue
             if ev is not None:
                 ev[li][0].record(stream)
-            eng._check(lib.gmapdp_plan_run_launch(eng.h, plan, li, C.c_void_p(d_q.data_ptr()),
-                                                  C.c_void_p(d_q.data_ptr()), C.c_void_p(d_res.data_ptr()),
-                                                  C.c_void_p(d_pairs.data_ptr()), C.c_void_p(stream.cuda_stream)),
-                       "gmapdp_plan_run_launch")
+            launch(li, stream)
             if ev is not None:
                 ev[li][1].record(stream)
+        for s in sides[:used]:
+            stream.wait_stream(s)
 
     with torch.cuda.stream(stream):
         for _ in range(args.warmup):
@@ -224,7 +317,8 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    launch_ms = [sum(evs[k][li][0].elapsed_time(evs[k][li][1]) for k in range(args.steps)) / args.steps
+    launch_ms = [None if tail[li] else
+                 sum(evs[k][li][0].elapsed_time(evs[k][li][1]) for k in range(args.steps)) / args.steps
                  for li in range(nl)]
 
     # results of the last pass (for algorithmic byte accounting)
@@ -233,16 +327,21 @@ def main():
     gpu_mask = dev_index >= 0
     npairs = np.zeros(nprob, dtype=np.int64)
     npairs[gpu_mask] = res["npairs"][dev_index[gpu_mask]]
+    rl = np.concatenate([sp["rlength"], np.minimum(ep["rlength"], 660)]).astype(np.int64)
+    gl = np.concatenate([sp["glength"], np.minimum(ep["glength"], 2000)]).astype(np.int64)
+    desc = np.concatenate([np.full(ns, 56), np.full(ne, 64)])
     dom_launches = per_kernel[dominant]
     dom_bytes_total = 0
     for li in dom_launches:
-        members = np.zeros(info[li][2], dtype=np.int32)
-        lib.gmapdp_plan_launch_members(plan, li, members.ctypes.data)
-        dom_bytes_total += algorithmic_bytes(probs[members], npairs[members])
+        m = np.zeros(info[li][2], dtype=np.int32)
+        lib.gmapdp_plan_launch_members(plan, li, m.ctypes.data)
+        dom_bytes_total += algorithmic_bytes(rl[m], gl[m], npairs[m], desc[m])
     dom_ms = sum(launch_ms[li] for li in dom_launches) / len(dom_launches)   # average dispatch duration
     dom_bytes = dom_bytes_total / len(dom_launches)                          # average bytes per dispatch
-    step_bytes = algorithmic_bytes(probs[gpu_mask], npairs[gpu_mask])
+    g_idx = np.nonzero(gpu_mask)[0]
+    step_bytes = algorithmic_bytes(rl[g_idx], gl[g_idx], npairs[g_idx], desc[g_idx])
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    cells = banded_cells(sp, ep)
 
     reads_total = args.reads * world * args.steps
     value = reads_total / elapsed
@@ -259,14 +358,15 @@ def main():
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic",
-        "config": {"workload": "configs[1]: synthetic 2-kb cDNA Dynprog_single_gap sub-problem stream vs a "
-                               "chr22-length i.i.d. genome (seed 22), %.1f calls/read; DP engine only "
-                               "(Dynprog_end on GPU not yet in this round)" % CALLS_PER_READ,
+        "config": {"workload": "configs[1]: synthetic 2-kb cDNA DP sub-problem stream vs a chr22-length i.i.d. "
+                               "genome (seed 22): %.1f Dynprog_single_gap + %.1f Dynprog_end5_gap + %.1f "
+                               "Dynprog_end3_gap calls per read; DP engine only (host stages 1-3 excluded)"
+                               % (SINGLE_PER_READ, END5_PER_READ, END3_PER_READ),
                    "reads_per_step_per_gpu": args.reads, "subproblems_per_step_per_gpu": nprob,
-                   "banded_cells_per_step_per_gpu": banded_cells(probs),
+                   "banded_cells_per_step_per_gpu": cells,
                    "parallelism": "dp%d (reads sharded by rank, genome replicated)" % world,
                    "launch_classes": info},
-        "gcups": banded_cells(probs) * world * args.steps / elapsed / 1e9,
+        "gcups": cells * world * args.steps / elapsed / 1e9,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": dominant, "dispatches_per_step": len(dom_launches),
@@ -276,7 +376,7 @@ def main():
         "step_algorithmic_bytes": step_bytes,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(probs, q, genome)
+        out["cpu_baseline"] = cpu_baseline(sp, ep, q, genome)
     elif rank == 0:
         out["cpu_baseline"] = None
     lib.gmapdp_plan_destroy(plan)

@@ -42,7 +42,7 @@
 
 namespace gmapdp {
 
-constexpr int kSent = -(1 << 28);  // scan identity, far below any reachable score
+constexpr int kSent = (int)0x80000000;  // max-scan identity (INT_MIN); only ever max'ed, never added to
 
 __device__ __forceinline__ int dpp_wave_shl1(int x, int fill) {
   // lane i <- lane i+1; lane 63 <- fill
@@ -54,18 +54,19 @@ __device__ __forceinline__ int dpp_wave_shr1(int x, int fill) {
 }
 
 // Inclusive max-scan over the 64 lanes (lane order).  Lanes without a source
-// keep their own value (old = x), which is the max identity for that step.
+// read the identity INT_MIN, so the DPP move folds into v_max_i32_dpp.
 __device__ __forceinline__ int wave_scan_max(int x) {
-  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x111, 0xf, 0xf, false));  // row_shr:1
-  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x112, 0xf, 0xf, false));  // row_shr:2
-  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x114, 0xf, 0xf, false));  // row_shr:4
-  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x118, 0xf, 0xf, false));  // row_shr:8
-  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x142, 0xa, 0xf, false));  // row_bcast:15
-  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  x = max(x, __builtin_amdgcn_update_dpp(kSent, x, 0x111, 0xf, 0xf, false));  // row_shr:1
+  x = max(x, __builtin_amdgcn_update_dpp(kSent, x, 0x112, 0xf, 0xf, false));  // row_shr:2
+  x = max(x, __builtin_amdgcn_update_dpp(kSent, x, 0x114, 0xf, 0xf, false));  // row_shr:4
+  x = max(x, __builtin_amdgcn_update_dpp(kSent, x, 0x118, 0xf, 0xf, false));  // row_shr:8
+  x = max(x, __builtin_amdgcn_update_dpp(kSent, x, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  x = max(x, __builtin_amdgcn_update_dpp(kSent, x, 0x143, 0xc, 0xf, false));  // row_bcast:31
   return x;
 }
 
-__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+// wave64 ballot straight from the compare mask (no bool materialisation)
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ int lanes_below(uint64_t m, int lane) {
   return __popcll(m & ((1ull << lane) - 1ull));
 }
@@ -385,13 +386,19 @@ __global__ __launch_bounds__(64) void dp_kernel(
     }
     // Hs holds the stored nogap value (clamped at `sat`) except on band offset 0, whose only reader is
     // itself as the diagonal of the band-top row, which the reference takes unclamped (first_nogap).
+    int kext[R];  // k*ext per element: r*ext = rtop*ext + k*ext without a per-column multiply
+#pragma unroll
+    for (int i = 0; i < R; i++) kext[i] = (lane * R + i) * ext;
+    const int track = track_all ? 1 : (track_row ? 2 : 0);
     for (int c = 1; c <= glen; c++) {
-      const int gi = gcl[c];
+      const int gi = __builtin_amdgcn_readfirstlane(gcl[c]);  // wave-uniform genome class
       const int rtop = c - uband;
       const int rlo = rtop < 1 ? 1 : rtop;
       const int rhigh = (c + lband) < rlen ? (c + lband) : rlen;
+      const int rtop_ext = rtop * ext;
       // last_nogap entering row rlo (dynprog.c:1411-1449)
       const int L0 = (c == 1) ? (kNegInf32 - open + 1) : (c <= uband ? open + c * ext : kNegInf32);
+      const int row0 = (c <= uband) ? open + c * ext : kNegInf32;  // row 0 of this column (dynprog.c:1318-1325)
       const int8_t* scg = sc + gi * srow;
 
       int Ein[R], Hin[R];
@@ -406,7 +413,7 @@ __global__ __launch_bounds__(64) void dp_kernel(
       for (int i = 0; i < R; i++) {
         const int k = lane * R + i;
         const int r = rtop + k;
-        valid[i] = (k < W) && (r >= rlo) && (r <= rhigh);
+        valid[i] = (k < W) & (r >= rlo) & (r <= rhigh);
         const int s = scg[min(max(r, 0), rlen + 1)];
         // Egap (dynprog.c:1518-1524)
         const int es = Hin[i] + open;
@@ -415,7 +422,7 @@ __global__ __launch_bounds__(64) void dp_kernel(
         const int dg = Hs[i] + s;
         hb[i] = En[i] > dg - late;
         Hp[i] = max(En[i], dg);
-        A[i] = valid[i] ? Hp[i] + open - r * ext : kSent;
+        A[i] = valid[i] ? Hp[i] + open - rtop_ext - kext[i] : kSent;
       }
       // F chain: F(r) = r*ext + max(init, max_{rlo<=j<r} (H'(j) + open - j*ext))
       int pre[R];
@@ -428,9 +435,8 @@ __global__ __launch_bounds__(64) void dp_kernel(
       bool vb[R];
 #pragma unroll
       for (int i = 0; i < R; i++) {
-        const int r = rtop + lane * R + i;
         const int ex = (i == 0) ? X : max(X, pre[i - 1]);
-        F[i] = r * ext + max(init, ex);
+        F[i] = rtop_ext + kext[i] + max(init, ex);
         vb[i] = F[i] > Hp[i] - late;
         Hun[i] = max(F[i], Hp[i]);
       }
@@ -442,36 +448,31 @@ __global__ __launch_bounds__(64) void dp_kernel(
       for (int i = 0; i < R; i++) {
         const int k = lane * R + i;
         const int r = rtop + k;
-        int fprev = (i == 0) ? Fup : F[i - 1];
-        int hprev = (i == 0) ? Hup : Hun[i - 1];
-        if (r == rlo) { fprev = kNegInf32; hprev = L0; }
+        const bool top = r == rlo;
+        const int fprev = top ? kNegInf32 : ((i == 0) ? Fup : F[i - 1]);
+        const int hprev = top ? L0 : ((i == 0) ? Hup : Hun[i - 1]);
         const bool fb = fprev > hprev + open - late;
-        mV[i] = ballot(valid[i] && vb[i]);
-        mH[i] = ballot(valid[i] && hb[i] && !vb[i]);
-        mE[i] = ballot(valid[i] && eb[i]);
-        mF[i] = ballot(valid[i] && fb);
+        mV[i] = ballot(valid[i] & vb[i]);
+        mH[i] = ballot(valid[i] & hb[i] & !vb[i]);
+        mE[i] = ballot(valid[i] & eb[i]);
+        mF[i] = ballot(valid[i] & fb);
         const int Hc = max(Hun[i], sat);
-        if (valid[i]) {
-          Hs[i] = (k == 0) ? Hun[i] : Hc;
-          E[i] = En[i];
-          // best endpoint (find_best_endpoint_std / _to_queryend_indels_std): scan-order first/last max
-          if ((track_all || (track_row && r == rlen)) && Hc > bv[i] - late) { bv[i] = Hc; bcol[i] = c; }
-        } else {
-          Hs[i] = (r == 0 && c <= uband) ? open + c * ext : kNegInf32;  // row 0 (dynprog.c:1318-1325)
-          E[i] = kNegInf32;
-        }
+        // branch-free state update for the next column
+        Hs[i] = valid[i] ? ((k == 0) ? Hun[i] : Hc) : ((r == 0) ? row0 : kNegInf32);
+        E[i] = valid[i] ? En[i] : kNegInf32;
+        // best endpoint (find_best_endpoint_std / _to_queryend_indels_std): scan-order first/last max
+        const bool cand = valid[i] & ((track == 1) | ((track == 2) & (r == rlen))) & (Hc > bv[i] - late);
+        bv[i] = cand ? Hc : bv[i];
+        bcol[i] = cand ? c : bcol[i];
       }
+      if (lane == 0) {  // one lane stores the column's 4R direction words
+        uint64_t* dcol = dirs + (size_t)c * 4 * R;
 #pragma unroll
-      for (int w0 = 0; w0 < 4 * R; w0 += 64) {  // 4R words per column, 64 lanes per pass
-        const int w = w0 + lane;
-        if (w < 4 * R) {
-          const int tt = w / R, i = w % R;
-          uint64_t m = 0;
-#pragma unroll
-          for (int ii = 0; ii < R; ii++) {
-            if (ii == i) m = (tt == 0) ? mH[ii] : (tt == 1) ? mV[ii] : (tt == 2) ? mE[ii] : mF[ii];
-          }
-          dirs[((size_t)c * 4 + tt) * R + i] = m;
+        for (int i = 0; i < R; i++) {
+          dcol[0 * R + i] = mH[i];
+          dcol[1 * R + i] = mV[i];
+          dcol[2 * R + i] = mE[i];
+          dcol[3 * R + i] = mF[i];
         }
       }
     }

@@ -133,6 +133,14 @@ struct gmapdp_ctx {
   int mode = 0;
   int user_open = 0, user_extend = 0, user_dynprog_p = 0;
   hipStream_t stream = nullptr;
+  // Side streams for the long-problem launch classes: a class of a few
+  // thousand long fills runs as a latency-bound tail, so it overlaps the
+  // bulk classes instead of following them (the launch order within a class
+  // is longest-first already).
+  static constexpr int kAux = 3;
+  hipStream_t aux[kAux] = {nullptr, nullptr, nullptr};
+  hipEvent_t ev_fork = nullptr;
+  hipEvent_t ev_join[kAux] = {nullptr, nullptr, nullptr};
   Tables* tables = nullptr;
   int8_t* d_sc = nullptr;
   uint8_t* d_cs = nullptr;
@@ -197,6 +205,11 @@ int gmapdp_create(gmapdp_ctx** out, int device, int mode, int user_open, int use
   ctx->user_dynprog_p = user_dynprog_p;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  for (int i = 0; i < gmapdp_ctx::kAux && e == hipSuccess; i++) {
+    e = hipStreamCreateWithFlags(&ctx->aux[i], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join[i], hipEventDisableTiming);
+  }
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
   ctx->tables = new Tables();
   build_tables(*ctx->tables, mode);
   if (e == hipSuccess) e = hipMalloc(&ctx->d_sc, sizeof(ctx->tables->sc));
@@ -218,6 +231,12 @@ void gmapdp_destroy(gmapdp_ctx* ctx) {
   if (ctx->d_sc) (void)hipFree(ctx->d_sc);
   if (ctx->d_cs) (void)hipFree(ctx->d_cs);
   if (ctx->d_genome) (void)hipFree(ctx->d_genome);
+  for (int i = 0; i < gmapdp_ctx::kAux; i++) {
+    if (ctx->aux[i]) (void)hipStreamSynchronize(ctx->aux[i]);
+    if (ctx->aux[i]) (void)hipStreamDestroy(ctx->aux[i]);
+    if (ctx->ev_join[i]) (void)hipEventDestroy(ctx->ev_join[i]);
+  }
+  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx->tables;
   delete ctx;
@@ -498,6 +517,12 @@ static int build_plan(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int
   return GMAPDP_OK;
 }
 
+// A class too small to fill the chip (< 16 waves per CU) or made of wide / spilled
+// problems is latency-bound: it runs concurrently with the bulk on a side stream.
+static bool launch_is_tail(const PlanCore::Launch& L) {
+  return L.count < 4096 || L.R > 1 || !L.dirs_lds;
+}
+
 static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, const DevProblem* d_probs,
                              const int* d_order, const char* d_q, const char* d_quc, gmapdp_result* d_results,
                              gmapdp_pair* d_pairs, hipStream_t stream) {
@@ -514,10 +539,26 @@ static int run_plan(gmapdp_ctx* ctx, const PlanCore& plan, const DevProblem* d_p
     hipError_t e = ctx->gdirs.ensure(plan.gdirs_bytes);
     if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "direction scratch: %s", e);
   }
-  for (size_t li = 0; li < plan.launches.size(); li++) {
-    hipError_t e = launch_one(ctx, plan, (int)li, d_probs, d_order, d_q, d_quc, d_results, d_pairs, stream);
-    if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "dp launch: %s", e);
+  // Tail classes (long problems) fork onto side streams first, the bulk follows on `stream`,
+  // then `stream` joins the side streams: the step ends when the slower of the two ends.
+  hipError_t e = hipEventRecord(ctx->ev_fork, stream);
+  int naux = 0;
+  for (size_t li = 0; li < plan.launches.size() && e == hipSuccess; li++) {
+    if (!launch_is_tail(plan.launches[li])) continue;
+    hipStream_t s = ctx->aux[naux % gmapdp_ctx::kAux];
+    if (naux < gmapdp_ctx::kAux) e = hipStreamWaitEvent(s, ctx->ev_fork, 0);
+    if (e == hipSuccess) e = launch_one(ctx, plan, (int)li, d_probs, d_order, d_q, d_quc, d_results, d_pairs, s);
+    naux++;
   }
+  for (size_t li = 0; li < plan.launches.size() && e == hipSuccess; li++) {
+    if (launch_is_tail(plan.launches[li])) continue;
+    e = launch_one(ctx, plan, (int)li, d_probs, d_order, d_q, d_quc, d_results, d_pairs, stream);
+  }
+  for (int i = 0; i < naux && i < gmapdp_ctx::kAux && e == hipSuccess; i++) {
+    e = hipEventRecord(ctx->ev_join[i], ctx->aux[i]);
+    if (e == hipSuccess) e = hipStreamWaitEvent(stream, ctx->ev_join[i], 0);
+  }
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "dp launch: %s", e);
   return GMAPDP_OK;
 }
 
@@ -667,6 +708,11 @@ int gmapdp_plan_launch_info(const gmapdp_plan* plan, int li, int* R, int* dirs_l
   if (count) *count = L.count;
   if (lds) *lds = L.lds;
   return GMAPDP_OK;
+}
+
+int gmapdp_plan_launch_is_tail(const gmapdp_plan* plan, int li) {
+  if (!plan || li < 0 || li >= (int)plan->in.launches.size()) return GMAPDP_EINVAL;
+  return launch_is_tail(plan->in.launches[li]) ? 1 : 0;
 }
 
 int gmapdp_plan_launch_members(const gmapdp_plan* plan, int li, int* problem_indices) {

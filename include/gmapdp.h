@@ -197,6 +197,9 @@ int gmapdp_plan_run (gmapdp_ctx *ctx, const gmapdp_plan *plan, const char *d_qse
                      gmapdp_result *d_results, gmapdp_pair *d_pairs, void *stream);
 /* Per-launch-class access (one kernel launch per class; for profiling). */
 int gmapdp_plan_launch_info (const gmapdp_plan *plan, int li, int *R, int *dirs_lds, int *count, size_t *lds);
+/* 1 if launch li is a latency-bound tail class that gmapdp_plan_run issues on
+ * a side stream concurrently with the bulk classes. */
+int gmapdp_plan_launch_is_tail (const gmapdp_plan *plan, int li);
 /* Original problem indices of launch li (count entries, launch order). */
 int gmapdp_plan_launch_members (const gmapdp_plan *plan, int li, int *problem_indices);
 int gmapdp_plan_run_launch (gmapdp_ctx *ctx, const gmapdp_plan *plan, int li, const char *d_qseq,

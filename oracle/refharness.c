@@ -176,6 +176,45 @@ refh_single_gap_batch (const RefSingleProblem *probs, int n, const char *qseq, c
   return total;
 }
 
+/* Same for Dynprog_end5_gap / Dynprog_end3_gap over include/gmapdp.h's
+   gmapdp_end_problem layout (restated). */
+typedef struct {
+  int qoff, rlength, glength, roffset, goffset;
+  unsigned int chroffset, chrhigh;
+  int flags, genestrand, extraband, end3p, endalign, require_pos_score_p, dynprogindex;
+  double defect_rate;
+} RefEndProblem;
+
+long
+refh_end_gap_batch (const RefEndProblem *probs, int n, const char *qseq, const char *qseq_uc) {
+  long total = 0;
+  int i, dpi, score, nmatches, nmismatches, nopens, nindels;
+  List_T pairs;
+  for (i = 0; i < n; i++) {
+    const RefEndProblem *p = &probs[i];
+    Pairpool_reset(pairpool);
+    dpi = p->dynprogindex;
+    if (p->end3p) {
+      pairs = Dynprog_end3_gap(&dpi, &score, &nmatches, &nmismatches, &nopens, &nindels, dynprogR,
+                               (char *) qseq + p->qoff, (char *) qseq_uc + p->qoff, p->rlength, p->glength,
+                               p->roffset, p->goffset, (Univcoord_T) p->chroffset, (Univcoord_T) p->chrhigh,
+                               (p->flags & 1) ? true : false, p->genestrand, (p->flags & 2) ? true : false,
+                               genome, genome, pairpool, p->extraband, p->defect_rate,
+                               (Endalign_T) p->endalign, p->require_pos_score_p ? true : false);
+    } else {
+      pairs = Dynprog_end5_gap(&dpi, &score, &nmatches, &nmismatches, &nopens, &nindels, dynprogL,
+                               (char *) qseq + p->qoff + p->rlength - 1, (char *) qseq_uc + p->qoff + p->rlength - 1,
+                               p->rlength, p->glength, p->roffset, p->goffset,
+                               (Univcoord_T) p->chroffset, (Univcoord_T) p->chrhigh,
+                               (p->flags & 1) ? true : false, p->genestrand, (p->flags & 2) ? true : false,
+                               genome, genome, pairpool, p->extraband, p->defect_rate,
+                               (Endalign_T) p->endalign, p->require_pos_score_p ? true : false);
+    }
+    total += List_length(pairs);
+  }
+  return total;
+}
+
 /* endalign: 0 QUERYEND_GAP, 1 QUERYEND_INDELS, 2 QUERYEND_NOGAPS, 3 BEST_LOCAL (dynprog.h:23) */
 int
 refh_end_gap (int end3p, const char *qbuf, const char *qucbuf, int qpos, int rlength, int glength,
