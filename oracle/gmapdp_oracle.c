@@ -58,6 +58,7 @@ static unsigned char consistent[3][128][128];
 static int use8p_size[4];
 static int g_mode;
 static int g_user_open, g_user_extend, g_user_dynprog_p;
+static void intron_score_setup (void);
 
 static const char *g_genome = NULL;
 static unsigned int g_genomelength = 0;
@@ -134,6 +135,7 @@ orc_init (int mode, int user_open, int user_extend, int user_dynprog_p) {
 
   memset(pairdistance, 0, sizeof(pairdistance));
   memset(consistent, 0, sizeof(consistent));
+  intron_score_setup();
   g_mode = mode;
   g_user_open = user_open;
   g_user_extend = user_extend;
@@ -810,4 +812,473 @@ orc_end_gap (int end3p, const char *qbuf, const char *qucbuf, int qpos, int rlen
   n -= first;
   if (!end3p) reverse_pairs(out, n); /* end5 returns List_reverse once more */
   return n > 0 ? n : -1;
+}
+
+/* ---------------------------------------------------------------------------
+ * Dynprog_genome_gap (dynprog_genome.c:3288-3901), nosimd build, no splicing
+ * IIT (Dynprog_genome_setup with splicing_iit NULL: get_known_splicesites
+ * :405 adds nothing, so left_known/right_known stay 0 and
+ * bridge_intron_gap_site_level :2469 is the bridge).  The MaxEnt splice-site
+ * probabilities (Maxent_hr_*_prob, maxent_hr.c:27357-27600) are host inputs:
+ * left_probs[c], c in [0, glengthL), and right_probs[c], c in [0, glengthR),
+ * at the positions orc_genome_splice_sites gives (:2573-2660, :332-401).
+ * ------------------------------------------------------------------------- */
+#define PAIRED_OPEN_HIGHQ -8
+#define PAIRED_OPEN_MEDQ -7
+#define PAIRED_OPEN_LOWQ -6
+#define PAIRED_EXTEND_HIGHQ -3
+#define PAIRED_EXTEND_MEDQ -2
+#define PAIRED_EXTEND_LOWQ -1
+#define PROB_CEILING 0.85                /* dynprog_genome.c:82 */
+#define GCAG_INTRON 8                    /* :98-103 */
+#define ATAC_INTRON 4
+#define FINAL_GCAG_INTRON 10
+#define FINAL_ATAC_INTRON 8
+#define CANONICAL_INTRON_HIGHQ 14        /* :109 */
+#define FINAL_CANONICAL_INTRON_HIGHQ 16  /* :114 */
+/* intron.h:11-35 */
+#define LEFT_GT 0x21
+#define LEFT_GC 0x10
+#define LEFT_AT 0x08
+#define LEFT_CT 0x06
+#define RIGHT_AG 0x30
+#define RIGHT_AC 0x0C
+#define RIGHT_GC 0x02
+#define RIGHT_AT 0x01
+#define GTAG_FWD 0x20
+#define GCAG_FWD 0x10
+#define ATAC_FWD 0x08
+#define GTAG_REV 0x04
+#define GCAG_REV 0x02
+#define ATAC_REV 0x01
+#define ORC_UNSET (-2147483647 - 1)
+
+/* intron_score_setup (dynprog_genome.c:144): [direction class][finalp][leftdi & rightdi];
+   class 0 = sense (cdna_direction > 0), 1 = antisense (< 0), 2 = either. */
+static int intron_score[3][2][64];
+
+static void
+intron_score_setup (void) {
+  memset(intron_score, 0, sizeof(intron_score));
+  intron_score[0][1][GTAG_FWD] = FINAL_CANONICAL_INTRON_HIGHQ;
+  intron_score[0][1][GCAG_FWD] = FINAL_GCAG_INTRON;
+  intron_score[0][1][ATAC_FWD] = FINAL_ATAC_INTRON;
+  intron_score[0][0][GTAG_FWD] = CANONICAL_INTRON_HIGHQ;
+  intron_score[0][0][GCAG_FWD] = GCAG_INTRON;
+  intron_score[0][0][ATAC_FWD] = ATAC_INTRON;
+  intron_score[1][1][GTAG_REV] = FINAL_CANONICAL_INTRON_HIGHQ;
+  intron_score[1][1][GCAG_REV] = FINAL_GCAG_INTRON;
+  intron_score[1][1][ATAC_REV] = FINAL_ATAC_INTRON;
+  intron_score[1][0][GTAG_REV] = CANONICAL_INTRON_HIGHQ;
+  intron_score[1][0][GCAG_REV] = GCAG_INTRON;
+  intron_score[1][0][ATAC_REV] = ATAC_INTRON;
+  /* "either" keeps the reference's mixed FINAL/regular values (:172-184) */
+  intron_score[2][1][GTAG_FWD] = FINAL_CANONICAL_INTRON_HIGHQ;
+  intron_score[2][1][GCAG_FWD] = FINAL_GCAG_INTRON;
+  intron_score[2][1][ATAC_FWD] = FINAL_ATAC_INTRON;
+  intron_score[2][1][GTAG_REV] = CANONICAL_INTRON_HIGHQ;
+  intron_score[2][1][GCAG_REV] = FINAL_GCAG_INTRON;
+  intron_score[2][1][ATAC_REV] = FINAL_ATAC_INTRON;
+  intron_score[2][0][GTAG_FWD] = FINAL_CANONICAL_INTRON_HIGHQ;
+  intron_score[2][0][GCAG_FWD] = GCAG_INTRON;
+  intron_score[2][0][ATAC_FWD] = ATAC_INTRON;
+  intron_score[2][0][GTAG_REV] = CANONICAL_INTRON_HIGHQ;
+  intron_score[2][0][GCAG_REV] = GCAG_INTRON;
+  intron_score[2][0][ATAC_REV] = ATAC_INTRON;
+}
+
+int
+orc_intron_scores (int *out3x2x64) {
+  intron_score_setup();
+  memcpy(out3x2x64, intron_score, sizeof(intron_score));
+  return 0;
+}
+
+/* dinucleotide codes (dynprog_genome.c:2518-2566, no genomealt: alt == ref) */
+static int
+left_dinucl (char left1, char left2) {
+  if (left1 == 'G' && left2 == 'T') return LEFT_GT;
+  if (left1 == 'G' && left2 == 'C') return LEFT_GC;
+  if (left1 == 'A' && left2 == 'T') return LEFT_AT;
+  if (left1 == 'C' && left2 == 'T') return LEFT_CT;
+  return 0;
+}
+
+static int
+right_dinucl (char right2, char right1) {
+  if (right2 == 'A' && right1 == 'G') return RIGHT_AG;
+  if (right2 == 'A' && right1 == 'C') return RIGHT_AC;
+  if (right2 == 'G' && right1 == 'C') return RIGHT_GC;
+  if (right2 == 'A' && right1 == 'T') return RIGHT_AT;
+  return 0;
+}
+
+/* Splice-site positions and models of the probability arrays
+   (bridge_intron_gap_site_level :2573-2660 = get_splicesite_probs :332-401).
+   model: 0 donor, 1 acceptor, 2 antidonor, 3 antiacceptor.  Univcoord_T
+   arithmetic is 32-bit unsigned. */
+int
+orc_genome_splice_sites (int glengthL, int glengthR, int goffsetL, int rev_goffsetR, unsigned int chroffset,
+                         unsigned int chrhigh, int cdna_direction, int watsonp, unsigned int *posL, int *modelL,
+                         unsigned int *posR, int *modelR) {
+  int c;
+  unsigned int leftoffset = (unsigned int) goffsetL, rightoffset = (unsigned int) rev_goffsetR;
+  for (c = 0; c < glengthL; c++) {
+    if (watsonp) {
+      posL[c] = chroffset + leftoffset + (unsigned int) c;
+      modelL[c] = cdna_direction > 0 ? 0 : 3;
+    } else {
+      posL[c] = chrhigh - leftoffset - (unsigned int) c + 1u;
+      modelL[c] = cdna_direction > 0 ? 2 : 1;
+    }
+  }
+  for (c = 0; c < glengthR; c++) {
+    if (watsonp) {
+      posR[c] = chroffset + rightoffset - (unsigned int) c + 1u;
+      modelR[c] = cdna_direction > 0 ? 1 : 2;
+    } else {
+      posR[c] = chrhigh - rightoffset + (unsigned int) c;
+      modelR[c] = cdna_direction > 0 ? 3 : 0;
+    }
+  }
+  return 0;
+}
+
+typedef struct {
+  int score, nmatches, nmismatches, nopens, nindels;
+  int new_left, new_right, exonhead, introntype, dpi;
+  double left_prob, right_prob;
+} GGOut;
+
+/* one diagonal cell pushed by genome_gap_simple (:3184-3272) */
+static void
+simple_push (PairSink *s, GGOut *o, char c1, char c1_uc, char c2, int querypos, int genomepos, int genestrand,
+             int dpi) {
+  if (c2 == '*') {
+  } else if (c1_uc == c2) {
+    o->score += MATCH; o->nmatches += 1;
+    sink_push(s, querypos, genomepos, c1, DYNPROG_MATCH_COMP, c2, c2, dpi);
+  } else if (consistent[genestrand][(unsigned char) c1_uc][(unsigned char) c2]) {
+    o->score += MATCH; o->nmatches += 1;
+    sink_push(s, querypos, genomepos, c1, AMBIGUOUS_COMP, c2, c2, dpi);
+  } else {
+    o->score += MISMATCH; o->nmismatches += 1;
+    sink_push(s, querypos, genomepos, c1, MISMATCH_COMP, c2, c2, dpi);
+  }
+}
+
+/* genome_gap_simple (dynprog_genome.c:3006-3280).  Returns the number of pairs
+   (reference list order) or -1 when it declines. */
+static int
+genome_gap_simple (PairSink *s, GGOut *o, const char *rsequence, const char *rsequenceuc,
+                   const char *rev_rsequence, const char *rev_rsequenceuc, int rlength, const char *gL,
+                   const char *revR, int roffset, int rev_roffset, int leftoffset, int rightoffset,
+                   int mismatchtype, int dirclass, const double *left_probs, const double *right_probs,
+                   int genestrand, int dpi, int halfp) {
+  const int *isc = intron_score[dirclass][0];  /* assumes finalp false (:3032) */
+  short (*pd)[128] = pairdistance[mismatchtype];
+  int scoreL = 0, scoreR = 0, bestscore = 0, bestscoreI = 0, bestrL = -1, bestrR = -1;
+  int rL, rR, r, score, scoreI, introntype, finalscore, n;
+
+  for (rR = 1; rR < rlength; rR++) scoreR += pd[(unsigned char) rev_rsequenceuc[1 - rR]][(unsigned char) revR[1 - rR]];
+  for (rL = 1, rR = rlength - 1; rL < rlength; rL++, rR--) {
+    scoreL += pd[(unsigned char) rsequenceuc[rL - 1]][(unsigned char) gL[rL - 1]];
+    introntype = left_dinucl(gL[rL], gL[rL + 1]) & right_dinucl(revR[-rR - 1], revR[-rR]);
+    scoreI = isc[introntype];
+    if (introntype != 0 && (score = scoreL + scoreI + scoreR) >= bestscore) {  /* >= : jump late */
+      bestscore = score;
+      bestscoreI = scoreI;
+      bestrL = rL;
+      bestrR = rR;
+      o->introntype = introntype;
+    }
+    scoreR -= pd[(unsigned char) rev_rsequenceuc[1 - rR]][(unsigned char) revR[1 - rR]];
+  }
+  finalscore = halfp ? bestscore - bestscoreI / 2 : bestscore;
+  o->score = o->nmatches = o->nmismatches = 0;
+  if (finalscore <= 0) return -1;
+  o->left_prob = left_probs[bestrL];
+  o->right_prob = right_probs[bestrR];
+  if (o->left_prob < 0.90 || o->right_prob < 0.90) return -1;
+
+  for (r = 1; r <= bestrL; r++)
+    simple_push(s, o, rsequence[r - 1], rsequenceuc[r - 1], gL[r - 1], roffset + r - 1, leftoffset + r - 1,
+                genestrand, dpi);
+  o->new_left = leftoffset + (bestrL - 1);
+  o->new_right = o->exonhead = rightoffset - (bestrR - 1);
+  sink_gapholder(s, 0, o->new_right - o->new_left - 1);
+  for (r = bestrR; r > 0; r--)
+    simple_push(s, o, rev_rsequence[1 - r], rev_rsequenceuc[1 - r], revR[1 - r], rev_roffset + 1 - r,
+                rightoffset + 1 - r, genestrand, dpi);
+  n = s->n < s->cap ? s->n : s->cap;
+  reverse_pairs(s->buf, n);  /* pushes prepend, no List_reverse ("Already reversed") */
+  return s->n;
+}
+
+/* bridge_intron_gap_site_level (dynprog_genome.c:2469-2893) with the bands of
+   bridge_intron_gap (:2924-2928).  Returns finalscore. */
+static int
+bridge_site_level (int *bestrL, int *bestrR, int *bestcL, int *bestcR, const int *matrixL, const int *matrixR,
+                   const char *gL, const char *revR, int rlength, int glengthL, int glengthR, int dirclass,
+                   int finalp, int halfp, int lbandL, int ubandL, int lbandR, int ubandR, int leftoffset,
+                   int rightoffset, const double *lp, const double *rp) {
+  const int *isc = intron_score[dirclass][finalp ? 1 : 0];
+  int *leftdi = (int *) malloc((glengthL + 1) * sizeof(int));
+  int *rightdi = (int *) malloc((glengthR + 1) * sizeof(int));
+  int rL, rR, cL, cR, cloL, chighL, cloR, chighR, scoreL, scoreR, scoreI, score;
+  int bestscore = NEG_INFINITY_32, bestscore_with_dinucl = NEG_INFINITY_32;
+  int bestrL_d = 0, bestrR_d = 0, bestcL_d = 0, bestcR_d = 0, use_dinucl_p;
+  double probL, probR, bestprob_with_score = 0.0, bestprob_with_dinucl = 0.0;
+#define ML(c, r) matrixL[(size_t) (c) * (size_t) (rlength + 1) + (size_t) (r)]
+#define MR(c, r) matrixR[(size_t) (c) * (size_t) (rlength + 1) + (size_t) (r)]
+#define CONSIDER()                                                                              \
+  do {                                                                                          \
+    if ((score = scoreL + scoreI + scoreR) > bestscore) {                                       \
+      bestscore = score; *bestrL = rL; *bestrR = rR; *bestcL = cL; *bestcR = cR;                 \
+      bestprob_with_score = probL + probR;                                                      \
+    } else if (score == bestscore && probL + probR > bestprob_with_score) {                     \
+      *bestrL = rL; *bestrR = rR; *bestcL = cL; *bestcR = cR;                                    \
+      bestprob_with_score = probL + probR;                                                      \
+    }                                                                                           \
+  } while (0)
+
+  for (cL = 0; cL < glengthL - 1; cL++) leftdi[cL] = left_dinucl(gL[cL], gL[cL + 1]);
+  leftdi[glengthL - 1] = leftdi[glengthL] = 0;
+  for (cR = 0; cR < glengthR - 1; cR++) rightdi[cR] = right_dinucl(revR[-cR - 1], revR[-cR]);
+  rightdi[glengthR - 1] = rightdi[glengthR] = 0;
+
+  for (rL = 1, rR = rlength - 1; rL < rlength; rL++, rR--) {
+    if ((cloL = rL - lbandL) < 1) cloL = 1;
+    if ((chighL = rL + ubandL) > glengthL - 1) chighL = glengthL - 1;
+    if ((cloR = rR - lbandR) < 1) cloR = 1;
+    if ((chighR = rR + ubandR) > glengthR - 1) chighR = glengthR - 1;
+
+    /* A: no indels */
+    cL = rL; probL = lp[cL]; scoreL = ML(cL, rL);
+    cR = rR; probR = rp[cR]; scoreR = MR(cR, rR);
+    scoreI = isc[leftdi[cL] & rightdi[cR]];
+    CONSIDER();
+    if (scoreI > 0 && probL + probR > bestprob_with_dinucl) {
+      bestscore_with_dinucl = scoreL + scoreI + scoreR;
+      bestcL_d = cL; bestcR_d = cR; bestrL_d = rL; bestrR_d = rR;
+      bestprob_with_dinucl = probL + probR;
+    }
+    /* B: indel on the right */
+    cL = rL; probL = lp[cL]; scoreL = ML(cL, rL);
+    for (cR = cloR; cR < chighR && cR < rightoffset - leftoffset - cL; cR++) {
+      probR = rp[cR];
+      scoreR = MR(cR, rR);
+      scoreI = isc[leftdi[cL] & rightdi[cR]];
+      CONSIDER();
+    }
+    /* C: indel on the left */
+    cR = rR; probR = rp[cR]; scoreR = MR(cR, rR);
+    for (cL = cloL; cL < chighL && cL < rightoffset - leftoffset - cR; cL++) {
+      probL = lp[cL];
+      scoreL = ML(cL, rL);
+      scoreI = isc[leftdi[cL] & rightdi[cR]];
+      CONSIDER();
+    }
+  }
+#undef CONSIDER
+#undef ML
+#undef MR
+
+  if (bestprob_with_score > 2 * PROB_CEILING) use_dinucl_p = 0;
+  else if (bestprob_with_dinucl == 0.0) use_dinucl_p = 0;
+  else if (bestscore_with_dinucl < 0 || bestscore_with_dinucl < bestscore - 9) use_dinucl_p = 0;
+  else use_dinucl_p = 1;
+  if (use_dinucl_p) {
+    *bestcL = bestcL_d; *bestcR = bestcR_d; *bestrL = bestrL_d; *bestrR = bestrR_d;
+    bestscore = bestscore_with_dinucl;
+  }
+  if (bestscore >= 0 && halfp) {
+    /* the reference reads leftdi/rightdi after FREEA (alloca: still valid) */
+    scoreI = isc[leftdi[*bestcL] & rightdi[*bestcR]];
+    bestscore = bestscore - scoreI / 2;
+  }
+  free(leftdi);
+  free(rightdi);
+  return bestscore;
+}
+
+/* Pair_maxnegscore (pair.c:8528) over pairs in list order */
+static int
+maxnegscore (const OrcPair *p, int n) {
+  int maxneg = 0, prevhigh = 0, score = 0, i = 0;
+  while (i < n) {
+    if (p[i].gapp) {
+      i++;
+    } else if (p[i].comp == MISMATCH_COMP) {
+      score += MISMATCH;
+      if (score - prevhigh < maxneg) maxneg = score - prevhigh;
+      i++;
+    } else if (p[i].comp == INDEL_COMP) {
+      score += QOPEN + QINDEL;
+      i++;
+      while (i < n && p[i].comp == INDEL_COMP) { score += QINDEL; i++; }
+      if (score - prevhigh < maxneg) maxneg = score - prevhigh;
+    } else {
+      score += MATCH;
+      if (score > prevhigh) prevhigh = score;
+      i++;
+    }
+  }
+  return maxneg;
+}
+
+static void
+gg_scalars (const GGOut *o, int *scalars, double *dscalars) {
+  scalars[0] = o->dpi; scalars[1] = o->score; scalars[2] = o->nmatches; scalars[3] = o->nmismatches;
+  scalars[4] = o->nopens; scalars[5] = o->nindels; scalars[6] = o->new_left; scalars[7] = o->new_right;
+  scalars[8] = o->exonhead; scalars[9] = o->introntype;
+  dscalars[0] = o->left_prob; dscalars[1] = o->right_prob;
+}
+
+/* flags: 1 watsonp, 2 jump_late_p, 8 halfp, 16 finalp. */
+int
+orc_genome_gap (const char *rsequence, const char *rsequenceuc, int rlength, int glengthL, int glengthR,
+                int roffset, int goffsetL, int rev_goffsetR, unsigned int chroffset, unsigned int chrhigh,
+                int cdna_direction, int flags, int genestrand, int extraband_paired, double defect_rate,
+                int maxpeelback, int dynprogindex, const double *left_probs, const double *right_probs,
+                int *scalars, double *dscalars, OrcPair *out, int max_pairs) {
+  const int watsonp = flags & 1, jump_late_p = (flags & 2) ? 1 : 0, halfp = (flags & 8) ? 1 : 0;
+  const int finalp = (flags & 16) ? 1 : 0;
+  const int dirclass = cdna_direction > 0 ? 0 : (cdna_direction < 0 ? 1 : 2);
+  int mismatchtype, open, extend, lbandL, ubandL, lbandR, ubandR, finalscore, n, nR, i;
+  int bestrL = -1, bestrR = 0, bestcL = 0, bestcR = 0;
+  int rev_roffset;
+  char *gL, *gLa, *gR, *gRa;
+  const char *revR, *rev_rsequence, *rev_rsequenceuc;
+  int *matrixL, *matrixR;
+  signed char *dirsL, *dirsR;
+  PairSink sink = {out, 0, max_pairs};
+  Tally t = {0, 0, 0, 0, 0};
+  GGOut o;
+
+  o.score = ORC_UNSET;
+  o.nmatches = o.nmismatches = o.nopens = o.nindels = 0;
+  o.new_left = o.new_right = o.exonhead = ORC_UNSET;
+  o.introntype = 0;
+  o.left_prob = o.right_prob = 0.0;
+  o.dpi = dynprogindex;
+  if (rlength <= 1) {
+    o.score = NEG_INFINITY_32;
+    gg_scalars(&o, scalars, dscalars);
+    return -1;
+  }
+  if (defect_rate < DEFECT_HIGHQ) mismatchtype = HIGHQ;
+  else if (defect_rate < DEFECT_MEDQ) mismatchtype = MEDQ;
+  else mismatchtype = LOWQ;
+  if (g_user_dynprog_p) { open = g_user_open; extend = g_user_extend; }
+  else if (defect_rate < DEFECT_HIGHQ) {
+    if (rlength > maxpeelback * 4) { open = SINGLE_OPEN_HIGHQ; extend = SINGLE_EXTEND_HIGHQ; }
+    else { open = PAIRED_OPEN_HIGHQ; extend = PAIRED_EXTEND_HIGHQ; }
+  } else if (defect_rate < DEFECT_MEDQ) {
+    if (rlength > maxpeelback * 4) { open = SINGLE_OPEN_MEDQ; extend = SINGLE_EXTEND_MEDQ; }
+    else { open = PAIRED_OPEN_MEDQ; extend = PAIRED_EXTEND_MEDQ; }
+  } else {
+    if (rlength > maxpeelback * 4) { open = SINGLE_OPEN_LOWQ; extend = SINGLE_EXTEND_LOWQ; }
+    else { open = PAIRED_OPEN_LOWQ; extend = PAIRED_EXTEND_LOWQ; }
+  }
+  if (rlength > ORC_MAX_RLENGTH || glengthL > ORC_MAX_GLENGTH || glengthR > ORC_MAX_GLENGTH) {
+    o.new_left = goffsetL - 1;
+    o.new_right = rev_goffsetR + 1;
+    o.exonhead = roffset + rlength - 1;
+    o.dpi = dynprogindex + (dynprogindex > 0 ? +1 : -1);
+    o.score = NEG_INFINITY_32;
+    gg_scalars(&o, scalars, dscalars);
+    return -1;
+  }
+  rev_rsequence = rsequence + rlength - 1;
+  rev_rsequenceuc = rsequenceuc + rlength - 1;
+  rev_roffset = roffset + rlength - 1;
+  gL = (char *) malloc(glengthL + 1); gLa = (char *) malloc(glengthL + 1);
+  gR = (char *) malloc(glengthR + 1); gRa = (char *) malloc(glengthR + 1);
+  if (watsonp) {
+    orc_get_segment(1, chroffset + (unsigned int) goffsetL, glengthL, chrhigh, 0, gL, gLa);
+    orc_get_segment(0, chroffset + (unsigned int) rev_goffsetR + 1u, glengthR, chroffset, 0, gR, gRa);
+  } else {
+    orc_get_segment(0, chrhigh - (unsigned int) goffsetL + 1u, glengthL, chroffset, 1, gL, gLa);
+    orc_get_segment(1, chrhigh - (unsigned int) rev_goffsetR, glengthR, chrhigh, 1, gR, gRa);
+  }
+  if (gL[0] == '\0' || gR[0] == '\0') {
+    o.score = NEG_INFINITY_32;
+    free(gL); free(gLa); free(gR); free(gRa);
+    gg_scalars(&o, scalars, dscalars);
+    return -1;
+  }
+  revR = gR + glengthR - 1;
+
+  if (!finalp && defect_rate < DEFECT_MEDQ) {
+    n = genome_gap_simple(&sink, &o, rsequence, rsequenceuc, rev_rsequence, rev_rsequenceuc, rlength, gL, revR,
+                          roffset, rev_roffset, goffsetL, rev_goffsetR, mismatchtype, dirclass, left_probs,
+                          right_probs, genestrand, dynprogindex, halfp);
+    if (n >= 0) {
+      o.dpi = dynprogindex + (dynprogindex > 0 ? +1 : -1);
+      free(gL); free(gLa); free(gR); free(gRa);
+      gg_scalars(&o, scalars, dscalars);
+      return n;
+    }
+    sink.n = 0;
+  }
+
+  compute_bands(&lbandL, &ubandL, rlength, glengthL, extraband_paired, 1);
+  matrixL = (int *) malloc((size_t) (glengthL + 1) * (rlength + 1) * sizeof(int));
+  dirsL = (signed char *) malloc((size_t) 3 * (glengthL + 1) * (rlength + 1));
+  orc_standard_fill(rsequence, gL, gL, rlength, glengthL, mismatchtype, open, extend, lbandL, ubandL,
+                    jump_late_p, /*revp*/0, NEG_INFINITY_32, 1, 1, matrixL, dirsL);
+  compute_bands(&lbandR, &ubandR, rlength, glengthR, extraband_paired, 1);
+  matrixR = (int *) malloc((size_t) (glengthR + 1) * (rlength + 1) * sizeof(int));
+  dirsR = (signed char *) malloc((size_t) 3 * (glengthR + 1) * (rlength + 1));
+  /* the reference passes lbandL here (dynprog_genome.c:3813) */
+  orc_standard_fill(rev_rsequence, revR, revR, rlength, glengthR, mismatchtype, open, extend, lbandL, ubandR,
+                    !jump_late_p, /*revp*/1, NEG_INFINITY_32, 1, 1, matrixR, dirsR);
+
+  /* bridge_intron_gap's own bands (:2924-2928) */
+  finalscore = bridge_site_level(&bestrL, &bestrR, &bestcL, &bestcR, matrixL, matrixR, gL, revR, rlength,
+                                 glengthL, glengthR, dirclass, finalp, halfp,
+                                 extraband_paired, glengthL - rlength + extraband_paired,
+                                 extraband_paired, glengthR - rlength + extraband_paired,
+                                 goffsetL, rev_goffsetR, left_probs, right_probs);
+  if (finalscore < 0) {
+    o.score = -100;
+    n = -1;
+  } else {
+    o.left_prob = left_probs[bestcL];
+    o.right_prob = right_probs[bestcR];
+    o.new_left = goffsetL + (bestcL - 1);
+    o.new_right = rev_goffsetR - (bestcR - 1);
+    o.exonhead = rev_roffset - (bestrR - 1);
+    traceback_std(&sink, &t, dirsR, rlength, glengthR, bestrR, bestcR, rev_rsequence, rev_rsequenceuc, revR, revR,
+                  rev_roffset, rev_goffsetR, /*revp*/1, chroffset, chrhigh, watsonp, genestrand, dynprogindex);
+    nR = sink.n < max_pairs ? sink.n : max_pairs;
+    reverse_pairs(out, nR);  /* List_reverse (:3848) */
+    sink_gapholder(&sink, (rev_roffset - bestrR) - (roffset + bestrL) + 1, o.new_right - o.new_left - 1);
+    traceback_std(&sink, &t, dirsL, rlength, glengthL, bestrL, bestcL, rsequence, rsequenceuc, gL, gL,
+                  roffset, goffsetL, /*revp*/0, chroffset, chrhigh, watsonp, genestrand, dynprogindex);
+    o.score = t.score; o.nmatches = t.nmatches; o.nmismatches = t.nmismatches;
+    o.nopens = t.nopens; o.nindels = t.nindels;
+    o.dpi = dynprogindex + (dynprogindex > 0 ? +1 : -1);
+    n = sink.n;
+    if (n == 1) {
+      n = -1;  /* only the gap holder: NULL (:3877) */
+    } else {
+      /* before the final List_reverse the list is reverse(TL), G, TR in its own order:
+         the reverse of what is returned */
+      OrcPair *tmp = (OrcPair *) malloc((size_t) n * sizeof(OrcPair));
+      int m = n < max_pairs ? n : max_pairs;
+      for (i = 0; i < m; i++) tmp[i] = out[m - 1 - i];
+      if (maxnegscore(tmp, m) < -10) {
+        o.score = -100;
+        n = -1;
+      }
+      free(tmp);
+    }
+  }
+  /* returned list: List_reverse of [reverse(TL) G TR] = reverse(TR) G TL, which is the sink order */
+  free(matrixL); free(dirsL); free(matrixR); free(dirsR);
+  free(gL); free(gLa); free(gR); free(gRa);
+  gg_scalars(&o, scalars, dscalars);
+  return n;
 }

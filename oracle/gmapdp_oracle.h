@@ -69,6 +69,27 @@ int orc_standard_fill (const char *rsequence, const char *gsequence, const char 
                        int lband, int uband, int jump_late_p, int revp, int saturation,
                        int upperp, int lowerp, int *matrix, signed char *dirs);
 
+/* Dynprog_genome_gap (dynprog_genome.c:3288), nosimd semantics, no splicing
+   IIT.  flags: 1 watsonp, 2 jump_late_p, 8 halfp, 16 finalp.  left_probs /
+   right_probs: glengthL / glengthR MaxEnt probabilities at the positions of
+   orc_genome_splice_sites (the host's Maxent_hr_*_prob values).
+   scalars[0..9] = dynprogindex(after), traceback_score, nmatches,
+   nmismatches, nopens, nindels, new_leftgenomepos, new_rightgenomepos,
+   exonhead, introntype (INT_MIN where the reference leaves an out-parameter
+   unwritten); dscalars[0..1] = left_prob, right_prob. */
+int orc_genome_gap (const char *rsequence, const char *rsequenceuc, int rlength, int glengthL, int glengthR,
+                    int roffset, int goffsetL, int rev_goffsetR, unsigned int chroffset, unsigned int chrhigh,
+                    int cdna_direction, int flags, int genestrand, int extraband_paired, double defect_rate,
+                    int maxpeelback, int dynprogindex, const double *left_probs, const double *right_probs,
+                    int *scalars, double *dscalars, OrcPair *out, int max_pairs);
+/* splice-site position + model (0 donor, 1 acceptor, 2 antidonor, 3
+   antiacceptor) of each probability-array entry */
+int orc_genome_splice_sites (int glengthL, int glengthR, int goffsetL, int rev_goffsetR, unsigned int chroffset,
+                             unsigned int chrhigh, int cdna_direction, int watsonp, unsigned int *posL, int *modelL,
+                             unsigned int *posR, int *modelR);
+/* intron_score_setup's six arrays: [sense, antisense, either][prelim, final][64] */
+int orc_intron_scores (int *out3x2x64);
+
 int orc_pairdistance (int mismatchtype, short *out128x128);
 int orc_consistent (int genestrand, unsigned char *out128x128);
 

@@ -57,7 +57,13 @@ FLAGS_nosimd :=
 FLAGS_avx2   := -mpopcnt -DHAVE_SSE2=1 -DHAVE_SSSE3=1 -DHAVE_SSE4_1=1 -DHAVE_SSE4_2=1 -DHAVE_AVX2=1 \
                 -msse2 -mssse3 -msse4.1 -msse4.2 -mavx2 -mno-avx512f -mno-avx512cd -mno-avx512vl -mno-avx512bw
 
-VARIANTS := nosimd avx2
+# nosimd built as `./configure --enable-alloca` would (configure.ac:220-228,
+# AC_FUNC_ALLOCA on glibc): MALLOCA/FREEA become alloca/no-op (mem.h:97-116).
+# Only used to pin Dynprog_genome_gap with halfp, where the default heap build
+# dereferences the FREEA-nulled leftdi (dynprog_genome.c:2879-2888) and crashes.
+FLAGS_nosimda := -DHAVE_ALLOCA=1 -DHAVE_ALLOCA_H=1
+
+VARIANTS := nosimd avx2 nosimda
 
 define variant_rules
 LIBOBJS_$(1) := $$(patsubst %.c,$(OUT)/$(1)/%.o,$(HARNESS_C))

@@ -33,6 +33,7 @@
 #include "dynprog_single.h"
 #include "dynprog_end.h"
 #include "dynprog_genome.h"
+#include "maxent_hr.h"
 
 /* Flat pair record (matches oracle/gmapdp_oracle.h RefPair / GmapdpPair
  * semantics: one record per Pair_T in list order). */
@@ -68,6 +69,10 @@ refh_init (int user_open, int user_extend, int user_dynprog_p) {
                     /*trieoffsets_obs*/NULL, /*triecontents_obs*/NULL,
                     /*trieoffsets_max*/NULL, /*triecontents_max*/NULL,
                     user_open, user_extend, user_dynprog_p ? true : false);
+  /* gmap.c:6548 with no splicing IIT (-s not given); novelsplicingp defaults to true (gmap.c:465) */
+  Dynprog_genome_setup(/*novelsplicingp*/true, /*splicing_iit*/NULL, /*splicing_divint_crosstable*/NULL,
+                       /*donor_typeint*/-1, /*acceptor_typeint*/-1,
+                       user_open, user_extend, user_dynprog_p ? true : false);
   dynprogM = Dynprog_new(NULLGAP, EXTRAQUERYGAP, MAXPEELBACK, EXTRAMATERIAL_END, EXTRAMATERIAL_PAIRED, false);
   dynprogL = Dynprog_new(NULLGAP, EXTRAQUERYGAP, MAXPEELBACK, EXTRAMATERIAL_END, EXTRAMATERIAL_PAIRED, true);
   dynprogR = Dynprog_new(NULLGAP, EXTRAQUERYGAP, MAXPEELBACK, EXTRAMATERIAL_END, EXTRAMATERIAL_PAIRED, true);
@@ -247,6 +252,86 @@ refh_end_gap (int end3p, const char *qbuf, const char *qucbuf, int qpos, int rle
   if (pairs == NULL) return -1;
   n = flatten(pairs, out, max_pairs);
   return n;
+}
+
+/* Dynprog_genome_gap (dynprog_genome.c:3288).  flags: 1 watsonp, 2 jump_late_p,
+   8 halfp, 16 finalp.  scalars[0..9] = dynprogindex(after), traceback_score,
+   nmatches, nmismatches, nopens, nindels, new_leftgenomepos,
+   new_rightgenomepos, exonhead, introntype; out-parameters the reference does
+   not write on the path taken keep the sentinel -2147483648.  dscalars[0..1] =
+   left_prob, right_prob.  Returns the number of pairs or -1 for NULL. */
+#define REFH_UNSET (-2147483647 - 1)
+
+int
+refh_genome_gap (const char *rsequence, const char *rsequenceuc, int rlength, int glengthL, int glengthR,
+                 int roffset, int goffsetL, int rev_goffsetR, unsigned int chroffset, unsigned int chrhigh,
+                 int cdna_direction, int flags, int genestrand, int extraband_paired, double defect_rate,
+                 int maxpeelback, int dynprogindex, int *scalars, double *dscalars, RefPair *out, int max_pairs) {
+  List_T pairs;
+  int new_left = REFH_UNSET, new_right = REFH_UNSET, exonhead = REFH_UNSET, introntype = REFH_UNSET;
+  int score = REFH_UNSET, nmatches = REFH_UNSET, nmismatches = REFH_UNSET, nopens = REFH_UNSET, nindels = REFH_UNSET;
+  double left_prob = -1.0, right_prob = -1.0;
+
+  Pairpool_reset(pairpool);
+  pairs = Dynprog_genome_gap(&dynprogindex, &new_left, &new_right, &left_prob, &right_prob,
+                             &score, &nmatches, &nmismatches, &nopens, &nindels, &exonhead, &introntype,
+                             dynprogL, dynprogR, (char *) rsequence, (char *) rsequenceuc, rlength, glengthL, glengthR,
+                             roffset, goffsetL, rev_goffsetR, /*chrnum*/1, (Univcoord_T) chroffset,
+                             (Univcoord_T) chrhigh, cdna_direction, (flags & 1) ? true : false, genestrand,
+                             (flags & 2) ? true : false, genome, genome, pairpool, extraband_paired, defect_rate,
+                             maxpeelback, (flags & 8) ? true : false, (flags & 16) ? true : false);
+  scalars[0] = dynprogindex; scalars[1] = score; scalars[2] = nmatches; scalars[3] = nmismatches;
+  scalars[4] = nopens; scalars[5] = nindels; scalars[6] = new_left; scalars[7] = new_right;
+  scalars[8] = exonhead; scalars[9] = introntype;
+  dscalars[0] = left_prob; dscalars[1] = right_prob;
+  if (pairs == NULL) return -1;
+  return flatten(pairs, out, max_pairs);
+}
+
+/* The reference's splice-site models (maxent_hr.c:27357-27600):
+   model 0 donor, 1 acceptor, 2 antidonor, 3 antiacceptor. */
+double
+refh_maxent (int model, unsigned int splicesitepos, unsigned int chroffset) {
+  switch (model) {
+  case 0: return Maxent_hr_donor_prob(genome, genome, (Univcoord_T) splicesitepos, (Univcoord_T) chroffset);
+  case 1: return Maxent_hr_acceptor_prob(genome, genome, (Univcoord_T) splicesitepos, (Univcoord_T) chroffset);
+  case 2: return Maxent_hr_antidonor_prob(genome, genome, (Univcoord_T) splicesitepos, (Univcoord_T) chroffset);
+  case 3: return Maxent_hr_antiacceptor_prob(genome, genome, (Univcoord_T) splicesitepos, (Univcoord_T) chroffset);
+  default: return -1.0;
+  }
+}
+
+/* CPU baseline loop over include/gmapdp.h's gmapdp_genome_problem layout
+   (restated). */
+typedef struct {
+  int qoff, rlength, glengthL, glengthR, roffset, goffsetL, rev_goffsetR;
+  unsigned int chroffset, chrhigh;
+  int flags, cdna_direction, genestrand, extraband, maxpeelback, dynprogindex, pad_;
+  double defect_rate;
+  long prob_offset;
+} RefGenomeProblem;
+
+long
+refh_genome_gap_batch (const RefGenomeProblem *probs, int n, const char *qseq, const char *qseq_uc) {
+  long total = 0;
+  int i, dpi, new_left, new_right, exonhead, introntype, score, nmatches, nmismatches, nopens, nindels;
+  double left_prob, right_prob;
+  List_T pairs;
+  for (i = 0; i < n; i++) {
+    const RefGenomeProblem *p = &probs[i];
+    Pairpool_reset(pairpool);
+    dpi = p->dynprogindex;
+    pairs = Dynprog_genome_gap(&dpi, &new_left, &new_right, &left_prob, &right_prob, &score, &nmatches,
+                               &nmismatches, &nopens, &nindels, &exonhead, &introntype, dynprogL, dynprogR,
+                               (char *) qseq + p->qoff, (char *) qseq_uc + p->qoff, p->rlength, p->glengthL,
+                               p->glengthR, p->roffset, p->goffsetL, p->rev_goffsetR, /*chrnum*/1,
+                               (Univcoord_T) p->chroffset, (Univcoord_T) p->chrhigh, p->cdna_direction,
+                               (p->flags & 1) ? true : false, p->genestrand, (p->flags & 2) ? true : false,
+                               genome, genome, pairpool, p->extraband, p->defect_rate, p->maxpeelback,
+                               (p->flags & 8) ? true : false, (p->flags & 16) ? true : false);
+    total += List_length(pairs);
+  }
+  return total;
 }
 
 /* Reference genome-segment extraction (genome.c:11023/11079), for the oracle's

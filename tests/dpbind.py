@@ -16,7 +16,7 @@ import random
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_SO = os.path.join(ROOT, "oracle", "libgmapdp_oracle.so")
-REF_SO = {v: os.path.join(ROOT, "oracle", "_ref", "librefdp_%s.so" % v) for v in ("nosimd", "avx2")}
+REF_SO = {v: os.path.join(ROOT, "oracle", "_ref", "librefdp_%s.so" % v) for v in ("nosimd", "avx2", "nosimda")}
 
 
 class Pair(C.Structure):
@@ -305,3 +305,173 @@ def call_single(impl, p):
     return impl.single_gap(p["q"], p["quc"], p["rlength"], p["glength"], p["roffset"], p["goffset"],
                            p["chroffset"], p["chrhigh"], p["watsonp"], p["genestrand"], p["jump_late_p"],
                            p["extraband"], p["widebandp"], p["defect_rate"], p["dynprogindex"])
+
+
+# ---------------------------------------------------------------------------
+# Dynprog_genome_gap (dynprog_genome.c:3288)
+# ---------------------------------------------------------------------------
+GG_FLAG_WATSON, GG_FLAG_LATE, GG_FLAG_HALF, GG_FLAG_FINAL = 1, 2, 8, 16
+_GG_ARGS = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint, C.c_uint,
+            C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int]
+
+
+def _gg_args(p):
+    return (p["q"], p["quc"], p["rlength"], p["glengthL"], p["glengthR"], p["roffset"], p["goffsetL"],
+            p["rev_goffsetR"], p["chroffset"], p["chrhigh"], p["cdna_direction"], p["flags"], p["genestrand"],
+            p["extraband"], p["defect_rate"], p["maxpeelback"], p["dynprogindex"])
+
+
+def _ref_genome_gap(self, p):
+    f = self.lib.refh_genome_gap
+    if not getattr(self, "_gg_ready", False):
+        f.argtypes = _GG_ARGS + [C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(Pair), C.c_int]
+        f.restype = C.c_int
+        self.lib.refh_maxent.argtypes = [C.c_int, C.c_uint, C.c_uint]
+        self.lib.refh_maxent.restype = C.c_double
+        self._gg_scal = (C.c_int * 10)()
+        self._gg_dscal = (C.c_double * 2)()
+        self._gg_ready = True
+    n = f(*_gg_args(p), self._gg_scal, self._gg_dscal, self._pairs, MAXPAIRS)
+    assert n <= MAXPAIRS
+    pairs = None if n < 0 else [self._pairs[i].key() for i in range(n)]
+    return tuple(self._gg_scal) + tuple(self._gg_dscal), pairs
+
+
+def _ref_maxent(self, model, pos, chroffset=0):
+    f = self.lib.refh_maxent
+    if f.restype is not C.c_double:
+        f.argtypes = [C.c_int, C.c_uint, C.c_uint]
+        f.restype = C.c_double
+    return f(model, pos, chroffset)
+
+
+Ref.genome_gap = _ref_genome_gap
+Ref.maxent = _ref_maxent
+
+
+def _orc_genome_gap(self, p, probsL, probsR):
+    f = self.lib.orc_genome_gap
+    if not getattr(self, "_gg_ready", False):
+        f.argtypes = _GG_ARGS + [C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int),
+                                 C.POINTER(C.c_double), C.POINTER(Pair), C.c_int]
+        f.restype = C.c_int
+        self._gg_scal = (C.c_int * 10)()
+        self._gg_dscal = (C.c_double * 2)()
+        self._gg_ready = True
+    lp = (C.c_double * max(1, len(probsL)))(*probsL)
+    rp = (C.c_double * max(1, len(probsR)))(*probsR)
+    n = f(*_gg_args(p), lp, rp, self._gg_scal, self._gg_dscal, self._pairs, MAXPAIRS)
+    assert n <= MAXPAIRS
+    pairs = None if n < 0 else [self._pairs[i].key() for i in range(n)]
+    return tuple(self._gg_scal) + tuple(self._gg_dscal), pairs
+
+
+def _orc_splice_sites(self, p):
+    gL, gR = max(0, p["glengthL"]), max(0, p["glengthR"])
+    posL, modL = (C.c_uint * max(1, gL))(), (C.c_int * max(1, gL))()
+    posR, modR = (C.c_uint * max(1, gR))(), (C.c_int * max(1, gR))()
+    self.lib.orc_genome_splice_sites(gL, gR, p["goffsetL"], p["rev_goffsetR"], C.c_uint(p["chroffset"]),
+                                     C.c_uint(p["chrhigh"]), p["cdna_direction"], p["flags"] & 1,
+                                     posL, modL, posR, modR)
+    return ([(posL[i], modL[i]) for i in range(gL)], [(posR[i], modR[i]) for i in range(gR)])
+
+
+Oracle.genome_gap = _orc_genome_gap
+Oracle.splice_sites = _orc_splice_sites
+
+_COMPL = {ord("A"): ord("T"), ord("C"): ord("G"), ord("G"): ord("C"), ord("T"): ord("A"), ord("N"): ord("N")}
+
+# canonical, GC-AG and AT-AC introns in the cDNA's sense / antisense orientation (intron.h)
+_MOTIFS_SENSE = [(b"GT", b"AG")] * 8 + [(b"GC", b"AG"), (b"AT", b"AC")]
+_MOTIFS_ANTI = [(b"CT", b"AC")] * 8 + [(b"CT", b"GC"), (b"GT", b"AT")]
+
+
+def _strand_get(genome, p, chroffset, chrhigh, watsonp):
+    """get_genomic_nt (dynprog_single.c:116)"""
+    q = chroffset + p if watsonp else chrhigh - p
+    if not (chroffset <= q < chrhigh):
+        return ord("*")
+    return genome[q] if watsonp else _COMPL.get(genome[q], ord("N"))
+
+
+def _strand_set(genome, p, chroffset, chrhigh, watsonp, ch):
+    q = chroffset + p if watsonp else chrhigh - p
+    if chroffset <= q < chrhigh:
+        genome[q] = ch if watsonp else _COMPL[ch]
+
+
+def genome_gap_problem(rng, genome: bytearray, edge=False):
+    """One Dynprog_genome_gap-shaped call (stage3.c:9504-9539): the query gap
+    spans the end of one exon and the start of the next; glengthL = glengthR =
+    queryjump + extramaterial_paired (8); rev_goffsetR = genomedp3.  A splice
+    motif is usually planted into `genome` (mutated in place) at the true
+    junction, sometimes with a decoy a few bases away.  The chromosome sits
+    1000 nt inside the genome so that segments running past its ends read '*'
+    while the host's MaxEnt lookups (which ignore chrhigh) stay in memory."""
+    chroffset, chrhigh = 1000, len(genome) - 1000
+    chrlen = chrhigh - chroffset
+    watsonp = rng.random() < 0.6
+    cdna_direction = rng.choice([1, 1, 1, -1, -1, 0])
+    if edge:
+        rl0 = rng.choice([0, 1, 2, 3, 5, rng.randint(300, 600), rng.randint(600, 700)])
+    else:
+        rl0 = max(2, min(600, int(rng.gammavariate(2.2, 50))))
+    a = rng.randint(0, rl0)
+    b = rl0 - a
+    intron = rng.randint(12, 4000) if rng.random() < 0.9 else rng.randint(1, 12)
+    span = a + intron + b
+    if edge and rng.random() < 0.3:
+        goffsetL = rng.choice([rng.randint(0, 30), max(1, chrlen - span - rng.randint(-20, 40))])
+    else:
+        goffsetL = rng.randint(60, max(61, chrlen - span - 1200))
+    rev_goffsetR = goffsetL + span - 1
+    motifs = _MOTIFS_SENSE if cdna_direction >= 0 else _MOTIFS_ANTI
+    if rng.random() < 0.85:
+        lm, rm = rng.choice(motifs)
+        for k, ch in enumerate(lm):
+            _strand_set(genome, goffsetL + a + k, chroffset, chrhigh, watsonp, ch)
+        for k, ch in enumerate(rm):
+            _strand_set(genome, rev_goffsetR - b - 1 + k, chroffset, chrhigh, watsonp, ch)
+        if rng.random() < 0.3:  # decoy site nearby
+            d = rng.choice([-4, -3, -2, -1, 1, 2, 3, 4])
+            lm2, rm2 = rng.choice(motifs)
+            side = rng.random() < 0.5
+            for k, ch in enumerate(lm2 if side else rm2):
+                pos = (goffsetL + a + d + k) if side else (rev_goffsetR - b - 1 + d + k)
+                _strand_set(genome, pos, chroffset, chrhigh, watsonp, ch)
+    left = bytes(_strand_get(genome, goffsetL + i, chroffset, chrhigh, watsonp) for i in range(a))
+    right = bytes(_strand_get(genome, rev_goffsetR - b + 1 + i, chroffset, chrhigh, watsonp) for i in range(b))
+    seg = (left + right).replace(b"*", b"A")
+    if rng.random() < 0.08:
+        q = quc = bytes(rng.choice(b"ACGT") for _ in range(len(seg)))
+    else:
+        q, quc = mutate(rng, seg, sub=rng.choice([0.0, 0.01, 0.03, 0.08]), indel=rng.choice([0.0, 0.0, 0.01, 0.03]))
+    if edge and rl0 <= 5:
+        q, quc = q[:rl0], quc[:rl0]
+    rlength = len(q)
+    extra = 8 if (not edge or rng.random() < 0.5) else rng.choice([1, 2, 20, 60])
+    glengthL = rlength + extra
+    glengthR = rlength + (extra if rng.random() < 0.9 else rng.choice([1, 3, 15]))
+    if edge and rng.random() < 0.1:
+        glengthL = rng.choice([glengthL, 2001, 2100])
+    flags = (GG_FLAG_WATSON if watsonp else 0) | (GG_FLAG_LATE if rng.random() < 0.5 else 0)
+    if rng.random() < 0.1:
+        flags |= GG_FLAG_HALF
+    if rng.random() < 0.3:
+        flags |= GG_FLAG_FINAL
+    return dict(q=q or b"A", quc=quc or b"A", rlength=rlength, glengthL=glengthL, glengthR=glengthR,
+                roffset=rng.randint(0, 3000), goffsetL=goffsetL, rev_goffsetR=rev_goffsetR, chroffset=chroffset,
+                chrhigh=chrhigh, cdna_direction=cdna_direction, flags=flags, genestrand=0,
+                extraband=rng.choice([14, 14, 14, 15, 18, 3, 6]),
+                defect_rate=rng.choice([0.001, 0.005, 0.01, 0.02, 0.05]),
+                maxpeelback=rng.choice([60, 60, 20]), dynprogindex=rng.choice([1, 5, -1, -7]))
+
+
+def splice_probs(ref, orc, p):
+    """The host-side MaxEnt probabilities the engine and the oracle take as
+    input: the reference's Maxent_hr_*_prob at the restated positions."""
+    if p["rlength"] <= 1 or p["rlength"] > 660 or p["glengthL"] > 2000 or p["glengthR"] > 2000:
+        return [0.0] * max(0, p["glengthL"]), [0.0] * max(0, p["glengthR"])  # never read (size guard)
+    sl, sr = orc.splice_sites(p)
+    return ([ref.maxent(m, pos, p["chroffset"]) for pos, m in sl],
+            [ref.maxent(m, pos, p["chroffset"]) for pos, m in sr])
