@@ -269,6 +269,226 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
   return x;
 }
 
+// ---- banded fill (Dynprog_standard, upperp = lowerp = true, saturation NEG_INFINITY_INT) ----
+// Rows r = c - uband + k, k = lane*R + i.  Writes the four direction ballots of every column to
+// `dirs`; with HST also the stored (clamped) matrix value of every band cell to hst[c*W + k]
+// (int16 is exact: stored values lie in [-32768, 3*660]).  track: 0 none, 1 best endpoint over
+// the whole band (find_best_endpoint_std), 2 best endpoint on row rlength (_to_queryend_indels_std).
+template <int R, bool HST>
+__device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lband, int uband, int open, int ext,
+                                          int late, int track, const int8_t* sc, int srow, const uint8_t* gcl,
+                                          uint64_t* dirs, int16_t* hst, int& bestr, int& bestc) {
+  const int sat = kNegInf32;
+  const int W = lband + uband + 1;
+  const int binit = (track == 2) ? kNegInf32 : 0;
+  int Hs[R], E[R], bv[R], bcol[R];
+#pragma unroll
+  for (int i = 0; i < R; i++) {  // column 0 (dynprog.c:1331-1369)
+    const int k = lane * R + i;
+    const int r = k - uband;
+    int v = kNegInf32;
+    if (k < W && r >= 0 && r <= rlen) v = (r == 0) ? 0 : (r <= lband ? open + r * ext : kNegInf32);
+    Hs[i] = v;
+    E[i] = kNegInf32;
+    bv[i] = binit;
+    bcol[i] = 0;
+  }
+  // Hs holds the stored nogap value (clamped at `sat`) except on band offset 0, whose only reader is
+  // itself as the diagonal of the band-top row, which the reference takes unclamped (first_nogap).
+  int kext[R];  // k*ext per element: r*ext = rtop*ext + k*ext without a per-column multiply
+#pragma unroll
+  for (int i = 0; i < R; i++) kext[i] = (lane * R + i) * ext;
+  for (int c = 1; c <= glen; c++) {
+    const int gi = __builtin_amdgcn_readfirstlane(gcl[c]);  // wave-uniform genome class
+    const int rtop = c - uband;
+    const int rlo = rtop < 1 ? 1 : rtop;
+    const int rhigh = (c + lband) < rlen ? (c + lband) : rlen;
+    const int rtop_ext = rtop * ext;
+    // last_nogap entering row rlo (dynprog.c:1411-1449)
+    const int L0 = (c == 1) ? (kNegInf32 - open + 1) : (c <= uband ? open + c * ext : kNegInf32);
+    const int row0 = (c <= uband) ? open + c * ext : kNegInf32;  // row 0 of this column (dynprog.c:1318-1325)
+    const int8_t* scg = sc + gi * srow;
+
+    int Ein[R], Hin[R];
+#pragma unroll
+    for (int i = 0; i < R - 1; i++) { Ein[i] = E[i + 1]; Hin[i] = Hs[i + 1]; }
+    Ein[R - 1] = dpp_wave_shl1(E[0], kNegInf32);
+    Hin[R - 1] = dpp_wave_shl1(Hs[0], kNegInf32);
+
+    int Hp[R], En[R], A[R];
+    bool valid[R], eb[R], hb[R];
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+      const int k = lane * R + i;
+      const int r = rtop + k;
+      valid[i] = (k < W) & (r >= rlo) & (r <= rhigh);
+      const int s = scg[min(max(r, 0), rlen + 1)];
+      // Egap (dynprog.c:1518-1524)
+      const int es = Hin[i] + open;
+      eb[i] = Ein[i] > es - late;
+      En[i] = max(Ein[i], es) + ext;
+      const int dg = Hs[i] + s;
+      hb[i] = En[i] > dg - late;
+      Hp[i] = max(En[i], dg);
+      A[i] = valid[i] ? Hp[i] + open - rtop_ext - kext[i] : kSent;
+    }
+    // F chain: F(r) = r*ext + max(init, max_{rlo<=j<r} (H'(j) + open - j*ext))
+    int pre[R];
+    pre[0] = A[0];
+#pragma unroll
+    for (int i = 1; i < R; i++) pre[i] = max(pre[i - 1], A[i]);
+    const int X = dpp_wave_shr1(wave_scan_max(pre[R - 1]), kSent);
+    const int init = max(kNegInf32, L0 + open) - (rlo - 1) * ext;
+    int F[R], Hun[R];
+    bool vb[R];
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+      const int ex = (i == 0) ? X : max(X, pre[i - 1]);
+      F[i] = rtop_ext + kext[i] + max(init, ex);
+      vb[i] = F[i] > Hp[i] - late;
+      Hun[i] = max(F[i], Hp[i]);
+    }
+    // Fgap direction needs F(r-1), H(r-1) of this column (dynprog.c:1486-1492)
+    const int Fup = dpp_wave_shr1(F[R - 1], kNegInf32);
+    const int Hup = dpp_wave_shr1(Hun[R - 1], kNegInf32);
+    uint64_t mH[R], mV[R], mE[R], mF[R];
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+      const int k = lane * R + i;
+      const int r = rtop + k;
+      const bool top = r == rlo;
+      const int fprev = top ? kNegInf32 : ((i == 0) ? Fup : F[i - 1]);
+      const int hprev = top ? L0 : ((i == 0) ? Hup : Hun[i - 1]);
+      const bool fb = fprev > hprev + open - late;
+      mV[i] = ballot(valid[i] & vb[i]);
+      mH[i] = ballot(valid[i] & hb[i] & !vb[i]);
+      mE[i] = ballot(valid[i] & eb[i]);
+      mF[i] = ballot(valid[i] & fb);
+      const int Hc = max(Hun[i], sat);
+      if (HST && k < W) hst[c * W + k] = (int16_t)Hc;
+      // branch-free state update for the next column
+      Hs[i] = valid[i] ? ((k == 0) ? Hun[i] : Hc) : ((r == 0) ? row0 : kNegInf32);
+      E[i] = valid[i] ? En[i] : kNegInf32;
+      // best endpoint (find_best_endpoint_std / _to_queryend_indels_std): scan-order first/last max
+      const bool cand = valid[i] & ((track == 1) | ((track == 2) & (r == rlen))) & (Hc > bv[i] - late);
+      bv[i] = cand ? Hc : bv[i];
+      bcol[i] = cand ? c : bcol[i];
+    }
+    if (lane == 0) {  // one lane stores the column's 4R direction words
+      uint64_t* dcol = dirs + (size_t)c * 4 * R;
+#pragma unroll
+      for (int i = 0; i < R; i++) {
+        dcol[0 * R + i] = mH[i];
+        dcol[1 * R + i] = mV[i];
+        dcol[2 * R + i] = mE[i];
+        dcol[3 * R + i] = mF[i];
+      }
+    }
+  }
+  if (track) {
+    // reduce the endpoint over the wave: key orders (score, r, c) so that the max key is the
+    // reference's choice (> keeps the first in r-major scan order, >= the last)
+    uint64_t key = 0;
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+      if (bcol[i] > 0) {
+        const int r = bcol[i] - uband + lane * R + i;
+        const uint32_t rk = late ? (uint32_t)r : 4095u - (uint32_t)r;
+        const uint32_t ck = late ? (uint32_t)bcol[i] : 4095u - (uint32_t)bcol[i];
+        const uint64_t kk = ((uint64_t)(uint32_t)(bv[i] + (1 << 30)) << 24) | ((uint64_t)rk << 12) | ck;
+        key = kk > key ? kk : key;
+      }
+    }
+    key = wave_max_u64(key);
+    if (key == 0) {
+      bestr = (track == 2) ? rlen : 0;
+      bestc = 0;
+    } else {
+      const uint32_t rk = (uint32_t)(key >> 12) & 4095u, ck = (uint32_t)key & 4095u;
+      bestr = late ? (int)rk : 4095 - (int)rk;
+      bestc = late ? (int)ck : 4095 - (int)ck;
+    }
+  } else {
+    bestr = rlen;
+    bestc = glen;
+  }
+}
+
+// ---- wave-cooperative traceback (Dynprog_traceback_std, dynprog.c:1796-1948) ----
+// Emits the reference's push order into out[t.count ...].
+template <int R>
+__device__ __forceinline__ void traceback_band(int lane, const uint64_t* dirs, int W, int uband, int r, int c,
+                                               const Geo& G, const char* q, const char* quc, const char* gch,
+                                               const uint8_t* __restrict__ cons, bool watson, uint32_t chroffset,
+                                               uint32_t chrhigh, const uint32_t* __restrict__ blocks,
+                                               uint64_t nwords, gmapdp_pair* out, Tally& t) {
+  while (r > 0 && c > 0) {
+    const int k = r - c + uband;
+    const uint32_t isV = dir_bit<R>(dirs, c, 1, k, W);
+    const uint32_t isH = dir_bit<R>(dirs, c, 0, k, W);
+    if (!isV && isH) {
+      // E chain along row r: columns c, c-1, ... while Egap == HORIZ
+      int n = 0;
+      for (int base = 0;; base += 64) {
+        const int j = base + lane;
+        const bool cont = (c - j >= 1) && dir_bit<R>(dirs, c - j, 2, k + j, W);
+        const uint64_t stop = ~ballot(cont);
+        if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
+      }
+      const int dist = n + 1;
+      const int c_end = (c - n - 1) > 0 ? (c - n - 1) : 0;
+      emit_genomeskip(lane, r, c_end + dist, dist, G, watson, chroffset, chrhigh, blocks, nwords, out, t);
+      c = c_end;
+    } else if (isV) {
+      // F chain up column c: rows r, r-1, ... while Fgap == VERT
+      int n = 0;
+      for (int base = 0;; base += 64) {
+        const int j = base + lane;
+        const bool cont = (r - j >= 1) && dir_bit<R>(dirs, c, 3, k - j, W);
+        const uint64_t stop = ~ballot(cont);
+        if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
+      }
+      const int dist = n + 1;
+      const int r_end = (r - n - 1) > 0 ? (r - n - 1) : 0;
+      emit_queryskip(lane, r_end + dist, c, dist, G, q, out, t);
+      r = r_end;
+    } else {
+      // diagonal run at fixed band offset k
+      int n = 0;
+      for (int base = 0;; base += 64) {
+        const int j = base + lane;
+        const bool inrange = (c - j >= 1) && (r - j >= 1);
+        const bool cont = (j == 0) || (inrange && !dir_bit<R>(dirs, c - j, 0, k, W) &&
+                                       !dir_bit<R>(dirs, c - j, 1, k, W));
+        const uint64_t stop = ~ballot(cont && inrange);
+        if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
+      }
+      emit_diag(lane, r, c, n, G, q, quc, gch, cons, out, t);
+      r -= n;
+      c -= n;
+    }
+  }
+  if (r == 0 && c == 0) {
+  } else if (c == 0) {
+    emit_queryskip(lane, r, 1, r, G, q, out, t);  // LAZY_INDEL
+  } else {
+    emit_genomeskip(lane, 1, c, c, G, watson, chroffset, chrhigh, blocks, nwords, out, t);
+  }
+}
+
+// reverse out[0..n) in place (List_reverse of an already emitted run)
+__device__ __forceinline__ void reverse_records(int lane, gmapdp_pair* out, int n) {
+  __threadfence_block();
+  int4* recs = reinterpret_cast<int4*>(out);
+  for (int a = lane; a < n / 2; a += 64) {
+    const int b = n - 1 - a;
+    const int4 x = recs[a], y = recs[b];
+    recs[a] = y;
+    recs[b] = x;
+  }
+  __threadfence_block();
+}
+
 template <int R, bool DIRS_LDS>
 __global__ __launch_bounds__(64) void dp_kernel(
     const DevProblem* __restrict__ probs, const int* __restrict__ order,
@@ -362,147 +582,14 @@ __global__ __launch_bounds__(64) void dp_kernel(
     }
   }
 
-  const int lband = P.lband, uband = P.uband, open = P.open, ext = P.extend;
+  const int lband = P.lband, uband = P.uband;
   const int W = lband + uband + 1;
   int bestr = 0, bestc = 0;
 
   if (!(is_end && endalign == kQueryendNogaps)) {
-    // ---- banded fill (Dynprog_standard, upperp = lowerp = true, saturation NEG_INFINITY_INT) ----
-    const int sat = kNegInf32;
-    const bool track_all = is_end && (endalign == kQueryendGap || endalign == kBestLocal);
-    const bool track_row = is_end && endalign == kQueryendIndels;
-    const int binit = track_row ? kNegInf32 : 0;
-    int Hs[R], E[R], bv[R], bcol[R];
-#pragma unroll
-    for (int i = 0; i < R; i++) {  // column 0 (dynprog.c:1331-1369)
-      const int k = lane * R + i;
-      const int r = k - uband;
-      int v = kNegInf32;
-      if (k < W && r >= 0 && r <= rlen) v = (r == 0) ? 0 : (r <= lband ? open + r * ext : kNegInf32);
-      Hs[i] = v;
-      E[i] = kNegInf32;
-      bv[i] = binit;
-      bcol[i] = 0;
-    }
-    // Hs holds the stored nogap value (clamped at `sat`) except on band offset 0, whose only reader is
-    // itself as the diagonal of the band-top row, which the reference takes unclamped (first_nogap).
-    int kext[R];  // k*ext per element: r*ext = rtop*ext + k*ext without a per-column multiply
-#pragma unroll
-    for (int i = 0; i < R; i++) kext[i] = (lane * R + i) * ext;
-    const int track = track_all ? 1 : (track_row ? 2 : 0);
-    for (int c = 1; c <= glen; c++) {
-      const int gi = __builtin_amdgcn_readfirstlane(gcl[c]);  // wave-uniform genome class
-      const int rtop = c - uband;
-      const int rlo = rtop < 1 ? 1 : rtop;
-      const int rhigh = (c + lband) < rlen ? (c + lband) : rlen;
-      const int rtop_ext = rtop * ext;
-      // last_nogap entering row rlo (dynprog.c:1411-1449)
-      const int L0 = (c == 1) ? (kNegInf32 - open + 1) : (c <= uband ? open + c * ext : kNegInf32);
-      const int row0 = (c <= uband) ? open + c * ext : kNegInf32;  // row 0 of this column (dynprog.c:1318-1325)
-      const int8_t* scg = sc + gi * srow;
-
-      int Ein[R], Hin[R];
-#pragma unroll
-      for (int i = 0; i < R - 1; i++) { Ein[i] = E[i + 1]; Hin[i] = Hs[i + 1]; }
-      Ein[R - 1] = dpp_wave_shl1(E[0], kNegInf32);
-      Hin[R - 1] = dpp_wave_shl1(Hs[0], kNegInf32);
-
-      int Hp[R], En[R], A[R];
-      bool valid[R], eb[R], hb[R];
-#pragma unroll
-      for (int i = 0; i < R; i++) {
-        const int k = lane * R + i;
-        const int r = rtop + k;
-        valid[i] = (k < W) & (r >= rlo) & (r <= rhigh);
-        const int s = scg[min(max(r, 0), rlen + 1)];
-        // Egap (dynprog.c:1518-1524)
-        const int es = Hin[i] + open;
-        eb[i] = Ein[i] > es - late;
-        En[i] = max(Ein[i], es) + ext;
-        const int dg = Hs[i] + s;
-        hb[i] = En[i] > dg - late;
-        Hp[i] = max(En[i], dg);
-        A[i] = valid[i] ? Hp[i] + open - rtop_ext - kext[i] : kSent;
-      }
-      // F chain: F(r) = r*ext + max(init, max_{rlo<=j<r} (H'(j) + open - j*ext))
-      int pre[R];
-      pre[0] = A[0];
-#pragma unroll
-      for (int i = 1; i < R; i++) pre[i] = max(pre[i - 1], A[i]);
-      const int X = dpp_wave_shr1(wave_scan_max(pre[R - 1]), kSent);
-      const int init = max(kNegInf32, L0 + open) - (rlo - 1) * ext;
-      int F[R], Hun[R];
-      bool vb[R];
-#pragma unroll
-      for (int i = 0; i < R; i++) {
-        const int ex = (i == 0) ? X : max(X, pre[i - 1]);
-        F[i] = rtop_ext + kext[i] + max(init, ex);
-        vb[i] = F[i] > Hp[i] - late;
-        Hun[i] = max(F[i], Hp[i]);
-      }
-      // Fgap direction needs F(r-1), H(r-1) of this column (dynprog.c:1486-1492)
-      const int Fup = dpp_wave_shr1(F[R - 1], kNegInf32);
-      const int Hup = dpp_wave_shr1(Hun[R - 1], kNegInf32);
-      uint64_t mH[R], mV[R], mE[R], mF[R];
-#pragma unroll
-      for (int i = 0; i < R; i++) {
-        const int k = lane * R + i;
-        const int r = rtop + k;
-        const bool top = r == rlo;
-        const int fprev = top ? kNegInf32 : ((i == 0) ? Fup : F[i - 1]);
-        const int hprev = top ? L0 : ((i == 0) ? Hup : Hun[i - 1]);
-        const bool fb = fprev > hprev + open - late;
-        mV[i] = ballot(valid[i] & vb[i]);
-        mH[i] = ballot(valid[i] & hb[i] & !vb[i]);
-        mE[i] = ballot(valid[i] & eb[i]);
-        mF[i] = ballot(valid[i] & fb);
-        const int Hc = max(Hun[i], sat);
-        // branch-free state update for the next column
-        Hs[i] = valid[i] ? ((k == 0) ? Hun[i] : Hc) : ((r == 0) ? row0 : kNegInf32);
-        E[i] = valid[i] ? En[i] : kNegInf32;
-        // best endpoint (find_best_endpoint_std / _to_queryend_indels_std): scan-order first/last max
-        const bool cand = valid[i] & ((track == 1) | ((track == 2) & (r == rlen))) & (Hc > bv[i] - late);
-        bv[i] = cand ? Hc : bv[i];
-        bcol[i] = cand ? c : bcol[i];
-      }
-      if (lane == 0) {  // one lane stores the column's 4R direction words
-        uint64_t* dcol = dirs + (size_t)c * 4 * R;
-#pragma unroll
-        for (int i = 0; i < R; i++) {
-          dcol[0 * R + i] = mH[i];
-          dcol[1 * R + i] = mV[i];
-          dcol[2 * R + i] = mE[i];
-          dcol[3 * R + i] = mF[i];
-        }
-      }
-    }
-    if (is_end) {
-      // reduce the endpoint over the wave: key orders (score, r, c) so that the max key is the
-      // reference's choice (> keeps the first in r-major scan order, >= the last)
-      uint64_t key = 0;
-#pragma unroll
-      for (int i = 0; i < R; i++) {
-        if (bcol[i] > 0) {
-          const int r = bcol[i] - uband + lane * R + i;
-          const uint32_t rk = late ? (uint32_t)r : 4095u - (uint32_t)r;
-          const uint32_t ck = late ? (uint32_t)bcol[i] : 4095u - (uint32_t)bcol[i];
-          const uint64_t kk = ((uint64_t)(uint32_t)(bv[i] + (1 << 30)) << 24) | ((uint64_t)rk << 12) | ck;
-          key = kk > key ? kk : key;
-        }
-      }
-      key = wave_max_u64(key);
-      if (key == 0) {
-        bestr = track_row ? rlen : 0;
-        bestc = 0;
-      } else {
-        const uint32_t rk = (uint32_t)(key >> 12) & 4095u, ck = (uint32_t)key & 4095u;
-        bestr = late ? (int)rk : 4095 - (int)rk;
-        bestc = late ? (int)ck : 4095 - (int)ck;
-      }
-    } else {
-      bestr = rlen;
-      bestc = glen;
-    }
+    const int track = !is_end ? 0 : ((endalign == kQueryendIndels) ? 2 : 1);
+    fill_band<R, false>(lane, rlen, glen, lband, uband, P.open, P.extend, late, track, sc, srow, gcl, dirs,
+                        nullptr, bestr, bestc);
     if (DIRS_LDS) __syncthreads();
     else __threadfence_block();
   } else {
@@ -513,60 +600,8 @@ __global__ __launch_bounds__(64) void dp_kernel(
   if (is_end && endalign == kQueryendNogaps) {
     emit_diag(lane, bestr, bestc, bestr, G, q, quc, gch, cons, out, t);  // traceback_nogaps
   } else if (!skip) {
-    // ---- wave-cooperative traceback (Dynprog_traceback_std, dynprog.c:1796-1948) ----
-    int r = bestr, c = bestc;
-    while (r > 0 && c > 0) {
-      const int k = r - c + uband;
-      const uint32_t isV = dir_bit<R>(dirs, c, 1, k, W);
-      const uint32_t isH = dir_bit<R>(dirs, c, 0, k, W);
-      if (!isV && isH) {
-        // E chain along row r: columns c, c-1, ... while Egap == HORIZ
-        int n = 0;
-        for (int base = 0;; base += 64) {
-          const int j = base + lane;
-          const bool cont = (c - j >= 1) && dir_bit<R>(dirs, c - j, 2, k + j, W);
-          const uint64_t stop = ~ballot(cont);
-          if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
-        }
-        const int dist = n + 1;
-        const int c_end = (c - n - 1) > 0 ? (c - n - 1) : 0;
-        emit_genomeskip(lane, r, c_end + dist, dist, G, watson, P.chroffset, P.chrhigh, blocks, nwords, out, t);
-        c = c_end;
-      } else if (isV) {
-        // F chain up column c: rows r, r-1, ... while Fgap == VERT
-        int n = 0;
-        for (int base = 0;; base += 64) {
-          const int j = base + lane;
-          const bool cont = (r - j >= 1) && dir_bit<R>(dirs, c, 3, k - j, W);
-          const uint64_t stop = ~ballot(cont);
-          if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
-        }
-        const int dist = n + 1;
-        const int r_end = (r - n - 1) > 0 ? (r - n - 1) : 0;
-        emit_queryskip(lane, r_end + dist, c, dist, G, q, out, t);
-        r = r_end;
-      } else {
-        // diagonal run at fixed band offset k
-        int n = 0;
-        for (int base = 0;; base += 64) {
-          const int j = base + lane;
-          const bool inrange = (c - j >= 1) && (r - j >= 1);
-          const bool cont = (j == 0) || (inrange && !dir_bit<R>(dirs, c - j, 0, k, W) &&
-                                         !dir_bit<R>(dirs, c - j, 1, k, W));
-          const uint64_t stop = ~ballot(cont && inrange);
-          if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
-        }
-        emit_diag(lane, r, c, n, G, q, quc, gch, cons, out, t);
-        r -= n;
-        c -= n;
-      }
-    }
-    if (r == 0 && c == 0) {
-    } else if (c == 0) {
-      emit_queryskip(lane, r, 1, r, G, q, out, t);  // LAZY_INDEL
-    } else {
-      emit_genomeskip(lane, 1, c, c, G, watson, P.chroffset, P.chrhigh, blocks, nwords, out, t);
-    }
+    traceback_band<R>(lane, dirs, W, uband, bestr, bestc, G, q, quc, gch, cons, watson, P.chroffset, P.chrhigh,
+                      blocks, nwords, out, t);
   }
 
   int score = t.score + t.nmatches * kMatch + t.nmismatches * kMismatch;
@@ -578,17 +613,8 @@ __global__ __launch_bounds__(64) void dp_kernel(
     } else {
       first = t.lead;  // INDEL pairs at the far end removed (dynprog_end.c:1629-1632)
       npairs = t.count - t.lead;
-      if (kind == kEnd5 && npairs > 1) {
-        // Dynprog_end5_gap returns List_reverse of that list (dynprog_end.c:1646)
-        __threadfence_block();
-        int4* recs = reinterpret_cast<int4*>(out + first);
-        for (int a = lane; a < npairs / 2; a += 64) {
-          const int b = npairs - 1 - a;
-          const int4 x = recs[a], y = recs[b];
-          recs[a] = y;
-          recs[b] = x;
-        }
-      }
+      // Dynprog_end5_gap returns List_reverse of that list (dynprog_end.c:1646)
+      if (kind == kEnd5 && npairs > 1) reverse_records(lane, out + first, npairs);
     }
   }
   if (lane == 0) {
@@ -601,6 +627,515 @@ __global__ __launch_bounds__(64) void dp_kernel(
     res.nopens = t.nopens;
     res.nindels = t.nindels;
     res.dynprogindex = dpi_next;
+    results[pid] = res;
+  }
+}
+
+// ===========================================================================
+// Dynprog_genome_gap (dynprog_genome.c:3288-3901), nosimd semantics, no
+// splicing IIT.  One wave per problem:
+//   1. genome_gap_simple (:3006) when !finalp && defect_rate < DEFECT_MEDQ:
+//      prefix sums of the two diagonals + one (score, rL) max-reduction;
+//   2. otherwise the R fill (reversed query vs rev_gsequenceR, lband = lbandL,
+//      !jump_late_p, :3810) then the L fill (:3801), both with the band-lane
+//      fill_band, each storing its matrix (int16, exact) for the bridge;
+//   3. bridge_intron_gap_site_level (:2469) with one lane per row rL: the
+//      reference's sequential "> score, or == score and > prob" scan is a
+//      lexicographic max over (score, probL+probR, scan order), so each lane
+//      scans its rows' candidates in the reference order (A, B over cR, C over
+//      cL) and the rows are merged by a wave reduction;
+//   4. traceback R, List_reverse, gap holder, traceback L, Pair_maxnegscore.
+// ===========================================================================
+struct CarveGG {
+  size_t scL, scR, qL, qucL, qR, qucR, gchL, gclL, gchR, gclR, ldi, rdi, pL, pR, diagL, diagR, bpart, hst,
+      dirsL, dirsR, total;
+};
+
+__host__ __device__ inline size_t gg_hst_bytes(int glengthL, int glengthR, int WL, int WR) {
+  const int g = glengthL > glengthR ? glengthL : glengthR;
+  const int W = WL > WR ? WL : WR;
+  return align16((size_t)(g + 1) * (size_t)W * 2u);
+}
+__host__ __device__ inline size_t gg_dirs_bytes(int glength, int R) { return (size_t)(glength + 1) * 4u * (size_t)R * 8u; }
+
+__host__ __device__ inline CarveGG carve_gg(int rlength, int glengthL, int glengthR, int R, int WL, int WR,
+                                            bool dirs_lds) {
+  CarveGG cv;
+  size_t off = 0;
+  const size_t srow = (size_t)(rlength + 2);
+  cv.pL = off;    off = align16(off + 8u * (size_t)glengthL);
+  cv.pR = off;    off = align16(off + 8u * (size_t)glengthR);
+  cv.bpart = off; off = align16(off + 16u * (size_t)(rlength + 1));
+  cv.diagL = off; off = align16(off + 4u * (size_t)(rlength + 1));
+  cv.diagR = off; off = align16(off + 4u * (size_t)(rlength + 1));
+  cv.scL = off;   off = align16(off + (size_t)kNClass * srow);
+  cv.scR = off;   off = align16(off + (size_t)kNClass * srow);
+  cv.qL = off;    off = align16(off + srow);
+  cv.qucL = off;  off = align16(off + srow);
+  cv.qR = off;    off = align16(off + srow);
+  cv.qucR = off;  off = align16(off + srow);
+  cv.gchL = off;  off = align16(off + (size_t)(glengthL + 2));
+  cv.gclL = off;  off = align16(off + (size_t)(glengthL + 2));
+  cv.gchR = off;  off = align16(off + (size_t)(glengthR + 2));
+  cv.gclR = off;  off = align16(off + (size_t)(glengthR + 2));
+  cv.ldi = off;   off = align16(off + (size_t)(glengthL + 2));
+  cv.rdi = off;   off = align16(off + (size_t)(glengthR + 2));
+  cv.hst = cv.dirsL = cv.dirsR = 0;
+  if (dirs_lds) {
+    cv.dirsL = off; off = align16(off + gg_dirs_bytes(glengthL, R));
+    cv.dirsR = off; off = align16(off + gg_dirs_bytes(glengthR, R));
+    cv.hst = off;   off = off + gg_hst_bytes(glengthL, glengthR, WL, WR);
+  }
+  cv.total = off;
+  return cv;
+}
+
+// intron.h dinucleotide codes; the engine's genome has no alternate alleles (alt == ref)
+__device__ __forceinline__ uint8_t left_dinucl(char a, char b) {
+  if (a == 'G' && b == 'T') return 0x21;  // LEFT_GT
+  if (a == 'G' && b == 'C') return 0x10;  // LEFT_GC
+  if (a == 'A' && b == 'T') return 0x08;  // LEFT_AT
+  if (a == 'C' && b == 'T') return 0x06;  // LEFT_CT
+  return 0;
+}
+__device__ __forceinline__ uint8_t right_dinucl(char right2, char right1) {
+  if (right2 == 'A' && right1 == 'G') return 0x30;  // RIGHT_AG
+  if (right2 == 'A' && right1 == 'C') return 0x0C;  // RIGHT_AC
+  if (right2 == 'G' && right1 == 'C') return 0x02;  // RIGHT_GC
+  if (right2 == 'A' && right1 == 'T') return 0x01;  // RIGHT_AT
+  return 0;
+}
+
+// inclusive prefix sum across the wave
+__device__ __forceinline__ int wave_scan_add(int lane, int x) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  return x;
+}
+__device__ __forceinline__ int wave_scan_maxi(int lane, int x) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off, 64);
+    if (lane >= off) x = max(x, y);
+  }
+  return x;
+}
+__device__ __forceinline__ int wave_min_i(int x) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) x = min(x, __shfl_xor(x, off, 64));
+  return x;
+}
+
+// Pair_maxnegscore (pair.c:8528) of the list held in out[0..n) in REVERSE order (it is evaluated
+// before Dynprog_genome_gap's final List_reverse).  Running score: match +1, mismatch -3, an
+// INDEL run -3 -1 per record; prevhigh = max(0, running max); minimum of score - prevhigh after
+// every mismatch and INDEL record.
+__device__ int wave_maxnegscore(int lane, const gmapdp_pair* out, int n) {
+  int carry = 0, high = 0, worst = 0;
+  bool prev_indel = false;
+  const int4* recs = reinterpret_cast<const int4*>(out);
+  for (int base = 0; base < n; base += 64) {
+    const int p = base + lane;
+    int delta = 0;
+    bool eval = false, indel = false;
+    if (p < n) {
+      const int4 rec = recs[n - 1 - p];
+      const bool gap = rec.x == -1 && rec.y == -1;
+      const char comp = (char)((rec.w >> 8) & 0xff);
+      if (gap) {
+      } else if (comp == ' ') {
+        delta = kMismatch;
+        eval = true;
+      } else if (comp == '-') {
+        indel = true;
+        eval = true;
+      } else {
+        delta = kMatch;
+      }
+    }
+    const int up = __shfl_up((int)indel, 1, 64);  // all lanes take part in the shuffle
+    const bool before = (lane == 0) ? prev_indel : (up != 0);
+    if (indel) delta = before ? kQindel : kQopen + kQindel;
+    const int score = carry + wave_scan_add(lane, delta);
+    const int hi = max(high, wave_scan_maxi(lane, score));
+    if (eval) worst = min(worst, score - hi);
+    carry = __shfl(score, 63, 64);
+    high = __shfl(hi, 63, 64);
+    prev_indel = __shfl((int)indel, 63, 64) != 0;
+  }
+  return wave_min_i(worst);
+}
+
+struct BPart {  // best B candidate (indel on the right) of row rL, without matrixL[rL][rL]
+  double p;
+  int s;
+  int c;
+};
+
+__device__ __forceinline__ bool lex_better(int s1, double p1, int s2, double p2) {
+  return s1 > s2 || (s1 == s2 && p1 > p2);
+}
+
+template <int R, bool DIRS_LDS>
+__global__ __launch_bounds__(64) void gg_kernel(
+    const DevGenomeProblem* __restrict__ probs, const int* __restrict__ order,
+    const uint32_t* __restrict__ blocks, uint64_t nwords,
+    const char* __restrict__ qseq, const char* __restrict__ qseq_uc, const double* __restrict__ sprob,
+    const int8_t* __restrict__ sctab, const uint8_t* __restrict__ constab, const int8_t* __restrict__ isctab,
+    gmapdp_genome_result* __restrict__ results, gmapdp_pair* __restrict__ pairs,
+    unsigned char* __restrict__ gscratch) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x;
+  const int pid = order[blockIdx.x];
+  const DevGenomeProblem P = probs[pid];
+  const int rlen = P.rlength, gL = P.glengthL, gR = P.glengthR;
+  const int flags = P.flags;
+  const bool watson = flags & kFWatson;
+  const int late = (flags & kFLate) ? 1 : 0;
+  const int lband = P.lbandL, ubandL = P.ubandL, ubandR = P.ubandR;
+  const int WL = lband + ubandL + 1, WR = lband + ubandR + 1;
+  const CarveGG cv = carve_gg(rlen, gL, gR, R, WL, WR, DIRS_LDS);
+  double* pL = reinterpret_cast<double*>(smem + cv.pL);
+  double* pR = reinterpret_cast<double*>(smem + cv.pR);
+  BPart* bpart = reinterpret_cast<BPart*>(smem + cv.bpart);
+  int* diagL = reinterpret_cast<int*>(smem + cv.diagL);
+  int* diagR = reinterpret_cast<int*>(smem + cv.diagR);
+  int8_t* scL = reinterpret_cast<int8_t*>(smem + cv.scL);
+  int8_t* scR = reinterpret_cast<int8_t*>(smem + cv.scR);
+  char* qL = reinterpret_cast<char*>(smem + cv.qL);
+  char* qucL = reinterpret_cast<char*>(smem + cv.qucL);
+  char* qR = reinterpret_cast<char*>(smem + cv.qR);
+  char* qucR = reinterpret_cast<char*>(smem + cv.qucR);
+  char* gchL = reinterpret_cast<char*>(smem + cv.gchL);
+  uint8_t* gclL = reinterpret_cast<uint8_t*>(smem + cv.gclL);
+  char* gchR = reinterpret_cast<char*>(smem + cv.gchR);
+  uint8_t* gclR = reinterpret_cast<uint8_t*>(smem + cv.gclR);
+  uint8_t* ldi = reinterpret_cast<uint8_t*>(smem + cv.ldi);
+  uint8_t* rdi = reinterpret_cast<uint8_t*>(smem + cv.rdi);
+  unsigned char* gbase = gscratch + P.dirs_offset;
+  uint64_t* dirsL = reinterpret_cast<uint64_t*>(DIRS_LDS ? smem + cv.dirsL : gbase);
+  uint64_t* dirsR = reinterpret_cast<uint64_t*>(DIRS_LDS ? smem + cv.dirsR : gbase + align16(gg_dirs_bytes(gL, R)));
+  int16_t* hst = reinterpret_cast<int16_t*>(
+      DIRS_LDS ? smem + cv.hst : gbase + align16(gg_dirs_bytes(gL, R)) + align16(gg_dirs_bytes(gR, R)));
+  const int8_t* sct = sctab + (size_t)P.mismatchtype * 128 * kNClass;
+  const uint8_t* cons = constab + (size_t)P.genestrand * 128 * kNClass;
+  gmapdp_pair* out = pairs + P.pair_offset;
+  const int rev_roffset = P.roffset + rlen - 1;
+  const Geo GL{P.roffset, P.goffsetL, 1};
+  const Geo GR{rev_roffset, P.rev_goffsetR, -1};
+  const int srow = rlen + 2;
+
+  // ---- stage: query in both DP orders with per-class score rows, both genome segments,
+  //      dinucleotide codes and the splice probabilities ----
+  for (int i = lane; i < rlen; i += 64) {
+    const char c1 = qseq[P.qbase + i];
+    const char c1u = qseq_uc[P.qbase + i];
+    qL[i + 1] = c1;
+    qucL[i + 1] = c1u;
+    qR[rlen - i] = c1;  // rev_rsequence[1-r] = rsequence[rlength-r]
+    qucR[rlen - i] = c1u;
+    const uint64_t row = *reinterpret_cast<const uint64_t*>(sct + (uint8_t)(c1 & 127) * kNClass);
+#pragma unroll
+    for (int g = 0; g < 6; g++) {
+      scL[g * srow + i + 1] = (int8_t)(row >> (8 * g));
+      scR[g * srow + rlen - i] = (int8_t)(row >> (8 * g));
+    }
+  }
+  if (lane < 6) {
+    scL[lane * srow] = scR[lane * srow] = 0;
+    scL[lane * srow + rlen + 1] = scR[lane * srow + rlen + 1] = 0;
+  }
+  for (int i = lane; i < gL; i += 64) {
+    const char c2 = segment_nt(blocks, nwords, (uint32_t)i, (uint32_t)gL, P.segposL, P.segboundL,
+                               flags & kGSegLLeft, flags & kGSegLRc);
+    gchL[i + 1] = c2;
+    gclL[i + 1] = gclass(c2);
+    pL[i] = sprob[P.prob_offset + i];
+  }
+  for (int i = lane; i < gR; i += 64) {
+    const char c2 = segment_nt(blocks, nwords, (uint32_t)i, (uint32_t)gR, P.segposR, P.segboundR,
+                               flags & kGSegRLeft, flags & kGSegRRc);
+    gchR[gR - i] = c2;  // rev_gsequenceR[1-c] = segment[glengthR-c]
+    gclR[gR - i] = gclass(c2);
+    pR[i] = sprob[P.prob_offset + gL + i];
+  }
+  __syncthreads();
+  // leftdi[cL] from gsequenceL[cL], [cL+1]; rightdi[cR] from rev_gsequenceR[-cR-1], [-cR] (:2518-2566)
+  for (int c = lane; c <= gL; c += 64) ldi[c] = (c < gL - 1) ? left_dinucl(gchL[c + 1], gchL[c + 2]) : 0;
+  for (int c = lane; c <= gR; c += 64) rdi[c] = (c < gR - 1) ? right_dinucl(gchR[c + 2], gchR[c + 1]) : 0;
+  __syncthreads();
+
+  gmapdp_genome_result res;
+  res.npairs = 0;
+  res.pair_offset = P.pair_offset;
+  res.traceback_score = 0;
+  res.nmatches = res.nmismatches = res.nopens = res.nindels = 0;
+  res.dynprogindex = P.dynprogindex;
+  res.new_leftgenomepos = res.new_rightgenomepos = res.exonhead = kUnset;
+  res.introntype = 0;
+  res.gap_index = -1;
+  res.gap_queryjump = 0;
+  res.left_prob = res.right_prob = 0.0;
+  const int dpi_next = P.dynprogindex + (P.dynprogindex > 0 ? 1 : -1);
+  const bool halfp = flags & kGHalf;
+
+  // ---- 1. genome_gap_simple (dynprog_genome.c:3006-3280) ----
+  if (flags & kGSimple) {
+    const int8_t* isc = isctab + (size_t)P.iclass * 128;  // prelim array (:3032)
+    // diagL[r] / diagR[r] hold the prefix sums scoreL(r) / scoreR(r) of the two diagonals
+    int carryL = 0, carryR = 0;
+    for (int base = 0; base < rlen; base += 64) {
+      const int r = base + lane + 1;
+      int vL = 0, vR = 0;
+      if (r <= rlen - 1) {
+        vL = sct[(uint8_t)(qucL[r] & 127) * kNClass + gclL[r]];
+        vR = sct[(uint8_t)(qucR[r] & 127) * kNClass + gclR[r]];
+      }
+      const int sL = carryL + wave_scan_add(lane, vL), sR = carryR + wave_scan_add(lane, vR);
+      if (r <= rlen - 1) {
+        diagL[r] = sL;
+        diagR[r] = sR;
+      }
+      carryL = __shfl(sL, 63, 64);
+      carryR = __shfl(sR, 63, 64);
+    }
+    __syncthreads();
+    // best: max score >= 0 among canonical-type sites, ties -> largest rL ("Use >= for jump late")
+    uint64_t key = 0;
+    for (int rL = lane + 1; rL <= rlen - 1; rL += 64) {
+      const int rR = rlen - rL;
+      const int it = ldi[rL] & rdi[rR];
+      const int score = diagL[rL] + isc[it] + diagR[rR];
+      if (it != 0 && score >= 0) {
+        const uint64_t kk = ((uint64_t)(uint32_t)score << 32) | (uint32_t)rL;
+        key = kk > key ? kk : key;
+      }
+    }
+    key = wave_max_u64(key);
+    if (key != 0) {
+      const int bestrL = (int)(key & 0xffffffffu), bestscore = (int)(key >> 32), bestrR = rlen - bestrL;
+      const int it = ldi[bestrL] & rdi[bestrR];
+      const int scoreI = isc[it];
+      res.introntype = it;
+      const int finalscore = halfp ? bestscore - scoreI / 2 : bestscore;
+      if (finalscore > 0) {
+        res.left_prob = pL[bestrL];
+        res.right_prob = pR[bestrR];
+        if (res.left_prob >= 0.90 && res.right_prob >= 0.90) {
+          Tally t = {0, 0, 0, 0, 0, 0, 0, false};
+          // list = reverse of the push order (no List_reverse): R diagonal r = 1..bestrR, gap, L r = bestrL..1
+          emit_diag(lane, bestrR, bestrR, bestrR, GR, qR, qucR, gchR, cons, out, t);
+          const int nR = t.count;
+          reverse_records(lane, out, nR);
+          const int new_left = P.goffsetL + (bestrL - 1);
+          const int new_right = P.rev_goffsetR - (bestrR - 1);
+          if (lane == 0) put_pair(out, nR, -1, -1, new_right - new_left - 1, ' ', ' ', ' ', ' ');
+          t.count += 1;
+          emit_diag(lane, bestrL, bestrL, bestrL, GL, qL, qucL, gchL, cons, out, t);
+          if (lane == 0) {
+            res.npairs = t.count;
+            res.traceback_score = t.nmatches * kMatch + t.nmismatches * kMismatch;
+            res.nmatches = t.nmatches;
+            res.nmismatches = t.nmismatches;
+            res.dynprogindex = dpi_next;
+            res.new_leftgenomepos = new_left;
+            res.new_rightgenomepos = res.exonhead = new_right;
+            res.gap_index = nR;
+            res.gap_queryjump = 0;
+            results[pid] = res;
+          }
+          return;
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- 2. fills: R first (its matrix feeds the B candidates), then L ----
+  const int8_t* isc = isctab + (size_t)P.iclass * 128 + ((flags & kGFinal) ? 64 : 0);
+  const int eb = lband;  // bridge_intron_gap: lbandL = lbandR = extraband_paired, uband = glength - rlength + eb
+  const int rdist = P.rev_goffsetR - P.goffsetL;  // "cR < rightoffset - leftoffset - cL"
+  int br, bc;
+  fill_band<R, true>(lane, rlen, gR, lband, ubandR, P.open, P.extend, 1 - late, 0, scR, srow, gclR, dirsR, hst,
+                     br, bc);
+  if (DIRS_LDS) __syncthreads();
+  else __threadfence_block();
+  for (int r = lane + 1; r <= rlen - 1; r += 64) diagR[r] = hst[r * WR + ubandR];
+  // B: row rL, cL = rL, cR over [max(1, rR - eb), min(rR + ubandR, gR - 1)) in scan order
+  for (int rL = lane + 1; rL <= rlen - 1; rL += 64) {
+    const int rR = rlen - rL;
+    const int ld = ldi[rL];
+    const double pl = pL[rL];
+    const int clo = max(1, rR - eb);
+    const int chi = min(min(rR + ubandR, gR - 1), rdist - rL);
+    int bs = 0, bcR = -1;
+    double bp = 0.0;
+    for (int cR = clo; cR < chi; cR++) {
+      const int s = isc[ld & rdi[cR]] + hst[cR * WR + (rR - cR + ubandR)];
+      const double p = pl + pR[cR];
+      if (bcR < 0 || lex_better(s, p, bs, bp)) {
+        bs = s;
+        bp = p;
+        bcR = cR;
+      }
+    }
+    bpart[rL].p = bp;
+    bpart[rL].s = bs;
+    bpart[rL].c = bcR;
+  }
+  __syncthreads();
+  fill_band<R, true>(lane, rlen, gL, lband, ubandL, P.open, P.extend, late, 0, scL, srow, gclL, dirsL, hst, br, bc);
+  if (DIRS_LDS) __syncthreads();
+  else __threadfence_block();
+
+  // ---- 3. bridge: per-lane scan of rows rL = lane+1, lane+65, ... (A, B, C per row) ----
+  int ws = kNegInf32, wrL = -1, wcL = 0, wcR = 0;  // (NEG_INFINITY_32, 0.0) is the reference's initial state
+  double wp = 0.0;
+  int ds = 0, drL = 0x7fffffff;                    // best dinucleotide (A) candidate: max prob, earliest
+  double dp = 0.0;
+  for (int rL = lane + 1; rL <= rlen - 1; rL += 64) {
+    const int rR = rlen - rL;
+    const int dL = hst[rL * WL + ubandL];
+    diagL[rL] = dL;
+    const int dR = diagR[rR];
+    // A: cL = rL, cR = rR
+    const int sI = isc[ldi[rL] & rdi[rR]];
+    int rs = dL + sI + dR, rcL = rL, rcR = rR;
+    double rp = pL[rL] + pR[rR];
+    if (sI > 0 && rp > dp) {
+      dp = rp;
+      ds = rs;
+      drL = rL;
+    }
+    // B
+    const BPart b = bpart[rL];
+    if (b.c >= 0 && lex_better(dL + b.s, b.p, rs, rp)) {
+      rs = dL + b.s;
+      rp = b.p;
+      rcL = rL;
+      rcR = b.c;
+    }
+    // C: cR = rR, cL over [max(1, rL - eb), min(rL + ubandL, gL - 1))
+    const int rd = rdi[rR];
+    const double pr = pR[rR];
+    const int clo = max(1, rL - eb);
+    const int chi = min(min(rL + ubandL, gL - 1), rdist - rR);
+    for (int cL = clo; cL < chi; cL++) {
+      const int s = hst[cL * WL + (rL - cL + ubandL)] + isc[ldi[cL] & rd] + dR;
+      const double p = pL[cL] + pr;
+      if (lex_better(s, p, rs, rp)) {
+        rs = s;
+        rp = p;
+        rcL = cL;
+        rcR = rR;
+      }
+    }
+    if (lex_better(rs, rp, ws, wp)) {  // later rows replace only when strictly better
+      ws = rs;
+      wp = rp;
+      wrL = rL;
+      wcL = rcL;
+      wcR = rcR;
+    }
+  }
+  // merge rows across lanes: (score desc, prob desc, rL asc)
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const int s2 = __shfl_xor(ws, off, 64);
+    const double p2 = __shfl_xor(wp, off, 64);
+    const int r2 = __shfl_xor(wrL, off, 64);
+    const int cl2 = __shfl_xor(wcL, off, 64);
+    const int cr2 = __shfl_xor(wcR, off, 64);
+    const int ds2 = __shfl_xor(ds, off, 64);
+    const double dp2 = __shfl_xor(dp, off, 64);
+    const int dr2 = __shfl_xor(drL, off, 64);
+    if (lex_better(s2, p2, ws, wp) || (s2 == ws && p2 == wp && r2 < wrL)) {
+      ws = s2;
+      wp = p2;
+      wrL = r2;
+      wcL = cl2;
+      wcR = cr2;
+    }
+    if (dp2 > dp || (dp2 == dp && dr2 < drL)) {
+      dp = dp2;
+      ds = ds2;
+      drL = dr2;
+    }
+  }
+  // one lane's view is authoritative
+  ws = __builtin_amdgcn_readfirstlane(ws);
+  wrL = __builtin_amdgcn_readfirstlane(wrL);
+  wcL = __builtin_amdgcn_readfirstlane(wcL);
+  wcR = __builtin_amdgcn_readfirstlane(wcR);
+  wp = __shfl(wp, 0, 64);
+  ds = __builtin_amdgcn_readfirstlane(ds);
+  drL = __builtin_amdgcn_readfirstlane(drL);
+  dp = __shfl(dp, 0, 64);
+
+  int bestscore = ws, bestrL = wrL, bestrR = rlen - wrL, bestcL = wcL, bestcR = wcR;
+  bool use_dinucl;
+  if (wp > 2 * 0.85) use_dinucl = false;  // bestprob_with_score > 2*PROB_CEILING
+  else if (dp == 0.0) use_dinucl = false;
+  else if (ds < 0 || ds < bestscore - 9) use_dinucl = false;
+  else use_dinucl = true;
+  if (use_dinucl) {
+    bestscore = ds;
+    bestrL = bestcL = drL;
+    bestrR = bestcR = rlen - drL;
+  }
+  int finalscore = bestscore;
+  if (bestscore >= 0 && halfp) finalscore = bestscore - isc[ldi[bestcL] & rdi[bestcR]] / 2;
+
+  if (finalscore < 0) {
+    if (lane == 0) {
+      res.traceback_score = -100;
+      results[pid] = res;
+    }
+    return;
+  }
+
+  // ---- 4. tracebacks around the intron gap holder ----
+  res.left_prob = pL[bestcL];
+  res.right_prob = pR[bestcR];
+  const int new_left = P.goffsetL + (bestcL - 1);
+  const int new_right = P.rev_goffsetR - (bestcR - 1);
+  Tally t = {0, 0, 0, 0, 0, 0, 0, false};
+  traceback_band<R>(lane, dirsR, WR, ubandR, bestrR, bestcR, GR, qR, qucR, gchR, cons, watson, P.chroffset,
+                    P.chrhigh, blocks, nwords, out, t);
+  const int nR = t.count;
+  reverse_records(lane, out, nR);
+  const int queryjump = (rev_roffset - bestrR) - (P.roffset + bestrL) + 1;
+  if (lane == 0) put_pair(out, nR, -1, -1, new_right - new_left - 1, ' ', ' ', ' ', ' ');
+  t.count += 1;
+  traceback_band<R>(lane, dirsL, WL, ubandL, bestrL, bestcL, GL, qL, qucL, gchL, cons, watson, P.chroffset,
+                    P.chrhigh, blocks, nwords, out, t);
+  int npairs = t.count;
+  int score = t.score + t.nmatches * kMatch + t.nmismatches * kMismatch;
+  if (npairs == 1) {
+    npairs = 0;  // only the gap holder: NULL (:3877-3880)
+  } else {
+    __threadfence_block();
+    if (wave_maxnegscore(lane, out, npairs) < -10) {
+      npairs = 0;
+      score = -100;
+    }
+  }
+  if (lane == 0) {
+    res.npairs = npairs;
+    res.traceback_score = score;
+    res.nmatches = t.nmatches;
+    res.nmismatches = t.nmismatches;
+    res.nopens = t.nopens;
+    res.nindels = t.nindels;
+    res.dynprogindex = dpi_next;
+    res.new_leftgenomepos = new_left;
+    res.new_rightgenomepos = new_right;
+    res.exonhead = rev_roffset - (bestrR - 1);
+    res.gap_index = npairs ? nR : -1;
+    res.gap_queryjump = queryjump;
     results[pid] = res;
   }
 }
@@ -639,6 +1174,48 @@ hipError_t launch_dp(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
   }
   void* args[] = {(void*)&probs, (void*)&order, (void*)&blocks, (void*)&nwords, (void*)&qseq, (void*)&qseq_uc,
                   (void*)&sctab, (void*)&constab, (void*)&results, (void*)&pairs, (void*)&gdirs};
+  return hipLaunchKernel(fn, dim3(nblocks), dim3(64), args, lds, stream);
+}
+
+template <int R, bool D>
+static void* gptr() { return reinterpret_cast<void*>(&gg_kernel<R, D>); }
+
+size_t lds_bytes_gg(int rlength, int glengthL, int glengthR, int R, int WL, int WR, bool dirs_lds) {
+  return carve_gg(rlength, glengthL, glengthR, R, WL, WR, dirs_lds).total;
+}
+size_t scratch_bytes_gg(int glengthL, int glengthR, int R, int WL, int WR) {
+  return align16(gg_dirs_bytes(glengthL, R)) + align16(gg_dirs_bytes(glengthR, R)) +
+         gg_hst_bytes(glengthL, glengthR, WL, WR);
+}
+
+hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevGenomeProblem* probs,
+                     const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
+                     const char* qseq_uc, const double* sprob, const int8_t* sctab, const uint8_t* constab,
+                     const int8_t* isctab, gmapdp_genome_result* results, gmapdp_pair* pairs,
+                     unsigned char* gscratch) {
+  void* fn = nullptr;
+#define GMAPDP_CASE(RR)                                          \
+  case RR:                                                       \
+    fn = dirs_lds ? gptr<RR, true>() : gptr<RR, false>();        \
+    break;
+  switch (R) {
+    GMAPDP_CASE(1)
+    GMAPDP_CASE(2)
+    GMAPDP_CASE(4)
+    GMAPDP_CASE(8)
+    GMAPDP_CASE(16)
+    GMAPDP_CASE(32)
+    GMAPDP_CASE(64)
+    default: return hipErrorInvalidValue;
+  }
+#undef GMAPDP_CASE
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  void* args[] = {(void*)&probs, (void*)&order, (void*)&blocks, (void*)&nwords, (void*)&qseq, (void*)&qseq_uc,
+                  (void*)&sprob, (void*)&sctab, (void*)&constab, (void*)&isctab, (void*)&results, (void*)&pairs,
+                  (void*)&gscratch};
   return hipLaunchKernel(fn, dim3(nblocks), dim3(64), args, lds, stream);
 }
 

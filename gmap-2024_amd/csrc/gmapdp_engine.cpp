@@ -28,6 +28,13 @@ hipError_t launch_dp(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
                      const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
                      const char* qseq_uc, const int8_t* sctab, const uint8_t* constab, gmapdp_result* results,
                      gmapdp_pair* pairs, uint64_t* gdirs);
+size_t lds_bytes_gg(int rlength, int glengthL, int glengthR, int R, int WL, int WR, bool dirs_lds);
+size_t scratch_bytes_gg(int glengthL, int glengthR, int R, int WL, int WR);
+hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevGenomeProblem* probs,
+                     const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
+                     const char* qseq_uc, const double* sprob, const int8_t* sctab, const uint8_t* constab,
+                     const int8_t* isctab, gmapdp_genome_result* results, gmapdp_pair* pairs,
+                     unsigned char* gscratch);
 
 // ---------------------------------------------------------------------------
 // Score tables.  The reference builds pairdistance_array[4][128][128] and
@@ -43,7 +50,24 @@ struct Tables {
   unsigned char cons[3][128][128];
   int8_t sc[4][128][kNClass];
   uint8_t cs[3][128][kNClass];
+  int8_t isc[3][2][64];  // intron_score_array_{sense,antisense,either}_{prelim,final}, [leftdi & rightdi]
 };
+
+// intron_score_setup (dynprog_genome.c:144-187) with the intron.h type codes.  The "either"
+// arrays keep the reference's mix of FINAL and regular rewards.
+static void build_intron_scores(Tables& T) {
+  enum { GTAG_FWD = 0x20, GCAG_FWD = 0x10, ATAC_FWD = 0x08, GTAG_REV = 0x04, GCAG_REV = 0x02, ATAC_REV = 0x01 };
+  const int canon = 14, final_canon = 16, gcag = 8, atac = 4, final_gcag = 10, final_atac = 8;
+  std::memset(T.isc, 0, sizeof(T.isc));
+  T.isc[0][1][GTAG_FWD] = final_canon; T.isc[0][1][GCAG_FWD] = final_gcag; T.isc[0][1][ATAC_FWD] = final_atac;
+  T.isc[0][0][GTAG_FWD] = canon;       T.isc[0][0][GCAG_FWD] = gcag;       T.isc[0][0][ATAC_FWD] = atac;
+  T.isc[1][1][GTAG_REV] = final_canon; T.isc[1][1][GCAG_REV] = final_gcag; T.isc[1][1][ATAC_REV] = final_atac;
+  T.isc[1][0][GTAG_REV] = canon;       T.isc[1][0][GCAG_REV] = gcag;       T.isc[1][0][ATAC_REV] = atac;
+  T.isc[2][1][GTAG_FWD] = final_canon; T.isc[2][1][GCAG_FWD] = final_gcag; T.isc[2][1][ATAC_FWD] = final_atac;
+  T.isc[2][1][GTAG_REV] = canon;       T.isc[2][1][GCAG_REV] = final_gcag; T.isc[2][1][ATAC_REV] = final_atac;
+  T.isc[2][0][GTAG_FWD] = final_canon; T.isc[2][0][GCAG_FWD] = gcag;       T.isc[2][0][ATAC_FWD] = atac;
+  T.isc[2][0][GTAG_REV] = canon;       T.isc[2][0][GCAG_REV] = gcag;       T.isc[2][0][ATAC_REV] = atac;
+}
 
 static bool stranded(int mode) { return mode == 0 || mode == 1 || mode == 3 || mode == 5; }
 
@@ -100,6 +124,7 @@ static void build_tables(Tables& T, int mode) {
   for (int s = 0; s < 3; s++)
     for (int a = 0; a < 128; a++)
       for (int g = 0; g < kNClass; g++) T.cs[s][a][g] = cls[g] ? T.cons[s][a][(int)cls[g]] : 0;
+  build_intron_scores(T);
 }
 
 // ---------------------------------------------------------------------------
@@ -144,23 +169,30 @@ struct gmapdp_ctx {
   Tables* tables = nullptr;
   int8_t* d_sc = nullptr;
   uint8_t* d_cs = nullptr;
+  int8_t* d_isc = nullptr;
   uint32_t* d_genome = nullptr;
   uint64_t genome_words = 0;
   uint64_t genome_length = 0;
   DevBuf probs, order, qseq, qseq_uc, results, pairs, gdirs;
+  DevBuf gprobs, gorder, sprob, gresults;
   std::string err;
 };
 
 // A batch resolved on the host: GPU problems grouped into launch classes.
 struct PlanCore {
-  std::vector<DevProblem> dev;       // one per GPU problem
+  std::vector<DevProblem> dev;       // one per GPU problem (single / end)
   std::vector<int> dev_index;        // problem index -> dev slot (-1: resolved on host)
   std::vector<int> dev_problem;      // dev slot -> problem index
-  struct Launch { int R; bool dirs_lds; size_t lds; int first, count; };
+  std::vector<DevGenomeProblem> gdev;  // Dynprog_genome_gap problems on the GPU
+  std::vector<int> gdev_index;       // genome problem index -> gdev slot (-1: resolved on host)
+  std::vector<int> gdev_problem;     // gdev slot -> genome problem index
+  enum Kind { kDp = 0, kGenomeGap = 1 };
+  struct Launch { int kind; int R; bool dirs_lds; size_t lds; int first, count; };
   std::vector<Launch> launches;
   std::vector<int> order;            // dev slots grouped by launch
+  std::vector<int> gorder;           // gdev slots grouped by launch
   size_t pair_capacity = 0;
-  size_t gdirs_bytes = 0;
+  size_t gdirs_bytes = 0;            // global scratch (spilled direction planes / bridge matrices)
 };
 
 static int fail(gmapdp_ctx* ctx, int code, const char* fmt, hipError_t e) {
@@ -214,6 +246,8 @@ int gmapdp_create(gmapdp_ctx** out, int device, int mode, int user_open, int use
   build_tables(*ctx->tables, mode);
   if (e == hipSuccess) e = hipMalloc(&ctx->d_sc, sizeof(ctx->tables->sc));
   if (e == hipSuccess) e = hipMalloc(&ctx->d_cs, sizeof(ctx->tables->cs));
+  if (e == hipSuccess) e = hipMalloc(&ctx->d_isc, sizeof(ctx->tables->isc));
+  if (e == hipSuccess) e = hipMemcpy(ctx->d_isc, ctx->tables->isc, sizeof(ctx->tables->isc), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(ctx->d_sc, ctx->tables->sc, sizeof(ctx->tables->sc), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(ctx->d_cs, ctx->tables->cs, sizeof(ctx->tables->cs), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
@@ -230,6 +264,7 @@ void gmapdp_destroy(gmapdp_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->d_sc) (void)hipFree(ctx->d_sc);
   if (ctx->d_cs) (void)hipFree(ctx->d_cs);
+  if (ctx->d_isc) (void)hipFree(ctx->d_isc);
   if (ctx->d_genome) (void)hipFree(ctx->d_genome);
   for (int i = 0; i < gmapdp_ctx::kAux; i++) {
     if (ctx->aux[i]) (void)hipStreamSynchronize(ctx->aux[i]);
@@ -446,8 +481,91 @@ static int convert_end(gmapdp_ctx* ctx, const gmapdp_end_problem& p, gmapdp_resu
   return 1;
 }
 
+// Dynprog_genome_gap prologue (dynprog_genome.c:3351-3470): returns 1 if the problem runs on the GPU.
+static int convert_genome(gmapdp_ctx* ctx, const gmapdp_genome_problem& p, gmapdp_genome_result& res,
+                          DevGenomeProblem& d, int* err) {
+  *err = 0;
+  res.npairs = 0;
+  res.pair_offset = 0;
+  res.nmatches = res.nmismatches = res.nopens = res.nindels = 0;
+  res.left_prob = res.right_prob = 0.0;
+  res.introntype = 0;
+  res.new_leftgenomepos = res.new_rightgenomepos = res.exonhead = GMAPDP_UNSET;
+  res.gap_index = -1;
+  res.gap_queryjump = 0;
+  res.dynprogindex = p.dynprogindex;
+  if (p.rlength <= 1) {
+    res.traceback_score = GMAPDP_NEG_INFINITY_32;
+    return 0;
+  }
+  const double dr = p.defect_rate;
+  std::memset(&d, 0, sizeof(d));
+  d.mismatchtype = dr < 0.003 ? kHighQ : (dr < 0.014 ? kMedQ : kLowQ);
+  if (ctx->user_dynprog_p) {
+    d.open = ctx->user_open;
+    d.extend = ctx->user_extend;
+  } else {
+    // SINGLE_* when rlength > maxpeelback*4, else PAIRED_* (dynprog.h:62-76; equal values)
+    d.open = dr < 0.003 ? -8 : (dr < 0.014 ? -7 : -6);
+    d.extend = dr < 0.003 ? -3 : (dr < 0.014 ? -2 : -1);
+  }
+  if (p.rlength > GMAPDP_MAX_RLENGTH || p.glengthL > GMAPDP_MAX_GLENGTH || p.glengthR > GMAPDP_MAX_GLENGTH) {
+    res.new_leftgenomepos = p.goffsetL - 1;  // size guard (:3405-3439)
+    res.new_rightgenomepos = p.rev_goffsetR + 1;
+    res.exonhead = p.roffset + p.rlength - 1;
+    res.dynprogindex = next_dpi(p.dynprogindex);
+    res.traceback_score = GMAPDP_NEG_INFINITY_32;
+    return 0;
+  }
+  if (p.glengthL <= p.rlength || p.glengthR <= p.rlength) {
+    *err = bad(ctx, "Dynprog_genome_gap needs glengthL, glengthR > rlength (the reference reads "
+                    "uninitialised splice probabilities otherwise)");
+    return 0;
+  }
+  if (p.extraband < 0) {
+    *err = bad(ctx, "negative extraband_paired");
+    return 0;
+  }
+  d.qbase = p.qoff;
+  d.rlength = p.rlength;
+  d.glengthL = p.glengthL;
+  d.glengthR = p.glengthR;
+  d.roffset = p.roffset;
+  d.goffsetL = p.goffsetL;
+  d.rev_goffsetR = p.rev_goffsetR;
+  d.chroffset = p.chroffset;
+  d.chrhigh = p.chrhigh;
+  const bool watson = p.flags & GMAPDP_WATSON;
+  d.flags = (watson ? kFWatson : 0) | ((p.flags & GMAPDP_JUMP_LATE) ? kFLate : 0) |
+            ((p.flags & GMAPDP_HALFP) ? kGHalf : 0) | ((p.flags & GMAPDP_FINALP) ? kGFinal : 0);
+  if (!(p.flags & GMAPDP_FINALP) && dr < 0.014) d.flags |= kGSimple;  // :3479
+  if (watson) {
+    d.segposL = p.chroffset + (uint32_t)p.goffsetL;  // Genome_get_segment_right(left, chrhigh)
+    d.segboundL = p.chrhigh;
+    d.segposR = p.chroffset + (uint32_t)p.rev_goffsetR + 1u;  // Genome_get_segment_left(right, chroffset)
+    d.segboundR = p.chroffset;
+    d.flags |= kGSegRLeft;
+  } else {
+    d.segposL = p.chrhigh - (uint32_t)p.goffsetL + 1u;  // _left(right, chroffset), revcomp
+    d.segboundL = p.chroffset;
+    d.segposR = p.chrhigh - (uint32_t)p.rev_goffsetR;   // _right(left, chrhigh), revcomp
+    d.segboundR = p.chrhigh;
+    d.flags |= kGSegLLeft | kGSegLRc | kGSegRRc;
+  }
+  // Dynprog_compute_bands(widebandp true) with glength > rlength: lband = extraband,
+  // uband = glength - rlength + extraband; these equal bridge_intron_gap's own bands (:2924-2928)
+  d.lbandL = p.extraband;
+  d.ubandL = p.glengthL - p.rlength + p.extraband;
+  d.ubandR = p.glengthR - p.rlength + p.extraband;
+  d.iclass = p.cdna_direction > 0 ? 0 : (p.cdna_direction < 0 ? 1 : 2);
+  d.genestrand = p.genestrand;
+  d.dynprogindex = p.dynprogindex;
+  d.prob_offset = p.prob_offset;
+  return 1;
+}
+
 static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
-  std::map<std::tuple<int, int, size_t>, std::vector<int>> classes;
+  std::map<std::tuple<int, int, int, size_t>, std::vector<int>> classes;  // (kind, R, dirs_lds, lds bucket)
   size_t pair_off = 0, gdirs_off = 0;
   for (size_t s = 0; s < plan.dev.size(); s++) {
     DevProblem& d = plan.dev[s];
@@ -470,22 +588,53 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
       }
     }
     if (lds > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
-    classes[std::make_tuple(R, dirs_lds ? 1 : 0, lds_bucket(lds))].push_back((int)s);
+    classes[std::make_tuple((int)PlanCore::kDp, R, dirs_lds ? 1 : 0, lds_bucket(lds))].push_back((int)s);
+  }
+  for (size_t s = 0; s < plan.gdev.size(); s++) {
+    DevGenomeProblem& d = plan.gdev[s];
+    d.pair_offset = (int32_t)pair_off;
+    // traceback R (<= r + gR records) + gap holder + traceback L (<= r + gL records)
+    pair_off += 2 * (size_t)d.rlength + (size_t)d.glengthL + (size_t)d.glengthR + 4;
+    if (d.open > 0) return bad(ctx, "positive gap-open penalty is not supported by the scan formulation");
+    const int WL = d.lbandL + d.ubandL + 1, WR = d.lbandL + d.ubandR + 1;
+    const int R = pick_R(std::max(WL, WR));
+    if (R > kMaxR) return bad(ctx, "band wider than 4096");
+    size_t lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, WL, WR, true);
+    const bool dirs_lds = lds <= kLdsBudget;
+    d.dirs_offset = 0;
+    if (!dirs_lds) {
+      lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, WL, WR, false);
+      d.dirs_offset = (int64_t)gdirs_off;
+      gdirs_off += (scratch_bytes_gg(d.glengthL, d.glengthR, R, WL, WR) + 255) & ~(size_t)255;
+    }
+    if (lds > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
+    classes[std::make_tuple((int)PlanCore::kGenomeGap, R, dirs_lds ? 1 : 0, lds_bucket(lds))].push_back((int)s);
   }
   for (auto& kv : classes) {
     PlanCore::Launch L;
-    L.R = std::get<0>(kv.first);
-    L.dirs_lds = std::get<1>(kv.first) != 0;
-    L.lds = std::get<2>(kv.first);
-    L.first = (int)plan.order.size();
+    L.kind = std::get<0>(kv.first);
+    L.R = std::get<1>(kv.first);
+    L.dirs_lds = std::get<2>(kv.first) != 0;
+    L.lds = std::get<3>(kv.first);
     L.count = (int)kv.second.size();
     // longest problems first, so the tail of the launch is short work
     std::vector<int> ids = kv.second;
-    std::stable_sort(ids.begin(), ids.end(), [&](int a, int b) {
-      return (size_t)plan.dev[a].glength * (plan.dev[a].lband + plan.dev[a].uband + 1) >
-             (size_t)plan.dev[b].glength * (plan.dev[b].lband + plan.dev[b].uband + 1);
-    });
-    plan.order.insert(plan.order.end(), ids.begin(), ids.end());
+    if (L.kind == PlanCore::kDp) {
+      std::stable_sort(ids.begin(), ids.end(), [&](int a, int b) {
+        return (size_t)plan.dev[a].glength * (plan.dev[a].lband + plan.dev[a].uband + 1) >
+               (size_t)plan.dev[b].glength * (plan.dev[b].lband + plan.dev[b].uband + 1);
+      });
+      L.first = (int)plan.order.size();
+      plan.order.insert(plan.order.end(), ids.begin(), ids.end());
+    } else {
+      auto work = [&](int a) {
+        const DevGenomeProblem& d = plan.gdev[a];
+        return (size_t)(d.glengthL + d.glengthR) * (size_t)(2 * d.lbandL + d.ubandL + d.ubandR + 2);
+      };
+      std::stable_sort(ids.begin(), ids.end(), [&](int a, int b) { return work(a) > work(b); });
+      L.first = (int)plan.gorder.size();
+      plan.gorder.insert(plan.gorder.end(), ids.begin(), ids.end());
+    }
     plan.launches.push_back(L);
   }
   plan.pair_capacity = pair_off;
@@ -493,9 +642,10 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
   return GMAPDP_OK;
 }
 
-// Results: singles first, then ends.
+// Results: singles first, then ends (host_results); genome-gap results separately.
 static int build_plan(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int nsingle,
-                      const gmapdp_end_problem* ends, int nend, gmapdp_result* results, PlanCore& plan) {
+                      const gmapdp_end_problem* ends, int nend, const gmapdp_genome_problem* genomes, int ngenome,
+                      gmapdp_result* results, gmapdp_genome_result* gresults, PlanCore& plan) {
   plan = PlanCore();
   const int n = nsingle + nend;
   plan.dev_index.assign(n, -1);
@@ -511,9 +661,21 @@ static int build_plan(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int
     plan.dev_problem.push_back(i);
     plan.dev.push_back(d);
   }
+  plan.gdev_index.assign(ngenome, -1);
+  for (int j = 0; j < ngenome; j++) {
+    DevGenomeProblem d;
+    int err = 0;
+    const int gpu = convert_genome(ctx, genomes[j], gresults[j], d, &err);
+    if (err) return err;
+    if (!gpu) continue;
+    plan.gdev_index[j] = (int)plan.gdev.size();
+    plan.gdev_problem.push_back(j);
+    plan.gdev.push_back(d);
+  }
   int rc = classify(ctx, plan);
   if (rc) return rc;
   for (size_t s = 0; s < plan.dev.size(); s++) results[plan.dev_problem[s]].pair_offset = plan.dev[s].pair_offset;
+  for (size_t s = 0; s < plan.gdev.size(); s++) gresults[plan.gdev_problem[s]].pair_offset = plan.gdev[s].pair_offset;
   return GMAPDP_OK;
 }
 
@@ -523,18 +685,33 @@ static bool launch_is_tail(const PlanCore::Launch& L) {
   return L.count < 4096 || L.R > 1 || !L.dirs_lds;
 }
 
-static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, const DevProblem* d_probs,
-                             const int* d_order, const char* d_q, const char* d_quc, gmapdp_result* d_results,
-                             gmapdp_pair* d_pairs, hipStream_t stream) {
+// Device-side inputs of one plan execution.
+struct RunArgs {
+  const DevProblem* d_probs;
+  const int* d_order;
+  const DevGenomeProblem* d_gprobs;
+  const int* d_gorder;
+  const char* d_q;
+  const char* d_quc;
+  const double* d_sprob;
+  gmapdp_result* d_results;
+  gmapdp_genome_result* d_gresults;
+  gmapdp_pair* d_pairs;
+};
+
+static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, const RunArgs& a, hipStream_t stream) {
   const auto& L = plan.launches[li];
-  return launch_dp(L.R, L.dirs_lds, L.count, L.lds, stream, d_probs, d_order + L.first, ctx->d_genome,
-                   ctx->genome_words, d_q, d_quc, ctx->d_sc, ctx->d_cs, d_results, d_pairs,
-                   (uint64_t*)ctx->gdirs.p);
+  if (L.kind == PlanCore::kDp)
+    return launch_dp(L.R, L.dirs_lds, L.count, L.lds, stream, a.d_probs, a.d_order + L.first, ctx->d_genome,
+                     ctx->genome_words, a.d_q, a.d_quc, ctx->d_sc, ctx->d_cs, a.d_results, a.d_pairs,
+                     (uint64_t*)ctx->gdirs.p);
+  if (!a.d_gresults || !a.d_sprob) return hipErrorInvalidValue;
+  return launch_gg(L.R, L.dirs_lds, L.count, L.lds, stream, a.d_gprobs, a.d_gorder + L.first, ctx->d_genome,
+                   ctx->genome_words, a.d_q, a.d_quc, a.d_sprob, ctx->d_sc, ctx->d_cs, ctx->d_isc, a.d_gresults,
+                   a.d_pairs, (unsigned char*)ctx->gdirs.p);
 }
 
-static int run_plan(gmapdp_ctx* ctx, const PlanCore& plan, const DevProblem* d_probs, const int* d_order,
-                    const char* d_q, const char* d_quc, gmapdp_result* d_results, gmapdp_pair* d_pairs,
-                    hipStream_t stream) {
+static int run_plan(gmapdp_ctx* ctx, const PlanCore& plan, const RunArgs& a, hipStream_t stream) {
   if (plan.gdirs_bytes) {
     hipError_t e = ctx->gdirs.ensure(plan.gdirs_bytes);
     if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "direction scratch: %s", e);
@@ -547,12 +724,12 @@ static int run_plan(gmapdp_ctx* ctx, const PlanCore& plan, const DevProblem* d_p
     if (!launch_is_tail(plan.launches[li])) continue;
     hipStream_t s = ctx->aux[naux % gmapdp_ctx::kAux];
     if (naux < gmapdp_ctx::kAux) e = hipStreamWaitEvent(s, ctx->ev_fork, 0);
-    if (e == hipSuccess) e = launch_one(ctx, plan, (int)li, d_probs, d_order, d_q, d_quc, d_results, d_pairs, s);
+    if (e == hipSuccess) e = launch_one(ctx, plan, (int)li, a, s);
     naux++;
   }
   for (size_t li = 0; li < plan.launches.size() && e == hipSuccess; li++) {
     if (launch_is_tail(plan.launches[li])) continue;
-    e = launch_one(ctx, plan, (int)li, d_probs, d_order, d_q, d_quc, d_results, d_pairs, stream);
+    e = launch_one(ctx, plan, (int)li, a, stream);
   }
   for (int i = 0; i < naux && i < gmapdp_ctx::kAux && e == hipSuccess; i++) {
     e = hipEventRecord(ctx->ev_join[i], ctx->aux[i]);
@@ -562,17 +739,19 @@ static int run_plan(gmapdp_ctx* ctx, const PlanCore& plan, const DevProblem* d_p
   return GMAPDP_OK;
 }
 
-// Synchronous host-array batch (both entry-point families).
+// Synchronous host-array batch (all entry-point families).
 static int run_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int nsingle,
-                     const gmapdp_end_problem* ends, int nend, const char* qseq, const char* qseq_uc,
-                     size_t qbytes, gmapdp_result* results, gmapdp_pair* pairs, size_t pair_capacity) {
+                     const gmapdp_end_problem* ends, int nend, const gmapdp_genome_problem* genomes, int ngenome,
+                     const char* qseq, const char* qseq_uc, size_t qbytes, const double* sprob, size_t nsprob,
+                     gmapdp_result* results, gmapdp_genome_result* gresults, gmapdp_pair* pairs,
+                     size_t pair_capacity) {
   const int n = nsingle + nend;
-  if (!ctx || n < 0 || (n && !results)) return GMAPDP_EINVAL;
+  if (!ctx || n < 0 || ngenome < 0 || (n && !results) || (ngenome && !gresults)) return GMAPDP_EINVAL;
   if (!ctx->d_genome) return GMAPDP_ENOGENOME;
-  if (n == 0) return GMAPDP_OK;
+  if (n + ngenome == 0) return GMAPDP_OK;
   (void)hipSetDevice(ctx->device);
   PlanCore plan;
-  int rc = build_plan(ctx, singles, nsingle, ends, nend, results, plan);
+  int rc = build_plan(ctx, singles, nsingle, ends, nend, genomes, ngenome, results, gresults, plan);
   if (rc) return rc;
   if (plan.pair_capacity > pair_capacity) return bad(ctx, "pair arena too small");
   for (size_t s = 0; s < plan.dev.size(); s++) {
@@ -581,31 +760,64 @@ static int run_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int 
     const long len = i < nsingle ? singles[i].rlength : ends[i - nsingle].rlength;
     if (lo < 0 || (size_t)(lo + len) > qbytes) return bad(ctx, "query slice outside the query arena");
   }
-  const int ndev = (int)plan.dev.size();
-  if (ndev == 0) return GMAPDP_OK;
-  hipError_t e = ctx->probs.ensure(sizeof(DevProblem) * ndev);
-  if (e == hipSuccess) e = ctx->order.ensure(sizeof(int) * ndev);
+  for (size_t s = 0; s < plan.gdev.size(); s++) {
+    const gmapdp_genome_problem& g = genomes[plan.gdev_problem[s]];
+    if (g.qoff < 0 || (size_t)((long)g.qoff + g.rlength) > qbytes)
+      return bad(ctx, "query slice outside the query arena");
+    if (!sprob || g.prob_offset < 0 || (size_t)g.prob_offset + (size_t)g.glengthL + (size_t)g.glengthR > nsprob)
+      return bad(ctx, "splice probabilities outside the probability arena");
+  }
+  const int ndev = (int)plan.dev.size(), ngdev = (int)plan.gdev.size();
+  if (ndev + ngdev == 0) return GMAPDP_OK;
+  hipError_t e = ctx->probs.ensure(sizeof(DevProblem) * std::max(ndev, 1));
+  if (e == hipSuccess) e = ctx->order.ensure(sizeof(int) * std::max(ndev, 1));
+  if (e == hipSuccess) e = ctx->gprobs.ensure(sizeof(DevGenomeProblem) * std::max(ngdev, 1));
+  if (e == hipSuccess) e = ctx->gorder.ensure(sizeof(int) * std::max(ngdev, 1));
   if (e == hipSuccess) e = ctx->qseq.ensure(qbytes);
   if (e == hipSuccess) e = ctx->qseq_uc.ensure(qbytes);
-  if (e == hipSuccess) e = ctx->results.ensure(sizeof(gmapdp_result) * ndev);
+  if (e == hipSuccess) e = ctx->results.ensure(sizeof(gmapdp_result) * std::max(ndev, 1));
+  if (e == hipSuccess) e = ctx->gresults.ensure(sizeof(gmapdp_genome_result) * std::max(ngdev, 1));
+  if (e == hipSuccess && ngdev) e = ctx->sprob.ensure(sizeof(double) * std::max<size_t>(nsprob, 1));
   if (e == hipSuccess) e = ctx->pairs.ensure(sizeof(gmapdp_pair) * std::max<size_t>(plan.pair_capacity, 1));
   if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "device buffers: %s", e);
   hipStream_t s = ctx->stream;
-  e = hipMemcpyAsync(ctx->probs.p, plan.dev.data(), sizeof(DevProblem) * ndev, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(ctx->order.p, plan.order.data(), sizeof(int) * ndev, hipMemcpyHostToDevice, s);
+  if (ndev) e = hipMemcpyAsync(ctx->probs.p, plan.dev.data(), sizeof(DevProblem) * ndev, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && ndev)
+    e = hipMemcpyAsync(ctx->order.p, plan.order.data(), sizeof(int) * ndev, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && ngdev)
+    e = hipMemcpyAsync(ctx->gprobs.p, plan.gdev.data(), sizeof(DevGenomeProblem) * ngdev, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && ngdev)
+    e = hipMemcpyAsync(ctx->gorder.p, plan.gorder.data(), sizeof(int) * ngdev, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && ngdev)
+    e = hipMemcpyAsync(ctx->sprob.p, sprob, sizeof(double) * nsprob, hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipMemcpyAsync(ctx->qseq.p, qseq, qbytes, hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipMemcpyAsync(ctx->qseq_uc.p, qseq_uc, qbytes, hipMemcpyHostToDevice, s);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "upload: %s", e);
-  rc = run_plan(ctx, plan, (const DevProblem*)ctx->probs.p, (const int*)ctx->order.p, (const char*)ctx->qseq.p,
-                (const char*)ctx->qseq_uc.p, (gmapdp_result*)ctx->results.p, (gmapdp_pair*)ctx->pairs.p, s);
+  RunArgs a;
+  a.d_probs = (const DevProblem*)ctx->probs.p;
+  a.d_order = (const int*)ctx->order.p;
+  a.d_gprobs = (const DevGenomeProblem*)ctx->gprobs.p;
+  a.d_gorder = (const int*)ctx->gorder.p;
+  a.d_q = (const char*)ctx->qseq.p;
+  a.d_quc = (const char*)ctx->qseq_uc.p;
+  a.d_sprob = (const double*)ctx->sprob.p;
+  a.d_results = (gmapdp_result*)ctx->results.p;
+  a.d_gresults = (gmapdp_genome_result*)ctx->gresults.p;
+  a.d_pairs = (gmapdp_pair*)ctx->pairs.p;
+  rc = run_plan(ctx, plan, a, s);
   if (rc) return rc;
   std::vector<gmapdp_result> dres(ndev);
-  e = hipMemcpyAsync(dres.data(), ctx->results.p, sizeof(gmapdp_result) * ndev, hipMemcpyDeviceToHost, s);
+  std::vector<gmapdp_genome_result> gres(ngdev);
+  if (ndev)
+    e = hipMemcpyAsync(dres.data(), ctx->results.p, sizeof(gmapdp_result) * ndev, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess && ngdev)
+    e = hipMemcpyAsync(gres.data(), ctx->gresults.p, sizeof(gmapdp_genome_result) * ngdev, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess && pairs && plan.pair_capacity)
     e = hipMemcpyAsync(pairs, ctx->pairs.p, sizeof(gmapdp_pair) * plan.pair_capacity, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "dp execution: %s", e);
   for (int d = 0; d < ndev; d++) results[plan.dev_problem[d]] = dres[d];
+  for (int d = 0; d < ngdev; d++) gresults[plan.gdev_problem[d]] = gres[d];
   return GMAPDP_OK;
 }
 
@@ -632,19 +844,87 @@ size_t gmapdp_single_pair_capacity(const gmapdp_single_problem* problems, int n)
 size_t gmapdp_end_pair_capacity(const gmapdp_end_problem* problems, int n) {
   return capacity(nullptr, 0, problems, n);
 }
+size_t gmapdp_genome_pair_capacity(const gmapdp_genome_problem* problems, int n) {
+  size_t cap = 0;
+  for (int i = 0; i < n; i++) {
+    const gmapdp_genome_problem& p = problems[i];
+    if (p.rlength > 1 && p.rlength <= GMAPDP_MAX_RLENGTH && p.glengthL <= GMAPDP_MAX_GLENGTH &&
+        p.glengthR <= GMAPDP_MAX_GLENGTH && p.glengthL > 0 && p.glengthR > 0)
+      cap += 2 * (size_t)p.rlength + (size_t)p.glengthL + (size_t)p.glengthR + 4;
+  }
+  return cap;
+}
+
+size_t gmapdp_genome_prob_entries(const gmapdp_genome_problem* problems, int n) {
+  size_t m = 0;
+  for (int i = 0; i < n; i++) {
+    const gmapdp_genome_problem& p = problems[i];
+    if (p.prob_offset < 0 || p.glengthL < 0 || p.glengthR < 0) continue;
+    m = std::max(m, (size_t)p.prob_offset + (size_t)p.glengthL + (size_t)p.glengthR);
+  }
+  return m;
+}
+
+// The Maxent_hr_*_prob call of each probability entry (bridge_intron_gap_site_level,
+// dynprog_genome.c:2573-2660; get_splicesite_probs :332-401).  Univcoord_T is 32-bit.
+int gmapdp_genome_splice_sites(const gmapdp_genome_problem* problems, int n, uint32_t* positions, uint8_t* models,
+                               size_t nentries) {
+  if (n < 0 || (n && (!problems || !positions || !models))) return GMAPDP_EINVAL;
+  if (gmapdp_genome_prob_entries(problems, n) > nentries) return GMAPDP_EINVAL;
+  for (int i = 0; i < n; i++) {
+    const gmapdp_genome_problem& p = problems[i];
+    if (p.prob_offset < 0 || p.glengthL < 0 || p.glengthR < 0) return GMAPDP_EINVAL;
+    const bool watson = p.flags & GMAPDP_WATSON;
+    const bool sense = p.cdna_direction > 0;
+    const uint32_t lo = (uint32_t)p.goffsetL, ro = (uint32_t)p.rev_goffsetR;
+    uint32_t* pos = positions + p.prob_offset;
+    uint8_t* mod = models + p.prob_offset;
+    for (int c = 0; c < p.glengthL; c++) {
+      if (watson) {
+        pos[c] = p.chroffset + lo + (uint32_t)c;
+        mod[c] = sense ? GMAPDP_MAXENT_DONOR : GMAPDP_MAXENT_ANTIACCEPTOR;
+      } else {
+        pos[c] = p.chrhigh - lo - (uint32_t)c + 1u;
+        mod[c] = sense ? GMAPDP_MAXENT_ANTIDONOR : GMAPDP_MAXENT_ACCEPTOR;
+      }
+    }
+    pos += p.glengthL;
+    mod += p.glengthL;
+    for (int c = 0; c < p.glengthR; c++) {
+      if (watson) {
+        pos[c] = p.chroffset + ro - (uint32_t)c + 1u;
+        mod[c] = sense ? GMAPDP_MAXENT_ACCEPTOR : GMAPDP_MAXENT_ANTIDONOR;
+      } else {
+        pos[c] = p.chrhigh - ro + (uint32_t)c;
+        mod[c] = sense ? GMAPDP_MAXENT_ANTIACCEPTOR : GMAPDP_MAXENT_DONOR;
+      }
+    }
+  }
+  return GMAPDP_OK;
+}
 
 int gmapdp_single_gap_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* problems, int n, const char* qseq,
                             const char* qseq_uc, size_t qbytes, gmapdp_result* results, gmapdp_pair* pairs,
                             size_t pair_capacity) {
   if (n > 0 && !problems) return GMAPDP_EINVAL;
-  return run_batch(ctx, problems, n, nullptr, 0, qseq, qseq_uc, qbytes, results, pairs, pair_capacity);
+  return run_batch(ctx, problems, n, nullptr, 0, nullptr, 0, qseq, qseq_uc, qbytes, nullptr, 0, results, nullptr,
+                   pairs, pair_capacity);
 }
 
 int gmapdp_end_gap_batch(gmapdp_ctx* ctx, const gmapdp_end_problem* problems, int n, const char* qseq,
                          const char* qseq_uc, size_t qbytes, gmapdp_result* results, gmapdp_pair* pairs,
                          size_t pair_capacity) {
   if (n > 0 && !problems) return GMAPDP_EINVAL;
-  return run_batch(ctx, nullptr, 0, problems, n, qseq, qseq_uc, qbytes, results, pairs, pair_capacity);
+  return run_batch(ctx, nullptr, 0, problems, n, nullptr, 0, qseq, qseq_uc, qbytes, nullptr, 0, results, nullptr,
+                   pairs, pair_capacity);
+}
+
+int gmapdp_genome_gap_batch(gmapdp_ctx* ctx, const gmapdp_genome_problem* problems, int n, const char* qseq,
+                            const char* qseq_uc, size_t qbytes, const double* splice_probs, size_t nprobs,
+                            gmapdp_genome_result* results, gmapdp_pair* pairs, size_t pair_capacity) {
+  if (n > 0 && !problems) return GMAPDP_EINVAL;
+  return run_batch(ctx, nullptr, 0, nullptr, 0, problems, n, qseq, qseq_uc, qbytes, splice_probs, nprobs, nullptr,
+                   results, pairs, pair_capacity);
 }
 
 }  // extern "C"
@@ -655,37 +935,80 @@ int gmapdp_end_gap_batch(gmapdp_ctx* ctx, const gmapdp_end_problem* problems, in
 // ---------------------------------------------------------------------------
 struct gmapdp_plan {
   PlanCore in;
+  int nsingle = 0, nend = 0, ngenome = 0;
   DevProblem* d_probs = nullptr;
   int* d_order = nullptr;
+  DevGenomeProblem* d_gprobs = nullptr;
+  int* d_gorder = nullptr;
+  const double* d_sprob = nullptr;            // bound by gmapdp_plan_bind_genome
+  gmapdp_genome_result* d_gresults = nullptr;
 };
+
+static void plan_free(gmapdp_plan* p) {
+  if (p->d_probs) (void)hipFree(p->d_probs);
+  if (p->d_order) (void)hipFree(p->d_order);
+  if (p->d_gprobs) (void)hipFree(p->d_gprobs);
+  if (p->d_gorder) (void)hipFree(p->d_gorder);
+  delete p;
+}
+
+static RunArgs plan_args(const gmapdp_plan* plan, const char* d_qseq, const char* d_qseq_uc, gmapdp_result* d_results,
+                         gmapdp_pair* d_pairs) {
+  RunArgs a;
+  a.d_probs = plan->d_probs;
+  a.d_order = plan->d_order;
+  a.d_gprobs = plan->d_gprobs;
+  a.d_gorder = plan->d_gorder;
+  a.d_q = d_qseq;
+  a.d_quc = d_qseq_uc;
+  a.d_sprob = plan->d_sprob;
+  a.d_results = d_results;
+  a.d_gresults = plan->d_gresults;
+  a.d_pairs = d_pairs;
+  return a;
+}
 
 extern "C" {
 
-int gmapdp_plan_create(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int nsingle,
-                       const gmapdp_end_problem* ends, int nend, gmapdp_result* host_results, gmapdp_plan** out) {
-  if (!ctx || !out || nsingle < 0 || nend < 0 || nsingle + nend <= 0 || !host_results) return GMAPDP_EINVAL;
-  if ((nsingle && !singles) || (nend && !ends)) return GMAPDP_EINVAL;
+int gmapdp_plan_create_all(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int nsingle,
+                           const gmapdp_end_problem* ends, int nend, const gmapdp_genome_problem* genomes,
+                           int ngenome, gmapdp_result* host_results, gmapdp_genome_result* host_genome_results,
+                           gmapdp_plan** out) {
+  if (!ctx || !out || nsingle < 0 || nend < 0 || ngenome < 0 || nsingle + nend + ngenome <= 0) return GMAPDP_EINVAL;
+  if ((nsingle && !singles) || (nend && !ends) || (ngenome && !genomes)) return GMAPDP_EINVAL;
+  if ((nsingle + nend && !host_results) || (ngenome && !host_genome_results)) return GMAPDP_EINVAL;
   (void)hipSetDevice(ctx->device);
   gmapdp_plan* p = new gmapdp_plan();
-  int rc = build_plan(ctx, singles, nsingle, ends, nend, host_results, p->in);
+  p->nsingle = nsingle;
+  p->nend = nend;
+  p->ngenome = ngenome;
+  int rc = build_plan(ctx, singles, nsingle, ends, nend, genomes, ngenome, host_results, host_genome_results, p->in);
   if (rc) {
     delete p;
     return rc;
   }
-  const size_t nd = p->in.dev.size();
+  const size_t nd = p->in.dev.size(), ng = p->in.gdev.size();
   hipError_t e = hipMalloc(&p->d_probs, sizeof(DevProblem) * std::max<size_t>(nd, 1));
   if (e == hipSuccess) e = hipMalloc(&p->d_order, sizeof(int) * std::max<size_t>(nd, 1));
+  if (e == hipSuccess) e = hipMalloc(&p->d_gprobs, sizeof(DevGenomeProblem) * std::max<size_t>(ng, 1));
+  if (e == hipSuccess) e = hipMalloc(&p->d_gorder, sizeof(int) * std::max<size_t>(ng, 1));
   if (e == hipSuccess && nd) e = hipMemcpy(p->d_probs, p->in.dev.data(), sizeof(DevProblem) * nd, hipMemcpyHostToDevice);
   if (e == hipSuccess && nd) e = hipMemcpy(p->d_order, p->in.order.data(), sizeof(int) * nd, hipMemcpyHostToDevice);
+  if (e == hipSuccess && ng)
+    e = hipMemcpy(p->d_gprobs, p->in.gdev.data(), sizeof(DevGenomeProblem) * ng, hipMemcpyHostToDevice);
+  if (e == hipSuccess && ng) e = hipMemcpy(p->d_gorder, p->in.gorder.data(), sizeof(int) * ng, hipMemcpyHostToDevice);
   if (e == hipSuccess && p->in.gdirs_bytes) e = ctx->gdirs.ensure(p->in.gdirs_bytes);
   if (e != hipSuccess) {
-    if (p->d_probs) (void)hipFree(p->d_probs);
-    if (p->d_order) (void)hipFree(p->d_order);
-    delete p;
+    plan_free(p);
     return fail(ctx, GMAPDP_ENOMEM, "plan upload: %s", e);
   }
   *out = p;
   return GMAPDP_OK;
+}
+
+int gmapdp_plan_create(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int nsingle,
+                       const gmapdp_end_problem* ends, int nend, gmapdp_result* host_results, gmapdp_plan** out) {
+  return gmapdp_plan_create_all(ctx, singles, nsingle, ends, nend, nullptr, 0, host_results, nullptr, out);
 }
 
 int gmapdp_plan_single(gmapdp_ctx* ctx, const gmapdp_single_problem* problems, int n, gmapdp_result* host_results,
@@ -693,10 +1016,21 @@ int gmapdp_plan_single(gmapdp_ctx* ctx, const gmapdp_single_problem* problems, i
   return gmapdp_plan_create(ctx, problems, n, nullptr, 0, host_results, out);
 }
 
+int gmapdp_plan_bind_genome(gmapdp_plan* plan, const double* d_splice_probs, gmapdp_genome_result* d_genome_results) {
+  if (!plan) return GMAPDP_EINVAL;
+  plan->d_sprob = d_splice_probs;
+  plan->d_gresults = d_genome_results;
+  return GMAPDP_OK;
+}
+
 size_t gmapdp_plan_pair_capacity(const gmapdp_plan* plan) { return plan ? plan->in.pair_capacity : 0; }
 int gmapdp_plan_gpu_problems(const gmapdp_plan* plan) { return plan ? (int)plan->in.dev.size() : 0; }
+int gmapdp_plan_genome_gpu_problems(const gmapdp_plan* plan) { return plan ? (int)plan->in.gdev.size() : 0; }
 int gmapdp_plan_dev_index(const gmapdp_plan* plan, int i) {
   return (plan && i >= 0 && i < (int)plan->in.dev_index.size()) ? plan->in.dev_index[i] : -1;
+}
+int gmapdp_plan_genome_dev_index(const gmapdp_plan* plan, int j) {
+  return (plan && j >= 0 && j < (int)plan->in.gdev_index.size()) ? plan->in.gdev_index[j] : -1;
 }
 int gmapdp_plan_nlaunches(const gmapdp_plan* plan) { return plan ? (int)plan->in.launches.size() : 0; }
 
@@ -710,6 +1044,11 @@ int gmapdp_plan_launch_info(const gmapdp_plan* plan, int li, int* R, int* dirs_l
   return GMAPDP_OK;
 }
 
+int gmapdp_plan_launch_kind(const gmapdp_plan* plan, int li) {
+  if (!plan || li < 0 || li >= (int)plan->in.launches.size()) return GMAPDP_EINVAL;
+  return plan->in.launches[li].kind;
+}
+
 int gmapdp_plan_launch_is_tail(const gmapdp_plan* plan, int li) {
   if (!plan || li < 0 || li >= (int)plan->in.launches.size()) return GMAPDP_EINVAL;
   return launch_is_tail(plan->in.launches[li]) ? 1 : 0;
@@ -718,7 +1057,10 @@ int gmapdp_plan_launch_is_tail(const gmapdp_plan* plan, int li) {
 int gmapdp_plan_launch_members(const gmapdp_plan* plan, int li, int* problem_indices) {
   if (!plan || li < 0 || li >= (int)plan->in.launches.size() || !problem_indices) return GMAPDP_EINVAL;
   const auto& L = plan->in.launches[li];
-  for (int k = 0; k < L.count; k++) problem_indices[k] = plan->in.dev_problem[plan->in.order[L.first + k]];
+  for (int k = 0; k < L.count; k++) {
+    if (L.kind == PlanCore::kDp) problem_indices[k] = plan->in.dev_problem[plan->in.order[L.first + k]];
+    else problem_indices[k] = plan->nsingle + plan->nend + plan->in.gdev_problem[plan->in.gorder[L.first + k]];
+  }
   return GMAPDP_OK;
 }
 
@@ -726,7 +1068,8 @@ int gmapdp_plan_run(gmapdp_ctx* ctx, const gmapdp_plan* plan, const char* d_qseq
                     gmapdp_result* d_results, gmapdp_pair* d_pairs, void* stream) {
   if (!ctx || !plan) return GMAPDP_EINVAL;
   if (!ctx->d_genome) return GMAPDP_ENOGENOME;
-  return run_plan(ctx, plan->in, plan->d_probs, plan->d_order, d_qseq, d_qseq_uc, d_results, d_pairs,
+  if (!plan->in.gdev.empty() && (!plan->d_sprob || !plan->d_gresults)) return bad(ctx, "genome-gap buffers not bound");
+  return run_plan(ctx, plan->in, plan_args(plan, d_qseq, d_qseq_uc, d_results, d_pairs),
                   stream ? (hipStream_t)stream : ctx->stream);
 }
 
@@ -734,17 +1077,18 @@ int gmapdp_plan_run_launch(gmapdp_ctx* ctx, const gmapdp_plan* plan, int li, con
                            const char* d_qseq_uc, gmapdp_result* d_results, gmapdp_pair* d_pairs, void* stream) {
   if (!ctx || !plan || li < 0 || li >= (int)plan->in.launches.size()) return GMAPDP_EINVAL;
   if (!ctx->d_genome) return GMAPDP_ENOGENOME;
-  hipError_t e = launch_one(ctx, plan->in, li, plan->d_probs, plan->d_order, d_qseq, d_qseq_uc, d_results, d_pairs,
+  if (plan->in.gdirs_bytes) {
+    hipError_t e = ctx->gdirs.ensure(plan->in.gdirs_bytes);
+    if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "direction scratch: %s", e);
+  }
+  hipError_t e = launch_one(ctx, plan->in, li, plan_args(plan, d_qseq, d_qseq_uc, d_results, d_pairs),
                             stream ? (hipStream_t)stream : ctx->stream);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "dp launch: %s", e);
   return GMAPDP_OK;
 }
 
 void gmapdp_plan_destroy(gmapdp_plan* plan) {
-  if (!plan) return;
-  if (plan->d_probs) (void)hipFree(plan->d_probs);
-  if (plan->d_order) (void)hipFree(plan->d_order);
-  delete plan;
+  if (plan) plan_free(plan);
 }
 
 void* gmapdp_stream(gmapdp_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }

@@ -55,4 +55,44 @@ struct DevProblem {
   int64_t dirs_offset;    // byte offset into the global direction scratch (global-dirs classes)
 };
 
+// DevGenomeProblem.flags (kFWatson / kFLate as above; kFLate is jump_late_p as given)
+constexpr int32_t kGHalf = 0x100;       // halfp
+constexpr int32_t kGFinal = 0x200;      // finalp
+constexpr int32_t kGSimple = 0x400;     // genome_gap_simple is tried first (!finalp && defect_rate < DEFECT_MEDQ)
+constexpr int32_t kGSegLLeft = 0x800;   // gsequenceL via Genome_get_segment_left (minus strand)
+constexpr int32_t kGSegLRc = 0x1000;
+constexpr int32_t kGSegRLeft = 0x2000;  // rev_gsequenceR via Genome_get_segment_left (plus strand)
+constexpr int32_t kGSegRRc = 0x4000;
+constexpr int32_t kUnset = (int32_t)0x80000000;  // out-parameter the reference leaves unwritten
+
+// Dynprog_genome_gap descriptor (dynprog_genome.c:3288): two fills share the
+// query; the R fill runs on the reversed query against rev_gsequenceR.
+struct DevGenomeProblem {
+  int32_t qbase;          // arena index of rsequence[0]
+  int32_t rlength;
+  int32_t glengthL;
+  int32_t glengthR;
+  int32_t roffset;
+  int32_t goffsetL;
+  int32_t rev_goffsetR;
+  uint32_t chroffset;
+  uint32_t chrhigh;
+  uint32_t segposL, segboundL;  // gsequenceL segment (see DevProblem.segpos)
+  uint32_t segposR, segboundR;  // rev_gsequenceR segment
+  int32_t lbandL;         // both fills (the R fill is called with lbandL, dynprog_genome.c:3813)
+  int32_t ubandL;
+  int32_t ubandR;
+  int32_t open;
+  int32_t extend;
+  int32_t mismatchtype;
+  int32_t flags;
+  int32_t iclass;         // intron score array: 0 sense, 1 antisense, 2 either
+  int32_t genestrand;
+  int32_t dynprogindex;
+  int32_t pair_offset;
+  int32_t pad_;
+  int64_t prob_offset;    // left probabilities at [prob_offset, +glengthL), right ones follow
+  int64_t dirs_offset;    // byte offset into the global scratch (global-dirs classes)
+};
+
 }  // namespace gmapdp

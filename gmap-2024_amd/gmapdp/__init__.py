@@ -17,6 +17,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libgmapdp.so")
 
 WATSON, JUMP_LATE, WIDEBAND = 0x1, 0x2, 0x4
+HALFP, FINALP = 0x8, 0x10
+UNSET = -2147483648
 NEG_INFINITY_32 = -32768
 MAX_RLENGTH, MAX_GLENGTH = 660, 2000
 
@@ -44,6 +46,32 @@ class Result(C.Structure):
                 ("nmatches", C.c_int32), ("nmismatches", C.c_int32), ("nopens", C.c_int32),
                 ("nindels", C.c_int32), ("dynprogindex", C.c_int32)]
 
+
+class GenomeProblem(C.Structure):
+    _fields_ = [("qoff", C.c_int32), ("rlength", C.c_int32), ("glengthL", C.c_int32), ("glengthR", C.c_int32),
+                ("roffset", C.c_int32), ("goffsetL", C.c_int32), ("rev_goffsetR", C.c_int32),
+                ("chroffset", C.c_uint32), ("chrhigh", C.c_uint32), ("flags", C.c_int32),
+                ("cdna_direction", C.c_int32), ("genestrand", C.c_int32), ("extraband", C.c_int32),
+                ("maxpeelback", C.c_int32), ("dynprogindex", C.c_int32), ("pad_", C.c_int32),
+                ("defect_rate", C.c_double), ("prob_offset", C.c_int64)]
+
+
+class GenomeResult(C.Structure):
+    _fields_ = [("npairs", C.c_int32), ("pair_offset", C.c_int32), ("traceback_score", C.c_int32),
+                ("nmatches", C.c_int32), ("nmismatches", C.c_int32), ("nopens", C.c_int32),
+                ("nindels", C.c_int32), ("dynprogindex", C.c_int32), ("new_leftgenomepos", C.c_int32),
+                ("new_rightgenomepos", C.c_int32), ("exonhead", C.c_int32), ("introntype", C.c_int32),
+                ("gap_index", C.c_int32), ("gap_queryjump", C.c_int32), ("left_prob", C.c_double),
+                ("right_prob", C.c_double)]
+
+
+def _struct_dtype(S, fmt):
+    return np.dtype({"names": [n for n, _ in S._fields_], "formats": fmt,
+                     "offsets": [S.__dict__[n].offset for n, _ in S._fields_], "itemsize": C.sizeof(S)})
+
+
+GENOME_PROBLEM_DTYPE = _struct_dtype(GenomeProblem, ["<i4"] * 7 + ["<u4", "<u4"] + ["<i4"] * 7 + ["<f8", "<i8"])
+GENOME_RESULT_DTYPE = _struct_dtype(GenomeResult, ["<i4"] * 14 + ["<f8", "<f8"])
 
 PAIR_DTYPE = np.dtype([("querypos", "<i4"), ("genomepos", "<i4"), ("jump", "<i4"), ("cdna", "S1"),
                        ("comp", "S1"), ("genome", "S1"), ("genomealt", "S1")])
@@ -100,6 +128,18 @@ def load_library(path=LIB_PATH):
         "gmapdp_plan_run_launch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                              C.c_void_p, C.c_void_p]),
         "gmapdp_stream": (C.c_void_p, [C.c_void_p]),
+        "gmapdp_genome_gap_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                              C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
+                                              C.c_size_t]),
+        "gmapdp_genome_pair_capacity": (C.c_size_t, [C.c_void_p, C.c_int]),
+        "gmapdp_genome_prob_entries": (C.c_size_t, [C.c_void_p, C.c_int]),
+        "gmapdp_genome_splice_sites": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t]),
+        "gmapdp_plan_create_all": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
+                                             C.c_int, C.c_void_p, C.c_void_p, P(C.c_void_p)]),
+        "gmapdp_plan_bind_genome": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+        "gmapdp_plan_genome_gpu_problems": (C.c_int, [C.c_void_p]),
+        "gmapdp_plan_genome_dev_index": (C.c_int, [C.c_void_p, C.c_int]),
+        "gmapdp_plan_launch_kind": (C.c_int, [C.c_void_p, C.c_int]),
         "gmapdp_compute_bands": (None, [P(C.c_int), P(C.c_int), C.c_int, C.c_int, C.c_int, C.c_int]),
         "gmapdp_last_error": (C.c_char_p, [C.c_void_p]),
     }
@@ -128,6 +168,42 @@ def pack_genome(seq: bytes) -> np.ndarray:
     if rc:
         raise GmapdpError("gmapdp_pack_genome failed: %d" % rc)
     return out
+
+
+def build_genome_batch(calls):
+    """calls: dicts with the Dynprog_genome_gap arguments (q, quc, rlength, glengthL, glengthR, roffset,
+    goffsetL, rev_goffsetR, chroffset, chrhigh, cdna_direction, flags, genestrand, extraband, defect_rate,
+    maxpeelback, dynprogindex).  Returns (problems, qbuf, qucbuf, nprob_entries); problem i's splice
+    probabilities go at [prob_offset, +glengthL+glengthR) of a double arena."""
+    calls = list(calls)
+    probs = np.zeros(len(calls), dtype=GENOME_PROBLEM_DTYPE)
+    qparts, qucparts, off, poff = [], [], 0, 0
+    for i, p in enumerate(calls):
+        probs[i]["qoff"] = off
+        for k in ("rlength", "glengthL", "glengthR", "roffset", "goffsetL", "rev_goffsetR", "chroffset", "chrhigh",
+                  "flags", "cdna_direction", "genestrand", "extraband", "maxpeelback", "dynprogindex",
+                  "defect_rate"):
+            probs[i][k] = p[k]
+        probs[i]["prob_offset"] = poff
+        poff += max(0, p["glengthL"]) + max(0, p["glengthR"])
+        qparts.append(p["q"])
+        qucparts.append(p["quc"])
+        off += len(p["q"])
+    return probs, (b"".join(qparts) or b"\0"), (b"".join(qucparts) or b"\0"), poff
+
+
+def genome_splice_sites(probs):
+    """(positions uint32, models uint8) of every splice-probability entry: the Maxent_hr_*_prob
+    calls (model 0 donor, 1 acceptor, 2 antidonor, 3 antiacceptor) whose values the engine reads."""
+    lib = load_library()
+    n = len(probs)
+    m = lib.gmapdp_genome_prob_entries(probs.ctypes.data, n)
+    pos = np.zeros(max(m, 1), dtype=np.uint32)
+    mod = np.zeros(max(m, 1), dtype=np.uint8)
+    rc = lib.gmapdp_genome_splice_sites(probs.ctypes.data, n, pos.ctypes.data, mod.ctypes.data, m)
+    if rc:
+        raise GmapdpError("gmapdp_genome_splice_sites failed: %d" % rc)
+    return pos[:m], mod[:m]
 
 
 class Engine:
@@ -250,6 +326,49 @@ class Engine:
                                            results.ctypes.data, pairs.ctypes.data, cap)
         self._check(rc, "gmapdp_end_gap_batch")
         return decode_results(results, pairs, [p["dynprogindex"] for p in calls])
+
+
+    # -- batched Dynprog_genome_gap -------------------------------------------
+    def genome_gap_batch_raw(self, probs, qbuf, qucbuf, splice_probs):
+        n = len(probs)
+        results = np.zeros(n, dtype=GENOME_RESULT_DTYPE)
+        cap = self.lib.gmapdp_genome_pair_capacity(probs.ctypes.data, n)
+        pairs = np.zeros(max(cap, 1), dtype=PAIR_DTYPE)
+        sp = np.ascontiguousarray(splice_probs, dtype=np.float64)
+        if sp.size == 0:
+            sp = np.zeros(1)
+        rc = self.lib.gmapdp_genome_gap_batch(self.h, probs.ctypes.data, n, qbuf, qucbuf, len(qbuf), sp.ctypes.data,
+                                              len(splice_probs), results.ctypes.data, pairs.ctypes.data, cap)
+        self._check(rc, "gmapdp_genome_gap_batch")
+        return results, pairs
+
+    def genome_gap_batch(self, calls, splice_probs):
+        """splice_probs: per call (left_probs, right_probs) lists.  Returns per call
+        ((dpi, score, nmatches, nmismatches, nopens, nindels, new_left, new_right, exonhead, introntype,
+        left_prob, right_prob), pairs-or-None) in the oracle's format (the intron gap holder carries
+        the queryjump)."""
+        calls = list(calls)
+        probs, qbuf, qucbuf, m = build_genome_batch(calls)
+        arena = np.zeros(max(m, 1))
+        for i, (lp, rp) in enumerate(splice_probs):
+            o = int(probs[i]["prob_offset"])
+            arena[o:o + len(lp)] = lp
+            arena[o + len(lp):o + len(lp) + len(rp)] = rp
+        results, pairs = self.genome_gap_batch_raw(probs, qbuf, qucbuf, arena[:m])
+        return decode_genome_results(results, pairs, [p["dynprogindex"] for p in calls])
+
+
+def decode_genome_results(results, pairs, dynprogindices):
+    base = decode_results(results, pairs, dynprogindices)
+    out = []
+    for (scal, lst), res in zip(base, results):
+        scal = scal + (int(res["new_leftgenomepos"]), int(res["new_rightgenomepos"]), int(res["exonhead"]),
+                       int(res["introntype"]), float(res["left_prob"]), float(res["right_prob"]))
+        if lst is not None and res["gap_index"] >= 0:
+            g = int(res["gap_index"])
+            lst[g] = (-1, -1, int(res["gap_queryjump"]), lst[g][3], 0, b" ", b" ", b" ", b" ", 1)
+        out.append((scal, lst))
+    return out
 
 
 def decode_results(results, pairs, dynprogindices):

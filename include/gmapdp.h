@@ -18,6 +18,9 @@
  *   gmapdp_single_gap_batch  Dynprog_single_gap (dynprog_single.c:429), one call per
  *                            problem, many problems per launch
  *   gmapdp_end_gap_batch     Dynprog_end5_gap / Dynprog_end3_gap (dynprog_end.c:1294/1924)
+ *   gmapdp_genome_gap_batch  Dynprog_genome_gap (dynprog_genome.c:3288) + Dynprog_genome_setup
+ *                            (:192, no splicing IIT); gmapdp_genome_splice_sites lists the
+ *                            Maxent_hr_*_prob calls (maxent_hr.c:27357-27600) whose values it takes
  *   gmapdp_plan_*            the same calls, planned once and replayed on device-resident
  *                            inputs (mixed single + end batches)
  *   gmapdp_compute_bands     Dynprog_compute_bands (dynprog.c:1247)
@@ -140,6 +143,96 @@ typedef struct {
   int32_t dynprogindex;    /* *dynprogindex on exit */
 } gmapdp_result;
 
+/* Dynprog_genome_gap flags (in addition to GMAPDP_WATSON / GMAPDP_JUMP_LATE) */
+#define GMAPDP_HALFP   0x8
+#define GMAPDP_FINALP  0x10
+
+/* One Dynprog_genome_gap call (dynprog_genome.c:3288 argument list).  The
+ * query slice is qseq[qoff .. qoff+rlength) (rsequence / rsequenceuc).
+ * chrnum is not needed (it only serves known-splice-site IIT lookups, which
+ * the engine does not perform: see splice probabilities below).
+ * Domain: glengthL and glengthR must exceed rlength (every stage3.c call
+ * passes queryjump + extramaterial_paired); outside it the reference reads
+ * uninitialised probabilities (dynprog_genome.c:2575-2660 leave the last
+ * entry unset), so the engine rejects such a batch with GMAPDP_EINVAL.
+ *
+ * Splice probabilities.  The reference's bridge (dynprog_genome.c:2569-2660)
+ * and genome_gap_simple (:3171) read MaxEnt splice-site probabilities
+ * (Maxent_hr_*_prob, maxent_hr.c, a host symbol the Dynprog objects import).
+ * The caller supplies them in a double arena: problem i's left
+ * probabilities at [prob_offset, prob_offset + glengthL) and its right ones
+ * at [prob_offset + glengthL, prob_offset + glengthL + glengthR);
+ * gmapdp_genome_splice_sites lists the (position, model) of every entry. */
+typedef struct {
+  int32_t qoff;
+  int32_t rlength;
+  int32_t glengthL;
+  int32_t glengthR;
+  int32_t roffset;
+  int32_t goffsetL;
+  int32_t rev_goffsetR;
+  uint32_t chroffset;
+  uint32_t chrhigh;
+  int32_t flags;          /* GMAPDP_WATSON | GMAPDP_JUMP_LATE | GMAPDP_HALFP | GMAPDP_FINALP */
+  int32_t cdna_direction;
+  int32_t genestrand;
+  int32_t extraband;      /* extraband_paired (+ peeled indels, stage3.c:9538) */
+  int32_t maxpeelback;
+  int32_t dynprogindex;
+  int32_t pad_;
+  double defect_rate;
+  int64_t prob_offset;
+} gmapdp_genome_problem;
+
+/* Out-parameters of Dynprog_genome_gap.  new_leftgenomepos,
+ * new_rightgenomepos and exonhead are GMAPDP_UNSET where the reference does
+ * not write them.  The intron gap holder (Pairpool_push_gapholder with
+ * queryjump, genomejump, introntype, donor_prob = left_prob, acceptor_prob =
+ * right_prob; dynprog_genome.c:3227-3232 / 3859-3865) is pairs[gap_index]
+ * (gap_index -1 for a NULL result); its record carries jump = genomejump. */
+#define GMAPDP_UNSET ((int32_t)0x80000000)
+typedef struct {
+  int32_t npairs;          /* 0 <=> NULL List_T */
+  int32_t pair_offset;
+  int32_t traceback_score;
+  int32_t nmatches;
+  int32_t nmismatches;
+  int32_t nopens;
+  int32_t nindels;
+  int32_t dynprogindex;
+  int32_t new_leftgenomepos;
+  int32_t new_rightgenomepos;
+  int32_t exonhead;
+  int32_t introntype;
+  int32_t gap_index;
+  int32_t gap_queryjump;
+  double left_prob;
+  double right_prob;
+} gmapdp_genome_result;
+
+/* Splice-site model of a probability-array entry */
+#define GMAPDP_MAXENT_DONOR        0  /* Maxent_hr_donor_prob */
+#define GMAPDP_MAXENT_ACCEPTOR     1  /* Maxent_hr_acceptor_prob */
+#define GMAPDP_MAXENT_ANTIDONOR    2  /* Maxent_hr_antidonor_prob */
+#define GMAPDP_MAXENT_ANTIACCEPTOR 3  /* Maxent_hr_antiacceptor_prob */
+
+/* For each problem, write glengthL + glengthR (splicesitepos, model) pairs
+ * at the problem's prob_offset: the arguments of the Maxent_hr_*_prob call
+ * (with the problem's chroffset) whose result belongs at that entry
+ * (dynprog_genome.c:2573-2660).  Host-only; no device needed. */
+int gmapdp_genome_splice_sites (const gmapdp_genome_problem *problems, int n, uint32_t *positions,
+                                uint8_t *models, size_t nentries);
+/* Entries of the probability arena needed by the batch (max prob_offset + glengthL + glengthR). */
+size_t gmapdp_genome_prob_entries (const gmapdp_genome_problem *problems, int n);
+
+/* Run n Dynprog_genome_gap problems (same conventions as the other batches).
+ * splice_probs: host arena of gmapdp_genome_prob_entries doubles. */
+int gmapdp_genome_gap_batch (gmapdp_ctx *ctx, const gmapdp_genome_problem *problems, int n,
+                             const char *qseq, const char *qseq_uc, size_t qbytes,
+                             const double *splice_probs, size_t nprobs,
+                             gmapdp_genome_result *results, gmapdp_pair *pairs, size_t pair_capacity);
+size_t gmapdp_genome_pair_capacity (const gmapdp_genome_problem *problems, int n);
+
 /* Create a context on HIP device `device`.  mode = Mode_T (mode.h:5;
  * 0 = STANDARD).  user_* mirror Dynprog_single_setup. */
 int gmapdp_create (gmapdp_ctx **ctx, int device, int mode,
@@ -189,6 +282,20 @@ int gmapdp_plan_create (gmapdp_ctx *ctx, const gmapdp_single_problem *singles, i
                         gmapdp_plan **plan);
 int gmapdp_plan_single (gmapdp_ctx *ctx, const gmapdp_single_problem *problems, int n,
                         gmapdp_result *host_results, gmapdp_plan **plan);
+/* All three families: host_results has nsingle + nend entries, host_genome_results
+ * ngenome entries.  Launch members number the problems singles, ends, genome gaps. */
+int gmapdp_plan_create_all (gmapdp_ctx *ctx, const gmapdp_single_problem *singles, int nsingle,
+                            const gmapdp_end_problem *ends, int nend, const gmapdp_genome_problem *genomes,
+                            int ngenome, gmapdp_result *host_results, gmapdp_genome_result *host_genome_results,
+                            gmapdp_plan **plan);
+/* Device buffers of the genome-gap problems: the splice-probability arena and the
+ * results (indexed by gmapdp_plan_genome_dev_index).  Required before running a plan
+ * that has genome-gap problems on the GPU. */
+int gmapdp_plan_bind_genome (gmapdp_plan *plan, const double *d_splice_probs, gmapdp_genome_result *d_genome_results);
+int gmapdp_plan_genome_gpu_problems (const gmapdp_plan *plan);
+int gmapdp_plan_genome_dev_index (const gmapdp_plan *plan, int j);
+/* 0: Dynprog_single_gap / end-gap kernel, 1: Dynprog_genome_gap kernel */
+int gmapdp_plan_launch_kind (const gmapdp_plan *plan, int li);
 size_t gmapdp_plan_pair_capacity (const gmapdp_plan *plan);
 int gmapdp_plan_gpu_problems (const gmapdp_plan *plan);
 int gmapdp_plan_dev_index (const gmapdp_plan *plan, int i);

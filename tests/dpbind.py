@@ -426,12 +426,28 @@ def genome_gap_problem(rng, genome: bytearray, edge=False):
         goffsetL = rng.randint(60, max(61, chrlen - span - 1200))
     rev_goffsetR = goffsetL + span - 1
     motifs = _MOTIFS_SENSE if cdna_direction >= 0 else _MOTIFS_ANTI
-    if rng.random() < 0.85:
+    x, y = goffsetL + a, rev_goffsetR - b  # first and last intron base (strand coordinates)
+    u = rng.random()
+    if u < 0.5:
+        # strong consensus sites (MaxEnt probabilities near 1): donor CAG|GTAAGT, acceptor
+        # pyrimidine tract + CAG|G; antisense genes see them reverse-complemented
+        if cdna_direction >= 0:
+            left, lx = b"CAG" + b"GTAAGT", x - 3
+            right, ry = b"TTCTTTTCTTTCTTTTCCAG" + b"GTA", y - 19
+        else:
+            left, lx = b"TAC" + b"CTGGAAAAGAAAGAAAAGAA", x - 3
+            right, ry = b"ACTTAC" + b"CTG", y - 5
+        for k, ch in enumerate(left):
+            _strand_set(genome, lx + k, chroffset, chrhigh, watsonp, ch)
+        for k, ch in enumerate(right):
+            _strand_set(genome, ry + k, chroffset, chrhigh, watsonp, ch)
+    elif u < 0.85:
         lm, rm = rng.choice(motifs)
         for k, ch in enumerate(lm):
-            _strand_set(genome, goffsetL + a + k, chroffset, chrhigh, watsonp, ch)
+            _strand_set(genome, x + k, chroffset, chrhigh, watsonp, ch)
         for k, ch in enumerate(rm):
-            _strand_set(genome, rev_goffsetR - b - 1 + k, chroffset, chrhigh, watsonp, ch)
+            _strand_set(genome, y - 1 + k, chroffset, chrhigh, watsonp, ch)
+    if u < 0.85:
         if rng.random() < 0.3:  # decoy site nearby
             d = rng.choice([-4, -3, -2, -1, 1, 2, 3, 4])
             lm2, rm2 = rng.choice(motifs)

@@ -13,6 +13,10 @@ and the reference's outputs.
 
   single_gap_golden.npz  Dynprog_single_gap   (dynprog_single.c:429)
   end_gap_golden.npz     Dynprog_end5_gap / Dynprog_end3_gap (dynprog_end.c:1294/1924)
+  genome_gap_golden.npz  Dynprog_genome_gap   (dynprog_genome.c:3288), with the reference's
+                         MaxEnt splice probabilities (Maxent_hr_*_prob) at every entry the
+                         engine reads; halfp problems come from the --enable-alloca nosimd
+                         build (the default heap build dereferences a freed array there)
 """
 import os
 import random
@@ -22,13 +26,15 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
-from dpbind import (Ref, call_end, call_single, edge_single_gap_problem, end_gap_problem,  # noqa: E402
-                    random_genome, single_gap_problem)
+from dpbind import (GG_FLAG_HALF, Oracle, Ref, call_end, call_single, edge_single_gap_problem,  # noqa: E402
+                    end_gap_problem, genome_gap_problem, random_genome, single_gap_problem, splice_probs)
 
 SINGLE_PARAMS = ["rlength", "glength", "roffset", "goffset", "chroffset", "chrhigh", "watsonp", "genestrand",
                  "jump_late_p", "extraband", "widebandp", "dynprogindex"]
 END_PARAMS = ["end3p", "rlength", "glength", "roffset", "goffset", "chroffset", "chrhigh", "watsonp",
               "genestrand", "jump_late_p", "extraband", "endalign", "require_pos_score_p", "dynprogindex"]
+GENOME_PARAMS = ["rlength", "glengthL", "glengthR", "roffset", "goffsetL", "rev_goffsetR", "chroffset", "chrhigh",
+                 "cdna_direction", "flags", "genestrand", "extraband", "maxpeelback", "dynprogindex"]
 PAIR_DT = np.dtype([("querypos", "<i4"), ("genomepos", "<i4"), ("queryjump", "<i4"), ("genomejump", "<i4"),
                     ("dynprogindex", "<i4"), ("cdna", "S1"), ("comp", "S1"), ("genome", "S1"), ("genomealt", "S1"),
                     ("gapp", "<i4")])
@@ -50,6 +56,14 @@ def end_problems(seed=2025, n_typical=1200, n_edge=400, genome_len=20000):
     return g, probs
 
 
+def genome_problems(seed=2026, n_typical=1200, n_edge=400, genome_len=60000):
+    rng = random.Random(seed)
+    g = bytearray(random_genome(rng, genome_len))
+    probs = [genome_gap_problem(rng, g) for _ in range(n_typical)]
+    probs += [genome_gap_problem(rng, g, edge=True) for _ in range(n_edge)]
+    return bytes(g), probs
+
+
 def pack(g, probs, outputs, names):
     par = np.array([[p[k] for k in names] for p in probs], dtype=np.int64)
     defect = np.array([p["defect_rate"] for p in probs], dtype=np.float64)
@@ -58,8 +72,14 @@ def pack(g, probs, outputs, names):
     qucbuf = np.frombuffer(b"".join(p["quc"] for p in probs) or b"\0", dtype=np.uint8)
     d = dict(genome=np.frombuffer(g, dtype=np.uint8), params=par, param_names=np.array(names), defect=defect,
              qlen=qlen, qbuf=qbuf, qucbuf=qucbuf)
+    if "probsL" in probs[0]:
+        d["splice_probs"] = np.array([x for p in probs for x in list(p["probsL"]) + list(p["probsR"])],
+                                     dtype=np.float64)
     for tag, outs in outputs.items():
-        scal = np.array([o[0] for o in outs], dtype=np.int32)
+        nint = sum(1 for x in outs[0][0] if isinstance(x, int))
+        if nint < len(outs[0][0]):
+            d[tag + "_dscalars"] = np.array([o[0][nint:] for o in outs], dtype=np.float64)
+        scal = np.array([o[0][:nint] for o in outs], dtype=np.int32)
         npairs = np.array([-1 if o[1] is None else len(o[1]) for o in outs], dtype=np.int32)
         flat = [pr for o in outs if o[1] is not None for pr in o[1]]
         d[tag + "_scalars"] = scal
@@ -75,26 +95,34 @@ def load(path):
     qoff = np.concatenate([[0], np.cumsum(z["qlen"])])
     qb, qub = z["qbuf"].tobytes(), z["qucbuf"].tobytes()
     probs = []
+    poff = 0
     for i, row in enumerate(z["params"]):
         p = {k: int(v) for k, v in zip(names, row)}
         p["defect_rate"] = float(z["defect"][i])
         p["q"] = qb[qoff[i]:qoff[i + 1]]
         p["quc"] = qub[qoff[i]:qoff[i + 1]]
+        if "splice_probs" in z.files:
+            gl, gr = max(0, p["glengthL"]), max(0, p["glengthR"])
+            p["probsL"] = [float(x) for x in z["splice_probs"][poff:poff + gl]]
+            p["probsR"] = [float(x) for x in z["splice_probs"][poff + gl:poff + gl + gr]]
+            poff += gl + gr
         probs.append(p)
     outs = {}
     for key in z.files:
         if key.endswith("_scalars"):
             tag = key[:-len("_scalars")]
             scal, npairs, pairs = z[tag + "_scalars"], z[tag + "_npairs"], z[tag + "_pairs"]
+            dscal = z[tag + "_dscalars"] if (tag + "_dscalars") in z.files else None
             res, pos = [], 0
             for i in range(len(scal)):
                 n = int(npairs[i])
+                sc = tuple(int(x) for x in scal[i]) + (() if dscal is None else tuple(float(x) for x in dscal[i]))
                 if n < 0:
-                    res.append((tuple(int(x) for x in scal[i]), None))
+                    res.append((sc, None))
                     continue
                 seg = pairs[pos:pos + n]
                 pos += n
-                res.append((tuple(int(x) for x in scal[i]),
+                res.append((sc,
                             [(int(r["querypos"]), int(r["genomepos"]), int(r["queryjump"]), int(r["genomejump"]),
                               int(r["dynprogindex"]), bytes(r["cdna"]) or b"\0", bytes(r["comp"]) or b"\0",
                               bytes(r["genome"]) or b"\0", bytes(r["genomealt"]) or b"\0", int(r["gapp"]))
@@ -115,6 +143,16 @@ def main():
         out = os.path.join(HERE, name)
         np.savez_compressed(out, **pack(g, probs, outputs, names))
         print("wrote %s: %d problems" % (out, len(probs)))
+    g, probs = genome_problems()
+    ref, refa, orc = Ref("nosimd"), Ref("nosimda"), Oracle()
+    for r in (ref, refa, orc):
+        r.set_genome(g)
+    for p in probs:
+        p["probsL"], p["probsR"] = splice_probs(ref, orc, p)
+    outputs = {"ref_nosimd": [(refa if p["flags"] & GG_FLAG_HALF else ref).genome_gap(p) for p in probs]}
+    out = os.path.join(HERE, "genome_gap_golden.npz")
+    np.savez_compressed(out, **pack(g, probs, outputs, GENOME_PARAMS))
+    print("wrote %s: %d problems" % (out, len(probs)))
 
 
 if __name__ == "__main__":

@@ -79,3 +79,27 @@ def test_problem_struct_layout():
     assert C.sizeof(gmapdp.Result) == 32
     assert gmapdp.PAIR_DTYPE.itemsize == 16
     assert gmapdp.PROBLEM_DTYPE.itemsize == 56
+
+
+def test_genome_struct_layout():
+    assert C.sizeof(gmapdp.GenomeProblem) == 80
+    assert C.sizeof(gmapdp.GenomeResult) == 72
+    assert gmapdp.GENOME_PROBLEM_DTYPE.itemsize == 80
+    assert gmapdp.GENOME_RESULT_DTYPE.itemsize == 72
+
+
+def test_genome_splice_sites_match_oracle():
+    """gmapdp_genome_splice_sites (host-only) lists the same Maxent_hr_*_prob calls as the oracle's
+    restatement of dynprog_genome.c:2573-2660."""
+    from dpbind import Oracle, genome_gap_problem, random_genome
+    rng = random.Random(31)
+    g = bytearray(random_genome(rng, 30000))
+    calls = [genome_gap_problem(rng, g) for _ in range(200)]
+    probs, _, _, m = gmapdp.build_genome_batch(calls)
+    pos, mod = gmapdp.genome_splice_sites(probs)
+    orc = Oracle()
+    for i, p in enumerate(calls):
+        sl, sr = orc.splice_sites(p)
+        o = int(probs[i]["prob_offset"])
+        got = list(zip(pos[o:o + len(sl) + len(sr)].tolist(), mod[o:o + len(sl) + len(sr)].tolist()))
+        assert got == sl + sr

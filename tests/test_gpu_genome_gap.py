@@ -1,0 +1,98 @@
+"""GPU parity tests for Dynprog_genome_gap (bit-exact, including the double
+splice-probability tie-breaks of bridge_intron_gap_site_level)."""
+import os
+import random
+
+import pytest
+
+import gmapdp
+from dpbind import (GG_FLAG_HALF, Oracle, Ref, genome_gap_problem, random_genome, ref_available, splice_probs)
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _golden():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(HERE, "golden", "make_golden.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m.load(os.path.join(HERE, "golden", "genome_gap_golden.npz"))
+
+
+@pytest.fixture(scope="module")
+def engine():
+    e = gmapdp.Engine(0)
+    yield e
+    e.close()
+
+
+def _first_diff(got, exp):
+    for i, (a, b) in enumerate(zip(got, exp)):
+        if a != b:
+            return i, a, b
+    return None
+
+
+def _msg(probs, d, what):
+    return "problem %d (%s): gpu %s vs %s %s" % (
+        d[0], {k: v for k, v in probs[d[0]].items() if k not in ("q", "quc", "probsL", "probsR")}, d[1], what, d[2])
+
+
+def test_gpu_genome_gap_matches_reference_golden(engine):
+    g, probs, outs = _golden()
+    engine.set_genome(g)
+    got = engine.genome_gap_batch(probs, [(p["probsL"], p["probsR"]) for p in probs])
+    d = _first_diff(got, outs["ref_nosimd"])
+    assert d is None, _msg(probs, d, "ref")
+
+
+def _synthetic_probs(rng, p):
+    """Coarse probabilities with many exact ties, to stress the (score, prob, scan order) rule."""
+    vals = [0.0, 0.25, 0.5, 0.5, 0.9, 0.95, 1.0]
+    return ([rng.choice(vals) for _ in range(max(0, p["glengthL"]))],
+            [rng.choice(vals) for _ in range(max(0, p["glengthR"]))])
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_gpu_genome_gap_matches_oracle_random(engine, seed):
+    rng = random.Random(3000 + seed)
+    g = bytearray(random_genome(rng, 120000))
+    probs = [genome_gap_problem(rng, g, edge=(i % 5 == 0)) for i in range(5000)]
+    g = bytes(g)
+    engine.set_genome(g)
+    orc = Oracle()
+    orc.set_genome(g)
+    sp = [_synthetic_probs(rng, p) for p in probs]
+    got = engine.genome_gap_batch(probs, sp)
+    exp = [orc.genome_gap(p, lp, rp) for p, (lp, rp) in zip(probs, sp)]
+    d = _first_diff(got, exp)
+    assert d is None, _msg(probs, d, "oracle")
+
+
+@pytest.mark.skipif(not ref_available("nosimda"), reason="reference objects did not travel")
+def test_gpu_genome_gap_matches_reference_objects(engine):
+    rng = random.Random(79)
+    g = bytearray(random_genome(rng, 80000))
+    probs = [genome_gap_problem(rng, g, edge=(i % 4 == 0)) for i in range(2000)]
+    g = bytes(g)
+    engine.set_genome(g)
+    ref, refa, orc = Ref("nosimd"), Ref("nosimda"), Oracle()
+    for r in (ref, refa, orc):
+        r.set_genome(g)
+    sp = [splice_probs(ref, orc, p) for p in probs]
+    got = engine.genome_gap_batch(probs, sp)
+    exp = [(refa if p["flags"] & GG_FLAG_HALF else ref).genome_gap(p) for p in probs]
+    d = _first_diff(got, exp)
+    assert d is None, _msg(probs, d, "ref")
+
+
+def test_gpu_genome_gap_domain_check(engine):
+    """glength <= rlength is outside the reference's defined domain: rejected, not guessed."""
+    rng = random.Random(5)
+    g = bytearray(random_genome(rng, 20000))
+    p = genome_gap_problem(rng, g)
+    p["glengthL"] = p["rlength"]
+    engine.set_genome(bytes(g))
+    with pytest.raises(gmapdp.GmapdpError):
+        engine.genome_gap_batch([p], [([0.0] * p["glengthL"], [0.0] * p["glengthR"])])

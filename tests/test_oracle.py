@@ -143,3 +143,85 @@ def test_oracle_end_gap_vs_reference_random(oracle):
         if call_end(ref, p) != call_end(oracle, p):
             bad += 1
     assert bad == 0
+
+
+# ---------------------------------------------------------------------------
+# Dynprog_genome_gap
+# ---------------------------------------------------------------------------
+def _golden_genome():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(HERE, "golden", "make_golden.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m.load(os.path.join(HERE, "golden", "genome_gap_golden.npz"))
+
+
+def test_oracle_genome_gap_matches_golden(oracle):
+    g, probs, outs = _golden_genome()
+    oracle.set_genome(g)
+    exp = outs["ref_nosimd"]
+    assert len(probs) == len(exp) == 1600
+    bad = [i for i, p in enumerate(probs) if oracle.genome_gap(p, p["probsL"], p["probsR"]) != exp[i]]
+    assert bad == [], "oracle differs from reference genome-gap golden on %d problems (first %s)" % (len(bad), bad[:5])
+
+
+def test_genome_golden_covers_every_branch():
+    """The golden set exercises each exit of Dynprog_genome_gap (dynprog_genome.c:3354-3897)."""
+    from dpbind import GG_FLAG_FINAL, GG_FLAG_HALF
+    g, probs, outs = _golden_genome()
+    exp = outs["ref_nosimd"]
+    kinds = {"small": 0, "guard": 0, "simple": 0, "bridge_fail": 0, "full": 0, "full_null": 0, "half": 0,
+             "full_indels": 0, "gapholder_inside": 0}
+    for p, (s, pairs) in zip(probs, exp):
+        simple_ok = pairs is not None and s[4] == 0 and s[5] == 0 and \
+            any(x[9] == 1 and x[2] == 0 for x in pairs) and p["defect_rate"] < 0.014 and not p["flags"] & GG_FLAG_FINAL
+        if p["rlength"] <= 1:
+            kinds["small"] += 1
+        elif s[1] == -32768:
+            kinds["guard"] += 1
+        elif s[1] == -100 and s[6] == -2147483648:
+            kinds["bridge_fail"] += 1
+        elif pairs is None:
+            kinds["full_null"] += 1
+        elif simple_ok:
+            kinds["simple"] += 1
+        else:
+            kinds["full"] += 1
+            if sum(1 for x in pairs if x[9] == 1) > 1:
+                kinds["gapholder_inside"] += 1
+            if s[4] > 0:
+                kinds["full_indels"] += 1
+        if p["flags"] & GG_FLAG_HALF and pairs is not None:
+            kinds["half"] += 1
+    for k in ("small", "guard", "simple", "bridge_fail", "full", "full_null", "half", "full_indels", "gapholder_inside"):
+        assert kinds[k] > 0, sorted(kinds.items())
+
+
+@pytest.mark.skipif(not ref_available("nosimda"), reason="reference objects (oracle/_ref) not built here")
+def test_oracle_genome_gap_vs_reference_random(oracle):
+    from dpbind import GG_FLAG_HALF, genome_gap_problem, splice_probs
+    ref, refa = Ref("nosimd"), Ref("nosimda")
+    rng = random.Random(4343)
+    g = bytearray(random_genome(rng, 80000))
+    probs = [genome_gap_problem(rng, g, edge=(i % 5 == 0)) for i in range(2500)]
+    for r in (ref, refa, oracle):
+        r.set_genome(bytes(g))
+    bad = []
+    for i, p in enumerate(probs):
+        lp, rp = splice_probs(ref, oracle, p)
+        exp = (refa if p["flags"] & GG_FLAG_HALF else ref).genome_gap(p)
+        if oracle.genome_gap(p, lp, rp) != exp:
+            bad.append(i)
+    assert bad == []
+
+
+def test_intron_scores_restate_setup(oracle):
+    """intron_score_setup (dynprog_genome.c:144-187): the engine's table equals the oracle's."""
+    import gmapdp  # noqa: F401  (table is internal to the engine; compare via the oracle's export)
+    out = (C.c_int * (3 * 2 * 64))()
+    oracle.lib.orc_intron_scores(out)
+    t = np.array(out[:]).reshape(3, 2, 64)
+    assert t[0, 0, 0x20] == 14 and t[0, 1, 0x20] == 16 and t[1, 0, 0x04] == 14
+    assert t[2, 0, 0x20] == 16 and t[2, 1, 0x04] == 14   # the reference's mixed "either" arrays
+    assert t.sum() == (14 + 8 + 4) + (16 + 10 + 8) + (14 + 8 + 4) + (16 + 10 + 8) + (16 + 8 + 4 + 14 + 8 + 4) + \
+        (16 + 10 + 8 + 14 + 10 + 8)
