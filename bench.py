@@ -14,6 +14,14 @@ endalign).  One "step" = one pass of the engine over the sub-problems of
 value = reads whose DP sub-problems were processed per second, whole job
 (all ranks).  This is the DP-engine throughput of the path, not end-to-end
 GMAP (stage 1/2/3 orchestration stays on the host; DESIGN.md "Measurement").
+
+The same JSON line carries "all_dynprog": the same measurement with the
+Dynprog_genome_gap calls added (49.4 per read; the configs[2]
+DP mix without stage 2): query gaps spanning a planted GT-AG intron,
+glength = rlength + extramaterial_paired (8), extraband_paired 14.  Their
+MaxEnt splice probabilities are a host input to the engine (the caller's
+Maxent_hr_*_prob values); the bench supplies synthetic ones (0.95 at the
+planted sites, U[0, 0.3) elsewhere).
 """
 import argparse
 import ctypes as C
@@ -31,6 +39,7 @@ CHR22_LEN = 50_818_468
 SINGLE_PER_READ = 43.7         # Dynprog_single_gap calls per 2-kb read (nosimd)
 END5_PER_READ = 7.1            # Dynprog_end5_gap
 END3_PER_READ = 6.5            # Dynprog_end3_gap
+GENOME_PER_READ = 49.4         # Dynprog_genome_gap
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 COMPL = np.zeros(256, dtype=np.uint8)
 for _a, _b in zip(b"ACGTN", b"TGCAN"):
@@ -139,6 +148,57 @@ def make_end(genome, n5, n3, rng):
     return probs, q
 
 
+def make_genome_gaps(genome, n, rng):
+    """Vectorised Dynprog_genome_gap sub-problems (stage3.c:9504-9539): a query gap of rlength
+    nt = a exonic nt before a planted GT..AG intron + b after it; goffsetL = first genomic
+    position after the left anchor, rev_goffsetR = last one before the right anchor,
+    glengthL = glengthR = rlength + 8.  Plants the dinucleotides into `genome` (in place)."""
+    import gmapdp
+    glen = len(genome)
+    r = np.clip(rng.gamma(2.2, 50.0, size=n).astype(np.int64), 2, 600)
+    a = (rng.random(n) * (r + 1)).astype(np.int64)
+    b = r - a
+    intron = rng.integers(60, 5000, size=n)
+    watson = rng.random(n) < 0.5
+    goffL = rng.integers(100, glen - 7000, size=n)
+    revR = goffL + a + intron + b - 1
+    x, y = goffL + a, revR - b            # first / last intron base, strand coordinates
+    # strand coordinate p -> genome index: watson p, minus glen - p (complemented)
+    def plant(pos, ch):
+        idx = np.where(watson, pos, glen - pos)
+        genome[idx] = np.where(watson, ord(ch), COMPL[ord(ch)])
+    plant(x, "G"); plant(x + 1, "T"); plant(y - 1, "A"); plant(y, "G")
+    q_off = np.concatenate([[0], np.cumsum(r)])
+    qpid = np.repeat(np.arange(n), r)
+    j = np.arange(q_off[-1]) - q_off[qpid]
+    src = np.where(j < a[qpid], goffL[qpid] + j, revR[qpid] - b[qpid] + 1 + (j - a[qpid]))
+    q = genomic_chars(genome, src, watson[qpid])
+    q = np.where(rng.random(q.size) < 0.02, ACGT[rng.integers(0, 4, size=q.size, dtype=np.uint8)], q)
+    gp = np.zeros(n, dtype=gmapdp.GENOME_PROBLEM_DTYPE)
+    gp["qoff"] = q_off[:-1]
+    gp["rlength"] = r
+    gp["glengthL"] = r + 8
+    gp["glengthR"] = r + 8
+    gp["roffset"] = rng.integers(0, 1500, size=n)
+    gp["goffsetL"] = goffL
+    gp["rev_goffsetR"] = revR
+    gp["chroffset"] = 0
+    gp["chrhigh"] = glen
+    gp["flags"] = watson.astype(np.int32) * gmapdp.WATSON | (rng.random(n) < 0.5) * gmapdp.JUMP_LATE
+    gp["cdna_direction"] = 1
+    gp["extraband"] = 14
+    gp["maxpeelback"] = 60
+    gp["dynprogindex"] = rng.integers(1, 50, size=n) * np.where(rng.random(n) < 0.5, 1, -1)
+    gp["defect_rate"] = np.where(rng.random(n) < 0.7, 0.02, 0.01)
+    ent = 2 * (r + 8)
+    p_off = np.concatenate([[0], np.cumsum(ent)])
+    gp["prob_offset"] = p_off[:-1]
+    sprob = rng.random(int(p_off[-1])) * 0.3
+    sprob[p_off[:-1] + a] = 0.95                 # left site (cL = a)
+    sprob[p_off[:-1] + (r + 8) + b] = 0.95       # right site (cR = b)
+    return gp, q.astype(np.uint8), sprob
+
+
 def make_workload(genome, reads, seed):
     rng = np.random.default_rng(seed)
     ns = int(round(reads * SINGLE_PER_READ))
@@ -212,6 +272,31 @@ def cpu_baseline(sp, ep, q, genome, budget_s=12.0):
                       % (ns, ne, t_single + t_end, SINGLE_PER_READ, END5_PER_READ + END3_PER_READ)}
 
 
+def cpu_baseline_genome(gp, q, genome, budget_s=8.0):
+    """The reference's Dynprog_genome_gap (1 core) on a bounded prefix of the genome-gap stream;
+    it computes its own MaxEnt probabilities (maxent_hr.c) inside the timed calls."""
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "librefdp_nosimd.so")
+    if not os.path.exists(ref_so):
+        return None
+    lib = C.CDLL(ref_so)
+    lib.refh_init(0, 0, 0)
+    gb = genome.tobytes()
+    lib.refh_set_genome(gb, len(gb))
+    f = lib.refh_genome_gap_batch
+    f.restype = C.c_long
+    f.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_char_p]
+    qb = q.tobytes()
+    t, n, chunk = 0.0, 0, 256
+    while t < budget_s and n + chunk <= len(gp):
+        a = np.ascontiguousarray(gp[n:n + chunk])
+        t0 = time.perf_counter()
+        f(a.ctypes.data, chunk, qb, qb)
+        t += time.perf_counter() - t0
+        n += chunk
+        chunk = min(chunk * 2, 8192)
+    return t / max(n, 1), n
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -237,92 +322,118 @@ def main():
     sp, ep, q = make_workload(genome, args.reads, seed=1000 + rank)
     ns, ne = len(sp), len(ep)
     nprob = ns + ne
+    rng_g = np.random.default_rng(2000 + rank)
+    ng = int(round(args.reads * GENOME_PER_READ))
+    gp, gq, sprob = make_genome_gaps(genome, ng, rng_g)   # plants intron motifs: before set_genome
+    gp["qoff"] += len(q)
+    q_all = np.concatenate([q, gq])
 
     eng = gmapdp.Engine(local)
     eng.set_genome(genome.tobytes())
     lib = eng.lib
-    host_res = np.zeros(nprob, dtype=gmapdp.RESULT_DTYPE)
-    plan = C.c_void_p()
-    eng._check(lib.gmapdp_plan_create(eng.h, sp.ctypes.data, ns, ep.ctypes.data, ne, host_res.ctypes.data,
-                                      C.byref(plan)), "gmapdp_plan_create")
-    ngpu = lib.gmapdp_plan_gpu_problems(plan)
-    cap = lib.gmapdp_plan_pair_capacity(plan)
-    d_q = torch.from_numpy(q).to(dev)
-    d_res = torch.zeros(max(ngpu, 1) * 32, dtype=torch.uint8, device=dev)
-    d_pairs = torch.empty(max(cap, 1) * 16, dtype=torch.uint8, device=dev)
-    nl = lib.gmapdp_plan_nlaunches(plan)
-    info = []
-    for li in range(nl):
-        R, dl, cnt, lds = C.c_int(), C.c_int(), C.c_int(), C.c_size_t()
-        lib.gmapdp_plan_launch_info(plan, li, C.byref(R), C.byref(dl), C.byref(cnt), C.byref(lds))
-        info.append((R.value, dl.value, cnt.value, lds.value))
-    # the kernel template each launch runs; the dominant kernel is the template with most problems
-    kname = ["dp_kernel<R=%d,dirs_lds=%d>" % (i[0], i[1]) for i in info]
-    tail = [lib.gmapdp_plan_launch_is_tail(plan, li) == 1 for li in range(nl)]
-    per_kernel = {}
-    for li in range(nl):
-        if not tail[li]:
-            per_kernel.setdefault(kname[li], []).append(li)
-    dominant = max(per_kernel, key=lambda k: sum(info[li][2] for li in per_kernel[k]))
+    d_q = torch.from_numpy(q_all).to(dev)
+    d_sprob = torch.from_numpy(sprob).to(dev)
+
+    def build(with_genome):
+        host_res = np.zeros(nprob, dtype=gmapdp.RESULT_DTYPE)
+        host_gres = np.zeros(max(ng, 1), dtype=gmapdp.GENOME_RESULT_DTYPE)
+        plan = C.c_void_p()
+        eng._check(lib.gmapdp_plan_create_all(eng.h, sp.ctypes.data, ns, ep.ctypes.data, ne,
+                                              gp.ctypes.data if with_genome else None, ng if with_genome else 0,
+                                              host_res.ctypes.data, host_gres.ctypes.data, C.byref(plan)),
+                   "gmapdp_plan_create_all")
+        P = {"plan": plan, "ngpu": lib.gmapdp_plan_gpu_problems(plan),
+             "nggpu": lib.gmapdp_plan_genome_gpu_problems(plan), "cap": lib.gmapdp_plan_pair_capacity(plan)}
+        P["d_res"] = torch.zeros(max(P["ngpu"], 1) * 32, dtype=torch.uint8, device=dev)
+        P["d_gres"] = torch.zeros(max(P["nggpu"], 1) * 72, dtype=torch.uint8, device=dev)
+        P["d_pairs"] = torch.empty(max(P["cap"], 1) * 16, dtype=torch.uint8, device=dev)
+        eng._check(lib.gmapdp_plan_bind_genome(plan, C.c_void_p(d_sprob.data_ptr()),
+                                               C.c_void_p(P["d_gres"].data_ptr())), "gmapdp_plan_bind_genome")
+        nl = lib.gmapdp_plan_nlaunches(plan)
+        info = []
+        for li in range(nl):
+            R, dl, cnt, lds = C.c_int(), C.c_int(), C.c_int(), C.c_size_t()
+            lib.gmapdp_plan_launch_info(plan, li, C.byref(R), C.byref(dl), C.byref(cnt), C.byref(lds))
+            info.append((R.value, dl.value, cnt.value, lds.value))
+        P["nl"], P["info"] = nl, info
+        P["kind"] = [lib.gmapdp_plan_launch_kind(plan, li) for li in range(nl)]
+        P["tail"] = [lib.gmapdp_plan_launch_is_tail(plan, li) == 1 for li in range(nl)]
+        return P
+
     # Same issue order as gmapdp_plan_run: tail classes (long problems, latency-bound) on side
     # streams, the bulk on the main stream, joined at the end of the step.  Real (non-null)
     # streams, so the per-launch events on the main stream see exactly the bulk launches.
     stream = torch.cuda.Stream(dev)
     sides = [torch.cuda.Stream(dev) for _ in range(3)]
 
-    def launch(li, s):
-        eng._check(lib.gmapdp_plan_run_launch(eng.h, plan, li, C.c_void_p(d_q.data_ptr()),
-                                              C.c_void_p(d_q.data_ptr()), C.c_void_p(d_res.data_ptr()),
-                                              C.c_void_p(d_pairs.data_ptr()), C.c_void_p(s.cuda_stream)),
-                   "gmapdp_plan_run_launch")
+    def timed(P, steps, warmup):
+        plan, nl, tail = P["plan"], P["nl"], P["tail"]
 
-    def step(ev=None):
-        fork = torch.cuda.Event()
-        fork.record(stream)
-        used = 0
-        for li in range(nl):
-            if tail[li]:
-                s = sides[used % len(sides)]
-                s.wait_event(fork)
-                launch(li, s)
-                used += 1
-        for li in range(nl):
-            if tail[li]:
-                continue
-            if ev is not None:
-                ev[li][0].record(stream)
-            launch(li, stream)
-            if ev is not None:
-                ev[li][1].record(stream)
-        for s in sides[:used]:
-            stream.wait_stream(s)
+        def launch(li, s):
+            eng._check(lib.gmapdp_plan_run_launch(eng.h, plan, li, C.c_void_p(d_q.data_ptr()),
+                                                  C.c_void_p(d_q.data_ptr()), C.c_void_p(P["d_res"].data_ptr()),
+                                                  C.c_void_p(P["d_pairs"].data_ptr()), C.c_void_p(s.cuda_stream)),
+                       "gmapdp_plan_run_launch")
 
-    with torch.cuda.stream(stream):
-        for _ in range(args.warmup):
-            step()
-        torch.cuda.synchronize()
-        evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nl)]
-               for _ in range(args.steps)]
+        def step(ev=None):
+            fork = torch.cuda.Event()
+            fork.record(stream)
+            used = 0
+            for li in range(nl):
+                if tail[li]:
+                    s = sides[used % len(sides)]
+                    s.wait_event(fork)
+                    launch(li, s)
+                    used += 1
+            for li in range(nl):
+                if tail[li]:
+                    continue
+                if ev is not None:
+                    ev[li][0].record(stream)
+                launch(li, stream)
+                if ev is not None:
+                    ev[li][1].record(stream)
+            for s in sides[:used]:
+                stream.wait_stream(s)
+
+        with torch.cuda.stream(stream):
+            for _ in range(warmup):
+                step()
+            torch.cuda.synchronize()
+            evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nl)]
+                   for _ in range(steps)]
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for k in range(steps):
+                step(evs[k])
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            elapsed = time.perf_counter() - t0
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for k in range(args.steps):
-            step(evs[k])
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
-    launch_ms = [None if tail[li] else
-                 sum(evs[k][li][0].elapsed_time(evs[k][li][1]) for k in range(args.steps)) / args.steps
-                 for li in range(nl)]
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        launch_ms = [None if tail[li] else
+                     sum(evs[k][li][0].elapsed_time(evs[k][li][1]) for k in range(steps)) / steps
+                     for li in range(nl)]
+        return float(t.item()), launch_ms
+
+    # ---- headline: configs[1] (Dynprog_single_gap + Dynprog_end{5,3}_gap) ----
+    P = build(False)
+    plan, nl, info, tail, ngpu = P["plan"], P["nl"], P["info"], P["tail"], P["ngpu"]
+    # the kernel template each launch runs; the dominant kernel is the template with most problems
+    kname = ["dp_kernel<R=%d,dirs_lds=%d>" % (i[0], i[1]) for i in info]
+    per_kernel = {}
+    for li in range(nl):
+        if not tail[li]:
+            per_kernel.setdefault(kname[li], []).append(li)
+    dominant = max(per_kernel, key=lambda k: sum(info[li][2] for li in per_kernel[k]))
+    elapsed, launch_ms = timed(P, args.steps, args.warmup)
 
     # results of the last pass (for algorithmic byte accounting)
-    res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=gmapdp.RESULT_DTYPE)[:ngpu]
+    res = np.frombuffer(P["d_res"].cpu().numpy().tobytes(), dtype=gmapdp.RESULT_DTYPE)[:ngpu]
     dev_index = np.array([lib.gmapdp_plan_dev_index(plan, i) for i in range(nprob)])
     gpu_mask = dev_index >= 0
     npairs = np.zeros(nprob, dtype=np.int64)
@@ -375,11 +486,36 @@ def main():
                      "note": "integer VALU/LDS-bound DP; HBM roofline reported as required (DESIGN.md)"},
         "step_algorithmic_bytes": step_bytes,
     }
+    lib.gmapdp_plan_destroy(plan)
+    del P
+
+    # ---- all Dynprog_* paths: + Dynprog_genome_gap ----
+    PA = build(True)
+    gsteps = max(1, args.steps // 2)
+    elapsed_all, launch_ms_all = timed(PA, gsteps, max(1, args.warmup // 2))
+    gk = [li for li in range(PA["nl"]) if PA["kind"][li] == 1]
+    gr = gp["rlength"].astype(np.int64)
+    gcells = int((2 * np.minimum(8 + 2 * 14 + 1, gr + 1) * (gr + 8)).sum())  # two fills, band W = 37
+    out["all_dynprog"] = {
+        "value": args.reads * world * gsteps / elapsed_all, "unit": "reads/s",
+        "ms_per_step": elapsed_all / gsteps * 1e3, "steps": gsteps,
+        "genome_gap_calls_per_read": GENOME_PER_READ, "genome_gap_subproblems_per_step_per_gpu": ng,
+        "gcups": (cells + gcells) * world * gsteps / elapsed_all / 1e9,
+        "genome_gap_launch_classes": [PA["info"][li] for li in gk],
+        "genome_gap_bulk_launch_ms": [launch_ms_all[li] for li in gk if launch_ms_all[li] is not None],
+        "splice_probabilities": "synthetic host input (0.95 at planted GT-AG sites, U[0,0.3) elsewhere)"}
+    lib.gmapdp_plan_destroy(PA["plan"])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(sp, ep, q, genome)
+        out["cpu_baseline"] = cpu_baseline(sp, ep, q_all, genome)
+        cg = cpu_baseline_genome(gp, q_all, genome)
+        if out["cpu_baseline"] is not None and cg is not None:
+            spr = 1.0 / out["cpu_baseline"]["value"] + GENOME_PER_READ * cg[0]
+            out["all_dynprog"]["cpu_baseline"] = {
+                "value": 1.0 / spr, "unit": "reads/s", "cores": 1, "kind": "reference",
+                "sample": "headline sample + %d Dynprog_genome_gap problems of the same stream (reference "
+                          "computes its own MaxEnt probabilities), weighted %.1f calls/read" % (cg[1], GENOME_PER_READ)}
     elif rank == 0:
         out["cpu_baseline"] = None
-    lib.gmapdp_plan_destroy(plan)
     if rank == 0:
         print(json.dumps(out))
     if world > 1:

@@ -271,13 +271,40 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
 
 // ---- banded fill (Dynprog_standard, upperp = lowerp = true, saturation NEG_INFINITY_INT) ----
 // Rows r = c - uband + k, k = lane*R + i.  Writes the four direction ballots of every column to
-// `dirs`; with HST also the stored (clamped) matrix value of every band cell to hst[c*W + k]
-// (int16 is exact: stored values lie in [-32768, 3*660]).  track: 0 none, 1 best endpoint over
+// `dirs`; with CARRY also the Dynprog_genome_gap bridge candidates (BridgeCarry).  track: 0 none, 1 best endpoint over
 // the whole band (find_best_endpoint_std), 2 best endpoint on row rlength (_to_queryend_indels_std).
-template <int R, bool HST>
+// Bridge candidates of Dynprog_genome_gap carried along band rows during a fill
+// (bridge_intron_gap_site_level, dynprog_genome.c:2736-2844).  A row's cells
+// arrive column by column, and a row moves one band offset down per column --
+// the path the E input already takes -- so each row's best candidate so far
+// travels with it (DPP wave_shl:1) and is final when the row leaves the band.
+// R fill ("B", indel on the right): row rR, other = rL = rlength - rR, candidate
+//   cR: isc[leftdi[rL] & rightdi[cR]] + matrixR[cR][rR], probL[rL] + probR[cR].
+// L fill ("C", indel on the left): row rL, other = rR, candidate cL:
+//   matrixL[cL][rL] + isc[leftdi[cL] & rightdi[rR]], probL[cL] + probR[rR].
+// A cell is a candidate when 1 <= r <= rlength-1, band offset k >= 1
+// (c < r + uband), c <= glength-2 and c < (rev_goffsetR - goffsetL) - other;
+// c >= r - lband holds inside the band.  Ties keep the earlier column.
+struct BridgeCarry {
+  const uint8_t* rowdi;   // dinucleotide code of the other side, indexed by `other`
+  const uint8_t* coldi;   // dinucleotide code of this side, indexed by column
+  const double* rowp;     // probability of the other side, indexed by `other`
+  const double* colp;     // probability of this side, indexed by column
+  const int8_t* isc;      // intron score array (64 entries)
+  int rdist;              // rev_goffsetR - goffsetL
+  struct Part* part;      // best candidate per row of this fill
+  int* diag;              // matrix[r][r] per row
+};
+struct Part {
+  double p;
+  int s;
+  int c;  // -1: no candidate
+};
+
+template <int R, bool CARRY>
 __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lband, int uband, int open, int ext,
                                           int late, int track, const int8_t* sc, int srow, const uint8_t* gcl,
-                                          uint64_t* dirs, int16_t* hst, int& bestr, int& bestc) {
+                                          uint64_t* dirs, const BridgeCarry* bc_, int& bestr, int& bestc) {
   const int sat = kNegInf32;
   const int W = lband + uband + 1;
   const int binit = (track == 2) ? kNegInf32 : 0;
@@ -298,6 +325,14 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
   int kext[R];  // k*ext per element: r*ext = rtop*ext + k*ext without a per-column multiply
 #pragma unroll
   for (int i = 0; i < R; i++) kext[i] = (lane * R + i) * ext;
+  int cs[R], cc[R];  // carried bridge candidate per band row: score, column (-1: none), probability
+  double cp[R];
+#pragma unroll
+  for (int i = 0; i < R; i++) {
+    cs[i] = 0;
+    cc[i] = -1;
+    cp[i] = 0.0;
+  }
   for (int c = 1; c <= glen; c++) {
     const int gi = __builtin_amdgcn_readfirstlane(gcl[c]);  // wave-uniform genome class
     const int rtop = c - uband;
@@ -365,7 +400,6 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
       mE[i] = ballot(valid[i] & eb[i]);
       mF[i] = ballot(valid[i] & fb);
       const int Hc = max(Hun[i], sat);
-      if (HST && k < W) hst[c * W + k] = (int16_t)Hc;
       // branch-free state update for the next column
       Hs[i] = valid[i] ? ((k == 0) ? Hun[i] : Hc) : ((r == 0) ? row0 : kNegInf32);
       E[i] = valid[i] ? En[i] : kNegInf32;
@@ -373,6 +407,50 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
       const bool cand = valid[i] & ((track == 1) | ((track == 2) & (r == rlen))) & (Hc > bv[i] - late);
       bv[i] = cand ? Hc : bv[i];
       bcol[i] = cand ? c : bcol[i];
+    }
+    if (CARRY) {
+      const BridgeCarry& B = *bc_;
+      const int cdi = __builtin_amdgcn_readfirstlane(B.coldi[c]);
+      const double cpc = B.colp[c];
+      // carried values arrive from band offset k+1 of the previous column
+      int ics[R], icc[R];
+      double icp[R];
+#pragma unroll
+      for (int i = 0; i < R - 1; i++) { ics[i] = cs[i + 1]; icc[i] = cc[i + 1]; icp[i] = cp[i + 1]; }
+      ics[R - 1] = dpp_wave_shl1(cs[0], 0);
+      icc[R - 1] = dpp_wave_shl1(cc[0], -1);
+      {
+        const int2 v = *reinterpret_cast<const int2*>(&cp[0]);
+        int2 w;
+        w.x = dpp_wave_shl1(v.x, 0);
+        w.y = dpp_wave_shl1(v.y, 0);
+        icp[R - 1] = *reinterpret_cast<const double*>(&w);
+      }
+#pragma unroll
+      for (int i = 0; i < R; i++) {
+        const int k = lane * R + i;
+        const int r = rtop + k;
+        const int other = rlen - r;
+        const bool inrow = (r >= 1) & (r <= rlen - 1) & (k < W);
+        const bool cand = inrow & (k >= 1) & valid[i] & (c <= glen - 2) & (c < B.rdist - other);
+        const int Hc = max(Hun[i], sat);
+        int s = 0;
+        double p = 0.0;
+        if (cand) {
+          s = B.isc[B.rowdi[other] & cdi] + Hc;
+          p = B.rowp[other] + cpc;
+        }
+        const bool take = cand & ((icc[i] < 0) | (s > ics[i]) | ((s == ics[i]) & (p > icp[i])));
+        cs[i] = take ? s : ics[i];
+        cc[i] = take ? c : icc[i];
+        cp[i] = take ? p : icp[i];
+        if (inrow && k == uband) B.diag[r] = Hc;  // matrix[r][r]
+        if (inrow && k == 0) {                    // the row leaves the band: its candidate is final
+          B.part[r].s = cs[i];
+          B.part[r].c = cc[i];
+          B.part[r].p = cp[i];
+        }
+      }
     }
     if (lane == 0) {  // one lane stores the column's 4R direction words
       uint64_t* dcol = dirs + (size_t)c * 4 * R;
@@ -382,6 +460,19 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
         dcol[1 * R + i] = mV[i];
         dcol[2 * R + i] = mE[i];
         dcol[3 * R + i] = mF[i];
+      }
+    }
+  }
+  if (CARRY) {  // rows still inside the band after the last column
+    const BridgeCarry& B = *bc_;
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+      const int k = lane * R + i;
+      const int r = glen - uband + k;
+      if (k < W && r >= 1 && r <= rlen - 1) {
+        B.part[r].s = cs[i];
+        B.part[r].c = cc[i];
+        B.part[r].p = cp[i];
       }
     }
   }
@@ -633,39 +724,35 @@ __global__ __launch_bounds__(64) void dp_kernel(
 
 // ===========================================================================
 // Dynprog_genome_gap (dynprog_genome.c:3288-3901), nosimd semantics, no
-// splicing IIT.  One wave per problem:
-//   1. genome_gap_simple (:3006) when !finalp && defect_rate < DEFECT_MEDQ:
-//      prefix sums of the two diagonals + one (score, rL) max-reduction;
-//   2. otherwise the R fill (reversed query vs rev_gsequenceR, lband = lbandL,
-//      !jump_late_p, :3810) then the L fill (:3801), both with the band-lane
-//      fill_band, each storing its matrix (int16, exact) for the bridge;
-//   3. bridge_intron_gap_site_level (:2469) with one lane per row rL: the
+// splicing IIT.  One workgroup of two waves per problem:
+//   1. genome_gap_simple (:3006) when !finalp && defect_rate < DEFECT_MEDQ
+//      (wave 0): prefix sums of the two diagonals + a (score, rL) max-reduction;
+//   2. otherwise the two fills run concurrently, wave 0 the R fill (reversed
+//      query vs rev_gsequenceR, lband = lbandL, !jump_late_p, :3810), wave 1 the
+//      L fill (:3801).  Each carries its side's bridge candidates along the band
+//      rows (BridgeCarry), so no score matrix is ever stored;
+//   3. bridge_intron_gap_site_level (:2469) on wave 0, one lane per row rL: the
 //      reference's sequential "> score, or == score and > prob" scan is a
-//      lexicographic max over (score, probL+probR, scan order), so each lane
-//      scans its rows' candidates in the reference order (A, B over cR, C over
-//      cL) and the rows are merged by a wave reduction;
+//      lexicographic max over (score, probL+probR, scan order), so each row's
+//      A, best B and best C are merged in scan order and the rows by a wave
+//      reduction;
 //   4. traceback R, List_reverse, gap holder, traceback L, Pair_maxnegscore.
 // ===========================================================================
 struct CarveGG {
-  size_t scL, scR, qL, qucL, qR, qucR, gchL, gclL, gchR, gclR, ldi, rdi, pL, pR, diagL, diagR, bpart, hst,
-      dirsL, dirsR, total;
+  size_t scL, scR, qL, qucL, qR, qucR, gchL, gclL, gchR, gclR, ldi, rdi, pL, pR, diagL, diagR, partB, partC, isc,
+      flag, dirsL, dirsR, total;
 };
 
-__host__ __device__ inline size_t gg_hst_bytes(int glengthL, int glengthR, int WL, int WR) {
-  const int g = glengthL > glengthR ? glengthL : glengthR;
-  const int W = WL > WR ? WL : WR;
-  return align16((size_t)(g + 1) * (size_t)W * 2u);
-}
 __host__ __device__ inline size_t gg_dirs_bytes(int glength, int R) { return (size_t)(glength + 1) * 4u * (size_t)R * 8u; }
 
-__host__ __device__ inline CarveGG carve_gg(int rlength, int glengthL, int glengthR, int R, int WL, int WR,
-                                            bool dirs_lds) {
+__host__ __device__ inline CarveGG carve_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds) {
   CarveGG cv;
   size_t off = 0;
   const size_t srow = (size_t)(rlength + 2);
   cv.pL = off;    off = align16(off + 8u * (size_t)glengthL);
   cv.pR = off;    off = align16(off + 8u * (size_t)glengthR);
-  cv.bpart = off; off = align16(off + 16u * (size_t)(rlength + 1));
+  cv.partB = off; off = align16(off + sizeof(Part) * (size_t)(rlength + 1));
+  cv.partC = off; off = align16(off + sizeof(Part) * (size_t)(rlength + 1));
   cv.diagL = off; off = align16(off + 4u * (size_t)(rlength + 1));
   cv.diagR = off; off = align16(off + 4u * (size_t)(rlength + 1));
   cv.scL = off;   off = align16(off + (size_t)kNClass * srow);
@@ -680,11 +767,12 @@ __host__ __device__ inline CarveGG carve_gg(int rlength, int glengthL, int gleng
   cv.gclR = off;  off = align16(off + (size_t)(glengthR + 2));
   cv.ldi = off;   off = align16(off + (size_t)(glengthL + 2));
   cv.rdi = off;   off = align16(off + (size_t)(glengthR + 2));
-  cv.hst = cv.dirsL = cv.dirsR = 0;
+  cv.isc = off;   off = align16(off + 64);
+  cv.flag = off;  off = align16(off + 4);
+  cv.dirsL = cv.dirsR = 0;
   if (dirs_lds) {
     cv.dirsL = off; off = align16(off + gg_dirs_bytes(glengthL, R));
     cv.dirsR = off; off = align16(off + gg_dirs_bytes(glengthR, R));
-    cv.hst = off;   off = off + gg_hst_bytes(glengthL, glengthR, WL, WR);
   }
   cv.total = off;
   return cv;
@@ -706,7 +794,7 @@ __device__ __forceinline__ uint8_t right_dinucl(char right2, char right1) {
   return 0;
 }
 
-// inclusive prefix sum across the wave
+// inclusive prefix sum / max across the wave
 __device__ __forceinline__ int wave_scan_add(int lane, int x) {
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -769,18 +857,12 @@ __device__ int wave_maxnegscore(int lane, const gmapdp_pair* out, int n) {
   return wave_min_i(worst);
 }
 
-struct BPart {  // best B candidate (indel on the right) of row rL, without matrixL[rL][rL]
-  double p;
-  int s;
-  int c;
-};
-
 __device__ __forceinline__ bool lex_better(int s1, double p1, int s2, double p2) {
   return s1 > s2 || (s1 == s2 && p1 > p2);
 }
 
 template <int R, bool DIRS_LDS>
-__global__ __launch_bounds__(64) void gg_kernel(
+__global__ __launch_bounds__(128) void gg_kernel(
     const DevGenomeProblem* __restrict__ probs, const int* __restrict__ order,
     const uint32_t* __restrict__ blocks, uint64_t nwords,
     const char* __restrict__ qseq, const char* __restrict__ qseq_uc, const double* __restrict__ sprob,
@@ -788,7 +870,9 @@ __global__ __launch_bounds__(64) void gg_kernel(
     gmapdp_genome_result* __restrict__ results, gmapdp_pair* __restrict__ pairs,
     unsigned char* __restrict__ gscratch) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int pid = order[blockIdx.x];
   const DevGenomeProblem P = probs[pid];
   const int rlen = P.rlength, gL = P.glengthL, gR = P.glengthR;
@@ -797,10 +881,11 @@ __global__ __launch_bounds__(64) void gg_kernel(
   const int late = (flags & kFLate) ? 1 : 0;
   const int lband = P.lbandL, ubandL = P.ubandL, ubandR = P.ubandR;
   const int WL = lband + ubandL + 1, WR = lband + ubandR + 1;
-  const CarveGG cv = carve_gg(rlen, gL, gR, R, WL, WR, DIRS_LDS);
+  const CarveGG cv = carve_gg(rlen, gL, gR, R, DIRS_LDS);
   double* pL = reinterpret_cast<double*>(smem + cv.pL);
   double* pR = reinterpret_cast<double*>(smem + cv.pR);
-  BPart* bpart = reinterpret_cast<BPart*>(smem + cv.bpart);
+  Part* partB = reinterpret_cast<Part*>(smem + cv.partB);  // indexed by rR
+  Part* partC = reinterpret_cast<Part*>(smem + cv.partC);  // indexed by rL
   int* diagL = reinterpret_cast<int*>(smem + cv.diagL);
   int* diagR = reinterpret_cast<int*>(smem + cv.diagR);
   int8_t* scL = reinterpret_cast<int8_t*>(smem + cv.scL);
@@ -815,11 +900,11 @@ __global__ __launch_bounds__(64) void gg_kernel(
   uint8_t* gclR = reinterpret_cast<uint8_t*>(smem + cv.gclR);
   uint8_t* ldi = reinterpret_cast<uint8_t*>(smem + cv.ldi);
   uint8_t* rdi = reinterpret_cast<uint8_t*>(smem + cv.rdi);
+  int8_t* isc = reinterpret_cast<int8_t*>(smem + cv.isc);
+  int* done = reinterpret_cast<int*>(smem + cv.flag);
   unsigned char* gbase = gscratch + P.dirs_offset;
   uint64_t* dirsL = reinterpret_cast<uint64_t*>(DIRS_LDS ? smem + cv.dirsL : gbase);
   uint64_t* dirsR = reinterpret_cast<uint64_t*>(DIRS_LDS ? smem + cv.dirsR : gbase + align16(gg_dirs_bytes(gL, R)));
-  int16_t* hst = reinterpret_cast<int16_t*>(
-      DIRS_LDS ? smem + cv.hst : gbase + align16(gg_dirs_bytes(gL, R)) + align16(gg_dirs_bytes(gR, R)));
   const int8_t* sct = sctab + (size_t)P.mismatchtype * 128 * kNClass;
   const uint8_t* cons = constab + (size_t)P.genestrand * 128 * kNClass;
   gmapdp_pair* out = pairs + P.pair_offset;
@@ -827,10 +912,11 @@ __global__ __launch_bounds__(64) void gg_kernel(
   const Geo GL{P.roffset, P.goffsetL, 1};
   const Geo GR{rev_roffset, P.rev_goffsetR, -1};
   const int srow = rlen + 2;
+  const bool halfp = flags & kGHalf;
 
-  // ---- stage: query in both DP orders with per-class score rows, both genome segments,
-  //      dinucleotide codes and the splice probabilities ----
-  for (int i = lane; i < rlen; i += 64) {
+  // ---- stage (both waves): query in both DP orders with per-class score rows, both genome
+  //      segments, dinucleotide codes, the splice probabilities and the intron score array ----
+  for (int i = tid; i < rlen; i += 128) {
     const char c1 = qseq[P.qbase + i];
     const char c1u = qseq_uc[P.qbase + i];
     qL[i + 1] = c1;
@@ -844,28 +930,30 @@ __global__ __launch_bounds__(64) void gg_kernel(
       scR[g * srow + rlen - i] = (int8_t)(row >> (8 * g));
     }
   }
-  if (lane < 6) {
-    scL[lane * srow] = scR[lane * srow] = 0;
-    scL[lane * srow + rlen + 1] = scR[lane * srow + rlen + 1] = 0;
+  if (tid < 6) {
+    scL[tid * srow] = scR[tid * srow] = 0;
+    scL[tid * srow + rlen + 1] = scR[tid * srow + rlen + 1] = 0;
   }
-  for (int i = lane; i < gL; i += 64) {
+  for (int i = tid; i < gL; i += 128) {
     const char c2 = segment_nt(blocks, nwords, (uint32_t)i, (uint32_t)gL, P.segposL, P.segboundL,
                                flags & kGSegLLeft, flags & kGSegLRc);
     gchL[i + 1] = c2;
     gclL[i + 1] = gclass(c2);
     pL[i] = sprob[P.prob_offset + i];
   }
-  for (int i = lane; i < gR; i += 64) {
+  for (int i = tid; i < gR; i += 128) {
     const char c2 = segment_nt(blocks, nwords, (uint32_t)i, (uint32_t)gR, P.segposR, P.segboundR,
                                flags & kGSegRLeft, flags & kGSegRRc);
     gchR[gR - i] = c2;  // rev_gsequenceR[1-c] = segment[glengthR-c]
     gclR[gR - i] = gclass(c2);
     pR[i] = sprob[P.prob_offset + gL + i];
   }
+  if (tid < 64) isc[tid] = isctab[(size_t)P.iclass * 128 + ((flags & kGFinal) ? 64 : 0) + tid];
+  if (tid == 0) *done = 0;
   __syncthreads();
   // leftdi[cL] from gsequenceL[cL], [cL+1]; rightdi[cR] from rev_gsequenceR[-cR-1], [-cR] (:2518-2566)
-  for (int c = lane; c <= gL; c += 64) ldi[c] = (c < gL - 1) ? left_dinucl(gchL[c + 1], gchL[c + 2]) : 0;
-  for (int c = lane; c <= gR; c += 64) rdi[c] = (c < gR - 1) ? right_dinucl(gchR[c + 2], gchR[c + 1]) : 0;
+  for (int c = tid; c <= gL; c += 128) ldi[c] = (c < gL - 1) ? left_dinucl(gchL[c + 1], gchL[c + 2]) : 0;
+  for (int c = tid; c <= gR; c += 128) rdi[c] = (c < gR - 1) ? right_dinucl(gchR[c + 2], gchR[c + 1]) : 0;
   __syncthreads();
 
   gmapdp_genome_result res;
@@ -880,116 +968,100 @@ __global__ __launch_bounds__(64) void gg_kernel(
   res.gap_queryjump = 0;
   res.left_prob = res.right_prob = 0.0;
   const int dpi_next = P.dynprogindex + (P.dynprogindex > 0 ? 1 : -1);
-  const bool halfp = flags & kGHalf;
 
-  // ---- 1. genome_gap_simple (dynprog_genome.c:3006-3280) ----
+  // ---- 1. genome_gap_simple (dynprog_genome.c:3006-3280), wave 0 ----
   if (flags & kGSimple) {
-    const int8_t* isc = isctab + (size_t)P.iclass * 128;  // prelim array (:3032)
-    // diagL[r] / diagR[r] hold the prefix sums scoreL(r) / scoreR(r) of the two diagonals
-    int carryL = 0, carryR = 0;
-    for (int base = 0; base < rlen; base += 64) {
-      const int r = base + lane + 1;
-      int vL = 0, vR = 0;
-      if (r <= rlen - 1) {
-        vL = sct[(uint8_t)(qucL[r] & 127) * kNClass + gclL[r]];
-        vR = sct[(uint8_t)(qucR[r] & 127) * kNClass + gclR[r]];
+    const int8_t* iscp = isctab + (size_t)P.iclass * 128;  // prelim array (:3032)
+    if (wave == 0) {
+      // diagL[r] / diagR[r] hold the prefix sums scoreL(r) / scoreR(r) of the two diagonals
+      int carryL = 0, carryR = 0;
+      for (int base = 0; base < rlen; base += 64) {
+        const int r = base + lane + 1;
+        int vL = 0, vR = 0;
+        if (r <= rlen - 1) {
+          vL = sct[(uint8_t)(qucL[r] & 127) * kNClass + gclL[r]];
+          vR = sct[(uint8_t)(qucR[r] & 127) * kNClass + gclR[r]];
+        }
+        const int sL = carryL + wave_scan_add(lane, vL), sR = carryR + wave_scan_add(lane, vR);
+        if (r <= rlen - 1) {
+          diagL[r] = sL;
+          diagR[r] = sR;
+        }
+        carryL = __shfl(sL, 63, 64);
+        carryR = __shfl(sR, 63, 64);
       }
-      const int sL = carryL + wave_scan_add(lane, vL), sR = carryR + wave_scan_add(lane, vR);
-      if (r <= rlen - 1) {
-        diagL[r] = sL;
-        diagR[r] = sR;
-      }
-      carryL = __shfl(sL, 63, 64);
-      carryR = __shfl(sR, 63, 64);
     }
     __syncthreads();
-    // best: max score >= 0 among canonical-type sites, ties -> largest rL ("Use >= for jump late")
-    uint64_t key = 0;
-    for (int rL = lane + 1; rL <= rlen - 1; rL += 64) {
-      const int rR = rlen - rL;
-      const int it = ldi[rL] & rdi[rR];
-      const int score = diagL[rL] + isc[it] + diagR[rR];
-      if (it != 0 && score >= 0) {
-        const uint64_t kk = ((uint64_t)(uint32_t)score << 32) | (uint32_t)rL;
-        key = kk > key ? kk : key;
+    if (wave == 0) {
+      // best: max score >= 0 among intron-type sites, ties -> largest rL ("Use >= for jump late")
+      uint64_t key = 0;
+      for (int rL = lane + 1; rL <= rlen - 1; rL += 64) {
+        const int rR = rlen - rL;
+        const int it = ldi[rL] & rdi[rR];
+        const int score = diagL[rL] + iscp[it] + diagR[rR];
+        if (it != 0 && score >= 0) {
+          const uint64_t kk = ((uint64_t)(uint32_t)score << 32) | (uint32_t)rL;
+          key = kk > key ? kk : key;
+        }
       }
-    }
-    key = wave_max_u64(key);
-    if (key != 0) {
-      const int bestrL = (int)(key & 0xffffffffu), bestscore = (int)(key >> 32), bestrR = rlen - bestrL;
-      const int it = ldi[bestrL] & rdi[bestrR];
-      const int scoreI = isc[it];
-      res.introntype = it;
-      const int finalscore = halfp ? bestscore - scoreI / 2 : bestscore;
-      if (finalscore > 0) {
-        res.left_prob = pL[bestrL];
-        res.right_prob = pR[bestrR];
-        if (res.left_prob >= 0.90 && res.right_prob >= 0.90) {
-          Tally t = {0, 0, 0, 0, 0, 0, 0, false};
-          // list = reverse of the push order (no List_reverse): R diagonal r = 1..bestrR, gap, L r = bestrL..1
-          emit_diag(lane, bestrR, bestrR, bestrR, GR, qR, qucR, gchR, cons, out, t);
-          const int nR = t.count;
-          reverse_records(lane, out, nR);
-          const int new_left = P.goffsetL + (bestrL - 1);
-          const int new_right = P.rev_goffsetR - (bestrR - 1);
-          if (lane == 0) put_pair(out, nR, -1, -1, new_right - new_left - 1, ' ', ' ', ' ', ' ');
-          t.count += 1;
-          emit_diag(lane, bestrL, bestrL, bestrL, GL, qL, qucL, gchL, cons, out, t);
-          if (lane == 0) {
-            res.npairs = t.count;
-            res.traceback_score = t.nmatches * kMatch + t.nmismatches * kMismatch;
-            res.nmatches = t.nmatches;
-            res.nmismatches = t.nmismatches;
-            res.dynprogindex = dpi_next;
-            res.new_leftgenomepos = new_left;
-            res.new_rightgenomepos = res.exonhead = new_right;
-            res.gap_index = nR;
-            res.gap_queryjump = 0;
-            results[pid] = res;
+      key = wave_max_u64(key);
+      if (key != 0) {
+        const int bestrL = (int)(key & 0xffffffffu), bestscore = (int)(key >> 32), bestrR = rlen - bestrL;
+        const int it = ldi[bestrL] & rdi[bestrR];
+        const int scoreI = iscp[it];
+        res.introntype = it;
+        const int finalscore = halfp ? bestscore - scoreI / 2 : bestscore;
+        if (finalscore > 0) {
+          res.left_prob = pL[bestrL];
+          res.right_prob = pR[bestrR];
+          if (res.left_prob >= 0.90 && res.right_prob >= 0.90) {
+            Tally t = {0, 0, 0, 0, 0, 0, 0, false};
+            // list = reverse of the push order (no List_reverse): R diagonal r = 1..bestrR, gap, L r = bestrL..1
+            emit_diag(lane, bestrR, bestrR, bestrR, GR, qR, qucR, gchR, cons, out, t);
+            const int nR = t.count;
+            reverse_records(lane, out, nR);
+            const int new_left = P.goffsetL + (bestrL - 1);
+            const int new_right = P.rev_goffsetR - (bestrR - 1);
+            if (lane == 0) put_pair(out, nR, -1, -1, new_right - new_left - 1, ' ', ' ', ' ', ' ');
+            t.count += 1;
+            emit_diag(lane, bestrL, bestrL, bestrL, GL, qL, qucL, gchL, cons, out, t);
+            if (lane == 0) {
+              res.npairs = t.count;
+              res.traceback_score = t.nmatches * kMatch + t.nmismatches * kMismatch;
+              res.nmatches = t.nmatches;
+              res.nmismatches = t.nmismatches;
+              res.dynprogindex = dpi_next;
+              res.new_leftgenomepos = new_left;
+              res.new_rightgenomepos = res.exonhead = new_right;
+              res.gap_index = nR;
+              res.gap_queryjump = 0;
+              results[pid] = res;
+              *done = 1;
+            }
           }
-          return;
         }
       }
     }
     __syncthreads();
+    if (*done) return;
   }
 
-  // ---- 2. fills: R first (its matrix feeds the B candidates), then L ----
-  const int8_t* isc = isctab + (size_t)P.iclass * 128 + ((flags & kGFinal) ? 64 : 0);
-  const int eb = lband;  // bridge_intron_gap: lbandL = lbandR = extraband_paired, uband = glength - rlength + eb
+  // ---- 2. fills, concurrently: wave 0 R (feeds the B candidates), wave 1 L (the C candidates) ----
   const int rdist = P.rev_goffsetR - P.goffsetL;  // "cR < rightoffset - leftoffset - cL"
-  int br, bc;
-  fill_band<R, true>(lane, rlen, gR, lband, ubandR, P.open, P.extend, 1 - late, 0, scR, srow, gclR, dirsR, hst,
-                     br, bc);
-  if (DIRS_LDS) __syncthreads();
-  else __threadfence_block();
-  for (int r = lane + 1; r <= rlen - 1; r += 64) diagR[r] = hst[r * WR + ubandR];
-  // B: row rL, cL = rL, cR over [max(1, rR - eb), min(rR + ubandR, gR - 1)) in scan order
-  for (int rL = lane + 1; rL <= rlen - 1; rL += 64) {
-    const int rR = rlen - rL;
-    const int ld = ldi[rL];
-    const double pl = pL[rL];
-    const int clo = max(1, rR - eb);
-    const int chi = min(min(rR + ubandR, gR - 1), rdist - rL);
-    int bs = 0, bcR = -1;
-    double bp = 0.0;
-    for (int cR = clo; cR < chi; cR++) {
-      const int s = isc[ld & rdi[cR]] + hst[cR * WR + (rR - cR + ubandR)];
-      const double p = pl + pR[cR];
-      if (bcR < 0 || lex_better(s, p, bs, bp)) {
-        bs = s;
-        bp = p;
-        bcR = cR;
-      }
+  {
+    int br, bc;
+    if (wave == 0) {
+      const BridgeCarry B{ldi, rdi, pL, pR, isc, rdist, partB, diagR};
+      fill_band<R, true>(lane, rlen, gR, lband, ubandR, P.open, P.extend, 1 - late, 0, scR, srow, gclR, dirsR, &B,
+                         br, bc);
+    } else {
+      const BridgeCarry B{rdi, ldi, pR, pL, isc, rdist, partC, diagL};
+      fill_band<R, true>(lane, rlen, gL, lband, ubandL, P.open, P.extend, late, 0, scL, srow, gclL, dirsL, &B,
+                         br, bc);
     }
-    bpart[rL].p = bp;
-    bpart[rL].s = bs;
-    bpart[rL].c = bcR;
   }
   __syncthreads();
-  fill_band<R, true>(lane, rlen, gL, lband, ubandL, P.open, P.extend, late, 0, scL, srow, gclL, dirsL, hst, br, bc);
-  if (DIRS_LDS) __syncthreads();
-  else __threadfence_block();
+  if (wave != 0) return;
 
   // ---- 3. bridge: per-lane scan of rows rL = lane+1, lane+65, ... (A, B, C per row) ----
   int ws = kNegInf32, wrL = -1, wcL = 0, wcR = 0;  // (NEG_INFINITY_32, 0.0) is the reference's initial state
@@ -998,9 +1070,7 @@ __global__ __launch_bounds__(64) void gg_kernel(
   double dp = 0.0;
   for (int rL = lane + 1; rL <= rlen - 1; rL += 64) {
     const int rR = rlen - rL;
-    const int dL = hst[rL * WL + ubandL];
-    diagL[rL] = dL;
-    const int dR = diagR[rR];
+    const int dL = diagL[rL], dR = diagR[rR];
     // A: cL = rL, cR = rR
     const int sI = isc[ldi[rL] & rdi[rR]];
     int rs = dL + sI + dR, rcL = rL, rcR = rR;
@@ -1010,28 +1080,21 @@ __global__ __launch_bounds__(64) void gg_kernel(
       ds = rs;
       drL = rL;
     }
-    // B
-    const BPart b = bpart[rL];
+    // B: cL = rL, best cR of R row rR (+ matrixL[rL][rL])
+    const Part b = partB[rR];
     if (b.c >= 0 && lex_better(dL + b.s, b.p, rs, rp)) {
       rs = dL + b.s;
       rp = b.p;
       rcL = rL;
       rcR = b.c;
     }
-    // C: cR = rR, cL over [max(1, rL - eb), min(rL + ubandL, gL - 1))
-    const int rd = rdi[rR];
-    const double pr = pR[rR];
-    const int clo = max(1, rL - eb);
-    const int chi = min(min(rL + ubandL, gL - 1), rdist - rR);
-    for (int cL = clo; cL < chi; cL++) {
-      const int s = hst[cL * WL + (rL - cL + ubandL)] + isc[ldi[cL] & rd] + dR;
-      const double p = pL[cL] + pr;
-      if (lex_better(s, p, rs, rp)) {
-        rs = s;
-        rp = p;
-        rcL = cL;
-        rcR = rR;
-      }
+    // C: cR = rR, best cL of L row rL (+ matrixR[rR][rR])
+    const Part cpart = partC[rL];
+    if (cpart.c >= 0 && lex_better(dR + cpart.s, cpart.p, rs, rp)) {
+      rs = dR + cpart.s;
+      rp = cpart.p;
+      rcL = cpart.c;
+      rcR = rR;
     }
     if (lex_better(rs, rp, ws, wp)) {  // later rows replace only when strictly better
       ws = rs;
@@ -1180,12 +1243,11 @@ hipError_t launch_dp(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
 template <int R, bool D>
 static void* gptr() { return reinterpret_cast<void*>(&gg_kernel<R, D>); }
 
-size_t lds_bytes_gg(int rlength, int glengthL, int glengthR, int R, int WL, int WR, bool dirs_lds) {
-  return carve_gg(rlength, glengthL, glengthR, R, WL, WR, dirs_lds).total;
+size_t lds_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds) {
+  return carve_gg(rlength, glengthL, glengthR, R, dirs_lds).total;
 }
-size_t scratch_bytes_gg(int glengthL, int glengthR, int R, int WL, int WR) {
-  return align16(gg_dirs_bytes(glengthL, R)) + align16(gg_dirs_bytes(glengthR, R)) +
-         gg_hst_bytes(glengthL, glengthR, WL, WR);
+size_t scratch_bytes_gg(int glengthL, int glengthR, int R) {
+  return align16(gg_dirs_bytes(glengthL, R)) + align16(gg_dirs_bytes(glengthR, R));
 }
 
 hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevGenomeProblem* probs,
@@ -1216,7 +1278,7 @@ hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
   void* args[] = {(void*)&probs, (void*)&order, (void*)&blocks, (void*)&nwords, (void*)&qseq, (void*)&qseq_uc,
                   (void*)&sprob, (void*)&sctab, (void*)&constab, (void*)&isctab, (void*)&results, (void*)&pairs,
                   (void*)&gscratch};
-  return hipLaunchKernel(fn, dim3(nblocks), dim3(64), args, lds, stream);
+  return hipLaunchKernel(fn, dim3(nblocks), dim3(128), args, lds, stream);
 }
 
 }  // namespace gmapdp

@@ -28,8 +28,8 @@ hipError_t launch_dp(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
                      const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
                      const char* qseq_uc, const int8_t* sctab, const uint8_t* constab, gmapdp_result* results,
                      gmapdp_pair* pairs, uint64_t* gdirs);
-size_t lds_bytes_gg(int rlength, int glengthL, int glengthR, int R, int WL, int WR, bool dirs_lds);
-size_t scratch_bytes_gg(int glengthL, int glengthR, int R, int WL, int WR);
+size_t lds_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds);
+size_t scratch_bytes_gg(int glengthL, int glengthR, int R);
 hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevGenomeProblem* probs,
                      const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
                      const char* qseq_uc, const double* sprob, const int8_t* sctab, const uint8_t* constab,
@@ -599,13 +599,13 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     const int WL = d.lbandL + d.ubandL + 1, WR = d.lbandL + d.ubandR + 1;
     const int R = pick_R(std::max(WL, WR));
     if (R > kMaxR) return bad(ctx, "band wider than 4096");
-    size_t lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, WL, WR, true);
+    size_t lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, true);
     const bool dirs_lds = lds <= kLdsBudget;
     d.dirs_offset = 0;
     if (!dirs_lds) {
-      lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, WL, WR, false);
+      lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, false);
       d.dirs_offset = (int64_t)gdirs_off;
-      gdirs_off += (scratch_bytes_gg(d.glengthL, d.glengthR, R, WL, WR) + 255) & ~(size_t)255;
+      gdirs_off += (scratch_bytes_gg(d.glengthL, d.glengthR, R) + 255) & ~(size_t)255;
     }
     if (lds > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
     classes[std::make_tuple((int)PlanCore::kGenomeGap, R, dirs_lds ? 1 : 0, lds_bucket(lds))].push_back((int)s);
