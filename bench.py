@@ -148,19 +148,22 @@ def make_end(genome, n5, n3, rng):
     return probs, q
 
 
-def make_genome_gaps(genome, n, rng):
+def make_genome_gaps(genome, n, rng, site_seed=23):
     """Vectorised Dynprog_genome_gap sub-problems (stage3.c:9504-9539): a query gap of rlength
     nt = a exonic nt before a planted GT..AG intron + b after it; goffsetL = first genomic
     position after the left anchor, rev_goffsetR = last one before the right anchor,
-    glengthL = glengthR = rlength + 8.  Plants the dinucleotides into `genome` (in place)."""
+    glengthL = glengthR = rlength + 8.  Plants the dinucleotides into `genome` (in place) at
+    sites drawn from `site_seed`, so every rank builds the same genome; call it before the
+    other sub-problems are cut from the genome."""
     import gmapdp
     glen = len(genome)
-    r = np.clip(rng.gamma(2.2, 50.0, size=n).astype(np.int64), 2, 600)
-    a = (rng.random(n) * (r + 1)).astype(np.int64)
+    srng = np.random.default_rng(site_seed)
+    r = np.clip(srng.gamma(2.2, 50.0, size=n).astype(np.int64), 2, 600)
+    a = (srng.random(n) * (r + 1)).astype(np.int64)
     b = r - a
-    intron = rng.integers(60, 5000, size=n)
-    watson = rng.random(n) < 0.5
-    goffL = rng.integers(100, glen - 7000, size=n)
+    intron = srng.integers(60, 5000, size=n)
+    watson = srng.random(n) < 0.5
+    goffL = srng.integers(100, glen - 7000, size=n)
     revR = goffL + a + intron + b - 1
     x, y = goffL + a, revR - b            # first / last intron base, strand coordinates
     # strand coordinate p -> genome index: watson p, minus glen - p (complemented)
@@ -217,6 +220,17 @@ def algorithmic_bytes(rlength, glength, npairs, desc_bytes):
     r = np.asarray(rlength, dtype=np.int64)
     g = np.asarray(glength, dtype=np.int64)
     return int((desc_bytes + 2 * r + 12 * ((g + 62) // 32) + 32).sum() + 16 * int(np.asarray(npairs).sum()))
+
+
+def genome_algorithmic_bytes(gp, npairs):
+    """Dynprog_genome_gap: descriptor (80 B) + query and upper-cased query (2 x rlength) + the
+    packed genome blocks of both segments + 8-B splice probability per column of both
+    segments + result (72 B) + one 16-B record per emitted pair."""
+    r = gp["rlength"].astype(np.int64)
+    gL = gp["glengthL"].astype(np.int64)
+    gR = gp["glengthR"].astype(np.int64)
+    return int((80 + 2 * r + 12 * ((gL + 62) // 32) + 12 * ((gR + 62) // 32) + 8 * (gL + gR) + 72).sum()
+               + 16 * int(np.asarray(npairs).sum()))
 
 
 def banded_cells(sp, ep):
@@ -319,12 +333,12 @@ def main():
     dev = torch.device("cuda", local)
 
     genome = make_genome()
+    rng_g = np.random.default_rng(2000 + rank)
+    ng = int(round(args.reads * GENOME_PER_READ))
+    gp, gq, sprob = make_genome_gaps(genome, ng, rng_g)   # plants intron motifs into the genome first
     sp, ep, q = make_workload(genome, args.reads, seed=1000 + rank)
     ns, ne = len(sp), len(ep)
     nprob = ns + ne
-    rng_g = np.random.default_rng(2000 + rank)
-    ng = int(round(args.reads * GENOME_PER_READ))
-    gp, gq, sprob = make_genome_gaps(genome, ng, rng_g)   # plants intron motifs: before set_genome
     gp["qoff"] += len(q)
     q_all = np.concatenate([q, gq])
 
@@ -376,6 +390,7 @@ def main():
                        "gmapdp_plan_run_launch")
 
         def step(ev=None):
+            # per-dispatch events on the stream each launch runs on (what rocprofv3's kernel trace times)
             fork = torch.cuda.Event()
             fork.record(stream)
             used = 0
@@ -383,7 +398,11 @@ def main():
                 if tail[li]:
                     s = sides[used % len(sides)]
                     s.wait_event(fork)
+                    if ev is not None:
+                        ev[li][0].record(s)
                     launch(li, s)
+                    if ev is not None:
+                        ev[li][1].record(s)
                     used += 1
             for li in range(nl):
                 if tail[li]:
@@ -415,45 +434,50 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        launch_ms = [None if tail[li] else
-                     sum(evs[k][li][0].elapsed_time(evs[k][li][1]) for k in range(steps)) / steps
+        launch_ms = [sum(evs[k][li][0].elapsed_time(evs[k][li][1]) for k in range(steps)) / steps
                      for li in range(nl)]
         return float(t.item()), launch_ms
 
     # ---- headline: configs[1] (Dynprog_single_gap + Dynprog_end{5,3}_gap) ----
     P = build(False)
     plan, nl, info, tail, ngpu = P["plan"], P["nl"], P["info"], P["tail"], P["ngpu"]
-    # the kernel template each launch runs; the dominant kernel is the template with most problems
-    kname = ["dp_kernel<R=%d,dirs_lds=%d>" % (i[0], i[1]) for i in info]
-    per_kernel = {}
-    for li in range(nl):
-        if not tail[li]:
-            per_kernel.setdefault(kname[li], []).append(li)
-    dominant = max(per_kernel, key=lambda k: sum(info[li][2] for li in per_kernel[k]))
     elapsed, launch_ms = timed(P, args.steps, args.warmup)
-
-    # results of the last pass (for algorithmic byte accounting)
-    res = np.frombuffer(P["d_res"].cpu().numpy().tobytes(), dtype=gmapdp.RESULT_DTYPE)[:ngpu]
-    dev_index = np.array([lib.gmapdp_plan_dev_index(plan, i) for i in range(nprob)])
-    gpu_mask = dev_index >= 0
-    npairs = np.zeros(nprob, dtype=np.int64)
-    npairs[gpu_mask] = res["npairs"][dev_index[gpu_mask]]
     rl = np.concatenate([sp["rlength"], np.minimum(ep["rlength"], 660)]).astype(np.int64)
     gl = np.concatenate([sp["glength"], np.minimum(ep["glength"], 2000)]).astype(np.int64)
     desc = np.concatenate([np.full(ns, 56), np.full(ne, 64)])
-    dom_launches = per_kernel[dominant]
-    dom_bytes_total = 0
-    for li in dom_launches:
-        m = np.zeros(info[li][2], dtype=np.int32)
-        lib.gmapdp_plan_launch_members(plan, li, m.ctypes.data)
-        dom_bytes_total += algorithmic_bytes(rl[m], gl[m], npairs[m], desc[m])
-    dom_ms = sum(launch_ms[li] for li in dom_launches) / len(dom_launches)   # average dispatch duration
-    dom_bytes = dom_bytes_total / len(dom_launches)                          # average bytes per dispatch
-    g_idx = np.nonzero(gpu_mask)[0]
-    step_bytes = algorithmic_bytes(rl[g_idx], gl[g_idx], npairs[g_idx], desc[g_idx])
-    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    cells = banded_cells(sp, ep)
 
+    def dispatches(PP, lms, steps):
+        """(kernel template, algorithmic bytes, ms, count) of every timed dispatch of a plan."""
+        plan_, info_ = PP["plan"], PP["info"]
+        res_ = np.frombuffer(PP["d_res"].cpu().numpy().tobytes(), dtype=gmapdp.RESULT_DTYPE)[:PP["ngpu"]]
+        gres_ = np.frombuffer(PP["d_gres"].cpu().numpy().tobytes(), dtype=gmapdp.GENOME_RESULT_DTYPE)[:PP["nggpu"]]
+        dev_index = np.array([lib.gmapdp_plan_dev_index(plan_, i) for i in range(nprob)])
+        npairs = np.zeros(nprob, dtype=np.int64)
+        npairs[dev_index >= 0] = res_["npairs"][dev_index[dev_index >= 0]]
+        out_ = []
+        for li in range(PP["nl"]):
+            m = np.zeros(info_[li][2], dtype=np.int32)
+            lib.gmapdp_plan_launch_members(plan_, li, m.ctypes.data)
+            if PP["kind"][li] == 0:
+                name = "dp_kernel<R=%d,dirs_lds=%d>" % (info_[li][0], info_[li][1])
+                nbytes = algorithmic_bytes(rl[m], gl[m], npairs[m], desc[m])
+            else:
+                name = "gg_kernel<R=%d,dirs_lds=%d>" % (info_[li][0], info_[li][1])
+                j = m - nprob
+                gi = np.array([lib.gmapdp_plan_genome_dev_index(plan_, int(x)) for x in j])
+                nbytes = genome_algorithmic_bytes(gp[j], gres_["npairs"][gi])
+            out_.append((name, nbytes, lms[li], steps, info_[li][2]))
+        return out_
+
+    disp = dispatches(P, launch_ms, args.steps)
+    cells = banded_cells(sp, ep)
+    step_bytes = sum(d[1] for d in disp)
+    counts = {}
+    for name, _, _, _, cnt in disp:
+        counts[name] = counts.get(name, 0) + cnt
+    dominant = max(counts, key=counts.get)   # the kernel template that processes the most problems
+    lib.gmapdp_plan_destroy(plan)
+    del P
     reads_total = args.reads * world * args.steps
     value = reads_total / elapsed
     out = {
@@ -478,22 +502,34 @@ def main():
                    "parallelism": "dp%d (reads sharded by rank, genome replicated)" % world,
                    "launch_classes": info},
         "gcups": cells * world * args.steps / elapsed / 1e9,
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": dominant, "dispatches_per_step": len(dom_launches),
-                     "kernel_ms_per_launch": dom_ms, "algorithmic_bytes_per_launch": dom_bytes,
-                     "launch_ms": launch_ms,
-                     "note": "integer VALU/LDS-bound DP; HBM roofline reported as required (DESIGN.md)"},
         "step_algorithmic_bytes": step_bytes,
     }
-    lib.gmapdp_plan_destroy(plan)
-    del P
 
     # ---- all Dynprog_* paths: + Dynprog_genome_gap ----
     PA = build(True)
     gsteps = max(1, args.steps // 2)
     elapsed_all, launch_ms_all = timed(PA, gsteps, max(1, args.warmup // 2))
+    disp_all = dispatches(PA, launch_ms_all, gsteps)
     gk = [li for li in range(PA["nl"]) if PA["kind"][li] == 1]
+
+    def roofline(name, dl):
+        """Average algorithmic bytes / average duration over every timed dispatch of one kernel
+        template (both phases) -- the quantity rocprofv3 --stats averages per kernel name."""
+        sel = [d for d in dl if d[0] == name]
+        n = sum(d[3] for d in sel)
+        ms = sum(d[2] * d[3] for d in sel) / n
+        nbytes = sum(d[1] * d[3] for d in sel) / n
+        ach = nbytes / (ms * 1e-3) / 1e9
+        return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                "traffic": None, "kernel": name, "dispatches": n, "kernel_ms_per_launch": ms,
+                "algorithmic_bytes_per_launch": nbytes,
+                "note": "integer VALU/LDS-bound DP; HBM roofline reported as required (DESIGN.md)"}
+
+    out["roofline"] = roofline(dominant, disp + disp_all)
+    gcount = {}
+    for d in disp_all:
+        if d[0].startswith("gg_"):
+            gcount[d[0]] = gcount.get(d[0], 0) + d[4]
     gr = gp["rlength"].astype(np.int64)
     gcells = int((2 * np.minimum(8 + 2 * 14 + 1, gr + 1) * (gr + 8)).sum())  # two fills, band W = 37
     out["all_dynprog"] = {
@@ -502,7 +538,8 @@ def main():
         "genome_gap_calls_per_read": GENOME_PER_READ, "genome_gap_subproblems_per_step_per_gpu": ng,
         "gcups": (cells + gcells) * world * gsteps / elapsed_all / 1e9,
         "genome_gap_launch_classes": [PA["info"][li] for li in gk],
-        "genome_gap_bulk_launch_ms": [launch_ms_all[li] for li in gk if launch_ms_all[li] is not None],
+        "genome_gap_launch_ms": [launch_ms_all[li] for li in gk],
+        "roofline_genome_gap": roofline(max(gcount, key=gcount.get), disp_all),
         "splice_probabilities": "synthetic host input (0.95 at planted GT-AG sites, U[0,0.3) elsewhere)"}
     lib.gmapdp_plan_destroy(PA["plan"])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
