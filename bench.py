@@ -27,6 +27,7 @@ import argparse
 import ctypes as C
 import json
 import os
+import re
 import sys
 import time
 
@@ -220,6 +221,25 @@ def algorithmic_bytes(rlength, glength, npairs, desc_bytes):
     r = np.asarray(rlength, dtype=np.int64)
     g = np.asarray(glength, dtype=np.int64)
     return int((desc_bytes + 2 * r + 12 * ((g + 62) // 32) + 32).sum() + 16 * int(np.asarray(npairs).sum()))
+
+
+def pmc_traffic(name):
+    """HBM bytes per dispatch of kernel template `name` from the newest committed rocprofv3 PMC
+    summary (profiles/*/pmc_summary.json: 2 x FETCH_SIZE + WRITE_SIZE of the same bench command,
+    per MI355X_MICROARCH.md's gfx950 correction), or (None, None)."""
+    import glob
+    m = re.match(r"(\w+)<R=(\d+),dirs_lds=(\d)>", name)
+    if not m:
+        return None, None
+    key = "gmapdp::%s<%s, %s>" % (m.group(1), m.group(2), "true" if m.group(3) == "1" else "false")
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")), reverse=True):
+        try:
+            k = json.load(open(path))["kernels"].get(key)
+        except (OSError, ValueError, KeyError):
+            continue
+        if k:
+            return k["hbm_bytes_per_dispatch"], os.path.relpath(path, ROOT)
+    return None, None
 
 
 def genome_algorithmic_bytes(gp, npairs):
@@ -520,8 +540,10 @@ def main():
         ms = sum(d[2] * d[3] for d in sel) / n
         nbytes = sum(d[1] * d[3] for d in sel) / n
         ach = nbytes / (ms * 1e-3) / 1e9
+        traffic, src = pmc_traffic(name)
         return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                "traffic": None, "kernel": name, "dispatches": n, "kernel_ms_per_launch": ms,
+                "traffic": traffic, "traffic_source": src, "kernel": name, "dispatches": n,
+                "kernel_ms_per_launch": ms,
                 "algorithmic_bytes_per_launch": nbytes,
                 "note": "integer VALU/LDS-bound DP; HBM roofline reported as required (DESIGN.md)"}
 
