@@ -1,0 +1,378 @@
+/* gmapdp_gmap_shim.c -- drop-in for GMAP's Dynprog_* entry points on the MI355X engine.
+ *
+ * Compiled INSIDE a GMAP build (against GMAP's own headers, -DHAVE_CONFIG_H)
+ * and linked with
+ *
+ *   -Wl,--wrap=Dynprog_init,--wrap=Dynprog_single_setup,--wrap=Dynprog_end_setup,
+ *   -Wl,--wrap=Dynprog_genome_setup,--wrap=Dynprog_single_gap,--wrap=Dynprog_end5_gap,
+ *   -Wl,--wrap=Dynprog_end3_gap,--wrap=Dynprog_genome_gap  -lgmapdp
+ *
+ * so that every call GMAP's stage 3 makes to these functions (stage3.c:9510,
+ * 9531, 10244-10600, ...) lands here with the reference's own signature
+ * (dynprog_single.h:22, dynprog_end.h:25/47, dynprog_genome.h:24) and returns
+ * the reference's List_T of Pair_T built in the caller's Pairpool
+ * (Pairpool_push / Pairpool_push_gapholder, pairpool.c:180/375).  The setup
+ * functions are wrapped only to learn Mode_T and the user gap penalties; the
+ * reference's own setup still runs.  See INTEGRATION.md.
+ *
+ * Scope (the engine's, include/gmapdp.h): nosimd semantics; no alternate-
+ * allele genome (genomealt must equal genome); Dynprog_T created with
+ * gmap.c's defaults (max_rlength 660, max_glength 2000); homopolymer mode
+ * off; no splicing IIT in Dynprog_genome_gap.  Anything else is refused with
+ * a message and abort() -- there is no silent CPU fallback.
+ *
+ * This file is one call per launch (a correctness drop-in).  Throughput comes
+ * from batching many calls per launch (gmapdp_*_batch / gmapdp_plan_*), which
+ * needs the caller to issue sub-problems of many reads together
+ * (INTEGRATION.md "Batching").
+ */
+#ifdef HAVE_CONFIG_H
+#include "config.h"
+#endif
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <pthread.h>
+
+#include "bool.h"
+#include "list.h"
+#include "pair.h"
+#include "pairdef.h"
+#include "pairpool.h"
+#include "genome.h"
+#include "maxent_hr.h"
+#include "dynprog.h"
+#include "dynprog_single.h"
+#include "dynprog_end.h"
+#include "dynprog_genome.h"
+
+#include "gmapdp.h"
+#include "gmapdp_dynprog.h"
+
+/* ---- the wrapped reference functions ---- */
+extern void __real_Dynprog_init (Mode_T mode);
+extern void __real_Dynprog_single_setup (int user_open_in, int user_extend_in, bool user_dynprog_p_in,
+                                         bool homopolymerp_in);
+extern void __real_Dynprog_end_setup (Univcoord_T *splicesites_in, Splicetype_T *splicetypes_in,
+                                      Chrpos_T *splicedists_in, int nsplicesites_in,
+                                      Trieoffset_T *trieoffsets_obs_in, Triecontent_T *triecontents_obs_in,
+                                      Trieoffset_T *trieoffsets_max_in, Triecontent_T *triecontents_max_in,
+                                      int user_open_in, int user_extend_in, bool user_dynprog_p_in);
+extern void __real_Dynprog_genome_setup (bool novelsplicingp_in, IIT_T splicing_iit_in,
+                                         int *splicing_divint_crosstable_in, int donor_typeint_in,
+                                         int acceptor_typeint_in, int user_open_in, int user_extend_in,
+                                         bool user_dynprog_p_in);
+
+static pthread_mutex_t shim_lock = PTHREAD_MUTEX_INITIALIZER;
+static gmapdp_ctx *shim_ctx = NULL;
+static Genome_T shim_genome = NULL;
+static int shim_mode = 0, shim_user_open = 0, shim_user_extend = 0, shim_user_dynprog_p = 0;
+static int shim_homopolymerp = 0, shim_splicing_iit = 0;
+
+static void
+shim_refuse (const char *what) {
+  fprintf(stderr, "gmapdp shim: %s is not supported by the MI355X Dynprog engine\n", what);
+  abort();
+}
+
+static void
+shim_check (int rc, const char *what) {
+  if (rc != GMAPDP_OK) {
+    fprintf(stderr, "gmapdp shim: %s failed (%d): %s\n", what, rc, gmapdp_last_error(shim_ctx));
+    abort();
+  }
+}
+
+void
+__wrap_Dynprog_init (Mode_T mode) {
+  __real_Dynprog_init(mode);
+  shim_mode = (int) mode;
+}
+
+void
+__wrap_Dynprog_single_setup (int user_open_in, int user_extend_in, bool user_dynprog_p_in, bool homopolymerp_in) {
+  __real_Dynprog_single_setup(user_open_in, user_extend_in, user_dynprog_p_in, homopolymerp_in);
+  shim_user_open = user_open_in;
+  shim_user_extend = user_extend_in;
+  shim_user_dynprog_p = user_dynprog_p_in ? 1 : 0;
+  shim_homopolymerp = homopolymerp_in ? 1 : 0;
+}
+
+void
+__wrap_Dynprog_end_setup (Univcoord_T *splicesites_in, Splicetype_T *splicetypes_in, Chrpos_T *splicedists_in,
+                          int nsplicesites_in, Trieoffset_T *trieoffsets_obs_in, Triecontent_T *triecontents_obs_in,
+                          Trieoffset_T *trieoffsets_max_in, Triecontent_T *triecontents_max_in,
+                          int user_open_in, int user_extend_in, bool user_dynprog_p_in) {
+  __real_Dynprog_end_setup(splicesites_in, splicetypes_in, splicedists_in, nsplicesites_in, trieoffsets_obs_in,
+                           triecontents_obs_in, trieoffsets_max_in, triecontents_max_in, user_open_in,
+                           user_extend_in, user_dynprog_p_in);
+}
+
+void
+__wrap_Dynprog_genome_setup (bool novelsplicingp_in, IIT_T splicing_iit_in, int *splicing_divint_crosstable_in,
+                             int donor_typeint_in, int acceptor_typeint_in, int user_open_in, int user_extend_in,
+                             bool user_dynprog_p_in) {
+  __real_Dynprog_genome_setup(novelsplicingp_in, splicing_iit_in, splicing_divint_crosstable_in, donor_typeint_in,
+                              acceptor_typeint_in, user_open_in, user_extend_in, user_dynprog_p_in);
+  shim_splicing_iit = splicing_iit_in != NULL;
+}
+
+/* The engine context (one per process, calls serialised) with `genome` resident in HBM. */
+static gmapdp_ctx *
+shim_context (Genome_T genome, Genome_T genomealt, Dynprog_T dynprog) {
+  const char *dev;
+  uint64_t length;
+  size_t nwords;
+  if (genomealt != NULL && genomealt != genome) shim_refuse("an alternate-allele genome (genomealt)");
+  if (dynprog->max_rlength != GMAPDP_MAX_RLENGTH || dynprog->max_glength != GMAPDP_MAX_GLENGTH)
+    shim_refuse("a Dynprog_T with non-default maximum lengths");
+  if (shim_ctx == NULL) {
+    dev = getenv("GMAPDP_DEVICE");
+    shim_check(gmapdp_create(&shim_ctx, dev ? atoi(dev) : 0, shim_mode, shim_user_open, shim_user_extend,
+                             shim_user_dynprog_p), "gmapdp_create");
+  }
+  if (genome != shim_genome) {
+    length = (uint64_t) Genome_genomelength(genome);
+    nwords = gmapdp_genome_words(length);
+    shim_check(gmapdp_set_genome(shim_ctx, (const uint32_t *) Genome_blocks(genome), nwords, length),
+               "gmapdp_set_genome");
+    shim_genome = genome;
+  }
+  return shim_ctx;
+}
+
+/* The engine's records in list order -> the reference's List_T (each push prepends). */
+static List_T
+shim_list (const gmapdp_pair *pairs, int n, int dynprogindex, int gap_index, int gap_queryjump, int introntype,
+           double donor_prob, double acceptor_prob, Pairpool_T pairpool) {
+  List_T list = NULL;
+  Pair_T gappair;
+  int i;
+  for (i = n - 1; i >= 0; i--) {
+    const gmapdp_pair *p = &pairs[i];
+    if (p->querypos == -1 && p->genomepos == -1) {
+      list = Pairpool_push_gapholder(list, pairpool, i == gap_index ? gap_queryjump : 0, p->jump,
+                                     /*leftpair*/NULL, /*rightpair*/NULL, /*knownp*/false);
+      if (i == gap_index) {
+        gappair = (Pair_T) list->first;
+        gappair->introntype = introntype;
+        gappair->donor_prob = donor_prob;
+        gappair->acceptor_prob = acceptor_prob;
+      }
+    } else {
+      list = Pairpool_push(list, pairpool, p->querypos, p->genomepos, p->cdna, p->comp, p->genome, p->genomealt,
+                           dynprogindex);
+    }
+  }
+  return list;
+}
+
+List_T
+__wrap_Dynprog_single_gap (int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches, int *nopens,
+                           int *nindels, Dynprog_T dynprog, char *sequence1, char *sequenceuc1, int length1,
+                           int length2, int offset1, int offset2, Univcoord_T chroffset, Univcoord_T chrhigh,
+                           bool watsonp, int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
+                           Pairpool_T pairpool, int extraband_single, bool widebandp, double defect_rate) {
+  gmapdp_single_problem p;
+  gmapdp_result res;
+  gmapdp_pair *pairs;
+  size_t cap;
+  List_T list;
+  if (shim_homopolymerp) shim_refuse("homopolymer mode (Dynprog_single_setup homopolymerp)");
+  pthread_mutex_lock(&shim_lock);
+  shim_context(genome, genomealt, dynprog);
+  memset(&p, 0, sizeof(p));
+  p.qoff = 0;
+  p.rlength = length1;
+  p.glength = length2;
+  p.roffset = offset1;
+  p.goffset = offset2;
+  p.chroffset = (uint32_t) chroffset;
+  p.chrhigh = (uint32_t) chrhigh;
+  p.flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0) | (widebandp ? GMAPDP_WIDEBAND : 0);
+  p.genestrand = genestrand;
+  p.extraband = extraband_single;
+  p.defect_rate = defect_rate;
+  p.dynprogindex = *dynprogindex;
+  cap = gmapdp_single_pair_capacity(&p, 1);
+  pairs = (gmapdp_pair *) malloc((cap ? cap : 1) * sizeof(gmapdp_pair));
+  shim_check(gmapdp_single_gap_batch(shim_ctx, &p, 1, sequence1, sequenceuc1, length1 > 0 ? (size_t) length1 : 0,
+                                     &res, pairs, cap), "gmapdp_single_gap_batch");
+  pthread_mutex_unlock(&shim_lock);
+  list = shim_list(pairs + res.pair_offset, res.npairs, p.dynprogindex, -1, 0, 0, 0.0, 0.0, pairpool);
+  free(pairs);
+  *dynprogindex = res.dynprogindex;
+  *finalscore = res.traceback_score;
+  *nmatches = res.nmatches;
+  *nmismatches = res.nmismatches;
+  *nopens = res.nopens;
+  *nindels = res.nindels;
+  return list;
+}
+
+static List_T
+shim_end_gap (int end3p, int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches, int *nopens,
+              int *nindels, Dynprog_T dynprog, char *seq, char *sequc, int length1, int length2, int offset1,
+              int offset2, Univcoord_T chroffset, Univcoord_T chrhigh, bool watsonp, int genestrand,
+              bool jump_late_p, Genome_T genome, Genome_T genomealt, Pairpool_T pairpool, int extraband_end,
+              double defect_rate, Endalign_T endalign, bool require_pos_score_p) {
+  gmapdp_end_problem p;
+  gmapdp_result res;
+  gmapdp_pair *pairs;
+  size_t cap;
+  List_T list;
+  const char *q, *quc;
+  pthread_mutex_lock(&shim_lock);
+  shim_context(genome, genomealt, dynprog);
+  memset(&p, 0, sizeof(p));
+  p.rlength = length1;
+  p.glength = length2;
+  p.roffset = offset1;
+  p.goffset = offset2;
+  p.chroffset = (uint32_t) chroffset;
+  p.chrhigh = (uint32_t) chrhigh;
+  p.flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0);
+  p.genestrand = genestrand;
+  p.extraband = extraband_end;
+  p.end3p = end3p;
+  p.endalign = (int32_t) endalign;
+  p.require_pos_score_p = require_pos_score_p ? 1 : 0;
+  p.dynprogindex = *dynprogindex;
+  p.defect_rate = defect_rate;
+  /* end5's revsequence points at the LAST character of the slice (dynprog_end.c:1294) */
+  q = (end3p || length1 <= 0) ? seq : seq - (length1 - 1);
+  quc = (end3p || length1 <= 0) ? sequc : sequc - (length1 - 1);
+  cap = gmapdp_end_pair_capacity(&p, 1);
+  pairs = (gmapdp_pair *) malloc((cap ? cap : 1) * sizeof(gmapdp_pair));
+  shim_check(gmapdp_end_gap_batch(shim_ctx, &p, 1, q, quc, length1 > 0 ? (size_t) length1 : 0, &res, pairs, cap),
+             "gmapdp_end_gap_batch");
+  pthread_mutex_unlock(&shim_lock);
+  list = shim_list(pairs + res.pair_offset, res.npairs, p.dynprogindex, -1, 0, 0, 0.0, 0.0, pairpool);
+  free(pairs);
+  *dynprogindex = res.dynprogindex;
+  *finalscore = res.traceback_score;
+  *nmatches = res.nmatches;
+  *nmismatches = res.nmismatches;
+  *nopens = res.nopens;
+  *nindels = res.nindels;
+  return list;
+}
+
+List_T
+__wrap_Dynprog_end5_gap (int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches, int *nopens,
+                         int *nindels, Dynprog_T dynprog, char *revsequence1, char *revsequenceuc1, int length1,
+                         int length2, int revoffset1, int revoffset2, Univcoord_T chroffset, Univcoord_T chrhigh,
+                         bool watsonp, int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
+                         Pairpool_T pairpool, int extraband_end, double defect_rate, Endalign_T endalign,
+                         bool require_pos_score_p) {
+  return shim_end_gap(0, dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels, dynprog, revsequence1,
+                      revsequenceuc1, length1, length2, revoffset1, revoffset2, chroffset, chrhigh, watsonp,
+                      genestrand, jump_late_p, genome, genomealt, pairpool, extraband_end, defect_rate, endalign,
+                      require_pos_score_p);
+}
+
+List_T
+__wrap_Dynprog_end3_gap (int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches, int *nopens,
+                         int *nindels, Dynprog_T dynprog, char *sequence1, char *sequenceuc1, int length1,
+                         int length2, int offset1, int offset2, Univcoord_T chroffset, Univcoord_T chrhigh,
+                         bool watsonp, int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
+                         Pairpool_T pairpool, int extraband_end, double defect_rate, Endalign_T endalign,
+                         bool require_pos_score_p) {
+  return shim_end_gap(1, dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels, dynprog, sequence1,
+                      sequenceuc1, length1, length2, offset1, offset2, chroffset, chrhigh, watsonp, genestrand,
+                      jump_late_p, genome, genomealt, pairpool, extraband_end, defect_rate, endalign,
+                      require_pos_score_p);
+}
+
+/* Maxent_hr_*_prob of one splice-site entry (the host's MaxEnt models, maxent_hr.c) */
+static double
+shim_maxent (Genome_T genome, Genome_T genomealt, uint8_t model, uint32_t pos, Univcoord_T chroffset) {
+  switch (model) {
+  case GMAPDP_MAXENT_DONOR: return Maxent_hr_donor_prob(genome, genomealt, (Univcoord_T) pos, chroffset);
+  case GMAPDP_MAXENT_ACCEPTOR: return Maxent_hr_acceptor_prob(genome, genomealt, (Univcoord_T) pos, chroffset);
+  case GMAPDP_MAXENT_ANTIDONOR: return Maxent_hr_antidonor_prob(genome, genomealt, (Univcoord_T) pos, chroffset);
+  default: return Maxent_hr_antiacceptor_prob(genome, genomealt, (Univcoord_T) pos, chroffset);
+  }
+}
+
+List_T
+__wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_rightgenomepos, double *left_prob,
+                           double *right_prob, int *traceback_score, int *nmatches, int *nmismatches, int *nopens,
+                           int *nindels, int *exonhead, int *introntype, Dynprog_T dynprogL, Dynprog_T dynprogR,
+                           char *rsequence, char *rsequenceuc, int rlength, int glengthL, int glengthR, int roffset,
+                           int goffsetL, int rev_goffsetR, Chrnum_T chrnum, Univcoord_T chroffset,
+                           Univcoord_T chrhigh, int cdna_direction, bool watsonp, int genestrand, bool jump_late_p,
+                           Genome_T genome, Genome_T genomealt, Pairpool_T pairpool, int extraband_paired,
+                           double defect_rate, int maxpeelback, bool halfp, bool finalp) {
+  gmapdp_genome_problem p;
+  gmapdp_genome_result res;
+  gmapdp_pair *pairs;
+  size_t cap, m, i;
+  uint32_t *pos;
+  uint8_t *model;
+  double *probs;
+  List_T list;
+  (void) chrnum;
+  if (shim_splicing_iit) shim_refuse("known splice sites (a splicing IIT) in Dynprog_genome_gap");
+  pthread_mutex_lock(&shim_lock);
+  shim_context(genome, genomealt, dynprogL);
+  shim_context(genome, genomealt, dynprogR);
+  memset(&p, 0, sizeof(p));
+  p.rlength = rlength;
+  p.glengthL = glengthL;
+  p.glengthR = glengthR;
+  p.roffset = roffset;
+  p.goffsetL = goffsetL;
+  p.rev_goffsetR = rev_goffsetR;
+  p.chroffset = (uint32_t) chroffset;
+  p.chrhigh = (uint32_t) chrhigh;
+  p.flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0) | (halfp ? GMAPDP_HALFP : 0) |
+            (finalp ? GMAPDP_FINALP : 0);
+  p.cdna_direction = cdna_direction;
+  p.genestrand = genestrand;
+  p.extraband = extraband_paired;
+  p.maxpeelback = maxpeelback;
+  p.dynprogindex = *dynprogindex;
+  p.defect_rate = defect_rate;
+  p.prob_offset = 0;
+  /* the MaxEnt probabilities the bridge reads, computed by the host as the reference does;
+     skipped where the engine resolves the call before reading them (rlength <= 1, size guard) */
+  m = 0;
+  if (rlength > 1 && rlength <= GMAPDP_MAX_RLENGTH && glengthL <= GMAPDP_MAX_GLENGTH &&
+      glengthR <= GMAPDP_MAX_GLENGTH && glengthL > 0 && glengthR > 0)
+    m = gmapdp_genome_prob_entries(&p, 1);
+  probs = (double *) calloc(m ? m : 1, sizeof(double));
+  if (m) {
+    pos = (uint32_t *) malloc(m * sizeof(uint32_t));
+    model = (uint8_t *) malloc(m);
+    shim_check(gmapdp_genome_splice_sites(&p, 1, pos, model, m), "gmapdp_genome_splice_sites");
+    /* the last entry of each side is never read (the reference leaves it unset too, :2575-2660) */
+    for (i = 0; i < m; i++)
+      if (i != (size_t) glengthL - 1 && i != m - 1)
+        probs[i] = shim_maxent(genome, genomealt, model[i], pos[i], chroffset);
+    free(pos);
+    free(model);
+  }
+  cap = gmapdp_genome_pair_capacity(&p, 1);
+  pairs = (gmapdp_pair *) malloc((cap ? cap : 1) * sizeof(gmapdp_pair));
+  shim_check(gmapdp_genome_gap_batch(shim_ctx, &p, 1, rsequence, rsequenceuc, rlength > 0 ? (size_t) rlength : 0,
+                                     probs, m, &res, pairs, cap), "gmapdp_genome_gap_batch");
+  pthread_mutex_unlock(&shim_lock);
+  list = shim_list(pairs + res.pair_offset, res.npairs, p.dynprogindex, res.gap_index, res.gap_queryjump,
+                   res.introntype, res.left_prob, res.right_prob, pairpool);
+  free(pairs);
+  free(probs);
+  *dynprogindex = res.dynprogindex;
+  *traceback_score = res.traceback_score;
+  *nmatches = res.nmatches;
+  *nmismatches = res.nmismatches;
+  *nopens = res.nopens;
+  *nindels = res.nindels;
+  *introntype = res.introntype;
+  *left_prob = res.left_prob;
+  *right_prob = res.right_prob;
+  if (res.new_leftgenomepos != GMAPDP_UNSET) *new_leftgenomepos = res.new_leftgenomepos;
+  if (res.new_rightgenomepos != GMAPDP_UNSET) *new_rightgenomepos = res.new_rightgenomepos;
+  if (res.exonhead != GMAPDP_UNSET) *exonhead = res.exonhead;
+  return list;
+}

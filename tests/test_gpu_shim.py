@@ -1,0 +1,51 @@
+"""The GMAP drop-in, end to end: the reference's own objects with Dynprog_single_gap,
+Dynprog_end5/3_gap and Dynprog_genome_gap routed (ld --wrap) through
+gmap-2024_amd/shim/gmapdp_gmap_shim.c to the GPU engine (oracle/_ref/librefdp_gpushim.so),
+against the same objects unmodified.  Pair_T lists (every field the call sets) and
+out-parameters must be identical."""
+import random
+
+import pytest
+
+from dpbind import (GG_FLAG_HALF, Ref, call_end, call_single, edge_single_gap_problem, end_gap_problem,
+                    genome_gap_problem, random_genome, ref_available, single_gap_problem)
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not (ref_available("gpushim") and ref_available("nosimda")),
+                                 reason="reference objects / shim harness did not travel")]
+
+
+@pytest.fixture(scope="module")
+def impls():
+    return Ref("nosimd"), Ref("nosimda"), Ref("gpushim")
+
+
+def test_shim_single_and_end_gaps(impls):
+    ref, _, shim = impls
+    rng = random.Random(606)
+    g = random_genome(rng, 30000)
+    ref.set_genome(g)
+    shim.set_genome(g)
+    bad = []
+    for i in range(600):
+        p = single_gap_problem(rng, g) if i % 3 else edge_single_gap_problem(rng, g)
+        if call_single(shim, p) != call_single(ref, p):
+            bad.append(("single", i))
+    for i in range(400):
+        p = end_gap_problem(rng, g, edge=(i % 4 == 0))
+        if call_end(shim, p) != call_end(ref, p):
+            bad.append(("end", i))
+    assert bad == []
+
+
+def test_shim_genome_gaps(impls):
+    ref, refa, shim = impls
+    rng = random.Random(707)
+    g = bytearray(random_genome(rng, 60000))
+    probs = [genome_gap_problem(rng, g, edge=(i % 5 == 0)) for i in range(500)]
+    g = bytes(g)
+    for r in impls:
+        r.set_genome(g)
+    bad = [i for i, p in enumerate(probs)
+           if shim.genome_gap(p) != (refa if p["flags"] & GG_FLAG_HALF else ref).genome_gap(p)]
+    assert bad == []
