@@ -361,6 +361,11 @@ def main():
     nprob = ns + ne
     gp["qoff"] += len(q)
     q_all = np.concatenate([q, gq])
+    if world > 1:
+        # the genome is replicated per GPU (read-only); the reads are this rank's --part=rank/world
+        # share (gmapdp.shard): weak scaling, no collective on the data path
+        from gmapdp import shard
+        shard.check_replicated(shard.genome_digest(genome), dist)
 
     eng = gmapdp.Engine(local)
     eng.set_genome(genome.tobytes())
@@ -451,12 +456,12 @@ def main():
             if world > 1:
                 dist.barrier()
             elapsed = time.perf_counter() - t0
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         if world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            from gmapdp import shard
+            elapsed = shard.max_over_ranks(elapsed, dist, device=dev)
         launch_ms = [sum(evs[k][li][0].elapsed_time(evs[k][li][1]) for k in range(steps)) / steps
                      for li in range(nl)]
-        return float(t.item()), launch_ms
+        return elapsed, launch_ms
 
     # ---- headline: configs[1] (Dynprog_single_gap + Dynprog_end{5,3}_gap) ----
     P = build(False)
