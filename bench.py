@@ -231,7 +231,10 @@ def pmc_traffic(name):
     m = re.match(r"(\w+)<R=(\d+),dirs_lds=(\d)>", name)
     if not m:
         return None, None
-    key = "gmapdp::%s<%s, %s>" % (m.group(1), m.group(2), "true" if m.group(3) == "1" else "false")
+    if m.group(1) == "dpx_kernel":
+        key = "gmapdp::dpx_kernel<%s>" % m.group(2)
+    else:
+        key = "gmapdp::%s<%s, %s>" % (m.group(1), m.group(2), "true" if m.group(3) == "1" else "false")
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")), reverse=True):
         try:
             k = json.load(open(path))["kernels"].get(key)
@@ -483,8 +486,9 @@ def main():
         for li in range(PP["nl"]):
             m = np.zeros(info_[li][2], dtype=np.int32)
             lib.gmapdp_plan_launch_members(plan_, li, m.ctypes.data)
-            if PP["kind"][li] == 0:
-                name = "dp_kernel<R=%d,dirs_lds=%d>" % (info_[li][0], info_[li][1])
+            if PP["kind"][li] in (0, 2):
+                name = ("dp_kernel<R=%d,dirs_lds=%d>" if PP["kind"][li] == 0 else "dpx_kernel<R=%d,dirs_lds=%d>") \
+                    % (info_[li][0], info_[li][1])
                 nbytes = algorithmic_bytes(rl[m], gl[m], npairs[m], desc[m])
             else:
                 name = "gg_kernel<R=%d,dirs_lds=%d>" % (info_[li][0], info_[li][1])

@@ -37,6 +37,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "gmapdp_internal.h"
 #include "../../include/gmapdp.h"
 
@@ -62,6 +64,44 @@ __device__ __forceinline__ int wave_scan_max(int x) {
   x = max(x, __builtin_amdgcn_update_dpp(kSent, x, 0x118, 0xf, 0xf, false));  // row_shr:8
   x = max(x, __builtin_amdgcn_update_dpp(kSent, x, 0x142, 0xa, 0xf, false));  // row_bcast:15
   x = max(x, __builtin_amdgcn_update_dpp(kSent, x, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return x;
+}
+
+// ---- segmented variants: a wave split into 64/S segments of S lanes, one DP problem each ----
+// lane i <- lane i+1 of its segment; the segment's last lane <- fill
+template <int S>
+__device__ __forceinline__ int seg_shl1(int x, int fill, int sl) {
+  if constexpr (S == 64) {
+    return dpp_wave_shl1(x, fill);
+  } else if constexpr (S == 16) {
+    return __builtin_amdgcn_update_dpp(fill, x, 0x101, 0xf, 0xf, false);  // row_shl:1
+  } else {
+    const int v = dpp_wave_shl1(x, fill);
+    return (sl == S - 1) ? fill : v;
+  }
+}
+// lane i <- lane i-1 of its segment; the segment's first lane <- fill
+template <int S>
+__device__ __forceinline__ int seg_shr1(int x, int fill, int sl) {
+  if constexpr (S == 64) {
+    return dpp_wave_shr1(x, fill);
+  } else if constexpr (S == 16) {
+    return __builtin_amdgcn_update_dpp(fill, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  } else {
+    const int v = dpp_wave_shr1(x, fill);
+    return (sl == 0) ? fill : v;
+  }
+}
+// inclusive max-scan within each segment
+template <int S>
+__device__ __forceinline__ int seg_scan_max(int x) {
+  if constexpr (S == 64) return wave_scan_max(x);
+  x = max(x, __builtin_amdgcn_update_dpp(kSent, x, 0x111, 0xf, 0xf, false));  // row_shr:1
+  x = max(x, __builtin_amdgcn_update_dpp(kSent, x, 0x112, 0xf, 0xf, false));  // row_shr:2
+  x = max(x, __builtin_amdgcn_update_dpp(kSent, x, 0x114, 0xf, 0xf, false));  // row_shr:4
+  x = max(x, __builtin_amdgcn_update_dpp(kSent, x, 0x118, 0xf, 0xf, false));  // row_shr:8
+  if constexpr (S == 32)
+    x = max(x, __builtin_amdgcn_update_dpp(kSent, x, 0x142, 0xa, 0xf, false));  // row_bcast:15 (rows 1, 3)
   return x;
 }
 
@@ -140,10 +180,10 @@ __host__ __device__ inline Carve carve_dp(int rlength, int glength, int R, bool 
 
 // direction planes: [c][t][i] 64-bit masks; t: 0 nogap=HORIZ, 1 nogap=VERT, 2 Egap=HORIZ, 3 Fgap=VERT;
 // band offset k lives in word i = k % R at bit k / R.
-template <int R>
-__device__ __forceinline__ uint32_t dir_bit(const uint64_t* dirs, int c, int t, int k, int W) {
+template <int R, typename WORD = uint64_t>
+__device__ __forceinline__ uint32_t dir_bit(const WORD* dirs, int c, int t, int k, int W) {
   if (k < 0 || k >= W) return 0u;  // outside the band: cleared to DIAG (dynprog.c:498)
-  const uint64_t m = dirs[((size_t)c * 4 + t) * R + (k % R)];
+  const WORD m = dirs[((size_t)c * 4 + t) * R + (k % R)];
   return (uint32_t)(m >> (k / R)) & 1u;
 }
 
@@ -268,6 +308,15 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
   }
   return x;
 }
+template <int S>
+__device__ __forceinline__ uint64_t seg_max_u64(uint64_t x) {
+#pragma unroll
+  for (int off = S / 2; off >= 1; off >>= 1) {
+    const uint64_t y = __shfl_xor(x, off, 64);
+    x = y > x ? y : x;
+  }
+  return x;
+}
 
 // ---- banded fill (Dynprog_standard, upperp = lowerp = true, saturation NEG_INFINITY_INT) ----
 // Rows r = c - uband + k, k = lane*R + i.  Writes the four direction ballots of every column to
@@ -301,17 +350,25 @@ struct Part {
   int c;  // -1: no candidate
 };
 
-template <int R, bool CARRY>
+// S < 64: the wave holds 64/S problems, one per S-lane segment (R must be 1); every argument
+// is then per segment, `gmax` is the wave's largest glength and a segment's direction words are
+// its S ballot bits (WORD = uint16_t / uint32_t), written by the segment's first lane.
+template <int R, bool CARRY, int S = 64, typename WORD = uint64_t>
 __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lband, int uband, int open, int ext,
                                           int late, int track, const int8_t* sc, int srow, const uint8_t* gcl,
-                                          uint64_t* dirs, const BridgeCarry* bc_, int& bestr, int& bestc) {
+                                          WORD* dirs, const BridgeCarry* bc_, int& bestr, int& bestc,
+                                          int gmax = 0) {
+  static_assert(S == 64 || (R == 1 && !CARRY), "segmented fills are single-word, no bridge carry");
+  const int lk = (S == 64) ? lane : (lane & (S - 1));  // lane within the segment
+  const int segshift = lane - lk;                      // first ballot bit of the segment
+  const int cend = (S == 64) ? glen : gmax;
   const int sat = kNegInf32;
   const int W = lband + uband + 1;
   const int binit = (track == 2) ? kNegInf32 : 0;
   int Hs[R], E[R], bv[R], bcol[R];
 #pragma unroll
   for (int i = 0; i < R; i++) {  // column 0 (dynprog.c:1331-1369)
-    const int k = lane * R + i;
+    const int k = lk * R + i;
     const int r = k - uband;
     int v = kNegInf32;
     if (k < W && r >= 0 && r <= rlen) v = (r == 0) ? 0 : (r <= lband ? open + r * ext : kNegInf32);
@@ -324,7 +381,7 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
   // itself as the diagonal of the band-top row, which the reference takes unclamped (first_nogap).
   int kext[R];  // k*ext per element: r*ext = rtop*ext + k*ext without a per-column multiply
 #pragma unroll
-  for (int i = 0; i < R; i++) kext[i] = (lane * R + i) * ext;
+  for (int i = 0; i < R; i++) kext[i] = (lk * R + i) * ext;
   int cs[R], cc[R];  // carried bridge candidate per band row: score, column (-1: none), probability
   double cp[R];
 #pragma unroll
@@ -333,8 +390,10 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
     cc[i] = -1;
     cp[i] = 0.0;
   }
-  for (int c = 1; c <= glen; c++) {
-    const int gi = __builtin_amdgcn_readfirstlane(gcl[c]);  // wave-uniform genome class
+  for (int c = 1; c <= cend; c++) {
+    const bool colact = (S == 64) || (c <= glen);
+    // genome class: wave-uniform (SGPR) for one problem per wave, per segment otherwise
+    const int gi = (S == 64) ? __builtin_amdgcn_readfirstlane(gcl[c]) : gcl[min(c, glen)];
     const int rtop = c - uband;
     const int rlo = rtop < 1 ? 1 : rtop;
     const int rhigh = (c + lband) < rlen ? (c + lband) : rlen;
@@ -347,16 +406,16 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
     int Ein[R], Hin[R];
 #pragma unroll
     for (int i = 0; i < R - 1; i++) { Ein[i] = E[i + 1]; Hin[i] = Hs[i + 1]; }
-    Ein[R - 1] = dpp_wave_shl1(E[0], kNegInf32);
-    Hin[R - 1] = dpp_wave_shl1(Hs[0], kNegInf32);
+    Ein[R - 1] = seg_shl1<S>(E[0], kNegInf32, lk);
+    Hin[R - 1] = seg_shl1<S>(Hs[0], kNegInf32, lk);
 
     int Hp[R], En[R], A[R];
     bool valid[R], eb[R], hb[R];
 #pragma unroll
     for (int i = 0; i < R; i++) {
-      const int k = lane * R + i;
+      const int k = lk * R + i;
       const int r = rtop + k;
-      valid[i] = (k < W) & (r >= rlo) & (r <= rhigh);
+      valid[i] = (k < W) & (r >= rlo) & (r <= rhigh) & colact;
       const int s = scg[min(max(r, 0), rlen + 1)];
       // Egap (dynprog.c:1518-1524)
       const int es = Hin[i] + open;
@@ -372,7 +431,7 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
     pre[0] = A[0];
 #pragma unroll
     for (int i = 1; i < R; i++) pre[i] = max(pre[i - 1], A[i]);
-    const int X = dpp_wave_shr1(wave_scan_max(pre[R - 1]), kSent);
+    const int X = seg_shr1<S>(seg_scan_max<S>(pre[R - 1]), kSent, lk);
     const int init = max(kNegInf32, L0 + open) - (rlo - 1) * ext;
     int F[R], Hun[R];
     bool vb[R];
@@ -384,12 +443,12 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
       Hun[i] = max(F[i], Hp[i]);
     }
     // Fgap direction needs F(r-1), H(r-1) of this column (dynprog.c:1486-1492)
-    const int Fup = dpp_wave_shr1(F[R - 1], kNegInf32);
-    const int Hup = dpp_wave_shr1(Hun[R - 1], kNegInf32);
+    const int Fup = seg_shr1<S>(F[R - 1], kNegInf32, lk);
+    const int Hup = seg_shr1<S>(Hun[R - 1], kNegInf32, lk);
     uint64_t mH[R], mV[R], mE[R], mF[R];
 #pragma unroll
     for (int i = 0; i < R; i++) {
-      const int k = lane * R + i;
+      const int k = lk * R + i;
       const int r = rtop + k;
       const bool top = r == rlo;
       const int fprev = top ? kNegInf32 : ((i == 0) ? Fup : F[i - 1]);
@@ -428,7 +487,7 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
       }
 #pragma unroll
       for (int i = 0; i < R; i++) {
-        const int k = lane * R + i;
+        const int k = lk * R + i;
         const int r = rtop + k;
         const int other = rlen - r;
         const bool inrow = (r >= 1) & (r <= rlen - 1) & (k < W);
@@ -452,14 +511,14 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
         }
       }
     }
-    if (lane == 0) {  // one lane stores the column's 4R direction words
-      uint64_t* dcol = dirs + (size_t)c * 4 * R;
+    if (lk == 0 && colact) {  // one lane per problem stores the column's 4R direction words
+      WORD* dcol = dirs + (size_t)c * 4 * R;
 #pragma unroll
       for (int i = 0; i < R; i++) {
-        dcol[0 * R + i] = mH[i];
-        dcol[1 * R + i] = mV[i];
-        dcol[2 * R + i] = mE[i];
-        dcol[3 * R + i] = mF[i];
+        dcol[0 * R + i] = (WORD)(mH[i] >> segshift);
+        dcol[1 * R + i] = (WORD)(mV[i] >> segshift);
+        dcol[2 * R + i] = (WORD)(mE[i] >> segshift);
+        dcol[3 * R + i] = (WORD)(mF[i] >> segshift);
       }
     }
   }
@@ -467,7 +526,7 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
     const BridgeCarry& B = *bc_;
 #pragma unroll
     for (int i = 0; i < R; i++) {
-      const int k = lane * R + i;
+      const int k = lk * R + i;
       const int r = glen - uband + k;
       if (k < W && r >= 1 && r <= rlen - 1) {
         B.part[r].s = cs[i];
@@ -483,14 +542,14 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
 #pragma unroll
     for (int i = 0; i < R; i++) {
       if (bcol[i] > 0) {
-        const int r = bcol[i] - uband + lane * R + i;
+        const int r = bcol[i] - uband + lk * R + i;
         const uint32_t rk = late ? (uint32_t)r : 4095u - (uint32_t)r;
         const uint32_t ck = late ? (uint32_t)bcol[i] : 4095u - (uint32_t)bcol[i];
         const uint64_t kk = ((uint64_t)(uint32_t)(bv[i] + (1 << 30)) << 24) | ((uint64_t)rk << 12) | ck;
         key = kk > key ? kk : key;
       }
     }
-    key = wave_max_u64(key);
+    key = seg_max_u64<S>(key);
     if (key == 0) {
       bestr = (track == 2) ? rlen : 0;
       bestc = 0;
@@ -507,22 +566,22 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
 
 // ---- wave-cooperative traceback (Dynprog_traceback_std, dynprog.c:1796-1948) ----
 // Emits the reference's push order into out[t.count ...].
-template <int R>
-__device__ __forceinline__ void traceback_band(int lane, const uint64_t* dirs, int W, int uband, int r, int c,
+template <int R, typename WORD = uint64_t>
+__device__ __forceinline__ void traceback_band(int lane, const WORD* dirs, int W, int uband, int r, int c,
                                                const Geo& G, const char* q, const char* quc, const char* gch,
                                                const uint8_t* __restrict__ cons, bool watson, uint32_t chroffset,
                                                uint32_t chrhigh, const uint32_t* __restrict__ blocks,
                                                uint64_t nwords, gmapdp_pair* out, Tally& t) {
   while (r > 0 && c > 0) {
     const int k = r - c + uband;
-    const uint32_t isV = dir_bit<R>(dirs, c, 1, k, W);
-    const uint32_t isH = dir_bit<R>(dirs, c, 0, k, W);
+    const uint32_t isV = dir_bit<R, WORD>(dirs, c, 1, k, W);
+    const uint32_t isH = dir_bit<R, WORD>(dirs, c, 0, k, W);
     if (!isV && isH) {
       // E chain along row r: columns c, c-1, ... while Egap == HORIZ
       int n = 0;
       for (int base = 0;; base += 64) {
         const int j = base + lane;
-        const bool cont = (c - j >= 1) && dir_bit<R>(dirs, c - j, 2, k + j, W);
+        const bool cont = (c - j >= 1) && dir_bit<R, WORD>(dirs, c - j, 2, k + j, W);
         const uint64_t stop = ~ballot(cont);
         if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
       }
@@ -535,7 +594,7 @@ __device__ __forceinline__ void traceback_band(int lane, const uint64_t* dirs, i
       int n = 0;
       for (int base = 0;; base += 64) {
         const int j = base + lane;
-        const bool cont = (r - j >= 1) && dir_bit<R>(dirs, c, 3, k - j, W);
+        const bool cont = (r - j >= 1) && dir_bit<R, WORD>(dirs, c, 3, k - j, W);
         const uint64_t stop = ~ballot(cont);
         if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
       }
@@ -549,8 +608,8 @@ __device__ __forceinline__ void traceback_band(int lane, const uint64_t* dirs, i
       for (int base = 0;; base += 64) {
         const int j = base + lane;
         const bool inrange = (c - j >= 1) && (r - j >= 1);
-        const bool cont = (j == 0) || (inrange && !dir_bit<R>(dirs, c - j, 0, k, W) &&
-                                       !dir_bit<R>(dirs, c - j, 1, k, W));
+        const bool cont = (j == 0) || (inrange && !dir_bit<R, WORD>(dirs, c - j, 0, k, W) &&
+                                       !dir_bit<R, WORD>(dirs, c - j, 1, k, W));
         const uint64_t stop = ~ballot(cont && inrange);
         if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
       }
@@ -719,6 +778,205 @@ __global__ __launch_bounds__(64) void dp_kernel(
     res.nindels = t.nindels;
     res.dynprogindex = dpi_next;
     results[pid] = res;
+  }
+}
+
+// ===========================================================================
+// dpx_kernel<S>: Dynprog_single_gap / Dynprog_end{5,3}_gap for narrow bands,
+// 64/S problems per wave.  Most sub-problems have band width <= 16
+// (extraband 6 around a near-square gap) or <= 32, so a whole 64-lane wave per
+// problem would leave 50-80 % of the lanes idle in the fill.  Here each S-lane
+// segment fills its own problem (fill_band<1, false, S>: row_shl/row_shr DPP
+// confined to the segment, segment-local F scan, S-bit direction words), and
+// the tracebacks -- short next to the fills -- then run one problem at a time
+// with the whole wave.  Semantics are those of dp_kernel.
+// ===========================================================================
+__host__ __device__ inline Carve carve_dpx(int rlength, int glength, int S) {
+  Carve cv;
+  size_t off = 0;
+  const size_t srow = (size_t)(rlength + 2);
+  cv.sc = off;   off = align16(off + (size_t)kNClass * srow);
+  cv.q = off;    off = align16(off + (size_t)(rlength + 1));
+  cv.quc = off;  off = align16(off + (size_t)(rlength + 1));
+  cv.gch = off;  off = align16(off + (size_t)(glength + 1));
+  cv.gcls = off; off = align16(off + (size_t)(glength + 1));
+  cv.dirs = off; off = align16(off + (size_t)(glength + 1) * 4u * (size_t)(S / 8));
+  cv.total = off;
+  return cv;
+}
+
+// Pair emission of one problem after its fill (the tail of dp_kernel): traceback or the
+// simple/no-gap diagonal, end-gap INDEL trimming and end5 reversal, the result record.
+template <typename WORD>
+__device__ __forceinline__ void finish_dp(int lane, const DevProblem& P, int pid, bool simple, int bestr, int bestc,
+                                          const WORD* dirs, const char* q, const char* quc, const char* gch,
+                                          const uint8_t* __restrict__ constab, const uint32_t* __restrict__ blocks,
+                                          uint64_t nwords, gmapdp_result* __restrict__ results,
+                                          gmapdp_pair* __restrict__ pairs) {
+  const int rlen = P.rlength, flags = P.flags, kind = P.kind, endalign = P.endalign;
+  const bool rev = flags & kFRev;
+  const bool is_end = kind != kSingle;
+  const uint8_t* cons = constab + (size_t)P.genestrand * 128 * kNClass;
+  gmapdp_pair* out = pairs + P.pair_offset;
+  const Geo G{P.roffset, P.goffset, rev ? -1 : 1};
+  const int dpi_next = P.dynprogindex + (P.dynprogindex > 0 ? 1 : -1);
+  Tally t = {0, 0, 0, 0, 0, 0, 0, false};
+  if (simple) {
+    // single_gap_simple: pushes r = 1..rlength without List_reverse: list order r = rlength .. 1
+    emit_diag(lane, rlen, rlen, rlen, G, q, quc, gch, cons, out, t);
+    if (lane == 0) {
+      gmapdp_result res;
+      res.npairs = t.count;
+      res.pair_offset = P.pair_offset;
+      res.traceback_score = t.nmatches * kMatch + t.nmismatches * kMismatch;
+      res.nmatches = t.nmatches;
+      res.nmismatches = t.nmismatches;
+      res.nopens = 0;
+      res.nindels = 0;
+      res.dynprogindex = dpi_next;
+      results[pid] = res;
+    }
+    return;
+  }
+  const bool skip = is_end && endalign != kQueryendNogaps && (flags & kFRequirePos);
+  if (is_end && endalign == kQueryendNogaps) {
+    emit_diag(lane, bestr, bestc, bestr, G, q, quc, gch, cons, out, t);  // traceback_nogaps
+  } else if (!skip) {
+    traceback_band<1, WORD>(lane, dirs, P.lband + P.uband + 1, P.uband, bestr, bestc, G, q, quc, gch, cons,
+                            flags & kFWatson, P.chroffset, P.chrhigh, blocks, nwords, out, t);
+  }
+  int score = t.score + t.nmatches * kMatch + t.nmismatches * kMismatch;
+  int first = 0, npairs = t.count;
+  if (is_end) {
+    if ((endalign == kQueryendGap || endalign == kBestLocal) && (t.nmatches + 1) < t.nmismatches) {
+      score = 0;  // dynprog_end.c:1623-1626: list dropped, counters kept
+      npairs = 0;
+    } else {
+      first = t.lead;  // INDEL pairs at the far end removed (dynprog_end.c:1629-1632)
+      npairs = t.count - t.lead;
+      if (kind == kEnd5 && npairs > 1) reverse_records(lane, out + first, npairs);  // dynprog_end.c:1646
+    }
+  }
+  if (lane == 0) {
+    gmapdp_result res;
+    res.npairs = npairs;
+    res.pair_offset = P.pair_offset + first;
+    res.traceback_score = score;
+    res.nmatches = t.nmatches;
+    res.nmismatches = t.nmismatches;
+    res.nopens = t.nopens;
+    res.nindels = t.nindels;
+    res.dynprogindex = dpi_next;
+    results[pid] = res;
+  }
+}
+
+template <int S>
+__global__ __launch_bounds__(64) void dpx_kernel(
+    const DevProblem* __restrict__ probs, const int* __restrict__ order, int count, int slot,
+    const uint32_t* __restrict__ blocks, uint64_t nwords,
+    const char* __restrict__ qseq, const char* __restrict__ qseq_uc,
+    const int8_t* __restrict__ sctab, const uint8_t* __restrict__ constab,
+    gmapdp_result* __restrict__ results, gmapdp_pair* __restrict__ pairs) {
+  using WORD = typename std::conditional<S == 16, uint16_t, uint32_t>::type;
+  constexpr int NP = 64 / S;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x;
+  const int seg = lane / S, sl = lane & (S - 1);
+  const int idx = blockIdx.x * NP + seg;
+  const bool live = idx < count;
+  const int pid = order[live ? idx : blockIdx.x * NP];
+  const DevProblem P = probs[pid];
+  const int rlen = live ? P.rlength : 0, glen = live ? P.glength : 0;
+  const int flags = P.flags;
+  const bool rev = flags & kFRev;
+  const int kind = P.kind, endalign = P.endalign;
+  const bool is_end = kind != kSingle;
+  unsigned char* base = smem + (size_t)seg * (size_t)slot;
+  const Carve cv = carve_dpx(rlen, glen, S);
+  int8_t* sc = reinterpret_cast<int8_t*>(base + cv.sc);
+  char* q = reinterpret_cast<char*>(base + cv.q);
+  char* quc = reinterpret_cast<char*>(base + cv.quc);
+  char* gch = reinterpret_cast<char*>(base + cv.gch);
+  uint8_t* gcl = reinterpret_cast<uint8_t*>(base + cv.gcls);
+  WORD* dirs = reinterpret_cast<WORD*>(base + cv.dirs);
+  const int8_t* sct = sctab + (size_t)P.mismatchtype * 128 * kNClass;
+  const uint8_t* cons = constab + (size_t)P.genestrand * 128 * kNClass;
+  const int srow = rlen + 2;
+
+  // ---- stage each segment's problem (as dp_kernel) ----
+  const int qstep = rev ? -1 : 1;
+  const bool score_uc = flags & kFScoreUC;
+  for (int i = sl; i < rlen; i += S) {
+    const char c1 = qseq[P.qbase + qstep * i];
+    const char c1u = qseq_uc[P.qbase + qstep * i];
+    q[i + 1] = c1;
+    quc[i + 1] = c1u;
+    const uint64_t row = *reinterpret_cast<const uint64_t*>(sct + (uint8_t)((score_uc ? c1u : c1) & 127) * kNClass);
+#pragma unroll
+    for (int g = 0; g < 6; g++) sc[g * srow + i + 1] = (int8_t)(row >> (8 * g));
+  }
+  if (live && sl < 6) {
+    sc[sl * srow] = 0;
+    sc[sl * srow + rlen + 1] = 0;
+  }
+  const bool segleft = flags & kFSegLeft, segrc = flags & kFSegRevcomp;
+  for (int i = sl; i < glen; i += S) {
+    const char c2 = segment_nt(blocks, nwords, (uint32_t)i, (uint32_t)glen, P.segpos, P.segbound, segleft, segrc);
+    const int c = rev ? glen - i : i + 1;
+    gch[c] = c2;
+    gcl[c] = gclass(c2);
+  }
+  __syncthreads();
+
+  // ---- single_gap_simple test per segment (glength == rlength, <= 1 mismatch) ----
+  const bool try_simple = live && kind == kSingle && glen == rlen;
+  int rmax = rlen;
+#pragma unroll
+  for (int off = S; off < 64; off <<= 1) rmax = max(rmax, __shfl_xor(rmax, off, 64));
+  int nmism = 0;
+  const uint64_t segmask = (S == 64 ? ~0ull : ((1ull << S) - 1ull)) << (seg * S);
+  for (int base0 = 0; base0 < rmax; base0 += S) {
+    const int r = base0 + sl + 1;
+    bool mism = false;
+    if (try_simple && r <= rlen) {
+      const char c1u = quc[r], c2 = gch[r];
+      mism = (c2 != '*') && (c1u != c2) && !cons[(uint8_t)(c1u & 127) * kNClass + gclass(c2)];
+    }
+    nmism += __popcll(ballot(mism) & segmask);
+  }
+  const bool simple = try_simple && nmism <= 1;
+
+  // ---- the segments' fills, side by side ----
+  const bool nogaps = is_end && endalign == kQueryendNogaps;
+  const bool fills = live && !simple && !nogaps;
+  const int gfill = fills ? glen : 0;
+  int gmax = gfill;
+#pragma unroll
+  for (int off = S; off < 64; off <<= 1) gmax = max(gmax, __shfl_xor(gmax, off, 64));
+  int bestr = 0, bestc = 0;
+  {
+    const int track = !is_end ? 0 : ((endalign == kQueryendIndels) ? 2 : 1);
+    fill_band<1, false, S, WORD>(lane, fills ? rlen : 0, gfill, P.lband, P.uband, P.open, P.extend,
+                                 (flags & kFLate) ? 1 : 0, fills ? track : 0, sc, srow, gcl, dirs, nullptr,
+                                 bestr, bestc, gmax);
+  }
+  if (nogaps) bestr = bestc = glen < rlen ? glen : rlen;  // find_best_endpoint_to_queryend_nogaps
+  __syncthreads();
+
+  // ---- emission, one problem at a time with the whole wave ----
+  for (int j = 0; j < NP; j++) {
+    const int src = j * S;
+    if (!__builtin_amdgcn_readlane((int)live, src)) continue;
+    const int pj = __builtin_amdgcn_readlane(pid, src);
+    const DevProblem Pj = probs[pj];
+    const Carve cj = carve_dpx(Pj.rlength, Pj.glength, S);
+    unsigned char* bj = smem + (size_t)j * (size_t)slot;
+    finish_dp<WORD>(lane, Pj, pj, __builtin_amdgcn_readlane((int)simple, src) != 0,
+                    __builtin_amdgcn_readlane(bestr, src), __builtin_amdgcn_readlane(bestc, src),
+                    reinterpret_cast<const WORD*>(bj + cj.dirs), reinterpret_cast<const char*>(bj + cj.q),
+                    reinterpret_cast<const char*>(bj + cj.quc), reinterpret_cast<const char*>(bj + cj.gch),
+                    constab, blocks, nwords, results, pairs);
   }
 }
 
@@ -1237,6 +1495,25 @@ hipError_t launch_dp(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
   }
   void* args[] = {(void*)&probs, (void*)&order, (void*)&blocks, (void*)&nwords, (void*)&qseq, (void*)&qseq_uc,
                   (void*)&sctab, (void*)&constab, (void*)&results, (void*)&pairs, (void*)&gdirs};
+  return hipLaunchKernel(fn, dim3(nblocks), dim3(64), args, lds, stream);
+}
+
+size_t lds_slot_dpx(int rlength, int glength, int S) { return carve_dpx(rlength, glength, S).total; }
+
+hipError_t launch_dpx(int S, int nproblems, int slot, hipStream_t stream, const DevProblem* probs, const int* order,
+                      const uint32_t* blocks, uint64_t nwords, const char* qseq, const char* qseq_uc,
+                      const int8_t* sctab, const uint8_t* constab, gmapdp_result* results, gmapdp_pair* pairs) {
+  void* fn = (S == 16) ? reinterpret_cast<void*>(&dpx_kernel<16>) : reinterpret_cast<void*>(&dpx_kernel<32>);
+  if (S != 16 && S != 32) return hipErrorInvalidValue;
+  const int np = 64 / S;
+  const size_t lds = (size_t)slot * np;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  const int nblocks = (nproblems + np - 1) / np;
+  void* args[] = {(void*)&probs, (void*)&order, (void*)&nproblems, (void*)&slot, (void*)&blocks, (void*)&nwords,
+                  (void*)&qseq, (void*)&qseq_uc, (void*)&sctab, (void*)&constab, (void*)&results, (void*)&pairs};
   return hipLaunchKernel(fn, dim3(nblocks), dim3(64), args, lds, stream);
 }
 

@@ -28,6 +28,10 @@ hipError_t launch_dp(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
                      const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
                      const char* qseq_uc, const int8_t* sctab, const uint8_t* constab, gmapdp_result* results,
                      gmapdp_pair* pairs, uint64_t* gdirs);
+size_t lds_slot_dpx(int rlength, int glength, int S);
+hipError_t launch_dpx(int S, int nproblems, int slot, hipStream_t stream, const DevProblem* probs, const int* order,
+                      const uint32_t* blocks, uint64_t nwords, const char* qseq, const char* qseq_uc,
+                      const int8_t* sctab, const uint8_t* constab, gmapdp_result* results, gmapdp_pair* pairs);
 size_t lds_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds);
 size_t scratch_bytes_gg(int glengthL, int glengthR, int R);
 hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevGenomeProblem* probs,
@@ -186,7 +190,7 @@ struct PlanCore {
   std::vector<DevGenomeProblem> gdev;  // Dynprog_genome_gap problems on the GPU
   std::vector<int> gdev_index;       // genome problem index -> gdev slot (-1: resolved on host)
   std::vector<int> gdev_problem;     // gdev slot -> genome problem index
-  enum Kind { kDp = 0, kGenomeGap = 1 };
+  enum Kind { kDp = 0, kGenomeGap = 1, kDpx = 2 };  // kDpx: 64/S narrow problems per wave, R = S
   struct Launch { int kind; int R; bool dirs_lds; size_t lds; int first, count; };
   std::vector<Launch> launches;
   std::vector<int> order;            // dev slots grouped by launch
@@ -353,6 +357,14 @@ static size_t lds_bucket(size_t lds) {
   for (size_t x : b)
     if (lds <= x) return x;
   return lds;
+}
+
+// per-problem LDS slot of the packed kernel (64/S slots per workgroup)
+static size_t slot_bucket(size_t b) {
+  static const size_t s[] = {1024, 1536, 2048, 3072, 4096, 6144, 8192, 12288, 16384};
+  for (size_t x : s)
+    if (b <= x) return x;
+  return 0;  // too big to pack
 }
 
 static void null_result(gmapdp_result& res, int score, int dpi) {
@@ -575,6 +587,15 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     if (d.open > 0 && !nofill) return bad(ctx, "positive gap-open penalty is not supported by the scan formulation");
     if (d.lband < 0 || d.uband < 0) return bad(ctx, "negative band");
     const int W = d.lband + d.uband + 1;
+    d.dirs_offset = 0;
+    if (nofill || W <= 32) {  // narrow band: pack 64/S problems per wave
+      const int S = (nofill || W <= 16) ? 16 : 32;
+      const size_t slot = slot_bucket(lds_slot_dpx(d.rlength, d.glength, S));
+      if (slot && slot * (64 / S) <= kLdsBudget) {
+        classes[std::make_tuple((int)PlanCore::kDpx, S, 1, slot)].push_back((int)s);
+        continue;
+      }
+    }
     const int R = nofill ? 1 : pick_R(W);
     if (R > kMaxR) return bad(ctx, "band wider than 4096");
     size_t lds = lds_bytes_dp(d.rlength, d.glength, R, !nofill);
@@ -619,7 +640,7 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     L.count = (int)kv.second.size();
     // longest problems first, so the tail of the launch is short work
     std::vector<int> ids = kv.second;
-    if (L.kind == PlanCore::kDp) {
+    if (L.kind != PlanCore::kGenomeGap) {
       std::stable_sort(ids.begin(), ids.end(), [&](int a, int b) {
         return (size_t)plan.dev[a].glength * (plan.dev[a].lband + plan.dev[a].uband + 1) >
                (size_t)plan.dev[b].glength * (plan.dev[b].lband + plan.dev[b].uband + 1);
@@ -682,6 +703,7 @@ static int build_plan(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int
 // A class too small to fill the chip (< 16 waves per CU) or made of wide / spilled
 // problems is latency-bound: it runs concurrently with the bulk on a side stream.
 static bool launch_is_tail(const PlanCore::Launch& L) {
+  if (L.kind == PlanCore::kDpx) return L.count < 4096;
   return L.count < 4096 || L.R > 1 || !L.dirs_lds;
 }
 
@@ -701,6 +723,9 @@ struct RunArgs {
 
 static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, const RunArgs& a, hipStream_t stream) {
   const auto& L = plan.launches[li];
+  if (L.kind == PlanCore::kDpx)
+    return launch_dpx(L.R, L.count, (int)L.lds, stream, a.d_probs, a.d_order + L.first, ctx->d_genome,
+                      ctx->genome_words, a.d_q, a.d_quc, ctx->d_sc, ctx->d_cs, a.d_results, a.d_pairs);
   if (L.kind == PlanCore::kDp)
     return launch_dp(L.R, L.dirs_lds, L.count, L.lds, stream, a.d_probs, a.d_order + L.first, ctx->d_genome,
                      ctx->genome_words, a.d_q, a.d_quc, ctx->d_sc, ctx->d_cs, a.d_results, a.d_pairs,
@@ -1058,7 +1083,7 @@ int gmapdp_plan_launch_members(const gmapdp_plan* plan, int li, int* problem_ind
   if (!plan || li < 0 || li >= (int)plan->in.launches.size() || !problem_indices) return GMAPDP_EINVAL;
   const auto& L = plan->in.launches[li];
   for (int k = 0; k < L.count; k++) {
-    if (L.kind == PlanCore::kDp) problem_indices[k] = plan->in.dev_problem[plan->in.order[L.first + k]];
+    if (L.kind != PlanCore::kGenomeGap) problem_indices[k] = plan->in.dev_problem[plan->in.order[L.first + k]];
     else problem_indices[k] = plan->nsingle + plan->nend + plan->in.gdev_problem[plan->in.gorder[L.first + k]];
   }
   return GMAPDP_OK;

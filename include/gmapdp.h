@@ -294,7 +294,9 @@ int gmapdp_plan_create_all (gmapdp_ctx *ctx, const gmapdp_single_problem *single
 int gmapdp_plan_bind_genome (gmapdp_plan *plan, const double *d_splice_probs, gmapdp_genome_result *d_genome_results);
 int gmapdp_plan_genome_gpu_problems (const gmapdp_plan *plan);
 int gmapdp_plan_genome_dev_index (const gmapdp_plan *plan, int j);
-/* 0: Dynprog_single_gap / end-gap kernel, 1: Dynprog_genome_gap kernel */
+/* 0: Dynprog_single_gap / end-gap kernel (one problem per wave), 1: Dynprog_genome_gap
+ * kernel, 2: packed single/end-gap kernel (64/S narrow-band problems per wave; for these
+ * gmapdp_plan_launch_info reports R = S and lds = the per-problem LDS slot) */
 int gmapdp_plan_launch_kind (const gmapdp_plan *plan, int li);
 size_t gmapdp_plan_pair_capacity (const gmapdp_plan *plan);
 int gmapdp_plan_gpu_problems (const gmapdp_plan *plan);
