@@ -529,7 +529,7 @@ def main():
                    "reads_per_step_per_gpu": args.reads, "subproblems_per_step_per_gpu": nprob,
                    "banded_cells_per_step_per_gpu": cells,
                    "parallelism": "dp%d (reads sharded by rank, genome replicated)" % world,
-                   "launch_classes": info},
+                   "launch_classes": info, "launch_ms": launch_ms},
         "gcups": cells * world * args.steps / elapsed / 1e9,
         "step_algorithmic_bytes": step_bytes,
     }

@@ -821,6 +821,10 @@ __device__ __forceinline__ void finish_dp(int lane, const DevProblem& P, int pid
   const Geo G{P.roffset, P.goffset, rev ? -1 : 1};
   const int dpi_next = P.dynprogindex + (P.dynprogindex > 0 ? 1 : -1);
   Tally t = {0, 0, 0, 0, 0, 0, 0, false};
+#ifdef GMAPDP_EXPERIMENT_NO_EMIT
+  if (lane == 0) results[pid].npairs = 0;  // timing experiment only: fills without the emission phase
+  return;
+#endif
   if (simple) {
     // single_gap_simple: pushes r = 1..rlength without List_reverse: list order r = rlength .. 1
     emit_diag(lane, rlen, rlen, rlen, G, q, quc, gch, cons, out, t);
