@@ -400,6 +400,7 @@ def main():
         P["nl"], P["info"] = nl, info
         P["kind"] = [lib.gmapdp_plan_launch_kind(plan, li) for li in range(nl)]
         P["tail"] = [lib.gmapdp_plan_launch_is_tail(plan, li) == 1 for li in range(nl)]
+        P["stream"] = [lib.gmapdp_plan_launch_stream(plan, li) for li in range(nl)]
         return P
 
     # Same issue order as gmapdp_plan_run: tail classes (long problems, latency-bound) on side
@@ -418,30 +419,25 @@ def main():
                        "gmapdp_plan_run_launch")
 
         def step(ev=None):
+            # the engine's schedule (gmapdp_plan_run): launches in issue order, each on its assigned
+            # stream (0 = main, 1..3 = sides) after a fork from the main stream, joined at the end;
             # per-dispatch events on the stream each launch runs on (what rocprofv3's kernel trace times)
             fork = torch.cuda.Event()
             fork.record(stream)
-            used = 0
+            used = set()
             for li in range(nl):
-                if tail[li]:
-                    s = sides[used % len(sides)]
+                k = P["stream"][li]
+                s = stream if k == 0 else sides[k - 1]
+                if k and k not in used:
                     s.wait_event(fork)
-                    if ev is not None:
-                        ev[li][0].record(s)
-                    launch(li, s)
-                    if ev is not None:
-                        ev[li][1].record(s)
-                    used += 1
-            for li in range(nl):
-                if tail[li]:
-                    continue
+                    used.add(k)
                 if ev is not None:
-                    ev[li][0].record(stream)
-                launch(li, stream)
+                    ev[li][0].record(s)
+                launch(li, s)
                 if ev is not None:
-                    ev[li][1].record(stream)
-            for s in sides[:used]:
-                stream.wait_stream(s)
+                    ev[li][1].record(s)
+            for k in used:
+                stream.wait_stream(sides[k - 1])
 
         with torch.cuda.stream(stream):
             for _ in range(warmup):

@@ -37,7 +37,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <type_traits>
 
 #include "gmapdp_internal.h"
 #include "../../include/gmapdp.h"
@@ -180,11 +179,12 @@ __host__ __device__ inline Carve carve_dp(int rlength, int glength, int R, bool 
 
 // direction planes: [c][t][i] 64-bit masks; t: 0 nogap=HORIZ, 1 nogap=VERT, 2 Egap=HORIZ, 3 Fgap=VERT;
 // band offset k lives in word i = k % R at bit k / R.
+// bitoff: first bit of the problem's segment when a packed wave stores whole-wave ballots
 template <int R, typename WORD = uint64_t>
-__device__ __forceinline__ uint32_t dir_bit(const WORD* dirs, int c, int t, int k, int W) {
+__device__ __forceinline__ uint32_t dir_bit(const WORD* dirs, int c, int t, int k, int W, int bitoff = 0) {
   if (k < 0 || k >= W) return 0u;  // outside the band: cleared to DIAG (dynprog.c:498)
   const WORD m = dirs[((size_t)c * 4 + t) * R + (k % R)];
-  return (uint32_t)(m >> (k / R)) & 1u;
+  return (uint32_t)(m >> (k / R + bitoff)) & 1u;
 }
 
 struct Tally {
@@ -351,16 +351,16 @@ struct Part {
 };
 
 // S < 64: the wave holds 64/S problems, one per S-lane segment (R must be 1); every argument
-// is then per segment, `gmax` is the wave's largest glength and a segment's direction words are
-// its S ballot bits (WORD = uint16_t / uint32_t), written by the segment's first lane.
-template <int R, bool CARRY, int S = 64, typename WORD = uint64_t>
+// is then per segment, `gmax` is the wave's largest glength, the score rows are transposed
+// (sc[r*8 + class], no per-column multiply) and lane 0 stores the whole-wave ballots (segment j
+// owns bits [j*S, j*S+S) of each word).
+template <int R, bool CARRY, int S = 64>
 __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lband, int uband, int open, int ext,
                                           int late, int track, const int8_t* sc, int srow, const uint8_t* gcl,
-                                          WORD* dirs, const BridgeCarry* bc_, int& bestr, int& bestc,
+                                          uint64_t* dirs, const BridgeCarry* bc_, int& bestr, int& bestc,
                                           int gmax = 0) {
   static_assert(S == 64 || (R == 1 && !CARRY), "segmented fills are single-word, no bridge carry");
   const int lk = (S == 64) ? lane : (lane & (S - 1));  // lane within the segment
-  const int segshift = lane - lk;                      // first ballot bit of the segment
   const int cend = (S == 64) ? glen : gmax;
   const int sat = kNegInf32;
   const int W = lband + uband + 1;
@@ -390,18 +390,29 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
     cc[i] = -1;
     cp[i] = 0.0;
   }
+  int rtop_ext = -uband * ext;  // (c - uband) * ext, advanced by ext per column
+  int oce = open;               // open + c * ext
+  int gi_next = (S == 64) ? 0 : gcl[min(1, glen)];
   for (int c = 1; c <= cend; c++) {
     const bool colact = (S == 64) || (c <= glen);
-    // genome class: wave-uniform (SGPR) for one problem per wave, per segment otherwise
-    const int gi = (S == 64) ? __builtin_amdgcn_readfirstlane(gcl[c]) : gcl[min(c, glen)];
+    // genome class: wave-uniform (SGPR) for one problem per wave; per segment otherwise, read one
+    // column ahead so the LDS latency is off the column's dependency chain
+    int gi;
+    if constexpr (S == 64) {
+      gi = __builtin_amdgcn_readfirstlane(gcl[c]);
+    } else {
+      gi = gi_next;
+      gi_next = gcl[min(c + 1, glen)];
+    }
     const int rtop = c - uband;
     const int rlo = rtop < 1 ? 1 : rtop;
     const int rhigh = (c + lband) < rlen ? (c + lband) : rlen;
-    const int rtop_ext = rtop * ext;
+    rtop_ext += ext;
+    oce += ext;
     // last_nogap entering row rlo (dynprog.c:1411-1449)
-    const int L0 = (c == 1) ? (kNegInf32 - open + 1) : (c <= uband ? open + c * ext : kNegInf32);
-    const int row0 = (c <= uband) ? open + c * ext : kNegInf32;  // row 0 of this column (dynprog.c:1318-1325)
-    const int8_t* scg = sc + gi * srow;
+    const int L0 = (c == 1) ? (kNegInf32 - open + 1) : (c <= uband ? oce : kNegInf32);
+    const int row0 = (c <= uband) ? oce : kNegInf32;  // row 0 of this column (dynprog.c:1318-1325)
+    const int8_t* scg = (S == 64) ? sc + gi * srow : sc + gi;
 
     int Ein[R], Hin[R];
 #pragma unroll
@@ -416,7 +427,8 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
       const int k = lk * R + i;
       const int r = rtop + k;
       valid[i] = (k < W) & (r >= rlo) & (r <= rhigh) & colact;
-      const int s = scg[min(max(r, 0), rlen + 1)];
+      const int rr = min(max(r, 0), rlen + 1);
+      const int s = (S == 64) ? scg[rr] : scg[rr << 3];
       // Egap (dynprog.c:1518-1524)
       const int es = Hin[i] + open;
       eb[i] = Ein[i] > es - late;
@@ -432,7 +444,7 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
 #pragma unroll
     for (int i = 1; i < R; i++) pre[i] = max(pre[i - 1], A[i]);
     const int X = seg_shr1<S>(seg_scan_max<S>(pre[R - 1]), kSent, lk);
-    const int init = max(kNegInf32, L0 + open) - (rlo - 1) * ext;
+    const int init = max(kNegInf32, L0 + open) - ((rtop > 1) ? rtop_ext - ext : 0);  // (rlo - 1) * ext
     int F[R], Hun[R];
     bool vb[R];
 #pragma unroll
@@ -454,10 +466,11 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
       const int fprev = top ? kNegInf32 : ((i == 0) ? Fup : F[i - 1]);
       const int hprev = top ? L0 : ((i == 0) ? Hup : Hun[i - 1]);
       const bool fb = fprev > hprev + open - late;
-      mV[i] = ballot(valid[i] & vb[i]);
-      mH[i] = ballot(valid[i] & hb[i] & !vb[i]);
-      mE[i] = ballot(valid[i] & eb[i]);
-      mF[i] = ballot(valid[i] & fb);
+      const uint64_t mvalid = ballot(valid[i]);
+      mV[i] = ballot(vb[i]) & mvalid;
+      mH[i] = ballot(hb[i]) & ~mV[i] & mvalid;
+      mE[i] = ballot(eb[i]) & mvalid;
+      mF[i] = ballot(fb) & mvalid;
       const int Hc = max(Hun[i], sat);
       // branch-free state update for the next column
       Hs[i] = valid[i] ? ((k == 0) ? Hun[i] : Hc) : ((r == 0) ? row0 : kNegInf32);
@@ -511,14 +524,14 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
         }
       }
     }
-    if (lk == 0 && colact) {  // one lane per problem stores the column's 4R direction words
-      WORD* dcol = dirs + (size_t)c * 4 * R;
+    if (lane == 0) {  // one lane stores the column's 4R direction words
+      uint64_t* dcol = dirs + (size_t)c * 4 * R;
 #pragma unroll
       for (int i = 0; i < R; i++) {
-        dcol[0 * R + i] = (WORD)(mH[i] >> segshift);
-        dcol[1 * R + i] = (WORD)(mV[i] >> segshift);
-        dcol[2 * R + i] = (WORD)(mE[i] >> segshift);
-        dcol[3 * R + i] = (WORD)(mF[i] >> segshift);
+        dcol[0 * R + i] = mH[i];
+        dcol[1 * R + i] = mV[i];
+        dcol[2 * R + i] = mE[i];
+        dcol[3 * R + i] = mF[i];
       }
     }
   }
@@ -571,17 +584,17 @@ __device__ __forceinline__ void traceback_band(int lane, const WORD* dirs, int W
                                                const Geo& G, const char* q, const char* quc, const char* gch,
                                                const uint8_t* __restrict__ cons, bool watson, uint32_t chroffset,
                                                uint32_t chrhigh, const uint32_t* __restrict__ blocks,
-                                               uint64_t nwords, gmapdp_pair* out, Tally& t) {
+                                               uint64_t nwords, gmapdp_pair* out, Tally& t, int bitoff = 0) {
   while (r > 0 && c > 0) {
     const int k = r - c + uband;
-    const uint32_t isV = dir_bit<R, WORD>(dirs, c, 1, k, W);
-    const uint32_t isH = dir_bit<R, WORD>(dirs, c, 0, k, W);
+    const uint32_t isV = dir_bit<R, WORD>(dirs, c, 1, k, W, bitoff);
+    const uint32_t isH = dir_bit<R, WORD>(dirs, c, 0, k, W, bitoff);
     if (!isV && isH) {
       // E chain along row r: columns c, c-1, ... while Egap == HORIZ
       int n = 0;
       for (int base = 0;; base += 64) {
         const int j = base + lane;
-        const bool cont = (c - j >= 1) && dir_bit<R, WORD>(dirs, c - j, 2, k + j, W);
+        const bool cont = (c - j >= 1) && dir_bit<R, WORD>(dirs, c - j, 2, k + j, W, bitoff);
         const uint64_t stop = ~ballot(cont);
         if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
       }
@@ -594,7 +607,7 @@ __device__ __forceinline__ void traceback_band(int lane, const WORD* dirs, int W
       int n = 0;
       for (int base = 0;; base += 64) {
         const int j = base + lane;
-        const bool cont = (r - j >= 1) && dir_bit<R, WORD>(dirs, c, 3, k - j, W);
+        const bool cont = (r - j >= 1) && dir_bit<R, WORD>(dirs, c, 3, k - j, W, bitoff);
         const uint64_t stop = ~ballot(cont);
         if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
       }
@@ -608,8 +621,8 @@ __device__ __forceinline__ void traceback_band(int lane, const WORD* dirs, int W
       for (int base = 0;; base += 64) {
         const int j = base + lane;
         const bool inrange = (c - j >= 1) && (r - j >= 1);
-        const bool cont = (j == 0) || (inrange && !dir_bit<R, WORD>(dirs, c - j, 0, k, W) &&
-                                       !dir_bit<R, WORD>(dirs, c - j, 1, k, W));
+        const bool cont = (j == 0) || (inrange && !dir_bit<R, WORD>(dirs, c - j, 0, k, W, bitoff) &&
+                                       !dir_bit<R, WORD>(dirs, c - j, 1, k, W, bitoff));
         const uint64_t stop = ~ballot(cont && inrange);
         if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
       }
@@ -791,25 +804,27 @@ __global__ __launch_bounds__(64) void dp_kernel(
 // the tracebacks -- short next to the fills -- then run one problem at a time
 // with the whole wave.  Semantics are those of dp_kernel.
 // ===========================================================================
-__host__ __device__ inline Carve carve_dpx(int rlength, int glength, int S) {
+// Per-problem LDS slot of the packed kernel: transposed score rows sc[r][8] (rows 0..rlength+1),
+// query, upper-cased query, genome characters and classes.  The direction words of the whole
+// wave (4 x u64 per column) precede the slots.
+__host__ __device__ inline Carve carve_dpx(int rlength, int glength) {
   Carve cv;
   size_t off = 0;
-  const size_t srow = (size_t)(rlength + 2);
-  cv.sc = off;   off = align16(off + (size_t)kNClass * srow);
+  cv.sc = off;   off = align16(off + 8u * (size_t)(rlength + 2));
   cv.q = off;    off = align16(off + (size_t)(rlength + 1));
   cv.quc = off;  off = align16(off + (size_t)(rlength + 1));
   cv.gch = off;  off = align16(off + (size_t)(glength + 1));
-  cv.gcls = off; off = align16(off + (size_t)(glength + 1));
-  cv.dirs = off; off = align16(off + (size_t)(glength + 1) * 4u * (size_t)(S / 8));
+  cv.gcls = off; off = align16(off + (size_t)(glength + 2));
+  cv.dirs = 0;
   cv.total = off;
   return cv;
 }
 
 // Pair emission of one problem after its fill (the tail of dp_kernel): traceback or the
 // simple/no-gap diagonal, end-gap INDEL trimming and end5 reversal, the result record.
-template <typename WORD>
 __device__ __forceinline__ void finish_dp(int lane, const DevProblem& P, int pid, bool simple, int bestr, int bestc,
-                                          const WORD* dirs, const char* q, const char* quc, const char* gch,
+                                          const uint64_t* dirs, int bitoff, const char* q, const char* quc,
+                                          const char* gch,
                                           const uint8_t* __restrict__ constab, const uint32_t* __restrict__ blocks,
                                           uint64_t nwords, gmapdp_result* __restrict__ results,
                                           gmapdp_pair* __restrict__ pairs) {
@@ -846,8 +861,8 @@ __device__ __forceinline__ void finish_dp(int lane, const DevProblem& P, int pid
   if (is_end && endalign == kQueryendNogaps) {
     emit_diag(lane, bestr, bestc, bestr, G, q, quc, gch, cons, out, t);  // traceback_nogaps
   } else if (!skip) {
-    traceback_band<1, WORD>(lane, dirs, P.lband + P.uband + 1, P.uband, bestr, bestc, G, q, quc, gch, cons,
-                            flags & kFWatson, P.chroffset, P.chrhigh, blocks, nwords, out, t);
+    traceback_band<1>(lane, dirs, P.lband + P.uband + 1, P.uband, bestr, bestc, G, q, quc, gch, cons,
+                      flags & kFWatson, P.chroffset, P.chrhigh, blocks, nwords, out, t, bitoff);
   }
   int score = t.score + t.nmatches * kMatch + t.nmismatches * kMismatch;
   int first = 0, npairs = t.count;
@@ -877,12 +892,11 @@ __device__ __forceinline__ void finish_dp(int lane, const DevProblem& P, int pid
 
 template <int S>
 __global__ __launch_bounds__(64) void dpx_kernel(
-    const DevProblem* __restrict__ probs, const int* __restrict__ order, int count, int slot,
+    const DevProblem* __restrict__ probs, const int* __restrict__ order, int count, int slot, int dirs_bytes,
     const uint32_t* __restrict__ blocks, uint64_t nwords,
     const char* __restrict__ qseq, const char* __restrict__ qseq_uc,
     const int8_t* __restrict__ sctab, const uint8_t* __restrict__ constab,
     gmapdp_result* __restrict__ results, gmapdp_pair* __restrict__ pairs) {
-  using WORD = typename std::conditional<S == 16, uint16_t, uint32_t>::type;
   constexpr int NP = 64 / S;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x;
@@ -896,19 +910,18 @@ __global__ __launch_bounds__(64) void dpx_kernel(
   const bool rev = flags & kFRev;
   const int kind = P.kind, endalign = P.endalign;
   const bool is_end = kind != kSingle;
-  unsigned char* base = smem + (size_t)seg * (size_t)slot;
-  const Carve cv = carve_dpx(rlen, glen, S);
+  uint64_t* wdirs = reinterpret_cast<uint64_t*>(smem);
+  unsigned char* base = smem + dirs_bytes + (size_t)seg * (size_t)slot;
+  const Carve cv = carve_dpx(rlen, glen);
   int8_t* sc = reinterpret_cast<int8_t*>(base + cv.sc);
   char* q = reinterpret_cast<char*>(base + cv.q);
   char* quc = reinterpret_cast<char*>(base + cv.quc);
   char* gch = reinterpret_cast<char*>(base + cv.gch);
   uint8_t* gcl = reinterpret_cast<uint8_t*>(base + cv.gcls);
-  WORD* dirs = reinterpret_cast<WORD*>(base + cv.dirs);
   const int8_t* sct = sctab + (size_t)P.mismatchtype * 128 * kNClass;
   const uint8_t* cons = constab + (size_t)P.genestrand * 128 * kNClass;
-  const int srow = rlen + 2;
 
-  // ---- stage each segment's problem (as dp_kernel) ----
+  // ---- stage each segment's problem: per query row one 8-byte score vector (by genome class) ----
   const int qstep = rev ? -1 : 1;
   const bool score_uc = flags & kFScoreUC;
   for (int i = sl; i < rlen; i += S) {
@@ -916,14 +929,10 @@ __global__ __launch_bounds__(64) void dpx_kernel(
     const char c1u = qseq_uc[P.qbase + qstep * i];
     q[i + 1] = c1;
     quc[i + 1] = c1u;
-    const uint64_t row = *reinterpret_cast<const uint64_t*>(sct + (uint8_t)((score_uc ? c1u : c1) & 127) * kNClass);
-#pragma unroll
-    for (int g = 0; g < 6; g++) sc[g * srow + i + 1] = (int8_t)(row >> (8 * g));
+    *reinterpret_cast<uint64_t*>(sc + 8 * (i + 1)) =
+        *reinterpret_cast<const uint64_t*>(sct + (uint8_t)((score_uc ? c1u : c1) & 127) * kNClass);
   }
-  if (live && sl < 6) {
-    sc[sl * srow] = 0;
-    sc[sl * srow + rlen + 1] = 0;
-  }
+  if (live && sl < 2) *reinterpret_cast<uint64_t*>(sc + 8 * (sl ? rlen + 1 : 0)) = 0ull;  // rows 0, rlength+1
   const bool segleft = flags & kFSegLeft, segrc = flags & kFSegRevcomp;
   for (int i = sl; i < glen; i += S) {
     const char c2 = segment_nt(blocks, nwords, (uint32_t)i, (uint32_t)glen, P.segpos, P.segbound, segleft, segrc);
@@ -939,7 +948,7 @@ __global__ __launch_bounds__(64) void dpx_kernel(
 #pragma unroll
   for (int off = S; off < 64; off <<= 1) rmax = max(rmax, __shfl_xor(rmax, off, 64));
   int nmism = 0;
-  const uint64_t segmask = (S == 64 ? ~0ull : ((1ull << S) - 1ull)) << (seg * S);
+  const uint64_t segmask = ((1ull << S) - 1ull) << (seg * S);
   for (int base0 = 0; base0 < rmax; base0 += S) {
     const int r = base0 + sl + 1;
     bool mism = false;
@@ -961,9 +970,9 @@ __global__ __launch_bounds__(64) void dpx_kernel(
   int bestr = 0, bestc = 0;
   {
     const int track = !is_end ? 0 : ((endalign == kQueryendIndels) ? 2 : 1);
-    fill_band<1, false, S, WORD>(lane, fills ? rlen : 0, gfill, P.lband, P.uband, P.open, P.extend,
-                                 (flags & kFLate) ? 1 : 0, fills ? track : 0, sc, srow, gcl, dirs, nullptr,
-                                 bestr, bestc, gmax);
+    fill_band<1, false, S>(lane, fills ? rlen : 0, gfill, P.lband, P.uband, P.open, P.extend,
+                           (flags & kFLate) ? 1 : 0, fills ? track : 0, sc, 8, gcl, wdirs, nullptr, bestr, bestc,
+                           gmax);
   }
   if (nogaps) bestr = bestc = glen < rlen ? glen : rlen;  // find_best_endpoint_to_queryend_nogaps
   __syncthreads();
@@ -974,13 +983,12 @@ __global__ __launch_bounds__(64) void dpx_kernel(
     if (!__builtin_amdgcn_readlane((int)live, src)) continue;
     const int pj = __builtin_amdgcn_readlane(pid, src);
     const DevProblem Pj = probs[pj];
-    const Carve cj = carve_dpx(Pj.rlength, Pj.glength, S);
-    unsigned char* bj = smem + (size_t)j * (size_t)slot;
-    finish_dp<WORD>(lane, Pj, pj, __builtin_amdgcn_readlane((int)simple, src) != 0,
-                    __builtin_amdgcn_readlane(bestr, src), __builtin_amdgcn_readlane(bestc, src),
-                    reinterpret_cast<const WORD*>(bj + cj.dirs), reinterpret_cast<const char*>(bj + cj.q),
-                    reinterpret_cast<const char*>(bj + cj.quc), reinterpret_cast<const char*>(bj + cj.gch),
-                    constab, blocks, nwords, results, pairs);
+    const Carve cj = carve_dpx(Pj.rlength, Pj.glength);
+    unsigned char* bj = smem + dirs_bytes + (size_t)j * (size_t)slot;
+    finish_dp(lane, Pj, pj, __builtin_amdgcn_readlane((int)simple, src) != 0,
+              __builtin_amdgcn_readlane(bestr, src), __builtin_amdgcn_readlane(bestc, src), wdirs, src,
+              reinterpret_cast<const char*>(bj + cj.q), reinterpret_cast<const char*>(bj + cj.quc),
+              reinterpret_cast<const char*>(bj + cj.gch), constab, blocks, nwords, results, pairs);
   }
 }
 
@@ -1502,22 +1510,25 @@ hipError_t launch_dp(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
   return hipLaunchKernel(fn, dim3(nblocks), dim3(64), args, lds, stream);
 }
 
-size_t lds_slot_dpx(int rlength, int glength, int S) { return carve_dpx(rlength, glength, S).total; }
+size_t lds_slot_dpx(int rlength, int glength) { return carve_dpx(rlength, glength).total; }
+size_t lds_dirs_dpx(int gmax) { return align16((size_t)(gmax + 1) * 4u * 8u); }
 
-hipError_t launch_dpx(int S, int nproblems, int slot, hipStream_t stream, const DevProblem* probs, const int* order,
-                      const uint32_t* blocks, uint64_t nwords, const char* qseq, const char* qseq_uc,
-                      const int8_t* sctab, const uint8_t* constab, gmapdp_result* results, gmapdp_pair* pairs) {
-  void* fn = (S == 16) ? reinterpret_cast<void*>(&dpx_kernel<16>) : reinterpret_cast<void*>(&dpx_kernel<32>);
+hipError_t launch_dpx(int S, int nproblems, int slot, int dirs_bytes, hipStream_t stream, const DevProblem* probs,
+                      const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
+                      const char* qseq_uc, const int8_t* sctab, const uint8_t* constab, gmapdp_result* results,
+                      gmapdp_pair* pairs) {
   if (S != 16 && S != 32) return hipErrorInvalidValue;
+  void* fn = (S == 16) ? reinterpret_cast<void*>(&dpx_kernel<16>) : reinterpret_cast<void*>(&dpx_kernel<32>);
   const int np = 64 / S;
-  const size_t lds = (size_t)slot * np;
+  const size_t lds = (size_t)dirs_bytes + (size_t)slot * np;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
   const int nblocks = (nproblems + np - 1) / np;
-  void* args[] = {(void*)&probs, (void*)&order, (void*)&nproblems, (void*)&slot, (void*)&blocks, (void*)&nwords,
-                  (void*)&qseq, (void*)&qseq_uc, (void*)&sctab, (void*)&constab, (void*)&results, (void*)&pairs};
+  void* args[] = {(void*)&probs, (void*)&order, (void*)&nproblems, (void*)&slot, (void*)&dirs_bytes,
+                  (void*)&blocks, (void*)&nwords, (void*)&qseq, (void*)&qseq_uc, (void*)&sctab, (void*)&constab,
+                  (void*)&results, (void*)&pairs};
   return hipLaunchKernel(fn, dim3(nblocks), dim3(64), args, lds, stream);
 }
 

@@ -28,10 +28,12 @@ hipError_t launch_dp(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
                      const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
                      const char* qseq_uc, const int8_t* sctab, const uint8_t* constab, gmapdp_result* results,
                      gmapdp_pair* pairs, uint64_t* gdirs);
-size_t lds_slot_dpx(int rlength, int glength, int S);
-hipError_t launch_dpx(int S, int nproblems, int slot, hipStream_t stream, const DevProblem* probs, const int* order,
-                      const uint32_t* blocks, uint64_t nwords, const char* qseq, const char* qseq_uc,
-                      const int8_t* sctab, const uint8_t* constab, gmapdp_result* results, gmapdp_pair* pairs);
+size_t lds_slot_dpx(int rlength, int glength);
+size_t lds_dirs_dpx(int gmax);
+hipError_t launch_dpx(int S, int nproblems, int slot, int dirs_bytes, hipStream_t stream, const DevProblem* probs,
+                      const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
+                      const char* qseq_uc, const int8_t* sctab, const uint8_t* constab, gmapdp_result* results,
+                      gmapdp_pair* pairs);
 size_t lds_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds);
 size_t scratch_bytes_gg(int glengthL, int glengthR, int R);
 hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevGenomeProblem* probs,
@@ -191,7 +193,16 @@ struct PlanCore {
   std::vector<int> gdev_index;       // genome problem index -> gdev slot (-1: resolved on host)
   std::vector<int> gdev_problem;     // gdev slot -> genome problem index
   enum Kind { kDp = 0, kGenomeGap = 1, kDpx = 2 };  // kDpx: 64/S narrow problems per wave, R = S
-  struct Launch { int kind; int R; bool dirs_lds; size_t lds; int first, count; };
+  struct Launch {
+    int kind;
+    int R;           // band words per lane (kDp, kGenomeGap) or segment width S (kDpx)
+    bool dirs_lds;
+    size_t lds;      // LDS bucket per workgroup (kDpx: per problem slot)
+    int first, count;
+    double work;     // estimated wave-columns, for stream assignment
+    size_t extra;    // kDpx: bytes of the whole-wave direction words ahead of the slots
+    int stream;      // 0: the caller's stream, 1..3: the context's side streams
+  };
   std::vector<Launch> launches;
   std::vector<int> order;            // dev slots grouped by launch
   std::vector<int> gorder;           // gdev slots grouped by launch
@@ -590,8 +601,8 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     d.dirs_offset = 0;
     if (nofill || W <= 32) {  // narrow band: pack 64/S problems per wave
       const int S = (nofill || W <= 16) ? 16 : 32;
-      const size_t slot = slot_bucket(lds_slot_dpx(d.rlength, d.glength, S));
-      if (slot && slot * (64 / S) <= kLdsBudget) {
+      const size_t slot = slot_bucket(lds_slot_dpx(d.rlength, d.glength));
+      if (slot && slot * (64 / S) + lds_dirs_dpx(d.glength) <= kLdsBudget) {
         classes[std::make_tuple((int)PlanCore::kDpx, S, 1, slot)].push_back((int)s);
         continue;
       }
@@ -656,7 +667,48 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
       L.first = (int)plan.gorder.size();
       plan.gorder.insert(plan.gorder.end(), ids.begin(), ids.end());
     }
+    // work estimate: fill wave-columns (a packed wave fills 64/S problems at once)
+    L.work = 0.0;
+    L.extra = 0;
+    if (L.kind == PlanCore::kDpx) {
+      int gmax = 0;
+      for (int id : ids) gmax = std::max(gmax, (int)plan.dev[id].glength);
+      L.extra = lds_dirs_dpx(gmax);
+    }
+    for (int id : ids) {
+      if (L.kind == PlanCore::kGenomeGap) {
+        const DevGenomeProblem& d = plan.gdev[id];
+        L.work += (double)std::max(d.glengthL, d.glengthR) * L.R + d.rlength;
+      } else {
+        const DevProblem& d = plan.dev[id];
+        L.work += (double)d.glength * (L.kind == PlanCore::kDpx ? L.R / 64.0 : L.R) + 0.25 * (d.rlength + d.glength);
+      }
+    }
+    L.stream = 0;
     plan.launches.push_back(L);
+  }
+  // Independent classes share the GPU: longest-processing-time-first over the caller's stream and
+  // the three side streams, so that LDS-heavy and LDS-light classes are co-resident on the CUs and
+  // no launch's drain leaves the chip idle.  Launches are then kept in issue order (per stream,
+  // largest first).
+  {
+    std::vector<int> idx(plan.launches.size());
+    for (size_t i = 0; i < idx.size(); i++) idx[i] = (int)i;
+    std::stable_sort(idx.begin(), idx.end(),
+                     [&](int a, int b) { return plan.launches[a].work > plan.launches[b].work; });
+    double load[1 + gmapdp_ctx::kAux] = {0.0, 0.0, 0.0, 0.0};
+    for (int i : idx) {
+      int best = 0;
+      for (int k = 1; k <= gmapdp_ctx::kAux; k++)
+        if (load[k] < load[best]) best = k;
+      plan.launches[i].stream = best;
+      load[best] += plan.launches[i].work;
+    }
+    std::vector<PlanCore::Launch> sorted;
+    for (int k = 0; k <= gmapdp_ctx::kAux; k++)
+      for (int i : idx)
+        if (plan.launches[i].stream == k) sorted.push_back(plan.launches[i]);
+    plan.launches.swap(sorted);
   }
   plan.pair_capacity = pair_off;
   plan.gdirs_bytes = gdirs_off;
@@ -700,12 +752,8 @@ static int build_plan(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int
   return GMAPDP_OK;
 }
 
-// A class too small to fill the chip (< 16 waves per CU) or made of wide / spilled
-// problems is latency-bound: it runs concurrently with the bulk on a side stream.
-static bool launch_is_tail(const PlanCore::Launch& L) {
-  if (L.kind == PlanCore::kDpx) return L.count < 4096;
-  return L.count < 4096 || L.R > 1 || !L.dirs_lds;
-}
+// Launches assigned to a side stream run concurrently with those on the caller's stream.
+static bool launch_is_tail(const PlanCore::Launch& L) { return L.stream != 0; }
 
 // Device-side inputs of one plan execution.
 struct RunArgs {
@@ -724,8 +772,9 @@ struct RunArgs {
 static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, const RunArgs& a, hipStream_t stream) {
   const auto& L = plan.launches[li];
   if (L.kind == PlanCore::kDpx)
-    return launch_dpx(L.R, L.count, (int)L.lds, stream, a.d_probs, a.d_order + L.first, ctx->d_genome,
-                      ctx->genome_words, a.d_q, a.d_quc, ctx->d_sc, ctx->d_cs, a.d_results, a.d_pairs);
+    return launch_dpx(L.R, L.count, (int)L.lds, (int)L.extra, stream, a.d_probs, a.d_order + L.first,
+                      ctx->d_genome, ctx->genome_words, a.d_q, a.d_quc, ctx->d_sc, ctx->d_cs, a.d_results,
+                      a.d_pairs);
   if (L.kind == PlanCore::kDp)
     return launch_dp(L.R, L.dirs_lds, L.count, L.lds, stream, a.d_probs, a.d_order + L.first, ctx->d_genome,
                      ctx->genome_words, a.d_q, a.d_quc, ctx->d_sc, ctx->d_cs, a.d_results, a.d_pairs,
@@ -741,22 +790,22 @@ static int run_plan(gmapdp_ctx* ctx, const PlanCore& plan, const RunArgs& a, hip
     hipError_t e = ctx->gdirs.ensure(plan.gdirs_bytes);
     if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "direction scratch: %s", e);
   }
-  // Tail classes (long problems) fork onto side streams first, the bulk follows on `stream`,
-  // then `stream` joins the side streams: the step ends when the slower of the two ends.
+  // Fork: the side streams wait for everything already queued on `stream`; each launch goes to
+  // its assigned stream; join: `stream` waits for the side streams.
   hipError_t e = hipEventRecord(ctx->ev_fork, stream);
-  int naux = 0;
+  bool used[gmapdp_ctx::kAux] = {false, false, false};
   for (size_t li = 0; li < plan.launches.size() && e == hipSuccess; li++) {
-    if (!launch_is_tail(plan.launches[li])) continue;
-    hipStream_t s = ctx->aux[naux % gmapdp_ctx::kAux];
-    if (naux < gmapdp_ctx::kAux) e = hipStreamWaitEvent(s, ctx->ev_fork, 0);
+    const int k = plan.launches[li].stream;
+    hipStream_t s = stream;
+    if (k > 0) {
+      s = ctx->aux[k - 1];
+      if (!used[k - 1]) e = hipStreamWaitEvent(s, ctx->ev_fork, 0);
+      used[k - 1] = true;
+    }
     if (e == hipSuccess) e = launch_one(ctx, plan, (int)li, a, s);
-    naux++;
   }
-  for (size_t li = 0; li < plan.launches.size() && e == hipSuccess; li++) {
-    if (launch_is_tail(plan.launches[li])) continue;
-    e = launch_one(ctx, plan, (int)li, a, stream);
-  }
-  for (int i = 0; i < naux && i < gmapdp_ctx::kAux && e == hipSuccess; i++) {
+  for (int i = 0; i < gmapdp_ctx::kAux && e == hipSuccess; i++) {
+    if (!used[i]) continue;
     e = hipEventRecord(ctx->ev_join[i], ctx->aux[i]);
     if (e == hipSuccess) e = hipStreamWaitEvent(stream, ctx->ev_join[i], 0);
   }
@@ -1072,6 +1121,11 @@ int gmapdp_plan_launch_info(const gmapdp_plan* plan, int li, int* R, int* dirs_l
 int gmapdp_plan_launch_kind(const gmapdp_plan* plan, int li) {
   if (!plan || li < 0 || li >= (int)plan->in.launches.size()) return GMAPDP_EINVAL;
   return plan->in.launches[li].kind;
+}
+
+int gmapdp_plan_launch_stream(const gmapdp_plan* plan, int li) {
+  if (!plan || li < 0 || li >= (int)plan->in.launches.size()) return GMAPDP_EINVAL;
+  return plan->in.launches[li].stream;
 }
 
 int gmapdp_plan_launch_is_tail(const gmapdp_plan* plan, int li) {

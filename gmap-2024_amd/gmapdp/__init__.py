@@ -126,6 +126,7 @@ def load_library(path=LIB_PATH):
                                               P(C.c_size_t)]),
         "gmapdp_plan_launch_members": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
         "gmapdp_plan_launch_is_tail": (C.c_int, [C.c_void_p, C.c_int]),
+        "gmapdp_plan_launch_stream": (C.c_int, [C.c_void_p, C.c_int]),
         "gmapdp_plan_run_launch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                              C.c_void_p, C.c_void_p]),
         "gmapdp_stream": (C.c_void_p, [C.c_void_p]),

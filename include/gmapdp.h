@@ -306,8 +306,10 @@ int gmapdp_plan_run (gmapdp_ctx *ctx, const gmapdp_plan *plan, const char *d_qse
                      gmapdp_result *d_results, gmapdp_pair *d_pairs, void *stream);
 /* Per-launch-class access (one kernel launch per class; for profiling). */
 int gmapdp_plan_launch_info (const gmapdp_plan *plan, int li, int *R, int *dirs_lds, int *count, size_t *lds);
-/* 1 if launch li is a latency-bound tail class that gmapdp_plan_run issues on
- * a side stream concurrently with the bulk classes. */
+/* Launch classes are spread over the caller's stream (0) and three side streams (1..3),
+ * longest-processing-time first; launches are numbered in issue order.  is_tail: 1 if the
+ * launch runs on a side stream. */
+int gmapdp_plan_launch_stream (const gmapdp_plan *plan, int li);
 int gmapdp_plan_launch_is_tail (const gmapdp_plan *plan, int li);
 /* Original problem indices of launch li (count entries, launch order). */
 int gmapdp_plan_launch_members (const gmapdp_plan *plan, int li, int *problem_indices);
