@@ -210,9 +210,23 @@ struct Geo {  // coordinate transform of a problem (revp flips both axes)
   __device__ int gpos(int c) const { return goffset + sgn * (c - 1); }
 };
 
+// Views of a problem's characters by DP row / column.  The kernels that stage them in LDS pass
+// plain `const char*` arrays (row r at q[r]); the packed kernel reads the query from the HBM arena
+// and derives genome characters from their classes, which keeps its LDS slot small.
+struct QView {  // character of DP row r: p[step * (r - 1)]
+  const char* p;
+  int step;
+  __device__ char operator[](int r) const { return p[step * (r - 1)]; }
+};
+struct GClassView {  // genome character of column c from its class (A C G T N *)
+  const uint8_t* cls;
+  __device__ char operator[](int c) const { return (char)((0x2A4E54474341ull >> (8u * cls[c])) & 0xffu); }
+};
+
 // Diagonal run: cells (r-j, c-j), j in [0, n)  (dynprog.c:1861-1915, traceback_nogaps)
-__device__ __forceinline__ void emit_diag(int lane, int r, int c, int n, const Geo& G, const char* q, const char* quc,
-                                          const char* gch, const uint8_t* __restrict__ cons, gmapdp_pair* out,
+template <typename QV, typename GV>
+__device__ __forceinline__ void emit_diag(int lane, int r, int c, int n, const Geo& G, const QV& q, const QV& quc,
+                                          const GV& gch, const uint8_t* __restrict__ cons, gmapdp_pair* out,
                                           Tally& t) {
   for (int base = 0; base < n; base += 64) {
     const int j = base + lane;
@@ -248,7 +262,8 @@ __device__ __forceinline__ void emit_diag(int lane, int r, int c, int n, const G
 }
 
 // Query skip: Pairpool_add_queryskip(pairs, rs, c, dist, ...) (pairpool.c:981): rows rs, rs-1, ...
-__device__ __forceinline__ void emit_queryskip(int lane, int rs, int c, int dist, const Geo& G, const char* q,
+template <typename QV>
+__device__ __forceinline__ void emit_queryskip(int lane, int rs, int c, int dist, const Geo& G, const QV& q,
                                                gmapdp_pair* out, Tally& t) {
   const int gp = G.gpos(c);
   for (int base = 0; base < dist; base += 64) {
@@ -412,7 +427,8 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
     // last_nogap entering row rlo (dynprog.c:1411-1449)
     const int L0 = (c == 1) ? (kNegInf32 - open + 1) : (c <= uband ? oce : kNegInf32);
     const int row0 = (c <= uband) ? oce : kNegInf32;  // row 0 of this column (dynprog.c:1318-1325)
-    const int8_t* scg = (S == 64) ? sc + gi * srow : sc + gi;
+    const int8_t* scg = (S == 64) ? sc + gi * srow : sc;
+    const int gi4 = gi << 2;  // segmented: bit offset of the class in the row's score word
 
     int Ein[R], Hin[R];
 #pragma unroll
@@ -428,7 +444,9 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
       const int r = rtop + k;
       valid[i] = (k < W) & (r >= rlo) & (r <= rhigh) & colact;
       const int rr = min(max(r, 0), rlen + 1);
-      const int s = (S == 64) ? scg[rr] : scg[rr << 3];
+      int s;
+      if constexpr (S == 64) s = scg[rr];
+      else s = __builtin_amdgcn_sbfe(reinterpret_cast<const int32_t*>(sc)[rr], gi4, 4);
       // Egap (dynprog.c:1518-1524)
       const int es = Hin[i] + open;
       eb[i] = Ein[i] > es - late;
@@ -579,9 +597,9 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
 
 // ---- wave-cooperative traceback (Dynprog_traceback_std, dynprog.c:1796-1948) ----
 // Emits the reference's push order into out[t.count ...].
-template <int R, typename WORD = uint64_t>
+template <int R, typename WORD = uint64_t, typename QV = const char*, typename GV = const char*>
 __device__ __forceinline__ void traceback_band(int lane, const WORD* dirs, int W, int uband, int r, int c,
-                                               const Geo& G, const char* q, const char* quc, const char* gch,
+                                               const Geo& G, const QV& q, const QV& quc, const GV& gch,
                                                const uint8_t* __restrict__ cons, bool watson, uint32_t chroffset,
                                                uint32_t chrhigh, const uint32_t* __restrict__ blocks,
                                                uint64_t nwords, gmapdp_pair* out, Tally& t, int bitoff = 0) {
@@ -804,27 +822,26 @@ __global__ __launch_bounds__(64) void dp_kernel(
 // the tracebacks -- short next to the fills -- then run one problem at a time
 // with the whole wave.  Semantics are those of dp_kernel.
 // ===========================================================================
-// Per-problem LDS slot of the packed kernel: transposed score rows sc[r][8] (rows 0..rlength+1),
-// query, upper-cased query, genome characters and classes.  The direction words of the whole
-// wave (4 x u64 per column) precede the slots.
+// Per-problem LDS slot of the packed kernel: one 32-bit score word per query row (rows
+// 0..rlength+1; 4-bit score per genome class -- every pairdistance value lies in [-5, 3]) and the
+// genome classes.  The query stays in HBM and genome characters derive from the classes.  The
+// direction words of the whole wave (4 x u64 per column) precede the slots.
 __host__ __device__ inline Carve carve_dpx(int rlength, int glength) {
   Carve cv;
   size_t off = 0;
-  cv.sc = off;   off = align16(off + 8u * (size_t)(rlength + 2));
-  cv.q = off;    off = align16(off + (size_t)(rlength + 1));
-  cv.quc = off;  off = align16(off + (size_t)(rlength + 1));
-  cv.gch = off;  off = align16(off + (size_t)(glength + 1));
+  cv.sc = off;   off = align16(off + 4u * (size_t)(rlength + 2));
   cv.gcls = off; off = align16(off + (size_t)(glength + 2));
-  cv.dirs = 0;
+  cv.q = cv.quc = cv.gch = cv.dirs = 0;
   cv.total = off;
   return cv;
 }
 
 // Pair emission of one problem after its fill (the tail of dp_kernel): traceback or the
 // simple/no-gap diagonal, end-gap INDEL trimming and end5 reversal, the result record.
+template <typename QV, typename GV>
 __device__ __forceinline__ void finish_dp(int lane, const DevProblem& P, int pid, bool simple, int bestr, int bestc,
-                                          const uint64_t* dirs, int bitoff, const char* q, const char* quc,
-                                          const char* gch,
+                                          const uint64_t* dirs, int bitoff, const QV& q, const QV& quc,
+                                          const GV& gch,
                                           const uint8_t* __restrict__ constab, const uint32_t* __restrict__ blocks,
                                           uint64_t nwords, gmapdp_result* __restrict__ results,
                                           gmapdp_pair* __restrict__ pairs) {
@@ -861,8 +878,9 @@ __device__ __forceinline__ void finish_dp(int lane, const DevProblem& P, int pid
   if (is_end && endalign == kQueryendNogaps) {
     emit_diag(lane, bestr, bestc, bestr, G, q, quc, gch, cons, out, t);  // traceback_nogaps
   } else if (!skip) {
-    traceback_band<1>(lane, dirs, P.lband + P.uband + 1, P.uband, bestr, bestc, G, q, quc, gch, cons,
-                      flags & kFWatson, P.chroffset, P.chrhigh, blocks, nwords, out, t, bitoff);
+    traceback_band<1, uint64_t, QV, GV>(lane, dirs, P.lband + P.uband + 1, P.uband, bestr, bestc, G, q, quc, gch,
+                                        cons, flags & kFWatson, P.chroffset, P.chrhigh, blocks, nwords, out, t,
+                                        bitoff);
   }
   int score = t.score + t.nmatches * kMatch + t.nmismatches * kMismatch;
   int first = 0, npairs = t.count;
@@ -913,32 +931,29 @@ __global__ __launch_bounds__(64) void dpx_kernel(
   uint64_t* wdirs = reinterpret_cast<uint64_t*>(smem);
   unsigned char* base = smem + dirs_bytes + (size_t)seg * (size_t)slot;
   const Carve cv = carve_dpx(rlen, glen);
-  int8_t* sc = reinterpret_cast<int8_t*>(base + cv.sc);
-  char* q = reinterpret_cast<char*>(base + cv.q);
-  char* quc = reinterpret_cast<char*>(base + cv.quc);
-  char* gch = reinterpret_cast<char*>(base + cv.gch);
+  int32_t* sc4 = reinterpret_cast<int32_t*>(base + cv.sc);
   uint8_t* gcl = reinterpret_cast<uint8_t*>(base + cv.gcls);
   const int8_t* sct = sctab + (size_t)P.mismatchtype * 128 * kNClass;
   const uint8_t* cons = constab + (size_t)P.genestrand * 128 * kNClass;
-
-  // ---- stage each segment's problem: per query row one 8-byte score vector (by genome class) ----
   const int qstep = rev ? -1 : 1;
+  const QView qucv{qseq_uc + P.qbase, qstep};
+  const GClassView gv{gcl};
+
+  // ---- stage each segment's problem: per query row one word of 4-bit scores (by genome class) ----
   const bool score_uc = flags & kFScoreUC;
   for (int i = sl; i < rlen; i += S) {
-    const char c1 = qseq[P.qbase + qstep * i];
-    const char c1u = qseq_uc[P.qbase + qstep * i];
-    q[i + 1] = c1;
-    quc[i + 1] = c1u;
-    *reinterpret_cast<uint64_t*>(sc + 8 * (i + 1)) =
-        *reinterpret_cast<const uint64_t*>(sct + (uint8_t)((score_uc ? c1u : c1) & 127) * kNClass);
+    const char c1 = score_uc ? qseq_uc[P.qbase + qstep * i] : qseq[P.qbase + qstep * i];
+    const uint64_t row = *reinterpret_cast<const uint64_t*>(sct + (uint8_t)(c1 & 127) * kNClass);
+    uint32_t w = 0;
+#pragma unroll
+    for (int g = 0; g < 6; g++) w |= (uint32_t)((row >> (8 * g)) & 0xfu) << (4 * g);
+    sc4[i + 1] = (int32_t)w;
   }
-  if (live && sl < 2) *reinterpret_cast<uint64_t*>(sc + 8 * (sl ? rlen + 1 : 0)) = 0ull;  // rows 0, rlength+1
+  if (live && sl < 2) sc4[sl ? rlen + 1 : 0] = 0;  // rows 0, rlength+1
   const bool segleft = flags & kFSegLeft, segrc = flags & kFSegRevcomp;
   for (int i = sl; i < glen; i += S) {
     const char c2 = segment_nt(blocks, nwords, (uint32_t)i, (uint32_t)glen, P.segpos, P.segbound, segleft, segrc);
-    const int c = rev ? glen - i : i + 1;
-    gch[c] = c2;
-    gcl[c] = gclass(c2);
+    gcl[rev ? glen - i : i + 1] = gclass(c2);
   }
   __syncthreads();
 
@@ -953,8 +968,8 @@ __global__ __launch_bounds__(64) void dpx_kernel(
     const int r = base0 + sl + 1;
     bool mism = false;
     if (try_simple && r <= rlen) {
-      const char c1u = quc[r], c2 = gch[r];
-      mism = (c2 != '*') && (c1u != c2) && !cons[(uint8_t)(c1u & 127) * kNClass + gclass(c2)];
+      const char c1u = qucv[r], c2 = gv[r];
+      mism = (c2 != '*') && (c1u != c2) && !cons[(uint8_t)(c1u & 127) * kNClass + gcl[r]];
     }
     nmism += __popcll(ballot(mism) & segmask);
   }
@@ -971,8 +986,8 @@ __global__ __launch_bounds__(64) void dpx_kernel(
   {
     const int track = !is_end ? 0 : ((endalign == kQueryendIndels) ? 2 : 1);
     fill_band<1, false, S>(lane, fills ? rlen : 0, gfill, P.lband, P.uband, P.open, P.extend,
-                           (flags & kFLate) ? 1 : 0, fills ? track : 0, sc, 8, gcl, wdirs, nullptr, bestr, bestc,
-                           gmax);
+                           (flags & kFLate) ? 1 : 0, fills ? track : 0, reinterpret_cast<const int8_t*>(sc4), 0,
+                           gcl, wdirs, nullptr, bestr, bestc, gmax);
   }
   if (nogaps) bestr = bestc = glen < rlen ? glen : rlen;  // find_best_endpoint_to_queryend_nogaps
   __syncthreads();
@@ -985,10 +1000,12 @@ __global__ __launch_bounds__(64) void dpx_kernel(
     const DevProblem Pj = probs[pj];
     const Carve cj = carve_dpx(Pj.rlength, Pj.glength);
     unsigned char* bj = smem + dirs_bytes + (size_t)j * (size_t)slot;
+    const int sj = (Pj.flags & kFRev) ? -1 : 1;
     finish_dp(lane, Pj, pj, __builtin_amdgcn_readlane((int)simple, src) != 0,
               __builtin_amdgcn_readlane(bestr, src), __builtin_amdgcn_readlane(bestc, src), wdirs, src,
-              reinterpret_cast<const char*>(bj + cj.q), reinterpret_cast<const char*>(bj + cj.quc),
-              reinterpret_cast<const char*>(bj + cj.gch), constab, blocks, nwords, results, pairs);
+              QView{qseq + Pj.qbase, sj}, QView{qseq_uc + Pj.qbase, sj},
+              GClassView{reinterpret_cast<const uint8_t*>(bj + cj.gcls)}, constab, blocks, nwords, results,
+              pairs);
   }
 }
 

@@ -372,7 +372,7 @@ static size_t lds_bucket(size_t lds) {
 
 // per-problem LDS slot of the packed kernel (64/S slots per workgroup)
 static size_t slot_bucket(size_t b) {
-  static const size_t s[] = {1024, 1536, 2048, 3072, 4096, 6144, 8192, 12288, 16384};
+  static const size_t s[] = {256, 384, 512, 768, 1024, 1536, 2048, 3072, 4096, 6144, 8192, 12288, 16384};
   for (size_t x : s)
     if (b <= x) return x;
   return 0;  // too big to pack
