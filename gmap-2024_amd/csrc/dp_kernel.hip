@@ -908,9 +908,12 @@ __device__ __forceinline__ void finish_dp(int lane, const DevProblem& P, int pid
   }
 }
 
-template <int S>
+// GD: the whole-wave direction words live in an L2-resident global scratch (one region of
+// dirs_bytes per workgroup) instead of LDS, for classes whose LDS footprint would limit occupancy.
+template <int S, bool GD>
 __global__ __launch_bounds__(64) void dpx_kernel(
     const DevProblem* __restrict__ probs, const int* __restrict__ order, int count, int slot, int dirs_bytes,
+    unsigned char* __restrict__ gdirs,
     const uint32_t* __restrict__ blocks, uint64_t nwords,
     const char* __restrict__ qseq, const char* __restrict__ qseq_uc,
     const int8_t* __restrict__ sctab, const uint8_t* __restrict__ constab,
@@ -928,8 +931,10 @@ __global__ __launch_bounds__(64) void dpx_kernel(
   const bool rev = flags & kFRev;
   const int kind = P.kind, endalign = P.endalign;
   const bool is_end = kind != kSingle;
-  uint64_t* wdirs = reinterpret_cast<uint64_t*>(smem);
-  unsigned char* base = smem + dirs_bytes + (size_t)seg * (size_t)slot;
+  uint64_t* wdirs = GD ? reinterpret_cast<uint64_t*>(gdirs + (size_t)blockIdx.x * (size_t)dirs_bytes)
+                       : reinterpret_cast<uint64_t*>(smem);
+  const int lds_dirs = GD ? 0 : dirs_bytes;
+  unsigned char* base = smem + lds_dirs + (size_t)seg * (size_t)slot;
   const Carve cv = carve_dpx(rlen, glen);
   int32_t* sc4 = reinterpret_cast<int32_t*>(base + cv.sc);
   uint8_t* gcl = reinterpret_cast<uint8_t*>(base + cv.gcls);
@@ -990,6 +995,7 @@ __global__ __launch_bounds__(64) void dpx_kernel(
                            gcl, wdirs, nullptr, bestr, bestc, gmax);
   }
   if (nogaps) bestr = bestc = glen < rlen ? glen : rlen;  // find_best_endpoint_to_queryend_nogaps
+  if (GD) __threadfence_block();
   __syncthreads();
 
   // ---- emission, one problem at a time with the whole wave ----
@@ -999,7 +1005,7 @@ __global__ __launch_bounds__(64) void dpx_kernel(
     const int pj = __builtin_amdgcn_readlane(pid, src);
     const DevProblem Pj = probs[pj];
     const Carve cj = carve_dpx(Pj.rlength, Pj.glength);
-    unsigned char* bj = smem + dirs_bytes + (size_t)j * (size_t)slot;
+    unsigned char* bj = smem + lds_dirs + (size_t)j * (size_t)slot;
     const int sj = (Pj.flags & kFRev) ? -1 : 1;
     finish_dp(lane, Pj, pj, __builtin_amdgcn_readlane((int)simple, src) != 0,
               __builtin_amdgcn_readlane(bestr, src), __builtin_amdgcn_readlane(bestc, src), wdirs, src,
@@ -1530,22 +1536,24 @@ hipError_t launch_dp(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
 size_t lds_slot_dpx(int rlength, int glength) { return carve_dpx(rlength, glength).total; }
 size_t lds_dirs_dpx(int gmax) { return align16((size_t)(gmax + 1) * 4u * 8u); }
 
-hipError_t launch_dpx(int S, int nproblems, int slot, int dirs_bytes, hipStream_t stream, const DevProblem* probs,
-                      const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
-                      const char* qseq_uc, const int8_t* sctab, const uint8_t* constab, gmapdp_result* results,
-                      gmapdp_pair* pairs) {
+hipError_t launch_dpx(int S, int nproblems, int slot, int dirs_bytes, unsigned char* gdirs, hipStream_t stream,
+                      const DevProblem* probs, const int* order, const uint32_t* blocks, uint64_t nwords,
+                      const char* qseq, const char* qseq_uc, const int8_t* sctab, const uint8_t* constab,
+                      gmapdp_result* results, gmapdp_pair* pairs) {
   if (S != 16 && S != 32) return hipErrorInvalidValue;
-  void* fn = (S == 16) ? reinterpret_cast<void*>(&dpx_kernel<16>) : reinterpret_cast<void*>(&dpx_kernel<32>);
+  void* fn;
+  if (S == 16) fn = gdirs ? reinterpret_cast<void*>(&dpx_kernel<16, true>) : reinterpret_cast<void*>(&dpx_kernel<16, false>);
+  else fn = gdirs ? reinterpret_cast<void*>(&dpx_kernel<32, true>) : reinterpret_cast<void*>(&dpx_kernel<32, false>);
   const int np = 64 / S;
-  const size_t lds = (size_t)dirs_bytes + (size_t)slot * np;
+  const size_t lds = (gdirs ? 0 : (size_t)dirs_bytes) + (size_t)slot * np;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
   const int nblocks = (nproblems + np - 1) / np;
   void* args[] = {(void*)&probs, (void*)&order, (void*)&nproblems, (void*)&slot, (void*)&dirs_bytes,
-                  (void*)&blocks, (void*)&nwords, (void*)&qseq, (void*)&qseq_uc, (void*)&sctab, (void*)&constab,
-                  (void*)&results, (void*)&pairs};
+                  (void*)&gdirs, (void*)&blocks, (void*)&nwords, (void*)&qseq, (void*)&qseq_uc, (void*)&sctab,
+                  (void*)&constab, (void*)&results, (void*)&pairs};
   return hipLaunchKernel(fn, dim3(nblocks), dim3(64), args, lds, stream);
 }
 

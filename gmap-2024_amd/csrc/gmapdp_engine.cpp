@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cctype>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -30,10 +31,10 @@ hipError_t launch_dp(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
                      gmapdp_pair* pairs, uint64_t* gdirs);
 size_t lds_slot_dpx(int rlength, int glength);
 size_t lds_dirs_dpx(int gmax);
-hipError_t launch_dpx(int S, int nproblems, int slot, int dirs_bytes, hipStream_t stream, const DevProblem* probs,
-                      const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
-                      const char* qseq_uc, const int8_t* sctab, const uint8_t* constab, gmapdp_result* results,
-                      gmapdp_pair* pairs);
+hipError_t launch_dpx(int S, int nproblems, int slot, int dirs_bytes, unsigned char* gdirs, hipStream_t stream,
+                      const DevProblem* probs, const int* order, const uint32_t* blocks, uint64_t nwords,
+                      const char* qseq, const char* qseq_uc, const int8_t* sctab, const uint8_t* constab,
+                      gmapdp_result* results, gmapdp_pair* pairs);
 size_t lds_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds);
 size_t scratch_bytes_gg(int glengthL, int glengthR, int R);
 hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevGenomeProblem* probs,
@@ -200,7 +201,8 @@ struct PlanCore {
     size_t lds;      // LDS bucket per workgroup (kDpx: per problem slot)
     int first, count;
     double work;     // estimated wave-columns, for stream assignment
-    size_t extra;    // kDpx: bytes of the whole-wave direction words ahead of the slots
+    size_t extra;    // kDpx: bytes of the whole-wave direction words (per workgroup)
+    size_t gdirs_offset;  // kDpx with !dirs_lds: the class's region of the global scratch
     int stream;      // 0: the caller's stream, 1..3: the context's side streams
   };
   std::vector<Launch> launches;
@@ -356,6 +358,15 @@ int gmapdp_set_genome(gmapdp_ctx* ctx, const uint32_t* blocks, size_t nwords, ui
 // the pair arena.
 // ---------------------------------------------------------------------------
 static const size_t kLdsBudget = 64 * 1024;  // per workgroup; keeps >= 2 problems resident per CU
+// Packed workgroups keep their direction words in LDS while the workgroup's LDS stays within
+// this; GMAPDP_DPX_LDS_DIRS_MAX overrides it (experiments).
+static size_t dpx_lds_dirs_max() {
+  static const size_t v = [] {
+    const char* e = getenv("GMAPDP_DPX_LDS_DIRS_MAX");
+    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)4 * 1024;
+  }();
+  return v;
+}
 
 static int pick_R(int W) {
   int R = 1;
@@ -670,10 +681,19 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     // work estimate: fill wave-columns (a packed wave fills 64/S problems at once)
     L.work = 0.0;
     L.extra = 0;
+    L.gdirs_offset = 0;
     if (L.kind == PlanCore::kDpx) {
       int gmax = 0;
       for (int id : ids) gmax = std::max(gmax, (int)plan.dev[id].glength);
       L.extra = lds_dirs_dpx(gmax);
+      // direction words in LDS while the workgroup stays small; beyond that they go to an
+      // L2-resident scratch so that more problems are resident per CU
+      L.dirs_lds = L.extra + L.lds * (64 / L.R) <= dpx_lds_dirs_max();
+      if (!L.dirs_lds) {
+        L.gdirs_offset = gdirs_off;
+        const size_t nblocks = ((size_t)L.count + (64 / L.R) - 1) / (64 / L.R);
+        gdirs_off += (nblocks * L.extra + 255) & ~(size_t)255;
+      }
     }
     for (int id : ids) {
       if (L.kind == PlanCore::kGenomeGap) {
@@ -772,9 +792,10 @@ struct RunArgs {
 static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, const RunArgs& a, hipStream_t stream) {
   const auto& L = plan.launches[li];
   if (L.kind == PlanCore::kDpx)
-    return launch_dpx(L.R, L.count, (int)L.lds, (int)L.extra, stream, a.d_probs, a.d_order + L.first,
-                      ctx->d_genome, ctx->genome_words, a.d_q, a.d_quc, ctx->d_sc, ctx->d_cs, a.d_results,
-                      a.d_pairs);
+    return launch_dpx(L.R, L.count, (int)L.lds, (int)L.extra,
+                      L.dirs_lds ? nullptr : (unsigned char*)ctx->gdirs.p + L.gdirs_offset, stream, a.d_probs,
+                      a.d_order + L.first, ctx->d_genome, ctx->genome_words, a.d_q, a.d_quc, ctx->d_sc, ctx->d_cs,
+                      a.d_results, a.d_pairs);
   if (L.kind == PlanCore::kDp)
     return launch_dp(L.R, L.dirs_lds, L.count, L.lds, stream, a.d_probs, a.d_order + L.first, ctx->d_genome,
                      ctx->genome_words, a.d_q, a.d_quc, ctx->d_sc, ctx->d_cs, a.d_results, a.d_pairs,
