@@ -231,8 +231,8 @@ def pmc_traffic(name):
     m = re.match(r"(\w+)<R=(\d+),dirs_lds=(\d)>", name)
     if not m:
         return None, None
-    if m.group(1) == "dpx_kernel":
-        key = "gmapdp::dpx_kernel<%s>" % m.group(2)
+    if m.group(1) == "dpx_kernel":  # dpx_kernel<S, GD>: GD = direction words in global scratch
+        key = "gmapdp::dpx_kernel<%s, %s>" % (m.group(2), "false" if m.group(3) == "1" else "true")
     else:
         key = "gmapdp::%s<%s, %s>" % (m.group(1), m.group(2), "true" if m.group(3) == "1" else "false")
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")), reverse=True):
