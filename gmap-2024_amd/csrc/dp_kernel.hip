@@ -369,7 +369,7 @@ struct Part {
 // is then per segment, `gmax` is the wave's largest glength, the score rows are transposed
 // (sc[r*8 + class], no per-column multiply) and lane 0 stores the whole-wave ballots (segment j
 // owns bits [j*S, j*S+S) of each word).
-template <int R, bool CARRY, int S = 64>
+template <int R, bool CARRY, int S = 64, bool PK = (S < 64)>
 __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lband, int uband, int open, int ext,
                                           int late, int track, const int8_t* sc, int srow, const uint8_t* gcl,
                                           uint64_t* dirs, const BridgeCarry* bc_, int& bestr, int& bestc,
@@ -427,8 +427,8 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
     // last_nogap entering row rlo (dynprog.c:1411-1449)
     const int L0 = (c == 1) ? (kNegInf32 - open + 1) : (c <= uband ? oce : kNegInf32);
     const int row0 = (c <= uband) ? oce : kNegInf32;  // row 0 of this column (dynprog.c:1318-1325)
-    const int8_t* scg = (S == 64) ? sc + gi * srow : sc;
-    const int gi4 = gi << 2;  // segmented: bit offset of the class in the row's score word
+    const int8_t* scg = PK ? sc : sc + gi * srow;
+    const int gi4 = gi << 2;  // packed: bit offset of the class in the row's score word
 
     int Ein[R], Hin[R];
 #pragma unroll
@@ -445,7 +445,7 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
       valid[i] = (k < W) & (r >= rlo) & (r <= rhigh) & colact;
       const int rr = min(max(r, 0), rlen + 1);
       int s;
-      if constexpr (S == 64) s = scg[rr];
+      if constexpr (!PK) s = scg[rr];
       else s = __builtin_amdgcn_sbfe(reinterpret_cast<const int32_t*>(sc)[rr], gi4, 4);
       // Egap (dynprog.c:1518-1524)
       const int es = Hin[i] + open;
@@ -1032,31 +1032,27 @@ __global__ __launch_bounds__(64) void dpx_kernel(
 //   4. traceback R, List_reverse, gap holder, traceback L, Pair_maxnegscore.
 // ===========================================================================
 struct CarveGG {
-  size_t scL, scR, qL, qucL, qR, qucR, gchL, gclL, gchR, gclR, ldi, rdi, pL, pR, diagL, diagR, partB, partC, isc,
-      flag, dirsL, dirsR, total;
+  size_t scL, scR, gclL, gclR, ldi, rdi, pL, pR, isc, flag, dirsL, dirsR, total;
+};
+// Global scratch of one genome-gap problem: the bridge candidates and diagonal of each fill
+// (written once by the fill, read once by the bridge), then the direction planes unless in LDS.
+struct ScratchGG {
+  size_t partB, partC, diagL, diagR, dirsL, dirsR, total;
 };
 
 __host__ __device__ inline size_t gg_dirs_bytes(int glength, int R) { return (size_t)(glength + 1) * 4u * (size_t)R * 8u; }
 
+// LDS: per query row one word of 4-bit scores per side (as the packed kernel), genome classes,
+// dinucleotide codes and splice probabilities per column; the query stays in HBM and genome
+// characters derive from the classes.
 __host__ __device__ inline CarveGG carve_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds) {
   CarveGG cv;
   size_t off = 0;
-  const size_t srow = (size_t)(rlength + 2);
   cv.pL = off;    off = align16(off + 8u * (size_t)glengthL);
   cv.pR = off;    off = align16(off + 8u * (size_t)glengthR);
-  cv.partB = off; off = align16(off + sizeof(Part) * (size_t)(rlength + 1));
-  cv.partC = off; off = align16(off + sizeof(Part) * (size_t)(rlength + 1));
-  cv.diagL = off; off = align16(off + 4u * (size_t)(rlength + 1));
-  cv.diagR = off; off = align16(off + 4u * (size_t)(rlength + 1));
-  cv.scL = off;   off = align16(off + (size_t)kNClass * srow);
-  cv.scR = off;   off = align16(off + (size_t)kNClass * srow);
-  cv.qL = off;    off = align16(off + srow);
-  cv.qucL = off;  off = align16(off + srow);
-  cv.qR = off;    off = align16(off + srow);
-  cv.qucR = off;  off = align16(off + srow);
-  cv.gchL = off;  off = align16(off + (size_t)(glengthL + 2));
+  cv.scL = off;   off = align16(off + 4u * (size_t)(rlength + 2));
+  cv.scR = off;   off = align16(off + 4u * (size_t)(rlength + 2));
   cv.gclL = off;  off = align16(off + (size_t)(glengthL + 2));
-  cv.gchR = off;  off = align16(off + (size_t)(glengthR + 2));
   cv.gclR = off;  off = align16(off + (size_t)(glengthR + 2));
   cv.ldi = off;   off = align16(off + (size_t)(glengthL + 2));
   cv.rdi = off;   off = align16(off + (size_t)(glengthR + 2));
@@ -1069,6 +1065,22 @@ __host__ __device__ inline CarveGG carve_gg(int rlength, int glengthL, int gleng
   }
   cv.total = off;
   return cv;
+}
+
+__host__ __device__ inline ScratchGG scratch_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds) {
+  ScratchGG sv;
+  size_t off = 0;
+  sv.partB = off; off = align16(off + 16u * (size_t)(rlength + 1));
+  sv.partC = off; off = align16(off + 16u * (size_t)(rlength + 1));
+  sv.diagL = off; off = align16(off + 4u * (size_t)(rlength + 1));
+  sv.diagR = off; off = align16(off + 4u * (size_t)(rlength + 1));
+  sv.dirsL = sv.dirsR = off;
+  if (!dirs_lds) {
+    sv.dirsL = off; off = align16(off + gg_dirs_bytes(glengthL, R));
+    sv.dirsR = off; off = align16(off + gg_dirs_bytes(glengthR, R));
+  }
+  sv.total = off;
+  return sv;
 }
 
 // intron.h dinucleotide codes; the engine's genome has no alternate alleles (alt == ref)
@@ -1175,70 +1187,61 @@ __global__ __launch_bounds__(128) void gg_kernel(
   const int lband = P.lbandL, ubandL = P.ubandL, ubandR = P.ubandR;
   const int WL = lband + ubandL + 1, WR = lband + ubandR + 1;
   const CarveGG cv = carve_gg(rlen, gL, gR, R, DIRS_LDS);
+  const ScratchGG sv = scratch_gg(rlen, gL, gR, R, DIRS_LDS);
+  unsigned char* gbase = gscratch + P.dirs_offset;
   double* pL = reinterpret_cast<double*>(smem + cv.pL);
   double* pR = reinterpret_cast<double*>(smem + cv.pR);
-  Part* partB = reinterpret_cast<Part*>(smem + cv.partB);  // indexed by rR
-  Part* partC = reinterpret_cast<Part*>(smem + cv.partC);  // indexed by rL
-  int* diagL = reinterpret_cast<int*>(smem + cv.diagL);
-  int* diagR = reinterpret_cast<int*>(smem + cv.diagR);
-  int8_t* scL = reinterpret_cast<int8_t*>(smem + cv.scL);
-  int8_t* scR = reinterpret_cast<int8_t*>(smem + cv.scR);
-  char* qL = reinterpret_cast<char*>(smem + cv.qL);
-  char* qucL = reinterpret_cast<char*>(smem + cv.qucL);
-  char* qR = reinterpret_cast<char*>(smem + cv.qR);
-  char* qucR = reinterpret_cast<char*>(smem + cv.qucR);
-  char* gchL = reinterpret_cast<char*>(smem + cv.gchL);
+  Part* partB = reinterpret_cast<Part*>(gbase + sv.partB);  // indexed by rR
+  Part* partC = reinterpret_cast<Part*>(gbase + sv.partC);  // indexed by rL
+  int* diagL = reinterpret_cast<int*>(gbase + sv.diagL);
+  int* diagR = reinterpret_cast<int*>(gbase + sv.diagR);
+  int32_t* scL = reinterpret_cast<int32_t*>(smem + cv.scL);
+  int32_t* scR = reinterpret_cast<int32_t*>(smem + cv.scR);
   uint8_t* gclL = reinterpret_cast<uint8_t*>(smem + cv.gclL);
-  char* gchR = reinterpret_cast<char*>(smem + cv.gchR);
   uint8_t* gclR = reinterpret_cast<uint8_t*>(smem + cv.gclR);
   uint8_t* ldi = reinterpret_cast<uint8_t*>(smem + cv.ldi);
   uint8_t* rdi = reinterpret_cast<uint8_t*>(smem + cv.rdi);
   int8_t* isc = reinterpret_cast<int8_t*>(smem + cv.isc);
   int* done = reinterpret_cast<int*>(smem + cv.flag);
-  unsigned char* gbase = gscratch + P.dirs_offset;
-  uint64_t* dirsL = reinterpret_cast<uint64_t*>(DIRS_LDS ? smem + cv.dirsL : gbase);
-  uint64_t* dirsR = reinterpret_cast<uint64_t*>(DIRS_LDS ? smem + cv.dirsR : gbase + align16(gg_dirs_bytes(gL, R)));
+  uint64_t* dirsL = reinterpret_cast<uint64_t*>(DIRS_LDS ? smem + cv.dirsL : gbase + sv.dirsL);
+  uint64_t* dirsR = reinterpret_cast<uint64_t*>(DIRS_LDS ? smem + cv.dirsR : gbase + sv.dirsR);
+  // query rows in both DP orders straight from HBM: qL[r] = rsequence[r-1], qR[r] = rsequence[rlength-r]
+  const QView qL{qseq + P.qbase, 1}, qucL{qseq_uc + P.qbase, 1};
+  const QView qR{qseq + P.qbase + rlen - 1, -1}, qucR{qseq_uc + P.qbase + rlen - 1, -1};
+  const GClassView gchL{gclL}, gchR{gclR};
   const int8_t* sct = sctab + (size_t)P.mismatchtype * 128 * kNClass;
   const uint8_t* cons = constab + (size_t)P.genestrand * 128 * kNClass;
   gmapdp_pair* out = pairs + P.pair_offset;
   const int rev_roffset = P.roffset + rlen - 1;
   const Geo GL{P.roffset, P.goffsetL, 1};
   const Geo GR{rev_roffset, P.rev_goffsetR, -1};
-  const int srow = rlen + 2;
   const bool halfp = flags & kGHalf;
 
-  // ---- stage (both waves): query in both DP orders with per-class score rows, both genome
-  //      segments, dinucleotide codes, the splice probabilities and the intron score array ----
+  // ---- stage (both waves): per query row the 4-bit score word in both DP orders, both genome
+  //      segments as classes, dinucleotide codes, the splice probabilities, the intron scores ----
   for (int i = tid; i < rlen; i += 128) {
     const char c1 = qseq[P.qbase + i];
-    const char c1u = qseq_uc[P.qbase + i];
-    qL[i + 1] = c1;
-    qucL[i + 1] = c1u;
-    qR[rlen - i] = c1;  // rev_rsequence[1-r] = rsequence[rlength-r]
-    qucR[rlen - i] = c1u;
     const uint64_t row = *reinterpret_cast<const uint64_t*>(sct + (uint8_t)(c1 & 127) * kNClass);
+    uint32_t w = 0;
 #pragma unroll
-    for (int g = 0; g < 6; g++) {
-      scL[g * srow + i + 1] = (int8_t)(row >> (8 * g));
-      scR[g * srow + rlen - i] = (int8_t)(row >> (8 * g));
-    }
+    for (int g = 0; g < 6; g++) w |= (uint32_t)((row >> (8 * g)) & 0xfu) << (4 * g);
+    scL[i + 1] = (int32_t)w;
+    scR[rlen - i] = (int32_t)w;
   }
-  if (tid < 6) {
-    scL[tid * srow] = scR[tid * srow] = 0;
-    scL[tid * srow + rlen + 1] = scR[tid * srow + rlen + 1] = 0;
+  if (tid < 2) {
+    scL[tid ? rlen + 1 : 0] = 0;
+    scR[tid ? rlen + 1 : 0] = 0;
   }
   for (int i = tid; i < gL; i += 128) {
     const char c2 = segment_nt(blocks, nwords, (uint32_t)i, (uint32_t)gL, P.segposL, P.segboundL,
                                flags & kGSegLLeft, flags & kGSegLRc);
-    gchL[i + 1] = c2;
     gclL[i + 1] = gclass(c2);
     pL[i] = sprob[P.prob_offset + i];
   }
   for (int i = tid; i < gR; i += 128) {
     const char c2 = segment_nt(blocks, nwords, (uint32_t)i, (uint32_t)gR, P.segposR, P.segboundR,
                                flags & kGSegRLeft, flags & kGSegRRc);
-    gchR[gR - i] = c2;  // rev_gsequenceR[1-c] = segment[glengthR-c]
-    gclR[gR - i] = gclass(c2);
+    gclR[gR - i] = gclass(c2);  // rev_gsequenceR[1-c] = segment[glengthR-c]
     pR[i] = sprob[P.prob_offset + gL + i];
   }
   if (tid < 64) isc[tid] = isctab[(size_t)P.iclass * 128 + ((flags & kGFinal) ? 64 : 0) + tid];
@@ -1284,6 +1287,7 @@ __global__ __launch_bounds__(128) void gg_kernel(
         carryR = __shfl(sR, 63, 64);
       }
     }
+    __threadfence_block();
     __syncthreads();
     if (wave == 0) {
       // best: max score >= 0 among intron-type sites, ties -> largest rL ("Use >= for jump late")
@@ -1345,14 +1349,15 @@ __global__ __launch_bounds__(128) void gg_kernel(
     int br, bc;
     if (wave == 0) {
       const BridgeCarry B{ldi, rdi, pL, pR, isc, rdist, partB, diagR};
-      fill_band<R, true>(lane, rlen, gR, lband, ubandR, P.open, P.extend, 1 - late, 0, scR, srow, gclR, dirsR, &B,
-                         br, bc);
+      fill_band<R, true, 64, true>(lane, rlen, gR, lband, ubandR, P.open, P.extend, 1 - late, 0,
+                                   reinterpret_cast<const int8_t*>(scR), 0, gclR, dirsR, &B, br, bc);
     } else {
       const BridgeCarry B{rdi, ldi, pR, pL, isc, rdist, partC, diagL};
-      fill_band<R, true>(lane, rlen, gL, lband, ubandL, P.open, P.extend, late, 0, scL, srow, gclL, dirsL, &B,
-                         br, bc);
+      fill_band<R, true, 64, true>(lane, rlen, gL, lband, ubandL, P.open, P.extend, late, 0,
+                                   reinterpret_cast<const int8_t*>(scL), 0, gclL, dirsL, &B, br, bc);
     }
   }
+  __threadfence_block();
   __syncthreads();
   if (wave != 0) return;
 
@@ -1563,8 +1568,8 @@ static void* gptr() { return reinterpret_cast<void*>(&gg_kernel<R, D>); }
 size_t lds_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds) {
   return carve_gg(rlength, glengthL, glengthR, R, dirs_lds).total;
 }
-size_t scratch_bytes_gg(int glengthL, int glengthR, int R) {
-  return align16(gg_dirs_bytes(glengthL, R)) + align16(gg_dirs_bytes(glengthR, R));
+size_t scratch_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds) {
+  return scratch_gg(rlength, glengthL, glengthR, R, dirs_lds).total;
 }
 
 hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevGenomeProblem* probs,

@@ -36,7 +36,7 @@ hipError_t launch_dpx(int S, int nproblems, int slot, int dirs_bytes, unsigned c
                       const char* qseq, const char* qseq_uc, const int8_t* sctab, const uint8_t* constab,
                       gmapdp_result* results, gmapdp_pair* pairs);
 size_t lds_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds);
-size_t scratch_bytes_gg(int glengthL, int glengthR, int R);
+size_t scratch_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds);
 hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevGenomeProblem* probs,
                      const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
                      const char* qseq_uc, const double* sprob, const int8_t* sctab, const uint8_t* constab,
@@ -360,11 +360,9 @@ int gmapdp_set_genome(gmapdp_ctx* ctx, const uint32_t* blocks, size_t nwords, ui
 static const size_t kLdsBudget = 64 * 1024;  // per workgroup; keeps >= 2 problems resident per CU
 // Packed workgroups keep their direction words in LDS while the workgroup's LDS stays within
 // this; GMAPDP_DPX_LDS_DIRS_MAX overrides it (experiments).
+static size_t env_size(const char* name, size_t dflt);
 static size_t dpx_lds_dirs_max() {
-  static const size_t v = [] {
-    const char* e = getenv("GMAPDP_DPX_LDS_DIRS_MAX");
-    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)4 * 1024;
-  }();
+  static const size_t v = env_size("GMAPDP_DPX_LDS_DIRS_MAX", 4 * 1024);
   return v;
 }
 
@@ -379,6 +377,28 @@ static size_t lds_bucket(size_t lds) {
   for (size_t x : b)
     if (lds <= x) return x;
   return lds;
+}
+
+// genome-gap workgroups: finer steps, since their LDS sets how many problems a CU holds
+static size_t gg_lds_bucket(size_t lds) {
+  static const size_t b[] = {4096,  6144,  8192,  10240, 12288, 14336, 16384, 20480, 24576,
+                             28672, 32768, 40960, 49152, 65536, 98304, 163840};
+  for (size_t x : b)
+    if (lds <= x) return x;
+  return lds;
+}
+
+static size_t env_size(const char* name, size_t dflt) {
+  const char* e = getenv(name);
+  return e ? (size_t)strtoull(e, nullptr, 10) : dflt;
+}
+
+// genome-gap direction planes stay in LDS while the workgroup's LDS stays within this; by default
+// they always go to the L2-resident scratch, which measured fastest (more problems per CU).
+// GMAPDP_GG_LDS_DIRS_MAX overrides it, for experiments.
+static size_t gg_lds_dirs_max() {
+  static const size_t v = env_size("GMAPDP_GG_LDS_DIRS_MAX", 0);
+  return v;
 }
 
 // per-problem LDS slot of the packed kernel (64/S slots per workgroup)
@@ -643,15 +663,12 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     const int R = pick_R(std::max(WL, WR));
     if (R > kMaxR) return bad(ctx, "band wider than 4096");
     size_t lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, true);
-    const bool dirs_lds = lds <= kLdsBudget;
-    d.dirs_offset = 0;
-    if (!dirs_lds) {
-      lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, false);
-      d.dirs_offset = (int64_t)gdirs_off;
-      gdirs_off += (scratch_bytes_gg(d.glengthL, d.glengthR, R) + 255) & ~(size_t)255;
-    }
+    const bool dirs_lds = lds <= gg_lds_dirs_max();
+    if (!dirs_lds) lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, false);
+    d.dirs_offset = (int64_t)gdirs_off;  // bridge candidates (+ direction planes) in global scratch
+    gdirs_off += (scratch_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, dirs_lds) + 255) & ~(size_t)255;
     if (lds > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
-    classes[std::make_tuple((int)PlanCore::kGenomeGap, R, dirs_lds ? 1 : 0, lds_bucket(lds))].push_back((int)s);
+    classes[std::make_tuple((int)PlanCore::kGenomeGap, R, dirs_lds ? 1 : 0, gg_lds_bucket(lds))].push_back((int)s);
   }
   for (auto& kv : classes) {
     PlanCore::Launch L;
