@@ -596,23 +596,25 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
 }
 
 // ---- wave-cooperative traceback (Dynprog_traceback_std, dynprog.c:1796-1948) ----
-// Emits the reference's push order into out[t.count ...].
-template <int R, typename WORD = uint64_t, typename QV = const char*, typename GV = const char*>
-__device__ __forceinline__ void traceback_band(int lane, const WORD* dirs, int W, int uband, int r, int c,
-                                               const Geo& G, const QV& q, const QV& quc, const GV& gch,
-                                               const uint8_t* __restrict__ cons, bool watson, uint32_t chroffset,
-                                               uint32_t chrhigh, const uint32_t* __restrict__ blocks,
-                                               uint64_t nwords, gmapdp_pair* out, Tally& t, int bitoff = 0) {
+// Emits the reference's push order into out[t.count ...].  `dir(c, t, r)` is the direction bit
+// t (0 nogap=HORIZ, 1 nogap=VERT, 2 Egap=HORIZ, 3 Fgap=VERT) of cell (r, c), 0 (DIAG) for
+// cells the fill did not write.  Dynprog_traceback_8/_16 (dynprog_simd.c:9154/9553) walk the
+// same way, so the SIMD-semantics kernel shares this with its own direction layout.
+template <typename DA, typename QV, typename GV>
+__device__ __forceinline__ void traceback_walk(int lane, const DA& dir, int r, int c, const Geo& G, const QV& q,
+                                               const QV& quc, const GV& gch, const uint8_t* __restrict__ cons,
+                                               bool watson, uint32_t chroffset, uint32_t chrhigh,
+                                               const uint32_t* __restrict__ blocks, uint64_t nwords,
+                                               gmapdp_pair* out, Tally& t) {
   while (r > 0 && c > 0) {
-    const int k = r - c + uband;
-    const uint32_t isV = dir_bit<R, WORD>(dirs, c, 1, k, W, bitoff);
-    const uint32_t isH = dir_bit<R, WORD>(dirs, c, 0, k, W, bitoff);
+    const uint32_t isV = dir(c, 1, r);
+    const uint32_t isH = dir(c, 0, r);
     if (!isV && isH) {
       // E chain along row r: columns c, c-1, ... while Egap == HORIZ
       int n = 0;
       for (int base = 0;; base += 64) {
         const int j = base + lane;
-        const bool cont = (c - j >= 1) && dir_bit<R, WORD>(dirs, c - j, 2, k + j, W, bitoff);
+        const bool cont = (c - j >= 1) && dir(c - j, 2, r);
         const uint64_t stop = ~ballot(cont);
         if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
       }
@@ -625,7 +627,7 @@ __device__ __forceinline__ void traceback_band(int lane, const WORD* dirs, int W
       int n = 0;
       for (int base = 0;; base += 64) {
         const int j = base + lane;
-        const bool cont = (r - j >= 1) && dir_bit<R, WORD>(dirs, c, 3, k - j, W, bitoff);
+        const bool cont = (r - j >= 1) && dir(c, 3, r - j);
         const uint64_t stop = ~ballot(cont);
         if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
       }
@@ -634,13 +636,12 @@ __device__ __forceinline__ void traceback_band(int lane, const WORD* dirs, int W
       emit_queryskip(lane, r_end + dist, c, dist, G, q, out, t);
       r = r_end;
     } else {
-      // diagonal run at fixed band offset k
+      // diagonal run
       int n = 0;
       for (int base = 0;; base += 64) {
         const int j = base + lane;
         const bool inrange = (c - j >= 1) && (r - j >= 1);
-        const bool cont = (j == 0) || (inrange && !dir_bit<R, WORD>(dirs, c - j, 0, k, W, bitoff) &&
-                                       !dir_bit<R, WORD>(dirs, c - j, 1, k, W, bitoff));
+        const bool cont = (j == 0) || (inrange && !dir(c - j, 0, r - j) && !dir(c - j, 1, r - j));
         const uint64_t stop = ~ballot(cont && inrange);
         if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
       }
@@ -655,6 +656,26 @@ __device__ __forceinline__ void traceback_band(int lane, const WORD* dirs, int W
   } else {
     emit_genomeskip(lane, 1, c, c, G, watson, chroffset, chrhigh, blocks, nwords, out, t);
   }
+}
+
+// direction bits of the banded fills: band offset k = r - c + uband (dir_bit)
+template <int R, typename WORD>
+struct BandDirs {
+  const WORD* dirs;
+  int W, uband, bitoff;
+  __device__ uint32_t operator()(int c, int t, int r) const {
+    return dir_bit<R, WORD>(dirs, c, t, r - c + uband, W, bitoff);
+  }
+};
+
+template <int R, typename WORD = uint64_t, typename QV = const char*, typename GV = const char*>
+__device__ __forceinline__ void traceback_band(int lane, const WORD* dirs, int W, int uband, int r, int c,
+                                               const Geo& G, const QV& q, const QV& quc, const GV& gch,
+                                               const uint8_t* __restrict__ cons, bool watson, uint32_t chroffset,
+                                               uint32_t chrhigh, const uint32_t* __restrict__ blocks,
+                                               uint64_t nwords, gmapdp_pair* out, Tally& t, int bitoff = 0) {
+  const BandDirs<R, WORD> d{dirs, W, uband, bitoff};
+  traceback_walk(lane, d, r, c, G, q, quc, gch, cons, watson, chroffset, chrhigh, blocks, nwords, out, t);
 }
 
 // reverse out[0..n) in place (List_reverse of an already emitted run)
@@ -838,10 +859,9 @@ __host__ __device__ inline Carve carve_dpx(int rlength, int glength) {
 
 // Pair emission of one problem after its fill (the tail of dp_kernel): traceback or the
 // simple/no-gap diagonal, end-gap INDEL trimming and end5 reversal, the result record.
-template <typename QV, typename GV>
+template <typename DA, typename QV, typename GV>
 __device__ __forceinline__ void finish_dp(int lane, const DevProblem& P, int pid, bool simple, int bestr, int bestc,
-                                          const uint64_t* dirs, int bitoff, const QV& q, const QV& quc,
-                                          const GV& gch,
+                                          const DA& dir, const QV& q, const QV& quc, const GV& gch,
                                           const uint8_t* __restrict__ constab, const uint32_t* __restrict__ blocks,
                                           uint64_t nwords, gmapdp_result* __restrict__ results,
                                           gmapdp_pair* __restrict__ pairs) {
@@ -878,9 +898,8 @@ __device__ __forceinline__ void finish_dp(int lane, const DevProblem& P, int pid
   if (is_end && endalign == kQueryendNogaps) {
     emit_diag(lane, bestr, bestc, bestr, G, q, quc, gch, cons, out, t);  // traceback_nogaps
   } else if (!skip) {
-    traceback_band<1, uint64_t, QV, GV>(lane, dirs, P.lband + P.uband + 1, P.uband, bestr, bestc, G, q, quc, gch,
-                                        cons, flags & kFWatson, P.chroffset, P.chrhigh, blocks, nwords, out, t,
-                                        bitoff);
+    traceback_walk(lane, dir, bestr, bestc, G, q, quc, gch, cons, flags & kFWatson, P.chroffset, P.chrhigh, blocks,
+                   nwords, out, t);
   }
   int score = t.score + t.nmatches * kMatch + t.nmismatches * kMismatch;
   int first = 0, npairs = t.count;
@@ -1007,11 +1026,262 @@ __global__ __launch_bounds__(64) void dpx_kernel(
     const Carve cj = carve_dpx(Pj.rlength, Pj.glength);
     unsigned char* bj = smem + lds_dirs + (size_t)j * (size_t)slot;
     const int sj = (Pj.flags & kFRev) ? -1 : 1;
+    const BandDirs<1, uint64_t> dj{wdirs, Pj.lband + Pj.uband + 1, Pj.uband, src};
     finish_dp(lane, Pj, pj, __builtin_amdgcn_readlane((int)simple, src) != 0,
-              __builtin_amdgcn_readlane(bestr, src), __builtin_amdgcn_readlane(bestc, src), wdirs, src,
+              __builtin_amdgcn_readlane(bestr, src), __builtin_amdgcn_readlane(bestc, src), dj,
               QView{qseq + Pj.qbase, sj}, QView{qseq_uc + Pj.qbase, sj},
               GClassView{reinterpret_cast<const uint8_t*>(bj + cj.gcls)}, constab, blocks, nwords, results,
               pairs);
+  }
+}
+
+// ===========================================================================
+// sx_kernel<B>: Dynprog_single_gap as the SIMD builds compute it
+// (gmap.sse42/.avx2/.avx512 link dynprog_simd.c, SURVEY §8 "S" semantics):
+// Dynprog_simd_8 (dynprog_simd.c:2987, B = 32 rows per block, int8
+// saturating) when rlength and glength are both below use8p_size, else
+// Dynprog_simd_16 (:6562, B = 16, int16 saturating), both in the AVX2 layout
+// (dynprog.h:128; AVX-512 builds use the same code), then
+// Dynprog_traceback_8/_16 (:9154/:9553), whose walk is traceback_std's.
+//
+// The reference fills block by block: block rlo covers every column in
+// [max(0, rlo-lband), min(rhigh+uband, glength)] for all B rows, in band or
+// not, then a scalar loop adds vertical gaps inside the band and the band's
+// bottom row is forced diagonal (:3391-3478).  Here one B-lane segment holds
+// one block (lane = row), 64/B problems per wave step side by side, each
+// segment through its own (block, column) sequence; the scalar F loop
+// becomes a segmented max-plus scan.  The row above a block and the F carry
+// live in LDS (two row buffers, one FF row); the direction words of a step go
+// to an L2-resident scratch (4 whole-wave u64 per step).
+//
+// Cells no block writes read as zero / DIAG: the reference reads whatever its
+// Dynprog_T arena held there (it is never cleared, dynprog.c:686-731), i.e. a
+// fresh arena's zeros; DESIGN.md "Parity" has the measured dependence.
+// ===========================================================================
+struct CarveSx {
+  size_t sc, gcls, pb0, pb1, ff, total;
+};
+__host__ __device__ inline int sx_ceil(int rlength, int B) { return ((rlength + B) / B) * B; }  // rlength_ceil
+__host__ __device__ inline CarveSx carve_sx(int rlength, int glength, int B) {
+  CarveSx cv;
+  size_t off = 0;
+  cv.sc = off;   off = align16(off + 4u * (size_t)sx_ceil(rlength, B));  // 4-bit scores by class, rows 0..ceil-1
+  cv.gcls = off; off = align16(off + (size_t)(glength + 2));
+  cv.pb0 = off;  off = align16(off + 2u * (size_t)(glength + 1));       // matrix row above the block (even k)
+  cv.pb1 = off;  off = align16(off + 2u * (size_t)(glength + 1));       // (odd k)
+  cv.ff = off;   off = align16(off + 4u * (size_t)(glength + 1));       // FF[c]: c_gap after the block's last row
+  cv.total = off;
+  return cv;
+}
+// fill steps of one problem: (rlength/B + 1) blocks, each at most B + lband + uband columns wide
+__host__ __device__ inline int sx_stride(int lband, int uband, int B) { return B + lband + uband; }
+__host__ __device__ inline int sx_steps(int rlength, int lband, int uband, int B) {
+  return (rlength / B + 1) * sx_stride(lband, uband, B);
+}
+
+// direction bit t of cell (r, c): block k = r / B holds it at step k*stride + (c - cs_k)
+template <int B>
+struct SxDirs {
+  const uint64_t* dirs;
+  int lband, uband, rlength, glength, bitoff;
+  __device__ uint32_t operator()(int c, int t, int r) const {
+    const int k = r / B, lk = r - k * B;
+    const int cs = max(0, k * B - lband);
+    const int ce = min(min(k * B + B - 1, rlength) + uband, glength);
+    if (c < cs || c > ce) return 0u;
+    const size_t step = (size_t)k * (size_t)sx_stride(lband, uband, B) + (size_t)(c - cs);
+    return (uint32_t)(dirs[step * 4 + t] >> (bitoff + lk)) & 1u;
+  }
+};
+
+__device__ __forceinline__ int sat_add(int a, int b, int lo, int hi) { return min(max(a + b, lo), hi); }
+
+template <int B>
+__global__ __launch_bounds__(64) void sx_kernel(
+    const DevProblem* __restrict__ probs, const int* __restrict__ order, int count, int slot,
+    long long wave_dirs_bytes, unsigned char* __restrict__ gdirs,
+    const uint32_t* __restrict__ blocks, uint64_t nwords,
+    const char* __restrict__ qseq, const char* __restrict__ qseq_uc,
+    const int8_t* __restrict__ sctab, const uint8_t* __restrict__ constab,
+    gmapdp_result* __restrict__ results, gmapdp_pair* __restrict__ pairs) {
+  constexpr int NP = 64 / B;
+  constexpr int NEG = (B == 32) ? -128 : -32768;  // NEG_INFINITY_8 / NEG_INFINITY_16
+  constexpr int POS = (B == 32) ? 127 : 32767;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x;
+  const int seg = lane / B, sl = lane & (B - 1);
+  const int idx = blockIdx.x * NP + seg;
+  const bool live = idx < count;
+  const int pid = order[live ? idx : blockIdx.x * NP];
+  const DevProblem P = probs[pid];
+  const int rlen = live ? P.rlength : 0, glen = live ? P.glength : 0;
+  const int flags = P.flags;
+  const int lband = P.lband, uband = P.uband, open = P.open, ext = P.extend;
+  const int late = (flags & kFLate) ? 1 : 0;
+  uint64_t* wdirs = reinterpret_cast<uint64_t*>(gdirs + (size_t)blockIdx.x * (size_t)wave_dirs_bytes);
+  unsigned char* base = smem + (size_t)seg * (size_t)slot;
+  const CarveSx cv = carve_sx(rlen, glen, B);
+  int32_t* sc4 = reinterpret_cast<int32_t*>(base + cv.sc);
+  uint8_t* gcl = reinterpret_cast<uint8_t*>(base + cv.gcls);
+  int16_t* pb0 = reinterpret_cast<int16_t*>(base + cv.pb0);
+  int16_t* pb1 = reinterpret_cast<int16_t*>(base + cv.pb1);
+  int* FF = reinterpret_cast<int*>(base + cv.ff);
+  const int8_t* sct = sctab + (size_t)P.mismatchtype * 128 * kNClass;
+  const uint8_t* cons = constab + (size_t)P.genestrand * 128 * kNClass;
+  const int ceil_r = sx_ceil(rlen, B);
+
+  // ---- stage: pairscores[5][rlength_ceil] as one word of 4-bit scores per row (row 0 scores
+  //      'N', rows past rlength never reach rows <= rlength), the genome classes, zeroed rows ----
+  const bool score_uc = flags & kFScoreUC;
+  for (int i = sl; i < ceil_r; i += B) {
+    uint32_t w = 0;
+    if (live && i <= rlen) {
+      const char c1 = (i == 0) ? 'N' : (score_uc ? qseq_uc[P.qbase + i - 1] : qseq[P.qbase + i - 1]);
+      const uint64_t row = *reinterpret_cast<const uint64_t*>(sct + (uint8_t)(c1 & 127) * kNClass);
+#pragma unroll
+      for (int g = 0; g < 5; g++) w |= (uint32_t)((row >> (8 * g)) & 0xfu) << (4 * g);
+    }
+    if (live) sc4[i] = (int32_t)w;
+  }
+  const bool segleft = flags & kFSegLeft, segrc = flags & kFSegRevcomp;
+  for (int i = sl; i < glen; i += B)
+    gcl[i + 1] = gclass(segment_nt(blocks, nwords, (uint32_t)i, (uint32_t)glen, P.segpos, P.segbound, segleft, segrc));
+  for (int i = sl; i <= glen; i += B) {
+    pb0[i] = 0;
+    pb1[i] = 0;
+  }
+  __syncthreads();
+
+  // ---- single_gap_simple test per segment (glength == rlength, <= 1 mismatch) ----
+  const QView qucv{qseq_uc + P.qbase, 1};
+  const GClassView gv{gcl};
+  const bool try_simple = live && P.kind == kSingle && glen == rlen;
+  int rmax = rlen;
+#pragma unroll
+  for (int off = B; off < 64; off <<= 1) rmax = max(rmax, __shfl_xor(rmax, off, 64));
+  int nmism = 0;
+  const uint64_t segmask = ((B == 64) ? ~0ull : ((1ull << B) - 1ull)) << (seg * B);
+  for (int b0 = 0; b0 < rmax; b0 += B) {
+    const int r = b0 + sl + 1;
+    bool mism = false;
+    if (try_simple && r <= rlen) {
+      const char c1u = qucv[r], c2 = gv[r];
+      mism = (c2 != '*') && (c1u != c2) && !cons[(uint8_t)(c1u & 127) * kNClass + gcl[r]];
+    }
+    nmism += __popcll(ballot(mism) & segmask);
+  }
+  const bool simple = try_simple && nmism <= 1;
+
+  // ---- the block fills, segments side by side ----
+  const bool fills = live && !simple;
+  const int nblk = fills ? rlen / B + 1 : 0;
+  const int stride = sx_stride(lband, uband, B);
+  int tmax = nblk * stride;
+#pragma unroll
+  for (int off = B; off < 64; off <<= 1) tmax = max(tmax, __shfl_xor(tmax, off, 64));
+  int k = 0, o = 0;        // block, column step within the block
+  int H = 0, E = 0;        // this lane's row: stored score / horizontal gap of the previous column
+  for (int t = 0; t < tmax; t++) {
+    const int rlo = k * B;
+    const int rhigh = min(rlo + B - 1, rlen);
+    const int cs = max(0, rlo - lband);
+    const int ce = min(rhigh + uband, glen);
+    const int c = cs + o;
+    const bool act = (k < nblk) && (c <= ce);
+    const int r = rlo + sl;
+    const int16_t* pin = (k & 1) ? pb0 : pb1;  // block k reads the row block k-1 wrote
+    int16_t* pout = (k & 1) ? pb1 : pb0;
+    if (o == 0) {  // INFINITE_INITIAL_GAP_PENALTY block start: "compensate for T1 = H + open"
+      E = late ? NEG : NEG + 1;
+      H = NEG - open;
+    }
+    int X = NEG, G0 = kNegInf32, Lv = kNegInf32, cls = 0;
+    if (act) {
+      X = (c == 0) ? (rlo == 0 ? 0 : NEG) : (rlo == 0 ? NEG : (int)pin[c - 1]);
+      cls = (c == 0) ? 0 : min((int)gcl[c], (int)kN);  // nt_to_int_array: '*' scores as 'N'
+      if (rlo > 0 && c < rlo + uband) {
+        G0 = FF[c];
+        Lv = pin[c];
+      }
+    }
+    // EGAP (horizontal): T1 = H + open, E >= T1 (late) / E > T1
+    const int T1 = sat_add(H, open, NEG, POS);
+    bool dE = late ? (E >= T1) : (E > T1);
+    const int En = sat_add(max(E, T1), ext, NEG, POS);
+    // NOGAP: H shifted down one row (row rlo from the row above), plus the pair score
+    const int Hs = seg_shr1<B>(H, X, sl);
+    int p;
+    if (c == 0) p = (r == 0) ? 0 : NEG;  // pairscores_col0
+    else p = __builtin_amdgcn_sbfe(sc4[min(r, ceil_r - 1)], cls * 4, 4);
+    const int Hd = sat_add(Hs, p, NEG, POS);
+    bool dN = late ? (En >= Hd) : (En > Hd);
+    int Hn = max(Hd, En);
+    int rhc = rhigh;
+    if (rhigh >= c + lband) {
+      rhc = c + lband;
+      if (c > 0 && r == rhc) {  // bottom of the band: diagonal only
+        Hn = Hd;
+        dE = false;
+        dN = false;
+      }
+    }
+    // F loop: vertical gaps in rows [rloc, rhc]; the band's top row starts a fresh chain
+    const int rloc = max(rlo, c - uband);
+    const bool top = rloc == c - uband;
+    const int Htop = __shfl(Hn, seg * B + min(max(rloc - rlo, 0), B - 1), 64);
+    int rs = rloc;
+    if (top) {
+      G0 = Lv + open + ext;
+      Lv = Htop;
+      rs = rloc + 1;
+    }
+    const int A = (r >= rs && r <= rhc - 1) ? Hn + open - r * ext : kSent;
+    const int A0 = max(G0, Lv + open) - (rs - 1) * ext;
+    const int Xex = seg_shr1<B>(seg_scan_max<B>(A), kSent, sl);
+    const int F = r * ext + max(A0, Xex);
+    const int Fup = seg_shr1<B>(F, G0, sl);
+    const int Lup = seg_shr1<B>(max(F, Hn), Lv, sl);
+    const bool inF = act && r >= rs && r <= rhc;
+    const int Fprev = (r == rs) ? G0 : Fup;
+    const int Lprev = (r == rs) ? Lv : Lup;
+    const bool vF = inF && (late ? (Fprev >= Lprev + open) : (Fprev > Lprev + open));
+    const bool vN = inF && (late ? (F >= Hn) : (F > Hn));
+    const int Hf = vN ? max(F, NEG) : Hn;
+    const int Flast = __shfl(F, seg * B + min(max(rhc - rlo, 0), B - 1), 64);
+    const uint64_t mH = ballot(act && dN && !vN), mV = ballot(vN), mE = ballot(act && dE), mF = ballot(vF);
+    if (act) {
+      H = Hf;
+      E = En;
+      if (sl == 0) FF[c] = (rhc >= rs) ? Flast : G0;
+      if (sl == B - 1) pout[c] = (int16_t)Hf;
+    }
+    if (lane == 0) {
+      uint64_t* d = wdirs + (size_t)t * 4;
+      d[0] = mH;
+      d[1] = mV;
+      d[2] = mE;
+      d[3] = mF;
+    }
+    if (k < nblk && ++o == stride) {
+      o = 0;
+      k++;
+    }
+  }
+  __threadfence_block();
+  __syncthreads();
+
+  // ---- emission, one problem at a time with the whole wave ----
+  for (int j = 0; j < NP; j++) {
+    const int src = j * B;
+    if (!__builtin_amdgcn_readlane((int)live, src)) continue;
+    const int pj = __builtin_amdgcn_readlane(pid, src);
+    const DevProblem Pj = probs[pj];
+    const CarveSx cj = carve_sx(Pj.rlength, Pj.glength, B);
+    unsigned char* bj = smem + (size_t)j * (size_t)slot;
+    const SxDirs<B> dj{wdirs, Pj.lband, Pj.uband, Pj.rlength, Pj.glength, src};
+    finish_dp(lane, Pj, pj, __builtin_amdgcn_readlane((int)simple, src) != 0, Pj.rlength, Pj.glength, dj,
+              QView{qseq + Pj.qbase, 1}, QView{qseq_uc + Pj.qbase, 1},
+              GClassView{reinterpret_cast<const uint8_t*>(bj + cj.gcls)}, constab, blocks, nwords, results, pairs);
   }
 }
 
@@ -1557,6 +1827,28 @@ hipError_t launch_dpx(int S, int nproblems, int slot, int dirs_bytes, unsigned c
   }
   const int nblocks = (nproblems + np - 1) / np;
   void* args[] = {(void*)&probs, (void*)&order, (void*)&nproblems, (void*)&slot, (void*)&dirs_bytes,
+                  (void*)&gdirs, (void*)&blocks, (void*)&nwords, (void*)&qseq, (void*)&qseq_uc, (void*)&sctab,
+                  (void*)&constab, (void*)&results, (void*)&pairs};
+  return hipLaunchKernel(fn, dim3(nblocks), dim3(64), args, lds, stream);
+}
+
+size_t lds_slot_sx(int rlength, int glength, int B) { return carve_sx(rlength, glength, B).total; }
+int steps_sx(int rlength, int lband, int uband, int B) { return sx_steps(rlength, lband, uband, B); }
+
+hipError_t launch_sx(int B, int nproblems, int slot, long long wave_dirs_bytes, unsigned char* gdirs,
+                     hipStream_t stream, const DevProblem* probs, const int* order, const uint32_t* blocks,
+                     uint64_t nwords, const char* qseq, const char* qseq_uc, const int8_t* sctab,
+                     const uint8_t* constab, gmapdp_result* results, gmapdp_pair* pairs) {
+  if (B != 16 && B != 32) return hipErrorInvalidValue;
+  void* fn = (B == 16) ? reinterpret_cast<void*>(&sx_kernel<16>) : reinterpret_cast<void*>(&sx_kernel<32>);
+  const int np = 64 / B;
+  const size_t lds = (size_t)slot * np;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  const int nblocks = (nproblems + np - 1) / np;
+  void* args[] = {(void*)&probs, (void*)&order, (void*)&nproblems, (void*)&slot, (void*)&wave_dirs_bytes,
                   (void*)&gdirs, (void*)&blocks, (void*)&nwords, (void*)&qseq, (void*)&qseq_uc, (void*)&sctab,
                   (void*)&constab, (void*)&results, (void*)&pairs};
   return hipLaunchKernel(fn, dim3(nblocks), dim3(64), args, lds, stream);

@@ -31,6 +31,12 @@ hipError_t launch_dp(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
                      gmapdp_pair* pairs, uint64_t* gdirs);
 size_t lds_slot_dpx(int rlength, int glength);
 size_t lds_dirs_dpx(int gmax);
+size_t lds_slot_sx(int rlength, int glength, int B);
+int steps_sx(int rlength, int lband, int uband, int B);
+hipError_t launch_sx(int B, int nproblems, int slot, long long wave_dirs_bytes, unsigned char* gdirs,
+                     hipStream_t stream, const DevProblem* probs, const int* order, const uint32_t* blocks,
+                     uint64_t nwords, const char* qseq, const char* qseq_uc, const int8_t* sctab,
+                     const uint8_t* constab, gmapdp_result* results, gmapdp_pair* pairs);
 hipError_t launch_dpx(int S, int nproblems, int slot, int dirs_bytes, unsigned char* gdirs, hipStream_t stream,
                       const DevProblem* probs, const int* order, const uint32_t* blocks, uint64_t nwords,
                       const char* qseq, const char* qseq_uc, const int8_t* sctab, const uint8_t* constab,
@@ -193,7 +199,8 @@ struct PlanCore {
   std::vector<DevGenomeProblem> gdev;  // Dynprog_genome_gap problems on the GPU
   std::vector<int> gdev_index;       // genome problem index -> gdev slot (-1: resolved on host)
   std::vector<int> gdev_problem;     // gdev slot -> genome problem index
-  enum Kind { kDp = 0, kGenomeGap = 1, kDpx = 2 };  // kDpx: 64/S narrow problems per wave, R = S
+  // kDpx: 64/S narrow problems per wave, R = S; kSx: SIMD-build semantics, 64/B problems per wave, R = B
+  enum Kind { kDp = 0, kGenomeGap = 1, kDpx = 2, kSx = 3 };
   struct Launch {
     int kind;
     int R;           // band words per lane (kDp, kGenomeGap) or segment width S (kDpx)
@@ -446,7 +453,8 @@ static int convert_single(const gmapdp_ctx* ctx, const gmapdp_single_problem& p,
     d.open = -6; d.extend = -1;
   }
   const bool watson = p.flags & GMAPDP_WATSON;
-  d.flags = (watson ? kFWatson : 0) | ((p.flags & GMAPDP_JUMP_LATE) ? kFLate : 0);
+  d.flags = (watson ? kFWatson : 0) | ((p.flags & GMAPDP_JUMP_LATE) ? kFLate : 0) |
+            ((p.flags & GMAPDP_SIMD) ? kFSimd : 0);
   if (watson) {
     d.segpos = p.chroffset + (uint32_t)p.goffset;  // Genome_get_segment_right(left, chrhigh)
     d.segbound = p.chrhigh;
@@ -470,6 +478,10 @@ static int convert_end(gmapdp_ctx* ctx, const gmapdp_end_problem& p, gmapdp_resu
   const bool nogaps = p.endalign == kQueryendNogaps;
   if (p.endalign < 0 || p.endalign > 3) {
     *err = bad(ctx, "endalign out of range");
+    return 0;
+  }
+  if (p.flags & GMAPDP_SIMD) {
+    *err = bad(ctx, "GMAPDP_SIMD: the SIMD builds' end-gap fills (Dynprog_simd_*_upper/_lower) are not implemented");
     return 0;
   }
   int rlength = p.rlength, glength = p.glength;
@@ -548,6 +560,10 @@ static int convert_genome(gmapdp_ctx* ctx, const gmapdp_genome_problem& p, gmapd
   res.gap_index = -1;
   res.gap_queryjump = 0;
   res.dynprogindex = p.dynprogindex;
+  if (p.flags & GMAPDP_SIMD) {
+    *err = bad(ctx, "GMAPDP_SIMD: the SIMD builds' genome-gap fills (bridge_intron_gap_*_ud) are not implemented");
+    return 0;
+  }
   if (p.rlength <= 1) {
     res.traceback_score = GMAPDP_NEG_INFINITY_32;
     return 0;
@@ -626,6 +642,16 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     d.pair_offset = (int32_t)pair_off;
     pair_off += (size_t)d.rlength + (size_t)d.glength + 2;
     const bool nofill = d.kind != kSingle && d.endalign == kQueryendNogaps;
+    if (d.flags & kFSimd) {
+      // Dynprog_single_gap of the SIMD builds (dynprog_single.c:593-631): 8-bit blocks of 32 rows when
+      // both lengths are below use8p_size (dynprog.c:1022-1025), else 16-bit blocks of 16 rows
+      static const int use8p[4] = {41, 63, 127, 24};
+      const int B = (d.rlength < use8p[d.mismatchtype] && d.glength < use8p[d.mismatchtype]) ? 32 : 16;
+      const size_t slot = gg_lds_bucket(lds_slot_sx(d.rlength, d.glength, B));
+      if (slot * (64 / B) > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
+      classes[std::make_tuple((int)PlanCore::kSx, B, 0, slot)].push_back((int)s);
+      continue;
+    }
     if (d.open > 0 && !nofill) return bad(ctx, "positive gap-open penalty is not supported by the scan formulation");
     if (d.lband < 0 || d.uband < 0) return bad(ctx, "negative band");
     const int W = d.lband + d.uband + 1;
@@ -699,6 +725,16 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     L.work = 0.0;
     L.extra = 0;
     L.gdirs_offset = 0;
+    if (L.kind == PlanCore::kSx) {  // per wave: 4 direction words per fill step
+      int smax = 0;
+      for (int id : ids)
+        smax = std::max(smax, steps_sx(plan.dev[id].rlength, plan.dev[id].lband, plan.dev[id].uband, L.R));
+      L.extra = (size_t)smax * 32u;
+      L.dirs_lds = false;
+      L.gdirs_offset = gdirs_off;
+      const size_t nblocks = ((size_t)L.count + (64 / L.R) - 1) / (64 / L.R);
+      gdirs_off += (nblocks * L.extra + 255) & ~(size_t)255;
+    }
     if (L.kind == PlanCore::kDpx) {
       int gmax = 0;
       for (int id : ids) gmax = std::max(gmax, (int)plan.dev[id].glength);
@@ -718,7 +754,10 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
         L.work += (double)std::max(d.glengthL, d.glengthR) * L.R + d.rlength;
       } else {
         const DevProblem& d = plan.dev[id];
-        L.work += (double)d.glength * (L.kind == PlanCore::kDpx ? L.R / 64.0 : L.R) + 0.25 * (d.rlength + d.glength);
+        if (L.kind == PlanCore::kSx)
+          L.work += (double)steps_sx(d.rlength, d.lband, d.uband, L.R) * L.R / 64.0 + 0.25 * (d.rlength + d.glength);
+        else
+          L.work += (double)d.glength * (L.kind == PlanCore::kDpx ? L.R / 64.0 : L.R) + 0.25 * (d.rlength + d.glength);
       }
     }
     L.stream = 0;
@@ -808,6 +847,10 @@ struct RunArgs {
 
 static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, const RunArgs& a, hipStream_t stream) {
   const auto& L = plan.launches[li];
+  if (L.kind == PlanCore::kSx)
+    return launch_sx(L.R, L.count, (int)L.lds, (long long)L.extra, (unsigned char*)ctx->gdirs.p + L.gdirs_offset,
+                     stream, a.d_probs, a.d_order + L.first, ctx->d_genome, ctx->genome_words, a.d_q, a.d_quc,
+                     ctx->d_sc, ctx->d_cs, a.d_results, a.d_pairs);
   if (L.kind == PlanCore::kDpx)
     return launch_dpx(L.R, L.count, (int)L.lds, (int)L.extra,
                       L.dirs_lds ? nullptr : (unsigned char*)ctx->gdirs.p + L.gdirs_offset, stream, a.d_probs,

@@ -28,6 +28,7 @@ constexpr int32_t kFSegLeft = 0x8;    // genome segment via Genome_get_segment_l
 constexpr int32_t kFSegRevcomp = 0x10;
 constexpr int32_t kFRev = 0x20;       // revp: DP runs away from the anchor (end5)
 constexpr int32_t kFScoreUC = 0x40;   // the fill scores rsequenceuc (Dynprog_end3_gap) instead of rsequence
+constexpr int32_t kFSimd = 0x80;      // SIMD-build semantics (Dynprog_simd_8/16, sx_kernel)
 
 // Device-side problem descriptor derived on the host (penalties, bands,
 // orientation and the launch class are resolved once, in the plan).

@@ -18,6 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GMAPDP_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libgmapdp.so")
 
 WATSON, JUMP_LATE, WIDEBAND = 0x1, 0x2, 0x4
+SIMD = 0x40  # GMAPDP_SIMD: the reference's SIMD builds' semantics (single gaps)
 HALFP, FINALP = 0x8, 0x10
 UNSET = -2147483648
 NEG_INFINITY_32 = -32768
@@ -262,7 +263,7 @@ class Engine:
             probs[i]["chroffset"] = p["chroffset"]
             probs[i]["chrhigh"] = p["chrhigh"]
             probs[i]["flags"] = ((WATSON if p["watsonp"] else 0) | (JUMP_LATE if p["jump_late_p"] else 0) |
-                                 (WIDEBAND if p["widebandp"] else 0))
+                                 (WIDEBAND if p["widebandp"] else 0) | (SIMD if p.get("simd") else 0))
             probs[i]["genestrand"] = p["genestrand"]
             probs[i]["extraband"] = p["extraband"]
             probs[i]["defect_rate"] = p["defect_rate"]
@@ -311,7 +312,8 @@ class Engine:
                       "end3p", "endalign", "require_pos_score_p", "dynprogindex", "defect_rate"):
                 probs[i][k] = p[k]
             probs[i]["extraband"] = p["extraband"]
-            probs[i]["flags"] = (WATSON if p["watsonp"] else 0) | (JUMP_LATE if p["jump_late_p"] else 0)
+            probs[i]["flags"] = ((WATSON if p["watsonp"] else 0) | (JUMP_LATE if p["jump_late_p"] else 0) |
+                                 (SIMD if p.get("simd") else 0))
             qparts.append(q)
             qucparts.append(quc)
             off += len(q)

@@ -80,6 +80,11 @@ typedef struct {
 #define GMAPDP_WATSON     0x1  /* watsonp */
 #define GMAPDP_JUMP_LATE  0x2  /* jump_late_p */
 #define GMAPDP_WIDEBAND   0x4  /* widebandp */
+/* Reproduce the reference's SIMD builds (gmap.sse42/.avx2/.avx512: Dynprog_simd_8/16 fills,
+ * dynprog_simd.c) instead of the nosimd build (Dynprog_standard).  Single gaps only so far:
+ * the end and genome-gap entry points return GMAPDP_EINVAL for it.  The SIMD fills read
+ * arena cells the call never wrote; the engine defines those as zero (a fresh arena). */
+#define GMAPDP_SIMD       0x40
 
 /* One Dynprog_single_gap call (dynprog_single.c:429 argument list).  The
  * query slice is qseq[qoff .. qoff+rlength) (rsequence, case as given) and

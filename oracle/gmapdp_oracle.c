@@ -57,6 +57,7 @@ static short pairdistance[4][128][128];
 static unsigned char consistent[3][128][128];
 static int use8p_size[4];
 static int g_mode;
+static int g_simd;  /* 1: the SIMD (AVX2) build's semantics, 0: nosimd */
 static int g_user_open, g_user_extend, g_user_dynprog_p;
 static void intron_score_setup (void);
 
@@ -168,6 +169,14 @@ orc_init (int mode, int user_open, int user_extend, int user_dynprog_p) {
   case TTOC_NONSTRANDED: set_oneway('C', 'T', FULLMATCH, 1); set_oneway('G', 'A', FULLMATCH, 2); break;
   default: return -1;
   }
+  return 0;
+}
+
+/* Select the semantics the oracle restates: 0 the nosimd build, 1 the SIMD (AVX2) build
+   (single gaps only so far; the other entry points keep nosimd). */
+int
+orc_set_simd (int simd) {
+  g_simd = simd ? 1 : 0;
   return 0;
 }
 
@@ -579,6 +588,166 @@ single_gap_simple (PairSink *s, Tally *t, const char *rsequence, const char *rse
   return t->nmismatches > 1 ? 0 : 1;
 }
 
+/* ---------------------------------------------------------------------------
+ * SIMD-build fills (the "S" semantics of SURVEY §8: gmap.sse42/.avx2/.avx512
+ * link dynprog_simd.c instead of Dynprog_standard).  Restated for the AVX2
+ * layout (dynprog.h:128: 32 8-bit / 16 16-bit rows per block; the AVX-512
+ * build uses the same dynprog code) with INFINITE_INITIAL_GAP_PENALTY
+ * (dynprog.h:14).
+ *
+ * Dynprog_simd_8 / Dynprog_simd_16 (dynprog_simd.c:2987 / :6562) fill the
+ * matrix in blocks of B rows.  Block rlo covers columns
+ * [max(0, rlo-lband), min(rhigh+uband, glength)] for all B rows, in band or
+ * not, with saturating 8/16-bit arithmetic; a scalar loop then adds the
+ * vertical gaps inside the band (:3391-3478).  The row above a block
+ * (matrix[c-1][rlo-1]) is read for every column of the block, including
+ * columns the block above never wrote, and the traceback can walk into cells
+ * no block wrote.  Those reads see whatever the Dynprog_T arena held before
+ * the call (Dynprog_new never clears it, dynprog.c:686-731): the reference's
+ * S output is not a function of its inputs alone.  This restatement, like the
+ * engine, defines it on an arena that reads zero (DIAG) wherever the call
+ * did not write -- what a fresh process's first call sees, and what the tests
+ * pin by zeroing the reference's arenas (refh_poison_arenas) before each call.
+ * ------------------------------------------------------------------------- */
+static inline int
+sat_add (int a, int b, int lo, int hi) {
+  int s = a + b;
+  return s < lo ? lo : (s > hi ? hi : s);
+}
+
+/* nt_to_int_array (dynprog.c:1012-1019): A C G T (either case) -> 0..3, anything else -> 4 ('N') */
+static inline int
+nt_to_int (int c) {
+  switch (c) {
+  case 'A': case 'a': return 0;
+  case 'C': case 'c': return 1;
+  case 'G': case 'g': return 2;
+  case 'T': case 't': return 3;
+  default: return 4;
+  }
+}
+
+/* Full-band S fill (Dynprog_simd_8 when bits == 8, else Dynprog_simd_16).  Writes the three
+   direction planes of traceback_std's layout (IDX(c, r), r <= rlength), DIAG where no block wrote. */
+static void
+simd_fill_full (int bits, const char *rsequence, const char *gsequence, const char *gsequence_alt,
+                int rlength, int glength, int mismatchtype, int open, int extend, int lband, int uband,
+                int late, int revp, signed char *dirs) {
+  const int B = (bits == 8) ? 32 : 16;
+  const int NEG = (bits == 8) ? -128 : -32768, POS = (bits == 8) ? 127 : 32767;
+  const int ceil = ((rlength + B) / B) * B;  /* rlength_ceil: the arena's column pitch */
+  const size_t cells = (size_t) (glength + 1) * (size_t) ceil;
+  size_t plane = (size_t) (glength + 1) * (size_t) (rlength + 1);
+  short (*pd)[128] = pairdistance[mismatchtype];
+  static const char acgtn[5] = {'A', 'C', 'G', 'T', 'N'};
+  int *mat = (int *) calloc(cells, sizeof(int));            /* Score8/16 matrix, zeroed arena */
+  signed char *dn = (signed char *) calloc(cells, 1), *de = (signed char *) calloc(cells, 1);
+  signed char *df = (signed char *) calloc(cells, 1);        /* Fgap is calloc'ed by the call itself */
+  int *ps = (int *) malloc((size_t) 5 * ceil * sizeof(int));  /* pairscores[5][rlength_ceil] */
+  int *FF = (int *) malloc((size_t) (glength + 1) * sizeof(int));
+  int H[32], E[32], Hs[32], Hn[32];
+  int rlo, rhigh, c, i, k, r, na1, na2, na2a, X, T1, rlo_calc, rhigh_calc, c_gap, last_nogap, score;
+
+  for (k = 0; k < 5; k++) {
+    for (r = 0; r < ceil; r++) {
+      if (r == 0) na1 = 'N';
+      else if (r <= rlength) na1 = (unsigned char) (revp ? rsequence[1 - r] : rsequence[r - 1]);
+      else { ps[k * ceil + r] = 0; continue; }  /* past rlength: never reaches rows <= rlength */
+      ps[k * ceil + r] = pd[na1][(int) acgtn[k]];
+    }
+  }
+
+  for (rlo = 0; rlo <= rlength; rlo += B) {
+    rhigh = (rlo + B - 1 > rlength) ? rlength : rlo + B - 1;
+    c = (rlo - lband < 0) ? 0 : rlo - lband;
+    for (i = 0; i < B; i++) {
+      E[i] = late ? NEG : NEG + 1;
+      H[i] = NEG - open;                       /* "compensate for T1 = H + open" */
+    }
+    for (; c <= rhigh + uband && c <= glength; c++) {
+      int *col = mat + (size_t) c * ceil;
+      if (c == 0) X = (rlo == 0) ? 0 : NEG;
+      else X = (rlo == 0) ? NEG : mat[(size_t) (c - 1) * ceil + rlo - 1];
+      na2 = na2a = 4;
+      if (c > 0) {
+        na2 = nt_to_int((unsigned char) (revp ? gsequence[1 - c] : gsequence[c - 1]));
+        na2a = nt_to_int((unsigned char) (revp ? gsequence_alt[1 - c] : gsequence_alt[c - 1]));
+      }
+      for (i = 0; i < B; i++) {
+        int p, pa, Hd;
+        /* EGAP */
+        T1 = sat_add(H[i], open, NEG, POS);
+        de[(size_t) c * ceil + rlo + i] = (late ? (E[i] >= T1) : (E[i] > T1)) ? HORIZ : DIAG;
+        E[i] = sat_add(E[i] > T1 ? E[i] : T1, extend, NEG, POS);
+        /* NOGAP: H shifted down one row, row rlo from the row above the block */
+        Hs[i] = (i == 0) ? X : H[i - 1];
+        if (c == 0) p = (rlo + i == 0) ? 0 : NEG;  /* pairscores_col0 */
+        else {
+          p = ps[na2 * ceil + rlo + i];
+          pa = ps[na2a * ceil + rlo + i];
+          if (pa > p) p = pa;
+        }
+        Hd = sat_add(Hs[i], p, NEG, POS);
+        dn[(size_t) c * ceil + rlo + i] = (late ? (E[i] >= Hd) : (E[i] > Hd)) ? HORIZ : DIAG;
+        Hn[i] = Hd > E[i] ? Hd : E[i];
+        col[rlo + i] = Hn[i];
+      }
+      /* F loop (:3391-3478) */
+      rlo_calc = (rlo < c - uband) ? c - uband : rlo;
+      if ((rhigh_calc = rhigh) >= c + lband) {
+        rhigh_calc = c + lband;
+        if (c > 0) {  /* bottom row: diagonal only, so no path leaves the band below */
+          int p = ps[na2 * ceil + rhigh_calc], pa = ps[na2a * ceil + rhigh_calc];
+          if (pa > p) p = pa;
+          score = mat[(size_t) (c - 1) * ceil + rhigh_calc - 1] + p;
+          col[rhigh_calc] = score < NEG ? NEG : (score > POS ? POS : score);
+          de[(size_t) c * ceil + rhigh_calc] = DIAG;
+          dn[(size_t) c * ceil + rhigh_calc] = DIAG;
+        }
+      }
+      if (rlo == 0 || c >= rlo + uband) {
+        c_gap = NEG_INFINITY_32;
+        last_nogap = NEG_INFINITY_32;
+      } else {
+        c_gap = FF[c];
+        last_nogap = col[rlo_calc - 1];
+      }
+      if ((r = rlo_calc) == c - uband) {  /* top of the band: no vertical gap into it */
+        c_gap = last_nogap + open + extend;
+        last_nogap = col[r];
+        r++;
+      }
+      for (; r <= rhigh_calc; r++) {
+        score = last_nogap + open;
+        if (late ? (c_gap >= score) : (c_gap > score)) {
+          c_gap += extend;
+          df[(size_t) c * ceil + r] = VERT;
+        } else {
+          c_gap = score + extend;
+        }
+        last_nogap = col[r];
+        if (late ? (c_gap >= last_nogap) : (c_gap > last_nogap)) {
+          last_nogap = c_gap;
+          col[r] = c_gap < NEG ? NEG : c_gap;
+          dn[(size_t) c * ceil + r] = VERT;
+        }
+      }
+      FF[c] = c_gap;
+      for (i = 0; i < B; i++) H[i] = col[rlo + i];  /* reload after the F loop */
+    }
+  }
+
+  memset(dirs, DIAG, 3 * plane);
+  for (c = 0; c <= glength; c++) {
+    for (r = 0; r <= rlength; r++) {
+      dirs[IDX(c, r)] = dn[(size_t) c * ceil + r];
+      dirs[plane + IDX(c, r)] = de[(size_t) c * ceil + r];
+      dirs[2 * plane + IDX(c, r)] = df[(size_t) c * ceil + r];
+    }
+  }
+  free(mat); free(dn); free(de); free(df); free(ps); free(FF);
+}
+
 static void
 reverse_pairs (OrcPair *p, int n) {
   int i, j;
@@ -643,8 +812,15 @@ orc_single_gap (const char *rsequence, const char *rsequenceuc, int rlength, int
   compute_bands(&lband, &uband, rlength, glength, extraband_single, widebandp);
   matrix = (int *) malloc((size_t) (glength + 1) * (rlength + 1) * sizeof(int));
   dirs = (signed char *) malloc((size_t) 3 * (glength + 1) * (rlength + 1));
-  orc_standard_fill(rsequence, gseq, gseq_alt, rlength, glength, mismatchtype, open, extend, lband, uband,
-                    jump_late_p, /*revp*/0, /*saturation*/NEG_INFINITY_32, 1, 1, matrix, dirs);
+  if (g_simd) {
+    /* dynprog_single.c:593-631: 8-bit fill when both lengths are below use8p_size */
+    int bits = (rlength < use8p_size[mismatchtype] && glength < use8p_size[mismatchtype]) ? 8 : 16;
+    simd_fill_full(bits, rsequence, gseq, gseq_alt, rlength, glength, mismatchtype, open, extend, lband, uband,
+                   jump_late_p, /*revp*/0, dirs);
+  } else {
+    orc_standard_fill(rsequence, gseq, gseq_alt, rlength, glength, mismatchtype, open, extend, lband, uband,
+                      jump_late_p, /*revp*/0, /*saturation*/NEG_INFINITY_32, 1, 1, matrix, dirs);
+  }
   traceback_std(&sink, &t, dirs, rlength, glength, rlength, glength, rsequence, rsequenceuc, gseq, gseq_alt,
                 roffset, goffset, /*revp*/0, chroffset, chrhigh, watsonp, genestrand, dynprogindex);
   /* pushes prepend; List_reverse (dynprog_single.c:675) => list order == push order */

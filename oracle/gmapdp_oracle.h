@@ -41,6 +41,7 @@ int orc_set_genome (const char *genome, unsigned int length);
 /* Dynprog_single_gap (dynprog_single.c:429), nosimd semantics.
    scalars[0..5] = dynprogindex(after), finalscore, nmatches, nmismatches,
    nopens, nindels.  Returns npairs (list order), or -1 for a NULL list. */
+int orc_set_simd (int simd);
 int orc_single_gap (const char *rsequence, const char *rsequenceuc, int rlength, int glength,
                     int roffset, int goffset, unsigned int chroffset, unsigned int chrhigh,
                     int watsonp, int genestrand, int jump_late_p, int extraband_single, int widebandp,

@@ -63,6 +63,8 @@ FLAGS_avx2   := -mpopcnt -DHAVE_SSE2=1 -DHAVE_SSSE3=1 -DHAVE_SSE4_1=1 -DHAVE_SSE
 # dereferences the FREEA-nulled leftdi (dynprog_genome.c:2879-2888) and crashes.
 FLAGS_nosimda := -DHAVE_ALLOCA=1 -DHAVE_ALLOCA_H=1
 
+.DEFAULT_GOAL := all
+
 VARIANTS := nosimd avx2 nosimda
 
 define variant_rules

@@ -81,6 +81,47 @@ refh_init (int user_open, int user_extend, int user_dynprog_p) {
   return 0;
 }
 
+/* Fill the SIMD builds' score and direction arenas (Dynprog_new, dynprog.c:686-731: posix_memalign'd, never
+   cleared) with one byte value.  Test instrumentation: Dynprog_simd_{8,16}[_upper/_lower] read
+   matrix cells outside the row block they computed (e.g. dynprog_simd.c:3290
+   matrix[c-1][rlo-1]), so their output can depend on what earlier calls left there; the tests
+   call this to measure that dependence.  A no-op for the nosimd build. */
+int
+refh_poison_arenas (int byte, int what) {
+#ifdef HAVE_SSE2
+  size_t one = (size_t)(dynprogM->max_glength + 1) * (dynprogM->max_rlength + SIMD_NCHARS + SIMD_NCHARS) * 2;
+  size_t up = (size_t)(dynprogL->max_glength + 1) * (dynprogL->max_rlength + SIMD_NCHARS + SIMD_NCHARS) * 2;
+  size_t lo = (size_t)(dynprogL->max_rlength + 1) * (dynprogL->max_glength + SIMD_NCHARS + SIMD_NCHARS) * 2;
+  Dynprog_T two[2];
+  int k;
+  if (what & 1) memset(dynprogM->aligned.one.matrix_space, byte, one);
+  if (what & 2) {
+    memset(dynprogM->aligned.one.directions_space_0, byte, one);
+    memset(dynprogM->aligned.one.directions_space_1, byte, one);
+    memset(dynprogM->aligned.one.directions_space_2, byte, one);
+  }
+  two[0] = dynprogL;
+  two[1] = dynprogR;
+  for (k = 0; k < 2; k++) {
+    if (what & 1) {
+      memset(two[k]->aligned.two.upper_matrix_space, byte, up);
+      memset(two[k]->aligned.two.lower_matrix_space, byte, lo);
+    }
+    if (what & 2) {
+      memset(two[k]->aligned.two.upper_directions_space_0, byte, up);
+      memset(two[k]->aligned.two.upper_directions_space_1, byte, up);
+      memset(two[k]->aligned.two.lower_directions_space_0, byte, lo);
+      memset(two[k]->aligned.two.lower_directions_space_1, byte, lo);
+    }
+  }
+  return 1;
+#else
+  (void) byte;
+  (void) what;
+  return 0;
+#endif
+}
+
 int
 refh_max_lengths (int *max_rlength, int *max_glength) {
   *max_rlength = dynprogM->max_rlength;

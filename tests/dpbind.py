@@ -55,8 +55,12 @@ class _Impl:
         self._scal = (C.c_int * 6)()
         self._genome_keep = None
 
+    def _before_call(self):
+        pass
+
     def single_gap(self, q, quc, rlength, glength, roffset, goffset, chroffset, chrhigh, watsonp,
                    genestrand, jump_late_p, extraband, widebandp, defect_rate, dynprogindex):
+        self._before_call()
         n = self._single(q, quc, rlength, glength, roffset, goffset, chroffset, chrhigh, watsonp,
                          genestrand, jump_late_p, extraband, widebandp, defect_rate, dynprogindex,
                          self._scal, self._pairs, MAXPAIRS)
@@ -66,6 +70,7 @@ class _Impl:
 
     def end_gap(self, end3p, q, quc, qpos, rlength, glength, roffset, goffset, chroffset, chrhigh, watsonp,
                 genestrand, jump_late_p, extraband, defect_rate, endalign, require_pos_score_p, dynprogindex):
+        self._before_call()
         n = self._end(end3p, q, quc, qpos, rlength, glength, roffset, goffset, chroffset, chrhigh, watsonp,
                       genestrand, jump_late_p, extraband, defect_rate, endalign, require_pos_score_p,
                       dynprogindex, self._scal, self._pairs, MAXPAIRS)
@@ -79,7 +84,15 @@ class Ref(_Impl):
 
     def __init__(self, variant="nosimd"):
         super().__init__(REF_SO[variant])
+        self.variant = variant
         self.lib.refh_init(0, 0, 0)
+        self.lib.refh_poison_arenas.argtypes = [C.c_int, C.c_int]
+
+    def _before_call(self):
+        # SIMD builds read Dynprog_T arena cells the call never writes (dynprog_simd.c, see
+        # oracle/gmapdp_oracle.c "SIMD-build fills"): zero the arenas so that every call sees a
+        # fresh arena, the semantics the engine and the oracle define.  No-op for nosimd.
+        self.lib.refh_poison_arenas(0, 3)
 
     def set_genome(self, g: bytes):
         self._genome_keep = C.create_string_buffer(g, len(g))
@@ -89,9 +102,13 @@ class Ref(_Impl):
 class Oracle(_Impl):
     prefix = "orc_"
 
-    def __init__(self):
+    def __init__(self, simd=False):
         super().__init__(ORACLE_SO)
         self.lib.orc_init(0, 0, 0, 0)
+        self.simd = 1 if simd else 0
+
+    def _before_call(self):
+        self.lib.orc_set_simd(self.simd)  # the oracle library's semantics switch is process-global
 
     def set_genome(self, g: bytes):
         self._genome_keep = C.create_string_buffer(g, len(g))
@@ -322,6 +339,7 @@ def _gg_args(p):
 
 
 def _ref_genome_gap(self, p):
+    self._before_call()
     f = self.lib.refh_genome_gap
     if not getattr(self, "_gg_ready", False):
         f.argtypes = _GG_ARGS + [C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(Pair), C.c_int]
@@ -350,6 +368,7 @@ Ref.maxent = _ref_maxent
 
 
 def _orc_genome_gap(self, p, probsL, probsR):
+    self._before_call()
     f = self.lib.orc_genome_gap
     if not getattr(self, "_gg_ready", False):
         f.argtypes = _GG_ARGS + [C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int),

@@ -225,3 +225,24 @@ def test_intron_scores_restate_setup(oracle):
     assert t[2, 0, 0x20] == 16 and t[2, 1, 0x04] == 14   # the reference's mixed "either" arrays
     assert t.sum() == (14 + 8 + 4) + (16 + 10 + 8) + (14 + 8 + 4) + (16 + 10 + 8) + (16 + 8 + 4 + 14 + 8 + 4) + \
         (16 + 10 + 8 + 14 + 10 + 8)
+
+
+@pytest.mark.skipif(not ref_available("avx2"), reason="reference AVX2 objects not built")
+def test_oracle_simd_single_gap_matches_reference_avx2():
+    """The oracle's restatement of the SIMD build's single gap (Dynprog_simd_8/16 +
+    traceback_8/16) against the reference's own AVX2 objects, each call on zeroed arenas."""
+    import random as _r
+    rng = _r.Random(31)
+    g = random_genome(rng, 50000)
+    ref = Ref("avx2")
+    ref.set_genome(g)
+    orc = Oracle(simd=True)
+    orc.set_genome(g)
+    n8 = 0
+    for i in range(2500):
+        p = single_gap_problem(rng, g) if i % 4 else edge_single_gap_problem(rng, g)
+        u = {0: 41, 1: 63, 2: 127}[0 if p["defect_rate"] < 0.003 else (1 if p["defect_rate"] < 0.014 else 2)]
+        n8 += p["rlength"] < u and p["glength"] < u
+        a, b = call_single(ref, p), call_single(orc, p)
+        assert a == b, (i, {k: v for k, v in p.items() if k not in ("q", "quc")}, a[0], b[0])
+    assert n8 > 300
