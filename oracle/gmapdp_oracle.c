@@ -173,7 +173,7 @@ orc_init (int mode, int user_open, int user_extend, int user_dynprog_p) {
 }
 
 /* Select the semantics the oracle restates: 0 the nosimd build, 1 the SIMD (AVX2) build
-   (single gaps only so far; the other entry points keep nosimd). */
+   (Dynprog_simd_8/16 for single gaps, the _upper/_lower triangles for end and genome gaps). */
 int
 orc_set_simd (int simd) {
   g_simd = simd ? 1 : 0;
@@ -472,11 +472,18 @@ typedef struct {
   int score, nmatches, nmismatches, nopens, nindels;
 } Tally;
 
+/* mode 0: Dynprog_traceback_std.  Modes 1/2: Dynprog_traceback_{8,16}_upper / _lower
+   (dynprog_simd.c:9319/9439, 9716/9836) over one triangle's planes mapped into this layout
+   (upper: nogap DIAG/HORIZ + Egap; lower: nogap DIAG/VERT + the vertical chain in dF).  Their
+   walk is this one; only the final skip differs: upper always ends with a genome skip of c
+   (the reference asserts r == 0), lower with a query skip of r (it asserts c == 0).  The
+   chains keep the c > 0 / r > 0 guards: without them the reference would index before its
+   arrays, which only a path through a diagonal tie at saturation can reach. */
 static void
-traceback_std (PairSink *s, Tally *t, const signed char *dirs, int rlength, int glength, int r, int c,
-               const char *rsequence, const char *rsequenceuc, const char *gsequence,
-               const char *gsequence_alt, int queryoffset, int genomeoffset, int revp,
-               unsigned int chroffset, unsigned int chrhigh, int watsonp, int genestrand, int dpi) {
+traceback_mode (PairSink *s, Tally *t, const signed char *dirs, int rlength, int glength, int r, int c,
+                const char *rsequence, const char *rsequenceuc, const char *gsequence,
+                const char *gsequence_alt, int queryoffset, int genomeoffset, int revp,
+                unsigned int chroffset, unsigned int chrhigh, int watsonp, int genestrand, int dpi, int mode) {
   size_t plane = (size_t) (glength + 1) * (size_t) (rlength + 1);
   const signed char *dnogap = dirs, *dE = dirs + plane, *dF = dirs + 2 * plane;
   int dist, querycoord, genomecoord;
@@ -525,9 +532,9 @@ traceback_std (PairSink *s, Tally *t, const signed char *dirs, int rlength, int 
     }
   }
 
-  if (r == 0 && c == 0) {
+  if ((mode == 1 && c == 0) || (mode == 2 && r == 0) || (r == 0 && c == 0)) {
     /* finished with a diagonal step */
-  } else if (c == 0) {
+  } else if (mode == 2 || (mode == 0 && c == 0)) {
     dist = r;
     add_queryskip(s, r, 0 + LAZY_INDEL, dist, rsequence, queryoffset, genomeoffset, revp, dpi);
     t->score += QOPEN + dist * QINDEL;
@@ -542,6 +549,15 @@ traceback_std (PairSink *s, Tally *t, const signed char *dirs, int rlength, int 
       t->nindels += dist;
     }
   }
+}
+
+static void
+traceback_std (PairSink *s, Tally *t, const signed char *dirs, int rlength, int glength, int r, int c,
+               const char *rsequence, const char *rsequenceuc, const char *gsequence,
+               const char *gsequence_alt, int queryoffset, int genomeoffset, int revp,
+               unsigned int chroffset, unsigned int chrhigh, int watsonp, int genestrand, int dpi) {
+  traceback_mode(s, t, dirs, rlength, glength, r, c, rsequence, rsequenceuc, gsequence, gsequence_alt,
+                 queryoffset, genomeoffset, revp, chroffset, chrhigh, watsonp, genestrand, dpi, 0);
 }
 
 /* Dynprog_compute_bands (dynprog.c:1247) */
@@ -748,6 +764,133 @@ simd_fill_full (int bits, const char *rsequence, const char *gsequence, const ch
   free(mat); free(dn); free(de); free(df); free(ps); free(FF);
 }
 
+/* Triangle fills of the SIMD builds: Dynprog_simd_8_upper / _16_upper (dynprog_simd.c:4304 /
+   7714) and Dynprog_simd_8_lower / _16_lower (:5340 / :8586), AVX2 layout (B = 32 / 16 lanes).
+   upper: matrix[c][r] for c >= r, horizontal gaps only; block rlo (B rows) covers columns
+   [rlo, min(rhigh + uband, glength)].  lower: matrix[r][c] for r >= c, vertical gaps only,
+   vectors along the genome; block clo (B columns) covers rows [clo, min(chigh + lband, rlength)].
+   In both, E_mask keeps the gap of lane i at NEG until the lane is strictly off the diagonal
+   (_MM_ADD_EPI8(E_mask, E_infinity) wraps 1 + POS to NEG), and the diagonal cell's directions
+   are forced DIAG after the store.  Pair scores: upper scores query row r against genome class
+   k (pairdistance[query char][ACGTN[k]], row 0 'N'); lower scores query class k against the
+   genome column, max over the alternate allele (pairdistance[ACGTN[k]][g]), column 0 against
+   byte 4 in the 8-bit fill, 'N' in the 16-bit one; scores past rlength (upper) / glength (lower) are
+   uninitialised in the reference and read 0 here (they only reach cells outside the matrix).
+   Output in traceback_std's layout (IDX(c, r), r <= rlength, c <= glength): score matrix and the
+   three planes (upper: nogap HORIZ / Egap HORIZ; lower: nogap VERT / Fgap VERT), 0 / DIAG where
+   no block wrote (a zeroed arena, as simd_fill_full). */
+static void
+simd_fill_ud (int bits, int upperp, const char *rsequence, const char *gsequence, const char *gsequence_alt,
+              int rlength, int glength, int mismatchtype, int open, int extend, int band, int late, int revp,
+              int *matrix, signed char *dirs) {
+  const int B = (bits == 8) ? 32 : 16;
+  const int NEG = (bits == 8) ? -128 : -32768, POS = (bits == 8) ? 127 : 32767;
+  const int nrow = upperp ? rlength : glength;   /* lanes index rows (upper) / columns (lower) */
+  const int ncol = upperp ? glength : rlength;   /* steps walk columns (upper) / rows (lower) */
+  const int ceil = ((nrow + B) / B) * B;
+  const size_t plane = (size_t) (glength + 1) * (size_t) (rlength + 1);
+  signed char *dnogap = dirs, *dE = dirs + plane, *dF = dirs + 2 * plane;
+  short (*pd)[128] = pairdistance[mismatchtype];
+  static const char acgtn[5] = {'A', 'C', 'G', 'T', 'N'};
+  int *mat = (int *) calloc((size_t) (ncol + 1) * ceil, sizeof(int));      /* [step][lane-row] */
+  signed char *dn = (signed char *) calloc((size_t) (ncol + 1) * ceil, 1);
+  signed char *de = (signed char *) calloc((size_t) (ncol + 1) * ceil, 1);
+  int *ps = (int *) calloc((size_t) 5 * ceil, sizeof(int));                /* pairscores[5][ceil] */
+  int H[32], E[32], Hs[32], mask[32];
+  int lo, hi, x, i, k, na, p, T1, Hd, X;
+  size_t at;
+
+  for (k = 0; k < 5; k++) {
+    for (i = 0; i <= nrow && i < ceil; i++) {
+      int s1, s2;
+      if (upperp) {
+        int na1 = (i == 0) ? 'N' : (unsigned char) (revp ? rsequence[1 - i] : rsequence[i - 1]);
+        ps[k * ceil + i] = pd[na1][(int) acgtn[k]];
+      } else if (i == 0) {
+        /* column 0: the 8-bit fill indexes byte 4 (dynprog_simd.c:5459), the 16-bit one 'N' (:8690) */
+        ps[k * ceil + i] = pd[(int) acgtn[k]][bits == 8 ? 4 : 'N'];
+      } else {
+        int g = (unsigned char) (revp ? gsequence[1 - i] : gsequence[i - 1]);
+        int ga = (unsigned char) (revp ? gsequence_alt[1 - i] : gsequence_alt[i - 1]);
+        s1 = pd[(int) acgtn[k]][g];
+        s2 = pd[(int) acgtn[k]][ga];
+        ps[k * ceil + i] = s1 > s2 ? s1 : s2;
+      }
+    }
+  }
+
+  for (lo = 0; lo <= nrow; lo += B) {
+    hi = (lo + B - 1 > nrow) ? nrow : lo + B - 1;
+    for (i = 0; i < B; i++) {
+      E[i] = late ? NEG : NEG + 1;
+      H[i] = NEG - open;               /* "compensate for T1 = H + open" */
+      mask[i] = 1;
+    }
+    for (x = lo; x <= hi + band && x <= ncol; x++) {
+      if (x == 0) {
+        na = 4;
+      } else if (upperp) {
+        na = nt_to_int((unsigned char) (revp ? gsequence[1 - x] : gsequence[x - 1]));
+      } else {
+        na = nt_to_int((unsigned char) (revp ? rsequence[1 - x] : rsequence[x - 1]));
+      }
+      if (x == 0) X = 0;
+      else if (lo == 0) X = NEG;
+      else X = mat[(size_t) (x - 1) * ceil + lo - 1];
+      for (i = 0; i < B; i++) {
+        at = (size_t) x * ceil + lo + i;
+        if (mask[i]) E[i] = NEG;                          /* min(E, wrap(1 + POS)) */
+        T1 = sat_add(H[i], open, NEG, POS);
+        de[at] = (late ? (E[i] >= T1) : (E[i] > T1)) ? -1 : 0;
+        E[i] = sat_add(E[i] > T1 ? E[i] : T1, extend, NEG, POS);
+        if (mask[i]) E[i] = NEG;
+        Hs[i] = (i == 0) ? X : H[i - 1];
+      }
+      for (i = 0; i < B; i++) {
+        at = (size_t) x * ceil + lo + i;
+        if (upperp) {
+          p = ps[na * ceil + lo + i];
+          {
+            int na_alt = (x == 0) ? 4 : nt_to_int((unsigned char) (revp ? gsequence_alt[1 - x] : gsequence_alt[x - 1]));
+            int pa = ps[na_alt * ceil + lo + i];
+            if (pa > p) p = pa;
+          }
+        } else {
+          p = ps[na * ceil + lo + i];
+        }
+        Hd = sat_add(Hs[i], p, NEG, POS);
+        dn[at] = (late ? (E[i] >= Hd) : (E[i] > Hd)) ? -1 : 0;
+        H[i] = Hd > E[i] ? Hd : E[i];
+        mat[at] = H[i];
+      }
+      if (hi >= x) {                                       /* diagonal forced DIAG */
+        de[(size_t) x * ceil + x] = 0;
+        dn[(size_t) x * ceil + x] = 0;
+      }
+      for (i = B - 1; i > 0; i--) mask[i] = mask[i - 1];
+      mask[0] = 0;
+    }
+  }
+
+  memset(matrix, 0, plane * sizeof(int));
+  memset(dirs, DIAG, 3 * plane);
+  for (x = 0; x <= ncol; x++) {
+    for (i = 0; i <= nrow; i++) {
+      at = (size_t) x * ceil + i;
+      if (upperp) {          /* x = c, i = r */
+        matrix[IDX(x, i)] = mat[at];
+        dnogap[IDX(x, i)] = dn[at] ? HORIZ : DIAG;
+        dE[IDX(x, i)] = de[at] ? HORIZ : DIAG;
+      } else {               /* x = r, i = c */
+        matrix[IDX(i, x)] = mat[at];
+        dnogap[IDX(i, x)] = dn[at] ? VERT : DIAG;
+        dF[IDX(i, x)] = de[at] ? VERT : DIAG;
+      }
+    }
+  }
+  free(mat); free(dn); free(de); free(ps);
+}
+
 static void
 reverse_pairs (OrcPair *p, int n) {
   int i, j;
@@ -875,6 +1018,30 @@ find_best_endpoint_to_queryend_indels_std (int *finalscore, int *bestr, int *bes
   *finalscore = bestscore;
 }
 
+/* find_best_endpoint_8/_16 (dynprog_end.c:144/220) and
+   find_best_endpoint_to_queryend_indels_8/_16 (:359/437): the same scans over the two
+   triangles, lower[r][c] for c < r (this loop is bounded by r, not by chigh), then upper[c][r]
+   for r <= c <= chigh; bestscore starts at 0 (resp. NEG_INFINITY_8/16) in the fill's width. */
+static void
+find_best_endpoint_ud (int *finalscore, int *bestr, int *bestc, const int *mupper, const int *mlower,
+                       int rlength, int glength, int lband, int uband, int late, int indels, int neg) {
+  int bestscore = indels ? neg : 0, r, c, clo, chigh, r0;
+  *bestr = *bestc = 0;
+  r0 = 1;
+  if (indels) { *bestr = r0 = rlength; }
+  for (r = r0; r <= rlength; r++) {
+    if ((clo = r - lband) < 1) clo = 1;
+    if ((chigh = r + uband) > glength) chigh = glength;
+    for (c = clo; c < r; c++) {
+      if (prefer(mlower[IDX(c, r)], bestscore, late)) { *bestr = r; *bestc = c; bestscore = mlower[IDX(c, r)]; }
+    }
+    for (; c <= chigh; c++) {
+      if (prefer(mupper[IDX(c, r)], bestscore, late)) { *bestr = r; *bestc = c; bestscore = mupper[IDX(c, r)]; }
+    }
+  }
+  *finalscore = bestscore;
+}
+
 /* traceback_nogaps (dynprog_end.c:649) */
 static void
 traceback_nogaps (PairSink *s, Tally *t, int r, int c, const char *rsequence, const char *rsequenceuc,
@@ -945,7 +1112,27 @@ orc_end_gap (int end3p, const char *qbuf, const char *qucbuf, int qpos, int rlen
   }
   if (gseq[0] == '\0') { free(gseq); free(gseq_alt); return -1; }
 
-  if (endalign == QUERYEND_GAP || endalign == BEST_LOCAL || endalign == QUERYEND_INDELS) {
+  if (g_simd && (endalign == QUERYEND_GAP || endalign == BEST_LOCAL || endalign == QUERYEND_INDELS)) {
+    /* dynprog_end.c:1406-1510 / 2027-2140: 8-bit triangles when either length is below use8p_size */
+    int bits = (rlength < use8p_size[ENDQ] || glength < use8p_size[ENDQ]) ? 8 : 16;
+    size_t plane;
+    compute_bands(&lband, &uband, rlength, glength, extraband_end, endalign != QUERYEND_INDELS);
+    plane = (size_t) (glength + 1) * (rlength + 1);
+    matrix = (int *) malloc(2 * plane * sizeof(int));
+    dirs = (signed char *) malloc((size_t) 6 * plane);
+    if (rlength > glength + 1) {
+      /* outside the domain: the lower-triangle scans would read columns past glength, which the
+         reference fills from uninitialised pair scores (stage3.c always passes glength >= rlength) */
+      free(matrix); free(dirs); free(gseq); free(gseq_alt);
+      return -3;
+    }
+    simd_fill_ud(bits, 1, end3p ? rsequenceuc : rsequence, gptr, gptr_alt, rlength, glength, ENDQ, open, extend,
+                 uband, late, revp, matrix, dirs);
+    simd_fill_ud(bits, 0, end3p ? rsequenceuc : rsequence, gptr, gptr_alt, rlength, glength, ENDQ, open, extend,
+                 lband, late, revp, matrix + plane, dirs + 3 * plane);
+    find_best_endpoint_ud(&finalscore, &bestr, &bestc, matrix, matrix + plane, rlength, glength, lband, uband,
+                          late, endalign == QUERYEND_INDELS, bits == 8 ? -128 : -32768);
+  } else if (endalign == QUERYEND_GAP || endalign == BEST_LOCAL || endalign == QUERYEND_INDELS) {
     compute_bands(&lband, &uband, rlength, glength, extraband_end, endalign != QUERYEND_INDELS);
     matrix = (int *) malloc((size_t) (glength + 1) * (rlength + 1) * sizeof(int));
     dirs = (signed char *) malloc((size_t) 3 * (glength + 1) * (rlength + 1));
@@ -968,6 +1155,13 @@ orc_end_gap (int end3p, const char *qbuf, const char *qucbuf, int qpos, int rlen
                      genestrand, revp, dynprogindex);
   } else if (require_pos_score_p) {
     /* *traceback_score was just zeroed, so this always skips (dynprog_end.c:1572) */
+  } else if (g_simd) {
+    /* Dynprog_traceback_{8,16}_upper when bestc >= bestr, else _lower (dynprog_end.c:1574-1610) */
+    size_t plane = (size_t) (glength + 1) * (rlength + 1);
+    int up = bestc >= bestr;
+    traceback_mode(&sink, &t, up ? dirs : dirs + 3 * plane, rlength, glength, bestr, bestc, rsequence, rsequenceuc,
+                   gptr, gptr_alt, roffset, goffset, revp, chroffset, chrhigh, watsonp, genestrand, dynprogindex,
+                   up ? 1 : 2);
   } else {
     traceback_std(&sink, &t, dirs, rlength, glength, bestr, bestc, rsequence, rsequenceuc, gptr, gptr_alt,
                   roffset, goffset, revp, chroffset, chrhigh, watsonp, genestrand, dynprogindex);
@@ -1278,6 +1472,105 @@ bridge_site_level (int *bestrL, int *bestrR, int *bestcL, int *bestcR, const int
   return bestscore;
 }
 
+/* bridge_intron_gap_8_site_level / _16_site_level (dynprog_genome.c:867 / :1742), reached through
+   bridge_intron_gap_8_ud / _16_ud (:1388 / :2263) with the bands of Dynprog_compute_bands: the
+   scan of bridge_site_level over the two triangles of each side.  B walks cR over the R lower
+   triangle up to the diagonal, skips it (A covered it) and continues in the R upper triangle;
+   C does the same for cL on the left.  bestscore starts at NEG_INFINITY_8/16. */
+static int
+bridge_ud (int *bestrL, int *bestrR, int *bestcL, int *bestcR, const int *mLu, const int *mLl, const int *mRu,
+           const int *mRl, const char *gL, const char *revR, int rlength, int glengthL, int glengthR, int dirclass,
+           int finalp, int halfp, int lbandL, int ubandL, int lbandR, int ubandR, int leftoffset,
+           int rightoffset, const double *lp, const double *rp, int neg) {
+  const int *isc = intron_score[dirclass][finalp ? 1 : 0];
+  int *leftdi = (int *) malloc((glengthL + 1) * sizeof(int));
+  int *rightdi = (int *) malloc((glengthR + 1) * sizeof(int));
+  int rL, rR, cL, cR, cloL, chighL, cloR, chighR, scoreL, scoreR, scoreI, score;
+  int bestscore = neg, bestscore_with_dinucl = neg;
+  int bestrL_d = 0, bestrR_d = 0, bestcL_d = 0, bestcR_d = 0, use_dinucl_p;
+  double probL, probR, bestprob_with_score = 0.0, bestprob_with_dinucl = 0.0;
+#define ML(m, c, r) m[(size_t) (c) * (size_t) (rlength + 1) + (size_t) (r)]
+#define CONSIDER()                                                                              \
+  do {                                                                                          \
+    if ((score = scoreL + scoreI + scoreR) > bestscore) {                                       \
+      bestscore = score; *bestrL = rL; *bestrR = rR; *bestcL = cL; *bestcR = cR;                 \
+      bestprob_with_score = probL + probR;                                                      \
+    } else if (score == bestscore && probL + probR > bestprob_with_score) {                     \
+      *bestrL = rL; *bestrR = rR; *bestcL = cL; *bestcR = cR;                                    \
+      bestprob_with_score = probL + probR;                                                      \
+    }                                                                                           \
+  } while (0)
+
+  for (cL = 0; cL < glengthL - 1; cL++) leftdi[cL] = left_dinucl(gL[cL], gL[cL + 1]);
+  leftdi[glengthL - 1] = leftdi[glengthL] = 0;
+  for (cR = 0; cR < glengthR - 1; cR++) rightdi[cR] = right_dinucl(revR[-cR - 1], revR[-cR]);
+  rightdi[glengthR - 1] = rightdi[glengthR] = 0;
+
+  for (rL = 1, rR = rlength - 1; rL < rlength; rL++, rR--) {
+    if ((cloL = rL - lbandL) < 1) cloL = 1;
+    if ((chighL = rL + ubandL) > glengthL - 1) chighL = glengthL - 1;
+    if ((cloR = rR - lbandR) < 1) cloR = 1;
+    if ((chighR = rR + ubandR) > glengthR - 1) chighR = glengthR - 1;
+
+    /* A: no indels (:1082-1134) */
+    cL = rL; probL = lp[cL]; scoreL = ML(mLu, cL, rL);
+    cR = rR; probR = rp[cR]; scoreR = ML(mRu, cR, rR);
+    scoreI = isc[leftdi[cL] & rightdi[cR]];
+    CONSIDER();
+    if (scoreI > 0 && probL + probR > bestprob_with_dinucl) {
+      bestscore_with_dinucl = scoreL + scoreI + scoreR;
+      bestcL_d = cL; bestcR_d = cR; bestrL_d = rL; bestrR_d = rR;
+      bestprob_with_dinucl = probL + probR;
+    }
+    /* B: indel on the right (:1137-1235) */
+    cL = rL; probL = lp[cL]; scoreL = ML(mLu, cL, rL);
+    for (cR = cloR; cR < rR && cR < rightoffset - leftoffset - cL; cR++) {
+      probR = rp[cR];
+      scoreR = ML(mRl, cR, rR);
+      scoreI = isc[leftdi[cL] & rightdi[cR]];
+      CONSIDER();
+    }
+    for (cR++; cR < chighR && cR < rightoffset - leftoffset - cL; cR++) {
+      probR = rp[cR];
+      scoreR = ML(mRu, cR, rR);
+      scoreI = isc[leftdi[cL] & rightdi[cR]];
+      CONSIDER();
+    }
+    /* C: indel on the left (:1237-1335) */
+    cR = rR; probR = rp[cR]; scoreR = ML(mRu, cR, rR);
+    for (cL = cloL; cL < rL && cL < rightoffset - leftoffset - cR; cL++) {
+      probL = lp[cL];
+      scoreL = ML(mLl, cL, rL);
+      scoreI = isc[leftdi[cL] & rightdi[cR]];
+      CONSIDER();
+    }
+    for (cL++; cL < chighL && cL < rightoffset - leftoffset - cR; cL++) {
+      probL = lp[cL];
+      scoreL = ML(mLu, cL, rL);
+      scoreI = isc[leftdi[cL] & rightdi[cR]];
+      CONSIDER();
+    }
+  }
+#undef CONSIDER
+#undef ML
+
+  if (bestprob_with_score > 2 * PROB_CEILING) use_dinucl_p = 0;
+  else if (bestprob_with_dinucl == 0.0) use_dinucl_p = 0;
+  else if (bestscore_with_dinucl < 0 || bestscore_with_dinucl < bestscore - 9) use_dinucl_p = 0;
+  else use_dinucl_p = 1;
+  if (use_dinucl_p) {
+    *bestcL = bestcL_d; *bestcR = bestcR_d; *bestrL = bestrL_d; *bestrR = bestrR_d;
+    bestscore = bestscore_with_dinucl;
+  }
+  if (bestscore >= 0 && halfp) {
+    scoreI = isc[leftdi[*bestcL] & rightdi[*bestcR]];
+    bestscore = bestscore - scoreI / 2;
+  }
+  free(leftdi);
+  free(rightdi);
+  return bestscore;
+}
+
 /* Pair_maxnegscore (pair.c:8528) over pairs in list order */
 static int
 maxnegscore (const OrcPair *p, int n) {
@@ -1311,6 +1604,32 @@ gg_scalars (const GGOut *o, int *scalars, double *dscalars) {
   dscalars[0] = o->left_prob; dscalars[1] = o->right_prob;
 }
 
+/* The tail of Dynprog_genome_gap after the second traceback (:3872-3896): counters, NULL when
+   only the gap holder was pushed, Pair_maxnegscore rejection.  Returns the pair count or -1. */
+static int
+gg_finish (PairSink *sink, const Tally *t, GGOut *o, OrcPair *out, int max_pairs, int dynprogindex) {
+  int n, i;
+  o->score = t->score; o->nmatches = t->nmatches; o->nmismatches = t->nmismatches;
+  o->nopens = t->nopens; o->nindels = t->nindels;
+  o->dpi = dynprogindex + (dynprogindex > 0 ? +1 : -1);
+  n = sink->n;
+  if (n == 1) {
+    n = -1;  /* only the gap holder: NULL (:3877) */
+  } else {
+    /* before the final List_reverse the list is reverse(TL), G, TR in its own order:
+       the reverse of what is returned */
+    OrcPair *tmp = (OrcPair *) malloc((size_t) n * sizeof(OrcPair));
+    int m = n < max_pairs ? n : max_pairs;
+    for (i = 0; i < m; i++) tmp[i] = out[m - 1 - i];
+    if (maxnegscore(tmp, m) < -10) {
+      o->score = -100;
+      n = -1;
+    }
+    free(tmp);
+  }
+  return n;
+}
+
 /* flags: 1 watsonp, 2 jump_late_p, 8 halfp, 16 finalp. */
 int
 orc_genome_gap (const char *rsequence, const char *rsequenceuc, int rlength, int glengthL, int glengthR,
@@ -1321,7 +1640,7 @@ orc_genome_gap (const char *rsequence, const char *rsequenceuc, int rlength, int
   const int watsonp = flags & 1, jump_late_p = (flags & 2) ? 1 : 0, halfp = (flags & 8) ? 1 : 0;
   const int finalp = (flags & 16) ? 1 : 0;
   const int dirclass = cdna_direction > 0 ? 0 : (cdna_direction < 0 ? 1 : 2);
-  int mismatchtype, open, extend, lbandL, ubandL, lbandR, ubandR, finalscore, n, nR, i;
+  int mismatchtype, open, extend, lbandL, ubandL, lbandR, ubandR, finalscore, n, nR;
   int bestrL = -1, bestrR = 0, bestcL = 0, bestcR = 0;
   int rev_roffset;
   char *gL, *gLa, *gR, *gRa;
@@ -1399,6 +1718,53 @@ orc_genome_gap (const char *rsequence, const char *rsequenceuc, int rlength, int
     sink.n = 0;
   }
 
+  if (g_simd) {
+    /* dynprog_genome.c:3501-3795: 8-bit triangles when rlength or both glengths are below use8p_size */
+    int bits = (rlength < use8p_size[mismatchtype] ||
+                (glengthL < use8p_size[mismatchtype] && glengthR < use8p_size[mismatchtype])) ? 8 : 16;
+    size_t pl = (size_t) (glengthL + 1) * (rlength + 1), pr = (size_t) (glengthR + 1) * (rlength + 1);
+    int *mL = (int *) malloc(2 * pl * sizeof(int)), *mR = (int *) malloc(2 * pr * sizeof(int));
+    signed char *dL = (signed char *) malloc(6 * pl), *dR = (signed char *) malloc(6 * pr);
+    compute_bands(&lbandL, &ubandL, rlength, glengthL, extraband_paired, 1);
+    simd_fill_ud(bits, 1, rsequence, gL, gL, rlength, glengthL, mismatchtype, open, extend, ubandL, jump_late_p, 0,
+                 mL, dL);
+    simd_fill_ud(bits, 0, rsequence, gL, gL, rlength, glengthL, mismatchtype, open, extend, lbandL, jump_late_p, 0,
+                 mL + pl, dL + 3 * pl);
+    compute_bands(&lbandR, &ubandR, rlength, glengthR, extraband_paired, 1);
+    simd_fill_ud(bits, 1, rev_rsequence, revR, revR, rlength, glengthR, mismatchtype, open, extend, ubandR,
+                 !jump_late_p, 1, mR, dR);
+    simd_fill_ud(bits, 0, rev_rsequence, revR, revR, rlength, glengthR, mismatchtype, open, extend, lbandR,
+                 !jump_late_p, 1, mR + pr, dR + 3 * pr);
+    finalscore = bridge_ud(&bestrL, &bestrR, &bestcL, &bestcR, mL, mL + pl, mR, mR + pr, gL, revR, rlength,
+                           glengthL, glengthR, dirclass, finalp, halfp, lbandL, ubandL, lbandR, ubandR, goffsetL,
+                           rev_goffsetR, left_probs, right_probs, bits == 8 ? -128 : -32768);
+    if (finalscore < 0) {
+      o.score = -100;
+      n = -1;
+    } else {
+      int upR = bestcR >= bestrR, upL = bestcL >= bestrL;
+      o.left_prob = left_probs[bestcL];
+      o.right_prob = right_probs[bestcR];
+      o.new_left = goffsetL + (bestcL - 1);
+      o.new_right = rev_goffsetR - (bestcR - 1);
+      o.exonhead = rev_roffset - (bestrR - 1);
+      traceback_mode(&sink, &t, upR ? dR : dR + 3 * pr, rlength, glengthR, bestrR, bestcR, rev_rsequence,
+                     rev_rsequenceuc, revR, revR, rev_roffset, rev_goffsetR, /*revp*/1, chroffset, chrhigh, watsonp,
+                     genestrand, dynprogindex, upR ? 1 : 2);
+      nR = sink.n < max_pairs ? sink.n : max_pairs;
+      reverse_pairs(out, nR);
+      sink_gapholder(&sink, (rev_roffset - bestrR) - (roffset + bestrL) + 1, o.new_right - o.new_left - 1);
+      traceback_mode(&sink, &t, upL ? dL : dL + 3 * pl, rlength, glengthL, bestrL, bestcL, rsequence, rsequenceuc,
+                     gL, gL, roffset, goffsetL, /*revp*/0, chroffset, chrhigh, watsonp, genestrand, dynprogindex,
+                     upL ? 1 : 2);
+      n = gg_finish(&sink, &t, &o, out, max_pairs, dynprogindex);
+    }
+    free(mL); free(mR); free(dL); free(dR);
+    free(gL); free(gLa); free(gR); free(gRa);
+    gg_scalars(&o, scalars, dscalars);
+    return n;
+  }
+
   compute_bands(&lbandL, &ubandL, rlength, glengthL, extraband_paired, 1);
   matrixL = (int *) malloc((size_t) (glengthL + 1) * (rlength + 1) * sizeof(int));
   dirsL = (signed char *) malloc((size_t) 3 * (glengthL + 1) * (rlength + 1));
@@ -1433,24 +1799,7 @@ orc_genome_gap (const char *rsequence, const char *rsequenceuc, int rlength, int
     sink_gapholder(&sink, (rev_roffset - bestrR) - (roffset + bestrL) + 1, o.new_right - o.new_left - 1);
     traceback_std(&sink, &t, dirsL, rlength, glengthL, bestrL, bestcL, rsequence, rsequenceuc, gL, gL,
                   roffset, goffsetL, /*revp*/0, chroffset, chrhigh, watsonp, genestrand, dynprogindex);
-    o.score = t.score; o.nmatches = t.nmatches; o.nmismatches = t.nmismatches;
-    o.nopens = t.nopens; o.nindels = t.nindels;
-    o.dpi = dynprogindex + (dynprogindex > 0 ? +1 : -1);
-    n = sink.n;
-    if (n == 1) {
-      n = -1;  /* only the gap holder: NULL (:3877) */
-    } else {
-      /* before the final List_reverse the list is reverse(TL), G, TR in its own order:
-         the reverse of what is returned */
-      OrcPair *tmp = (OrcPair *) malloc((size_t) n * sizeof(OrcPair));
-      int m = n < max_pairs ? n : max_pairs;
-      for (i = 0; i < m; i++) tmp[i] = out[m - 1 - i];
-      if (maxnegscore(tmp, m) < -10) {
-        o.score = -100;
-        n = -1;
-      }
-      free(tmp);
-    }
+    n = gg_finish(&sink, &t, &o, out, max_pairs, dynprogindex);
   }
   /* returned list: List_reverse of [reverse(TL) G TR] = reverse(TR) G TL, which is the sink order */
   free(matrixL); free(dirsL); free(matrixR); free(dirsR);

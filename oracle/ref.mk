@@ -62,10 +62,13 @@ FLAGS_avx2   := -mpopcnt -DHAVE_SSE2=1 -DHAVE_SSSE3=1 -DHAVE_SSE4_1=1 -DHAVE_SSE
 # Only used to pin Dynprog_genome_gap with halfp, where the default heap build
 # dereferences the FREEA-nulled leftdi (dynprog_genome.c:2879-2888) and crashes.
 FLAGS_nosimda := -DHAVE_ALLOCA=1 -DHAVE_ALLOCA_H=1
+# The same for the AVX2 build (bridge_intron_gap_8/16_site_level reads leftdi after FREEA too,
+# dynprog_genome.c:1370-1379 / :2245-2254).
+FLAGS_avx2a  := $(FLAGS_avx2) -DHAVE_ALLOCA=1 -DHAVE_ALLOCA_H=1
 
 .DEFAULT_GOAL := all
 
-VARIANTS := nosimd avx2 nosimda
+VARIANTS := nosimd avx2 nosimda avx2a
 
 define variant_rules
 LIBOBJS_$(1) := $$(patsubst %.c,$(OUT)/$(1)/%.o,$(HARNESS_C))

@@ -17,6 +17,12 @@ and the reference's outputs.
                          MaxEnt splice probabilities (Maxent_hr_*_prob) at every entry the
                          engine reads; halfp problems come from the --enable-alloca nosimd
                          build (the default heap build dereferences a freed array there)
+  simd_{single,end,genome}_gap_golden.npz
+                         the same entry points as the SIMD builds compute them (gmap.avx2:
+                         Dynprog_simd_8/16, the _upper/_lower triangles, bridge_intron_gap_*_ud),
+                         from the reference's AVX2 objects called on zeroed Dynprog_T arenas, on
+                         problems inside the domain where that build is defined (see
+                         simd_domain below); halfp genome gaps from the --enable-alloca AVX2 build
 """
 import os
 import random
@@ -131,9 +137,45 @@ def load(path):
     return z["genome"].tobytes(), probs, outs
 
 
+def simd_domain(kind, p):
+    """Problems on which the AVX2 build is defined: single gaps whose band reaches the corner
+    (otherwise Dynprog_traceback_8/16 aborts with "Bad dir", dynprog_simd.c:9278), end gaps with
+    rlength <= glength + 1 (otherwise the lower-triangle scans read columns filled from
+    uninitialised pair scores), genome gaps with glengthL, glengthR > rlength (as for nosimd)."""
+    if kind == "single":
+        return p["widebandp"] or abs(p["rlength"] - p["glength"]) <= p["extraband"]
+    if kind == "end":
+        return p["endalign"] == 2 or p["rlength"] <= p["glength"] + 1
+    return p["rlength"] <= 1 or (p["glengthL"] > p["rlength"] and p["glengthR"] > p["rlength"])
+
+
+def main_simd():
+    for name, maker, call, names, kind, seed in (
+            ("simd_single_gap_golden.npz", single_problems, call_single, SINGLE_PARAMS, "single", 3024),
+            ("simd_end_gap_golden.npz", end_problems, call_end, END_PARAMS, "end", 3025)):
+        g, probs = maker(seed=seed)
+        probs = [p for p in probs if simd_domain(kind, p)]
+        ref = Ref("avx2")
+        ref.set_genome(g)
+        outputs = {"ref_avx2": [call(ref, p) for p in probs]}
+        out = os.path.join(HERE, name)
+        np.savez_compressed(out, **pack(g, probs, outputs, names))
+        print("wrote %s: %d problems" % (out, len(probs)))
+    g, probs = genome_problems(seed=3026)
+    probs = [p for p in probs if simd_domain("genome", p)]
+    ref, refa, orc = Ref("avx2"), Ref("avx2a"), Oracle()
+    for r in (ref, refa, orc):
+        r.set_genome(g)
+    for p in probs:
+        p["probsL"], p["probsR"] = splice_probs(ref, orc, p)
+    outputs = {"ref_avx2": [(refa if p["flags"] & GG_FLAG_HALF else ref).genome_gap(p) for p in probs]}
+    out = os.path.join(HERE, "simd_genome_gap_golden.npz")
+    np.savez_compressed(out, **pack(g, probs, outputs, GENOME_PARAMS))
+    print("wrote %s: %d problems" % (out, len(probs)))
+
+
 def main():
-    # SIMD (avx2) outputs are not generated here: that build aborts ("Bad dir",
-    # dynprog_simd.c:9278) on narrow bands that miss the corner; see DESIGN.md.
+    # nosimd goldens (the SIMD build's are main_simd)
     for name, maker, call, names in (("single_gap_golden.npz", single_problems, call_single, SINGLE_PARAMS),
                                      ("end_gap_golden.npz", end_problems, call_end, END_PARAMS)):
         g, probs = maker()
@@ -156,4 +198,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "simd":
+        main_simd()
+    else:
+        main()

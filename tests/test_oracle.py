@@ -246,3 +246,73 @@ def test_oracle_simd_single_gap_matches_reference_avx2():
         a, b = call_single(ref, p), call_single(orc, p)
         assert a == b, (i, {k: v for k, v in p.items() if k not in ("q", "quc")}, a[0], b[0])
     assert n8 > 300
+
+
+# ---------------------------------------------------------------------------
+# SIMD-build semantics (gmap.avx2): goldens from the reference's AVX2 objects
+# ---------------------------------------------------------------------------
+def _load_golden(name):
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(HERE, "golden", "make_golden.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m.load(os.path.join(HERE, "golden", name))
+
+
+def _check_simd_golden(name, call):
+    g, probs, outs = _load_golden(name)
+    orc = Oracle(simd=True)
+    orc.set_genome(g)
+    exp = outs["ref_avx2"]
+    assert len(probs) == len(exp) > 1000
+    bad = [i for i, p in enumerate(probs) if call(orc, p) != exp[i]]
+    assert bad == [], "%s: oracle differs on %d problems (first %s)" % (name, len(bad), bad[:5])
+    return probs, exp
+
+
+def test_oracle_simd_goldens():
+    """The oracle's SIMD semantics against the AVX2 goldens of all three entry points."""
+    from dpbind import call_end
+    _check_simd_golden("simd_single_gap_golden.npz", call_single)
+    probs, exp = _check_simd_golden("simd_end_gap_golden.npz", call_end)
+    # both fill widths, both triangles at the endpoint and every endalign exercised
+    u8 = sum(1 for p in probs if p["endalign"] != 2 and p["rlength"] > 0 and (p["rlength"] < 24 or p["glength"] < 24))
+    assert u8 > 100 and len(probs) - u8 > 400
+    assert {p["endalign"] for p in probs} == {0, 1, 2, 3}
+    gp, gexp = _check_simd_golden("simd_genome_gap_golden.npz",
+                                  lambda o, p: o.genome_gap(p, p["probsL"], p["probsR"]))
+    indel_both_sides = sum(1 for s, pr in gexp if pr and s[5] > 0)
+    assert indel_both_sides > 50
+    assert sum(1 for p in gp if p["flags"] & 8) > 50  # halfp (from the --enable-alloca AVX2 build)
+
+
+@pytest.mark.skipif(not ref_available("avx2a"), reason="reference AVX2 objects not built")
+def test_oracle_simd_end_and_genome_gaps_vs_reference_avx2():
+    """Fresh seeded end and genome gaps: the oracle's triangle fills, endpoint scans, bridge and
+    upper/lower tracebacks against the reference's AVX2 objects (zeroed arenas)."""
+    from dpbind import call_end, end_gap_problem, genome_gap_problem, splice_probs
+    rng = random.Random(77)
+    ref, orc = Ref("avx2a"), Oracle(simd=True)
+    g = random_genome(rng, 30000)
+    ref.set_genome(g)
+    orc.set_genome(g)
+    n = 0
+    for i in range(1500):
+        p = end_gap_problem(rng, g, edge=(i % 5 == 0))
+        if p["endalign"] != 2 and p["rlength"] > p["glength"] + 1:
+            continue
+        n += 1
+        a, b = call_end(ref, p), call_end(orc, p)
+        assert a == b, (i, {k: v for k, v in p.items() if k not in ("q", "quc")}, a[0], b[0])
+    assert n > 1200
+    gg = bytearray(random_genome(rng, 80000))
+    probs = [genome_gap_problem(rng, gg, edge=(i % 5 == 0)) for i in range(700)]
+    gg = bytes(gg)
+    ref.set_genome(gg)
+    orc.set_genome(gg)
+    for i, p in enumerate(probs):
+        if p["rlength"] > 1 and (p["glengthL"] <= p["rlength"] or p["glengthR"] <= p["rlength"]):
+            continue
+        lp, rp = splice_probs(ref, orc, p)
+        a, b = ref.genome_gap(p), orc.genome_gap(p, lp, rp)
+        assert a == b, (i, {k: v for k, v in p.items() if k not in ("q", "quc")}, a[0], b[0])
