@@ -48,6 +48,20 @@ hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
                      const char* qseq_uc, const double* sprob, const int8_t* sctab, const uint8_t* constab,
                      const int8_t* isctab, gmapdp_genome_result* results, gmapdp_pair* pairs,
                      unsigned char* gscratch);
+size_t lds_bytes_uxe(int rlength, int glength, int B);
+size_t scratch_bytes_uxe(int rlength, int glength, int lband, int uband, int B);
+size_t lds_bytes_uxg(int rlength, int glengthL, int glengthR, int B);
+size_t scratch_bytes_uxg(int rlength, int glengthL, int glengthR, int extraband, int B);
+hipError_t launch_uxe(int B, int nproblems, size_t lds, hipStream_t stream, const DevProblem* probs, const int* order,
+                      unsigned char* gscratch, const uint32_t* blocks, uint64_t nwords, const char* qseq,
+                      const char* qseq_uc, const int8_t* sctab, const uint8_t* constab, gmapdp_result* results,
+                      gmapdp_pair* pairs);
+hipError_t launch_uxg(int B, int nproblems, size_t lds, hipStream_t stream, const DevGenomeProblem* probs,
+                      const int* order, unsigned char* gscratch, const uint32_t* blocks, uint64_t nwords,
+                      const char* qseq, const char* qseq_uc, const double* sprob, const int8_t* sctab,
+                      const uint8_t* constab, const int8_t* isctab, gmapdp_genome_result* results,
+                      gmapdp_pair* pairs);
+static const int kUse8pSize[4] = {41, 63, 127, 24};  // use8p_size (dynprog.c:1022-1025)
 
 // ---------------------------------------------------------------------------
 // Score tables.  The reference builds pairdistance_array[4][128][128] and
@@ -199,8 +213,9 @@ struct PlanCore {
   std::vector<DevGenomeProblem> gdev;  // Dynprog_genome_gap problems on the GPU
   std::vector<int> gdev_index;       // genome problem index -> gdev slot (-1: resolved on host)
   std::vector<int> gdev_problem;     // gdev slot -> genome problem index
-  // kDpx: 64/S narrow problems per wave, R = S; kSx: SIMD-build semantics, 64/B problems per wave, R = B
-  enum Kind { kDp = 0, kGenomeGap = 1, kDpx = 2, kSx = 3 };
+  // kDpx: 64/S narrow problems per wave, R = S; kSx: SIMD-build single gaps, 64/B problems per wave,
+  // R = B; kUxe / kUxg: SIMD-build end / genome gaps (triangle fills), one wave per problem, R = B
+  enum Kind { kDp = 0, kGenomeGap = 1, kDpx = 2, kSx = 3, kUxe = 4, kUxg = 5 };
   struct Launch {
     int kind;
     int R;           // band words per lane (kDp, kGenomeGap) or segment width S (kDpx)
@@ -480,10 +495,6 @@ static int convert_end(gmapdp_ctx* ctx, const gmapdp_end_problem& p, gmapdp_resu
     *err = bad(ctx, "endalign out of range");
     return 0;
   }
-  if (p.flags & GMAPDP_SIMD) {
-    *err = bad(ctx, "GMAPDP_SIMD: the SIMD builds' end-gap fills (Dynprog_simd_*_upper/_lower) are not implemented");
-    return 0;
-  }
   int rlength = p.rlength, glength = p.glength;
   if (rlength <= 0) { null_result(res, 0, p.dynprogindex); return 0; }
   if (!nogaps && rlength > GMAPDP_MAX_RLENGTH) rlength = GMAPDP_MAX_RLENGTH;
@@ -542,6 +553,21 @@ static int convert_end(gmapdp_ctx* ctx, const gmapdp_end_problem& p, gmapdp_resu
   if (!nogaps)
     gmapdp_compute_bands(&d.lband, &d.uband, rlength, glength, p.extraband,
                          /*widebandp*/ p.endalign != kQueryendIndels);
+  if ((p.flags & GMAPDP_SIMD) && !nogaps) {
+    // The SIMD builds' triangles (QUERYEND_NOGAPS has no fill: the same path in every build).
+    // find_best_endpoint_8/16 scans lower[r][c] for every c < r, so rlength > glength + 1 reads
+    // columns past glength, which the reference fills from uninitialised pair scores.
+    if (rlength > glength + 1) {
+      *err = bad(ctx, "GMAPDP_SIMD end gap with rlength > glength + 1: the reference's lower-triangle scan "
+                      "reads uninitialised pair scores there (stage3.c passes glength >= rlength)");
+      return 0;
+    }
+    if (d.lband < 0 || d.uband < 0) {
+      *err = bad(ctx, "negative band");
+      return 0;
+    }
+    d.flags |= kFSimd;
+  }
   d.genestrand = p.genestrand;
   d.dynprogindex = p.dynprogindex;
   return 1;
@@ -560,10 +586,6 @@ static int convert_genome(gmapdp_ctx* ctx, const gmapdp_genome_problem& p, gmapd
   res.gap_index = -1;
   res.gap_queryjump = 0;
   res.dynprogindex = p.dynprogindex;
-  if (p.flags & GMAPDP_SIMD) {
-    *err = bad(ctx, "GMAPDP_SIMD: the SIMD builds' genome-gap fills (bridge_intron_gap_*_ud) are not implemented");
-    return 0;
-  }
   if (p.rlength <= 1) {
     res.traceback_score = GMAPDP_NEG_INFINITY_32;
     return 0;
@@ -609,6 +631,7 @@ static int convert_genome(gmapdp_ctx* ctx, const gmapdp_genome_problem& p, gmapd
   d.flags = (watson ? kFWatson : 0) | ((p.flags & GMAPDP_JUMP_LATE) ? kFLate : 0) |
             ((p.flags & GMAPDP_HALFP) ? kGHalf : 0) | ((p.flags & GMAPDP_FINALP) ? kGFinal : 0);
   if (!(p.flags & GMAPDP_FINALP) && dr < 0.014) d.flags |= kGSimple;  // :3479
+  if (p.flags & GMAPDP_SIMD) d.flags |= kGSimd;
   if (watson) {
     d.segposL = p.chroffset + (uint32_t)p.goffsetL;  // Genome_get_segment_right(left, chrhigh)
     d.segboundL = p.chrhigh;
@@ -642,6 +665,17 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     d.pair_offset = (int32_t)pair_off;
     pair_off += (size_t)d.rlength + (size_t)d.glength + 2;
     const bool nofill = d.kind != kSingle && d.endalign == kQueryendNogaps;
+    if ((d.flags & kFSimd) && d.kind != kSingle) {
+      // Dynprog_end5/3_gap of the SIMD builds (dynprog_end.c:1406 / 2027): 8-bit triangles when
+      // either length is below use8p_size[ENDQ]
+      const int B = (d.rlength < kUse8pSize[kEndQ] || d.glength < kUse8pSize[kEndQ]) ? 32 : 16;
+      const size_t lds = lds_bytes_uxe(d.rlength, d.glength, B);
+      if (lds > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
+      d.dirs_offset = (int64_t)gdirs_off;
+      gdirs_off += (scratch_bytes_uxe(d.rlength, d.glength, d.lband, d.uband, B) + 255) & ~(size_t)255;
+      classes[std::make_tuple((int)PlanCore::kUxe, B, 0, gg_lds_bucket(lds))].push_back((int)s);
+      continue;
+    }
     if (d.flags & kFSimd) {
       // Dynprog_single_gap of the SIMD builds (dynprog_single.c:593-631): 8-bit blocks of 32 rows when
       // both lengths are below use8p_size (dynprog.c:1022-1025), else 16-bit blocks of 16 rows
@@ -684,6 +718,18 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     d.pair_offset = (int32_t)pair_off;
     // traceback R (<= r + gR records) + gap holder + traceback L (<= r + gL records)
     pair_off += 2 * (size_t)d.rlength + (size_t)d.glengthL + (size_t)d.glengthR + 4;
+    if (d.flags & kGSimd) {
+      // the SIMD builds' genome gap (dynprog_genome.c:3501-3507): 8-bit triangles when rlength, or
+      // both glengths, are below use8p_size
+      const int u = kUse8pSize[d.mismatchtype];
+      const int B = (d.rlength < u || (d.glengthL < u && d.glengthR < u)) ? 32 : 16;
+      const size_t lds = lds_bytes_uxg(d.rlength, d.glengthL, d.glengthR, B);
+      if (lds > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
+      d.dirs_offset = (int64_t)gdirs_off;
+      gdirs_off += (scratch_bytes_uxg(d.rlength, d.glengthL, d.glengthR, d.lbandL, B) + 255) & ~(size_t)255;
+      classes[std::make_tuple((int)PlanCore::kUxg, B, 0, gg_lds_bucket(lds))].push_back((int)s);
+      continue;
+    }
     if (d.open > 0) return bad(ctx, "positive gap-open penalty is not supported by the scan formulation");
     const int WL = d.lbandL + d.ubandL + 1, WR = d.lbandL + d.ubandR + 1;
     const int R = pick_R(std::max(WL, WR));
@@ -705,7 +751,7 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     L.count = (int)kv.second.size();
     // longest problems first, so the tail of the launch is short work
     std::vector<int> ids = kv.second;
-    if (L.kind != PlanCore::kGenomeGap) {
+    if (L.kind != PlanCore::kGenomeGap && L.kind != PlanCore::kUxg) {
       std::stable_sort(ids.begin(), ids.end(), [&](int a, int b) {
         return (size_t)plan.dev[a].glength * (plan.dev[a].lband + plan.dev[a].uband + 1) >
                (size_t)plan.dev[b].glength * (plan.dev[b].lband + plan.dev[b].uband + 1);
@@ -752,6 +798,12 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
       if (L.kind == PlanCore::kGenomeGap) {
         const DevGenomeProblem& d = plan.gdev[id];
         L.work += (double)std::max(d.glengthL, d.glengthR) * L.R + d.rlength;
+      } else if (L.kind == PlanCore::kUxg) {
+        const DevGenomeProblem& d = plan.gdev[id];
+        L.work += (double)(d.glengthL + d.glengthR + 2 * d.rlength) + 4.0 * d.rlength;
+      } else if (L.kind == PlanCore::kUxe) {
+        const DevProblem& d = plan.dev[id];
+        L.work += (double)(d.rlength + d.glength) + 0.5 * d.rlength;
       } else {
         const DevProblem& d = plan.dev[id];
         if (L.kind == PlanCore::kSx)
@@ -847,6 +899,16 @@ struct RunArgs {
 
 static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, const RunArgs& a, hipStream_t stream) {
   const auto& L = plan.launches[li];
+  if (L.kind == PlanCore::kUxe)
+    return launch_uxe(L.R, L.count, L.lds, stream, a.d_probs, a.d_order + L.first, (unsigned char*)ctx->gdirs.p,
+                      ctx->d_genome, ctx->genome_words, a.d_q, a.d_quc, ctx->d_sc, ctx->d_cs, a.d_results,
+                      a.d_pairs);
+  if (L.kind == PlanCore::kUxg) {
+    if (!a.d_gresults || !a.d_sprob) return hipErrorInvalidValue;
+    return launch_uxg(L.R, L.count, L.lds, stream, a.d_gprobs, a.d_gorder + L.first, (unsigned char*)ctx->gdirs.p,
+                      ctx->d_genome, ctx->genome_words, a.d_q, a.d_quc, a.d_sprob, ctx->d_sc, ctx->d_cs, ctx->d_isc,
+                      a.d_gresults, a.d_pairs);
+  }
   if (L.kind == PlanCore::kSx)
     return launch_sx(L.R, L.count, (int)L.lds, (long long)L.extra, (unsigned char*)ctx->gdirs.p + L.gdirs_offset,
                      stream, a.d_probs, a.d_order + L.first, ctx->d_genome, ctx->genome_words, a.d_q, a.d_quc,

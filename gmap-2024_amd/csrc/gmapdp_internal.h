@@ -64,6 +64,7 @@ constexpr int32_t kGSegLLeft = 0x800;   // gsequenceL via Genome_get_segment_lef
 constexpr int32_t kGSegLRc = 0x1000;
 constexpr int32_t kGSegRLeft = 0x2000;  // rev_gsequenceR via Genome_get_segment_left (plus strand)
 constexpr int32_t kGSegRRc = 0x4000;
+constexpr int32_t kGSimd = 0x8000;      // SIMD-build semantics (triangle fills, uxg_kernel)
 constexpr int32_t kUnset = (int32_t)0x80000000;  // out-parameter the reference leaves unwritten
 
 // Dynprog_genome_gap descriptor (dynprog_genome.c:3288): two fills share the

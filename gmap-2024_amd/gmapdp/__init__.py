@@ -18,7 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GMAPDP_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libgmapdp.so")
 
 WATSON, JUMP_LATE, WIDEBAND = 0x1, 0x2, 0x4
-SIMD = 0x40  # GMAPDP_SIMD: the reference's SIMD builds' semantics (single gaps)
+SIMD = 0x40  # GMAPDP_SIMD: the reference's SIMD builds' semantics (every problem family)
 HALFP, FINALP = 0x8, 0x10
 UNSET = -2147483648
 NEG_INFINITY_32 = -32768
@@ -187,6 +187,8 @@ def build_genome_batch(calls):
                   "flags", "cdna_direction", "genestrand", "extraband", "maxpeelback", "dynprogindex",
                   "defect_rate"):
             probs[i][k] = p[k]
+        if p.get("simd"):
+            probs[i]["flags"] |= SIMD
         probs[i]["prob_offset"] = poff
         poff += max(0, p["glengthL"]) + max(0, p["glengthR"])
         qparts.append(p["q"])

@@ -80,10 +80,13 @@ typedef struct {
 #define GMAPDP_WATSON     0x1  /* watsonp */
 #define GMAPDP_JUMP_LATE  0x2  /* jump_late_p */
 #define GMAPDP_WIDEBAND   0x4  /* widebandp */
-/* Reproduce the reference's SIMD builds (gmap.sse42/.avx2/.avx512: Dynprog_simd_8/16 fills,
- * dynprog_simd.c) instead of the nosimd build (Dynprog_standard).  Single gaps only so far:
- * the end and genome-gap entry points return GMAPDP_EINVAL for it.  The SIMD fills read
- * arena cells the call never wrote; the engine defines those as zero (a fresh arena). */
+/* Reproduce the reference's SIMD builds (gmap.sse42/.avx2/.avx512, dynprog_simd.c) instead of
+ * the nosimd build (Dynprog_standard): Dynprog_simd_8/16 for single gaps, the
+ * Dynprog_simd_8/16_upper/_lower triangles with their endpoint scans, bridge and tracebacks for
+ * end and genome gaps.  Valid in every problem family (genome gaps: in `flags` as well).  The
+ * SIMD fills read arena cells the call never wrote; the engine defines those as zero (a fresh
+ * arena).  End gaps with rlength > glength + 1 (chopped lengths, QUERYEND_NOGAPS excepted) are
+ * GMAPDP_EINVAL: the reference's lower-triangle scan reads uninitialised scores there. */
 #define GMAPDP_SIMD       0x40
 
 /* One Dynprog_single_gap call (dynprog_single.c:429 argument list).  The

@@ -1807,3 +1807,178 @@ orc_genome_gap (const char *rsequence, const char *rsequenceuc, int rlength, int
   gg_scalars(&o, scalars, dscalars);
   return n;
 }
+
+/* ---------------------------------------------------------------------------
+ * Dynprog_cdna_gap (dynprog_cdna.c:787-1300): a cDNA insertion.  L fills the
+ * query piece rsequenceL forward against gsequence, R the piece ending at
+ * rev_rsequenceR backwards against rev_gsequence (the same genome interval);
+ * the bridge picks the split (cL, cR, rL, rR) allowing a genomic insertion
+ * (pen = 0 for cR = glength - cL, else open + extend per further column).
+ * Penalties are CDNA_OPEN/EXTEND (-10/-7) for every defect rate; user
+ * penalties are not consulted.  Both builds: nosimd (Dynprog_standard,
+ * bridge_cdna_gap :652 with its own bands, the R fill called with lbandL)
+ * and SIMD (the triangles, bridge_cdna_gap_8/16_ud :124/387 with the fill
+ * bands, upper cells for r < c and lower cells for r >= c).
+ * ------------------------------------------------------------------------- */
+#define CDNA_OPEN -10
+#define CDNA_EXTEND -7
+#define INSERT_PAIRS 9
+#define SHORTGAP_COMP '~'
+
+/* The candidate scan shared by both bridges: for cL, cR (descending), rL, rR the score
+   cell(L, cL, rL) + cell(R, cR, rR) + pen, > (jump early) or >= (jump late). */
+typedef int (*CellFn) (const int *mu, const int *ml, int rlength, int c, int r);
+static int cell_std (const int *mu, const int *ml, int rlength, int c, int r) {
+  (void) ml;
+  return mu[(size_t) c * (rlength + 1) + r];
+}
+static int cell_ud (const int *mu, const int *ml, int rlength, int c, int r) {
+  return (r < c ? mu : ml)[(size_t) c * (rlength + 1) + r];   /* upper[c][r] for r < c, else lower[r][c] */
+}
+
+static int
+bridge_cdna (int *bestcL, int *bestcR, int *bestrL, int *bestrR, CellFn cell, const int *mLu, const int *mLl,
+             const int *mRu, const int *mRl, int glength, int rlengthL, int rlengthR, int lbandL, int ubandL,
+             int lbandR, int ubandR, int open, int extend, int leftoffset, int rightoffset, int late, int neg) {
+  int bestscore = neg, score, scoreL, scoreR, pen, rL, rR, cL, cR, rloL, rhighL, rloR, rhighR;
+  for (cL = 1; cL < glength; cL++) {
+    for (cR = glength - cL, pen = 0; cR >= 0; cR--, pen += extend) {
+      if ((rloL = cL - ubandL) < 1) rloL = 1;
+      if ((rhighL = cL + lbandL) > rlengthL - 1) rhighL = rlengthL - 1;
+      if ((rloR = cR - ubandR) < 1) rloR = 1;
+      if ((rhighR = cR + lbandR) > rlengthR - 1) rhighR = rlengthR - 1;
+      for (rL = rloL; rL <= rhighL; rL++) {
+        scoreL = cell(mLu, mLl, rlengthL, cL, rL);
+        for (rR = rloR; rR <= rhighR && rR < rightoffset - leftoffset - rL; rR++) {
+          scoreR = cell(mRu, mRl, rlengthR, cR, rR);
+          if (prefer(score = scoreL + scoreR + pen, bestscore, late)) {
+            bestscore = score;
+            *bestcL = cL; *bestcR = cR; *bestrL = rL; *bestrR = rR;
+          }
+        }
+      }
+      pen = open - extend;
+    }
+  }
+  return bestscore;
+}
+
+/* Domain: rlengthL == rlengthR >= glength >= 2 -- what stage3.c passes (both lengths
+   queryjump = genomejump + extramaterial_paired, stage3.c:9275).  There the nosimd bridge's own
+   bands equal the fills' (and lbandL = lbandR), so every cell it reads was computed; outside it
+   the reference reads cells no fill wrote.  Returns -3 outside the domain. */
+int
+orc_cdna_gap (const char *qbuf, const char *qucbuf, int qposL, int qposR, int rlengthL, int rlengthR, int glength,
+              int roffsetL, int rev_roffsetR, int goffset, unsigned int chroffset, unsigned int chrhigh,
+              int watsonp, int genestrand, int jump_late_p, int extraband_paired, double defect_rate,
+              int dynprogindex, int *scalars, OrcPair *out, int max_pairs) {
+  const char *rsequenceL = qbuf + qposL, *rsequence_ucL = qucbuf + qposL;
+  const char *rev_rsequenceR = qbuf + qposR, *rev_rsequence_ucR = qucbuf + qposR;
+  int mismatchtype, lbandL, ubandL, lbandR, ubandR, rev_goffset, bestrL = 0, bestrR = 0, bestcL = 0, bestcR = 0;
+  int queryjump, genomejump, k, n, bits = 32;
+  char *gs, *gsa, *rgs, *rgsa, c2, c2_alt;
+  const char *revg;
+  size_t pl, pr;
+  int *mL, *mR;
+  signed char *dL, *dR;
+  PairSink sink = {out, 0, max_pairs};
+  Tally t = {0, 0, 0, 0, 0};
+
+  scalars[0] = dynprogindex; scalars[1] = ORC_UNSET; scalars[2] = 0;
+  if (glength <= 1) return -1;
+  if (defect_rate < DEFECT_HIGHQ) mismatchtype = HIGHQ;
+  else if (defect_rate < DEFECT_MEDQ) mismatchtype = MEDQ;
+  else mismatchtype = LOWQ;
+  if (glength > ORC_MAX_GLENGTH || rlengthR > ORC_MAX_RLENGTH || rlengthL > ORC_MAX_RLENGTH) {
+    scalars[0] = dynprogindex + (dynprogindex > 0 ? +1 : -1);
+    return -1;
+  }
+  if (rlengthL != rlengthR || rlengthL < glength) return -3;
+  rev_goffset = goffset + glength - 1;
+  gs = (char *) malloc(glength + 1); gsa = (char *) malloc(glength + 1);
+  rgs = (char *) malloc(glength + 1); rgsa = (char *) malloc(glength + 1);
+  if (watsonp) {
+    orc_get_segment(0, chroffset + (unsigned int) rev_goffset + 1u, glength, chroffset, 0, rgs, rgsa);
+    orc_get_segment(1, chroffset + (unsigned int) goffset, glength, chrhigh, 0, gs, gsa);
+  } else {
+    orc_get_segment(1, chrhigh - (unsigned int) rev_goffset, glength, chrhigh, 1, rgs, rgsa);
+    orc_get_segment(0, chrhigh - (unsigned int) goffset + 1u, glength, chroffset, 1, gs, gsa);
+  }
+  if (gs[0] == '\0' || rgs[0] == '\0') {
+    free(gs); free(gsa); free(rgs); free(rgsa);
+    return -1;
+  }
+  revg = rgs + glength - 1;
+  pl = (size_t) (glength + 1) * (rlengthL + 1);
+  pr = (size_t) (glength + 1) * (rlengthR + 1);
+  mL = (int *) malloc(2 * pl * sizeof(int)); mR = (int *) malloc(2 * pr * sizeof(int));
+  dL = (signed char *) malloc(6 * pl); dR = (signed char *) malloc(6 * pr);
+  compute_bands(&lbandL, &ubandL, rlengthL, glength, extraband_paired, 1);
+  compute_bands(&lbandR, &ubandR, rlengthR, glength, extraband_paired, 1);
+  if (g_simd) {
+    /* :898-904: 8-bit when glength is below use8p_size, or rlengthL is and rlengthR is not above it */
+    const int u = use8p_size[mismatchtype];
+    bits = (glength < u || (rlengthL < u && rlengthR <= u)) ? 8 : 16;
+    simd_fill_ud(bits, 1, rsequenceL, gs, gs, rlengthL, glength, mismatchtype, CDNA_OPEN, CDNA_EXTEND, ubandL,
+                 jump_late_p, 0, mL, dL);
+    simd_fill_ud(bits, 0, rsequenceL, gs, gs, rlengthL, glength, mismatchtype, CDNA_OPEN, CDNA_EXTEND, lbandL,
+                 jump_late_p, 0, mL + pl, dL + 3 * pl);
+    simd_fill_ud(bits, 1, rev_rsequenceR, revg, revg, rlengthR, glength, mismatchtype, CDNA_OPEN, CDNA_EXTEND,
+                 ubandR, !jump_late_p, 1, mR, dR);
+    simd_fill_ud(bits, 0, rev_rsequenceR, revg, revg, rlengthR, glength, mismatchtype, CDNA_OPEN, CDNA_EXTEND,
+                 lbandR, !jump_late_p, 1, mR + pr, dR + 3 * pr);
+    bridge_cdna(&bestcL, &bestcR, &bestrL, &bestrR, cell_ud, mL, mL + pl, mR, mR + pr, glength, rlengthL, rlengthR,
+                lbandL, ubandL, lbandR, ubandR, CDNA_OPEN, CDNA_EXTEND, roffsetL, rev_roffsetR, jump_late_p,
+                bits == 8 ? -128 : -32768);
+  } else {
+    orc_standard_fill(rsequenceL, gs, gs, rlengthL, glength, mismatchtype, CDNA_OPEN, CDNA_EXTEND, lbandL, ubandL,
+                      jump_late_p, 0, NEG_INFINITY_32, 1, 1, mL, dL);
+    /* the reference passes lbandL to the R fill (dynprog_cdna.c:1227) */
+    orc_standard_fill(rev_rsequenceR, revg, revg, rlengthR, glength, mismatchtype, CDNA_OPEN, CDNA_EXTEND, lbandL,
+                      ubandR, !jump_late_p, 1, NEG_INFINITY_32, 1, 1, mR, dR);
+    /* bridge_cdna_gap's own bands (:667-670) */
+    bridge_cdna(&bestcL, &bestcR, &bestrL, &bestrR, cell_std, mL, NULL, mR, NULL, glength, rlengthL, rlengthR,
+                rlengthL - glength + extraband_paired, extraband_paired, rlengthR - glength + extraband_paired,
+                extraband_paired, CDNA_OPEN, CDNA_EXTEND, roffsetL, rev_roffsetR, jump_late_p, NEG_INFINITY_32);
+  }
+  /* traceback R (upper/lower by bestc >= bestr in the SIMD build), List_reverse */
+  if (g_simd) {
+    int up = bestcR >= bestrR;
+    traceback_mode(&sink, &t, up ? dR : dR + 3 * pr, rlengthR, glength, bestrR, bestcR, rev_rsequenceR,
+                   rev_rsequence_ucR, revg, revg, rev_roffsetR, rev_goffset, 1, chroffset, chrhigh, watsonp,
+                   genestrand, dynprogindex, up ? 1 : 2);
+  } else {
+    traceback_std(&sink, &t, dR, rlengthR, glength, bestrR, bestcR, rev_rsequenceR, rev_rsequence_ucR, revg, revg,
+                  rev_roffsetR, rev_goffset, 1, chroffset, chrhigh, watsonp, genestrand, dynprogindex);
+  }
+  n = sink.n < max_pairs ? sink.n : max_pairs;
+  reverse_pairs(out, n);
+  queryjump = (rev_roffsetR - bestrR) - (roffsetL + bestrL) + 1;
+  genomejump = (rev_goffset - bestcR) - (goffset + bestcL) + 1;
+  if (queryjump == INSERT_PAIRS && genomejump == INSERT_PAIRS) {
+    for (k = rev_roffsetR - bestrR; k >= roffsetL + bestrL; k--)
+      sink_push(&sink, k, rev_goffset - bestcR + 1, rsequenceL[k - roffsetL], SHORTGAP_COMP, ' ', ' ', dynprogindex);
+    for (k = rev_goffset - bestcR; k >= goffset + bestcL; k--) {
+      c2 = get_genomic_nt(&c2_alt, k, chroffset, chrhigh, watsonp);
+      sink_push(&sink, roffsetL + bestrL, k, ' ', SHORTGAP_COMP, c2, c2_alt, dynprogindex);
+    }
+  } else {
+    sink_gapholder(&sink, queryjump, genomejump);
+    scalars[2] = 1;
+  }
+  if (g_simd) {
+    int up = bestcL >= bestrL;
+    traceback_mode(&sink, &t, up ? dL : dL + 3 * pl, rlengthL, glength, bestrL, bestcL, rsequenceL, rsequence_ucL,
+                   gs, gs, roffsetL, goffset, 0, chroffset, chrhigh, watsonp, genestrand, dynprogindex, up ? 1 : 2);
+  } else {
+    traceback_std(&sink, &t, dL, rlengthL, glength, bestrL, bestcL, rsequenceL, rsequence_ucL, gs, gs, roffsetL,
+                  goffset, 0, chroffset, chrhigh, watsonp, genestrand, dynprogindex);
+  }
+  scalars[0] = dynprogindex + (dynprogindex > 0 ? +1 : -1);
+  scalars[1] = t.score;
+  n = sink.n;
+  free(mL); free(mR); free(dL); free(dR); free(gs); free(gsa); free(rgs); free(rgsa);
+  if (n == 1) return -1;  /* only the gap added (:1284) */
+  /* returned: List_reverse of [reverse(TL) reverse(I) TR] = reverse(TR) I TL, the sink order */
+  return n;
+}

@@ -94,6 +94,15 @@ int orc_intron_scores (int *out3x2x64);
 int orc_pairdistance (int mismatchtype, short *out128x128);
 int orc_consistent (int genestrand, unsigned char *out128x128);
 
+/* Dynprog_cdna_gap (dynprog_cdna.c:787), nosimd or SIMD semantics (orc_set_simd).
+   rsequenceL = qbuf + qposL, rev_rsequenceR = qbuf + qposR (the R piece's last character).
+   scalars[0..2] = dynprogindex(after), traceback_score (INT_MIN when unwritten), incompletep.
+   Returns npairs, -1 for NULL, -3 outside the domain (rlengthL == rlengthR >= glength). */
+int orc_cdna_gap (const char *qbuf, const char *qucbuf, int qposL, int qposR, int rlengthL, int rlengthR,
+                  int glength, int roffsetL, int rev_roffsetR, int goffset, unsigned int chroffset,
+                  unsigned int chrhigh, int watsonp, int genestrand, int jump_late_p, int extraband_paired,
+                  double defect_rate, int dynprogindex, int *scalars, OrcPair *out, int max_pairs);
+
 #ifdef __cplusplus
 }
 #endif

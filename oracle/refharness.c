@@ -33,6 +33,7 @@
 #include "dynprog_single.h"
 #include "dynprog_end.h"
 #include "dynprog_genome.h"
+#include "dynprog_cdna.h"
 #include "maxent_hr.h"
 
 /* Flat pair record (matches oracle/gmapdp_oracle.h RefPair / GmapdpPair
@@ -325,6 +326,30 @@ refh_genome_gap (const char *rsequence, const char *rsequenceuc, int rlength, in
   scalars[4] = nopens; scalars[5] = nindels; scalars[6] = new_left; scalars[7] = new_right;
   scalars[8] = exonhead; scalars[9] = introntype;
   dscalars[0] = left_prob; dscalars[1] = right_prob;
+  if (pairs == NULL) return -1;
+  return flatten(pairs, out, max_pairs);
+}
+
+/* Dynprog_cdna_gap (dynprog_cdna.c:787).  The query is one buffer: rsequenceL = qbuf + qposL,
+   rev_rsequenceR = qbuf + qposR (the R piece's LAST character).  scalars[0..2] =
+   dynprogindex(after), traceback_score (REFH_UNSET where the reference leaves it unwritten),
+   incompletep (starts 0).  Returns the number of pairs or -1 for NULL. */
+int
+refh_cdna_gap (const char *qbuf, const char *qucbuf, int qposL, int qposR, int rlengthL, int rlengthR,
+               int glength, int roffsetL, int rev_roffsetR, int goffset, unsigned int chroffset,
+               unsigned int chrhigh, int watsonp, int genestrand, int jump_late_p, int extraband_paired,
+               double defect_rate, int dynprogindex, int *scalars, RefPair *out, int max_pairs) {
+  List_T pairs;
+  int score = REFH_UNSET;
+  bool incompletep = false;
+
+  Pairpool_reset(pairpool);
+  pairs = Dynprog_cdna_gap(&dynprogindex, &score, &incompletep, dynprogL, dynprogR,
+                           (char *) qbuf + qposL, (char *) qucbuf + qposL, (char *) qbuf + qposR,
+                           (char *) qucbuf + qposR, rlengthL, rlengthR, glength, roffsetL, rev_roffsetR, goffset,
+                           (Univcoord_T) chroffset, (Univcoord_T) chrhigh, watsonp ? true : false, genestrand,
+                           jump_late_p ? true : false, genome, genome, pairpool, extraband_paired, defect_rate);
+  scalars[0] = dynprogindex; scalars[1] = score; scalars[2] = incompletep ? 1 : 0;
   if (pairs == NULL) return -1;
   return flatten(pairs, out, max_pairs);
 }

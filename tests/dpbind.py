@@ -510,3 +510,83 @@ def splice_probs(ref, orc, p):
     sl, sr = orc.splice_sites(p)
     return ([ref.maxent(m, pos, p["chroffset"]) for pos, m in sl],
             [ref.maxent(m, pos, p["chroffset"]) for pos, m in sr])
+
+
+# ---------------------------------------------------------------------------
+# Dynprog_cdna_gap (dynprog_cdna.c:787)
+# ---------------------------------------------------------------------------
+_CG_ARGS = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+            C.c_uint, C.c_uint, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int]
+
+
+def _cdna_gap(self, p):
+    """((dynprogindex, traceback_score, incompletep), pairs-or-None); None for pairs also when the
+    oracle reports the call outside its domain (scalars then end with -3)."""
+    self._before_call()
+    f = getattr(self.lib, self.prefix + "cdna_gap")
+    if not getattr(self, "_cg_ready", False):
+        f.argtypes = _CG_ARGS + [C.POINTER(C.c_int), C.POINTER(Pair), C.c_int]
+        f.restype = C.c_int
+        self._cg_scal = (C.c_int * 3)()
+        self._cg_ready = True
+    n = f(p["q"], p["quc"], p["qposL"], p["qposR"], p["rlengthL"], p["rlengthR"], p["glength"], p["roffsetL"],
+          p["rev_roffsetR"], p["goffset"], p["chroffset"], p["chrhigh"], p["watsonp"], p["genestrand"],
+          p["jump_late_p"], p["extraband"], p["defect_rate"], p["dynprogindex"], self._cg_scal, self._pairs, MAXPAIRS)
+    assert n <= MAXPAIRS
+    if n == -3:
+        return tuple(self._cg_scal) + (-3,), None
+    return tuple(self._cg_scal), (None if n < 0 else [self._pairs[i].key() for i in range(n)])
+
+
+Ref.cdna_gap = _cdna_gap
+Oracle.cdna_gap = _cdna_gap
+
+
+def cdna_gap_problem(rng, genome: bytes, edge=False):
+    """One Dynprog_cdna_gap-shaped call (stage3.c:9270-9285): a cDNA insertion between two anchors.
+    The query gap is the genome gap (glength = genomejump) with `ins` extra bases inserted, so
+    queryjump > genomejump + MININTRONLEN; both query pieces are queryjump' = glength +
+    extramaterial_paired (8) long, the L piece from querydp5 forward, the R piece ending at
+    querydp3."""
+    # the chromosome sits 1000 nt inside the genome: segments running past its ends read '*'
+    # (or, for the Genome_get_segment variant without that bound, genome bytes) but stay in memory
+    chroffset, chrhigh = 1000, len(genome) - 1000
+    chrlen = chrhigh - chroffset
+    watsonp = rng.random() < 0.6
+    G = rng.randint(2, 8) if edge and rng.random() < 0.5 else max(2, min(400, int(rng.gammavariate(2.0, 30))))
+    if edge and rng.random() < 0.15:
+        G = rng.choice([1, 1, 660])  # glength <= 1: NULL; rlength = G + 8 > 660: the size guard
+    ins = rng.randint(10, 14) if rng.random() < 0.3 else rng.randint(10, 250)
+    goffset = rng.randint(10, chrlen - G - 10)
+    if edge and rng.random() < 0.2:
+        goffset = rng.choice([0, 1, chrlen - G - rng.randint(-3, 3)])
+    seg = bytes(_strand_get(genome, goffset + i, chroffset, chrhigh, watsonp) for i in range(G)).replace(b"*", b"A")
+    a = rng.randint(0, G)
+    insert = bytes(rng.choice(b"ACGT") for _ in range(ins))
+    if rng.random() < 0.15:  # the insertion copies flanking genome (repeats make ties)
+        insert = (seg * (ins // max(1, G) + 2))[:ins]
+    gap = seg[:a] + insert + seg[a:]
+    q, quc = mutate(rng, gap, sub=rng.choice([0.0, 0.01, 0.03, 0.08]), indel=rng.choice([0.0, 0.0, 0.01]))
+    block9 = G >= 24 and rng.random() < 0.15
+    if block9:
+        # a 9 x 9 unaligned block: the bridge leaves queryjump = genomejump = INSERT_PAIRS and the
+        # reference pushes the block as SHORTGAP pairs instead of a gap holder (dynprog_cdna.c:1240);
+        # both query pieces then reach into the flanks
+        a = rng.randint(3, G - 12)
+        q = quc = seg[:a] + bytes(rng.choice(b"ACGT") for _ in range(9)) + seg[a + 9:]
+    f5 = bytes(rng.choice(b"ACGT") for _ in range(rng.randint(10 if block9 else 0, 20)))
+    f3 = bytes(rng.choice(b"ACGT") for _ in range(rng.randint(10 if block9 else 0, 20)))
+    Q = len(q)
+    rlength = G + 8
+    if Q < rlength + 1 and not block9:  # keep queryjump > genomejump + MININTRONLEN after the mutations
+        pad = bytes(rng.choice(b"ACGT") for _ in range(rlength + 1 - Q))
+        q, quc, Q = q + pad, quc + pad, Q + len(pad)
+    qbuf, qucbuf = f5 + q + f3, f5 + quc + f3
+    qposL = len(f5)
+    qposR = qposL + Q - 1
+    roffsetL = rng.randint(0, 3000)
+    return dict(q=qbuf, quc=qucbuf, qposL=qposL, qposR=qposR, rlengthL=rlength, rlengthR=rlength, glength=G,
+                roffsetL=roffsetL, rev_roffsetR=roffsetL + (qposR - qposL), goffset=goffset, chroffset=chroffset,
+                chrhigh=chrhigh, watsonp=int(watsonp), genestrand=0, jump_late_p=rng.randint(0, 1),
+                extraband=rng.choice([14, 14, 3, 6]), defect_rate=rng.choice([0.001, 0.005, 0.02, 0.05]),
+                dynprogindex=rng.choice([1, 5, -1, -7]))

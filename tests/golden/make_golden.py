@@ -17,6 +17,8 @@ and the reference's outputs.
                          MaxEnt splice probabilities (Maxent_hr_*_prob) at every entry the
                          engine reads; halfp problems come from the --enable-alloca nosimd
                          build (the default heap build dereferences a freed array there)
+  cdna_gap_golden.npz, simd_cdna_gap_golden.npz
+                         Dynprog_cdna_gap (dynprog_cdna.c:787) from the nosimd and AVX2 objects
   simd_{single,end,genome}_gap_golden.npz
                          the same entry points as the SIMD builds compute them (gmap.avx2:
                          Dynprog_simd_8/16, the _upper/_lower triangles, bridge_intron_gap_*_ud),
@@ -32,13 +34,16 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
-from dpbind import (GG_FLAG_HALF, Oracle, Ref, call_end, call_single, edge_single_gap_problem,  # noqa: E402
-                    end_gap_problem, genome_gap_problem, random_genome, single_gap_problem, splice_probs)
+from dpbind import (GG_FLAG_HALF, Oracle, Ref, call_end, call_single, cdna_gap_problem,  # noqa: E402
+                    edge_single_gap_problem, end_gap_problem, genome_gap_problem, random_genome,
+                    single_gap_problem, splice_probs)
 
 SINGLE_PARAMS = ["rlength", "glength", "roffset", "goffset", "chroffset", "chrhigh", "watsonp", "genestrand",
                  "jump_late_p", "extraband", "widebandp", "dynprogindex"]
 END_PARAMS = ["end3p", "rlength", "glength", "roffset", "goffset", "chroffset", "chrhigh", "watsonp",
               "genestrand", "jump_late_p", "extraband", "endalign", "require_pos_score_p", "dynprogindex"]
+CDNA_PARAMS = ["qposL", "qposR", "rlengthL", "rlengthR", "glength", "roffsetL", "rev_roffsetR", "goffset",
+               "chroffset", "chrhigh", "watsonp", "genestrand", "jump_late_p", "extraband", "dynprogindex"]
 GENOME_PARAMS = ["rlength", "glengthL", "glengthR", "roffset", "goffsetL", "rev_goffsetR", "chroffset", "chrhigh",
                  "cdna_direction", "flags", "genestrand", "extraband", "maxpeelback", "dynprogindex"]
 PAIR_DT = np.dtype([("querypos", "<i4"), ("genomepos", "<i4"), ("queryjump", "<i4"), ("genomejump", "<i4"),
@@ -68,6 +73,30 @@ def genome_problems(seed=2026, n_typical=1200, n_edge=400, genome_len=60000):
     probs = [genome_gap_problem(rng, g) for _ in range(n_typical)]
     probs += [genome_gap_problem(rng, g, edge=True) for _ in range(n_edge)]
     return bytes(g), probs
+
+
+def cdna_problems(seed=2027, n_typical=1000, n_edge=300, genome_len=30000):
+    rng = random.Random(seed)
+    g = random_genome(rng, genome_len)
+    probs = [cdna_gap_problem(rng, g) for _ in range(n_typical)]
+    probs += [cdna_gap_problem(rng, g, edge=True) for _ in range(n_edge)]
+    return g, probs
+
+
+def call_cdna(impl, p):
+    return impl.cdna_gap(p)
+
+
+def main_cdna():
+    """Dynprog_cdna_gap goldens of both builds (the same problems; halfp does not apply)."""
+    g, probs = cdna_problems()
+    for name, variant in (("cdna_gap_golden.npz", "nosimd"), ("simd_cdna_gap_golden.npz", "avx2")):
+        ref = Ref(variant)
+        ref.set_genome(g)
+        outputs = {"ref_" + variant: [call_cdna(ref, p) for p in probs]}
+        out = os.path.join(HERE, name)
+        np.savez_compressed(out, **pack(g, probs, outputs, CDNA_PARAMS))
+        print("wrote %s: %d problems" % (out, len(probs)))
 
 
 def pack(g, probs, outputs, names):
@@ -200,5 +229,7 @@ def main():
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "simd":
         main_simd()
+    elif len(sys.argv) > 1 and sys.argv[1] == "cdna":
+        main_cdna()
     else:
         main()

@@ -316,3 +316,37 @@ def test_oracle_simd_end_and_genome_gaps_vs_reference_avx2():
         lp, rp = splice_probs(ref, orc, p)
         a, b = ref.genome_gap(p), orc.genome_gap(p, lp, rp)
         assert a == b, (i, {k: v for k, v in p.items() if k not in ("q", "quc")}, a[0], b[0])
+
+
+# ---------------------------------------------------------------------------
+# Dynprog_cdna_gap (dynprog_cdna.c:787), both builds
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("simd", [0, 1])
+def test_oracle_cdna_gap_matches_golden(simd):
+    name, tag = ("simd_cdna_gap_golden.npz", "ref_avx2") if simd else ("cdna_gap_golden.npz", "ref_nosimd")
+    g, probs, outs = _load_golden(name)
+    orc = Oracle(simd=bool(simd))
+    orc.set_genome(g)
+    exp = outs[tag]
+    assert len(probs) == len(exp) == 1300
+    bad = [i for i, p in enumerate(probs) if orc.cdna_gap(p) != exp[i]]
+    assert bad == [], "%s: oracle differs on %d problems (first %s)" % (name, len(bad), bad[:5])
+    # both the gap-holder and the INSERT_PAIRS (9 x 9 SHORTGAP block) exits, and NULL lists
+    assert sum(1 for s, pr in exp if pr and any(x[6] == b"~" for x in pr)) > 10
+    assert sum(1 for s, pr in exp if s[2] == 1) > 1000
+    assert sum(1 for s, pr in exp if pr is None) > 0
+
+
+@pytest.mark.skipif(not ref_available("avx2"), reason="reference objects not built")
+def test_oracle_cdna_gap_vs_reference_random():
+    from dpbind import cdna_gap_problem
+    rng = random.Random(91)
+    g = random_genome(rng, 30000)
+    for variant in ("nosimd", "avx2"):
+        ref, orc = Ref(variant), Oracle(simd=(variant == "avx2"))
+        ref.set_genome(g)
+        orc.set_genome(g)
+        for i in range(300):
+            p = cdna_gap_problem(rng, g, edge=(i % 4 == 0))
+            a, b = ref.cdna_gap(p), orc.cdna_gap(p)
+            assert a == b, (variant, i, {k: v for k, v in p.items() if k not in ("q", "quc")}, a[0], b[0])
