@@ -338,12 +338,15 @@ struct Part {
 // is then per segment, `gmax` is the wave's largest glength, the score rows are transposed
 // (sc[r*8 + class], no per-column multiply) and lane 0 stores the whole-wave ballots (segment j
 // owns bits [j*S, j*S+S) of each word).
-template <int R, bool CARRY, int S = 64, bool PK = (S < 64)>
+// STORE: also write the stored score of every band cell, smat[c * W + k] (the `matrix` that
+// Dynprog_cdna_gap's bridge reads at arbitrary cells).
+template <int R, bool CARRY, int S = 64, bool PK = (S < 64), bool STORE = false>
 __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lband, int uband, int open, int ext,
                                           int late, int track, const int8_t* sc, int srow, const uint8_t* gcl,
                                           uint64_t* dirs, const BridgeCarry* bc_, int& bestr, int& bestc,
-                                          int gmax = 0) {
+                                          int gmax = 0, int* smat = nullptr) {
   static_assert(S == 64 || (R == 1 && !CARRY), "segmented fills are single-word, no bridge carry");
+  static_assert(!STORE || S == 64, "score matrices are stored by whole-wave fills only");
   const int lk = (S == 64) ? lane : (lane & (S - 1));  // lane within the segment
   const int cend = (S == 64) ? glen : gmax;
   const int sat = kNegInf32;
@@ -459,6 +462,7 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
       mE[i] = ballot(eb[i]) & mvalid;
       mF[i] = ballot(fb) & mvalid;
       const int Hc = max(Hun[i], sat);
+      if (STORE && valid[i]) smat[(size_t)c * W + k] = Hc;
       // branch-free state update for the next column
       Hs[i] = valid[i] ? ((k == 0) ? Hun[i] : Hc) : ((r == 0) ? row0 : kNegInf32);
       E[i] = valid[i] ? En[i] : kNegInf32;

@@ -61,6 +61,12 @@ hipError_t launch_uxg(int B, int nproblems, size_t lds, hipStream_t stream, cons
                       const char* qseq, const char* qseq_uc, const double* sprob, const int8_t* sctab,
                       const uint8_t* constab, const int8_t* isctab, gmapdp_genome_result* results,
                       gmapdp_pair* pairs);
+size_t lds_bytes_cg(int rlength, int glength, bool simd, int RB);
+size_t scratch_bytes_cg(int rlength, int glength, int lband, int uband, bool simd, int RB);
+hipError_t launch_cg(bool simd, int RB, int nproblems, size_t lds, hipStream_t stream, const DevCdnaProblem* probs,
+                     const int* order, unsigned char* gscratch, const uint32_t* blocks, uint64_t nwords,
+                     const char* qseq, const char* qseq_uc, const int8_t* sctab, const uint8_t* constab,
+                     gmapdp_cdna_result* results, gmapdp_pair* pairs);
 static const int kUse8pSize[4] = {41, 63, 127, 24};  // use8p_size (dynprog.c:1022-1025)
 
 // ---------------------------------------------------------------------------
@@ -202,6 +208,7 @@ struct gmapdp_ctx {
   uint64_t genome_length = 0;
   DevBuf probs, order, qseq, qseq_uc, results, pairs, gdirs;
   DevBuf gprobs, gorder, sprob, gresults;
+  DevBuf cprobs, corder, cresults, cscratch;  // Dynprog_cdna_gap batches
   std::string err;
 };
 
@@ -1142,6 +1149,188 @@ int gmapdp_genome_gap_batch(gmapdp_ctx* ctx, const gmapdp_genome_problem* proble
   if (n > 0 && !problems) return GMAPDP_EINVAL;
   return run_batch(ctx, nullptr, 0, nullptr, 0, problems, n, qseq, qseq_uc, qbytes, splice_probs, nprobs, nullptr,
                    results, pairs, pair_capacity);
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Dynprog_cdna_gap (dynprog_cdna.c:787).  Rare in GMAP's pipeline, so it has its
+// own synchronous batch path: the prologue on the host, one launch per (semantics, R or B) class.
+// ---------------------------------------------------------------------------
+static const int kInsertPairsHost = 9;  // INSERT_PAIRS (dynprog_cdna.c:40)
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+static bool cdna_on_host(const gmapdp_cdna_problem& p) {
+  return p.glength <= 1 || p.glength > GMAPDP_MAX_GLENGTH || p.rlengthL > GMAPDP_MAX_RLENGTH ||
+         p.rlengthR > GMAPDP_MAX_RLENGTH;
+}
+
+// Dynprog_cdna_gap prologue (:830-940): returns 1 if the problem runs on the GPU.
+static int convert_cdna(gmapdp_ctx* ctx, const gmapdp_cdna_problem& p, size_t qbytes, gmapdp_cdna_result& res,
+                        DevCdnaProblem& d, int* err) {
+  *err = 0;
+  std::memset(&res, 0, sizeof(res));
+  res.traceback_score = GMAPDP_UNSET;
+  res.dynprogindex = p.dynprogindex;
+  res.gap_index = -1;
+  if (p.glength <= 1) return 0;  // :830, dynprogindex unchanged
+  if (cdna_on_host(p)) {         // size guard (:869-893)
+    res.dynprogindex = next_dpi(p.dynprogindex);
+    return 0;
+  }
+  if (p.rlengthL != p.rlengthR || p.rlengthL < p.glength) {
+    *err = bad(ctx, "Dynprog_cdna_gap needs rlengthL == rlengthR >= glength (the reference's bridge reads "
+                    "cells no fill wrote otherwise)");
+    return 0;
+  }
+  if (p.extraband < 0) {
+    *err = bad(ctx, "negative extraband_paired");
+    return 0;
+  }
+  const long span = std::max<long>(p.rlengthL, (long)p.rev_roffsetR - p.roffsetL + 1);
+  if (p.qoffL < 0 || p.qoffR - p.rlengthR + 1 < 0 || (size_t)(p.qoffL + span) > qbytes ||
+      (size_t)p.qoffR >= qbytes) {
+    *err = bad(ctx, "query pieces outside the query arena");
+    return 0;
+  }
+  std::memset(&d, 0, sizeof(d));
+  const double dr = p.defect_rate;
+  d.mismatchtype = dr < 0.003 ? kHighQ : (dr < 0.014 ? kMedQ : kLowQ);
+  d.open = -10;  // CDNA_OPEN_* / CDNA_EXTEND_* (:32-38), for every defect rate
+  d.extend = -7;
+  d.qbaseL = p.qoffL;
+  d.qbaseR = p.qoffR;
+  d.rlength = p.rlengthL;
+  d.glength = p.glength;
+  d.roffsetL = p.roffsetL;
+  d.rev_roffsetR = p.rev_roffsetR;
+  d.goffset = p.goffset;
+  d.chroffset = p.chroffset;
+  d.chrhigh = p.chrhigh;
+  // Dynprog_compute_bands(widebandp) with glength <= rlength; equal to bridge_cdna_gap's own bands
+  d.lband = p.rlengthL - p.glength + p.extraband;
+  d.uband = p.extraband;
+  const bool watson = p.flags & GMAPDP_WATSON;
+  const uint32_t rev_goffset = (uint32_t)(p.goffset + p.glength - 1);
+  d.flags = (watson ? kFWatson : 0) | ((p.flags & GMAPDP_JUMP_LATE) ? kFLate : 0) |
+            ((p.flags & GMAPDP_SIMD) ? kCSimd : 0);
+  if (watson) {  // :922-926
+    d.segpos = p.chroffset + (uint32_t)p.goffset;  // Genome_get_segment_right(left, chrhigh)
+    d.segbound = p.chrhigh;
+    d.rsegpos = p.chroffset + rev_goffset + 1u;    // Genome_get_segment_left(right, chroffset)
+    d.rsegbound = p.chroffset;
+    d.flags |= kCRSegLeft;
+  } else {       // :928-931
+    d.rsegpos = p.chrhigh - rev_goffset;           // _right(left, chrhigh), revcomp
+    d.rsegbound = p.chrhigh;
+    d.segpos = p.chrhigh - (uint32_t)p.goffset + 1u;  // _left(right, chroffset), revcomp
+    d.segbound = p.chroffset;
+    d.flags |= kCSegLeft | kCSegRc | kCRSegRc;
+  }
+  d.genestrand = p.genestrand;
+  d.dynprogindex = p.dynprogindex;
+  return 1;
+}
+
+static size_t cdna_capacity_one(const gmapdp_cdna_problem& p) {
+  if (cdna_on_host(p)) return 0;
+  // two tracebacks (each <= rlength + glength records) + the 9 + 9 SHORTGAP block or a gap holder
+  return 2 * ((size_t)p.rlengthL + (size_t)p.glength + 1) + 2 * kInsertPairsHost;
+}
+
+extern "C" {
+
+size_t gmapdp_cdna_pair_capacity(const gmapdp_cdna_problem* problems, int n) {
+  size_t cap = 0;
+  for (int i = 0; i < n; i++) cap += cdna_capacity_one(problems[i]);
+  return cap;
+}
+
+int gmapdp_cdna_gap_batch(gmapdp_ctx* ctx, const gmapdp_cdna_problem* problems, int n, const char* qseq,
+                          const char* qseq_uc, size_t qbytes, gmapdp_cdna_result* results, gmapdp_pair* pairs,
+                          size_t pair_capacity) {
+  if (!ctx || n < 0 || (n > 0 && (!problems || !results))) return GMAPDP_EINVAL;
+  if (!ctx->d_genome) return GMAPDP_ENOGENOME;
+  if (n == 0) return GMAPDP_OK;
+  (void)hipSetDevice(ctx->device);
+  std::vector<DevCdnaProblem> dev;
+  std::vector<int> dev_problem;
+  // launch classes: (simd, R or B) -> device slots
+  std::map<std::pair<int, int>, std::vector<int>> classes;
+  size_t pair_off = 0, scratch_off = 0;
+  for (int i = 0; i < n; i++) {
+    DevCdnaProblem d;
+    int err = 0;
+    if (!convert_cdna(ctx, problems[i], qbytes, results[i], d, &err)) {
+      if (err) return err;
+      continue;
+    }
+    const bool simd = d.flags & kCSimd;
+    const int W = d.lband + d.uband + 1;
+    int RB;
+    if (simd) {  // use8p (:909)
+      const int u = kUse8pSize[d.mismatchtype];
+      RB = (d.glength < u || (d.rlength < u && d.rlength <= u)) ? 32 : 16;
+    } else {
+      RB = pick_R(W);
+      if (RB > kMaxR) return bad(ctx, "Dynprog_cdna_gap band wider than 4096 cells");
+    }
+    d.pair_offset = (int32_t)pair_off;
+    pair_off += cdna_capacity_one(problems[i]);
+    d.scratch_offset = (int64_t)scratch_off;
+    scratch_off += align_up(scratch_bytes_cg(d.rlength, d.glength, d.lband, d.uband, simd, RB), 256);
+    classes[{simd ? 1 : 0, RB}].push_back((int)dev.size());
+    dev.push_back(d);
+    dev_problem.push_back(i);
+  }
+  if (pair_off > pair_capacity) return bad(ctx, "pair arena too small");
+  const int ndev = (int)dev.size();
+  if (ndev == 0) return GMAPDP_OK;
+  std::vector<int> order;
+  order.reserve(ndev);
+  struct CL {
+    bool simd;
+    int RB, first, count;
+    size_t lds;
+  };
+  std::vector<CL> launches;
+  for (auto& kv : classes) {
+    CL L{kv.first.first != 0, kv.first.second, (int)order.size(), (int)kv.second.size(), 0};
+    for (int s : kv.second) {
+      L.lds = std::max(L.lds, lds_bytes_cg(dev[s].rlength, dev[s].glength, L.simd, L.RB));
+      order.push_back(s);
+    }
+    launches.push_back(L);
+  }
+  hipError_t e = ctx->cprobs.ensure(sizeof(DevCdnaProblem) * ndev);
+  if (e == hipSuccess) e = ctx->corder.ensure(sizeof(int) * ndev);
+  if (e == hipSuccess) e = ctx->cresults.ensure(sizeof(gmapdp_cdna_result) * ndev);
+  if (e == hipSuccess) e = ctx->cscratch.ensure(std::max<size_t>(scratch_off, 256));
+  if (e == hipSuccess) e = ctx->qseq.ensure(qbytes);
+  if (e == hipSuccess) e = ctx->qseq_uc.ensure(qbytes);
+  if (e == hipSuccess) e = ctx->pairs.ensure(sizeof(gmapdp_pair) * std::max<size_t>(pair_off, 1));
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "device buffers: %s", e);
+  hipStream_t s = ctx->stream;
+  e = hipMemcpyAsync(ctx->cprobs.p, dev.data(), sizeof(DevCdnaProblem) * ndev, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(ctx->corder.p, order.data(), sizeof(int) * ndev, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(ctx->qseq.p, qseq, qbytes, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(ctx->qseq_uc.p, qseq_uc, qbytes, hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "upload: %s", e);
+  for (const CL& L : launches) {
+    e = launch_cg(L.simd, L.RB, L.count, L.lds, s, (const DevCdnaProblem*)ctx->cprobs.p,
+                  (const int*)ctx->corder.p + L.first, (unsigned char*)ctx->cscratch.p, ctx->d_genome,
+                  ctx->genome_words, (const char*)ctx->qseq.p, (const char*)ctx->qseq_uc.p, ctx->d_sc, ctx->d_cs,
+                  (gmapdp_cdna_result*)ctx->cresults.p, (gmapdp_pair*)ctx->pairs.p);
+    if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "cdna launch: %s", e);
+  }
+  std::vector<gmapdp_cdna_result> dres(ndev);
+  e = hipMemcpyAsync(dres.data(), ctx->cresults.p, sizeof(gmapdp_cdna_result) * ndev, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess && pairs)
+    e = hipMemcpyAsync(pairs, ctx->pairs.p, sizeof(gmapdp_pair) * pair_off, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "cdna execution: %s", e);
+  for (int d = 0; d < ndev; d++) results[dev_problem[d]] = dres[d];
+  return GMAPDP_OK;
 }
 
 }  // extern "C"

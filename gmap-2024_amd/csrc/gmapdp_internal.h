@@ -97,4 +97,39 @@ struct DevGenomeProblem {
   int64_t dirs_offset;    // byte offset into the global scratch (global-dirs classes)
 };
 
+// DevCdnaProblem.flags (kFWatson / kFLate as above)
+constexpr int32_t kCSegLeft = 0x100;    // gsequence via Genome_get_segment_left (minus strand)
+constexpr int32_t kCSegRc = 0x200;
+constexpr int32_t kCRSegLeft = 0x400;   // rev_gsequence via Genome_get_segment_left (plus strand)
+constexpr int32_t kCRSegRc = 0x800;
+constexpr int32_t kCSimd = 0x1000;      // SIMD-build semantics (triangle fills, uxc_kernel)
+
+// Dynprog_cdna_gap descriptor (dynprog_cdna.c:787).  The L fill runs rsequenceL forward against
+// gsequence, the R fill rev_rsequenceR backwards against rev_gsequence (the same genome interval).
+// Inside the engine's domain (rlengthL == rlengthR >= glength) the fills' and both bridges' bands
+// coincide: lband = rlength - glength + extraband_paired, uband = extraband_paired.
+struct DevCdnaProblem {
+  int32_t qbaseL;         // arena index of rsequenceL[0]
+  int32_t qbaseR;         // arena index of rev_rsequenceR[0] (the R piece's last character)
+  int32_t rlength;        // rlengthL = rlengthR
+  int32_t glength;
+  int32_t roffsetL;
+  int32_t rev_roffsetR;
+  int32_t goffset;
+  int32_t lband;
+  int32_t uband;
+  uint32_t chroffset;
+  uint32_t chrhigh;
+  uint32_t segpos, segbound;    // gsequence segment (see DevProblem.segpos)
+  uint32_t rsegpos, rsegbound;  // rev_gsequence segment
+  int32_t open;
+  int32_t extend;
+  int32_t mismatchtype;
+  int32_t flags;
+  int32_t genestrand;
+  int32_t dynprogindex;
+  int32_t pair_offset;
+  int64_t scratch_offset; // byte offset of the problem's region of the global scratch
+};
+
 }  // namespace gmapdp

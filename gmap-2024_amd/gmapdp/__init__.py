@@ -67,6 +67,19 @@ class GenomeResult(C.Structure):
                 ("right_prob", C.c_double)]
 
 
+class CdnaProblem(C.Structure):
+    _fields_ = [("qoffL", C.c_int32), ("qoffR", C.c_int32), ("rlengthL", C.c_int32), ("rlengthR", C.c_int32),
+                ("glength", C.c_int32), ("roffsetL", C.c_int32), ("rev_roffsetR", C.c_int32), ("goffset", C.c_int32),
+                ("chroffset", C.c_uint32), ("chrhigh", C.c_uint32), ("flags", C.c_int32), ("genestrand", C.c_int32),
+                ("extraband", C.c_int32), ("dynprogindex", C.c_int32), ("defect_rate", C.c_double)]
+
+
+class CdnaResult(C.Structure):
+    _fields_ = [("npairs", C.c_int32), ("pair_offset", C.c_int32), ("traceback_score", C.c_int32),
+                ("dynprogindex", C.c_int32), ("incompletep", C.c_int32), ("gap_index", C.c_int32),
+                ("gap_queryjump", C.c_int32), ("pad_", C.c_int32)]
+
+
 def _struct_dtype(S, fmt):
     return np.dtype({"names": [n for n, _ in S._fields_], "formats": fmt,
                      "offsets": [S.__dict__[n].offset for n, _ in S._fields_], "itemsize": C.sizeof(S)})
@@ -74,6 +87,8 @@ def _struct_dtype(S, fmt):
 
 GENOME_PROBLEM_DTYPE = _struct_dtype(GenomeProblem, ["<i4"] * 7 + ["<u4", "<u4"] + ["<i4"] * 7 + ["<f8", "<i8"])
 GENOME_RESULT_DTYPE = _struct_dtype(GenomeResult, ["<i4"] * 14 + ["<f8", "<f8"])
+CDNA_PROBLEM_DTYPE = _struct_dtype(CdnaProblem, ["<i4"] * 8 + ["<u4", "<u4"] + ["<i4"] * 4 + ["<f8"])
+CDNA_RESULT_DTYPE = _struct_dtype(CdnaResult, ["<i4"] * 8)
 
 PAIR_DTYPE = np.dtype([("querypos", "<i4"), ("genomepos", "<i4"), ("jump", "<i4"), ("cdna", "S1"),
                        ("comp", "S1"), ("genome", "S1"), ("genomealt", "S1")])
@@ -135,6 +150,9 @@ def load_library(path=LIB_PATH):
                                               C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
                                               C.c_size_t]),
         "gmapdp_genome_pair_capacity": (C.c_size_t, [C.c_void_p, C.c_int]),
+        "gmapdp_cdna_gap_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t,
+                                            C.c_void_p, C.c_void_p, C.c_size_t]),
+        "gmapdp_cdna_pair_capacity": (C.c_size_t, [C.c_void_p, C.c_int]),
         "gmapdp_genome_prob_entries": (C.c_size_t, [C.c_void_p, C.c_int]),
         "gmapdp_genome_splice_sites": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t]),
         "gmapdp_plan_create_all": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
@@ -363,6 +381,51 @@ class Engine:
         results, pairs = self.genome_gap_batch_raw(probs, qbuf, qucbuf, arena[:m])
         return decode_genome_results(results, pairs, [p["dynprogindex"] for p in calls])
 
+    # -- batched Dynprog_cdna_gap ---------------------------------------------
+    @staticmethod
+    def build_cdna_batch(calls):
+        """calls: dicts with the Dynprog_cdna_gap arguments (q, quc, qposL, qposR, rlengthL, rlengthR, glength,
+        roffsetL, rev_roffsetR, goffset, chroffset, chrhigh, watsonp, genestrand, jump_late_p, extraband,
+        defect_rate, dynprogindex); rsequenceL = q + qposL, rev_rsequenceR = q + qposR."""
+        calls = list(calls)
+        probs = np.zeros(len(calls), dtype=CDNA_PROBLEM_DTYPE)
+        qparts, qucparts, off = [], [], 0
+        for i, p in enumerate(calls):
+            probs[i]["qoffL"] = off + p["qposL"]
+            probs[i]["qoffR"] = off + p["qposR"]
+            for k in ("rlengthL", "rlengthR", "glength", "roffsetL", "rev_roffsetR", "goffset", "chroffset",
+                      "chrhigh", "genestrand", "extraband", "dynprogindex", "defect_rate"):
+                probs[i][k] = p[k]
+            probs[i]["flags"] = ((WATSON if p["watsonp"] else 0) | (JUMP_LATE if p["jump_late_p"] else 0) |
+                                 (SIMD if p.get("simd") else 0))
+            qparts.append(p["q"])
+            qucparts.append(p["quc"])
+            off += len(p["q"])
+        return probs, (b"".join(qparts) or b"\0"), (b"".join(qucparts) or b"\0")
+
+    def cdna_gap_batch(self, calls):
+        """Returns per call ((dynprogindex, traceback_score, incompletep), pairs-or-None) in the oracle's
+        format (the gap holder carries the queryjump)."""
+        calls = list(calls)
+        probs, qbuf, qucbuf = self.build_cdna_batch(calls)
+        n = len(probs)
+        results = np.zeros(n, dtype=CDNA_RESULT_DTYPE)
+        cap = self.lib.gmapdp_cdna_pair_capacity(probs.ctypes.data, n)
+        pairs = np.zeros(max(cap, 1), dtype=PAIR_DTYPE)
+        rc = self.lib.gmapdp_cdna_gap_batch(self.h, probs.ctypes.data, n, qbuf, qucbuf, len(qbuf),
+                                            results.ctypes.data, pairs.ctypes.data, cap)
+        self._check(rc, "gmapdp_cdna_gap_batch")
+        out = []
+        for i, res in enumerate(results):
+            scal = (int(res["dynprogindex"]), int(res["traceback_score"]), int(res["incompletep"]))
+            n_ = int(res["npairs"])
+            lst = decode_pairs(pairs, int(res["pair_offset"]), n_, calls[i]["dynprogindex"]) if n_ else None
+            if lst is not None and res["gap_index"] >= 0:
+                g = int(res["gap_index"])
+                lst[g] = (-1, -1, int(res["gap_queryjump"]), lst[g][3], 0, b" ", b" ", b" ", b" ", 1)
+            out.append((scal, lst))
+        return out
+
 
 def decode_genome_results(results, pairs, dynprogindices):
     base = decode_results(results, pairs, dynprogindices)
@@ -386,14 +449,17 @@ def decode_results(results, pairs, dynprogindices):
         if n == 0:
             out.append((scal, None))
             continue
-        dpi = dynprogindices[i]
-        seg = pairs[int(res["pair_offset"]):int(res["pair_offset"]) + n]
-        lst = []
-        for rec in seg:
-            if rec["querypos"] == -1 and rec["genomepos"] == -1:
-                lst.append((-1, -1, 0, int(rec["jump"]), 0, b" ", b" ", b" ", b" ", 1))
-            else:
-                lst.append((int(rec["querypos"]), int(rec["genomepos"]), 0, 0, dpi, rec["cdna"], rec["comp"],
-                            rec["genome"], rec["genomealt"], 0))
-        out.append((scal, lst))
+        out.append((scal, decode_pairs(pairs, int(res["pair_offset"]), n, dynprogindices[i])))
     return out
+
+
+def decode_pairs(pairs, offset, n, dpi):
+    """Pair records [offset, offset + n) as the oracle's Pair keys (gap holders: queryjump 0)."""
+    lst = []
+    for rec in pairs[offset:offset + n]:
+        if rec["querypos"] == -1 and rec["genomepos"] == -1:
+            lst.append((-1, -1, 0, int(rec["jump"]), 0, b" ", b" ", b" ", b" ", 1))
+        else:
+            lst.append((int(rec["querypos"]), int(rec["genomepos"]), 0, 0, dpi, rec["cdna"], rec["comp"],
+                        rec["genome"], rec["genomealt"], 0))
+    return lst

@@ -241,6 +241,53 @@ int gmapdp_genome_gap_batch (gmapdp_ctx *ctx, const gmapdp_genome_problem *probl
                              gmapdp_genome_result *results, gmapdp_pair *pairs, size_t pair_capacity);
 size_t gmapdp_genome_pair_capacity (const gmapdp_genome_problem *problems, int n);
 
+/* One Dynprog_cdna_gap call (dynprog_cdna.c:787 argument list): a cDNA insertion between two
+ * anchors.  rsequenceL / rsequence_ucL = qseq / qseq_uc + qoffL (the L piece's first character),
+ * rev_rsequenceR / rev_rsequence_ucR = qseq / qseq_uc + qoffR (the R piece's LAST character).  The
+ * SHORTGAP block pushed when the bridge leaves a 9 x 9 gap reads rsequenceL up to
+ * rev_roffsetR - roffsetL, so the arena must hold qseq[qoffL .. qoffL + rev_roffsetR - roffsetL].
+ * Penalties are CDNA_OPEN/CDNA_EXTEND (dynprog_cdna.c:32-38) whatever the mode.
+ * Domain: rlengthL == rlengthR >= glength, as stage3.c passes (both pieces queryjump' = genomejump +
+ * extramaterial_paired, stage3.c:9275); outside it the reference's bridge reads cells no fill wrote,
+ * and the engine rejects the batch with GMAPDP_EINVAL. */
+typedef struct {
+  int32_t qoffL;
+  int32_t qoffR;
+  int32_t rlengthL;
+  int32_t rlengthR;
+  int32_t glength;
+  int32_t roffsetL;
+  int32_t rev_roffsetR;
+  int32_t goffset;
+  uint32_t chroffset;
+  uint32_t chrhigh;
+  int32_t flags;          /* GMAPDP_WATSON | GMAPDP_JUMP_LATE | GMAPDP_SIMD */
+  int32_t genestrand;
+  int32_t extraband;      /* extraband_paired */
+  int32_t dynprogindex;
+  double defect_rate;
+} gmapdp_cdna_problem;
+
+/* Out-parameters of Dynprog_cdna_gap.  traceback_score is GMAPDP_UNSET where the reference leaves
+ * it unwritten (the glength <= 1 and size-guard NULL returns).  When the bridge leaves anything but
+ * a 9 x 9 block, the list carries a gap holder (Pairpool_push_gapholder, dynprog_cdna.c:1270) at
+ * pairs[gap_index] with jump = genomejump and incompletep = 1. */
+typedef struct {
+  int32_t npairs;          /* 0 <=> NULL List_T */
+  int32_t pair_offset;
+  int32_t traceback_score;
+  int32_t dynprogindex;
+  int32_t incompletep;
+  int32_t gap_index;       /* -1: no gap holder */
+  int32_t gap_queryjump;
+  int32_t pad_;
+} gmapdp_cdna_result;
+
+int gmapdp_cdna_gap_batch (gmapdp_ctx *ctx, const gmapdp_cdna_problem *problems, int n,
+                           const char *qseq, const char *qseq_uc, size_t qbytes,
+                           gmapdp_cdna_result *results, gmapdp_pair *pairs, size_t pair_capacity);
+size_t gmapdp_cdna_pair_capacity (const gmapdp_cdna_problem *problems, int n);
+
 /* Create a context on HIP device `device`.  mode = Mode_T (mode.h:5;
  * 0 = STANDARD).  user_* mirror Dynprog_single_setup. */
 int gmapdp_create (gmapdp_ctx **ctx, int device, int mode,

@@ -88,6 +88,26 @@ def test_genome_struct_layout():
     assert gmapdp.GENOME_RESULT_DTYPE.itemsize == 72
 
 
+def test_struct_layouts_match_the_c_header(tmp_path):
+    """The ctypes mirrors against sizeof/offsetof as a C compiler lays out include/gmapdp.h."""
+    import subprocess
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "gmapdp.h"\nint main(void) {\n'
+                   'printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(gmapdp_single_problem), sizeof(gmapdp_end_problem),\n'
+                   '  sizeof(gmapdp_genome_problem), sizeof(gmapdp_genome_result), sizeof(gmapdp_cdna_problem),\n'
+                   '  sizeof(gmapdp_cdna_result));\n'
+                   'printf("%zu %zu\\n", offsetof(gmapdp_cdna_problem, defect_rate), offsetof(gmapdp_cdna_result, gap_queryjump));\n'
+                   'return 0; }\n')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(os.path.dirname(HERE), "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
+    sizes = [int(x) for x in out]
+    assert sizes[:6] == [C.sizeof(gmapdp.SingleProblem), C.sizeof(gmapdp.EndProblem), C.sizeof(gmapdp.GenomeProblem),
+                         C.sizeof(gmapdp.GenomeResult), C.sizeof(gmapdp.CdnaProblem), C.sizeof(gmapdp.CdnaResult)]
+    assert sizes[6:] == [gmapdp.CdnaProblem.defect_rate.offset, gmapdp.CdnaResult.gap_queryjump.offset]
+    assert gmapdp.CDNA_PROBLEM_DTYPE.itemsize == sizes[4] and gmapdp.CDNA_RESULT_DTYPE.itemsize == sizes[5]
+
+
 def test_genome_splice_sites_match_oracle():
     """gmapdp_genome_splice_sites (host-only) lists the same Maxent_hr_*_prob calls as the oracle's
     restatement of dynprog_genome.c:2573-2660."""
