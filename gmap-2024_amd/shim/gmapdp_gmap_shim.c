@@ -5,17 +5,21 @@
  *
  *   -Wl,--wrap=Dynprog_init,--wrap=Dynprog_single_setup,--wrap=Dynprog_end_setup,
  *   -Wl,--wrap=Dynprog_genome_setup,--wrap=Dynprog_single_gap,--wrap=Dynprog_end5_gap,
- *   -Wl,--wrap=Dynprog_end3_gap,--wrap=Dynprog_genome_gap  -lgmapdp
+ *   -Wl,--wrap=Dynprog_end3_gap,--wrap=Dynprog_genome_gap,--wrap=Dynprog_cdna_gap  -lgmapdp
  *
- * so that every call GMAP's stage 3 makes to these functions (stage3.c:9510,
- * 9531, 10244-10600, ...) lands here with the reference's own signature
- * (dynprog_single.h:22, dynprog_end.h:25/47, dynprog_genome.h:24) and returns
+ * so that every call GMAP's stage 3 makes to these functions (stage3.c:9081,
+ * 9275, 9510, 9531, 10244-10600, ...) lands here with the reference's own signature
+ * (dynprog_single.h:22, dynprog_end.h:25/47, dynprog_genome.h:24, dynprog_cdna.h:12) and returns
  * the reference's List_T of Pair_T built in the caller's Pairpool
  * (Pairpool_push / Pairpool_push_gapholder, pairpool.c:180/375).  The setup
  * functions are wrapped only to learn Mode_T and the user gap penalties; the
  * reference's own setup still runs.  See INTEGRATION.md.
  *
- * Scope (the engine's, include/gmapdp.h): nosimd semantics; no alternate-
+ * Semantics follow the GMAP build the shim is compiled into: a SIMD build
+ * (HAVE_SSE2: gmap.sse42 / .avx2 / .avx512, dynprog_simd.c) gets GMAPDP_SIMD on
+ * every call, a nosimd build the Dynprog_standard semantics.
+ *
+ * Scope (the engine's, include/gmapdp.h): no alternate-
  * allele genome (genomealt must equal genome); Dynprog_T created with
  * gmap.c's defaults (max_rlength 660, max_glength 2000); homopolymer mode
  * off; no splicing IIT in Dynprog_genome_gap.  Anything else is refused with
@@ -45,6 +49,7 @@
 #include "dynprog_single.h"
 #include "dynprog_end.h"
 #include "dynprog_genome.h"
+#include "dynprog_cdna.h"
 
 #include "gmapdp.h"
 #include "gmapdp_dynprog.h"
@@ -62,6 +67,13 @@ extern void __real_Dynprog_genome_setup (bool novelsplicingp_in, IIT_T splicing_
                                          int *splicing_divint_crosstable_in, int donor_typeint_in,
                                          int acceptor_typeint_in, int user_open_in, int user_extend_in,
                                          bool user_dynprog_p_in);
+
+/* the semantics of the GMAP build this file is compiled into */
+#ifdef HAVE_SSE2
+#define SHIM_SIMD GMAPDP_SIMD
+#else
+#define SHIM_SIMD 0
+#endif
 
 static pthread_mutex_t shim_lock = PTHREAD_MUTEX_INITIALIZER;
 static gmapdp_ctx *shim_ctx = NULL;
@@ -141,7 +153,9 @@ shim_context (Genome_T genome, Genome_T genomealt, Dynprog_T dynprog) {
   return shim_ctx;
 }
 
-/* The engine's records in list order -> the reference's List_T (each push prepends). */
+/* The engine's records in list order -> the reference's List_T (each push prepends).  The gap
+   holder at gap_index carries gap_queryjump and, for introntype >= 0, the intron's type and
+   splice probabilities (Dynprog_genome_gap); other gap holders carry queryjump 0. */
 static List_T
 shim_list (const gmapdp_pair *pairs, int n, int dynprogindex, int gap_index, int gap_queryjump, int introntype,
            double donor_prob, double acceptor_prob, Pairpool_T pairpool) {
@@ -153,7 +167,7 @@ shim_list (const gmapdp_pair *pairs, int n, int dynprogindex, int gap_index, int
     if (p->querypos == -1 && p->genomepos == -1) {
       list = Pairpool_push_gapholder(list, pairpool, i == gap_index ? gap_queryjump : 0, p->jump,
                                      /*leftpair*/NULL, /*rightpair*/NULL, /*knownp*/false);
-      if (i == gap_index) {
+      if (i == gap_index && introntype >= 0) {
         gappair = (Pair_T) list->first;
         gappair->introntype = introntype;
         gappair->donor_prob = donor_prob;
@@ -189,7 +203,8 @@ __wrap_Dynprog_single_gap (int *dynprogindex, int *finalscore, int *nmatches, in
   p.goffset = offset2;
   p.chroffset = (uint32_t) chroffset;
   p.chrhigh = (uint32_t) chrhigh;
-  p.flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0) | (widebandp ? GMAPDP_WIDEBAND : 0);
+  p.flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0) | (widebandp ? GMAPDP_WIDEBAND : 0) |
+            SHIM_SIMD;
   p.genestrand = genestrand;
   p.extraband = extraband_single;
   p.defect_rate = defect_rate;
@@ -231,7 +246,7 @@ shim_end_gap (int end3p, int *dynprogindex, int *finalscore, int *nmatches, int 
   p.goffset = offset2;
   p.chroffset = (uint32_t) chroffset;
   p.chrhigh = (uint32_t) chrhigh;
-  p.flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0);
+  p.flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0) | SHIM_SIMD;
   p.genestrand = genestrand;
   p.extraband = extraband_end;
   p.end3p = end3p;
@@ -327,7 +342,7 @@ __wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_r
   p.chroffset = (uint32_t) chroffset;
   p.chrhigh = (uint32_t) chrhigh;
   p.flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0) | (halfp ? GMAPDP_HALFP : 0) |
-            (finalp ? GMAPDP_FINALP : 0);
+            (finalp ? GMAPDP_FINALP : 0) | SHIM_SIMD;
   p.cdna_direction = cdna_direction;
   p.genestrand = genestrand;
   p.extraband = extraband_paired;
@@ -374,5 +389,62 @@ __wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_r
   if (res.new_leftgenomepos != GMAPDP_UNSET) *new_leftgenomepos = res.new_leftgenomepos;
   if (res.new_rightgenomepos != GMAPDP_UNSET) *new_rightgenomepos = res.new_rightgenomepos;
   if (res.exonhead != GMAPDP_UNSET) *exonhead = res.exonhead;
+  return list;
+}
+
+List_T
+__wrap_Dynprog_cdna_gap (int *dynprogindex, int *traceback_score, bool *incompletep, Dynprog_T dynprogL,
+                         Dynprog_T dynprogR, char *rsequenceL, char *rsequence_ucL, char *rev_rsequenceR,
+                         char *rev_rsequence_ucR, int rlengthL, int rlengthR, int glength, int roffsetL,
+                         int rev_roffsetR, int goffset, Univcoord_T chroffset, Univcoord_T chrhigh, bool watsonp,
+                         int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
+                         Pairpool_T pairpool, int extraband_paired, double defect_rate) {
+  gmapdp_cdna_problem p;
+  gmapdp_cdna_result res;
+  gmapdp_pair *pairs;
+  size_t cap;
+  List_T list;
+  const char *lo, *hi, *lo_uc;
+  long span;
+  /* one arena holds both query pieces (stage3.c passes two pointers into the same query,
+     :9275-9285) and the stretch between them, which the SHORTGAP block reads */
+  span = (long) rev_roffsetR - roffsetL + 1;
+  if (span < rlengthL) span = rlengthL;
+  lo = rsequenceL;
+  if (rlengthR > 0 && rev_rsequenceR - (rlengthR - 1) < lo) lo = rev_rsequenceR - (rlengthR - 1);
+  hi = rsequenceL + span;
+  if (rev_rsequenceR + 1 > hi) hi = rev_rsequenceR + 1;
+  lo_uc = rsequence_ucL - (rsequenceL - lo);
+  if (rev_rsequence_ucR - lo_uc != rev_rsequenceR - lo) shim_refuse("query pieces from two different buffers");
+  pthread_mutex_lock(&shim_lock);
+  shim_context(genome, genomealt, dynprogL);
+  shim_context(genome, genomealt, dynprogR);
+  memset(&p, 0, sizeof(p));
+  p.qoffL = (int32_t) (rsequenceL - lo);
+  p.qoffR = (int32_t) (rev_rsequenceR - lo);
+  p.rlengthL = rlengthL;
+  p.rlengthR = rlengthR;
+  p.glength = glength;
+  p.roffsetL = roffsetL;
+  p.rev_roffsetR = rev_roffsetR;
+  p.goffset = goffset;
+  p.chroffset = (uint32_t) chroffset;
+  p.chrhigh = (uint32_t) chrhigh;
+  p.flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0) | SHIM_SIMD;
+  p.genestrand = genestrand;
+  p.extraband = extraband_paired;
+  p.dynprogindex = *dynprogindex;
+  p.defect_rate = defect_rate;
+  cap = gmapdp_cdna_pair_capacity(&p, 1);
+  pairs = (gmapdp_pair *) malloc((cap ? cap : 1) * sizeof(gmapdp_pair));
+  shim_check(gmapdp_cdna_gap_batch(shim_ctx, &p, 1, lo, lo_uc, (size_t) (hi - lo), &res, pairs, cap),
+             "gmapdp_cdna_gap_batch");
+  pthread_mutex_unlock(&shim_lock);
+  list = shim_list(pairs + res.pair_offset, res.npairs, p.dynprogindex, res.gap_index, res.gap_queryjump, -1, 0.0,
+                   0.0, pairpool);
+  free(pairs);
+  *dynprogindex = res.dynprogindex;
+  if (res.traceback_score != GMAPDP_UNSET) *traceback_score = res.traceback_score;
+  if (res.incompletep) *incompletep = true;
   return list;
 }

@@ -90,14 +90,15 @@ $(foreach v,$(VARIANTS),$(eval $(call variant_rules,$(v))))
 SHIM_SRC   := ../gmap-2024_amd/shim/gmapdp_gmap_shim.c
 GMAPDP_LIB := ../gmap-2024_amd/lib
 
-all: $(foreach v,$(VARIANTS),$(OUT)/librefdp_$(v).so) $(if $(wildcard $(GMAPDP_LIB)/libgmapdp.so),$(OUT)/librefdp_gpushim.so)
+all: $(foreach v,$(VARIANTS),$(OUT)/librefdp_$(v).so) \
+     $(if $(wildcard $(GMAPDP_LIB)/libgmapdp.so),$(OUT)/librefdp_gpushim.so $(OUT)/librefdp_gpushim_avx2.so)
 
 # The drop-in check: the same nosimd reference objects, with Dynprog_init / _*_setup /
 # _single_gap / _end5_gap / _end3_gap / _genome_gap routed by `ld --wrap` to the engine's
 # GMAP shim (gmap-2024_amd/shim, compiled against the reference's headers exactly as a GMAP
 # build would) and libgmapdp.so.  Tests call it through the same refh_* entry points.
 WRAPPED    := Dynprog_init Dynprog_single_setup Dynprog_end_setup Dynprog_genome_setup \
-              Dynprog_single_gap Dynprog_end5_gap Dynprog_end3_gap Dynprog_genome_gap
+              Dynprog_single_gap Dynprog_end5_gap Dynprog_end3_gap Dynprog_genome_gap Dynprog_cdna_gap
 
 $(OUT)/gpushim/gmapdp_gmap_shim.o: $(SHIM_SRC) ../include/gmapdp.h
 	@mkdir -p $(dir $@)
@@ -105,6 +106,18 @@ $(OUT)/gpushim/gmapdp_gmap_shim.o: $(SHIM_SRC) ../include/gmapdp.h
 
 $(OUT)/librefdp_gpushim.so: $(LIBOBJS_nosimd) $(OUT)/nosimd/refharness.o $(OUT)/gpushim/gmapdp_gmap_shim.o \
                             $(GMAPDP_LIB)/libgmapdp.so
+	$(CC) -shared -pthread -Wl,--gc-sections -Wl,--version-script=refharness.map \
+	  $(foreach w,$(WRAPPED),-Wl,--wrap=$(w)) -o $@ $(filter %.o,$^) \
+	  -L$(GMAPDP_LIB) -lgmapdp -Wl,-rpath,'$$ORIGIN/../../gmap-2024_amd/lib' -lz -lm
+
+# The same drop-in inside a SIMD build: the AVX2 objects (alloca variant, see FLAGS_avx2a) and the
+# shim compiled with the AVX2 build's defines, so every call carries GMAPDP_SIMD.
+$(OUT)/gpushim_avx2/gmapdp_gmap_shim.o: $(SHIM_SRC) ../include/gmapdp.h
+	@mkdir -p $(dir $@)
+	$(CC) $(BASEFLAGS) -DHAVE_CONFIG_H $(FLAGS_avx2a) -I../include -c $< -o $@
+
+$(OUT)/librefdp_gpushim_avx2.so: $(LIBOBJS_avx2a) $(OUT)/avx2a/refharness.o $(OUT)/gpushim_avx2/gmapdp_gmap_shim.o \
+                                 $(GMAPDP_LIB)/libgmapdp.so
 	$(CC) -shared -pthread -Wl,--gc-sections -Wl,--version-script=refharness.map \
 	  $(foreach w,$(WRAPPED),-Wl,--wrap=$(w)) -o $@ $(filter %.o,$^) \
 	  -L$(GMAPDP_LIB) -lgmapdp -Wl,-rpath,'$$ORIGIN/../../gmap-2024_amd/lib' -lz -lm

@@ -16,7 +16,7 @@ import random
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_SO = os.path.join(ROOT, "oracle", "libgmapdp_oracle.so")
-REF_SO = {v: os.path.join(ROOT, "oracle", "_ref", "librefdp_%s.so" % v) for v in ("nosimd", "avx2", "nosimda", "avx2a", "gpushim")}
+REF_SO = {v: os.path.join(ROOT, "oracle", "_ref", "librefdp_%s.so" % v) for v in ("nosimd", "avx2", "nosimda", "avx2a", "gpushim", "gpushim_avx2")}
 
 
 class Pair(C.Structure):

@@ -1,14 +1,15 @@
 """The GMAP drop-in, end to end: the reference's own objects with Dynprog_single_gap,
-Dynprog_end5/3_gap and Dynprog_genome_gap routed (ld --wrap) through
-gmap-2024_amd/shim/gmapdp_gmap_shim.c to the GPU engine (oracle/_ref/librefdp_gpushim.so),
-against the same objects unmodified.  Pair_T lists (every field the call sets) and
-out-parameters must be identical."""
+Dynprog_end5/3_gap, Dynprog_genome_gap and Dynprog_cdna_gap routed (ld --wrap) through
+gmap-2024_amd/shim/gmapdp_gmap_shim.c to the GPU engine, against the same objects unmodified:
+the nosimd build (oracle/_ref/librefdp_gpushim.so) and the AVX2 build
+(librefdp_gpushim_avx2.so, where the shim passes GMAPDP_SIMD).  Pair_T lists (every field the
+call sets) and out-parameters must be identical."""
 import random
 
 import pytest
 
-from dpbind import (GG_FLAG_HALF, Ref, call_end, call_single, edge_single_gap_problem, end_gap_problem,
-                    genome_gap_problem, random_genome, ref_available, single_gap_problem)
+from dpbind import (GG_FLAG_HALF, Ref, call_end, call_single, cdna_gap_problem, edge_single_gap_problem,
+                    end_gap_problem, genome_gap_problem, random_genome, ref_available, single_gap_problem)
 
 pytestmark = [pytest.mark.gpu,
               pytest.mark.skipif(not (ref_available("gpushim") and ref_available("nosimda")),
@@ -48,4 +49,47 @@ def test_shim_genome_gaps(impls):
         r.set_genome(g)
     bad = [i for i, p in enumerate(probs)
            if shim.genome_gap(p) != (refa if p["flags"] & GG_FLAG_HALF else ref).genome_gap(p)]
+    assert bad == []
+
+
+def test_shim_cdna_gaps(impls):
+    ref, _, shim = impls
+    rng = random.Random(808)
+    g = random_genome(rng, 30000)
+    ref.set_genome(g)
+    shim.set_genome(g)
+    probs = [cdna_gap_problem(rng, g, edge=(i % 4 == 0)) for i in range(300)]
+    bad = [i for i, p in enumerate(probs) if shim.cdna_gap(p) != ref.cdna_gap(p)]
+    assert bad == []
+
+
+@pytest.mark.skipif(not (ref_available("gpushim_avx2") and ref_available("avx2a")),
+                    reason="AVX2 shim harness did not travel")
+def test_shim_simd_build_all_entry_points():
+    """Inside an AVX2 GMAP build the drop-in reproduces gmap.avx2 (the shim passes GMAPDP_SIMD)."""
+    ref, shim = Ref("avx2a"), Ref("gpushim_avx2")
+    rng = random.Random(909)
+    g = bytearray(random_genome(rng, 60000))
+    gprobs = [genome_gap_problem(rng, g, edge=(i % 5 == 0)) for i in range(300)]
+    g = bytes(g)
+    ref.set_genome(g)
+    shim.set_genome(g)
+    bad = []
+    for i in range(400):
+        p = single_gap_problem(rng, g) if i % 3 else edge_single_gap_problem(rng, g)
+        if call_single(shim, p) != call_single(ref, p):
+            bad.append(("single", i))
+    for i in range(400):
+        p = end_gap_problem(rng, g, edge=(i % 4 == 0))
+        if p["endalign"] != 2 and p["rlength"] > p["glength"] + 1:
+            continue  # outside the engine's SIMD end-gap domain (the reference reads unset cells)
+        if call_end(shim, p) != call_end(ref, p):
+            bad.append(("end", i))
+    for i, p in enumerate(gprobs):
+        if shim.genome_gap(p) != ref.genome_gap(p):
+            bad.append(("genome", i))
+    for i in range(200):
+        p = cdna_gap_problem(rng, g, edge=(i % 4 == 0))
+        if shim.cdna_gap(p) != ref.cdna_gap(p):
+            bad.append(("cdna", i))
     assert bad == []
