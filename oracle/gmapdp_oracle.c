@@ -199,6 +199,13 @@ orc_set_genome (const char *genome, unsigned int length) {
   return 0;
 }
 
+/* The genome bytes orc_set_genome holds (stage2_oracle.c reads them as .genomecomp codes). */
+const char *
+orc_genome_seq (unsigned int *length) {
+  *length = g_genomelength;
+  return g_genome;
+}
+
 /* ---------------------------------------------------------------------------
  * Genome access: get_genomic_nt (dynprog_single.c:116, pairpool.c) and
  * Genome_get_segment_right/left (genome.c:11023/11079).  Univcoord_T is the

@@ -103,6 +103,18 @@ int orc_cdna_gap (const char *qbuf, const char *qucbuf, int qposL, int qposR, in
                   unsigned int chrhigh, int watsonp, int genestrand, int jump_late_p, int extraband_paired,
                   double defect_rate, int dynprogindex, int *scalars, OrcPair *out, int max_pairs);
 
+/* The genome set by orc_set_genome. */
+const char *orc_genome_seq (unsigned int *length);
+
+/* Stage-2 seeding (stage2_oracle.c): Oligoindex_hr_tally + Oligoindex_get_mappings as
+   Stage2_compute runs them for GMAP; same arguments and outputs as refh_oligo_mappings
+   (oracle/refharness.c).  Returns the positions written, -1 when a capacity is too small, -3 for
+   querylength <= 8 (outside the reference's defined behaviour), -4 for a diagonal past the
+   genomicdiag array (the reference asserts). */
+int orc_oligo_mappings (const char *queryuc, int querylength, unsigned int chrstart, unsigned int chrend,
+                        unsigned int chroffset, unsigned int chrhigh, int plusp, int minor, int *npositions,
+                        unsigned int *positions, int pos_cap, int *scalars, int *diags, int diag_cap);
+
 #ifdef __cplusplus
 }
 #endif

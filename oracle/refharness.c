@@ -15,6 +15,8 @@
  *   Dynprog_end3_gap        dynprog_end.c:1924
  *   Genome_from_sequence    genome.c:307
  *   Pairpool_new/reset      pairpool.c
+ *   Oligoindex_hr_setup / _array_new_major / _minor / _hr_tally / _get_mappings / _untally
+ *                           oligoindex_hr.c:8672/8808/33849/34127/33994 (stage-2 seeding)
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -35,6 +37,9 @@
 #include "dynprog_genome.h"
 #include "dynprog_cdna.h"
 #include "maxent_hr.h"
+#include "oligoindex_hr.h"
+#include "diag.h"
+#include "diagpool.h"
 
 /* Flat pair record (matches oracle/gmapdp_oracle.h RefPair / GmapdpPair
  * semantics: one record per Pair_T in list order). */
@@ -451,4 +456,79 @@ refh_use8p_size (int *out4) {
   int i;
   for (i = 0; i < 4; i++) out4[i] = use8p_size[i];
   return 0;
+}
+
+
+/* Stage-2 seeding as GMAP's Stage2_compute runs it (stage2.c:6413-6501, one oligoindex source):
+   Oligoindex_hr_tally (oligoindex_hr.c:33849) over the genomic window, then
+   Oligoindex_get_mappings (:34127) with coveredp all false.  major: the 8-mer index with
+   diag_lookback 120 / suffnconsecutive 20 (Oligoindex_array_new_major, :8606-8610), else the
+   minor one (60 / 10).  Outputs: npositions[querylength] (0 where the query has no full 8-mer),
+   positions: the mapping list of every querypos with npositions > 0, concatenated in querypos
+   order; scalars = {totalpositions, maxnconsecutive, oned_matrix_p, ndiagonals}; diags: per
+   diagonal in list order {diagonal, querystart, queryend, nconsecutive}.  Returns the number of
+   positions written, -1 if pos_cap / diag_cap is too small. */
+static Oligoindex_array_T oligo_major = NULL, oligo_minor = NULL;
+static Diagpool_T diagpool = NULL;
+
+int
+refh_oligo_mappings (const char *queryuc, int querylength, unsigned int chrstart, unsigned int chrend,
+                     unsigned int chroffset, unsigned int chrhigh, int plusp, int minor, int *npositions,
+                     unsigned int *positions, int pos_cap, int *scalars, int *diags, int diag_cap) {
+  Oligoindex_array_T array;
+  Oligoindex_T oligoindex;
+  Chrpos_T **mappings;
+  bool *coveredp, oned_matrix_p = false;
+  int totalpositions = 0, maxnconsecutive = 0, q, k, n = 0, nd = 0;
+  List_T diagonals = NULL, p;
+  char *quc;
+  if (oligo_major == NULL) {
+    Oligoindex_hr_setup(STANDARD);
+    oligo_major = Oligoindex_array_new_major(100000, 1000000);  /* gmap.c:113-114, 4739-4740 */
+    oligo_minor = Oligoindex_array_new_minor(100000, 1000000);
+    diagpool = Diagpool_new();
+  }
+  array = minor ? oligo_minor : oligo_major;
+  oligoindex = Oligoindex_array_elt(array, 0);
+  quc = (char *) malloc(querylength + 1);
+  memcpy(quc, queryuc, querylength);
+  quc[querylength] = '\0';
+  coveredp = (bool *) calloc(querylength + 1, sizeof(bool));
+  mappings = (Chrpos_T **) calloc(querylength + 1, sizeof(Chrpos_T *));
+  memset(npositions, 0, querylength * sizeof(int));
+  Diagpool_reset(diagpool);
+  if (plusp) {
+    Oligoindex_hr_tally(oligoindex, (Univcoord_T) chroffset + chrstart, (Univcoord_T) chroffset + chrend, true,
+                        quc, 0, querylength, chrstart, genome, 0);
+  } else {
+    Oligoindex_hr_tally(oligoindex, (Univcoord_T) chroffset + chrstart, (Univcoord_T) chroffset + chrend + 1, false,
+                        quc, 0, querylength, (chrhigh - chroffset) - chrend, genome, 0);
+  }
+  diagonals = Oligoindex_get_mappings(diagonals, coveredp, mappings, npositions, &totalpositions, &oned_matrix_p,
+                                      &maxnconsecutive, array, oligoindex, quc, 0, querylength, querylength,
+                                      chrstart, chrend, chroffset, chrhigh, plusp ? true : false, diagpool);
+  for (q = 0; q < querylength && n >= 0; q++) {
+    if (npositions[q] <= 0) continue;
+    if (n + npositions[q] > pos_cap) { n = -1; break; }
+    for (k = 0; k < npositions[q]; k++) positions[n++] = mappings[q][k];
+  }
+  for (p = diagonals; p != NULL; p = List_next(p)) {
+    Diag_T d = (Diag_T) List_head(p);
+    if (nd < diag_cap) {
+      diags[4 * nd + 0] = (int) Diag_diagonal(d);
+      diags[4 * nd + 1] = Diag_querystart(d);
+      diags[4 * nd + 2] = Diag_queryend(d);
+      diags[4 * nd + 3] = Diag_nconsecutive(d);
+    }
+    nd++;
+  }
+  scalars[0] = totalpositions;
+  scalars[1] = maxnconsecutive;
+  scalars[2] = oned_matrix_p ? 1 : 0;
+  scalars[3] = nd;
+  Oligoindex_untally(oligoindex);
+  free(mappings);
+  free(coveredp);
+  free(quc);
+  return nd > diag_cap ? -1 : n;
 }

@@ -590,3 +590,86 @@ def cdna_gap_problem(rng, genome: bytes, edge=False):
                 chrhigh=chrhigh, watsonp=int(watsonp), genestrand=0, jump_late_p=rng.randint(0, 1),
                 extraband=rng.choice([14, 14, 3, 6]), defect_rate=rng.choice([0.001, 0.005, 0.02, 0.05]),
                 dynprogindex=rng.choice([1, 5, -1, -7]))
+
+
+# ---------------------------------------------------------------------------
+# Stage-2 seeding: Oligoindex_hr_tally + Oligoindex_get_mappings (oligoindex_hr.c:33849/34127)
+# ---------------------------------------------------------------------------
+_OM_ARGS = [C.c_char_p, C.c_int, C.c_uint, C.c_uint, C.c_uint, C.c_uint, C.c_int, C.c_int]
+
+
+def _oligo_mappings(self, p):
+    """(scalars (totalpositions, maxnconsecutive, oned_matrix_p, ndiagonals), npositions list,
+    positions list, diagonals list of (diagonal, querystart, queryend, nconsecutive)); None for
+    everything but the status when the implementation reports the call outside its domain."""
+    f = getattr(self.lib, self.prefix + "oligo_mappings")
+    if not getattr(self, "_om_ready", False):
+        f.argtypes = _OM_ARGS + [C.POINTER(C.c_int), C.POINTER(C.c_uint), C.c_int, C.POINTER(C.c_int),
+                                 C.POINTER(C.c_int), C.c_int]
+        f.restype = C.c_int
+        self._om_cap = 1 << 21
+        self._om_pos = (C.c_uint * self._om_cap)()
+        self._om_dg = (C.c_int * (4 * 65536))()
+        self._om_sc = (C.c_int * 4)()
+        self._om_ready = True
+    n = len(p["quc"])
+    npos = (C.c_int * max(n, 1))()
+    r = f(p["quc"], n, C.c_uint(p["chrstart"]), C.c_uint(p["chrend"]), C.c_uint(p["chroffset"]),
+          C.c_uint(p["chrhigh"]), int(p["plusp"]), int(p.get("minor", 0)), npos, self._om_pos, self._om_cap,
+          self._om_sc, self._om_dg, 65536)
+    if r < 0:
+        return (r,)
+    sc = tuple(self._om_sc)
+    return sc, list(npos[:n]), list(self._om_pos[:r]), [tuple(self._om_dg[4 * i:4 * i + 4]) for i in range(sc[3])]
+
+
+Ref.oligo_mappings = _oligo_mappings
+Oracle.oligo_mappings = _oligo_mappings
+
+
+def oligo_problem(rng, genome: bytes, edge=False):
+    """One Stage2_compute-shaped seeding call: a 2-kb-style cDNA (exons cut from the genome on one
+    strand, substitutions, an occasional N) against the genomic window [chrstart, chrend) that
+    spans it, plus/minus strand, with chromosome bounds inside the genome."""
+    chroffset = rng.choice([0, 0, 1000])
+    chrhigh = len(genome) - rng.choice([0, 0, 1000])
+    chrlen = chrhigh - chroffset
+    nex = rng.randint(1, 6)
+    exlen = [rng.randint(30, 500) for _ in range(nex)]
+    introns = [rng.randint(60, 6000) for _ in range(nex - 1)]
+    span = sum(exlen) + sum(introns)
+    if span + 400 >= chrlen:
+        introns = [60] * (nex - 1)
+        span = sum(exlen) + sum(introns)
+    s = rng.randint(200, max(200, chrlen - span - 200))
+    plusp = rng.random() < 0.5
+    parts, pos = [], s
+    for e in range(nex):
+        parts.append(genome[chroffset + pos:chroffset + pos + exlen[e]])
+        if e < nex - 1:
+            pos += exlen[e] + introns[e]
+    q = bytearray(b"".join(parts))
+    for i in range(len(q)):
+        u = rng.random()
+        if u < 0.02:
+            q[i] = rng.choice(b"ACGT")
+        elif u < 0.0025 + 0.02 and rng.random() < 0.1:
+            q[i] = ord("N")
+    chrstart = max(0, s - rng.randint(0, 300))
+    chrend = min(chrlen - 1, s + span + rng.randint(0, 300))
+    if not plusp:
+        # the minus-strand query is the reverse complement; the window is the same interval
+        comp = bytes.maketrans(b"ACGTN", b"TGCAN")
+        q = bytearray(bytes(q).translate(comp)[::-1])
+    if edge:
+        k = rng.randint(0, 3)
+        if k == 0:
+            q = q[:rng.randint(9, 20)]
+        elif k == 1:
+            chrend = chrstart + rng.randint(0, 9)
+        elif k == 2:
+            q = bytearray(b"A" * rng.randint(9, 400)) + q  # poly-A: counts past 256 in A-rich windows
+        else:
+            chrstart, chrend = 0, min(chrlen - 1, chrstart + rng.randint(1000, 40000))
+    return dict(quc=bytes(q), chrstart=chrstart, chrend=chrend, chroffset=chroffset, chrhigh=chrhigh,
+                plusp=int(plusp), minor=int(rng.random() < 0.3))

@@ -25,6 +25,9 @@ and the reference's outputs.
                          from the reference's AVX2 objects called on zeroed Dynprog_T arenas, on
                          problems inside the domain where that build is defined (see
                          simd_domain below); halfp genome gaps from the --enable-alloca AVX2 build
+  oligo_golden.npz       stage-2 seeding: Oligoindex_hr_tally + Oligoindex_get_mappings
+                         (oligoindex_hr.c:33849/34127) as Stage2_compute runs them for GMAP
+                         (python tests/golden/make_golden.py oligo)
 """
 import os
 import random
@@ -35,8 +38,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 from dpbind import (GG_FLAG_HALF, Oracle, Ref, call_end, call_single, cdna_gap_problem,  # noqa: E402
-                    edge_single_gap_problem, end_gap_problem, genome_gap_problem, random_genome,
-                    single_gap_problem, splice_probs)
+                    edge_single_gap_problem, end_gap_problem, genome_gap_problem, oligo_problem,
+                    random_genome, single_gap_problem, splice_probs)
 
 SINGLE_PARAMS = ["rlength", "glength", "roffset", "goffset", "chroffset", "chrhigh", "watsonp", "genestrand",
                  "jump_late_p", "extraband", "widebandp", "dynprogindex"]
@@ -226,10 +229,66 @@ def main():
     print("wrote %s: %d problems" % (out, len(probs)))
 
 
+OLIGO_PARAMS = ["chrstart", "chrend", "chroffset", "chrhigh", "plusp", "minor"]
+
+
+def oligo_problems(seed=2028, n_typical=300, n_edge=100, genome_len=200000):
+    rng = random.Random(seed)
+    g = bytearray(random_genome(rng, genome_len))
+    g[90000:91500] = b"A" * 1500  # an A-rich stretch: 8-mer counts past 256 (Count_T wraps)
+    g = bytes(g)
+    probs = [oligo_problem(rng, g) for _ in range(n_typical)]
+    probs += [oligo_problem(rng, g, edge=True) for _ in range(n_edge)]
+    return g, probs
+
+
+def main_oligo():
+    g, probs = oligo_problems()
+    ref = Ref("nosimd")
+    ref.set_genome(g)
+    outs = [ref.oligo_mappings(p) for p in probs]
+    assert all(len(o) == 4 for o in outs)
+    d = dict(genome=np.frombuffer(g, dtype=np.uint8),
+             params=np.array([[p[k] for k in OLIGO_PARAMS] for p in probs], dtype=np.int64),
+             param_names=np.array(OLIGO_PARAMS), qlen=np.array([len(p["quc"]) for p in probs], dtype=np.int32),
+             qucbuf=np.frombuffer(b"".join(p["quc"] for p in probs), dtype=np.uint8),
+             scalars=np.array([o[0] for o in outs], dtype=np.int32),
+             npositions=np.array([x for o in outs for x in o[1]], dtype=np.int32),
+             npos_total=np.array([len(o[2]) for o in outs], dtype=np.int32),
+             positions=np.array([x for o in outs for x in o[2]], dtype=np.uint32),
+             diags=np.array([x for o in outs for d_ in o[3] for x in d_], dtype=np.int32))
+    out = os.path.join(HERE, "oligo_golden.npz")
+    np.savez_compressed(out, **d)
+    print("wrote %s: %d problems" % (out, len(probs)))
+
+
+def load_oligo(path):
+    """(genome bytes, [problem dicts], [(scalars, npositions, positions, diagonals)])."""
+    z = np.load(path, allow_pickle=False)
+    names = [str(x) for x in z["param_names"]]
+    qoff = np.concatenate([[0], np.cumsum(z["qlen"])])
+    poff = np.concatenate([[0], np.cumsum(z["npos_total"])])
+    qub = z["qucbuf"].tobytes()
+    probs, outs, doff = [], [], 0
+    for i, row in enumerate(z["params"]):
+        p = {k: int(v) for k, v in zip(names, row)}
+        p["quc"] = qub[qoff[i]:qoff[i + 1]]
+        probs.append(p)
+        sc = tuple(int(x) for x in z["scalars"][i])
+        nd = sc[3]
+        dg = [tuple(int(x) for x in z["diags"][doff + 4 * k:doff + 4 * k + 4]) for k in range(nd)]
+        doff += 4 * nd
+        outs.append((sc, [int(x) for x in z["npositions"][qoff[i]:qoff[i + 1]]],
+                     [int(x) for x in z["positions"][poff[i]:poff[i + 1]]], dg))
+    return z["genome"].tobytes(), probs, outs
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "simd":
         main_simd()
     elif len(sys.argv) > 1 and sys.argv[1] == "cdna":
         main_cdna()
+    elif len(sys.argv) > 1 and sys.argv[1] == "oligo":
+        main_oligo()
     else:
         main()

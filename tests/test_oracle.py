@@ -350,3 +350,45 @@ def test_oracle_cdna_gap_vs_reference_random():
             p = cdna_gap_problem(rng, g, edge=(i % 4 == 0))
             a, b = ref.cdna_gap(p), orc.cdna_gap(p)
             assert a == b, (variant, i, {k: v for k, v in p.items() if k not in ("q", "quc")}, a[0], b[0])
+
+
+# ---------------------------------------------------------------------------
+# Stage-2 seeding: Oligoindex_hr_tally + Oligoindex_get_mappings (oligoindex_hr.c:33849/34127)
+# ---------------------------------------------------------------------------
+def _load_oligo_golden():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(HERE, "golden", "make_golden.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m.load_oligo(os.path.join(HERE, "golden", "oligo_golden.npz"))
+
+
+def test_oracle_oligo_mappings_match_golden():
+    g, probs, exp = _load_oligo_golden()
+    orc = Oracle()
+    orc.set_genome(g)
+    bad = [i for i, p in enumerate(probs) if orc.oligo_mappings(p) != exp[i]]
+    assert bad == [], "oracle differs on %d problems (first %s)" % (len(bad), bad[:5])
+    # both strands, both oligoindex arrays, windows without diagonals, and 8-mer counts wrapping
+    # past Count_T's 255 (the A-rich stretch) are all covered
+    assert {p["plusp"] for p in probs} == {0, 1} and {p["minor"] for p in probs} == {0, 1}
+    assert any(e[0][3] == 0 for e in exp) and sum(1 for e in exp if e[0][3] > 1) > 50
+    assert any(max(e[1]) >= 200 for e in exp if e[1])
+
+
+@pytest.mark.skipif(not ref_available("avx2"), reason="reference objects not built")
+def test_oracle_oligo_mappings_vs_reference_random():
+    from dpbind import oligo_problem
+    rng = random.Random(92)
+    g = bytearray(random_genome(rng, 150000))
+    g[70000:71000] = b"A" * 1000
+    g = bytes(g)
+    orc = Oracle()
+    orc.set_genome(g)
+    for variant in ("nosimd", "avx2"):
+        ref = Ref(variant)
+        ref.set_genome(g)
+        for i in range(120):
+            p = oligo_problem(rng, g, edge=(i % 4 == 0))
+            a, b = ref.oligo_mappings(p), orc.oligo_mappings(p)
+            assert a == b, (variant, i, {k: v for k, v in p.items() if k != "quc"})
