@@ -67,6 +67,11 @@ hipError_t launch_cg(bool simd, int RB, int nproblems, size_t lds, hipStream_t s
                      const int* order, unsigned char* gscratch, const uint32_t* blocks, uint64_t nwords,
                      const char* qseq, const char* qseq_uc, const int8_t* sctab, const uint8_t* constab,
                      gmapdp_cdna_result* results, gmapdp_pair* pairs);
+size_t lds_bytes_oi(int umax);
+size_t scratch_bytes_oi(int querylength, uint32_t genomiclength);
+hipError_t launch_oi(int nproblems, size_t lds, hipStream_t stream, const DevOligoProblem* probs,
+                     const uint32_t* blocks, const char* quc, unsigned char* scratch, gmapdp_oligo_result* results,
+                     int32_t* npos, int32_t* map, uint32_t* table, int32_t* diags);
 static const int kUse8pSize[4] = {41, 63, 127, 24};  // use8p_size (dynprog.c:1022-1025)
 
 // ---------------------------------------------------------------------------
@@ -209,6 +214,7 @@ struct gmapdp_ctx {
   DevBuf probs, order, qseq, qseq_uc, results, pairs, gdirs;
   DevBuf gprobs, gorder, sprob, gresults;
   DevBuf cprobs, corder, cresults, cscratch;  // Dynprog_cdna_gap batches
+  DevBuf oprobs, oresults, oscratch, onpos, omap, otable, odiag;  // stage-2 seeding batches
   std::string err;
 };
 
@@ -1503,5 +1509,171 @@ void gmapdp_plan_destroy(gmapdp_plan* plan) {
 }
 
 void* gmapdp_stream(gmapdp_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Stage-2 seeding: Oligoindex_hr_tally + Oligoindex_get_mappings as
+// Stage2_compute calls them for GMAP (stage2.c:6480-6495).  Synchronous batch path.
+// ---------------------------------------------------------------------------
+static const int kOligoMaxDistinct = 16384;
+
+// 8-mer starts the tally visits (count_positions_fwd/rev_std, oligoindex_hr.c:19268-19281)
+static uint64_t oligo_window(const gmapdp_oligo_problem& p) {
+  const uint64_t left = (uint64_t)p.chroffset + p.chrstart;
+  uint64_t lpl = (uint64_t)p.chroffset + p.chrend + (p.plusp ? 0 : 1);
+  lpl = lpl < 8 ? 0 : lpl - 8;
+  return lpl > left ? lpl - left + 1 : 0;
+}
+static size_t oligo_table_cap(const gmapdp_oligo_problem& p) {
+  if (p.querylength <= 8) return 0;
+  return (size_t)std::min<uint64_t>(oligo_window(p), 255ull * (uint64_t)(p.querylength - 7));
+}
+// a good diagonal takes suffnconsecutive + 1 >= 11 hits, each query position at most 255
+static size_t oligo_diag_cap(const gmapdp_oligo_problem& p) {
+  if (p.querylength <= 8) return 0;
+  return (size_t)(p.querylength - 7) * 24 + 1;
+}
+// distinct 8-mers of the query, as Oligoindex_set_inquery marks them (:33490-33515)
+static int oligo_distinct(const char* q, int qlen, std::vector<uint32_t>& bm) {
+  int n = 0, in_counter = 0;
+  uint32_t oligo = 0;
+  std::vector<uint32_t> touched;
+  for (int i = 0; i < qlen; i++) {
+    in_counter++;
+    switch (q[i]) {
+      case 'A': oligo = oligo << 2; break;
+      case 'C': oligo = (oligo << 2) | 1; break;
+      case 'G': oligo = (oligo << 2) | 2; break;
+      case 'T': oligo = (oligo << 2) | 3; break;
+      default: oligo = 0; in_counter = 0; break;
+    }
+    if (in_counter == 8) {
+      const uint32_t m = oligo & 0xFFFFu;
+      if (!((bm[m >> 5] >> (m & 31)) & 1u)) {
+        bm[m >> 5] |= 1u << (m & 31);
+        touched.push_back(m >> 5);
+        n++;
+      }
+      in_counter--;
+    }
+  }
+  for (uint32_t w : touched) bm[w] = 0;
+  return n;
+}
+
+extern "C" {
+
+size_t gmapdp_oligo_positions_capacity(const gmapdp_oligo_problem* problems, int n) {
+  size_t c = 0;
+  for (int i = 0; i < n; i++) c += oligo_table_cap(problems[i]);
+  return c;
+}
+size_t gmapdp_oligo_diagonal_capacity(const gmapdp_oligo_problem* problems, int n) {
+  size_t c = 0;
+  for (int i = 0; i < n; i++) c += oligo_diag_cap(problems[i]);
+  return c;
+}
+
+int gmapdp_oligo_mappings_batch(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problems, int n, const char* qseq_uc,
+                                size_t qbytes, gmapdp_oligo_result* results, int32_t* npositions, int32_t* mappings,
+                                uint32_t* positions, size_t positions_capacity, int32_t* diagonals,
+                                size_t diagonal_capacity) {
+  if (!ctx || n < 0 || (n > 0 && (!problems || !results || !qseq_uc || !npositions || !mappings)))
+    return GMAPDP_EINVAL;
+  if (!ctx->d_genome) return GMAPDP_ENOGENOME;
+  if (n == 0) return GMAPDP_OK;
+  (void)hipSetDevice(ctx->device);
+  std::vector<uint32_t> bm(2048, 0u);
+  std::vector<DevOligoProblem> dev(n);
+  size_t toff = 0, doff = 0, soff = 0;
+  // launch classes by the LDS the distinct 8-mers need
+  static const int kBuckets[] = {1024, 2048, 4096, 8192, 16384};
+  std::map<int, std::vector<int>> classes;
+  for (int i = 0; i < n; i++) {
+    const gmapdp_oligo_problem& p = problems[i];
+    if (p.querylength <= 8) return bad(ctx, "stage-2 seeding needs querylength > 8 (Oligoindex_set_inquery)");
+    if (p.qoff < 0 || (size_t)p.qoff + (size_t)p.querylength > qbytes) return bad(ctx, "query outside the arena");
+    if (oligo_window(p) > 0) {  // the last 8-mer start's half-word and the one after it (window8)
+      const uint64_t lpl = (uint64_t)p.chroffset + p.chrend + (p.plusp ? 0 : 1) - 8;
+      const uint64_t h = (lpl >> 4) + 1;
+      if (3 * (h >> 1) + 1 >= ctx->genome_words) return bad(ctx, "stage-2 window past the genome");
+    }
+    const int U = oligo_distinct(qseq_uc + p.qoff, p.querylength, bm);
+    if (U > kOligoMaxDistinct) return bad(ctx, "query with more than 16384 distinct 8-mers");
+    int umax = kBuckets[0];
+    for (int b : kBuckets)
+      if (U <= b) { umax = b; break; }
+    DevOligoProblem& d = dev[i];
+    std::memset(&d, 0, sizeof(d));
+    d.qoff = p.qoff;
+    d.querylength = p.querylength;
+    d.chrstart = p.chrstart;
+    d.chrend = p.chrend;
+    d.chroffset = p.chroffset;
+    d.chrhigh = p.chrhigh;
+    d.plusp = p.plusp ? 1 : 0;
+    d.minor = p.minor ? 1 : 0;
+    d.umax = umax;
+    d.table_offset = (int64_t)toff;
+    d.diag_offset = (int64_t)doff;
+    d.scratch_offset = (int64_t)soff;
+    toff += oligo_table_cap(p);
+    doff += oligo_diag_cap(p);
+    soff += align_up(scratch_bytes_oi(p.querylength, p.chrend > p.chrstart ? p.chrend - p.chrstart : 0), 256);
+    classes[umax].push_back(i);
+  }
+  if (toff > positions_capacity || doff > diagonal_capacity || (toff && !positions) || (doff && !diagonals))
+    return bad(ctx, "positions or diagonal arena too small");
+  if (toff > 0x7fffffffull) return bad(ctx, "stage-2 table arena beyond 2^31 entries");
+  // problems grouped by class; results come back in that order
+  std::vector<DevOligoProblem> ord;
+  std::vector<int> ord_problem;
+  std::vector<std::pair<int, int>> launches;  // (first, count) per class
+  std::vector<int> lumax;
+  for (auto& kv : classes) {
+    launches.push_back({(int)ord.size(), (int)kv.second.size()});
+    lumax.push_back(kv.first);
+    for (int i : kv.second) {
+      ord.push_back(dev[i]);
+      ord_problem.push_back(i);
+    }
+  }
+  hipError_t e = ctx->oprobs.ensure(sizeof(DevOligoProblem) * n);
+  if (e == hipSuccess) e = ctx->oresults.ensure(sizeof(gmapdp_oligo_result) * n);
+  if (e == hipSuccess) e = ctx->oscratch.ensure(std::max<size_t>(soff, 256));
+  if (e == hipSuccess) e = ctx->onpos.ensure(sizeof(int32_t) * qbytes);
+  if (e == hipSuccess) e = ctx->omap.ensure(sizeof(int32_t) * qbytes);
+  if (e == hipSuccess) e = ctx->otable.ensure(sizeof(uint32_t) * std::max<size_t>(toff, 1));
+  if (e == hipSuccess) e = ctx->odiag.ensure(4 * sizeof(int32_t) * std::max<size_t>(doff, 1));
+  if (e == hipSuccess) e = ctx->qseq_uc.ensure(qbytes);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "device buffers: %s", e);
+  hipStream_t s = ctx->stream;
+  e = hipMemcpyAsync(ctx->oprobs.p, ord.data(), sizeof(DevOligoProblem) * n, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(ctx->qseq_uc.p, qseq_uc, qbytes, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemsetAsync(ctx->onpos.p, 0, sizeof(int32_t) * qbytes, s);
+  if (e == hipSuccess) e = hipMemsetAsync(ctx->omap.p, 0xff, sizeof(int32_t) * qbytes, s);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "upload: %s", e);
+  for (size_t li = 0; li < launches.size(); li++) {
+    const int first = launches[li].first, count = launches[li].second;
+    e = launch_oi(count, lds_bytes_oi(lumax[li]), s, (const DevOligoProblem*)ctx->oprobs.p + first, ctx->d_genome,
+                  (const char*)ctx->qseq_uc.p, (unsigned char*)ctx->oscratch.p,
+                  (gmapdp_oligo_result*)ctx->oresults.p + first, (int32_t*)ctx->onpos.p, (int32_t*)ctx->omap.p,
+                  (uint32_t*)ctx->otable.p, (int32_t*)ctx->odiag.p);
+    if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "oligo launch: %s", e);
+  }
+  std::vector<gmapdp_oligo_result> dres(n);
+  e = hipMemcpyAsync(dres.data(), ctx->oresults.p, sizeof(gmapdp_oligo_result) * n, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(npositions, ctx->onpos.p, sizeof(int32_t) * qbytes, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(mappings, ctx->omap.p, sizeof(int32_t) * qbytes, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess && toff)
+    e = hipMemcpyAsync(positions, ctx->otable.p, sizeof(uint32_t) * toff, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess && doff)
+    e = hipMemcpyAsync(diagonals, ctx->odiag.p, 4 * sizeof(int32_t) * doff, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "oligo execution: %s", e);
+  for (int k = 0; k < n; k++) results[ord_problem[k]] = dres[k];
+  return GMAPDP_OK;
+}
 
 }  // extern "C"

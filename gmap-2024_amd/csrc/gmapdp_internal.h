@@ -132,4 +132,18 @@ struct DevCdnaProblem {
   int64_t scratch_offset; // byte offset of the problem's region of the global scratch
 };
 
+// Stage-2 seeding descriptor (Oligoindex_hr_tally + Oligoindex_get_mappings, oligoindex_hr.c:33849/34127)
+struct DevOligoProblem {
+  int32_t qoff;           // arena index of queryuc_ptr[0]
+  int32_t querylength;
+  uint32_t chrstart, chrend, chroffset, chrhigh;
+  int32_t plusp;
+  int32_t minor;          // oligoindices_minor (diag_lookback 60, suffnconsecutive 10), else major (120, 20)
+  int32_t umax;           // LDS slots for the query's distinct 8-mers (>= their number)
+  int32_t pad_;
+  int64_t table_offset;   // first entry of the problem's table in the positions arena
+  int64_t diag_offset;    // first diagonal record (4 x int32)
+  int64_t scratch_offset; // byte offset of the problem's region of the global scratch
+};
+
 }  // namespace gmapdp

@@ -1,0 +1,327 @@
+// oi_kernel.hip -- CDNA4 (gfx950) kernel for GMAP's stage-2 seeding:
+// Oligoindex_hr_tally + Oligoindex_get_mappings as Stage2_compute runs them for GMAP
+// (stage2.c:6413-6501; one oligoindex source, indexsize 8, coveredp all false).
+//
+// Reference semantics restated (paths under the reference tree's src/):
+//   Oligoindex_set_inquery         oligoindex_hr.c:33454 (the query's 8-mers; trimp false)
+//   count_positions_fwd/rev_std    :19260 / :30761 (8-mers starting in [mappingstart, mappingend-8],
+//                                  none unless that range has two starts; Count_T wraps mod 256)
+//   Oligoindex_allocate_positions  :32520 (counts masked by inquery; one table slice per oligo)
+//   store_positions_fwd/rev_std    :20426 / :31741 (walking from the far end of the chrpos origin,
+//                                  an oligo keeps its `count` occurrences nearest that end, stored
+//                                  in ascending chrpos)
+//   Oligoindex_get_mappings        :34127 (mappings/npositions per querypos, cum_nohits, the
+//                                  Genomicdiag_T consecutive-run state per diagonal, the good
+//                                  diagonals in the order they reach suffnconsecutive, else the best)
+//
+// Design.  One wave per (read, genomic window).  The query's distinct 8-mers are a 64-K-bit bitmap
+// in LDS; the bitmap's per-word prefix popcounts give every query 8-mer a dense id in oligo order,
+// so membership and the id of a window 8-mer are two LDS reads and a popcount -- no 64-K count
+// table, no hash.  A window 8-mer is one 64-bit funnel of two 16-nt genome half-words: the reverse
+// complement is its bitwise complement, the forward oligo its 2-bit reversal.  Pass 1 counts per id
+// (LDS atomics); an exclusive scan lays out the table; pass 2 walks the window in descending chrpos
+// in 64-position tiles and places each tile's hits in lane order (scalar loop over the ballot), which
+// reproduces the reference's keep-the-nearest-`count` rule exactly.  get_mappings then runs query
+// position by query position -- its state machine is sequential along the query -- with the hits of
+// one position (distinct diagonals) in parallel lanes, per-diagonal state in an L2-resident scratch.
+#include "dp_device.h"
+
+namespace gmapdp {
+
+constexpr int kOiK = 8;
+constexpr int kOiWords = 65536 / 32;  // bitmap words
+
+// 16-nt half-word h of the packed genome (.genomecomp: {high nt 16-31, low nt 0-15, flags})
+__device__ __forceinline__ uint32_t half_word(const uint32_t* __restrict__ blocks, uint64_t h) {
+  return blocks[3 * (h >> 1) + ((h & 1) ? 0 : 1)];
+}
+// the 8 nt starting at pos, nt j in bits 2j..2j+1
+__device__ __forceinline__ uint32_t window8(const uint32_t* __restrict__ blocks, uint64_t pos) {
+  const uint64_t h = pos >> 4;
+  const uint64_t v = (uint64_t)half_word(blocks, h) | ((uint64_t)half_word(blocks, h + 1) << 32);
+  return (uint32_t)(v >> (2 * (pos & 15))) & 0xFFFFu;
+}
+// forward oligo: first nt most significant (reverse the 2-bit groups)
+__device__ __forceinline__ uint32_t oligo_fwd(uint32_t x) {
+  x = ((x & 0x3333u) << 2) | ((x >> 2) & 0x3333u);
+  x = ((x & 0x0F0Fu) << 4) | ((x >> 4) & 0x0F0Fu);
+  x = ((x & 0x00FFu) << 8) | ((x >> 8) & 0x00FFu);
+  return x & 0xFFFFu;
+}
+
+struct OiState {  // struct Genomicdiag_T (oligoindex_hr.c:106); i is the array index
+  int querypos, best_n, n, cstart, best_start, best_end;
+};
+
+__device__ __forceinline__ int nt_code(char c) {  // -1 resets the 8-mer (oligoindex_hr.c:34213-34223)
+  return c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : c == 'T' ? 3 : -1;
+}
+
+// the query 8-mer at querypos i (characters i .. i+7), -1 if one of them is not ACGT
+__device__ __forceinline__ int query_oligo(const char* __restrict__ q, int i) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int j = 0; j < kOiK; j++) {
+    const int c = nt_code(q[i + j]);
+    if (c < 0) return -1;
+    m = (m << 2) | (uint32_t)c;
+  }
+  return (int)m;
+}
+
+__device__ __forceinline__ int oligo_id(const uint32_t* bitmap, const uint16_t* wrank, uint32_t m, bool& in) {
+  const uint32_t wbits = bitmap[m >> 5];
+  in = (wbits >> (m & 31)) & 1u;
+  return wrank[m >> 5] + __popc(wbits & ((1u << (m & 31)) - 1u));
+}
+
+// per-problem scratch: cum_nohits (querylength + 1 ints), the genomicdiag init flags, the states
+struct ScratchOi {
+  size_t initp, states, total;
+};
+__host__ __device__ inline ScratchOi scratch_oi(int querylength, uint32_t genomiclength) {
+  const size_t nd = (size_t)querylength + genomiclength + 1;
+  ScratchOi s;
+  s.initp = align16(4 * (size_t)(querylength + 1));
+  s.states = align16(s.initp + nd);
+  s.total = align16(s.states + nd * sizeof(OiState));
+  return s;
+}
+
+__global__ __launch_bounds__(64) void oi_kernel(
+    const DevOligoProblem* __restrict__ probs, const uint32_t* __restrict__ blocks, const char* __restrict__ quc_all,
+    unsigned char* __restrict__ scratch, gmapdp_oligo_result* __restrict__ results, int32_t* __restrict__ npos_out,
+    int32_t* __restrict__ map_out, uint32_t* __restrict__ table_all, int32_t* __restrict__ diag_all) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x;
+  const DevOligoProblem P = probs[blockIdx.x];
+  uint32_t* bitmap = reinterpret_cast<uint32_t*>(smem);                  // 2048 words
+  uint16_t* wrank = reinterpret_cast<uint16_t*>(smem + 4 * kOiWords);     // set bits before word w
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(smem + 6 * kOiWords);       // per id: count, then remaining
+  uint32_t* offs = cnt + P.umax;                                          // per id: table offset
+  const char* quc = quc_all + P.qoff;
+  const int qlen = P.querylength;
+  const int nq = qlen - kOiK + 1;  // query positions with a full 8-mer
+
+  // ---- the query's 8-mers (Oligoindex_set_inquery) ----
+  for (int w = lane; w < kOiWords; w += 64) bitmap[w] = 0u;
+  __syncthreads();
+  for (int i = lane; i < nq; i += 64) {
+    const int m = query_oligo(quc, i);
+    if (m >= 0) atomicOr(&bitmap[m >> 5], 1u << (m & 31));
+  }
+  __syncthreads();
+  int run = 0;  // ids in oligo order: prefix popcounts over the bitmap words
+  for (int base = 0; base < kOiWords; base += 64) {
+    const int c = __popc(bitmap[base + lane]);
+    const int incl = wave_scan_add(lane, c);
+    wrank[base + lane] = (uint16_t)(run + incl - c);
+    run += __builtin_amdgcn_readlane(incl, 63);
+  }
+  const int U = run;  // <= umax (the host counted them)
+  for (int u = lane; u < U; u += 64) cnt[u] = 0u;
+  __syncthreads();
+
+  // ---- pass 1: counts of the window's query 8-mers ----
+  const uint64_t left = (uint64_t)P.chroffset + P.chrstart;
+  uint64_t lpl = (uint64_t)P.chroffset + P.chrend + (P.plusp ? 0 : 1);
+  lpl = lpl < (uint64_t)kOiK ? 0 : lpl - kOiK;
+  const uint64_t npos = lpl > left ? lpl - left + 1 : 0;
+  for (uint64_t t = 0; t < npos; t += 64) {
+    const uint64_t k = t + lane;
+    if (k < npos) {
+      const uint32_t x = window8(blocks, left + k);
+      bool in;
+      const int u = oligo_id(bitmap, wrank, P.plusp ? oligo_fwd(x) : (~x & 0xFFFFu), in);
+      if (in) atomicAdd(&cnt[u], 1u);
+    }
+  }
+  __syncthreads();
+  // Count_T wraps; the table slices follow oligo order
+  uint32_t tot = 0;
+  for (int base = 0; base < U; base += 64) {
+    const int u = base + lane;
+    const uint32_t c = u < U ? (cnt[u] & 255u) : 0u;
+    const uint32_t incl = (uint32_t)wave_scan_add(lane, (int)c);
+    if (u < U) {
+      offs[u] = tot + incl - c;
+      cnt[u] = c;
+    }
+    tot += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  }
+  __syncthreads();
+
+  // ---- pass 2: store in descending chrpos (plus: right to left; minus: left to right) ----
+  uint32_t* table = table_all + P.table_offset;
+  const uint32_t chrpos0 = P.plusp ? P.chrstart : (P.chrhigh - P.chroffset) - P.chrend;
+  for (uint64_t t = 0; t < npos; t += 64) {
+    const uint64_t k = t + lane;  // k-th position in store order
+    int id = -1;
+    uint32_t cp = 0;
+    if (k < npos) {
+      const uint64_t pos = P.plusp ? lpl - k : left + k;
+      const uint32_t x = window8(blocks, pos);
+      bool in;
+      const int u = oligo_id(bitmap, wrank, P.plusp ? oligo_fwd(x) : (~x & 0xFFFFu), in);
+      if (in) id = u;
+      cp = chrpos0 + (uint32_t)(P.plusp ? pos - left : lpl - pos);
+    }
+    uint64_t hits = ballot(id >= 0);
+    while (hits) {  // lane order = store order; a scalar loop keeps same-oligo hits in sequence
+      const int l = __ffsll((long long)hits) - 1;
+      hits &= hits - 1;
+      const int hid = __builtin_amdgcn_readlane(id, l);
+      const uint32_t hcp = (uint32_t)__builtin_amdgcn_readlane((int)cp, l);
+      if (lane == 0) {
+        const uint32_t r = cnt[hid];
+        if (r) {
+          cnt[hid] = r - 1;
+          table[offs[hid] + r - 1] = hcp;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // the per-id counts again (nhits of lookup, :34074)
+  for (int u = lane; u < U; u += 64) cnt[u] = (u + 1 < U ? offs[u + 1] : tot) - offs[u];
+  __threadfence_block();
+  __syncthreads();
+
+  // ---- Oligoindex_get_mappings ----
+  gmapdp_oligo_result res;
+  res.totalpositions = 0;
+  res.maxnconsecutive = 0;
+  res.oned_matrix_p = 0;
+  res.ndiagonals = 0;
+  res.table_offset = P.table_offset;
+  res.diag_offset = P.diag_offset;
+  int32_t* npq = npos_out + P.qoff;
+  int32_t* mpq = map_out + P.qoff;
+  for (int i = lane; i < qlen; i += 64) {
+    npq[i] = 0;
+    mpq[i] = -1;
+  }
+  __threadfence_block();
+  // per querypos: nhits and table offset; cum_nohits as an inclusive prefix count of the positions
+  // whose 8-mer has no hit (a position without a full 8-mer carries it forward)
+  unsigned char* base_s = scratch + P.scratch_offset;
+  int* cum = reinterpret_cast<int*>(base_s);
+  int totalpositions = 0, cumrun = 0;
+  for (int base = 0; base < nq; base += 64) {
+    const int i = base + lane;
+    int nh = -1;
+    if (i < nq) {
+      const int m = query_oligo(quc, i);
+      if (m >= 0) {
+        bool in;
+        const int u = oligo_id(bitmap, wrank, (uint32_t)m, in);
+        nh = (int)cnt[u];
+        npq[i] = nh;
+        mpq[i] = nh > 0 ? (int32_t)(P.table_offset + offs[u]) : -1;
+      }
+    }
+    const int incl = wave_scan_add(lane, nh == 0 ? 1 : 0);
+    if (i < nq) cum[i] = cumrun + incl;
+    cumrun += __builtin_amdgcn_readlane(incl, 63);
+    totalpositions += __builtin_amdgcn_readlane(wave_scan_add(lane, nh > 0 ? nh : 0), 63);
+  }
+  if (P.chrend > P.chrstart) {
+    const int diag_lookback = P.minor ? 60 : 120, suffn = P.minor ? 10 : 20;
+    const uint32_t chrinit = P.plusp ? P.chrstart : (P.chrhigh - P.chroffset) - P.chrend;
+    const ScratchOi so = scratch_oi(qlen, P.chrend - P.chrstart);
+    unsigned char* initp = base_s + so.initp;
+    OiState* st = reinterpret_cast<OiState*>(base_s + so.states);
+    for (size_t b = 16 * (size_t)lane; b < so.states - so.initp; b += 16 * 64)
+      *reinterpret_cast<uint4*>(initp + b) = make_uint4(0u, 0u, 0u, 0u);
+    __threadfence_block();
+    int32_t* good = diag_all + 4 * P.diag_offset;  // diagi of each good diagonal, in field 0 of its record
+    int ngood = 0, maxn = 0, best = -1;
+    for (int q = 0; q < nq; q++) {
+      const int nh = npq[q];
+      if (nh <= 0) continue;
+      const uint32_t* hits = table + (mpq[q] - (int32_t)P.table_offset);
+      const int cq = cum[q];
+      for (int base = 0; base < nh; base += 64) {
+        const int h = base + lane;
+        int reached = 0, nb = 0;
+        uint32_t diagi = 0;
+        if (h < nh) {
+          diagi = hits[h] + (uint32_t)(qlen - q) - chrinit;
+          OiState s;
+          if (!initp[diagi]) {
+            initp[diagi] = 1;
+            s.querypos = -diag_lookback;  // the first check is never consecutive
+            s.best_n = s.n = s.cstart = s.best_start = s.best_end = 0;
+          } else {
+            s = st[diagi];
+          }
+          if (s.querypos < 0) {
+            s.n = 0;
+            s.cstart = q;
+          } else if (q - s.querypos >= diag_lookback + cq - cum[s.querypos]) {
+            s.n = 0;
+            s.cstart = q;
+          } else if (++s.n > s.best_n) {
+            s.best_start = s.cstart;
+            s.best_end = q;
+            s.best_n = s.n;
+            reached = (s.best_n == suffn);
+            nb = s.best_n;
+          }
+          s.querypos = q;
+          st[diagi] = s;
+        }
+        // the good list in lane order; the global best: the first lane reaching the new maximum
+        const uint64_t rm = ballot(reached);
+        if (reached) good[4 * (ngood + lanes_below(rm, lane))] = (int32_t)diagi;
+        ngood += __popcll(rm);
+        int mx = nb;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) mx = max(mx, __shfl_xor(mx, off, 64));
+        if (mx > maxn) {
+          const int l = __ffsll((long long)ballot(nb == mx)) - 1;
+          best = __builtin_amdgcn_readlane((int)diagi, l);
+          maxn = mx;
+        }
+      }
+    }
+    if (ngood == 0 && maxn > 0) {
+      if (lane == 0) good[0] = best;
+      ngood = 1;
+    }
+    __threadfence_block();
+    for (int g = lane; g < ngood; g += 64) {
+      const int di = good[4 * g];
+      const OiState s = st[di];
+      good[4 * g + 0] = di >= qlen ? di - qlen : qlen - di;
+      good[4 * g + 1] = s.best_start;
+      good[4 * g + 2] = s.best_end;
+      good[4 * g + 3] = s.best_n + 1;
+    }
+    res.maxnconsecutive = maxn;
+    res.oned_matrix_p = 1;
+    res.ndiagonals = ngood;
+  }
+  res.totalpositions = totalpositions;
+  if (lane == 0) results[blockIdx.x] = res;
+}
+
+size_t lds_bytes_oi(int umax) { return 6 * (size_t)kOiWords + 8 * (size_t)umax; }
+size_t scratch_bytes_oi(int querylength, uint32_t genomiclength) {
+  return scratch_oi(querylength, genomiclength).total;
+}
+
+hipError_t launch_oi(int nproblems, size_t lds, hipStream_t stream, const DevOligoProblem* probs,
+                     const uint32_t* blocks, const char* quc, unsigned char* scratch, gmapdp_oligo_result* results,
+                     int32_t* npos, int32_t* map, uint32_t* table, int32_t* diags) {
+  void* fn = reinterpret_cast<void*>(&oi_kernel);
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  void* args[] = {(void*)&probs, (void*)&blocks, (void*)&quc, (void*)&scratch, (void*)&results, (void*)&npos,
+                  (void*)&map, (void*)&table, (void*)&diags};
+  return hipLaunchKernel(fn, dim3(nproblems), dim3(64), args, lds, stream);
+}
+
+}  // namespace gmapdp

@@ -80,6 +80,16 @@ class CdnaResult(C.Structure):
                 ("gap_queryjump", C.c_int32), ("pad_", C.c_int32)]
 
 
+class OligoProblem(C.Structure):
+    _fields_ = [("qoff", C.c_int32), ("querylength", C.c_int32), ("chrstart", C.c_uint32), ("chrend", C.c_uint32),
+                ("chroffset", C.c_uint32), ("chrhigh", C.c_uint32), ("plusp", C.c_int32), ("minor", C.c_int32)]
+
+
+class OligoResult(C.Structure):
+    _fields_ = [("totalpositions", C.c_int32), ("maxnconsecutive", C.c_int32), ("oned_matrix_p", C.c_int32),
+                ("ndiagonals", C.c_int32), ("table_offset", C.c_int64), ("diag_offset", C.c_int64)]
+
+
 def _struct_dtype(S, fmt):
     return np.dtype({"names": [n for n, _ in S._fields_], "formats": fmt,
                      "offsets": [S.__dict__[n].offset for n, _ in S._fields_], "itemsize": C.sizeof(S)})
@@ -89,6 +99,8 @@ GENOME_PROBLEM_DTYPE = _struct_dtype(GenomeProblem, ["<i4"] * 7 + ["<u4", "<u4"]
 GENOME_RESULT_DTYPE = _struct_dtype(GenomeResult, ["<i4"] * 14 + ["<f8", "<f8"])
 CDNA_PROBLEM_DTYPE = _struct_dtype(CdnaProblem, ["<i4"] * 8 + ["<u4", "<u4"] + ["<i4"] * 4 + ["<f8"])
 CDNA_RESULT_DTYPE = _struct_dtype(CdnaResult, ["<i4"] * 8)
+OLIGO_PROBLEM_DTYPE = _struct_dtype(OligoProblem, ["<i4", "<i4", "<u4", "<u4", "<u4", "<u4", "<i4", "<i4"])
+OLIGO_RESULT_DTYPE = _struct_dtype(OligoResult, ["<i4"] * 4 + ["<i8", "<i8"])
 
 PAIR_DTYPE = np.dtype([("querypos", "<i4"), ("genomepos", "<i4"), ("jump", "<i4"), ("cdna", "S1"),
                        ("comp", "S1"), ("genome", "S1"), ("genomealt", "S1")])
@@ -153,6 +165,11 @@ def load_library(path=LIB_PATH):
         "gmapdp_cdna_gap_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t,
                                             C.c_void_p, C.c_void_p, C.c_size_t]),
         "gmapdp_cdna_pair_capacity": (C.c_size_t, [C.c_void_p, C.c_int]),
+        "gmapdp_oligo_mappings_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_size_t,
+                                                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                                  C.c_void_p, C.c_size_t]),
+        "gmapdp_oligo_positions_capacity": (C.c_size_t, [C.c_void_p, C.c_int]),
+        "gmapdp_oligo_diagonal_capacity": (C.c_size_t, [C.c_void_p, C.c_int]),
         "gmapdp_genome_prob_entries": (C.c_size_t, [C.c_void_p, C.c_int]),
         "gmapdp_genome_splice_sites": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t]),
         "gmapdp_plan_create_all": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
@@ -424,6 +441,59 @@ class Engine:
                 g = int(res["gap_index"])
                 lst[g] = (-1, -1, int(res["gap_queryjump"]), lst[g][3], 0, b" ", b" ", b" ", b" ", 1)
             out.append((scal, lst))
+        return out
+
+    # -- batched stage-2 seeding (Oligoindex_hr_tally + Oligoindex_get_mappings) --------------
+    @staticmethod
+    def build_oligo_batch(calls):
+        """calls: dicts (quc, chrstart, chrend, chroffset, chrhigh, plusp, minor) -> (problems, qucbuf)."""
+        calls = list(calls)
+        probs = np.zeros(len(calls), dtype=OLIGO_PROBLEM_DTYPE)
+        parts, off = [], 0
+        for i, p in enumerate(calls):
+            probs[i]["qoff"] = off
+            probs[i]["querylength"] = len(p["quc"])
+            for k in ("chrstart", "chrend", "chroffset", "chrhigh", "plusp", "minor"):
+                probs[i][k] = int(p.get(k, 0))
+            parts.append(p["quc"])
+            off += len(p["quc"])
+        return probs, (b"".join(parts) or b"\0")
+
+    def oligo_mappings_batch_raw(self, probs, qucbuf):
+        n = len(probs)
+        results = np.zeros(n, dtype=OLIGO_RESULT_DTYPE)
+        npos = np.zeros(max(len(qucbuf), 1), dtype=np.int32)
+        maps = np.zeros(max(len(qucbuf), 1), dtype=np.int32)
+        pc = self.lib.gmapdp_oligo_positions_capacity(probs.ctypes.data, n)
+        dc = self.lib.gmapdp_oligo_diagonal_capacity(probs.ctypes.data, n)
+        positions = np.zeros(max(pc, 1), dtype=np.uint32)
+        diags = np.zeros(4 * max(dc, 1), dtype=np.int32)
+        rc = self.lib.gmapdp_oligo_mappings_batch(self.h, probs.ctypes.data, n, qucbuf, len(qucbuf),
+                                                  results.ctypes.data, npos.ctypes.data, maps.ctypes.data,
+                                                  positions.ctypes.data, pc, diags.ctypes.data, dc)
+        self._check(rc, "gmapdp_oligo_mappings_batch")
+        return results, npos, maps, positions, diags
+
+    def oligo_mappings_batch(self, calls):
+        """Per call ((totalpositions, maxnconsecutive, oned_matrix_p, ndiagonals), npositions list,
+        positions of every query position with hits concatenated in query order, diagonals as
+        (diagonal, querystart, queryend, nconsecutive)) -- the oracle's format."""
+        calls = list(calls)
+        probs, qucbuf = self.build_oligo_batch(calls)
+        results, npos, maps, positions, diags = self.oligo_mappings_batch_raw(probs, qucbuf)
+        out = []
+        for i, r in enumerate(results):
+            o, n = int(probs[i]["qoff"]), int(probs[i]["querylength"])
+            np_ = [int(x) for x in npos[o:o + n]]
+            plist = []
+            for q in range(n):
+                if np_[q] > 0:
+                    m = int(maps[o + q])
+                    plist.extend(int(x) for x in positions[m:m + np_[q]])
+            d0, nd = int(r["diag_offset"]), int(r["ndiagonals"])
+            dg = [tuple(int(x) for x in diags[4 * (d0 + k):4 * (d0 + k) + 4]) for k in range(nd)]
+            out.append(((int(r["totalpositions"]), int(r["maxnconsecutive"]), int(r["oned_matrix_p"]), nd),
+                        np_, plist, dg))
         return out
 
 

@@ -24,6 +24,9 @@
  *   gmapdp_plan_*            the same calls, planned once and replayed on device-resident
  *                            inputs (mixed single + end batches)
  *   gmapdp_compute_bands     Dynprog_compute_bands (dynprog.c:1247)
+ *   gmapdp_cdna_gap_batch    Dynprog_cdna_gap (dynprog_cdna.c:787)
+ *   gmapdp_oligo_mappings_batch  stage-2 seeding: Oligoindex_hr_tally + Oligoindex_get_mappings
+ *                            (oligoindex_hr.c:33849/34127) as Stage2_compute calls them (stage2.c:6480-6495)
  *
  * Semantics: every result is bit-identical to the reference's nosimd build
  * (Dynprog_standard + Dynprog_traceback_std); see DESIGN.md "Parity".
@@ -287,6 +290,49 @@ int gmapdp_cdna_gap_batch (gmapdp_ctx *ctx, const gmapdp_cdna_problem *problems,
                            const char *qseq, const char *qseq_uc, size_t qbytes,
                            gmapdp_cdna_result *results, gmapdp_pair *pairs, size_t pair_capacity);
 size_t gmapdp_cdna_pair_capacity (const gmapdp_cdna_problem *problems, int n);
+
+/* Stage-2 seeding: Oligoindex_hr_tally + Oligoindex_get_mappings
+ * (oligoindex_hr.c:33849/34127) as Stage2_compute runs them for GMAP (stage2.c:6413-6501: one
+ * 8-mer oligoindex, coveredp all false).  One problem = one (query, genomic window) pair:
+ * queryuc_ptr = qseq_uc + qoff (upper-case query), the window [chrstart, chrend) of the chromosome
+ * at chroffset..chrhigh on the plus (plusp) or minus strand.  minor selects
+ * Oligoindex_array_new_minor's index (diag_lookback 60, suffnconsecutive 10) instead of the major
+ * one (120, 20).  Domain: querylength > 8 (Oligoindex_set_inquery leaves stale state below that)
+ * and at most 16384 distinct query 8-mers. */
+typedef struct {
+  int32_t qoff;
+  int32_t querylength;
+  uint32_t chrstart;
+  uint32_t chrend;
+  uint32_t chroffset;
+  uint32_t chrhigh;
+  int32_t plusp;
+  int32_t minor;
+} gmapdp_oligo_problem;
+
+/* Per problem: *totalpositions, *maxnconsecutive, *oned_matrix_p (0 where the reference leaves it
+ * unwritten: chrend <= chrstart) and the diagonals list (Diagpool_push records, list order) at
+ * diagonals[4 * diag_offset ...]: {diagonal, querystart, queryend, nconsecutive} each.  Per query
+ * position q: npositions[qoff + q] (0 without a full 8-mer or without hits) and
+ * mappings[qoff + q], the index in `positions` of mappings[q][0] (-1 without hits); the problem's
+ * table occupies positions[table_offset ...]. */
+typedef struct {
+  int32_t totalpositions;
+  int32_t maxnconsecutive;
+  int32_t oned_matrix_p;
+  int32_t ndiagonals;
+  int64_t table_offset;
+  int64_t diag_offset;
+} gmapdp_oligo_result;
+
+/* npositions, mappings: qbytes entries each (indexed like the query arena). */
+int gmapdp_oligo_mappings_batch (gmapdp_ctx *ctx, const gmapdp_oligo_problem *problems, int n,
+                                 const char *qseq_uc, size_t qbytes, gmapdp_oligo_result *results,
+                                 int32_t *npositions, int32_t *mappings, uint32_t *positions,
+                                 size_t positions_capacity, int32_t *diagonals, size_t diagonal_capacity);
+/* Table entries / diagonal records (4 x int32) a batch may need. */
+size_t gmapdp_oligo_positions_capacity (const gmapdp_oligo_problem *problems, int n);
+size_t gmapdp_oligo_diagonal_capacity (const gmapdp_oligo_problem *problems, int n);
 
 /* Create a context on HIP device `device`.  mode = Mode_T (mode.h:5;
  * 0 = STANDARD).  user_* mirror Dynprog_single_setup. */

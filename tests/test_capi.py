@@ -97,6 +97,7 @@ def test_struct_layouts_match_the_c_header(tmp_path):
                    '  sizeof(gmapdp_genome_problem), sizeof(gmapdp_genome_result), sizeof(gmapdp_cdna_problem),\n'
                    '  sizeof(gmapdp_cdna_result));\n'
                    'printf("%zu %zu\\n", offsetof(gmapdp_cdna_problem, defect_rate), offsetof(gmapdp_cdna_result, gap_queryjump));\n'
+                   'printf("%zu %zu %zu\\n", sizeof(gmapdp_oligo_problem), sizeof(gmapdp_oligo_result), offsetof(gmapdp_oligo_result, diag_offset));\n'
                    'return 0; }\n')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(os.path.dirname(HERE), "include"), str(src), "-o", str(exe)], check=True)
@@ -104,8 +105,10 @@ def test_struct_layouts_match_the_c_header(tmp_path):
     sizes = [int(x) for x in out]
     assert sizes[:6] == [C.sizeof(gmapdp.SingleProblem), C.sizeof(gmapdp.EndProblem), C.sizeof(gmapdp.GenomeProblem),
                          C.sizeof(gmapdp.GenomeResult), C.sizeof(gmapdp.CdnaProblem), C.sizeof(gmapdp.CdnaResult)]
-    assert sizes[6:] == [gmapdp.CdnaProblem.defect_rate.offset, gmapdp.CdnaResult.gap_queryjump.offset]
+    assert sizes[6:8] == [gmapdp.CdnaProblem.defect_rate.offset, gmapdp.CdnaResult.gap_queryjump.offset]
     assert gmapdp.CDNA_PROBLEM_DTYPE.itemsize == sizes[4] and gmapdp.CDNA_RESULT_DTYPE.itemsize == sizes[5]
+    assert sizes[8:] == [C.sizeof(gmapdp.OligoProblem), C.sizeof(gmapdp.OligoResult), gmapdp.OligoResult.diag_offset.offset]
+    assert gmapdp.OLIGO_PROBLEM_DTYPE.itemsize == sizes[8] and gmapdp.OLIGO_RESULT_DTYPE.itemsize == sizes[9]
 
 
 def test_genome_splice_sites_match_oracle():

@@ -1,0 +1,94 @@
+"""GPU parity tests for stage-2 seeding: oi_kernel's Oligoindex_hr_tally +
+Oligoindex_get_mappings (oligoindex_hr.c:33849/34127, as Stage2_compute runs them for GMAP) against
+the goldens from the reference's own objects, the oracle restatement (oracle/stage2_oracle.c) and
+the reference objects directly.  Bar: bit-exact npositions, mapping lists (order included),
+totalpositions, maxnconsecutive, oned_matrix_p and the diagonals list."""
+import os
+import random
+
+import pytest
+
+import gmapdp
+from dpbind import Oracle, Ref, oligo_problem, random_genome, ref_available
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _golden():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(HERE, "golden", "make_golden.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m.load_oligo(os.path.join(HERE, "golden", "oligo_golden.npz"))
+
+
+@pytest.fixture(scope="module")
+def engine():
+    e = gmapdp.Engine(0)
+    yield e
+    e.close()
+
+
+def _first_diff(got, exp):
+    for i, (a, b) in enumerate(zip(got, exp)):
+        if a != b:
+            return i, a, b
+    return None
+
+
+def _msg(probs, d, what):
+    i, a, b = d
+    p = {k: v for k, v in probs[i].items() if k != "quc"}
+    if len(a) == 4 and len(b) == 4:
+        parts = [k for k, x, y in zip(("scalars", "npositions", "positions", "diagonals"), a, b) if x != y]
+        return "problem %d (%s, qlen %d): %s differ; gpu %s vs %s %s" % (i, p, len(probs[i]["quc"]), parts, a[0],
+                                                                          what, b[0])
+    return "problem %d (%s): gpu %s vs %s %s" % (i, p, a[:1], what, b[:1])
+
+
+def test_gpu_oligo_matches_reference_golden(engine):
+    g, probs, exp = _golden()
+    engine.set_genome(g)
+    got = engine.oligo_mappings_batch(probs)
+    d = _first_diff(got, exp)
+    assert d is None, _msg(probs, d, "ref")
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_gpu_oligo_matches_oracle_random(engine, seed):
+    rng = random.Random(8100 + seed)
+    g = bytearray(random_genome(rng, 400000))
+    g[200000:202500] = b"A" * 2500  # 8-mer counts past Count_T's 255
+    g = bytes(g)
+    engine.set_genome(g)
+    orc = Oracle()
+    orc.set_genome(g)
+    probs = [oligo_problem(rng, g, edge=(i % 5 == 0)) for i in range(600)]
+    got = engine.oligo_mappings_batch(probs)
+    exp = [orc.oligo_mappings(p) for p in probs]
+    d = _first_diff(got, exp)
+    assert d is None, _msg(probs, d, "oracle")
+
+
+@pytest.mark.skipif(not ref_available("nosimd"), reason="reference objects did not travel")
+def test_gpu_oligo_matches_reference_objects(engine):
+    rng = random.Random(8200)
+    g = random_genome(rng, 200000)
+    engine.set_genome(g)
+    ref = Ref("nosimd")
+    ref.set_genome(g)
+    probs = [oligo_problem(rng, g, edge=(i % 4 == 0)) for i in range(300)]
+    got = engine.oligo_mappings_batch(probs)
+    d = _first_diff(got, [ref.oligo_mappings(p) for p in probs])
+    assert d is None, _msg(probs, d, "ref")
+
+
+def test_gpu_oligo_domain_check(engine):
+    """querylength <= 8 leaves the reference's inquery table stale: rejected, not guessed."""
+    rng = random.Random(9)
+    g = random_genome(rng, 20000)
+    engine.set_genome(g)
+    p = dict(quc=b"ACGTACGT", chrstart=100, chrend=5000, chroffset=0, chrhigh=20000, plusp=1, minor=0)
+    with pytest.raises(gmapdp.GmapdpError):
+        engine.oligo_mappings_batch([p])
