@@ -231,7 +231,9 @@ def pmc_traffic(name):
     m = re.match(r"(\w+)<R=(\d+),dirs_lds=(\d)>", name)
     if not m:
         return None, None
-    if m.group(1) == "dpx_kernel":  # dpx_kernel<S, GD>: GD = direction words in global scratch
+    if m.group(1) == "oi_kernel":  # not a template
+        key = "gmapdp::oi_kernel"
+    elif m.group(1) == "dpx_kernel":  # dpx_kernel<S, GD>: GD = direction words in global scratch
         key = "gmapdp::dpx_kernel<%s, %s>" % (m.group(2), "false" if m.group(3) == "1" else "true")
     else:
         key = "gmapdp::%s<%s, %s>" % (m.group(1), m.group(2), "true" if m.group(3) == "1" else "false")
@@ -267,6 +269,80 @@ def banded_cells(sp, ep):
     W = np.where(ep["endalign"] == 1, 2 * eb + 1, np.abs(g - r) + 2 * eb + 1)
     W = np.where(ep["endalign"] == 2, 0, W)
     return cells + int(np.minimum(W, r + 1).dot(g))
+
+
+def make_stage2(genome, n, rng, exons=5, exlen=400, pad=1000):
+    """Stage-2 seeding calls, one per 2-kb read (SURVEY §8d read model): 5 exons x 400 nt cut from
+    the genome with log-uniform [80, 20000] introns, 2 % substitutions, half reverse-complemented
+    (seeded on the minus strand), against the window spanning the locus plus 1 kb each side (the
+    gregion).  Returns (gmapdp_oligo_problem array, upper-case query arena)."""
+    import gmapdp
+    glen = len(genome)
+    probs = np.zeros(n, dtype=gmapdp.OLIGO_PROBLEM_DTYPE)
+    parts, off = [], 0
+    for i in range(n):
+        introns = np.exp(rng.uniform(np.log(80), np.log(20000), size=exons - 1)).astype(np.int64)
+        span = exons * exlen + int(introns.sum())
+        start = int(rng.integers(pad, glen - span - pad))
+        segs, p = [], start
+        for e in range(exons):
+            segs.append(genome[p:p + exlen])
+            p += exlen + (int(introns[e]) if e < exons - 1 else 0)
+        q = np.concatenate(segs)
+        m = rng.random(q.size) < 0.02
+        q[m] = ACGT[rng.integers(0, 4, size=int(m.sum()))]
+        plus = rng.random() < 0.5
+        if not plus:
+            q = COMPL[q[::-1]]
+        probs[i] = (off, q.size, start - pad, start + span + pad, 0, glen, int(plus), 0)
+        parts.append(q)
+        off += q.size
+    return probs, np.concatenate(parts)
+
+
+def stage2_algorithmic_bytes(op, res):
+    """Stage-2 seeding per call: descriptor (32 B) + the query (1 B/nt) + the window's packed genome
+    (12 B per 32 nt) + npositions and mappings (8 B per query position) + the table (4 B per stored
+    position) + the result (32 B) + the diagonal records (16 B each)."""
+    w = (op["chrend"].astype(np.int64) - op["chrstart"].astype(np.int64))
+    ql = op["querylength"].astype(np.int64)
+    return int((32 + ql + 12 * ((w + 31) // 32) + 8 * ql + 32).sum()
+               + 4 * int(res["totalpositions"].astype(np.int64).sum())
+               + 16 * int(res["ndiagonals"].astype(np.int64).sum()))
+
+
+def cpu_baseline_stage2(op, oq, genome, budget_s=8.0):
+    """The reference's Oligoindex_hr_tally + Oligoindex_get_mappings (1 core, nosimd objects) on a
+    bounded prefix of the same seeding calls."""
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "librefdp_nosimd.so")
+    if not os.path.exists(ref_so):
+        return None
+    lib = C.CDLL(ref_so)
+    lib.refh_init(0, 0, 0)
+    gb = genome.tobytes()
+    lib.refh_set_genome(gb, len(gb))
+    f = lib.refh_oligo_mappings
+    f.restype = C.c_int
+    f.argtypes = [C.c_char_p, C.c_int, C.c_uint, C.c_uint, C.c_uint, C.c_uint, C.c_int, C.c_int, C.c_void_p,
+                  C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int]
+    cap = 1 << 21
+    pos = np.zeros(cap, dtype=np.uint32)
+    npos = np.zeros(int(op["querylength"].max()) + 1, dtype=np.int32)
+    sc = np.zeros(4, dtype=np.int32)
+    dg = np.zeros(4 * 65536, dtype=np.int32)
+    qb = oq.tobytes()
+    t, n = 0.0, 0
+    while t < budget_s and n < len(op):
+        p = op[n]
+        o, ql = int(p["qoff"]), int(p["querylength"])
+        t0 = time.perf_counter()
+        f(qb[o:o + ql], ql, int(p["chrstart"]), int(p["chrend"]), int(p["chroffset"]), int(p["chrhigh"]),
+          int(p["plusp"]), 0, npos.ctypes.data, pos.ctypes.data, cap, sc.ctypes.data, dg.ctypes.data, 65536)
+        t += time.perf_counter() - t0
+        n += 1
+    return {"value": n / t, "unit": "reads/s", "cores": 1, "kind": "reference",
+            "sample": "%d seeding calls of the same stream (%.1f s, 1 thread, gmap nosimd oligoindex_hr.o via "
+                      "oracle/_ref refh_oligo_mappings)" % (n, t)}
 
 
 def cpu_baseline(sp, ep, q, genome, budget_s=12.0):
@@ -569,6 +645,66 @@ def main():
         "roofline_genome_gap": roofline(max(gcount, key=gcount.get), disp_all),
         "splice_probabilities": "synthetic host input (0.95 at planted GT-AG sites, U[0,0.3) elsewhere)"}
     lib.gmapdp_plan_destroy(PA["plan"])
+
+    # ---- stage-2 seeding: Oligoindex_hr_tally + Oligoindex_get_mappings ----
+    op, oq = make_stage2(genome, args.reads, np.random.default_rng(3000 + rank))
+    oplan = C.c_void_p()
+    eng._check(lib.gmapdp_oligo_plan_create(eng.h, op.ctypes.data, len(op), oq.ctypes.data, len(oq), C.byref(oplan)),
+               "gmapdp_oligo_plan_create")
+    pcap = lib.gmapdp_oligo_plan_positions_capacity(oplan)
+    dcap = lib.gmapdp_oligo_plan_diagonal_capacity(oplan)
+    d_oq = torch.from_numpy(oq).to(dev)
+    d_ores = torch.zeros(len(op) * 32, dtype=torch.uint8, device=dev)
+    d_onpos = torch.empty(len(oq) * 4, dtype=torch.uint8, device=dev)
+    d_omap = torch.empty(len(oq) * 4, dtype=torch.uint8, device=dev)
+    d_opos = torch.empty(max(pcap, 1) * 4, dtype=torch.uint8, device=dev)
+    d_odiag = torch.empty(max(dcap, 1) * 16, dtype=torch.uint8, device=dev)
+
+    def orun():
+        eng._check(lib.gmapdp_oligo_plan_run(eng.h, oplan, C.c_void_p(d_oq.data_ptr()), C.c_void_p(d_ores.data_ptr()),
+                                             C.c_void_p(d_onpos.data_ptr()), C.c_void_p(d_omap.data_ptr()),
+                                             C.c_void_p(d_opos.data_ptr()), C.c_void_p(d_odiag.data_ptr()),
+                                             C.c_void_p(stream.cuda_stream)), "gmapdp_oligo_plan_run")
+
+    osteps = max(1, args.steps // 2)
+    with torch.cuda.stream(stream):
+        orun()
+        torch.cuda.synchronize()
+        oev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(osteps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(osteps):
+            oev[k][0].record(stream)
+            orun()
+            oev[k][1].record(stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        oelapsed = time.perf_counter() - t0
+    if world > 1:
+        from gmapdp import shard
+        oelapsed = shard.max_over_ranks(oelapsed, dist, device=dev)
+    oms = sum(a.elapsed_time(b) for a, b in oev) / osteps
+    ores = np.frombuffer(d_ores.cpu().numpy().tobytes(), dtype=gmapdp.OLIGO_RESULT_DTYPE)
+    obytes = stage2_algorithmic_bytes(op, ores)
+    otraffic, osrc = pmc_traffic("oi_kernel<R=0,dirs_lds=0>")
+    nol = lib.gmapdp_oligo_plan_nlaunches(oplan)
+    out["stage2_seeding"] = {
+        "value": args.reads * world * osteps / oelapsed, "unit": "reads/s", "ms_per_step": oelapsed / osteps * 1e3,
+        "steps": osteps, "calls_per_read": 1, "window_nt_per_step_per_gpu": int((op["chrend"] - op["chrstart"]).sum()),
+        "totalpositions_per_step_per_gpu": int(ores["totalpositions"].astype(np.int64).sum()),
+        "diagonals_per_step_per_gpu": int(ores["ndiagonals"].astype(np.int64).sum()),
+        "roofline": {"bound": "hbm", "achieved": obytes / (oms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": obytes / (oms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": otraffic, "traffic_source": osrc,
+                     "kernel": "oi_kernel", "dispatches": nol * osteps, "kernel_ms_per_launch": oms / max(nol, 1),
+                     "algorithmic_bytes_per_launch": obytes / max(nol, 1),
+                     "note": "one wave per read: LDS-atomic counting sort of the window's 8-mers + the sequential "
+                             "get_mappings state machine; latency-bound (DESIGN.md)"}}
+    lib.gmapdp_oligo_plan_destroy(oplan)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["stage2_seeding"]["cpu_baseline"] = cpu_baseline_stage2(op, oq, genome)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(sp, ep, q_all, genome)
         cg = cpu_baseline_genome(gp, q_all, genome)

@@ -1575,20 +1575,38 @@ size_t gmapdp_oligo_diagonal_capacity(const gmapdp_oligo_problem* problems, int 
   return c;
 }
 
-int gmapdp_oligo_mappings_batch(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problems, int n, const char* qseq_uc,
-                                size_t qbytes, gmapdp_oligo_result* results, int32_t* npositions, int32_t* mappings,
-                                uint32_t* positions, size_t positions_capacity, int32_t* diagonals,
-                                size_t diagonal_capacity) {
-  if (!ctx || n < 0 || (n > 0 && (!problems || !results || !qseq_uc || !npositions || !mappings)))
-    return GMAPDP_EINVAL;
+}  // extern "C"
+
+// A planned stage-2 batch: descriptors (in launch-class order) resident on the device, the launch
+// classes, the per-problem scratch, the output capacities.
+struct gmapdp_oligo_plan {
+  int n = 0;
+  DevOligoProblem* d_probs = nullptr;
+  unsigned char* d_scratch = nullptr;
+  std::vector<std::pair<int, int>> launches;  // (first, count)
+  std::vector<int> umax;
+  size_t table_cap = 0, diag_cap = 0;
+};
+
+static void oligo_plan_free(gmapdp_oligo_plan* p) {
+  if (!p) return;
+  if (p->d_probs) (void)hipFree(p->d_probs);
+  if (p->d_scratch) (void)hipFree(p->d_scratch);
+  delete p;
+}
+
+extern "C" {
+
+int gmapdp_oligo_plan_create(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problems, int n, const char* qseq_uc,
+                             size_t qbytes, gmapdp_oligo_plan** plan) {
+  if (!ctx || !plan || n < 0 || (n > 0 && (!problems || !qseq_uc))) return GMAPDP_EINVAL;
+  *plan = nullptr;
   if (!ctx->d_genome) return GMAPDP_ENOGENOME;
-  if (n == 0) return GMAPDP_OK;
   (void)hipSetDevice(ctx->device);
   std::vector<uint32_t> bm(2048, 0u);
   std::vector<DevOligoProblem> dev(n);
   size_t toff = 0, doff = 0, soff = 0;
-  // launch classes by the LDS the distinct 8-mers need
-  static const int kBuckets[] = {1024, 2048, 4096, 8192, 16384};
+  static const int kBuckets[] = {1024, 2048, 4096, 8192, 16384};  // launch classes by LDS
   std::map<int, std::vector<int>> classes;
   for (int i = 0; i < n; i++) {
     const gmapdp_oligo_problem& p = problems[i];
@@ -1615,6 +1633,7 @@ int gmapdp_oligo_mappings_batch(gmapdp_ctx* ctx, const gmapdp_oligo_problem* pro
     d.plusp = p.plusp ? 1 : 0;
     d.minor = p.minor ? 1 : 0;
     d.umax = umax;
+    d.index = i;
     d.table_offset = (int64_t)toff;
     d.diag_offset = (int64_t)doff;
     d.scratch_offset = (int64_t)soff;
@@ -1623,47 +1642,89 @@ int gmapdp_oligo_mappings_batch(gmapdp_ctx* ctx, const gmapdp_oligo_problem* pro
     soff += align_up(scratch_bytes_oi(p.querylength, p.chrend > p.chrstart ? p.chrend - p.chrstart : 0), 256);
     classes[umax].push_back(i);
   }
-  if (toff > positions_capacity || doff > diagonal_capacity || (toff && !positions) || (doff && !diagonals))
-    return bad(ctx, "positions or diagonal arena too small");
   if (toff > 0x7fffffffull) return bad(ctx, "stage-2 table arena beyond 2^31 entries");
-  // problems grouped by class; results come back in that order
+  gmapdp_oligo_plan* P = new gmapdp_oligo_plan();
+  P->n = n;
+  P->table_cap = toff;
+  P->diag_cap = doff;
   std::vector<DevOligoProblem> ord;
-  std::vector<int> ord_problem;
-  std::vector<std::pair<int, int>> launches;  // (first, count) per class
-  std::vector<int> lumax;
+  ord.reserve(n);
   for (auto& kv : classes) {
-    launches.push_back({(int)ord.size(), (int)kv.second.size()});
-    lumax.push_back(kv.first);
-    for (int i : kv.second) {
-      ord.push_back(dev[i]);
-      ord_problem.push_back(i);
-    }
+    P->launches.push_back({(int)ord.size(), (int)kv.second.size()});
+    P->umax.push_back(kv.first);
+    for (int i : kv.second) ord.push_back(dev[i]);
   }
-  hipError_t e = ctx->oprobs.ensure(sizeof(DevOligoProblem) * n);
-  if (e == hipSuccess) e = ctx->oresults.ensure(sizeof(gmapdp_oligo_result) * n);
-  if (e == hipSuccess) e = ctx->oscratch.ensure(std::max<size_t>(soff, 256));
+  hipError_t e = hipMalloc(&P->d_probs, sizeof(DevOligoProblem) * std::max(n, 1));
+  if (e == hipSuccess) e = hipMalloc(&P->d_scratch, std::max<size_t>(soff, 256));
+  if (e == hipSuccess && n)
+    e = hipMemcpy(P->d_probs, ord.data(), sizeof(DevOligoProblem) * n, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    oligo_plan_free(P);
+    return fail(ctx, GMAPDP_ENOMEM, "oligo plan: %s", e);
+  }
+  *plan = P;
+  return GMAPDP_OK;
+}
+
+size_t gmapdp_oligo_plan_positions_capacity(const gmapdp_oligo_plan* plan) { return plan ? plan->table_cap : 0; }
+size_t gmapdp_oligo_plan_diagonal_capacity(const gmapdp_oligo_plan* plan) { return plan ? plan->diag_cap : 0; }
+int gmapdp_oligo_plan_nlaunches(const gmapdp_oligo_plan* plan) { return plan ? (int)plan->launches.size() : 0; }
+void gmapdp_oligo_plan_destroy(gmapdp_oligo_plan* plan) { oligo_plan_free(plan); }
+
+int gmapdp_oligo_plan_run(gmapdp_ctx* ctx, const gmapdp_oligo_plan* plan, const char* d_qseq_uc,
+                          gmapdp_oligo_result* d_results, int32_t* d_npositions, int32_t* d_mappings,
+                          uint32_t* d_positions, int32_t* d_diagonals, void* stream) {
+  if (!ctx || !plan) return GMAPDP_EINVAL;
+  if (plan->n == 0) return GMAPDP_OK;
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  for (size_t li = 0; li < plan->launches.size(); li++) {
+    const hipError_t e = launch_oi(plan->launches[li].second, lds_bytes_oi(plan->umax[li]), s,
+                                   plan->d_probs + plan->launches[li].first, ctx->d_genome, d_qseq_uc,
+                                   plan->d_scratch, d_results, d_npositions, d_mappings, d_positions, d_diagonals);
+    if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "oligo launch: %s", e);
+  }
+  return GMAPDP_OK;
+}
+
+int gmapdp_oligo_mappings_batch(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problems, int n, const char* qseq_uc,
+                                size_t qbytes, gmapdp_oligo_result* results, int32_t* npositions, int32_t* mappings,
+                                uint32_t* positions, size_t positions_capacity, int32_t* diagonals,
+                                size_t diagonal_capacity) {
+  if (!ctx || n < 0 || (n > 0 && (!problems || !results || !qseq_uc || !npositions || !mappings)))
+    return GMAPDP_EINVAL;
+  if (!ctx->d_genome) return GMAPDP_ENOGENOME;
+  if (n == 0) return GMAPDP_OK;
+  gmapdp_oligo_plan* plan = nullptr;
+  int rc = gmapdp_oligo_plan_create(ctx, problems, n, qseq_uc, qbytes, &plan);
+  if (rc) return rc;
+  const size_t toff = plan->table_cap, doff = plan->diag_cap;
+  if (toff > positions_capacity || doff > diagonal_capacity || (toff && !positions) || (doff && !diagonals)) {
+    oligo_plan_free(plan);
+    return bad(ctx, "positions or diagonal arena too small");
+  }
+  hipError_t e = ctx->oresults.ensure(sizeof(gmapdp_oligo_result) * n);
   if (e == hipSuccess) e = ctx->onpos.ensure(sizeof(int32_t) * qbytes);
   if (e == hipSuccess) e = ctx->omap.ensure(sizeof(int32_t) * qbytes);
   if (e == hipSuccess) e = ctx->otable.ensure(sizeof(uint32_t) * std::max<size_t>(toff, 1));
   if (e == hipSuccess) e = ctx->odiag.ensure(4 * sizeof(int32_t) * std::max<size_t>(doff, 1));
   if (e == hipSuccess) e = ctx->qseq_uc.ensure(qbytes);
-  if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "device buffers: %s", e);
   hipStream_t s = ctx->stream;
-  e = hipMemcpyAsync(ctx->oprobs.p, ord.data(), sizeof(DevOligoProblem) * n, hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipMemcpyAsync(ctx->qseq_uc.p, qseq_uc, qbytes, hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipMemsetAsync(ctx->onpos.p, 0, sizeof(int32_t) * qbytes, s);
   if (e == hipSuccess) e = hipMemsetAsync(ctx->omap.p, 0xff, sizeof(int32_t) * qbytes, s);
-  if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "upload: %s", e);
-  for (size_t li = 0; li < launches.size(); li++) {
-    const int first = launches[li].first, count = launches[li].second;
-    e = launch_oi(count, lds_bytes_oi(lumax[li]), s, (const DevOligoProblem*)ctx->oprobs.p + first, ctx->d_genome,
-                  (const char*)ctx->qseq_uc.p, (unsigned char*)ctx->oscratch.p,
-                  (gmapdp_oligo_result*)ctx->oresults.p + first, (int32_t*)ctx->onpos.p, (int32_t*)ctx->omap.p,
-                  (uint32_t*)ctx->otable.p, (int32_t*)ctx->odiag.p);
-    if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "oligo launch: %s", e);
+  if (e != hipSuccess) {
+    oligo_plan_free(plan);
+    return fail(ctx, GMAPDP_ENOMEM, "oligo buffers: %s", e);
   }
-  std::vector<gmapdp_oligo_result> dres(n);
-  e = hipMemcpyAsync(dres.data(), ctx->oresults.p, sizeof(gmapdp_oligo_result) * n, hipMemcpyDeviceToHost, s);
+  rc = gmapdp_oligo_plan_run(ctx, plan, (const char*)ctx->qseq_uc.p, (gmapdp_oligo_result*)ctx->oresults.p,
+                             (int32_t*)ctx->onpos.p, (int32_t*)ctx->omap.p, (uint32_t*)ctx->otable.p,
+                             (int32_t*)ctx->odiag.p, nullptr);
+  if (rc) {
+    oligo_plan_free(plan);
+    return rc;
+  }
+  e = hipMemcpyAsync(results, ctx->oresults.p, sizeof(gmapdp_oligo_result) * n, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipMemcpyAsync(npositions, ctx->onpos.p, sizeof(int32_t) * qbytes, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipMemcpyAsync(mappings, ctx->omap.p, sizeof(int32_t) * qbytes, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess && toff)
@@ -1671,8 +1732,8 @@ int gmapdp_oligo_mappings_batch(gmapdp_ctx* ctx, const gmapdp_oligo_problem* pro
   if (e == hipSuccess && doff)
     e = hipMemcpyAsync(diagonals, ctx->odiag.p, 4 * sizeof(int32_t) * doff, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
+  oligo_plan_free(plan);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "oligo execution: %s", e);
-  for (int k = 0; k < n; k++) results[ord_problem[k]] = dres[k];
   return GMAPDP_OK;
 }
 

@@ -140,7 +140,7 @@ struct DevOligoProblem {
   int32_t plusp;
   int32_t minor;          // oligoindices_minor (diag_lookback 60, suffnconsecutive 10), else major (120, 20)
   int32_t umax;           // LDS slots for the query's distinct 8-mers (>= their number)
-  int32_t pad_;
+  int32_t index;          // the problem's index in the batch (its result slot)
   int64_t table_offset;   // first entry of the problem's table in the positions arena
   int64_t diag_offset;    // first diagonal record (4 x int32)
   int64_t scratch_offset; // byte offset of the problem's region of the global scratch

@@ -303,7 +303,7 @@ __global__ __launch_bounds__(64) void oi_kernel(
     res.ndiagonals = ngood;
   }
   res.totalpositions = totalpositions;
-  if (lane == 0) results[blockIdx.x] = res;
+  if (lane == 0) results[P.index] = res;
 }
 
 size_t lds_bytes_oi(int umax) { return 6 * (size_t)kOiWords + 8 * (size_t)umax; }

@@ -170,6 +170,14 @@ def load_library(path=LIB_PATH):
                                                   C.c_void_p, C.c_size_t]),
         "gmapdp_oligo_positions_capacity": (C.c_size_t, [C.c_void_p, C.c_int]),
         "gmapdp_oligo_diagonal_capacity": (C.c_size_t, [C.c_void_p, C.c_int]),
+        "gmapdp_oligo_plan_create": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_size_t,
+                                               P(C.c_void_p)]),
+        "gmapdp_oligo_plan_positions_capacity": (C.c_size_t, [C.c_void_p]),
+        "gmapdp_oligo_plan_diagonal_capacity": (C.c_size_t, [C.c_void_p]),
+        "gmapdp_oligo_plan_nlaunches": (C.c_int, [C.c_void_p]),
+        "gmapdp_oligo_plan_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                            C.c_void_p, C.c_void_p, C.c_void_p]),
+        "gmapdp_oligo_plan_destroy": (None, [C.c_void_p]),
         "gmapdp_genome_prob_entries": (C.c_size_t, [C.c_void_p, C.c_int]),
         "gmapdp_genome_splice_sites": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t]),
         "gmapdp_plan_create_all": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p,

@@ -29,7 +29,8 @@
  *                            (oligoindex_hr.c:33849/34127) as Stage2_compute calls them (stage2.c:6480-6495)
  *
  * Semantics: every result is bit-identical to the reference's nosimd build
- * (Dynprog_standard + Dynprog_traceback_std); see DESIGN.md "Parity".
+ * (Dynprog_standard + Dynprog_traceback_std), or with GMAPDP_SIMD to its SIMD builds
+ * (dynprog_simd.c); stage-2 seeding has one semantics (both builds agree); see DESIGN.md "Parity".
  *
  * Errors: functions return 0 on success and a negative GMAPDP_E* code on
  * failure (no errno).  A per-problem NULL result (the reference returning a
@@ -333,6 +334,21 @@ int gmapdp_oligo_mappings_batch (gmapdp_ctx *ctx, const gmapdp_oligo_problem *pr
 /* Table entries / diagonal records (4 x int32) a batch may need. */
 size_t gmapdp_oligo_positions_capacity (const gmapdp_oligo_problem *problems, int n);
 size_t gmapdp_oligo_diagonal_capacity (const gmapdp_oligo_problem *problems, int n);
+/* Device-resident path (bench / pipelined callers): plan once (distinct 8-mers, launch classes,
+ * table / diagonal / scratch offsets; the descriptors are uploaded), then run asynchronously on
+ * `stream` (hipStream_t; NULL = the context's stream) against a device-resident upper-case query
+ * arena.  d_results has n entries in problem order; d_npositions / d_mappings are indexed like the
+ * query arena; d_positions / d_diagonals hold the plan's capacities. */
+typedef struct gmapdp_oligo_plan gmapdp_oligo_plan;
+int gmapdp_oligo_plan_create (gmapdp_ctx *ctx, const gmapdp_oligo_problem *problems, int n, const char *qseq_uc,
+                              size_t qbytes, gmapdp_oligo_plan **plan);
+size_t gmapdp_oligo_plan_positions_capacity (const gmapdp_oligo_plan *plan);
+size_t gmapdp_oligo_plan_diagonal_capacity (const gmapdp_oligo_plan *plan);
+int gmapdp_oligo_plan_nlaunches (const gmapdp_oligo_plan *plan);
+int gmapdp_oligo_plan_run (gmapdp_ctx *ctx, const gmapdp_oligo_plan *plan, const char *d_qseq_uc,
+                           gmapdp_oligo_result *d_results, int32_t *d_npositions, int32_t *d_mappings,
+                           uint32_t *d_positions, int32_t *d_diagonals, void *stream);
+void gmapdp_oligo_plan_destroy (gmapdp_oligo_plan *plan);
 
 /* Create a context on HIP device `device`.  mode = Mode_T (mode.h:5;
  * 0 = STANDARD).  user_* mirror Dynprog_single_setup. */

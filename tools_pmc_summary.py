@@ -21,7 +21,7 @@ from collections import defaultdict
 
 def short(name):
     """'void gmapdp::dpx_kernel<16, true>(...)' -> 'gmapdp::dpx_kernel<16, true>'."""
-    m = re.match(r"(?:void )?(gmapdp::\w+<[^>]*>)", name)
+    m = re.match(r"(?:void )?(gmapdp::\w+(?:<[^>]*>)?)", name)
     return m.group(1) if m else None
 
 
