@@ -225,6 +225,7 @@ __global__ __launch_bounds__(64) void oi_kernel(
     cumrun += __builtin_amdgcn_readlane(incl, 63);
     totalpositions += __builtin_amdgcn_readlane(wave_scan_add(lane, nh > 0 ? nh : 0), 63);
   }
+  __threadfence_block();
   if (P.chrend > P.chrstart) {
     const int diag_lookback = P.minor ? 60 : 120, suffn = P.minor ? 10 : 20;
     const uint32_t chrinit = P.plusp ? P.chrstart : (P.chrhigh - P.chroffset) - P.chrend;
@@ -236,52 +237,67 @@ __global__ __launch_bounds__(64) void oi_kernel(
     __threadfence_block();
     int32_t* good = diag_all + 4 * P.diag_offset;  // diagi of each good diagonal, in field 0 of its record
     int ngood = 0, maxn = 0, best = -1;
-    for (int q = 0; q < nq; q++) {
-      const int nh = npq[q];
-      if (nh <= 0) continue;
-      const uint32_t* hits = table + (mpq[q] - (int32_t)P.table_offset);
-      const int cq = cum[q];
-      for (int base = 0; base < nh; base += 64) {
-        const int h = base + lane;
-        int reached = 0, nb = 0;
-        uint32_t diagi = 0;
-        if (h < nh) {
-          diagi = hits[h] + (uint32_t)(qlen - q) - chrinit;
-          OiState s;
-          if (!initp[diagi]) {
-            initp[diagi] = 1;
-            s.querypos = -diag_lookback;  // the first check is never consecutive
-            s.best_n = s.n = s.cstart = s.best_start = s.best_end = 0;
-          } else {
-            s = st[diagi];
+    // query positions in chunks of 64: one coalesced load of their nhits, table offsets, cum_nohits
+    // and first hits, then the sequential walk takes them by readlane (off the latency chain)
+    for (int cb = 0; cb < nq; cb += 64) {
+      const int qi = cb + lane;
+      int c_nh = 0, c_mo = 0, c_cum = 0;
+      uint32_t c_h0 = 0;
+      if (qi < nq) {
+        c_nh = npq[qi];
+        c_mo = mpq[qi];
+        c_cum = cum[qi];
+        if (c_nh > 0) c_h0 = table_all[c_mo];
+      }
+      const int cend = min(64, nq - cb);
+      for (int j = 0; j < cend; j++) {
+        const int nh = __builtin_amdgcn_readlane(c_nh, j);
+        if (nh <= 0) continue;
+        const int q = cb + j;
+        const int mo = __builtin_amdgcn_readlane(c_mo, j);
+        const int cq = __builtin_amdgcn_readlane(c_cum, j);
+        const uint32_t h0 = (uint32_t)__builtin_amdgcn_readlane((int)c_h0, j);
+        for (int base = 0; base < nh; base += 64) {
+          const int h = base + lane;
+          int reached = 0, nb = 0;
+          uint32_t diagi = 0;
+          if (h < nh) {
+            diagi = (h == 0 ? h0 : table_all[mo + h]) + (uint32_t)(qlen - q) - chrinit;
+            const unsigned char ini = initp[diagi];
+            OiState s = st[diagi];  // loaded with the flag; ignored when the flag is clear
+            if (!ini) {
+              initp[diagi] = 1;
+              s.querypos = -diag_lookback;  // the first check is never consecutive
+              s.best_n = s.n = s.cstart = s.best_start = s.best_end = 0;
+            }
+            if (s.querypos < 0) {
+              s.n = 0;
+              s.cstart = q;
+            } else if (q - s.querypos >= diag_lookback + cq - cum[s.querypos]) {
+              s.n = 0;
+              s.cstart = q;
+            } else if (++s.n > s.best_n) {
+              s.best_start = s.cstart;
+              s.best_end = q;
+              s.best_n = s.n;
+              reached = (s.best_n == suffn);
+              nb = s.best_n;
+            }
+            s.querypos = q;
+            st[diagi] = s;
           }
-          if (s.querypos < 0) {
-            s.n = 0;
-            s.cstart = q;
-          } else if (q - s.querypos >= diag_lookback + cq - cum[s.querypos]) {
-            s.n = 0;
-            s.cstart = q;
-          } else if (++s.n > s.best_n) {
-            s.best_start = s.cstart;
-            s.best_end = q;
-            s.best_n = s.n;
-            reached = (s.best_n == suffn);
-            nb = s.best_n;
-          }
-          s.querypos = q;
-          st[diagi] = s;
-        }
-        // the good list in lane order; the global best: the first lane reaching the new maximum
-        const uint64_t rm = ballot(reached);
-        if (reached) good[4 * (ngood + lanes_below(rm, lane))] = (int32_t)diagi;
-        ngood += __popcll(rm);
-        int mx = nb;
+          // the good list in lane order; the global best: the first lane reaching the new maximum
+          const uint64_t rm = ballot(reached);
+          if (reached) good[4 * (ngood + lanes_below(rm, lane))] = (int32_t)diagi;
+          ngood += __popcll(rm);
+          int mx = nb;
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) mx = max(mx, __shfl_xor(mx, off, 64));
-        if (mx > maxn) {
-          const int l = __ffsll((long long)ballot(nb == mx)) - 1;
-          best = __builtin_amdgcn_readlane((int)diagi, l);
-          maxn = mx;
+          for (int off = 32; off >= 1; off >>= 1) mx = max(mx, __shfl_xor(mx, off, 64));
+          if (mx > maxn) {
+            const int l = __ffsll((long long)ballot(nb == mx)) - 1;
+            best = __builtin_amdgcn_readlane((int)diagi, l);
+            maxn = mx;
+          }
         }
       }
     }
