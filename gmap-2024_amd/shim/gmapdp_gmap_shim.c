@@ -5,7 +5,8 @@
  *
  *   -Wl,--wrap=Dynprog_init,--wrap=Dynprog_single_setup,--wrap=Dynprog_end_setup,
  *   -Wl,--wrap=Dynprog_genome_setup,--wrap=Dynprog_single_gap,--wrap=Dynprog_end5_gap,
- *   -Wl,--wrap=Dynprog_end3_gap,--wrap=Dynprog_genome_gap,--wrap=Dynprog_cdna_gap  -lgmapdp
+ *   -Wl,--wrap=Dynprog_end3_gap,--wrap=Dynprog_genome_gap,--wrap=Dynprog_cdna_gap
+ *   -Wl,--wrap=Oligoindex_hr_tally,--wrap=Oligoindex_get_mappings  -lgmapdp
  *
  * so that every call GMAP's stage 3 makes to these functions (stage3.c:9081,
  * 9275, 9510, 9531, 10244-10600, ...) lands here with the reference's own signature
@@ -50,6 +51,8 @@
 #include "dynprog_end.h"
 #include "dynprog_genome.h"
 #include "dynprog_cdna.h"
+#include "oligoindex_hr.h"
+#include "diagpool.h"
 
 #include "gmapdp.h"
 #include "gmapdp_dynprog.h"
@@ -136,7 +139,7 @@ shim_context (Genome_T genome, Genome_T genomealt, Dynprog_T dynprog) {
   uint64_t length;
   size_t nwords;
   if (genomealt != NULL && genomealt != genome) shim_refuse("an alternate-allele genome (genomealt)");
-  if (dynprog->max_rlength != GMAPDP_MAX_RLENGTH || dynprog->max_glength != GMAPDP_MAX_GLENGTH)
+  if (dynprog != NULL && (dynprog->max_rlength != GMAPDP_MAX_RLENGTH || dynprog->max_glength != GMAPDP_MAX_GLENGTH))
     shim_refuse("a Dynprog_T with non-default maximum lengths");
   if (shim_ctx == NULL) {
     dev = getenv("GMAPDP_DEVICE");
@@ -447,4 +450,108 @@ __wrap_Dynprog_cdna_gap (int *dynprogindex, int *traceback_score, bool *incomple
   if (res.traceback_score != GMAPDP_UNSET) *traceback_score = res.traceback_score;
   if (res.incompletep) *incompletep = true;
   return list;
+}
+
+/* ---- stage-2 seeding: Oligoindex_hr_tally + Oligoindex_get_mappings (oligoindex_hr.c:33849/34127) ----
+   Stage2_compute (stage2.c:6480-6495) calls the tally and then get_mappings for the same window; the
+   tally only records its arguments here and the GPU runs both in get_mappings.  The table is allocated
+   with GMAP's own MALLOC as this->table, so Oligoindex_untally frees it as usual. */
+static struct {
+  Oligoindex_T oligoindex;
+  Univcoord_T mappingstart, mappingend;
+  Chrpos_T chrpos;
+  bool plusp;
+  int querystart, queryend;
+  Genome_T genome;
+} shim_tally;
+
+void
+__wrap_Oligoindex_hr_tally (Oligoindex_T this, Univcoord_T mappingstart, Univcoord_T mappingend, bool plusp,
+                            char *queryuc_ptr, int querystart, int queryend, Chrpos_T chrpos, Genome_T genome,
+                            int genestrand) {
+  (void) queryuc_ptr;
+  (void) genestrand;
+  if (shim_mode != 0) shim_refuse("stage-2 seeding outside STANDARD mode (cmet / atoi / ttoc reductions)");
+  if (this->indexsize != 8) shim_refuse("an oligoindex with indexsize other than 8");
+  shim_tally.oligoindex = this;
+  shim_tally.mappingstart = mappingstart;
+  shim_tally.mappingend = mappingend;
+  shim_tally.plusp = plusp;
+  shim_tally.chrpos = chrpos;
+  shim_tally.querystart = querystart;
+  shim_tally.queryend = queryend;
+  shim_tally.genome = genome;
+  this->table = NULL;
+}
+
+List_T
+__wrap_Oligoindex_get_mappings (List_T diagonals, bool *coveredp, Chrpos_T **mappings, int *npositions,
+                                int *totalpositions, bool *oned_matrix_p, int *maxnconsecutive,
+                                Oligoindex_array_T array, Oligoindex_T this, char *queryuc_ptr, int querystart,
+                                int queryend, int querylength, Chrpos_T chrstart, Chrpos_T chrend,
+                                Univcoord_T chroffset, Univcoord_T chrhigh, bool plusp, Diagpool_T diagpool) {
+  gmapdp_oligo_problem p;
+  gmapdp_oligo_result res;
+  int32_t *np, *mp, *dg;
+  uint32_t *pos;
+  size_t pc, dc;
+  int q, k;
+  (void) array;
+  if (this != shim_tally.oligoindex || plusp != shim_tally.plusp || querystart != 0 || queryend != querylength ||
+      shim_tally.querystart != 0 || shim_tally.queryend != querylength ||
+      shim_tally.mappingstart != chroffset + chrstart ||
+      shim_tally.mappingend != chroffset + chrend + (plusp ? 0 : 1) ||
+      shim_tally.chrpos != (plusp ? chrstart : (Chrpos_T) (chrhigh - chroffset) - chrend))
+    shim_refuse("Oligoindex_get_mappings on another window than Stage2_compute's tally");
+  if (*totalpositions != 0 || *maxnconsecutive != 0) shim_refuse("a second oligoindex source (coverage loop)");
+  for (q = 0; q < querylength; q++)
+    if (coveredp[q]) shim_refuse("stage-2 seeding with covered query positions");
+  memset(&p, 0, sizeof(p));
+  p.qoff = 0;
+  p.querylength = querylength;
+  p.chrstart = chrstart;
+  p.chrend = chrend;
+  p.chroffset = (uint32_t) chroffset;
+  p.chrhigh = (uint32_t) chrhigh;
+  p.plusp = plusp ? 1 : 0;
+  p.minor = this->diag_lookback == 60 ? 1 : 0;  /* Oligoindex_array_new_minor's index (oligoindex_hr.c:8612) */
+  pthread_mutex_lock(&shim_lock);
+  shim_context(shim_tally.genome, NULL, NULL);
+  pc = gmapdp_oligo_positions_capacity(&p, 1);
+  dc = gmapdp_oligo_diagonal_capacity(&p, 1);
+  np = (int32_t *) malloc((querylength + 1) * sizeof(int32_t));
+  mp = (int32_t *) malloc((querylength + 1) * sizeof(int32_t));
+  pos = (uint32_t *) malloc((pc ? pc : 1) * sizeof(uint32_t));
+  dg = (int32_t *) malloc(4 * (dc ? dc : 1) * sizeof(int32_t));
+  shim_check(gmapdp_oligo_mappings_batch(shim_ctx, &p, 1, queryuc_ptr, (size_t) querylength, &res, np, mp, pos, pc,
+                                         dg, dc), "gmapdp_oligo_mappings_batch");
+  pthread_mutex_unlock(&shim_lock);
+  /* the table, owned by the oligoindex (freed by Oligoindex_untally) */
+  this->table = NULL;
+  if (pc > 0) {
+    this->table = (Chrpos_T *) MALLOC(pc * sizeof(Chrpos_T));
+    memcpy(this->table, pos, pc * sizeof(Chrpos_T));
+  }
+  for (q = 0; q < querylength; q++) {
+    if (np[q] > 0) {
+      npositions[q] = np[q];
+      mappings[q] = &this->table[mp[q]];
+    } else if (q <= querylength - 8 && strspn(queryuc_ptr + q, "ACGT") >= 8) {
+      /* lookup (:34069) on a full 8-mer without hits: nhits 0, mappings NULL; others stay as given */
+      npositions[q] = 0;
+      mappings[q] = NULL;
+    }
+  }
+  *totalpositions = res.totalpositions;
+  *maxnconsecutive = res.maxnconsecutive;
+  if (chrend > chrstart) *oned_matrix_p = res.oned_matrix_p ? true : false;
+  for (k = res.ndiagonals - 1; k >= 0; k--) {
+    const int32_t *d = dg + 4 * (res.diag_offset + k);
+    diagonals = Diagpool_push(diagonals, diagpool, d[0], d[1], d[2], d[3]);
+  }
+  free(np);
+  free(mp);
+  free(pos);
+  free(dg);
+  return diagonals;
 }

@@ -98,7 +98,8 @@ all: $(foreach v,$(VARIANTS),$(OUT)/librefdp_$(v).so) \
 # GMAP shim (gmap-2024_amd/shim, compiled against the reference's headers exactly as a GMAP
 # build would) and libgmapdp.so.  Tests call it through the same refh_* entry points.
 WRAPPED    := Dynprog_init Dynprog_single_setup Dynprog_end_setup Dynprog_genome_setup \
-              Dynprog_single_gap Dynprog_end5_gap Dynprog_end3_gap Dynprog_genome_gap Dynprog_cdna_gap
+              Dynprog_single_gap Dynprog_end5_gap Dynprog_end3_gap Dynprog_genome_gap Dynprog_cdna_gap \
+              Oligoindex_hr_tally Oligoindex_get_mappings
 
 $(OUT)/gpushim/gmapdp_gmap_shim.o: $(SHIM_SRC) ../include/gmapdp.h
 	@mkdir -p $(dir $@)

@@ -93,3 +93,19 @@ def test_shim_simd_build_all_entry_points():
         if shim.cdna_gap(p) != ref.cdna_gap(p):
             bad.append(("cdna", i))
     assert bad == []
+
+
+def test_shim_stage2_seeding():
+    """Stage2_compute's Oligoindex_hr_tally + Oligoindex_get_mappings routed to oi_kernel."""
+    from dpbind import oligo_problem
+    ref = Ref("nosimd")
+    shim = Ref("gpushim")
+    rng = random.Random(1010)
+    g = bytearray(random_genome(rng, 120000))
+    g[60000:61000] = b"A" * 1000
+    g = bytes(g)
+    ref.set_genome(g)
+    shim.set_genome(g)
+    probs = [oligo_problem(rng, g, edge=(i % 4 == 0)) for i in range(150)]
+    bad = [i for i, p in enumerate(probs) if shim.oligo_mappings(p) != ref.oligo_mappings(p)]
+    assert bad == []
