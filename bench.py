@@ -700,8 +700,8 @@ def main():
                      "frac": obytes / (oms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": otraffic, "traffic_source": osrc,
                      "kernel": "oi_kernel", "dispatches": nol * osteps, "kernel_ms_per_launch": oms / max(nol, 1),
                      "algorithmic_bytes_per_launch": obytes / max(nol, 1),
-                     "note": "one wave per read: LDS-atomic counting sort of the window's 8-mers + the sequential "
-                             "get_mappings state machine; latency-bound (DESIGN.md)"}}
+                     "note": "one wave per read: LDS-atomic counting sort of the window's 8-mers + get_mappings "
+                             "as a diagonal radix sort and segmented scans; latency-bound (DESIGN.md)"}}
     lib.gmapdp_oligo_plan_destroy(oplan)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["stage2_seeding"]["cpu_baseline"] = cpu_baseline_stage2(op, oq, genome)

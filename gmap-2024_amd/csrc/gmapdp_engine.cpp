@@ -71,7 +71,8 @@ size_t lds_bytes_oi(int umax);
 size_t scratch_bytes_oi(int querylength, uint32_t genomiclength);
 hipError_t launch_oi(int nproblems, size_t lds, hipStream_t stream, const DevOligoProblem* probs,
                      const uint32_t* blocks, const char* quc, unsigned char* scratch, gmapdp_oligo_result* results,
-                     int32_t* npos, int32_t* map, uint32_t* table, int32_t* diags);
+                     int32_t* npos, int32_t* map, uint32_t* table, int32_t* diags, uint64_t* pool,
+                     unsigned long long* pool_counter, unsigned long long pool_cap);
 static const int kUse8pSize[4] = {41, 63, 127, 24};  // use8p_size (dynprog.c:1022-1025)
 
 // ---------------------------------------------------------------------------
@@ -1586,12 +1587,19 @@ struct gmapdp_oligo_plan {
   std::vector<std::pair<int, int>> launches;  // (first, count)
   std::vector<int> umax;
   size_t table_cap = 0, diag_cap = 0;
+  // get_mappings' event pool (5 slots per hit, shared by the batch through an atomic cursor; a
+  // problem that no longer fits runs the sequential walk in its own scratch instead)
+  uint64_t* d_pool = nullptr;
+  unsigned long long* d_pool_counter = nullptr;
+  unsigned long long pool_cap = 0;
 };
 
 static void oligo_plan_free(gmapdp_oligo_plan* p) {
   if (!p) return;
   if (p->d_probs) (void)hipFree(p->d_probs);
   if (p->d_scratch) (void)hipFree(p->d_scratch);
+  if (p->d_pool) (void)hipFree(p->d_pool);
+  if (p->d_pool_counter) (void)hipFree(p->d_pool_counter);
   delete p;
 }
 
@@ -1605,7 +1613,7 @@ int gmapdp_oligo_plan_create(gmapdp_ctx* ctx, const gmapdp_oligo_problem* proble
   (void)hipSetDevice(ctx->device);
   std::vector<uint32_t> bm(2048, 0u);
   std::vector<DevOligoProblem> dev(n);
-  size_t toff = 0, doff = 0, soff = 0;
+  size_t toff = 0, doff = 0, soff = 0, pslots = 0;
   static const int kBuckets[] = {1024, 2048, 4096, 8192, 16384};  // launch classes by LDS
   std::map<int, std::vector<int>> classes;
   for (int i = 0; i < n; i++) {
@@ -1638,6 +1646,7 @@ int gmapdp_oligo_plan_create(gmapdp_ctx* ctx, const gmapdp_oligo_problem* proble
     d.diag_offset = (int64_t)doff;
     d.scratch_offset = (int64_t)soff;
     toff += oligo_table_cap(p);
+    pslots += 5 * std::min<size_t>(oligo_table_cap(p), 2 * (size_t)p.querylength + 256);  // hits ~ query 8-mers
     doff += oligo_diag_cap(p);
     soff += align_up(scratch_bytes_oi(p.querylength, p.chrend > p.chrstart ? p.chrend - p.chrstart : 0), 256);
     classes[umax].push_back(i);
@@ -1656,6 +1665,10 @@ int gmapdp_oligo_plan_create(gmapdp_ctx* ctx, const gmapdp_oligo_problem* proble
   }
   hipError_t e = hipMalloc(&P->d_probs, sizeof(DevOligoProblem) * std::max(n, 1));
   if (e == hipSuccess) e = hipMalloc(&P->d_scratch, std::max<size_t>(soff, 256));
+  if (const char* ev = std::getenv("GMAPDP_OLIGO_POOL_SLOTS")) pslots = std::strtoull(ev, nullptr, 10);  // tests
+  P->pool_cap = pslots;
+  if (e == hipSuccess) e = hipMalloc(&P->d_pool, sizeof(uint64_t) * std::max<size_t>(pslots, 1));
+  if (e == hipSuccess) e = hipMalloc(&P->d_pool_counter, sizeof(unsigned long long));
   if (e == hipSuccess && n)
     e = hipMemcpy(P->d_probs, ord.data(), sizeof(DevOligoProblem) * n, hipMemcpyHostToDevice);
   if (e != hipSuccess) {
@@ -1678,10 +1691,13 @@ int gmapdp_oligo_plan_run(gmapdp_ctx* ctx, const gmapdp_oligo_plan* plan, const 
   if (plan->n == 0) return GMAPDP_OK;
   (void)hipSetDevice(ctx->device);
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  if (hipMemsetAsync(plan->d_pool_counter, 0, sizeof(unsigned long long), s) != hipSuccess)
+    return fail(ctx, GMAPDP_ELAUNCH, "oligo pool reset: %s", hipGetLastError());
   for (size_t li = 0; li < plan->launches.size(); li++) {
     const hipError_t e = launch_oi(plan->launches[li].second, lds_bytes_oi(plan->umax[li]), s,
                                    plan->d_probs + plan->launches[li].first, ctx->d_genome, d_qseq_uc,
-                                   plan->d_scratch, d_results, d_npositions, d_mappings, d_positions, d_diagonals);
+                                   plan->d_scratch, d_results, d_npositions, d_mappings, d_positions, d_diagonals,
+                                   plan->d_pool, plan->d_pool_counter, plan->pool_cap);
     if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "oligo launch: %s", e);
   }
   return GMAPDP_OK;

@@ -21,9 +21,9 @@
 // complement is its bitwise complement, the forward oligo its 2-bit reversal.  Pass 1 counts per id
 // (LDS atomics); an exclusive scan lays out the table; pass 2 walks the window in descending chrpos
 // in 64-position tiles and places each tile's hits in lane order (scalar loop over the ballot), which
-// reproduces the reference's keep-the-nearest-`count` rule exactly.  get_mappings then runs query
-// position by query position -- its state machine is sequential along the query -- with the hits of
-// one position (distinct diagonals) in parallel lanes, per-diagonal state in an L2-resident scratch.
+// reproduces the reference's keep-the-nearest-`count` rule exactly.  get_mappings sorts the hits by
+// diagonal and evaluates each diagonal's state machine with segmented scans (oi_mappings_sorted); a
+// problem that does not fit the batch's event pool walks the query sequentially instead.
 #include "dp_device.h"
 
 namespace gmapdp {
@@ -88,10 +88,225 @@ __host__ __device__ inline ScratchOi scratch_oi(int querylength, uint32_t genomi
   return s;
 }
 
+// ---- get_mappings over events sorted by diagonal ----
+// The reference visits the hits query position by query position; a diagonal's state only ever sees
+// its own hits, in ascending querypos.  So the events (diagi, querypos), generated in query order and
+// stably sorted by diagi, put every diagonal's hits in one contiguous segment in the order the
+// reference visits them, and its consecutive-run state becomes segmented scans:
+//   a run starts at the diagonal's first hit and wherever q - q_prev >= diag_lookback + cum[q] - cum[q_prev];
+//   n after a hit = its distance from the run start; best_nconsecutive = the segment's maximum n,
+//   reached first at the first hit carrying it (best_end; best_start = its run's first querypos);
+//   a diagonal is good when n reaches suffnconsecutive, at the first such hit; the reference appends
+//   it there, so the good list is ordered by (querypos, diagi) of that hit (hits of one querypos are
+//   visited in ascending chrpos = ascending diagi); maxnconsecutive = the largest n, and the fallback
+//   best diagonal the one owning the first (querypos, diagi) hit with that n.
+
+// inclusive max-scan within segments [segstart, e] of consecutive lanes (64-bit values)
+__device__ __forceinline__ uint64_t seg_scan_max64(int lane, uint64_t x, int e, int segstart) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t y = __shfl_up(x, off, 64);
+    if (lane >= off && e - off >= segstart && y > x) x = y;
+  }
+  return x;
+}
+__device__ __forceinline__ int seg_scan_min(int lane, int x, int e, int segstart) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off, 64);
+    if (lane >= off && e - off >= segstart) x = min(x, y);
+  }
+  return x;
+}
+
+// Returns false (nothing written) when the shared event pool cannot hold this problem's 5 E slots.
+__device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t chrinit, int lookback, int suffn,
+                                   const int32_t* __restrict__ npq, const int32_t* __restrict__ mpq,
+                                   const int* __restrict__ cum, const uint32_t* __restrict__ table_all,
+                                   uint64_t* __restrict__ pool, unsigned long long* pool_counter,
+                                   unsigned long long pool_cap, uint32_t* hist, int32_t* __restrict__ good,
+                                   int& ngood_out, int& maxn_out) {
+  unsigned long long base = 0;
+  if (lane == 0) base = atomicAdd(pool_counter, 5ull * (unsigned long long)E);
+  base = __shfl(base, 0, 64);
+  if (base + 5ull * (unsigned long long)E > pool_cap) return false;
+  uint64_t* evA = pool + base;                                  // events (diagi << 32 | q)
+  uint64_t* evB = evA + E;                                      // radix-sort ping-pong
+  int2* rsds = reinterpret_cast<int2*>(evB + E);                // per event: run start, diagonal start
+  int2* head = rsds + E;                                        // at a diagonal's start: best n, its first event
+  int4* grec = reinterpret_cast<int4*>(head + E);               // good records before ordering (<= E/2)
+
+  // events in query order, hits of one querypos in table (ascending chrpos) order
+  int eoff = 0;
+  for (int cb = 0; cb < nq; cb += 64) {
+    const int q = cb + lane;
+    int nh = 0, mo = 0;
+    if (q < nq) {
+      nh = npq[q];
+      if (nh > 0) mo = mpq[q];
+      else nh = 0;
+    }
+    const int incl = wave_scan_add(lane, nh);
+    const int o = eoff + incl - nh;
+    for (int h = 0; h < nh; h++)
+      evA[o + h] = ((uint64_t)(table_all[mo + h] + (uint32_t)(qlen - q) - chrinit) << 32) | (uint32_t)q;
+    eoff += __builtin_amdgcn_readlane(incl, 63);
+  }
+  __threadfence_block();
+
+  // stable LSD radix sort on diagi, 8-bit digits (diagi <= qlen + genomiclength)
+  uint64_t* src = evA;
+  uint64_t* dst = evB;
+  uint32_t maxd = 0;
+  for (int e = lane; e < E; e += 64) maxd = max(maxd, (uint32_t)(evA[e] >> 32));
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) maxd = max(maxd, (uint32_t)__shfl_xor((int)maxd, off, 64));
+  for (int shift = 0; shift < 32 && (maxd >> shift) != 0; shift += 8) {
+    for (int i = lane; i < 256; i += 64) hist[i] = 0u;
+    __syncthreads();
+    for (int e = lane; e < E; e += 64) atomicAdd(&hist[(uint32_t)(src[e] >> (32 + shift)) & 255u], 1u);
+    __syncthreads();
+    uint32_t h4[4], hs = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      h4[k] = hist[4 * lane + k];
+      hs += h4[k];
+    }
+    uint32_t at = (uint32_t)wave_scan_add(lane, (int)hs) - hs;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      hist[4 * lane + k] = at;
+      at += h4[k];
+    }
+    __syncthreads();
+    for (int e0 = 0; e0 < E; e0 += 64) {
+      const int e = e0 + lane;
+      const bool v = e < E;
+      const uint64_t key = v ? src[e] : 0ull;
+      const uint32_t d = (uint32_t)(key >> (32 + shift)) & 255u;
+      uint64_t eq = ballot(v);
+#pragma unroll
+      for (int b = 0; b < 8; b++) {
+        const uint64_t m = ballot((d >> b) & 1u);
+        eq &= ((d >> b) & 1u) ? m : ~m;
+      }
+      const int rank = lanes_below(eq, lane);
+      const uint32_t pos = v ? hist[d] : 0u;  // every lane reads before any lane bumps
+      __syncthreads();
+      if (v) dst[pos + rank] = key;
+      if (v && rank == 0) hist[d] = pos + (uint32_t)__popcll(eq);
+      __syncthreads();
+    }
+    __threadfence_block();
+    uint64_t* t = src;
+    src = dst;
+    dst = t;
+  }
+  const uint64_t* S = src;
+  __threadfence_block();
+
+  // sweep: runs, diagonal maxima, the first hit reaching suffn per diagonal, the global maximum
+  int c_rs = -1, c_ds = -1, c_fs = 0x7fffffff, ngood = 0, M = 0;
+  uint64_t c_mk = 0, c_key = 0;
+  for (int e0 = 0; e0 < E; e0 += 64) {
+    const int e = e0 + lane;
+    const bool v = e < E;
+    const uint64_t key = v ? S[e] : ~0ull;
+    uint64_t pk = __shfl_up(key, 1, 64);
+    if (lane == 0) pk = c_key;
+    const uint32_t d = (uint32_t)(key >> 32), q = (uint32_t)key;
+    const bool newdiag = v && (e == 0 || (uint32_t)(pk >> 32) != d);
+    bool newrun = newdiag;
+    if (v && !newdiag) {
+      const uint32_t pq = (uint32_t)pk;
+      newrun = (int)(q - pq) >= lookback + cum[q] - cum[pq];
+    }
+    const int rs = max(wave_scan_max(newrun ? e : -1), c_rs);
+    const int ds = max(wave_scan_max(newdiag ? e : -1), c_ds);
+    const int n = e - rs;
+    if (v) rsds[e] = make_int2(rs, ds);
+    uint64_t mk = v ? (((uint64_t)(uint32_t)n << 32) | (uint64_t)(~(uint32_t)e)) : 0ull;
+    mk = seg_scan_max64(lane, mk, e, ds);
+    if (ds < e0 && c_mk > mk) mk = c_mk;
+    int fs = (v && n == suffn) ? e : 0x7fffffff;
+    fs = seg_scan_min(lane, fs, e, ds);
+    if (ds < e0) fs = min(fs, c_fs);
+    // the diagonal's last hit records its maximum at the diagonal's head
+    uint64_t nk = __shfl_down(key, 1, 64);
+    if (lane == 63) nk = (e + 1 < E) ? S[e + 1] : ~0ull;
+    if (v && (e + 1 == E || (uint32_t)(nk >> 32) != d)) head[ds] = make_int2((int)(mk >> 32), (int)~(uint32_t)mk);
+    const bool isgood = v && n == suffn && fs == e;
+    const uint64_t gm = ballot(isgood);
+    if (isgood) grec[ngood + lanes_below(gm, lane)] = make_int4(e, 0, 0, 0);
+    ngood += __popcll(gm);
+    int mx = v ? n : 0;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) mx = max(mx, __shfl_xor(mx, off, 64));
+    M = max(M, mx);
+    c_rs = __builtin_amdgcn_readlane(rs, 63);
+    c_ds = __builtin_amdgcn_readlane(ds, 63);
+    c_fs = __builtin_amdgcn_readlane(fs, 63);
+    c_mk = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(mk >> 32), 63) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mk, 63);
+    c_key = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(key >> 32), 63) << 32) |
+            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, 63);
+  }
+  __threadfence_block();
+  if (ngood == 0 && M > 0) {  // the best diagonal: the first (querypos, diagi) hit with n == M
+    uint64_t bk = ~0ull;
+    int be = -1;
+    for (int e = lane; e < E; e += 64) {
+      if (e - rsds[e].x == M) {
+        const uint64_t key = S[e];
+        const uint64_t k2 = (key << 32) | (key >> 32);
+        if (k2 < bk) {
+          bk = k2;
+          be = e;
+        }
+      }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const uint64_t ok = __shfl_xor(bk, off, 64);
+      const int oe = __shfl_xor(be, off, 64);
+      if (ok < bk) {
+        bk = ok;
+        be = oe;
+      }
+    }
+    if (lane == 0) grec[0] = make_int4(be, 0, 0, 0);
+    ngood = 1;
+  }
+  __threadfence_block();
+  // records and their (querypos, diagi) keys; then the reference's order
+  uint64_t* gkey = (S == evA) ? evB : evA;  // the free sort buffer
+  for (int g = lane; g < ngood; g += 64) {
+    const int e = grec[g].x;
+    const uint64_t key = S[e];
+    const int2 hb = head[rsds[e].y];  // (best n, the first event reaching it)
+    const int eb = hb.y;
+    const uint32_t di = (uint32_t)(key >> 32);
+    gkey[g] = (key << 32) | (key >> 32);
+    grec[g] = make_int4(di >= (uint32_t)qlen ? (int)(di - (uint32_t)qlen) : (int)((uint32_t)qlen - di),
+                        (int)(uint32_t)S[rsds[eb].x], (int)(uint32_t)S[eb], hb.x + 1);
+  }
+  __threadfence_block();
+  for (int g = lane; g < ngood; g += 64) {
+    const uint64_t k = gkey[g];
+    int rank = 0;
+    for (int h = 0; h < ngood; h++) rank += gkey[h] < k ? 1 : 0;
+    reinterpret_cast<int4*>(good)[rank] = grec[g];
+  }
+  ngood_out = ngood;
+  maxn_out = M;
+  return true;
+}
+
 __global__ __launch_bounds__(64) void oi_kernel(
     const DevOligoProblem* __restrict__ probs, const uint32_t* __restrict__ blocks, const char* __restrict__ quc_all,
     unsigned char* __restrict__ scratch, gmapdp_oligo_result* __restrict__ results, int32_t* __restrict__ npos_out,
-    int32_t* __restrict__ map_out, uint32_t* __restrict__ table_all, int32_t* __restrict__ diag_all) {
+    int32_t* __restrict__ map_out, uint32_t* __restrict__ table_all, int32_t* __restrict__ diag_all,
+    uint64_t* __restrict__ pool, unsigned long long* __restrict__ pool_counter, unsigned long long pool_cap) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x;
   const DevOligoProblem P = probs[blockIdx.x];
@@ -229,90 +444,96 @@ __global__ __launch_bounds__(64) void oi_kernel(
   if (P.chrend > P.chrstart) {
     const int diag_lookback = P.minor ? 60 : 120, suffn = P.minor ? 10 : 20;
     const uint32_t chrinit = P.plusp ? P.chrstart : (P.chrhigh - P.chroffset) - P.chrend;
-    const ScratchOi so = scratch_oi(qlen, P.chrend - P.chrstart);
-    unsigned char* initp = base_s + so.initp;
-    OiState* st = reinterpret_cast<OiState*>(base_s + so.states);
-    for (size_t b = 16 * (size_t)lane; b < so.states - so.initp; b += 16 * 64)
-      *reinterpret_cast<uint4*>(initp + b) = make_uint4(0u, 0u, 0u, 0u);
-    __threadfence_block();
-    int32_t* good = diag_all + 4 * P.diag_offset;  // diagi of each good diagonal, in field 0 of its record
-    int ngood = 0, maxn = 0, best = -1;
-    // query positions in chunks of 64: one coalesced load of their nhits, table offsets, cum_nohits
-    // and first hits, then the sequential walk takes them by readlane (off the latency chain)
-    for (int cb = 0; cb < nq; cb += 64) {
-      const int qi = cb + lane;
-      int c_nh = 0, c_mo = 0, c_cum = 0;
-      uint32_t c_h0 = 0;
-      if (qi < nq) {
-        c_nh = npq[qi];
-        c_mo = mpq[qi];
-        c_cum = cum[qi];
-        if (c_nh > 0) c_h0 = table_all[c_mo];
-      }
-      const int cend = min(64, nq - cb);
-      for (int j = 0; j < cend; j++) {
-        const int nh = __builtin_amdgcn_readlane(c_nh, j);
-        if (nh <= 0) continue;
-        const int q = cb + j;
-        const int mo = __builtin_amdgcn_readlane(c_mo, j);
-        const int cq = __builtin_amdgcn_readlane(c_cum, j);
-        const uint32_t h0 = (uint32_t)__builtin_amdgcn_readlane((int)c_h0, j);
-        for (int base = 0; base < nh; base += 64) {
-          const int h = base + lane;
-          int reached = 0, nb = 0;
-          uint32_t diagi = 0;
-          if (h < nh) {
-            diagi = (h == 0 ? h0 : table_all[mo + h]) + (uint32_t)(qlen - q) - chrinit;
-            const unsigned char ini = initp[diagi];
-            OiState s = st[diagi];  // loaded with the flag; ignored when the flag is clear
-            if (!ini) {
-              initp[diagi] = 1;
-              s.querypos = -diag_lookback;  // the first check is never consecutive
-              s.best_n = s.n = s.cstart = s.best_start = s.best_end = 0;
+    int32_t* good = diag_all + 4 * P.diag_offset;  // records {diag, best_start, best_end, best_n + 1}
+    int ngood = 0, maxn = 0;
+    __syncthreads();  // cnt is dead: the sorted path's digit histogram
+    if (!oi_mappings_sorted(lane, qlen, nq, totalpositions, chrinit, diag_lookback, suffn, npq, mpq, cum, table_all,
+                            pool, pool_counter, pool_cap, cnt, good, ngood, maxn)) {
+      // the event pool is full: the sequential walk (per-diagonal states in this problem's scratch)
+      const ScratchOi so = scratch_oi(qlen, P.chrend - P.chrstart);
+      unsigned char* initp = base_s + so.initp;
+      OiState* st = reinterpret_cast<OiState*>(base_s + so.states);
+      for (size_t b = 16 * (size_t)lane; b < so.states - so.initp; b += 16 * 64)
+        *reinterpret_cast<uint4*>(initp + b) = make_uint4(0u, 0u, 0u, 0u);
+      __threadfence_block();
+      int best = -1;  // diagi of each good diagonal goes in field 0 of its record first
+      // query positions in chunks of 64: one coalesced load of their nhits, table offsets, cum_nohits
+      // and first hits, then the sequential walk takes them by readlane (off the latency chain)
+      for (int cb = 0; cb < nq; cb += 64) {
+        const int qi = cb + lane;
+        int c_nh = 0, c_mo = 0, c_cum = 0;
+        uint32_t c_h0 = 0;
+        if (qi < nq) {
+          c_nh = npq[qi];
+          c_mo = mpq[qi];
+          c_cum = cum[qi];
+          if (c_nh > 0) c_h0 = table_all[c_mo];
+        }
+        const int cend = min(64, nq - cb);
+        for (int j = 0; j < cend; j++) {
+          const int nh = __builtin_amdgcn_readlane(c_nh, j);
+          if (nh <= 0) continue;
+          const int q = cb + j;
+          const int mo = __builtin_amdgcn_readlane(c_mo, j);
+          const int cq = __builtin_amdgcn_readlane(c_cum, j);
+          const uint32_t h0 = (uint32_t)__builtin_amdgcn_readlane((int)c_h0, j);
+          for (int base = 0; base < nh; base += 64) {
+            const int h = base + lane;
+            int reached = 0, nb = 0;
+            uint32_t diagi = 0;
+            if (h < nh) {
+              diagi = (h == 0 ? h0 : table_all[mo + h]) + (uint32_t)(qlen - q) - chrinit;
+              const unsigned char ini = initp[diagi];
+              OiState s = st[diagi];  // loaded with the flag; ignored when the flag is clear
+              if (!ini) {
+                initp[diagi] = 1;
+                s.querypos = -diag_lookback;  // the first check is never consecutive
+                s.best_n = s.n = s.cstart = s.best_start = s.best_end = 0;
+              }
+              if (s.querypos < 0) {
+                s.n = 0;
+                s.cstart = q;
+              } else if (q - s.querypos >= diag_lookback + cq - cum[s.querypos]) {
+                s.n = 0;
+                s.cstart = q;
+              } else if (++s.n > s.best_n) {
+                s.best_start = s.cstart;
+                s.best_end = q;
+                s.best_n = s.n;
+                reached = (s.best_n == suffn);
+                nb = s.best_n;
+              }
+              s.querypos = q;
+              st[diagi] = s;
             }
-            if (s.querypos < 0) {
-              s.n = 0;
-              s.cstart = q;
-            } else if (q - s.querypos >= diag_lookback + cq - cum[s.querypos]) {
-              s.n = 0;
-              s.cstart = q;
-            } else if (++s.n > s.best_n) {
-              s.best_start = s.cstart;
-              s.best_end = q;
-              s.best_n = s.n;
-              reached = (s.best_n == suffn);
-              nb = s.best_n;
+            // the good list in lane order; the global best: the first lane reaching the new maximum
+            const uint64_t rm = ballot(reached);
+            if (reached) good[4 * (ngood + lanes_below(rm, lane))] = (int32_t)diagi;
+            ngood += __popcll(rm);
+            int mx = nb;
+  #pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) mx = max(mx, __shfl_xor(mx, off, 64));
+            if (mx > maxn) {
+              const int l = __ffsll((long long)ballot(nb == mx)) - 1;
+              best = __builtin_amdgcn_readlane((int)diagi, l);
+              maxn = mx;
             }
-            s.querypos = q;
-            st[diagi] = s;
-          }
-          // the good list in lane order; the global best: the first lane reaching the new maximum
-          const uint64_t rm = ballot(reached);
-          if (reached) good[4 * (ngood + lanes_below(rm, lane))] = (int32_t)diagi;
-          ngood += __popcll(rm);
-          int mx = nb;
-#pragma unroll
-          for (int off = 32; off >= 1; off >>= 1) mx = max(mx, __shfl_xor(mx, off, 64));
-          if (mx > maxn) {
-            const int l = __ffsll((long long)ballot(nb == mx)) - 1;
-            best = __builtin_amdgcn_readlane((int)diagi, l);
-            maxn = mx;
           }
         }
       }
-    }
-    if (ngood == 0 && maxn > 0) {
-      if (lane == 0) good[0] = best;
-      ngood = 1;
-    }
-    __threadfence_block();
-    for (int g = lane; g < ngood; g += 64) {
-      const int di = good[4 * g];
-      const OiState s = st[di];
-      good[4 * g + 0] = di >= qlen ? di - qlen : qlen - di;
-      good[4 * g + 1] = s.best_start;
-      good[4 * g + 2] = s.best_end;
-      good[4 * g + 3] = s.best_n + 1;
+      if (ngood == 0 && maxn > 0) {
+        if (lane == 0) good[0] = best;
+        ngood = 1;
+      }
+      __threadfence_block();
+      for (int g = lane; g < ngood; g += 64) {
+        const int di = good[4 * g];
+        const OiState s = st[di];
+        good[4 * g + 0] = di >= qlen ? di - qlen : qlen - di;
+        good[4 * g + 1] = s.best_start;
+        good[4 * g + 2] = s.best_end;
+        good[4 * g + 3] = s.best_n + 1;
+      }
     }
     res.maxnconsecutive = maxn;
     res.oned_matrix_p = 1;
@@ -329,14 +550,16 @@ size_t scratch_bytes_oi(int querylength, uint32_t genomiclength) {
 
 hipError_t launch_oi(int nproblems, size_t lds, hipStream_t stream, const DevOligoProblem* probs,
                      const uint32_t* blocks, const char* quc, unsigned char* scratch, gmapdp_oligo_result* results,
-                     int32_t* npos, int32_t* map, uint32_t* table, int32_t* diags) {
+                     int32_t* npos, int32_t* map, uint32_t* table, int32_t* diags, uint64_t* pool,
+                     unsigned long long* pool_counter, unsigned long long pool_cap) {
   void* fn = reinterpret_cast<void*>(&oi_kernel);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
   void* args[] = {(void*)&probs, (void*)&blocks, (void*)&quc, (void*)&scratch, (void*)&results, (void*)&npos,
-                  (void*)&map, (void*)&table, (void*)&diags};
+                  (void*)&map, (void*)&table, (void*)&diags, (void*)&pool, (void*)&pool_counter,
+                  (void*)&pool_cap};
   return hipLaunchKernel(fn, dim3(nproblems), dim3(64), args, lds, stream);
 }
 

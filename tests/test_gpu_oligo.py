@@ -92,3 +92,46 @@ def test_gpu_oligo_domain_check(engine):
     p = dict(quc=b"ACGTACGT", chrstart=100, chrend=5000, chroffset=0, chrhigh=20000, plusp=1, minor=0)
     with pytest.raises(gmapdp.GmapdpError):
         engine.oligo_mappings_batch([p])
+
+
+def _repeat_genome(rng, n):
+    """A genome with tandem copies of short units: queries drawn over them put many diagonals past
+    suffnconsecutive, which exercises the order of the good list."""
+    g = bytearray(random_genome(rng, n))
+    for start in range(5000, n - 20000, 25000):
+        unit = bytes(g[start:start + rng.randint(40, 400)])
+        pos = start
+        for _ in range(rng.randint(3, 12)):
+            g[pos:pos + len(unit)] = unit
+            pos += len(unit) + rng.randint(0, 30)
+    return bytes(g)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_gpu_oligo_repeats_match_oracle(engine, seed):
+    rng = random.Random(8300 + seed)
+    g = _repeat_genome(rng, 300000)
+    engine.set_genome(g)
+    orc = Oracle()
+    orc.set_genome(g)
+    probs = [oligo_problem(rng, g, edge=(i % 7 == 0)) for i in range(400)]
+    got = engine.oligo_mappings_batch(probs)
+    exp = [orc.oligo_mappings(p) for p in probs]
+    assert max(len(e[3]) for e in exp) > 3  # the test is only worth it with many good diagonals
+    d = _first_diff(got, exp)
+    assert d is None, _msg(probs, d, "oracle")
+
+
+def test_gpu_oligo_pool_overflow_falls_back(engine, monkeypatch):
+    """A small event pool: the problems that no longer fit run the sequential walk; same results."""
+    rng = random.Random(8400)
+    g = _repeat_genome(rng, 200000)
+    engine.set_genome(g)
+    orc = Oracle()
+    orc.set_genome(g)
+    probs = [oligo_problem(rng, g) for i in range(200)]
+    exp = [orc.oligo_mappings(p) for p in probs]
+    for slots in ("0", "20000"):
+        monkeypatch.setenv("GMAPDP_OLIGO_POOL_SLOTS", slots)
+        d = _first_diff(engine.oligo_mappings_batch(probs), exp)
+        assert d is None, _msg(probs, d, "oracle (pool %s)" % slots)
