@@ -29,6 +29,24 @@
 namespace gmapdp {
 
 constexpr int kOiK = 8;
+
+// Phase timing (tools/oi_timing.py; built only into the GMAPDP_OI_TIMING variant of the library):
+// every wave adds its wall-clock timestamp at each mark, so mark k - mark k-1 summed over the waves
+// is the time spent in phase k.
+#ifdef GMAPDP_OI_TIMING
+__device__ unsigned long long g_oi_marks[2][16];
+#define OI_MARK(k)                                                 \
+  do {                                                             \
+    if (threadIdx.x == 0) {                                        \
+      atomicAdd(&g_oi_marks[0][k], (unsigned long long)wall_clock64()); \
+      atomicAdd(&g_oi_marks[1][k], 1ull);                          \
+    }                                                              \
+  } while (0)
+#else
+#define OI_MARK(k) \
+  do {             \
+  } while (0)
+#endif
 constexpr int kOiWords = 65536 / 32;  // bitmap words
 
 // 16-nt half-word h of the packed genome (.genomecomp: {high nt 16-31, low nt 0-15, flags})
@@ -60,13 +78,14 @@ __device__ __forceinline__ int nt_code(char c) {  // -1 resets the 8-mer (oligoi
 // the query 8-mer at querypos i (characters i .. i+7), -1 if one of them is not ACGT
 __device__ __forceinline__ int query_oligo(const char* __restrict__ q, int i) {
   uint32_t m = 0;
+  bool ok = true;
 #pragma unroll
-  for (int j = 0; j < kOiK; j++) {
+  for (int j = 0; j < kOiK; j++) {  // no early exit: the 8 loads issue together
     const int c = nt_code(q[i + j]);
-    if (c < 0) return -1;
-    m = (m << 2) | (uint32_t)c;
+    ok = ok && c >= 0;
+    m = (m << 2) | ((uint32_t)c & 3u);
   }
-  return (int)m;
+  return ok ? (int)m : -1;
 }
 
 __device__ __forceinline__ int oligo_id(const uint32_t* bitmap, const uint16_t* wrank, uint32_t m, bool& in) {
@@ -77,14 +96,15 @@ __device__ __forceinline__ int oligo_id(const uint32_t* bitmap, const uint16_t* 
 
 // per-problem scratch: cum_nohits (querylength + 1 ints), the genomicdiag init flags, the states
 struct ScratchOi {
-  size_t initp, states, total;
+  size_t initp, states, hits, total;
 };
 __host__ __device__ inline ScratchOi scratch_oi(int querylength, uint32_t genomiclength) {
   const size_t nd = (size_t)querylength + genomiclength + 1;
   ScratchOi s;
   s.initp = align16(4 * (size_t)(querylength + 1));
   s.states = align16(s.initp + nd);
-  s.total = align16(s.states + nd * sizeof(OiState));
+  s.hits = align16(s.states + nd * sizeof(OiState));
+  s.total = align16(s.hits + 8 * ((size_t)genomiclength + 2));
   return s;
 }
 
@@ -153,6 +173,7 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t c
     eoff += __builtin_amdgcn_readlane(incl, 63);
   }
   __threadfence_block();
+  OI_MARK(5);
 
   // stable LSD radix sort on diagi, 8-bit digits (diagi <= qlen + genomiclength)
   uint64_t* src = evA;
@@ -204,6 +225,7 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t c
   }
   const uint64_t* S = src;
   __threadfence_block();
+  OI_MARK(6);
 
   // sweep: runs, diagonal maxima, the first hit reaching suffn per diagonal, the global maximum
   int c_rs = -1, c_ds = -1, c_fs = 0x7fffffff, ngood = 0, M = 0;
@@ -316,13 +338,18 @@ __global__ __launch_bounds__(64) void oi_kernel(
   uint32_t* offs = cnt + P.umax;                                          // per id: table offset
   const char* quc = quc_all + P.qoff;
   const int qlen = P.querylength;
+  OI_MARK(0);
   const int nq = qlen - kOiK + 1;  // query positions with a full 8-mer
 
   // ---- the query's 8-mers (Oligoindex_set_inquery) ----
   for (int w = lane; w < kOiWords; w += 64) bitmap[w] = 0u;
   __syncthreads();
-  for (int i = lane; i < nq; i += 64) {
-    const int m = query_oligo(quc, i);
+  int32_t* npq = npos_out + P.qoff;
+  int32_t* mpq = map_out + P.qoff;  // holds each querypos's 8-mer (or -1) until get_mappings
+  for (int i = lane; i < qlen; i += 64) {
+    const int m = i < nq ? query_oligo(quc, i) : -1;
+    mpq[i] = m;
+    npq[i] = 0;
     if (m >= 0) atomicOr(&bitmap[m >> 5], 1u << (m & 31));
   }
   __syncthreads();
@@ -334,6 +361,7 @@ __global__ __launch_bounds__(64) void oi_kernel(
     run += __builtin_amdgcn_readlane(incl, 63);
   }
   const int U = run;  // <= umax (the host counted them)
+  OI_MARK(1);
   for (int u = lane; u < U; u += 64) cnt[u] = 0u;
   __syncthreads();
 
@@ -342,13 +370,48 @@ __global__ __launch_bounds__(64) void oi_kernel(
   uint64_t lpl = (uint64_t)P.chroffset + P.chrend + (P.plusp ? 0 : 1);
   lpl = lpl < (uint64_t)kOiK ? 0 : lpl - kOiK;
   const uint64_t npos = lpl > left ? lpl - left + 1 : 0;
-  for (uint64_t t = 0; t < npos; t += 64) {
-    const uint64_t k = t + lane;
-    if (k < npos) {
-      const uint32_t x = window8(blocks, left + k);
-      bool in;
-      const int u = oligo_id(bitmap, wrank, P.plusp ? oligo_fwd(x) : (~x & 0xFFFFu), in);
-      if (in) atomicAdd(&cnt[u], 1u);
+  // Each lane takes one 16-nt genome half-word (its 16 8-mer starts, from the half-word and the
+  // next); the next step's two loads are issued before this step's LDS work.  Every hit is appended
+  // to the problem's hit list {window index, id} in ascending position, so pass 2 never re-reads the
+  // window.
+  unsigned char* base_s = scratch + P.scratch_offset;
+  const ScratchOi so = scratch_oi(qlen, P.chrend > P.chrstart ? P.chrend - P.chrstart : 0);
+  uint2* hitlist = reinterpret_cast<uint2*>(base_s + so.hits);
+  int nhits = 0;
+  if (npos > 0) {
+    const uint64_t hlo = left >> 4, hhi = lpl >> 4;
+    uint32_t w0 = 0, w1 = 0;
+    if (hlo + lane <= hhi) {
+      w0 = half_word(blocks, hlo + lane);
+      w1 = half_word(blocks, hlo + lane + 1);
+    }
+    for (uint64_t hb = hlo; hb <= hhi; hb += 64) {
+      const uint64_t h = hb + lane;
+      const uint64_t v = (uint64_t)w0 | ((uint64_t)w1 << 32);
+      if (hb + 64 + lane <= hhi) {  // prefetch the next step
+        w0 = half_word(blocks, hb + 64 + lane);
+        w1 = half_word(blocks, hb + 64 + lane + 1);
+      }
+      int id[16];
+      uint32_t hm = 0;
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const uint64_t p = 16 * h + j;
+        const uint32_t x = (uint32_t)(v >> (2 * j)) & 0xFFFFu;
+        bool in;
+        id[j] = oligo_id(bitmap, wrank, P.plusp ? oligo_fwd(x) : (~x & 0xFFFFu), in);
+        if (in && h <= hhi && p >= left && p <= lpl) hm |= 1u << j;
+      }
+#pragma unroll
+      for (int j = 0; j < 16; j++)
+        if ((hm >> j) & 1u) atomicAdd(&cnt[id[j]], 1u);
+      const int c = __popc(hm);
+      const int incl = wave_scan_add(lane, c);
+      int o = nhits + incl - c;
+#pragma unroll
+      for (int j = 0; j < 16; j++)
+        if ((hm >> j) & 1u) hitlist[o++] = make_uint2((uint32_t)(16 * h + j - left), (uint32_t)id[j]);
+      nhits += __builtin_amdgcn_readlane(incl, 63);
     }
   }
   __syncthreads();
@@ -365,39 +428,42 @@ __global__ __launch_bounds__(64) void oi_kernel(
     tot += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   }
   __syncthreads();
+  OI_MARK(2);
 
   // ---- pass 2: store in descending chrpos (plus: right to left; minus: left to right) ----
   uint32_t* table = table_all + P.table_offset;
   const uint32_t chrpos0 = P.plusp ? P.chrstart : (P.chrhigh - P.chroffset) - P.chrend;
-  for (uint64_t t = 0; t < npos; t += 64) {
-    const uint64_t k = t + lane;  // k-th position in store order
+  const int idbits = U > 1 ? 32 - __clz(U - 1) : 1;
+  __threadfence_block();
+  for (int c = 0; c < nhits; c += 64) {
+    const int sl = c + lane;  // sl-th hit in store order: plus walks the list backwards
     int id = -1;
-    uint32_t cp = 0;
-    if (k < npos) {
-      const uint64_t pos = P.plusp ? lpl - k : left + k;
-      const uint32_t x = window8(blocks, pos);
-      bool in;
-      const int u = oligo_id(bitmap, wrank, P.plusp ? oligo_fwd(x) : (~x & 0xFFFFu), in);
-      if (in) id = u;
-      cp = chrpos0 + (uint32_t)(P.plusp ? pos - left : lpl - pos);
+    uint32_t k = 0;
+    if (sl < nhits) {
+      const uint2 hv = hitlist[P.plusp ? nhits - 1 - sl : sl];
+      k = hv.x;
+      id = (int)hv.y;
     }
-    uint64_t hits = ballot(id >= 0);
-    while (hits) {  // lane order = store order; a scalar loop keeps same-oligo hits in sequence
-      const int l = __ffsll((long long)hits) - 1;
-      hits &= hits - 1;
-      const int hid = __builtin_amdgcn_readlane(id, l);
-      const uint32_t hcp = (uint32_t)__builtin_amdgcn_readlane((int)cp, l);
-      if (lane == 0) {
-        const uint32_t r = cnt[hid];
-        if (r) {
-          cnt[hid] = r - 1;
-          table[offs[hid] + r - 1] = hcp;
-        }
-      }
+    const uint64_t hits = ballot(id >= 0);
+    // lane order = store order: a hit's rank among the chunk's hits of its oligo (ballot match on the
+    // id bits) is how many of that oligo's remaining slots the lower lanes take first
+    uint64_t eq = hits;
+    for (int b = 0; b < idbits; b++) {
+      const uint64_t m = ballot((id >> b) & 1);
+      eq &= ((id >> b) & 1) ? m : ~m;
+    }
+    if (id >= 0) {
+      const int rank = lanes_below(eq, lane);
+      const int same = __popcll(eq);
+      const int r0 = (int)cnt[id];  // every lane reads before the first lane of each oligo writes
+      if (r0 - rank > 0)
+        table[offs[id] + r0 - rank - 1] = chrpos0 + (P.plusp ? k : (uint32_t)(npos - 1) - k);
+      if (rank == 0) cnt[id] = (uint32_t)max(r0 - same, 0);
     }
   }
   __syncthreads();
   // the per-id counts again (nhits of lookup, :34074)
+  OI_MARK(3);
   for (int u = lane; u < U; u += 64) cnt[u] = (u + 1 < U ? offs[u + 1] : tot) - offs[u];
   __threadfence_block();
   __syncthreads();
@@ -410,23 +476,17 @@ __global__ __launch_bounds__(64) void oi_kernel(
   res.ndiagonals = 0;
   res.table_offset = P.table_offset;
   res.diag_offset = P.diag_offset;
-  int32_t* npq = npos_out + P.qoff;
-  int32_t* mpq = map_out + P.qoff;
-  for (int i = lane; i < qlen; i += 64) {
-    npq[i] = 0;
-    mpq[i] = -1;
-  }
   __threadfence_block();
   // per querypos: nhits and table offset; cum_nohits as an inclusive prefix count of the positions
   // whose 8-mer has no hit (a position without a full 8-mer carries it forward)
-  unsigned char* base_s = scratch + P.scratch_offset;
   int* cum = reinterpret_cast<int*>(base_s);
   int totalpositions = 0, cumrun = 0;
   for (int base = 0; base < nq; base += 64) {
     const int i = base + lane;
     int nh = -1;
     if (i < nq) {
-      const int m = query_oligo(quc, i);
+      const int m = mpq[i];
+      mpq[i] = -1;
       if (m >= 0) {
         bool in;
         const int u = oligo_id(bitmap, wrank, (uint32_t)m, in);
@@ -441,6 +501,7 @@ __global__ __launch_bounds__(64) void oi_kernel(
     totalpositions += __builtin_amdgcn_readlane(wave_scan_add(lane, nh > 0 ? nh : 0), 63);
   }
   __threadfence_block();
+  OI_MARK(4);
   if (P.chrend > P.chrstart) {
     const int diag_lookback = P.minor ? 60 : 120, suffn = P.minor ? 10 : 20;
     const uint32_t chrinit = P.plusp ? P.chrstart : (P.chrhigh - P.chroffset) - P.chrend;
@@ -450,7 +511,6 @@ __global__ __launch_bounds__(64) void oi_kernel(
     if (!oi_mappings_sorted(lane, qlen, nq, totalpositions, chrinit, diag_lookback, suffn, npq, mpq, cum, table_all,
                             pool, pool_counter, pool_cap, cnt, good, ngood, maxn)) {
       // the event pool is full: the sequential walk (per-diagonal states in this problem's scratch)
-      const ScratchOi so = scratch_oi(qlen, P.chrend - P.chrstart);
       unsigned char* initp = base_s + so.initp;
       OiState* st = reinterpret_cast<OiState*>(base_s + so.states);
       for (size_t b = 16 * (size_t)lane; b < so.states - so.initp; b += 16 * 64)
@@ -541,7 +601,17 @@ __global__ __launch_bounds__(64) void oi_kernel(
   }
   res.totalpositions = totalpositions;
   if (lane == 0) results[P.index] = res;
+  OI_MARK(7);
 }
+
+#ifdef GMAPDP_OI_TIMING
+// copies out and clears the marks: [0..15] timestamp sums (100 MHz), [16..31] wave counts
+extern "C" int gmapdp_debug_oi_marks(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_oi_marks), sizeof(g_oi_marks)) != hipSuccess) return 1;
+  static const unsigned long long zero[2][16] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_oi_marks), zero, sizeof(zero)) != hipSuccess;
+}
+#endif
 
 size_t lds_bytes_oi(int umax) { return 6 * (size_t)kOiWords + 8 * (size_t)umax; }
 size_t scratch_bytes_oi(int querylength, uint32_t genomiclength) {

@@ -1,0 +1,50 @@
+"""Phase breakdown of oi_kernel (stage-2 seeding) on bench.py's stage-2 workload.
+
+Loads the GMAPDP_OI_TIMING variant of the library (make -C gmap-2024_amd timing), runs one plan and
+prints, per phase, the wave-summed wall-clock time as a share of the total.  Diagnostic only."""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gmap-2024_amd"))
+sys.path.insert(0, ROOT)
+import gmapdp  # noqa: E402
+import bench  # noqa: E402
+
+PHASES = ["set_inquery (bitmap, ids)", "pass 1 (counts) + layout", "pass 2 (store)", "npositions/mappings/cum",
+          "events", "radix sort", "sweep + records"]
+
+
+def main():
+    import torch
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
+    lib = gmapdp.load_library(os.path.join(ROOT, "gmap-2024_amd", "lib", "libgmapdp_oitiming.so"))
+    lib.gmapdp_debug_oi_marks.argtypes = [C.c_void_p]
+    genome = bench.make_genome()
+    eng = gmapdp.Engine(0)
+    eng.set_genome(genome.tobytes())
+    op, oq = bench.make_stage2(genome, n, np.random.default_rng(3000))
+    qb = oq.tobytes()
+    res = eng.oligo_mappings_batch_raw(op, qb)
+    marks = np.zeros(32, dtype=np.uint64)
+    lib.gmapdp_debug_oi_marks(marks.ctypes.data)  # clear (includes the first run's warm-up)
+    res = eng.oligo_mappings_batch_raw(op, qb)
+    torch.cuda.synchronize()
+    lib.gmapdp_debug_oi_marks(marks.ctypes.data)
+    t, c = marks[:16].astype(np.float64), marks[16:]
+    out = {"waves": [int(x) for x in c[:8]]}
+    tot = t[7] - t[0]
+    out["wave_ms_total"] = tot / 1e5
+    out["phases"] = {name: round(float(t[k + 1] - t[k]) / tot, 4) for k, name in enumerate(PHASES) if k + 1 < 8}
+    out["mean_wave_us"] = tot / 1e2 / max(int(c[0]), 1)
+    print(json.dumps(out))
+    eng.close()
+    del res
+
+
+if __name__ == "__main__":
+    main()
