@@ -157,20 +157,38 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t c
   int4* grec = reinterpret_cast<int4*>(head + E);               // good records before ordering (<= E/2)
 
   // events in query order, hits of one querypos in table (ascending chrpos) order
+  // 64 query positions per chunk (their nhits / table offsets loaded a chunk ahead); the chunk's
+  // events go out 64 at a time, each lane finding its event's query position by a binary search
+  // over the positions' exclusive offsets (ds_bpermute), so the table loads all issue together
   int eoff = 0;
+  int nh_n = 0, mo_n = 0;
+  if (lane < nq) {
+    nh_n = npq[lane];
+    mo_n = mpq[lane];
+  }
   for (int cb = 0; cb < nq; cb += 64) {
-    const int q = cb + lane;
-    int nh = 0, mo = 0;
-    if (q < nq) {
-      nh = npq[q];
-      if (nh > 0) mo = mpq[q];
-      else nh = 0;
+    const int nh = max(nh_n, 0), mo = mo_n;
+    nh_n = 0;
+    if (cb + 64 + lane < nq) {
+      nh_n = npq[cb + 64 + lane];
+      mo_n = mpq[cb + 64 + lane];
     }
     const int incl = wave_scan_add(lane, nh);
-    const int o = eoff + incl - nh;
-    for (int h = 0; h < nh; h++)
-      evA[o + h] = ((uint64_t)(table_all[mo + h] + (uint32_t)(qlen - q) - chrinit) << 32) | (uint32_t)q;
-    eoff += __builtin_amdgcn_readlane(incl, 63);
+    const int excl = incl - nh;
+    const int T = __builtin_amdgcn_readlane(incl, 63);
+    for (int j0 = 0; j0 < T; j0 += 64) {
+      const int j = j0 + lane;
+      int l = 0;  // the last position whose events start at or before j
+#pragma unroll
+      for (int step = 32; step >= 1; step >>= 1)
+        if (__shfl(excl, l + step, 64) <= j) l += step;
+      const int h = j - __shfl(excl, l, 64);
+      const int mol = __shfl(mo, l, 64);
+      const int q = cb + l;
+      if (j < T)
+        evA[eoff + j] = ((uint64_t)(table_all[mol + h] + (uint32_t)(qlen - q) - chrinit) << 32) | (uint32_t)q;
+    }
+    eoff += T;
   }
   __threadfence_block();
   OI_MARK(5);
@@ -185,7 +203,17 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t c
   for (int shift = 0; shift < 32 && (maxd >> shift) != 0; shift += 8) {
     for (int i = lane; i < 256; i += 64) hist[i] = 0u;
     __syncthreads();
-    for (int e = lane; e < E; e += 64) atomicAdd(&hist[(uint32_t)(src[e] >> (32 + shift)) & 255u], 1u);
+    for (int e0 = 0; e0 < E; e0 += 4 * 64) {  // 4 chunks' loads in flight, then their atomics
+      uint64_t kk[4];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int e = e0 + 64 * r + lane;
+        kk[r] = e < E ? src[e] : 0ull;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+        if (e0 + 64 * r + lane < E) atomicAdd(&hist[(uint32_t)(kk[r] >> (32 + shift)) & 255u], 1u);
+    }
     __syncthreads();
     uint32_t h4[4], hs = 0;
 #pragma unroll
@@ -200,10 +228,12 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t c
       at += h4[k];
     }
     __syncthreads();
+    uint64_t knext = lane < E ? src[lane] : 0ull;  // one chunk ahead
     for (int e0 = 0; e0 < E; e0 += 64) {
       const int e = e0 + lane;
       const bool v = e < E;
-      const uint64_t key = v ? src[e] : 0ull;
+      const uint64_t key = knext;
+      knext = e + 64 < E ? src[e + 64] : 0ull;
       const uint32_t d = (uint32_t)(key >> (32 + shift)) & 255u;
       uint64_t eq = ballot(v);
 #pragma unroll
@@ -230,10 +260,12 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t c
   // sweep: runs, diagonal maxima, the first hit reaching suffn per diagonal, the global maximum
   int c_rs = -1, c_ds = -1, c_fs = 0x7fffffff, ngood = 0, M = 0;
   uint64_t c_mk = 0, c_key = 0;
+  uint64_t knext = lane < E ? S[lane] : ~0ull;  // one chunk ahead
   for (int e0 = 0; e0 < E; e0 += 64) {
     const int e = e0 + lane;
     const bool v = e < E;
-    const uint64_t key = v ? S[e] : ~0ull;
+    const uint64_t key = knext;
+    knext = e + 64 < E ? S[e + 64] : ~0ull;
     uint64_t pk = __shfl_up(key, 1, 64);
     if (lane == 0) pk = c_key;
     const uint32_t d = (uint32_t)(key >> 32), q = (uint32_t)key;
@@ -255,7 +287,11 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t c
     if (ds < e0) fs = min(fs, c_fs);
     // the diagonal's last hit records its maximum at the diagonal's head
     uint64_t nk = __shfl_down(key, 1, 64);
-    if (lane == 63) nk = (e + 1 < E) ? S[e + 1] : ~0ull;
+    {
+      const uint64_t first_next = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(knext >> 32), 0) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)knext, 0);
+      if (lane == 63) nk = (e + 1 < E) ? first_next : ~0ull;
+    }
     if (v && (e + 1 == E || (uint32_t)(nk >> 32) != d)) head[ds] = make_int2((int)(mk >> 32), (int)~(uint32_t)mk);
     const bool isgood = v && n == suffn && fs == e;
     const uint64_t gm = ballot(isgood);
@@ -327,8 +363,7 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t c
 __global__ __launch_bounds__(64) void oi_kernel(
     const DevOligoProblem* __restrict__ probs, const uint32_t* __restrict__ blocks, const char* __restrict__ quc_all,
     unsigned char* __restrict__ scratch, gmapdp_oligo_result* __restrict__ results, int32_t* __restrict__ npos_out,
-    int32_t* __restrict__ map_out, uint32_t* __restrict__ table_all, int32_t* __restrict__ diag_all,
-    uint64_t* __restrict__ pool, unsigned long long* __restrict__ pool_counter, unsigned long long pool_cap) {
+    int32_t* __restrict__ map_out, uint32_t* __restrict__ table_all) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x;
   const DevOligoProblem P = probs[blockIdx.x];
@@ -346,11 +381,31 @@ __global__ __launch_bounds__(64) void oi_kernel(
   __syncthreads();
   int32_t* npq = npos_out + P.qoff;
   int32_t* mpq = map_out + P.qoff;  // holds each querypos's 8-mer (or -1) until get_mappings
-  for (int i = lane; i < qlen; i += 64) {
-    const int m = i < nq ? query_oligo(quc, i) : -1;
-    mpq[i] = m;
-    npq[i] = 0;
-    if (m >= 0) atomicOr(&bitmap[m >> 5], 1u << (m & 31));
+  // one coalesced character load per lane and chunk, issued two chunks ahead; the 8-mer at i takes
+  // the codes of lanes i..i+7 of this chunk and the next (ds_bpermute)
+  int c0 = lane < qlen ? nt_code(quc[lane]) : -1;
+  int c1 = 64 + lane < qlen ? nt_code(quc[64 + lane]) : -1;
+  for (int base = 0; base < qlen; base += 64) {
+    const int i2 = base + 128 + lane;
+    const int c2 = i2 < qlen ? nt_code(quc[i2]) : -1;
+    const int i = base + lane;
+    uint32_t m = 0;
+    bool ok = i < nq;
+#pragma unroll
+    for (int j = 0; j < kOiK; j++) {
+      const int src = (lane + j) & 63;
+      const int a = __shfl(c0, src, 64), b = __shfl(c1, src, 64);
+      const int cj = lane + j < 64 ? a : b;
+      ok = ok && cj >= 0;
+      m = (m << 2) | ((uint32_t)cj & 3u);
+    }
+    if (i < qlen) {
+      mpq[i] = ok ? (int)m : -1;
+      npq[i] = 0;
+    }
+    if (ok) atomicOr(&bitmap[m >> 5], 1u << (m & 31));
+    c0 = c1;
+    c1 = c2;
   }
   __syncthreads();
   int run = 0;  // ids in oligo order: prefix popcounts over the bitmap words
@@ -481,11 +536,13 @@ __global__ __launch_bounds__(64) void oi_kernel(
   // whose 8-mer has no hit (a position without a full 8-mer carries it forward)
   int* cum = reinterpret_cast<int*>(base_s);
   int totalpositions = 0, cumrun = 0;
+  int mnext = lane < nq ? mpq[lane] : -1;  // one chunk ahead
   for (int base = 0; base < nq; base += 64) {
     const int i = base + lane;
+    const int m = mnext;
+    mnext = i + 64 < nq ? mpq[i + 64] : -1;
     int nh = -1;
     if (i < nq) {
-      const int m = mpq[i];
       mpq[i] = -1;
       if (m >= 0) {
         bool in;
@@ -501,15 +558,39 @@ __global__ __launch_bounds__(64) void oi_kernel(
     totalpositions += __builtin_amdgcn_readlane(wave_scan_add(lane, nh > 0 ? nh : 0), 63);
   }
   __threadfence_block();
+  res.totalpositions = totalpositions;
+  if (lane == 0) results[P.index] = res;
   OI_MARK(4);
-  if (P.chrend > P.chrstart) {
+}
+
+// ---- Oligoindex_get_mappings' diagonal state machine, one wave per problem, after oi_kernel ----
+// A kernel of its own: its only LDS is the 1-KB radix histogram, so many more waves share a CU and
+// hide the L2 latency of the event passes than oi_kernel's query tables would allow.
+__global__ __launch_bounds__(64) void oi_map_kernel(
+    const DevOligoProblem* __restrict__ probs, unsigned char* __restrict__ scratch,
+    gmapdp_oligo_result* __restrict__ results, const int32_t* __restrict__ npos_out,
+    const int32_t* __restrict__ map_out, const uint32_t* __restrict__ table_all, int32_t* __restrict__ diag_all,
+    uint64_t* __restrict__ pool, unsigned long long* __restrict__ pool_counter, unsigned long long pool_cap) {
+  __shared__ uint32_t hist[256];
+  const int lane = threadIdx.x;
+  const DevOligoProblem P = probs[blockIdx.x];
+  if (P.chrend <= P.chrstart) return;  // oned_matrix_p stays 0 (oi_kernel wrote the record)
+  OI_MARK(8);
+  const int qlen = P.querylength;
+  const int nq = qlen - kOiK + 1;
+  const int32_t* npq = npos_out + P.qoff;
+  const int32_t* mpq = map_out + P.qoff;
+  unsigned char* base_s = scratch + P.scratch_offset;
+  const int* cum = reinterpret_cast<const int*>(base_s);
+  const ScratchOi so = scratch_oi(qlen, P.chrend - P.chrstart);
+  const int totalpositions = results[P.index].totalpositions;
+  {
     const int diag_lookback = P.minor ? 60 : 120, suffn = P.minor ? 10 : 20;
     const uint32_t chrinit = P.plusp ? P.chrstart : (P.chrhigh - P.chroffset) - P.chrend;
     int32_t* good = diag_all + 4 * P.diag_offset;  // records {diag, best_start, best_end, best_n + 1}
     int ngood = 0, maxn = 0;
-    __syncthreads();  // cnt is dead: the sorted path's digit histogram
     if (!oi_mappings_sorted(lane, qlen, nq, totalpositions, chrinit, diag_lookback, suffn, npq, mpq, cum, table_all,
-                            pool, pool_counter, pool_cap, cnt, good, ngood, maxn)) {
+                            pool, pool_counter, pool_cap, hist, good, ngood, maxn)) {
       // the event pool is full: the sequential walk (per-diagonal states in this problem's scratch)
       unsigned char* initp = base_s + so.initp;
       OiState* st = reinterpret_cast<OiState*>(base_s + so.states);
@@ -595,12 +676,12 @@ __global__ __launch_bounds__(64) void oi_kernel(
         good[4 * g + 3] = s.best_n + 1;
       }
     }
-    res.maxnconsecutive = maxn;
-    res.oned_matrix_p = 1;
-    res.ndiagonals = ngood;
+    if (lane == 0) {
+      results[P.index].maxnconsecutive = maxn;
+      results[P.index].oned_matrix_p = 1;
+      results[P.index].ndiagonals = ngood;
+    }
   }
-  res.totalpositions = totalpositions;
-  if (lane == 0) results[P.index] = res;
   OI_MARK(7);
 }
 
@@ -628,9 +709,12 @@ hipError_t launch_oi(int nproblems, size_t lds, hipStream_t stream, const DevOli
     if (e != hipSuccess) return e;
   }
   void* args[] = {(void*)&probs, (void*)&blocks, (void*)&quc, (void*)&scratch, (void*)&results, (void*)&npos,
-                  (void*)&map, (void*)&table, (void*)&diags, (void*)&pool, (void*)&pool_counter,
-                  (void*)&pool_cap};
-  return hipLaunchKernel(fn, dim3(nproblems), dim3(64), args, lds, stream);
+                  (void*)&map, (void*)&table};
+  hipError_t e = hipLaunchKernel(fn, dim3(nproblems), dim3(64), args, lds, stream);
+  if (e != hipSuccess) return e;
+  void* margs[] = {(void*)&probs, (void*)&scratch, (void*)&results, (void*)&npos, (void*)&map, (void*)&table,
+                   (void*)&diags, (void*)&pool, (void*)&pool_counter, (void*)&pool_cap};
+  return hipLaunchKernel(reinterpret_cast<void*>(&oi_map_kernel), dim3(nproblems), dim3(64), margs, 0, stream);
 }
 
 }  // namespace gmapdp

@@ -36,11 +36,15 @@ def main():
     torch.cuda.synchronize()
     lib.gmapdp_debug_oi_marks(marks.ctypes.data)
     t, c = marks[:16].astype(np.float64), marks[16:]
-    out = {"waves": [int(x) for x in c[:8]]}
-    tot = t[7] - t[0]
+    # oi_kernel: marks 0..4; oi_map_kernel: 8 (start), 5, 6, 7
+    spans = [(0, 1), (1, 2), (2, 3), (3, 4), (8, 5), (5, 6), (6, 7)]
+    out = {"waves": [int(c[k]) for k in (0, 1, 2, 3, 4, 8, 5, 6, 7)]}
+    dur = [float(t[b] - t[a]) for a, b in spans]
+    tot = sum(dur)
     out["wave_ms_total"] = tot / 1e5
-    out["phases"] = {name: round(float(t[k + 1] - t[k]) / tot, 4) for k, name in enumerate(PHASES) if k + 1 < 8}
-    out["mean_wave_us"] = tot / 1e2 / max(int(c[0]), 1)
+    out["phases"] = {name: round(d / tot, 4) for name, d in zip(PHASES, dur)}
+    out["mean_wave_us"] = {"oi_kernel": sum(dur[:4]) / 1e2 / max(int(c[0]), 1),
+                           "oi_map_kernel": sum(dur[4:]) / 1e2 / max(int(c[8]), 1)}
     print(json.dumps(out))
     eng.close()
     del res
