@@ -228,12 +228,20 @@ def pmc_traffic(name):
     summary (profiles/*/pmc_summary.json: 2 x FETCH_SIZE + WRITE_SIZE of the same bench command,
     per MI355X_MICROARCH.md's gfx950 correction), or (None, None)."""
     import glob
+    if name == "oi_kernel+oi_map_kernel":  # stage-2 seeding: the two kernels of one launch, summed
+        keys = ["gmapdp::oi_kernel", "gmapdp::oi_map_kernel"]
+        for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")), reverse=True):
+            try:
+                ks = json.load(open(path))["kernels"]
+            except (OSError, ValueError, KeyError):
+                continue
+            if all(k in ks for k in keys):
+                return sum(ks[k]["hbm_bytes_per_dispatch"] for k in keys), os.path.relpath(path, ROOT)
+        return None, None
     m = re.match(r"(\w+)<R=(\d+),dirs_lds=(\d)>", name)
     if not m:
         return None, None
-    if m.group(1) == "oi_kernel":  # not a template
-        key = "gmapdp::oi_kernel"
-    elif m.group(1) == "dpx_kernel":  # dpx_kernel<S, GD>: GD = direction words in global scratch
+    if m.group(1) == "dpx_kernel":  # dpx_kernel<S, GD>: GD = direction words in global scratch
         key = "gmapdp::dpx_kernel<%s, %s>" % (m.group(2), "false" if m.group(3) == "1" else "true")
     else:
         key = "gmapdp::%s<%s, %s>" % (m.group(1), m.group(2), "true" if m.group(3) == "1" else "false")
@@ -689,7 +697,7 @@ def main():
     oms = sum(a.elapsed_time(b) for a, b in oev) / osteps
     ores = np.frombuffer(d_ores.cpu().numpy().tobytes(), dtype=gmapdp.OLIGO_RESULT_DTYPE)
     obytes = stage2_algorithmic_bytes(op, ores)
-    otraffic, osrc = pmc_traffic("oi_kernel<R=0,dirs_lds=0>")
+    otraffic, osrc = pmc_traffic("oi_kernel+oi_map_kernel")
     nol = lib.gmapdp_oligo_plan_nlaunches(oplan)
     out["stage2_seeding"] = {
         "value": args.reads * world * osteps / oelapsed, "unit": "reads/s", "ms_per_step": oelapsed / osteps * 1e3,
@@ -698,10 +706,11 @@ def main():
         "diagonals_per_step_per_gpu": int(ores["ndiagonals"].astype(np.int64).sum()),
         "roofline": {"bound": "hbm", "achieved": obytes / (oms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": obytes / (oms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": otraffic, "traffic_source": osrc,
-                     "kernel": "oi_kernel", "dispatches": nol * osteps, "kernel_ms_per_launch": oms / max(nol, 1),
+                     "kernel": "oi_kernel+oi_map_kernel", "dispatches": nol * osteps, "kernel_ms_per_launch": oms / max(nol, 1),
                      "algorithmic_bytes_per_launch": obytes / max(nol, 1),
-                     "note": "one wave per read: LDS-atomic counting sort of the window's 8-mers + get_mappings "
-                             "as a diagonal radix sort and segmented scans; latency-bound (DESIGN.md)"}}
+                     "note": "per launch oi_kernel (LDS counting sort of the window's 8-mers, one wave per read) "
+                             "+ oi_map_kernel (get_mappings as a diagonal radix sort and segmented scans); "
+                             "latency-bound (DESIGN.md)"}}
     lib.gmapdp_oligo_plan_destroy(oplan)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["stage2_seeding"]["cpu_baseline"] = cpu_baseline_stage2(op, oq, genome)

@@ -38,6 +38,36 @@
 
 namespace gmapdp {
 
+// Phase timing of gg_kernel (tools_oi_timing.py gg; GMAPDP_OI_TIMING variant of the library only):
+// wave 0 of every block adds its wall-clock timestamp at each mark; blocks that finish early add
+// the remaining marks at once.
+#ifdef GMAPDP_OI_TIMING
+__device__ unsigned long long g_gg_marks[2][16];
+#define GG_MARK(k)                                                          \
+  do {                                                                      \
+    if (threadIdx.x == 0) {                                                 \
+      atomicAdd(&g_gg_marks[0][k], (unsigned long long)wall_clock64());     \
+      atomicAdd(&g_gg_marks[1][k], 1ull);                                   \
+    }                                                                       \
+  } while (0)
+#define GG_MARK_TO(a, b) \
+  do {                   \
+    for (int gk_ = (a); gk_ <= (b); gk_++) GG_MARK(gk_); \
+  } while (0)
+extern "C" int gmapdp_debug_gg_marks(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gg_marks), sizeof(g_gg_marks)) != hipSuccess) return 1;
+  static const unsigned long long zero[2][16] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_gg_marks), zero, sizeof(zero)) != hipSuccess;
+}
+#else
+#define GG_MARK(k) \
+  do {             \
+  } while (0)
+#define GG_MARK_TO(a, b) \
+  do {                   \
+  } while (0)
+#endif
+
 template <int R, bool DIRS_LDS>
 __global__ __launch_bounds__(64) void dp_kernel(
     const DevProblem* __restrict__ probs, const int* __restrict__ order,
@@ -643,6 +673,7 @@ __global__ __launch_bounds__(128) void gg_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int pid = order[blockIdx.x];
   const DevGenomeProblem P = probs[pid];
+  GG_MARK(0);
   const int rlen = P.rlength, gL = P.glengthL, gR = P.glengthR;
   const int flags = P.flags;
   const bool watson = flags & kFWatson;
@@ -714,6 +745,7 @@ __global__ __launch_bounds__(128) void gg_kernel(
   for (int c = tid; c <= gL; c += 128) ldi[c] = (c < gL - 1) ? left_dinucl(gchL[c + 1], gchL[c + 2]) : 0;
   for (int c = tid; c <= gR; c += 128) rdi[c] = (c < gR - 1) ? right_dinucl(gchR[c + 2], gchR[c + 1]) : 0;
   __syncthreads();
+  GG_MARK(1);
 
   gmapdp_genome_result res;
   res.npairs = 0;
@@ -736,8 +768,12 @@ __global__ __launch_bounds__(128) void gg_kernel(
       if (lane == 0) *done = ok ? 1 : 0;
     }
     __syncthreads();
-    if (*done) return;
+    if (*done) {
+      GG_MARK_TO(2, 7);
+      return;
+    }
   }
+  GG_MARK(2);
 
   // ---- 2. fills, concurrently: wave 0 R (feeds the B candidates), wave 1 L (the C candidates) ----
   const int rdist = P.rev_goffsetR - P.goffsetL;  // "cR < rightoffset - leftoffset - cL"
@@ -755,6 +791,7 @@ __global__ __launch_bounds__(128) void gg_kernel(
   }
   __threadfence_block();
   __syncthreads();
+  GG_MARK(3);
   if (wave != 0) return;
 
   // ---- 3. bridge: per-lane scan of rows rL = lane+1, lane+65, ... (A, B, C per row) ----
@@ -846,11 +883,13 @@ __global__ __launch_bounds__(128) void gg_kernel(
   int finalscore = bestscore;
   if (bestscore >= 0 && halfp) finalscore = bestscore - isc[ldi[bestcL] & rdi[bestcR]] / 2;
 
+  GG_MARK(4);
   if (finalscore < 0) {
     if (lane == 0) {
       res.traceback_score = -100;
       results[pid] = res;
     }
+    GG_MARK_TO(5, 7);
     return;
   }
 
@@ -864,11 +903,13 @@ __global__ __launch_bounds__(128) void gg_kernel(
                     P.chrhigh, blocks, nwords, out, t);
   const int nR = t.count;
   reverse_records(lane, out, nR);
+  GG_MARK(5);
   const int queryjump = (rev_roffset - bestrR) - (P.roffset + bestrL) + 1;
   if (lane == 0) put_pair(out, nR, -1, -1, new_right - new_left - 1, ' ', ' ', ' ', ' ');
   t.count += 1;
   traceback_band<R>(lane, dirsL, WL, ubandL, bestrL, bestcL, GL, qL, qucL, gchL, cons, watson, P.chroffset,
                     P.chrhigh, blocks, nwords, out, t);
+  GG_MARK(6);
   int npairs = t.count;
   int score = t.score + t.nmatches * kMatch + t.nmismatches * kMismatch;
   if (npairs == 1) {
@@ -895,6 +936,7 @@ __global__ __launch_bounds__(128) void gg_kernel(
     res.gap_queryjump = queryjump;
     results[pid] = res;
   }
+  GG_MARK(7);
 }
 
 // ---- host-side launch table ----

@@ -19,8 +19,39 @@ PHASES = ["set_inquery (bitmap, ids)", "pass 1 (counts) + layout", "pass 2 (stor
           "events", "radix sort", "sweep + records"]
 
 
+GG_PHASES = ["stage", "genome_gap_simple", "fills (L and R waves)", "bridge", "traceback R + reverse",
+             "traceback L", "maxnegscore + result"]
+
+
+def main_gg(reads=10000):
+    """gg_kernel phases on bench.py's genome-gap stream (GENOME_PER_READ calls per read)."""
+    import torch
+    lib = gmapdp.load_library(os.path.join(ROOT, "gmap-2024_amd", "lib", "libgmapdp_oitiming.so"))
+    lib.gmapdp_debug_gg_marks.argtypes = [C.c_void_p]
+    genome = bench.make_genome()
+    ng = int(round(reads * bench.GENOME_PER_READ))
+    gp, gq, sprob = bench.make_genome_gaps(genome, ng, np.random.default_rng(2000))
+    eng = gmapdp.Engine(0)
+    eng.set_genome(genome.tobytes())
+    qb = gq.tobytes()
+    eng.genome_gap_batch_raw(gp, qb, qb, sprob)
+    marks = np.zeros(32, dtype=np.uint64)
+    lib.gmapdp_debug_gg_marks(marks.ctypes.data)
+    eng.genome_gap_batch_raw(gp, qb, qb, sprob)
+    torch.cuda.synchronize()
+    lib.gmapdp_debug_gg_marks(marks.ctypes.data)
+    t, c = marks[:16].astype(np.float64), marks[16:]
+    dur = [float(t[k + 1] - t[k]) for k in range(7)]
+    tot = sum(dur)
+    print(json.dumps({"blocks": [int(x) for x in c[:8]], "phases": {n: round(d / tot, 4) for n, d in zip(GG_PHASES, dur)},
+                      "mean_block_us": tot / 1e2 / max(int(c[0]), 1)}))
+    eng.close()
+
+
 def main():
     import torch
+    if len(sys.argv) > 1 and sys.argv[1] == "gg":
+        return main_gg()
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
     lib = gmapdp.load_library(os.path.join(ROOT, "gmap-2024_amd", "lib", "libgmapdp_oitiming.so"))
     lib.gmapdp_debug_oi_marks.argtypes = [C.c_void_p]
