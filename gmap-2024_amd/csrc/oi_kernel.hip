@@ -14,16 +14,18 @@
 //                                  Genomicdiag_T consecutive-run state per diagonal, the good
 //                                  diagonals in the order they reach suffnconsecutive, else the best)
 //
-// Design.  One wave per (read, genomic window).  The query's distinct 8-mers are a 64-K-bit bitmap
-// in LDS; the bitmap's per-word prefix popcounts give every query 8-mer a dense id in oligo order,
-// so membership and the id of a window 8-mer are two LDS reads and a popcount -- no 64-K count
-// table, no hash.  A window 8-mer is one 64-bit funnel of two 16-nt genome half-words: the reverse
-// complement is its bitwise complement, the forward oligo its 2-bit reversal.  Pass 1 counts per id
-// (LDS atomics); an exclusive scan lays out the table; pass 2 walks the window in descending chrpos
-// in 64-position tiles and places each tile's hits in lane order (scalar loop over the ballot), which
-// reproduces the reference's keep-the-nearest-`count` rule exactly.  get_mappings sorts the hits by
-// diagonal and evaluates each diagonal's state machine with segmented scans (oi_mappings_sorted); a
-// problem that does not fit the batch's event pool walks the query sequentially instead.
+// Design.  Two kernels, one wave per (read, genomic window) each.  oi_kernel: the query's distinct
+// 8-mers are a 64-K-bit bitmap in LDS; the bitmap's per-word prefix popcounts give every query 8-mer
+// a dense id in oligo order, so membership and the id of a window 8-mer are two LDS reads and a
+// popcount -- no 64-K count table, no hash.  A window 8-mer is one 64-bit funnel of two 16-nt genome
+// half-words (one half-word per lane and step): the reverse complement is its bitwise complement,
+// the forward oligo its 2-bit reversal.  Pass 1 counts per id (LDS atomics) and appends the hits to a
+// hit list; an exclusive scan lays out the table; pass 2 walks the hit list in descending chrpos and
+// places 64 hits at a time, each hit's rank among the step's hits of its oligo coming from a ballot
+// match on the id bits, which reproduces the reference's keep-the-nearest-`count` rule exactly.
+// oi_map_kernel (1 KB of LDS, so many waves per CU) sorts the hits by diagonal and evaluates each
+// diagonal's state machine with segmented scans (oi_mappings_sorted); a problem that does not fit the
+// batch's event pool walks the query sequentially instead.
 #include "dp_device.h"
 
 namespace gmapdp {
