@@ -32,7 +32,7 @@ namespace gmapdp {
 
 constexpr int kOiK = 8;
 
-// Phase timing (tools/oi_timing.py; built only into the GMAPDP_OI_TIMING variant of the library):
+// Phase timing (tools_oi_timing.py; built only into the GMAPDP_OI_TIMING variant of the library):
 // every wave adds its wall-clock timestamp at each mark, so mark k - mark k-1 summed over the waves
 // is the time spent in phase k.
 #ifdef GMAPDP_OI_TIMING
@@ -55,12 +55,6 @@ constexpr int kOiWords = 65536 / 32;  // bitmap words
 __device__ __forceinline__ uint32_t half_word(const uint32_t* __restrict__ blocks, uint64_t h) {
   return blocks[3 * (h >> 1) + ((h & 1) ? 0 : 1)];
 }
-// the 8 nt starting at pos, nt j in bits 2j..2j+1
-__device__ __forceinline__ uint32_t window8(const uint32_t* __restrict__ blocks, uint64_t pos) {
-  const uint64_t h = pos >> 4;
-  const uint64_t v = (uint64_t)half_word(blocks, h) | ((uint64_t)half_word(blocks, h + 1) << 32);
-  return (uint32_t)(v >> (2 * (pos & 15))) & 0xFFFFu;
-}
 // forward oligo: first nt most significant (reverse the 2-bit groups)
 __device__ __forceinline__ uint32_t oligo_fwd(uint32_t x) {
   x = ((x & 0x3333u) << 2) | ((x >> 2) & 0x3333u);
@@ -75,19 +69,6 @@ struct OiState {  // struct Genomicdiag_T (oligoindex_hr.c:106); i is the array 
 
 __device__ __forceinline__ int nt_code(char c) {  // -1 resets the 8-mer (oligoindex_hr.c:34213-34223)
   return c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : c == 'T' ? 3 : -1;
-}
-
-// the query 8-mer at querypos i (characters i .. i+7), -1 if one of them is not ACGT
-__device__ __forceinline__ int query_oligo(const char* __restrict__ q, int i) {
-  uint32_t m = 0;
-  bool ok = true;
-#pragma unroll
-  for (int j = 0; j < kOiK; j++) {  // no early exit: the 8 loads issue together
-    const int c = nt_code(q[i + j]);
-    ok = ok && c >= 0;
-    m = (m << 2) | ((uint32_t)c & 3u);
-  }
-  return ok ? (int)m : -1;
 }
 
 __device__ __forceinline__ int oligo_id(const uint32_t* bitmap, const uint16_t* wrank, uint32_t m, bool& in) {
