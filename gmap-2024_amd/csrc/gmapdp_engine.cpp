@@ -1587,7 +1587,7 @@ struct gmapdp_oligo_plan {
   std::vector<std::pair<int, int>> launches;  // (first, count)
   std::vector<int> umax;
   size_t table_cap = 0, diag_cap = 0;
-  // get_mappings' event pool (5 slots per hit, shared by the batch through an atomic cursor; a
+  // get_mappings' event pool (3 slots per hit, shared by the batch through an atomic cursor; a
   // problem that no longer fits runs the sequential walk in its own scratch instead)
   uint64_t* d_pool = nullptr;
   unsigned long long* d_pool_counter = nullptr;
@@ -1646,7 +1646,7 @@ int gmapdp_oligo_plan_create(gmapdp_ctx* ctx, const gmapdp_oligo_problem* proble
     d.diag_offset = (int64_t)doff;
     d.scratch_offset = (int64_t)soff;
     toff += oligo_table_cap(p);
-    pslots += 5 * std::min<size_t>(oligo_table_cap(p), 2 * (size_t)p.querylength + 256);  // hits ~ query 8-mers
+    pslots += 3 * std::min<size_t>(oligo_table_cap(p), 2 * (size_t)p.querylength + 256);  // hits ~ query 8-mers
     doff += oligo_diag_cap(p);
     soff += align_up(scratch_bytes_oi(p.querylength, p.chrend > p.chrstart ? p.chrend - p.chrstart : 0), 256);
     classes[umax].push_back(i);

@@ -122,27 +122,31 @@ __device__ __forceinline__ int seg_scan_min(int lane, int x, int e, int segstart
   return x;
 }
 
-// Returns false (nothing written) when the shared event pool cannot hold this problem's 5 E slots.
-__device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t chrinit, int lookback, int suffn,
-                                   const int32_t* __restrict__ npq, const int32_t* __restrict__ mpq,
-                                   const int* __restrict__ cum, const uint32_t* __restrict__ table_all,
-                                   uint64_t* __restrict__ pool, unsigned long long* pool_counter,
-                                   unsigned long long pool_cap, uint32_t* hist, int32_t* __restrict__ good,
-                                   int& ngood_out, int& maxn_out) {
+// Returns false (nothing written) when the shared event pool cannot hold this problem's 3 E slots.
+// maxdiag bounds every diagi (querylength + genomiclength); hist is 4 x 256 LDS counters.
+__device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t maxdiag, uint32_t chrinit,
+                                   int lookback, int suffn, const int32_t* __restrict__ npq,
+                                   const int32_t* __restrict__ mpq, const int* __restrict__ cum,
+                                   const uint32_t* __restrict__ table_all, uint64_t* __restrict__ pool,
+                                   unsigned long long* pool_counter, unsigned long long pool_cap, uint32_t* hist,
+                                   int32_t* __restrict__ good, int& ngood_out, int& maxn_out) {
   unsigned long long base = 0;
-  if (lane == 0) base = atomicAdd(pool_counter, 5ull * (unsigned long long)E);
+  if (lane == 0) base = atomicAdd(pool_counter, 3ull * (unsigned long long)E);
   base = __shfl(base, 0, 64);
-  if (base + 5ull * (unsigned long long)E > pool_cap) return false;
-  uint64_t* evA = pool + base;                                  // events (diagi << 32 | q)
-  uint64_t* evB = evA + E;                                      // radix-sort ping-pong
-  int2* rsds = reinterpret_cast<int2*>(evB + E);                // per event: run start, diagonal start
-  int2* head = rsds + E;                                        // at a diagonal's start: best n, its first event
-  int4* grec = reinterpret_cast<int4*>(head + E);               // good records before ordering (<= E/2)
+  if (base + 3ull * (unsigned long long)E > pool_cap) return false;
+  uint64_t* evA = pool + base;                      // events (diagi << 32 | q)
+  uint64_t* evB = evA + E;                          // radix-sort ping-pong
+  int4* grec = reinterpret_cast<int4*>(evB + E);    // good records (at most E / 2)
+  int npass = 0;                                    // 8-bit digits of the largest possible diagi
+  while (npass < 4 && (maxdiag >> (8 * npass)) != 0) npass++;
+  for (int i = lane; i < 4 * 256; i += 64) hist[i] = 0u;
+  __syncthreads();
 
-  // events in query order, hits of one querypos in table (ascending chrpos) order
-  // 64 query positions per chunk (their nhits / table offsets loaded a chunk ahead); the chunk's
-  // events go out 64 at a time, each lane finding its event's query position by a binary search
-  // over the positions' exclusive offsets (ds_bpermute), so the table loads all issue together
+  // Events in query order, hits of one querypos in table (ascending chrpos) order, 64 query positions
+  // per chunk (their nhits / table offsets loaded a chunk ahead).  The chunk's events go out 64 at a
+  // time, each lane finding its event's query position by a binary search over the positions'
+  // exclusive offsets (ds_bpermute), so the table loads all issue together.  The digit histograms of
+  // every radix pass are counted here, so the sort never re-reads the keys to count them.
   int eoff = 0;
   int nh_n = 0, mo_n = 0;
   if (lane < nq) {
@@ -168,46 +172,34 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t c
       const int h = j - __shfl(excl, l, 64);
       const int mol = __shfl(mo, l, 64);
       const int q = cb + l;
-      if (j < T)
-        evA[eoff + j] = ((uint64_t)(table_all[mol + h] + (uint32_t)(qlen - q) - chrinit) << 32) | (uint32_t)q;
+      if (j < T) {
+        const uint32_t di = table_all[mol + h] + (uint32_t)(qlen - q) - chrinit;
+        evA[eoff + j] = ((uint64_t)di << 32) | (uint32_t)q;
+        for (int p = 0; p < npass; p++) atomicAdd(&hist[256 * p + ((di >> (8 * p)) & 255u)], 1u);
+      }
     }
     eoff += T;
   }
   __threadfence_block();
+  __syncthreads();
   OI_MARK(5);
 
-  // stable LSD radix sort on diagi, 8-bit digits (diagi <= qlen + genomiclength)
+  // stable LSD radix sort on diagi
   uint64_t* src = evA;
   uint64_t* dst = evB;
-  uint32_t maxd = 0;
-  for (int e = lane; e < E; e += 64) maxd = max(maxd, (uint32_t)(evA[e] >> 32));
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) maxd = max(maxd, (uint32_t)__shfl_xor((int)maxd, off, 64));
-  for (int shift = 0; shift < 32 && (maxd >> shift) != 0; shift += 8) {
-    for (int i = lane; i < 256; i += 64) hist[i] = 0u;
-    __syncthreads();
-    for (int e0 = 0; e0 < E; e0 += 4 * 64) {  // 4 chunks' loads in flight, then their atomics
-      uint64_t kk[4];
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int e = e0 + 64 * r + lane;
-        kk[r] = e < E ? src[e] : 0ull;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; r++)
-        if (e0 + 64 * r + lane < E) atomicAdd(&hist[(uint32_t)(kk[r] >> (32 + shift)) & 255u], 1u);
-    }
-    __syncthreads();
+  for (int p = 0; p < npass; p++) {
+    uint32_t* hp = hist + 256 * p;
+    const int shift = 8 * p;
     uint32_t h4[4], hs = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      h4[k] = hist[4 * lane + k];
+      h4[k] = hp[4 * lane + k];
       hs += h4[k];
     }
     uint32_t at = (uint32_t)wave_scan_add(lane, (int)hs) - hs;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      hist[4 * lane + k] = at;
+      hp[4 * lane + k] = at;
       at += h4[k];
     }
     __syncthreads();
@@ -225,10 +217,10 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t c
         eq &= ((d >> b) & 1u) ? m : ~m;
       }
       const int rank = lanes_below(eq, lane);
-      const uint32_t pos = v ? hist[d] : 0u;  // every lane reads before any lane bumps
+      const uint32_t pos = v ? hp[d] : 0u;  // every lane reads before any lane bumps
       __syncthreads();
       if (v) dst[pos + rank] = key;
-      if (v && rank == 0) hist[d] = pos + (uint32_t)__popcll(eq);
+      if (v && rank == 0) hp[d] = pos + (uint32_t)__popcll(eq);
       __syncthreads();
     }
     __threadfence_block();
@@ -240,9 +232,13 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t c
   __threadfence_block();
   OI_MARK(6);
 
-  // sweep: runs, diagonal maxima, the first hit reaching suffn per diagonal, the global maximum
-  int c_rs = -1, c_ds = -1, c_fs = 0x7fffffff, ngood = 0, M = 0;
+  // Sweep: runs, each diagonal's maximum and its first event, the first event reaching suffn; a
+  // diagonal's last event appends its record when it is good.  Per lane, the largest n seen and the
+  // smallest (querypos, diagi) event carrying it (the fallback best).  Nothing is stored per event.
+  int c_rs = -1, c_ds = -1, c_fs = 0x7fffffff, ngood = 0;
   uint64_t c_mk = 0, c_key = 0;
+  int bm = -1, be = -1;
+  uint64_t bkey = ~0ull;
   uint64_t knext = lane < E ? S[lane] : ~0ull;  // one chunk ahead
   for (int e0 = 0; e0 < E; e0 += 64) {
     const int e = e0 + lane;
@@ -261,29 +257,32 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t c
     const int rs = max(wave_scan_max(newrun ? e : -1), c_rs);
     const int ds = max(wave_scan_max(newdiag ? e : -1), c_ds);
     const int n = e - rs;
-    if (v) rsds[e] = make_int2(rs, ds);
     uint64_t mk = v ? (((uint64_t)(uint32_t)n << 32) | (uint64_t)(~(uint32_t)e)) : 0ull;
     mk = seg_scan_max64(lane, mk, e, ds);
     if (ds < e0 && c_mk > mk) mk = c_mk;
     int fs = (v && n == suffn) ? e : 0x7fffffff;
     fs = seg_scan_min(lane, fs, e, ds);
     if (ds < e0) fs = min(fs, c_fs);
-    // the diagonal's last hit records its maximum at the diagonal's head
     uint64_t nk = __shfl_down(key, 1, 64);
     {
       const uint64_t first_next = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(knext >> 32), 0) << 32) |
                                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)knext, 0);
       if (lane == 63) nk = (e + 1 < E) ? first_next : ~0ull;
     }
-    if (v && (e + 1 == E || (uint32_t)(nk >> 32) != d)) head[ds] = make_int2((int)(mk >> 32), (int)~(uint32_t)mk);
-    const bool isgood = v && n == suffn && fs == e;
+    const bool dend = v && (e + 1 == E || (uint32_t)(nk >> 32) != d);
+    const bool isgood = dend && fs != 0x7fffffff;
     const uint64_t gm = ballot(isgood);
-    if (isgood) grec[ngood + lanes_below(gm, lane)] = make_int4(e, 0, 0, 0);
+    if (isgood)  // {first event with n == suffn, first event with the maximum, the maximum, diagi}
+      grec[ngood + lanes_below(gm, lane)] = make_int4(fs, (int)~(uint32_t)mk, (int)(mk >> 32), (int)d);
     ngood += __popcll(gm);
-    int mx = v ? n : 0;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) mx = max(mx, __shfl_xor(mx, off, 64));
-    M = max(M, mx);
+    if (v) {
+      const uint64_t k2 = ((uint64_t)q << 32) | d;
+      if (n > bm || (n == bm && k2 < bkey)) {
+        bm = n;
+        bkey = k2;
+        be = e;
+      }
+    }
     c_rs = __builtin_amdgcn_readlane(rs, 63);
     c_ds = __builtin_amdgcn_readlane(ds, 63);
     c_fs = __builtin_amdgcn_readlane(fs, 63);
@@ -292,44 +291,35 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t c
     c_key = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(key >> 32), 63) << 32) |
             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, 63);
   }
-  __threadfence_block();
-  if (ngood == 0 && M > 0) {  // the best diagonal: the first (querypos, diagi) hit with n == M
-    uint64_t bk = ~0ull;
-    int be = -1;
-    for (int e = lane; e < E; e += 64) {
-      if (e - rsds[e].x == M) {
-        const uint64_t key = S[e];
-        const uint64_t k2 = (key << 32) | (key >> 32);
-        if (k2 < bk) {
-          bk = k2;
-          be = e;
-        }
-      }
-    }
+  // the global maximum and the first (querypos, diagi) event carrying it
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      const uint64_t ok = __shfl_xor(bk, off, 64);
-      const int oe = __shfl_xor(be, off, 64);
-      if (ok < bk) {
-        bk = ok;
-        be = oe;
-      }
+  for (int off = 32; off >= 1; off >>= 1) {
+    const int om = __shfl_xor(bm, off, 64);
+    const uint64_t ok = __shfl_xor(bkey, off, 64);
+    const int oe = __shfl_xor(be, off, 64);
+    if (om > bm || (om == bm && ok < bkey)) {
+      bm = om;
+      bkey = ok;
+      be = oe;
     }
-    if (lane == 0) grec[0] = make_int4(be, 0, 0, 0);
+  }
+  const int M = max(bm, 0);
+  __threadfence_block();
+  if (ngood == 0 && M > 0) {
+    if (lane == 0) grec[0] = make_int4(-1, be, M, (int)(uint32_t)bkey);
     ngood = 1;
   }
   __threadfence_block();
   // records and their (querypos, diagi) keys; then the reference's order
   uint64_t* gkey = (S == evA) ? evB : evA;  // the free sort buffer
   for (int g = lane; g < ngood; g += 64) {
-    const int e = grec[g].x;
-    const uint64_t key = S[e];
-    const int2 hb = head[rsds[e].y];  // (best n, the first event reaching it)
-    const int eb = hb.y;
-    const uint32_t di = (uint32_t)(key >> 32);
-    gkey[g] = (key << 32) | (key >> 32);
+    const int4 r = grec[g];
+    const uint32_t di = (uint32_t)r.w;
+    const int eb = r.y, bn = r.z;
+    const uint32_t qreach = r.x >= 0 ? (uint32_t)S[r.x] : 0u;
+    gkey[g] = ((uint64_t)qreach << 32) | di;
     grec[g] = make_int4(di >= (uint32_t)qlen ? (int)(di - (uint32_t)qlen) : (int)((uint32_t)qlen - di),
-                        (int)(uint32_t)S[rsds[eb].x], (int)(uint32_t)S[eb], hb.x + 1);
+                        (int)(uint32_t)S[eb - bn], (int)(uint32_t)S[eb], bn + 1);
   }
   __threadfence_block();
   for (int g = lane; g < ngood; g += 64) {
@@ -554,7 +544,7 @@ __global__ __launch_bounds__(64) void oi_map_kernel(
     gmapdp_oligo_result* __restrict__ results, const int32_t* __restrict__ npos_out,
     const int32_t* __restrict__ map_out, const uint32_t* __restrict__ table_all, int32_t* __restrict__ diag_all,
     uint64_t* __restrict__ pool, unsigned long long* __restrict__ pool_counter, unsigned long long pool_cap) {
-  __shared__ uint32_t hist[256];
+  __shared__ uint32_t hist[4 * 256];
   const int lane = threadIdx.x;
   const DevOligoProblem P = probs[blockIdx.x];
   if (P.chrend <= P.chrstart) return;  // oned_matrix_p stays 0 (oi_kernel wrote the record)
@@ -572,8 +562,9 @@ __global__ __launch_bounds__(64) void oi_map_kernel(
     const uint32_t chrinit = P.plusp ? P.chrstart : (P.chrhigh - P.chroffset) - P.chrend;
     int32_t* good = diag_all + 4 * P.diag_offset;  // records {diag, best_start, best_end, best_n + 1}
     int ngood = 0, maxn = 0;
-    if (!oi_mappings_sorted(lane, qlen, nq, totalpositions, chrinit, diag_lookback, suffn, npq, mpq, cum, table_all,
-                            pool, pool_counter, pool_cap, hist, good, ngood, maxn)) {
+    const uint32_t maxdiag = (uint32_t)qlen + (P.chrend - P.chrstart);
+    if (!oi_mappings_sorted(lane, qlen, nq, totalpositions, maxdiag, chrinit, diag_lookback, suffn, npq, mpq, cum,
+                            table_all, pool, pool_counter, pool_cap, hist, good, ngood, maxn)) {
       // the event pool is full: the sequential walk (per-diagonal states in this problem's scratch)
       unsigned char* initp = base_s + so.initp;
       OiState* st = reinterpret_cast<OiState*>(base_s + so.states);
