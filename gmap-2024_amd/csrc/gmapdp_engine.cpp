@@ -67,9 +67,9 @@ hipError_t launch_cg(bool simd, int RB, int nproblems, size_t lds, hipStream_t s
                      const int* order, unsigned char* gscratch, const uint32_t* blocks, uint64_t nwords,
                      const char* qseq, const char* qseq_uc, const int8_t* sctab, const uint8_t* constab,
                      gmapdp_cdna_result* results, gmapdp_pair* pairs);
-size_t lds_bytes_oi(int umax);
+size_t lds_bytes_oi(int umax, bool wide);
 size_t scratch_bytes_oi(int querylength, uint32_t genomiclength);
-hipError_t launch_oi(int nproblems, size_t lds, hipStream_t stream, const DevOligoProblem* probs,
+hipError_t launch_oi(bool wide, int nproblems, size_t lds, hipStream_t stream, const DevOligoProblem* probs,
                      const uint32_t* blocks, const char* quc, unsigned char* scratch, gmapdp_oligo_result* results,
                      int32_t* npos, int32_t* map, uint32_t* table, int32_t* diags, uint64_t* pool,
                      unsigned long long* pool_counter, unsigned long long pool_cap);
@@ -1585,7 +1585,7 @@ struct gmapdp_oligo_plan {
   DevOligoProblem* d_probs = nullptr;
   unsigned char* d_scratch = nullptr;
   std::vector<std::pair<int, int>> launches;  // (first, count)
-  std::vector<int> umax;
+  std::vector<int> umax;  // per launch: 2 * umax + (32-bit counters)
   size_t table_cap = 0, diag_cap = 0;
   // get_mappings' event pool (3 slots per hit, shared by the batch through an atomic cursor; a
   // problem that no longer fits runs the sequential walk in its own scratch instead)
@@ -1649,7 +1649,9 @@ int gmapdp_oligo_plan_create(gmapdp_ctx* ctx, const gmapdp_oligo_problem* proble
     pslots += 3 * std::min<size_t>(oligo_table_cap(p), 2 * (size_t)p.querylength + 256);  // hits ~ query 8-mers
     doff += oligo_diag_cap(p);
     soff += align_up(scratch_bytes_oi(p.querylength, p.chrend > p.chrstart ? p.chrend - p.chrstart : 0), 256);
-    classes[umax].push_back(i);
+    // launch class: (umax, 32-bit counters); 16-bit counters when no count can reach 2^16
+    const int wide = oligo_window(p) >= 65536 ? 1 : 0;
+    classes[2 * umax + wide].push_back(i);
   }
   if (toff > 0x7fffffffull) return bad(ctx, "stage-2 table arena beyond 2^31 entries");
   gmapdp_oligo_plan* P = new gmapdp_oligo_plan();
@@ -1694,7 +1696,8 @@ int gmapdp_oligo_plan_run(gmapdp_ctx* ctx, const gmapdp_oligo_plan* plan, const 
   if (hipMemsetAsync(plan->d_pool_counter, 0, sizeof(unsigned long long), s) != hipSuccess)
     return fail(ctx, GMAPDP_ELAUNCH, "oligo pool reset: %s", hipGetLastError());
   for (size_t li = 0; li < plan->launches.size(); li++) {
-    const hipError_t e = launch_oi(plan->launches[li].second, lds_bytes_oi(plan->umax[li]), s,
+    const int key = plan->umax[li];
+    const hipError_t e = launch_oi(key & 1, plan->launches[li].second, lds_bytes_oi(key >> 1, key & 1), s,
                                    plan->d_probs + plan->launches[li].first, ctx->d_genome, d_qseq_uc,
                                    plan->d_scratch, d_results, d_npositions, d_mappings, d_positions, d_diagonals,
                                    plan->d_pool, plan->d_pool_counter, plan->pool_cap);

@@ -333,6 +333,19 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
   return true;
 }
 
+// Per-id counters: 16-bit when the window has fewer than 65536 8-mer starts (no count or table
+// offset can reach 2^16, and the 28-KB LDS of a 2-kb read drops to 20 KB: 8 waves per CU, not 5),
+// 32-bit otherwise.  Pass 1 increments a 16-bit counter through its 32-bit word.
+template <typename CT>
+__device__ __forceinline__ void count_inc(CT* cnt, int u) {
+  if constexpr (sizeof(CT) == 4) {
+    atomicAdd(reinterpret_cast<uint32_t*>(cnt) + u, 1u);
+  } else {
+    atomicAdd(reinterpret_cast<uint32_t*>(cnt) + (u >> 1), 1u << (16 * (u & 1)));
+  }
+}
+
+template <typename CT>
 __global__ __launch_bounds__(64) void oi_kernel(
     const DevOligoProblem* __restrict__ probs, const uint32_t* __restrict__ blocks, const char* __restrict__ quc_all,
     unsigned char* __restrict__ scratch, gmapdp_oligo_result* __restrict__ results, int32_t* __restrict__ npos_out,
@@ -342,8 +355,8 @@ __global__ __launch_bounds__(64) void oi_kernel(
   const DevOligoProblem P = probs[blockIdx.x];
   uint32_t* bitmap = reinterpret_cast<uint32_t*>(smem);                  // 2048 words
   uint16_t* wrank = reinterpret_cast<uint16_t*>(smem + 4 * kOiWords);     // set bits before word w
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(smem + 6 * kOiWords);       // per id: count, then remaining
-  uint32_t* offs = cnt + P.umax;                                          // per id: table offset
+  CT* cnt = reinterpret_cast<CT*>(smem + 6 * kOiWords);                   // per id: count, then remaining
+  CT* offs = cnt + P.umax;                                                // per id: table offset
   const char* quc = quc_all + P.qoff;
   const int qlen = P.querylength;
   OI_MARK(0);
@@ -390,7 +403,7 @@ __global__ __launch_bounds__(64) void oi_kernel(
   }
   const int U = run;  // <= umax (the host counted them)
   OI_MARK(1);
-  for (int u = lane; u < U; u += 64) cnt[u] = 0u;
+  for (int u = lane; u < U; u += 64) cnt[u] = 0;
   __syncthreads();
 
   // ---- pass 1: counts of the window's query 8-mers ----
@@ -432,7 +445,7 @@ __global__ __launch_bounds__(64) void oi_kernel(
       }
 #pragma unroll
       for (int j = 0; j < 16; j++)
-        if ((hm >> j) & 1u) atomicAdd(&cnt[id[j]], 1u);
+        if ((hm >> j) & 1u) count_inc(cnt, id[j]);
       const int c = __popc(hm);
       const int incl = wave_scan_add(lane, c);
       int o = nhits + incl - c;
@@ -447,11 +460,11 @@ __global__ __launch_bounds__(64) void oi_kernel(
   uint32_t tot = 0;
   for (int base = 0; base < U; base += 64) {
     const int u = base + lane;
-    const uint32_t c = u < U ? (cnt[u] & 255u) : 0u;
+    const uint32_t c = u < U ? ((uint32_t)cnt[u] & 255u) : 0u;
     const uint32_t incl = (uint32_t)wave_scan_add(lane, (int)c);
     if (u < U) {
-      offs[u] = tot + incl - c;
-      cnt[u] = c;
+      offs[u] = (CT)(tot + incl - c);
+      cnt[u] = (CT)c;
     }
     tot += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   }
@@ -486,13 +499,13 @@ __global__ __launch_bounds__(64) void oi_kernel(
       const int r0 = (int)cnt[id];  // every lane reads before the first lane of each oligo writes
       if (r0 - rank > 0)
         table[offs[id] + r0 - rank - 1] = chrpos0 + (P.plusp ? k : (uint32_t)(npos - 1) - k);
-      if (rank == 0) cnt[id] = (uint32_t)max(r0 - same, 0);
+      if (rank == 0) cnt[id] = (CT)max(r0 - same, 0);
     }
   }
   __syncthreads();
   // the per-id counts again (nhits of lookup, :34074)
   OI_MARK(3);
-  for (int u = lane; u < U; u += 64) cnt[u] = (u + 1 < U ? offs[u + 1] : tot) - offs[u];
+  for (int u = lane; u < U; u += 64) cnt[u] = (CT)((u + 1 < U ? (uint32_t)offs[u + 1] : tot) - (uint32_t)offs[u]);
   __threadfence_block();
   __syncthreads();
 
@@ -522,7 +535,7 @@ __global__ __launch_bounds__(64) void oi_kernel(
         const int u = oligo_id(bitmap, wrank, (uint32_t)m, in);
         nh = (int)cnt[u];
         npq[i] = nh;
-        mpq[i] = nh > 0 ? (int32_t)(P.table_offset + offs[u]) : -1;
+        mpq[i] = nh > 0 ? (int32_t)(P.table_offset + (uint32_t)offs[u]) : -1;
       }
     }
     const int incl = wave_scan_add(lane, nh == 0 ? 1 : 0);
@@ -668,16 +681,16 @@ extern "C" int gmapdp_debug_oi_marks(unsigned long long* out) {
 }
 #endif
 
-size_t lds_bytes_oi(int umax) { return 6 * (size_t)kOiWords + 8 * (size_t)umax; }
+size_t lds_bytes_oi(int umax, bool wide) { return 6 * (size_t)kOiWords + (wide ? 8 : 4) * (size_t)umax; }
 size_t scratch_bytes_oi(int querylength, uint32_t genomiclength) {
   return scratch_oi(querylength, genomiclength).total;
 }
 
-hipError_t launch_oi(int nproblems, size_t lds, hipStream_t stream, const DevOligoProblem* probs,
+hipError_t launch_oi(bool wide, int nproblems, size_t lds, hipStream_t stream, const DevOligoProblem* probs,
                      const uint32_t* blocks, const char* quc, unsigned char* scratch, gmapdp_oligo_result* results,
                      int32_t* npos, int32_t* map, uint32_t* table, int32_t* diags, uint64_t* pool,
                      unsigned long long* pool_counter, unsigned long long pool_cap) {
-  void* fn = reinterpret_cast<void*>(&oi_kernel);
+  void* fn = wide ? reinterpret_cast<void*>(&oi_kernel<uint32_t>) : reinterpret_cast<void*>(&oi_kernel<uint16_t>);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;

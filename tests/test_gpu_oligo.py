@@ -135,3 +135,28 @@ def test_gpu_oligo_pool_overflow_falls_back(engine, monkeypatch):
         monkeypatch.setenv("GMAPDP_OLIGO_POOL_SLOTS", slots)
         d = _first_diff(engine.oligo_mappings_batch(probs), exp)
         assert d is None, _msg(probs, d, "oracle (pool %s)" % slots)
+
+
+def test_gpu_oligo_wide_windows_match_oracle(engine):
+    """Windows of 65 536 or more 8-mer starts take the 32-bit-counter build of oi_kernel; with a
+    poly-A stretch some counts wrap Count_T many times over."""
+    rng = random.Random(8500)
+    g = bytearray(random_genome(rng, 400000))
+    g[250000:252000] = b"A" * 2000
+    g = bytes(g)
+    engine.set_genome(g)
+    orc = Oracle()
+    orc.set_genome(g)
+    probs = []
+    for i in range(40):
+        p = oligo_problem(rng, g, edge=(i % 5 == 0))
+        span = rng.randint(65536, 180000)
+        p["chrstart"] = max(0, min(p["chrstart"], len(g) - 2000 - span))
+        p["chrend"] = p["chrstart"] + span
+        if i % 3 == 0:
+            p["quc"] = b"A" * rng.randint(9, 300) + p["quc"]
+        probs.append(p)
+    got = engine.oligo_mappings_batch(probs)
+    exp = [orc.oligo_mappings(p) for p in probs]
+    d = _first_diff(got, exp)
+    assert d is None, _msg(probs, d, "oracle")
