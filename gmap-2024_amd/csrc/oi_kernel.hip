@@ -153,6 +153,9 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
     nh_n = npq[lane];
     mo_n = mpq[lane];
   }
+  bool p_live = false, p_ok = false;  // the previous group of 64 events, its table values in flight
+  uint32_t p_tv = 0;
+  int p_q = 0, p_dst = 0;
   for (int cb = 0; cb < nq; cb += 64) {
     const int nh = max(nh_n, 0), mo = mo_n;
     nh_n = 0;
@@ -172,13 +175,25 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
       const int h = j - __shfl(excl, l, 64);
       const int mol = __shfl(mo, l, 64);
       const int q = cb + l;
-      if (j < T) {
-        const uint32_t di = table_all[mol + h] + (uint32_t)(qlen - q) - chrinit;
-        evA[eoff + j] = ((uint64_t)di << 32) | (uint32_t)q;
+      // the table load of this group is in flight while the previous group is written out
+      const uint32_t tv = j < T ? table_all[mol + h] : 0u;
+      if (p_live && p_ok) {
+        const uint32_t di = p_tv + (uint32_t)(qlen - p_q) - chrinit;
+        evA[p_dst] = ((uint64_t)di << 32) | (uint32_t)p_q;
         for (int p = 0; p < npass; p++) atomicAdd(&hist[256 * p + ((di >> (8 * p)) & 255u)], 1u);
       }
+      p_live = true;
+      p_ok = j < T;
+      p_tv = tv;
+      p_q = q;
+      p_dst = eoff + j;
     }
     eoff += T;
+  }
+  if (p_live && p_ok) {
+    const uint32_t di = p_tv + (uint32_t)(qlen - p_q) - chrinit;
+    evA[p_dst] = ((uint64_t)di << 32) | (uint32_t)p_q;
+    for (int p = 0; p < npass; p++) atomicAdd(&hist[256 * p + ((di >> (8 * p)) & 255u)], 1u);
   }
   __threadfence_block();
   __syncthreads();
@@ -203,25 +218,36 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
       at += h4[k];
     }
     __syncthreads();
-    uint64_t knext = lane < E ? src[lane] : 0ull;  // one chunk ahead
-    for (int e0 = 0; e0 < E; e0 += 64) {
-      const int e = e0 + lane;
-      const bool v = e < E;
-      const uint64_t key = knext;
-      knext = e + 64 < E ? src[e + 64] : 0ull;
-      const uint32_t d = (uint32_t)(key >> (32 + shift)) & 255u;
-      uint64_t eq = ballot(v);
+    // 256 keys per step: their 4 loads and 4 stores each go out together (one memory round trip per
+    // step); the ranks are taken chunk by chunk in order, which keeps the sort stable
+    for (int e0 = 0; e0 < E; e0 += 4 * 64) {
+      uint64_t key[4];
+      uint32_t dpos[4];
 #pragma unroll
-      for (int b = 0; b < 8; b++) {
-        const uint64_t m = ballot((d >> b) & 1u);
-        eq &= ((d >> b) & 1u) ? m : ~m;
+      for (int r = 0; r < 4; r++) {
+        const int e = e0 + 64 * r + lane;
+        key[r] = e < E ? src[e] : 0ull;
       }
-      const int rank = lanes_below(eq, lane);
-      const uint32_t pos = v ? hp[d] : 0u;  // every lane reads before any lane bumps
-      __syncthreads();
-      if (v) dst[pos + rank] = key;
-      if (v && rank == 0) hp[d] = pos + (uint32_t)__popcll(eq);
-      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const bool v = e0 + 64 * r + lane < E;
+        const uint32_t d = (uint32_t)(key[r] >> (32 + shift)) & 255u;
+        uint64_t eq = ballot(v);
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+          const uint64_t m = ballot((d >> b) & 1u);
+          eq &= ((d >> b) & 1u) ? m : ~m;
+        }
+        const int rank = lanes_below(eq, lane);
+        const uint32_t pos = v ? hp[d] : 0u;  // every lane reads before any lane bumps
+        __syncthreads();
+        dpos[r] = pos + (uint32_t)rank;
+        if (v && rank == 0) hp[d] = pos + (uint32_t)__popcll(eq);
+        __syncthreads();
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+        if (e0 + 64 * r + lane < E) dst[dpos[r]] = key[r];
     }
     __threadfence_block();
     uint64_t* t = src;
@@ -239,57 +265,76 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
   uint64_t c_mk = 0, c_key = 0;
   int bm = -1, be = -1;
   uint64_t bkey = ~0ull;
-  uint64_t knext = lane < E ? S[lane] : ~0ull;  // one chunk ahead
-  for (int e0 = 0; e0 < E; e0 += 64) {
-    const int e = e0 + lane;
-    const bool v = e < E;
-    const uint64_t key = knext;
-    knext = e + 64 < E ? S[e + 64] : ~0ull;
-    uint64_t pk = __shfl_up(key, 1, 64);
-    if (lane == 0) pk = c_key;
-    const uint32_t d = (uint32_t)(key >> 32), q = (uint32_t)key;
-    const bool newdiag = v && (e == 0 || (uint32_t)(pk >> 32) != d);
-    bool newrun = newdiag;
-    if (v && !newdiag) {
-      const uint32_t pq = (uint32_t)pk;
-      newrun = (int)(q - pq) >= lookback + cum[q] - cum[pq];
+  // 256 events per step: their key loads, then their cum_nohits loads, go out together (two memory
+  // round trips per step); the 4 chunks are then scanned in order with the carries
+  for (int s0 = 0; s0 < E; s0 += 4 * 64) {
+    uint64_t key[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int e = s0 + 64 * r + lane;
+      key[r] = e < E ? S[e] : ~0ull;
     }
-    const int rs = max(wave_scan_max(newrun ? e : -1), c_rs);
-    const int ds = max(wave_scan_max(newdiag ? e : -1), c_ds);
-    const int n = e - rs;
-    uint64_t mk = v ? (((uint64_t)(uint32_t)n << 32) | (uint64_t)(~(uint32_t)e)) : 0ull;
-    mk = seg_scan_max64(lane, mk, e, ds);
-    if (ds < e0 && c_mk > mk) mk = c_mk;
-    int fs = (v && n == suffn) ? e : 0x7fffffff;
-    fs = seg_scan_min(lane, fs, e, ds);
-    if (ds < e0) fs = min(fs, c_fs);
-    uint64_t nk = __shfl_down(key, 1, 64);
-    {
-      const uint64_t first_next = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(knext >> 32), 0) << 32) |
-                                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)knext, 0);
-      if (lane == 63) nk = (e + 1 < E) ? first_next : ~0ull;
+    const uint64_t after = s0 + 4 * 64 < E ? S[s0 + 4 * 64] : ~0ull;  // the event after this step
+    uint64_t pkey[4];
+    int cq[4], cpq[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      uint64_t pk = __shfl_up(key[r], 1, 64);
+      if (lane == 0)
+        pk = r == 0 ? c_key
+                    : (((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(key[r - 1] >> 32), 63) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key[r - 1], 63));
+      pkey[r] = pk;
+      const bool v = s0 + 64 * r + lane < E;
+      cq[r] = v ? cum[(uint32_t)key[r]] : 0;
+      cpq[r] = v ? cum[(uint32_t)pk] : 0;
     }
-    const bool dend = v && (e + 1 == E || (uint32_t)(nk >> 32) != d);
-    const bool isgood = dend && fs != 0x7fffffff;
-    const uint64_t gm = ballot(isgood);
-    if (isgood)  // {first event with n == suffn, first event with the maximum, the maximum, diagi}
-      grec[ngood + lanes_below(gm, lane)] = make_int4(fs, (int)~(uint32_t)mk, (int)(mk >> 32), (int)d);
-    ngood += __popcll(gm);
-    if (v) {
-      const uint64_t k2 = ((uint64_t)q << 32) | d;
-      if (n > bm || (n == bm && k2 < bkey)) {
-        bm = n;
-        bkey = k2;
-        be = e;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int e0 = s0 + 64 * r;
+      const int e = e0 + lane;
+      const bool v = e < E;
+      const uint64_t key_r = key[r], pk = pkey[r];
+      const uint32_t d = (uint32_t)(key_r >> 32), q = (uint32_t)key_r;
+      const bool newdiag = v && (e == 0 || (uint32_t)(pk >> 32) != d);
+      bool newrun = newdiag;
+      if (v && !newdiag) newrun = (int)(q - (uint32_t)pk) >= lookback + cq[r] - cpq[r];
+      const int rs = max(wave_scan_max(newrun ? e : -1), c_rs);
+      const int ds = max(wave_scan_max(newdiag ? e : -1), c_ds);
+      const int n = e - rs;
+      uint64_t mk = v ? (((uint64_t)(uint32_t)n << 32) | (uint64_t)(~(uint32_t)e)) : 0ull;
+      mk = seg_scan_max64(lane, mk, e, ds);
+      if (ds < e0 && c_mk > mk) mk = c_mk;
+      int fs = (v && n == suffn) ? e : 0x7fffffff;
+      fs = seg_scan_min(lane, fs, e, ds);
+      if (ds < e0) fs = min(fs, c_fs);
+      uint64_t nk = __shfl_down(key_r, 1, 64);
+      if (lane == 63)
+        nk = r < 3 ? (((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(key[r + 1] >> 32), 0) << 32) |
+                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key[r + 1], 0))
+                   : after;
+      const bool dend = v && (e + 1 == E || (uint32_t)(nk >> 32) != d);
+      const bool isgood = dend && fs != 0x7fffffff;
+      const uint64_t gm = ballot(isgood);
+      if (isgood)  // {first event with n == suffn, first event with the maximum, the maximum, diagi}
+        grec[ngood + lanes_below(gm, lane)] = make_int4(fs, (int)~(uint32_t)mk, (int)(mk >> 32), (int)d);
+      ngood += __popcll(gm);
+      if (v) {
+        const uint64_t k2 = ((uint64_t)q << 32) | d;
+        if (n > bm || (n == bm && k2 < bkey)) {
+          bm = n;
+          bkey = k2;
+          be = e;
+        }
       }
+      c_rs = __builtin_amdgcn_readlane(rs, 63);
+      c_ds = __builtin_amdgcn_readlane(ds, 63);
+      c_fs = __builtin_amdgcn_readlane(fs, 63);
+      c_mk = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(mk >> 32), 63) << 32) |
+             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mk, 63);
+      c_key = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(key_r >> 32), 63) << 32) |
+              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key_r, 63);
     }
-    c_rs = __builtin_amdgcn_readlane(rs, 63);
-    c_ds = __builtin_amdgcn_readlane(ds, 63);
-    c_fs = __builtin_amdgcn_readlane(fs, 63);
-    c_mk = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(mk >> 32), 63) << 32) |
-           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mk, 63);
-    c_key = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(key >> 32), 63) << 32) |
-            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, 63);
   }
   // the global maximum and the first (querypos, diagi) event carrying it
 #pragma unroll
