@@ -79,12 +79,13 @@ __device__ __forceinline__ int oligo_id(const uint32_t* bitmap, const uint16_t* 
 
 // per-problem scratch: cum_nohits (querylength + 1 ints), the genomicdiag init flags, the states
 struct ScratchOi {
-  size_t initp, states, hits, total;
+  size_t poolbase, initp, states, hits, total;
 };
 __host__ __device__ inline ScratchOi scratch_oi(int querylength, uint32_t genomiclength) {
   const size_t nd = (size_t)querylength + genomiclength + 1;
   ScratchOi s;
-  s.initp = align16(4 * (size_t)(querylength + 1));
+  s.poolbase = align16(4 * (size_t)(querylength + 1));  // the problem's event-pool offset (or ~0)
+  s.initp = align16(s.poolbase + 8);
   s.states = align16(s.initp + nd);
   s.hits = align16(s.states + nd * sizeof(OiState));
   s.total = align16(s.hits + 8 * ((size_t)genomiclength + 2));
@@ -122,18 +123,17 @@ __device__ __forceinline__ int seg_scan_min(int lane, int x, int e, int segstart
   return x;
 }
 
-// Returns false (nothing written) when the shared event pool cannot hold this problem's 3 E slots.
+// Returns false (nothing written) when the shared event pool could not hold this problem's 3 E slots
+// (oi_kernel took them, `base`, with one atomic as it finished).
 // maxdiag bounds every diagi (querylength + genomiclength); hist is 4 x 256 LDS counters.
 __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t maxdiag, uint32_t chrinit,
                                    int lookback, int suffn, const int32_t* __restrict__ npq,
                                    const int32_t* __restrict__ mpq, const int* __restrict__ cum,
                                    const uint32_t* __restrict__ table_all, uint64_t* __restrict__ pool,
-                                   unsigned long long* pool_counter, unsigned long long pool_cap, uint32_t* hist,
-                                   int32_t* __restrict__ good, int& ngood_out, int& maxn_out) {
-  unsigned long long base = 0;
-  if (lane == 0) base = atomicAdd(pool_counter, 3ull * (unsigned long long)E);
-  base = __shfl(base, 0, 64);
-  if (base + 3ull * (unsigned long long)E > pool_cap) return false;
+                                   unsigned long long base, uint32_t* hist,
+                                   int* evq, int32_t* __restrict__ good, int& ngood_out, int& maxn_out) {
+  OI_MARK(9);
+  if (base == ~0ull) return false;
   uint64_t* evA = pool + base;                      // events (diagi << 32 | q)
   uint64_t* evB = evA + E;                          // radix-sort ping-pong
   int4* grec = reinterpret_cast<int4*>(evB + E);    // good records (at most E / 2)
@@ -142,58 +142,66 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
   for (int i = lane; i < 4 * 256; i += 64) hist[i] = 0u;
   __syncthreads();
 
-  // Events in query order, hits of one querypos in table (ascending chrpos) order, 64 query positions
-  // per chunk (their nhits / table offsets loaded a chunk ahead).  The chunk's events go out 64 at a
-  // time, each lane finding its event's query position by a binary search over the positions'
-  // exclusive offsets (ds_bpermute), so the table loads all issue together.  The digit histograms of
-  // every radix pass are counted here, so the sort never re-reads the keys to count them.
+  // Events in query order, hits of one querypos in table (ascending chrpos) order, 256 query
+  // positions per step (their nhits / table offsets loaded a step ahead).  The step's exclusive event
+  // offsets and table offsets go to LDS; each event finds its query position there by binary search,
+  // 256 events at a time, so their table loads all issue together.  The digit histograms of every
+  // radix pass are counted here, so the sort never re-reads the keys to count them.
+  int* exo = evq;          // [256] exclusive event offset of each query position of the step
+  int* mos = evq + 256;    // [256] its table offset
   int eoff = 0;
-  int nh_n = 0, mo_n = 0;
-  if (lane < nq) {
-    nh_n = npq[lane];
-    mo_n = mpq[lane];
-  }
-  bool p_live = false, p_ok = false;  // the previous group of 64 events, its table values in flight
-  uint32_t p_tv = 0;
-  int p_q = 0, p_dst = 0;
-  for (int cb = 0; cb < nq; cb += 64) {
-    const int nh = max(nh_n, 0), mo = mo_n;
-    nh_n = 0;
-    if (cb + 64 + lane < nq) {
-      nh_n = npq[cb + 64 + lane];
-      mo_n = mpq[cb + 64 + lane];
-    }
-    const int incl = wave_scan_add(lane, nh);
-    const int excl = incl - nh;
-    const int T = __builtin_amdgcn_readlane(incl, 63);
-    for (int j0 = 0; j0 < T; j0 += 64) {
-      const int j = j0 + lane;
-      int l = 0;  // the last position whose events start at or before j
+  int nh_n[4], mo_n[4];
 #pragma unroll
-      for (int step = 32; step >= 1; step >>= 1)
-        if (__shfl(excl, l + step, 64) <= j) l += step;
-      const int h = j - __shfl(excl, l, 64);
-      const int mol = __shfl(mo, l, 64);
-      const int q = cb + l;
-      // the table load of this group is in flight while the previous group is written out
-      const uint32_t tv = j < T ? table_all[mol + h] : 0u;
-      if (p_live && p_ok) {
-        const uint32_t di = p_tv + (uint32_t)(qlen - p_q) - chrinit;
-        evA[p_dst] = ((uint64_t)di << 32) | (uint32_t)p_q;
-        for (int p = 0; p < npass; p++) atomicAdd(&hist[256 * p + ((di >> (8 * p)) & 255u)], 1u);
+  for (int r = 0; r < 4; r++) {
+    const int q = 64 * r + lane;
+    nh_n[r] = q < nq ? npq[q] : 0;
+    mo_n[r] = q < nq ? mpq[q] : 0;
+  }
+  for (int sb = 0; sb < nq; sb += 4 * 64) {
+    int nh[4], mo[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      nh[r] = max(nh_n[r], 0);
+      mo[r] = mo_n[r];
+      const int q = sb + 4 * 64 + 64 * r + lane;
+      nh_n[r] = q < nq ? npq[q] : 0;
+      mo_n[r] = q < nq ? mpq[q] : 0;
+    }
+    int run = 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int incl = wave_scan_add(lane, nh[r]);
+      exo[64 * r + lane] = run + incl - nh[r];
+      mos[64 * r + lane] = mo[r];
+      run += __builtin_amdgcn_readlane(incl, 63);
+    }
+    const int T = run;
+    __syncthreads();
+    for (int g0 = 0; g0 < T; g0 += 4 * 64) {
+      uint32_t tv[4];
+      int qv[4];
+#pragma unroll
+      for (int gi = 0; gi < 4; gi++) {
+        const int j = g0 + 64 * gi + lane;
+        int l = 0;  // the last position whose events start at or before j
+#pragma unroll
+        for (int step = 128; step >= 1; step >>= 1)
+          if (exo[l + step] <= j) l += step;
+        qv[gi] = sb + l;
+        tv[gi] = j < T ? table_all[mos[l] + (j - exo[l])] : 0u;
       }
-      p_live = true;
-      p_ok = j < T;
-      p_tv = tv;
-      p_q = q;
-      p_dst = eoff + j;
+#pragma unroll
+      for (int gi = 0; gi < 4; gi++) {
+        const int j = g0 + 64 * gi + lane;
+        if (j < T) {
+          const uint32_t di = tv[gi] + (uint32_t)(qlen - qv[gi]) - chrinit;
+          evA[eoff + j] = ((uint64_t)di << 32) | (uint32_t)qv[gi];
+          for (int p = 0; p < npass; p++) atomicAdd(&hist[256 * p + ((di >> (8 * p)) & 255u)], 1u);
+        }
+      }
     }
     eoff += T;
-  }
-  if (p_live && p_ok) {
-    const uint32_t di = p_tv + (uint32_t)(qlen - p_q) - chrinit;
-    evA[p_dst] = ((uint64_t)di << 32) | (uint32_t)p_q;
-    for (int p = 0; p < npass; p++) atomicAdd(&hist[256 * p + ((di >> (8 * p)) & 255u)], 1u);
+    __syncthreads();
   }
   __threadfence_block();
   __syncthreads();
@@ -394,7 +402,8 @@ template <typename CT>
 __global__ __launch_bounds__(64) void oi_kernel(
     const DevOligoProblem* __restrict__ probs, const uint32_t* __restrict__ blocks, const char* __restrict__ quc_all,
     unsigned char* __restrict__ scratch, gmapdp_oligo_result* __restrict__ results, int32_t* __restrict__ npos_out,
-    int32_t* __restrict__ map_out, uint32_t* __restrict__ table_all) {
+    int32_t* __restrict__ map_out, uint32_t* __restrict__ table_all, unsigned long long* __restrict__ pool_counter,
+    unsigned long long pool_cap) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x;
   const DevOligoProblem P = probs[blockIdx.x];
@@ -590,7 +599,18 @@ __global__ __launch_bounds__(64) void oi_kernel(
   }
   __threadfence_block();
   res.totalpositions = totalpositions;
-  if (lane == 0) results[P.index] = res;
+  if (lane == 0) {
+    results[P.index] = res;
+    // get_mappings' event pool: taken here, as the waves finish at scattered times, rather than by
+    // every oi_map_kernel wave at once on one address
+    unsigned long long b = ~0ull;
+    if (P.chrend > P.chrstart) {
+      const unsigned long long need = 3ull * (unsigned long long)totalpositions;
+      b = atomicAdd(pool_counter, need);
+      if (b + need > pool_cap) b = ~0ull;
+    }
+    *reinterpret_cast<unsigned long long*>(base_s + so.poolbase) = b;
+  }
   OI_MARK(4);
 }
 
@@ -601,8 +621,9 @@ __global__ __launch_bounds__(64) void oi_map_kernel(
     const DevOligoProblem* __restrict__ probs, unsigned char* __restrict__ scratch,
     gmapdp_oligo_result* __restrict__ results, const int32_t* __restrict__ npos_out,
     const int32_t* __restrict__ map_out, const uint32_t* __restrict__ table_all, int32_t* __restrict__ diag_all,
-    uint64_t* __restrict__ pool, unsigned long long* __restrict__ pool_counter, unsigned long long pool_cap) {
+    uint64_t* __restrict__ pool) {
   __shared__ uint32_t hist[4 * 256];
+  __shared__ int evq[2 * 256];
   const int lane = threadIdx.x;
   const DevOligoProblem P = probs[blockIdx.x];
   if (P.chrend <= P.chrstart) return;  // oned_matrix_p stays 0 (oi_kernel wrote the record)
@@ -622,7 +643,8 @@ __global__ __launch_bounds__(64) void oi_map_kernel(
     int ngood = 0, maxn = 0;
     const uint32_t maxdiag = (uint32_t)qlen + (P.chrend - P.chrstart);
     if (!oi_mappings_sorted(lane, qlen, nq, totalpositions, maxdiag, chrinit, diag_lookback, suffn, npq, mpq, cum,
-                            table_all, pool, pool_counter, pool_cap, hist, good, ngood, maxn)) {
+                            table_all, pool, *reinterpret_cast<const unsigned long long*>(base_s + so.poolbase), hist,
+                            evq, good, ngood, maxn)) {
       // the event pool is full: the sequential walk (per-diagonal states in this problem's scratch)
       unsigned char* initp = base_s + so.initp;
       OiState* st = reinterpret_cast<OiState*>(base_s + so.states);
@@ -741,11 +763,11 @@ hipError_t launch_oi(bool wide, int nproblems, size_t lds, hipStream_t stream, c
     if (e != hipSuccess) return e;
   }
   void* args[] = {(void*)&probs, (void*)&blocks, (void*)&quc, (void*)&scratch, (void*)&results, (void*)&npos,
-                  (void*)&map, (void*)&table};
+                  (void*)&map, (void*)&table, (void*)&pool_counter, (void*)&pool_cap};
   hipError_t e = hipLaunchKernel(fn, dim3(nproblems), dim3(64), args, lds, stream);
   if (e != hipSuccess) return e;
   void* margs[] = {(void*)&probs, (void*)&scratch, (void*)&results, (void*)&npos, (void*)&map, (void*)&table,
-                   (void*)&diags, (void*)&pool, (void*)&pool_counter, (void*)&pool_cap};
+                   (void*)&diags, (void*)&pool};
   return hipLaunchKernel(reinterpret_cast<void*>(&oi_map_kernel), dim3(nproblems), dim3(64), margs, 0, stream);
 }
 

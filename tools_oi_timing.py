@@ -16,7 +16,7 @@ import gmapdp  # noqa: E402
 import bench  # noqa: E402
 
 PHASES = ["set_inquery (bitmap, ids)", "pass 1 (counts) + layout", "pass 2 (store)", "npositions/mappings/cum",
-          "events", "radix sort", "sweep + records"]
+          "event pool allocation", "events", "radix sort", "sweep + records"]
 
 
 GG_PHASES = ["stage", "genome_gap_simple", "fills (L and R waves)", "bridge", "traceback R + reverse",
@@ -67,9 +67,9 @@ def main():
     torch.cuda.synchronize()
     lib.gmapdp_debug_oi_marks(marks.ctypes.data)
     t, c = marks[:16].astype(np.float64), marks[16:]
-    # oi_kernel: marks 0..4; oi_map_kernel: 8 (start), 5, 6, 7
-    spans = [(0, 1), (1, 2), (2, 3), (3, 4), (8, 5), (5, 6), (6, 7)]
-    out = {"waves": [int(c[k]) for k in (0, 1, 2, 3, 4, 8, 5, 6, 7)]}
+    # oi_kernel: marks 0..4; oi_map_kernel: 8 (start), 9 (pool allocated), 5, 6, 7
+    spans = [(0, 1), (1, 2), (2, 3), (3, 4), (8, 9), (9, 5), (5, 6), (6, 7)]
+    out = {"waves": [int(c[k]) for k in (0, 1, 2, 3, 4, 8, 9, 5, 6, 7)]}
     dur = [float(t[b] - t[a]) for a, b in spans]
     tot = sum(dur)
     out["wave_ms_total"] = tot / 1e5
