@@ -193,10 +193,20 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
 #pragma unroll
       for (int gi = 0; gi < 4; gi++) {
         const int j = g0 + 64 * gi + lane;
-        if (j < T) {
-          const uint32_t di = tv[gi] + (uint32_t)(qlen - qv[gi]) - chrinit;
-          evA[eoff + j] = ((uint64_t)di << 32) | (uint32_t)qv[gi];
-          for (int p = 0; p < npass; p++) atomicAdd(&hist[256 * p + ((di >> (8 * p)) & 255u)], 1u);
+        const bool v = j < T;
+        const uint32_t di = tv[gi] + (uint32_t)(qlen - qv[gi]) - chrinit;
+        if (v) evA[eoff + j] = ((uint64_t)di << 32) | (uint32_t)qv[gi];
+        // one LDS atomic per distinct digit: the hits of a group mostly share a few diagonals, and
+        // same-address atomics serialise
+        for (int p = 0; p < npass; p++) {
+          const uint32_t dg = (di >> (8 * p)) & 255u;
+          uint64_t eq = ballot(v);
+#pragma unroll
+          for (int b = 0; b < 8; b++) {
+            const uint64_t m = ballot((dg >> b) & 1u);
+            eq &= ((dg >> b) & 1u) ? m : ~m;
+          }
+          if (v && lanes_below(eq, lane) == 0) atomicAdd(&hist[256 * p + dg], (uint32_t)__popcll(eq));
         }
       }
     }
