@@ -229,14 +229,16 @@ def pmc_traffic(name):
     per MI355X_MICROARCH.md's gfx950 correction), or (None, None)."""
     import glob
     if name == "oi_kernel+oi_map_kernel":  # stage-2 seeding: the two kernels of one launch, summed
-        keys = ["gmapdp::oi_kernel", "gmapdp::oi_map_kernel"]
+        # oi_kernel<unsigned short>: the 16-bit-counter build every bench window (< 65536 starts) takes
         for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")), reverse=True):
             try:
                 ks = json.load(open(path))["kernels"]
             except (OSError, ValueError, KeyError):
                 continue
-            if all(k in ks for k in keys):
-                return sum(ks[k]["hbm_bytes_per_dispatch"] for k in keys), os.path.relpath(path, ROOT)
+            a = ks.get("gmapdp::oi_kernel<unsigned short>") or ks.get("gmapdp::oi_kernel")
+            b = ks.get("gmapdp::oi_map_kernel")
+            if a and b:
+                return a["hbm_bytes_per_dispatch"] + b["hbm_bytes_per_dispatch"], os.path.relpath(path, ROOT)
         return None, None
     m = re.match(r"(\w+)<R=(\d+),dirs_lds=(\d)>", name)
     if not m:
