@@ -237,6 +237,7 @@ struct PlanCore {
     size_t lds;      // LDS bucket per workgroup (kDpx: per problem slot)
     int first, count;
     double work;     // estimated wave-columns, for stream assignment
+    double span;     // the longest single problem's estimate: the class's latency floor
     size_t extra;    // kDpx: bytes of the whole-wave direction words (per workgroup)
     size_t gdirs_offset;  // kDpx with !dirs_lds: the class's region of the global scratch
     int stream;      // 0: the caller's stream, 1..3: the context's side streams
@@ -783,6 +784,7 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     }
     // work estimate: fill wave-columns (a packed wave fills 64/S problems at once)
     L.work = 0.0;
+    L.span = 0.0;
     L.extra = 0;
     L.gdirs_offset = 0;
     if (L.kind == PlanCore::kSx) {  // per wave: 4 direction words per fill step
@@ -809,6 +811,7 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
       }
     }
     for (int id : ids) {
+      const double w0 = L.work;
       if (L.kind == PlanCore::kGenomeGap) {
         const DevGenomeProblem& d = plan.gdev[id];
         L.work += (double)std::max(d.glengthL, d.glengthR) * L.R + d.rlength;
@@ -825,6 +828,9 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
         else
           L.work += (double)d.glength * (L.kind == PlanCore::kDpx ? L.R / 64.0 : L.R) + 0.25 * (d.rlength + d.glength);
       }
+      // a packed wave's problems fill side by side: its latency is one problem's columns
+      const double one = (L.kind == PlanCore::kDpx || L.kind == PlanCore::kSx) ? (L.work - w0) * 64.0 / L.R : L.work - w0;
+      L.span = std::max(L.span, one);
     }
     L.stream = 0;
     plan.launches.push_back(L);
@@ -846,9 +852,14 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
       plan.launches[i].stream = best;
       load[best] += plan.launches[i].work;
     }
+    // per stream, the classes with the longest single problems go first: they set the step's
+    // critical path, so they start at the fork instead of after the bulk classes
+    std::vector<int> byspan(idx);
+    std::stable_sort(byspan.begin(), byspan.end(),
+                     [&](int a, int b) { return plan.launches[a].span > plan.launches[b].span; });
     std::vector<PlanCore::Launch> sorted;
     for (int k = 0; k <= gmapdp_ctx::kAux; k++)
-      for (int i : idx)
+      for (int i : byspan)
         if (plan.launches[i].stream == k) sorted.push_back(plan.launches[i]);
     plan.launches.swap(sorted);
   }
