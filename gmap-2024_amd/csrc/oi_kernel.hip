@@ -431,31 +431,35 @@ __global__ __launch_bounds__(64) void oi_kernel(
   __syncthreads();
   int32_t* npq = npos_out + P.qoff;
   int32_t* mpq = map_out + P.qoff;  // holds each querypos's 8-mer (or -1) until get_mappings
-  // one coalesced character load per lane and chunk, issued two chunks ahead; the 8-mer at i takes
-  // the codes of lanes i..i+7 of this chunk and the next (ds_bpermute)
-  int c0 = lane < qlen ? nt_code(quc[lane]) : -1;
-  int c1 = 64 + lane < qlen ? nt_code(quc[64 + lane]) : -1;
-  for (int base = 0; base < qlen; base += 64) {
-    const int i2 = base + 128 + lane;
-    const int c2 = i2 < qlen ? nt_code(quc[i2]) : -1;
-    const int i = base + lane;
-    uint32_t m = 0;
-    bool ok = i < nq;
+  // 256 query positions per step: one coalesced character load per lane and chunk (5 chunks: the
+  // last supplies the 7-character overlap), all issued together; the 8-mer at i takes the codes of
+  // lanes i..i+7 of its chunk and the next (ds_bpermute)
+  for (int sb = 0; sb < qlen; sb += 4 * 64) {
+    int ch[5];
 #pragma unroll
-    for (int j = 0; j < kOiK; j++) {
-      const int src = (lane + j) & 63;
-      const int a = __shfl(c0, src, 64), b = __shfl(c1, src, 64);
-      const int cj = lane + j < 64 ? a : b;
-      ok = ok && cj >= 0;
-      m = (m << 2) | ((uint32_t)cj & 3u);
+    for (int r = 0; r < 5; r++) {
+      const int i = sb + 64 * r + lane;
+      ch[r] = i < qlen ? nt_code(quc[i]) : -1;
     }
-    if (i < qlen) {
-      mpq[i] = ok ? (int)m : -1;
-      npq[i] = 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int i = sb + 64 * r + lane;
+      uint32_t m = 0;
+      bool ok = i < nq;
+#pragma unroll
+      for (int j = 0; j < kOiK; j++) {
+        const int src = (lane + j) & 63;
+        const int a = __shfl(ch[r], src, 64), b = __shfl(ch[r + 1], src, 64);
+        const int cj = lane + j < 64 ? a : b;
+        ok = ok && cj >= 0;
+        m = (m << 2) | ((uint32_t)cj & 3u);
+      }
+      if (i < qlen) {
+        mpq[i] = ok ? (int)m : -1;
+        npq[i] = 0;
+      }
+      if (ok) atomicOr(&bitmap[m >> 5], 1u << (m & 31));
     }
-    if (ok) atomicOr(&bitmap[m >> 5], 1u << (m & 31));
-    c0 = c1;
-    c1 = c2;
   }
   __syncthreads();
   int run = 0;  // ids in oligo order: prefix popcounts over the bitmap words
@@ -586,26 +590,34 @@ __global__ __launch_bounds__(64) void oi_kernel(
   // whose 8-mer has no hit (a position without a full 8-mer carries it forward)
   int* cum = reinterpret_cast<int*>(base_s);
   int totalpositions = 0, cumrun = 0;
-  int mnext = lane < nq ? mpq[lane] : -1;  // one chunk ahead
-  for (int base = 0; base < nq; base += 64) {
-    const int i = base + lane;
-    const int m = mnext;
-    mnext = i + 64 < nq ? mpq[i + 64] : -1;
-    int nh = -1;
-    if (i < nq) {
-      mpq[i] = -1;
-      if (m >= 0) {
-        bool in;
-        const int u = oligo_id(bitmap, wrank, (uint32_t)m, in);
-        nh = (int)cnt[u];
-        npq[i] = nh;
-        mpq[i] = nh > 0 ? (int32_t)(P.table_offset + (uint32_t)offs[u]) : -1;
-      }
+  for (int sb = 0; sb < nq; sb += 4 * 64) {  // 256 query positions per step, loads issued together
+    int mm[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int i = sb + 64 * r + lane;
+      mm[r] = i < nq ? mpq[i] : -1;
     }
-    const int incl = wave_scan_add(lane, nh == 0 ? 1 : 0);
-    if (i < nq) cum[i] = cumrun + incl;
-    cumrun += __builtin_amdgcn_readlane(incl, 63);
-    totalpositions += __builtin_amdgcn_readlane(wave_scan_add(lane, nh > 0 ? nh : 0), 63);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int i = sb + 64 * r + lane;
+      const int m = mm[r];
+      int nh = -1;
+      if (i < nq) {
+        int mo = -1;
+        if (m >= 0) {
+          bool in;
+          const int u = oligo_id(bitmap, wrank, (uint32_t)m, in);
+          nh = (int)cnt[u];
+          npq[i] = nh;
+          if (nh > 0) mo = (int32_t)(P.table_offset + (uint32_t)offs[u]);
+        }
+        mpq[i] = mo;
+      }
+      const int incl = wave_scan_add(lane, nh == 0 ? 1 : 0);
+      if (i < nq) cum[i] = cumrun + incl;
+      cumrun += __builtin_amdgcn_readlane(incl, 63);
+      totalpositions += __builtin_amdgcn_readlane(wave_scan_add(lane, nh > 0 ? nh : 0), 63);
+    }
   }
   __threadfence_block();
   res.totalpositions = totalpositions;
