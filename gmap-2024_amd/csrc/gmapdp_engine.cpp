@@ -375,6 +375,8 @@ int gmapdp_pack_genome(const char* seq, uint64_t length, uint32_t* blocks) {
 
 int gmapdp_set_genome(gmapdp_ctx* ctx, const uint32_t* blocks, size_t nwords, uint64_t length) {
   if (!ctx || !blocks || nwords < (size_t)((length + 31) / 32) * 3) return GMAPDP_EINVAL;
+  // descriptors carry 32-bit coordinates (gmap's Univcoord_T); a gmapl-sized genome is refused
+  if (length > 0xFFFFFFFFull) return bad(ctx, "genome length >= 2^32 (gmapl genomes) is not supported");
   (void)hipSetDevice(ctx->device);
   if (ctx->d_genome) (void)hipFree(ctx->d_genome);
   ctx->d_genome = nullptr;

@@ -84,10 +84,43 @@ static Genome_T shim_genome = NULL;
 static int shim_mode = 0, shim_user_open = 0, shim_user_extend = 0, shim_user_dynprog_p = 0;
 static int shim_homopolymerp = 0, shim_splicing_iit = 0;
 
+/* Calls that reached the engine, per wrapped entry point (printed at exit with GMAPDP_SHIM_STATS=1;
+   tests use it to prove the pipeline really ran on the GPU). */
+enum { ST_SINGLE, ST_END5, ST_END3, ST_GENOME, ST_CDNA, ST_OLIGO, ST_N };
+static const char *const shim_stat_name[ST_N] = {"Dynprog_single_gap", "Dynprog_end5_gap", "Dynprog_end3_gap",
+                                                 "Dynprog_genome_gap", "Dynprog_cdna_gap",
+                                                 "Oligoindex_get_mappings"};
+static unsigned long shim_stats[ST_N];
+
+static void
+shim_print_stats (void) {
+  int i;
+  fprintf(stderr, "gmapdp shim calls:");
+  for (i = 0; i < ST_N; i++) fprintf(stderr, " %s=%lu", shim_stat_name[i], __atomic_load_n(&shim_stats[i], __ATOMIC_RELAXED));
+  fprintf(stderr, "\n");
+}
+
+static void
+shim_count (int which) {
+  __atomic_fetch_add(&shim_stats[which], 1UL, __ATOMIC_RELAXED);
+}
+
 static void
 shim_refuse (const char *what) {
   fprintf(stderr, "gmapdp shim: %s is not supported by the MI355X Dynprog engine\n", what);
   abort();
+}
+
+/* The engine's descriptors carry 32-bit genome coordinates (gmap's Univcoord_T, univcoord.h:9-11).
+   A gmapl build (LARGE_GENOMES, 64-bit Univcoord_T) or any coordinate at or above 2^32 is refused
+   instead of being truncated. */
+#ifdef LARGE_GENOMES
+#error "gmapdp shim: LARGE_GENOMES (gmapl, 64-bit Univcoord_T) is not supported by this engine build"
+#endif
+static uint32_t
+shim_coord (Univcoord_T x) {
+  if ((uint64_t) x > 0xFFFFFFFFu) shim_refuse("a genome coordinate at or above 2^32 (gmapl genomes)");
+  return (uint32_t) x;
 }
 
 static void
@@ -142,12 +175,15 @@ shim_context (Genome_T genome, Genome_T genomealt, Dynprog_T dynprog) {
   if (dynprog != NULL && (dynprog->max_rlength != GMAPDP_MAX_RLENGTH || dynprog->max_glength != GMAPDP_MAX_GLENGTH))
     shim_refuse("a Dynprog_T with non-default maximum lengths");
   if (shim_ctx == NULL) {
+    dev = getenv("GMAPDP_SHIM_STATS");
+    if (dev != NULL && dev[0] == '1') atexit(shim_print_stats);
     dev = getenv("GMAPDP_DEVICE");
     shim_check(gmapdp_create(&shim_ctx, dev ? atoi(dev) : 0, shim_mode, shim_user_open, shim_user_extend,
                              shim_user_dynprog_p), "gmapdp_create");
   }
   if (genome != shim_genome) {
     length = (uint64_t) Genome_genomelength(genome);
+    if (length > 0xFFFFFFFFull) shim_refuse("a genome of 2^32 nt or more (gmapl genomes)");
     nwords = gmapdp_genome_words(length);
     shim_check(gmapdp_set_genome(shim_ctx, (const uint32_t *) Genome_blocks(genome), nwords, length),
                "gmapdp_set_genome");
@@ -204,8 +240,8 @@ __wrap_Dynprog_single_gap (int *dynprogindex, int *finalscore, int *nmatches, in
   p.glength = length2;
   p.roffset = offset1;
   p.goffset = offset2;
-  p.chroffset = (uint32_t) chroffset;
-  p.chrhigh = (uint32_t) chrhigh;
+  p.chroffset = shim_coord(chroffset);
+  p.chrhigh = shim_coord(chrhigh);
   p.flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0) | (widebandp ? GMAPDP_WIDEBAND : 0) |
             SHIM_SIMD;
   p.genestrand = genestrand;
@@ -216,6 +252,7 @@ __wrap_Dynprog_single_gap (int *dynprogindex, int *finalscore, int *nmatches, in
   pairs = (gmapdp_pair *) malloc((cap ? cap : 1) * sizeof(gmapdp_pair));
   shim_check(gmapdp_single_gap_batch(shim_ctx, &p, 1, sequence1, sequenceuc1, length1 > 0 ? (size_t) length1 : 0,
                                      &res, pairs, cap), "gmapdp_single_gap_batch");
+  shim_count(ST_SINGLE);
   pthread_mutex_unlock(&shim_lock);
   list = shim_list(pairs + res.pair_offset, res.npairs, p.dynprogindex, -1, 0, 0, 0.0, 0.0, pairpool);
   free(pairs);
@@ -247,8 +284,8 @@ shim_end_gap (int end3p, int *dynprogindex, int *finalscore, int *nmatches, int 
   p.glength = length2;
   p.roffset = offset1;
   p.goffset = offset2;
-  p.chroffset = (uint32_t) chroffset;
-  p.chrhigh = (uint32_t) chrhigh;
+  p.chroffset = shim_coord(chroffset);
+  p.chrhigh = shim_coord(chrhigh);
   p.flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0) | SHIM_SIMD;
   p.genestrand = genestrand;
   p.extraband = extraband_end;
@@ -264,6 +301,7 @@ shim_end_gap (int end3p, int *dynprogindex, int *finalscore, int *nmatches, int 
   pairs = (gmapdp_pair *) malloc((cap ? cap : 1) * sizeof(gmapdp_pair));
   shim_check(gmapdp_end_gap_batch(shim_ctx, &p, 1, q, quc, length1 > 0 ? (size_t) length1 : 0, &res, pairs, cap),
              "gmapdp_end_gap_batch");
+  shim_count(end3p ? ST_END3 : ST_END5);
   pthread_mutex_unlock(&shim_lock);
   list = shim_list(pairs + res.pair_offset, res.npairs, p.dynprogindex, -1, 0, 0, 0.0, 0.0, pairpool);
   free(pairs);
@@ -342,8 +380,8 @@ __wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_r
   p.roffset = roffset;
   p.goffsetL = goffsetL;
   p.rev_goffsetR = rev_goffsetR;
-  p.chroffset = (uint32_t) chroffset;
-  p.chrhigh = (uint32_t) chrhigh;
+  p.chroffset = shim_coord(chroffset);
+  p.chrhigh = shim_coord(chrhigh);
   p.flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0) | (halfp ? GMAPDP_HALFP : 0) |
             (finalp ? GMAPDP_FINALP : 0) | SHIM_SIMD;
   p.cdna_direction = cdna_direction;
@@ -375,6 +413,7 @@ __wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_r
   pairs = (gmapdp_pair *) malloc((cap ? cap : 1) * sizeof(gmapdp_pair));
   shim_check(gmapdp_genome_gap_batch(shim_ctx, &p, 1, rsequence, rsequenceuc, rlength > 0 ? (size_t) rlength : 0,
                                      probs, m, &res, pairs, cap), "gmapdp_genome_gap_batch");
+  shim_count(ST_GENOME);
   pthread_mutex_unlock(&shim_lock);
   list = shim_list(pairs + res.pair_offset, res.npairs, p.dynprogindex, res.gap_index, res.gap_queryjump,
                    res.introntype, res.left_prob, res.right_prob, pairpool);
@@ -431,8 +470,8 @@ __wrap_Dynprog_cdna_gap (int *dynprogindex, int *traceback_score, bool *incomple
   p.roffsetL = roffsetL;
   p.rev_roffsetR = rev_roffsetR;
   p.goffset = goffset;
-  p.chroffset = (uint32_t) chroffset;
-  p.chrhigh = (uint32_t) chrhigh;
+  p.chroffset = shim_coord(chroffset);
+  p.chrhigh = shim_coord(chrhigh);
   p.flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0) | SHIM_SIMD;
   p.genestrand = genestrand;
   p.extraband = extraband_paired;
@@ -442,6 +481,7 @@ __wrap_Dynprog_cdna_gap (int *dynprogindex, int *traceback_score, bool *incomple
   pairs = (gmapdp_pair *) malloc((cap ? cap : 1) * sizeof(gmapdp_pair));
   shim_check(gmapdp_cdna_gap_batch(shim_ctx, &p, 1, lo, lo_uc, (size_t) (hi - lo), &res, pairs, cap),
              "gmapdp_cdna_gap_batch");
+  shim_count(ST_CDNA);
   pthread_mutex_unlock(&shim_lock);
   list = shim_list(pairs + res.pair_offset, res.npairs, p.dynprogindex, res.gap_index, res.gap_queryjump, -1, 0.0,
                    0.0, pairpool);
@@ -456,7 +496,9 @@ __wrap_Dynprog_cdna_gap (int *dynprogindex, int *traceback_score, bool *incomple
    Stage2_compute (stage2.c:6480-6495) calls the tally and then get_mappings for the same window; the
    tally only records its arguments here and the GPU runs both in get_mappings.  The table is allocated
    with GMAP's own MALLOC as this->table, so Oligoindex_untally frees it as usual. */
-static struct {
+/* Thread-local: each GMAP worker runs Stage2_compute on its own oligoindices (gmap.c:4896), so the
+   tally record of one thread must not be seen by another's get_mappings. */
+static __thread struct {
   Oligoindex_T oligoindex;
   Univcoord_T mappingstart, mappingend;
   Chrpos_T chrpos;
@@ -511,8 +553,8 @@ __wrap_Oligoindex_get_mappings (List_T diagonals, bool *coveredp, Chrpos_T **map
   p.querylength = querylength;
   p.chrstart = chrstart;
   p.chrend = chrend;
-  p.chroffset = (uint32_t) chroffset;
-  p.chrhigh = (uint32_t) chrhigh;
+  p.chroffset = shim_coord(chroffset);
+  p.chrhigh = shim_coord(chrhigh);
   p.plusp = plusp ? 1 : 0;
   p.minor = this->diag_lookback == 60 ? 1 : 0;  /* Oligoindex_array_new_minor's index (oligoindex_hr.c:8612) */
   pthread_mutex_lock(&shim_lock);
@@ -525,6 +567,7 @@ __wrap_Oligoindex_get_mappings (List_T diagonals, bool *coveredp, Chrpos_T **map
   dg = (int32_t *) malloc(4 * (dc ? dc : 1) * sizeof(int32_t));
   shim_check(gmapdp_oligo_mappings_batch(shim_ctx, &p, 1, queryuc_ptr, (size_t) querylength, &res, np, mp, pos, pc,
                                          dg, dc), "gmapdp_oligo_mappings_batch");
+  shim_count(ST_OLIGO);
   pthread_mutex_unlock(&shim_lock);
   /* the table, owned by the oligoindex (freed by Oligoindex_untally) */
   this->table = NULL;

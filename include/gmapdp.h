@@ -38,8 +38,11 @@
  * convention in traceback_score (NEG_INFINITY_32 = -32768 for the size
  * guard).
  *
- * Threading: a gmapdp_ctx is owned by one host thread at a time; create one
- * per worker (mirrors GMAP's per-thread Dynprog_T, gmap.c:4898-4903).
+ * Threading: a gmapdp_ctx and its plans are NOT thread-safe.  A context (its
+ * scratch buffers, fork/join events and side streams) and every plan created on
+ * it must be used by one host thread at a time, and a plan must not run on two
+ * streams at once (its pool counter and the context scratch are shared).  Use
+ * one context per thread, or serialise (the GMAP shim does the latter).
  */
 #ifndef GMAPDP_H
 #define GMAPDP_H
@@ -363,7 +366,8 @@ size_t gmapdp_genome_words (uint64_t length);
  * gmapdp_genome_words(length) words. */
 int gmapdp_pack_genome (const char *seq, uint64_t length, uint32_t *blocks);
 /* Upload packed blocks (e.g. Genome_blocks(genome) of a loaded GMAP
- * genome) to HBM.  nwords as returned by gmapdp_genome_words. */
+ * genome) to HBM.  nwords as returned by gmapdp_genome_words.  Genomes of
+ * 2^32 nt or more (gmapl, 64-bit Univcoord_T) are GMAPDP_EINVAL. */
 int gmapdp_set_genome (gmapdp_ctx *ctx, const uint32_t *blocks, size_t nwords, uint64_t length);
 
 /* Run n Dynprog_single_gap problems.  Host arrays in, host arrays out

@@ -12,18 +12,23 @@
 # it sets HAVE_BZLIB (no <bzlib.h> here) and PAGESIZE_VIA_SYSCTL (macOS-only
 # <sys/sysctl.h>).  bzip2.c and getline.c use config.h only for HAVE_BZLIB, so
 # they are compiled without -DHAVE_CONFIG_H (their own no-bzip2 configuration).
-# access.c does not compile here in either configuration, so the full `gmap`
-# program is UNBUILDABLE in this image without a regenerated config.h
-# (generated code we do not write).  The Dynprog_* path does not need
-# access.c: the harness library links every other GMAP object with
-# --gc-sections and exports only refh_*, so the unreachable callers of
-# Access_* drop out (tests check the .so has no unresolved GMAP symbols).
+# access.c uses config.h for PAGESIZE_VIA_SYSCTL (<sys/sysctl.h>, macOS-only)
+# and mmap/shm feature switches, so it is compiled WITHOUT config.h, with the
+# Linux values of the switches it reads given as -D flags (ACCESS_DEFS below;
+# the same values `./configure` reports on this image, config.log).  The
+# harness library does not need access.c (it links with --gc-sections and
+# exports only refh_*); the full `gmap` programs below do.
 #
 # Products (per variant V in {nosimd, avx2}):
 #   _ref/V/*.o                 reference objects
 #   _ref/librefdp_V.so         reference objects + refharness.c: a flat C API
 #                              over the reference's own Dynprog_* entry points,
 #                              used only by tests/ and the golden generator.
+#   _ref/gmap_V                the reference `gmap` program itself (all of
+#                              GMAP_FILES, unmodified): the end-to-end oracle
+#   _ref/gmap_gpu_V            the same objects linked with the drop-in shim
+#                              (`ld --wrap`) and libgmapdp.so:
+#                              GMAP's own per-read pipeline on the MI355X engine
 
 REF      ?= /root/reference
 SRC      := $(REF)/src
@@ -45,8 +50,15 @@ GMAP_C := except.c assert.c mem.c intlist.c uintlist.c list.c littleendian.c big
   changepoint.c stage3.c request.c result.c output.c inbuffer.c samheader.c printbuffer.c \
   outbuffer.c chimera.c datadir.c parserange.c getline.c getopt.c getopt1.c gmap.c
 
-# Not buildable with the shipped (macOS) config.h, and not on the Dynprog_* path.
+# Not buildable with the shipped (macOS) config.h: compiled with ACCESS_DEFS instead.
 UNBUILDABLE_C := access.c
+ACCESS_DEFS := -DHAVE_UNISTD_H=1 -DHAVE_SYS_TYPES_H=1 -DHAVE_STDDEF_H=1 -DHAVE_SYS_STAT_H=1 -DHAVE_FCNTL_H=1 \
+  -DHAVE_STDINT_H=1 -DHAVE_INTTYPES_H=1 -DHAVE_INLINE=1 -DHAVE_PTHREAD=1 -DPAGESIZE_VIA_SYSCONF=1 -DHAVE_SYSCONF=1 \
+  -DHAVE_MMAP=1 -DHAVE_MUNMAP=1 -DHAVE_MMAP_MAP_PRIVATE=1 -DHAVE_MMAP_MAP_FILE=1 -DHAVE_MMAP_MAP_SHARED=1 \
+  -DHAVE_CADDR_T=1 -DHAVE_MADVISE=1 -DHAVE_MADVISE_MADV_RANDOM=1 -DHAVE_MADVISE_MADV_DONTNEED=1 \
+  -DHAVE_MADVISE_MADV_WILLNEED=1 -DHAVE_MADVISE_MADV_SEQUENTIAL=1 -DHAVE_SHMAT=1 -DHAVE_SHMGET=1 -DHAVE_SHMCTL=1 \
+  -DHAVE_SHMDT=1 -DHAVE_SEMCTL=1 -DHAVE_SEMGET=1 -DHAVE_SEMOP=1 -DHAVE_STAT64=1 \
+  -DSIZEOF_UNSIGNED_LONG=8 -DSIZEOF_UNSIGNED_LONG_LONG=8 -DSIZEOF_OFF_T=8
 # Compiled without config.h (their only config switch is HAVE_BZLIB).
 NOCONFIG_C := bzip2.c getline.c
 # Driver (main) and output/threading layers: not linked into the harness.
@@ -83,6 +95,12 @@ $(OUT)/$(1)/refharness.o: refharness.c
 
 $(OUT)/librefdp_$(1).so: $$(LIBOBJS_$(1)) $(OUT)/$(1)/refharness.o
 	$$(CC) -shared -pthread -Wl,--gc-sections -Wl,--version-script=refharness.map -o $$@ $$^ -lz -lm
+
+$(OUT)/$(1)/access.o: $(SRC)/access.c
+	@mkdir -p $$(dir $$@)
+	$$(CC) $(BASEFLAGS) $(ACCESS_DEFS) $$(FLAGS_$(1)) -c $$< -o $$@
+
+PROGOBJS_$(1) := $$(patsubst %.c,$(OUT)/$(1)/%.o,$(GMAP_C))
 endef
 
 $(foreach v,$(VARIANTS),$(eval $(call variant_rules,$(v))))
@@ -90,7 +108,7 @@ $(foreach v,$(VARIANTS),$(eval $(call variant_rules,$(v))))
 SHIM_SRC   := ../gmap-2024_amd/shim/gmapdp_gmap_shim.c
 GMAPDP_LIB := ../gmap-2024_amd/lib
 
-all: $(foreach v,$(VARIANTS),$(OUT)/librefdp_$(v).so) \
+all: programs $(foreach v,$(VARIANTS),$(OUT)/librefdp_$(v).so) \
      $(if $(wildcard $(GMAPDP_LIB)/libgmapdp.so),$(OUT)/librefdp_gpushim.so $(OUT)/librefdp_gpushim_avx2.so)
 
 # The drop-in check: the same nosimd reference objects, with Dynprog_init / _*_setup /
@@ -123,4 +141,23 @@ $(OUT)/librefdp_gpushim_avx2.so: $(LIBOBJS_avx2a) $(OUT)/avx2a/refharness.o $(OU
 	  $(foreach w,$(WRAPPED),-Wl,--wrap=$(w)) -o $@ $(filter %.o,$^) \
 	  -L$(GMAPDP_LIB) -lgmapdp -Wl,-rpath,'$$ORIGIN/../../gmap-2024_amd/lib' -lz -lm
 
-.PHONY: all
+# ---- the full gmap program (end-to-end oracle) and the same program on the MI355X engine ----
+PROG_VARIANTS := nosimd avx2
+define prog_rules
+$(OUT)/gmap_$(1): $$(PROGOBJS_$(1))
+	$$(CC) -pthread -s -o $$@ $$^ -lz -lm
+
+$(OUT)/gmap_gpu_$(1): $$(PROGOBJS_$(1)) $(OUT)/gpushim_$(1)/gmapdp_gmap_shim.o $(GMAPDP_LIB)/libgmapdp.so
+	$$(CC) -pthread -s $(foreach w,$(WRAPPED),-Wl,--wrap=$(w)) -o $$@ $$(filter %.o,$$^) \
+	  -L$(GMAPDP_LIB) -lgmapdp -Wl,-rpath,'$$$$ORIGIN/../../gmap-2024_amd/lib' -lz -lm
+
+$(OUT)/gpushim_$(1)/gmapdp_gmap_shim.o: $(SHIM_SRC) ../include/gmapdp.h
+	@mkdir -p $$(dir $$@)
+	$$(CC) $(BASEFLAGS) -DHAVE_CONFIG_H $$(FLAGS_$(1)) -I../include -c $$< -o $$@
+endef
+$(foreach v,$(PROG_VARIANTS),$(eval $(call prog_rules,$(v))))
+
+programs: $(foreach v,$(PROG_VARIANTS),$(OUT)/gmap_$(v)) \
+          $(if $(wildcard $(GMAPDP_LIB)/libgmapdp.so),$(foreach v,$(PROG_VARIANTS),$(OUT)/gmap_gpu_$(v)))
+
+.PHONY: all programs

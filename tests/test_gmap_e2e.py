@@ -1,0 +1,123 @@
+"""End-to-end: GMAP's own per-read pipeline (gmap.c process_request:4486 -> stage 2 -> stage 3 -> every
+Dynprog_* call) through the drop-in shim on the MI355X engine, compared byte-for-byte with the
+reference program's outputs.
+
+Binaries (oracle/ref.mk, built from /root/reference/src where it lies; they travel to the GPU box):
+  oracle/_ref/gmap_{nosimd,avx2}      the unmodified reference `gmap` (the end-to-end oracle)
+  oracle/_ref/gmap_gpu_{nosimd,avx2}  the same objects linked with gmap-2024_amd/shim via ld --wrap and
+                                      libgmapdp.so
+
+Fixtures (tests/golden/, data only):
+  align.test.ok       the reference's own golden (tests/align.test.in:9: gmap -A -g ss.chr17test ss.her2)
+  cdna2_genetest2_*   `gmap -g genetest2.fa cdna2.fa` (BASELINE configs[0] inputs), both builds
+  e2e_{nosimd,avx2}.sam  200 synthetic 2-kb spliced reads vs a 300-kb segment (make_e2e.py), both builds
+"""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = os.path.join(ROOT, "oracle", "_ref")
+GOLD = os.path.join(ROOT, "tests", "golden")
+BUILDS = ("nosimd", "avx2")
+
+
+def _exe(name):
+    path = os.path.join(REF, name)
+    if not os.path.exists(path):
+        pytest.skip("%s not built (make -C oracle ref)" % name)
+    return path
+
+
+def _run(exe, args, env=None, timeout=300):
+    e = dict(os.environ)
+    if env:
+        e.update(env)
+    r = subprocess.run([exe] + args, cwd=GOLD, env=e, capture_output=True, timeout=timeout)
+    assert r.returncode == 0, "%s %s failed (%d): %s" % (exe, args, r.returncode, r.stderr.decode()[-2000:])
+    return r.stdout.decode(), r.stderr.decode()
+
+
+def _read(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return f.read()
+
+
+ALIGN_ARGS = ["-A", "-g", "ss.chr17test.fa", "ss.her2.fa"]
+CDNA2_ARGS = ["-g", "genetest2.fa", "cdna2.fa"]
+E2E_ARGS = ["-g", "e2e_genome.fa", "-f", "samse", "--no-sam-headers", "e2e_reads.fa"]
+
+
+def _stats(stderr):
+    m = re.search(r"gmapdp shim calls:(.*)", stderr)
+    assert m, "shim statistics missing (GMAPDP_SHIM_STATS): " + stderr[-500:]
+    return {k: int(v) for k, v in re.findall(r"(\w+)=(\d+)", m.group(1))}
+
+
+# ---- the oracle itself: the reference program reproduces the reference's golden and our fixtures ----
+
+@pytest.mark.parametrize("build", BUILDS)
+def test_reference_gmap_reproduces_align_golden(build):
+    out, _ = _run(_exe("gmap_" + build), ALIGN_ARGS)
+    assert out == _read("align.test.ok")
+
+
+@pytest.mark.parametrize("build", BUILDS)
+def test_reference_gmap_reproduces_fixtures(build):
+    exe = _exe("gmap_" + build)
+    assert _run(exe, CDNA2_ARGS)[0] == _read("cdna2_genetest2_%s.txt" % build)
+    assert _run(exe, E2E_ARGS)[0] == _read("e2e_%s.sam" % build)
+
+
+def test_fixtures_pin_both_semantics():
+    """nosimd and SIMD builds differ on a few reads: both fixtures are needed."""
+    a = _read("e2e_nosimd.sam").splitlines()
+    b = _read("e2e_avx2.sam").splitlines()
+    assert len(a) == len(b) == 200
+    ndiff = sum(1 for x, y in zip(a, b) if x != y)
+    assert 1 <= ndiff <= 20
+
+
+# ---- the drop-in on the GPU ----
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("build", BUILDS)
+def test_gpu_gmap_align_golden(build):
+    """tests/align.test.in:9 through the drop-in: byte-identical to the reference's align.test.ok."""
+    out, err = _run(_exe("gmap_gpu_" + build), ALIGN_ARGS, env={"GMAPDP_SHIM_STATS": "1"})
+    st = _stats(err)
+    assert out == _read("align.test.ok")
+    assert st["Dynprog_single_gap"] > 0 and st["Dynprog_genome_gap"] > 0 and st["Oligoindex_get_mappings"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("build", BUILDS)
+def test_gpu_gmap_cdna2_genetest2(build):
+    out, _ = _run(_exe("gmap_gpu_" + build), CDNA2_ARGS)
+    assert out == _read("cdna2_genetest2_%s.txt" % build)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("build", BUILDS)
+def test_gpu_gmap_synthetic_reads(build):
+    """200 spliced 2-kb reads: every SAM record identical to the reference build's; every DP family and
+    stage-2 seeding ran on the GPU (no GMAPDP_EINVAL domain refusal: the shim aborts on one)."""
+    out, err = _run(_exe("gmap_gpu_" + build), E2E_ARGS, env={"GMAPDP_SHIM_STATS": "1"})
+    st = _stats(err)
+    exp = _read("e2e_%s.sam" % build).splitlines()
+    got = out.splitlines()
+    bad = [i for i, (x, y) in enumerate(zip(got, exp)) if x != y]
+    assert len(got) == len(exp) and not bad, "reads differing: %s" % bad[:10]
+    for k in ("Dynprog_single_gap", "Dynprog_genome_gap", "Dynprog_end5_gap", "Dynprog_end3_gap",
+              "Oligoindex_get_mappings"):
+        assert st[k] > 0, st
+
+
+@pytest.mark.gpu
+def test_gpu_gmap_worker_threads():
+    """-t 4 worker threads sharing the engine (the shim's per-thread stage-2 tally record and the
+    shared context): output identical to the single-threaded reference."""
+    out, _ = _run(_exe("gmap_gpu_nosimd"), ["-t", "4", "-O"] + E2E_ARGS)
+    assert out == _read("e2e_nosimd.sam")

@@ -1,0 +1,85 @@
+"""Phase breakdown of oi_kernel (stage-2 seeding) on bench.py's stage-2 workload.
+
+Loads the GMAPDP_OI_TIMING variant of the library (make -C gmap-2024_amd timing), runs one plan and
+prints, per phase, the wave-summed wall-clock time as a share of the total.  Diagnostic only."""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gmap-2024_amd"))
+sys.path.insert(0, ROOT)
+import gmapdp  # noqa: E402
+import bench  # noqa: E402
+
+PHASES = ["set_inquery (bitmap, ids)", "pass 1 (counts) + layout", "pass 2 (store)", "npositions/mappings/cum",
+          "event pool allocation", "events", "radix sort", "sweep + records"]
+
+
+GG_PHASES = ["stage", "genome_gap_simple", "fills (L and R waves)", "bridge", "traceback R + reverse",
+             "traceback L", "maxnegscore + result"]
+
+
+def main_gg(reads=10000):
+    """gg_kernel phases on bench.py's genome-gap stream (GENOME_PER_READ calls per read)."""
+    import torch
+    lib = gmapdp.load_library(os.path.join(ROOT, "gmap-2024_amd", "lib", "libgmapdp_oitiming.so"))
+    lib.gmapdp_debug_gg_marks.argtypes = [C.c_void_p]
+    genome = bench.make_genome()
+    ng = int(round(reads * bench.GENOME_PER_READ))
+    gp, gq, sprob = bench.make_genome_gaps(genome, ng, np.random.default_rng(2000))
+    eng = gmapdp.Engine(0)
+    eng.set_genome(genome.tobytes())
+    qb = gq.tobytes()
+    eng.genome_gap_batch_raw(gp, qb, qb, sprob)
+    marks = np.zeros(32, dtype=np.uint64)
+    lib.gmapdp_debug_gg_marks(marks.ctypes.data)
+    eng.genome_gap_batch_raw(gp, qb, qb, sprob)
+    torch.cuda.synchronize()
+    lib.gmapdp_debug_gg_marks(marks.ctypes.data)
+    t, c = marks[:16].astype(np.float64), marks[16:]
+    dur = [float(t[k + 1] - t[k]) for k in range(7)]
+    tot = sum(dur)
+    print(json.dumps({"blocks": [int(x) for x in c[:8]], "phases": {n: round(d / tot, 4) for n, d in zip(GG_PHASES, dur)},
+                      "mean_block_us": tot / 1e2 / max(int(c[0]), 1)}))
+    eng.close()
+
+
+def main():
+    import torch
+    if len(sys.argv) > 1 and sys.argv[1] == "gg":
+        return main_gg()
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
+    lib = gmapdp.load_library(os.path.join(ROOT, "gmap-2024_amd", "lib", "libgmapdp_oitiming.so"))
+    lib.gmapdp_debug_oi_marks.argtypes = [C.c_void_p]
+    genome = bench.make_genome()
+    eng = gmapdp.Engine(0)
+    eng.set_genome(genome.tobytes())
+    op, oq = bench.make_stage2(genome, n, np.random.default_rng(3000))
+    qb = oq.tobytes()
+    res = eng.oligo_mappings_batch_raw(op, qb)
+    marks = np.zeros(32, dtype=np.uint64)
+    lib.gmapdp_debug_oi_marks(marks.ctypes.data)  # clear (includes the first run's warm-up)
+    res = eng.oligo_mappings_batch_raw(op, qb)
+    torch.cuda.synchronize()
+    lib.gmapdp_debug_oi_marks(marks.ctypes.data)
+    t, c = marks[:16].astype(np.float64), marks[16:]
+    # oi_kernel: marks 0..4; oi_map_kernel: 8 (start), 9 (pool allocated), 5, 6, 7
+    spans = [(0, 1), (1, 2), (2, 3), (3, 4), (8, 9), (9, 5), (5, 6), (6, 7)]
+    out = {"waves": [int(c[k]) for k in (0, 1, 2, 3, 4, 8, 9, 5, 6, 7)]}
+    dur = [float(t[b] - t[a]) for a, b in spans]
+    tot = sum(dur)
+    out["wave_ms_total"] = tot / 1e5
+    out["phases"] = {name: round(d / tot, 4) for name, d in zip(PHASES, dur)}
+    out["mean_wave_us"] = {"oi_kernel": sum(dur[:4]) / 1e2 / max(int(c[0]), 1),
+                           "oi_map_kernel": sum(dur[4:]) / 1e2 / max(int(c[8]), 1)}
+    print(json.dumps(out))
+    eng.close()
+    del res
+
+
+if __name__ == "__main__":
+    main()
