@@ -89,7 +89,8 @@ def test_gpu_gmap_align_golden(build):
     out, err = _run(_exe("gmap_gpu_" + build), ALIGN_ARGS, env={"GMAPDP_SHIM_STATS": "1"})
     st = _stats(err)
     assert out == _read("align.test.ok")
-    assert st["Dynprog_single_gap"] > 0 and st["Dynprog_genome_gap"] > 0 and st["Oligoindex_get_mappings"] > 0
+    # a 100 %-identity mRNA: introns and ends, no single gaps
+    assert st["Dynprog_genome_gap"] > 0 and st["Oligoindex_get_mappings"] > 0, st
 
 
 @pytest.mark.gpu
