@@ -496,6 +496,14 @@ static int convert_single(const gmapdp_ctx* ctx, const gmapdp_single_problem& p,
     d.flags |= kFSegLeft | kFSegRevcomp;
   }
   gmapdp_compute_bands(&d.lband, &d.uband, p.rlength, p.glength, p.extraband, p.flags & GMAPDP_WIDEBAND);
+  if (!(p.flags & GMAPDP_SIMD)) {
+    // stage3.c:9070-9077 passes extraband_single = |queryjump - genomejump|, so the band can be
+    // ~3x glength wide.  Dynprog_standard only asks whether c - uband < 1 and c + lband > rlength
+    // (dynprog.c:1411-1449), so a band past the matrix edges fills exactly the same cells as one
+    // clamped to them: uband >= glength keeps every rlo at 1, lband >= rlength every rhigh at rlength.
+    d.uband = std::min(d.uband, p.glength);
+    d.lband = std::min(d.lband, p.rlength);
+  }
   d.genestrand = p.genestrand;
   d.dynprogindex = p.dynprogindex;
   d.endalign = 0;

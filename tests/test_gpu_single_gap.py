@@ -112,3 +112,41 @@ def test_gpu_deterministic_and_self_consistent_at_scale(engine):
     orc.set_genome(g)
     for i in rng.sample(range(len(probs)), 1500):
         assert a[i] == call_single(orc, probs[i]), i
+
+
+def _stage3_band_problem(rng, g):
+    """stage3.c:9070-9077: Dynprog_single_gap with extraband_single = |queryjump - genomejump|
+    (widebandp), so the band runs to ~3 x glength -- wider than the matrix (seen on real reads:
+    a 1,400-nt genome jump over a short query gap)."""
+    p = edge_single_gap_problem(rng, g)
+    glength = rng.choice([rng.randint(900, 2000), rng.randint(40, 900)])
+    rlength = rng.choice([rng.randint(1, 60), rng.randint(1, 660)])
+    goffset = rng.randint(1, len(g) - glength - 1)
+    seg = g[goffset:goffset + glength]
+    a = rng.randint(0, max(0, glength - rlength))
+    q = bytes(seg[a:a + rlength]) if rng.random() < 0.7 else bytes(rng.choice(b"ACGT") for _ in range(rlength))
+    q = (q + b"A" * rlength)[:rlength]
+    if rng.random() < 0.3:  # swap: query gap longer than the genome gap
+        glength, q = max(1, rlength // 3), q
+    p.update(q=q, quc=q, rlength=len(q), glength=glength, goffset=goffset, watsonp=1, widebandp=1,
+             extraband=max(3, abs(len(q) - glength)))
+    return p
+
+
+def test_gpu_stage3_band_wider_than_matrix(engine):
+    """Bands far past the matrix edges (found by the end-to-end run: band > 4096 cells) give the
+    same cells as the clamped band: engine vs oracle, and vs the reference objects when present."""
+    rng = random.Random(4242)
+    g = random_genome(rng, 60000)
+    engine.set_genome(g)
+    probs = [_stage3_band_problem(rng, g) for _ in range(600)]
+    assert max(abs(p["rlength"] - p["glength"]) * 3 + 1 for p in probs) > 4096
+    got = engine.single_gap_batch(probs)
+    orc = Oracle()
+    orc.set_genome(g)
+    d = _first_diff(got, [call_single(orc, p) for p in probs])
+    assert d is None, "problem %d: gpu %s vs oracle %s" % d
+    if ref_available("nosimd"):
+        ref = Ref("nosimd")
+        ref.set_genome(g)
+        assert _first_diff(got, [call_single(ref, p) for p in probs[:200]]) is None
