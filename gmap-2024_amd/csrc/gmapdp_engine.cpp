@@ -344,27 +344,33 @@ int gmapdp_pack_genome(const char* seq, uint64_t length, uint32_t* blocks) {
   const size_t nw = gmapdp_genome_words(length);
   std::memset(blocks, 0, nw * sizeof(uint32_t));
   for (int i = 0; i < 4; i++) blocks[3 * nblocks + i] = 0xFFFFFFFFu;
+  // per byte: code in bits 0-1, flag in bit 2
+  uint8_t lut[256];
+  for (int c = 0; c < 256; c++) lut[c] = 4;                  // 'N' and anything else: A code + flag
+  lut['A'] = lut['a'] = 0;
+  lut['C'] = lut['c'] = 1;
+  lut['G'] = lut['g'] = 2;
+  lut['T'] = lut['t'] = 3;
+  lut['X'] = lut['x'] = 3 | 4;                               // put_compressed_one: 'X' = T code + flag
+  const unsigned char* s = (const unsigned char*)seq;
   for (uint64_t b = 0; b < nblocks; b++) {
     uint32_t high = 0, low = 0, flags = 0;
     const uint64_t base = b * 32;
     const int n = (int)std::min<uint64_t>(32, length - base);
-    for (int j = 0; j < 32; j++) {
-      uint32_t code;
-      if (j >= n) {  // tail of the last block reads as 'X'
-        code = 3;
-        flags |= 1u << j;
-      } else {
-        switch (seq[base + j]) {
-          case 'A': case 'a': code = 0; break;
-          case 'C': case 'c': code = 1; break;
-          case 'G': case 'g': code = 2; break;
-          case 'T': case 't': code = 3; break;
-          case 'X': case 'x': code = 3; flags |= 1u << j; break;  // put_compressed_one: 'X' = T code + flag
-          default: code = 0; flags |= 1u << j; break;            // 'N' and anything else: A code + flag
-        }
+    if (n == 32) {
+      for (int j = 0; j < 16; j++) {
+        const uint32_t v = lut[s[base + j]], w = lut[s[base + 16 + j]];
+        low |= (v & 3u) << (2 * j);
+        high |= (w & 3u) << (2 * j);
+        flags |= ((v >> 2) << j) | ((w >> 2) << (j + 16));
       }
-      if (j < 16) low |= code << (2 * j);
-      else high |= code << (2 * (j - 16));
+    } else {
+      for (int j = 0; j < 32; j++) {
+        const uint32_t v = j < n ? lut[s[base + j]] : (3 | 4);  // tail of the last block reads as 'X'
+        if (j < 16) low |= (v & 3u) << (2 * j);
+        else high |= (v & 3u) << (2 * (j - 16));
+        flags |= (v >> 2) << j;
+      }
     }
     blocks[3 * b] = high;
     blocks[3 * b + 1] = low;

@@ -1,0 +1,123 @@
+"""CPU baseline leg of bench.py (TEST/MEASUREMENT INFRASTRUCTURE: it loads the reference's own objects
+from oracle/_ref, never the product library).
+
+Times the reference GMAP 2024-02-22 path -- Oligoindex_hr_tally + Oligoindex_get_mappings (one
+Stage2_compute seeding call) and Dynprog_single_gap / _end5_gap / _end3_gap / _genome_gap -- on the
+host cores, one process per core, each on a bounded sample of the configs[2] per-read call stream
+(gmapdp.workload, same generators and per-read mix as the GPU bench).  The reference's harness takes
+an int genome length, so the CPU sample is cut from a chr22-length (50.8 Mnt) i.i.d. genome; the DP and
+seeding costs depend on the sub-problem shapes, not on the genome size.  The reference computes its own
+MaxEnt splice probabilities inside Dynprog_genome_gap (the GPU bench takes them as an input).
+
+Run as a child process of bench.py (never forked from a process that has touched the GPU):
+  python tools/cpu_baseline.py --build avx2 --cores 16 --budget 10
+prints one JSON object.
+"""
+import argparse
+import ctypes as C
+import json
+import multiprocessing as mp
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gmap-2024_amd"))
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def worker(args):
+    wid, build, budget, reads = args
+    from gmapdp import workload as W
+    layout = W.Layout(W.CHR22)
+    genome = W.make_genome(layout, seed=22)
+    d = W.make_reads(genome, layout, reads, seed=7000 + 17 * wid)
+    lib = C.CDLL(os.path.join(ROOT, "oracle", "_ref", "librefdp_%s.so" % build))
+    lib.refh_init(0, 0, 0)
+    lib.refh_set_genome(genome.tobytes(), len(genome))
+    for name in ("refh_single_gap_batch", "refh_end_gap_batch", "refh_genome_gap_batch"):
+        f = getattr(lib, name)
+        f.restype = C.c_long
+        f.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_char_p]
+    fo = lib.refh_oligo_mappings
+    fo.restype = C.c_int
+    fo.argtypes = [C.c_char_p, C.c_int, C.c_uint, C.c_uint, C.c_uint, C.c_uint, C.c_int, C.c_int, C.c_void_p,
+                   C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int]
+    qb = d["q"].tobytes()
+    oq = d["oq"].tobytes()
+    cap = 1 << 21
+    pos = np.zeros(cap, dtype=np.uint32)
+    npos = np.zeros(int(d["oligo"]["querylength"].max()) + 1, dtype=np.int32)
+    sc = np.zeros(4, dtype=np.int32)
+    dg = np.zeros(4 * 65536, dtype=np.int32)
+    fams = [("single", lib.refh_single_gap_batch, d["single"], W.SINGLE_PER_READ),
+            ("end", lib.refh_end_gap_batch, d["end"], W.END5_PER_READ + W.END3_PER_READ),
+            ("genome", lib.refh_genome_gap_batch, d["genome"], W.GENOME_PER_READ)]
+    t = {k: 0.0 for k in ("single", "end", "genome", "oligo")}
+    n = {k: 0 for k in t}
+    t_start = time.perf_counter()
+    # one read's worth of calls per round, so every family is sampled in proportion
+    while time.perf_counter() - t_start < budget:
+        for name, f, arr, per in fams:
+            k = max(1, int(round(per)))
+            i = n[name] % max(1, len(arr) - k)
+            a = np.ascontiguousarray(arr[i:i + k])
+            t0 = time.perf_counter()
+            f(a.ctypes.data, k, qb, qb)
+            t[name] += time.perf_counter() - t0
+            n[name] += k
+        p = d["oligo"][n["oligo"] % len(d["oligo"])]
+        o, ql = int(p["qoff"]), int(p["querylength"])
+        t0 = time.perf_counter()
+        fo(oq[o:o + ql], ql, int(p["chrstart"]), int(p["chrend"]), int(p["chroffset"]), int(p["chrhigh"]),
+           int(p["plusp"]), 0, npos.ctypes.data, pos.ctypes.data, cap, sc.ctypes.data, dg.ctypes.data, 65536)
+        t["oligo"] += time.perf_counter() - t0
+        n["oligo"] += 1
+    per_call = {k: t[k] / max(n[k], 1) for k in t}
+    sec_per_read = (W.SINGLE_PER_READ * per_call["single"] + (W.END5_PER_READ + W.END3_PER_READ) * per_call["end"]
+                    + W.GENOME_PER_READ * per_call["genome"] + W.STAGE2_PER_READ * per_call["oligo"])
+    return {"reads_per_s": 1.0 / sec_per_read, "calls": n, "seconds": t, "per_call_us":
+            {k: v * 1e6 for k, v in per_call.items()}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", default="avx2", choices=["avx2", "nosimd"])
+    ap.add_argument("--cores", type=int, default=0, help="worker processes (0: the CPUs this process may use, <= 16)")
+    ap.add_argument("--budget", type=float, default=10.0, help="seconds of timed calls per worker")
+    ap.add_argument("--reads", type=int, default=200, help="reads generated per worker (the sample is cycled)")
+    a = ap.parse_args()
+    so = os.path.join(ROOT, "oracle", "_ref", "librefdp_%s.so" % a.build)
+    if not os.path.exists(so):
+        print(json.dumps(None))
+        return
+    cores = a.cores or min(16, len(os.sched_getaffinity(0)))
+    with mp.get_context("fork").Pool(cores) as pool:
+        res = pool.map(worker, [(w, a.build, a.budget, a.reads) for w in range(cores)])
+    total = sum(r["reads_per_s"] for r in res)
+    calls = {k: sum(r["calls"][k] for r in res) for k in res[0]["calls"]}
+    per_call = {k: float(np.mean([r["per_call_us"][k] for r in res])) for k in res[0]["per_call_us"]}
+    print(json.dumps({
+        "value": total, "unit": "reads/s", "cores": cores, "kind": "reference",
+        "build": "gmap.%s objects (oracle/_ref/librefdp_%s.so)" % (a.build, a.build),
+        "cpu_model": cpu_model(), "per_core_reads_per_s": total / cores, "per_call_us": per_call,
+        "sample": "%d worker processes x %.0f s of timed reference calls (%s) on the configs[2] per-read mix "
+                  "(1 seeding call + %.1f single + %.1f end + %.1f genome-gap calls per read) cut from a chr22-length "
+                  "i.i.d. genome; per-read time composed from per-call averages"
+                  % (cores, a.budget, ", ".join("%d %s" % (v, k) for k, v in calls.items()), 43.7, 13.6, 49.4)}))
+
+
+if __name__ == "__main__":
+    main()
