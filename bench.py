@@ -100,8 +100,11 @@ def pmc_traffic(key):
     return None, None
 
 
-def rocprof_name(kind, R, dl):
-    """The rocprofv3 kernel name of a DP launch class."""
+def rocprof_name(kind, R, dl, lds=0):
+    """The rocprofv3 kernel name(s) of a DP launch class ('+'-joined when a class is several kernels)."""
+    if kind == 6:  # packed genome gaps: prep + fill<S, R> + tail<S, R> (ggp_kernel.hip), lds = S
+        return ("gmapdp::ggp_prep_kernel+gmapdp::ggp_fill_kernel<%d, %d>+gmapdp::ggp_tail_kernel<%d, %d>"
+                % (lds, R, lds, R))
     if kind == 0:
         return "gmapdp::dp_kernel<%d, %s>" % (R, "true" if dl else "false")
     if kind == 2:  # dpx_kernel<S, GD>: GD = direction words in global scratch
@@ -303,7 +306,7 @@ def main():
     for li in range(nl):
         m = np.zeros(info[li][2], dtype=np.int32)
         lib.gmapdp_plan_launch_members(plan, li, m.ctypes.data)
-        name = rocprof_name(kinds[li], info[li][0], info[li][1])
+        name = rocprof_name(kinds[li], info[li][0], info[li][1], info[li][3])
         if kinds[li] in (0, 2):
             nbytes = algorithmic_bytes(rl[m], gl[m], npairs[m], desc[m])
         else:

@@ -96,3 +96,31 @@ def test_gpu_genome_gap_domain_check(engine):
     engine.set_genome(bytes(g))
     with pytest.raises(gmapdp.GmapdpError):
         engine.genome_gap_batch([p], [([0.0] * p["glengthL"], [0.0] * p["glengthR"])])
+
+
+def test_gpu_genome_gap_every_packed_band_class(engine):
+    """Band widths across every packed class (ggp_kernel.hip: W <= 40, <= 48, <= 64) and past it
+    (gg_kernel), with glength - rlength from 1 to 12: engine vs oracle."""
+    rng = random.Random(4711)
+    g = bytearray(random_genome(rng, 150000))
+    probs = []
+    for i in range(3000):
+        p = genome_gap_problem(rng, g, edge=(i % 7 == 0))
+        if p["rlength"] >= 2:
+            d = rng.choice([1, 2, 4, 8, 12])
+            p["glengthL"] = p["rlength"] + d
+            p["glengthR"] = p["rlength"] + rng.choice([1, 2, 4, 8, 12])
+            p["extraband"] = rng.choice([0, 1, 3, 8, 14, 16, 18, 19, 20, 22, 24, 26, 27, 28, 30, 34])
+        probs.append(p)
+    g = bytes(g)
+    W = [2 * p["extraband"] + max(p["glengthL"], p["glengthR"]) - p["rlength"] + 1 for p in probs if p["rlength"] >= 2]
+    for lo, hi in ((1, 40), (41, 48), (49, 64), (65, 200)):
+        assert sum(lo <= w <= hi for w in W) > 50, (lo, hi)
+    engine.set_genome(g)
+    orc = Oracle()
+    orc.set_genome(g)
+    sp = [_synthetic_probs(rng, p) for p in probs]
+    got = engine.genome_gap_batch(probs, sp)
+    exp = [orc.genome_gap(p, lp, rp) for p, (lp, rp) in zip(probs, sp)]
+    d = _first_diff(got, exp)
+    assert d is None, _msg(probs, d, "oracle")

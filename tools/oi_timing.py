@@ -1,4 +1,4 @@
-"""Phase breakdown of oi_kernel (stage-2 seeding) on bench.py's stage-2 workload.
+"""Phase breakdown of oi_kernel (stage-2 seeding) / gg_kernel (`gg`) on the bench workload (chr22 layout).
 
 Loads the GMAPDP_OI_TIMING variant of the library (make -C gmap-2024_amd timing), runs one plan and
 prints, per phase, the wave-summed wall-clock time as a share of the total.  Diagnostic only."""
@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gmap-2024_amd"))
 sys.path.insert(0, ROOT)
 import gmapdp  # noqa: E402
-import bench  # noqa: E402
+from gmapdp import workload as W  # noqa: E402
 
 PHASES = ["set_inquery (bitmap, ids)", "pass 1 (counts) + layout", "pass 2 (store)", "npositions/mappings/cum",
           "event pool allocation", "events", "radix sort", "sweep + records"]
@@ -28,9 +28,10 @@ def main_gg(reads=10000):
     import torch
     lib = gmapdp.load_library(os.path.join(ROOT, "gmap-2024_amd", "lib", "libgmapdp_oitiming.so"))
     lib.gmapdp_debug_gg_marks.argtypes = [C.c_void_p]
-    genome = bench.make_genome()
-    ng = int(round(reads * bench.GENOME_PER_READ))
-    gp, gq, sprob = bench.make_genome_gaps(genome, ng, np.random.default_rng(2000))
+    layout = W.Layout(W.CHR22)
+    genome = W.make_genome(layout, seed=22)
+    ng = int(round(reads * W.GENOME_PER_READ))
+    gp, gq, sprob = W.make_genome_gaps(genome, layout, ng, np.random.default_rng(2000))
     eng = gmapdp.Engine(0)
     eng.set_genome(genome.tobytes())
     qb = gq.tobytes()
@@ -55,10 +56,11 @@ def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
     lib = gmapdp.load_library(os.path.join(ROOT, "gmap-2024_amd", "lib", "libgmapdp_oitiming.so"))
     lib.gmapdp_debug_oi_marks.argtypes = [C.c_void_p]
-    genome = bench.make_genome()
+    layout = W.Layout(W.CHR22)
+    genome = W.make_genome(layout, seed=22)
     eng = gmapdp.Engine(0)
     eng.set_genome(genome.tobytes())
-    op, oq = bench.make_stage2(genome, n, np.random.default_rng(3000))
+    op, oq = W.make_stage2(genome, layout, n, np.random.default_rng(3000))
     qb = oq.tobytes()
     res = eng.oligo_mappings_batch_raw(op, qb)
     marks = np.zeros(32, dtype=np.uint64)
