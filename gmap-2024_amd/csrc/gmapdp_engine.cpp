@@ -194,6 +194,27 @@ struct DevBuf {
   }
 };
 
+// Pinned host staging (hipHostMalloc): the synchronous batch entry points gather every input into
+// one of these and move it with one asynchronous copy each way.
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max(bytes, (size_t)65536);
+    want = want + want / 4;
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  ~HostBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+};
+
 }  // namespace gmapdp
 
 using namespace gmapdp;
@@ -219,6 +240,8 @@ struct gmapdp_ctx {
   uint64_t genome_words = 0;
   uint64_t genome_length = 0;
   DevBuf probs, order, qseq, qseq_uc, results, pairs, gdirs;
+  DevBuf din, dout;    // run_batch: all inputs / all outputs of one synchronous batch
+  HostBuf hin, hout;   // their pinned host images
   DevBuf gprobs, gorder, sprob, gresults;
   DevBuf cprobs, corder, cresults, cscratch;  // Dynprog_cdna_gap batches
   DevBuf oprobs, oresults, oscratch, onpos, omap, otable, odiag;  // stage-2 seeding batches
@@ -1024,11 +1047,14 @@ static int run_plan(gmapdp_ctx* ctx, const PlanCore& plan, const RunArgs& a, hip
     if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "direction scratch: %s", e);
   }
   // Fork: the side streams wait for everything already queued on `stream`; each launch goes to
-  // its assigned stream; join: `stream` waits for the side streams.
-  hipError_t e = hipEventRecord(ctx->ev_fork, stream);
+  // its assigned stream; join: `stream` waits for the side streams.  A small batch (the drop-in's
+  // dispatcher batches) runs on `stream` alone: a process has few hardware queues (GPU_MAX_HW_QUEUES)
+  // and several dispatcher contexts share them.
+  const bool one_stream = plan.dev.size() + plan.gdev.size() < 2048;
+  hipError_t e = one_stream ? hipSuccess : hipEventRecord(ctx->ev_fork, stream);
   bool used[gmapdp_ctx::kAux] = {false, false, false};
   for (size_t li = 0; li < plan.launches.size() && e == hipSuccess; li++) {
-    const int k = plan.launches[li].stream;
+    const int k = one_stream ? 0 : plan.launches[li].stream;
     hipStream_t s = stream;
     if (k > 0) {
       s = ctx->aux[k - 1];
@@ -1076,53 +1102,62 @@ static int run_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int 
   }
   const int ndev = (int)plan.dev.size(), ngdev = (int)plan.gdev.size();
   if (ndev + ngdev == 0) return GMAPDP_OK;
-  hipError_t e = ctx->probs.ensure(sizeof(DevProblem) * std::max(ndev, 1));
-  if (e == hipSuccess) e = ctx->order.ensure(sizeof(int) * std::max(ndev, 1));
-  if (e == hipSuccess) e = ctx->gprobs.ensure(sizeof(DevGenomeProblem) * std::max(ngdev, 1));
-  if (e == hipSuccess) e = ctx->gorder.ensure(sizeof(int) * std::max(ngdev, 1));
-  if (e == hipSuccess) e = ctx->qseq.ensure(qbytes);
-  if (e == hipSuccess) e = ctx->qseq_uc.ensure(qbytes);
-  if (e == hipSuccess) e = ctx->results.ensure(sizeof(gmapdp_result) * std::max(ndev, 1));
-  if (e == hipSuccess) e = ctx->gresults.ensure(sizeof(gmapdp_genome_result) * std::max(ngdev, 1));
-  if (e == hipSuccess && ngdev) e = ctx->sprob.ensure(sizeof(double) * std::max<size_t>(nsprob, 1));
-  if (e == hipSuccess) e = ctx->pairs.ensure(sizeof(gmapdp_pair) * std::max<size_t>(plan.pair_capacity, 1));
-  if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "device buffers: %s", e);
+  // one pinned image of every input and one of every output: a single copy each way
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_probs = 0;
+  const size_t o_order = o_probs + al(sizeof(DevProblem) * ndev);
+  const size_t o_gprobs = o_order + al(sizeof(int) * ndev);
+  const size_t o_gorder = o_gprobs + al(sizeof(DevGenomeProblem) * ngdev);
+  const size_t o_sprob = o_gorder + al(sizeof(int) * ngdev);
+  const size_t o_q = o_sprob + al(ngdev ? sizeof(double) * nsprob : 0);
+  const size_t o_quc = o_q + al(qbytes);
+  const size_t in_bytes = o_quc + al(qbytes);
+  const size_t r_res = 0;
+  const size_t r_gres = r_res + al(sizeof(gmapdp_result) * ndev);
+  const size_t r_pairs = r_gres + al(sizeof(gmapdp_genome_result) * ngdev);
+  const size_t out_bytes = r_pairs + al(sizeof(gmapdp_pair) * plan.pair_capacity);
+  hipError_t e = ctx->hin.ensure(in_bytes);
+  if (e == hipSuccess) e = ctx->din.ensure(in_bytes);
+  if (e == hipSuccess) e = ctx->hout.ensure(out_bytes);
+  if (e == hipSuccess) e = ctx->dout.ensure(out_bytes);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "batch buffers: %s", e);
+  unsigned char* hin = (unsigned char*)ctx->hin.p;
+  unsigned char* din = (unsigned char*)ctx->din.p;
+  unsigned char* hout = (unsigned char*)ctx->hout.p;
+  unsigned char* dout = (unsigned char*)ctx->dout.p;
+  if (ndev) {
+    std::memcpy(hin + o_probs, plan.dev.data(), sizeof(DevProblem) * ndev);
+    std::memcpy(hin + o_order, plan.order.data(), sizeof(int) * ndev);
+  }
+  if (ngdev) {
+    std::memcpy(hin + o_gprobs, plan.gdev.data(), sizeof(DevGenomeProblem) * ngdev);
+    std::memcpy(hin + o_gorder, plan.gorder.data(), sizeof(int) * ngdev);
+    std::memcpy(hin + o_sprob, sprob, sizeof(double) * nsprob);
+  }
+  std::memcpy(hin + o_q, qseq, qbytes);
+  std::memcpy(hin + o_quc, qseq_uc, qbytes);
   hipStream_t s = ctx->stream;
-  if (ndev) e = hipMemcpyAsync(ctx->probs.p, plan.dev.data(), sizeof(DevProblem) * ndev, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && ndev)
-    e = hipMemcpyAsync(ctx->order.p, plan.order.data(), sizeof(int) * ndev, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && ngdev)
-    e = hipMemcpyAsync(ctx->gprobs.p, plan.gdev.data(), sizeof(DevGenomeProblem) * ngdev, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && ngdev)
-    e = hipMemcpyAsync(ctx->gorder.p, plan.gorder.data(), sizeof(int) * ngdev, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && ngdev)
-    e = hipMemcpyAsync(ctx->sprob.p, sprob, sizeof(double) * nsprob, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(ctx->qseq.p, qseq, qbytes, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(ctx->qseq_uc.p, qseq_uc, qbytes, hipMemcpyHostToDevice, s);
+  e = hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, s);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "upload: %s", e);
   RunArgs a;
-  a.d_probs = (const DevProblem*)ctx->probs.p;
-  a.d_order = (const int*)ctx->order.p;
-  a.d_gprobs = (const DevGenomeProblem*)ctx->gprobs.p;
-  a.d_gorder = (const int*)ctx->gorder.p;
-  a.d_q = (const char*)ctx->qseq.p;
-  a.d_quc = (const char*)ctx->qseq_uc.p;
-  a.d_sprob = (const double*)ctx->sprob.p;
-  a.d_results = (gmapdp_result*)ctx->results.p;
-  a.d_gresults = (gmapdp_genome_result*)ctx->gresults.p;
-  a.d_pairs = (gmapdp_pair*)ctx->pairs.p;
+  a.d_probs = (const DevProblem*)(din + o_probs);
+  a.d_order = (const int*)(din + o_order);
+  a.d_gprobs = (const DevGenomeProblem*)(din + o_gprobs);
+  a.d_gorder = (const int*)(din + o_gorder);
+  a.d_q = (const char*)(din + o_q);
+  a.d_quc = (const char*)(din + o_quc);
+  a.d_sprob = (const double*)(din + o_sprob);
+  a.d_results = (gmapdp_result*)(dout + r_res);
+  a.d_gresults = (gmapdp_genome_result*)(dout + r_gres);
+  a.d_pairs = (gmapdp_pair*)(dout + r_pairs);
   rc = run_plan(ctx, plan, a, s);
   if (rc) return rc;
-  std::vector<gmapdp_result> dres(ndev);
-  std::vector<gmapdp_genome_result> gres(ngdev);
-  if (ndev)
-    e = hipMemcpyAsync(dres.data(), ctx->results.p, sizeof(gmapdp_result) * ndev, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess && ngdev)
-    e = hipMemcpyAsync(gres.data(), ctx->gresults.p, sizeof(gmapdp_genome_result) * ngdev, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess && pairs && plan.pair_capacity)
-    e = hipMemcpyAsync(pairs, ctx->pairs.p, sizeof(gmapdp_pair) * plan.pair_capacity, hipMemcpyDeviceToHost, s);
+  e = hipMemcpyAsync(hout, dout, out_bytes, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "dp execution: %s", e);
+  const gmapdp_result* dres = (const gmapdp_result*)(hout + r_res);
+  const gmapdp_genome_result* gres = (const gmapdp_genome_result*)(hout + r_gres);
+  if (pairs && plan.pair_capacity) std::memcpy(pairs, hout + r_pairs, sizeof(gmapdp_pair) * plan.pair_capacity);
   for (int d = 0; d < ndev; d++) results[plan.dev_problem[d]] = dres[d];
   for (int d = 0; d < ngdev; d++) gresults[plan.gdev_problem[d]] = gres[d];
   return GMAPDP_OK;
@@ -1232,6 +1267,16 @@ int gmapdp_genome_gap_batch(gmapdp_ctx* ctx, const gmapdp_genome_problem* proble
   if (n > 0 && !problems) return GMAPDP_EINVAL;
   return run_batch(ctx, nullptr, 0, nullptr, 0, problems, n, qseq, qseq_uc, qbytes, splice_probs, nprobs, nullptr,
                    results, pairs, pair_capacity);
+}
+
+int gmapdp_dynprog_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int nsingle,
+                         const gmapdp_end_problem* ends, int nend, const gmapdp_genome_problem* genomes, int ngenome,
+                         const char* qseq, const char* qseq_uc, size_t qbytes, const double* splice_probs,
+                         size_t nprobs, gmapdp_result* results, gmapdp_genome_result* genome_results,
+                         gmapdp_pair* pairs, size_t pair_capacity) {
+  if ((nsingle > 0 && !singles) || (nend > 0 && !ends) || (ngenome > 0 && !genomes)) return GMAPDP_EINVAL;
+  return run_batch(ctx, singles, nsingle, ends, nend, genomes, ngenome, qseq, qseq_uc, qbytes, splice_probs, nprobs,
+                   results, genome_results, pairs, pair_capacity);
 }
 
 }  // extern "C"

@@ -162,6 +162,9 @@ def load_library(path=LIB_PATH):
                                               C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
                                               C.c_size_t]),
         "gmapdp_genome_pair_capacity": (C.c_size_t, [C.c_void_p, C.c_int]),
+        "gmapdp_dynprog_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
+                                           C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p,
+                                           C.c_void_p, C.c_void_p, C.c_size_t]),
         "gmapdp_cdna_gap_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t,
                                             C.c_void_p, C.c_void_p, C.c_size_t]),
         "gmapdp_cdna_pair_capacity": (C.c_size_t, [C.c_void_p, C.c_int]),

@@ -26,10 +26,15 @@
  * off; no splicing IIT in Dynprog_genome_gap.  Anything else is refused with
  * a message and abort() -- there is no silent CPU fallback.
  *
- * This file is one call per launch (a correctness drop-in).  Throughput comes
- * from batching many calls per launch (gmapdp_*_batch / gmapdp_plan_*), which
- * needs the caller to issue sub-problems of many reads together
- * (INTEGRATION.md "Batching").
+ * Batching.  GMAP's worker threads (gmap.c:4867) each issue their calls one at a time and wait for
+ * the answer (the API is synchronous).  Here a call becomes a request on a process-wide queue and the
+ * calling thread sleeps on it.  GMAPDP_SHIM_DISPATCHERS (default 4) dispatcher threads each own an
+ * engine context (its own streams and HBM copy of the genome), so that many batches are in flight;
+ * a free dispatcher takes every request queued meanwhile and runs them together: all single / end /
+ * genome gaps in one gmapdp_dynprog_batch, cDNA gaps and stage-2 seeding in their own batches.  The
+ * callers then build their List_T from their own results in their own Pairpool.  With many worker
+ * threads per GPU (gmap -t N, N well above the core count: the workers mostly wait) one launch set
+ * carries many reads' calls.  GMAPDP_SHIM_STATS=1 prints the call counts and the mean batch size.
  */
 #ifdef HAVE_CONFIG_H
 #include "config.h"
@@ -78,9 +83,8 @@ extern void __real_Dynprog_genome_setup (bool novelsplicingp_in, IIT_T splicing_
 #define SHIM_SIMD 0
 #endif
 
-static pthread_mutex_t shim_lock = PTHREAD_MUTEX_INITIALIZER;
-static gmapdp_ctx *shim_ctx = NULL;
-static Genome_T shim_genome = NULL;
+static __thread gmapdp_ctx *shim_ctx = NULL;   /* each dispatcher thread owns one engine context */
+static __thread Genome_T shim_genome = NULL;  /* the genome resident in that context's HBM */
 static int shim_mode = 0, shim_user_open = 0, shim_user_extend = 0, shim_user_dynprog_p = 0;
 static int shim_homopolymerp = 0, shim_splicing_iit = 0;
 
@@ -92,12 +96,24 @@ static const char *const shim_stat_name[ST_N] = {"Dynprog_single_gap", "Dynprog_
                                                  "Oligoindex_get_mappings"};
 static unsigned long shim_stats[ST_N];
 
+static unsigned long shim_batches, shim_batched;
+static double shim_secs[3];  /* dispatcher wall time in the DP, cDNA and stage-2 batches */
+
+#include <time.h>
+static double
+shim_now (void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double) ts.tv_sec + 1e-9 * (double) ts.tv_nsec;
+}
+
 static void
 shim_print_stats (void) {
   int i;
   fprintf(stderr, "gmapdp shim calls:");
   for (i = 0; i < ST_N; i++) fprintf(stderr, " %s=%lu", shim_stat_name[i], __atomic_load_n(&shim_stats[i], __ATOMIC_RELAXED));
-  fprintf(stderr, "\n");
+  fprintf(stderr, " batches=%lu mean_batch=%.2f dp_s=%.3f cdna_s=%.3f stage2_s=%.3f\n", shim_batches,
+          shim_batches ? (double) shim_batched / (double) shim_batches : 0.0, shim_secs[0], shim_secs[1], shim_secs[2]);
 }
 
 static void
@@ -165,18 +181,21 @@ __wrap_Dynprog_genome_setup (bool novelsplicingp_in, IIT_T splicing_iit_in, int 
   shim_splicing_iit = splicing_iit_in != NULL;
 }
 
-/* The engine context (one per process, calls serialised) with `genome` resident in HBM. */
-static gmapdp_ctx *
-shim_context (Genome_T genome, Genome_T genomealt, Dynprog_T dynprog) {
-  const char *dev;
-  uint64_t length;
-  size_t nwords;
+/* Refusals that depend on the caller's Dynprog_T / genomes (checked on the calling thread). */
+static void
+shim_check_call (Genome_T genome, Genome_T genomealt, Dynprog_T dynprog) {
   if (genomealt != NULL && genomealt != genome) shim_refuse("an alternate-allele genome (genomealt)");
   if (dynprog != NULL && (dynprog->max_rlength != GMAPDP_MAX_RLENGTH || dynprog->max_glength != GMAPDP_MAX_GLENGTH))
     shim_refuse("a Dynprog_T with non-default maximum lengths");
+}
+
+/* The engine context with `genome` resident in HBM (dispatcher thread only). */
+static gmapdp_ctx *
+shim_context (Genome_T genome) {
+  const char *dev;
+  uint64_t length;
+  size_t nwords;
   if (shim_ctx == NULL) {
-    dev = getenv("GMAPDP_SHIM_STATS");
-    if (dev != NULL && dev[0] == '1') atexit(shim_print_stats);
     dev = getenv("GMAPDP_DEVICE");
     shim_check(gmapdp_create(&shim_ctx, dev ? atoi(dev) : 0, shim_mode, shim_user_open, shim_user_extend,
                              shim_user_dynprog_p), "gmapdp_create");
@@ -190,6 +209,340 @@ shim_context (Genome_T genome, Genome_T genomealt, Dynprog_T dynprog) {
     shim_genome = genome;
   }
   return shim_ctx;
+}
+
+/* ---- requests and the dispatcher ---- */
+enum { K_SINGLE, K_END, K_GENOME, K_CDNA, K_OLIGO };
+
+typedef struct shim_req {
+  int kind;
+  Genome_T genome;
+  union {
+    gmapdp_single_problem s;
+    gmapdp_end_problem e;
+    gmapdp_genome_problem g;
+    gmapdp_cdna_problem c;
+    gmapdp_oligo_problem o;
+  } p;                          /* qoff / prob_offset relative to q and probs below */
+  const char *q, *quc;          /* the query slice (borrowed: the caller waits) */
+  size_t qlen;
+  const double *probs;          /* genome gaps: the splice probabilities */
+  size_t nprobs;
+  /* outputs, filled by the dispatcher (pair_offset / table_offset / diag_offset rebased to 0) */
+  gmapdp_result r;
+  gmapdp_genome_result gr;
+  gmapdp_cdna_result cr;
+  gmapdp_oligo_result orr;
+  /* per-thread buffers (grown by the caller before submitting) */
+  gmapdp_pair *pairs;
+  size_t pcap;
+  double *pbuf;
+  size_t pbufcap;
+  int32_t *np, *mp, *dg;
+  uint32_t *pos;
+  size_t npcap, mpcap, poscap, dgcap;
+  size_t tabn;                  /* stage-2 seeding: the problem's table capacity */
+  int done;
+  pthread_cond_t cv;
+  struct shim_req *next;
+} shim_req;
+
+static pthread_mutex_t q_lock = PTHREAD_MUTEX_INITIALIZER;
+static pthread_cond_t q_cond = PTHREAD_COND_INITIALIZER;
+static shim_req *q_head = NULL, *q_tail = NULL;
+static int dispatcher_started = 0;
+static __thread shim_req *tl_req = NULL;
+
+static void *
+shim_grow (void *p, size_t *cap, size_t want, size_t elt) {
+  if (want <= *cap && p != NULL) return p;
+  want = want < 64 ? 64 : want;
+  p = realloc(p, want * elt);
+  if (p == NULL) shim_refuse("host memory for a request (out of memory)");
+  *cap = want;
+  return p;
+}
+
+/* the calling thread's request (one outstanding call per thread) */
+static shim_req *
+shim_request (int kind) {
+  shim_req *r = tl_req;
+  if (r == NULL) {
+    r = (shim_req *) calloc(1, sizeof(shim_req));
+    if (r == NULL) shim_refuse("host memory for a request (out of memory)");
+    pthread_cond_init(&r->cv, NULL);
+    tl_req = r;
+  }
+  r->kind = kind;
+  r->q = r->quc = NULL;
+  r->qlen = 0;
+  r->probs = NULL;
+  r->nprobs = 0;
+  memset(&r->p, 0, sizeof(r->p));
+  return r;
+}
+
+static void shim_run (shim_req *batch);
+
+static void *
+shim_dispatch (void *arg) {
+  shim_req *batch, *r, *next;
+  (void) arg;
+  for (;;) {
+    pthread_mutex_lock(&q_lock);
+    while (q_head == NULL) pthread_cond_wait(&q_cond, &q_lock);
+    batch = q_head;
+    q_head = q_tail = NULL;
+    pthread_mutex_unlock(&q_lock);
+    shim_run(batch);
+    pthread_mutex_lock(&q_lock);
+    for (r = batch; r != NULL; r = next) {
+      next = r->next;
+      r->done = 1;
+      pthread_cond_signal(&r->cv);
+    }
+    pthread_mutex_unlock(&q_lock);
+  }
+  return NULL;
+}
+
+/* queue the calling thread's request and sleep until the dispatcher has run it */
+static void
+shim_submit (shim_req *r) {
+  pthread_t th;
+  pthread_attr_t attr;
+  const char *st;
+  int nd, k;
+  pthread_mutex_lock(&q_lock);
+  if (!dispatcher_started) {
+    st = getenv("GMAPDP_SHIM_STATS");
+    if (st != NULL && st[0] == '1') atexit(shim_print_stats);
+    st = getenv("GMAPDP_SHIM_DISPATCHERS");
+    nd = st != NULL ? atoi(st) : 4;
+    if (nd < 1) nd = 1;
+    pthread_attr_init(&attr);
+    pthread_attr_setdetachstate(&attr, PTHREAD_CREATE_DETACHED);
+    for (k = 0; k < nd; k++)
+      if (pthread_create(&th, &attr, shim_dispatch, NULL) != 0) shim_refuse("a dispatcher thread (pthread_create)");
+    pthread_attr_destroy(&attr);
+    dispatcher_started = 1;
+  }
+  r->done = 0;
+  r->next = NULL;
+  if (q_tail != NULL) q_tail->next = r;
+  else q_head = r;
+  q_tail = r;
+  pthread_cond_signal(&q_cond);
+  while (!r->done) pthread_cond_wait(&r->cv, &q_lock);
+  pthread_mutex_unlock(&q_lock);
+}
+
+/* dispatcher-owned staging, grown as needed */
+typedef struct {
+  gmapdp_single_problem *s;
+  gmapdp_end_problem *e;
+  gmapdp_genome_problem *g;
+  gmapdp_cdna_problem *c;
+  gmapdp_oligo_problem *o;
+  shim_req **rs, **re, **rg, **rc, **ro;
+  size_t scap, ecap, gcap, ccap, ocap, rscap, recap, rgcap, rccap, rocap;
+  char *q, *quc;
+  size_t qcap, quccap;
+  double *pr;
+  size_t prcap;
+  gmapdp_result *res;
+  gmapdp_genome_result *gres;
+  gmapdp_cdna_result *cres;
+  gmapdp_oligo_result *ores;
+  size_t rescap, grescap, crescap, orescap;
+  gmapdp_pair *pairs;
+  size_t paircap;
+  int32_t *np, *mp, *dg;
+  uint32_t *pos;
+  size_t npcap, mpcap, poscap, dgcap;
+} shim_staging;
+static __thread shim_staging D;  /* per dispatcher thread */
+
+#define GROW(ptr, cap, want) ((ptr) = shim_grow((ptr), &(cap), (want), sizeof(*(ptr))))
+
+static void
+shim_copy_pairs (shim_req *r, const gmapdp_pair *src, int n) {
+  if (n > 0) memcpy(r->pairs, src, (size_t) n * sizeof(gmapdp_pair));
+}
+
+static void
+shim_run (shim_req *batch) {
+  shim_req *r;
+  size_t ns = 0, ne = 0, ng = 0, nc = 0, no = 0, n = 0, qb = 0, pb = 0, cap, i;
+  double t0, t1, td[3];
+  Genome_T genome = NULL;
+  for (r = batch; r != NULL; r = r->next) {
+    n++;
+    if (genome == NULL) genome = r->genome;
+    else if (r->genome != genome) shim_refuse("two genomes in one process");
+    switch (r->kind) {
+    case K_SINGLE: GROW(D.rs, D.rscap, ns + 1); D.rs[ns++] = r; break;
+    case K_END: GROW(D.re, D.recap, ne + 1); D.re[ne++] = r; break;
+    case K_GENOME: GROW(D.rg, D.rgcap, ng + 1); D.rg[ng++] = r; break;
+    case K_CDNA: GROW(D.rc, D.rccap, nc + 1); D.rc[nc++] = r; break;
+    default: GROW(D.ro, D.rocap, no + 1); D.ro[no++] = r; break;
+    }
+  }
+  shim_context(genome);
+  pthread_mutex_lock(&q_lock);
+  shim_batches++;
+  shim_batched += n;
+  pthread_mutex_unlock(&q_lock);
+
+  /* single, end and genome gaps: one batch over one query arena */
+  t0 = shim_now();
+  if (ns + ne + ng > 0) {
+    qb = 0;
+    pb = 0;
+    GROW(D.s, D.scap, ns + 1);
+    GROW(D.e, D.ecap, ne + 1);
+    GROW(D.g, D.gcap, ng + 1);
+    for (i = 0; i < ns; i++) qb += D.rs[i]->qlen;
+    for (i = 0; i < ne; i++) qb += D.re[i]->qlen;
+    for (i = 0; i < ng; i++) {
+      qb += D.rg[i]->qlen;
+      pb += D.rg[i]->nprobs;
+    }
+    GROW(D.q, D.qcap, qb + 1);
+    GROW(D.quc, D.quccap, qb + 1);
+    GROW(D.pr, D.prcap, pb + 1);
+    qb = 0;
+    pb = 0;
+#define STAGE(R, P)                                            \
+    do {                                                        \
+      (P).qoff = (int32_t) qb;                                  \
+      if ((R)->qlen) {                                          \
+        memcpy(D.q + qb, (R)->q, (R)->qlen);                    \
+        memcpy(D.quc + qb, (R)->quc, (R)->qlen);                \
+      }                                                         \
+      qb += (R)->qlen;                                          \
+    } while (0)
+    for (i = 0; i < ns; i++) {
+      D.s[i] = D.rs[i]->p.s;
+      STAGE(D.rs[i], D.s[i]);
+    }
+    for (i = 0; i < ne; i++) {
+      D.e[i] = D.re[i]->p.e;
+      STAGE(D.re[i], D.e[i]);
+    }
+    for (i = 0; i < ng; i++) {
+      D.g[i] = D.rg[i]->p.g;
+      STAGE(D.rg[i], D.g[i]);
+      D.g[i].prob_offset = (int64_t) pb;
+      if (D.rg[i]->nprobs) memcpy(D.pr + pb, D.rg[i]->probs, D.rg[i]->nprobs * sizeof(double));
+      pb += D.rg[i]->nprobs;
+    }
+#undef STAGE
+    cap = gmapdp_single_pair_capacity(D.s, (int) ns) + gmapdp_end_pair_capacity(D.e, (int) ne) +
+          gmapdp_genome_pair_capacity(D.g, (int) ng);
+    GROW(D.pairs, D.paircap, cap + 1);
+    GROW(D.res, D.rescap, ns + ne + 1);
+    GROW(D.gres, D.grescap, ng + 1);
+    shim_check(gmapdp_dynprog_batch(shim_ctx, D.s, (int) ns, D.e, (int) ne, D.g, (int) ng, D.q, D.quc, qb, D.pr, pb,
+                                    D.res, D.gres, D.pairs, cap), "gmapdp_dynprog_batch");
+    for (i = 0; i < ns; i++) {
+      r = D.rs[i];
+      r->r = D.res[i];
+      shim_copy_pairs(r, D.pairs + r->r.pair_offset, r->r.npairs);
+      r->r.pair_offset = 0;
+    }
+    for (i = 0; i < ne; i++) {
+      r = D.re[i];
+      r->r = D.res[ns + i];
+      shim_copy_pairs(r, D.pairs + r->r.pair_offset, r->r.npairs);
+      r->r.pair_offset = 0;
+    }
+    for (i = 0; i < ng; i++) {
+      r = D.rg[i];
+      r->gr = D.gres[i];
+      shim_copy_pairs(r, D.pairs + r->gr.pair_offset, r->gr.npairs);
+      r->gr.pair_offset = 0;
+    }
+  }
+
+  t1 = shim_now();
+  td[0] = t1 - t0;
+  /* cDNA gaps (rare): their own batch, each problem's arena span copied whole */
+  if (nc > 0) {
+    GROW(D.c, D.ccap, nc + 1);
+    qb = 0;
+    for (i = 0; i < nc; i++) qb += D.rc[i]->qlen;
+    GROW(D.q, D.qcap, qb + 1);
+    GROW(D.quc, D.quccap, qb + 1);
+    qb = 0;
+    for (i = 0; i < nc; i++) {
+      r = D.rc[i];
+      D.c[i] = r->p.c;
+      D.c[i].qoffL += (int32_t) qb;
+      D.c[i].qoffR += (int32_t) qb;
+      memcpy(D.q + qb, r->q, r->qlen);
+      memcpy(D.quc + qb, r->quc, r->qlen);
+      qb += r->qlen;
+    }
+    cap = gmapdp_cdna_pair_capacity(D.c, (int) nc);
+    GROW(D.pairs, D.paircap, cap + 1);
+    GROW(D.cres, D.crescap, nc + 1);
+    shim_check(gmapdp_cdna_gap_batch(shim_ctx, D.c, (int) nc, D.q, D.quc, qb, D.cres, D.pairs, cap),
+               "gmapdp_cdna_gap_batch");
+    for (i = 0; i < nc; i++) {
+      r = D.rc[i];
+      r->cr = D.cres[i];
+      shim_copy_pairs(r, D.pairs + r->cr.pair_offset, r->cr.npairs);
+      r->cr.pair_offset = 0;
+    }
+  }
+
+  t0 = shim_now();
+  td[1] = t0 - t1;
+  /* stage-2 seeding */
+  if (no > 0) {
+    size_t pc, dc;
+    GROW(D.o, D.ocap, no + 1);
+    qb = 0;
+    for (i = 0; i < no; i++) qb += D.ro[i]->qlen;
+    GROW(D.quc, D.quccap, qb + 1);
+    qb = 0;
+    for (i = 0; i < no; i++) {
+      r = D.ro[i];
+      D.o[i] = r->p.o;
+      D.o[i].qoff = (int32_t) qb;
+      memcpy(D.quc + qb, r->quc, r->qlen);
+      qb += r->qlen;
+    }
+    pc = gmapdp_oligo_positions_capacity(D.o, (int) no);
+    dc = gmapdp_oligo_diagonal_capacity(D.o, (int) no);
+    GROW(D.np, D.npcap, qb + 1);
+    GROW(D.mp, D.mpcap, qb + 1);
+    GROW(D.pos, D.poscap, pc + 1);
+    GROW(D.dg, D.dgcap, 4 * dc + 4);
+    GROW(D.ores, D.orescap, no + 1);
+    shim_check(gmapdp_oligo_mappings_batch(shim_ctx, D.o, (int) no, D.quc, qb, D.ores, D.np, D.mp, D.pos, pc, D.dg,
+                                           dc), "gmapdp_oligo_mappings_batch");
+    for (i = 0; i < no; i++) {
+      size_t q, ql;
+      r = D.ro[i];
+      r->orr = D.ores[i];
+      ql = r->qlen;
+      for (q = 0; q < ql; q++) {
+        r->np[q] = D.np[D.o[i].qoff + q];
+        r->mp[q] = r->np[q] > 0 ? D.mp[D.o[i].qoff + q] - (int32_t) r->orr.table_offset : -1;
+      }
+      if (r->tabn) memcpy(r->pos, D.pos + r->orr.table_offset, r->tabn * sizeof(uint32_t));
+      if (r->orr.ndiagonals > 0)
+        memcpy(r->dg, D.dg + 4 * r->orr.diag_offset, 4 * (size_t) r->orr.ndiagonals * sizeof(int32_t));
+      r->orr.table_offset = 0;
+      r->orr.diag_offset = 0;
+    }
+  }
+  td[2] = shim_now() - t0;
+  pthread_mutex_lock(&q_lock);
+  for (i = 0; i < 3; i++) shim_secs[i] += td[i];
+  pthread_mutex_unlock(&q_lock);
 }
 
 /* The engine's records in list order -> the reference's List_T (each push prepends).  The gap
@@ -226,42 +579,39 @@ __wrap_Dynprog_single_gap (int *dynprogindex, int *finalscore, int *nmatches, in
                            int length2, int offset1, int offset2, Univcoord_T chroffset, Univcoord_T chrhigh,
                            bool watsonp, int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
                            Pairpool_T pairpool, int extraband_single, bool widebandp, double defect_rate) {
-  gmapdp_single_problem p;
-  gmapdp_result res;
-  gmapdp_pair *pairs;
-  size_t cap;
+  shim_req *r;
+  gmapdp_single_problem *p;
   List_T list;
   if (shim_homopolymerp) shim_refuse("homopolymer mode (Dynprog_single_setup homopolymerp)");
-  pthread_mutex_lock(&shim_lock);
-  shim_context(genome, genomealt, dynprog);
-  memset(&p, 0, sizeof(p));
-  p.qoff = 0;
-  p.rlength = length1;
-  p.glength = length2;
-  p.roffset = offset1;
-  p.goffset = offset2;
-  p.chroffset = shim_coord(chroffset);
-  p.chrhigh = shim_coord(chrhigh);
-  p.flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0) | (widebandp ? GMAPDP_WIDEBAND : 0) |
-            SHIM_SIMD;
-  p.genestrand = genestrand;
-  p.extraband = extraband_single;
-  p.defect_rate = defect_rate;
-  p.dynprogindex = *dynprogindex;
-  cap = gmapdp_single_pair_capacity(&p, 1);
-  pairs = (gmapdp_pair *) malloc((cap ? cap : 1) * sizeof(gmapdp_pair));
-  shim_check(gmapdp_single_gap_batch(shim_ctx, &p, 1, sequence1, sequenceuc1, length1 > 0 ? (size_t) length1 : 0,
-                                     &res, pairs, cap), "gmapdp_single_gap_batch");
+  shim_check_call(genome, genomealt, dynprog);
+  r = shim_request(K_SINGLE);
+  p = &r->p.s;
+  p->rlength = length1;
+  p->glength = length2;
+  p->roffset = offset1;
+  p->goffset = offset2;
+  p->chroffset = shim_coord(chroffset);
+  p->chrhigh = shim_coord(chrhigh);
+  p->flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0) | (widebandp ? GMAPDP_WIDEBAND : 0) |
+             SHIM_SIMD;
+  p->genestrand = genestrand;
+  p->extraband = extraband_single;
+  p->defect_rate = defect_rate;
+  p->dynprogindex = *dynprogindex;
+  r->genome = genome;
+  r->q = sequence1;
+  r->quc = sequenceuc1;
+  r->qlen = length1 > 0 ? (size_t) length1 : 0;
+  GROW(r->pairs, r->pcap, gmapdp_single_pair_capacity(p, 1) + 1);
+  shim_submit(r);
   shim_count(ST_SINGLE);
-  pthread_mutex_unlock(&shim_lock);
-  list = shim_list(pairs + res.pair_offset, res.npairs, p.dynprogindex, -1, 0, 0, 0.0, 0.0, pairpool);
-  free(pairs);
-  *dynprogindex = res.dynprogindex;
-  *finalscore = res.traceback_score;
-  *nmatches = res.nmatches;
-  *nmismatches = res.nmismatches;
-  *nopens = res.nopens;
-  *nindels = res.nindels;
+  list = shim_list(r->pairs, r->r.npairs, p->dynprogindex, -1, 0, 0, 0.0, 0.0, pairpool);
+  *dynprogindex = r->r.dynprogindex;
+  *finalscore = r->r.traceback_score;
+  *nmatches = r->r.nmatches;
+  *nmismatches = r->r.nmismatches;
+  *nopens = r->r.nopens;
+  *nindels = r->r.nindels;
   return list;
 }
 
@@ -271,46 +621,41 @@ shim_end_gap (int end3p, int *dynprogindex, int *finalscore, int *nmatches, int 
               int offset2, Univcoord_T chroffset, Univcoord_T chrhigh, bool watsonp, int genestrand,
               bool jump_late_p, Genome_T genome, Genome_T genomealt, Pairpool_T pairpool, int extraband_end,
               double defect_rate, Endalign_T endalign, bool require_pos_score_p) {
-  gmapdp_end_problem p;
-  gmapdp_result res;
-  gmapdp_pair *pairs;
-  size_t cap;
+  shim_req *r;
+  gmapdp_end_problem *p;
   List_T list;
-  const char *q, *quc;
-  pthread_mutex_lock(&shim_lock);
-  shim_context(genome, genomealt, dynprog);
-  memset(&p, 0, sizeof(p));
-  p.rlength = length1;
-  p.glength = length2;
-  p.roffset = offset1;
-  p.goffset = offset2;
-  p.chroffset = shim_coord(chroffset);
-  p.chrhigh = shim_coord(chrhigh);
-  p.flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0) | SHIM_SIMD;
-  p.genestrand = genestrand;
-  p.extraband = extraband_end;
-  p.end3p = end3p;
-  p.endalign = (int32_t) endalign;
-  p.require_pos_score_p = require_pos_score_p ? 1 : 0;
-  p.dynprogindex = *dynprogindex;
-  p.defect_rate = defect_rate;
+  shim_check_call(genome, genomealt, dynprog);
+  r = shim_request(K_END);
+  p = &r->p.e;
+  p->rlength = length1;
+  p->glength = length2;
+  p->roffset = offset1;
+  p->goffset = offset2;
+  p->chroffset = shim_coord(chroffset);
+  p->chrhigh = shim_coord(chrhigh);
+  p->flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0) | SHIM_SIMD;
+  p->genestrand = genestrand;
+  p->extraband = extraband_end;
+  p->end3p = end3p;
+  p->endalign = (int32_t) endalign;
+  p->require_pos_score_p = require_pos_score_p ? 1 : 0;
+  p->dynprogindex = *dynprogindex;
+  p->defect_rate = defect_rate;
   /* end5's revsequence points at the LAST character of the slice (dynprog_end.c:1294) */
-  q = (end3p || length1 <= 0) ? seq : seq - (length1 - 1);
-  quc = (end3p || length1 <= 0) ? sequc : sequc - (length1 - 1);
-  cap = gmapdp_end_pair_capacity(&p, 1);
-  pairs = (gmapdp_pair *) malloc((cap ? cap : 1) * sizeof(gmapdp_pair));
-  shim_check(gmapdp_end_gap_batch(shim_ctx, &p, 1, q, quc, length1 > 0 ? (size_t) length1 : 0, &res, pairs, cap),
-             "gmapdp_end_gap_batch");
+  r->genome = genome;
+  r->q = (end3p || length1 <= 0) ? seq : seq - (length1 - 1);
+  r->quc = (end3p || length1 <= 0) ? sequc : sequc - (length1 - 1);
+  r->qlen = length1 > 0 ? (size_t) length1 : 0;
+  GROW(r->pairs, r->pcap, gmapdp_end_pair_capacity(p, 1) + 1);
+  shim_submit(r);
   shim_count(end3p ? ST_END3 : ST_END5);
-  pthread_mutex_unlock(&shim_lock);
-  list = shim_list(pairs + res.pair_offset, res.npairs, p.dynprogindex, -1, 0, 0, 0.0, 0.0, pairpool);
-  free(pairs);
-  *dynprogindex = res.dynprogindex;
-  *finalscore = res.traceback_score;
-  *nmatches = res.nmatches;
-  *nmismatches = res.nmismatches;
-  *nopens = res.nopens;
-  *nindels = res.nindels;
+  list = shim_list(r->pairs, r->r.npairs, p->dynprogindex, -1, 0, 0, 0.0, 0.0, pairpool);
+  *dynprogindex = r->r.dynprogindex;
+  *finalscore = r->r.traceback_score;
+  *nmatches = r->r.nmatches;
+  *nmismatches = r->r.nmismatches;
+  *nopens = r->r.nopens;
+  *nindels = r->r.nindels;
   return list;
 }
 
@@ -360,77 +705,79 @@ __wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_r
                            Univcoord_T chrhigh, int cdna_direction, bool watsonp, int genestrand, bool jump_late_p,
                            Genome_T genome, Genome_T genomealt, Pairpool_T pairpool, int extraband_paired,
                            double defect_rate, int maxpeelback, bool halfp, bool finalp) {
-  gmapdp_genome_problem p;
-  gmapdp_genome_result res;
-  gmapdp_pair *pairs;
-  size_t cap, m, i;
-  uint32_t *pos;
-  uint8_t *model;
-  double *probs;
+  shim_req *r;
+  gmapdp_genome_problem *p;
+  gmapdp_genome_result *res;
+  size_t m, i;
+  static __thread uint32_t *pos = NULL;
+  static __thread uint8_t *model = NULL;
+  static __thread size_t poscap = 0, modelcap = 0;
   List_T list;
   (void) chrnum;
   if (shim_splicing_iit) shim_refuse("known splice sites (a splicing IIT) in Dynprog_genome_gap");
-  pthread_mutex_lock(&shim_lock);
-  shim_context(genome, genomealt, dynprogL);
-  shim_context(genome, genomealt, dynprogR);
-  memset(&p, 0, sizeof(p));
-  p.rlength = rlength;
-  p.glengthL = glengthL;
-  p.glengthR = glengthR;
-  p.roffset = roffset;
-  p.goffsetL = goffsetL;
-  p.rev_goffsetR = rev_goffsetR;
-  p.chroffset = shim_coord(chroffset);
-  p.chrhigh = shim_coord(chrhigh);
-  p.flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0) | (halfp ? GMAPDP_HALFP : 0) |
-            (finalp ? GMAPDP_FINALP : 0) | SHIM_SIMD;
-  p.cdna_direction = cdna_direction;
-  p.genestrand = genestrand;
-  p.extraband = extraband_paired;
-  p.maxpeelback = maxpeelback;
-  p.dynprogindex = *dynprogindex;
-  p.defect_rate = defect_rate;
-  p.prob_offset = 0;
-  /* the MaxEnt probabilities the bridge reads, computed by the host as the reference does;
-     skipped where the engine resolves the call before reading them (rlength <= 1, size guard) */
+  shim_check_call(genome, genomealt, dynprogL);
+  shim_check_call(genome, genomealt, dynprogR);
+  r = shim_request(K_GENOME);
+  p = &r->p.g;
+  p->rlength = rlength;
+  p->glengthL = glengthL;
+  p->glengthR = glengthR;
+  p->roffset = roffset;
+  p->goffsetL = goffsetL;
+  p->rev_goffsetR = rev_goffsetR;
+  p->chroffset = shim_coord(chroffset);
+  p->chrhigh = shim_coord(chrhigh);
+  p->flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0) | (halfp ? GMAPDP_HALFP : 0) |
+             (finalp ? GMAPDP_FINALP : 0) | SHIM_SIMD;
+  p->cdna_direction = cdna_direction;
+  p->genestrand = genestrand;
+  p->extraband = extraband_paired;
+  p->maxpeelback = maxpeelback;
+  p->dynprogindex = *dynprogindex;
+  p->defect_rate = defect_rate;
+  p->prob_offset = 0;
+  /* the MaxEnt probabilities the bridge reads, computed on this thread with the host's own
+     Maxent_hr_*_prob as the reference does; skipped where the engine resolves the call before
+     reading them (rlength <= 1, size guard) */
   m = 0;
   if (rlength > 1 && rlength <= GMAPDP_MAX_RLENGTH && glengthL <= GMAPDP_MAX_GLENGTH &&
       glengthR <= GMAPDP_MAX_GLENGTH && glengthL > 0 && glengthR > 0)
-    m = gmapdp_genome_prob_entries(&p, 1);
-  probs = (double *) calloc(m ? m : 1, sizeof(double));
+    m = gmapdp_genome_prob_entries(p, 1);
+  GROW(r->pbuf, r->pbufcap, m + 1);
+  memset(r->pbuf, 0, (m + 1) * sizeof(double));
   if (m) {
-    pos = (uint32_t *) malloc(m * sizeof(uint32_t));
-    model = (uint8_t *) malloc(m);
-    shim_check(gmapdp_genome_splice_sites(&p, 1, pos, model, m), "gmapdp_genome_splice_sites");
+    GROW(pos, poscap, m);
+    GROW(model, modelcap, m);
+    shim_check(gmapdp_genome_splice_sites(p, 1, pos, model, m), "gmapdp_genome_splice_sites");
     /* the last entry of each side is never read (the reference leaves it unset too, :2575-2660) */
     for (i = 0; i < m; i++)
       if (i != (size_t) glengthL - 1 && i != m - 1)
-        probs[i] = shim_maxent(genome, genomealt, model[i], pos[i], chroffset);
-    free(pos);
-    free(model);
+        r->pbuf[i] = shim_maxent(genome, genomealt, model[i], pos[i], chroffset);
   }
-  cap = gmapdp_genome_pair_capacity(&p, 1);
-  pairs = (gmapdp_pair *) malloc((cap ? cap : 1) * sizeof(gmapdp_pair));
-  shim_check(gmapdp_genome_gap_batch(shim_ctx, &p, 1, rsequence, rsequenceuc, rlength > 0 ? (size_t) rlength : 0,
-                                     probs, m, &res, pairs, cap), "gmapdp_genome_gap_batch");
+  r->genome = genome;
+  r->q = rsequence;
+  r->quc = rsequenceuc;
+  r->qlen = rlength > 0 ? (size_t) rlength : 0;
+  r->probs = r->pbuf;
+  r->nprobs = m;
+  GROW(r->pairs, r->pcap, gmapdp_genome_pair_capacity(p, 1) + 1);
+  shim_submit(r);
   shim_count(ST_GENOME);
-  pthread_mutex_unlock(&shim_lock);
-  list = shim_list(pairs + res.pair_offset, res.npairs, p.dynprogindex, res.gap_index, res.gap_queryjump,
-                   res.introntype, res.left_prob, res.right_prob, pairpool);
-  free(pairs);
-  free(probs);
-  *dynprogindex = res.dynprogindex;
-  *traceback_score = res.traceback_score;
-  *nmatches = res.nmatches;
-  *nmismatches = res.nmismatches;
-  *nopens = res.nopens;
-  *nindels = res.nindels;
-  *introntype = res.introntype;
-  *left_prob = res.left_prob;
-  *right_prob = res.right_prob;
-  if (res.new_leftgenomepos != GMAPDP_UNSET) *new_leftgenomepos = res.new_leftgenomepos;
-  if (res.new_rightgenomepos != GMAPDP_UNSET) *new_rightgenomepos = res.new_rightgenomepos;
-  if (res.exonhead != GMAPDP_UNSET) *exonhead = res.exonhead;
+  res = &r->gr;
+  list = shim_list(r->pairs, res->npairs, p->dynprogindex, res->gap_index, res->gap_queryjump, res->introntype,
+                   res->left_prob, res->right_prob, pairpool);
+  *dynprogindex = res->dynprogindex;
+  *traceback_score = res->traceback_score;
+  *nmatches = res->nmatches;
+  *nmismatches = res->nmismatches;
+  *nopens = res->nopens;
+  *nindels = res->nindels;
+  *introntype = res->introntype;
+  *left_prob = res->left_prob;
+  *right_prob = res->right_prob;
+  if (res->new_leftgenomepos != GMAPDP_UNSET) *new_leftgenomepos = res->new_leftgenomepos;
+  if (res->new_rightgenomepos != GMAPDP_UNSET) *new_rightgenomepos = res->new_rightgenomepos;
+  if (res->exonhead != GMAPDP_UNSET) *exonhead = res->exonhead;
   return list;
 }
 
@@ -441,10 +788,8 @@ __wrap_Dynprog_cdna_gap (int *dynprogindex, int *traceback_score, bool *incomple
                          int rev_roffsetR, int goffset, Univcoord_T chroffset, Univcoord_T chrhigh, bool watsonp,
                          int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
                          Pairpool_T pairpool, int extraband_paired, double defect_rate) {
-  gmapdp_cdna_problem p;
-  gmapdp_cdna_result res;
-  gmapdp_pair *pairs;
-  size_t cap;
+  shim_req *r;
+  gmapdp_cdna_problem *p;
   List_T list;
   const char *lo, *hi, *lo_uc;
   long span;
@@ -458,37 +803,37 @@ __wrap_Dynprog_cdna_gap (int *dynprogindex, int *traceback_score, bool *incomple
   if (rev_rsequenceR + 1 > hi) hi = rev_rsequenceR + 1;
   lo_uc = rsequence_ucL - (rsequenceL - lo);
   if (rev_rsequence_ucR - lo_uc != rev_rsequenceR - lo) shim_refuse("query pieces from two different buffers");
-  pthread_mutex_lock(&shim_lock);
-  shim_context(genome, genomealt, dynprogL);
-  shim_context(genome, genomealt, dynprogR);
-  memset(&p, 0, sizeof(p));
-  p.qoffL = (int32_t) (rsequenceL - lo);
-  p.qoffR = (int32_t) (rev_rsequenceR - lo);
-  p.rlengthL = rlengthL;
-  p.rlengthR = rlengthR;
-  p.glength = glength;
-  p.roffsetL = roffsetL;
-  p.rev_roffsetR = rev_roffsetR;
-  p.goffset = goffset;
-  p.chroffset = shim_coord(chroffset);
-  p.chrhigh = shim_coord(chrhigh);
-  p.flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0) | SHIM_SIMD;
-  p.genestrand = genestrand;
-  p.extraband = extraband_paired;
-  p.dynprogindex = *dynprogindex;
-  p.defect_rate = defect_rate;
-  cap = gmapdp_cdna_pair_capacity(&p, 1);
-  pairs = (gmapdp_pair *) malloc((cap ? cap : 1) * sizeof(gmapdp_pair));
-  shim_check(gmapdp_cdna_gap_batch(shim_ctx, &p, 1, lo, lo_uc, (size_t) (hi - lo), &res, pairs, cap),
-             "gmapdp_cdna_gap_batch");
+  shim_check_call(genome, genomealt, dynprogL);
+  shim_check_call(genome, genomealt, dynprogR);
+  r = shim_request(K_CDNA);
+  p = &r->p.c;
+  p->qoffL = (int32_t) (rsequenceL - lo);
+  p->qoffR = (int32_t) (rev_rsequenceR - lo);
+  p->rlengthL = rlengthL;
+  p->rlengthR = rlengthR;
+  p->glength = glength;
+  p->roffsetL = roffsetL;
+  p->rev_roffsetR = rev_roffsetR;
+  p->goffset = goffset;
+  p->chroffset = shim_coord(chroffset);
+  p->chrhigh = shim_coord(chrhigh);
+  p->flags = (watsonp ? GMAPDP_WATSON : 0) | (jump_late_p ? GMAPDP_JUMP_LATE : 0) | SHIM_SIMD;
+  p->genestrand = genestrand;
+  p->extraband = extraband_paired;
+  p->dynprogindex = *dynprogindex;
+  p->defect_rate = defect_rate;
+  r->genome = genome;
+  r->q = lo;
+  r->quc = lo_uc;
+  r->qlen = (size_t) (hi - lo);
+  GROW(r->pairs, r->pcap, gmapdp_cdna_pair_capacity(p, 1) + 1);
+  shim_submit(r);
   shim_count(ST_CDNA);
-  pthread_mutex_unlock(&shim_lock);
-  list = shim_list(pairs + res.pair_offset, res.npairs, p.dynprogindex, res.gap_index, res.gap_queryjump, -1, 0.0,
-                   0.0, pairpool);
-  free(pairs);
-  *dynprogindex = res.dynprogindex;
-  if (res.traceback_score != GMAPDP_UNSET) *traceback_score = res.traceback_score;
-  if (res.incompletep) *incompletep = true;
+  list = shim_list(r->pairs, r->cr.npairs, p->dynprogindex, r->cr.gap_index, r->cr.gap_queryjump, -1, 0.0, 0.0,
+                   pairpool);
+  *dynprogindex = r->cr.dynprogindex;
+  if (r->cr.traceback_score != GMAPDP_UNSET) *traceback_score = r->cr.traceback_score;
+  if (r->cr.incompletep) *incompletep = true;
   return list;
 }
 
@@ -532,11 +877,9 @@ __wrap_Oligoindex_get_mappings (List_T diagonals, bool *coveredp, Chrpos_T **map
                                 Oligoindex_array_T array, Oligoindex_T this, char *queryuc_ptr, int querystart,
                                 int queryend, int querylength, Chrpos_T chrstart, Chrpos_T chrend,
                                 Univcoord_T chroffset, Univcoord_T chrhigh, bool plusp, Diagpool_T diagpool) {
-  gmapdp_oligo_problem p;
-  gmapdp_oligo_result res;
-  int32_t *np, *mp, *dg;
-  uint32_t *pos;
-  size_t pc, dc;
+  shim_req *r;
+  gmapdp_oligo_problem *p;
+  size_t dc;
   int q, k;
   (void) array;
   if (this != shim_tally.oligoindex || plusp != shim_tally.plusp || querystart != 0 || queryend != querylength ||
@@ -548,53 +891,48 @@ __wrap_Oligoindex_get_mappings (List_T diagonals, bool *coveredp, Chrpos_T **map
   if (*totalpositions != 0 || *maxnconsecutive != 0) shim_refuse("a second oligoindex source (coverage loop)");
   for (q = 0; q < querylength; q++)
     if (coveredp[q]) shim_refuse("stage-2 seeding with covered query positions");
-  memset(&p, 0, sizeof(p));
-  p.qoff = 0;
-  p.querylength = querylength;
-  p.chrstart = chrstart;
-  p.chrend = chrend;
-  p.chroffset = shim_coord(chroffset);
-  p.chrhigh = shim_coord(chrhigh);
-  p.plusp = plusp ? 1 : 0;
-  p.minor = this->diag_lookback == 60 ? 1 : 0;  /* Oligoindex_array_new_minor's index (oligoindex_hr.c:8612) */
-  pthread_mutex_lock(&shim_lock);
-  shim_context(shim_tally.genome, NULL, NULL);
-  pc = gmapdp_oligo_positions_capacity(&p, 1);
-  dc = gmapdp_oligo_diagonal_capacity(&p, 1);
-  np = (int32_t *) malloc((querylength + 1) * sizeof(int32_t));
-  mp = (int32_t *) malloc((querylength + 1) * sizeof(int32_t));
-  pos = (uint32_t *) malloc((pc ? pc : 1) * sizeof(uint32_t));
-  dg = (int32_t *) malloc(4 * (dc ? dc : 1) * sizeof(int32_t));
-  shim_check(gmapdp_oligo_mappings_batch(shim_ctx, &p, 1, queryuc_ptr, (size_t) querylength, &res, np, mp, pos, pc,
-                                         dg, dc), "gmapdp_oligo_mappings_batch");
+  r = shim_request(K_OLIGO);
+  p = &r->p.o;
+  p->querylength = querylength;
+  p->chrstart = chrstart;
+  p->chrend = chrend;
+  p->chroffset = shim_coord(chroffset);
+  p->chrhigh = shim_coord(chrhigh);
+  p->plusp = plusp ? 1 : 0;
+  p->minor = this->diag_lookback == 60 ? 1 : 0;  /* Oligoindex_array_new_minor's index (oligoindex_hr.c:8612) */
+  r->genome = shim_tally.genome;
+  r->q = r->quc = queryuc_ptr;
+  r->qlen = querylength > 0 ? (size_t) querylength : 0;
+  r->tabn = gmapdp_oligo_positions_capacity(p, 1);
+  dc = gmapdp_oligo_diagonal_capacity(p, 1);
+  GROW(r->np, r->npcap, r->qlen + 1);
+  GROW(r->mp, r->mpcap, r->qlen + 1);
+  GROW(r->pos, r->poscap, r->tabn + 1);
+  GROW(r->dg, r->dgcap, 4 * dc + 4);
+  shim_submit(r);
   shim_count(ST_OLIGO);
-  pthread_mutex_unlock(&shim_lock);
   /* the table, owned by the oligoindex (freed by Oligoindex_untally) */
   this->table = NULL;
-  if (pc > 0) {
-    this->table = (Chrpos_T *) MALLOC(pc * sizeof(Chrpos_T));
-    memcpy(this->table, pos, pc * sizeof(Chrpos_T));
+  if (r->tabn > 0) {
+    this->table = (Chrpos_T *) MALLOC(r->tabn * sizeof(Chrpos_T));
+    memcpy(this->table, r->pos, r->tabn * sizeof(Chrpos_T));
   }
   for (q = 0; q < querylength; q++) {
-    if (np[q] > 0) {
-      npositions[q] = np[q];
-      mappings[q] = &this->table[mp[q]];
+    if (r->np[q] > 0) {
+      npositions[q] = r->np[q];
+      mappings[q] = &this->table[r->mp[q]];
     } else if (q <= querylength - 8 && strspn(queryuc_ptr + q, "ACGT") >= 8) {
       /* lookup (:34069) on a full 8-mer without hits: nhits 0, mappings NULL; others stay as given */
       npositions[q] = 0;
       mappings[q] = NULL;
     }
   }
-  *totalpositions = res.totalpositions;
-  *maxnconsecutive = res.maxnconsecutive;
-  if (chrend > chrstart) *oned_matrix_p = res.oned_matrix_p ? true : false;
-  for (k = res.ndiagonals - 1; k >= 0; k--) {
-    const int32_t *d = dg + 4 * (res.diag_offset + k);
+  *totalpositions = r->orr.totalpositions;
+  *maxnconsecutive = r->orr.maxnconsecutive;
+  if (chrend > chrstart) *oned_matrix_p = r->orr.oned_matrix_p ? true : false;
+  for (k = r->orr.ndiagonals - 1; k >= 0; k--) {
+    const int32_t *d = r->dg + 4 * k;
     diagonals = Diagpool_push(diagonals, diagpool, d[0], d[1], d[2], d[3]);
   }
-  free(np);
-  free(mp);
-  free(pos);
-  free(dg);
   return diagonals;
 }

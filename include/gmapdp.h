@@ -248,6 +248,17 @@ int gmapdp_genome_gap_batch (gmapdp_ctx *ctx, const gmapdp_genome_problem *probl
                              gmapdp_genome_result *results, gmapdp_pair *pairs, size_t pair_capacity);
 size_t gmapdp_genome_pair_capacity (const gmapdp_genome_problem *problems, int n);
 
+/* Dynprog_single_gap + Dynprog_end5/3_gap + Dynprog_genome_gap calls of many callers in one
+ * synchronous batch (the drop-in's dispatcher: one launch set for whatever GMAP's worker threads have
+ * issued meanwhile).  One query arena (all qoff index qseq / qseq_uc), one splice-probability arena;
+ * results has nsingle + nend entries (singles first), genome_results ngenome; pair_capacity at least
+ * gmapdp_single_pair_capacity + gmapdp_end_pair_capacity + gmapdp_genome_pair_capacity. */
+int gmapdp_dynprog_batch (gmapdp_ctx *ctx, const gmapdp_single_problem *singles, int nsingle,
+                          const gmapdp_end_problem *ends, int nend, const gmapdp_genome_problem *genomes, int ngenome,
+                          const char *qseq, const char *qseq_uc, size_t qbytes, const double *splice_probs,
+                          size_t nprobs, gmapdp_result *results, gmapdp_genome_result *genome_results,
+                          gmapdp_pair *pairs, size_t pair_capacity);
+
 /* One Dynprog_cdna_gap call (dynprog_cdna.c:787 argument list): a cDNA insertion between two
  * anchors.  rsequenceL / rsequence_ucL = qseq / qseq_uc + qoffL (the L piece's first character),
  * rev_rsequenceR / rev_rsequence_ucR = qseq / qseq_uc + qoffR (the R piece's LAST character).  The

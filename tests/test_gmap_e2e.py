@@ -53,7 +53,7 @@ E2E_ARGS = ["-g", "e2e_genome.fa", "-f", "samse", "--no-sam-headers", "e2e_reads
 def _stats(stderr):
     m = re.search(r"gmapdp shim calls:(.*)", stderr)
     assert m, "shim statistics missing (GMAPDP_SHIM_STATS): " + stderr[-500:]
-    return {k: int(v) for k, v in re.findall(r"(\w+)=(\d+)", m.group(1))}
+    return {k: float(v) for k, v in re.findall(r"(\w+)=([\d.]+)", m.group(1))}
 
 
 # ---- the oracle itself: the reference program reproduces the reference's golden and our fixtures ----
@@ -117,8 +117,13 @@ def test_gpu_gmap_synthetic_reads(build):
 
 
 @pytest.mark.gpu
-def test_gpu_gmap_worker_threads():
-    """-t 4 worker threads sharing the engine (the shim's per-thread stage-2 tally record and the
-    shared context): output identical to the single-threaded reference."""
-    out, _ = _run(_exe("gmap_gpu_nosimd"), ["-t", "4", "-O"] + E2E_ARGS)
+@pytest.mark.parametrize("threads", [4, 32])
+def test_gpu_gmap_worker_threads(threads):
+    """GMAP worker threads sharing the engine through the shim's dispatcher (per-thread requests and
+    stage-2 tally records, one engine context): output identical to the single-threaded reference,
+    and the dispatcher really ran several threads' calls per batch."""
+    out, err = _run(_exe("gmap_gpu_nosimd"), ["-t", str(threads), "-O"] + E2E_ARGS,
+                    env={"GMAPDP_SHIM_STATS": "1", "GMAPDP_SHIM_DISPATCHERS": "2"})
     assert out == _read("e2e_nosimd.sam")
+    st = _stats(err)
+    assert st["batches"] > 0 and (threads < 8 or st["mean_batch"] > 1.5), st

@@ -1,0 +1,70 @@
+"""End-to-end timing of GMAP's own per-read pipeline: the unmodified reference `gmap` (CPU) against the
+same program linked with the drop-in shim (every Dynprog_* call and stage-2 seeding on the MI355X
+engine), on the same host cores.  Measurement tool, run on the GPU box:
+
+    python tools/e2e_timing.py --reads 2000 --threads 1,16
+
+Reads are tests/golden/make_e2e.py's synthetic 2-kb spliced reads (5 exons x 400 nt, 2 % subs) against
+its 300-kb segment, in user-segment mode (-g: stage 2 over the whole segment, then stage 3).  Both
+programs' SAM outputs are compared; the JSON line gives reads/s per program and thread count and the
+shim's call counts.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reads", type=int, default=2000)
+    ap.add_argument("--threads", default="1,16")
+    ap.add_argument("--build", default="nosimd", choices=["nosimd", "avx2"])
+    ap.add_argument("--gpu-threads", default=None, help="thread counts for the GPU program (default: --threads)")
+    ap.add_argument("--dispatchers", type=int, default=4, help="GMAPDP_SHIM_DISPATCHERS")
+    a = ap.parse_args()
+    import make_e2e as M
+    genome = list(M.synth_genome())
+    reads = [M.synth_read(genome, i) for i in range(a.reads)]
+    tmp = tempfile.mkdtemp(prefix="e2e_")
+    M.write_fasta(os.path.join(tmp, "g.fa"), [("synseg", "".join(genome))])
+    M.write_fasta(os.path.join(tmp, "r.fa"), reads)
+    ref = os.path.join(ROOT, "oracle", "_ref")
+    out = {"reads": a.reads, "build": a.build, "cpu_model": None, "runs": []}
+    try:
+        out["cpu_model"] = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    sams = {}
+    cpu_t = [int(x) for x in a.threads.split(",")]
+    gpu_t = [int(x) for x in (a.gpu_threads or a.threads).split(",")]
+    runs = [("gmap_%s" % a.build, t) for t in cpu_t] + [("gmap_gpu_%s" % a.build, t) for t in gpu_t]
+    out["dispatchers"] = a.dispatchers
+    for prog, t in runs:
+        if True:
+            env = dict(os.environ, GMAPDP_SHIM_STATS="1", GMAPDP_SHIM_DISPATCHERS=str(a.dispatchers))
+            args = [os.path.join(ref, prog), "-t", str(t), "-O", "-g", "g.fa", "-f", "samse", "--no-sam-headers",
+                    "r.fa"]
+            t0 = time.perf_counter()
+            r = subprocess.run(args, cwd=tmp, env=env, capture_output=True, text=True, timeout=1500)
+            dt = time.perf_counter() - t0
+            if r.returncode != 0:
+                raise SystemExit("%s failed: %s" % (prog, r.stderr[-2000:]))
+            sams[(prog, t)] = r.stdout
+            stats = [l for l in r.stderr.splitlines() if l.startswith("gmapdp shim calls")]
+            out["runs"].append({"program": prog, "threads": t, "seconds": dt, "reads_per_s": a.reads / dt,
+                                "shim_calls": stats[0] if stats else None})
+            print(json.dumps(out["runs"][-1]), file=sys.stderr, flush=True)
+    base = sams[("gmap_%s" % a.build, min(cpu_t))]
+    out["outputs_identical"] = all(v == base for v in sams.values())
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
