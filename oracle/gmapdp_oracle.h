@@ -115,6 +115,17 @@ int orc_oligo_mappings (const char *queryuc, int querylength, unsigned int chrst
                         unsigned int chroffset, unsigned int chrhigh, int plusp, int minor, int *npositions,
                         unsigned int *positions, int pos_cap, int *scalars, int *diags, int diag_cap);
 
+/* Stage2_compute (stage2.c:6325) as GMAP calls it (stage2_chain_oracle.c): the seeding above, then
+   Diag_update_coverage, the proceed test, Diag_compute_bounds, align_compute_lookback,
+   convert_to_nucleotides and Stage2_filter_unique.  Same arguments and outputs as
+   refh_stage2_compute (oracle/refharness.c): the kept results' middle lists in `pairs`, result i at
+   pairs[paths[2 i]] with paths[2 i + 1] records.  scalars[0..5] = results kept, paths traced,
+   ncovered, exit (0 no positions, 1 coverage filter, 2 chained), diag_querystart, diag_queryend.
+   Returns the number of results, -1 when a capacity is too small, the seeding's codes below 0. */
+int orc_stage2_compute (const char *queryseq, const char *queryuc, int querylength, unsigned int chrstart,
+                        unsigned int chrend, unsigned int chroffset, unsigned int chrhigh, int plusp, int splicingp,
+                        int maxintronlen, int *scalars, int *paths, int path_cap, OrcPair *pairs, int pair_cap);
+
 #ifdef __cplusplus
 }
 #endif

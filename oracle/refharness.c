@@ -40,6 +40,8 @@
 #include "oligoindex_hr.h"
 #include "diag.h"
 #include "diagpool.h"
+#include "cellpool.h"
+#include "stage2.h"
 
 /* Flat pair record (matches oracle/gmapdp_oracle.h RefPair / GmapdpPair
  * semantics: one record per Pair_T in list order). */
@@ -531,4 +533,86 @@ refh_oligo_mappings (const char *queryuc, int querylength, unsigned int chrstart
   free(coveredp);
   free(quc);
   return nd > diag_cap ? -1 : n;
+}
+
+
+/* Stage2_compute (stage2.c:6325) itself, with GMAP's arguments (gmap.c:1208-1215: query_offset 0,
+   genestrand 0, proceed_pctcoverage 0.3, the major oligoindex array, genomealt = genome, localp,
+   skip_repetitive_p, favor_right_p false, max_nalignments MAX_NALIGNMENTS = 10, no stopwatch) after
+   Stage2_setup (gmap.c:6544: cross_species_p false, suboptimal_score_start -1 / _end 3,
+   sufflookback 60, nsufflookback 5, STANDARD mode, no SNPs).  Each returned Stage2_T's middle list
+   is flattened into `pairs` (list order); paths[2 i] / paths[2 i + 1] = its first record / count.
+   scalars[0] = number of results; scalars[1] = 1 if any result has start or end lists (they stay
+   NULL without MOVE_TO_STAGE3).  Returns the number of results, -1 when a capacity is too small. */
+static Stage2_alloc_T stage2_alloc = NULL;
+static Cellpool_T cellpool = NULL;
+static int stage2_splicingp = -1, stage2_maxintronlen = -1;
+
+int
+refh_stage2_compute (const char *queryseq, const char *queryuc, int querylength, unsigned int chrstart,
+                     unsigned int chrend, unsigned int chroffset, unsigned int chrhigh, int plusp, int splicingp,
+                     int maxintronlen, int *scalars, int *paths, int path_cap, RefPair *pairs, int pair_cap) {
+  List_T results, p, q;
+  char *qs, *quc;
+  int nres = 0, n = 0, k;
+  if (oligo_major == NULL) {
+    Oligoindex_hr_setup(STANDARD);
+    oligo_major = Oligoindex_array_new_major(100000, 1000000);  /* gmap.c:113-114, 4739-4740 */
+    oligo_minor = Oligoindex_array_new_minor(100000, 1000000);
+    diagpool = Diagpool_new();
+  }
+  if (stage2_alloc == NULL) {
+    stage2_alloc = Stage2_alloc_new(100000);  /* MAX_QUERYLENGTH_FOR_ALLOC, gmap.c:113 */
+    cellpool = Cellpool_new();
+  }
+  if (splicingp != stage2_splicingp || maxintronlen != stage2_maxintronlen) {
+    Stage2_setup(splicingp ? true : false, /*cross_species_p*/false, /*suboptimal_score_start*/-1,
+                 /*suboptimal_score_end*/3, /*sufflookback*/60, /*nsufflookback*/5, maxintronlen, STANDARD,
+                 /*snps_p*/false);
+    stage2_splicingp = splicingp;
+    stage2_maxintronlen = maxintronlen;
+  }
+  qs = (char *) malloc(querylength + 1);
+  quc = (char *) malloc(querylength + 1);
+  memcpy(qs, queryseq, querylength);
+  memcpy(quc, queryuc, querylength);
+  qs[querylength] = quc[querylength] = '\0';
+  Pairpool_reset(pairpool);
+  results = Stage2_compute(qs, quc, querylength, /*query_offset*/0, chrstart, chrend, chroffset, chrhigh,
+                           plusp ? true : false, /*genestrand*/0, stage2_alloc, /*proceed_pctcoverage*/0.3,
+                           oligo_major, genome, genome, pairpool, diagpool, cellpool, /*localp*/true,
+                           /*skip_repetitive_p*/true, /*favor_right_p*/false, /*max_nalignments*/10,
+                           /*stopwatch*/NULL, /*diag_debug*/false);
+  scalars[0] = scalars[1] = 0;
+  for (p = results; p != NULL; p = List_next(p)) {
+    Stage2_T s2 = (Stage2_T) List_head(p);
+    if (Stage2_all_starts(s2) != NULL || Stage2_all_ends(s2) != NULL) scalars[1] = 1;
+    if (nres < path_cap) paths[2 * nres] = n;
+    k = 0;
+    for (q = Stage2_middle(s2); q != NULL; q = List_next(q), k++) {
+      Pair_T pr = (Pair_T) List_head(q);
+      if (n < pair_cap) {
+        RefPair *r = &pairs[n];
+        r->querypos = pr->querypos;
+        r->genomepos = pr->genomepos;
+        r->queryjump = pr->gapp ? pr->queryjump : 0;
+        r->genomejump = pr->gapp ? pr->genomejump : 0;
+        r->dynprogindex = pr->dynprogindex;
+        r->cdna = pr->cdna;
+        r->comp = pr->comp;
+        r->genome = pr->genome;
+        r->genomealt = pr->genomealt;
+        r->gapp = pr->gapp ? 1 : 0;
+      }
+      n++;
+    }
+    if (nres < path_cap) paths[2 * nres + 1] = k;
+    nres++;
+    Stage2_free(&s2);
+  }
+  List_free(&results);
+  scalars[0] = nres;
+  free(qs);
+  free(quc);
+  return (nres > path_cap || n > pair_cap) ? -1 : nres;
 }

@@ -673,3 +673,72 @@ def oligo_problem(rng, genome: bytes, edge=False):
             chrstart, chrend = 0, min(chrlen - 1, chrstart + rng.randint(1000, 40000))
     return dict(quc=bytes(q), chrstart=chrstart, chrend=chrend, chroffset=chroffset, chrhigh=chrhigh,
                 plusp=int(plusp), minor=int(rng.random() < 0.3))
+
+
+# ---------------------------------------------------------------------------
+# Stage2_compute (stage2.c:6325): seeding + chaining + convert_to_nucleotides + filter_unique
+# ---------------------------------------------------------------------------
+S2_PAIR_CAP = 1 << 18
+S2_PATH_CAP = 1024
+
+
+def _stage2_compute(self, p):
+    """(number of results, [middle pair list of each result]) or ("err", code).  Each pair is a
+    Pair.key() tuple; gap holders carry queryjump / genomejump and gapp = 1."""
+    f = getattr(self.lib, self.prefix + "stage2_compute")
+    if not getattr(self, "_s2_ready", False):
+        f.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_uint, C.c_uint, C.c_uint, C.c_uint, C.c_int, C.c_int,
+                      C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int, C.POINTER(Pair), C.c_int]
+        f.restype = C.c_int
+        self._s2_sc = (C.c_int * 8)()
+        self._s2_paths = (C.c_int * (2 * S2_PATH_CAP))()
+        self._s2_pairs = (Pair * S2_PAIR_CAP)()
+        self._s2_ready = True
+    r = f(p["q"], p["quc"], len(p["quc"]), C.c_uint(p["chrstart"]), C.c_uint(p["chrend"]), C.c_uint(p["chroffset"]),
+          C.c_uint(p["chrhigh"]), int(p["plusp"]), int(p.get("splicingp", 1)), int(p.get("maxintronlen", 500000)),
+          self._s2_sc, self._s2_paths, S2_PATH_CAP, self._s2_pairs, S2_PAIR_CAP)
+    if r < 0:
+        return ("err", r)
+    pr, pa = self._s2_pairs, self._s2_paths
+    return r, [[pr[pa[2 * i] + j].key() for j in range(pa[2 * i + 1])] for i in range(r)]
+
+
+Ref.stage2_compute = _stage2_compute
+Oracle.stage2_compute = _stage2_compute
+
+
+def repeat_genome(rng, n, nfrac=0.002):
+    """An i.i.d. genome with planted tandem repeats and duplicated segments (many hits per 8-mer,
+    several chains per read)."""
+    g = bytearray(random_genome(rng, n, nfrac))
+    for _ in range(n // 20000):
+        unit = bytes(rng.choice(b"ACGT") for _ in range(rng.randint(1, 12)))
+        L = rng.randint(200, 3000)
+        s = rng.randint(0, n - L - 1)
+        g[s:s + L] = (unit * (L // len(unit) + 1))[:L]
+    for _ in range(n // 50000):
+        L = rng.randint(300, 3000)
+        a, b = rng.randint(0, n - L - 1), rng.randint(0, n - L - 1)
+        g[b:b + L] = g[a:a + L]
+    return bytes(g)
+
+
+def stage2_problem(rng, genome: bytes, edge=False):
+    """One Stage2_compute call as GMAP makes it (gmap.c:1208): the seeding problem of oligo_problem
+    with the major oligoindex, a query in mixed case (queryseq) and upper case (queryuc), sometimes a
+    segment of another locus spliced into the read, and the splicing switch / maxintronlen GMAP's
+    options set (Stage2_setup)."""
+    p = oligo_problem(rng, genome, edge=edge)
+    p["minor"] = 0
+    q = bytearray(p["quc"])
+    if rng.random() < 0.3:
+        s = rng.randint(0, len(genome) - 600)
+        q[len(q) // 2:len(q) // 2] = genome[s:s + rng.randint(50, 500)]
+    for j in range(len(q)):
+        if rng.random() < 0.05:
+            q[j] = ord(chr(q[j]).lower())
+    p["q"] = bytes(q)
+    p["quc"] = bytes(q).upper()
+    p["splicingp"] = 0 if rng.random() < 0.15 else 1
+    p["maxintronlen"] = rng.choice([500000, 500000, 500000, 2000, 200])
+    return p

@@ -25,6 +25,8 @@ and the reference's outputs.
                          from the reference's AVX2 objects called on zeroed Dynprog_T arenas, on
                          problems inside the domain where that build is defined (see
                          simd_domain below); halfp genome gaps from the --enable-alloca AVX2 build
+  stage2_golden.npz      Stage2_compute (stage2.c:6325): seeding, chaining, convert_to_nucleotides,
+                         filter_unique (python tests/golden/make_golden.py stage2)
   oligo_golden.npz       stage-2 seeding: Oligoindex_hr_tally + Oligoindex_get_mappings
                          (oligoindex_hr.c:33849/34127) as Stage2_compute runs them for GMAP
                          (python tests/golden/make_golden.py oligo)
@@ -128,7 +130,7 @@ def pack(g, probs, outputs, names):
 
 def load(path):
     """Inverse of pack: (genome bytes, [problem dicts], {tag: [(scalars, pairs-or-None)]})."""
-    z = np.load(path, allow_pickle=False)
+    z = dict(np.load(path, allow_pickle=False))  # NpzFile re-reads an array on every subscript
     names = [str(x) for x in z["param_names"]]
     qoff = np.concatenate([[0], np.cumsum(z["qlen"])])
     qb, qub = z["qbuf"].tobytes(), z["qucbuf"].tobytes()
@@ -139,18 +141,18 @@ def load(path):
         p["defect_rate"] = float(z["defect"][i])
         p["q"] = qb[qoff[i]:qoff[i + 1]]
         p["quc"] = qub[qoff[i]:qoff[i + 1]]
-        if "splice_probs" in z.files:
+        if "splice_probs" in z:
             gl, gr = max(0, p["glengthL"]), max(0, p["glengthR"])
             p["probsL"] = [float(x) for x in z["splice_probs"][poff:poff + gl]]
             p["probsR"] = [float(x) for x in z["splice_probs"][poff + gl:poff + gl + gr]]
             poff += gl + gr
         probs.append(p)
     outs = {}
-    for key in z.files:
+    for key in z:
         if key.endswith("_scalars"):
             tag = key[:-len("_scalars")]
             scal, npairs, pairs = z[tag + "_scalars"], z[tag + "_npairs"], z[tag + "_pairs"]
-            dscal = z[tag + "_dscalars"] if (tag + "_dscalars") in z.files else None
+            dscal = z[tag + "_dscalars"] if (tag + "_dscalars") in z else None
             res, pos = [], 0
             for i in range(len(scal)):
                 n = int(npairs[i])
@@ -264,7 +266,7 @@ def main_oligo():
 
 def load_oligo(path):
     """(genome bytes, [problem dicts], [(scalars, npositions, positions, diagonals)])."""
-    z = np.load(path, allow_pickle=False)
+    z = dict(np.load(path, allow_pickle=False))
     names = [str(x) for x in z["param_names"]]
     qoff = np.concatenate([[0], np.cumsum(z["qlen"])])
     poff = np.concatenate([[0], np.cumsum(z["npos_total"])])
@@ -283,6 +285,64 @@ def load_oligo(path):
     return z["genome"].tobytes(), probs, outs
 
 
+STAGE2_PARAMS = ["chrstart", "chrend", "chroffset", "chrhigh", "plusp", "splicingp", "maxintronlen"]
+
+
+def stage2_problems(seed=2029, n_typical=240, n_edge=60, genome_len=300000):
+    from dpbind import repeat_genome, stage2_problem
+    rng = random.Random(seed)
+    g = repeat_genome(rng, genome_len)
+    probs = [stage2_problem(rng, g) for _ in range(n_typical)]
+    probs += [stage2_problem(rng, g, edge=True) for _ in range(n_edge)]
+    return g, probs
+
+
+def main_stage2():
+    g, probs = stage2_problems()
+    ref = Ref("nosimd")
+    ref.set_genome(g)
+    outs = [ref.stage2_compute(p) for p in probs]
+    assert all(o[0] != "err" for o in outs)
+    flat = [pr for o in outs for path in o[1] for pr in path]
+    d = dict(genome=np.frombuffer(g, dtype=np.uint8),
+             params=np.array([[p[k] for k in STAGE2_PARAMS] for p in probs], dtype=np.int64),
+             param_names=np.array(STAGE2_PARAMS), qlen=np.array([len(p["quc"]) for p in probs], dtype=np.int32),
+             qbuf=np.frombuffer(b"".join(p["q"] for p in probs), dtype=np.uint8),
+             nresults=np.array([o[0] for o in outs], dtype=np.int32),
+             path_npairs=np.array([len(path) for o in outs for path in o[1]], dtype=np.int32),
+             pairs_int=np.array([pr[:5] + (pr[9],) for pr in flat], dtype=np.int32).reshape(-1, 6),
+             pairs_chr=np.array([[ord(c) for c in pr[5:9]] for pr in flat], dtype=np.uint8).reshape(-1, 4))
+    out = os.path.join(HERE, "stage2_golden.npz")
+    np.savez_compressed(out, **d)
+    print("wrote %s: %d problems, %d results, %d pair records" % (out, len(probs), len(d["path_npairs"]), len(flat)))
+
+
+def load_stage2(path):
+    """(genome bytes, [problem dicts], [(nresults, [pair-key lists])])."""
+    z = dict(np.load(path, allow_pickle=False))  # NpzFile re-reads an array on every subscript
+    names = [str(x) for x in z["param_names"]]
+    qoff = np.concatenate([[0], np.cumsum(z["qlen"])])
+    qb = z["qbuf"].tobytes()
+    z["pairs_int"] = z["pairs_int"].tolist()
+    z["pairs_chr"] = z["pairs_chr"].tolist()
+    probs, outs, pi, ri = [], [], 0, 0
+    for i, row in enumerate(z["params"]):
+        p = {k: int(v) for k, v in zip(names, row)}
+        p["q"] = qb[qoff[i]:qoff[i + 1]]
+        p["quc"] = p["q"].upper()
+        probs.append(p)
+        paths = []
+        for _ in range(int(z["nresults"][i])):
+            n = int(z["path_npairs"][ri])
+            ri += 1
+            paths.append([tuple(int(x) for x in z["pairs_int"][pi + j][:5])
+                          + tuple(bytes([int(c)]) for c in z["pairs_chr"][pi + j])
+                          + (int(z["pairs_int"][pi + j][5]),) for j in range(n)])
+            pi += n
+        outs.append((int(z["nresults"][i]), paths))
+    return z["genome"].tobytes(), probs, outs
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "simd":
         main_simd()
@@ -290,5 +350,7 @@ if __name__ == "__main__":
         main_cdna()
     elif len(sys.argv) > 1 and sys.argv[1] == "oligo":
         main_oligo()
+    elif len(sys.argv) > 1 and sys.argv[1] == "stage2":
+        main_stage2()
     else:
         main()

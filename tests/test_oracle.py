@@ -392,3 +392,43 @@ def test_oracle_oligo_mappings_vs_reference_random():
             p = oligo_problem(rng, g, edge=(i % 4 == 0))
             a, b = ref.oligo_mappings(p), orc.oligo_mappings(p)
             assert a == b, (variant, i, {k: v for k, v in p.items() if k != "quc"})
+
+
+# ---------------------------------------------------------------------------
+# Stage2_compute (stage2.c:6325): seeding, Diag_compute_bounds, align_compute_lookback,
+# convert_to_nucleotides, Stage2_filter_unique
+# ---------------------------------------------------------------------------
+def _load_stage2_golden():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(HERE, "golden", "make_golden.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m.load_stage2(os.path.join(HERE, "golden", "stage2_golden.npz"))
+
+
+def test_oracle_stage2_compute_matches_golden():
+    g, probs, exp = _load_stage2_golden()
+    orc = Oracle()
+    orc.set_genome(g)
+    bad = [i for i, p in enumerate(probs) if orc.stage2_compute(p) != exp[i]]
+    assert not bad, "stage-2 problems differing from the golden: %s" % bad[:10]
+    # the golden holds the exits and shapes the chaining has: no positions, several kept results,
+    # gap holders, both strands, splicing off, short maxintronlen
+    assert any(o[0] == 0 for o in exp) and any(o[0] > 1 for o in exp)
+    assert any(pr[9] for o in exp for path in o[1] for pr in path)
+    assert {p["plusp"] for p in probs} == {0, 1} and {p["splicingp"] for p in probs} == {0, 1}
+
+
+@pytest.mark.skipif(not ref_available(), reason="reference objects not built")
+def test_oracle_stage2_compute_vs_reference_random():
+    from dpbind import random_genome, repeat_genome, stage2_problem
+    ref, orc = Ref("nosimd"), Oracle()
+    for seed in (11, 12):
+        rng = random.Random(seed)
+        g = repeat_genome(rng, 300000) if seed % 2 else random_genome(rng, 300000)
+        ref.set_genome(g)
+        orc.set_genome(g)
+        for i in range(150):
+            p = stage2_problem(rng, g, edge=(i % 5 == 0))
+            a, b = ref.stage2_compute(p), orc.stage2_compute(p)
+            assert a == b, "seed %d problem %d: reference %s vs oracle %s" % (seed, i, a[0], b[0])
