@@ -75,6 +75,13 @@ hipError_t launch_cg(bool simd, int RB, int nproblems, size_t lds, hipStream_t s
                      gmapdp_cdna_result* results, gmapdp_pair* pairs);
 size_t lds_bytes_oi(int umax, bool wide);
 size_t scratch_bytes_oi(int querylength, uint32_t genomiclength);
+size_t scratch_bytes_s2c(int querylength, int totalpositions, int ndiagonals);
+hipError_t launch_s2c(int nproblems, hipStream_t stream, const DevStage2Problem* probs, const uint32_t* blocks,
+                      uint64_t nwords, const char* qseq, const char* quc, const gmapdp_oligo_result* ores,
+                      const int32_t* npos, const int32_t* map, const uint32_t* table, const int32_t* diags,
+                      unsigned char* scratch, unsigned long long* counters, unsigned long long scratch_cap,
+                      gmapdp_stage2_result* results, gmapdp_path* paths, unsigned long long path_cap,
+                      gmapdp_path_pair* pairs, unsigned long long pair_cap);
 hipError_t launch_oi(bool wide, int nproblems, size_t lds, hipStream_t stream, const DevOligoProblem* probs,
                      const uint32_t* blocks, const char* quc, unsigned char* scratch, gmapdp_oligo_result* results,
                      int32_t* npos, int32_t* map, uint32_t* table, int32_t* diags, uint64_t* pool,
@@ -245,6 +252,7 @@ struct gmapdp_ctx {
   DevBuf gprobs, gorder, sprob, gresults;
   DevBuf cprobs, corder, cresults, cscratch;  // Dynprog_cdna_gap batches
   DevBuf oprobs, oresults, oscratch, onpos, omap, otable, odiag;  // stage-2 seeding batches
+  DevBuf s2probs, s2results, s2scratch, s2counters, s2paths, s2pairs, s2qseq;  // Stage2_compute batches
   std::string err;
 };
 
@@ -1879,3 +1887,130 @@ int gmapdp_oligo_mappings_batch(gmapdp_ctx* ctx, const gmapdp_oligo_problem* pro
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Stage2_compute: seeding (oi_kernel + oi_map_kernel) then chaining (s2c_kernel)
+// on the device; one synchronous batch.
+// ---------------------------------------------------------------------------
+extern "C" int gmapdp_stage2_batch(gmapdp_ctx* ctx, const gmapdp_stage2_problem* problems, int n, const char* qseq,
+                                   const char* qseq_uc, size_t qbytes, gmapdp_stage2_result* results,
+                                   gmapdp_path* paths, size_t path_cap, gmapdp_path_pair* pairs, size_t pair_cap,
+                                   size_t* paths_needed, size_t* pairs_needed) {
+  if (!ctx || n < 0 || (n > 0 && (!problems || !results || !qseq || !qseq_uc))) return GMAPDP_EINVAL;
+  if (paths_needed) *paths_needed = 0;
+  if (pairs_needed) *pairs_needed = 0;
+  if (!ctx->d_genome) return GMAPDP_ENOGENOME;
+  if (n == 0) return GMAPDP_OK;
+  (void)hipSetDevice(ctx->device);
+  std::vector<gmapdp_oligo_problem> op(n);
+  std::vector<DevStage2Problem> dp(n);
+  for (int i = 0; i < n; i++) {
+    const gmapdp_stage2_problem& p = problems[i];
+    if (p.maxintronlen < 0) return bad(ctx, "stage 2: negative maxintronlen");
+    op[i].qoff = p.qoff;
+    op[i].querylength = p.querylength;
+    op[i].chrstart = p.chrstart;
+    op[i].chrend = p.chrend;
+    op[i].chroffset = p.chroffset;
+    op[i].chrhigh = p.chrhigh;
+    op[i].plusp = p.plusp ? 1 : 0;
+    op[i].minor = 0;  // Stage2_compute takes oligoindices_major (gmap.c:1211)
+    DevStage2Problem& d = dp[i];
+    d.qoff = p.qoff;
+    d.querylength = p.querylength;
+    d.chrstart = p.chrstart;
+    d.chrend = p.chrend;
+    d.chroffset = p.chroffset;
+    d.chrhigh = p.chrhigh;
+    d.plusp = p.plusp ? 1 : 0;
+    d.splicingp = p.splicingp ? 1 : 0;
+    d.maxintronlen = (uint32_t)p.maxintronlen;
+    d.index = i;
+  }
+  gmapdp_oligo_plan* plan = nullptr;
+  int rc = gmapdp_oligo_plan_create(ctx, op.data(), n, qseq_uc, qbytes, &plan);
+  if (rc) return rc;
+  const size_t toff = plan->table_cap, doff = plan->diag_cap;
+  hipStream_t s = ctx->stream;
+  hipError_t e = ctx->oresults.ensure(sizeof(gmapdp_oligo_result) * n);
+  if (e == hipSuccess) e = ctx->onpos.ensure(sizeof(int32_t) * qbytes);
+  if (e == hipSuccess) e = ctx->omap.ensure(sizeof(int32_t) * qbytes);
+  if (e == hipSuccess) e = ctx->otable.ensure(sizeof(uint32_t) * std::max<size_t>(toff, 1));
+  if (e == hipSuccess) e = ctx->odiag.ensure(4 * sizeof(int32_t) * std::max<size_t>(doff, 1));
+  if (e == hipSuccess) e = ctx->qseq_uc.ensure(qbytes);
+  if (e == hipSuccess) e = ctx->s2qseq.ensure(qbytes);
+  if (e == hipSuccess) e = ctx->s2probs.ensure(sizeof(DevStage2Problem) * n);
+  if (e == hipSuccess) e = ctx->s2results.ensure(sizeof(gmapdp_stage2_result) * n);
+  if (e == hipSuccess) e = ctx->s2counters.ensure(4 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemcpyAsync(ctx->qseq_uc.p, qseq_uc, qbytes, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(ctx->s2qseq.p, qseq, qbytes, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(ctx->s2probs.p, dp.data(), sizeof(DevStage2Problem) * n, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemsetAsync(ctx->onpos.p, 0, sizeof(int32_t) * qbytes, s);
+  if (e == hipSuccess) e = hipMemsetAsync(ctx->omap.p, 0xff, sizeof(int32_t) * qbytes, s);
+  if (e != hipSuccess) {
+    oligo_plan_free(plan);
+    return fail(ctx, GMAPDP_ENOMEM, "stage-2 buffers: %s", e);
+  }
+  rc = gmapdp_oligo_plan_run(ctx, plan, (const char*)ctx->qseq_uc.p, (gmapdp_oligo_result*)ctx->oresults.p,
+                             (int32_t*)ctx->onpos.p, (int32_t*)ctx->omap.p, (uint32_t*)ctx->otable.p,
+                             (int32_t*)ctx->odiag.p, nullptr);
+  oligo_plan_free(plan);
+  if (rc) return rc;
+  // the chaining scratch is sized exactly from the seeding (totalpositions, ndiagonals per call)
+  std::vector<gmapdp_oligo_result> ores(n);
+  e = hipMemcpyAsync(ores.data(), ctx->oresults.p, sizeof(gmapdp_oligo_result) * n, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "stage-2 seeding: %s", e);
+  size_t scratch = 0, qsum = 0;
+  for (int i = 0; i < n; i++) {
+    scratch += scratch_bytes_s2c(problems[i].querylength, ores[i].totalpositions, ores[i].ndiagonals);
+    qsum += (size_t)problems[i].querylength;
+  }
+  size_t pcap = 16 + 2 * (size_t)n, qcap = 64 + 2 * qsum;  // first guesses; grown on overflow
+  for (int attempt = 0;; attempt++) {
+    e = ctx->s2scratch.ensure(std::max<size_t>(scratch, 256));
+    if (e == hipSuccess) e = ctx->s2paths.ensure(sizeof(gmapdp_path) * pcap);
+    if (e == hipSuccess) e = ctx->s2pairs.ensure(sizeof(gmapdp_path_pair) * qcap);
+    if (e == hipSuccess) e = hipMemsetAsync(ctx->s2counters.p, 0, 4 * sizeof(unsigned long long), s);
+    if (e == hipSuccess)
+      e = launch_s2c(n, s, (const DevStage2Problem*)ctx->s2probs.p, ctx->d_genome, ctx->genome_words,
+                     (const char*)ctx->s2qseq.p, (const char*)ctx->qseq_uc.p, (const gmapdp_oligo_result*)ctx->oresults.p,
+                     (const int32_t*)ctx->onpos.p, (const int32_t*)ctx->omap.p, (const uint32_t*)ctx->otable.p,
+                     (const int32_t*)ctx->odiag.p, (unsigned char*)ctx->s2scratch.p,
+                     (unsigned long long*)ctx->s2counters.p, (unsigned long long)scratch,
+                     (gmapdp_stage2_result*)ctx->s2results.p, (gmapdp_path*)ctx->s2paths.p, pcap,
+                     (gmapdp_path_pair*)ctx->s2pairs.p, qcap);
+    unsigned long long cnt[4] = {0, 0, 0, 0};
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(results, ctx->s2results.p, sizeof(gmapdp_stage2_result) * n, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(cnt, ctx->s2counters.p, sizeof(cnt), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "stage-2 chaining: %s", e);
+    bool overflow = false;
+    for (int i = 0; i < n; i++) {
+      if (results[i].status == -3) return bad(ctx, "stage 2: chromosome positions past 2^31");
+      overflow |= results[i].status == -2;
+    }
+    if (!overflow) {
+      if (paths_needed) *paths_needed = (size_t)cnt[1];
+      if (pairs_needed) *pairs_needed = (size_t)cnt[2];
+      if (cnt[1] > path_cap || cnt[2] > pair_cap || (cnt[1] && !paths) || (cnt[2] && !pairs)) return GMAPDP_ESPACE;
+      if (cnt[1]) e = hipMemcpyAsync(paths, ctx->s2paths.p, sizeof(gmapdp_path) * cnt[1], hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess && cnt[2])
+        e = hipMemcpyAsync(pairs, ctx->s2pairs.p, sizeof(gmapdp_path_pair) * cnt[2], hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "stage-2 copy-out: %s", e);
+      return GMAPDP_OK;
+    }
+    if (attempt >= 8) return fail(ctx, GMAPDP_ENOMEM, "stage-2 output pools keep overflowing%s", hipSuccess);
+    pcap = std::max<size_t>(2 * pcap, (size_t)cnt[1] + 16);
+    qcap = std::max<size_t>(2 * qcap, (size_t)cnt[2] + 64);
+  }
+}
+
+// Test instrumentation: the chaining scratch of the last gmapdp_stage2_batch (its layout is
+// s2_scratch in s2c_kernel.hip; for a one-problem batch it starts at byte 0).
+extern "C" int gmapdp_debug_stage2_scratch(gmapdp_ctx* ctx, void* out, size_t bytes) {
+  if (!ctx || !out || bytes > ctx->s2scratch.cap) return GMAPDP_EINVAL;
+  return hipMemcpy(out, ctx->s2scratch.p, bytes, hipMemcpyDeviceToHost) == hipSuccess ? GMAPDP_OK : GMAPDP_ELAUNCH;
+}

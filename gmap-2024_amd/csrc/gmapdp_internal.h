@@ -150,4 +150,16 @@ struct DevOligoProblem {
   int64_t scratch_offset; // byte offset of the problem's region of the global scratch
 };
 
+// Stage2_compute descriptor (stage2.c:6325): the seeding problem's results slot plus the chaining
+// parameters (Stage2_setup)
+struct DevStage2Problem {
+  int32_t qoff;           // arena index of queryseq_ptr[0] / queryuc_ptr[0]
+  int32_t querylength;
+  uint32_t chrstart, chrend, chroffset, chrhigh;
+  int32_t plusp;
+  int32_t splicingp;
+  uint32_t maxintronlen;
+  int32_t index;          // the problem's index in the batch (seeding result and stage-2 result slot)
+};
+
 }  // namespace gmapdp

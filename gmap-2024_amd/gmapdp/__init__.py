@@ -90,6 +90,17 @@ class OligoResult(C.Structure):
                 ("ndiagonals", C.c_int32), ("table_offset", C.c_int64), ("diag_offset", C.c_int64)]
 
 
+class Stage2Problem(C.Structure):
+    _fields_ = [("qoff", C.c_int32), ("querylength", C.c_int32), ("chrstart", C.c_uint32), ("chrend", C.c_uint32),
+                ("chroffset", C.c_uint32), ("chrhigh", C.c_uint32), ("plusp", C.c_int32), ("splicingp", C.c_int32),
+                ("maxintronlen", C.c_int32), ("pad_", C.c_int32)]
+
+
+class Stage2Result(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("nresults", "npaths", "ncovered", "status", "diag_querystart",
+                                          "diag_queryend", "path_offset", "npairs")]
+
+
 def _struct_dtype(S, fmt):
     return np.dtype({"names": [n for n, _ in S._fields_], "formats": fmt,
                      "offsets": [S.__dict__[n].offset for n, _ in S._fields_], "itemsize": C.sizeof(S)})
@@ -101,6 +112,11 @@ CDNA_PROBLEM_DTYPE = _struct_dtype(CdnaProblem, ["<i4"] * 8 + ["<u4", "<u4"] + [
 CDNA_RESULT_DTYPE = _struct_dtype(CdnaResult, ["<i4"] * 8)
 OLIGO_PROBLEM_DTYPE = _struct_dtype(OligoProblem, ["<i4", "<i4", "<u4", "<u4", "<u4", "<u4", "<i4", "<i4"])
 OLIGO_RESULT_DTYPE = _struct_dtype(OligoResult, ["<i4"] * 4 + ["<i8", "<i8"])
+STAGE2_PROBLEM_DTYPE = _struct_dtype(Stage2Problem, ["<i4", "<i4"] + ["<u4"] * 4 + ["<i4"] * 4)
+STAGE2_RESULT_DTYPE = _struct_dtype(Stage2Result, ["<i4"] * 8)
+PATH_DTYPE = np.dtype([("pair_offset", "<i8"), ("npairs", "<i4"), ("pad_", "<i4")])
+PATH_PAIR_DTYPE = np.dtype([("querypos", "<i4"), ("genomepos", "<i4"), ("queryjump", "<i4"), ("genomejump", "<i4"),
+                            ("cdna", "S1"), ("comp", "S1"), ("genome", "S1"), ("genomealt", "S1")])
 
 PAIR_DTYPE = np.dtype([("querypos", "<i4"), ("genomepos", "<i4"), ("jump", "<i4"), ("cdna", "S1"),
                        ("comp", "S1"), ("genome", "S1"), ("genomealt", "S1")])
@@ -132,6 +148,10 @@ def load_library(path=LIB_PATH):
         "gmapdp_create": (C.c_int, [P(C.c_void_p), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
         "gmapdp_destroy": (None, [C.c_void_p]),
         "gmapdp_genome_words": (C.c_size_t, [C.c_uint64]),
+        "gmapdp_debug_stage2_scratch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+        "gmapdp_stage2_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_char_p, C.c_char_p, C.c_size_t,
+                                          C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                          C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
         "gmapdp_pack_genome": (C.c_int, [C.c_char_p, C.c_uint64, C.c_void_p]),
         "gmapdp_set_genome": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint64]),
         "gmapdp_single_gap_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t,
@@ -505,6 +525,64 @@ class Engine:
             dg = [tuple(int(x) for x in diags[4 * (d0 + k):4 * (d0 + k) + 4]) for k in range(nd)]
             out.append(((int(r["totalpositions"]), int(r["maxnconsecutive"]), int(r["oned_matrix_p"]), nd),
                         np_, plist, dg))
+        return out
+
+    # -- batched Stage2_compute (seeding + chaining) -----------------------------------------------
+    @staticmethod
+    def build_stage2_batch(calls):
+        """calls: dicts (q, quc, chrstart, chrend, chroffset, chrhigh, plusp, splicingp, maxintronlen)
+        -> (problems, qbuf, qucbuf)."""
+        calls = list(calls)
+        probs = np.zeros(len(calls), dtype=STAGE2_PROBLEM_DTYPE)
+        qs, qus, off = [], [], 0
+        for i, p in enumerate(calls):
+            probs[i]["qoff"] = off
+            probs[i]["querylength"] = len(p["quc"])
+            for k in ("chrstart", "chrend", "chroffset", "chrhigh", "plusp"):
+                probs[i][k] = int(p.get(k, 0))
+            probs[i]["splicingp"] = int(p.get("splicingp", 1))
+            probs[i]["maxintronlen"] = int(p.get("maxintronlen", 500000))
+            qs.append(p.get("q", p["quc"]))
+            qus.append(p["quc"])
+            off += len(p["quc"])
+        return probs, (b"".join(qs) or b"\0"), (b"".join(qus) or b"\0")
+
+    def stage2_batch_raw(self, probs, qbuf, qucbuf):
+        n = len(probs)
+        results = np.zeros(n, dtype=STAGE2_RESULT_DTYPE)
+        pcap, qcap = 4 * n + 16, 2 * len(qucbuf) + 64
+        while True:
+            paths = np.zeros(pcap, dtype=PATH_DTYPE)
+            pairs = np.zeros(qcap, dtype=PATH_PAIR_DTYPE)
+            pn, qn = C.c_size_t(), C.c_size_t()
+            rc = self.lib.gmapdp_stage2_batch(self.h, probs.ctypes.data, n, qbuf, qucbuf, len(qucbuf),
+                                              results.ctypes.data, paths.ctypes.data, pcap, pairs.ctypes.data,
+                                              qcap, C.byref(pn), C.byref(qn))
+            if rc == -6:  # GMAPDP_ESPACE
+                pcap, qcap = max(pcap, pn.value), max(qcap, qn.value)
+                continue
+            self._check(rc, "gmapdp_stage2_batch")
+            return results, paths[:pn.value], pairs[:qn.value]
+
+    def stage2_batch(self, calls):
+        """Per call (number of results, [pair-key list per result]) -- the oracle's format (dpbind)."""
+        calls = list(calls)
+        probs, qbuf, qucbuf = self.build_stage2_batch(calls)
+        results, paths, pairs = self.stage2_batch_raw(probs, qbuf, qucbuf)
+        out = []
+        for r in results:
+            lists = []
+            for k in range(int(r["nresults"])):
+                pr = paths[int(r["path_offset"]) + k]
+                o, m = int(pr["pair_offset"]), int(pr["npairs"])
+                lst = []
+                for x in pairs[o:o + m]:
+                    gap = 1 if x["querypos"] == -1 and x["genomepos"] == -1 else 0
+                    lst.append((int(x["querypos"]), int(x["genomepos"]), int(x["queryjump"]), int(x["genomejump"]), 0,
+                                bytes(x["cdna"]) or b"\0", bytes(x["comp"]) or b"\0", bytes(x["genome"]) or b"\0",
+                                bytes(x["genomealt"]) or b"\0", gap))
+                lists.append(lst)
+            out.append((int(r["nresults"]), lists))
         return out
 
 

@@ -27,6 +27,10 @@
  *   gmapdp_cdna_gap_batch    Dynprog_cdna_gap (dynprog_cdna.c:787)
  *   gmapdp_oligo_mappings_batch  stage-2 seeding: Oligoindex_hr_tally + Oligoindex_get_mappings
  *                            (oligoindex_hr.c:33849/34127) as Stage2_compute calls them (stage2.c:6480-6495)
+ *   gmapdp_stage2_batch      Stage2_compute (stage2.c:6325) as GMAP calls it (gmap.c:1208): the
+ *                            seeding above, then Diag_compute_bounds (diag.c:597),
+ *                            align_compute_lookback (stage2.c:4402), convert_to_nucleotides (:5334)
+ *                            and Stage2_filter_unique (:6013)
  *
  * Semantics: every result is bit-identical to the reference's nosimd build
  * (Dynprog_standard + Dynprog_traceback_std), or with GMAPDP_SIMD to its SIMD builds
@@ -363,6 +367,71 @@ int gmapdp_oligo_plan_run (gmapdp_ctx *ctx, const gmapdp_oligo_plan *plan, const
                            gmapdp_oligo_result *d_results, int32_t *d_npositions, int32_t *d_mappings,
                            uint32_t *d_positions, int32_t *d_diagonals, void *stream);
 void gmapdp_oligo_plan_destroy (gmapdp_oligo_plan *plan);
+
+/* Stage2_compute (stage2.c:6325) as GMAP's update_stage3middle_list calls it (gmap.c:1208-1215):
+ * query_offset 0, genestrand 0, proceed_pctcoverage 0.3, the major oligoindex array (8-mers,
+ * diag_lookback 120, suffnconsecutive 20), localp, skip_repetitive_p, favor_right_p false,
+ * max_nalignments 10; Stage2_setup (gmap.c:6544) without cross-species canonical scoring, without SNPs,
+ * STANDARD mode, sufflookback 60, nsufflookback 5.  queryseq_ptr = qseq + qoff (case as given, the
+ * Pair cdna), queryuc_ptr = qseq_uc + qoff.  Domain as gmapdp_oligo_problem (querylength > 8), and
+ * genomic positions below 2^31 (Pairpool_push drops negative ones; the engine does not model that). */
+typedef struct {
+  int32_t qoff;
+  int32_t querylength;
+  uint32_t chrstart;
+  uint32_t chrend;
+  uint32_t chroffset;
+  uint32_t chrhigh;
+  int32_t plusp;
+  int32_t splicingp;       /* Stage2_setup's splicingp_in (novelsplicingp || knownsplicingp) */
+  int32_t maxintronlen;    /* Stage2_setup's maxintronlen_in */
+  int32_t pad_;
+} gmapdp_stage2_problem;
+
+/* Per call: the returned List_T of Stage2_T, in list order, as nresults path records starting at
+ * paths[path_offset]; each record's pairs are its Stage2_middle list (all_starts / all_ends are NULL
+ * in this build of the reference).  status: 0 no positions, 1 the coverage filter declined
+ * (stage2.c:6526), 2 chained; negative: GMAPDP internal (never returned by gmapdp_stage2_batch). */
+typedef struct {
+  int32_t nresults;
+  int32_t npaths;          /* paths traced before Stage2_filter_unique */
+  int32_t ncovered;        /* Diag_update_coverage's ncovered */
+  int32_t status;
+  int32_t diag_querystart; /* Diag_compute_bounds' query bounds (status 2) */
+  int32_t diag_queryend;
+  int32_t path_offset;
+  int32_t npairs;          /* pair records of all nresults paths */
+} gmapdp_stage2_result;
+
+typedef struct {
+  int64_t pair_offset;     /* first record in the pair arena */
+  int32_t npairs;
+  int32_t pad_;
+} gmapdp_path;
+
+/* One Pair_T of a stage-2 path (convert_to_nucleotides): querypos, genomepos, cdna, comp ('|'),
+ * genome, genomealt; a gap holder (Pairpool_push_gapholder) has querypos = genomepos = -1, its
+ * queryjump / genomejump, and blanks; ordinary pairs carry queryjump = genomejump = 0. */
+typedef struct {
+  int32_t querypos;
+  int32_t genomepos;
+  int32_t queryjump;
+  int32_t genomejump;
+  char cdna;
+  char comp;
+  char genome;
+  char genomealt;
+} gmapdp_path_pair;
+
+#define GMAPDP_ESPACE (-6)  /* an output arena is too small: *_needed say how large it must be */
+
+/* n Stage2_compute calls.  results: n entries.  paths / pairs: caller arenas of path_cap / pair_cap
+ * records; on GMAPDP_ESPACE nothing else is valid and *paths_needed / *pairs_needed hold the sizes the
+ * call needs (call again with larger arenas).  On success they hold the records used. */
+int gmapdp_stage2_batch (gmapdp_ctx *ctx, const gmapdp_stage2_problem *problems, int n, const char *qseq,
+                         const char *qseq_uc, size_t qbytes, gmapdp_stage2_result *results, gmapdp_path *paths,
+                         size_t path_cap, gmapdp_path_pair *pairs, size_t pair_cap, size_t *paths_needed,
+                         size_t *pairs_needed);
 
 /* Create a context on HIP device `device`.  mode = Mode_T (mode.h:5;
  * 0 = STANDARD).  user_* mirror Dynprog_single_setup. */

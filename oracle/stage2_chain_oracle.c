@@ -614,6 +614,16 @@ overlap_p (const OPath *x, const OPath *y) {
   return fraction > 0.5;
 }
 
+/* Test instrumentation: when set, the next orc_stage2_compute writes its minactive, maxactive
+   (querylength each) and per hit {map, consec, root, fpos, fhit, tracei, score, active} (8 ints, hits
+   in querypos order) here. */
+static int *S_debug = NULL;
+int
+orc_stage2_debug (int *buf) {
+  S_debug = buf;
+  return 0;
+}
+
 int
 orc_stage2_compute (const char *queryseq, const char *queryuc, int querylength, unsigned int chrstart,
                     unsigned int chrend, unsigned int chroffset, unsigned int chrhigh, int plusp, int splicingp,
@@ -800,6 +810,18 @@ orc_stage2_compute (const char *queryseq, const char *queryuc, int querylength, 
     revise_active(C, q, low, high);
     if (npos[q] > 0) proc[np++] = q;
     q = next_q;
+  }
+
+  if (S_debug) {
+    int *d = S_debug;
+    memcpy(d, minactive, (size_t) querylength * 4);
+    memcpy(d + querylength, maxactive, (size_t) querylength * 4);
+    d += 2 * querylength;
+    for (i = 0; i < npositions_total; i++, d += 8) {
+      d[0] = (int) positions[i]; d[1] = C->consec[i]; d[2] = C->root[i]; d[3] = C->fpos[i]; d[4] = C->fhit[i];
+      d[5] = C->tracei[i]; d[6] = C->score[i]; d[7] = C->active[i];
+    }
+    S_debug = NULL;
   }
 
   /* get_cells_fwd (stage2.c:3437) */
