@@ -4,20 +4,22 @@ Workload (configs[2]: "1M synthetic 2-kb cDNA (5 exons, 2 % mismatch) vs GRCh38,
 stage2 + all Dynprog_* paths"), gmap-2024_amd/gmapdp/workload.py:
   * genome: an i.i.d. ACGT genome laid out as GRCh38's 24 primary chromosomes (3.09 Gnt, universal
     coordinates past 2^31), packed in the reference's .genomecomp format and resident in HBM (1.16 GB);
-  * per 2-kb read, the calls GMAP's pipeline makes into the path: one stage-2
-    seeding call (Oligoindex_hr_tally + Oligoindex_get_mappings over the read's gregion) and
-    43.7 Dynprog_single_gap + 7.1 Dynprog_end5_gap + 6.5 Dynprog_end3_gap + 49.4 Dynprog_genome_gap.
-One step = one pass of the engine over every call of --reads reads (stage-2 seeding on its own
+  * per 2-kb read, the calls GMAP's pipeline makes into the path: one Stage2_compute
+    call (gmap.c:1208: Oligoindex_hr_tally + Oligoindex_get_mappings over the read's gregion, then the
+    chaining -- Diag_compute_bounds, align_compute_lookback, convert_to_nucleotides,
+    Stage2_filter_unique) and 43.7 Dynprog_single_gap + 7.1 Dynprog_end5_gap + 6.5 Dynprog_end3_gap +
+    49.4 Dynprog_genome_gap.
+One step = one pass of the engine over every call of --reads reads (Stage2_compute on its own
 stream, the DP launch classes on four more, joined at the end of the step); the batch is generated
 once and replayed, every step recomputes everything.  Inputs (descriptors, query arenas, splice
 probabilities) are resident in HBM before the timed region (the contract's `value`); the host plan
 (bands, launch classes) is made once per batch and its cost is reported as plan_ms.
 
-value = reads whose stage-2 seeding and DP calls were processed per second, whole job (all ranks).
-Stage-2 chaining (align_compute_scores_lookback) and stage 1/3 orchestration are not in the step
-(DESIGN.md §7).  The JSON line also carries the stage-2-only and DP-only step times, the
-roofline of the kernel that takes most of the step, and the reference CPU baseline
-(tools/cpu_baseline.py: the reference's own objects on the host cores, AVX2 and nosimd builds).
+value = reads whose Stage2_compute and DP calls were processed per second, whole job (all ranks).
+Stage 1/3 orchestration stays on the host and is not in the step.  The JSON line also
+carries the stage-2-only and DP-only step times, the roofline of the kernel that takes most of the
+step, and the reference CPU baseline (tools/cpu_baseline.py: the reference's own objects on the
+host cores, AVX2 and nosimd builds).
 """
 import argparse
 import ctypes as C
@@ -66,6 +68,17 @@ def stage2_algorithmic_bytes(op, res):
     return int((32 + ql + 12 * ((w + 31) // 32) + 8 * ql + 32).sum()
                + 4 * int(res["totalpositions"].astype(np.int64).sum())
                + 16 * int(res["ndiagonals"].astype(np.int64).sum()))
+
+
+def chain_algorithmic_bytes(op, s2res):
+    """Stage-2 chaining per call (s2c_kernel): descriptor (40 B) + seeding result (32 B) + npositions
+    and mappings (8 B per query position) + the query twice (cdna and upper case, 2 B per query
+    position) + the result (32 B) + 16-B path records + 20-B pair records of the kept paths.  The
+    mapping positions (4 B each) are read once; totalpositions is not in the stage-2 result, so
+    they are estimated as one per query position."""
+    ql = op["querylength"].astype(np.int64)
+    return int((40 + 32 + 8 * ql + 2 * ql + 4 * ql + 32).sum() + 16 * int(s2res["nresults"].sum())
+               + 20 * int(s2res["npairs"].sum()))
 
 
 def banded_cells(sp, ep, gp):
@@ -182,10 +195,18 @@ def main():
                                           host_res.ctypes.data, host_gres.ctypes.data, C.byref(plan)),
                "gmapdp_plan_create_all")
     t_plan = time.perf_counter() - t0
+    # Stage2_compute per read (gmap.c:1208): seeding + chaining, GMAP's defaults (splicing on,
+    # maxintronlen 500000)
+    s2p = np.zeros(len(op), dtype=gmapdp.STAGE2_PROBLEM_DTYPE)
+    for k in ("qoff", "querylength", "chrstart", "chrend", "chroffset", "chrhigh", "plusp"):
+        s2p[k] = op[k]
+    s2p["splicingp"] = 1
+    s2p["maxintronlen"] = 500000
     t0 = time.perf_counter()
     oplan = C.c_void_p()
-    eng._check(lib.gmapdp_oligo_plan_create(eng.h, op.ctypes.data, len(op), data["oq"].ctypes.data, len(data["oq"]),
-                                            C.byref(oplan)), "gmapdp_oligo_plan_create")
+    eng._check(lib.gmapdp_stage2_plan_create(eng.h, s2p.ctypes.data, len(s2p), data["oq"].ctypes.data,
+                                             data["oq"].ctypes.data, len(data["oq"]), C.byref(oplan)),
+               "gmapdp_stage2_plan_create")
     t_oplan = time.perf_counter() - t0
     ngpu, nggpu = lib.gmapdp_plan_gpu_problems(plan), lib.gmapdp_plan_genome_gpu_problems(plan)
     cap = lib.gmapdp_plan_pair_capacity(plan)
@@ -202,14 +223,7 @@ def main():
         info.append((R.value, dl.value, cnt.value, lds.value))
         kinds.append(lib.gmapdp_plan_launch_kind(plan, li))
         lstream.append(lib.gmapdp_plan_launch_stream(plan, li))
-    pcap = lib.gmapdp_oligo_plan_positions_capacity(oplan)
-    dcap = lib.gmapdp_oligo_plan_diagonal_capacity(oplan)
-    d_ores = torch.zeros(len(op) * 32, dtype=torch.uint8, device=dev)
-    d_onpos = torch.empty(len(data["oq"]) * 4, dtype=torch.uint8, device=dev)
-    d_omap = torch.empty(len(data["oq"]) * 4, dtype=torch.uint8, device=dev)
-    d_opos = torch.empty(max(pcap, 1) * 4, dtype=torch.uint8, device=dev)
-    d_odiag = torch.empty(max(dcap, 1) * 16, dtype=torch.uint8, device=dev)
-    nol = lib.gmapdp_oligo_plan_nlaunches(oplan)
+    d_s2res = torch.zeros(len(op) * 32, dtype=torch.uint8, device=dev)
 
     # Streams: stage-2 seeding on its own stream, the DP launch classes on the engine's schedule
     # (0 = main, 1..3 = sides, longest-processing-time first), forked from and joined into main.
@@ -223,11 +237,10 @@ def main():
                                               C.c_void_p(d_res.data_ptr()), C.c_void_p(d_pairs.data_ptr()),
                                               C.c_void_p(s.cuda_stream)), "gmapdp_plan_run_launch")
 
-    def orun(s):
-        eng._check(lib.gmapdp_oligo_plan_run(eng.h, oplan, C.c_void_p(d_oq.data_ptr()), C.c_void_p(d_ores.data_ptr()),
-                                             C.c_void_p(d_onpos.data_ptr()), C.c_void_p(d_omap.data_ptr()),
-                                             C.c_void_p(d_opos.data_ptr()), C.c_void_p(d_odiag.data_ptr()),
-                                             C.c_void_p(s.cuda_stream)), "gmapdp_oligo_plan_run")
+    def orun(s, what):
+        eng._check(lib.gmapdp_stage2_plan_run(eng.h, oplan, C.c_void_p(d_oq.data_ptr()), C.c_void_p(d_oq.data_ptr()),
+                                              C.c_void_p(d_s2res.data_ptr()), what, C.c_void_p(s.cuda_stream)),
+                   "gmapdp_stage2_plan_run")
 
     def step(do_oligo=True, do_dp=True, ev=None):
         fork = torch.cuda.Event()
@@ -237,9 +250,12 @@ def main():
             ostream.wait_event(fork)
             if ev is not None:
                 ev["oligo"][0].record(ostream)
-            orun(ostream)
+            orun(ostream, 1)
             if ev is not None:
                 ev["oligo"][1].record(ostream)
+            orun(ostream, 2)
+            if ev is not None:
+                ev["chain"][1].record(ostream)
         if do_dp:
             for li in range(nl):
                 k = lstream[li]
@@ -263,7 +279,7 @@ def main():
             for _ in range(warmup):
                 step(**kw)
             torch.cuda.synchronize()
-            evs = [{"oligo": mk(), "dp": [mk() for _ in range(nl)]} for _ in range(steps)]
+            evs = [{"oligo": mk(), "chain": mk(), "dp": [mk() for _ in range(nl)]} for _ in range(steps)]
             if world > 1:
                 dist.barrier()
             torch.cuda.synchronize()
@@ -280,10 +296,11 @@ def main():
         dp_ms = [sum(e["dp"][li][0].elapsed_time(e["dp"][li][1]) for e in evs) / steps for li in range(nl)] \
             if kw.get("do_dp", True) else None
         o_ms = sum(e["oligo"][0].elapsed_time(e["oligo"][1]) for e in evs) / steps if kw.get("do_oligo", True) else None
-        return elapsed, dp_ms, o_ms
+        c_ms = sum(e["oligo"][1].elapsed_time(e["chain"][1]) for e in evs) / steps if kw.get("do_oligo", True) else None
+        return elapsed, dp_ms, (o_ms, c_ms)
 
     # ---- headline: stage-2 seeding + every Dynprog_* call of the batch ----
-    elapsed, launch_ms, oligo_ms = timed(args.steps, args.warmup)
+    elapsed, launch_ms, (oligo_ms, chain_ms) = timed(args.steps, args.warmup)
     # split of the same step (fewer steps): each half alone
     half = max(2, args.steps // 4)
     el_dp, _, _ = timed(half, 1, do_oligo=False)
@@ -292,7 +309,10 @@ def main():
     # ---- outputs: spot check, per-dispatch algorithmic bytes ----
     res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=gmapdp.RESULT_DTYPE)[:ngpu]
     gres = np.frombuffer(d_gres.cpu().numpy().tobytes(), dtype=gmapdp.GENOME_RESULT_DTYPE)[:nggpu]
-    ores = np.frombuffer(d_ores.cpu().numpy().tobytes(), dtype=gmapdp.OLIGO_RESULT_DTYPE)
+    s2res = np.frombuffer(d_s2res.cpu().numpy().tobytes(), dtype=gmapdp.STAGE2_RESULT_DTYPE)
+    pp_, qp_, cp_, sb_ = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_size_t()
+    lib.gmapdp_stage2_plan_outputs(oplan, C.byref(pp_), C.byref(qp_), C.byref(cp_), C.byref(sb_))
+
     dev_index = np.array([lib.gmapdp_plan_dev_index(plan, i) for i in range(nprob)])
     gdev_index = np.array([lib.gmapdp_plan_genome_dev_index(plan, j) for j in range(ng)])
     npairs = np.zeros(nprob, dtype=np.int64)
@@ -313,19 +333,21 @@ def main():
             j = m - nprob
             nbytes = genome_algorithmic_bytes(gp[j], gnp[j])
         disp.append((name, nbytes, launch_ms[li], info[li][2]))
-    obytes = stage2_algorithmic_bytes(op, ores)
-    disp.append(("gmapdp::oi_kernel<unsigned short>+gmapdp::oi_map_kernel", obytes, oligo_ms, len(op)))
+    disp.append(("gmapdp::oi_kernel<unsigned short>+gmapdp::oi_map_kernel", None, oligo_ms, len(op)))
+    cbytes = chain_algorithmic_bytes(op, s2res)
+    disp.append(("gmapdp::s2c_kernel", cbytes, chain_ms, len(op)))
     # the kernel template with the most time per step
     tot = {}
-    for name, _, ms, _ in disp:
-        tot[name] = tot.get(name, 0.0) + ms
+    for name, nb, ms, _ in disp:
+        if nb is not None:
+            tot[name] = tot.get(name, 0.0) + ms
     dominant = max(tot, key=tot.get)
     sel = [d for d in disp if d[0] == dominant]
     kms = sum(d[2] for d in sel) / len(sel)
     kbytes = sum(d[1] for d in sel) / len(sel)
     ach = kbytes / (kms * 1e-3) / 1e9
     traffic, tsrc = pmc_traffic(dominant)
-    step_bytes = sum(d[1] for d in disp)
+    step_bytes = sum(d[1] for d in disp if d[1] is not None)
     cells = banded_cells(sp, ep, gp)
     reads_total = args.reads * world * args.steps
     ms_step = elapsed / args.steps * 1e3
@@ -344,13 +366,13 @@ def main():
         "data": "synthetic",
         "config": {"workload": "configs[2]: synthetic 2-kb cDNA reads (5 exons x 400 nt, 2 %% subs) vs a "
                                "GRCh38-layout i.i.d. genome (24 chromosomes, %d nt, universal coordinates to %d): per "
-                               "read 1 stage-2 seeding call + %.1f Dynprog_single_gap + %.1f Dynprog_end5_gap + "
-                               "%.1f Dynprog_end3_gap + %.1f Dynprog_genome_gap; inputs HBM-resident; stage-2 "
-                               "chaining and host stages 1/3 not in the step"
+                               "read 1 Stage2_compute call (seeding + chaining) + %.1f Dynprog_single_gap + %.1f Dynprog_end5_gap + "
+                               "%.1f Dynprog_end3_gap + %.1f Dynprog_genome_gap; inputs HBM-resident; host "
+                               "stages 1/3 not in the step"
                                % (layout.total, layout.total - 1, W.SINGLE_PER_READ, W.END5_PER_READ,
                                   W.END3_PER_READ, W.GENOME_PER_READ),
                    "genome": args.genome, "reads_per_step_per_gpu": args.reads,
-                   "subproblems_per_step_per_gpu": {"stage2_seeding": len(op), "single": ns, "end": ne, "genome": ng},
+                   "subproblems_per_step_per_gpu": {"stage2_compute": len(op), "single": ns, "end": ne, "genome": ng},
                    "banded_cells_per_step_per_gpu": cells,
                    "parallelism": "dp%d (reads sharded by rank, genome replicated)" % world},
         "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
@@ -359,18 +381,23 @@ def main():
                      "step_algorithmic_gbs": step_bytes / (ms_step * 1e-3) / 1e9,
                      "note": "integer VALU/LDS/latency-bound DP (SURVEY §8d); HBM roofline reported as required"},
         "gcups": cells * world * args.steps / elapsed / 1e9,
-        "step_split_ms": {"stage2_seeding_alone": el_o / half * 1e3, "dynprog_alone": el_dp / half * 1e3,
+        "step_split_ms": {"stage2_alone": el_o / half * 1e3, "dynprog_alone": el_dp / half * 1e3,
                           "together": ms_step},
         "stage2_seeding_launch_ms": oligo_ms,
+        "stage2_chaining_launch_ms": chain_ms,
         "launch_classes": [{"kernel": d[0], "problems": d[3], "ms": round(d[2], 4)} for d in disp],
         "host": {"plan_ms": t_plan * 1e3, "oligo_plan_ms": t_oplan * 1e3, "setup_s": t_gen},
     }
     # spot check of the step's outputs: size-independent invariants (the oracle parity is tests/)
-    assert np.all(res["npairs"] >= 0) and np.all(gres["npairs"] >= 0) and np.all(ores["totalpositions"] >= 0)
+    assert np.all(res["npairs"] >= 0) and np.all(gres["npairs"] >= 0) and np.all(s2res["status"] >= 0)
     out["checks"] = {"pairs_per_read": float((npairs.sum() + gnp.sum()) / args.reads),
-                     "genome_gaps_bridged": int((gnp > 0).sum()), "stage2_diagonals": int(ores["ndiagonals"].sum())}
+                     "genome_gaps_bridged": int((gnp > 0).sum()),
+                     "stage2_chained": int((s2res["status"] == 2).sum()),
+                     "stage2_results": int(s2res["nresults"].sum()),
+                     "stage2_path_pairs_per_read": float(s2res["npairs"].sum() / args.reads),
+                     "stage2_scratch_mb": sb_.value / 1e6}
     lib.gmapdp_plan_destroy(plan)
-    lib.gmapdp_oligo_plan_destroy(oplan)
+    lib.gmapdp_stage2_plan_destroy(oplan)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baselines()
         out["cpu_baseline"] = cb.get("avx2")

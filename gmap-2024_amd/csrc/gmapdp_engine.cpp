@@ -1926,6 +1926,7 @@ extern "C" int gmapdp_stage2_batch(gmapdp_ctx* ctx, const gmapdp_stage2_problem*
     d.splicingp = p.splicingp ? 1 : 0;
     d.maxintronlen = (uint32_t)p.maxintronlen;
     d.index = i;
+    d.scratch_offset = 0;
   }
   gmapdp_oligo_plan* plan = nullptr;
   int rc = gmapdp_oligo_plan_create(ctx, op.data(), n, qseq_uc, qbytes, &plan);
@@ -1963,9 +1964,12 @@ extern "C" int gmapdp_stage2_batch(gmapdp_ctx* ctx, const gmapdp_stage2_problem*
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "stage-2 seeding: %s", e);
   size_t scratch = 0, qsum = 0;
   for (int i = 0; i < n; i++) {
+    dp[i].scratch_offset = (int64_t)scratch;
     scratch += scratch_bytes_s2c(problems[i].querylength, ores[i].totalpositions, ores[i].ndiagonals);
     qsum += (size_t)problems[i].querylength;
   }
+  e = hipMemcpyAsync(ctx->s2probs.p, dp.data(), sizeof(DevStage2Problem) * n, hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "stage-2 descriptors: %s", e);
   size_t pcap = 16 + 2 * (size_t)n, qcap = 64 + 2 * qsum;  // first guesses; grown on overflow
   for (int attempt = 0;; attempt++) {
     e = ctx->s2scratch.ensure(std::max<size_t>(scratch, 256));
@@ -2014,3 +2018,147 @@ extern "C" int gmapdp_debug_stage2_scratch(gmapdp_ctx* ctx, void* out, size_t by
   if (!ctx || !out || bytes > ctx->s2scratch.cap) return GMAPDP_EINVAL;
   return hipMemcpy(out, ctx->s2scratch.p, bytes, hipMemcpyDeviceToHost) == hipSuccess ? GMAPDP_OK : GMAPDP_ELAUNCH;
 }
+
+// ---------------------------------------------------------------------------
+// Stage2_compute, device-resident plan (bench / pipelined callers): the seeding plan plus the chaining
+// kernel's pools, sized once by running the seeding at plan time.
+// ---------------------------------------------------------------------------
+struct gmapdp_stage2_plan {
+  int n = 0;
+  gmapdp_oligo_plan* oplan = nullptr;
+  DevStage2Problem* d_probs = nullptr;
+  gmapdp_oligo_result* d_ores = nullptr;
+  int32_t *d_npos = nullptr, *d_map = nullptr, *d_diag = nullptr;
+  uint32_t* d_table = nullptr;
+  unsigned char* d_scratch = nullptr;
+  unsigned long long* d_counters = nullptr;
+  gmapdp_path* d_paths = nullptr;
+  gmapdp_path_pair* d_pairs = nullptr;
+  size_t qbytes = 0, scratch = 0, path_cap = 0, pair_cap = 0;
+};
+
+static void stage2_plan_free(gmapdp_stage2_plan* p) {
+  if (!p) return;
+  oligo_plan_free(p->oplan);
+  void* bufs[] = {p->d_probs, p->d_ores, p->d_npos, p->d_map, p->d_diag, p->d_table, p->d_scratch, p->d_counters,
+                  p->d_paths, p->d_pairs};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  delete p;
+}
+
+static int stage2_plan_launch(gmapdp_ctx* ctx, const gmapdp_stage2_plan* P, const char* d_qseq, const char* d_qseq_uc,
+                              gmapdp_stage2_result* d_results, hipStream_t s, bool seed, bool chain) {
+  if (seed) {
+    if (hipMemsetAsync(P->d_npos, 0, sizeof(int32_t) * P->qbytes, s) != hipSuccess)
+      return fail(ctx, GMAPDP_ELAUNCH, "stage-2 plan: %s", hipGetLastError());
+    int rc = gmapdp_oligo_plan_run(ctx, P->oplan, d_qseq_uc, P->d_ores, P->d_npos, P->d_map, P->d_table, P->d_diag, s);
+    if (rc) return rc;
+  }
+  if (chain) {
+    if (hipMemsetAsync(P->d_counters, 0, 4 * sizeof(unsigned long long), s) != hipSuccess)
+      return fail(ctx, GMAPDP_ELAUNCH, "stage-2 plan: %s", hipGetLastError());
+    hipError_t e = launch_s2c(P->n, s, P->d_probs, ctx->d_genome, ctx->genome_words, d_qseq, d_qseq_uc, P->d_ores,
+                              P->d_npos, P->d_map, P->d_table, P->d_diag, P->d_scratch, P->d_counters, P->scratch,
+                              d_results, P->d_paths, P->path_cap, P->d_pairs, P->pair_cap);
+    if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "stage-2 chaining launch: %s", e);
+  }
+  return GMAPDP_OK;
+}
+
+extern "C" {
+
+int gmapdp_stage2_plan_create(gmapdp_ctx* ctx, const gmapdp_stage2_problem* problems, int n, const char* qseq,
+                              const char* qseq_uc, size_t qbytes, gmapdp_stage2_plan** plan) {
+  if (!ctx || !plan || n <= 0 || !problems || !qseq || !qseq_uc) return GMAPDP_EINVAL;
+  *plan = nullptr;
+  if (!ctx->d_genome) return GMAPDP_ENOGENOME;
+  (void)hipSetDevice(ctx->device);
+  std::vector<gmapdp_oligo_problem> op(n);
+  std::vector<DevStage2Problem> dp(n);
+  size_t qsum = 0;
+  for (int i = 0; i < n; i++) {
+    const gmapdp_stage2_problem& p = problems[i];
+    if (p.maxintronlen < 0) return bad(ctx, "stage 2: negative maxintronlen");
+    op[i] = gmapdp_oligo_problem{p.qoff, p.querylength, p.chrstart, p.chrend, p.chroffset, p.chrhigh,
+                                 p.plusp ? 1 : 0, 0};
+    dp[i] = DevStage2Problem{p.qoff, p.querylength, p.chrstart, p.chrend, p.chroffset, p.chrhigh, p.plusp ? 1 : 0,
+                             p.splicingp ? 1 : 0, (uint32_t)p.maxintronlen, i, 0};
+    qsum += (size_t)p.querylength;
+  }
+  gmapdp_stage2_plan* P = new gmapdp_stage2_plan();
+  P->n = n;
+  P->qbytes = qbytes;
+  int rc = gmapdp_oligo_plan_create(ctx, op.data(), n, qseq_uc, qbytes, &P->oplan);
+  if (rc) {
+    delete P;
+    return rc;
+  }
+  const size_t toff = P->oplan->table_cap, doff = P->oplan->diag_cap;
+  hipError_t e = hipMalloc(&P->d_probs, sizeof(DevStage2Problem) * n);
+  if (e == hipSuccess) e = hipMalloc(&P->d_ores, sizeof(gmapdp_oligo_result) * n);
+  if (e == hipSuccess) e = hipMalloc(&P->d_npos, sizeof(int32_t) * qbytes);
+  if (e == hipSuccess) e = hipMalloc(&P->d_map, sizeof(int32_t) * qbytes);
+  if (e == hipSuccess) e = hipMalloc(&P->d_table, sizeof(uint32_t) * std::max<size_t>(toff, 1));
+  if (e == hipSuccess) e = hipMalloc(&P->d_diag, 4 * sizeof(int32_t) * std::max<size_t>(doff, 1));
+  if (e == hipSuccess) e = hipMalloc(&P->d_counters, 4 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemcpy(P->d_probs, dp.data(), sizeof(DevStage2Problem) * n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = ctx->qseq_uc.ensure(qbytes);
+  if (e == hipSuccess) e = hipMemcpy(ctx->qseq_uc.p, qseq_uc, qbytes, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    stage2_plan_free(P);
+    return fail(ctx, GMAPDP_ENOMEM, "stage-2 plan: %s", e);
+  }
+  // size the chaining scratch from one seeding run
+  rc = stage2_plan_launch(ctx, P, nullptr, (const char*)ctx->qseq_uc.p, nullptr, ctx->stream, true, false);
+  std::vector<gmapdp_oligo_result> ores(n);
+  if (!rc) {
+    e = hipMemcpyAsync(ores.data(), P->d_ores, sizeof(gmapdp_oligo_result) * n, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) rc = fail(ctx, GMAPDP_ELAUNCH, "stage-2 plan seeding: %s", e);
+  }
+  if (rc) {
+    stage2_plan_free(P);
+    return rc;
+  }
+  for (int i = 0; i < n; i++) {
+    dp[i].scratch_offset = (int64_t)P->scratch;
+    P->scratch += scratch_bytes_s2c(problems[i].querylength, ores[i].totalpositions, ores[i].ndiagonals);
+  }
+  P->path_cap = 16 + 4 * (size_t)n;
+  P->pair_cap = 64 + 3 * qsum;
+  e = hipMalloc(&P->d_scratch, std::max<size_t>(P->scratch, 256));
+  if (e == hipSuccess) e = hipMemcpy(P->d_probs, dp.data(), sizeof(DevStage2Problem) * n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc(&P->d_paths, sizeof(gmapdp_path) * P->path_cap);
+  if (e == hipSuccess) e = hipMalloc(&P->d_pairs, sizeof(gmapdp_path_pair) * P->pair_cap);
+  if (e != hipSuccess) {
+    stage2_plan_free(P);
+    return fail(ctx, GMAPDP_ENOMEM, "stage-2 plan pools: %s", e);
+  }
+  *plan = P;
+  return GMAPDP_OK;
+}
+
+// what: 1 seeding, 2 chaining, 3 both.  d_results: n gmapdp_stage2_result (problem order).  Outputs stay in
+// the plan's pools (gmapdp_stage2_plan_outputs); a result with status -2 overflowed them.
+int gmapdp_stage2_plan_run(gmapdp_ctx* ctx, const gmapdp_stage2_plan* plan, const char* d_qseq, const char* d_qseq_uc,
+                           gmapdp_stage2_result* d_results, int what, void* stream) {
+  if (!ctx || !plan || !d_qseq || !d_qseq_uc || !d_results) return GMAPDP_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  return stage2_plan_launch(ctx, plan, d_qseq, d_qseq_uc, d_results, stream ? (hipStream_t)stream : ctx->stream,
+                            (what & 1) != 0, (what & 2) != 0);
+}
+
+int gmapdp_stage2_plan_outputs(const gmapdp_stage2_plan* plan, gmapdp_path** d_paths, gmapdp_path_pair** d_pairs,
+                               unsigned long long** d_counters, size_t* scratch_bytes) {
+  if (!plan) return GMAPDP_EINVAL;
+  if (d_paths) *d_paths = plan->d_paths;
+  if (d_pairs) *d_pairs = plan->d_pairs;
+  if (d_counters) *d_counters = plan->d_counters;
+  if (scratch_bytes) *scratch_bytes = plan->scratch;
+  return GMAPDP_OK;
+}
+
+void gmapdp_stage2_plan_destroy(gmapdp_stage2_plan* plan) { stage2_plan_free(plan); }
+
+}  // extern "C"

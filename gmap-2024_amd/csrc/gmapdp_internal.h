@@ -160,6 +160,7 @@ struct DevStage2Problem {
   int32_t splicingp;
   uint32_t maxintronlen;
   int32_t index;          // the problem's index in the batch (seeding result and stage-2 result slot)
+  int64_t scratch_offset; // byte offset of the problem's chaining scratch (s2_scratch, sized from the seeding)
 };
 
 }  // namespace gmapdp

@@ -28,6 +28,7 @@
 // pools (one atomic per problem); a problem that does not fit reports kS2Overflow and the host reruns
 // the batch with larger pools.
 #include "dp_device.h"
+#include <climits>
 
 namespace gmapdp {
 
@@ -45,6 +46,29 @@ constexpr int kS2FinalTolerance = 20;   // FINAL_SCORE_TOLERANCE
 constexpr int kS2MaxNalignments = 10;   // gmap.c:142
 constexpr int kS2Sufflookback = 60, kS2Nsufflookback = 5;  // gmap.c:269-270
 constexpr int kS2ExtraBounds = 20;      // diag.c:14
+
+// Phase timing (tools/oi_timing.py s2; the GMAPDP_OI_TIMING variant of the library only)
+#ifdef GMAPDP_OI_TIMING
+__device__ unsigned long long g_s2_marks[2][16];
+#define S2_MARK(k)                                                  \
+  do {                                                              \
+    if (threadIdx.x == 0) {                                         \
+      atomicAdd(&g_s2_marks[0][k], (unsigned long long)wall_clock64()); \
+      atomicAdd(&g_s2_marks[1][k], 1ull);                           \
+    }                                                               \
+  } while (0)
+#define S2_COUNT(k, v)                                             \
+  do {                                                              \
+    if (threadIdx.x == 0) atomicAdd(&g_s2_marks[0][k], (unsigned long long)(v)); \
+  } while (0)
+#else
+#define S2_MARK(k) \
+  do {             \
+  } while (0)
+#define S2_COUNT(k, v) \
+  do {                 \
+  } while (0)
+#endif
 
 // result status
 constexpr int kS2NoPositions = 0, kS2Coverage = 1, kS2Chained = 2, kS2Overflow = -2, kS2Domain = -3;
@@ -161,233 +185,521 @@ __device__ __forceinline__ void fill_range(int lane, uint32_t* dst, int a, int b
   for (int q = a + lane; q <= b; q += 64) dst[q] = f(q);
 }
 
-// ---- the sequential sweep (lane 0) ----
 struct S2Best {
   int consec, root, pp, ph, score, tracei;
 };
-struct S2Chain {
-  S2Hit* h;
+
+// ---- align_compute_scores_lookback, wave-uniform ----
+// Every lane runs the sweep's control flow; per-position metadata is prefetched 64 query positions at
+// a time (one coalesced load each, then readlane), the active hits of the most recently processed
+// query positions sit in an LDS ring, and one processed position's ranges 0-4 are evaluated across
+// lanes: the range boundaries are ballots (the active hits ascend in chrpos, so every range
+// condition but range 0's is monotone), the best link of a range is a wave max plus the first lane
+// holding it (the reference's strict '>' keeps the first maximum).  tracei values only ever meet in
+// equality tests (range 0), so a fresh value per improvement event replaces the reference's
+// per-improvement counter without changing any decision.
+constexpr int kS2Ring = 128;
+constexpr int kS2Meta = 64;  // processed entries whose metadata stays in LDS
+struct S2Ring {
+  uint32_t map[kS2Ring];
+  int score[kS2Ring], consec[kS2Ring], tracei[kS2Ring], root[kS2Ring], hit[kS2Ring];
+  int eq[kS2Meta], en[kS2Meta], eoff[kS2Meta], estart[kS2Meta];
+};
+struct S2HV {  // one hit's link state
+  uint32_t map;
+  int score, consec, tracei, root, hit;
+};
+struct S2E {  // a processed query position: its active hits
+  int q, n, start, offq;
+  bool inring;
+};
+struct S2W {
+  S2Hit* hits;
   const int* off;
-  int* first;
-  int tracectr, splicingp;
+  int* actn;       // per query position: number of active hits (firstactive != -1 <=> actn > 0)
+  int* alist;      // active hits of q at alist[off[q] ...] (hit indices, ascending)
+  int *pq, *pn, *poff, *pstart;  // per processed entry: q, active count, off[q], ring start
+  S2Ring* ring;
+  int pushed, tracectr, splicingp, lane;
   uint32_t maxintronlen;
-  __device__ __forceinline__ S2Hit& at(int q, int hit) const { return h[off[q] + hit]; }
 };
 
-__device__ void s2_finish(S2Chain& C, int q, int hit, const S2Best& b) {
-  S2Hit& x = C.at(q, hit);
-  x.consec = b.consec;
-  x.root = b.root;
-  x.fpos = b.pp;
-  x.fhit = b.ph;
-  if (b.pp >= 0) {
-    x.tracei = b.tracei;
-    x.score = b.score;
-  } else {  // localp
-    x.tracei = ++C.tracectr;
-    x.score = kS2K;
-  }
+__device__ __forceinline__ S2HV s2_bcast(const S2HV& v, int j) {
+  S2HV u;
+  u.map = (uint32_t)__builtin_amdgcn_readlane((int)v.map, j);
+  u.score = __builtin_amdgcn_readlane(v.score, j);
+  u.consec = __builtin_amdgcn_readlane(v.consec, j);
+  u.tracei = __builtin_amdgcn_readlane(v.tracei, j);
+  u.root = __builtin_amdgcn_readlane(v.root, j);
+  u.hit = __builtin_amdgcn_readlane(v.hit, j);
+  return u;
 }
 
-// ranges 0-4 against processed query position pq from active hit ph; returns the range-1 frontier
-__device__ int s2_ranges(S2Chain& C, S2Best& b, int q, uint32_t position, int pq, int ph, int& last_tr,
-                         bool range1) {
-  const int qd = q - pq, credit = -qd / kS2K;
-  const S2Hit* H = C.h + C.off[pq];
-  while (ph != -1 && H[ph].tracei == last_tr) ph = H[ph].active;
-  if (ph != -1) last_tr = H[ph].tracei;
-  if (range1)
-    while (ph != -1 && H[ph].map + C.maxintronlen + (uint32_t)qd <= position) ph = H[ph].active;
-  const int frontier = ph;
-  while (ph != -1) {
-    const uint32_t pp = H[ph].map;
-    if (!(pp + (uint32_t)kS2EqualNotSplicing + (uint32_t)qd < position)) break;
-    const int diff = (int)(position - pp) - qd;
-    const int fs = H[ph].score + credit - (C.splicingp ? (diff / kS2TenThousand + 1) : (diff + 1));
-    if (fs > b.score) {
-      b.consec = (diff <= 0) ? H[ph].consec + qd : 0;
-      b.root = H[ph].root;
-      b.score = fs;
-      b.pp = pq;
-      b.ph = ph;
-      b.tracei = ++C.tracectr;
-    }
-    ph = H[ph].active;
+__device__ __forceinline__ S2HV s2_load(const S2W& W, const S2E& e, int k) {
+  S2HV v;
+  if (e.inring) {
+    const int s = (e.start + k) & (kS2Ring - 1);
+    v.map = W.ring->map[s];
+    v.score = W.ring->score[s];
+    v.consec = W.ring->consec[s];
+    v.tracei = W.ring->tracei[s];
+    v.root = W.ring->root[s];
+    v.hit = W.ring->hit[s];
+  } else {  // (callers fence before reading entries outside the ring)
+    const int h = W.alist[e.offq + k];
+    const S2Hit& x = W.hits[e.offq + h];
+    v.map = x.map;
+    v.score = x.score;
+    v.consec = x.consec;
+    v.tracei = x.tracei;
+    v.root = x.root;
+    v.hit = h;
   }
-  while (ph != -1) {
-    const uint32_t pp = H[ph].map;
-    if (!(pp + (uint32_t)kS2K <= position)) break;
-    const int g = (int)(position - pp);
-    const int diff = g > qd ? g - qd : qd - g;
-    const int fs = H[ph].score + 1;
-    if (fs > b.score) {
-      b.consec = (diff <= 0) ? H[ph].consec + qd : 0;
-      b.root = H[ph].root;
-      b.score = fs;
-      b.pp = pq;
-      b.ph = ph;
-      b.tracei = H[ph].tracei;
+  return v;
+}
+
+__device__ __forceinline__ S2E s2_mkentry(const S2W& W, int q, int n, int offq, int start) {
+  S2E e;
+  e.q = q;
+  e.n = n;
+  e.offq = offq;
+  e.start = start;
+  e.inring = n <= kS2Ring && start >= W.pushed - kS2Ring;
+  return e;
+}
+
+// Section A: from active index k_io, the first hit with map + qd >= position (k_io := it, or -1 when
+// the list runs out); true when it sits exactly qd before position (its state in `out`)
+__device__ bool s2_adj(const S2W& W, const S2E& e, int& k_io, int qd, uint32_t position, S2HV& out) {
+  if (k_io < 0) return false;
+  if (e.n == 1 && e.inring) {  // one active hit (the common case): uniform LDS reads, no ballots
+    const int sl = e.start & (kS2Ring - 1);
+    const uint32_t mp = W.ring->map[sl];
+    if (!(mp + (uint32_t)qd >= position)) {
+      k_io = -1;
+      return false;
     }
-    ph = H[ph].active;
+    k_io = 0;
+    if (mp + (uint32_t)qd != position) return false;
+    out.map = mp;
+    out.score = W.ring->score[sl];
+    out.consec = W.ring->consec[sl];
+    out.tracei = W.ring->tracei[sl];
+    out.root = W.ring->root[sl];
+    out.hit = W.ring->hit[sl];
+    return true;
+  }
+  if (!e.inring) wave_sync();
+  for (int c0 = k_io; c0 < e.n; c0 += 64) {
+    const int k = c0 + W.lane;
+    const bool valid = k < e.n;
+    S2HV v = {};
+    if (valid) v = s2_load(W, e, k);
+    const uint64_t m = ballot(valid && v.map + (uint32_t)qd >= position);
+    if (m) {
+      const int j = __ffsll((long long)m) - 1;
+      k_io = c0 + j;
+      const S2HV u = s2_bcast(v, j);
+      if (u.map + (uint32_t)qd == position) {
+        out = u;
+        return true;
+      }
+      return false;
+    }
+  }
+  k_io = -1;
+  return false;
+}
+
+// Ranges 0-4 of score_querypos_lookback_one/_mult against processed entry e from active index start;
+// returns the index where the range-0/1 skipping stopped (the _mult frontier), -1 when the list ran out.
+__device__ int s2_eval(S2W& W, const S2E& e, int start, int q, uint32_t position, int& last_tr, S2Best& b,
+                       bool range1) {
+  const int qd = q - e.q, credit = -qd / kS2K;
+  if (e.n == 1 && e.inring && start == 0) {  // one active hit: the ranges in scalar form
+    const int sl = e.start & (kS2Ring - 1);
+    const int tr = W.ring->tracei[sl];
+    if (tr == last_tr) return -1;  // range 0 (nothing left for the frontier either)
+    last_tr = tr;
+    const uint32_t mp = W.ring->map[sl];
+    if (range1 && mp + W.maxintronlen + (uint32_t)qd <= position) return -1;
+    if (mp + (uint32_t)kS2EqualNotSplicing + (uint32_t)qd < position) {
+      const int diff = (int)(position - mp) - qd;
+      const int fs = W.ring->score[sl] + credit - (W.splicingp ? (diff / kS2TenThousand + 1) : (diff + 1));
+      if (fs > b.score) {
+        b.consec = 0;
+        b.root = W.ring->root[sl];
+        b.score = fs;
+        b.pp = e.q;
+        b.ph = W.ring->hit[sl];
+        b.tracei = ++W.tracectr;
+      }
+    } else if (mp + (uint32_t)kS2K <= position) {
+      const int fs = W.ring->score[sl] + 1;
+      if (fs > b.score) {
+        const int g = (int)(position - mp);
+        const int diff = g > qd ? g - qd : qd - g;
+        b.consec = (diff <= 0) ? W.ring->consec[sl] + qd : 0;
+        b.root = W.ring->root[sl];
+        b.score = fs;
+        b.pp = e.q;
+        b.ph = W.ring->hit[sl];
+        b.tracei = tr;
+      }
+    }
+    return 0;
+  }
+  int state = 0, frontier = -1;  // 0 range 0, 1 range 1, 2 range 2, 4 ranges 3-4, 5 done
+  if (!e.inring) wave_sync();
+  for (int c0 = start; c0 < e.n && state != 5; c0 += 64) {
+    const int k = c0 + W.lane;
+    const bool valid = k < e.n;
+    S2HV v = {};
+    if (valid) v = s2_load(W, e, k);
+    int cs = 0;  // first lane of the current range in this chunk
+    if (state == 0) {
+      const uint64_t m = ballot(valid && v.tracei != last_tr);
+      if (!m) continue;  // every hit of this chunk carries last_tr
+      cs = __ffsll((long long)m) - 1;
+      last_tr = __builtin_amdgcn_readlane(v.tracei, cs);
+      state = range1 ? 1 : 2;
+      if (!range1) frontier = c0 + cs;
+    }
+    if (state == 1) {
+      const uint64_t m = ballot(valid && W.lane >= cs && !(v.map + W.maxintronlen + (uint32_t)qd <= position));
+      if (!m) continue;
+      cs = __ffsll((long long)m) - 1;
+      frontier = c0 + cs;
+      state = 2;
+    }
+    if (state == 2) {
+      const bool in2 = valid && W.lane >= cs && v.map + (uint32_t)kS2EqualNotSplicing + (uint32_t)qd < position;
+      const uint64_t m = ballot(in2);
+      int fs = INT_MIN;
+      if (in2) {
+        const int diff = (int)(position - v.map) - qd;
+        fs = v.score + credit - (W.splicingp ? (diff / kS2TenThousand + 1) : (diff + 1));
+      }
+      const int mx = wave_max_i(fs);
+      if (m && mx > b.score) {
+        const int j = __ffsll((long long)ballot(in2 && fs == mx)) - 1;
+        const S2HV u = s2_bcast(v, j);
+        b.consec = 0;  // diff > EQUAL_DISTANCE_NOT_SPLICING
+        b.root = u.root;
+        b.score = mx;
+        b.pp = e.q;
+        b.ph = u.hit;
+        b.tracei = ++W.tracectr;
+      }
+      const uint64_t rest = ballot(valid && W.lane >= cs) & ~m;
+      if (!rest) continue;  // the chunk ended inside range 2
+      cs = __ffsll((long long)rest) - 1;
+      state = 4;
+    }
+    if (state == 4) {
+      const bool in4 = valid && W.lane >= cs && v.map + (uint32_t)kS2K <= position;
+      const uint64_t m = ballot(in4);
+      const int fs = in4 ? v.score + 1 : INT_MIN;
+      const int mx = wave_max_i(fs);
+      if (m && mx > b.score) {
+        const int j = __ffsll((long long)ballot(in4 && fs == mx)) - 1;
+        const S2HV u = s2_bcast(v, j);
+        const int g = (int)(position - u.map);
+        const int diff = g > qd ? g - qd : qd - g;
+        b.consec = (diff <= 0) ? u.consec + qd : 0;
+        b.root = u.root;
+        b.score = mx;
+        b.pp = e.q;
+        b.ph = u.hit;
+        b.tracei = u.tracei;
+      }
+      if (ballot(valid && W.lane >= cs) & ~m) state = 5;
+    }
   }
   return frontier;
 }
 
-__device__ __forceinline__ bool s2_adjacent(const S2Chain& C, int pq, int& ph, int qd, uint32_t position) {
-  const S2Hit* H = C.h + C.off[pq];
-  uint32_t pp = position;
-  while (ph != -1 && (pp = H[ph].map) + (uint32_t)qd < position) ph = H[ph].active;
-  return pp + (uint32_t)qd == position;
+// the kk-th newest processed entry: LDS for the newest kS2Meta, global (after a full wait) beyond
+struct S2EntryCache {
+  __device__ __forceinline__ S2E get(const S2W& W, int np, int kk) {
+    const int k = np - 1 - kk;
+    if (kk < kS2Meta) {
+      const int s = k & (kS2Meta - 1);
+      return s2_mkentry(W, W.ring->eq[s], W.ring->en[s], W.ring->eoff[s], W.ring->estart[s]);
+    }
+    wave_sync();
+    return s2_mkentry(W, W.pq[k], W.pn[k], W.poff[k], W.pstart[k]);
+  }
+};
+
+// The 64 newest processed entries, one per lane (metadata, and the hit of one-hit entries in the
+// ring), loaded once per lookback so the sequential walk over them reads registers.
+struct S2Pref {
+  int q = 0, n = 0, off = 0, start = 0;
+  S2HV h = {};
+  __device__ __forceinline__ void load(const S2W& W, int np) {
+    const int k = np - 1 - W.lane;
+    if (W.lane < kS2Meta && k >= 0) {
+      const int s = k & (kS2Meta - 1);
+      q = W.ring->eq[s];
+      n = W.ring->en[s];
+      off = W.ring->eoff[s];
+      start = W.ring->estart[s];
+      if (n == 1 && start >= W.pushed - kS2Ring) {
+        const int sl = start & (kS2Ring - 1);
+        h.map = W.ring->map[sl];
+        h.score = W.ring->score[sl];
+        h.consec = W.ring->consec[sl];
+        h.tracei = W.ring->tracei[sl];
+        h.root = W.ring->root[sl];
+        h.hit = W.ring->hit[sl];
+      }
+    }
+  }
+  __device__ __forceinline__ S2E entry(const S2W& W, int kk) const {
+    return s2_mkentry(W, __builtin_amdgcn_readlane(q, kk), __builtin_amdgcn_readlane(n, kk),
+                      __builtin_amdgcn_readlane(off, kk), __builtin_amdgcn_readlane(start, kk));
+  }
+};
+
+// ranges 0-4 against a processed entry with a single active hit u (scalar); the frontier is 0 or -1
+__device__ __forceinline__ int s2_eval1(S2W& W, int eq, const S2HV& u, int q, uint32_t position, int& last_tr,
+                                        S2Best& b, bool range1) {
+  const int qd = q - eq;
+  if (u.tracei == last_tr) return -1;
+  last_tr = u.tracei;
+  if (range1 && u.map + W.maxintronlen + (uint32_t)qd <= position) return -1;
+  if (u.map + (uint32_t)kS2EqualNotSplicing + (uint32_t)qd < position) {
+    const int diff = (int)(position - u.map) - qd;
+    const int fs = u.score + (-qd / kS2K) - (W.splicingp ? (diff / kS2TenThousand + 1) : (diff + 1));
+    if (fs > b.score) {
+      b.consec = 0;
+      b.root = u.root;
+      b.score = fs;
+      b.pp = eq;
+      b.ph = u.hit;
+      b.tracei = ++W.tracectr;
+    }
+  } else if (u.map + (uint32_t)kS2K <= position) {
+    const int fs = u.score + 1;
+    if (fs > b.score) {
+      const int g = (int)(position - u.map);
+      const int diff = g > qd ? g - qd : qd - g;
+      b.consec = (diff <= 0) ? u.consec + qd : 0;
+      b.root = u.root;
+      b.score = fs;
+      b.pp = eq;
+      b.ph = u.hit;
+      b.tracei = u.tracei;
+    }
+  }
+  return 0;
 }
 
-__device__ void s2_one(S2Chain& C, int q, int hit, const int* proc, int np) {
-  const uint32_t position = C.at(q, hit).map;
+// one processed entry of a lookback: prefetched (kk < 64) or fetched
+__device__ __forceinline__ int s2_entry_eval(S2W& W, const S2Pref& pf, S2EntryCache& ec, int np, int kk, int start,
+                                             int q, uint32_t position, int& last_tr, S2Best& b, bool range1,
+                                             int* qd_out) {
+  const S2E e = kk < kS2Meta ? pf.entry(W, kk) : ec.get(W, np, kk);
+  *qd_out = q - e.q;
+  if (e.n <= 0 || start < 0) return -1;
+  if (kk < kS2Meta && e.n == 1 && e.inring && start == 0)
+    return s2_eval1(W, e.q, s2_bcast(pf.h, kk), q, position, last_tr, b, range1);
+  return s2_eval(W, e, start, q, position, last_tr, b, range1);
+}
+
+// score_querypos_lookback_one (stage2.c:1073); returns the link
+__device__ S2Best s2_one(S2W& W, int q, uint32_t position, int np, const S2E& last) {
   S2Best b = {kS2K, (int)position, -1, -1, 0, 0};
   int nlookback = kS2Nsufflookback, lookback = kS2Sufflookback;
   if (np > 0) {
-    const int pq = proc[np - 1], qd = q - pq;
-    int ph = C.first[pq];
-    if (s2_adjacent(C, pq, ph, qd, position)) {
-      const S2Hit& x = C.at(pq, ph);
-      b.consec = x.consec + qd;
-      b.root = x.root;
-      b.score = x.score + qd;
-      b.pp = pq;
-      b.ph = ph;
-      b.tracei = x.tracei;
+    int k = last.n > 0 ? 0 : -1;
+    S2HV u;
+    if (s2_adj(W, last, k, q - last.q, position, u)) {
+      b.consec = u.consec + (q - last.q);
+      b.root = u.root;
+      b.score = u.score + (q - last.q);
+      b.pp = last.q;
+      b.ph = u.hit;
+      b.tracei = u.tracei;
       nlookback = 1;
       lookback = kS2Sufflookback / 2;
     }
   }
   bool donep = false;
   int last_tr = -1;
-  for (int k = np - 1, nseen = 0; k >= 0 && b.consec < kS2EnoughConsec && !donep; k--, nseen++) {
-    const int pq = proc[k], qd = q - pq;
-    if (nseen > nlookback && qd - kS2K > lookback) donep = true;
-    const int ph = C.first[pq];
-    if (ph != -1) s2_ranges(C, b, q, position, pq, ph, last_tr, C.splicingp);
+  if (np > 0 && b.consec < kS2EnoughConsec) {
+    S2Pref pf;
+    pf.load(W, np);
+    S2EntryCache ec;
+    for (int kk = 0; kk < np && b.consec < kS2EnoughConsec && !donep; kk++) {
+      const int eq = kk < kS2Meta ? __builtin_amdgcn_readlane(pf.q, kk) : ec.get(W, np, kk).q;
+      if (kk > nlookback && (q - eq) - kS2K > lookback) donep = true;
+      int qd;
+      (void)s2_entry_eval(W, pf, ec, np, kk, 0, q, position, last_tr, b, W.splicingp != 0, &qd);
+    }
   }
-  s2_finish(C, q, hit, b);
+  if (b.pp < 0) {  // localp
+    b.tracei = ++W.tracectr;
+    b.score = kS2K;
+  }
+  return b;
 }
 
-__device__ void s2_mult(S2Chain& C, int q, int low, int high, const int* proc, int np, int* frontier) {
+__device__ __forceinline__ void s2_store_link(S2W& W, int offq, int hit, const S2Best& b) {
+  if (W.lane == 0) {
+    S2Hit& x = W.hits[offq + hit];
+    x.consec = b.consec;
+    x.root = b.root;
+    x.fpos = b.pp;
+    x.fhit = b.ph;
+    x.tracei = b.tracei;
+    x.score = b.score;
+  }
+}
+
+// score_querypos_lookback_mult (stage2.c:1470) over hits [low, high) of q; links to global
+__device__ void s2_mult(S2W& W, int q, int offq, int low, int high, int np, const S2E& last, int* fr) {
   const int nhits = high - low;
   if (np == 0) {
-    for (int i = 0; i < nhits; i++) {
-      S2Hit& x = C.at(q, low + i);
+    for (int i = W.lane; i < nhits; i += 64) {
+      S2Hit& x = W.hits[offq + low + i];
       x.consec = kS2K;
       x.root = (int)x.map;
       x.fpos = x.fhit = -1;
-      x.tracei = ++C.tracectr;
+      x.tracei = W.tracectr + 1 + i;
       x.score = kS2K;
     }
+    W.tracectr += nhits;
+    wave_sync();
     return;
   }
-  const int adj = proc[np - 1], adq = q - adj;
-  int maxadj = 0, maxnon = 0, overall = 0;
-  for (int n = 0; n < np; n++) {
-    const int qd = q - proc[np - 1 - n];
+  const int adq = q - last.q;
+  int maxadj = 0, maxnon = 0, nfr = 0;
+  S2EntryCache ec;
+  for (int n = 0; n < np && n < 128; n++) {
+    const S2E e = ec.get(W, np, n);
+    const int qd = q - e.q;
+    if (n > kS2Nsufflookback && n > 1 && qd - kS2K > kS2Sufflookback) break;  // later entries only shrink
     if (n <= 1 || qd - kS2K <= kS2Sufflookback / 2) maxadj = n;
     if (n <= kS2Nsufflookback || qd - kS2K <= kS2Sufflookback) maxnon = n;
-    if (n > kS2Nsufflookback && n > 1 && qd - kS2K > kS2Sufflookback) break;  // later entries only shrink
-    frontier[n] = C.first[proc[np - 1 - n]];
+    if (W.lane == 0) fr[n] = e.n > 0 ? 0 : -1;
+    nfr = n + 1;
   }
-  int adjf = C.first[adj];
+  wave_sync();
+  int overall = 0, adjf = last.n > 0 ? 0 : -1;
   for (int i = 0; i < nhits; i++) {
-    const uint32_t position = C.at(q, low + i).map;
-    int ph = adjf;
-    if (s2_adjacent(C, adj, ph, adq, position) && C.at(adj, ph).consec + adq > overall)
-      overall = C.at(adj, ph).consec + adq;
-    adjf = ph;
+    const uint32_t position = W.hits[offq + low + i].map;
+    S2HV u;
+    if (s2_adj(W, last, adjf, adq, position, u) && u.consec + adq > overall) overall = u.consec + adq;
   }
-  adjf = C.first[adj];
+  adjf = last.n > 0 ? 0 : -1;
   for (int i = 0; i < nhits; i++) {
-    const uint32_t position = C.at(q, low + i).map;
-    int ph = adjf;
+    const uint32_t position = W.hits[offq + low + i].map;
     S2Best b;
     int maxseen;
-    if (s2_adjacent(C, adj, ph, adq, position)) {
-      const S2Hit& x = C.at(adj, ph);
-      b.consec = x.consec + adq;
-      b.root = x.root;
-      b.pp = adj;
-      b.ph = ph;
-      b.score = x.score + adq;
-      b.tracei = x.tracei;
+    S2HV u;
+    if (s2_adj(W, last, adjf, adq, position, u)) {
+      b = {u.consec + adq, u.root, last.q, u.hit, u.score + adq, u.tracei};
       maxseen = maxadj;
     } else {
-      b.consec = kS2K;
-      b.root = (int)position;
-      b.pp = b.ph = -1;
-      b.score = 0;
-      b.tracei = -1;
+      b = {kS2K, (int)position, -1, -1, 0, -1};
       maxseen = maxnon;
     }
-    adjf = ph;
     if (overall < kS2GreedyConsec) {
       int last_tr = -1;
-      for (int k = np - 1, nseen = 0; k >= 0 && b.consec < kS2EnoughConsec && nseen <= maxseen; k--, nseen++) {
-        const int ph0 = frontier[nseen];
-        if (ph0 != -1) frontier[nseen] = s2_ranges(C, b, q, position, proc[k], ph0, last_tr, true);
+      for (int kk = 0; kk < np && b.consec < kS2EnoughConsec && kk <= maxseen && kk < nfr; kk++) {
+        const int f = fr[kk];
+        if (f != -1) {
+          const S2E e = ec.get(W, np, kk);
+          const int nf = s2_eval(W, e, f, q, position, last_tr, b, true);
+          wave_sync();
+          if (W.lane == 0) fr[kk] = nf;
+          wave_sync();
+        }
       }
     }
-    s2_finish(C, q, low + i, b);
-  }
-}
-
-__device__ void s2_revise_active(S2Chain& C, int q, int low, int high) {
-  if (low >= high) {
-    C.first[q] = -1;
-    return;
-  }
-  S2Hit* H = C.h + C.off[q];
-  int best = H[low].score;
-  for (int hit = low + 1; hit < high; hit++) best = max(best, H[hit].score);
-  const int threshold = max(best - kS2ScoreRestrict, 0);
-  int* ptr = &C.first[q];
-  int hit = low;
-  *ptr = -1;
-  while (hit < high) {
-    while (hit < high && H[hit].score <= threshold) hit++;
-    *ptr = hit;
-    if (hit < high) {
-      ptr = &H[hit].active;
-      hit++;
+    if (b.pp < 0) {
+      b.tracei = ++W.tracectr;
+      b.score = kS2K;
     }
+    s2_store_link(W, offq, low + i, b);
   }
-  *ptr = -1;
+  wave_sync();
 }
 
-// align_compute_scores_lookback's sweep (stage2.c:3746-4080), lane 0
-__device__ void s2_sweep(S2Chain& C, const int32_t* npq, int nq, const uint32_t* minact, const uint32_t* maxact,
-                         int qstart, int qend, int* proc, int* frontier) {
+// the sweep (stage2.c:3746-4080)
+__device__ void s2_sweep(S2W& W, const int32_t* npq, int nq, const uint32_t* minact, const uint32_t* maxact,
+                         int qstart, int qend, int* fr) {
+  const int lane = W.lane;
   auto npos = [&](int q) { return q < nq ? npq[q] : 0; };
-  int q, np = 0;
-  for (q = 0; q < qstart; q++) C.first[q] = -1;
-  while (q <= qend && npos(q) <= 0) C.first[q++] = -1;
-  if (q <= qend) {
-    const int n = npos(q);
-    for (int hit = 0; hit < n; hit++) {
-      S2Hit& x = C.at(q, hit);
+  int q = 0, np = 0;
+  for (int i = lane; i < qstart; i += 64) W.actn[i] = 0;
+  q = qstart;
+  while (q <= qend && npos(q) <= 0) {
+    if (lane == 0) W.actn[q] = 0;
+    q++;
+  }
+  if (q <= qend) {  // the first position with hits: every hit starts a path
+    const int n = npos(q), offq = W.off[q];
+    for (int i = lane; i < n; i += 64) {
+      S2Hit& x = W.hits[offq + i];
       x.fpos = x.fhit = -1;
       x.consec = kS2K;
       x.tracei = -1;
       x.score = kS2K;
     }
-    s2_revise_active(C, q, 0, n);
   }
+  wave_sync();
   int grand_score = 0, grand_q = -1, grand_hit = -1, nskipped = 0, min_hits = 1000000, specific_q = -1,
       specific_low = 0, specific_high = 0;
+  uint32_t grand_map = 0;
+  S2E last = {0, 0, 0, 0, false};
+  // per-position metadata for the chunk [cb, cb + 64): npositions, off, minactive, maxactive, first map
+  int cb = -1, m_n = 0, m_off = 0;
+  uint32_t m_min = 0, m_max = 0, m_map0 = 0;
+#ifdef GMAPDP_OI_TIMING
+  unsigned long long t_one = 0, t_mult = 0, t_tail = 0, t_meta = 0, t0c = 0;
+#define S2_T0() t0c = wall_clock64()
+#define S2_TACC(acc) (acc += wall_clock64() - t0c, t0c = wall_clock64())
+#else
+#define S2_T0() (void)0
+#define S2_TACC(acc) (void)0
+#endif
   while (q <= qend) {
-    const S2Hit* H = C.h + C.off[q];
-    const int nq0 = npos(q);
-    int hit = 0;
-    while (hit < nq0 && H[hit].map < minact[q]) hit++;
-    int low = hit;
-    while (hit < nq0 && H[hit].map <= maxact[q]) hit++;
-    int high = hit;
+    S2_T0();
+    if ((q & ~63) != cb) {
+      cb = q & ~63;
+      const int qq = cb + lane;
+      m_n = qq < nq ? npq[qq] : 0;
+      m_off = qq <= qend + 1 ? W.off[qq] : 0;
+      m_min = qq <= qend ? minact[qq] : 0u;
+      m_max = qq <= qend ? maxact[qq] : 0u;
+      m_map0 = m_n > 0 ? W.hits[m_off].map : 0u;
+    }
+    const int j = q - cb;
+    const int n = __builtin_amdgcn_readlane(m_n, j);
+    const int offq = __builtin_amdgcn_readlane(m_off, j);
+    const uint32_t mn = (uint32_t)__builtin_amdgcn_readlane((int)m_min, j);
+    const uint32_t mx = (uint32_t)__builtin_amdgcn_readlane((int)m_max, j);
+    int low = 0, high = 0;
+    if (n == 1) {
+      const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)m_map0, j);
+      low = m0 < mn ? 1 : 0;
+      high = (low == 0 && m0 <= mx) ? 1 : low;
+    } else if (n > 1) {
+      int cl = 0, ch = 0;
+      for (int c0 = 0; c0 < n; c0 += 64) {
+        const int i = c0 + lane;
+        const uint32_t mp = i < n ? W.hits[offq + i].map : 0u;
+        cl += __popcll(ballot(i < n && mp < mn));
+        ch += __popcll(ballot(i < n && mp <= mx));
+      }
+      low = cl;
+      high = max(cl, ch);
+    }
     if (high - low >= kS2MaxNactive && nskipped <= kS2MaxSkipped) {
-      C.first[q] = -1;
+      if (lane == 0) W.actn[q] = 0;
       nskipped++;
       if (high - low < min_hits) {
         min_hits = high - low;
@@ -398,60 +710,291 @@ __device__ void s2_sweep(S2Chain& C, const int32_t* npq, int nq, const uint32_t*
       q++;
       continue;
     }
-    int next_q;
+    int next_q, qoff = offq;
     if (nskipped > kS2MaxSkipped) {
       next_q = q;
       q = specific_q;
       low = specific_low;
       high = specific_high;
+      qoff = W.off[q];
     } else {
       next_q = q + 1;
     }
-    if (high - low > 0) {
-      int best_score = 0, best_hit = -1;
-      if (high - low == 1) {
-        s2_one(C, q, low, proc, np);
-        if (C.at(q, low).score > 0) {
-          best_score = C.at(q, low).score;
-          best_hit = low;
-        }
-      } else {
-        s2_mult(C, q, low, high, proc, np, frontier);
-        for (int h = low; h < high; h++)
-          if (C.at(q, h).score > best_score) {
-            best_score = C.at(q, h).score;
-            best_hit = h;
+    S2_TACC(t_meta);
+    int nact = 0;
+    if (high - low == 1) {
+      // one hit in the active range (the common case): everything stays in registers and LDS
+      const uint32_t position = (low == 0 && q == cb + j) ? (uint32_t)__builtin_amdgcn_readlane((int)m_map0, j)
+                                                          : W.hits[qoff + low].map;
+      S2Best b = s2_one(W, q, position, np, last);
+      int best_score = b.score > 0 ? b.score : 0;
+      const bool have_best = b.score > 0;
+      nskipped = 0;
+      min_hits = 1000000;
+      specific_q = -1;
+      if (W.splicingp && have_best && b.ph < 0 && grand_q >= 0 && q >= grand_q + kS2K) {
+        if ((best_score = grand_score - (q - grand_q)) > 0) {
+          if (!(position > grand_map + W.maxintronlen) && position >= grand_map + (uint32_t)kS2K) {
+            b.consec = kS2K;
+            b.pp = grand_q;
+            b.ph = grand_hit;
+            b.tracei = ++W.tracectr;
+            b.score = best_score;
           }
+        }
+      }
+      if (have_best && best_score >= grand_score && b.consec > kS2ExonDefn) {
+        grand_score = best_score;
+        grand_q = q;
+        grand_hit = low;
+        grand_map = position;
+      }
+      s2_store_link(W, qoff, low, b);
+      const int threshold = max(b.score - kS2ScoreRestrict, 0);
+      if (b.score > threshold) {
+        nact = 1;
+        if (lane == 0) {
+          W.alist[qoff] = low;
+          const int sl = W.pushed & (kS2Ring - 1);
+          W.ring->map[sl] = position;
+          W.ring->score[sl] = b.score;
+          W.ring->consec[sl] = b.consec;
+          W.ring->tracei[sl] = b.tracei;
+          W.ring->root[sl] = b.root;
+          W.ring->hit[sl] = low;
+        }
+      }
+    } else if (high - low > 1 && high - low <= 64) {
+      // several hits (<= 64): lane i holds hit low + i and its link
+      const int nh = high - low;
+      const uint32_t cm = lane < nh ? W.hits[qoff + low + lane].map : 0u;
+      S2Best mb = {0, 0, -1, -1, 0, 0};
+      if (np == 0) {
+        if (lane < nh) mb = {kS2K, (int)cm, -1, -1, kS2K, W.tracectr + 1 + lane};
+        W.tracectr += nh;
+      } else {
+        const int adq = q - last.q;
+        S2Pref pf;
+        pf.load(W, np);
+        S2EntryCache ec;
+        int maxadj = 0, maxnon = 0, nfr = 0;
+        for (int n = 0; n < np && n < 128; n++) {
+          const int eq = n < kS2Meta ? __builtin_amdgcn_readlane(pf.q, n) : ec.get(W, np, n).q;
+          const int en = n < kS2Meta ? __builtin_amdgcn_readlane(pf.n, n) : ec.get(W, np, n).n;
+          const int qd = q - eq;
+          if (n > kS2Nsufflookback && n > 1 && qd - kS2K > kS2Sufflookback) break;  // later entries only shrink
+          if (n <= 1 || qd - kS2K <= kS2Sufflookback / 2) maxadj = n;
+          if (n <= kS2Nsufflookback || qd - kS2K <= kS2Sufflookback) maxnon = n;
+          if (lane == 0) fr[n] = en > 0 ? 0 : -1;
+          nfr = n + 1;
+        }
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        int overall = 0, adjf = last.n > 0 ? 0 : -1;
+        for (int i = 0; i < nh; i++) {
+          const uint32_t position = (uint32_t)__builtin_amdgcn_readlane((int)cm, i);
+          S2HV u;
+          if (s2_adj(W, last, adjf, adq, position, u) && u.consec + adq > overall) overall = u.consec + adq;
+        }
+        adjf = last.n > 0 ? 0 : -1;
+        for (int i = 0; i < nh; i++) {
+          const uint32_t position = (uint32_t)__builtin_amdgcn_readlane((int)cm, i);
+          S2Best b;
+          int maxseen;
+          S2HV u;
+          if (s2_adj(W, last, adjf, adq, position, u)) {
+            b = {u.consec + adq, u.root, last.q, u.hit, u.score + adq, u.tracei};
+            maxseen = maxadj;
+          } else {
+            b = {kS2K, (int)position, -1, -1, 0, -1};
+            maxseen = maxnon;
+          }
+          if (overall < kS2GreedyConsec) {
+            int last_tr = -1;
+            for (int kk = 0; kk < np && b.consec < kS2EnoughConsec && kk <= maxseen && kk < nfr; kk++) {
+              const int f = fr[kk];
+              if (f != -1) {
+                int qd;
+                const int nf = s2_entry_eval(W, pf, ec, np, kk, f, q, position, last_tr, b, true, &qd);
+                if (lane == 0) fr[kk] = nf;
+                __atomic_signal_fence(__ATOMIC_SEQ_CST);
+              }
+            }
+          }
+          if (b.pp < 0) {
+            b.tracei = ++W.tracectr;
+            b.score = kS2K;
+          }
+          if (lane == i) mb = b;
+        }
+      }
+      // best of the position: the first hit with the maximal score (> 0)
+      const int sc = lane < nh ? mb.score : INT_MIN;
+      const int smax = wave_max_i(sc);
+      int best_score = 0, best_hit = -1, bl = 0;
+      if (smax > 0) {
+        bl = __ffsll((long long)ballot(lane < nh && sc == smax)) - 1;
+        best_score = smax;
+        best_hit = low + bl;
       }
       nskipped = 0;
       min_hits = 1000000;
       specific_q = -1;
-      if (C.splicingp && best_hit >= 0 && C.at(q, best_hit).fhit < 0 && grand_q >= 0 && q >= grand_q + kS2K) {
-        if ((best_score = C.at(grand_q, grand_hit).score - (q - grand_q)) > 0) {
-          const uint32_t prevposition = C.at(grand_q, grand_hit).map;
-          for (int h = low; h < high; h++) {
-            S2Hit& x = C.at(q, h);
-            if (x.map > prevposition + C.maxintronlen) continue;
-            if (x.map >= prevposition + (uint32_t)kS2K) {
-              x.consec = kS2K;
-              x.fpos = grand_q;
-              x.fhit = grand_hit;
-              x.tracei = ++C.tracectr;
-              x.score = best_score;
-            }
+      if (W.splicingp && best_hit >= 0 && __builtin_amdgcn_readlane(mb.ph, bl) < 0 && grand_q >= 0 &&
+          q >= grand_q + kS2K) {
+        if ((best_score = grand_score - (q - grand_q)) > 0) {
+          if (lane < nh && !(cm > grand_map + W.maxintronlen) && cm >= grand_map + (uint32_t)kS2K) {
+            mb.consec = kS2K;
+            mb.pp = grand_q;
+            mb.ph = grand_hit;
+            mb.tracei = W.tracectr + 1 + lane;  // fresh per relinked hit
+            mb.score = best_score;
           }
+          W.tracectr += nh;
         }
       }
-      if (best_hit >= 0 && best_score >= grand_score && C.at(q, best_hit).consec > kS2ExonDefn) {
+      if (best_hit >= 0 && best_score >= grand_score && __builtin_amdgcn_readlane(mb.consec, bl) > kS2ExonDefn) {
         grand_score = best_score;
         grand_q = q;
         grand_hit = best_hit;
+        grand_map = (uint32_t)__builtin_amdgcn_readlane((int)cm, bl);
+      }
+      if (lane < nh) {
+        S2Hit& x = W.hits[qoff + low + lane];
+        x.consec = mb.consec;
+        x.root = mb.root;
+        x.fpos = mb.pp;
+        x.fhit = mb.ph;
+        x.tracei = mb.tracei;
+        x.score = mb.score;
+      }
+      // revise_active_lookback + the entry's active hits into the ring
+      const int threshold = max(wave_max_i(lane < nh ? mb.score : INT_MIN) - kS2ScoreRestrict, 0);
+      const bool a = lane < nh && mb.score > threshold;
+      const uint64_t am = ballot(a);
+      if (a) {
+        const int r = lanes_below(am, lane);
+        W.alist[qoff + r] = low + lane;
+        const int sl = (W.pushed + r) & (kS2Ring - 1);
+        W.ring->map[sl] = cm;
+        W.ring->score[sl] = mb.score;
+        W.ring->consec[sl] = mb.consec;
+        W.ring->tracei[sl] = mb.tracei;
+        W.ring->root[sl] = mb.root;
+        W.ring->hit[sl] = low + lane;
+      }
+      nact = __popcll(am);
+    } else {
+      int best_score = 0, best_hit = -1, best_fhit = 0, best_consec = 0;
+      if (high - low > 1) {
+        s2_mult(W, q, qoff, low, high, np, last, fr);
+        int bs = 0, bh = -1;
+        for (int c0 = low; c0 < high; c0 += 64) {
+          const int i = c0 + lane;
+          const int sc = i < high ? W.hits[qoff + i].score : INT_MIN;
+          const int m = wave_max_i(sc);
+          if (m > bs) {
+            bs = m;
+            bh = c0 + __ffsll((long long)ballot(i < high && sc == m)) - 1;
+          }
+        }
+        best_score = bs;
+        best_hit = bh;
+        if (bh >= 0) {
+          best_fhit = W.hits[qoff + bh].fhit;
+          best_consec = W.hits[qoff + bh].consec;
+        }
+        nskipped = 0;
+        min_hits = 1000000;
+        specific_q = -1;
+        if (W.splicingp && best_hit >= 0 && best_fhit < 0 && grand_q >= 0 && q >= grand_q + kS2K) {
+          if ((best_score = grand_score - (q - grand_q)) > 0) {  // fwd_scores[grand] is grand_score
+            for (int i = low + lane; i < high; i += 64) {
+              S2Hit& x = W.hits[qoff + i];
+              if (x.map > grand_map + W.maxintronlen) continue;
+              if (x.map >= grand_map + (uint32_t)kS2K) {
+                x.consec = kS2K;
+                x.fpos = grand_q;
+                x.fhit = grand_hit;
+                x.tracei = W.tracectr + 1 + (i - low);  // fresh per relinked hit
+                x.score = best_score;
+              }
+            }
+            W.tracectr += high - low;
+            wave_sync();
+            best_consec = W.hits[qoff + best_hit].consec;
+          }
+        }
+        if (best_hit >= 0 && best_score >= grand_score && best_consec > kS2ExonDefn) {
+          grand_score = best_score;
+          grand_q = q;
+          grand_hit = best_hit;
+          grand_map = W.hits[qoff + best_hit].map;
+        }
+        // revise_active_lookback + the entry's active hits into the ring
+        int best = INT_MIN;
+        for (int c0 = low; c0 < high; c0 += 64) {
+          const int i = c0 + lane;
+          best = max(best, i < high ? W.hits[qoff + i].score : INT_MIN);
+        }
+        const int threshold = max(wave_max_i(best) - kS2ScoreRestrict, 0);
+        for (int c0 = low; c0 < high; c0 += 64) {
+          const int i = c0 + lane;
+          S2Hit x = {};
+          bool a = false;
+          if (i < high) {
+            x = W.hits[qoff + i];
+            a = x.score > threshold;
+          }
+          const uint64_t m = ballot(a);
+          if (a) {
+            const int r = nact + lanes_below(m, lane);
+            W.alist[qoff + r] = i;
+            if (high - low <= kS2Ring) {
+              const int sl = (W.pushed + r) & (kS2Ring - 1);
+              W.ring->map[sl] = x.map;
+              W.ring->score[sl] = x.score;
+              W.ring->consec[sl] = x.consec;
+              W.ring->tracei[sl] = x.tracei;
+              W.ring->root[sl] = x.root;
+              W.ring->hit[sl] = i;
+            }
+          }
+          nact += __popcll(m);
+        }
       }
     }
-    s2_revise_active(C, q, low, high);
-    if (npos(q) > 0) proc[np++] = q;  // q may be the specific position gone back to
+    if (high - low == 1) S2_TACC(t_one); else S2_TACC(t_mult);
+    if (lane == 0) W.actn[q] = nact;
+    if (npos(q) > 0) {
+      const bool ringed = high - low <= kS2Ring;
+      const int start = ringed ? W.pushed : W.pushed - 2 * kS2Ring;  // never in the ring
+      if (lane == 0) {
+        W.pq[np] = q;
+        W.pn[np] = nact;
+        W.poff[np] = qoff;
+        W.pstart[np] = start;
+        const int s = np & (kS2Meta - 1);
+        W.ring->eq[s] = q;
+        W.ring->en[s] = nact;
+        W.ring->eoff[s] = qoff;
+        W.ring->estart[s] = start;
+      }
+      if (ringed) W.pushed += nact;
+      np++;
+      last = s2_mkentry(W, q, nact, qoff, start);
+    }
+    // one wave: its LDS operations execute in order, so the ring writes above are visible to the next
+    // position's reads; only the compiler must not move memory operations across this point.  Global
+    // data written here is read back only after a full wait (wave_sync) on the slow paths.
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_wave_barrier();
+    S2_TACC(t_tail);
     q = next_q;
   }
+  S2_COUNT(8, t_meta);
+  S2_COUNT(9, t_one);
+  S2_COUNT(10, t_mult);
+  S2_COUNT(11, t_tail);
 }
 
 __device__ __forceinline__ char s2_genomic_nt(const uint32_t* __restrict__ blocks, uint64_t nwords, uint32_t chrpos,
@@ -497,7 +1040,7 @@ __device__ __forceinline__ void s2_entry(const int* pathq, const int* pathg, int
   gap = ((gj - fill) > 0 || (qj - fill) > 0) ? 1 : 0;
 }
 
-__global__ __launch_bounds__(64) void s2c_kernel(
+__global__ __launch_bounds__(64) void s2a_kernel(
     const DevStage2Problem* __restrict__ probs, const uint32_t* __restrict__ blocks, uint64_t nwords,
     const char* __restrict__ qseq, const char* __restrict__ quc, const gmapdp_oligo_result* __restrict__ ores,
     const int32_t* __restrict__ npos_all, const int32_t* __restrict__ map_all, const uint32_t* __restrict__ table_all,
@@ -512,28 +1055,8 @@ __global__ __launch_bounds__(64) void s2c_kernel(
   const int T = O.totalpositions, nd = O.ndiagonals;
   const int32_t* npq = npos_all + P.qoff;
   const int32_t* mpq = map_all + P.qoff;
-  gmapdp_stage2_result R;
-  R.nresults = 0;
-  R.npaths = 0;
-  R.ncovered = 0;
-  R.status = kS2NoPositions;
-  R.diag_querystart = R.diag_queryend = 0;
-  R.path_offset = 0;
-  R.npairs = 0;
-
-  // ---- scratch ----
   const S2Scratch so = s2_scratch(ql, T, nd);
-  unsigned long long base = 0;
-  if (lane == 0) base = atomicAdd(&counters[0], (unsigned long long)so.total);
-  base = __shfl(base, 0, 64);
-  if (base + so.total > scratch_cap) {
-    if (lane == 0) {
-      R.status = kS2Overflow;
-      results[P.index] = R;
-    }
-    return;
-  }
-  unsigned char* S = scratch + base;
+  unsigned char* S = scratch + P.scratch_offset;
   int* diff = reinterpret_cast<int*>(S + so.diff);
   double* run = reinterpret_cast<double*>(S + so.run);
   int* off = reinterpret_cast<int*>(S + so.off);
@@ -551,6 +1074,26 @@ __global__ __launch_bounds__(64) void s2c_kernel(
   int* pathq = reinterpret_cast<int*>(S + so.pq);
   int* pathh = reinterpret_cast<int*>(S + so.ph);
   int* sbuf = reinterpret_cast<int*>(S + so.sbuf);
+  (void)sh; (void)diff; (void)run; (void)off; (void)minact; (void)maxact; (void)first; (void)proc; (void)dg;
+  (void)ord; (void)tmp; (void)hits; (void)cand; (void)keep; (void)pth; (void)pathq; (void)pathh; (void)sbuf;
+  (void)npq; (void)mpq; (void)nq; (void)blocks; (void)nwords; (void)qseq; (void)quc; (void)table_all;
+  (void)diag_all; (void)counters; (void)scratch_cap; (void)paths_out; (void)path_cap; (void)pairs_out; (void)pair_cap;
+  gmapdp_stage2_result R;
+  R.nresults = 0;
+  R.npaths = 0;
+  R.ncovered = 0;
+  R.status = kS2NoPositions;
+  R.diag_querystart = R.diag_queryend = 0;
+  R.path_offset = 0;
+  R.npairs = 0;
+  S2_MARK(0);
+  if (P.scratch_offset + (unsigned long long)so.total > scratch_cap) {
+    if (lane == 0) {
+      R.status = kS2Overflow;
+      results[P.index] = R;
+    }
+    return;
+  }
 
   // ---- Diag_update_coverage: depth per query position from a difference array ----
   for (int q = lane; q <= ql; q += 64) diff[q] = 0;
@@ -596,6 +1139,7 @@ __global__ __launch_bounds__(64) void s2c_kernel(
   }
   wave_sync();
 
+  S2_MARK(1);
   // ---- Diag_compute_bounds ----
   const uint32_t chrinit = P.plusp ? P.chrstart : (P.chrhigh - P.chroffset) - P.chrend;
   const uint32_t chrterm = P.plusp ? P.chrend : (P.chrhigh - P.chroffset) - P.chrstart;
@@ -766,6 +1310,7 @@ __global__ __launch_bounds__(64) void s2c_kernel(
   R.diag_querystart = qstart;
   R.diag_queryend = qend;
 
+  S2_MARK(2);
   // ---- per-hit arrays: the hits of query position q at hits[off[q] ...] (Linkmatrix_1d_new) ----
   carry = 0;
   for (int cb = 0; cb < ql; cb += 64) {
@@ -800,19 +1345,120 @@ __global__ __launch_bounds__(64) void s2c_kernel(
   }
   wave_sync();
 
+  if (lane == 0) results[P.index] = R;  // status 2 with the query bounds: the sweep and the paths follow
+}
+
+// the lookback sweep (align_compute_scores_lookback) of the calls s2a_kernel left chained
+__global__ __launch_bounds__(64) void s2b_kernel(
+    const DevStage2Problem* __restrict__ probs, const uint32_t* __restrict__ blocks, uint64_t nwords,
+    const char* __restrict__ qseq, const char* __restrict__ quc, const gmapdp_oligo_result* __restrict__ ores,
+    const int32_t* __restrict__ npos_all, const int32_t* __restrict__ map_all, const uint32_t* __restrict__ table_all,
+    const int32_t* __restrict__ diag_all, unsigned char* __restrict__ scratch, unsigned long long* __restrict__ counters,
+    unsigned long long scratch_cap, gmapdp_stage2_result* __restrict__ results, gmapdp_path* __restrict__ paths_out,
+    unsigned long long path_cap, gmapdp_path_pair* __restrict__ pairs_out, unsigned long long pair_cap) {
+  __shared__ int sh[8];
+  const int lane = threadIdx.x;
+  const DevStage2Problem P = probs[blockIdx.x];
+  const int ql = P.querylength, nq = ql - kS2K + 1;
+  const gmapdp_oligo_result O = ores[P.index];
+  const int T = O.totalpositions, nd = O.ndiagonals;
+  const int32_t* npq = npos_all + P.qoff;
+  const int32_t* mpq = map_all + P.qoff;
+  const S2Scratch so = s2_scratch(ql, T, nd);
+  unsigned char* S = scratch + P.scratch_offset;
+  int* diff = reinterpret_cast<int*>(S + so.diff);
+  double* run = reinterpret_cast<double*>(S + so.run);
+  int* off = reinterpret_cast<int*>(S + so.off);
+  uint32_t* minact = reinterpret_cast<uint32_t*>(S + so.minact);
+  uint32_t* maxact = reinterpret_cast<uint32_t*>(S + so.maxact);
+  int* first = reinterpret_cast<int*>(S + so.first);
+  int* proc = reinterpret_cast<int*>(S + so.proc);
+  S2Diag* dg = reinterpret_cast<S2Diag*>(S + so.diags);
+  int* ord = reinterpret_cast<int*>(S + so.ord);
+  int* tmp = reinterpret_cast<int*>(S + so.tmp);
+  S2Hit* hits = reinterpret_cast<S2Hit*>(S + so.hits);
+  int* cand = reinterpret_cast<int*>(S + so.cand);
+  int* keep = reinterpret_cast<int*>(S + so.keep);
+  S2Path* pth = reinterpret_cast<S2Path*>(S + so.paths);
+  int* pathq = reinterpret_cast<int*>(S + so.pq);
+  int* pathh = reinterpret_cast<int*>(S + so.ph);
+  int* sbuf = reinterpret_cast<int*>(S + so.sbuf);
+  (void)sh; (void)diff; (void)run; (void)off; (void)minact; (void)maxact; (void)first; (void)proc; (void)dg;
+  (void)ord; (void)tmp; (void)hits; (void)cand; (void)keep; (void)pth; (void)pathq; (void)pathh; (void)sbuf;
+  (void)npq; (void)mpq; (void)nq; (void)blocks; (void)nwords; (void)qseq; (void)quc; (void)table_all;
+  (void)diag_all; (void)counters; (void)scratch_cap; (void)paths_out; (void)path_cap; (void)pairs_out; (void)pair_cap;
+  const gmapdp_stage2_result R0 = results[P.index];
+  if (R0.status != kS2Chained) return;
+  const int qstart = R0.diag_querystart, qend = R0.diag_queryend;
+  S2_MARK(3);
   // ---- align_compute_scores_lookback: the sweep on lane 0 ----
-  if (lane == 0) {
-    S2Chain C;
-    C.h = hits;
-    C.off = off;
-    C.first = first;
-    C.tracectr = 0;
-    C.splicingp = P.splicingp;
-    C.maxintronlen = P.maxintronlen;
-    s2_sweep(C, npq, nq, minact, maxact, qstart, qend, proc, pathh /* frontier (<= 70 entries used) */);
+  {
+    __shared__ S2Ring ring;
+    __shared__ int fr[128];
+    S2W W;
+    W.hits = hits;
+    W.off = off;
+    W.actn = first;
+    W.alist = keep;
+    W.pq = proc;
+    W.pn = pathq;
+    W.poff = pathh;
+    W.pstart = reinterpret_cast<int*>(run);
+    W.ring = &ring;
+    W.pushed = 0;
+    W.tracectr = 0;
+    W.splicingp = P.splicingp;
+    W.lane = lane;
+    W.maxintronlen = P.maxintronlen;
+    s2_sweep(W, npq, nq, minact, maxact, qstart, qend, fr);
   }
   wave_sync();
 
+  S2_MARK(4);
+}
+
+// cells, traceback_one, Stage2_filter_unique, convert_to_nucleotides
+__global__ __launch_bounds__(64) void s2c_kernel(
+    const DevStage2Problem* __restrict__ probs, const uint32_t* __restrict__ blocks, uint64_t nwords,
+    const char* __restrict__ qseq, const char* __restrict__ quc, const gmapdp_oligo_result* __restrict__ ores,
+    const int32_t* __restrict__ npos_all, const int32_t* __restrict__ map_all, const uint32_t* __restrict__ table_all,
+    const int32_t* __restrict__ diag_all, unsigned char* __restrict__ scratch, unsigned long long* __restrict__ counters,
+    unsigned long long scratch_cap, gmapdp_stage2_result* __restrict__ results, gmapdp_path* __restrict__ paths_out,
+    unsigned long long path_cap, gmapdp_path_pair* __restrict__ pairs_out, unsigned long long pair_cap) {
+  __shared__ int sh[8];
+  const int lane = threadIdx.x;
+  const DevStage2Problem P = probs[blockIdx.x];
+  const int ql = P.querylength, nq = ql - kS2K + 1;
+  const gmapdp_oligo_result O = ores[P.index];
+  const int T = O.totalpositions, nd = O.ndiagonals;
+  const int32_t* npq = npos_all + P.qoff;
+  const int32_t* mpq = map_all + P.qoff;
+  const S2Scratch so = s2_scratch(ql, T, nd);
+  unsigned char* S = scratch + P.scratch_offset;
+  int* diff = reinterpret_cast<int*>(S + so.diff);
+  double* run = reinterpret_cast<double*>(S + so.run);
+  int* off = reinterpret_cast<int*>(S + so.off);
+  uint32_t* minact = reinterpret_cast<uint32_t*>(S + so.minact);
+  uint32_t* maxact = reinterpret_cast<uint32_t*>(S + so.maxact);
+  int* first = reinterpret_cast<int*>(S + so.first);
+  int* proc = reinterpret_cast<int*>(S + so.proc);
+  S2Diag* dg = reinterpret_cast<S2Diag*>(S + so.diags);
+  int* ord = reinterpret_cast<int*>(S + so.ord);
+  int* tmp = reinterpret_cast<int*>(S + so.tmp);
+  S2Hit* hits = reinterpret_cast<S2Hit*>(S + so.hits);
+  int* cand = reinterpret_cast<int*>(S + so.cand);
+  int* keep = reinterpret_cast<int*>(S + so.keep);
+  S2Path* pth = reinterpret_cast<S2Path*>(S + so.paths);
+  int* pathq = reinterpret_cast<int*>(S + so.pq);
+  int* pathh = reinterpret_cast<int*>(S + so.ph);
+  int* sbuf = reinterpret_cast<int*>(S + so.sbuf);
+  (void)sh; (void)diff; (void)run; (void)off; (void)minact; (void)maxact; (void)first; (void)proc; (void)dg;
+  (void)ord; (void)tmp; (void)hits; (void)cand; (void)keep; (void)pth; (void)pathq; (void)pathh; (void)sbuf;
+  (void)npq; (void)mpq; (void)nq; (void)blocks; (void)nwords; (void)qseq; (void)quc; (void)table_all;
+  (void)diag_all; (void)counters; (void)scratch_cap; (void)paths_out; (void)path_cap; (void)pairs_out; (void)pair_cap;
+  gmapdp_stage2_result R = results[P.index];
+  if (R.status != kS2Chained) return;
+  const int qstart = R.diag_querystart, qend = R.diag_queryend;
   // ---- get_cells_fwd + the path loop: cells within FINAL_SCORE_TOLERANCE of the best, each the best
   // of its root position, in (score desc, root asc, querypos desc, hit asc) order ----
   const int h0 = off[qstart], h1 = off[qend + 1];
@@ -875,6 +1521,7 @@ __global__ __launch_bounds__(64) void s2c_kernel(
   while (npaths < nkeep && (npaths < kS2MaxNalignments || hits[cand[npaths]].score == best)) npaths++;
   R.npaths = npaths;
 
+  S2_MARK(5);
   // ---- traceback_one per selected cell: length and extent of the converted list ----
   if (lane == 0) {
     for (int p = 0; p < npaths; p++) {
@@ -927,6 +1574,7 @@ __global__ __launch_bounds__(64) void s2c_kernel(
   for (int i = 0; i < npaths; i++) nres += keep[i] ? 0 : 1;
   R.nresults = nres;
 
+  S2_MARK(6);
   // ---- outputs: the kept results' path records and their pairs (convert_to_nucleotides) ----
   unsigned long long pbase = 0;
   if (lane == 0 && nres > 0) pbase = atomicAdd(&counters[1], (unsigned long long)nres);
@@ -1036,7 +1684,16 @@ __global__ __launch_bounds__(64) void s2c_kernel(
   }
   R.npairs = allpairs;
   if (lane == 0) results[P.index] = R;
+  S2_MARK(7);
 }
+
+#ifdef GMAPDP_OI_TIMING
+extern "C" int gmapdp_debug_s2_marks(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_s2_marks), sizeof(g_s2_marks)) != hipSuccess) return 1;
+  static const unsigned long long zero[2][16] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_s2_marks), zero, sizeof(zero)) != hipSuccess;
+}
+#endif
 
 size_t scratch_bytes_s2c(int querylength, int totalpositions, int ndiagonals) {
   return s2_scratch(querylength, totalpositions, ndiagonals).total;
@@ -1052,7 +1709,12 @@ hipError_t launch_s2c(int nproblems, hipStream_t stream, const DevStage2Problem*
                   (void*)&npos, (void*)&map, (void*)&table, (void*)&diags, (void*)&scratch, (void*)&counters,
                   (void*)&scratch_cap, (void*)&results, (void*)&paths, (void*)&path_cap, (void*)&pairs,
                   (void*)&pair_cap};
-  return hipLaunchKernel(reinterpret_cast<void*>(&s2c_kernel), dim3(nproblems), dim3(64), args, 0, stream);
+  hipError_t e = hipLaunchKernel(reinterpret_cast<void*>(&s2a_kernel), dim3(nproblems), dim3(64), args, 0, stream);
+  if (e == hipSuccess)
+    e = hipLaunchKernel(reinterpret_cast<void*>(&s2b_kernel), dim3(nproblems), dim3(64), args, 0, stream);
+  if (e == hipSuccess)
+    e = hipLaunchKernel(reinterpret_cast<void*>(&s2c_kernel), dim3(nproblems), dim3(64), args, 0, stream);
+  return e;
 }
 
 }  // namespace gmapdp

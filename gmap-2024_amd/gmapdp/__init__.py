@@ -201,6 +201,13 @@ def load_library(path=LIB_PATH):
         "gmapdp_oligo_plan_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.c_void_p, C.c_void_p, C.c_void_p]),
         "gmapdp_oligo_plan_destroy": (None, [C.c_void_p]),
+        "gmapdp_stage2_plan_create": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t,
+                                                P(C.c_void_p)]),
+        "gmapdp_stage2_plan_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                             C.c_void_p]),
+        "gmapdp_stage2_plan_outputs": (C.c_int, [C.c_void_p, P(C.c_void_p), P(C.c_void_p), P(C.c_void_p),
+                                                 P(C.c_size_t)]),
+        "gmapdp_stage2_plan_destroy": (None, [C.c_void_p]),
         "gmapdp_genome_prob_entries": (C.c_size_t, [C.c_void_p, C.c_int]),
         "gmapdp_genome_splice_sites": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t]),
         "gmapdp_plan_create_all": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p,

@@ -6,10 +6,12 @@
  *   -Wl,--wrap=Dynprog_init,--wrap=Dynprog_single_setup,--wrap=Dynprog_end_setup,
  *   -Wl,--wrap=Dynprog_genome_setup,--wrap=Dynprog_single_gap,--wrap=Dynprog_end5_gap,
  *   -Wl,--wrap=Dynprog_end3_gap,--wrap=Dynprog_genome_gap,--wrap=Dynprog_cdna_gap
- *   -Wl,--wrap=Oligoindex_hr_tally,--wrap=Oligoindex_get_mappings  -lgmapdp
+ *   -Wl,--wrap=Oligoindex_hr_tally,--wrap=Oligoindex_get_mappings
+ *   -Wl,--wrap=Stage2_setup,--wrap=Stage2_compute  -lgmapdp
  *
  * so that every call GMAP's stage 3 makes to these functions (stage3.c:9081,
- * 9275, 9510, 9531, 10244-10600, ...) lands here with the reference's own signature
+ * 9275, 9510, 9531, 10244-10600, ...), and GMAP's per-read Stage2_compute (gmap.c:1208, 1323: seeding
+ * and chaining, one call per genomic region), lands here with the reference's own signature
  * (dynprog_single.h:22, dynprog_end.h:25/47, dynprog_genome.h:24, dynprog_cdna.h:12) and returns
  * the reference's List_T of Pair_T built in the caller's Pairpool
  * (Pairpool_push / Pairpool_push_gapholder, pairpool.c:180/375).  The setup
@@ -58,6 +60,10 @@
 #include "dynprog_cdna.h"
 #include "oligoindex_hr.h"
 #include "diagpool.h"
+#include "cellpool.h"
+#include "stopwatch.h"
+#include "stage2.h"
+#include "mem.h"
 
 #include "gmapdp.h"
 #include "gmapdp_dynprog.h"
@@ -90,14 +96,14 @@ static int shim_homopolymerp = 0, shim_splicing_iit = 0;
 
 /* Calls that reached the engine, per wrapped entry point (printed at exit with GMAPDP_SHIM_STATS=1;
    tests use it to prove the pipeline really ran on the GPU). */
-enum { ST_SINGLE, ST_END5, ST_END3, ST_GENOME, ST_CDNA, ST_OLIGO, ST_N };
+enum { ST_SINGLE, ST_END5, ST_END3, ST_GENOME, ST_CDNA, ST_OLIGO, ST_STAGE2, ST_N };
 static const char *const shim_stat_name[ST_N] = {"Dynprog_single_gap", "Dynprog_end5_gap", "Dynprog_end3_gap",
                                                  "Dynprog_genome_gap", "Dynprog_cdna_gap",
-                                                 "Oligoindex_get_mappings"};
+                                                 "Oligoindex_get_mappings", "Stage2_compute"};
 static unsigned long shim_stats[ST_N];
 
 static unsigned long shim_batches, shim_batched;
-static double shim_secs[3];  /* dispatcher wall time in the DP, cDNA and stage-2 batches */
+static double shim_secs[4];  /* dispatcher wall time in the DP, cDNA, seeding and Stage2_compute batches */
 
 #include <time.h>
 static double
@@ -112,8 +118,9 @@ shim_print_stats (void) {
   int i;
   fprintf(stderr, "gmapdp shim calls:");
   for (i = 0; i < ST_N; i++) fprintf(stderr, " %s=%lu", shim_stat_name[i], __atomic_load_n(&shim_stats[i], __ATOMIC_RELAXED));
-  fprintf(stderr, " batches=%lu mean_batch=%.2f dp_s=%.3f cdna_s=%.3f stage2_s=%.3f\n", shim_batches,
-          shim_batches ? (double) shim_batched / (double) shim_batches : 0.0, shim_secs[0], shim_secs[1], shim_secs[2]);
+  fprintf(stderr, " batches=%lu mean_batch=%.2f dp_s=%.3f cdna_s=%.3f stage2_s=%.3f chain_s=%.3f\n", shim_batches,
+          shim_batches ? (double) shim_batched / (double) shim_batches : 0.0, shim_secs[0], shim_secs[1], shim_secs[2],
+          shim_secs[3]);
 }
 
 static void
@@ -212,7 +219,7 @@ shim_context (Genome_T genome) {
 }
 
 /* ---- requests and the dispatcher ---- */
-enum { K_SINGLE, K_END, K_GENOME, K_CDNA, K_OLIGO };
+enum { K_SINGLE, K_END, K_GENOME, K_CDNA, K_OLIGO, K_STAGE2 };
 
 typedef struct shim_req {
   int kind;
@@ -223,6 +230,7 @@ typedef struct shim_req {
     gmapdp_genome_problem g;
     gmapdp_cdna_problem c;
     gmapdp_oligo_problem o;
+    gmapdp_stage2_problem s2;
   } p;                          /* qoff / prob_offset relative to q and probs below */
   const char *q, *quc;          /* the query slice (borrowed: the caller waits) */
   size_t qlen;
@@ -233,6 +241,7 @@ typedef struct shim_req {
   gmapdp_genome_result gr;
   gmapdp_cdna_result cr;
   gmapdp_oligo_result orr;
+  gmapdp_stage2_result s2r;     /* path_offset rebased to 0, pair_offset of each path to the request's pairs */
   /* per-thread buffers (grown by the caller before submitting) */
   gmapdp_pair *pairs;
   size_t pcap;
@@ -242,6 +251,9 @@ typedef struct shim_req {
   uint32_t *pos;
   size_t npcap, mpcap, poscap, dgcap;
   size_t tabn;                  /* stage-2 seeding: the problem's table capacity */
+  gmapdp_path *s2paths;         /* Stage2_compute: the results' path records and pairs */
+  gmapdp_path_pair *s2pairs;
+  size_t s2pathcap, s2paircap;
   int done;
   pthread_cond_t cv;
   struct shim_req *next;
@@ -344,8 +356,9 @@ typedef struct {
   gmapdp_genome_problem *g;
   gmapdp_cdna_problem *c;
   gmapdp_oligo_problem *o;
-  shim_req **rs, **re, **rg, **rc, **ro;
-  size_t scap, ecap, gcap, ccap, ocap, rscap, recap, rgcap, rccap, rocap;
+  gmapdp_stage2_problem *s2;
+  shim_req **rs, **re, **rg, **rc, **ro, **r2;
+  size_t scap, ecap, gcap, ccap, ocap, s2cap, rscap, recap, rgcap, rccap, rocap, r2cap;
   char *q, *quc;
   size_t qcap, quccap;
   double *pr;
@@ -360,6 +373,10 @@ typedef struct {
   int32_t *np, *mp, *dg;
   uint32_t *pos;
   size_t npcap, mpcap, poscap, dgcap;
+  gmapdp_stage2_result *s2res;
+  gmapdp_path *paths;
+  gmapdp_path_pair *ppairs;
+  size_t s2rescap, pathcap, ppaircap;
 } shim_staging;
 static __thread shim_staging D;  /* per dispatcher thread */
 
@@ -373,8 +390,8 @@ shim_copy_pairs (shim_req *r, const gmapdp_pair *src, int n) {
 static void
 shim_run (shim_req *batch) {
   shim_req *r;
-  size_t ns = 0, ne = 0, ng = 0, nc = 0, no = 0, n = 0, qb = 0, pb = 0, cap, i;
-  double t0, t1, td[3];
+  size_t ns = 0, ne = 0, ng = 0, nc = 0, no = 0, n2 = 0, n = 0, qb = 0, pb = 0, cap, i;
+  double t0, t1, td[4];
   Genome_T genome = NULL;
   for (r = batch; r != NULL; r = r->next) {
     n++;
@@ -385,6 +402,7 @@ shim_run (shim_req *batch) {
     case K_END: GROW(D.re, D.recap, ne + 1); D.re[ne++] = r; break;
     case K_GENOME: GROW(D.rg, D.rgcap, ng + 1); D.rg[ng++] = r; break;
     case K_CDNA: GROW(D.rc, D.rccap, nc + 1); D.rc[nc++] = r; break;
+    case K_STAGE2: GROW(D.r2, D.r2cap, n2 + 1); D.r2[n2++] = r; break;
     default: GROW(D.ro, D.rocap, no + 1); D.ro[no++] = r; break;
     }
   }
@@ -539,9 +557,57 @@ shim_run (shim_req *batch) {
       r->orr.diag_offset = 0;
     }
   }
-  td[2] = shim_now() - t0;
+  t1 = shim_now();
+  td[2] = t1 - t0;
+  /* Stage2_compute: seeding and chaining in one batch */
+  if (n2 > 0) {
+    size_t pneed = 0, qneed = 0, k;
+    int rc;
+    GROW(D.s2, D.s2cap, n2 + 1);
+    qb = 0;
+    for (i = 0; i < n2; i++) qb += D.r2[i]->qlen;
+    GROW(D.q, D.qcap, qb + 1);
+    GROW(D.quc, D.quccap, qb + 1);
+    qb = 0;
+    for (i = 0; i < n2; i++) {
+      r = D.r2[i];
+      D.s2[i] = r->p.s2;
+      D.s2[i].qoff = (int32_t) qb;
+      memcpy(D.q + qb, r->q, r->qlen);
+      memcpy(D.quc + qb, r->quc, r->qlen);
+      qb += r->qlen;
+    }
+    GROW(D.s2res, D.s2rescap, n2 + 1);
+    GROW(D.paths, D.pathcap, 4 * n2 + 16);
+    GROW(D.ppairs, D.ppaircap, 3 * qb + 64);
+    for (;;) {
+      rc = gmapdp_stage2_batch(shim_ctx, D.s2, (int) n2, D.q, D.quc, qb, D.s2res, D.paths, D.pathcap, D.ppairs,
+                               D.ppaircap, &pneed, &qneed);
+      if (rc != GMAPDP_ESPACE) break;
+      GROW(D.paths, D.pathcap, pneed + 16);
+      GROW(D.ppairs, D.ppaircap, qneed + 64);
+    }
+    shim_check(rc, "gmapdp_stage2_batch");
+    for (i = 0; i < n2; i++) {
+      gmapdp_stage2_result *res = &D.s2res[i];
+      size_t npairs = 0;
+      r = D.r2[i];
+      r->s2r = *res;
+      GROW(r->s2paths, r->s2pathcap, (size_t) res->nresults + 1);
+      GROW(r->s2pairs, r->s2paircap, (size_t) res->npairs + 1);
+      for (k = 0; k < (size_t) res->nresults; k++) {
+        const gmapdp_path *pa = &D.paths[res->path_offset + k];
+        memcpy(r->s2pairs + npairs, D.ppairs + pa->pair_offset, (size_t) pa->npairs * sizeof(gmapdp_path_pair));
+        r->s2paths[k] = *pa;
+        r->s2paths[k].pair_offset = (int64_t) npairs;
+        npairs += (size_t) pa->npairs;
+      }
+      r->s2r.path_offset = 0;
+    }
+  }
+  td[3] = shim_now() - t1;
   pthread_mutex_lock(&q_lock);
-  for (i = 0; i < 3; i++) shim_secs[i] += td[i];
+  for (i = 0; i < 4; i++) shim_secs[i] += td[i];
   pthread_mutex_unlock(&q_lock);
 }
 
@@ -935,4 +1001,107 @@ __wrap_Oligoindex_get_mappings (List_T diagonals, bool *coveredp, Chrpos_T **map
     diagonals = Diagpool_push(diagonals, diagpool, d[0], d[1], d[2], d[3]);
   }
   return diagonals;
+}
+
+/* ---- Stage2_compute (stage2.c:6325): seeding + chaining on the engine ----
+   gmap.c's calls (update_stage3middle_list / update_stage3list, gmap.c:1208 / 1323) pass the major
+   oligoindex array, localp, skip_repetitive_p, favor_right_p false and max_nalignments 10; the engine
+   restates exactly that configuration and the shim refuses any other.  Each returned Stage2_T holds
+   the middle path's pairs, pushed into the caller's Pairpool in list order; its all_starts / all_ends
+   stay NULL as in the reference (MOVE_TO_STAGE3 undefined). */
+extern void __real_Stage2_setup (bool splicingp_in, bool cross_species_p, int suboptimal_score_start_in,
+                                 int suboptimal_score_end_in, int sufflookback_in, int nsufflookback_in,
+                                 int maxintronlen_in, Mode_T mode_in, bool snps_p_in);
+static int s2_splicingp = 1, s2_cross_species_p = 0, s2_sufflookback = 60, s2_nsufflookback = 5,
+           s2_maxintronlen = 500000, s2_mode = 0, s2_snps_p = 0;
+
+void
+__wrap_Stage2_setup (bool splicingp_in, bool cross_species_p, int suboptimal_score_start_in,
+                     int suboptimal_score_end_in, int sufflookback_in, int nsufflookback_in, int maxintronlen_in,
+                     Mode_T mode_in, bool snps_p_in) {
+  __real_Stage2_setup(splicingp_in, cross_species_p, suboptimal_score_start_in, suboptimal_score_end_in,
+                      sufflookback_in, nsufflookback_in, maxintronlen_in, mode_in, snps_p_in);
+  s2_splicingp = splicingp_in ? 1 : 0;
+  s2_cross_species_p = cross_species_p ? 1 : 0;
+  s2_sufflookback = sufflookback_in;
+  s2_nsufflookback = nsufflookback_in;
+  s2_maxintronlen = maxintronlen_in;
+  s2_mode = (int) mode_in;
+  s2_snps_p = snps_p_in ? 1 : 0;
+}
+
+/* struct Stage2_T (stage2.c:302): Stage2_free (FREE) and Stage2_middle read it */
+struct shim_stage2 {
+  List_T middle;
+  List_T all_starts;
+  List_T all_ends;
+};
+
+List_T
+__wrap_Stage2_compute (char *queryseq_ptr, char *queryuc_ptr, int querylength, int query_offset, Chrpos_T chrstart,
+                       Chrpos_T chrend, Univcoord_T chroffset, Univcoord_T chrhigh, bool plusp, int genestrand,
+                       Stage2_alloc_T stage2_alloc, double proceed_pctcoverage, Oligoindex_array_T oligoindices,
+                       Genome_T genome, Genome_T genomealt, Pairpool_T pairpool, Diagpool_T diagpool,
+                       Cellpool_T cellpool, bool localp, bool skip_repetitive_p, bool favor_right_p,
+                       int max_nalignments, Stopwatch_T stopwatch, bool diag_debug) {
+  shim_req *r;
+  gmapdp_stage2_problem *p;
+  Oligoindex_T major;
+  List_T results = NULL, middle;
+  struct shim_stage2 *s2;
+  int k, i;
+  (void) stage2_alloc;
+  (void) diagpool;
+  (void) cellpool;
+  (void) stopwatch;
+  (void) genestrand;
+  if (s2_mode != 0 || shim_mode != 0) shim_refuse("Stage2_compute outside STANDARD mode (cmet / atoi / ttoc)");
+  if (s2_cross_species_p) shim_refuse("Stage2_compute with cross-species canonical scoring");
+  if (s2_snps_p || (genomealt != NULL && genomealt != genome)) shim_refuse("Stage2_compute with an SNP genome");
+  if (s2_sufflookback != 60 || s2_nsufflookback != 5) shim_refuse("Stage2_compute with non-default lookback");
+  if (diag_debug) shim_refuse("Stage2_compute diagnostics (diag_debug)");
+  if (query_offset != 0 || !localp || !skip_repetitive_p || favor_right_p || max_nalignments != 10 ||
+      proceed_pctcoverage != 0.3)
+    shim_refuse("a Stage2_compute call other than gmap.c's (localp, 0.3 coverage, 10 alignments)");
+  if (Oligoindex_array_length(oligoindices) != 1) shim_refuse("more than one stage-2 oligoindex source");
+  major = Oligoindex_array_elt(oligoindices, 0);
+  if (major->indexsize != 8 || major->diag_lookback != 120 || major->suffnconsecutive != 20)
+    shim_refuse("an oligoindex other than GMAP's major 8-mer index");
+  if (querylength <= 8) shim_refuse("Stage2_compute on a query of 8 nt or less");
+  r = shim_request(K_STAGE2);
+  p = &r->p.s2;
+  p->querylength = querylength;
+  p->chrstart = chrstart;
+  p->chrend = chrend;
+  p->chroffset = shim_coord(chroffset);
+  p->chrhigh = shim_coord(chrhigh);
+  p->plusp = plusp ? 1 : 0;
+  p->splicingp = s2_splicingp;
+  p->maxintronlen = s2_maxintronlen;
+  r->genome = genome;
+  r->q = queryseq_ptr;
+  r->quc = queryuc_ptr;
+  r->qlen = (size_t) querylength;
+  shim_submit(r);
+  shim_count(ST_STAGE2);
+  /* the results in list order: build from the last (each List_push prepends) */
+  for (k = r->s2r.nresults - 1; k >= 0; k--) {
+    const gmapdp_path *pa = &r->s2paths[k];
+    const gmapdp_path_pair *pr = r->s2pairs + pa->pair_offset;
+    middle = NULL;
+    for (i = pa->npairs - 1; i >= 0; i--) {
+      if (pr[i].querypos == -1 && pr[i].genomepos == -1)
+        middle = Pairpool_push_gapholder(middle, pairpool, pr[i].queryjump, pr[i].genomejump, /*leftpair*/NULL,
+                                         /*rightpair*/NULL, /*knownp*/false);
+      else
+        middle = Pairpool_push(middle, pairpool, pr[i].querypos, pr[i].genomepos, pr[i].cdna, pr[i].comp,
+                               pr[i].genome, pr[i].genomealt, /*dynprogindex*/0);
+    }
+    s2 = (struct shim_stage2 *) MALLOC(sizeof(struct shim_stage2));
+    s2->middle = middle;
+    s2->all_starts = NULL;
+    s2->all_ends = NULL;
+    results = List_push(results, (void *) s2);
+  }
+  return results;
 }

@@ -433,6 +433,21 @@ int gmapdp_stage2_batch (gmapdp_ctx *ctx, const gmapdp_stage2_problem *problems,
                          size_t path_cap, gmapdp_path_pair *pairs, size_t pair_cap, size_t *paths_needed,
                          size_t *pairs_needed);
 
+/* Device-resident Stage2_compute (bench / pipelined callers): plan once (the seeding plan, the
+ * chaining scratch sized from one seeding run at plan time, output pools), then run asynchronously on
+ * `stream` against device-resident query arenas.  what: 1 seeding only, 2 chaining only (after a
+ * seeding run), 3 both.  d_results: n entries in problem order; paths and pairs stay in the plan's
+ * pools (gmapdp_stage2_plan_outputs: device pointers and the counters {scratch, paths, pairs} bytes /
+ * records used); a result with status -2 did not fit them. */
+typedef struct gmapdp_stage2_plan gmapdp_stage2_plan;
+int gmapdp_stage2_plan_create (gmapdp_ctx *ctx, const gmapdp_stage2_problem *problems, int n, const char *qseq,
+                               const char *qseq_uc, size_t qbytes, gmapdp_stage2_plan **plan);
+int gmapdp_stage2_plan_run (gmapdp_ctx *ctx, const gmapdp_stage2_plan *plan, const char *d_qseq,
+                            const char *d_qseq_uc, gmapdp_stage2_result *d_results, int what, void *stream);
+int gmapdp_stage2_plan_outputs (const gmapdp_stage2_plan *plan, gmapdp_path **d_paths, gmapdp_path_pair **d_pairs,
+                                unsigned long long **d_counters, size_t *scratch_bytes);
+void gmapdp_stage2_plan_destroy (gmapdp_stage2_plan *plan);
+
 /* Create a context on HIP device `device`.  mode = Mode_T (mode.h:5;
  * 0 = STANDARD).  user_* mirror Dynprog_single_setup. */
 int gmapdp_create (gmapdp_ctx **ctx, int device, int mode,

@@ -109,3 +109,22 @@ def test_shim_stage2_seeding():
     probs = [oligo_problem(rng, g, edge=(i % 4 == 0)) for i in range(150)]
     bad = [i for i, p in enumerate(probs) if shim.oligo_mappings(p) != ref.oligo_mappings(p)]
     assert bad == []
+
+
+@pytest.mark.parametrize("build", ["nosimd", "avx2"])
+def test_shim_stage2_compute(build):
+    """Stage2_compute itself wrapped (seeding + chaining on oi_kernel / s2a-s2c): the Stage2_T list and
+    every middle-path Pair_T equal the unmodified reference objects', in both builds."""
+    from dpbind import repeat_genome, stage2_problem
+    refv, shimv = ("nosimd", "gpushim") if build == "nosimd" else ("avx2a", "gpushim_avx2")
+    if not (ref_available(refv) and ref_available(shimv)):
+        pytest.skip("reference objects did not travel")
+    ref, shim = Ref(refv), Ref(shimv)
+    rng = random.Random(1020)
+    g = repeat_genome(rng, 250000)
+    ref.set_genome(g)
+    shim.set_genome(g)
+    probs = [stage2_problem(rng, g, edge=(i % 4 == 0)) for i in range(120)]
+    probs = [p for p in probs if len(p["quc"]) > 8]
+    bad = [i for i, p in enumerate(probs) if shim.stage2_compute(p) != ref.stage2_compute(p)]
+    assert bad == []

@@ -1,8 +1,8 @@
 """CPU baseline leg of bench.py (TEST/MEASUREMENT INFRASTRUCTURE: it loads the reference's own objects
 from oracle/_ref, never the product library).
 
-Times the reference GMAP 2024-02-22 path -- Oligoindex_hr_tally + Oligoindex_get_mappings (one
-Stage2_compute seeding call) and Dynprog_single_gap / _end5_gap / _end3_gap / _genome_gap -- on the
+Times the reference GMAP 2024-02-22 path -- Stage2_compute (stage2.c:6325: seeding and chaining, as
+gmap.c:1208 calls it) and Dynprog_single_gap / _end5_gap / _end3_gap / _genome_gap -- on the
 host cores, one process per core, each on a bounded sample of the configs[2] per-read call stream
 (gmapdp.workload, same generators and per-read mix as the GPU bench).  The reference's harness takes
 an int genome length, so the CPU sample is cut from a chr22-length (50.8 Mnt) i.i.d. genome; the DP and
@@ -51,17 +51,16 @@ def worker(args):
         f = getattr(lib, name)
         f.restype = C.c_long
         f.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_char_p]
-    fo = lib.refh_oligo_mappings
+    fo = lib.refh_stage2_compute
     fo.restype = C.c_int
-    fo.argtypes = [C.c_char_p, C.c_int, C.c_uint, C.c_uint, C.c_uint, C.c_uint, C.c_int, C.c_int, C.c_void_p,
-                   C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int]
+    fo.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_uint, C.c_uint, C.c_uint, C.c_uint, C.c_int, C.c_int, C.c_int,
+                   C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int]
     qb = d["q"].tobytes()
     oq = d["oq"].tobytes()
-    cap = 1 << 21
-    pos = np.zeros(cap, dtype=np.uint32)
-    npos = np.zeros(int(d["oligo"]["querylength"].max()) + 1, dtype=np.int32)
-    sc = np.zeros(4, dtype=np.int32)
-    dg = np.zeros(4 * 65536, dtype=np.int32)
+    cap = 1 << 18
+    pairs = np.zeros(cap * 32, dtype=np.uint8)  # RefPair records (oracle/refharness.c)
+    paths = np.zeros(2 * 1024, dtype=np.int32)
+    sc = np.zeros(8, dtype=np.int32)
     fams = [("single", lib.refh_single_gap_batch, d["single"], W.SINGLE_PER_READ),
             ("end", lib.refh_end_gap_batch, d["end"], W.END5_PER_READ + W.END3_PER_READ),
             ("genome", lib.refh_genome_gap_batch, d["genome"], W.GENOME_PER_READ)]
@@ -81,8 +80,9 @@ def worker(args):
         p = d["oligo"][n["oligo"] % len(d["oligo"])]
         o, ql = int(p["qoff"]), int(p["querylength"])
         t0 = time.perf_counter()
-        fo(oq[o:o + ql], ql, int(p["chrstart"]), int(p["chrend"]), int(p["chroffset"]), int(p["chrhigh"]),
-           int(p["plusp"]), 0, npos.ctypes.data, pos.ctypes.data, cap, sc.ctypes.data, dg.ctypes.data, 65536)
+        fo(oq[o:o + ql], oq[o:o + ql], ql, int(p["chrstart"]), int(p["chrend"]), int(p["chroffset"]),
+           int(p["chrhigh"]), int(p["plusp"]), 1, 500000, sc.ctypes.data, paths.ctypes.data, 1024,
+           pairs.ctypes.data, cap)
         t["oligo"] += time.perf_counter() - t0
         n["oligo"] += 1
     per_call = {k: t[k] / max(n[k], 1) for k in t}
@@ -114,7 +114,7 @@ def main():
         "build": "gmap.%s objects (oracle/_ref/librefdp_%s.so)" % (a.build, a.build),
         "cpu_model": cpu_model(), "per_core_reads_per_s": total / cores, "per_call_us": per_call,
         "sample": "%d worker processes x %.0f s of timed reference calls (%s) on the configs[2] per-read mix "
-                  "(1 seeding call + %.1f single + %.1f end + %.1f genome-gap calls per read) cut from a chr22-length "
+                  "(1 Stage2_compute call + %.1f single + %.1f end + %.1f genome-gap calls per read) cut from a chr22-length "
                   "i.i.d. genome; per-read time composed from per-call averages"
                   % (cores, a.budget, ", ".join("%d %s" % (v, k) for k, v in calls.items()), 43.7, 13.6, 49.4)}))
 

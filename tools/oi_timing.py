@@ -49,10 +49,46 @@ def main_gg(reads=10000):
     eng.close()
 
 
+S2_PHASES = ["coverage", "Diag_compute_bounds", "hit arrays", "lookback sweep", "cells", "traceback + filter",
+             "convert_to_nucleotides"]
+
+
+def main_s2(reads=10000):
+    """s2c_kernel (Stage2_compute chaining) phases on bench.py's stage-2 stream."""
+    import torch
+    lib = gmapdp.load_library(os.path.join(ROOT, "gmap-2024_amd", "lib", "libgmapdp_oitiming.so"))
+    lib.gmapdp_debug_s2_marks.argtypes = [C.c_void_p]
+    layout = W.Layout(W.CHR22)
+    genome = W.make_genome(layout, seed=22)
+    eng = gmapdp.Engine(0)
+    eng.set_genome(genome.tobytes())
+    op, oq = W.make_stage2(genome, layout, reads, np.random.default_rng(3000))
+    calls = [dict(quc=oq[int(p["qoff"]):int(p["qoff"]) + int(p["querylength"])].tobytes(),
+                  **{k: int(p[k]) for k in ("chrstart", "chrend", "chroffset", "chrhigh", "plusp")}) for p in op]
+    probs, qb, qub = eng.build_stage2_batch(calls)
+    eng.stage2_batch_raw(probs, qb, qub)
+    marks = np.zeros(32, dtype=np.uint64)
+    lib.gmapdp_debug_s2_marks(marks.ctypes.data)
+    res, _, _ = eng.stage2_batch_raw(probs, qb, qub)
+    torch.cuda.synchronize()
+    lib.gmapdp_debug_s2_marks(marks.ctypes.data)
+    t, c = marks[:16].astype(np.float64), marks[16:]
+    dur = [float(t[k + 1] - t[k]) for k in range(7)]
+    tot = sum(dur)
+    cnt = {k: round(float(marks[i]) / 1e2 / max(int(c[0]), 1), 1)
+           for k, i in (("sweep_meta_us", 8), ("sweep_one_us", 9), ("sweep_mult_us", 10), ("sweep_tail_us", 11))}
+    print(json.dumps({"waves": [int(x) for x in c[:8]], "phases": {n: round(d / tot, 4) for n, d in zip(S2_PHASES, dur)},
+                      "mean_wave_us": tot / 1e2 / max(int(c[0]), 1), "status": np.bincount(res["status"] + 3).tolist(),
+                      "counts": cnt}))
+    eng.close()
+
+
 def main():
     import torch
     if len(sys.argv) > 1 and sys.argv[1] == "gg":
         return main_gg()
+    if len(sys.argv) > 1 and sys.argv[1] == "s2":
+        return main_s2()
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
     lib = gmapdp.load_library(os.path.join(ROOT, "gmap-2024_amd", "lib", "libgmapdp_oitiming.so"))
     lib.gmapdp_debug_oi_marks.argtypes = [C.c_void_p]
