@@ -205,6 +205,14 @@ struct S2Ring {
   int score[kS2Ring], consec[kS2Ring], tracei[kS2Ring], root[kS2Ring], hit[kS2Ring];
   int eq[kS2Meta], en[kS2Meta], eoff[kS2Meta], estart[kS2Meta];
 };
+// the sweep's LDS (one wave per workgroup): ds_* instructions rather than flat ones
+static __shared__ S2Ring s2_ring;
+static __shared__ int s2_fr[128];
+
+// a value every lane holds (loaded from a uniform address) as a scalar: scalar branches
+__device__ __forceinline__ int s2_u(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t s2_u(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
 struct S2HV {  // one hit's link state
   uint32_t map;
   int score, consec, tracei, root, hit;
@@ -219,7 +227,6 @@ struct S2W {
   int* actn;       // per query position: number of active hits (firstactive != -1 <=> actn > 0)
   int* alist;      // active hits of q at alist[off[q] ...] (hit indices, ascending)
   int *pq, *pn, *poff, *pstart;  // per processed entry: q, active count, off[q], ring start
-  S2Ring* ring;
   int pushed, tracectr, splicingp, lane;
   uint32_t maxintronlen;
 };
@@ -235,26 +242,31 @@ __device__ __forceinline__ S2HV s2_bcast(const S2HV& v, int j) {
   return u;
 }
 
-__device__ __forceinline__ S2HV s2_load(const S2W& W, const S2E& e, int k) {
+// an entry's hit outside the ring (rare): its own function so that the ring path's loads stay
+// ds_* instructions instead of being merged into flat loads through a selected pointer
+__device__ __attribute__((noinline)) S2HV s2_load_global(const S2Hit* hits, const int* alist, int offq, int k) {
   S2HV v;
-  if (e.inring) {
-    const int s = (e.start + k) & (kS2Ring - 1);
-    v.map = W.ring->map[s];
-    v.score = W.ring->score[s];
-    v.consec = W.ring->consec[s];
-    v.tracei = W.ring->tracei[s];
-    v.root = W.ring->root[s];
-    v.hit = W.ring->hit[s];
-  } else {  // (callers fence before reading entries outside the ring)
-    const int h = W.alist[e.offq + k];
-    const S2Hit& x = W.hits[e.offq + h];
-    v.map = x.map;
-    v.score = x.score;
-    v.consec = x.consec;
-    v.tracei = x.tracei;
-    v.root = x.root;
-    v.hit = h;
-  }
+  const int h = alist[offq + k];
+  const S2Hit& x = hits[offq + h];
+  v.map = x.map;
+  v.score = x.score;
+  v.consec = x.consec;
+  v.tracei = x.tracei;
+  v.root = x.root;
+  v.hit = h;
+  return v;
+}
+
+__device__ __forceinline__ S2HV s2_load(const S2W& W, const S2E& e, int k) {
+  if (!e.inring) return s2_load_global(W.hits, W.alist, e.offq, k);  // (callers fence first)
+  S2HV v;
+  const int s = (e.start + k) & (kS2Ring - 1);
+  v.map = s2_ring.map[s];
+  v.score = s2_ring.score[s];
+  v.consec = s2_ring.consec[s];
+  v.tracei = s2_ring.tracei[s];
+  v.root = s2_ring.root[s];
+  v.hit = s2_ring.hit[s];
   return v;
 }
 
@@ -270,11 +282,11 @@ __device__ __forceinline__ S2E s2_mkentry(const S2W& W, int q, int n, int offq, 
 
 // Section A: from active index k_io, the first hit with map + qd >= position (k_io := it, or -1 when
 // the list runs out); true when it sits exactly qd before position (its state in `out`)
-__device__ bool s2_adj(const S2W& W, const S2E& e, int& k_io, int qd, uint32_t position, S2HV& out) {
+__device__ __forceinline__ bool s2_adj(const S2W& W, const S2E& e, int& k_io, int qd, uint32_t position, S2HV& out) {
   if (k_io < 0) return false;
   if (e.n == 1 && e.inring) {  // one active hit (the common case): uniform LDS reads, no ballots
     const int sl = e.start & (kS2Ring - 1);
-    const uint32_t mp = W.ring->map[sl];
+    const uint32_t mp = s2_u(s2_ring.map[sl]);
     if (!(mp + (uint32_t)qd >= position)) {
       k_io = -1;
       return false;
@@ -282,11 +294,11 @@ __device__ bool s2_adj(const S2W& W, const S2E& e, int& k_io, int qd, uint32_t p
     k_io = 0;
     if (mp + (uint32_t)qd != position) return false;
     out.map = mp;
-    out.score = W.ring->score[sl];
-    out.consec = W.ring->consec[sl];
-    out.tracei = W.ring->tracei[sl];
-    out.root = W.ring->root[sl];
-    out.hit = W.ring->hit[sl];
+    out.score = s2_u(s2_ring.score[sl]);
+    out.consec = s2_u(s2_ring.consec[sl]);
+    out.tracei = s2_u(s2_ring.tracei[sl]);
+    out.root = s2_u(s2_ring.root[sl]);
+    out.hit = s2_u(s2_ring.hit[sl]);
     return true;
   }
   if (!e.inring) wave_sync();
@@ -313,37 +325,37 @@ __device__ bool s2_adj(const S2W& W, const S2E& e, int& k_io, int qd, uint32_t p
 
 // Ranges 0-4 of score_querypos_lookback_one/_mult against processed entry e from active index start;
 // returns the index where the range-0/1 skipping stopped (the _mult frontier), -1 when the list ran out.
-__device__ int s2_eval(S2W& W, const S2E& e, int start, int q, uint32_t position, int& last_tr, S2Best& b,
+__device__ __forceinline__ int s2_eval(S2W& W, const S2E& e, int start, int q, uint32_t position, int& last_tr, S2Best& b,
                        bool range1) {
   const int qd = q - e.q, credit = -qd / kS2K;
   if (e.n == 1 && e.inring && start == 0) {  // one active hit: the ranges in scalar form
     const int sl = e.start & (kS2Ring - 1);
-    const int tr = W.ring->tracei[sl];
+    const int tr = s2_u(s2_ring.tracei[sl]);
     if (tr == last_tr) return -1;  // range 0 (nothing left for the frontier either)
     last_tr = tr;
-    const uint32_t mp = W.ring->map[sl];
+    const uint32_t mp = s2_u(s2_ring.map[sl]);
     if (range1 && mp + W.maxintronlen + (uint32_t)qd <= position) return -1;
     if (mp + (uint32_t)kS2EqualNotSplicing + (uint32_t)qd < position) {
       const int diff = (int)(position - mp) - qd;
-      const int fs = W.ring->score[sl] + credit - (W.splicingp ? (diff / kS2TenThousand + 1) : (diff + 1));
+      const int fs = s2_u(s2_ring.score[sl]) + credit - (W.splicingp ? (diff / kS2TenThousand + 1) : (diff + 1));
       if (fs > b.score) {
         b.consec = 0;
-        b.root = W.ring->root[sl];
+        b.root = s2_u(s2_ring.root[sl]);
         b.score = fs;
         b.pp = e.q;
-        b.ph = W.ring->hit[sl];
+        b.ph = s2_u(s2_ring.hit[sl]);
         b.tracei = ++W.tracectr;
       }
     } else if (mp + (uint32_t)kS2K <= position) {
-      const int fs = W.ring->score[sl] + 1;
+      const int fs = s2_u(s2_ring.score[sl]) + 1;
       if (fs > b.score) {
         const int g = (int)(position - mp);
         const int diff = g > qd ? g - qd : qd - g;
-        b.consec = (diff <= 0) ? W.ring->consec[sl] + qd : 0;
-        b.root = W.ring->root[sl];
+        b.consec = (diff <= 0) ? s2_u(s2_ring.consec[sl]) + qd : 0;
+        b.root = s2_u(s2_ring.root[sl]);
         b.score = fs;
         b.pp = e.q;
-        b.ph = W.ring->hit[sl];
+        b.ph = s2_u(s2_ring.hit[sl]);
         b.tracei = tr;
       }
     }
@@ -425,7 +437,7 @@ struct S2EntryCache {
     const int k = np - 1 - kk;
     if (kk < kS2Meta) {
       const int s = k & (kS2Meta - 1);
-      return s2_mkentry(W, W.ring->eq[s], W.ring->en[s], W.ring->eoff[s], W.ring->estart[s]);
+      return s2_mkentry(W, s2_u(s2_ring.eq[s]), s2_u(s2_ring.en[s]), s2_u(s2_ring.eoff[s]), s2_u(s2_ring.estart[s]));
     }
     wave_sync();
     return s2_mkentry(W, W.pq[k], W.pn[k], W.poff[k], W.pstart[k]);
@@ -441,18 +453,18 @@ struct S2Pref {
     const int k = np - 1 - W.lane;
     if (W.lane < kS2Meta && k >= 0) {
       const int s = k & (kS2Meta - 1);
-      q = W.ring->eq[s];
-      n = W.ring->en[s];
-      off = W.ring->eoff[s];
-      start = W.ring->estart[s];
+      q = s2_ring.eq[s];
+      n = s2_ring.en[s];
+      off = s2_ring.eoff[s];
+      start = s2_ring.estart[s];
       if (n == 1 && start >= W.pushed - kS2Ring) {
         const int sl = start & (kS2Ring - 1);
-        h.map = W.ring->map[sl];
-        h.score = W.ring->score[sl];
-        h.consec = W.ring->consec[sl];
-        h.tracei = W.ring->tracei[sl];
-        h.root = W.ring->root[sl];
-        h.hit = W.ring->hit[sl];
+        h.map = s2_ring.map[sl];
+        h.score = s2_ring.score[sl];
+        h.consec = s2_ring.consec[sl];
+        h.tracei = s2_ring.tracei[sl];
+        h.root = s2_ring.root[sl];
+        h.hit = s2_ring.hit[sl];
       }
     }
   }
@@ -508,8 +520,75 @@ __device__ __forceinline__ int s2_entry_eval(S2W& W, const S2Pref& pf, S2EntryCa
   return s2_eval(W, e, start, q, position, last_tr, b, range1);
 }
 
+// Section D over the newest processed entries [0, kmax] in one wave step, when every entry that would
+// be evaluated holds a single active hit in the ring (the common case).  For such entries range 0
+// leaves last_tr = the entry's tracei whether it skips or not, so "skipped" is "same tracei as the
+// nearest earlier evaluated entry" (a ballot and one lane shuffle); only the remaining candidates are
+// walked in order, and only they can change the link or end the loop (consec >= ENOUGH_CONSECUTIVE).
+// use_f: _mult's per-entry frontiers (lane kk holds f, 0 or -1), updated for the visited entries.
+// Returns false (nothing done) when the window holds another kind of entry.
+__device__ __forceinline__ bool s2_dloop_fast(S2W& W, const S2Pref& pf, int np, int kmax, int q, uint32_t position,
+                                              S2Best& b, bool range1, bool use_f, int& f) {
+  if (kmax >= 64) return false;
+  const int kk = W.lane;
+  const bool inw = kk <= kmax && kk < np;
+  const bool valid = inw && pf.n > 0 && (!use_f || f != -1);
+  const bool simple = pf.n == 1 && pf.start >= W.pushed - kS2Ring;
+  if (ballot(valid && !simple)) return false;
+  if (b.consec >= kS2EnoughConsec) return true;
+  const uint64_t V = ballot(valid);
+  const uint64_t below = kk ? (V & ((1ull << kk) - 1ull)) : 0ull;
+  const int prev = below ? 63 - __clzll((long long)below) : 0;
+  const int ptr = __shfl(pf.h.tracei, prev, 64);
+  const int last_tr = below ? ptr : -1;
+  const int qd = q - pf.q;
+  const bool skip = valid && pf.h.tracei == last_tr;
+  const bool r1skip = valid && !skip && range1 && pf.h.map + W.maxintronlen + (uint32_t)qd <= position;
+  int kind = 0, fs = 0;
+  if (valid && !skip && !r1skip) {
+    if (pf.h.map + (uint32_t)kS2EqualNotSplicing + (uint32_t)qd < position) {
+      const int diff = (int)(position - pf.h.map) - qd;
+      kind = 2;
+      fs = pf.h.score + (-qd / kS2K) - (W.splicingp ? (diff / kS2TenThousand + 1) : (diff + 1));
+    } else if (pf.h.map + (uint32_t)kS2K <= position) {
+      kind = 4;
+      fs = pf.h.score + 1;
+    }
+  }
+  uint64_t C = ballot(kind != 0);
+  int last_visited = kmax;
+  while (C) {
+    const int j = __ffsll((long long)C) - 1;
+    C &= C - 1;
+    const int fsj = __builtin_amdgcn_readlane(fs, j);
+    if (fsj > b.score) {
+      const S2HV u = s2_bcast(pf.h, j);
+      const int eq = __builtin_amdgcn_readlane(pf.q, j);
+      if (__builtin_amdgcn_readlane(kind, j) == 2) {
+        b.consec = 0;
+        b.tracei = ++W.tracectr;
+      } else {
+        const int g = (int)(position - u.map), qdj = q - eq;
+        const int diff = g > qdj ? g - qdj : qdj - g;
+        b.consec = (diff <= 0) ? u.consec + qdj : 0;
+        b.tracei = u.tracei;
+      }
+      b.root = u.root;
+      b.score = fsj;
+      b.pp = eq;
+      b.ph = u.hit;
+      if (b.consec >= kS2EnoughConsec) {
+        last_visited = j;
+        break;
+      }
+    }
+  }
+  if (use_f && kk <= last_visited && (skip || r1skip)) f = -1;
+  return true;
+}
+
 // score_querypos_lookback_one (stage2.c:1073); returns the link
-__device__ S2Best s2_one(S2W& W, int q, uint32_t position, int np, const S2E& last) {
+__device__ __forceinline__ S2Best s2_one(S2W& W, int q, uint32_t position, int np, const S2E& last) {
   S2Best b = {kS2K, (int)position, -1, -1, 0, 0};
   int nlookback = kS2Nsufflookback, lookback = kS2Sufflookback;
   if (np > 0) {
@@ -531,6 +610,11 @@ __device__ S2Best s2_one(S2W& W, int q, uint32_t position, int np, const S2E& la
   if (np > 0 && b.consec < kS2EnoughConsec) {
     S2Pref pf;
     pf.load(W, np);
+    // the entry that ends the walk (donep): the first beyond nlookback more than lookback + 8 back
+    const uint64_t dm = ballot(W.lane < np && W.lane > nlookback && (q - pf.q) - kS2K > lookback);
+    const int kmax = dm ? __ffsll((long long)dm) - 1 : (np <= 64 ? np - 1 : 64);
+    int fdummy = 0;
+    if (s2_dloop_fast(W, pf, np, kmax, q, position, b, W.splicingp != 0, false, fdummy)) np = 0;  // done
     S2EntryCache ec;
     for (int kk = 0; kk < np && b.consec < kS2EnoughConsec && !donep; kk++) {
       const int eq = kk < kS2Meta ? __builtin_amdgcn_readlane(pf.q, kk) : ec.get(W, np, kk).q;
@@ -559,7 +643,8 @@ __device__ __forceinline__ void s2_store_link(S2W& W, int offq, int hit, const S
 }
 
 // score_querypos_lookback_mult (stage2.c:1470) over hits [low, high) of q; links to global
-__device__ void s2_mult(S2W& W, int q, int offq, int low, int high, int np, const S2E& last, int* fr) {
+__device__ __forceinline__ void s2_mult(S2W& W, int q, int offq, int low, int high, int np, const S2E& last) {
+  int* fr = s2_fr;
   const int nhits = high - low;
   if (np == 0) {
     for (int i = W.lane; i < nhits; i += 64) {
@@ -609,7 +694,7 @@ __device__ void s2_mult(S2W& W, int q, int offq, int low, int high, int np, cons
     if (overall < kS2GreedyConsec) {
       int last_tr = -1;
       for (int kk = 0; kk < np && b.consec < kS2EnoughConsec && kk <= maxseen && kk < nfr; kk++) {
-        const int f = fr[kk];
+        const int f = s2_u(s2_fr[kk]);
         if (f != -1) {
           const S2E e = ec.get(W, np, kk);
           const int nf = s2_eval(W, e, f, q, position, last_tr, b, true);
@@ -629,8 +714,8 @@ __device__ void s2_mult(S2W& W, int q, int offq, int low, int high, int np, cons
 }
 
 // the sweep (stage2.c:3746-4080)
-__device__ void s2_sweep(S2W& W, const int32_t* npq, int nq, const uint32_t* minact, const uint32_t* maxact,
-                         int qstart, int qend, int* fr) {
+__device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, const uint32_t* minact, const uint32_t* maxact,
+                         int qstart, int qend) {
   const int lane = W.lane;
   auto npos = [&](int q) { return q < nq ? npq[q] : 0; };
   int q = 0, np = 0;
@@ -756,12 +841,12 @@ __device__ void s2_sweep(S2W& W, const int32_t* npq, int nq, const uint32_t* min
         if (lane == 0) {
           W.alist[qoff] = low;
           const int sl = W.pushed & (kS2Ring - 1);
-          W.ring->map[sl] = position;
-          W.ring->score[sl] = b.score;
-          W.ring->consec[sl] = b.consec;
-          W.ring->tracei[sl] = b.tracei;
-          W.ring->root[sl] = b.root;
-          W.ring->hit[sl] = low;
+          s2_ring.map[sl] = position;
+          s2_ring.score[sl] = b.score;
+          s2_ring.consec[sl] = b.consec;
+          s2_ring.tracei[sl] = b.tracei;
+          s2_ring.root[sl] = b.root;
+          s2_ring.hit[sl] = low;
         }
       }
     } else if (high - low > 1 && high - low <= 64) {
@@ -785,7 +870,7 @@ __device__ void s2_sweep(S2W& W, const int32_t* npq, int nq, const uint32_t* min
           if (n > kS2Nsufflookback && n > 1 && qd - kS2K > kS2Sufflookback) break;  // later entries only shrink
           if (n <= 1 || qd - kS2K <= kS2Sufflookback / 2) maxadj = n;
           if (n <= kS2Nsufflookback || qd - kS2K <= kS2Sufflookback) maxnon = n;
-          if (lane == 0) fr[n] = en > 0 ? 0 : -1;
+          if (lane == 0) s2_fr[n] = en > 0 ? 0 : -1;
           nfr = n + 1;
         }
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -808,14 +893,24 @@ __device__ void s2_sweep(S2W& W, const int32_t* npq, int nq, const uint32_t* min
             b = {kS2K, (int)position, -1, -1, 0, -1};
             maxseen = maxnon;
           }
+          bool fast = false;
           if (overall < kS2GreedyConsec) {
+            const int kmax = min(min(maxseen, nfr - 1), np - 1);
+            if (kmax < 64) {
+              int f = lane <= kmax ? s2_fr[lane] : -1;
+              fast = s2_dloop_fast(W, pf, np, kmax, q, position, b, true, true, f);
+              if (fast && lane <= kmax) s2_fr[lane] = f;
+              __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            }
+          }
+          if (overall < kS2GreedyConsec && !fast) {
             int last_tr = -1;
             for (int kk = 0; kk < np && b.consec < kS2EnoughConsec && kk <= maxseen && kk < nfr; kk++) {
-              const int f = fr[kk];
+              const int f = s2_u(s2_fr[kk]);
               if (f != -1) {
                 int qd;
                 const int nf = s2_entry_eval(W, pf, ec, np, kk, f, q, position, last_tr, b, true, &qd);
-                if (lane == 0) fr[kk] = nf;
+                if (lane == 0) s2_fr[kk] = nf;
                 __atomic_signal_fence(__ATOMIC_SEQ_CST);
               }
             }
@@ -875,18 +970,18 @@ __device__ void s2_sweep(S2W& W, const int32_t* npq, int nq, const uint32_t* min
         const int r = lanes_below(am, lane);
         W.alist[qoff + r] = low + lane;
         const int sl = (W.pushed + r) & (kS2Ring - 1);
-        W.ring->map[sl] = cm;
-        W.ring->score[sl] = mb.score;
-        W.ring->consec[sl] = mb.consec;
-        W.ring->tracei[sl] = mb.tracei;
-        W.ring->root[sl] = mb.root;
-        W.ring->hit[sl] = low + lane;
+        s2_ring.map[sl] = cm;
+        s2_ring.score[sl] = mb.score;
+        s2_ring.consec[sl] = mb.consec;
+        s2_ring.tracei[sl] = mb.tracei;
+        s2_ring.root[sl] = mb.root;
+        s2_ring.hit[sl] = low + lane;
       }
       nact = __popcll(am);
     } else {
       int best_score = 0, best_hit = -1, best_fhit = 0, best_consec = 0;
       if (high - low > 1) {
-        s2_mult(W, q, qoff, low, high, np, last, fr);
+        s2_mult(W, q, qoff, low, high, np, last);
         int bs = 0, bh = -1;
         for (int c0 = low; c0 < high; c0 += 64) {
           const int i = c0 + lane;
@@ -951,12 +1046,12 @@ __device__ void s2_sweep(S2W& W, const int32_t* npq, int nq, const uint32_t* min
             W.alist[qoff + r] = i;
             if (high - low <= kS2Ring) {
               const int sl = (W.pushed + r) & (kS2Ring - 1);
-              W.ring->map[sl] = x.map;
-              W.ring->score[sl] = x.score;
-              W.ring->consec[sl] = x.consec;
-              W.ring->tracei[sl] = x.tracei;
-              W.ring->root[sl] = x.root;
-              W.ring->hit[sl] = i;
+              s2_ring.map[sl] = x.map;
+              s2_ring.score[sl] = x.score;
+              s2_ring.consec[sl] = x.consec;
+              s2_ring.tracei[sl] = x.tracei;
+              s2_ring.root[sl] = x.root;
+              s2_ring.hit[sl] = i;
             }
           }
           nact += __popcll(m);
@@ -974,10 +1069,10 @@ __device__ void s2_sweep(S2W& W, const int32_t* npq, int nq, const uint32_t* min
         W.poff[np] = qoff;
         W.pstart[np] = start;
         const int s = np & (kS2Meta - 1);
-        W.ring->eq[s] = q;
-        W.ring->en[s] = nact;
-        W.ring->eoff[s] = qoff;
-        W.ring->estart[s] = start;
+        s2_ring.eq[s] = q;
+        s2_ring.en[s] = nact;
+        s2_ring.eoff[s] = qoff;
+        s2_ring.estart[s] = start;
       }
       if (ringed) W.pushed += nact;
       np++;
@@ -1393,8 +1488,6 @@ __global__ __launch_bounds__(64) void s2b_kernel(
   S2_MARK(3);
   // ---- align_compute_scores_lookback: the sweep on lane 0 ----
   {
-    __shared__ S2Ring ring;
-    __shared__ int fr[128];
     S2W W;
     W.hits = hits;
     W.off = off;
@@ -1404,17 +1497,38 @@ __global__ __launch_bounds__(64) void s2b_kernel(
     W.pn = pathq;
     W.poff = pathh;
     W.pstart = reinterpret_cast<int*>(run);
-    W.ring = &ring;
     W.pushed = 0;
     W.tracectr = 0;
     W.splicingp = P.splicingp;
     W.lane = lane;
     W.maxintronlen = P.maxintronlen;
-    s2_sweep(W, npq, nq, minact, maxact, qstart, qend, fr);
+    s2_sweep(W, npq, nq, minact, maxact, qstart, qend);
   }
   wave_sync();
 
   S2_MARK(4);
+}
+
+// traceback_one over the LDS link table: link[i] = predecessor hit index (0x7fffffff: none) with bit 31
+// set when the hit has fewer than MIN_TERMINAL_NCONSECUTIVE consecutive matches; map[i] its chrpos
+constexpr int kS2cCap = 4096;  // hits whose links fit the s2c kernel's LDS (12 B each)
+constexpr uint32_t kS2NoPred = 0x7fffffffu;
+template <class F>
+__device__ void s2_walk_lds(const uint32_t* link, const uint32_t* map, int gi, F visit) {
+  uint32_t w = link[gi];
+  while (w & 0x80000000u) {  // prune the 3' end
+    const uint32_t pr = w & kS2NoPred;
+    if (pr == kS2NoPred) return;
+    gi = (int)pr;
+    w = link[gi];
+  }
+  for (;;) {
+    if ((int)map[gi] >= 0) visit(gi);
+    const uint32_t pr = w & kS2NoPred;
+    if (pr == kS2NoPred) return;
+    gi = (int)pr;
+    w = link[gi];
+  }
 }
 
 // cells, traceback_one, Stage2_filter_unique, convert_to_nucleotides
@@ -1523,19 +1637,37 @@ __global__ __launch_bounds__(64) void s2c_kernel(
 
   S2_MARK(5);
   // ---- traceback_one per selected cell: length and extent of the converted list ----
+  // the links go to LDS first (coalesced loads), so the pointer chases run at LDS latency
+  extern __shared__ uint32_t s2c_lds[];
+  uint32_t* llink = s2c_lds;
+  uint32_t* lmap = s2c_lds + kS2cCap;
+  uint32_t* lq = s2c_lds + 2 * kS2cCap;
+  const bool lds_walk = T <= kS2cCap;
+  if (lds_walk && npaths > 0) {
+    for (int i = lane; i < T; i += 64) {
+      const S2Hit& x = hits[i];
+      const uint32_t pr = x.fpos >= 0 ? (uint32_t)(off[x.fpos] + x.fhit) : kS2NoPred;
+      llink[i] = pr | (x.consec < kS2MinTerminal ? 0x80000000u : 0u);
+      lmap[i] = x.map;
+      lq[i] = (uint32_t)x.q;
+    }
+  }
+  wave_sync();
   if (lane == 0) {
     for (int p = 0; p < npaths; p++) {
       int n = 0, top = -1, bottom = -1;
-      s2_walk(hits, off, cand[p], [&](int gi) {
+      auto vis = [&](int gi) {
         if (n == 0) top = gi;
         bottom = gi;
         n++;
-      });
+      };
+      if (lds_walk) s2_walk_lds(llink, lmap, cand[p], vis);
+      else s2_walk(hits, off, cand[p], vis);
       S2Path r;
       r.cell = cand[p];
       r.n = n;
-      r.start = n ? hits[bottom].map : 0u;
-      r.end = n ? hits[top].map + (uint32_t)(kS2K - 1) : 0u;
+      r.start = n ? (lds_walk ? lmap[bottom] : hits[bottom].map) : 0u;
+      r.end = n ? (lds_walk ? lmap[top] : hits[top].map) + (uint32_t)(kS2K - 1) : 0u;
       pth[p] = r;
     }
   }
@@ -1597,11 +1729,19 @@ __global__ __launch_bounds__(64) void s2c_kernel(
     const int n = x.n;
     if (lane == 0) {  // entries, 3' end first
       int e = 0;
-      s2_walk(hits, off, x.cell, [&](int gi) {
-        pathq[e] = hits[gi].q;
-        pathh[e] = (int)hits[gi].map;
-        e++;
-      });
+      if (lds_walk) {
+        s2_walk_lds(llink, lmap, x.cell, [&](int gi) {
+          pathq[e] = (int)lq[gi];
+          pathh[e] = (int)lmap[gi];
+          e++;
+        });
+      } else {
+        s2_walk(hits, off, x.cell, [&](int gi) {
+          pathq[e] = hits[gi].q;
+          pathh[e] = (int)hits[gi].map;
+          e++;
+        });
+      }
     }
     wave_sync();
     // records per entry in generation (prepend) order: [gap holder], fills, the observed pair
@@ -1713,7 +1853,10 @@ hipError_t launch_s2c(int nproblems, hipStream_t stream, const DevStage2Problem*
   if (e == hipSuccess)
     e = hipLaunchKernel(reinterpret_cast<void*>(&s2b_kernel), dim3(nproblems), dim3(64), args, 0, stream);
   if (e == hipSuccess)
-    e = hipLaunchKernel(reinterpret_cast<void*>(&s2c_kernel), dim3(nproblems), dim3(64), args, 0, stream);
+    e = hipFuncSetAttribute(reinterpret_cast<void*>(&s2c_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(12 * kS2cCap));
+  if (e == hipSuccess)
+    e = hipLaunchKernel(reinterpret_cast<void*>(&s2c_kernel), dim3(nproblems), dim3(64), args, 12 * kS2cCap, stream);
   return e;
 }
 

@@ -88,7 +88,7 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] == "gg":
         return main_gg()
     if len(sys.argv) > 1 and sys.argv[1] == "s2":
-        return main_s2()
+        return main_s2(int(sys.argv[2]) if len(sys.argv) > 2 else 10000)
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
     lib = gmapdp.load_library(os.path.join(ROOT, "gmap-2024_amd", "lib", "libgmapdp_oitiming.so"))
     lib.gmapdp_debug_oi_marks.argtypes = [C.c_void_p]
