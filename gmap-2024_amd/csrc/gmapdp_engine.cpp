@@ -251,7 +251,7 @@ struct gmapdp_ctx {
   HostBuf hin, hout;   // their pinned host images
   DevBuf gprobs, gorder, sprob, gresults;
   DevBuf cprobs, corder, cresults, cscratch;  // Dynprog_cdna_gap batches
-  DevBuf oprobs, oresults, oscratch, onpos, omap, otable, odiag;  // stage-2 seeding batches
+  DevBuf oprobs, oresults, oscratch, onpos, omap, otable, odiag, opool, opoolctr;  // stage-2 seeding batches
   DevBuf s2probs, s2results, s2scratch, s2counters, s2paths, s2pairs, s2qseq;  // Stage2_compute batches
   std::string err;
 };
@@ -1722,10 +1722,19 @@ struct gmapdp_oligo_plan {
   uint64_t* d_pool = nullptr;
   unsigned long long* d_pool_counter = nullptr;
   unsigned long long pool_cap = 0;
+  // A plan made inside a synchronous batch call borrows the context's grow-only buffers: no
+  // hipMalloc / hipFree per call (hipFree waits for the whole device, which would serialise the
+  // shim's concurrent batches).  `ord` is the host image of d_probs, kept until the plan is freed.
+  bool borrowed = false;
+  std::vector<DevOligoProblem> ord;
 };
 
 static void oligo_plan_free(gmapdp_oligo_plan* p) {
   if (!p) return;
+  if (p->borrowed) {
+    delete p;
+    return;
+  }
   if (p->d_probs) (void)hipFree(p->d_probs);
   if (p->d_scratch) (void)hipFree(p->d_scratch);
   if (p->d_pool) (void)hipFree(p->d_pool);
@@ -1735,8 +1744,10 @@ static void oligo_plan_free(gmapdp_oligo_plan* p) {
 
 extern "C" {
 
-int gmapdp_oligo_plan_create(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problems, int n, const char* qseq_uc,
-                             size_t qbytes, gmapdp_oligo_plan** plan) {
+}  // extern "C"
+
+static int oligo_plan_build(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problems, int n, const char* qseq_uc,
+                            size_t qbytes, gmapdp_oligo_plan** plan, bool borrow) {
   if (!ctx || !plan || n < 0 || (n > 0 && (!problems || !qseq_uc))) return GMAPDP_EINVAL;
   *plan = nullptr;
   if (!ctx->d_genome) return GMAPDP_ENOGENOME;
@@ -1788,27 +1799,49 @@ int gmapdp_oligo_plan_create(gmapdp_ctx* ctx, const gmapdp_oligo_problem* proble
   P->n = n;
   P->table_cap = toff;
   P->diag_cap = doff;
-  std::vector<DevOligoProblem> ord;
+  std::vector<DevOligoProblem>& ord = P->ord;
   ord.reserve(n);
   for (auto& kv : classes) {
     P->launches.push_back({(int)ord.size(), (int)kv.second.size()});
     P->umax.push_back(kv.first);
     for (int i : kv.second) ord.push_back(dev[i]);
   }
-  hipError_t e = hipMalloc(&P->d_probs, sizeof(DevOligoProblem) * std::max(n, 1));
-  if (e == hipSuccess) e = hipMalloc(&P->d_scratch, std::max<size_t>(soff, 256));
   if (const char* ev = std::getenv("GMAPDP_OLIGO_POOL_SLOTS")) pslots = std::strtoull(ev, nullptr, 10);  // tests
   P->pool_cap = pslots;
-  if (e == hipSuccess) e = hipMalloc(&P->d_pool, sizeof(uint64_t) * std::max<size_t>(pslots, 1));
-  if (e == hipSuccess) e = hipMalloc(&P->d_pool_counter, sizeof(unsigned long long));
-  if (e == hipSuccess && n)
-    e = hipMemcpy(P->d_probs, ord.data(), sizeof(DevOligoProblem) * n, hipMemcpyHostToDevice);
+  hipError_t e = hipSuccess;
+  if (borrow) {
+    P->borrowed = true;
+    e = ctx->oprobs.ensure(sizeof(DevOligoProblem) * std::max(n, 1));
+    if (e == hipSuccess) e = ctx->oscratch.ensure(std::max<size_t>(soff, 256));
+    if (e == hipSuccess) e = ctx->opool.ensure(sizeof(uint64_t) * std::max<size_t>(pslots, 1));
+    if (e == hipSuccess) e = ctx->opoolctr.ensure(sizeof(unsigned long long));
+    P->d_probs = (DevOligoProblem*)ctx->oprobs.p;
+    P->d_scratch = (unsigned char*)ctx->oscratch.p;
+    P->d_pool = (uint64_t*)ctx->opool.p;
+    P->d_pool_counter = (unsigned long long*)ctx->opoolctr.p;
+    if (e == hipSuccess && n)
+      e = hipMemcpyAsync(P->d_probs, ord.data(), sizeof(DevOligoProblem) * n, hipMemcpyHostToDevice, ctx->stream);
+  } else {
+    e = hipMalloc(&P->d_probs, sizeof(DevOligoProblem) * std::max(n, 1));
+    if (e == hipSuccess) e = hipMalloc(&P->d_scratch, std::max<size_t>(soff, 256));
+    if (e == hipSuccess) e = hipMalloc(&P->d_pool, sizeof(uint64_t) * std::max<size_t>(pslots, 1));
+    if (e == hipSuccess) e = hipMalloc(&P->d_pool_counter, sizeof(unsigned long long));
+    if (e == hipSuccess && n)
+      e = hipMemcpy(P->d_probs, ord.data(), sizeof(DevOligoProblem) * n, hipMemcpyHostToDevice);
+  }
   if (e != hipSuccess) {
     oligo_plan_free(P);
     return fail(ctx, GMAPDP_ENOMEM, "oligo plan: %s", e);
   }
   *plan = P;
   return GMAPDP_OK;
+}
+
+extern "C" {
+
+int gmapdp_oligo_plan_create(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problems, int n, const char* qseq_uc,
+                             size_t qbytes, gmapdp_oligo_plan** plan) {
+  return oligo_plan_build(ctx, problems, n, qseq_uc, qbytes, plan, false);
 }
 
 size_t gmapdp_oligo_plan_positions_capacity(const gmapdp_oligo_plan* plan) { return plan ? plan->table_cap : 0; }
@@ -1845,7 +1878,7 @@ int gmapdp_oligo_mappings_batch(gmapdp_ctx* ctx, const gmapdp_oligo_problem* pro
   if (!ctx->d_genome) return GMAPDP_ENOGENOME;
   if (n == 0) return GMAPDP_OK;
   gmapdp_oligo_plan* plan = nullptr;
-  int rc = gmapdp_oligo_plan_create(ctx, problems, n, qseq_uc, qbytes, &plan);
+  int rc = oligo_plan_build(ctx, problems, n, qseq_uc, qbytes, &plan, true);
   if (rc) return rc;
   const size_t toff = plan->table_cap, doff = plan->diag_cap;
   if (toff > positions_capacity || doff > diagonal_capacity || (toff && !positions) || (doff && !diagonals)) {
@@ -1870,6 +1903,7 @@ int gmapdp_oligo_mappings_batch(gmapdp_ctx* ctx, const gmapdp_oligo_problem* pro
                              (int32_t*)ctx->onpos.p, (int32_t*)ctx->omap.p, (uint32_t*)ctx->otable.p,
                              (int32_t*)ctx->odiag.p, nullptr);
   if (rc) {
+    (void)hipStreamSynchronize(s);
     oligo_plan_free(plan);
     return rc;
   }
@@ -1929,7 +1963,7 @@ extern "C" int gmapdp_stage2_batch(gmapdp_ctx* ctx, const gmapdp_stage2_problem*
     d.scratch_offset = 0;
   }
   gmapdp_oligo_plan* plan = nullptr;
-  int rc = gmapdp_oligo_plan_create(ctx, op.data(), n, qseq_uc, qbytes, &plan);
+  int rc = oligo_plan_build(ctx, op.data(), n, qseq_uc, qbytes, &plan, true);
   if (rc) return rc;
   const size_t toff = plan->table_cap, doff = plan->diag_cap;
   hipStream_t s = ctx->stream;
@@ -1955,12 +1989,16 @@ extern "C" int gmapdp_stage2_batch(gmapdp_ctx* ctx, const gmapdp_stage2_problem*
   rc = gmapdp_oligo_plan_run(ctx, plan, (const char*)ctx->qseq_uc.p, (gmapdp_oligo_result*)ctx->oresults.p,
                              (int32_t*)ctx->onpos.p, (int32_t*)ctx->omap.p, (uint32_t*)ctx->otable.p,
                              (int32_t*)ctx->odiag.p, nullptr);
-  oligo_plan_free(plan);
-  if (rc) return rc;
+  if (rc) {
+    (void)hipStreamSynchronize(s);
+    oligo_plan_free(plan);
+    return rc;
+  }
   // the chaining scratch is sized exactly from the seeding (totalpositions, ndiagonals per call)
   std::vector<gmapdp_oligo_result> ores(n);
   e = hipMemcpyAsync(ores.data(), ctx->oresults.p, sizeof(gmapdp_oligo_result) * n, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
+  oligo_plan_free(plan);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "stage-2 seeding: %s", e);
   size_t scratch = 0, qsum = 0;
   for (int i = 0; i < n; i++) {

@@ -32,6 +32,7 @@
  * the answer (the API is synchronous).  Here a call becomes a request on a process-wide queue and the
  * calling thread sleeps on it.  GMAPDP_SHIM_DISPATCHERS (default 4) dispatcher threads each own an
  * engine context (its own streams and HBM copy of the genome), so that many batches are in flight;
+ * stage-2 calls have their own queue and GMAPDP_SHIM_STAGE2_DISPATCHERS (default 2) dispatchers;
  * a free dispatcher takes every request queued meanwhile and runs them together: all single / end /
  * genome gaps in one gmapdp_dynprog_batch, cDNA gaps and stage-2 seeding in their own batches.  The
  * callers then build their List_T from their own results in their own Pairpool.  With many worker
@@ -259,9 +260,11 @@ typedef struct shim_req {
   struct shim_req *next;
 } shim_req;
 
+/* Two queues: 0 for the Dynprog_* calls (short, ~150 per read), 1 for stage 2 (one long call per
+   read), so that a stage-2 batch never holds back the DP calls queued behind it. */
 static pthread_mutex_t q_lock = PTHREAD_MUTEX_INITIALIZER;
-static pthread_cond_t q_cond = PTHREAD_COND_INITIALIZER;
-static shim_req *q_head = NULL, *q_tail = NULL;
+static pthread_cond_t q_cond[2] = {PTHREAD_COND_INITIALIZER, PTHREAD_COND_INITIALIZER};
+static shim_req *q_head[2] = {NULL, NULL}, *q_tail[2] = {NULL, NULL};
 static int dispatcher_started = 0;
 static __thread shim_req *tl_req = NULL;
 
@@ -299,12 +302,12 @@ static void shim_run (shim_req *batch);
 static void *
 shim_dispatch (void *arg) {
   shim_req *batch, *r, *next;
-  (void) arg;
+  const int qi = (int) (intptr_t) arg;
   for (;;) {
     pthread_mutex_lock(&q_lock);
-    while (q_head == NULL) pthread_cond_wait(&q_cond, &q_lock);
-    batch = q_head;
-    q_head = q_tail = NULL;
+    while (q_head[qi] == NULL) pthread_cond_wait(&q_cond[qi], &q_lock);
+    batch = q_head[qi];
+    q_head[qi] = q_tail[qi] = NULL;
     pthread_mutex_unlock(&q_lock);
     shim_run(batch);
     pthread_mutex_lock(&q_lock);
@@ -324,7 +327,8 @@ shim_submit (shim_req *r) {
   pthread_t th;
   pthread_attr_t attr;
   const char *st;
-  int nd, k;
+  int nd, nd2, k;
+  const int qi = r->kind >= K_OLIGO ? 1 : 0;
   pthread_mutex_lock(&q_lock);
   if (!dispatcher_started) {
     st = getenv("GMAPDP_SHIM_STATS");
@@ -332,19 +336,23 @@ shim_submit (shim_req *r) {
     st = getenv("GMAPDP_SHIM_DISPATCHERS");
     nd = st != NULL ? atoi(st) : 4;
     if (nd < 1) nd = 1;
+    st = getenv("GMAPDP_SHIM_STAGE2_DISPATCHERS");
+    nd2 = st != NULL ? atoi(st) : 2;
+    if (nd2 < 1) nd2 = 1;
     pthread_attr_init(&attr);
     pthread_attr_setdetachstate(&attr, PTHREAD_CREATE_DETACHED);
-    for (k = 0; k < nd; k++)
-      if (pthread_create(&th, &attr, shim_dispatch, NULL) != 0) shim_refuse("a dispatcher thread (pthread_create)");
+    for (k = 0; k < nd + nd2; k++)
+      if (pthread_create(&th, &attr, shim_dispatch, (void *) (intptr_t) (k < nd ? 0 : 1)) != 0)
+        shim_refuse("a dispatcher thread (pthread_create)");
     pthread_attr_destroy(&attr);
     dispatcher_started = 1;
   }
   r->done = 0;
   r->next = NULL;
-  if (q_tail != NULL) q_tail->next = r;
-  else q_head = r;
-  q_tail = r;
-  pthread_cond_signal(&q_cond);
+  if (q_tail[qi] != NULL) q_tail[qi]->next = r;
+  else q_head[qi] = r;
+  q_tail[qi] = r;
+  pthread_cond_signal(&q_cond[qi]);
   while (!r->done) pthread_cond_wait(&r->cv, &q_lock);
   pthread_mutex_unlock(&q_lock);
 }
