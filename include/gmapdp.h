@@ -373,7 +373,7 @@ void gmapdp_oligo_plan_destroy (gmapdp_oligo_plan *plan);
  * diag_lookback 120, suffnconsecutive 20), localp, skip_repetitive_p, favor_right_p false,
  * max_nalignments 10; Stage2_setup (gmap.c:6544) without cross-species canonical scoring, without SNPs,
  * STANDARD mode, sufflookback 60, nsufflookback 5.  queryseq_ptr = qseq + qoff (case as given, the
- * Pair cdna), queryuc_ptr = qseq_uc + qoff.  Domain as gmapdp_oligo_problem (querylength > 8), and
+ * Pair cdna), queryuc_ptr = qseq_uc + qoff.  Domain as for gmapdp_oligo_problem: querylength > 8, and
  * genomic positions below 2^31 (Pairpool_push drops negative ones; the engine does not model that). */
 typedef struct {
   int32_t qoff;
