@@ -103,6 +103,22 @@ int orc_cdna_gap (const char *qbuf, const char *qucbuf, int qposL, int qposR, in
                   unsigned int chrhigh, int watsonp, int genestrand, int jump_late_p, int extraband_paired,
                   double defect_rate, int dynprogindex, int *scalars, OrcPair *out, int max_pairs);
 
+/* Dynprog_microexon_int (dynprog_single.c:900; microexon_oracle.c).  rsequence / rsequenceuc: the
+   query slice (stage3.c:9664 passes queryseq + querydp5 and roffset = querydp5).
+   orc_microexon_candidates lists the candidates in the reference's loop order: cands[4 k..] = cL, cR,
+   candidate, middlelength; positions / models [2 k..] = the splice sites of prob2 and prob3 (models
+   as orc_genome_splice_sites).  Returns their number, -1 when cap is too small, -2 for cdna_direction 0.
+   orc_microexon_int takes those probabilities (cand_probs[2 k], [2 k + 1], the host's
+   Maxent_hr_*_prob values).  scalars[0..1] = dynprogindex(after), microintrontype; dscalars[0..1] =
+   bestprob2, bestprob3.  Returns npairs (list order) or -1 for NULL. */
+int orc_microexon_candidates (const char *rsequence, const char *rsequenceuc, int rlength, int goffsetL,
+                              int rev_goffsetR, int cdna_direction, unsigned int chroffset, unsigned int chrhigh,
+                              int watsonp, int *cands, unsigned int *positions, int *models, int cap);
+int orc_microexon_int (const char *rsequence, const char *rsequenceuc, int rlength, int roffset, int goffsetL,
+                       int rev_goffsetR, int cdna_direction, unsigned int chroffset, unsigned int chrhigh,
+                       int watsonp, int genestrand, int dynprogindex, const double *cand_probs, int *scalars,
+                       double *dscalars, OrcPair *out, int max_pairs);
+
 /* The genome set by orc_set_genome. */
 const char *orc_genome_seq (unsigned int *length);
 

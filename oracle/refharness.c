@@ -337,6 +337,30 @@ refh_genome_gap (const char *rsequence, const char *rsequenceuc, int rlength, in
   return flatten(pairs, out, max_pairs);
 }
 
+/* Dynprog_microexon_int (dynprog_single.c:900) as stage3.c:9664 calls it: rsequence is the query slice
+   (queryseq + roffset), the MaxEnt probabilities are the reference's own.  scalars[0..1] =
+   dynprogindex(after), microintrontype; dscalars[0..1] = bestprob2, bestprob3.  Returns the number of
+   pairs (list order) or -1 for NULL. */
+int
+refh_microexon_int (const char *rsequence, const char *rsequenceuc, int rlength, int roffset, int goffsetL,
+                    int rev_goffsetR, int cdna_direction, unsigned int chroffset, unsigned int chrhigh, int watsonp,
+                    int genestrand, int dynprogindex, int *scalars, double *dscalars, RefPair *out, int max_pairs) {
+  List_T pairs;
+  int microintrontype = REFH_UNSET;
+  double prob2 = -1.0, prob3 = -1.0;
+  Pairpool_reset(pairpool);
+  pairs = Dynprog_microexon_int(&prob2, &prob3, &dynprogindex, &microintrontype, (char *) rsequence,
+                                (char *) rsequenceuc, rlength, roffset, goffsetL, rev_goffsetR, cdna_direction,
+                                (char *) rsequence - roffset, (char *) rsequenceuc - roffset, (Univcoord_T) chroffset,
+                                (Univcoord_T) chrhigh, watsonp ? true : false, genestrand, genome, genome, pairpool);
+  scalars[0] = dynprogindex;
+  scalars[1] = microintrontype;
+  dscalars[0] = prob2;
+  dscalars[1] = prob3;
+  if (pairs == NULL) return -1;
+  return flatten(pairs, out, max_pairs);
+}
+
 /* Dynprog_cdna_gap (dynprog_cdna.c:787).  The query is one buffer: rsequenceL = qbuf + qposL,
    rev_rsequenceR = qbuf + qposR (the R piece's LAST character).  scalars[0..2] =
    dynprogindex(after), traceback_score (REFH_UNSET where the reference leaves it unwritten),

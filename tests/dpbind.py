@@ -742,3 +742,150 @@ def stage2_problem(rng, genome: bytes, edge=False):
     p["splicingp"] = 0 if rng.random() < 0.15 else 1
     p["maxintronlen"] = rng.choice([500000, 500000, 500000, 2000, 200])
     return p
+
+
+# ---------------------------------------------------------------------------
+# Dynprog_microexon_int (dynprog_single.c:900)
+# ---------------------------------------------------------------------------
+_ME_ARGS = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint, C.c_uint, C.c_int]
+MAXCANDS = 4096
+
+
+def _me_args(p):
+    return (p["q"], p["quc"], p["rlength"], p["goffsetL"], p["rev_goffsetR"], p["cdna_direction"], p["chroffset"],
+            p["chrhigh"], p["watsonp"])
+
+
+def _orc_microexon_candidates(self, p):
+    """[(cL, cR, candidate, middlelength, pos2, model2, pos3, model3)] in the reference's loop order, or
+    None for cdna_direction 0."""
+    f = self.lib.orc_microexon_candidates
+    if not getattr(self, "_mc_ready", False):
+        f.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint, C.c_uint, C.c_int,
+                      C.POINTER(C.c_int), C.POINTER(C.c_uint), C.POINTER(C.c_int), C.c_int]
+        f.restype = C.c_int
+        self._mc_c = (C.c_int * (4 * MAXCANDS))()
+        self._mc_p = (C.c_uint * (2 * MAXCANDS))()
+        self._mc_m = (C.c_int * (2 * MAXCANDS))()
+        self._mc_ready = True
+    n = f(*_me_args(p), self._mc_c, self._mc_p, self._mc_m, MAXCANDS)
+    assert n >= -2 and n != -1
+    if n == -2:
+        return None
+    c, ps, ms = self._mc_c, self._mc_p, self._mc_m
+    return [(c[4 * k], c[4 * k + 1], c[4 * k + 2], c[4 * k + 3], ps[2 * k], ms[2 * k], ps[2 * k + 1], ms[2 * k + 1])
+            for k in range(n)]
+
+
+def _orc_microexon_int(self, p, cand_probs):
+    """((dynprogindex after, microintrontype), (bestprob2, bestprob3), pairs-or-None); cand_probs: the
+    flat [prob2, prob3, ...] list of the candidates."""
+    self._before_call()
+    f = self.lib.orc_microexon_int
+    if not getattr(self, "_me_ready", False):
+        f.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint, C.c_uint,
+                      C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_double),
+                      C.POINTER(Pair), C.c_int]
+        f.restype = C.c_int
+        self._me_s = (C.c_int * 2)()
+        self._me_d = (C.c_double * 2)()
+        self._me_ready = True
+    cp = (C.c_double * max(1, len(cand_probs)))(*cand_probs)
+    n = f(p["q"], p["quc"], p["rlength"], p["roffset"], p["goffsetL"], p["rev_goffsetR"], p["cdna_direction"],
+          p["chroffset"], p["chrhigh"], p["watsonp"], p["genestrand"], p["dynprogindex"], cp, self._me_s, self._me_d,
+          self._pairs, MAXPAIRS)
+    assert -1 <= n <= MAXPAIRS
+    return tuple(self._me_s), tuple(self._me_d), (None if n < 0 else [self._pairs[i].key() for i in range(n)])
+
+
+def _ref_microexon_int(self, p):
+    self._before_call()
+    f = self.lib.refh_microexon_int
+    if not getattr(self, "_me_ready", False):
+        f.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint, C.c_uint,
+                      C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(Pair), C.c_int]
+        f.restype = C.c_int
+        self._me_s = (C.c_int * 2)()
+        self._me_d = (C.c_double * 2)()
+        self._me_ready = True
+    n = f(p["q"], p["quc"], p["rlength"], p["roffset"], p["goffsetL"], p["rev_goffsetR"], p["cdna_direction"],
+          p["chroffset"], p["chrhigh"], p["watsonp"], p["genestrand"], p["dynprogindex"], self._me_s, self._me_d,
+          self._pairs, MAXPAIRS)
+    assert -1 <= n <= MAXPAIRS
+    return tuple(self._me_s), tuple(self._me_d), (None if n < 0 else [self._pairs[i].key() for i in range(n)])
+
+
+Oracle.microexon_candidates = _orc_microexon_candidates
+Oracle.microexon_int = _orc_microexon_int
+Ref.microexon_int = _ref_microexon_int
+
+
+def microexon_probs(ref, cands, chroffset):
+    """The host's Maxent_hr_*_prob at the candidates' splice sites (flat prob2, prob3 list)."""
+    out = []
+    for c in cands or []:
+        out.append(ref.maxent(c[5], c[4], chroffset))
+        out.append(ref.maxent(c[7], c[6], chroffset))
+    return out
+
+
+def microexon_problem(rng, genome: bytearray, edge=False, at=None):
+    """One Dynprog_microexon_int-shaped call (stage3.c:9664): the query gap between two exons' anchors
+    (rlength = queryjump), goffsetL = genomedp5 just after the left anchor, rev_goffsetR = genomedp3 just
+    before the right one.  Usually a microexon is planted: left piece | intron (5' GT..AG 3' in the
+    cDNA's sense) | microexon | intron | right piece, sometimes with decoy copies of the microexon in the
+    introns, lower-case or mismatched query characters, or a random query.  Mutates `genome` in place;
+    the chromosome sits 1000 nt inside it.  `at`: a list holding the next free chromosome position, so
+    that consecutive problems do not overwrite each other's sites (advanced past this problem)."""
+    chroffset, chrhigh = 1000, len(genome) - 1000
+    watsonp = rng.random() < 0.6
+    cdna_direction = rng.choice([1, 1, -1, -1, 0]) if edge else rng.choice([1, -1])
+    i1, i2, i3, i4 = (b"G", b"T", b"A", b"G") if cdna_direction >= 0 else (b"C", b"T", b"A", b"C")
+    lenL = rng.randint(1, 14)
+    lenM = rng.randint(3, 12)
+    lenR = rng.randint(1, 14)
+    intronA = rng.randint(12, 1200) if not edge else rng.choice([12, 15, 30, rng.randint(12, 20000)])
+    intronB = rng.randint(12, 1200) if not edge else rng.choice([12, 15, 30, rng.randint(12, 20000)])
+    span = lenL + intronA + lenM + intronB + lenR
+    if at is not None:
+        goffsetL = at[0] + rng.randint(0, 50)
+        at[0] = goffsetL + span
+        assert at[0] < chrhigh - chroffset - 50, "genome too small for the problems"
+    else:
+        goffsetL = rng.randint(50, chrhigh - chroffset - span - 50)
+    seq = bytearray(rng.choice(b"ACGT") for _ in range(span))
+    micro = bytes(rng.choice(b"ACGT") for _ in range(lenM))
+    a = lenL
+    seq[a:a + 2] = i1 + i2
+    seq[a + intronA - 2:a + intronA] = i3 + i4
+    seq[a + intronA:a + intronA + lenM] = micro
+    b = a + intronA + lenM
+    seq[b:b + 2] = i1 + i2
+    seq[b + intronB - 2:b + intronB] = i3 + i4
+    if rng.random() < 0.3:  # decoys: flanked copies of the microexon inside the introns
+        for _ in range(rng.randint(1, 3)):
+            which = rng.random() < 0.5
+            lo, hi = (a + 12, a + intronA - lenM - 12) if which else (b + 12, b + intronB - lenM - 12)
+            if hi > lo:
+                s = rng.randint(lo, hi)
+                seq[s - 2:s] = i3 + i4
+                seq[s:s + lenM] = micro
+                seq[s + lenM:s + lenM + 2] = i1 + i2
+    for k in range(span):
+        _strand_set(genome, goffsetL + k, chroffset, chrhigh, watsonp, seq[k])
+    q = bytearray(seq[:lenL] + micro + seq[span - lenR:])
+    kind = rng.random()
+    if kind < 0.1:
+        q = bytearray(rng.choice(b"ACGT") for _ in range(len(q)))
+    elif kind < 0.25:
+        j = rng.randrange(len(q))
+        q[j] = rng.choice(b"ACGT")
+    quc = bytes(q)
+    if rng.random() < 0.1:
+        j = rng.randrange(len(q))
+        q[j] = ord(chr(q[j]).lower())
+    q = bytes(q)
+    roffset = rng.randint(0, 1500)
+    return dict(q=q, quc=quc, rlength=len(q), roffset=roffset, goffsetL=goffsetL,
+                rev_goffsetR=goffsetL + span - 1, cdna_direction=cdna_direction, chroffset=chroffset,
+                chrhigh=chrhigh, watsonp=int(watsonp), genestrand=0, dynprogindex=rng.choice([1, 5, -1, -7]))

@@ -343,6 +343,78 @@ def load_stage2(path):
     return z["genome"].tobytes(), probs, outs
 
 
+ME_PARAMS = ["rlength", "roffset", "goffsetL", "rev_goffsetR", "cdna_direction", "chroffset", "chrhigh", "watsonp",
+             "genestrand", "dynprogindex"]
+
+
+def microexon_problems(seed=2030, n=600, genome_len=1500000):
+    from dpbind import microexon_problem
+    rng = random.Random(seed)
+    g = bytearray(random_genome(rng, genome_len))
+    at = [100]
+    probs = [microexon_problem(rng, g, edge=(i % 4 == 0), at=at) for i in range(n)]
+    return bytes(g), probs
+
+
+def main_microexon():
+    """Dynprog_microexon_int: the reference's outputs, and per problem the candidate list (the oracle's,
+    in the reference's loop order) with the reference's own MaxEnt probabilities at its splice sites."""
+    from dpbind import Oracle, microexon_probs
+    g, probs = microexon_problems()
+    ref, orc = Ref("nosimd"), Oracle()
+    ref.set_genome(g)
+    orc.set_genome(g)
+    outs = [ref.microexon_int(p) for p in probs]
+    cands = [orc.microexon_candidates(p) or [] for p in probs]
+    cprobs = [microexon_probs(ref, c, p["chroffset"]) for c, p in zip(cands, probs)]
+    assert all(orc.microexon_int(p, cp) == o for p, cp, o in zip(probs, cprobs, outs))
+    flat = [pr for o in outs for pr in (o[2] or [])]
+    d = dict(genome=np.frombuffer(g, dtype=np.uint8),
+             params=np.array([[p[k] for k in ME_PARAMS] for p in probs], dtype=np.int64),
+             param_names=np.array(ME_PARAMS), qbuf=np.frombuffer(b"".join(p["q"] for p in probs), dtype=np.uint8),
+             scalars=np.array([o[0] for o in outs], dtype=np.int32),
+             dscalars=np.array([o[1] for o in outs], dtype=np.float64),
+             npairs=np.array([-1 if o[2] is None else len(o[2]) for o in outs], dtype=np.int32),
+             ncands=np.array([len(c) for c in cands], dtype=np.int32),
+             cands=np.array([list(x) for c in cands for x in c], dtype=np.int64).reshape(-1, 8),
+             cand_probs=np.array([x for cp in cprobs for x in cp], dtype=np.float64),
+             pairs_int=np.array([pr[:5] + (pr[9],) for pr in flat], dtype=np.int32).reshape(-1, 6),
+             pairs_chr=np.array([[ord(c) for c in pr[5:9]] for pr in flat], dtype=np.uint8).reshape(-1, 4))
+    out = os.path.join(HERE, "microexon_golden.npz")
+    np.savez_compressed(out, **d)
+    print("wrote %s: %d problems, %d found, %d candidates" % (out, len(probs), sum(o[2] is not None for o in outs),
+                                                             len(d["cands"])))
+
+
+def load_microexon(path):
+    """(genome bytes, [problem dicts], [candidate lists], [flat candidate probabilities],
+    [((dpi, microintrontype), (prob2, prob3), pairs-or-None)])."""
+    z = dict(np.load(path, allow_pickle=False))
+    names = [str(x) for x in z["param_names"]]
+    qoff = np.concatenate([[0], np.cumsum(z["params"][:, names.index("rlength")])])
+    qb = z["qbuf"].tobytes()
+    pint, pchr, cands_all = z["pairs_int"].tolist(), z["pairs_chr"].tolist(), z["cands"].tolist()
+    cp_all = z["cand_probs"].tolist()
+    probs, cands, cprobs, outs, pi, ci = [], [], [], [], 0, 0
+    for i, row in enumerate(z["params"]):
+        p = {k: int(v) for k, v in zip(names, row)}
+        p["q"] = qb[qoff[i]:qoff[i + 1]]
+        p["quc"] = p["q"].upper()
+        probs.append(p)
+        k = int(z["ncands"][i])
+        cands.append([tuple(int(x) for x in c) for c in cands_all[ci:ci + k]])
+        cprobs.append(cp_all[2 * ci:2 * (ci + k)])
+        ci += k
+        n = int(z["npairs"][i])
+        pairs = None
+        if n >= 0:
+            pairs = [tuple(int(x) for x in pint[pi + j][:5]) + tuple(bytes([int(c)]) for c in pchr[pi + j])
+                     + (int(pint[pi + j][5]),) for j in range(n)]
+            pi += n
+        outs.append((tuple(int(x) for x in z["scalars"][i]), tuple(float(x) for x in z["dscalars"][i]), pairs))
+    return z["genome"].tobytes(), probs, cands, cprobs, outs
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "simd":
         main_simd()
@@ -352,5 +424,7 @@ if __name__ == "__main__":
         main_oligo()
     elif len(sys.argv) > 1 and sys.argv[1] == "stage2":
         main_stage2()
+    elif len(sys.argv) > 1 and sys.argv[1] == "microexon":
+        main_microexon()
     else:
         main()

@@ -432,3 +432,48 @@ def test_oracle_stage2_compute_vs_reference_random():
             p = stage2_problem(rng, g, edge=(i % 5 == 0))
             a, b = ref.stage2_compute(p), orc.stage2_compute(p)
             assert a == b, "seed %d problem %d: reference %s vs oracle %s" % (seed, i, a[0], b[0])
+
+
+# ---- Dynprog_microexon_int (dynprog_single.c:900) ----
+
+def _load_microexon_golden():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(HERE, "golden", "make_golden.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m.load_microexon(os.path.join(HERE, "golden", "microexon_golden.npz"))
+
+
+def test_oracle_microexon_matches_golden():
+    g, probs, cands, cprobs, exp = _load_microexon_golden()
+    orc = Oracle()
+    orc.set_genome(g)
+    bad = [i for i, p in enumerate(probs) if (orc.microexon_candidates(p) or []) != cands[i]]
+    assert not bad, "candidate lists differing from the golden: %s" % bad[:10]
+    bad = [i for i, p in enumerate(probs) if orc.microexon_int(p, cprobs[i]) != exp[i]]
+    assert not bad, "microexon problems differing from the golden: %s" % bad[:10]
+    # the golden holds every exit: found (both intron directions, both strands), no candidate,
+    # cdna_direction 0 (NONINTRON), several candidates (the float tie rule)
+    found = [p for p, o in zip(probs, exp) if o[2] is not None]
+    assert {p["cdna_direction"] for p in found} == {1, -1} and {p["watsonp"] for p in found} == {0, 1}
+    assert any(o[2] is None and p["cdna_direction"] != 0 for p, o in zip(probs, exp))
+    assert any(o[0][1] == 0 and p["cdna_direction"] == 0 for p, o in zip(probs, exp))
+    assert any(len(c) > 1 for c in cands)
+
+
+@pytest.mark.skipif(not ref_available(), reason="reference objects not built")
+def test_oracle_microexon_vs_reference_random():
+    from dpbind import microexon_probs, microexon_problem, random_genome
+    ref, orc = Ref("nosimd"), Oracle()
+    for seed in (21, 22):
+        rng = random.Random(seed)
+        g = bytearray(random_genome(rng, 2500000))
+        at = [100]
+        probs = [microexon_problem(rng, g, edge=(i % 4 == 0), at=at) for i in range(800)]
+        g = bytes(g)
+        ref.set_genome(g)
+        orc.set_genome(g)
+        for i, p in enumerate(probs):
+            cp = microexon_probs(ref, orc.microexon_candidates(p), p["chroffset"])
+            a, b = ref.microexon_int(p), orc.microexon_int(p, cp)
+            assert a == b, "seed %d problem %d: reference %s vs oracle %s" % (seed, i, a[:2], b[:2])
