@@ -86,6 +86,14 @@ hipError_t launch_oi(bool wide, int nproblems, size_t lds, hipStream_t stream, c
                      const uint32_t* blocks, const char* quc, unsigned char* scratch, gmapdp_oligo_result* results,
                      int32_t* npos, int32_t* map, uint32_t* table, int32_t* diags, uint64_t* pool,
                      unsigned long long* pool_counter, unsigned long long pool_cap);
+hipError_t launch_mx_search(int n, hipStream_t s, const gmapdp_microexon_problem* probs, const uint32_t* blocks,
+                            uint64_t nwords, const char* qseq, const char* qseq_uc, gmapdp_microexon_result* results,
+                            gmapdp_microexon_candidate* cands, unsigned long long cap, unsigned long long* counter,
+                            const int64_t* direct);
+hipError_t launch_mx_finish(int n, hipStream_t s, const gmapdp_microexon_problem* probs, const uint32_t* blocks,
+                            uint64_t nwords, const char* qseq, const char* qseq_uc, const uint8_t* constab,
+                            const gmapdp_microexon_candidate* cands, const double* cand_probs,
+                            gmapdp_microexon_result* results, gmapdp_pair* pairs);
 static const int kUse8pSize[4] = {41, 63, 127, 24};  // use8p_size (dynprog.c:1022-1025)
 
 // ---------------------------------------------------------------------------
@@ -253,6 +261,7 @@ struct gmapdp_ctx {
   DevBuf cprobs, corder, cresults, cscratch;  // Dynprog_cdna_gap batches
   DevBuf oprobs, oresults, oscratch, onpos, omap, otable, odiag, opool, opoolctr;  // stage-2 seeding batches
   DevBuf s2probs, s2results, s2scratch, s2counters, s2paths, s2pairs, s2qseq;  // Stage2_compute batches
+  DevBuf mxprobs, mxres, mxcands, mxcnt, mxdirect, mxprobs2, mxpairs;  // Dynprog_microexon_int batches
   std::string err;
 };
 
@@ -2048,6 +2057,158 @@ extern "C" int gmapdp_stage2_batch(gmapdp_ctx* ctx, const gmapdp_stage2_problem*
     pcap = std::max<size_t>(2 * pcap, (size_t)cnt[1] + 16);
     qcap = std::max<size_t>(2 * qcap, (size_t)cnt[2] + 64);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Dynprog_microexon_int (dynprog_single.c:900): candidate search, then selection + pairs
+// (mx_kernel.hip).  Synchronous host-array batches.
+// ---------------------------------------------------------------------------
+static int mx_upload(gmapdp_ctx* ctx, const gmapdp_microexon_problem* problems, int n, const char* qseq,
+                     const char* qseq_uc, size_t qbytes) {
+  for (int i = 0; i < n; i++) {
+    const gmapdp_microexon_problem& p = problems[i];
+    if (p.rlength < 0 || p.qoff < 0 || (size_t)p.qoff + (size_t)p.rlength > qbytes)
+      return bad(ctx, "microexon: query slice outside the query arena");
+  }
+  hipStream_t s = ctx->stream;
+  hipError_t e = ctx->mxprobs.ensure(sizeof(gmapdp_microexon_problem) * n);
+  if (e == hipSuccess) e = ctx->mxres.ensure(sizeof(gmapdp_microexon_result) * n);
+  if (e == hipSuccess) e = ctx->qseq.ensure(std::max<size_t>(qbytes, 1));
+  if (e == hipSuccess) e = ctx->qseq_uc.ensure(std::max<size_t>(qbytes, 1));
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(ctx->mxprobs.p, problems, sizeof(gmapdp_microexon_problem) * n, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && qbytes) e = hipMemcpyAsync(ctx->qseq.p, qseq, qbytes, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && qbytes) e = hipMemcpyAsync(ctx->qseq_uc.p, qseq_uc, qbytes, hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "microexon buffers: %s", e);
+  return GMAPDP_OK;
+}
+
+extern "C" size_t gmapdp_microexon_pair_capacity(const gmapdp_microexon_problem* problems, int n) {
+  size_t c = 0;
+  for (int i = 0; i < n; i++) c += (size_t)std::max(problems[i].rlength, 0) + 2;
+  return c;
+}
+
+extern "C" int gmapdp_microexon_search(gmapdp_ctx* ctx, const gmapdp_microexon_problem* problems, int n,
+                                       const char* qseq, const char* qseq_uc, size_t qbytes,
+                                       gmapdp_microexon_result* results, gmapdp_microexon_candidate* candidates,
+                                       size_t cand_capacity, size_t* cands_needed) {
+  if (!ctx || n < 0 || (n > 0 && (!problems || !results || !qseq || !qseq_uc))) return GMAPDP_EINVAL;
+  if (cands_needed) *cands_needed = 0;
+  if (!ctx->d_genome) return GMAPDP_ENOGENOME;
+  if (n == 0) return GMAPDP_OK;
+  (void)hipSetDevice(ctx->device);
+  int rc = mx_upload(ctx, problems, n, qseq, qseq_uc, qbytes);
+  if (rc) return rc;
+  hipStream_t s = ctx->stream;
+  size_t cap = std::max<size_t>(ctx->mxcands.cap / sizeof(gmapdp_microexon_candidate), 4096);
+  unsigned long long cnt = 0;
+  for (int attempt = 0;; attempt++) {
+    hipError_t e = ctx->mxcands.ensure(sizeof(gmapdp_microexon_candidate) * cap);
+    if (e == hipSuccess) e = ctx->mxcnt.ensure(sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemsetAsync(ctx->mxcnt.p, 0, sizeof(unsigned long long), s);
+    if (e == hipSuccess)
+      e = launch_mx_search(n, s, (const gmapdp_microexon_problem*)ctx->mxprobs.p, ctx->d_genome, ctx->genome_words,
+                           (const char*)ctx->qseq.p, (const char*)ctx->qseq_uc.p,
+                           (gmapdp_microexon_result*)ctx->mxres.p, (gmapdp_microexon_candidate*)ctx->mxcands.p, cap,
+                           (unsigned long long*)ctx->mxcnt.p, nullptr);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(results, ctx->mxres.p, sizeof(gmapdp_microexon_result) * n, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(&cnt, ctx->mxcnt.p, sizeof(cnt), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "microexon search: %s", e);
+    bool regrow = false;
+    for (int i = 0; i < n; i++) regrow |= results[i].cand_offset == -2;
+    if (!regrow) break;
+    if (attempt >= 8) return fail(ctx, GMAPDP_ENOMEM, "microexon candidate pool keeps overflowing%s", hipSuccess);
+    cap = std::max<size_t>(2 * cap, (size_t)cnt + 64);
+  }
+  // calls with more candidates than the kernel holds in LDS: rerun them into regions of their own
+  std::vector<int64_t> direct(n, -1);
+  size_t total = (size_t)cnt;
+  bool any = false;
+  for (int i = 0; i < n; i++)
+    if (results[i].cand_offset == -1) {
+      direct[i] = (int64_t)total;
+      total += (size_t)results[i].ncandidates;
+      any = true;
+    }
+  hipError_t e = hipSuccess;
+  if (any) {
+    if (total > ctx->mxcands.cap / sizeof(gmapdp_microexon_candidate)) {
+      // grow, keeping the candidates already found
+      DevBuf keep;
+      e = keep.ensure(sizeof(gmapdp_microexon_candidate) * std::max<size_t>(total, 1));
+      if (e == hipSuccess && cnt)
+        e = hipMemcpyAsync(keep.p, ctx->mxcands.p, sizeof(gmapdp_microexon_candidate) * cnt, hipMemcpyDeviceToDevice, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e == hipSuccess) std::swap(keep.p, ctx->mxcands.p), std::swap(keep.cap, ctx->mxcands.cap);
+    }
+    if (e == hipSuccess) e = ctx->mxdirect.ensure(sizeof(int64_t) * n);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(ctx->mxdirect.p, direct.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+      e = launch_mx_search(n, s, (const gmapdp_microexon_problem*)ctx->mxprobs.p, ctx->d_genome, ctx->genome_words,
+                           (const char*)ctx->qseq.p, (const char*)ctx->qseq_uc.p,
+                           (gmapdp_microexon_result*)ctx->mxres.p, (gmapdp_microexon_candidate*)ctx->mxcands.p,
+                           total, (unsigned long long*)ctx->mxcnt.p, (const int64_t*)ctx->mxdirect.p);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(results, ctx->mxres.p, sizeof(gmapdp_microexon_result) * n, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "microexon search (large): %s", e);
+  }
+  if (cands_needed) *cands_needed = total;
+  if (total > cand_capacity || (total && !candidates)) return GMAPDP_ESPACE;
+  if (total) e = hipMemcpyAsync(candidates, ctx->mxcands.p, sizeof(gmapdp_microexon_candidate) * total,
+                                hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "microexon candidates: %s", e);
+  return GMAPDP_OK;
+}
+
+extern "C" int gmapdp_microexon_finish(gmapdp_ctx* ctx, const gmapdp_microexon_problem* problems, int n,
+                                       const char* qseq, const char* qseq_uc, size_t qbytes,
+                                       const gmapdp_microexon_candidate* candidates, const double* cand_probs,
+                                       size_t ncands, gmapdp_microexon_result* results, gmapdp_pair* pairs,
+                                       size_t pair_capacity) {
+  if (!ctx || n < 0 || (n > 0 && (!problems || !results || !qseq || !qseq_uc))) return GMAPDP_EINVAL;
+  if (!ctx->d_genome) return GMAPDP_ENOGENOME;
+  if (n == 0) return GMAPDP_OK;
+  if (ncands && (!candidates || !cand_probs)) return GMAPDP_EINVAL;
+  size_t poff = 0;
+  std::vector<gmapdp_microexon_result> res(results, results + n);
+  for (int i = 0; i < n; i++) {
+    if (res[i].ncandidates < 0 || (res[i].ncandidates > 0 && (res[i].cand_offset < 0 ||
+                                                              (size_t)res[i].cand_offset + res[i].ncandidates > ncands)))
+      return bad(ctx, "microexon: candidates outside the candidate array");
+    res[i].pair_offset = (int64_t)poff;
+    poff += (size_t)std::max(problems[i].rlength, 0) + 2;
+  }
+  if (poff > pair_capacity || !pairs) return bad(ctx, "microexon: pair arena too small");
+  (void)hipSetDevice(ctx->device);
+  int rc = mx_upload(ctx, problems, n, qseq, qseq_uc, qbytes);
+  if (rc) return rc;
+  hipStream_t s = ctx->stream;
+  hipError_t e = ctx->mxcands.ensure(sizeof(gmapdp_microexon_candidate) * std::max<size_t>(ncands, 1));
+  if (e == hipSuccess) e = ctx->mxprobs2.ensure(sizeof(double) * 2 * std::max<size_t>(ncands, 1));
+  if (e == hipSuccess) e = ctx->mxpairs.ensure(sizeof(gmapdp_pair) * std::max<size_t>(poff, 1));
+  if (e == hipSuccess && ncands)
+    e = hipMemcpyAsync(ctx->mxcands.p, candidates, sizeof(gmapdp_microexon_candidate) * ncands, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && ncands)
+    e = hipMemcpyAsync(ctx->mxprobs2.p, cand_probs, sizeof(double) * 2 * ncands, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(ctx->mxres.p, res.data(), sizeof(gmapdp_microexon_result) * n, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess)
+    e = launch_mx_finish(n, s, (const gmapdp_microexon_problem*)ctx->mxprobs.p, ctx->d_genome, ctx->genome_words,
+                         (const char*)ctx->qseq.p, (const char*)ctx->qseq_uc.p, ctx->d_cs,
+                         (const gmapdp_microexon_candidate*)ctx->mxcands.p, (const double*)ctx->mxprobs2.p,
+                         (gmapdp_microexon_result*)ctx->mxres.p, (gmapdp_pair*)ctx->mxpairs.p);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(results, ctx->mxres.p, sizeof(gmapdp_microexon_result) * n, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(pairs, ctx->mxpairs.p, sizeof(gmapdp_pair) * poff, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "microexon finish: %s", e);
+  return GMAPDP_OK;
 }
 
 // Test instrumentation: the chaining scratch of the last gmapdp_stage2_batch (its layout is

@@ -1,0 +1,296 @@
+// mx_kernel.hip -- CDNA4 (gfx950) kernels for Dynprog_microexon_int (SURVEY §8a a15;
+// dynprog_single.c:900-1182), the microexon search stage 3 runs inside an intron (stage3.c:9664).
+//
+// mx_search_kernel, one wave per call:
+//   - leftbound / rightbound (:1001-1047): mismatch flags of 64 query positions per step as one
+//     ballot; the bound is the second mismatch (the popcount of the ballots so far);
+//   - the cL with the intron's 5' dinucleotide (:1053-1062), 64 per ballot, visited in ascending
+//     order; for each, the cR in [mincR, maxcR] with its 3' dinucleotide (:1063-1085);
+//   - the exact search of the middle piece in the intron text (BoyerMoore_nt, boyer-moore.c:356:
+//     every occurrence j in [0, textlen - querylen]; none when the piece holds anything but A/C/G/T):
+//     64 offsets per step, the text staged in LDS, lane l tests j = top - l so that the ballot order is
+//     the reference's hit order (Intlist_push: descending j);
+//   - the flank test (:1109-1116) and the candidate's two splice sites (:1120-1144).
+//   Candidates collect in LDS and leave with one atomic per call; a call with more than kMxCap of
+//   them reports its exact count and the host reruns it writing straight to its own region.
+// mx_finish_kernel, one wave per call: the (float) prob2 + prob3 > best rule (:1147) over the
+//   candidates in order, then make_microexon_pairs_double (:683) with every record placed by a ballot
+//   rank (Pairpool_push drops negative positions, pairpool.c:188) in List_T order.
+#include "dp_device.h"
+
+namespace gmapdp {
+
+constexpr int kMxMin = 3;       // MIN_MICROEXON_LENGTH (dynprog_single.c:83)
+constexpr int kMxMax = 12;      // MAX_MICROEXON_LENGTH (:87, GMAP)
+constexpr int kMxIntron = 9;    // MICROINTRON_LENGTH (:89)
+constexpr int kMxCap = 256;     // candidates per call held in LDS
+
+// the second mismatch among n flags produced 64 at a time by `flag(i)`; n - 1 when there is none
+template <class F>
+__device__ __forceinline__ int mx_second_mismatch(int n, int lane, F flag) {
+  int seen = 0;
+  for (int base = 0; base < n; base += 64) {
+    const int i = base + lane;
+    const uint64_t m = ballot(i < n && flag(i));
+    const int c = __popcll(m);
+    if (seen + c >= 2) {
+      uint64_t x = m;
+      if (seen == 0) x &= x - 1;  // drop the first mismatch of this step
+      return base + __ffsll((long long)x) - 1;
+    }
+    seen += c;
+  }
+  return n - 1;
+}
+
+__global__ __launch_bounds__(64) void mx_search_kernel(const gmapdp_microexon_problem* __restrict__ probs, int n,
+                                                       const uint32_t* __restrict__ blocks, uint64_t nwords,
+                                                       const char* __restrict__ qseq,
+                                                       const char* __restrict__ qseq_uc,
+                                                       gmapdp_microexon_result* __restrict__ results,
+                                                       gmapdp_microexon_candidate* __restrict__ cands,
+                                                       unsigned long long cand_cap,
+                                                       unsigned long long* __restrict__ counter,
+                                                       const int64_t* __restrict__ direct) {
+  __shared__ gmapdp_microexon_candidate lc[kMxCap];
+  __shared__ char text[64 + kMxMax + 4];
+  __shared__ char piece[kMxMax + 4];
+  const int pi = blockIdx.x;
+  if (pi >= n) return;
+  const int lane = threadIdx.x;
+  const gmapdp_microexon_problem P = probs[pi];
+  const int64_t dst = direct ? direct[pi] : -1;  // rerun of an overflowing call: its own region
+  if (direct && dst < 0) return;
+  gmapdp_microexon_result R;
+  R.ncandidates = 0;
+  R.dynprogindex = P.dynprogindex;
+  R.microintrontype = P.cdna_direction > 0 ? 0x20 : P.cdna_direction < 0 ? 0x04 : 0;
+  R.npairs = -1;
+  R.cand_offset = 0;
+  R.pair_offset = 0;
+  R.bestprob2 = R.bestprob3 = 0.0;
+  const bool watson = P.watsonp != 0;
+  const char* rs = qseq + P.qoff;
+  const char* ruc = qseq_uc + P.qoff;
+  int ncand = 0;
+  if (P.cdna_direction != 0) {
+    const char i1 = P.cdna_direction > 0 ? 'G' : 'C', i2 = 'T', i3 = 'A', i4 = P.cdna_direction > 0 ? 'G' : 'C';
+    auto gnt = [&](int g) { return genomic_nt(blocks, nwords, g, P.chroffset, P.chrhigh, watson); };
+    const int rl = P.rlength;
+    const int leftbound = rl - 1 <= 0 ? -1
+                                      : mx_second_mismatch(rl - 1, lane, [&](int i) { return ruc[i] != gnt(P.goffsetL + i); });
+    const int rightbound = rl <= 0 ? -1
+                                   : mx_second_mismatch(rl, lane, [&](int k) { return ruc[rl - 1 - k] != gnt(P.rev_goffsetR - k); });
+    for (int base = 1; base <= leftbound; base += 64) {
+      const int cl = base + lane;
+      uint64_t mL = ballot(cl <= leftbound && gnt(P.goffsetL + cl) == i1 && gnt(P.goffsetL + cl + 1) == i2);
+      while (mL) {
+        const int cL = base + __ffsll((long long)mL) - 1;
+        mL &= mL - 1;
+        const int mincR = max(rl - kMxMax - cL, 1);
+        const int maxcR = min(rl - kMxMin - cL, rightbound);
+        for (int cR = mincR; cR <= maxcR; cR++) {
+          if (gnt(P.rev_goffsetR - cR - 1) != i3 || gnt(P.rev_goffsetR - cR) != i4) continue;
+          const int ml = rl - cL - cR;
+          const int textleft = P.goffsetL + cL + kMxIntron;
+          const int textright = P.rev_goffsetR - cR - kMxIntron;
+          if (textright < textleft + ml) continue;
+          // query_okay (boyer-moore.c:263) on the mixed-case piece
+          const char qc = lane < ml ? rs[cL + lane] : 'A';
+          if (ballot(qc != 'A' && qc != 'C' && qc != 'G' && qc != 'T')) continue;
+          if (lane < ml) piece[lane] = qc;
+          const int textlen = textright - textleft;
+          const uint32_t L = (uint32_t)(textlen + ml);
+          // Genome_get_segment_right / _left as BoyerMoore_nt calls them (boyer-moore.c:372-378)
+          const uint32_t spos = watson ? P.chroffset + (uint32_t)textleft : P.chrhigh - (uint32_t)textleft + 1u;
+          const uint32_t sbound = watson ? P.chrhigh : P.chroffset;
+          for (int top = textlen - ml; top >= 0; top -= 64) {
+            const int lo = top - 63;  // text[lo .. top + ml) staged at text[0 ..)
+            for (int t = lane; t < 64 + ml; t += 64) {
+              const int ti = lo + t;
+              text[t] = ti >= 0 ? segment_nt(blocks, nwords, (uint32_t)ti, L, spos, sbound, !watson, !watson) : 0;
+            }
+            __builtin_amdgcn_wave_barrier();
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            const int j = top - lane;
+            bool hit = j >= 0;
+            for (int k = 0; k < ml && hit; k++) hit = text[63 - lane + k] == piece[k];
+            const int cand = textleft + j;
+            hit = hit && gnt(cand - 2) == i3 && gnt(cand - 1) == i4 && gnt(cand + ml) == i1 && gnt(cand + ml + 1) == i2;
+            const uint64_t mh = ballot(hit);
+            if (hit) {
+              const int idx = ncand + lanes_below(mh, lane);
+              gmapdp_microexon_candidate c;
+              c.cL = cL;
+              c.cR = cR;
+              c.candidate = cand;
+              c.middlelength = ml;
+              if (watson) {
+                c.pos2 = P.chroffset + (uint32_t)(cand - 1) + 1u;
+                c.pos3 = P.chroffset + (uint32_t)(cand + ml);
+                c.model2 = P.cdna_direction > 0 ? GMAPDP_MAXENT_ACCEPTOR : GMAPDP_MAXENT_ANTIDONOR;
+                c.model3 = P.cdna_direction > 0 ? GMAPDP_MAXENT_DONOR : GMAPDP_MAXENT_ANTIACCEPTOR;
+              } else {
+                c.pos2 = P.chrhigh - (uint32_t)(cand - 1);
+                c.pos3 = P.chrhigh - (uint32_t)(cand + ml) + 1u;
+                c.model2 = P.cdna_direction > 0 ? GMAPDP_MAXENT_ANTIACCEPTOR : GMAPDP_MAXENT_DONOR;
+                c.model3 = P.cdna_direction > 0 ? GMAPDP_MAXENT_ANTIDONOR : GMAPDP_MAXENT_ACCEPTOR;
+              }
+              if (dst >= 0) cands[dst + idx] = c;
+              else if (idx < kMxCap) lc[idx] = c;
+            }
+            ncand += __popcll(mh);
+            __builtin_amdgcn_wave_barrier();
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+          }
+        }
+      }
+    }
+  }
+  R.ncandidates = ncand;
+  if (dst >= 0) {
+    R.cand_offset = dst;
+  } else if (ncand > kMxCap) {
+    R.cand_offset = -1;  // the host reruns this call with a region of ncand records
+  } else if (ncand > 0) {
+    unsigned long long b = 0;
+    if (lane == 0) b = atomicAdd(counter, (unsigned long long)ncand);
+    b = __shfl(b, 0);
+    if (b + (unsigned long long)ncand <= cand_cap) {
+      for (int k = lane; k < ncand; k += 64) cands[b + k] = lc[k];
+      R.cand_offset = (int64_t)b;
+    } else {
+      R.cand_offset = -2;  // pool too small: the host grows it and reruns the batch
+    }
+  }
+  if (lane == 0) results[pi] = R;
+}
+
+__global__ __launch_bounds__(64) void mx_finish_kernel(const gmapdp_microexon_problem* __restrict__ probs, int n,
+                                                       const uint32_t* __restrict__ blocks, uint64_t nwords,
+                                                       const char* __restrict__ qseq,
+                                                       const char* __restrict__ qseq_uc,
+                                                       const uint8_t* __restrict__ constab,
+                                                       const gmapdp_microexon_candidate* __restrict__ cands,
+                                                       const double* __restrict__ cand_probs,
+                                                       gmapdp_microexon_result* __restrict__ results,
+                                                       gmapdp_pair* __restrict__ pairs) {
+  const int pi = blockIdx.x;
+  if (pi >= n) return;
+  const int lane = threadIdx.x;
+  const gmapdp_microexon_problem P = probs[pi];
+  gmapdp_microexon_result R = results[pi];
+  R.dynprogindex = P.dynprogindex;
+  R.npairs = -1;
+  R.bestprob2 = R.bestprob3 = 0.0;
+  R.microintrontype = P.cdna_direction > 0 ? 0x20 : P.cdna_direction < 0 ? 0x04 : 0;
+  // the selection (:1147): float sums, strict >, candidates in order
+  int best = -1;
+  float bestprob = 0.0f, b2 = 0.0f, b3 = 0.0f;
+  if (P.cdna_direction != 0) {
+    for (int k = 0; k < R.ncandidates; k++) {
+      const float p2 = (float)cand_probs[2 * (R.cand_offset + k)];
+      const float p3 = (float)cand_probs[2 * (R.cand_offset + k) + 1];
+      if (p2 + p3 > bestprob) {
+        best = k;
+        b2 = p2;
+        b3 = p3;
+        bestprob = p2 + p3;
+      }
+    }
+  }
+  if (best < 0) {
+    R.microintrontype = 0;  // NONINTRON
+    if (lane == 0) results[pi] = R;
+    return;
+  }
+  const gmapdp_microexon_candidate C = cands[R.cand_offset + best];
+  const bool watson = P.watsonp != 0;
+  const char* rs = qseq + P.qoff;
+  const char* ruc = qseq_uc + P.qoff;
+  const uint8_t* cons = constab + (size_t)P.genestrand * 128 * kNClass;
+  const char gapchar = P.cdna_direction > 0 ? '>' : '<';
+  const int lenL = C.cL, lenM = C.middlelength, lenR = C.cR;
+  const int goffsetM = C.candidate, goffsetR = P.rev_goffsetR - C.cR + 1;
+  const int total = lenL + 1 + lenM + 1 + lenR;  // records in push order
+  // valid records (Pairpool_push drops querypos < 0 or genomepos < 0; gap holders always stay)
+  auto record = [&](int t, int& r, int& g, int& jump) {  // returns 0 pair, 1 gap holder
+    if (t < lenL) {
+      r = t;
+      g = P.goffsetL + t;
+      return 0;
+    }
+    if (t == lenL) {
+      jump = goffsetM - (P.goffsetL + lenL);
+      return 1;
+    }
+    if (t <= lenL + lenM) {
+      r = lenL + (t - lenL - 1);
+      g = goffsetM + (t - lenL - 1);
+      return 0;
+    }
+    if (t == lenL + lenM + 1) {
+      jump = goffsetR - (goffsetM + lenM);
+      return 1;
+    }
+    r = lenL + lenM + (t - lenL - lenM - 2);
+    g = goffsetR + (t - lenL - lenM - 2);
+    return 0;
+  };
+  int nvalid = 0;
+  for (int base = 0; base < total; base += 64) {
+    const int t = base + lane;
+    int r = 0, g = 0, jump = 0, kind = 0;
+    if (t < total) kind = record(t, r, g, jump);
+    const bool valid = t < total && (kind == 1 || (P.roffset + r >= 0 && g >= 0));
+    nvalid += __popcll(ballot(valid));
+  }
+  gmapdp_pair* out = pairs + R.pair_offset;
+  int rank0 = 0;
+  for (int base = 0; base < total; base += 64) {
+    const int t = base + lane;
+    int r = 0, g = 0, jump = 0, kind = 0;
+    if (t < total) kind = record(t, r, g, jump);
+    const bool valid = t < total && (kind == 1 || (P.roffset + r >= 0 && g >= 0));
+    const uint64_t m = ballot(valid);
+    if (valid) {
+      const int idx = nvalid - 1 - (rank0 + lanes_below(m, lane));  // List_T order: last push first
+      if (kind == 1) {
+        put_pair(out, idx, -1, -1, jump, ' ', gapchar, ' ', ' ');
+      } else {
+        const char c1 = rs[r], c1u = ruc[r];
+        const char c2 = genomic_nt(blocks, nwords, g, P.chroffset, P.chrhigh, watson);
+        const char comp = c1u == c2 ? '*' : cons[(uint8_t)(c1u & 127) * kNClass + gclass(c2)] ? ':' : ' ';
+        put_pair(out, idx, P.roffset + r, g, 0, c1, comp, c2, c2);
+      }
+    }
+    rank0 += __popcll(m);
+  }
+  R.npairs = nvalid;
+  R.dynprogindex = P.dynprogindex + (P.dynprogindex > 0 ? 1 : -1);
+  R.bestprob2 = (double)b2;
+  R.bestprob3 = (double)b3;
+  if (lane == 0) results[pi] = R;
+}
+
+hipError_t launch_mx_search(int n, hipStream_t s, const gmapdp_microexon_problem* probs, const uint32_t* blocks,
+                            uint64_t nwords, const char* qseq, const char* qseq_uc, gmapdp_microexon_result* results,
+                            gmapdp_microexon_candidate* cands, unsigned long long cap, unsigned long long* counter,
+                            const int64_t* direct) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mx_search_kernel, dim3(n), dim3(64), 0, s, probs, n, blocks, nwords, qseq, qseq_uc, results,
+                     cands, cap, counter, direct);
+  return hipGetLastError();
+}
+
+hipError_t launch_mx_finish(int n, hipStream_t s, const gmapdp_microexon_problem* probs, const uint32_t* blocks,
+                            uint64_t nwords, const char* qseq, const char* qseq_uc, const uint8_t* constab,
+                            const gmapdp_microexon_candidate* cands, const double* cand_probs,
+                            gmapdp_microexon_result* results, gmapdp_pair* pairs) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mx_finish_kernel, dim3(n), dim3(64), 0, s, probs, n, blocks, nwords, qseq, qseq_uc, constab,
+                     cands, cand_probs, results, pairs);
+  return hipGetLastError();
+}
+
+}  // namespace gmapdp

@@ -101,6 +101,17 @@ class Stage2Result(C.Structure):
                                           "diag_queryend", "path_offset", "npairs")]
 
 
+MICROEXON_PROBLEM_DTYPE = np.dtype([("qoff", "<i4"), ("rlength", "<i4"), ("roffset", "<i4"), ("goffsetL", "<i4"),
+                                    ("rev_goffsetR", "<i4"), ("cdna_direction", "<i4"), ("chroffset", "<u4"),
+                                    ("chrhigh", "<u4"), ("watsonp", "<i4"), ("genestrand", "<i4"),
+                                    ("dynprogindex", "<i4"), ("pad_", "<i4")])
+MICROEXON_CANDIDATE_DTYPE = np.dtype([("cL", "<i4"), ("cR", "<i4"), ("candidate", "<i4"), ("middlelength", "<i4"),
+                                      ("pos2", "<u4"), ("pos3", "<u4"), ("model2", "<i4"), ("model3", "<i4")])
+MICROEXON_RESULT_DTYPE = np.dtype([("ncandidates", "<i4"), ("dynprogindex", "<i4"), ("microintrontype", "<i4"),
+                                   ("npairs", "<i4"), ("cand_offset", "<i8"), ("pair_offset", "<i8"),
+                                   ("bestprob2", "<f8"), ("bestprob3", "<f8")])
+
+
 def _struct_dtype(S, fmt):
     return np.dtype({"names": [n for n, _ in S._fields_], "formats": fmt,
                      "offsets": [S.__dict__[n].offset for n, _ in S._fields_], "itemsize": C.sizeof(S)})
@@ -218,6 +229,12 @@ def load_library(path=LIB_PATH):
         "gmapdp_plan_launch_kind": (C.c_int, [C.c_void_p, C.c_int]),
         "gmapdp_compute_bands": (None, [P(C.c_int), P(C.c_int), C.c_int, C.c_int, C.c_int, C.c_int]),
         "gmapdp_last_error": (C.c_char_p, [C.c_void_p]),
+        "gmapdp_microexon_search": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_char_p, C.c_char_p, C.c_size_t,
+                                              C.c_void_p, C.c_void_p, C.c_size_t, P(C.c_size_t)]),
+        "gmapdp_microexon_finish": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_char_p, C.c_char_p, C.c_size_t,
+                                              C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
+                                              C.c_size_t]),
+        "gmapdp_microexon_pair_capacity": (C.c_size_t, [C.c_void_p, C.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -604,6 +621,105 @@ def decode_genome_results(results, pairs, dynprogindices):
             lst[g] = (-1, -1, int(res["gap_queryjump"]), lst[g][3], 0, b" ", b" ", b" ", b" ", 1)
         out.append((scal, lst))
     return out
+
+
+def _microexon_engine_methods():
+    def build_microexon_batch(calls):
+        """calls: dicts with the Dynprog_microexon_int arguments (q, quc: the query slice; rlength, roffset,
+        goffsetL, rev_goffsetR, cdna_direction, chroffset, chrhigh, watsonp, genestrand, dynprogindex)."""
+        calls = list(calls)
+        probs = np.zeros(len(calls), dtype=MICROEXON_PROBLEM_DTYPE)
+        off = 0
+        for i, p in enumerate(calls):
+            probs[i]["qoff"] = off
+            for k in ("rlength", "roffset", "goffsetL", "rev_goffsetR", "cdna_direction", "chroffset", "chrhigh",
+                      "watsonp", "genestrand", "dynprogindex"):
+                probs[i][k] = p[k]
+            off += len(p["q"])
+        return probs, (b"".join(p["q"] for p in calls) or b"\0"), (b"".join(p["quc"] for p in calls) or b"\0")
+
+    def microexon_search_raw(self, probs, qb, qub):
+        n = len(probs)
+        results = np.zeros(n, dtype=MICROEXON_RESULT_DTYPE)
+        need = C.c_size_t(0)
+        cands = np.zeros(max(1, 4 * n), dtype=MICROEXON_CANDIDATE_DTYPE)
+        rc = self.lib.gmapdp_microexon_search(self.h, probs.ctypes.data, n, qb, qub, len(qb), results.ctypes.data,
+                                              cands.ctypes.data, len(cands), C.byref(need))
+        if rc == -6:
+            cands = np.zeros(need.value, dtype=MICROEXON_CANDIDATE_DTYPE)
+            rc = self.lib.gmapdp_microexon_search(self.h, probs.ctypes.data, n, qb, qub, len(qb),
+                                                  results.ctypes.data, cands.ctypes.data, len(cands), C.byref(need))
+        self._check(rc, "gmapdp_microexon_search")
+        return results, cands[:need.value]
+
+    def microexon_finish_raw(self, probs, qb, qub, cands, cand_probs, results):
+        n = len(probs)
+        cap = self.lib.gmapdp_microexon_pair_capacity(probs.ctypes.data, n)
+        pairs = np.zeros(max(cap, 1), dtype=PAIR_DTYPE)
+        cp = np.ascontiguousarray(cand_probs, dtype=np.float64)
+        if cp.size == 0:
+            cp = np.zeros(2)
+        res = results.copy()
+        rc = self.lib.gmapdp_microexon_finish(self.h, probs.ctypes.data, n, qb, qub, len(qb), cands.ctypes.data,
+                                              cp.ctypes.data, len(cands), res.ctypes.data, pairs.ctypes.data,
+                                              len(pairs))
+        self._check(rc, "gmapdp_microexon_finish")
+        return res, pairs
+
+    def microexon_candidates(self, calls):
+        """Per call the candidate tuples (cL, cR, candidate, middlelength, pos2, model2, pos3, model3) in the
+        reference's loop order (None for cdna_direction 0), as the oracle lists them."""
+        calls = list(calls)
+        probs, qb, qub = build_microexon_batch(calls)
+        results, cands = self.microexon_search_raw(probs, qb, qub)
+        out = []
+        for p, r in zip(calls, results):
+            if p["cdna_direction"] == 0:
+                out.append(None)
+                continue
+            o = int(r["cand_offset"])
+            out.append([(int(c["cL"]), int(c["cR"]), int(c["candidate"]), int(c["middlelength"]), int(c["pos2"]),
+                         int(c["model2"]), int(c["pos3"]), int(c["model3"]))
+                        for c in cands[o:o + int(r["ncandidates"])]])
+        return out
+
+    def microexon_batch(self, calls, maxent):
+        """Dynprog_microexon_int over a batch: search, the caller's MaxEnt (maxent(model, pos, chroffset)
+        -> probability, e.g. the host's Maxent_hr_*_prob), finish.  Returns per call ((dynprogindex after,
+        microintrontype), (bestprob2, bestprob3), pairs-or-None) in the oracle's format."""
+        calls = list(calls)
+        probs, qb, qub = build_microexon_batch(calls)
+        results, cands = self.microexon_search_raw(probs, qb, qub)
+        cp = np.zeros(2 * len(cands))
+        for i, (p, r) in enumerate(zip(calls, results)):
+            o = int(r["cand_offset"])
+            for k in range(int(r["ncandidates"])):
+                c = cands[o + k]
+                cp[2 * (o + k)] = maxent(int(c["model2"]), int(c["pos2"]), p["chroffset"])
+                cp[2 * (o + k) + 1] = maxent(int(c["model3"]), int(c["pos3"]), p["chroffset"])
+        res, pairs = self.microexon_finish_raw(probs, qb, qub, cands, cp, results)
+        out = []
+        for p, r in zip(calls, res):
+            lst = None
+            if r["npairs"] >= 0:
+                lst = []
+                for rec in pairs[int(r["pair_offset"]):int(r["pair_offset"]) + int(r["npairs"])]:
+                    if rec["querypos"] == -1 and rec["genomepos"] == -1:
+                        lst.append((-1, -1, 0, int(rec["jump"]), 0, b" ", rec["comp"], b" ", b" ", 1))
+                    else:
+                        lst.append((int(rec["querypos"]), int(rec["genomepos"]), 0, 0, p["dynprogindex"], rec["cdna"],
+                                    rec["comp"], rec["genome"], rec["genomealt"], 0))
+            out.append(((int(r["dynprogindex"]), int(r["microintrontype"])),
+                        (float(r["bestprob2"]), float(r["bestprob3"])), lst))
+        return out
+
+    return dict(build_microexon_batch=staticmethod(build_microexon_batch), microexon_search_raw=microexon_search_raw,
+                microexon_finish_raw=microexon_finish_raw, microexon_candidates=microexon_candidates,
+                microexon_batch=microexon_batch)
+
+
+for _k, _v in _microexon_engine_methods().items():
+    setattr(Engine, _k, _v)
 
 
 def decode_results(results, pairs, dynprogindices):

@@ -310,6 +310,63 @@ int gmapdp_cdna_gap_batch (gmapdp_ctx *ctx, const gmapdp_cdna_problem *problems,
                            gmapdp_cdna_result *results, gmapdp_pair *pairs, size_t pair_capacity);
 size_t gmapdp_cdna_pair_capacity (const gmapdp_cdna_problem *problems, int n);
 
+/* Dynprog_microexon_int (dynprog_single.c:900, replaced at stage3.c:9664): the
+ * microexon search inside an intron, in two steps because the reference scores each candidate with the
+ * host's MaxEnt model (Maxent_hr_*_prob, maxent_hr.c:27357-27600) between finding and choosing:
+ *   1. gmapdp_microexon_search lists each problem's candidates in the reference's loop order (cL
+ *      ascending, cR ascending, occurrences as BoyerMoore_nt lists them: descending), with the two
+ *      splice sites (position, GMAPDP_MAXENT_* model) whose probabilities prob2 / prob3 it needs;
+ *   2. the caller evaluates them (candidate k's prob2 at cand_probs[2 (cand_offset + k)], prob3 next);
+ *   3. gmapdp_microexon_finish keeps the first candidate whose (float) prob2 + prob3 beats the best so
+ *      far and emits make_microexon_pairs_double's list (dynprog_single.c:683): left piece, gap holder,
+ *      microexon, gap holder, right piece.  The gap holders carry comp = '>' (cdna_direction > 0) or
+ *      '<' and jump = genomejump; queryjump is 0.
+ * rsequence = qseq + qoff (queryseq + roffset as stage3.c passes it); results[i].pair_offset is
+ * problem i's slot in the pair arena (rlength + 2 records, gmapdp_microexon_pair_capacity). */
+typedef struct {
+  int32_t qoff;
+  int32_t rlength;
+  int32_t roffset;
+  int32_t goffsetL;
+  int32_t rev_goffsetR;
+  int32_t cdna_direction;
+  uint32_t chroffset;
+  uint32_t chrhigh;
+  int32_t watsonp;
+  int32_t genestrand;
+  int32_t dynprogindex;
+  int32_t pad_;
+} gmapdp_microexon_problem;
+
+typedef struct {
+  int32_t cL, cR;          /* lengths of the left and right pieces */
+  int32_t candidate;       /* genomic offset of the microexon (goffsetM) */
+  int32_t middlelength;
+  uint32_t pos2, pos3;     /* splice_pos of prob2 and prob3 (universal coordinates) */
+  int32_t model2, model3;  /* GMAPDP_MAXENT_* */
+} gmapdp_microexon_candidate;
+
+typedef struct {
+  int32_t ncandidates;
+  int32_t dynprogindex;    /* after the call */
+  int32_t microintrontype; /* intron.h: GTAG_FWD 0x20, GTAG_REV 0x04, NONINTRON 0 */
+  int32_t npairs;          /* -1: NULL List_T */
+  int64_t cand_offset;     /* first candidate in the candidate array */
+  int64_t pair_offset;
+  double bestprob2, bestprob3;
+} gmapdp_microexon_result;
+
+/* Step 1.  On GMAPDP_ESPACE (cand_capacity too small) *cands_needed holds the size required. */
+int gmapdp_microexon_search (gmapdp_ctx *ctx, const gmapdp_microexon_problem *problems, int n,
+                             const char *qseq, const char *qseq_uc, size_t qbytes, gmapdp_microexon_result *results,
+                             gmapdp_microexon_candidate *candidates, size_t cand_capacity, size_t *cands_needed);
+/* Step 3: results and candidates as step 1 left them; cand_probs as above. */
+int gmapdp_microexon_finish (gmapdp_ctx *ctx, const gmapdp_microexon_problem *problems, int n,
+                             const char *qseq, const char *qseq_uc, size_t qbytes,
+                             const gmapdp_microexon_candidate *candidates, const double *cand_probs, size_t ncands,
+                             gmapdp_microexon_result *results, gmapdp_pair *pairs, size_t pair_capacity);
+size_t gmapdp_microexon_pair_capacity (const gmapdp_microexon_problem *problems, int n);
+
 /* Stage-2 seeding: Oligoindex_hr_tally + Oligoindex_get_mappings
  * (oligoindex_hr.c:33849/34127) as Stage2_compute runs them for GMAP (stage2.c:6413-6501: one
  * 8-mer oligoindex, coveredp all false).  One problem = one (query, genomic window) pair:
