@@ -97,10 +97,11 @@ static int shim_homopolymerp = 0, shim_splicing_iit = 0;
 
 /* Calls that reached the engine, per wrapped entry point (printed at exit with GMAPDP_SHIM_STATS=1;
    tests use it to prove the pipeline really ran on the GPU). */
-enum { ST_SINGLE, ST_END5, ST_END3, ST_GENOME, ST_CDNA, ST_OLIGO, ST_STAGE2, ST_N };
+enum { ST_SINGLE, ST_END5, ST_END3, ST_GENOME, ST_CDNA, ST_OLIGO, ST_STAGE2, ST_MICROEXON, ST_N };
 static const char *const shim_stat_name[ST_N] = {"Dynprog_single_gap", "Dynprog_end5_gap", "Dynprog_end3_gap",
                                                  "Dynprog_genome_gap", "Dynprog_cdna_gap",
-                                                 "Oligoindex_get_mappings", "Stage2_compute"};
+                                                 "Oligoindex_get_mappings", "Stage2_compute",
+                                                 "Dynprog_microexon_int"};
 static unsigned long shim_stats[ST_N];
 
 static unsigned long shim_batches, shim_batched;
@@ -220,7 +221,8 @@ shim_context (Genome_T genome) {
 }
 
 /* ---- requests and the dispatcher ---- */
-enum { K_SINGLE, K_END, K_GENOME, K_CDNA, K_OLIGO, K_STAGE2 };
+enum { K_SINGLE, K_END, K_GENOME, K_CDNA, K_MXS, K_MXF, K_OLIGO, K_STAGE2 };  /* K_MXS / K_MXF: microexon
+                                                                                   search / finish */
 
 typedef struct shim_req {
   int kind;
@@ -232,6 +234,7 @@ typedef struct shim_req {
     gmapdp_cdna_problem c;
     gmapdp_oligo_problem o;
     gmapdp_stage2_problem s2;
+    gmapdp_microexon_problem mx;
   } p;                          /* qoff / prob_offset relative to q and probs below */
   const char *q, *quc;          /* the query slice (borrowed: the caller waits) */
   size_t qlen;
@@ -255,6 +258,10 @@ typedef struct shim_req {
   gmapdp_path *s2paths;         /* Stage2_compute: the results' path records and pairs */
   gmapdp_path_pair *s2pairs;
   size_t s2pathcap, s2paircap;
+  gmapdp_microexon_result mxr;  /* microexon: cand_offset rebased to 0, pair_offset to 0 */
+  gmapdp_microexon_candidate *mxc;
+  double *mxp;                  /* the caller's MaxEnt probabilities of its candidates (2 per candidate) */
+  size_t mxccap, mxpcap;
   int done;
   pthread_cond_t cv;
   struct shim_req *next;
@@ -365,8 +372,13 @@ typedef struct {
   gmapdp_cdna_problem *c;
   gmapdp_oligo_problem *o;
   gmapdp_stage2_problem *s2;
-  shim_req **rs, **re, **rg, **rc, **ro, **r2;
-  size_t scap, ecap, gcap, ccap, ocap, s2cap, rscap, recap, rgcap, rccap, rocap, r2cap;
+  shim_req **rs, **re, **rg, **rc, **ro, **r2, **rxs, **rxf;
+  size_t scap, ecap, gcap, ccap, ocap, s2cap, rscap, recap, rgcap, rccap, rocap, r2cap, rxscap, rxfcap;
+  gmapdp_microexon_problem *mx;
+  gmapdp_microexon_result *mxres;
+  gmapdp_microexon_candidate *mxc;
+  double *mxp;
+  size_t mxcap, mxrescap, mxccap, mxpcap;
   char *q, *quc;
   size_t qcap, quccap;
   double *pr;
@@ -398,7 +410,7 @@ shim_copy_pairs (shim_req *r, const gmapdp_pair *src, int n) {
 static void
 shim_run (shim_req *batch) {
   shim_req *r;
-  size_t ns = 0, ne = 0, ng = 0, nc = 0, no = 0, n2 = 0, n = 0, qb = 0, pb = 0, cap, i;
+  size_t ns = 0, ne = 0, ng = 0, nc = 0, no = 0, n2 = 0, nxs = 0, nxf = 0, n = 0, qb = 0, pb = 0, cap, i;
   double t0, t1, td[4];
   Genome_T genome = NULL;
   for (r = batch; r != NULL; r = r->next) {
@@ -411,6 +423,8 @@ shim_run (shim_req *batch) {
     case K_GENOME: GROW(D.rg, D.rgcap, ng + 1); D.rg[ng++] = r; break;
     case K_CDNA: GROW(D.rc, D.rccap, nc + 1); D.rc[nc++] = r; break;
     case K_STAGE2: GROW(D.r2, D.r2cap, n2 + 1); D.r2[n2++] = r; break;
+    case K_MXS: GROW(D.rxs, D.rxscap, nxs + 1); D.rxs[nxs++] = r; break;
+    case K_MXF: GROW(D.rxf, D.rxfcap, nxf + 1); D.rxf[nxf++] = r; break;
     default: GROW(D.ro, D.rocap, no + 1); D.ro[no++] = r; break;
     }
   }
@@ -520,6 +534,84 @@ shim_run (shim_req *batch) {
       r->cr = D.cres[i];
       shim_copy_pairs(r, D.pairs + r->cr.pair_offset, r->cr.npairs);
       r->cr.pair_offset = 0;
+    }
+  }
+
+  /* Dynprog_microexon_int: the candidate searches, then the choices of calls whose MaxEnt is done */
+  if (nxs > 0) {
+    size_t need = 0;
+    int rc;
+    GROW(D.mx, D.mxcap, nxs + 1);
+    GROW(D.mxres, D.mxrescap, nxs + 1);
+    qb = 0;
+    for (i = 0; i < nxs; i++) qb += D.rxs[i]->qlen;
+    GROW(D.q, D.qcap, qb + 1);
+    GROW(D.quc, D.quccap, qb + 1);
+    qb = 0;
+    for (i = 0; i < nxs; i++) {
+      r = D.rxs[i];
+      D.mx[i] = r->p.mx;
+      D.mx[i].qoff = (int32_t) qb;
+      memcpy(D.q + qb, r->q, r->qlen);
+      memcpy(D.quc + qb, r->quc, r->qlen);
+      qb += r->qlen;
+    }
+    GROW(D.mxc, D.mxccap, 8 * nxs + 64);
+    for (;;) {
+      rc = gmapdp_microexon_search(shim_ctx, D.mx, (int) nxs, D.q, D.quc, qb, D.mxres, D.mxc, D.mxccap, &need);
+      if (rc != GMAPDP_ESPACE) break;
+      GROW(D.mxc, D.mxccap, need + 64);
+    }
+    shim_check(rc, "gmapdp_microexon_search");
+    for (i = 0; i < nxs; i++) {
+      r = D.rxs[i];
+      r->mxr = D.mxres[i];
+      GROW(r->mxc, r->mxccap, (size_t) r->mxr.ncandidates + 1);
+      if (r->mxr.ncandidates > 0)
+        memcpy(r->mxc, D.mxc + r->mxr.cand_offset, (size_t) r->mxr.ncandidates * sizeof(gmapdp_microexon_candidate));
+      r->mxr.cand_offset = 0;
+    }
+  }
+  if (nxf > 0) {
+    size_t nct = 0, poff = 0;
+    GROW(D.mx, D.mxcap, nxf + 1);
+    GROW(D.mxres, D.mxrescap, nxf + 1);
+    qb = 0;
+    for (i = 0; i < nxf; i++) {
+      qb += D.rxf[i]->qlen;
+      nct += (size_t) D.rxf[i]->mxr.ncandidates;
+    }
+    GROW(D.q, D.qcap, qb + 1);
+    GROW(D.quc, D.quccap, qb + 1);
+    GROW(D.mxc, D.mxccap, nct + 1);
+    GROW(D.mxp, D.mxpcap, 2 * nct + 2);
+    qb = 0;
+    nct = 0;
+    for (i = 0; i < nxf; i++) {
+      r = D.rxf[i];
+      D.mx[i] = r->p.mx;
+      D.mx[i].qoff = (int32_t) qb;
+      memcpy(D.q + qb, r->q, r->qlen);
+      memcpy(D.quc + qb, r->quc, r->qlen);
+      qb += r->qlen;
+      D.mxres[i] = r->mxr;
+      D.mxres[i].cand_offset = (int64_t) nct;
+      if (r->mxr.ncandidates > 0) {
+        memcpy(D.mxc + nct, r->mxc, (size_t) r->mxr.ncandidates * sizeof(gmapdp_microexon_candidate));
+        memcpy(D.mxp + 2 * nct, r->mxp, 2 * (size_t) r->mxr.ncandidates * sizeof(double));
+      }
+      nct += (size_t) r->mxr.ncandidates;
+    }
+    cap = gmapdp_microexon_pair_capacity(D.mx, (int) nxf);
+    GROW(D.pairs, D.paircap, cap + 1);
+    shim_check(gmapdp_microexon_finish(shim_ctx, D.mx, (int) nxf, D.q, D.quc, qb, D.mxc, D.mxp, nct, D.mxres,
+                                       D.pairs, cap), "gmapdp_microexon_finish");
+    for (i = 0; i < nxf; i++) {
+      r = D.rxf[i];
+      r->mxr = D.mxres[i];
+      if (r->mxr.npairs > 0) shim_copy_pairs(r, D.pairs + r->mxr.pair_offset, r->mxr.npairs);
+      r->mxr.pair_offset = 0;
+      (void) poff;
     }
   }
 
@@ -909,6 +1001,72 @@ __wrap_Dynprog_cdna_gap (int *dynprogindex, int *traceback_score, bool *incomple
   if (r->cr.traceback_score != GMAPDP_UNSET) *traceback_score = r->cr.traceback_score;
   if (r->cr.incompletep) *incompletep = true;
   return list;
+}
+
+/* ---- Dynprog_microexon_int (dynprog_single.c:900, called at stage3.c:9664) ----
+   Two requests: the GPU lists the candidates, this thread scores them with the host's MaxEnt models (as
+   the reference does, maxent_hr.c), the GPU picks the winner and builds make_microexon_pairs_double's
+   list, which is rebuilt here in the caller's Pairpool with the gap holders' comp set. */
+List_T
+__wrap_Dynprog_microexon_int (double *bestprob2, double *bestprob3, int *dynprogindex, int *microintrontype,
+                              char *rsequence, char *rsequenceuc, int rlength, int roffset, int goffsetL,
+                              int rev_goffsetR, int cdna_direction, char *queryseq, char *queryuc,
+                              Univcoord_T chroffset, Univcoord_T chrhigh, bool watsonp, int genestrand,
+                              Genome_T genome, Genome_T genomealt, Pairpool_T pairpool) {
+  shim_req *r;
+  gmapdp_microexon_problem *p;
+  List_T list = NULL;
+  Pair_T gappair;
+  int k;
+  shim_check_call(genome, genomealt, NULL);
+  /* make_microexon_pairs_double reads queryseq[roffset + i]; the engine reads the slice */
+  if (rsequence != queryseq + roffset || rsequenceuc != queryuc + roffset)
+    shim_refuse("Dynprog_microexon_int with rsequence other than queryseq + roffset");
+  r = shim_request(K_MXS);
+  p = &r->p.mx;
+  p->qoff = 0;
+  p->rlength = rlength;
+  p->roffset = roffset;
+  p->goffsetL = goffsetL;
+  p->rev_goffsetR = rev_goffsetR;
+  p->cdna_direction = cdna_direction;
+  p->chroffset = shim_coord(chroffset);
+  p->chrhigh = shim_coord(chrhigh);
+  p->watsonp = watsonp ? 1 : 0;
+  p->genestrand = genestrand;
+  p->dynprogindex = *dynprogindex;
+  r->genome = genome;
+  r->q = rsequence;
+  r->quc = rsequenceuc;
+  r->qlen = (size_t) (rlength > 0 ? rlength : 0);
+  shim_submit(r);
+  GROW(r->mxp, r->mxpcap, 2 * (size_t) r->mxr.ncandidates + 2);
+  for (k = 0; k < r->mxr.ncandidates; k++) {
+    const gmapdp_microexon_candidate *c = &r->mxc[k];
+    r->mxp[2 * k] = shim_maxent(genome, genomealt, c->model2, c->pos2, chroffset);
+    r->mxp[2 * k + 1] = shim_maxent(genome, genomealt, c->model3, c->pos3, chroffset);
+  }
+  GROW(r->pairs, r->pcap, gmapdp_microexon_pair_capacity(p, 1) + 1);
+  r->kind = K_MXF;
+  shim_submit(r);
+  shim_count(ST_MICROEXON);
+  for (k = r->mxr.npairs - 1; k >= 0; k--) {
+    const gmapdp_pair *e = &r->pairs[k];
+    if (e->querypos == -1 && e->genomepos == -1) {
+      list = Pairpool_push_gapholder(list, pairpool, /*queryjump*/0, e->jump, /*leftpair*/NULL, /*rightpair*/NULL,
+                                     /*knownp*/false);
+      gappair = (Pair_T) list->first;
+      gappair->comp = e->comp;
+    } else {
+      list = Pairpool_push(list, pairpool, e->querypos, e->genomepos, e->cdna, e->comp, e->genome, e->genomealt,
+                           p->dynprogindex);
+    }
+  }
+  *bestprob2 = r->mxr.bestprob2;
+  *bestprob3 = r->mxr.bestprob3;
+  *microintrontype = r->mxr.microintrontype;
+  *dynprogindex = r->mxr.dynprogindex;
+  return r->mxr.npairs < 0 ? NULL : list;
 }
 
 /* ---- stage-2 seeding: Oligoindex_hr_tally + Oligoindex_get_mappings (oligoindex_hr.c:33849/34127) ----

@@ -7,7 +7,9 @@
  *
  *   -Wl,--wrap=Dynprog_init -Wl,--wrap=Dynprog_single_setup -Wl,--wrap=Dynprog_end_setup
  *   -Wl,--wrap=Dynprog_genome_setup -Wl,--wrap=Dynprog_single_gap -Wl,--wrap=Dynprog_end5_gap
- *   -Wl,--wrap=Dynprog_end3_gap -Wl,--wrap=Dynprog_genome_gap  gmapdp_gmap_shim.o -lgmapdp
+ *   -Wl,--wrap=Dynprog_end3_gap -Wl,--wrap=Dynprog_genome_gap -Wl,--wrap=Dynprog_cdna_gap
+ *   -Wl,--wrap=Dynprog_microexon_int -Wl,--wrap=Oligoindex_hr_tally -Wl,--wrap=Oligoindex_get_mappings
+ *   -Wl,--wrap=Stage2_setup -Wl,--wrap=Stage2_compute  gmapdp_gmap_shim.o -lgmapdp
  *
  * makes every existing call site (stage3.c) resolve to the __wrap_ functions
  * below, which have exactly the reference's prototypes:
@@ -16,6 +18,12 @@
  *   __wrap_Dynprog_end5_gap     replaces Dynprog_end5_gap     (dynprog_end.h:25,    dynprog_end.c:1294)
  *   __wrap_Dynprog_end3_gap     replaces Dynprog_end3_gap     (dynprog_end.h:47,    dynprog_end.c:1924)
  *   __wrap_Dynprog_genome_gap   replaces Dynprog_genome_gap   (dynprog_genome.h:24, dynprog_genome.c:3288)
+ *   __wrap_Dynprog_cdna_gap     replaces Dynprog_cdna_gap     (dynprog_cdna.h:18,   dynprog_cdna.c:787)
+ *   __wrap_Dynprog_microexon_int replaces Dynprog_microexon_int (dynprog_single.h:33, dynprog_single.c:900)
+ *   __wrap_Stage2_compute       replaces Stage2_compute       (stage2.h:58,         stage2.c:6325)
+ *   __wrap_Stage2_setup         observes Stage2_setup         (stage2.h:42,         stage2.c:129) and forwards it
+ *   __wrap_Oligoindex_hr_tally + __wrap_Oligoindex_get_mappings replace the stage-2 seeding pair
+ *                               (oligoindex_hr.h:106/117) for callers other than Stage2_compute
  *   __wrap_Dynprog_init / _single_setup / _end_setup / _genome_setup observe the
  *                               reference's setup calls (dynprog.c:1008, dynprog_single.c:101,
  *                               dynprog_end.c, dynprog_genome.c:192) and forward them
@@ -34,6 +42,11 @@
 #include "iit-read.h"
 #include "dynprog.h"
 #include "dynprog_end.h"
+#include "diagpool.h"
+#include "cellpool.h"
+#include "stopwatch.h"
+#include "oligoindex_hr.h"
+#include "stage2.h"
 
 extern void __wrap_Dynprog_init (Mode_T mode);
 extern void __wrap_Dynprog_single_setup (int user_open_in, int user_extend_in, bool user_dynprog_p_in,
@@ -80,5 +93,45 @@ __wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_r
                            Univcoord_T chrhigh, int cdna_direction, bool watsonp, int genestrand, bool jump_late_p,
                            Genome_T genome, Genome_T genomealt, Pairpool_T pairpool, int extraband_paired,
                            double defect_rate, int maxpeelback, bool halfp, bool finalp);
+
+extern List_T
+__wrap_Dynprog_cdna_gap (int *dynprogindex, int *traceback_score, bool *incompletep, Dynprog_T dynprogL,
+                         Dynprog_T dynprogR, char *rsequenceL, char *rsequence_ucL, char *rev_rsequenceR,
+                         char *rev_rsequence_ucR, int rlengthL, int rlengthR, int glength, int roffsetL,
+                         int rev_roffsetR, int goffset, Univcoord_T chroffset, Univcoord_T chrhigh, bool watsonp,
+                         int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
+                         Pairpool_T pairpool, int extraband_paired, double defect_rate);
+
+extern List_T
+__wrap_Dynprog_microexon_int (double *bestprob2, double *bestprob3, int *dynprogindex, int *microintrontype,
+                              char *rsequence, char *rsequenceuc, int rlength, int roffset, int goffsetL,
+                              int rev_goffsetR, int cdna_direction, char *queryseq, char *queryuc,
+                              Univcoord_T chroffset, Univcoord_T chrhigh, bool watsonp, int genestrand,
+                              Genome_T genome, Genome_T genomealt, Pairpool_T pairpool);
+
+extern void
+__wrap_Oligoindex_hr_tally (Oligoindex_T this, Univcoord_T mappingstart, Univcoord_T mappingend, bool plusp,
+                            char *queryuc_ptr, int querystart, int queryend, Chrpos_T chrpos, Genome_T genome,
+                            int genestrand);
+
+extern List_T
+__wrap_Oligoindex_get_mappings (List_T diagonals, bool *coveredp, Chrpos_T **mappings, int *npositions,
+                                int *totalpositions, bool *oned_matrix_p, int *maxnconsecutive,
+                                Oligoindex_array_T array, Oligoindex_T this, char *queryuc_ptr, int querystart,
+                                int queryend, int querylength, Chrpos_T chrstart, Chrpos_T chrend,
+                                Univcoord_T chroffset, Univcoord_T chrhigh, bool plusp, Diagpool_T diagpool);
+
+extern void
+__wrap_Stage2_setup (bool splicingp_in, bool cross_species_p, int suboptimal_score_start_in,
+                     int suboptimal_score_end_in, int sufflookback_in, int nsufflookback_in, int maxintronlen_in,
+                     Mode_T mode_in, bool snps_p_in);
+
+extern List_T
+__wrap_Stage2_compute (char *queryseq_ptr, char *queryuc_ptr, int querylength, int query_offset, Chrpos_T chrstart,
+                       Chrpos_T chrend, Univcoord_T chroffset, Univcoord_T chrhigh, bool plusp, int genestrand,
+                       Stage2_alloc_T stage2_alloc, double proceed_pctcoverage, Oligoindex_array_T oligoindices,
+                       Genome_T genome, Genome_T genomealt, Pairpool_T pairpool, Diagpool_T diagpool,
+                       Cellpool_T cellpool, bool localp, bool skip_repetitive_p, bool favor_right_p,
+                       int max_nalignments, Stopwatch_T stopwatch, bool diag_debug);
 
 #endif

@@ -117,7 +117,7 @@ all: programs $(foreach v,$(VARIANTS),$(OUT)/librefdp_$(v).so) \
 # build would) and libgmapdp.so.  Tests call it through the same refh_* entry points.
 WRAPPED    := Dynprog_init Dynprog_single_setup Dynprog_end_setup Dynprog_genome_setup \
               Dynprog_single_gap Dynprog_end5_gap Dynprog_end3_gap Dynprog_genome_gap Dynprog_cdna_gap \
-              Oligoindex_hr_tally Oligoindex_get_mappings Stage2_setup Stage2_compute
+              Dynprog_microexon_int Oligoindex_hr_tally Oligoindex_get_mappings Stage2_setup Stage2_compute
 
 $(OUT)/gpushim/gmapdp_gmap_shim.o: $(SHIM_SRC) ../include/gmapdp.h
 	@mkdir -p $(dir $@)

@@ -104,7 +104,7 @@ def test_gpu_gmap_cdna2_genetest2(build):
 @pytest.mark.parametrize("build", BUILDS)
 def test_gpu_gmap_synthetic_reads(build):
     """200 spliced 2-kb reads: every SAM record identical to the reference build's; every DP family and
-    Stage2_compute (seeding + chaining) ran on the GPU (no GMAPDP_EINVAL domain refusal: the shim aborts on one)."""
+    Stage2_compute (seeding + chaining) and Dynprog_microexon_int ran on the GPU (no GMAPDP_EINVAL domain refusal: the shim aborts on one)."""
     out, err = _run(_exe("gmap_gpu_" + build), E2E_ARGS, env={"GMAPDP_SHIM_STATS": "1"})
     st = _stats(err)
     exp = _read("e2e_%s.sam" % build).splitlines()
@@ -112,7 +112,7 @@ def test_gpu_gmap_synthetic_reads(build):
     bad = [i for i, (x, y) in enumerate(zip(got, exp)) if x != y]
     assert len(got) == len(exp) and not bad, "reads differing: %s" % bad[:10]
     for k in ("Dynprog_single_gap", "Dynprog_genome_gap", "Dynprog_end5_gap", "Dynprog_end3_gap",
-              "Stage2_compute"):
+              "Stage2_compute", "Dynprog_microexon_int"):
         assert st[k] > 0, st
 
 

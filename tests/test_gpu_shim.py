@@ -128,3 +128,25 @@ def test_shim_stage2_compute(build):
     probs = [p for p in probs if len(p["quc"]) > 8]
     bad = [i for i, p in enumerate(probs) if shim.stage2_compute(p) != ref.stage2_compute(p)]
     assert bad == []
+
+
+@pytest.mark.parametrize("build", ["nosimd", "avx2"])
+def test_shim_microexon_int(build):
+    """Dynprog_microexon_int wrapped (mx_search_kernel, the host's MaxEnt, mx_finish_kernel): the list,
+    its gap holders' comp and every out-parameter equal the unmodified reference objects'."""
+    from dpbind import microexon_problem, random_genome
+    refv, shimv = ("nosimd", "gpushim") if build == "nosimd" else ("avx2a", "gpushim_avx2")
+    if not (ref_available(refv) and ref_available(shimv)):
+        pytest.skip("reference objects did not travel")
+    ref, shim = Ref(refv), Ref(shimv)
+    rng = random.Random(1030)
+    g = bytearray(random_genome(rng, 1500000))
+    at = [100]
+    probs = [microexon_problem(rng, g, edge=(i % 4 == 0), at=at) for i in range(300)]
+    g = bytes(g)
+    ref.set_genome(g)
+    shim.set_genome(g)
+    exp = [ref.microexon_int(p) for p in probs]
+    bad = [i for i, p in enumerate(probs) if shim.microexon_int(p) != exp[i]]
+    assert bad == []
+    assert sum(e[2] is not None for e in exp) > 100
