@@ -1572,6 +1572,7 @@ __global__ __launch_bounds__(64) void s2c_kernel(
   (void)diag_all; (void)counters; (void)scratch_cap; (void)paths_out; (void)path_cap; (void)pairs_out; (void)pair_cap;
   gmapdp_stage2_result R = results[P.index];
   if (R.status != kS2Chained) return;
+  S2_MARK(12);
   const int qstart = R.diag_querystart, qend = R.diag_queryend;
   // ---- get_cells_fwd + the path loop: cells within FINAL_SCORE_TOLERANCE of the best, each the best
   // of its root position, in (score desc, root asc, querypos desc, hit asc) order ----

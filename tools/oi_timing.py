@@ -75,11 +75,13 @@ def main_s2(reads=10000):
     t, c = marks[:16].astype(np.float64), marks[16:]
     dur = [float(t[k + 1] - t[k]) for k in range(7)]
     tot = sum(dur)
+    s2c = {n: round(float(t[b] - t[a]) / 1e2 / max(int(c[0]), 1), 1)
+           for n, a, b in (("cells_us", 12, 5), ("traceback_filter_us", 5, 6), ("convert_us", 6, 7))}
     cnt = {k: round(float(marks[i]) / 1e2 / max(int(c[0]), 1), 1)
            for k, i in (("sweep_meta_us", 8), ("sweep_one_us", 9), ("sweep_mult_us", 10), ("sweep_tail_us", 11))}
     print(json.dumps({"waves": [int(x) for x in c[:8]], "phases": {n: round(d / tot, 4) for n, d in zip(S2_PHASES, dur)},
                       "mean_wave_us": tot / 1e2 / max(int(c[0]), 1), "status": np.bincount(res["status"] + 3).tolist(),
-                      "counts": cnt}))
+                      "counts": cnt, "s2c_per_wave": s2c}))
     eng.close()
 
 
