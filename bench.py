@@ -8,7 +8,8 @@ stage2 + all Dynprog_* paths"), gmap-2024_amd/gmapdp/workload.py:
     call (gmap.c:1208: Oligoindex_hr_tally + Oligoindex_get_mappings over the read's gregion, then the
     chaining -- Diag_compute_bounds, align_compute_lookback, convert_to_nucleotides,
     Stage2_filter_unique) and 43.7 Dynprog_single_gap + 7.1 Dynprog_end5_gap + 6.5 Dynprog_end3_gap +
-    49.4 Dynprog_genome_gap.
+    49.4 Dynprog_genome_gap + 25.6 Dynprog_microexon_int (over genome-gap gaps; the MaxEnt scores
+    between its search and its choice are synthetic device inputs, the engine takes MaxEnt as input).
 One step = one pass of the engine over every call of --reads reads (Stage2_compute on its own
 stream, the DP launch classes on four more, joined at the end of the step); the batch is generated
 once and replayed, every step recomputes everything.  Inputs (descriptors, query arenas, splice
@@ -208,6 +209,20 @@ def main():
                                              data["oq"].ctypes.data, len(data["oq"]), C.byref(oplan)),
                "gmapdp_stage2_plan_create")
     t_oplan = time.perf_counter() - t0
+    # Dynprog_microexon_int per read (stage3.c:9664) over genome-gap gaps: search + choice; the MaxEnt
+    # probabilities between them are synthetic device inputs (the engine takes MaxEnt as an input)
+    mp = data["microexon"]
+    mplan = C.c_void_p()
+    eng._check(lib.gmapdp_microexon_plan_create(eng.h, mp.ctypes.data, len(mp), data["q"].ctypes.data,
+                                                data["q"].ctypes.data, len(data["q"]), C.byref(mplan)),
+               "gmapdp_microexon_plan_create")
+    ncands = lib.gmapdp_microexon_plan_candidates(mplan)
+    d_mres = torch.zeros(max(len(mp), 1) * gmapdp.MICROEXON_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    d_mpairs = torch.empty(max(lib.gmapdp_microexon_plan_pair_capacity(mplan), 1) * 16, dtype=torch.uint8,
+                           device=dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(77)
+    d_mxp = torch.rand(max(2 * ncands, 2), dtype=torch.float64, device=dev, generator=gen)
     ngpu, nggpu = lib.gmapdp_plan_gpu_problems(plan), lib.gmapdp_plan_genome_gpu_problems(plan)
     cap = lib.gmapdp_plan_pair_capacity(plan)
     d_res = torch.zeros(max(ngpu, 1) * 32, dtype=torch.uint8, device=dev)
@@ -242,6 +257,12 @@ def main():
                                               C.c_void_p(d_s2res.data_ptr()), what, C.c_void_p(s.cuda_stream)),
                    "gmapdp_stage2_plan_run")
 
+    def mrun(s, what):
+        eng._check(lib.gmapdp_microexon_plan_run(eng.h, mplan, C.c_void_p(d_q.data_ptr()), C.c_void_p(d_q.data_ptr()),
+                                                 C.c_void_p(d_mxp.data_ptr()), C.c_void_p(d_mres.data_ptr()),
+                                                 C.c_void_p(d_mpairs.data_ptr()), what, C.c_void_p(s.cuda_stream)),
+                   "gmapdp_microexon_plan_run")
+
     def step(do_oligo=True, do_dp=True, ev=None):
         fork = torch.cuda.Event()
         fork.record(stream)
@@ -268,6 +289,11 @@ def main():
                 launch(li, s)
                 if ev is not None:
                     ev["dp"][li][1].record(s)
+            if ev is not None:
+                ev["mx"][0].record(stream)
+            mrun(stream, 3)
+            if ev is not None:
+                ev["mx"][1].record(stream)
         for k in used:
             stream.wait_stream(sides[k - 1])
         if do_oligo:
@@ -279,7 +305,7 @@ def main():
             for _ in range(warmup):
                 step(**kw)
             torch.cuda.synchronize()
-            evs = [{"oligo": mk(), "chain": mk(), "dp": [mk() for _ in range(nl)]} for _ in range(steps)]
+            evs = [{"oligo": mk(), "chain": mk(), "mx": mk(), "dp": [mk() for _ in range(nl)]} for _ in range(steps)]
             if world > 1:
                 dist.barrier()
             torch.cuda.synchronize()
@@ -297,10 +323,11 @@ def main():
             if kw.get("do_dp", True) else None
         o_ms = sum(e["oligo"][0].elapsed_time(e["oligo"][1]) for e in evs) / steps if kw.get("do_oligo", True) else None
         c_ms = sum(e["oligo"][1].elapsed_time(e["chain"][1]) for e in evs) / steps if kw.get("do_oligo", True) else None
-        return elapsed, dp_ms, (o_ms, c_ms)
+        m_ms = sum(e["mx"][0].elapsed_time(e["mx"][1]) for e in evs) / steps if kw.get("do_dp", True) else None
+        return elapsed, dp_ms, (o_ms, c_ms, m_ms)
 
     # ---- headline: stage-2 seeding + every Dynprog_* call of the batch ----
-    elapsed, launch_ms, (oligo_ms, chain_ms) = timed(args.steps, args.warmup)
+    elapsed, launch_ms, (oligo_ms, chain_ms, mx_ms) = timed(args.steps, args.warmup)
     # split of the same step (fewer steps): each half alone
     half = max(2, args.steps // 4)
     el_dp, _, _ = timed(half, 1, do_oligo=False)
@@ -336,6 +363,8 @@ def main():
     disp.append(("gmapdp::oi_kernel<unsigned short>+gmapdp::oi_map_kernel", None, oligo_ms, len(op)))
     cbytes = chain_algorithmic_bytes(op, s2res)
     disp.append(("gmapdp::s2c_kernel", cbytes, chain_ms, len(op)))
+    disp.append(("gmapdp::mx_search_kernel+gmapdp::mx_finish_kernel", None, mx_ms, len(mp)))
+    mres = np.frombuffer(d_mres.cpu().numpy().tobytes(), dtype=gmapdp.MICROEXON_RESULT_DTYPE)
     # the kernel template with the most time per step
     tot = {}
     for name, nb, ms, _ in disp:
@@ -367,12 +396,13 @@ def main():
         "config": {"workload": "configs[2]: synthetic 2-kb cDNA reads (5 exons x 400 nt, 2 %% subs) vs a "
                                "GRCh38-layout i.i.d. genome (24 chromosomes, %d nt, universal coordinates to %d): per "
                                "read 1 Stage2_compute call (seeding + chaining) + %.1f Dynprog_single_gap + %.1f Dynprog_end5_gap + "
-                               "%.1f Dynprog_end3_gap + %.1f Dynprog_genome_gap; inputs HBM-resident; host "
-                               "stages 1/3 not in the step"
+                               "%.1f Dynprog_end3_gap + %.1f Dynprog_genome_gap + %.1f Dynprog_microexon_int; inputs "
+                               "HBM-resident; host stages 1/3 not in the step"
                                % (layout.total, layout.total - 1, W.SINGLE_PER_READ, W.END5_PER_READ,
-                                  W.END3_PER_READ, W.GENOME_PER_READ),
+                                  W.END3_PER_READ, W.GENOME_PER_READ, W.MICROEXON_PER_READ),
                    "genome": args.genome, "reads_per_step_per_gpu": args.reads,
-                   "subproblems_per_step_per_gpu": {"stage2_compute": len(op), "single": ns, "end": ne, "genome": ng},
+                   "subproblems_per_step_per_gpu": {"stage2_compute": len(op), "single": ns, "end": ne, "genome": ng,
+                                                    "microexon": len(mp)},
                    "banded_cells_per_step_per_gpu": cells,
                    "parallelism": "dp%d (reads sharded by rank, genome replicated)" % world},
         "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
@@ -390,14 +420,18 @@ def main():
     }
     # spot check of the step's outputs: size-independent invariants (the oracle parity is tests/)
     assert np.all(res["npairs"] >= 0) and np.all(gres["npairs"] >= 0) and np.all(s2res["status"] >= 0)
+    assert np.all(mres["ncandidates"] >= 0) and np.all(mres["cand_offset"] >= 0)
     out["checks"] = {"pairs_per_read": float((npairs.sum() + gnp.sum()) / args.reads),
                      "genome_gaps_bridged": int((gnp > 0).sum()),
                      "stage2_chained": int((s2res["status"] == 2).sum()),
                      "stage2_results": int(s2res["nresults"].sum()),
                      "stage2_path_pairs_per_read": float(s2res["npairs"].sum() / args.reads),
-                     "stage2_scratch_mb": sb_.value / 1e6}
+                     "stage2_scratch_mb": sb_.value / 1e6,
+                     "microexon_candidates": int(ncands),
+                     "microexons_found": int((mres["npairs"] > 0).sum())}
     lib.gmapdp_plan_destroy(plan)
     lib.gmapdp_stage2_plan_destroy(oplan)
+    lib.gmapdp_microexon_plan_destroy(mplan)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baselines()
         out["cpu_baseline"] = cb.get("avx2")

@@ -93,7 +93,7 @@ hipError_t launch_mx_search(int n, hipStream_t s, const gmapdp_microexon_problem
 hipError_t launch_mx_finish(int n, hipStream_t s, const gmapdp_microexon_problem* probs, const uint32_t* blocks,
                             uint64_t nwords, const char* qseq, const char* qseq_uc, const uint8_t* constab,
                             const gmapdp_microexon_candidate* cands, const double* cand_probs,
-                            gmapdp_microexon_result* results, gmapdp_pair* pairs);
+                            gmapdp_microexon_result* results, gmapdp_pair* pairs, const int64_t* poff);
 static const int kUse8pSize[4] = {41, 63, 127, 24};  // use8p_size (dynprog.c:1022-1025)
 
 // ---------------------------------------------------------------------------
@@ -2202,7 +2202,7 @@ extern "C" int gmapdp_microexon_finish(gmapdp_ctx* ctx, const gmapdp_microexon_p
     e = launch_mx_finish(n, s, (const gmapdp_microexon_problem*)ctx->mxprobs.p, ctx->d_genome, ctx->genome_words,
                          (const char*)ctx->qseq.p, (const char*)ctx->qseq_uc.p, ctx->d_cs,
                          (const gmapdp_microexon_candidate*)ctx->mxcands.p, (const double*)ctx->mxprobs2.p,
-                         (gmapdp_microexon_result*)ctx->mxres.p, (gmapdp_pair*)ctx->mxpairs.p);
+                         (gmapdp_microexon_result*)ctx->mxres.p, (gmapdp_pair*)ctx->mxpairs.p, nullptr);
   if (e == hipSuccess)
     e = hipMemcpyAsync(results, ctx->mxres.p, sizeof(gmapdp_microexon_result) * n, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipMemcpyAsync(pairs, ctx->mxpairs.p, sizeof(gmapdp_pair) * poff, hipMemcpyDeviceToHost, s);
@@ -2210,6 +2210,96 @@ extern "C" int gmapdp_microexon_finish(gmapdp_ctx* ctx, const gmapdp_microexon_p
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "microexon finish: %s", e);
   return GMAPDP_OK;
 }
+
+// Device-resident microexon plan (bench / pipelined callers): the search is run once at plan time to
+// size every call's candidate region exactly, so the plan's runs write candidates straight to fixed
+// regions (no atomics, deterministic offsets) and the caller's probabilities line up with them.
+struct gmapdp_microexon_plan {
+  int n = 0;
+  size_t ncands = 0, npairs = 0;
+  gmapdp_microexon_problem* d_probs = nullptr;
+  int64_t* d_direct = nullptr;
+  int64_t* d_poff = nullptr;
+  gmapdp_microexon_candidate* d_cands = nullptr;
+  unsigned long long* d_counter = nullptr;
+};
+
+static void mx_plan_free(gmapdp_microexon_plan* P) {
+  if (!P) return;
+  for (void* b : {(void*)P->d_probs, (void*)P->d_direct, (void*)P->d_poff, (void*)P->d_cands, (void*)P->d_counter})
+    if (b) (void)hipFree(b);
+  delete P;
+}
+
+extern "C" int gmapdp_microexon_plan_create(gmapdp_ctx* ctx, const gmapdp_microexon_problem* problems, int n,
+                                            const char* qseq, const char* qseq_uc, size_t qbytes,
+                                            gmapdp_microexon_plan** plan) {
+  if (!ctx || !plan || n < 0 || (n > 0 && (!problems || !qseq || !qseq_uc))) return GMAPDP_EINVAL;
+  *plan = nullptr;
+  if (!ctx->d_genome) return GMAPDP_ENOGENOME;
+  std::vector<gmapdp_microexon_result> res(std::max(n, 1));
+  size_t need = 0;
+  int rc = gmapdp_microexon_search(ctx, problems, n, qseq, qseq_uc, qbytes, res.data(), nullptr, 0, &need);
+  if (rc && rc != GMAPDP_ESPACE) return rc;
+  std::vector<int64_t> direct(std::max(n, 1)), poff(std::max(n, 1));
+  size_t c = 0, q = 0;
+  for (int i = 0; i < n; i++) {
+    direct[i] = (int64_t)c;
+    c += (size_t)res[i].ncandidates;
+    poff[i] = (int64_t)q;
+    q += (size_t)std::max(problems[i].rlength, 0) + 2;
+  }
+  gmapdp_microexon_plan* P = new gmapdp_microexon_plan();
+  P->n = n;
+  P->ncands = c;
+  P->npairs = q;
+  hipError_t e = hipMalloc(&P->d_probs, sizeof(gmapdp_microexon_problem) * std::max(n, 1));
+  if (e == hipSuccess) e = hipMalloc(&P->d_direct, sizeof(int64_t) * std::max(n, 1));
+  if (e == hipSuccess) e = hipMalloc(&P->d_poff, sizeof(int64_t) * std::max(n, 1));
+  if (e == hipSuccess) e = hipMalloc(&P->d_cands, sizeof(gmapdp_microexon_candidate) * std::max<size_t>(c, 1));
+  if (e == hipSuccess) e = hipMalloc(&P->d_counter, sizeof(unsigned long long));
+  if (e == hipSuccess && n)
+    e = hipMemcpy(P->d_probs, problems, sizeof(gmapdp_microexon_problem) * n, hipMemcpyHostToDevice);
+  if (e == hipSuccess && n) e = hipMemcpy(P->d_direct, direct.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice);
+  if (e == hipSuccess && n) e = hipMemcpy(P->d_poff, poff.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    mx_plan_free(P);
+    return fail(ctx, GMAPDP_ENOMEM, "microexon plan: %s", e);
+  }
+  *plan = P;
+  return GMAPDP_OK;
+}
+
+extern "C" size_t gmapdp_microexon_plan_candidates(const gmapdp_microexon_plan* plan) { return plan ? plan->ncands : 0; }
+extern "C" size_t gmapdp_microexon_plan_pair_capacity(const gmapdp_microexon_plan* plan) {
+  return plan ? plan->npairs : 0;
+}
+
+extern "C" int gmapdp_microexon_plan_run(gmapdp_ctx* ctx, const gmapdp_microexon_plan* plan, const char* d_qseq,
+                                         const char* d_qseq_uc, const double* d_cand_probs,
+                                         gmapdp_microexon_result* d_results, gmapdp_pair* d_pairs, int what,
+                                         void* stream) {
+  if (!ctx || !plan || !d_results) return GMAPDP_EINVAL;
+  if (plan->n == 0) return GMAPDP_OK;
+  if ((what & 2) && ((plan->ncands && !d_cand_probs) || !d_pairs)) return GMAPDP_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  hipError_t e = hipSuccess;
+  if (what & 1)
+    e = launch_mx_search(plan->n, s, plan->d_probs, ctx->d_genome, ctx->genome_words, d_qseq, d_qseq_uc,
+                         d_results, plan->d_cands, plan->ncands, plan->d_counter, plan->d_direct);
+  if (e == hipSuccess && (what & 2))
+    e = launch_mx_finish(plan->n, s, plan->d_probs, ctx->d_genome, ctx->genome_words, d_qseq, d_qseq_uc, ctx->d_cs,
+                         plan->d_cands, d_cand_probs, d_results, d_pairs, plan->d_poff);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "microexon plan launch: %s", e);
+  return GMAPDP_OK;
+}
+
+extern "C" const gmapdp_microexon_candidate* gmapdp_microexon_plan_device_candidates(const gmapdp_microexon_plan* plan) {
+  return plan ? plan->d_cands : nullptr;
+}
+
+extern "C" void gmapdp_microexon_plan_destroy(gmapdp_microexon_plan* plan) { mx_plan_free(plan); }
 
 // Test instrumentation: the chaining scratch of the last gmapdp_stage2_batch (its layout is
 // s2_scratch in s2c_kernel.hip; for a one-problem batch it starts at byte 0).

@@ -174,12 +174,14 @@ __global__ __launch_bounds__(64) void mx_finish_kernel(const gmapdp_microexon_pr
                                                        const gmapdp_microexon_candidate* __restrict__ cands,
                                                        const double* __restrict__ cand_probs,
                                                        gmapdp_microexon_result* __restrict__ results,
-                                                       gmapdp_pair* __restrict__ pairs) {
+                                                       gmapdp_pair* __restrict__ pairs,
+                                                       const int64_t* __restrict__ poff) {
   const int pi = blockIdx.x;
   if (pi >= n) return;
   const int lane = threadIdx.x;
   const gmapdp_microexon_problem P = probs[pi];
   gmapdp_microexon_result R = results[pi];
+  if (poff) R.pair_offset = poff[pi];
   R.dynprogindex = P.dynprogindex;
   R.npairs = -1;
   R.bestprob2 = R.bestprob3 = 0.0;
@@ -286,10 +288,10 @@ hipError_t launch_mx_search(int n, hipStream_t s, const gmapdp_microexon_problem
 hipError_t launch_mx_finish(int n, hipStream_t s, const gmapdp_microexon_problem* probs, const uint32_t* blocks,
                             uint64_t nwords, const char* qseq, const char* qseq_uc, const uint8_t* constab,
                             const gmapdp_microexon_candidate* cands, const double* cand_probs,
-                            gmapdp_microexon_result* results, gmapdp_pair* pairs) {
+                            gmapdp_microexon_result* results, gmapdp_pair* pairs, const int64_t* poff) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(mx_finish_kernel, dim3(n), dim3(64), 0, s, probs, n, blocks, nwords, qseq, qseq_uc, constab,
-                     cands, cand_probs, results, pairs);
+                     cands, cand_probs, results, pairs, poff);
   return hipGetLastError();
 }
 

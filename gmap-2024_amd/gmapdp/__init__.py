@@ -235,6 +235,14 @@ def load_library(path=LIB_PATH):
                                               C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
                                               C.c_size_t]),
         "gmapdp_microexon_pair_capacity": (C.c_size_t, [C.c_void_p, C.c_int]),
+        "gmapdp_microexon_plan_create": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                                   C.c_size_t, P(C.c_void_p)]),
+        "gmapdp_microexon_plan_candidates": (C.c_size_t, [C.c_void_p]),
+        "gmapdp_microexon_plan_pair_capacity": (C.c_size_t, [C.c_void_p]),
+        "gmapdp_microexon_plan_device_candidates": (C.c_void_p, [C.c_void_p]),
+        "gmapdp_microexon_plan_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
+        "gmapdp_microexon_plan_destroy": (None, [C.c_void_p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -29,6 +29,7 @@ END5_PER_READ = 7.1            # Dynprog_end5_gap
 END3_PER_READ = 6.5            # Dynprog_end3_gap
 GENOME_PER_READ = 49.4         # Dynprog_genome_gap
 STAGE2_PER_READ = 1            # Stage2_compute seeding calls
+MICROEXON_PER_READ = 25.6      # Dynprog_microexon_int
 
 COMPL = np.zeros(256, dtype=np.uint8)
 for _a, _b in zip(b"ACGTN", b"TGCAN"):
@@ -247,6 +248,23 @@ def make_stage2(genome, layout, n, rng, exons=5, exlen=400, pad=1000):
     return probs, q.reshape(-1)
 
 
+def make_microexon(gp, n, rng):
+    """Dynprog_microexon_int calls (stage3.c:9664): stage 3 tries a microexon inside a genome gap it
+    just bridged (a noncanonical intron or one that scores below the peeled anchors), over the same
+    gap: rsequence = the query gap, goffsetL = genomedp5, rev_goffsetR = genomedp3.  So the calls are
+    the first n genome-gap sub-problems' gaps (their query slices in the same arena), cdna_direction as
+    there.  Returns a gmapdp_microexon_problem array."""
+    import gmapdp
+    k = np.arange(n) % len(gp)
+    g = gp[k]
+    mp = np.zeros(n, dtype=gmapdp.MICROEXON_PROBLEM_DTYPE)
+    for f in ("qoff", "rlength", "roffset", "goffsetL", "rev_goffsetR", "cdna_direction", "chroffset", "chrhigh",
+              "genestrand", "dynprogindex"):
+        mp[f] = g[f]
+    mp["watsonp"] = (g["flags"] & gmapdp.WATSON) != 0
+    return mp
+
+
 def make_reads(genome, layout, reads, seed, site_seed=23):
     """The per-read call stream of `reads` reads: dict of descriptor arrays and arenas.  Genome gaps
     plant their intron motifs first (in place), then every other sub-problem is cut."""
@@ -263,5 +281,6 @@ def make_reads(genome, layout, reads, seed, site_seed=23):
     gp["qoff"] += len(sq) + len(eq)
     q = np.concatenate([sq, eq, gq])
     op, oq = make_stage2(genome, layout, reads, np.random.default_rng(seed + 3))
+    mp = make_microexon(gp, int(round(reads * MICROEXON_PER_READ)), np.random.default_rng(seed + 4))
     return {"single": sp, "end": ep, "genome": gp, "q": q, "sprob": sprob, "oligo": op, "oq": oq,
-            "reads": reads}
+            "microexon": mp, "reads": reads}

@@ -367,6 +367,25 @@ int gmapdp_microexon_finish (gmapdp_ctx *ctx, const gmapdp_microexon_problem *pr
                              gmapdp_microexon_result *results, gmapdp_pair *pairs, size_t pair_capacity);
 size_t gmapdp_microexon_pair_capacity (const gmapdp_microexon_problem *problems, int n);
 
+/* Device-resident microexon plan (the bench's path): descriptors uploaded once; the search is run at
+ * plan time to size each call's candidate region, so gmapdp_microexon_plan_run writes candidates to
+ * fixed regions (call i's at the prefix sum of the earlier calls' counts, device array
+ * gmapdp_microexon_plan_device_candidates) and d_cand_probs (2 doubles per candidate, that order)
+ * lines up with them.  what: 1 search, 2 finish, 3 both; qoff index the device arenas d_qseq /
+ * d_qseq_uc; d_results (n records) and d_pairs (gmapdp_microexon_plan_pair_capacity records, call i's
+ * at the prefix sum of rlength + 2) are the caller's device buffers. */
+typedef struct gmapdp_microexon_plan gmapdp_microexon_plan;
+int gmapdp_microexon_plan_create (gmapdp_ctx *ctx, const gmapdp_microexon_problem *problems, int n,
+                                  const char *qseq, const char *qseq_uc, size_t qbytes,
+                                  gmapdp_microexon_plan **plan);
+size_t gmapdp_microexon_plan_candidates (const gmapdp_microexon_plan *plan);
+size_t gmapdp_microexon_plan_pair_capacity (const gmapdp_microexon_plan *plan);
+const gmapdp_microexon_candidate *gmapdp_microexon_plan_device_candidates (const gmapdp_microexon_plan *plan);
+int gmapdp_microexon_plan_run (gmapdp_ctx *ctx, const gmapdp_microexon_plan *plan, const char *d_qseq,
+                               const char *d_qseq_uc, const double *d_cand_probs, gmapdp_microexon_result *d_results,
+                               gmapdp_pair *d_pairs, int what, void *stream);
+void gmapdp_microexon_plan_destroy (gmapdp_microexon_plan *plan);
+
 /* Stage-2 seeding: Oligoindex_hr_tally + Oligoindex_get_mappings
  * (oligoindex_hr.c:33849/34127) as Stage2_compute runs them for GMAP (stage2.c:6413-6501: one
  * 8-mer oligoindex, coveredp all false).  One problem = one (query, genomic window) pair:

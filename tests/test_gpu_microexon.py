@@ -113,3 +113,67 @@ def test_gpu_microexon_empty_and_direction0(engine):
     got = engine.microexon_batch([call], lambda m, pos, c: 0.5)
     assert got == [orc.microexon_int(call, [])] == [((1, 0), (0.0, 0.0), None)]
     assert engine.microexon_batch([], lambda m, pos, c: 0.5) == []
+
+
+def test_gpu_microexon_plan_matches_batch(engine):
+    """The device-resident plan (bench.py's path: fixed candidate regions, caller-owned device outputs)
+    gives the synchronous API's results and pairs."""
+    import ctypes as C
+    import numpy as np
+    rng = random.Random(9800)
+    g = bytearray(random_genome(rng, 1500000))
+    at = [100]
+    probs = [microexon_problem(rng, g, edge=(i % 4 == 0), at=at) for i in range(400)]
+    g = bytes(g)
+    engine.set_genome(g)
+    table = {}
+
+    def maxent(m, pos, chroffset):
+        return table.setdefault((m, pos), random.Random(m * 1000003 + pos).random())
+    exp = engine.microexon_batch(probs, maxent)
+    cands = engine.microexon_candidates(probs)
+    mp, qb, qub = engine.build_microexon_batch(probs)
+    lib = engine.lib
+    plan = C.c_void_p()
+    engine._check(lib.gmapdp_microexon_plan_create(engine.h, mp.ctypes.data, len(mp), qb, qub, len(qb),
+                                                   C.byref(plan)), "gmapdp_microexon_plan_create")
+    try:
+        assert lib.gmapdp_microexon_plan_candidates(plan) == sum(len(c or []) for c in cands)
+        cp = np.array([maxent(x[m], x[p], 0) for c in cands for x in (c or []) for p, m in ((4, 5), (6, 7))]
+                      + [0.0, 0.0])
+        hip = C.CDLL("libamdhip64.so")  # test plumbing: device buffers for the plan's caller-owned outputs
+        hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+        hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        hip.hipFree.argtypes = [C.c_void_p]
+
+        def dbuf(nbytes, src=None):
+            ptr = C.c_void_p()
+            assert hip.hipMalloc(C.byref(ptr), max(nbytes, 16)) == 0
+            if src is not None:
+                assert hip.hipMemcpy(ptr, src, nbytes, 1) == 0  # hipMemcpyHostToDevice
+            return ptr
+        npc = lib.gmapdp_microexon_plan_pair_capacity(plan)
+        d_q = dbuf(len(qb), qb)
+        d_quc = dbuf(len(qub), qub)
+        d_cp = dbuf(cp.nbytes, cp.ctypes.data)
+        d_res = dbuf(len(mp) * gmapdp.MICROEXON_RESULT_DTYPE.itemsize)
+        d_pairs = dbuf(npc * 16)
+        engine._check(lib.gmapdp_microexon_plan_run(engine.h, plan, d_q, d_quc, d_cp, d_res, d_pairs, 3, None),
+                      "gmapdp_microexon_plan_run")
+        assert hip.hipDeviceSynchronize() == 0  # the plan ran on the engine's own (non-blocking) stream
+        res = np.zeros(len(mp), dtype=gmapdp.MICROEXON_RESULT_DTYPE)
+        pairs = np.zeros(max(npc, 1), dtype=gmapdp.PAIR_DTYPE)
+        assert hip.hipMemcpy(res.ctypes.data, d_res, res.nbytes, 2) == 0  # hipMemcpyDeviceToHost (synchronous)
+        assert hip.hipMemcpy(pairs.ctypes.data, d_pairs, npc * 16, 2) == 0
+        for b in (d_q, d_quc, d_cp, d_res, d_pairs):
+            hip.hipFree(b)
+    finally:
+        lib.gmapdp_microexon_plan_destroy(plan)
+    for i, (p, r, e) in enumerate(zip(probs, res, exp)):
+        assert (int(r["dynprogindex"]), int(r["microintrontype"])) == e[0], i
+        assert (float(r["bestprob2"]), float(r["bestprob3"])) == e[1], i
+        assert int(r["npairs"]) == (-1 if e[2] is None else len(e[2])), i
+        if e[2]:
+            got = pairs[int(r["pair_offset"]):int(r["pair_offset"]) + int(r["npairs"])]
+            assert [int(x["genomepos"]) for x in got] == [x[1] for x in e[2]], i
+            assert [bytes(x["comp"]) for x in got] == [x[6] for x in e[2]], i

@@ -2,7 +2,8 @@
 from oracle/_ref, never the product library).
 
 Times the reference GMAP 2024-02-22 path -- Stage2_compute (stage2.c:6325: seeding and chaining, as
-gmap.c:1208 calls it) and Dynprog_single_gap / _end5_gap / _end3_gap / _genome_gap -- on the
+gmap.c:1208 calls it) and Dynprog_single_gap / _end5_gap / _end3_gap / _genome_gap /
+_microexon_int (with the reference's own MaxEnt) -- on the
 host cores, one process per core, each on a bounded sample of the configs[2] per-read call stream
 (gmapdp.workload, same generators and per-read mix as the GPU bench).  The reference's harness takes
 an int genome length, so the CPU sample is cut from a chr22-length (50.8 Mnt) i.i.d. genome; the DP and
@@ -51,6 +52,12 @@ def worker(args):
         f = getattr(lib, name)
         f.restype = C.c_long
         f.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_char_p]
+    fm = lib.refh_microexon_int
+    fm.restype = C.c_int
+    fm.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint, C.c_uint, C.c_int,
+                   C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    msc = np.zeros(2, dtype=np.int32)
+    mds = np.zeros(2, dtype=np.float64)
     fo = lib.refh_stage2_compute
     fo.restype = C.c_int
     fo.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_uint, C.c_uint, C.c_uint, C.c_uint, C.c_int, C.c_int, C.c_int,
@@ -64,7 +71,7 @@ def worker(args):
     fams = [("single", lib.refh_single_gap_batch, d["single"], W.SINGLE_PER_READ),
             ("end", lib.refh_end_gap_batch, d["end"], W.END5_PER_READ + W.END3_PER_READ),
             ("genome", lib.refh_genome_gap_batch, d["genome"], W.GENOME_PER_READ)]
-    t = {k: 0.0 for k in ("single", "end", "genome", "oligo")}
+    t = {k: 0.0 for k in ("single", "end", "genome", "oligo", "microexon")}
     n = {k: 0 for k in t}
     t_start = time.perf_counter()
     # one read's worth of calls per round, so every family is sampled in proportion
@@ -85,9 +92,19 @@ def worker(args):
            pairs.ctypes.data, cap)
         t["oligo"] += time.perf_counter() - t0
         n["oligo"] += 1
+        for _ in range(int(round(W.MICROEXON_PER_READ))):
+            m = d["microexon"][n["microexon"] % len(d["microexon"])]
+            mo, ml = int(m["qoff"]), int(m["rlength"])
+            t0 = time.perf_counter()
+            fm(qb[mo:mo + ml], qb[mo:mo + ml], ml, int(m["roffset"]), int(m["goffsetL"]), int(m["rev_goffsetR"]),
+               int(m["cdna_direction"]), int(m["chroffset"]), int(m["chrhigh"]), int(m["watsonp"]),
+               int(m["genestrand"]), int(m["dynprogindex"]), msc.ctypes.data, mds.ctypes.data, pairs.ctypes.data, cap)
+            t["microexon"] += time.perf_counter() - t0
+            n["microexon"] += 1
     per_call = {k: t[k] / max(n[k], 1) for k in t}
     sec_per_read = (W.SINGLE_PER_READ * per_call["single"] + (W.END5_PER_READ + W.END3_PER_READ) * per_call["end"]
-                    + W.GENOME_PER_READ * per_call["genome"] + W.STAGE2_PER_READ * per_call["oligo"])
+                    + W.GENOME_PER_READ * per_call["genome"] + W.STAGE2_PER_READ * per_call["oligo"]
+                    + W.MICROEXON_PER_READ * per_call["microexon"])
     return {"reads_per_s": 1.0 / sec_per_read, "calls": n, "seconds": t, "per_call_us":
             {k: v * 1e6 for k, v in per_call.items()}}
 
@@ -114,9 +131,10 @@ def main():
         "build": "gmap.%s objects (oracle/_ref/librefdp_%s.so)" % (a.build, a.build),
         "cpu_model": cpu_model(), "per_core_reads_per_s": total / cores, "per_call_us": per_call,
         "sample": "%d worker processes x %.0f s of timed reference calls (%s) on the configs[2] per-read mix "
-                  "(1 Stage2_compute call + %.1f single + %.1f end + %.1f genome-gap calls per read) cut from a chr22-length "
-                  "i.i.d. genome; per-read time composed from per-call averages"
-                  % (cores, a.budget, ", ".join("%d %s" % (v, k) for k, v in calls.items()), 43.7, 13.6, 49.4)}))
+                  "(1 Stage2_compute call + %.1f single + %.1f end + %.1f genome-gap + %.1f microexon calls per read) "
+                  "cut from a chr22-length i.i.d. genome; per-read time composed from per-call averages"
+                  % (cores, a.budget, ", ".join("%d %s" % (v, k) for k, v in calls.items()), 43.7, 13.6, 49.4,
+                     25.6)}))
 
 
 if __name__ == "__main__":
