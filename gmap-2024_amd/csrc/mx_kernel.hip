@@ -8,8 +8,10 @@
 //     order; for each, the cR in [mincR, maxcR] with its 3' dinucleotide (:1063-1085);
 //   - the exact search of the middle piece in the intron text (BoyerMoore_nt, boyer-moore.c:356:
 //     every occurrence j in [0, textlen - querylen]; none when the piece holds anything but A/C/G/T):
-//     64 offsets per step, the text staged in LDS, lane l tests j = top - l so that the ballot order is
-//     the reference's hit order (Intlist_push: descending j);
+//     64 offsets per step, lane l tests j = top - l so that the ballot order is the reference's hit
+//     order (Intlist_push: descending j), each offset one compare of the piece's 2-bit codes (its
+//     reverse complement on the minus strand) with the packed genome words, N flags and the
+//     segment's chromosome bound included;
 //   - the flank test (:1109-1116) and the candidate's two splice sites (:1120-1144).
 //   Candidates collect in LDS and leave with one atomic per call; a call with more than kMxCap of
 //   them reports its exact count and the host reruns it writing straight to its own region.
@@ -24,6 +26,28 @@ constexpr int kMxMin = 3;       // MIN_MICROEXON_LENGTH (dynprog_single.c:83)
 constexpr int kMxMax = 12;      // MAX_MICROEXON_LENGTH (:87, GMAP)
 constexpr int kMxIntron = 9;    // MICROINTRON_LENGTH (:89)
 constexpr int kMxCap = 256;     // candidates per call held in LDS
+
+// 2-bit codes (A0 C1 G2 T3, first position in bits 1:0) of genome positions [lo, lo + ml), ml <= 12, straight
+// from the packed .genomecomp words; false when one of them is an N (flags) or past the allocation
+// (decode_nt reads those as N, which no A/C/G/T piece matches)
+__device__ __forceinline__ bool mx_window(const uint32_t* __restrict__ blocks, uint64_t nwords, uint32_t lo, int ml,
+                                          uint32_t& codes) {
+  const uint32_t hi = lo + (uint32_t)ml - 1u;
+  const uint64_t b0 = lo >> 5, b1 = hi >> 5;
+  if (3 * b1 + 2 >= nwords) return false;
+  uint64_t f = blocks[3 * b0 + 2];
+  if (b1 != b0) f |= (uint64_t)blocks[3 * b1 + 2] << 32;
+  if ((f >> (lo & 31u)) & ((1ull << ml) - 1ull)) return false;
+  const uint32_t h = lo >> 4;  // half-words: even = low word (nt 0-15 of the block), odd = high word
+  const uint32_t w0 = blocks[3 * (size_t)(h >> 1) + ((h & 1u) ? 0 : 1)];
+  uint64_t x = w0;
+  if ((lo & 15u) + (uint32_t)ml > 16u) {
+    const uint32_t h1 = h + 1u;
+    x |= (uint64_t)blocks[3 * (size_t)(h1 >> 1) + ((h1 & 1u) ? 0 : 1)] << 32;
+  }
+  codes = (uint32_t)(x >> (2u * (lo & 15u))) & ((1u << (2 * ml)) - 1u);
+  return true;
+}
 
 // the second mismatch among n flags produced 64 at a time by `flag(i)`; n - 1 when there is none
 template <class F>
@@ -53,8 +77,6 @@ __global__ __launch_bounds__(64) void mx_search_kernel(const gmapdp_microexon_pr
                                                        unsigned long long* __restrict__ counter,
                                                        const int64_t* __restrict__ direct) {
   __shared__ gmapdp_microexon_candidate lc[kMxCap];
-  __shared__ char text[64 + kMxMax + 4];
-  __shared__ char piece[kMxMax + 4];
   const int pi = blockIdx.x;
   if (pi >= n) return;
   const int lane = threadIdx.x;
@@ -98,23 +120,28 @@ __global__ __launch_bounds__(64) void mx_search_kernel(const gmapdp_microexon_pr
           // query_okay (boyer-moore.c:263) on the mixed-case piece
           const char qc = lane < ml ? rs[cL + lane] : 'A';
           if (ballot(qc != 'A' && qc != 'C' && qc != 'G' && qc != 'T')) continue;
-          if (lane < ml) piece[lane] = qc;
+          // the piece as 2-bit codes, and as the genome shows it on the minus strand (reverse complement)
+          const uint32_t qcode = qc == 'A' ? 0u : qc == 'C' ? 1u : qc == 'G' ? 2u : 3u;
+          uint32_t pat = 0, rcpat = 0;
+          for (int k = 0; k < ml; k++) {
+            const uint32_t ck = (uint32_t)__builtin_amdgcn_readlane((int)qcode, k);
+            pat |= ck << (2 * k);
+            rcpat |= (3u - ck) << (2 * (ml - 1 - k));
+          }
           const int textlen = textright - textleft;
-          const uint32_t L = (uint32_t)(textlen + ml);
-          // Genome_get_segment_right / _left as BoyerMoore_nt calls them (boyer-moore.c:372-378)
-          const uint32_t spos = watson ? P.chroffset + (uint32_t)textleft : P.chrhigh - (uint32_t)textleft + 1u;
-          const uint32_t sbound = watson ? P.chrhigh : P.chroffset;
+          // BoyerMoore_nt's text (Genome_get_segment_right / _left, boyer-moore.c:372-378): text[i] is
+          // genome[chroffset + textleft + i] (plus; '*' from chrhigh on) or the complement of
+          // genome[chrhigh - textleft - i] (minus; '*' below chroffset)
+          const int64_t base = watson ? (int64_t)P.chroffset + textleft : (int64_t)P.chrhigh - textleft;
           for (int top = textlen - ml; top >= 0; top -= 64) {
-            const int lo = top - 63;  // text[lo .. top + ml) staged at text[0 ..)
-            for (int t = lane; t < 64 + ml; t += 64) {
-              const int ti = lo + t;
-              text[t] = ti >= 0 ? segment_nt(blocks, nwords, (uint32_t)ti, L, spos, sbound, !watson, !watson) : 0;
-            }
-            __builtin_amdgcn_wave_barrier();
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
             const int j = top - lane;
-            bool hit = j >= 0;
-            for (int k = 0; k < ml && hit; k++) hit = text[63 - lane + k] == piece[k];
+            bool hit = false;
+            if (j >= 0) {
+              const int64_t lo = watson ? base + j : base - j - (ml - 1);  // the window, ascending
+              const bool inb = watson ? lo + ml <= (int64_t)P.chrhigh : lo >= (int64_t)P.chroffset;
+              uint32_t codes;
+              hit = inb && mx_window(blocks, nwords, (uint32_t)lo, ml, codes) && codes == (watson ? pat : rcpat);
+            }
             const int cand = textleft + j;
             hit = hit && gnt(cand - 2) == i3 && gnt(cand - 1) == i4 && gnt(cand + ml) == i1 && gnt(cand + ml + 1) == i2;
             const uint64_t mh = ballot(hit);
@@ -140,8 +167,6 @@ __global__ __launch_bounds__(64) void mx_search_kernel(const gmapdp_microexon_pr
               else if (idx < kMxCap) lc[idx] = c;
             }
             ncand += __popcll(mh);
-            __builtin_amdgcn_wave_barrier();
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
           }
         }
       }
