@@ -1511,7 +1511,7 @@ __global__ __launch_bounds__(64) void s2b_kernel(
 
 // traceback_one over the LDS link table: link[i] = predecessor hit index (0x7fffffff: none) with bit 31
 // set when the hit has fewer than MIN_TERMINAL_NCONSECUTIVE consecutive matches; map[i] its chrpos
-constexpr int kS2cCap = 4096;  // hits whose links fit the s2c kernel's LDS (12 B each)
+constexpr int kS2cCap = 3072;  // hits whose links fit the s2c kernel's LDS (12 B each; 36 KB: 4 waves per CU)
 constexpr uint32_t kS2NoPred = 0x7fffffffu;
 template <class F>
 __device__ void s2_walk_lds(const uint32_t* link, const uint32_t* map, int gi, F visit) {
@@ -1654,12 +1654,19 @@ __global__ __launch_bounds__(64) void s2c_kernel(
     }
   }
   wave_sync();
+  // a single selected cell is the single result (Stage2_filter_unique keeps it): its walk records the
+  // entries convert_to_nucleotides needs, and the second walk below is skipped
+  const bool single = npaths == 1;
   if (lane == 0) {
     for (int p = 0; p < npaths; p++) {
       int n = 0, top = -1, bottom = -1;
       auto vis = [&](int gi) {
         if (n == 0) top = gi;
         bottom = gi;
+        if (single) {
+          pathq[n] = lds_walk ? (int)lq[gi] : hits[gi].q;
+          pathh[n] = lds_walk ? (int)lmap[gi] : (int)hits[gi].map;
+        }
         n++;
       };
       if (lds_walk) s2_walk_lds(llink, lmap, cand[p], vis);
@@ -1728,7 +1735,7 @@ __global__ __launch_bounds__(64) void s2c_kernel(
     if (keep[i]) continue;
     const S2Path x = pth[pord[i]];
     const int n = x.n;
-    if (lane == 0) {  // entries, 3' end first
+    if (lane == 0 && !single) {  // entries, 3' end first
       int e = 0;
       if (lds_walk) {
         s2_walk_lds(llink, lmap, x.cell, [&](int gi) {
