@@ -1645,12 +1645,36 @@ __global__ __launch_bounds__(64) void s2c_kernel(
   uint32_t* lq = s2c_lds + 2 * kS2cCap;
   const bool lds_walk = T <= kS2cCap;
   if (lds_walk && npaths > 0) {
-    for (int i = lane; i < T; i += 64) {
-      const S2Hit& x = hits[i];
-      const uint32_t pr = x.fpos >= 0 ? (uint32_t)(off[x.fpos] + x.fhit) : kS2NoPred;
-      llink[i] = pr | (x.consec < kS2MinTerminal ? 0x80000000u : 0u);
-      lmap[i] = x.map;
-      lq[i] = (uint32_t)x.q;
+    // four hits per lane per step: their loads, then their off[] gathers, overlap
+    for (int b0 = lane; b0 < T; b0 += 256) {
+      int fp[4], fh[4], cs[4], qq[4];
+      uint32_t mp[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int i = b0 + 64 * k;
+        fp[k] = -1;
+        if (i < T) {
+          const S2Hit& x = hits[i];
+          fp[k] = x.fpos;
+          fh[k] = x.fhit;
+          cs[k] = x.consec;
+          mp[k] = x.map;
+          qq[k] = x.q;
+        }
+      }
+      int ob[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) ob[k] = fp[k] >= 0 ? off[fp[k]] : 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int i = b0 + 64 * k;
+        if (i < T) {
+          const uint32_t pr = fp[k] >= 0 ? (uint32_t)(ob[k] + fh[k]) : kS2NoPred;
+          llink[i] = pr | (cs[k] < kS2MinTerminal ? 0x80000000u : 0u);
+          lmap[i] = mp[k];
+          lq[i] = (uint32_t)qq[k];
+        }
+      }
     }
   }
   wave_sync();
