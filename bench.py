@@ -50,35 +50,35 @@ def algorithmic_bytes(rlength, glength, npairs, desc_bytes):
 
 
 def genome_algorithmic_bytes(gp, npairs):
-    """Dynprog_genome_gap: descriptor (80 B) + query and upper-cased query (2 x rlength) + the packed
+    """Dynprog_genome_gap: descriptor (96 B) + query and upper-cased query (2 x rlength) + the packed
     genome blocks of both segments + 8-B splice probability per column of both segments + result
     (72 B) + one 16-B record per emitted pair."""
     r = gp["rlength"].astype(np.int64)
     gL = gp["glengthL"].astype(np.int64)
     gR = gp["glengthR"].astype(np.int64)
-    return int((80 + 2 * r + 12 * ((gL + 62) // 32) + 12 * ((gR + 62) // 32) + 8 * (gL + gR) + 72).sum()
+    return int((96 + 2 * r + 12 * ((gL + 62) // 32) + 12 * ((gR + 62) // 32) + 8 * (gL + gR) + 72).sum()
                + 16 * int(np.asarray(npairs).sum()))
 
 
 def stage2_algorithmic_bytes(op, res):
-    """Stage-2 seeding per call: descriptor (32 B) + the query (1 B/nt) + the window's packed genome
+    """Stage-2 seeding per call: descriptor (40 B) + the query (1 B/nt) + the window's packed genome
     (12 B per 32 nt) + npositions and mappings (8 B per query position) + the table (4 B per stored
     position) + the result (32 B) + the diagonal records (16 B each)."""
     w = (op["chrend"].astype(np.int64) - op["chrstart"].astype(np.int64))
     ql = op["querylength"].astype(np.int64)
-    return int((32 + ql + 12 * ((w + 31) // 32) + 8 * ql + 32).sum()
+    return int((40 + ql + 12 * ((w + 31) // 32) + 8 * ql + 32).sum()
                + 4 * int(res["totalpositions"].astype(np.int64).sum())
                + 16 * int(res["ndiagonals"].astype(np.int64).sum()))
 
 
 def chain_algorithmic_bytes(op, s2res):
-    """Stage-2 chaining per call (s2c_kernel): descriptor (40 B) + seeding result (32 B) + npositions
+    """Stage-2 chaining per call (s2c_kernel): descriptor (48 B) + seeding result (32 B) + npositions
     and mappings (8 B per query position) + the query twice (cdna and upper case, 2 B per query
     position) + the result (32 B) + 16-B path records + 20-B pair records of the kept paths.  The
     mapping positions (4 B each) are read once; totalpositions is not in the stage-2 result, so
     they are estimated as one per query position."""
     ql = op["querylength"].astype(np.int64)
-    return int((40 + 32 + 8 * ql + 2 * ql + 4 * ql + 32).sum() + 16 * int(s2res["nresults"].sum())
+    return int((48 + 32 + 8 * ql + 2 * ql + 4 * ql + 32).sum() + 16 * int(s2res["nresults"].sum())
                + 20 * int(s2res["npairs"].sum()))
 
 
@@ -348,7 +348,7 @@ def main():
     gnp[gdev_index >= 0] = gres["npairs"][gdev_index[gdev_index >= 0]]
     rl = np.concatenate([sp["rlength"], np.minimum(ep["rlength"], 660)]).astype(np.int64)
     gl = np.concatenate([sp["glength"], np.minimum(ep["glength"], 2000)]).astype(np.int64)
-    desc = np.concatenate([np.full(ns, 56), np.full(ne, 64)])
+    desc = np.concatenate([np.full(ns, gmapdp.PROBLEM_DTYPE.itemsize), np.full(ne, gmapdp.END_PROBLEM_DTYPE.itemsize)])
     disp = []   # (rocprof name, algorithmic bytes, ms per launch, problems)
     for li in range(nl):
         m = np.zeros(info[li][2], dtype=np.int32)

@@ -80,8 +80,8 @@ __device__ __forceinline__ int lanes_below(uint64_t m, int lane) {
 }
 
 // ---- genome access (.genomecomp: {high nt16-31, low nt0-15, flags} per 32 nt) ----
-__device__ __forceinline__ char decode_nt(const uint32_t* __restrict__ blocks, uint64_t nwords, uint32_t pos) {
-  const uint64_t ptr = (uint64_t)(pos >> 5) * 3u;
+__device__ __forceinline__ char decode_nt(const uint32_t* __restrict__ blocks, uint64_t nwords, uint64_t pos) {
+  const uint64_t ptr = (pos >> 5) * 3u;
   if (ptr + 2 >= nwords) return 'N';  // beyond the allocation (reference: undefined)
   const uint32_t bit = pos & 31u;
   if ((blocks[ptr + 2] >> bit) & 1u) return 'N';
@@ -96,10 +96,11 @@ __device__ __forceinline__ char compl_nt(char c) {
 __device__ __forceinline__ uint8_t gclass(char c) {
   return (c == 'A') ? kA : (c == 'C') ? kC : (c == 'G') ? kG : (c == 'T') ? kT : (c == '*') ? kStar : kN;
 }
-// get_genomic_nt (dynprog_single.c:116; Univcoord_T is 32-bit)
+// get_genomic_nt (dynprog_single.c:116): Univcoord_T arithmetic, the int position sign-extended
 __device__ __forceinline__ char genomic_nt(const uint32_t* __restrict__ blocks, uint64_t nwords, int genomicpos,
-                                           uint32_t chroffset, uint32_t chrhigh, bool watson) {
-  const uint32_t pos = watson ? chroffset + (uint32_t)genomicpos : chrhigh - (uint32_t)genomicpos;
+                                           uint64_t chroffset, uint64_t chrhigh, bool watson) {
+  const uint64_t g = (uint64_t)(int64_t)genomicpos;
+  const uint64_t pos = watson ? chroffset + g : chrhigh - g;
   if (pos < chroffset || pos >= chrhigh) return '*';
   const char c = decode_nt(blocks, nwords, pos);
   return watson ? c : compl_nt(c);
@@ -108,17 +109,17 @@ __device__ __forceinline__ char genomic_nt(const uint32_t* __restrict__ blocks, 
 // Genome_get_segment_left(right=pos, L, chroffset=bound), optionally
 // reverse-complemented (genome.c:11023-11135).
 __device__ __forceinline__ char segment_nt(const uint32_t* __restrict__ blocks, uint64_t nwords, uint32_t i,
-                                           uint32_t L, uint32_t pos, uint32_t bound, bool leftvariant,
+                                           uint32_t L, uint64_t pos, uint64_t bound, bool leftvariant,
                                            bool revcomp) {
-  const uint32_t j = revcomp ? L - 1u - i : i;  // index into the forward segment
+  const uint64_t j = revcomp ? L - 1u - i : i;  // index into the forward segment
   char c;
   if (!leftvariant) {
-    const uint32_t left = pos, chrhigh = bound;
+    const uint64_t left = pos, chrhigh = bound;
     if (left >= chrhigh) return '*';
     if (left + L >= chrhigh && j + (left + L - chrhigh) >= L) return '*';
     c = decode_nt(blocks, nwords, left + j);
   } else {
-    const uint32_t right = pos, chroffset = bound;
+    const uint64_t right = pos, chroffset = bound;
     if (right < chroffset) return '*';
     if (right < chroffset + L && j < chroffset + L - right) return '*';
     c = decode_nt(blocks, nwords, right - L + j);
@@ -255,7 +256,7 @@ __device__ __forceinline__ void emit_queryskip(int lane, int rs, int c, int dist
 // Genome skip: Pairpool_add_genomeskip(&add_dashes_p, pairs, r, cs, dist, NULL, ...) (pairpool.c:1068):
 // columns cs, cs-1, ...; dist >= 9 gives one gap holder
 __device__ __forceinline__ void emit_genomeskip(int lane, int r, int cs, int dist, const Geo& G, bool watson,
-                                                uint32_t chroffset, uint32_t chrhigh, const uint32_t* blocks,
+                                                uint64_t chroffset, uint64_t chrhigh, const uint32_t* blocks,
                                                 uint64_t nwords, gmapdp_pair* out, Tally& t) {
   if (dist >= kMicrointronLength) {
     if (lane == 0) put_pair(out, t.count, -1, -1, dist, ' ', ' ', ' ', ' ');
@@ -576,7 +577,7 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
 template <typename DA, typename QV, typename GV>
 __device__ __forceinline__ void traceback_walk(int lane, const DA& dir, int r, int c, const Geo& G, const QV& q,
                                                const QV& quc, const GV& gch, const uint8_t* __restrict__ cons,
-                                               bool watson, uint32_t chroffset, uint32_t chrhigh,
+                                               bool watson, uint64_t chroffset, uint64_t chrhigh,
                                                const uint32_t* __restrict__ blocks, uint64_t nwords,
                                                gmapdp_pair* out, Tally& t, int mode = 0) {
   while (r > 0 && c > 0) {
@@ -646,8 +647,8 @@ struct BandDirs {
 template <int R, typename WORD = uint64_t, typename QV = const char*, typename GV = const char*>
 __device__ __forceinline__ void traceback_band(int lane, const WORD* dirs, int W, int uband, int r, int c,
                                                const Geo& G, const QV& q, const QV& quc, const GV& gch,
-                                               const uint8_t* __restrict__ cons, bool watson, uint32_t chroffset,
-                                               uint32_t chrhigh, const uint32_t* __restrict__ blocks,
+                                               const uint8_t* __restrict__ cons, bool watson, uint64_t chroffset,
+                                               uint64_t chrhigh, const uint32_t* __restrict__ blocks,
                                                uint64_t nwords, gmapdp_pair* out, Tally& t, int bitoff = 0) {
   const BandDirs<R, WORD> d{dirs, W, uband, bitoff};
   traceback_walk(lane, d, r, c, G, q, quc, gch, cons, watson, chroffset, chrhigh, blocks, nwords, out, t);

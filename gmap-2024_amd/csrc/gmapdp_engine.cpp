@@ -429,8 +429,7 @@ int gmapdp_pack_genome(const char* seq, uint64_t length, uint32_t* blocks) {
 
 int gmapdp_set_genome(gmapdp_ctx* ctx, const uint32_t* blocks, size_t nwords, uint64_t length) {
   if (!ctx || !blocks || nwords < (size_t)((length + 31) / 32) * 3) return GMAPDP_EINVAL;
-  // descriptors carry 32-bit coordinates (gmap's Univcoord_T); a gmapl-sized genome is refused
-  if (length > 0xFFFFFFFFull) return bad(ctx, "genome length >= 2^32 (gmapl genomes) is not supported");
+  // coordinates are 64-bit (gmapdp_coord_t): gmapl genomes past 2^32 nt are supported
   (void)hipSetDevice(ctx->device);
   if (ctx->d_genome) (void)hipFree(ctx->d_genome);
   ctx->d_genome = nullptr;
@@ -553,10 +552,10 @@ static int convert_single(const gmapdp_ctx* ctx, const gmapdp_single_problem& p,
   d.flags = (watson ? kFWatson : 0) | ((p.flags & GMAPDP_JUMP_LATE) ? kFLate : 0) |
             ((p.flags & GMAPDP_SIMD) ? kFSimd : 0);
   if (watson) {
-    d.segpos = p.chroffset + (uint32_t)p.goffset;  // Genome_get_segment_right(left, chrhigh)
+    d.segpos = p.chroffset + (uint64_t)(int64_t)p.goffset;  // Genome_get_segment_right(left, chrhigh)
     d.segbound = p.chrhigh;
   } else {
-    d.segpos = p.chrhigh - (uint32_t)p.goffset + 1u;  // Genome_get_segment_left(right, chroffset), revcomp
+    d.segpos = p.chrhigh - (uint64_t)(int64_t)p.goffset + 1u;  // Genome_get_segment_left(right, chroffset), revcomp
     d.segbound = p.chroffset;
     d.flags |= kFSegLeft | kFSegRevcomp;
   }
@@ -620,10 +619,10 @@ static int convert_end(gmapdp_ctx* ctx, const gmapdp_end_problem& p, gmapdp_resu
     d.qbase = p.qoff;
     d.flags |= (jl ? kFLate : 0) | kFScoreUC;  // end3 fills on rsequenceuc (dynprog_end.c:2061)
     if (watson) {
-      d.segpos = p.chroffset + (uint32_t)p.goffset;
+      d.segpos = p.chroffset + (uint64_t)(int64_t)p.goffset;
       d.segbound = p.chrhigh;
     } else {
-      d.segpos = p.chrhigh - (uint32_t)p.goffset + 1u;
+      d.segpos = p.chrhigh - (uint64_t)(int64_t)p.goffset + 1u;
       d.segbound = p.chroffset;
       d.flags |= kFSegLeft | kFSegRevcomp;
     }
@@ -631,11 +630,11 @@ static int convert_end(gmapdp_ctx* ctx, const gmapdp_end_problem& p, gmapdp_resu
     d.qbase = p.qoff + p.rlength - 1;          // rev_rsequence: the slice's last character
     d.flags |= (jl ? 0 : kFLate) | kFRev;      // fills with !jump_late_p, revp
     if (watson) {
-      d.segpos = p.chroffset + (uint32_t)p.goffset + 1u;  // Genome_get_segment_left(right, chroffset)
+      d.segpos = p.chroffset + (uint64_t)(int64_t)p.goffset + 1u;  // Genome_get_segment_left(right, chroffset)
       d.segbound = p.chroffset;
       d.flags |= kFSegLeft;
     } else {
-      d.segpos = p.chrhigh - (uint32_t)p.goffset;  // Genome_get_segment_right(left, chrhigh), revcomp
+      d.segpos = p.chrhigh - (uint64_t)(int64_t)p.goffset;  // Genome_get_segment_right(left, chrhigh), revcomp
       d.segbound = p.chrhigh;
       d.flags |= kFSegRevcomp;
     }
@@ -723,15 +722,15 @@ static int convert_genome(gmapdp_ctx* ctx, const gmapdp_genome_problem& p, gmapd
   if (!(p.flags & GMAPDP_FINALP) && dr < 0.014) d.flags |= kGSimple;  // :3479
   if (p.flags & GMAPDP_SIMD) d.flags |= kGSimd;
   if (watson) {
-    d.segposL = p.chroffset + (uint32_t)p.goffsetL;  // Genome_get_segment_right(left, chrhigh)
+    d.segposL = p.chroffset + (uint64_t)(int64_t)p.goffsetL;  // Genome_get_segment_right(left, chrhigh)
     d.segboundL = p.chrhigh;
-    d.segposR = p.chroffset + (uint32_t)p.rev_goffsetR + 1u;  // Genome_get_segment_left(right, chroffset)
+    d.segposR = p.chroffset + (uint64_t)(int64_t)p.rev_goffsetR + 1u;  // Genome_get_segment_left(right, chroffset)
     d.segboundR = p.chroffset;
     d.flags |= kGSegRLeft;
   } else {
-    d.segposL = p.chrhigh - (uint32_t)p.goffsetL + 1u;  // _left(right, chroffset), revcomp
+    d.segposL = p.chrhigh - (uint64_t)(int64_t)p.goffsetL + 1u;  // _left(right, chroffset), revcomp
     d.segboundL = p.chroffset;
-    d.segposR = p.chrhigh - (uint32_t)p.rev_goffsetR;   // _right(left, chrhigh), revcomp
+    d.segposR = p.chrhigh - (uint64_t)(int64_t)p.rev_goffsetR;   // _right(left, chrhigh), revcomp
     d.segboundR = p.chrhigh;
     d.flags |= kGSegLLeft | kGSegLRc | kGSegRRc;
   }
@@ -1226,7 +1225,7 @@ size_t gmapdp_genome_prob_entries(const gmapdp_genome_problem* problems, int n) 
 
 // The Maxent_hr_*_prob call of each probability entry (bridge_intron_gap_site_level,
 // dynprog_genome.c:2573-2660; get_splicesite_probs :332-401).  Univcoord_T is 32-bit.
-int gmapdp_genome_splice_sites(const gmapdp_genome_problem* problems, int n, uint32_t* positions, uint8_t* models,
+int gmapdp_genome_splice_sites(const gmapdp_genome_problem* problems, int n, gmapdp_coord_t* positions, uint8_t* models,
                                size_t nentries) {
   if (n < 0 || (n && (!problems || !positions || !models))) return GMAPDP_EINVAL;
   if (gmapdp_genome_prob_entries(problems, n) > nentries) return GMAPDP_EINVAL;
@@ -1235,15 +1234,15 @@ int gmapdp_genome_splice_sites(const gmapdp_genome_problem* problems, int n, uin
     if (p.prob_offset < 0 || p.glengthL < 0 || p.glengthR < 0) return GMAPDP_EINVAL;
     const bool watson = p.flags & GMAPDP_WATSON;
     const bool sense = p.cdna_direction > 0;
-    const uint32_t lo = (uint32_t)p.goffsetL, ro = (uint32_t)p.rev_goffsetR;
-    uint32_t* pos = positions + p.prob_offset;
+    const uint64_t lo = (uint64_t)(int64_t)p.goffsetL, ro = (uint64_t)(int64_t)p.rev_goffsetR;
+    gmapdp_coord_t* pos = positions + p.prob_offset;
     uint8_t* mod = models + p.prob_offset;
     for (int c = 0; c < p.glengthL; c++) {
       if (watson) {
-        pos[c] = p.chroffset + lo + (uint32_t)c;
+        pos[c] = p.chroffset + lo + (uint64_t)c;
         mod[c] = sense ? GMAPDP_MAXENT_DONOR : GMAPDP_MAXENT_ANTIACCEPTOR;
       } else {
-        pos[c] = p.chrhigh - lo - (uint32_t)c + 1u;
+        pos[c] = p.chrhigh - lo - (uint64_t)c + 1u;
         mod[c] = sense ? GMAPDP_MAXENT_ANTIDONOR : GMAPDP_MAXENT_ACCEPTOR;
       }
     }
@@ -1251,10 +1250,10 @@ int gmapdp_genome_splice_sites(const gmapdp_genome_problem* problems, int n, uin
     mod += p.glengthL;
     for (int c = 0; c < p.glengthR; c++) {
       if (watson) {
-        pos[c] = p.chroffset + ro - (uint32_t)c + 1u;
+        pos[c] = p.chroffset + ro - (uint64_t)c + 1u;
         mod[c] = sense ? GMAPDP_MAXENT_ACCEPTOR : GMAPDP_MAXENT_ANTIDONOR;
       } else {
-        pos[c] = p.chrhigh - ro + (uint32_t)c;
+        pos[c] = p.chrhigh - ro + (uint64_t)c;
         mod[c] = sense ? GMAPDP_MAXENT_ANTIACCEPTOR : GMAPDP_MAXENT_DONOR;
       }
     }
@@ -1360,7 +1359,7 @@ static int convert_cdna(gmapdp_ctx* ctx, const gmapdp_cdna_problem& p, size_t qb
   d.flags = (watson ? kFWatson : 0) | ((p.flags & GMAPDP_JUMP_LATE) ? kFLate : 0) |
             ((p.flags & GMAPDP_SIMD) ? kCSimd : 0);
   if (watson) {  // :922-926
-    d.segpos = p.chroffset + (uint32_t)p.goffset;  // Genome_get_segment_right(left, chrhigh)
+    d.segpos = p.chroffset + (uint64_t)(int64_t)p.goffset;  // Genome_get_segment_right(left, chrhigh)
     d.segbound = p.chrhigh;
     d.rsegpos = p.chroffset + rev_goffset + 1u;    // Genome_get_segment_left(right, chroffset)
     d.rsegbound = p.chroffset;
@@ -1368,7 +1367,7 @@ static int convert_cdna(gmapdp_ctx* ctx, const gmapdp_cdna_problem& p, size_t qb
   } else {       // :928-931
     d.rsegpos = p.chrhigh - rev_goffset;           // _right(left, chrhigh), revcomp
     d.rsegbound = p.chrhigh;
-    d.segpos = p.chrhigh - (uint32_t)p.goffset + 1u;  // _left(right, chroffset), revcomp
+    d.segpos = p.chrhigh - (uint64_t)(int64_t)p.goffset + 1u;  // _left(right, chroffset), revcomp
     d.segbound = p.chroffset;
     d.flags |= kCSegLeft | kCSegRc | kCRSegRc;
   }

@@ -38,10 +38,10 @@ struct DevProblem {
   int32_t glength;        // DP columns
   int32_t roffset;        // querypos of row r = roffset + sgn*(r-1)
   int32_t goffset;        // genomepos of column c = goffset + sgn*(c-1)
-  uint32_t chroffset;
-  uint32_t chrhigh;
-  uint32_t segpos;        // left (right variant) or right (left variant) coordinate of the segment
-  uint32_t segbound;      // chrhigh (right variant) or chroffset (left variant)
+  uint64_t chroffset;
+  uint64_t chrhigh;
+  uint64_t segpos;        // left (right variant) or right (left variant) coordinate of the segment
+  uint64_t segbound;      // chrhigh (right variant) or chroffset (left variant)
   int32_t lband;
   int32_t uband;
   int32_t open;
@@ -77,10 +77,10 @@ struct DevGenomeProblem {
   int32_t roffset;
   int32_t goffsetL;
   int32_t rev_goffsetR;
-  uint32_t chroffset;
-  uint32_t chrhigh;
-  uint32_t segposL, segboundL;  // gsequenceL segment (see DevProblem.segpos)
-  uint32_t segposR, segboundR;  // rev_gsequenceR segment
+  uint64_t chroffset;
+  uint64_t chrhigh;
+  uint64_t segposL, segboundL;  // gsequenceL segment (see DevProblem.segpos)
+  uint64_t segposR, segboundR;  // rev_gsequenceR segment
   int32_t lbandL;         // both fills (the R fill is called with lbandL, dynprog_genome.c:3813)
   int32_t ubandL;
   int32_t ubandR;
@@ -122,10 +122,10 @@ struct DevCdnaProblem {
   int32_t goffset;
   int32_t lband;
   int32_t uband;
-  uint32_t chroffset;
-  uint32_t chrhigh;
-  uint32_t segpos, segbound;    // gsequence segment (see DevProblem.segpos)
-  uint32_t rsegpos, rsegbound;  // rev_gsequence segment
+  uint64_t chroffset;
+  uint64_t chrhigh;
+  uint64_t segpos, segbound;    // gsequence segment (see DevProblem.segpos)
+  uint64_t rsegpos, rsegbound;  // rev_gsequence segment
   int32_t open;
   int32_t extend;
   int32_t mismatchtype;
@@ -140,7 +140,8 @@ struct DevCdnaProblem {
 struct DevOligoProblem {
   int32_t qoff;           // arena index of queryuc_ptr[0]
   int32_t querylength;
-  uint32_t chrstart, chrend, chroffset, chrhigh;
+  uint32_t chrstart, chrend;
+  uint64_t chroffset, chrhigh;
   int32_t plusp;
   int32_t minor;          // oligoindices_minor (diag_lookback 60, suffnconsecutive 10), else major (120, 20)
   int32_t umax;           // LDS slots for the query's distinct 8-mers (>= their number)
@@ -155,7 +156,8 @@ struct DevOligoProblem {
 struct DevStage2Problem {
   int32_t qoff;           // arena index of queryseq_ptr[0] / queryuc_ptr[0]
   int32_t querylength;
-  uint32_t chrstart, chrend, chroffset, chrhigh;
+  uint32_t chrstart, chrend;
+  uint64_t chroffset, chrhigh;
   int32_t plusp;
   int32_t splicingp;
   uint32_t maxintronlen;

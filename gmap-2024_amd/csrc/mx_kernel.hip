@@ -30,19 +30,19 @@ constexpr int kMxCap = 256;     // candidates per call held in LDS
 // 2-bit codes (A0 C1 G2 T3, first position in bits 1:0) of genome positions [lo, lo + ml), ml <= 12, straight
 // from the packed .genomecomp words; false when one of them is an N (flags) or past the allocation
 // (decode_nt reads those as N, which no A/C/G/T piece matches)
-__device__ __forceinline__ bool mx_window(const uint32_t* __restrict__ blocks, uint64_t nwords, uint32_t lo, int ml,
+__device__ __forceinline__ bool mx_window(const uint32_t* __restrict__ blocks, uint64_t nwords, uint64_t lo, int ml,
                                           uint32_t& codes) {
-  const uint32_t hi = lo + (uint32_t)ml - 1u;
+  const uint64_t hi = lo + (uint64_t)ml - 1u;
   const uint64_t b0 = lo >> 5, b1 = hi >> 5;
   if (3 * b1 + 2 >= nwords) return false;
   uint64_t f = blocks[3 * b0 + 2];
   if (b1 != b0) f |= (uint64_t)blocks[3 * b1 + 2] << 32;
   if ((f >> (lo & 31u)) & ((1ull << ml) - 1ull)) return false;
-  const uint32_t h = lo >> 4;  // half-words: even = low word (nt 0-15 of the block), odd = high word
+  const uint64_t h = lo >> 4;  // half-words: even = low word (nt 0-15 of the block), odd = high word
   const uint32_t w0 = blocks[3 * (size_t)(h >> 1) + ((h & 1u) ? 0 : 1)];
   uint64_t x = w0;
   if ((lo & 15u) + (uint32_t)ml > 16u) {
-    const uint32_t h1 = h + 1u;
+    const uint64_t h1 = h + 1u;
     x |= (uint64_t)blocks[3 * (size_t)(h1 >> 1) + ((h1 & 1u) ? 0 : 1)] << 32;
   }
   codes = (uint32_t)(x >> (2u * (lo & 15u))) & ((1u << (2 * ml)) - 1u);
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(64) void mx_search_kernel(const gmapdp_microexon_pr
               const int64_t lo = watson ? base + j : base - j - (ml - 1);  // the window, ascending
               const bool inb = watson ? lo + ml <= (int64_t)P.chrhigh : lo >= (int64_t)P.chroffset;
               uint32_t codes;
-              hit = inb && mx_window(blocks, nwords, (uint32_t)lo, ml, codes) && codes == (watson ? pat : rcpat);
+              hit = inb && mx_window(blocks, nwords, (uint64_t)lo, ml, codes) && codes == (watson ? pat : rcpat);
             }
             const int cand = textleft + j;
             hit = hit && gnt(cand - 2) == i3 && gnt(cand - 1) == i4 && gnt(cand + ml) == i1 && gnt(cand + ml + 1) == i2;
@@ -153,13 +153,13 @@ __global__ __launch_bounds__(64) void mx_search_kernel(const gmapdp_microexon_pr
               c.candidate = cand;
               c.middlelength = ml;
               if (watson) {
-                c.pos2 = P.chroffset + (uint32_t)(cand - 1) + 1u;
-                c.pos3 = P.chroffset + (uint32_t)(cand + ml);
+                c.pos2 = P.chroffset + (uint64_t)(int64_t)(cand - 1) + 1u;  // Univcoord_T arithmetic
+                c.pos3 = P.chroffset + (uint64_t)(int64_t)(cand + ml);
                 c.model2 = P.cdna_direction > 0 ? GMAPDP_MAXENT_ACCEPTOR : GMAPDP_MAXENT_ANTIDONOR;
                 c.model3 = P.cdna_direction > 0 ? GMAPDP_MAXENT_DONOR : GMAPDP_MAXENT_ANTIACCEPTOR;
               } else {
-                c.pos2 = P.chrhigh - (uint32_t)(cand - 1);
-                c.pos3 = P.chrhigh - (uint32_t)(cand + ml) + 1u;
+                c.pos2 = P.chrhigh - (uint64_t)(int64_t)(cand - 1);
+                c.pos3 = P.chrhigh - (uint64_t)(int64_t)(cand + ml) + 1u;
                 c.model2 = P.cdna_direction > 0 ? GMAPDP_MAXENT_ANTIACCEPTOR : GMAPDP_MAXENT_DONOR;
                 c.model3 = P.cdna_direction > 0 ? GMAPDP_MAXENT_ANTIDONOR : GMAPDP_MAXENT_ACCEPTOR;
               }

@@ -1093,7 +1093,7 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
 }
 
 __device__ __forceinline__ char s2_genomic_nt(const uint32_t* __restrict__ blocks, uint64_t nwords, uint32_t chrpos,
-                                              uint32_t chroffset, uint32_t chrhigh, bool plusp) {
+                                              uint64_t chroffset, uint64_t chrhigh, bool plusp) {
   // get_genomic_nt (stage2.c:4124): no chromosome-bound check
   const char c = decode_nt(blocks, nwords, plusp ? chroffset + chrpos : chrhigh - chrpos);
   return plusp ? c : compl_nt(c);

@@ -31,14 +31,14 @@ class GmapdpError(RuntimeError):
 
 class SingleProblem(C.Structure):
     _fields_ = [("qoff", C.c_int32), ("rlength", C.c_int32), ("glength", C.c_int32), ("roffset", C.c_int32),
-                ("goffset", C.c_int32), ("chroffset", C.c_uint32), ("chrhigh", C.c_uint32), ("flags", C.c_int32),
+                ("goffset", C.c_int32), ("chroffset", C.c_uint64), ("chrhigh", C.c_uint64), ("flags", C.c_int32),
                 ("genestrand", C.c_int32), ("extraband", C.c_int32), ("defect_rate", C.c_double),
                 ("dynprogindex", C.c_int32), ("pad_", C.c_int32)]
 
 
 class EndProblem(C.Structure):
     _fields_ = [("qoff", C.c_int32), ("rlength", C.c_int32), ("glength", C.c_int32), ("roffset", C.c_int32),
-                ("goffset", C.c_int32), ("chroffset", C.c_uint32), ("chrhigh", C.c_uint32), ("flags", C.c_int32),
+                ("goffset", C.c_int32), ("chroffset", C.c_uint64), ("chrhigh", C.c_uint64), ("flags", C.c_int32),
                 ("genestrand", C.c_int32), ("extraband", C.c_int32), ("end3p", C.c_int32), ("endalign", C.c_int32),
                 ("require_pos_score_p", C.c_int32), ("dynprogindex", C.c_int32), ("defect_rate", C.c_double)]
 
@@ -52,7 +52,7 @@ class Result(C.Structure):
 class GenomeProblem(C.Structure):
     _fields_ = [("qoff", C.c_int32), ("rlength", C.c_int32), ("glengthL", C.c_int32), ("glengthR", C.c_int32),
                 ("roffset", C.c_int32), ("goffsetL", C.c_int32), ("rev_goffsetR", C.c_int32),
-                ("chroffset", C.c_uint32), ("chrhigh", C.c_uint32), ("flags", C.c_int32),
+                ("chroffset", C.c_uint64), ("chrhigh", C.c_uint64), ("flags", C.c_int32),
                 ("cdna_direction", C.c_int32), ("genestrand", C.c_int32), ("extraband", C.c_int32),
                 ("maxpeelback", C.c_int32), ("dynprogindex", C.c_int32), ("pad_", C.c_int32),
                 ("defect_rate", C.c_double), ("prob_offset", C.c_int64)]
@@ -70,7 +70,7 @@ class GenomeResult(C.Structure):
 class CdnaProblem(C.Structure):
     _fields_ = [("qoffL", C.c_int32), ("qoffR", C.c_int32), ("rlengthL", C.c_int32), ("rlengthR", C.c_int32),
                 ("glength", C.c_int32), ("roffsetL", C.c_int32), ("rev_roffsetR", C.c_int32), ("goffset", C.c_int32),
-                ("chroffset", C.c_uint32), ("chrhigh", C.c_uint32), ("flags", C.c_int32), ("genestrand", C.c_int32),
+                ("chroffset", C.c_uint64), ("chrhigh", C.c_uint64), ("flags", C.c_int32), ("genestrand", C.c_int32),
                 ("extraband", C.c_int32), ("dynprogindex", C.c_int32), ("defect_rate", C.c_double)]
 
 
@@ -82,7 +82,7 @@ class CdnaResult(C.Structure):
 
 class OligoProblem(C.Structure):
     _fields_ = [("qoff", C.c_int32), ("querylength", C.c_int32), ("chrstart", C.c_uint32), ("chrend", C.c_uint32),
-                ("chroffset", C.c_uint32), ("chrhigh", C.c_uint32), ("plusp", C.c_int32), ("minor", C.c_int32)]
+                ("chroffset", C.c_uint64), ("chrhigh", C.c_uint64), ("plusp", C.c_int32), ("minor", C.c_int32)]
 
 
 class OligoResult(C.Structure):
@@ -92,7 +92,7 @@ class OligoResult(C.Structure):
 
 class Stage2Problem(C.Structure):
     _fields_ = [("qoff", C.c_int32), ("querylength", C.c_int32), ("chrstart", C.c_uint32), ("chrend", C.c_uint32),
-                ("chroffset", C.c_uint32), ("chrhigh", C.c_uint32), ("plusp", C.c_int32), ("splicingp", C.c_int32),
+                ("chroffset", C.c_uint64), ("chrhigh", C.c_uint64), ("plusp", C.c_int32), ("splicingp", C.c_int32),
                 ("maxintronlen", C.c_int32), ("pad_", C.c_int32)]
 
 
@@ -101,30 +101,39 @@ class Stage2Result(C.Structure):
                                           "diag_queryend", "path_offset", "npairs")]
 
 
-MICROEXON_PROBLEM_DTYPE = np.dtype([("qoff", "<i4"), ("rlength", "<i4"), ("roffset", "<i4"), ("goffsetL", "<i4"),
-                                    ("rev_goffsetR", "<i4"), ("cdna_direction", "<i4"), ("chroffset", "<u4"),
-                                    ("chrhigh", "<u4"), ("watsonp", "<i4"), ("genestrand", "<i4"),
-                                    ("dynprogindex", "<i4"), ("pad_", "<i4")])
-MICROEXON_CANDIDATE_DTYPE = np.dtype([("cL", "<i4"), ("cR", "<i4"), ("candidate", "<i4"), ("middlelength", "<i4"),
-                                      ("pos2", "<u4"), ("pos3", "<u4"), ("model2", "<i4"), ("model3", "<i4")])
+class MicroexonProblem(C.Structure):
+    _fields_ = [("qoff", C.c_int32), ("rlength", C.c_int32), ("roffset", C.c_int32), ("goffsetL", C.c_int32),
+                ("rev_goffsetR", C.c_int32), ("cdna_direction", C.c_int32), ("chroffset", C.c_uint64),
+                ("chrhigh", C.c_uint64), ("watsonp", C.c_int32), ("genestrand", C.c_int32),
+                ("dynprogindex", C.c_int32), ("pad_", C.c_int32)]
+
+
+class MicroexonCandidate(C.Structure):
+    _fields_ = [("cL", C.c_int32), ("cR", C.c_int32), ("candidate", C.c_int32), ("middlelength", C.c_int32),
+                ("pos2", C.c_uint64), ("pos3", C.c_uint64), ("model2", C.c_int32), ("model3", C.c_int32)]
 MICROEXON_RESULT_DTYPE = np.dtype([("ncandidates", "<i4"), ("dynprogindex", "<i4"), ("microintrontype", "<i4"),
                                    ("npairs", "<i4"), ("cand_offset", "<i8"), ("pair_offset", "<i8"),
                                    ("bestprob2", "<f8"), ("bestprob3", "<f8")])
 
 
-def _struct_dtype(S, fmt):
+_CFMT = {C.c_int32: "<i4", C.c_uint32: "<u4", C.c_int64: "<i8", C.c_uint64: "<u8", C.c_double: "<f8"}
+
+
+def _struct_dtype(S, fmt=None):
+    """numpy view of a ctypes structure (field formats from the ctypes types unless given)."""
+    fmt = fmt or [_CFMT[t] for _, t in S._fields_]
     return np.dtype({"names": [n for n, _ in S._fields_], "formats": fmt,
                      "offsets": [S.__dict__[n].offset for n, _ in S._fields_], "itemsize": C.sizeof(S)})
 
 
-GENOME_PROBLEM_DTYPE = _struct_dtype(GenomeProblem, ["<i4"] * 7 + ["<u4", "<u4"] + ["<i4"] * 7 + ["<f8", "<i8"])
-GENOME_RESULT_DTYPE = _struct_dtype(GenomeResult, ["<i4"] * 14 + ["<f8", "<f8"])
-CDNA_PROBLEM_DTYPE = _struct_dtype(CdnaProblem, ["<i4"] * 8 + ["<u4", "<u4"] + ["<i4"] * 4 + ["<f8"])
-CDNA_RESULT_DTYPE = _struct_dtype(CdnaResult, ["<i4"] * 8)
-OLIGO_PROBLEM_DTYPE = _struct_dtype(OligoProblem, ["<i4", "<i4", "<u4", "<u4", "<u4", "<u4", "<i4", "<i4"])
-OLIGO_RESULT_DTYPE = _struct_dtype(OligoResult, ["<i4"] * 4 + ["<i8", "<i8"])
-STAGE2_PROBLEM_DTYPE = _struct_dtype(Stage2Problem, ["<i4", "<i4"] + ["<u4"] * 4 + ["<i4"] * 4)
-STAGE2_RESULT_DTYPE = _struct_dtype(Stage2Result, ["<i4"] * 8)
+GENOME_PROBLEM_DTYPE = _struct_dtype(GenomeProblem)
+GENOME_RESULT_DTYPE = _struct_dtype(GenomeResult)
+CDNA_PROBLEM_DTYPE = _struct_dtype(CdnaProblem)
+CDNA_RESULT_DTYPE = _struct_dtype(CdnaResult)
+OLIGO_PROBLEM_DTYPE = _struct_dtype(OligoProblem)
+OLIGO_RESULT_DTYPE = _struct_dtype(OligoResult)
+STAGE2_PROBLEM_DTYPE = _struct_dtype(Stage2Problem)
+STAGE2_RESULT_DTYPE = _struct_dtype(Stage2Result)
 PATH_DTYPE = np.dtype([("pair_offset", "<i8"), ("npairs", "<i4"), ("pad_", "<i4")])
 PATH_PAIR_DTYPE = np.dtype([("querypos", "<i4"), ("genomepos", "<i4"), ("queryjump", "<i4"), ("genomejump", "<i4"),
                             ("cdna", "S1"), ("comp", "S1"), ("genome", "S1"), ("genomealt", "S1")])
@@ -132,16 +141,10 @@ PATH_PAIR_DTYPE = np.dtype([("querypos", "<i4"), ("genomepos", "<i4"), ("queryju
 PAIR_DTYPE = np.dtype([("querypos", "<i4"), ("genomepos", "<i4"), ("jump", "<i4"), ("cdna", "S1"),
                        ("comp", "S1"), ("genome", "S1"), ("genomealt", "S1")])
 RESULT_DTYPE = np.dtype([(n, "<i4") for n, _ in Result._fields_])
-PROBLEM_DTYPE = np.dtype({"names": [n for n, _ in SingleProblem._fields_],
-                          "formats": ["<i4", "<i4", "<i4", "<i4", "<i4", "<u4", "<u4", "<i4", "<i4", "<i4", "<f8",
-                                      "<i4", "<i4"],
-                          "offsets": [SingleProblem.__dict__[n].offset for n, _ in SingleProblem._fields_],
-                          "itemsize": C.sizeof(SingleProblem)})
-END_PROBLEM_DTYPE = np.dtype({"names": [n for n, _ in EndProblem._fields_],
-                              "formats": ["<i4", "<i4", "<i4", "<i4", "<i4", "<u4", "<u4", "<i4", "<i4", "<i4",
-                                          "<i4", "<i4", "<i4", "<i4", "<f8"],
-                              "offsets": [EndProblem.__dict__[n].offset for n, _ in EndProblem._fields_],
-                              "itemsize": C.sizeof(EndProblem)})
+PROBLEM_DTYPE = _struct_dtype(SingleProblem)
+MICROEXON_PROBLEM_DTYPE = _struct_dtype(MicroexonProblem)
+MICROEXON_CANDIDATE_DTYPE = _struct_dtype(MicroexonCandidate)
+END_PROBLEM_DTYPE = _struct_dtype(EndProblem)
 
 _lib = None
 
@@ -296,12 +299,12 @@ def build_genome_batch(calls):
 
 
 def genome_splice_sites(probs):
-    """(positions uint32, models uint8) of every splice-probability entry: the Maxent_hr_*_prob
+    """(positions uint64, models uint8) of every splice-probability entry: the Maxent_hr_*_prob
     calls (model 0 donor, 1 acceptor, 2 antidonor, 3 antiacceptor) whose values the engine reads."""
     lib = load_library()
     n = len(probs)
     m = lib.gmapdp_genome_prob_entries(probs.ctypes.data, n)
-    pos = np.zeros(max(m, 1), dtype=np.uint32)
+    pos = np.zeros(max(m, 1), dtype=np.uint64)
     mod = np.zeros(max(m, 1), dtype=np.uint8)
     rc = lib.gmapdp_genome_splice_sites(probs.ctypes.data, n, pos.ctypes.data, mod.ctypes.data, m)
     if rc:

@@ -136,16 +136,11 @@ shim_refuse (const char *what) {
   abort();
 }
 
-/* The engine's descriptors carry 32-bit genome coordinates (gmap's Univcoord_T, univcoord.h:9-11).
-   A gmapl build (LARGE_GENOMES, 64-bit Univcoord_T) or any coordinate at or above 2^32 is refused
-   instead of being truncated. */
-#ifdef LARGE_GENOMES
-#error "gmapdp shim: LARGE_GENOMES (gmapl, 64-bit Univcoord_T) is not supported by this engine build"
-#endif
-static uint32_t
+/* Universal coordinates travel as 64-bit gmapdp_coord_t, so the same shim serves gmap (32-bit
+   Univcoord_T) and gmapl (LARGE_GENOMES, 64-bit Univcoord_T, univcoord.h:9-11). */
+static gmapdp_coord_t
 shim_coord (Univcoord_T x) {
-  if ((uint64_t) x > 0xFFFFFFFFu) shim_refuse("a genome coordinate at or above 2^32 (gmapl genomes)");
-  return (uint32_t) x;
+  return (gmapdp_coord_t) x;
 }
 
 static void
@@ -211,7 +206,6 @@ shim_context (Genome_T genome) {
   }
   if (genome != shim_genome) {
     length = (uint64_t) Genome_genomelength(genome);
-    if (length > 0xFFFFFFFFull) shim_refuse("a genome of 2^32 nt or more (gmapl genomes)");
     nwords = gmapdp_genome_words(length);
     shim_check(gmapdp_set_genome(shim_ctx, (const uint32_t *) Genome_blocks(genome), nwords, length),
                "gmapdp_set_genome");
@@ -853,7 +847,7 @@ __wrap_Dynprog_end3_gap (int *dynprogindex, int *finalscore, int *nmatches, int 
 
 /* Maxent_hr_*_prob of one splice-site entry (the host's MaxEnt models, maxent_hr.c) */
 static double
-shim_maxent (Genome_T genome, Genome_T genomealt, uint8_t model, uint32_t pos, Univcoord_T chroffset) {
+shim_maxent (Genome_T genome, Genome_T genomealt, uint8_t model, gmapdp_coord_t pos, Univcoord_T chroffset) {
   switch (model) {
   case GMAPDP_MAXENT_DONOR: return Maxent_hr_donor_prob(genome, genomealt, (Univcoord_T) pos, chroffset);
   case GMAPDP_MAXENT_ACCEPTOR: return Maxent_hr_acceptor_prob(genome, genomealt, (Univcoord_T) pos, chroffset);
@@ -875,7 +869,7 @@ __wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_r
   gmapdp_genome_problem *p;
   gmapdp_genome_result *res;
   size_t m, i;
-  static __thread uint32_t *pos = NULL;
+  static __thread gmapdp_coord_t *pos = NULL;
   static __thread uint8_t *model = NULL;
   static __thread size_t poscap = 0, modelcap = 0;
   List_T list;

@@ -54,6 +54,11 @@
 #include <stddef.h>
 #include <stdint.h>
 
+/* A universal genome coordinate (GMAP's Univcoord_T, univcoord.h:9-11): 64 bits so that one ABI
+ * serves gmap (32-bit Univcoord_T) and gmapl (LARGE_GENOMES, genomes past 2^32 nt).  Chromosome
+ * positions (Chrpos_T) stay 32-bit, as in both GMAP builds. */
+typedef uint64_t gmapdp_coord_t;
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -109,8 +114,8 @@ typedef struct {
   int32_t glength;
   int32_t roffset;
   int32_t goffset;
-  uint32_t chroffset;
-  uint32_t chrhigh;
+  gmapdp_coord_t chroffset;
+  gmapdp_coord_t chrhigh;
   int32_t flags;          /* GMAPDP_WATSON | GMAPDP_JUMP_LATE | GMAPDP_WIDEBAND */
   int32_t genestrand;     /* 0, +1, +2 */
   int32_t extraband;      /* extraband_single */
@@ -138,8 +143,8 @@ typedef struct {
   int32_t glength;
   int32_t roffset;
   int32_t goffset;
-  uint32_t chroffset;
-  uint32_t chrhigh;
+  gmapdp_coord_t chroffset;
+  gmapdp_coord_t chrhigh;
   int32_t flags;          /* GMAPDP_WATSON | GMAPDP_JUMP_LATE */
   int32_t genestrand;
   int32_t extraband;      /* extraband_end */
@@ -190,8 +195,8 @@ typedef struct {
   int32_t roffset;
   int32_t goffsetL;
   int32_t rev_goffsetR;
-  uint32_t chroffset;
-  uint32_t chrhigh;
+  gmapdp_coord_t chroffset;
+  gmapdp_coord_t chrhigh;
   int32_t flags;          /* GMAPDP_WATSON | GMAPDP_JUMP_LATE | GMAPDP_HALFP | GMAPDP_FINALP */
   int32_t cdna_direction;
   int32_t genestrand;
@@ -239,7 +244,7 @@ typedef struct {
  * at the problem's prob_offset: the arguments of the Maxent_hr_*_prob call
  * (with the problem's chroffset) whose result belongs at that entry
  * (dynprog_genome.c:2573-2660).  Host-only; no device needed. */
-int gmapdp_genome_splice_sites (const gmapdp_genome_problem *problems, int n, uint32_t *positions,
+int gmapdp_genome_splice_sites (const gmapdp_genome_problem *problems, int n, gmapdp_coord_t *positions,
                                 uint8_t *models, size_t nentries);
 /* Entries of the probability arena needed by the batch (max prob_offset + glengthL + glengthR). */
 size_t gmapdp_genome_prob_entries (const gmapdp_genome_problem *problems, int n);
@@ -281,8 +286,8 @@ typedef struct {
   int32_t roffsetL;
   int32_t rev_roffsetR;
   int32_t goffset;
-  uint32_t chroffset;
-  uint32_t chrhigh;
+  gmapdp_coord_t chroffset;
+  gmapdp_coord_t chrhigh;
   int32_t flags;          /* GMAPDP_WATSON | GMAPDP_JUMP_LATE | GMAPDP_SIMD */
   int32_t genestrand;
   int32_t extraband;      /* extraband_paired */
@@ -330,8 +335,8 @@ typedef struct {
   int32_t goffsetL;
   int32_t rev_goffsetR;
   int32_t cdna_direction;
-  uint32_t chroffset;
-  uint32_t chrhigh;
+  gmapdp_coord_t chroffset;
+  gmapdp_coord_t chrhigh;
   int32_t watsonp;
   int32_t genestrand;
   int32_t dynprogindex;
@@ -342,7 +347,7 @@ typedef struct {
   int32_t cL, cR;          /* lengths of the left and right pieces */
   int32_t candidate;       /* genomic offset of the microexon (goffsetM) */
   int32_t middlelength;
-  uint32_t pos2, pos3;     /* splice_pos of prob2 and prob3 (universal coordinates) */
+  gmapdp_coord_t pos2, pos3;  /* splice_pos of prob2 and prob3 (universal coordinates) */
   int32_t model2, model3;  /* GMAPDP_MAXENT_* */
 } gmapdp_microexon_candidate;
 
@@ -399,8 +404,8 @@ typedef struct {
   int32_t querylength;
   uint32_t chrstart;
   uint32_t chrend;
-  uint32_t chroffset;
-  uint32_t chrhigh;
+  gmapdp_coord_t chroffset;
+  gmapdp_coord_t chrhigh;
   int32_t plusp;
   int32_t minor;
 } gmapdp_oligo_problem;
@@ -456,8 +461,8 @@ typedef struct {
   int32_t querylength;
   uint32_t chrstart;
   uint32_t chrend;
-  uint32_t chroffset;
-  uint32_t chrhigh;
+  gmapdp_coord_t chroffset;
+  gmapdp_coord_t chrhigh;
   int32_t plusp;
   int32_t splicingp;       /* Stage2_setup's splicingp_in (novelsplicingp || knownsplicingp) */
   int32_t maxintronlen;    /* Stage2_setup's maxintronlen_in */

@@ -26,6 +26,8 @@
 #                              used only by tests/ and the golden generator.
 #   _ref/gmap_V                the reference `gmap` program itself (all of
 #                              GMAP_FILES, unmodified): the end-to-end oracle
+#   _ref/gmap_large            gmapl (the nosimd build with LARGE_GENOMES: 64-bit Univcoord_T), and
+#   _ref/gmap_gpu_large        gmapl linked with the drop-in shim
 #   _ref/gmap_gpu_V            the same objects linked with the drop-in shim
 #                              (`ld --wrap`) and libgmapdp.so:
 #                              GMAP's own per-read pipeline on the MI355X engine
@@ -77,13 +79,17 @@ FLAGS_nosimda := -DHAVE_ALLOCA=1 -DHAVE_ALLOCA_H=1
 # The same for the AVX2 build (bridge_intron_gap_8/16_site_level reads leftdi after FREEA too,
 # dynprog_genome.c:1370-1379 / :2245-2254).
 FLAGS_avx2a  := $(FLAGS_avx2) -DHAVE_ALLOCA=1 -DHAVE_ALLOCA_H=1
+# gmapl: the nosimd build with 64-bit Univcoord_T (src/Makefile.am:366, -DLARGE_GENOMES=1) and the two
+# extra sources of GMAPL_FILES (src/Makefile.am:324).
+FLAGS_large  := -DLARGE_GENOMES=1
+SRCS_large   := $(GMAP_C) uint8list.c uint8table_rh.c
 
 .DEFAULT_GOAL := all
 
-VARIANTS := nosimd avx2 nosimda avx2a
+VARIANTS := nosimd avx2 nosimda avx2a large
 
 define variant_rules
-LIBOBJS_$(1) := $$(patsubst %.c,$(OUT)/$(1)/%.o,$(HARNESS_C))
+LIBOBJS_$(1) := $$(patsubst %.c,$(OUT)/$(1)/%.o,$$(filter-out $(UNBUILDABLE_C) $(NOTLINKED_C),$$(or $$(SRCS_$(1)),$(GMAP_C))))
 
 $(OUT)/$(1)/%.o: $(SRC)/%.c
 	@mkdir -p $$(dir $$@)
@@ -100,7 +106,7 @@ $(OUT)/$(1)/access.o: $(SRC)/access.c
 	@mkdir -p $$(dir $$@)
 	$$(CC) $(BASEFLAGS) $(ACCESS_DEFS) $$(FLAGS_$(1)) -c $$< -o $$@
 
-PROGOBJS_$(1) := $$(patsubst %.c,$(OUT)/$(1)/%.o,$(GMAP_C))
+PROGOBJS_$(1) := $$(patsubst %.c,$(OUT)/$(1)/%.o,$$(or $$(SRCS_$(1)),$(GMAP_C)))
 endef
 
 $(foreach v,$(VARIANTS),$(eval $(call variant_rules,$(v))))
@@ -142,7 +148,7 @@ $(OUT)/librefdp_gpushim_avx2.so: $(LIBOBJS_avx2a) $(OUT)/avx2a/refharness.o $(OU
 	  -L$(GMAPDP_LIB) -lgmapdp -Wl,-rpath,'$$ORIGIN/../../gmap-2024_amd/lib' -lz -lm
 
 # ---- the full gmap program (end-to-end oracle) and the same program on the MI355X engine ----
-PROG_VARIANTS := nosimd avx2
+PROG_VARIANTS := nosimd avx2 large
 define prog_rules
 $(OUT)/gmap_$(1): $$(PROGOBJS_$(1))
 	$$(CC) -pthread -s -o $$@ $$^ -lz -lm

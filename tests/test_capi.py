@@ -75,16 +75,16 @@ def test_engine_fails_loudly_without_device():
 
 
 def test_problem_struct_layout():
-    assert C.sizeof(gmapdp.SingleProblem) == 56
+    assert C.sizeof(gmapdp.SingleProblem) == 72  # 64-bit universal coordinates (gmapdp_coord_t)
     assert C.sizeof(gmapdp.Result) == 32
     assert gmapdp.PAIR_DTYPE.itemsize == 16
-    assert gmapdp.PROBLEM_DTYPE.itemsize == 56
+    assert gmapdp.PROBLEM_DTYPE.itemsize == 72
 
 
 def test_genome_struct_layout():
-    assert C.sizeof(gmapdp.GenomeProblem) == 80
+    assert C.sizeof(gmapdp.GenomeProblem) == 96
     assert C.sizeof(gmapdp.GenomeResult) == 72
-    assert gmapdp.GENOME_PROBLEM_DTYPE.itemsize == 80
+    assert gmapdp.GENOME_PROBLEM_DTYPE.itemsize == 96
     assert gmapdp.GENOME_RESULT_DTYPE.itemsize == 72
 
 

@@ -6,6 +6,8 @@ Binaries (oracle/ref.mk, built from /root/reference/src where it lies; they trav
   oracle/_ref/gmap_{nosimd,avx2}      the unmodified reference `gmap` (the end-to-end oracle)
   oracle/_ref/gmap_gpu_{nosimd,avx2}  the same objects linked with gmap-2024_amd/shim via ld --wrap and
                                       libgmapdp.so (INTEGRATION.md)
+  oracle/_ref/gmap_large, gmap_gpu_large  gmapl: the nosimd build with LARGE_GENOMES (64-bit
+                                      Univcoord_T), unmodified and with the shim (BASELINE configs[4])
 
 Fixtures (tests/golden/, data only):
   align.test.ok       the reference's own golden (tests/align.test.in:9: gmap -A -g ss.chr17test ss.her2)
@@ -127,3 +129,27 @@ def test_gpu_gmap_worker_threads(threads):
     assert out == _read("e2e_nosimd.sam")
     st = _stats(err)
     assert st["batches"] > 0 and (threads < 8 or st["mean_batch"] > 1.5), st
+
+
+# ---- gmapl (LARGE_GENOMES, 64-bit Univcoord_T): the nosimd semantics, the same fixtures ----
+
+def test_reference_gmapl_reproduces_fixtures():
+    exe = _exe("gmap_large")
+    assert _run(exe, ALIGN_ARGS)[0] == _read("align.test.ok")
+    assert _run(exe, CDNA2_ARGS)[0] == _read("cdna2_genetest2_nosimd.txt")
+    assert _run(exe, E2E_ARGS)[0] == _read("e2e_nosimd.sam")
+
+
+@pytest.mark.gpu
+def test_gpu_gmapl_end_to_end():
+    """The shim compiled with LARGE_GENOMES into gmapl: 64-bit universal coordinates through the whole
+    drop-in, output identical to the reference's."""
+    exe = _exe("gmap_gpu_large")
+    out, err = _run(exe, ALIGN_ARGS, env={"GMAPDP_SHIM_STATS": "1"})
+    assert out == _read("align.test.ok")
+    assert _run(exe, CDNA2_ARGS)[0] == _read("cdna2_genetest2_nosimd.txt")
+    out, err = _run(exe, E2E_ARGS, env={"GMAPDP_SHIM_STATS": "1"})
+    assert out == _read("e2e_nosimd.sam")
+    st = _stats(err)
+    for k in ("Dynprog_single_gap", "Dynprog_genome_gap", "Stage2_compute", "Dynprog_microexon_int"):
+        assert st[k] > 0, st
