@@ -76,6 +76,8 @@ hipError_t launch_cg(bool simd, int RB, int nproblems, size_t lds, hipStream_t s
 size_t lds_bytes_oi(int umax, bool wide);
 size_t scratch_bytes_oi(int querylength, uint32_t genomiclength);
 size_t scratch_bytes_s2c(int querylength, int totalpositions, int ndiagonals);
+// the chaining kernels' counters (paths, pairs, ...) followed by their launch order (one int per call)
+inline size_t s2_counters_bytes(int n) { return 4 * sizeof(unsigned long long) + sizeof(int) * (size_t)(n > 0 ? n : 1); }
 hipError_t launch_s2c(int nproblems, hipStream_t stream, const DevStage2Problem* probs, const uint32_t* blocks,
                       uint64_t nwords, const char* qseq, const char* quc, const gmapdp_oligo_result* ores,
                       const int32_t* npos, const int32_t* map, const uint32_t* table, const int32_t* diags,
@@ -1984,7 +1986,7 @@ extern "C" int gmapdp_stage2_batch(gmapdp_ctx* ctx, const gmapdp_stage2_problem*
   if (e == hipSuccess) e = ctx->s2qseq.ensure(qbytes);
   if (e == hipSuccess) e = ctx->s2probs.ensure(sizeof(DevStage2Problem) * n);
   if (e == hipSuccess) e = ctx->s2results.ensure(sizeof(gmapdp_stage2_result) * n);
-  if (e == hipSuccess) e = ctx->s2counters.ensure(4 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = ctx->s2counters.ensure(s2_counters_bytes(n));
   if (e == hipSuccess) e = hipMemcpyAsync(ctx->qseq_uc.p, qseq_uc, qbytes, hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipMemcpyAsync(ctx->s2qseq.p, qseq, qbytes, hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipMemcpyAsync(ctx->s2probs.p, dp.data(), sizeof(DevStage2Problem) * n, hipMemcpyHostToDevice, s);
@@ -2389,7 +2391,7 @@ int gmapdp_stage2_plan_create(gmapdp_ctx* ctx, const gmapdp_stage2_problem* prob
   if (e == hipSuccess) e = hipMalloc(&P->d_map, sizeof(int32_t) * qbytes);
   if (e == hipSuccess) e = hipMalloc(&P->d_table, sizeof(uint32_t) * std::max<size_t>(toff, 1));
   if (e == hipSuccess) e = hipMalloc(&P->d_diag, 4 * sizeof(int32_t) * std::max<size_t>(doff, 1));
-  if (e == hipSuccess) e = hipMalloc(&P->d_counters, 4 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc(&P->d_counters, s2_counters_bytes(n));
   if (e == hipSuccess) e = hipMemcpy(P->d_probs, dp.data(), sizeof(DevStage2Problem) * n, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = ctx->qseq_uc.ensure(qbytes);
   if (e == hipSuccess) e = hipMemcpy(ctx->qseq_uc.p, qseq_uc, qbytes, hipMemcpyHostToDevice);

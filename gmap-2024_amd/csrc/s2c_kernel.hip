@@ -50,6 +50,7 @@ constexpr int kS2ExtraBounds = 20;      // diag.c:14
 // Phase timing (tools/oi_timing.py s2; the GMAPDP_OI_TIMING variant of the library only)
 #ifdef GMAPDP_OI_TIMING
 __device__ unsigned long long g_s2_marks[2][16];
+__device__ unsigned int g_s2_wave[3][16384];  // per s2b wave: sweep duration (wall-clock ticks), positions, hits
 #define S2_MARK(k)                                                  \
   do {                                                              \
     if (threadIdx.x == 0) {                                         \
@@ -1135,6 +1136,42 @@ __device__ __forceinline__ void s2_entry(const int* pathq, const int* pathg, int
   gap = ((gj - fill) > 0 || (qj - fill) > 0) ? 1 : 0;
 }
 
+// Launch order of the chaining kernels: blockIdx -> problem, the calls with the most seeding hits first.
+// A wave's sweep time grows with its hits (tools/oi_timing.py s2: correlation 0.89, 6.6 ms median and
+// 17.7 ms slowest per wave on the bench's reads), and the grid is ~1.4 waves of residency deep, so a
+// heavy call dispatched late sets the kernel's end; longest-first leaves the light ones for the tail.
+// The order sits after the four counters in the counters buffer (s2_order_kernel writes it).
+__device__ __forceinline__ int s2_problem(const unsigned long long* counters) {
+  return reinterpret_cast<const int*>(counters + 4)[blockIdx.x];
+}
+
+__global__ __launch_bounds__(1024) void s2_order_kernel(const DevStage2Problem* __restrict__ probs, int n,
+                                                        const gmapdp_oligo_result* __restrict__ ores,
+                                                        unsigned long long* __restrict__ counters) {
+  __shared__ int hist[1024];
+  __shared__ int wsum[16];
+  int* order = reinterpret_cast<int*>(counters + 4);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  hist[t] = 0;
+  __syncthreads();
+  auto bucket = [&](int i) {  // descending totalpositions, 4 per bucket
+    const int T = ores[probs[i].index].totalpositions;
+    return 1023 - min(max(T, 0) >> 2, 1023);
+  };
+  for (int i = t; i < n; i += 1024) atomicAdd(&hist[bucket(i)], 1);
+  __syncthreads();
+  const int v = hist[t];
+  const int incl = wave_incl_sum(v, lane);
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int base = 0;
+  for (int k = 0; k < w; k++) base += wsum[k];
+  __syncthreads();
+  hist[t] = base + incl - v;  // exclusive prefix: the bucket's first slot
+  __syncthreads();
+  for (int i = t; i < n; i += 1024) order[atomicAdd(&hist[bucket(i)], 1)] = i;
+}
+
 __global__ __launch_bounds__(64) void s2a_kernel(
     const DevStage2Problem* __restrict__ probs, const uint32_t* __restrict__ blocks, uint64_t nwords,
     const char* __restrict__ qseq, const char* __restrict__ quc, const gmapdp_oligo_result* __restrict__ ores,
@@ -1144,7 +1181,7 @@ __global__ __launch_bounds__(64) void s2a_kernel(
     unsigned long long path_cap, gmapdp_path_pair* __restrict__ pairs_out, unsigned long long pair_cap) {
   __shared__ int sh[8];
   const int lane = threadIdx.x;
-  const DevStage2Problem P = probs[blockIdx.x];
+  const DevStage2Problem P = probs[s2_problem(counters)];
   const int ql = P.querylength, nq = ql - kS2K + 1;
   const gmapdp_oligo_result O = ores[P.index];
   const int T = O.totalpositions, nd = O.ndiagonals;
@@ -1453,7 +1490,7 @@ __global__ __launch_bounds__(64) void s2b_kernel(
     unsigned long long path_cap, gmapdp_path_pair* __restrict__ pairs_out, unsigned long long pair_cap) {
   __shared__ int sh[8];
   const int lane = threadIdx.x;
-  const DevStage2Problem P = probs[blockIdx.x];
+  const DevStage2Problem P = probs[s2_problem(counters)];
   const int ql = P.querylength, nq = ql - kS2K + 1;
   const gmapdp_oligo_result O = ores[P.index];
   const int T = O.totalpositions, nd = O.ndiagonals;
@@ -1486,6 +1523,9 @@ __global__ __launch_bounds__(64) void s2b_kernel(
   if (R0.status != kS2Chained) return;
   const int qstart = R0.diag_querystart, qend = R0.diag_queryend;
   S2_MARK(3);
+#ifdef GMAPDP_OI_TIMING
+  const unsigned long long tw0 = wall_clock64();
+#endif
   // ---- align_compute_scores_lookback: the sweep on lane 0 ----
   {
     S2W W;
@@ -1505,6 +1545,13 @@ __global__ __launch_bounds__(64) void s2b_kernel(
     s2_sweep(W, npq, nq, minact, maxact, qstart, qend);
   }
   wave_sync();
+#ifdef GMAPDP_OI_TIMING
+  if (lane == 0 && blockIdx.x < 16384) {
+    g_s2_wave[0][blockIdx.x] = (unsigned int)(wall_clock64() - tw0);
+    g_s2_wave[1][blockIdx.x] = (unsigned int)(qend - qstart + 1);
+    g_s2_wave[2][blockIdx.x] = (unsigned int)T;
+  }
+#endif
 
   S2_MARK(4);
 }
@@ -1541,7 +1588,7 @@ __global__ __launch_bounds__(64) void s2c_kernel(
     unsigned long long path_cap, gmapdp_path_pair* __restrict__ pairs_out, unsigned long long pair_cap) {
   __shared__ int sh[8];
   const int lane = threadIdx.x;
-  const DevStage2Problem P = probs[blockIdx.x];
+  const DevStage2Problem P = probs[s2_problem(counters)];
   const int ql = P.querylength, nq = ql - kS2K + 1;
   const gmapdp_oligo_result O = ores[P.index];
   const int T = O.totalpositions, nd = O.ndiagonals;
@@ -1860,6 +1907,9 @@ __global__ __launch_bounds__(64) void s2c_kernel(
 }
 
 #ifdef GMAPDP_OI_TIMING
+extern "C" int gmapdp_debug_s2_waves(unsigned int* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_s2_wave), sizeof(g_s2_wave)) != hipSuccess;
+}
 extern "C" int gmapdp_debug_s2_marks(unsigned long long* out) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_s2_marks), sizeof(g_s2_marks)) != hipSuccess) return 1;
   static const unsigned long long zero[2][16] = {};
@@ -1881,7 +1931,10 @@ hipError_t launch_s2c(int nproblems, hipStream_t stream, const DevStage2Problem*
                   (void*)&npos, (void*)&map, (void*)&table, (void*)&diags, (void*)&scratch, (void*)&counters,
                   (void*)&scratch_cap, (void*)&results, (void*)&paths, (void*)&path_cap, (void*)&pairs,
                   (void*)&pair_cap};
-  hipError_t e = hipLaunchKernel(reinterpret_cast<void*>(&s2a_kernel), dim3(nproblems), dim3(64), args, 0, stream);
+  void* oargs[] = {(void*)&probs, (void*)&nproblems, (void*)&ores, (void*)&counters};
+  hipError_t e = hipLaunchKernel(reinterpret_cast<void*>(&s2_order_kernel), dim3(1), dim3(1024), oargs, 0, stream);
+  if (e == hipSuccess)
+    e = hipLaunchKernel(reinterpret_cast<void*>(&s2a_kernel), dim3(nproblems), dim3(64), args, 0, stream);
   if (e == hipSuccess)
     e = hipLaunchKernel(reinterpret_cast<void*>(&s2b_kernel), dim3(nproblems), dim3(64), args, 0, stream);
   if (e == hipSuccess)

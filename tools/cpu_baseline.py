@@ -39,6 +39,17 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
+def ref_layout(arr):
+    """a gmapdp problem array in the reference harness's struct layout (oracle/refharness.c: the same
+    fields in the same order, 32-bit chroffset/chrhigh, C alignment)"""
+    dt = np.dtype([(n, "<u4" if n in ("chroffset", "chrhigh") else arr.dtype.fields[n][0].str) for n in arr.dtype.names],
+                  align=True)
+    out = np.zeros(len(arr), dtype=dt)
+    for n in arr.dtype.names:
+        out[n] = arr[n]
+    return out
+
+
 def worker(args):
     wid, build, budget, reads = args
     from gmapdp import workload as W
@@ -68,9 +79,9 @@ def worker(args):
     pairs = np.zeros(cap * 32, dtype=np.uint8)  # RefPair records (oracle/refharness.c)
     paths = np.zeros(2 * 1024, dtype=np.int32)
     sc = np.zeros(8, dtype=np.int32)
-    fams = [("single", lib.refh_single_gap_batch, d["single"], W.SINGLE_PER_READ),
-            ("end", lib.refh_end_gap_batch, d["end"], W.END5_PER_READ + W.END3_PER_READ),
-            ("genome", lib.refh_genome_gap_batch, d["genome"], W.GENOME_PER_READ)]
+    fams = [("single", lib.refh_single_gap_batch, ref_layout(d["single"]), W.SINGLE_PER_READ),
+            ("end", lib.refh_end_gap_batch, ref_layout(d["end"]), W.END5_PER_READ + W.END3_PER_READ),
+            ("genome", lib.refh_genome_gap_batch, ref_layout(d["genome"]), W.GENOME_PER_READ)]
     t = {k: 0.0 for k in ("single", "end", "genome", "oligo", "microexon")}
     n = {k: 0 for k in t}
     t_start = time.perf_counter()

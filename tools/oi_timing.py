@@ -58,6 +58,7 @@ def main_s2(reads=10000):
     import torch
     lib = gmapdp.load_library(os.path.join(ROOT, "gmap-2024_amd", "lib", "libgmapdp_oitiming.so"))
     lib.gmapdp_debug_s2_marks.argtypes = [C.c_void_p]
+    lib.gmapdp_debug_s2_waves.argtypes = [C.c_void_p]
     layout = W.Layout(W.CHR22)
     genome = W.make_genome(layout, seed=22)
     eng = gmapdp.Engine(0)
@@ -79,9 +80,18 @@ def main_s2(reads=10000):
            for n, a, b in (("cells_us", 12, 5), ("traceback_filter_us", 5, 6), ("convert_us", 6, 7))}
     cnt = {k: round(float(marks[i]) / 1e2 / max(int(c[0]), 1), 1)
            for k, i in (("sweep_meta_us", 8), ("sweep_one_us", 9), ("sweep_mult_us", 10), ("sweep_tail_us", 11))}
+    wv = np.zeros((3, 16384), dtype=np.uint32)
+    lib.gmapdp_debug_s2_waves(wv.ctypes.data)
+    k = min(len(probs), 16384)
+    us, npq, nh = wv[0, :k] / 1e2, wv[1, :k].astype(np.float64), wv[2, :k].astype(np.float64)
+    sweep = {"p50_us": float(np.percentile(us, 50)), "p90_us": float(np.percentile(us, 90)),
+             "p99_us": float(np.percentile(us, 99)), "max_us": float(us.max()), "mean_us": float(us.mean()),
+             "mean_positions": float(npq.mean()), "mean_hits": float(nh.mean()), "max_hits": float(nh.max()),
+             "corr_us_hits": float(np.corrcoef(us, nh)[0, 1]), "corr_us_positions": float(np.corrcoef(us, npq)[0, 1]),
+             "slowest": [[float(us[i]), int(npq[i]), int(nh[i])] for i in np.argsort(-us)[:8]]}
     print(json.dumps({"waves": [int(x) for x in c[:8]], "phases": {n: round(d / tot, 4) for n, d in zip(S2_PHASES, dur)},
                       "mean_wave_us": tot / 1e2 / max(int(c[0]), 1), "status": np.bincount(res["status"] + 3).tolist(),
-                      "counts": cnt, "s2c_per_wave": s2c}))
+                      "counts": cnt, "s2c_per_wave": s2c, "s2b_sweep_per_wave": sweep}))
     eng.close()
 
 
