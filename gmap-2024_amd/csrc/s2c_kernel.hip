@@ -131,6 +131,14 @@ __device__ __forceinline__ int wave_incl_sum(int x, int lane) {
   }
   return x;
 }
+__device__ __forceinline__ int wave_incl_max(int x, int lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off, 64);
+    if (lane >= off) x = max(x, y);
+  }
+  return x;
+}
 __device__ __forceinline__ int wave_max_i(int x) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) x = max(x, __shfl_xor(x, off, 64));
@@ -209,6 +217,7 @@ struct S2Ring {
 // the sweep's LDS (one wave per workgroup): ds_* instructions rather than flat ones
 static __shared__ S2Ring s2_ring;
 static __shared__ int s2_fr[128];
+static __shared__ int s2_head[64];  // s2_dloop_multi: the entry whose hits start at each lane
 
 // a value every lane holds (loaded from a uniform address) as a scalar: scalar branches
 __device__ __forceinline__ int s2_u(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -230,6 +239,12 @@ struct S2W {
   int *pq, *pn, *poff, *pstart;  // per processed entry: q, active count, off[q], ring start
   int pushed, tracectr, splicingp, lane;
   uint32_t maxintronlen;
+#ifdef GMAPDP_OI_TIMING
+  unsigned long long n_cand = 0, n_fast = 0, n_slow = 0, n_multi = 0;  // candidates, fast/multi windows, slow evals
+#define S2_TALLY(f, v) (W.f += (v))
+#else
+#define S2_TALLY(f, v) (void)0
+#endif
 };
 
 __device__ __forceinline__ S2HV s2_bcast(const S2HV& v, int j) {
@@ -514,6 +529,7 @@ __device__ __forceinline__ int s2_entry_eval(S2W& W, const S2Pref& pf, S2EntryCa
                                              int q, uint32_t position, int& last_tr, S2Best& b, bool range1,
                                              int* qd_out) {
   const S2E e = kk < kS2Meta ? pf.entry(W, kk) : ec.get(W, np, kk);
+  S2_TALLY(n_slow, 1);
   *qd_out = q - e.q;
   if (e.n <= 0 || start < 0) return -1;
   if (kk < kS2Meta && e.n == 1 && e.inring && start == 0)
@@ -558,9 +574,11 @@ __device__ __forceinline__ bool s2_dloop_fast(S2W& W, const S2Pref& pf, int np, 
   }
   uint64_t C = ballot(kind != 0);
   int last_visited = kmax;
+  S2_TALLY(n_fast, 1);
   while (C) {
     const int j = __ffsll((long long)C) - 1;
     C &= C - 1;
+    S2_TALLY(n_cand, 1);
     const int fsj = __builtin_amdgcn_readlane(fs, j);
     if (fsj > b.score) {
       const S2HV u = s2_bcast(pf.h, j);
@@ -585,6 +603,137 @@ __device__ __forceinline__ bool s2_dloop_fast(S2W& W, const S2Pref& pf, int np, 
     }
   }
   if (use_f && kk <= last_visited && (skip || r1skip)) f = -1;
+  return true;
+}
+
+// Section D over the newest processed entries [0, kmax] in one wave step when the window holds entries
+// with several active hits (s2_dloop_fast takes the all-single case): every hit the sequential walk
+// would look at (entry by entry, each from its frontier) gets a lane, in walk order, when they number
+// <= 64 and all sit in the ring.  The walk's sequential state reduces to:
+//  - last_tr (range 0): an entry's hits are skipped while they carry the incoming last_tr, which then
+//    becomes the first differing tracei, so each entry maps last_tr to its first tracei a, or (when
+//    last_tr == a) to its first tracei b != a: a scalar pass over the entries (a few SALU each);
+//  - the link: strict improvements over lanes in walk order are the records of a prefix max seeded
+//    with the current score; the walk stops after the first entry whose last record has
+//    consec >= ENOUGH_CONSECUTIVE, else the last record wins (the first lane holding the maximum);
+//  - _mult's frontiers: per visited entry, the first hit past ranges 0-1, or -1.
+// Fresh tracei values are drawn only for the winning range-2 link (values only meet in equality tests).
+// Returns false (nothing done) when the window does not fit.
+__device__ __forceinline__ bool s2_dloop_multi(S2W& W, const S2Pref& pf, int np, int kmax, int q, uint32_t position,
+                                               S2Best& b, bool range1, bool use_f, int& f) {
+  if (kmax >= 64) return false;
+  const int lane = W.lane;
+  const int f0 = use_f ? f : 0;
+  const bool inw = lane <= kmax && lane < np && f0 != -1;
+  const bool valid = inw && pf.n > 0;
+  const bool inring = pf.n <= kS2Ring && pf.start >= W.pushed - kS2Ring;
+  if (ballot(valid && !inring)) return false;
+  const int c = valid ? max(pf.n - f0, 0) : 0;
+  const int incl = wave_incl_sum(c, lane);
+  const int total = __builtin_amdgcn_readlane(incl, 63);
+  if (total > 64) return false;
+  S2_TALLY(n_multi, 1);
+  if (b.consec >= kS2EnoughConsec) return true;
+  const int excl = incl - c;
+  // one wave: its LDS operations run in order; the fence keeps the compiler from forwarding a lane's own
+  // 0 to its load (other lanes' stores must be read back)
+  s2_head[lane] = 0;
+  if (c > 0) s2_head[excl] = lane + 1;
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  const int hd = s2_head[lane];
+  const uint64_t H = ballot(hd > 0);
+  const bool act = lane < total;
+  // this lane's hit: entry e (its first lane s), hit index k
+  const uint64_t hb = H & ((2ull << lane) - 1ull);
+  const int sl = hb ? 63 - __clzll((long long)hb) : 0;
+  const int e = __shfl(hd, sl, 64) - 1;
+  const int ee = e < 0 ? 0 : e;
+  const int eq = __shfl(pf.q, ee, 64), est = __shfl(pf.start, ee, 64), ef = __shfl(f0, ee, 64),
+            ec = __shfl(c, ee, 64);
+  const int k = ef + (lane - sl);
+  S2HV v = {};
+  if (act) {
+    const int r = (est + k) & (kS2Ring - 1);
+    v.map = s2_ring.map[r];
+    v.score = s2_ring.score[r];
+    v.consec = s2_ring.consec[r];
+    v.tracei = s2_ring.tracei[r];
+    v.root = s2_ring.root[r];
+    v.hit = s2_ring.hit[r];
+  }
+  const int eend = sl + ec;  // one past the entry's last lane
+  const int a = __shfl(v.tracei, sl, 64);
+  const uint64_t N = ballot(act && v.tracei != a);
+  const uint64_t Nm = N & ~((1ull << sl) - 1ull);
+  const int nx = Nm ? __ffsll((long long)Nm) - 1 : 64;
+  const int nxt = nx < eend ? nx : eend;  // first lane of the entry whose tracei differs from a
+  const int bt = __shfl(v.tracei, nx < eend ? nx : sl, 64);
+  // range 0 across entries (scalar): eqm bit s set when the entry starting at lane s meets last_tr == a
+  uint64_t eqm = 0, Hm = H;
+  int last_tr = -1;
+  while (Hm) {
+    const int s0 = __ffsll((long long)Hm) - 1;
+    Hm &= Hm - 1ull;
+    const int as = __builtin_amdgcn_readlane(a, s0);
+    if (last_tr == as) {
+      eqm |= 1ull << s0;
+      last_tr = __builtin_amdgcn_readlane(bt, s0);
+    } else {
+      last_tr = as;
+    }
+  }
+  const bool skip0 = act && ((eqm >> sl) & 1ull) && lane < nxt;
+  const int qd = q - eq;
+  const bool r1 = act && !skip0 && range1 && v.map + W.maxintronlen + (uint32_t)qd <= position;
+  int kind = 0, fs = INT_MIN;
+  if (act && !skip0 && !r1) {
+    if (v.map + (uint32_t)kS2EqualNotSplicing + (uint32_t)qd < position) {
+      const int diff = (int)(position - v.map) - qd;
+      kind = 2;
+      fs = v.score + (-qd / kS2K) - (W.splicingp ? (diff / kS2TenThousand + 1) : (diff + 1));
+    } else if (v.map + (uint32_t)kS2K <= position) {
+      kind = 4;
+      fs = v.score + 1;
+    }
+  }
+  const int im = wave_incl_max(fs, lane);
+  int pm = __shfl_up(im, 1, 64);
+  if (lane == 0) pm = INT_MIN;
+  pm = max(pm, b.score);
+  const bool rec = kind != 0 && fs > pm;
+  int cons = 0;
+  if (kind == 4) {
+    const int g = (int)(position - v.map);
+    const int diff = g > qd ? g - qd : qd - g;
+    cons = (diff <= 0) ? v.consec + qd : 0;
+  }
+  const uint64_t R = ballot(rec);
+  const uint64_t upto_end = eend >= 64 ? ~0ull : ((1ull << eend) - 1ull);
+  const uint64_t after = ~((2ull << lane) - 1ull);
+  const bool lastrec = rec && !(R & upto_end & after);
+  const uint64_t S = ballot(lastrec && cons >= kS2EnoughConsec);
+  int w = -1, stop_e = kmax;
+  if (S) {
+    w = __ffsll((long long)S) - 1;
+    stop_e = __builtin_amdgcn_readlane(e, w);
+  } else if (R) {
+    w = 63 - __clzll((long long)R);
+  }
+  S2_TALLY(n_cand, __popcll(R));
+  if (w >= 0) {
+    b.score = __builtin_amdgcn_readlane(fs, w);
+    b.consec = __builtin_amdgcn_readlane(cons, w);
+    b.root = __builtin_amdgcn_readlane(v.root, w);
+    b.pp = __builtin_amdgcn_readlane(eq, w);
+    b.ph = __builtin_amdgcn_readlane(v.hit, w);
+    b.tracei = __builtin_amdgcn_readlane(kind, w) == 2 ? ++W.tracectr : __builtin_amdgcn_readlane(v.tracei, w);
+  }
+  if (use_f) {
+    const uint64_t G = ballot(act && !skip0 && !r1);
+    const uint64_t Gm = G & ~((1ull << (excl & 63)) - 1ull);
+    const int g = Gm ? __ffsll((long long)Gm) - 1 : 64;
+    if (inw && lane <= stop_e) f = (c > 0 && g < excl + c) ? f0 + (g - excl) : -1;
+  }
   return true;
 }
 
@@ -615,7 +764,9 @@ __device__ __forceinline__ S2Best s2_one(S2W& W, int q, uint32_t position, int n
     const uint64_t dm = ballot(W.lane < np && W.lane > nlookback && (q - pf.q) - kS2K > lookback);
     const int kmax = dm ? __ffsll((long long)dm) - 1 : (np <= 64 ? np - 1 : 64);
     int fdummy = 0;
-    if (s2_dloop_fast(W, pf, np, kmax, q, position, b, W.splicingp != 0, false, fdummy)) np = 0;  // done
+    if (s2_dloop_fast(W, pf, np, kmax, q, position, b, W.splicingp != 0, false, fdummy) ||
+        s2_dloop_multi(W, pf, np, kmax, q, position, b, W.splicingp != 0, false, fdummy))
+      np = 0;  // done
     S2EntryCache ec;
     for (int kk = 0; kk < np && b.consec < kS2EnoughConsec && !donep; kk++) {
       const int eq = kk < kS2Meta ? __builtin_amdgcn_readlane(pf.q, kk) : ec.get(W, np, kk).q;
@@ -899,7 +1050,8 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
             const int kmax = min(min(maxseen, nfr - 1), np - 1);
             if (kmax < 64) {
               int f = lane <= kmax ? s2_fr[lane] : -1;
-              fast = s2_dloop_fast(W, pf, np, kmax, q, position, b, true, true, f);
+              fast = s2_dloop_fast(W, pf, np, kmax, q, position, b, true, true, f) ||
+                     s2_dloop_multi(W, pf, np, kmax, q, position, b, true, true, f);
               if (fast && lane <= kmax) s2_fr[lane] = f;
               __atomic_signal_fence(__ATOMIC_SEQ_CST);
             }
@@ -1091,6 +1243,12 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
   S2_COUNT(9, t_one);
   S2_COUNT(10, t_mult);
   S2_COUNT(11, t_tail);
+#ifdef GMAPDP_OI_TIMING
+  S2_COUNT(13, W.n_cand);
+  S2_COUNT(14, W.n_fast);
+  S2_COUNT(15, W.n_slow);
+  if (threadIdx.x == 0) atomicAdd(&g_s2_marks[1][15], W.n_multi);
+#endif
 }
 
 __device__ __forceinline__ char s2_genomic_nt(const uint32_t* __restrict__ blocks, uint64_t nwords, uint32_t chrpos,

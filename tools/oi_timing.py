@@ -88,6 +88,10 @@ def main_s2(reads=10000):
              "p99_us": float(np.percentile(us, 99)), "max_us": float(us.max()), "mean_us": float(us.mean()),
              "mean_positions": float(npq.mean()), "mean_hits": float(nh.mean()), "max_hits": float(nh.max()),
              "corr_us_hits": float(np.corrcoef(us, nh)[0, 1]), "corr_us_positions": float(np.corrcoef(us, npq)[0, 1]),
+             "per_wave_candidate_visits": float(marks[13]) / max(int(c[0]), 1),
+             "per_wave_fast_windows": float(marks[14]) / max(int(c[0]), 1),
+             "per_wave_slow_entry_evals": float(marks[15]) / max(int(c[0]), 1),
+             "per_wave_multi_windows": float(marks[31]) / max(int(c[0]), 1),
              "slowest": [[float(us[i]), int(npq[i]), int(nh[i])] for i in np.argsort(-us)[:8]]}
     print(json.dumps({"waves": [int(x) for x in c[:8]], "phases": {n: round(d / tot, 4) for n, d in zip(S2_PHASES, dur)},
                       "mean_wave_us": tot / 1e2 / max(int(c[0]), 1), "status": np.bincount(res["status"] + 3).tolist(),
