@@ -543,16 +543,17 @@ __device__ __forceinline__ int s2_entry_eval(S2W& W, const S2Pref& pf, S2EntryCa
 // nearest earlier evaluated entry" (a ballot and one lane shuffle); only the remaining candidates are
 // walked in order, and only they can change the link or end the loop (consec >= ENOUGH_CONSECUTIVE).
 // use_f: _mult's per-entry frontiers (lane kk holds f, 0 or -1), updated for the visited entries.
-// Returns false (nothing done) when the window holds another kind of entry.
-__device__ __forceinline__ bool s2_dloop_fast(S2W& W, const S2Pref& pf, int np, int kmax, int q, uint32_t position,
-                                              S2Best& b, bool range1, bool use_f, int& f) {
-  if (kmax >= 64) return false;
+// Windows past 64 entries: the first 64 here, then (return 2) the walk goes on from entry 64 with
+// last_tr = lt.  Returns 0 (nothing done) when the window holds another kind of entry, 1 when done.
+__device__ __forceinline__ int s2_dloop_fast(S2W& W, const S2Pref& pf, int np, int kmax, int q, uint32_t position,
+                                             S2Best& b, bool range1, bool use_f, int& f, int& lt) {
+  const int kend = kmax < 63 ? kmax : 63;
   const int kk = W.lane;
-  const bool inw = kk <= kmax && kk < np;
+  const bool inw = kk <= kend && kk < np;
   const bool valid = inw && pf.n > 0 && (!use_f || f != -1);
   const bool simple = pf.n == 1 && pf.start >= W.pushed - kS2Ring;
-  if (ballot(valid && !simple)) return false;
-  if (b.consec >= kS2EnoughConsec) return true;
+  if (ballot(valid && !simple)) return 0;
+  if (b.consec >= kS2EnoughConsec) return 1;
   const uint64_t V = ballot(valid);
   const uint64_t below = kk ? (V & ((1ull << kk) - 1ull)) : 0ull;
   const int prev = below ? 63 - __clzll((long long)below) : 0;
@@ -573,7 +574,8 @@ __device__ __forceinline__ bool s2_dloop_fast(S2W& W, const S2Pref& pf, int np, 
     }
   }
   uint64_t C = ballot(kind != 0);
-  int last_visited = kmax;
+  int last_visited = kend;
+  bool stopped = false;
   S2_TALLY(n_fast, 1);
   while (C) {
     const int j = __ffsll((long long)C) - 1;
@@ -598,12 +600,15 @@ __device__ __forceinline__ bool s2_dloop_fast(S2W& W, const S2Pref& pf, int np, 
       b.ph = u.hit;
       if (b.consec >= kS2EnoughConsec) {
         last_visited = j;
+        stopped = true;
         break;
       }
     }
   }
   if (use_f && kk <= last_visited && (skip || r1skip)) f = -1;
-  return true;
+  if (stopped || kmax < 64) return 1;
+  if (V) lt = __builtin_amdgcn_readlane(pf.h.tracei, 63 - __clzll((long long)V));  // every entry leaves its tracei
+  return 2;
 }
 
 // Section D over the newest processed entries [0, kmax] in one wave step when the window holds entries
@@ -618,22 +623,22 @@ __device__ __forceinline__ bool s2_dloop_fast(S2W& W, const S2Pref& pf, int np, 
 //    consec >= ENOUGH_CONSECUTIVE, else the last record wins (the first lane holding the maximum);
 //  - _mult's frontiers: per visited entry, the first hit past ranges 0-1, or -1.
 // Fresh tracei values are drawn only for the winning range-2 link (values only meet in equality tests).
-// Returns false (nothing done) when the window does not fit.
-__device__ __forceinline__ bool s2_dloop_multi(S2W& W, const S2Pref& pf, int np, int kmax, int q, uint32_t position,
-                                               S2Best& b, bool range1, bool use_f, int& f) {
-  if (kmax >= 64) return false;
+// Returns 0 (nothing done) when the window does not fit, else as s2_dloop_fast.
+__device__ __forceinline__ int s2_dloop_multi(S2W& W, const S2Pref& pf, int np, int kmax, int q, uint32_t position,
+                                              S2Best& b, bool range1, bool use_f, int& f, int& lt) {
+  const int kend = kmax < 63 ? kmax : 63;
   const int lane = W.lane;
   const int f0 = use_f ? f : 0;
-  const bool inw = lane <= kmax && lane < np && f0 != -1;
+  const bool inw = lane <= kend && lane < np && f0 != -1;
   const bool valid = inw && pf.n > 0;
   const bool inring = pf.n <= kS2Ring && pf.start >= W.pushed - kS2Ring;
-  if (ballot(valid && !inring)) return false;
+  if (ballot(valid && !inring)) return 0;
   const int c = valid ? max(pf.n - f0, 0) : 0;
   const int incl = wave_incl_sum(c, lane);
   const int total = __builtin_amdgcn_readlane(incl, 63);
-  if (total > 64) return false;
+  if (total > 64) return 0;
   S2_TALLY(n_multi, 1);
-  if (b.consec >= kS2EnoughConsec) return true;
+  if (b.consec >= kS2EnoughConsec) return 1;
   const int excl = incl - c;
   // one wave: its LDS operations run in order; the fence keeps the compiler from forwarding a lane's own
   // 0 to its load (other lanes' stores must be read back)
@@ -712,7 +717,7 @@ __device__ __forceinline__ bool s2_dloop_multi(S2W& W, const S2Pref& pf, int np,
   const uint64_t after = ~((2ull << lane) - 1ull);
   const bool lastrec = rec && !(R & upto_end & after);
   const uint64_t S = ballot(lastrec && cons >= kS2EnoughConsec);
-  int w = -1, stop_e = kmax;
+  int w = -1, stop_e = kend;
   if (S) {
     w = __ffsll((long long)S) - 1;
     stop_e = __builtin_amdgcn_readlane(e, w);
@@ -734,7 +739,9 @@ __device__ __forceinline__ bool s2_dloop_multi(S2W& W, const S2Pref& pf, int np,
     const int g = Gm ? __ffsll((long long)Gm) - 1 : 64;
     if (inw && lane <= stop_e) f = (c > 0 && g < excl + c) ? f0 + (g - excl) : -1;
   }
-  return true;
+  if (S || kmax < 64) return 1;
+  lt = last_tr;
+  return 2;
 }
 
 // score_querypos_lookback_one (stage2.c:1073); returns the link
@@ -763,12 +770,13 @@ __device__ __forceinline__ S2Best s2_one(S2W& W, int q, uint32_t position, int n
     // the entry that ends the walk (donep): the first beyond nlookback more than lookback + 8 back
     const uint64_t dm = ballot(W.lane < np && W.lane > nlookback && (q - pf.q) - kS2K > lookback);
     const int kmax = dm ? __ffsll((long long)dm) - 1 : (np <= 64 ? np - 1 : 64);
-    int fdummy = 0;
-    if (s2_dloop_fast(W, pf, np, kmax, q, position, b, W.splicingp != 0, false, fdummy) ||
-        s2_dloop_multi(W, pf, np, kmax, q, position, b, W.splicingp != 0, false, fdummy))
-      np = 0;  // done
+    int fdummy = 0, lt = -1;
+    int st = s2_dloop_fast(W, pf, np, kmax, q, position, b, W.splicingp != 0, false, fdummy, lt);
+    if (!st) st = s2_dloop_multi(W, pf, np, kmax, q, position, b, W.splicingp != 0, false, fdummy, lt);
+    if (st == 1) np = 0;  // done
+    if (st == 2) last_tr = lt;
     S2EntryCache ec;
-    for (int kk = 0; kk < np && b.consec < kS2EnoughConsec && !donep; kk++) {
+    for (int kk = st == 2 ? 64 : 0; kk < np && b.consec < kS2EnoughConsec && !donep; kk++) {
       const int eq = kk < kS2Meta ? __builtin_amdgcn_readlane(pf.q, kk) : ec.get(W, np, kk).q;
       if (kk > nlookback && (q - eq) - kS2K > lookback) donep = true;
       int qd;
@@ -1014,16 +1022,31 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
         S2Pref pf;
         pf.load(W, np);
         S2EntryCache ec;
+        // the entries any hit of q may look back to (stage2.c:1470's maxadj / maxnon bounds) and their
+        // frontiers, 64 entries per wave step: qd grows with n, so each bound is the last lane of a ballot
         int maxadj = 0, maxnon = 0, nfr = 0;
-        for (int n = 0; n < np && n < 128; n++) {
-          const int eq = n < kS2Meta ? __builtin_amdgcn_readlane(pf.q, n) : ec.get(W, np, n).q;
-          const int en = n < kS2Meta ? __builtin_amdgcn_readlane(pf.n, n) : ec.get(W, np, n).n;
+        for (int base = 0; base < np && base < 128; base += 64) {
+          const int n = base + lane;
+          const bool in = n < np && n < 128;
+          int eq = pf.q, en = pf.n;
+          if (base) {
+            wave_sync();  // the older entries' metadata was stored by lane 0
+            const int k = np - 1 - n;
+            eq = in ? W.pq[k] : 0;
+            en = in ? W.pn[k] : 0;
+          }
           const int qd = q - eq;
-          if (n > kS2Nsufflookback && n > 1 && qd - kS2K > kS2Sufflookback) break;  // later entries only shrink
-          if (n <= 1 || qd - kS2K <= kS2Sufflookback / 2) maxadj = n;
-          if (n <= kS2Nsufflookback || qd - kS2K <= kS2Sufflookback) maxnon = n;
-          if (lane == 0) s2_fr[n] = en > 0 ? 0 : -1;
-          nfr = n + 1;
+          const uint64_t B = ballot(in && n > kS2Nsufflookback && n > 1 && qd - kS2K > kS2Sufflookback);
+          const int lim = B ? __ffsll((long long)B) - 1 : 64;  // later entries only shrink
+          const bool v = in && lane < lim;
+          const uint64_t A = ballot(v && (n <= 1 || qd - kS2K <= kS2Sufflookback / 2));
+          const uint64_t M = ballot(v && (n <= kS2Nsufflookback || qd - kS2K <= kS2Sufflookback));
+          if (A) maxadj = base + 63 - __clzll((long long)A);
+          if (M) maxnon = base + 63 - __clzll((long long)M);
+          if (v) s2_fr[n] = en > 0 ? 0 : -1;
+          const uint64_t Vm = ballot(v);
+          if (Vm) nfr = base + 64 - __clzll((long long)Vm);
+          if (B || !(Vm >> 63)) break;
         }
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         int overall = 0, adjf = last.n > 0 ? 0 : -1;
@@ -1045,20 +1068,20 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
             b = {kS2K, (int)position, -1, -1, 0, -1};
             maxseen = maxnon;
           }
-          bool fast = false;
+          int st = 0, lt = -1;
           if (overall < kS2GreedyConsec) {
             const int kmax = min(min(maxseen, nfr - 1), np - 1);
-            if (kmax < 64) {
-              int f = lane <= kmax ? s2_fr[lane] : -1;
-              fast = s2_dloop_fast(W, pf, np, kmax, q, position, b, true, true, f) ||
-                     s2_dloop_multi(W, pf, np, kmax, q, position, b, true, true, f);
-              if (fast && lane <= kmax) s2_fr[lane] = f;
-              __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            }
+            const int kend = min(kmax, 63);
+            int f = lane <= kend ? s2_fr[lane] : -1;
+            st = s2_dloop_fast(W, pf, np, kmax, q, position, b, true, true, f, lt);
+            if (!st) st = s2_dloop_multi(W, pf, np, kmax, q, position, b, true, true, f, lt);
+            if (st && lane <= kend) s2_fr[lane] = f;
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
           }
-          if (overall < kS2GreedyConsec && !fast) {
-            int last_tr = -1;
-            for (int kk = 0; kk < np && b.consec < kS2EnoughConsec && kk <= maxseen && kk < nfr; kk++) {
+          if (overall < kS2GreedyConsec && st != 1) {
+            int last_tr = st == 2 ? lt : -1;
+            for (int kk = st == 2 ? 64 : 0; kk < np && b.consec < kS2EnoughConsec && kk <= maxseen && kk < nfr;
+                 kk++) {
               const int f = s2_u(s2_fr[kk]);
               if (f != -1) {
                 int qd;
