@@ -208,7 +208,10 @@ struct S2Best {
 // equality tests (range 0), so a fresh value per improvement event replaces the reference's
 // per-improvement counter without changing any decision.
 constexpr int kS2Ring = 128;
-constexpr int kS2Meta = 64;  // processed entries whose metadata stays in LDS
+// processed entries whose metadata stays in LDS: every lookback stays within the newest 128 (entries
+// sit at distinct query positions, so donep ends a walk by entry 73; the _mult bounds stop at 128)
+constexpr int kS2Meta = 128;
+constexpr int kS2Pref = 64;  // entries S2Pref holds (one per lane)
 struct S2Ring {
   uint32_t map[kS2Ring];
   int score[kS2Ring], consec[kS2Ring], tracei[kS2Ring], root[kS2Ring], hit[kS2Ring];
@@ -447,16 +450,11 @@ __device__ __forceinline__ int s2_eval(S2W& W, const S2E& e, int start, int q, u
   return frontier;
 }
 
-// the kk-th newest processed entry: LDS for the newest kS2Meta, global (after a full wait) beyond
+// the kk-th newest processed entry (kk < kS2Meta) from the LDS metadata ring
 struct S2EntryCache {
   __device__ __forceinline__ S2E get(const S2W& W, int np, int kk) {
-    const int k = np - 1 - kk;
-    if (kk < kS2Meta) {
-      const int s = k & (kS2Meta - 1);
-      return s2_mkentry(W, s2_u(s2_ring.eq[s]), s2_u(s2_ring.en[s]), s2_u(s2_ring.eoff[s]), s2_u(s2_ring.estart[s]));
-    }
-    wave_sync();
-    return s2_mkentry(W, W.pq[k], W.pn[k], W.poff[k], W.pstart[k]);
+    const int s = (np - 1 - kk) & (kS2Meta - 1);
+    return s2_mkentry(W, s2_u(s2_ring.eq[s]), s2_u(s2_ring.en[s]), s2_u(s2_ring.eoff[s]), s2_u(s2_ring.estart[s]));
   }
 };
 
@@ -467,7 +465,7 @@ struct S2Pref {
   S2HV h = {};
   __device__ __forceinline__ void load(const S2W& W, int np) {
     const int k = np - 1 - W.lane;
-    if (W.lane < kS2Meta && k >= 0) {
+    if (k >= 0) {
       const int s = k & (kS2Meta - 1);
       q = s2_ring.eq[s];
       n = s2_ring.en[s];
@@ -528,11 +526,11 @@ __device__ __forceinline__ int s2_eval1(S2W& W, int eq, const S2HV& u, int q, ui
 __device__ __forceinline__ int s2_entry_eval(S2W& W, const S2Pref& pf, S2EntryCache& ec, int np, int kk, int start,
                                              int q, uint32_t position, int& last_tr, S2Best& b, bool range1,
                                              int* qd_out) {
-  const S2E e = kk < kS2Meta ? pf.entry(W, kk) : ec.get(W, np, kk);
+  const S2E e = kk < kS2Pref ? pf.entry(W, kk) : ec.get(W, np, kk);
   S2_TALLY(n_slow, 1);
   *qd_out = q - e.q;
   if (e.n <= 0 || start < 0) return -1;
-  if (kk < kS2Meta && e.n == 1 && e.inring && start == 0)
+  if (kk < kS2Pref && e.n == 1 && e.inring && start == 0)
     return s2_eval1(W, e.q, s2_bcast(pf.h, kk), q, position, last_tr, b, range1);
   return s2_eval(W, e, start, q, position, last_tr, b, range1);
 }
@@ -777,7 +775,7 @@ __device__ __forceinline__ S2Best s2_one(S2W& W, int q, uint32_t position, int n
     if (st == 2) last_tr = lt;
     S2EntryCache ec;
     for (int kk = st == 2 ? 64 : 0; kk < np && b.consec < kS2EnoughConsec && !donep; kk++) {
-      const int eq = kk < kS2Meta ? __builtin_amdgcn_readlane(pf.q, kk) : ec.get(W, np, kk).q;
+      const int eq = kk < kS2Pref ? __builtin_amdgcn_readlane(pf.q, kk) : ec.get(W, np, kk).q;
       if (kk > nlookback && (q - eq) - kS2K > lookback) donep = true;
       int qd;
       (void)s2_entry_eval(W, pf, ec, np, kk, 0, q, position, last_tr, b, W.splicingp != 0, &qd);
@@ -1030,10 +1028,9 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
           const bool in = n < np && n < 128;
           int eq = pf.q, en = pf.n;
           if (base) {
-            wave_sync();  // the older entries' metadata was stored by lane 0
-            const int k = np - 1 - n;
-            eq = in ? W.pq[k] : 0;
-            en = in ? W.pn[k] : 0;
+            const int k = (np - 1 - n) & (kS2Meta - 1);
+            eq = in ? s2_ring.eq[k] : 0;
+            en = in ? s2_ring.en[k] : 0;
           }
           const int qd = q - eq;
           const uint64_t B = ballot(in && n > kS2Nsufflookback && n > 1 && qd - kS2K > kS2Sufflookback);
@@ -1240,10 +1237,6 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
       const bool ringed = high - low <= kS2Ring;
       const int start = ringed ? W.pushed : W.pushed - 2 * kS2Ring;  // never in the ring
       if (lane == 0) {
-        W.pq[np] = q;
-        W.pn[np] = nact;
-        W.poff[np] = qoff;
-        W.pstart[np] = start;
         const int s = np & (kS2Meta - 1);
         s2_ring.eq[s] = q;
         s2_ring.en[s] = nact;
