@@ -1319,31 +1319,57 @@ __device__ __forceinline__ int s2_problem(const unsigned long long* counters) {
   return reinterpret_cast<const int*>(counters + 4)[blockIdx.x];
 }
 
-__global__ __launch_bounds__(1024) void s2_order_kernel(const DevStage2Problem* __restrict__ probs, int n,
-                                                        const gmapdp_oligo_result* __restrict__ ores,
-                                                        unsigned long long* __restrict__ counters) {
+constexpr int kS2OrderThreads = 512, kS2OrderPer = 16;  // a tile of 8192 calls: keys held in registers
+__global__ __launch_bounds__(kS2OrderThreads) void s2_order_kernel(const DevStage2Problem* __restrict__ probs, int n,
+                                                                   const gmapdp_oligo_result* __restrict__ ores,
+                                                                   unsigned long long* __restrict__ counters) {
   __shared__ int hist[1024];
   __shared__ int wsum[16];
   int* order = reinterpret_cast<int*>(counters + 4);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  hist[t] = 0;
+  for (int b = t; b < 1024; b += kS2OrderThreads) hist[b] = 0;
   __syncthreads();
-  auto bucket = [&](int i) {  // descending totalpositions, 4 per bucket
-    const int T = ores[probs[i].index].totalpositions;
-    return 1023 - min(max(T, 0) >> 2, 1023);
+  constexpr int kTile = kS2OrderThreads * kS2OrderPer;
+  // bucket: descending totalpositions, 4 per bucket; the loads of a tile are issued together
+  auto keys = [&](int base, int* key) {
+    int idx[kS2OrderPer];
+#pragma unroll
+    for (int j = 0; j < kS2OrderPer; j++) {
+      const int i = base + j * kS2OrderThreads + t;
+      idx[j] = i < n ? probs[i].index : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < kS2OrderPer; j++) {
+      const int T = idx[j] >= 0 ? ores[idx[j]].totalpositions : 0;
+      key[j] = idx[j] >= 0 ? 1023 - min(max(T, 0) >> 2, 1023) : -1;
+    }
   };
-  for (int i = t; i < n; i += 1024) atomicAdd(&hist[bucket(i)], 1);
+  for (int base = 0; base < n; base += kTile) {
+    int key[kS2OrderPer];
+    keys(base, key);
+#pragma unroll
+    for (int j = 0; j < kS2OrderPer; j++)
+      if (key[j] >= 0) atomicAdd(&hist[key[j]], 1);
+  }
   __syncthreads();
-  const int v = hist[t];
-  const int incl = wave_incl_sum(v, lane);
+  // exclusive prefix over the 1024 buckets, two per thread
+  const int v0 = hist[2 * t], v1 = hist[2 * t + 1];
+  const int incl = wave_incl_sum(v0 + v1, lane);
   if (lane == 63) wsum[w] = incl;
   __syncthreads();
-  int base = 0;
-  for (int k = 0; k < w; k++) base += wsum[k];
+  int off = 0;
+  for (int k = 0; k < w; k++) off += wsum[k];
   __syncthreads();
-  hist[t] = base + incl - v;  // exclusive prefix: the bucket's first slot
+  hist[2 * t] = off + incl - v0 - v1;
+  hist[2 * t + 1] = off + incl - v1;
   __syncthreads();
-  for (int i = t; i < n; i += 1024) order[atomicAdd(&hist[bucket(i)], 1)] = i;
+  for (int base = 0; base < n; base += kTile) {
+    int key[kS2OrderPer];
+    keys(base, key);
+#pragma unroll
+    for (int j = 0; j < kS2OrderPer; j++)
+      if (key[j] >= 0) order[atomicAdd(&hist[key[j]], 1)] = base + j * kS2OrderThreads + t;
+  }
 }
 
 __global__ __launch_bounds__(64) void s2a_kernel(
@@ -1734,21 +1760,46 @@ __global__ __launch_bounds__(64) void s2b_kernel(
 // set when the hit has fewer than MIN_TERMINAL_NCONSECUTIVE consecutive matches; map[i] its chrpos
 constexpr int kS2cCap = 3072;  // hits whose links fit the s2c kernel's LDS (12 B each; 36 KB: 4 waves per CU)
 constexpr uint32_t kS2NoPred = 0x7fffffffu;
-template <class F>
-__device__ void s2_walk_lds(const uint32_t* link, const uint32_t* map, int gi, F visit) {
+// traceback_one over the LDS link table, by the whole wave: a link to the previous hit index (consecutive query positions with one
+// hit each, the common case) continues a run, so each step takes the run of up to 64 nodes from gi down
+// (one LDS read per lane, a ballot for the run's end) instead of one dependent LDS read per node.
+// Visited nodes (chrpos < 2^31) are numbered in walk order; pq/ph (optional) receive their query and
+// genomic positions.  Returns the count and the first and last visited nodes (wave-uniform).
+struct S2WalkOut {
+  int n, top, bottom;
+};
+__device__ S2WalkOut s2_walk_wave(const uint32_t* link, const uint32_t* map, const uint32_t* lq, int gi, int lane,
+                                  int* pq, int* ph) {
+  S2WalkOut o = {0, -1, -1};
   uint32_t w = link[gi];
   while (w & 0x80000000u) {  // prune the 3' end
     const uint32_t pr = w & kS2NoPred;
-    if (pr == kS2NoPred) return;
+    if (pr == kS2NoPred) return o;
     gi = (int)pr;
     w = link[gi];
   }
   for (;;) {
-    if ((int)map[gi] >= 0) visit(gi);
-    const uint32_t pr = w & kS2NoPred;
-    if (pr == kS2NoPred) return;
+    const int x = gi - lane;
+    const uint32_t px = (x >= 0 ? link[x] : kS2NoPred) & kS2NoPred;
+    const bool cont = x >= 1 && px == (uint32_t)(x - 1);
+    const uint64_t stop = ballot(!cont);
+    const int r = stop ? __ffsll((long long)stop) - 1 : 63;  // lanes 0..r hold the run's nodes
+    const uint32_t mx = lane <= r ? map[x] : 0x80000000u;
+    const bool vis = (int)mx >= 0;
+    const uint64_t vm = ballot(vis);
+    if (vis && pq) {
+      const int idx = o.n + lanes_below(vm, lane);
+      pq[idx] = (int)lq[x];
+      ph[idx] = (int)mx;
+    }
+    if (vm) {
+      if (o.top < 0) o.top = gi - (__ffsll((long long)vm) - 1);
+      o.bottom = gi - (63 - __clzll((long long)vm));
+    }
+    o.n += __popcll(vm);
+    const uint32_t pr = (uint32_t)__builtin_amdgcn_readlane((int)px, r);
+    if (pr == kS2NoPred) return o;
     gi = (int)pr;
-    w = link[gi];
   }
 }
 
@@ -1902,22 +1953,28 @@ __global__ __launch_bounds__(64) void s2c_kernel(
   // a single selected cell is the single result (Stage2_filter_unique keeps it): its walk records the
   // entries convert_to_nucleotides needs, and the second walk below is skipped
   const bool single = npaths == 1;
-  if (lane == 0) {
-    for (int p = 0; p < npaths; p++) {
-      int n = 0, top = -1, bottom = -1;
-      auto vis = [&](int gi) {
+  for (int p = 0; p < npaths; p++) {
+    const int cell = s2_u(cand[p]);
+    int n = 0, top = -1, bottom = -1;
+    if (lds_walk) {
+      const S2WalkOut o = s2_walk_wave(llink, lmap, lq, cell, lane, single ? pathq : nullptr, pathh);
+      n = o.n;
+      top = o.top;
+      bottom = o.bottom;
+    } else if (lane == 0) {
+      s2_walk(hits, off, cell, [&](int gi) {
         if (n == 0) top = gi;
         bottom = gi;
         if (single) {
-          pathq[n] = lds_walk ? (int)lq[gi] : hits[gi].q;
-          pathh[n] = lds_walk ? (int)lmap[gi] : (int)hits[gi].map;
+          pathq[n] = hits[gi].q;
+          pathh[n] = (int)hits[gi].map;
         }
         n++;
-      };
-      if (lds_walk) s2_walk_lds(llink, lmap, cand[p], vis);
-      else s2_walk(hits, off, cand[p], vis);
+      });
+    }
+    if (lane == 0) {
       S2Path r;
-      r.cell = cand[p];
+      r.cell = cell;
       r.n = n;
       r.start = n ? (lds_walk ? lmap[bottom] : hits[bottom].map) : 0u;
       r.end = n ? (lds_walk ? lmap[top] : hits[top].map) + (uint32_t)(kS2K - 1) : 0u;
@@ -1980,15 +2037,11 @@ __global__ __launch_bounds__(64) void s2c_kernel(
     if (keep[i]) continue;
     const S2Path x = pth[pord[i]];
     const int n = x.n;
-    if (lane == 0 && !single) {  // entries, 3' end first
+    if (!single && lds_walk) {  // entries, 3' end first
+      (void)s2_walk_wave(llink, lmap, lq, x.cell, lane, pathq, pathh);
+    } else if (lane == 0 && !single) {
       int e = 0;
-      if (lds_walk) {
-        s2_walk_lds(llink, lmap, x.cell, [&](int gi) {
-          pathq[e] = (int)lq[gi];
-          pathh[e] = (int)lmap[gi];
-          e++;
-        });
-      } else {
+      {
         s2_walk(hits, off, x.cell, [&](int gi) {
           pathq[e] = hits[gi].q;
           pathh[e] = (int)hits[gi].map;
@@ -2106,7 +2159,7 @@ hipError_t launch_s2c(int nproblems, hipStream_t stream, const DevStage2Problem*
                   (void*)&scratch_cap, (void*)&results, (void*)&paths, (void*)&path_cap, (void*)&pairs,
                   (void*)&pair_cap};
   void* oargs[] = {(void*)&probs, (void*)&nproblems, (void*)&ores, (void*)&counters};
-  hipError_t e = hipLaunchKernel(reinterpret_cast<void*>(&s2_order_kernel), dim3(1), dim3(1024), oargs, 0, stream);
+  hipError_t e = hipLaunchKernel(reinterpret_cast<void*>(&s2_order_kernel), dim3(1), dim3(kS2OrderThreads), oargs, 0, stream);
   if (e == hipSuccess)
     e = hipLaunchKernel(reinterpret_cast<void*>(&s2a_kernel), dim3(nproblems), dim3(64), args, 0, stream);
   if (e == hipSuccess)
