@@ -197,6 +197,16 @@ __device__ __forceinline__ void fill_range(int lane, uint32_t* dst, int a, int b
 struct S2Best {
   int consec, root, pp, ph, score, tracei;
 };
+// The link is wave-uniform by construction (every update comes from readlane/readfirstlane values);
+// restating that keeps it in SGPRs, so the tests on it are scalar branches rather than exec-mask ones.
+__device__ __forceinline__ void s2_uniform(S2Best& b) {
+  b.consec = __builtin_amdgcn_readfirstlane(b.consec);
+  b.root = __builtin_amdgcn_readfirstlane(b.root);
+  b.pp = __builtin_amdgcn_readfirstlane(b.pp);
+  b.ph = __builtin_amdgcn_readfirstlane(b.ph);
+  b.score = __builtin_amdgcn_readfirstlane(b.score);
+  b.tracei = __builtin_amdgcn_readfirstlane(b.tracei);
+}
 
 // ---- align_compute_scores_lookback, wave-uniform ----
 // Every lane runs the sweep's control flow; per-position metadata is prefetched 64 query positions at
@@ -551,6 +561,7 @@ __device__ __forceinline__ int s2_dloop_fast(S2W& W, const S2Pref& pf, int np, i
   const bool valid = inw && pf.n > 0 && (!use_f || f != -1);
   const bool simple = pf.n == 1 && pf.start >= W.pushed - kS2Ring;
   if (ballot(valid && !simple)) return 0;
+  s2_uniform(b);
   if (b.consec >= kS2EnoughConsec) return 1;
   const uint64_t V = ballot(valid);
   const uint64_t below = kk ? (V & ((1ull << kk) - 1ull)) : 0ull;
@@ -636,6 +647,7 @@ __device__ __forceinline__ int s2_dloop_multi(S2W& W, const S2Pref& pf, int np, 
   const int total = __builtin_amdgcn_readlane(incl, 63);
   if (total > 64) return 0;
   S2_TALLY(n_multi, 1);
+  s2_uniform(b);
   if (b.consec >= kS2EnoughConsec) return 1;
   const int excl = incl - c;
   // one wave: its LDS operations run in order; the fence keeps the compiler from forwarding a lane's own
@@ -760,6 +772,7 @@ __device__ __forceinline__ S2Best s2_one(S2W& W, int q, uint32_t position, int n
       lookback = kS2Sufflookback / 2;
     }
   }
+  s2_uniform(b);
   bool donep = false;
   int last_tr = -1;
   if (np > 0 && b.consec < kS2EnoughConsec) {
@@ -781,6 +794,7 @@ __device__ __forceinline__ S2Best s2_one(S2W& W, int q, uint32_t position, int n
       (void)s2_entry_eval(W, pf, ec, np, kk, 0, q, position, last_tr, b, W.splicingp != 0, &qd);
     }
   }
+  s2_uniform(b);
   if (b.pp < 0) {  // localp
     b.tracei = ++W.tracectr;
     b.score = kS2K;
@@ -911,6 +925,8 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
 #endif
   while (q <= qend) {
     S2_T0();
+    W.tracectr = s2_u(W.tracectr);
+    W.pushed = s2_u(W.pushed);
     if ((q & ~63) != cb) {
       cb = q & ~63;
       const int qq = cb + lane;
@@ -1065,6 +1081,7 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
             b = {kS2K, (int)position, -1, -1, 0, -1};
             maxseen = maxnon;
           }
+          s2_uniform(b);
           int st = 0, lt = -1;
           if (overall < kS2GreedyConsec) {
             const int kmax = min(min(maxseen, nfr - 1), np - 1);
@@ -1088,6 +1105,7 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
               }
             }
           }
+          s2_uniform(b);
           if (b.pp < 0) {
             b.tracei = ++W.tracectr;
             b.score = kS2K;
