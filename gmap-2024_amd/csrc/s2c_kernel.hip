@@ -1309,13 +1309,12 @@ __device__ void s2_walk(const S2Hit* hits, const int* off, int gi, F visit) {
 
 // convert_to_nucleotides (stage2.c:5334) for path entry e (3' end first): fill pairs between it and
 // the entry before, and whether a gap holder precedes them
-__device__ __forceinline__ void s2_entry(const int* pathq, const int* pathg, int e, int& fill, int& gap) {
+__device__ __forceinline__ void s2_entry_v(int e, int qpos, int gpos, int lq, int lg, int& fill, int& gap) {
   gap = 0;
   if (e == 0) {
     fill = kS2K - 1;
     return;
   }
-  const int qpos = pathq[e], gpos = pathg[e], lq = pathq[e - 1], lg = pathg[e - 1];
   const int qj = lq - 1 - qpos, gj = lg - 1 - gpos;
   if (qj == 0 && gj == 0) {
     fill = 0;
@@ -2068,15 +2067,29 @@ __global__ __launch_bounds__(64) void s2c_kernel(
       }
     }
     wave_sync();
-    // records per entry in generation (prepend) order: [gap holder], fills, the observed pair
+    // records per entry in generation (prepend) order: [gap holder], fills, the observed pair.
+    // Four 64-entry chunks per step, their loads issued together (the entries are in L2 scratch).
+    constexpr int kC = 4;
     int total = 0;
-    for (int cb = 0; cb < n; cb += 64) {
-      const int e = cb + lane;
+    for (int cb = 0; cb < n; cb += 64 * kC) {
+      int qp[kC], gp[kC], lqv[kC], lgv[kC];
+#pragma unroll
+      for (int k = 0; k < kC; k++) {
+        const int e = cb + 64 * k + lane;
+        qp[k] = e < n ? pathq[e] : 0;
+        gp[k] = e < n ? pathh[e] : 0;
+        lqv[k] = (e < n && e > 0) ? pathq[e - 1] : 0;
+        lgv[k] = (e < n && e > 0) ? pathh[e - 1] : 0;
+      }
       int cnt = 0;
-      if (e < n) {
-        int fill, gap;
-        s2_entry(pathq, pathh, e, fill, gap);
-        cnt = gap + fill + 1;
+#pragma unroll
+      for (int k = 0; k < kC; k++) {
+        const int e = cb + 64 * k + lane;
+        if (e < n) {
+          int fill, gap;
+          s2_entry_v(e, qp[k], gp[k], lqv[k], lgv[k], fill, gap);
+          cnt += gap + fill + 1;
+        }
       }
       total += wave_sum_i(cnt);
     }
@@ -2092,48 +2105,66 @@ __global__ __launch_bounds__(64) void s2c_kernel(
     }
     gmapdp_path_pair* dst = pairs_out + qb;
     int gen = 0;
-    for (int cb = 0; cb < n; cb += 64) {
-      const int e = cb + lane;
-      int cnt = 0, fill = 0, gap = 0;
-      if (e < n) {
-        s2_entry(pathq, pathh, e, fill, gap);
-        cnt = gap + fill + 1;
+    for (int cb = 0; cb < n; cb += 64 * kC) {
+      int qp[kC], gp[kC], lqv[kC], lgv[kC];
+#pragma unroll
+      for (int k = 0; k < kC; k++) {
+        const int e = cb + 64 * k + lane;
+        qp[k] = e < n ? pathq[e] : 0;
+        gp[k] = e < n ? pathh[e] : 0;
+        lqv[k] = (e < n && e > 0) ? pathq[e - 1] : 0;
+        lgv[k] = (e < n && e > 0) ? pathh[e - 1] : 0;
       }
-      const int incl = wave_incl_sum(cnt, lane);
-      if (e < n) {
-        int g = gen + incl - cnt;  // generation index of the entry's first record
-        const int qpos = pathq[e], gpos = pathh[e];
-        if (gap) {
-          const int lq = pathq[e - 1], lg = pathh[e - 1];
-          gmapdp_path_pair rr;
-          rr.querypos = rr.genomepos = -1;
-          rr.queryjump = (lq - 1 - qpos) - fill;
-          rr.genomejump = (lg - 1 - gpos) - fill;
-          rr.cdna = rr.comp = rr.genome = rr.genomealt = ' ';
-          dst[total - 1 - g++] = rr;
+      char cq[kC], cu[kC];
+#pragma unroll
+      for (int k = 0; k < kC; k++) {
+        const int e = cb + 64 * k + lane;
+        cq[k] = e < n ? qs[qp[k]] : 0;
+        cu[k] = e < n ? qu[qp[k]] : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < kC; k++) {
+        const int e = cb + 64 * k + lane;
+        int cnt = 0, fill = 0, gap = 0;
+        if (e < n) {
+          s2_entry_v(e, qp[k], gp[k], lqv[k], lgv[k], fill, gap);
+          cnt = gap + fill + 1;
         }
-        for (int k = 0; k < fill; k++) {
-          const int lq = qpos + fill - k, lg = gpos + fill - k;
-          const char c = s2_genomic_nt(blocks, nwords, (uint32_t)lg, P.chroffset, P.chrhigh, plusp);
+        const int incl = wave_incl_sum(cnt, lane);
+        if (e < n) {
+          int g = gen + incl - cnt;  // generation index of the entry's first record
+          const int qpos = qp[k], gpos = gp[k];
+          if (gap) {
+            gmapdp_path_pair rr;
+            rr.querypos = rr.genomepos = -1;
+            rr.queryjump = (lqv[k] - 1 - qpos) - fill;
+            rr.genomejump = (lgv[k] - 1 - gpos) - fill;
+            rr.cdna = rr.comp = rr.genome = rr.genomealt = ' ';
+            dst[total - 1 - g++] = rr;
+          }
+          for (int j = 0; j < fill; j++) {
+            const int lq = qpos + fill - j, lg = gpos + fill - j;
+            const char c = s2_genomic_nt(blocks, nwords, (uint32_t)lg, P.chroffset, P.chrhigh, plusp);
+            gmapdp_path_pair rr;
+            rr.querypos = lq;
+            rr.genomepos = lg;
+            rr.queryjump = rr.genomejump = 0;
+            rr.cdna = qs[lq];
+            rr.comp = '|';
+            rr.genome = rr.genomealt = c;
+            dst[total - 1 - g++] = rr;
+          }
           gmapdp_path_pair rr;
-          rr.querypos = lq;
-          rr.genomepos = lg;
+          rr.querypos = qpos;
+          rr.genomepos = gpos;
           rr.queryjump = rr.genomejump = 0;
-          rr.cdna = qs[lq];
+          rr.cdna = cq[k];
           rr.comp = '|';
-          rr.genome = rr.genomealt = c;
-          dst[total - 1 - g++] = rr;
+          rr.genome = rr.genomealt = cu[k];
+          dst[total - 1 - g] = rr;
         }
-        gmapdp_path_pair rr;
-        rr.querypos = qpos;
-        rr.genomepos = gpos;
-        rr.queryjump = rr.genomejump = 0;
-        rr.cdna = qs[qpos];
-        rr.comp = '|';
-        rr.genome = rr.genomealt = qu[qpos];
-        dst[total - 1 - g] = rr;
+        gen += __shfl(incl, 63, 64);
       }
-      gen += __shfl(incl, 63, 64);
     }
     if (lane == 0) {
       gmapdp_path pr;
