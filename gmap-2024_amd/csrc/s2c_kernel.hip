@@ -1698,7 +1698,7 @@ __global__ __launch_bounds__(64) void s2a_kernel(
 }
 
 // the lookback sweep (align_compute_scores_lookback) of the calls s2a_kernel left chained
-__global__ __launch_bounds__(64) void s2b_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void s2b_kernel(
     const DevStage2Problem* __restrict__ probs, const uint32_t* __restrict__ blocks, uint64_t nwords,
     const char* __restrict__ qseq, const char* __restrict__ quc, const gmapdp_oligo_result* __restrict__ ores,
     const int32_t* __restrict__ npos_all, const int32_t* __restrict__ map_all, const uint32_t* __restrict__ table_all,
