@@ -1773,31 +1773,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void s2
   S2_MARK(4);
 }
 
-// traceback_one over the LDS link table: link[i] = predecessor hit index (0x7fffffff: none) with bit 31
-// set when the hit has fewer than MIN_TERMINAL_NCONSECUTIVE consecutive matches; map[i] its chrpos
-constexpr int kS2cCap = 3072;  // hits whose links fit the s2c kernel's LDS (12 B each; 36 KB: 4 waves per CU)
-constexpr uint32_t kS2NoPred = 0x7fffffffu;
-// traceback_one over the LDS link table, by the whole wave: a link to the previous hit index (consecutive query positions with one
-// hit each, the common case) continues a run, so each step takes the run of up to 64 nodes from gi down
-// (one LDS read per lane, a ballot for the run's end) instead of one dependent LDS read per node.
+// traceback_one over the LDS link table, 8 B per hit: lql[i] = query position << 16 | a bit 15 set when
+// the hit has fewer than MIN_TERMINAL_NCONSECUTIVE consecutive matches | the predecessor's hit index
+// (0x7fff: none); map[i] its chrpos.  Calls with more hits or query positions past 2^16 walk the global
+// arrays instead.
+constexpr int kS2cCap = 4096;  // 32 KB: 5 waves per CU
+constexpr uint32_t kS2NoPred = 0x7fffu;
+// The walk runs on the whole wave: a link to the previous hit index (consecutive query positions with
+// one hit each, the common case) continues a run, so each step takes the run of up to 64 nodes from gi
+// down (one LDS read per lane, a ballot for the run's end) instead of one dependent LDS read per node.
 // Visited nodes (chrpos < 2^31) are numbered in walk order; pq/ph (optional) receive their query and
 // genomic positions.  Returns the count and the first and last visited nodes (wave-uniform).
 struct S2WalkOut {
   int n, top, bottom;
 };
-__device__ S2WalkOut s2_walk_wave(const uint32_t* link, const uint32_t* map, const uint32_t* lq, int gi, int lane,
-                                  int* pq, int* ph) {
+__device__ S2WalkOut s2_walk_wave(const uint32_t* lql, const uint32_t* map, int gi, int lane, int* pq, int* ph) {
   S2WalkOut o = {0, -1, -1};
-  uint32_t w = link[gi];
-  while (w & 0x80000000u) {  // prune the 3' end
+  uint32_t w = lql[gi];
+  while (w & 0x8000u) {  // prune the 3' end
     const uint32_t pr = w & kS2NoPred;
     if (pr == kS2NoPred) return o;
     gi = (int)pr;
-    w = link[gi];
+    w = lql[gi];
   }
   for (;;) {
     const int x = gi - lane;
-    const uint32_t px = (x >= 0 ? link[x] : kS2NoPred) & kS2NoPred;
+    const uint32_t wx = x >= 0 ? lql[x] : kS2NoPred;
+    const uint32_t px = wx & kS2NoPred;
     const bool cont = x >= 1 && px == (uint32_t)(x - 1);
     const uint64_t stop = ballot(!cont);
     const int r = stop ? __ffsll((long long)stop) - 1 : 63;  // lanes 0..r hold the run's nodes
@@ -1806,7 +1808,7 @@ __device__ S2WalkOut s2_walk_wave(const uint32_t* link, const uint32_t* map, con
     const uint64_t vm = ballot(vis);
     if (vis && pq) {
       const int idx = o.n + lanes_below(vm, lane);
-      pq[idx] = (int)lq[x];
+      pq[idx] = (int)(wx >> 16);
       ph[idx] = (int)mx;
     }
     if (vm) {
@@ -1929,10 +1931,9 @@ __global__ __launch_bounds__(64) void s2c_kernel(
   // ---- traceback_one per selected cell: length and extent of the converted list ----
   // the links go to LDS first (coalesced loads), so the pointer chases run at LDS latency
   extern __shared__ uint32_t s2c_lds[];
-  uint32_t* llink = s2c_lds;
+  uint32_t* llq = s2c_lds;
   uint32_t* lmap = s2c_lds + kS2cCap;
-  uint32_t* lq = s2c_lds + 2 * kS2cCap;
-  const bool lds_walk = T <= kS2cCap;
+  const bool lds_walk = T <= kS2cCap && nq <= 65536;
   if (lds_walk && npaths > 0) {
     // four hits per lane per step: their loads, then their off[] gathers, overlap
     for (int b0 = lane; b0 < T; b0 += 256) {
@@ -1959,9 +1960,8 @@ __global__ __launch_bounds__(64) void s2c_kernel(
         const int i = b0 + 64 * k;
         if (i < T) {
           const uint32_t pr = fp[k] >= 0 ? (uint32_t)(ob[k] + fh[k]) : kS2NoPred;
-          llink[i] = pr | (cs[k] < kS2MinTerminal ? 0x80000000u : 0u);
+          llq[i] = ((uint32_t)qq[k] << 16) | (cs[k] < kS2MinTerminal ? 0x8000u : 0u) | pr;
           lmap[i] = mp[k];
-          lq[i] = (uint32_t)qq[k];
         }
       }
     }
@@ -1974,7 +1974,7 @@ __global__ __launch_bounds__(64) void s2c_kernel(
     const int cell = s2_u(cand[p]);
     int n = 0, top = -1, bottom = -1;
     if (lds_walk) {
-      const S2WalkOut o = s2_walk_wave(llink, lmap, lq, cell, lane, single ? pathq : nullptr, pathh);
+      const S2WalkOut o = s2_walk_wave(llq, lmap, cell, lane, single ? pathq : nullptr, pathh);
       n = o.n;
       top = o.top;
       bottom = o.bottom;
@@ -2055,7 +2055,7 @@ __global__ __launch_bounds__(64) void s2c_kernel(
     const S2Path x = pth[pord[i]];
     const int n = x.n;
     if (!single && lds_walk) {  // entries, 3' end first
-      (void)s2_walk_wave(llink, lmap, lq, x.cell, lane, pathq, pathh);
+      (void)s2_walk_wave(llq, lmap, x.cell, lane, pathq, pathh);
     } else if (lane == 0 && !single) {
       int e = 0;
       {
@@ -2215,9 +2215,9 @@ hipError_t launch_s2c(int nproblems, hipStream_t stream, const DevStage2Problem*
     e = hipLaunchKernel(reinterpret_cast<void*>(&s2b_kernel), dim3(nproblems), dim3(64), args, 0, stream);
   if (e == hipSuccess)
     e = hipFuncSetAttribute(reinterpret_cast<void*>(&s2c_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(12 * kS2cCap));
+                            (int)(8 * kS2cCap));
   if (e == hipSuccess)
-    e = hipLaunchKernel(reinterpret_cast<void*>(&s2c_kernel), dim3(nproblems), dim3(64), args, 12 * kS2cCap, stream);
+    e = hipLaunchKernel(reinterpret_cast<void*>(&s2c_kernel), dim3(nproblems), dim3(64), args, 8 * kS2cCap, stream);
   return e;
 }
 
