@@ -1251,7 +1251,7 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
     }
     if (high - low == 1) S2_TACC(t_one); else S2_TACC(t_mult);
     if (lane == 0) W.actn[q] = nact;
-    if (npos(q) > 0) {
+    if ((q == cb + j ? n : npos(q)) > 0) {  // the prefetched count unless the MAX_SKIPPED jump moved q
       const bool ringed = high - low <= kS2Ring;
       const int start = ringed ? W.pushed : W.pushed - 2 * kS2Ring;  // never in the ring
       if (lane == 0) {
