@@ -250,12 +250,17 @@ def main():
         lstream.append(lib.gmapdp_plan_launch_stream(plan, li))
     d_s2res = torch.zeros(len(op) * 32, dtype=torch.uint8, device=dev)
 
-    # Streams: stage-2 seeding on its own stream, the DP launch classes on the engine's schedule
-    # (0 = main, 1..3 = sides, longest-processing-time first), forked from and joined into main.
-    # Real (non-null) streams, so per-launch events time exactly the launches on their stream.
+    # Streams: stage 2 on its own stream, the DP launch classes on the engine's schedule (0 = main,
+    # 1..3 = sides, longest-processing-time first), forked from and joined into main.  The process
+    # has four hardware queues (GPU_MAX_HW_QUEUES, HIP's default), so four streams: the plan's third
+    # side list joins its second (the two lightest), where the microexon plan runs too.  A fifth
+    # stream would share a queue with another and wait behind its kernels (the 14-ms genome-gap
+    # class on main, in the trace that showed it).  Real (non-null) streams, so per-launch events
+    # time exactly the launches on their stream.
     stream = torch.cuda.Stream(dev)
-    sides = [torch.cuda.Stream(dev) for _ in range(3)]
+    sides = [torch.cuda.Stream(dev) for _ in range(2)]
     ostream = torch.cuda.Stream(dev)
+    side_of = lambda k: min(k, len(sides))  # noqa: E731  plan stream k >= 1 -> side index + 1
 
     def launch(li, s):
         eng._check(lib.gmapdp_plan_run_launch(eng.h, plan, li, C.c_void_p(d_q.data_ptr()), C.c_void_p(d_q.data_ptr()),
@@ -289,7 +294,7 @@ def main():
                 ev["chain"][1].record(ostream)
         if do_dp:
             for li in range(nl):
-                k = lstream[li]
+                k = side_of(lstream[li])
                 s = stream if k == 0 else sides[k - 1]
                 if k and k not in used:
                     s.wait_event(fork)
@@ -299,11 +304,15 @@ def main():
                 launch(li, s)
                 if ev is not None:
                     ev["dp"][li][1].record(s)
+            ms = sides[-1]
+            if len(sides) not in used:
+                ms.wait_event(fork)
+                used.add(len(sides))
             if ev is not None:
-                ev["mx"][0].record(stream)
-            mrun(stream, 3)
+                ev["mx"][0].record(ms)
+            mrun(ms, 3)
             if ev is not None:
-                ev["mx"][1].record(stream)
+                ev["mx"][1].record(ms)
         for k in used:
             stream.wait_stream(sides[k - 1])
         if do_oligo:
