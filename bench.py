@@ -1,32 +1,43 @@
-"""bench.py -- MI355X GMAP hot path throughput (BASELINE.json metric on configs[2]).
+"""bench.py -- MI355X GMAP hot path throughput (BASELINE.json metric on configs[2]; configs[4] with --config 4).
 
-Workload (configs[2]: "1M synthetic 2-kb cDNA (5 exons, 2 % mismatch) vs GRCh38, 1xMI355X, full
-stage2 + all Dynprog_* paths"), gmap-2024_amd/gmapdp/workload.py:
-  * genome: an i.i.d. ACGT genome laid out as GRCh38's 24 primary chromosomes (3.09 Gnt, universal
-    coordinates past 2^31), packed in the reference's .genomecomp format and resident in HBM (1.16 GB);
-  * per 2-kb read, the calls GMAP's pipeline makes into the path: one Stage2_compute
-    call (gmap.c:1208: Oligoindex_hr_tally + Oligoindex_get_mappings over the read's gregion, then the
-    chaining -- Diag_compute_bounds, align_compute_lookback, convert_to_nucleotides,
+Workload (gmap-2024_amd/gmapdp/workload.py):
+  * configs[2] (default; "1M synthetic 2-kb cDNA (5 exons, 2 % mismatch) vs GRCh38, 1xMI355X, full stage2 +
+    all Dynprog_* paths"): an i.i.d. ACGT genome laid out as GRCh38's 24 primary chromosomes (3.09 Gnt,
+    universal coordinates past 2^31), generated directly as the reference's .genomecomp blocks and resident
+    in HBM (1.16 GB); per 2-kb read the calls GMAP's pipeline makes into the path: one
+    Stage2_compute call (gmap.c:1208: Oligoindex_hr_tally + Oligoindex_get_mappings over the read's
+    gregion, then the chaining -- Diag_compute_bounds, align_compute_lookback, convert_to_nucleotides,
     Stage2_filter_unique) and 43.7 Dynprog_single_gap + 7.1 Dynprog_end5_gap + 6.5 Dynprog_end3_gap +
-    49.4 Dynprog_genome_gap + 25.6 Dynprog_microexon_int (over genome-gap gaps; the MaxEnt scores
-    between its search and its choice are synthetic device inputs, the engine takes MaxEnt as input).
-One step = one pass of the engine over every call of --reads reads (Stage2_compute on its own
-stream, the DP launch classes on four more, joined at the end of the step); the batch is generated
-once and replayed, every step recomputes everything.  Inputs (descriptors, query arenas, splice
-probabilities) are resident in HBM before the timed region (the contract's `value`); the host plan
-(bands, launch classes) is made once per batch and its cost is reported as plan_ms.
+    49.4 Dynprog_genome_gap + 25.6 Dynprog_microexon_int;
+  * configs[4] (--config 4; gmapl, "500k 5-kb Iso-Seq-style reads vs 17-Gb wheat genome"): 5-kb reads of
+    10 exons with 1 % substitutions + 1 % indels against a 17-Gnt wheat-layout genome (6.4 GB packed,
+    universal coordinates past 2^32), the per-read call mix of that read shape (workload.ISOSEQ5K).
+The splice probabilities of the genome gaps and the MaxEnt scores between the microexon search and its
+choice are synthetic device inputs (the engine takes MaxEnt as an input).
 
-value = reads whose Stage2_compute and DP calls were processed per second, whole job (all ranks).
-Stage 1/3 orchestration stays on the host and is not in the step.  The JSON line also
-carries the stage-2-only and DP-only step times, the roofline of the kernel that takes most of the
-step, and the reference CPU baseline (tools/cpu_baseline.py: the reference's own objects on the
-host cores, AVX2 and nosimd builds).
+Read stream: blocks of --reads reads, each generated from its own seeds; rank r of N takes the blocks
+b % N == r (GMAP's --part=r/N rule, inbuffer.c:283, per block) and cycles through --batches of them, so
+consecutive steps process different reads and genomic windows (a stream, not one warm replay).  One step
+= one pass of the engine over every call of one block (Stage2_compute on its own stream, the DP launch
+classes on three more, joined at the end of the step).  Inputs (descriptors, query arenas, splice
+probabilities) are resident in HBM before the timed region (the contract's `value`); the host plans
+(bands, launch classes) are made once per block and their cost is reported as plan_ms.
+
+value = reads whose Stage2_compute and DP calls were processed per second, whole job (all ranks).  Stage
+1/3 orchestration stays on the host and is not in the step.
+
+Multi-GPU: `--gpus N` without a WORLD_SIZE in the environment starts N rank processes (this file, with
+RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set) before anything touches the GPU and exits with their
+status; under torch.distributed.run the ranks come from the environment.  One process per GPU, RCCL
+(backend nccl) for the barrier and the max-over-ranks step time only: the path has no exchange step.
+`--dry-run` runs the launcher, the process group (gloo), the block sharding and the workload generation on
+the CPU without a GPU (tests/test_bench_launcher.py).
 """
 import argparse
 import ctypes as C
 import json
 import os
-import re
+import socket
 import subprocess
 import sys
 import time
@@ -36,10 +47,26 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gmap-2024_amd"))
 
-HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
+# VALU issue: a wave64 instruction issues over 2 cycles on a SIMD-32 (MI355X_MICROARCH.md), 4 SIMDs x 256 CUs
+# at 2.4 GHz: 1.2288 T wave-instructions/s; lane-ops: 256 x 4 x 32 x 2.4 GHz = 78.6 T int32 ops/s
+VALU_WAVE_INSTR_PEAK = 256 * 4 * 2.4e9 / 2
+INT_OPS_PEAK = 256 * 4 * 32 * 2.4e9
+OPS_PER_CELL = 11                # E 3 + F 3 + H 4 + clamp 1 integer ops per banded cell
 METRIC = "aligned cDNA reads/sec (2 kb, GRCh38) at 1/2/4/8 MI355X; DP HBM GB/s vs peak"
+T_START = time.perf_counter()
 
 
+def progress(msg):
+    """a progress line on stderr (stdout carries only the result line)"""
+    r = os.environ.get("RANK")
+    print("[bench%s %.0fs] %s" % ("" if r is None else " r" + r, time.perf_counter() - T_START, msg),
+          file=sys.stderr, flush=True)
+
+
+# ---------------------------------------------------------------------------------------------------
+# algorithmic bytes and cells (DESIGN.md §6)
+# ---------------------------------------------------------------------------------------------------
 def algorithmic_bytes(rlength, glength, npairs, desc_bytes):
     """Dynprog_single_gap / _end{5,3}_gap: descriptor + query and upper-cased query (2 x rlength) +
     packed genome blocks covering the segment (12 B per 32 nt) + result (32 B) + one 16-B Pair
@@ -60,17 +87,6 @@ def genome_algorithmic_bytes(gp, npairs):
                + 16 * int(np.asarray(npairs).sum()))
 
 
-def stage2_algorithmic_bytes(op, res):
-    """Stage-2 seeding per call: descriptor (40 B) + the query (1 B/nt) + the window's packed genome
-    (12 B per 32 nt) + npositions and mappings (8 B per query position) + the table (4 B per stored
-    position) + the result (32 B) + the diagonal records (16 B each)."""
-    w = (op["chrend"].astype(np.int64) - op["chrstart"].astype(np.int64))
-    ql = op["querylength"].astype(np.int64)
-    return int((40 + ql + 12 * ((w + 31) // 32) + 8 * ql + 32).sum()
-               + 4 * int(res["totalpositions"].astype(np.int64).sum())
-               + 16 * int(res["ndiagonals"].astype(np.int64).sum()))
-
-
 def chain_algorithmic_bytes(op, s2res):
     """Stage-2 chaining per call (s2c_kernel): descriptor (48 B) + seeding result (32 B) + npositions
     and mappings (8 B per query position) + the query twice (cdna and upper case, 2 B per query
@@ -82,26 +98,50 @@ def chain_algorithmic_bytes(op, s2res):
                + 20 * int(s2res["npairs"].sum()))
 
 
-def banded_cells(sp, ep, gp):
-    """Banded DP cells of the fills (wide band for single/GAP/BEST_LOCAL, narrow for INDELS; two
-    fills per genome gap, band W = 8 + 2 x 14 + 1)."""
-    r = sp["rlength"].astype(np.int64)
-    g = sp["glength"].astype(np.int64)
-    cells = int(np.minimum(np.abs(g - r) + 2 * sp["extraband"].astype(np.int64) + 1, r + 1).dot(g))
+def band_cells(rlength, glength, lband, uband):
+    """Cells of a banded fill: sum over columns c = 1..glength of |[max(1, c - uband), min(rlength,
+    c + lband)]| (dynprog.c:1411-1449 row range), per problem."""
+    R = np.asarray(rlength, dtype=np.int64)
+    G = np.asarray(glength, dtype=np.int64)
+    lo, up = np.asarray(lband, dtype=np.int64), np.asarray(uband, dtype=np.int64)
+    tot = np.zeros(len(R), dtype=np.int64)
+    for c in range(1, int(G.max(initial=0)) + 1):
+        live = G >= c
+        tot += np.where(live, np.maximum(0, np.minimum(R, c + lo) - np.maximum(1, c - up) + 1), 0)
+    return tot
+
+
+def dp_cells(sp, ep, gp, g_fills):
+    """Banded DP cells of the step: single gaps (wide band), end gaps (wide band, INDELS narrow, NOGAPS
+    none), two fills per genome gap where `g_fills` (False where genome_gap_simple answered)."""
+    r, g = sp["rlength"].astype(np.int64), sp["glength"].astype(np.int64)
+    eb = sp["extraband"].astype(np.int64)
+    cells = int(np.minimum(np.abs(g - r) + 2 * eb + 1, r + 1).dot(g))
     r = np.minimum(ep["rlength"].astype(np.int64), 660)
     g = np.minimum(ep["glength"].astype(np.int64), 2000)
     eb = ep["extraband"].astype(np.int64)
     W = np.where(ep["endalign"] == 1, 2 * eb + 1, np.abs(g - r) + 2 * eb + 1)
     W = np.where(ep["endalign"] == 2, 0, W)
     cells += int(np.minimum(W, r + 1).dot(g))
-    gr = gp["rlength"].astype(np.int64)
-    return cells + int((2 * np.minimum(8 + 2 * 14 + 1, gr + 1) * (gr + 8)).sum())
+    return cells + int(genome_cells(gp, g_fills).sum())
 
 
-def pmc_traffic(key):
-    """HBM bytes per dispatch of the kernel `key` (rocprofv3 name) from the newest committed PMC
-    summary (profiles/*/pmc_summary.json: 2 x FETCH_SIZE + WRITE_SIZE of the same bench command, the
-    gfx950 correction of MI355X_MICROARCH.md), or (None, None)."""
+def genome_cells(gp, g_fills):
+    """Cells of the two fills of each genome gap (L: lbandL, ubandL; R: lbandL, ubandR, as
+    dynprog_genome.c:3801-3813 calls them), zero where genome_gap_simple answered."""
+    r = gp["rlength"].astype(np.int64)
+    eb = gp["extraband"].astype(np.int64)
+    gL, gR = gp["glengthL"].astype(np.int64), gp["glengthR"].astype(np.int64)
+    c = band_cells(r, gL, eb, gL - r + eb) + band_cells(r, gR, eb, gR - r + eb)
+    return np.where(g_fills, c, 0)
+
+
+# ---------------------------------------------------------------------------------------------------
+# committed profiles (profiles/*): PMC traffic, VALU instructions, rocprof average duration
+# ---------------------------------------------------------------------------------------------------
+def pmc_entry(key):
+    """The newest committed PMC summary's record of kernel `key` ('+'-joined names are summed), or
+    (None, None)."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")), reverse=True):
         try:
@@ -110,7 +150,11 @@ def pmc_traffic(key):
             continue
         parts = key.split("+")
         if all(p in ks for p in parts):
-            return sum(ks[p]["hbm_bytes_per_dispatch"] for p in parts), os.path.relpath(path, ROOT)
+            rec = {}
+            for f in ("hbm_bytes_per_dispatch", "sq_SQ_INSTS_VALU_sum_avg", "avg_duration_ns"):
+                vals = [ks[p].get(f) for p in parts]
+                rec[f] = None if any(v is None for v in vals) else sum(vals)
+            return rec, os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -123,6 +167,12 @@ def rocprof_name(kind, R, dl, lds=0):
         return "gmapdp::dp_kernel<%d, %s>" % (R, "true" if dl else "false")
     if kind == 2:  # dpx_kernel<S, GD>: GD = direction words in global scratch
         return "gmapdp::dpx_kernel<%d, %s>" % (R, "false" if dl else "true")
+    if kind == 3:
+        return "gmapdp::sx_kernel<%d>" % R
+    if kind == 4:
+        return "gmapdp::uxe_kernel<%d>" % R
+    if kind == 5:
+        return "gmapdp::uxg_kernel<%d>" % R
     return "gmapdp::gg_kernel<%d, %s>" % (R, "true" if dl else "false")
 
 
@@ -141,12 +191,91 @@ def cpu_baselines():
     return out
 
 
-def progress(msg):
-    """a progress line on stderr (stdout carries only the result line)"""
-    print("[bench %.0fs] %s" % (time.perf_counter() - T_START, msg), file=sys.stderr, flush=True)
+# ---------------------------------------------------------------------------------------------------
+# launcher: N rank processes, started before anything touches the GPU
+# ---------------------------------------------------------------------------------------------------
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
-T_START = time.perf_counter()
+def launch_ranks(n):
+    """Start n copies of this script as ranks 0..n-1 (torchrun's environment contract, rendezvous on
+    127.0.0.1), wait for them, and return the first nonzero exit status (0 when all succeed).  A rank
+    that fails ends the others (their exact PIDs)."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
+# ---------------------------------------------------------------------------------------------------
+# one rank
+# ---------------------------------------------------------------------------------------------------
+def config_of(args):
+    from gmapdp import workload as W
+    if args.config == 4:
+        return W.Layout(W.WHEAT17), W.ISOSEQ5K, "wheat17"
+    if args.genome == "chr22":
+        return W.Layout(W.CHR22), W.CDNA2K, "chr22"
+    return W.Layout(W.GRCH38), W.CDNA2K, "grch38"
+
+
+def make_stream(args, rank, world):
+    """genome (planted for the whole stream) + this rank's blocks; no GPU work"""
+    from gmapdp import workload as W
+    from gmapdp import shard
+    layout, shape, gname = config_of(args)
+    mine = shard.blocks_of_rank(rank, world, args.batches)
+    t0 = time.perf_counter()
+    genome = W.PackedGenome(layout.total, seed=38)
+    W.plant_stream(genome, layout, args.reads, range(world * args.batches), shape)
+    workers = int(os.environ.get("GMAPDP_BENCH_WORKERS", "0")) or max(1, min(args.batches, 16 // world))
+    data = W.make_blocks(genome, layout, args.reads, mine, shape=shape, sprob=False, workers=workers)
+    progress("genome (%s, %d nt) and %d blocks of %d reads ready (%.0f s, %d workers)"
+             % (gname, layout.total, len(mine), args.reads, time.perf_counter() - t0, workers))
+    return layout, shape, gname, genome, mine, data, time.perf_counter() - t0
+
+
+def dry_run(args, rank, world):
+    """The launcher / process group / sharding / generation path without a GPU (gloo)."""
+    import torch
+    import torch.distributed as dist
+    from gmapdp import shard
+    layout, shape, gname, genome, mine, data, t_gen = make_stream(args, rank, world)
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")
+    digest = shard.genome_digest(genome.blocks[::4097])
+    rec = shard.gather_blocks(mine, [int(d["reads"]) for d in data], dist if world > 1 else None)
+    if world > 1:
+        shard.check_replicated(digest, dist)
+    rank_line = {"rank": rank, "world_size": dist.get_world_size() if world > 1 else 1,
+                 "backend": dist.get_backend() if world > 1 else None, "blocks": mine,
+                 "stage2_calls": [int(len(d["oligo"])) for d in data]}
+    print(json.dumps({"rank_line": rank_line}), file=sys.stderr, flush=True)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "config": gname, "shard": rec,
+                          "genome_digest": digest.hex(), "setup_s": t_gen}))
+    if world > 1:
+        dist.destroy_process_group()
+    _ = torch
 
 
 def main():
@@ -154,131 +283,149 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--reads", type=int, default=10000, help="reads per step per GPU")
-    ap.add_argument("--genome", default="grch38", choices=["grch38", "chr22"])
+    ap.add_argument("--reads", type=int, default=10000, help="reads per step per GPU (one block)")
+    ap.add_argument("--batches", type=int, default=8, help="distinct read blocks per rank, cycled over the steps")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 4], help="BASELINE.json configs index")
+    ap.add_argument("--genome", default="grch38", choices=["grch38", "chr22"], help="configs[2] genome layout")
+    ap.add_argument("--simd", action="store_true", help="the SIMD builds' semantics (gmap.avx2: sx/uxe/uxg kernels)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dry-run", action="store_true", help="CPU only: launcher, gloo process group, sharding")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and "WORLD_SIZE" in os.environ and args.gpus != 1:
+        raise SystemExit("bench: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    if args.dry_run:
+        return dry_run(args, rank, world)
+
+    # ---- workload first (forked generator workers must not inherit a GPU context) ----
+    layout, shape, gname, genome, mine, data, t_gen = make_stream(args, rank, world)
 
     import torch
     import torch.distributed as dist
     import gmapdp
-    from gmapdp import workload as W
+    from gmapdp import shard
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-
-    t_gen = time.perf_counter()
-    layout = W.Layout(W.GRCH38 if args.genome == "grch38" else W.CHR22)
-    genome = W.make_genome(layout, seed=38)
-    # every rank plants the same intron sites (site seeds depend on the rank-independent seed below)
-    # and cuts its own reads (--part=rank/world share of the read stream: weak scaling)
-    data = W.make_reads(genome, layout, args.reads, seed=1000 + 10 * rank)
-    eng = gmapdp.Engine(local)
-    nw = eng.lib.gmapdp_genome_words(layout.total)
-    blocks = np.zeros(nw, dtype=np.uint32)
-    eng._check(eng.lib.gmapdp_pack_genome(C.cast(genome.ctypes.data, C.c_char_p), layout.total, blocks.ctypes.data), "gmapdp_pack_genome")
     if world > 1:
-        from gmapdp import shard
-        shard.check_replicated(shard.genome_digest(blocks[::4097]), dist)
-    eng.set_genome(blocks=blocks, length=layout.total)
-    del blocks, genome
-    t_gen = time.perf_counter() - t_gen
-    progress("genome and reads ready (%.0f s)" % t_gen)
+        dist.init_process_group("nccl", init_method="env://", device_id=dev)
+    eng = gmapdp.Engine(local)
+    if world > 1:
+        shard.check_replicated(shard.genome_digest(genome.blocks[::4097]), dist)
+    eng.set_genome(blocks=genome.blocks, length=genome.length)
+    del genome
     lib = eng.lib
-    sp, ep, gp, op = data["single"], data["end"], data["genome"], data["oligo"]
-    ns, ne, ng = len(sp), len(ep), len(gp)
-    nprob = ns + ne
-    d_q = torch.from_numpy(data["q"]).to(dev)
-    d_sprob = torch.from_numpy(data["sprob"]).to(dev)
-    d_oq = torch.from_numpy(data["oq"]).to(dev)
-
-    # ---- plans (host: bands, launch classes, offsets; descriptors uploaded) ----
-    t0 = time.perf_counter()
-    host_res = np.zeros(nprob, dtype=gmapdp.RESULT_DTYPE)
-    host_gres = np.zeros(max(ng, 1), dtype=gmapdp.GENOME_RESULT_DTYPE)
-    plan = C.c_void_p()
-    eng._check(lib.gmapdp_plan_create_all(eng.h, sp.ctypes.data, ns, ep.ctypes.data, ne, gp.ctypes.data, ng,
-                                          host_res.ctypes.data, host_gres.ctypes.data, C.byref(plan)),
-               "gmapdp_plan_create_all")
-    t_plan = time.perf_counter() - t0
-    # Stage2_compute per read (gmap.c:1208): seeding + chaining, GMAP's defaults (splicing on,
-    # maxintronlen 500000)
-    s2p = np.zeros(len(op), dtype=gmapdp.STAGE2_PROBLEM_DTYPE)
-    for k in ("qoff", "querylength", "chrstart", "chrend", "chroffset", "chrhigh", "plusp"):
-        s2p[k] = op[k]
-    s2p["splicingp"] = 1
-    s2p["maxintronlen"] = 500000
-    t0 = time.perf_counter()
-    oplan = C.c_void_p()
-    eng._check(lib.gmapdp_stage2_plan_create(eng.h, s2p.ctypes.data, len(s2p), data["oq"].ctypes.data,
-                                             data["oq"].ctypes.data, len(data["oq"]), C.byref(oplan)),
-               "gmapdp_stage2_plan_create")
-    t_oplan = time.perf_counter() - t0
-    # Dynprog_microexon_int per read (stage3.c:9664) over genome-gap gaps: search + choice; the MaxEnt
-    # probabilities between them are synthetic device inputs (the engine takes MaxEnt as an input)
-    mp = data["microexon"]
-    mplan = C.c_void_p()
-    eng._check(lib.gmapdp_microexon_plan_create(eng.h, mp.ctypes.data, len(mp), data["q"].ctypes.data,
-                                                data["q"].ctypes.data, len(data["q"]), C.byref(mplan)),
-               "gmapdp_microexon_plan_create")
-    ncands = lib.gmapdp_microexon_plan_candidates(mplan)
-    d_mres = torch.zeros(max(len(mp), 1) * gmapdp.MICROEXON_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-    d_mpairs = torch.empty(max(lib.gmapdp_microexon_plan_pair_capacity(mplan), 1) * 16, dtype=torch.uint8,
-                           device=dev)
     gen = torch.Generator(device=dev)
-    gen.manual_seed(77)
-    d_mxp = torch.rand(max(2 * ncands, 2), dtype=torch.float64, device=dev, generator=gen)
-    ngpu, nggpu = lib.gmapdp_plan_gpu_problems(plan), lib.gmapdp_plan_genome_gpu_problems(plan)
-    cap = lib.gmapdp_plan_pair_capacity(plan)
-    d_res = torch.zeros(max(ngpu, 1) * 32, dtype=torch.uint8, device=dev)
-    d_gres = torch.zeros(max(nggpu, 1) * 72, dtype=torch.uint8, device=dev)
-    d_pairs = torch.empty(max(cap, 1) * 16, dtype=torch.uint8, device=dev)
-    eng._check(lib.gmapdp_plan_bind_genome(plan, C.c_void_p(d_sprob.data_ptr()), C.c_void_p(d_gres.data_ptr())),
-               "gmapdp_plan_bind_genome")
-    nl = lib.gmapdp_plan_nlaunches(plan)
-    info, kinds, lstream = [], [], []
-    for li in range(nl):
-        R, dl, cnt, lds = C.c_int(), C.c_int(), C.c_int(), C.c_size_t()
-        lib.gmapdp_plan_launch_info(plan, li, C.byref(R), C.byref(dl), C.byref(cnt), C.byref(lds))
-        info.append((R.value, dl.value, cnt.value, lds.value))
-        kinds.append(lib.gmapdp_plan_launch_kind(plan, li))
-        lstream.append(lib.gmapdp_plan_launch_stream(plan, li))
-    d_s2res = torch.zeros(len(op) * 32, dtype=torch.uint8, device=dev)
+
+    # ---- per block: device arenas and plans (host: bands, launch classes, offsets) ----
+    B = []
+    t_plan = t_oplan = 0.0
+    for bi, d in zip(mine, data):
+        sp, ep, gp, op, mp = d["single"], d["end"], d["genome"], d["oligo"], d["microexon"]
+        if args.simd:
+            sp["flags"] |= gmapdp.SIMD
+            ep["flags"] |= gmapdp.SIMD
+            gp["flags"] |= gmapdp.SIMD
+        blk = {"id": bi, "d": d, "ns": len(sp), "ne": len(ep), "ng": len(gp)}
+        blk["d_q"] = torch.from_numpy(d["q"]).to(dev)
+        blk["d_oq"] = torch.from_numpy(d["oq"]).to(dev)
+        gen.manual_seed(5000 + bi)
+        sprob = torch.rand(max(d["sprob_len"], 1), dtype=torch.float64, device=dev, generator=gen) * 0.3
+        sprob[torch.from_numpy(d["sprob_hi"]).to(dev)] = 0.95
+        blk["d_sprob"] = sprob
+        nprob = len(sp) + len(ep)
+        blk["host_res"] = np.zeros(nprob, dtype=gmapdp.RESULT_DTYPE)
+        blk["host_gres"] = np.zeros(max(len(gp), 1), dtype=gmapdp.GENOME_RESULT_DTYPE)
+        t0 = time.perf_counter()
+        plan = C.c_void_p()
+        eng._check(lib.gmapdp_plan_create_all(eng.h, sp.ctypes.data, len(sp), ep.ctypes.data, len(ep),
+                                              gp.ctypes.data, len(gp), blk["host_res"].ctypes.data,
+                                              blk["host_gres"].ctypes.data, C.byref(plan)), "gmapdp_plan_create_all")
+        t_plan += time.perf_counter() - t0
+        blk["plan"] = plan
+        # Stage2_compute per read (gmap.c:1208): seeding + chaining, GMAP's defaults (splicing on,
+        # maxintronlen 500000)
+        s2p = np.zeros(len(op), dtype=gmapdp.STAGE2_PROBLEM_DTYPE)
+        for k in ("qoff", "querylength", "chrstart", "chrend", "chroffset", "chrhigh", "plusp"):
+            s2p[k] = op[k]
+        s2p["splicingp"] = 1
+        s2p["maxintronlen"] = 500000
+        t0 = time.perf_counter()
+        oplan = C.c_void_p()
+        eng._check(lib.gmapdp_stage2_plan_create(eng.h, s2p.ctypes.data, len(s2p), d["oq"].ctypes.data,
+                                                 d["oq"].ctypes.data, len(d["oq"]), C.byref(oplan)),
+                   "gmapdp_stage2_plan_create")
+        t_oplan += time.perf_counter() - t0
+        blk["oplan"] = oplan
+        # Dynprog_microexon_int per read (stage3.c:9664) over genome-gap gaps: search + choice
+        mplan = C.c_void_p()
+        eng._check(lib.gmapdp_microexon_plan_create(eng.h, mp.ctypes.data, len(mp), d["q"].ctypes.data,
+                                                    d["q"].ctypes.data, len(d["q"]), C.byref(mplan)),
+                   "gmapdp_microexon_plan_create")
+        blk["mplan"] = mplan
+        blk["ncands"] = lib.gmapdp_microexon_plan_candidates(mplan)
+        gen.manual_seed(7700 + bi)
+        blk["d_mxp"] = torch.rand(max(2 * blk["ncands"], 2), dtype=torch.float64, device=dev, generator=gen)
+        blk["ngpu"], blk["nggpu"] = lib.gmapdp_plan_gpu_problems(plan), lib.gmapdp_plan_genome_gpu_problems(plan)
+        blk["cap"] = lib.gmapdp_plan_pair_capacity(plan)
+        blk["mcap"] = lib.gmapdp_microexon_plan_pair_capacity(mplan)
+        nl = lib.gmapdp_plan_nlaunches(plan)
+        blk["info"], blk["kinds"], blk["lstream"] = [], [], []
+        for li in range(nl):
+            R, dl, cnt, lds = C.c_int(), C.c_int(), C.c_int(), C.c_size_t()
+            lib.gmapdp_plan_launch_info(plan, li, C.byref(R), C.byref(dl), C.byref(cnt), C.byref(lds))
+            blk["info"].append((R.value, dl.value, cnt.value, lds.value))
+            blk["kinds"].append(lib.gmapdp_plan_launch_kind(plan, li))
+            blk["lstream"].append(lib.gmapdp_plan_launch_stream(plan, li))
+        blk["names"] = [rocprof_name(blk["kinds"][li], *blk["info"][li][:2], blk["info"][li][3]) for li in range(nl)]
+        B.append(blk)
+    # outputs shared by the blocks (the steps are serialised: each forks from and joins into `stream`)
+    mx = lambda k: max(b[k] for b in B)  # noqa: E731
+    d_res = torch.zeros(max(mx("ngpu"), 1) * 32, dtype=torch.uint8, device=dev)
+    d_gres = torch.zeros(max(mx("nggpu"), 1) * 72, dtype=torch.uint8, device=dev)
+    d_pairs = torch.empty(max(mx("cap"), 1) * 16, dtype=torch.uint8, device=dev)
+    d_s2res = torch.zeros(args.reads * 32, dtype=torch.uint8, device=dev)
+    d_mres = torch.zeros(max(max(len(b["d"]["microexon"]) for b in B), 1) * gmapdp.MICROEXON_RESULT_DTYPE.itemsize,
+                         dtype=torch.uint8, device=dev)
+    d_mpairs = torch.empty(max(mx("mcap"), 1) * 16, dtype=torch.uint8, device=dev)
+    for b in B:
+        eng._check(lib.gmapdp_plan_bind_genome(b["plan"], C.c_void_p(b["d_sprob"].data_ptr()),
+                                               C.c_void_p(d_gres.data_ptr())), "gmapdp_plan_bind_genome")
+    progress("plans ready (%d blocks, %.2f s DP plans, %.2f s stage-2 plans)" % (len(B), t_plan, t_oplan))
 
     # Streams: stage 2 on its own stream, the DP launch classes on the engine's schedule (0 = main,
     # 1..3 = sides, longest-processing-time first), forked from and joined into main.  The process
     # has four hardware queues (GPU_MAX_HW_QUEUES, HIP's default), so four streams: the plan's third
-    # side list joins its second (the two lightest), where the microexon plan runs too.  A fifth
-    # stream would share a queue with another and wait behind its kernels (the 14-ms genome-gap
-    # class on main, in the trace that showed it).  Real (non-null) streams, so per-launch events
-    # time exactly the launches on their stream.
+    # side list joins its second (the two lightest), where the microexon plan runs too.  Real
+    # (non-null) streams, so per-launch events time exactly the launches on their stream.
     stream = torch.cuda.Stream(dev)
     sides = [torch.cuda.Stream(dev) for _ in range(2)]
     ostream = torch.cuda.Stream(dev)
     side_of = lambda k: min(k, len(sides))  # noqa: E731  plan stream k >= 1 -> side index + 1
 
-    def launch(li, s):
-        eng._check(lib.gmapdp_plan_run_launch(eng.h, plan, li, C.c_void_p(d_q.data_ptr()), C.c_void_p(d_q.data_ptr()),
-                                              C.c_void_p(d_res.data_ptr()), C.c_void_p(d_pairs.data_ptr()),
-                                              C.c_void_p(s.cuda_stream)), "gmapdp_plan_run_launch")
+    def launch(b, li, s):
+        eng._check(lib.gmapdp_plan_run_launch(eng.h, b["plan"], li, C.c_void_p(b["d_q"].data_ptr()),
+                                              C.c_void_p(b["d_q"].data_ptr()), C.c_void_p(d_res.data_ptr()),
+                                              C.c_void_p(d_pairs.data_ptr()), C.c_void_p(s.cuda_stream)),
+                   "gmapdp_plan_run_launch")
 
-    def orun(s, what):
-        eng._check(lib.gmapdp_stage2_plan_run(eng.h, oplan, C.c_void_p(d_oq.data_ptr()), C.c_void_p(d_oq.data_ptr()),
-                                              C.c_void_p(d_s2res.data_ptr()), what, C.c_void_p(s.cuda_stream)),
-                   "gmapdp_stage2_plan_run")
+    def orun(b, s, what):
+        eng._check(lib.gmapdp_stage2_plan_run(eng.h, b["oplan"], C.c_void_p(b["d_oq"].data_ptr()),
+                                              C.c_void_p(b["d_oq"].data_ptr()), C.c_void_p(d_s2res.data_ptr()),
+                                              what, C.c_void_p(s.cuda_stream)), "gmapdp_stage2_plan_run")
 
-    def mrun(s, what):
-        eng._check(lib.gmapdp_microexon_plan_run(eng.h, mplan, C.c_void_p(d_q.data_ptr()), C.c_void_p(d_q.data_ptr()),
-                                                 C.c_void_p(d_mxp.data_ptr()), C.c_void_p(d_mres.data_ptr()),
-                                                 C.c_void_p(d_mpairs.data_ptr()), what, C.c_void_p(s.cuda_stream)),
-                   "gmapdp_microexon_plan_run")
+    def mrun(b, s, what):
+        eng._check(lib.gmapdp_microexon_plan_run(eng.h, b["mplan"], C.c_void_p(b["d_q"].data_ptr()),
+                                                 C.c_void_p(b["d_q"].data_ptr()), C.c_void_p(b["d_mxp"].data_ptr()),
+                                                 C.c_void_p(d_mres.data_ptr()), C.c_void_p(d_mpairs.data_ptr()),
+                                                 what, C.c_void_p(s.cuda_stream)), "gmapdp_microexon_plan_run")
 
-    def step(do_oligo=True, do_dp=True, ev=None):
+    def step(b, do_oligo=True, do_dp=True, ev=None):
         fork = torch.cuda.Event()
         fork.record(stream)
         used = set()
@@ -286,22 +433,22 @@ def main():
             ostream.wait_event(fork)
             if ev is not None:
                 ev["oligo"][0].record(ostream)
-            orun(ostream, 1)
+            orun(b, ostream, 1)
             if ev is not None:
                 ev["oligo"][1].record(ostream)
-            orun(ostream, 2)
+            orun(b, ostream, 2)
             if ev is not None:
                 ev["chain"][1].record(ostream)
         if do_dp:
-            for li in range(nl):
-                k = side_of(lstream[li])
+            for li in range(len(b["names"])):
+                k = side_of(b["lstream"][li])
                 s = stream if k == 0 else sides[k - 1]
                 if k and k not in used:
                     s.wait_event(fork)
                     used.add(k)
                 if ev is not None:
                     ev["dp"][li][0].record(s)
-                launch(li, s)
+                launch(b, li, s)
                 if ev is not None:
                     ev["dp"][li][1].record(s)
             ms = sides[-1]
@@ -310,7 +457,7 @@ def main():
                 used.add(len(sides))
             if ev is not None:
                 ev["mx"][0].record(ms)
-            mrun(ms, 3)
+            mrun(b, ms, 3)
             if ev is not None:
                 ev["mx"][1].record(ms)
         for k in used:
@@ -318,89 +465,151 @@ def main():
         if do_oligo:
             stream.wait_stream(ostream)
 
+    mk = lambda: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))  # noqa: E731
+
     def timed(steps, warmup, **kw):
-        mk = lambda: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))  # noqa: E731
         with torch.cuda.stream(stream):
-            for _ in range(warmup):
-                step(**kw)
+            for k in range(warmup):
+                step(B[k % len(B)], **kw)
             torch.cuda.synchronize()
-            evs = [{"oligo": mk(), "chain": mk(), "mx": mk(), "dp": [mk() for _ in range(nl)]} for _ in range(steps)]
+            evs = [{"oligo": mk(), "chain": mk(), "mx": mk(), "dp": [mk() for _ in B[k % len(B)]["names"]]}
+                   for k in range(steps)]
             if world > 1:
                 dist.barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for k in range(steps):
-                step(ev=evs[k], **kw)
+                step(B[k % len(B)], ev=evs[k], **kw)
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
             elapsed = time.perf_counter() - t0
         if world > 1:
-            from gmapdp import shard
             elapsed = shard.max_over_ranks(elapsed, dist, device=dev)
-        dp_ms = [sum(e["dp"][li][0].elapsed_time(e["dp"][li][1]) for e in evs) / steps for li in range(nl)] \
-            if kw.get("do_dp", True) else None
-        o_ms = sum(e["oligo"][0].elapsed_time(e["oligo"][1]) for e in evs) / steps if kw.get("do_oligo", True) else None
-        c_ms = sum(e["oligo"][1].elapsed_time(e["chain"][1]) for e in evs) / steps if kw.get("do_oligo", True) else None
-        m_ms = sum(e["mx"][0].elapsed_time(e["mx"][1]) for e in evs) / steps if kw.get("do_dp", True) else None
-        return elapsed, dp_ms, (o_ms, c_ms, m_ms)
+        return elapsed, evs
 
-    # ---- headline: stage-2 seeding + every Dynprog_* call of the batch ----
-    progress("plans ready; timing %d steps" % args.steps)
-    elapsed, launch_ms, (oligo_ms, chain_ms, mx_ms) = timed(args.steps, args.warmup)
+    # every block once before anything is timed: the context's grow-only scratch reaches its size
+    with torch.cuda.stream(stream):
+        for b in B:
+            step(b)
+    torch.cuda.synchronize()
+
+    # ---- headline: Stage2_compute + every Dynprog_* call of a block per step ----
+    progress("timing %d steps over %d blocks" % (args.steps, len(B)))
+    elapsed, evs = timed(args.steps, args.warmup)
     progress("headline %.2f ms per step" % (elapsed / args.steps * 1e3))
-    # split of the same step (fewer steps): each half alone
     half = max(2, args.steps // 4)
-    el_dp, _, _ = timed(half, 1, do_oligo=False)
-    el_o, _, _ = timed(half, 1, do_dp=False)
+    el_dp, _ = timed(half, 1, do_oligo=False)
+    el_o, _ = timed(half, 1, do_dp=False)
 
-    # ---- outputs: spot check, per-dispatch algorithmic bytes ----
-    res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=gmapdp.RESULT_DTYPE)[:ngpu]
-    gres = np.frombuffer(d_gres.cpu().numpy().tobytes(), dtype=gmapdp.GENOME_RESULT_DTYPE)[:nggpu]
-    s2res = np.frombuffer(d_s2res.cpu().numpy().tobytes(), dtype=gmapdp.STAGE2_RESULT_DTYPE)
-    pp_, qp_, cp_, sb_ = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_size_t()
-    lib.gmapdp_stage2_plan_outputs(oplan, C.byref(pp_), C.byref(qp_), C.byref(cp_), C.byref(sb_))
+    # ---- per-launch times of the timed steps, by kernel template ----
+    per_kernel = {}   # name -> [ms total, dispatches, algorithmic bytes total]
 
-    dev_index = np.array([lib.gmapdp_plan_dev_index(plan, i) for i in range(nprob)])
-    gdev_index = np.array([lib.gmapdp_plan_genome_dev_index(plan, j) for j in range(ng)])
-    npairs = np.zeros(nprob, dtype=np.int64)
-    npairs[dev_index >= 0] = res["npairs"][dev_index[dev_index >= 0]]
-    gnp = np.zeros(ng, dtype=np.int64)
-    gnp[gdev_index >= 0] = gres["npairs"][gdev_index[gdev_index >= 0]]
-    rl = np.concatenate([sp["rlength"], np.minimum(ep["rlength"], 660)]).astype(np.int64)
-    gl = np.concatenate([sp["glength"], np.minimum(ep["glength"], 2000)]).astype(np.int64)
-    desc = np.concatenate([np.full(ns, gmapdp.PROBLEM_DTYPE.itemsize), np.full(ne, gmapdp.END_PROBLEM_DTYPE.itemsize)])
-    disp = []   # (rocprof name, algorithmic bytes, ms per launch, problems)
-    for li in range(nl):
-        m = np.zeros(info[li][2], dtype=np.int32)
-        lib.gmapdp_plan_launch_members(plan, li, m.ctypes.data)
-        name = rocprof_name(kinds[li], info[li][0], info[li][1], info[li][3])
-        if kinds[li] in (0, 2):
-            nbytes = algorithmic_bytes(rl[m], gl[m], npairs[m], desc[m])
-        else:
-            j = m - nprob
-            nbytes = genome_algorithmic_bytes(gp[j], gnp[j])
-        disp.append((name, nbytes, launch_ms[li], info[li][2]))
-    disp.append(("gmapdp::oi_kernel<unsigned short>+gmapdp::oi_map_kernel", None, oligo_ms, len(op)))
-    cbytes = chain_algorithmic_bytes(op, s2res)
-    disp.append(("gmapdp::s2c_kernel", cbytes, chain_ms, len(op)))
-    disp.append(("gmapdp::mx_search_kernel+gmapdp::mx_finish_kernel", None, mx_ms, len(mp)))
-    mres = np.frombuffer(d_mres.cpu().numpy().tobytes(), dtype=gmapdp.MICROEXON_RESULT_DTYPE)
-    # the kernel template with the most time per step
-    tot = {}
-    for name, nb, ms, _ in disp:
-        if nb is not None:
-            tot[name] = tot.get(name, 0.0) + ms
-    dominant = max(tot, key=tot.get)
-    sel = [d for d in disp if d[0] == dominant]
-    kms = sum(d[2] for d in sel) / len(sel)
-    kbytes = sum(d[1] for d in sel) / len(sel)
+    def add(name, ms, nbytes, n=1):
+        e = per_kernel.setdefault(name, [0.0, 0, 0])
+        e[0] += ms
+        e[1] += n
+        e[2] += nbytes if nbytes is not None else 0
+
+    # outputs and algorithmic bytes per launch class, per block (each block's outputs: re-run it once)
+    checks = {"pairs": 0, "genome_gaps_bridged": 0, "genome_gap_simple": 0, "stage2_chained": 0, "stage2_results": 0,
+              "stage2_path_pairs": 0, "microexon_candidates": 0, "microexons_found": 0, "reads": 0}
+    cells_total = 0
+    for b in B:
+        with torch.cuda.stream(stream):
+            step(b)
+        torch.cuda.synchronize()
+        d = b["d"]
+        sp, ep, gp, op, mp = d["single"], d["end"], d["genome"], d["oligo"], d["microexon"]
+        ns, ne, ng = b["ns"], b["ne"], b["ng"]
+        res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=gmapdp.RESULT_DTYPE)[:b["ngpu"]]
+        gres = np.frombuffer(d_gres.cpu().numpy().tobytes(), dtype=gmapdp.GENOME_RESULT_DTYPE)[:b["nggpu"]]
+        s2res = np.frombuffer(d_s2res.cpu().numpy().tobytes(), dtype=gmapdp.STAGE2_RESULT_DTYPE)[:len(op)]
+        mres = np.frombuffer(d_mres.cpu().numpy().tobytes(), dtype=gmapdp.MICROEXON_RESULT_DTYPE)[:len(mp)]
+        # size-independent invariants of the step's outputs (the oracle parity of this same workload is
+        # tests/test_gpu_bench_workload.py)
+        assert np.all(res["npairs"] >= 0) and np.all(gres["npairs"] >= 0) and np.all(s2res["status"] >= 0)
+        assert np.all(mres["ncandidates"] >= 0) and np.all(mres["cand_offset"] >= 0)
+        nprob = ns + ne
+        dev_index = np.array([lib.gmapdp_plan_dev_index(b["plan"], i) for i in range(nprob)])
+        gdev_index = np.array([lib.gmapdp_plan_genome_dev_index(b["plan"], j) for j in range(ng)])
+        npairs = np.zeros(nprob, dtype=np.int64)
+        npairs[dev_index >= 0] = res["npairs"][dev_index[dev_index >= 0]]
+        gnp = np.zeros(ng, dtype=np.int64)
+        gsel = gdev_index >= 0
+        gnp[gsel] = gres["npairs"][gdev_index[gsel]]
+        # genome_gap_simple answered (dynprog_genome.c:3479): its result sets exonhead = new_rightgenomepos
+        gsimple = np.zeros(ng, dtype=bool)
+        gr = gres[gdev_index[gsel]]
+        gsimple[gsel] = (gr["npairs"] > 0) & (gr["exonhead"] == gr["new_rightgenomepos"])
+        g_fills = gsel & ~gsimple
+        b["gcells"] = genome_cells(gp, g_fills)
+        cells_total += dp_cells(sp, ep, gp, g_fills)
+        rl = np.concatenate([sp["rlength"], np.minimum(ep["rlength"], 660)]).astype(np.int64)
+        gl = np.concatenate([sp["glength"], np.minimum(ep["glength"], 2000)]).astype(np.int64)
+        desc = np.concatenate([np.full(ns, gmapdp.PROBLEM_DTYPE.itemsize), np.full(ne, gmapdp.END_PROBLEM_DTYPE.itemsize)])
+        b["bytes"], b["cells"] = [], []
+        for li in range(len(b["names"])):
+            m = np.zeros(b["info"][li][2], dtype=np.int32)
+            lib.gmapdp_plan_launch_members(b["plan"], li, m.ctypes.data)
+            if b["kinds"][li] in (0, 2, 3, 4):
+                b["bytes"].append(algorithmic_bytes(rl[m], gl[m], npairs[m], desc[m]))
+                b["cells"].append(None)
+            else:
+                j = m - nprob
+                b["bytes"].append(genome_algorithmic_bytes(gp[j], gnp[j]))
+                b["cells"].append(int(b["gcells"][j].sum()))
+        b["chain_bytes"] = chain_algorithmic_bytes(op, s2res)
+        checks["pairs"] += int(npairs.sum() + gnp.sum())
+        checks["genome_gaps_bridged"] += int((gnp > 0).sum())
+        checks["genome_gap_simple"] += int(gsimple.sum())
+        checks["stage2_chained"] += int((s2res["status"] == 2).sum())
+        checks["stage2_results"] += int(s2res["nresults"].sum())
+        checks["stage2_path_pairs"] += int(s2res["npairs"].sum())
+        checks["microexon_candidates"] += int(b["ncands"])
+        checks["microexons_found"] += int((mres["npairs"] > 0).sum())
+        checks["reads"] += args.reads
+    for k, e in enumerate(evs):
+        b = B[k % len(B)]
+        for li, name in enumerate(b["names"]):
+            add(name, e["dp"][li][0].elapsed_time(e["dp"][li][1]), b["bytes"][li])
+        add("gmapdp::oi_kernel<unsigned short>+gmapdp::oi_map_kernel", e["oligo"][0].elapsed_time(e["oligo"][1]), None)
+        add("gmapdp::s2a_kernel+gmapdp::s2b_kernel+gmapdp::s2c_kernel", e["oligo"][1].elapsed_time(e["chain"][1]),
+            b["chain_bytes"])
+        add("gmapdp::mx_search_kernel+gmapdp::mx_finish_kernel", e["mx"][0].elapsed_time(e["mx"][1]), None)
+    dominant = max((n for n in per_kernel if per_kernel[n][2] > 0 and "+" not in n), key=lambda n: per_kernel[n][0])
+    dms, dn, dbytes = per_kernel[dominant]
+
+    # ---- the dominant kernel alone (its launches of every block, one at a time on one stream) ----
+    iso_ms, iso_n, iso_bytes, iso_cells = 0.0, 0, 0, 0
+    reps = 3
+    with torch.cuda.stream(stream):
+        for _ in range(reps):
+            for b in B:
+                for li, name in enumerate(b["names"]):
+                    if name != dominant:
+                        continue
+                    e0, e1 = mk()
+                    e0.record(stream)
+                    launch(b, li, stream)
+                    e1.record(stream)
+                    torch.cuda.synchronize()
+                    iso_ms += e0.elapsed_time(e1)
+                    iso_n += 1
+                    iso_bytes += b["bytes"][li]
+                    iso_cells += b["cells"][li] or 0
+    kms = iso_ms / iso_n
+    kbytes = iso_bytes / iso_n
+    kcells = iso_cells / iso_n
     ach = kbytes / (kms * 1e-3) / 1e9
-    traffic, tsrc = pmc_traffic(dominant)
-    step_bytes = sum(d[1] for d in disp if d[1] is not None)
-    cells = banded_cells(sp, ep, gp)
-    reads_total = args.reads * world * args.steps
+    pmc, psrc = pmc_entry(dominant)
+    traffic = pmc["hbm_bytes_per_dispatch"] if pmc else None
+    valu = pmc["sq_SQ_INSTS_VALU_sum_avg"] if pmc else None
+    prof_ms = pmc["avg_duration_ns"] / 1e6 if pmc and pmc.get("avg_duration_ns") else None
+
     ms_step = elapsed / args.steps * 1e3
+    reads_total = args.reads * world * args.steps
+    nsub = {k: int(np.mean([len(b["d"][k]) for b in B])) for k in ("oligo", "single", "end", "genome", "microexon")}
     out = {
         "metric": METRIC,
         "value": reads_total / elapsed,
@@ -412,58 +621,83 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "int32",
+        "dtype": "int16/int8 saturating (SIMD-build semantics)" if args.simd else "int32",
         "data": "synthetic",
-        "config": {"workload": "configs[2]: synthetic 2-kb cDNA reads (5 exons x 400 nt, 2 %% subs) vs a "
-                               "GRCh38-layout i.i.d. genome (24 chromosomes, %d nt, universal coordinates to %d): per "
-                               "read 1 Stage2_compute call (seeding + chaining) + %.1f Dynprog_single_gap + %.1f Dynprog_end5_gap + "
-                               "%.1f Dynprog_end3_gap + %.1f Dynprog_genome_gap + %.1f Dynprog_microexon_int; inputs "
-                               "HBM-resident; host stages 1/3 not in the step"
-                               % (layout.total, layout.total - 1, W.SINGLE_PER_READ, W.END5_PER_READ,
-                                  W.END3_PER_READ, W.GENOME_PER_READ, W.MICROEXON_PER_READ),
-                   "genome": args.genome, "reads_per_step_per_gpu": args.reads,
-                   "subproblems_per_step_per_gpu": {"stage2_compute": len(op), "single": ns, "end": ne, "genome": ng,
-                                                    "microexon": len(mp)},
-                   "banded_cells_per_step_per_gpu": cells,
-                   "parallelism": "dp%d (reads sharded by rank, genome replicated)" % world},
+        "config": {"workload": "configs[%d]: synthetic %d-nt %s reads (%d exons x %d nt, %g %% subs, %g %% indels) vs a "
+                               "%s-layout i.i.d. genome (%d chromosomes, %d nt, universal coordinates to %d): per read "
+                               "1 Stage2_compute call (seeding + chaining) + %.1f Dynprog_single_gap + %.1f "
+                               "Dynprog_end5_gap + %.1f Dynprog_end3_gap + %.1f Dynprog_genome_gap + %.1f "
+                               "Dynprog_microexon_int (%s semantics); %d distinct blocks of %d reads cycled per rank; "
+                               "inputs HBM-resident; host stages 1/3 not in the step"
+                               % (args.config, shape.readlength, "Iso-Seq-style" if args.config == 4 else "cDNA",
+                                  shape.exons, shape.exlen, 100 * shape.subs, 100 * shape.indel, gname,
+                                  len(layout.lens), layout.total, layout.total - 1, shape.single, shape.end5,
+                                  shape.end3, shape.genome, shape.microexon, "gmap.avx2" if args.simd else "nosimd",
+                                  len(B), args.reads),
+                   "genome": gname, "reads_per_step_per_gpu": args.reads, "blocks_per_rank": len(B),
+                   "call_mix_source": shape.source,
+                   "subproblems_per_step_per_gpu": {"stage2_compute": nsub["oligo"], "single": nsub["single"],
+                                                    "end": nsub["end"], "genome": nsub["genome"],
+                                                    "microexon": nsub["microexon"]},
+                   "banded_cells_per_step_per_gpu": cells_total // len(B),
+                   "parallelism": "dp%d (reads sharded by rank, --part=r/%d over read blocks; genome replicated)"
+                                  % (world, world)},
         "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                     "traffic": traffic, "traffic_source": tsrc, "kernel": dominant, "dispatches": len(sel) * args.steps,
+                     "traffic": traffic, "traffic_source": psrc, "kernel": dominant,
                      "kernel_ms_per_launch": kms, "algorithmic_bytes_per_launch": kbytes,
-                     "step_algorithmic_gbs": step_bytes / (ms_step * 1e-3) / 1e9,
-                     "note": "integer VALU/LDS/latency-bound DP (SURVEY §8d); HBM roofline reported as required"},
-        "gcups": cells * world * args.steps / elapsed / 1e9,
+                     "timing": "HIP events around each of the kernel's launches run alone on one stream (%d "
+                               "dispatches, after the timed region); in the timed steps, which share the CUs "
+                               "four streams wide, its launches average %.3f ms" % (iso_n, dms / dn),
+                     "kernel_ms_per_launch_in_step": dms / dn, "rocprof_avg_ms_committed": prof_ms,
+                     "step_algorithmic_gbs": sum(e[2] for e in per_kernel.values()) / args.steps
+                                             / (ms_step * 1e-3) / 1e9,
+                     "valu": {"insts_per_launch": valu,
+                              "issue_frac": valu / (VALU_WAVE_INSTR_PEAK * kms * 1e-3) if valu else None,
+                              "peak_wave_insts_per_s": VALU_WAVE_INSTR_PEAK,
+                              "source": psrc},
+                     "int_ops": {"cells_per_launch": kcells, "ops_per_cell": OPS_PER_CELL,
+                                 "frac": OPS_PER_CELL * kcells / (INT_OPS_PEAK * kms * 1e-3) if kcells else None,
+                                 "peak_ops_per_s": INT_OPS_PEAK,
+                                 "note": "genome-gap fills counted only where genome_gap_simple did not answer"},
+                     "note": "integer VALU/LDS/latency-bound DP (SURVEY §8d); the HBM roofline is reported as "
+                             "required, the VALU issue and algorithmic int-op fractions are the binding bounds "
+                             "(BASELINE.md §3(i))"},
+        "gcups": cells_total / len(B) * world * args.steps / elapsed / 1e9,
         "step_split_ms": {"stage2_alone": el_o / half * 1e3, "dynprog_alone": el_dp / half * 1e3,
                           "together": ms_step},
-        "stage2_seeding_launch_ms": oligo_ms,
-        "stage2_chaining_launch_ms": chain_ms,
-        "launch_classes": [{"kernel": d[0], "problems": d[3], "ms": round(d[2], 4)} for d in disp],
-        "host": {"plan_ms": t_plan * 1e3, "oligo_plan_ms": t_oplan * 1e3, "setup_s": t_gen},
+        "launch_classes": sorted(({"kernel": n, "dispatches": e[1], "ms_per_step": round(e[0] / args.steps, 4)}
+                                  for n, e in per_kernel.items()), key=lambda x: -x["ms_per_step"]),
+        "host": {"plan_ms_per_block": t_plan * 1e3 / len(B), "stage2_plan_ms_per_block": t_oplan * 1e3 / len(B),
+                 "setup_s": t_gen},
+        "checks": {"pairs_per_read": checks["pairs"] / checks["reads"],
+                   "genome_gaps_bridged": checks["genome_gaps_bridged"],
+                   "genome_gap_simple": checks["genome_gap_simple"],
+                   "stage2_chained": checks["stage2_chained"], "stage2_results": checks["stage2_results"],
+                   "stage2_path_pairs_per_read": checks["stage2_path_pairs"] / checks["reads"],
+                   "microexon_candidates": checks["microexon_candidates"],
+                   "microexons_found": checks["microexons_found"], "reads_checked": checks["reads"]},
     }
-    # spot check of the step's outputs: size-independent invariants (the oracle parity is tests/)
-    assert np.all(res["npairs"] >= 0) and np.all(gres["npairs"] >= 0) and np.all(s2res["status"] >= 0)
-    assert np.all(mres["ncandidates"] >= 0) and np.all(mres["cand_offset"] >= 0)
-    out["checks"] = {"pairs_per_read": float((npairs.sum() + gnp.sum()) / args.reads),
-                     "genome_gaps_bridged": int((gnp > 0).sum()),
-                     "stage2_chained": int((s2res["status"] == 2).sum()),
-                     "stage2_results": int(s2res["nresults"].sum()),
-                     "stage2_path_pairs_per_read": float(s2res["npairs"].sum() / args.reads),
-                     "stage2_scratch_mb": sb_.value / 1e6,
-                     "microexon_candidates": int(ncands),
-                     "microexons_found": int((mres["npairs"] > 0).sum())}
-    lib.gmapdp_plan_destroy(plan)
-    lib.gmapdp_stage2_plan_destroy(oplan)
-    lib.gmapdp_microexon_plan_destroy(mplan)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    # shard record: every rank's blocks, checked disjoint and complete
+    out["shard"] = shard.gather_blocks(mine, [b["d"]["reads"] for b in B], dist if world > 1 else None)
+    rank_line = {"rank": rank, "world_size": dist.get_world_size() if world > 1 else 1,
+                 "backend": dist.get_backend() if world > 1 else None, "device": local,
+                 "blocks": mine, "ms_per_step_local": ms_step}
+    print(json.dumps({"rank_line": rank_line}), file=sys.stderr, flush=True)
+    for b in B:
+        lib.gmapdp_plan_destroy(b["plan"])
+        lib.gmapdp_stage2_plan_destroy(b["oplan"])
+        lib.gmapdp_microexon_plan_destroy(b["mplan"])
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == 2 and not args.simd:
         progress("CPU baselines")
         cb = cpu_baselines()
         # the faster of the reference's two builds is the baseline; the other is kept beside it
-        done = sorted((b for b in cb.values() if b), key=lambda b: -b["value"])
+        done = sorted((c for c in cb.values() if c), key=lambda c: -c["value"])
         out["cpu_baseline"] = done[0] if done else None
         out["cpu_baseline_other_build"] = done[1] if len(done) > 1 else None
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

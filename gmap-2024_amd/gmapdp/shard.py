@@ -44,3 +44,32 @@ def max_over_ranks(value, dist, device=None):
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def blocks_of_rank(rank, world, nbatches):
+    """The read blocks rank `rank` of `world` processes: block b of the stream's first world x nbatches
+    blocks goes to the rank with b % world == rank (--part=rank/world applied to blocks of reads)."""
+    ids = np.arange(world * nbatches)
+    return [int(b) for b in ids[part_mask(ids, rank, world)]]
+
+
+def gather_blocks(mine, reads, dist=None):
+    """all_gather every rank's (block ids, reads per block); check that the blocks are disjoint and
+    together cover 0 .. nblocks-1, and return the shard record bench.py reports."""
+    world = dist.get_world_size() if dist is not None else 1
+    if dist is None:
+        every = [list(mine)]
+        every_reads = [list(reads)]
+    else:
+        every = [None] * world
+        every_reads = [None] * world
+        dist.all_gather_object(every, list(mine))
+        dist.all_gather_object(every_reads, [int(r) for r in reads])
+    flat = [b for ids in every for b in ids]
+    if len(set(flat)) != len(flat):
+        raise RuntimeError("read blocks assigned to more than one rank: %s" % every)
+    if sorted(flat) != list(range(len(flat))):
+        raise RuntimeError("read blocks missing from the shard: %s" % every)
+    return {"rule": "--part=r/N over blocks of reads (inbuffer.c:283)", "blocks_per_rank": every,
+            "reads_per_rank": [int(sum(r)) for r in every_reads], "reads_total": int(sum(sum(r) for r in every_reads)),
+            "disjoint": True}

@@ -12,6 +12,18 @@ Per 2-kb read (nosimd instrumentation):
   43.7 Dynprog_single_gap, 7.1 Dynprog_end5_gap, 6.5 Dynprog_end3_gap, 49.4 Dynprog_genome_gap.
 Sub-problem shapes follow the measured size distributions (replay mode); genome gaps
 span planted GT-AG introns.  Everything is vectorised numpy and seeded.
+
+configs[4] (gmapl, 5-kb Iso-Seq-style reads, 10 exons, 1 % substitutions + 1 % indels, 17-Gnt wheat
+genome): the same generators with the ISOSEQ shape (per-read call mix measured with the reference's own
+gmap on reads of that shape, oracle/callmix.c) and the WHEAT17 layout, whose universal
+coordinates run past 2^32 (64-bit Univcoord_T, univcoord.h:9-11).  Genomes of that size are generated
+directly as packed .genomecomp blocks (PackedGenome): no ASCII copy is ever made.
+
+Read stream and sharding: the stream is cut into blocks of `reads` reads; block b is generated from its
+own seeds (reads: 1000 + 7919 b, intron sites: 23 + b), so the stream is the same whatever the world
+size, and rank r of N takes the blocks b with b % N == r (GMAP's --part=r/N rule, inbuffer.c:283,
+applied per block; gmapdp.shard).  Every rank plants the intron sites of every block of the stream in
+block order, so all ranks hold the same genome.
 """
 import numpy as np
 
@@ -24,17 +36,53 @@ GRCH38 = [("chr1", 248956422), ("chr2", 242193529), ("chr3", 198295559), ("chr4"
           ("chr21", 46709983), ("chr22", 50818468), ("chrX", 156040895), ("chrY", 57227415)]
 CHR22 = [("chr22", 50818468)]
 
-SINGLE_PER_READ = 43.7         # Dynprog_single_gap calls per 2-kb read (nosimd)
-END5_PER_READ = 7.1            # Dynprog_end5_gap
-END3_PER_READ = 6.5            # Dynprog_end3_gap
-GENOME_PER_READ = 49.4         # Dynprog_genome_gap
-STAGE2_PER_READ = 1            # Stage2_compute seeding calls
-MICROEXON_PER_READ = 25.6      # Dynprog_microexon_int
+# Wheat (Chinese Spring) 21 chromosomes + unplaced, lengths rounded from IWGSC RefSeq v1.0 and scaled by
+# 17 / 14.55 so the genome is the 17 Gnt BASELINE configs[4] names; every chromosome stays below 2^31
+# (Chrpos_T), universal coordinates run to 1.7e10 > 2^32 (gmapl).
+_WHEAT = [("1A", 594.1), ("1B", 689.9), ("1D", 495.5), ("2A", 780.8), ("2B", 801.3), ("2D", 651.9), ("3A", 750.8),
+          ("3B", 830.8), ("3D", 615.6), ("4A", 744.6), ("4B", 673.6), ("4D", 509.9), ("5A", 709.8), ("5B", 713.1),
+          ("5D", 566.1), ("6A", 618.1), ("6B", 721.0), ("6D", 473.6), ("7A", 736.7), ("7B", 750.6), ("7D", 638.7),
+          ("Un", 481.0)]
+WHEAT17 = [("chr" + c, int(round(m * 1e6 * 17e9 / (sum(x for _, x in _WHEAT) * 1e6)))) for c, m in _WHEAT]
+
+
+class Shape:
+    """Read shape and per-read call mix of one BASELINE config."""
+
+    def __init__(self, name, exons, exlen, subs, indel, single, end5, end3, genome, microexon, source):
+        self.name, self.exons, self.exlen, self.subs, self.indel = name, exons, exlen, subs, indel
+        self.single, self.end5, self.end3, self.genome, self.microexon = single, end5, end3, genome, microexon
+        self.source = source
+
+    @property
+    def readlength(self):
+        return self.exons * self.exlen
+
+
+# configs[2]: 2-kb cDNA, 5 x 400 nt, 2 % substitutions; call mix from SURVEY App. B (nosimd instrumentation)
+CDNA2K = Shape("cdna2k", 5, 400, 0.02, 0.0, 43.7, 7.1, 6.5, 49.4, 25.6, "SURVEY App. B")
+# configs[4]: 5-kb Iso-Seq-style reads, 10 x 500 nt, 1 % substitutions + 1 % indels; the call mix is
+# measured by oracle/callmix.c (tools/callmix.py) -- see ISOSEQ_MIX below
+ISOSEQ5K = Shape("isoseq5k", 10, 500, 0.01, 0.01, 43.7 * 2.5, 7.1, 6.5, 49.4 * 9 / 4, 25.6 * 9 / 4,
+                 "scaled from SURVEY App. B (per kb / per intron)")
+
+SINGLE_PER_READ = CDNA2K.single        # Dynprog_single_gap calls per 2-kb read (SURVEY App. B, nosimd)
+END5_PER_READ = CDNA2K.end5            # Dynprog_end5_gap
+END3_PER_READ = CDNA2K.end3            # Dynprog_end3_gap
+GENOME_PER_READ = CDNA2K.genome        # Dynprog_genome_gap
+STAGE2_PER_READ = 1                    # Stage2_compute seeding calls
+MICROEXON_PER_READ = CDNA2K.microexon  # Dynprog_microexon_int
 
 COMPL = np.zeros(256, dtype=np.uint8)
 for _a, _b in zip(b"ACGTN", b"TGCAN"):
     COMPL[_a] = _b
 ACGT = np.frombuffer(b"ACGT", dtype=np.uint8)
+CODE = np.zeros(256, dtype=np.uint8)
+for _k, _c in enumerate(b"ACGT"):
+    CODE[_c] = _k
+# one packed byte (4 nt, nt j in bits 2j..2j+1) -> 4 ASCII bytes as a little-endian uint32
+_LUT4 = np.array([sum(int(ACGT[(x >> (2 * k)) & 3]) << (8 * k) for k in range(4)) for x in range(256)],
+                 dtype=np.uint32)
 
 
 class Layout:
@@ -52,6 +100,69 @@ class Layout:
         c = np.searchsorted(np.cumsum(self.lens), u, side="right")
         c = np.minimum(c, len(self.lens) - 1)
         return self.offsets[c], self.offsets[c] + self.lens[c], self.lens[c]
+
+
+class PackedGenome:
+    """An i.i.d. ACGT genome held only as the reference's .genomecomp blocks (3 words per 32 nt: high
+    nt 16-31, low nt 0-15, flags; 2 bits per nt A0 C1 G2 T3; the last block's tail and 4 trailing
+    words are 'X' padding: gmapdp_pack_genome / Compress_create_blocks_comp).  Indexing with an integer
+    array of universal positions returns ASCII bytes; assigning ASCII bytes plants them."""
+
+    def __init__(self, length, seed=38, chunk=1 << 24):
+        self.length = int(length)
+        nb = (self.length + 31) // 32
+        self.blocks = np.empty(3 * nb + 4, dtype=np.uint32)
+        v = self.blocks[:3 * nb].reshape(nb, 3)
+        rng = np.random.default_rng(seed)
+        for a in range(0, nb, chunk):
+            b = min(nb, a + chunk)
+            raw = rng.integers(0, 1 << 32, size=(b - a, 2), dtype=np.uint32)
+            v[a:b, 0] = raw[:, 0]
+            v[a:b, 1] = raw[:, 1]
+            v[a:b, 2] = 0
+        tail = 32 * nb - self.length
+        if tail:
+            j = np.arange(32 - tail, 32)
+            for k in j:
+                word = 0 if k >= 16 else 1
+                v[nb - 1, word] |= np.uint32(3 << (2 * (k & 15)))
+                v[nb - 1, 2] |= np.uint32(1 << int(k))
+        self.blocks[3 * nb:] = 0xFFFFFFFF
+
+    def __len__(self):
+        return self.length
+
+    def _where(self, idx):
+        idx = np.asarray(idx, dtype=np.int64)
+        j = (idx & 31).astype(np.uint32)
+        w = 3 * (idx >> 5) + 1 - (j >> 4).astype(np.int64)
+        return w, (j & 15) << 1
+
+    def __getitem__(self, idx):
+        w, sh = self._where(idx)
+        return ACGT[(self.blocks[w] >> sh) & 3]
+
+    def __setitem__(self, idx, ch):
+        idx = np.asarray(idx, dtype=np.int64).ravel()
+        code = CODE[np.broadcast_to(np.asarray(ch, dtype=np.uint8), idx.shape)].astype(np.uint32)
+        # one write per position (the last wins, as plain fancy assignment), then read-modify-write
+        # per word with ufunc.at so two positions of one word both land
+        _, last = np.unique(idx[::-1], return_index=True)
+        keep = len(idx) - 1 - last
+        idx, code = idx[keep], code[keep]
+        w, sh = self._where(idx)
+        np.bitwise_and.at(self.blocks, w, ~(np.uint32(3) << sh))
+        np.bitwise_or.at(self.blocks, w, code << sh)
+
+    def ascii(self, start, end):
+        """bytes of universal positions [start, end) (whole blocks through a byte -> 4-nt table; the
+        stream has no flagged positions below `length`)"""
+        b0, b1 = start // 32, (end + 31) // 32
+        v = self.blocks[3 * b0:3 * b1].reshape(b1 - b0, 3)
+        out = np.empty((b1 - b0, 32), dtype=np.uint8)
+        out[:, :16] = _LUT4[np.ascontiguousarray(v[:, 1]).view(np.uint8)].view(np.uint8).reshape(-1, 16)
+        out[:, 16:] = _LUT4[np.ascontiguousarray(v[:, 0]).view(np.uint8)].view(np.uint8).reshape(-1, 16)
+        return out.reshape(-1)[start - 32 * b0:end - 32 * b0].tobytes()
 
 
 def make_genome(layout, seed=38):
@@ -162,15 +273,11 @@ def make_end(genome, layout, n5, n3, rng):
     return probs, q
 
 
-def make_genome_gaps(genome, layout, n, rng, site_seed=23):
-    """Dynprog_genome_gap sub-problems (stage3.c:9504-9539): a query gap of rlength nt = a exonic nt
-    before a planted GT..AG intron + b after it; goffsetL = first genomic position after the left
-    anchor, rev_goffsetR = last one before the right anchor, glengthL = glengthR = rlength + 8
-    (extramaterial_paired), extraband_paired 14.  Plants the dinucleotides into `genome` (in place)
-    at sites drawn from `site_seed`, so every rank builds the same genome; call it before the other
-    sub-problems are cut from the genome.  Splice probabilities are synthetic host inputs (0.95 at
-    the planted sites, U[0, 0.3) elsewhere)."""
-    import gmapdp
+def genome_gap_sites(layout, n, site_seed=23):
+    """The intron sites of n genome-gap sub-problems (stage3.c:9504-9539), drawn from `site_seed` only
+    (rank-independent): a query gap of rlength nt = a exonic nt before a GT..AG intron + b after it;
+    goffsetL = first genomic position after the left anchor, rev_goffsetR = last one before the right
+    anchor."""
     srng = np.random.default_rng(site_seed)
     r = np.clip(srng.gamma(2.2, 50.0, size=n).astype(np.int64), 2, 600)
     a = (srng.random(n) * (r + 1)).astype(np.int64)
@@ -180,12 +287,34 @@ def make_genome_gaps(genome, layout, n, rng, site_seed=23):
     choff, chrhigh, clen = layout.sample(srng, n, 8000)
     goffL = (srng.random(n) * (clen - 7200)).astype(np.int64) + 100
     revR = goffL + a + intron + b - 1
-    x, y = goffL + a, revR - b            # first / last intron base, strand coordinates
+    return {"r": r, "a": a, "b": b, "watson": watson, "choff": choff, "chrhigh": chrhigh, "goffL": goffL,
+            "revR": revR}
 
-    def plant(pos, ch):
-        idx = np.where(watson, choff + pos, chrhigh - pos)
-        genome[idx] = np.where(watson, ord(ch), COMPL[ord(ch)])
-    plant(x, "G"); plant(x + 1, "T"); plant(y - 1, "A"); plant(y, "G")
+
+def plant_sites(genome, st):
+    """Write the GT..AG dinucleotides of genome_gap_sites into `genome` (in place)."""
+    watson, choff, chrhigh = st["watson"], st["choff"], st["chrhigh"]
+    x, y = st["goffL"] + st["a"], st["revR"] - st["b"]   # first / last intron base, strand coordinates
+    idx, ch = [], []
+    for pos, c in ((x, "G"), (x + 1, "T"), (y - 1, "A"), (y, "G")):
+        idx.append(np.where(watson, choff + pos, chrhigh - pos))
+        ch.append(np.where(watson, ord(c), COMPL[ord(c)]).astype(np.uint8))
+    genome[np.concatenate(idx)] = np.concatenate(ch)
+
+
+def make_genome_gaps(genome, layout, n, rng, site_seed=23, plant=True, sprob=True):
+    """Dynprog_genome_gap sub-problems (stage3.c:9504-9539) over the sites of genome_gap_sites:
+    glengthL = glengthR = rlength + 8 (extramaterial_paired), extraband_paired 14.  With `plant`, the
+    dinucleotides are planted first (in place; call it before the other sub-problems are cut from the
+    genome).  Splice probabilities are synthetic host inputs (0.95 at the planted sites, U[0, 0.3)
+    elsewhere): with `sprob` the array, otherwise (length, indices of the 0.95 entries) for a caller
+    that draws them where they are used (bench.py: on the device)."""
+    import gmapdp
+    st = genome_gap_sites(layout, n, site_seed)
+    if plant:
+        plant_sites(genome, st)
+    r, a, b, watson = st["r"], st["a"], st["b"], st["watson"]
+    choff, chrhigh, goffL, revR = st["choff"], st["chrhigh"], st["goffL"], st["revR"]
     q_off = np.concatenate([[0], np.cumsum(r)])
     qpid = np.repeat(np.arange(n), r)
     j = np.arange(q_off[-1]) - q_off[qpid]
@@ -211,16 +340,34 @@ def make_genome_gaps(genome, layout, n, rng, site_seed=23):
     ent = 2 * (r + 8)
     p_off = np.concatenate([[0], np.cumsum(ent)])
     gp["prob_offset"] = p_off[:-1]
-    sprob = rng.random(int(p_off[-1])) * 0.3
-    sprob[p_off[:-1] + a] = 0.95                 # left site (cL = a)
-    sprob[p_off[:-1] + (r + 8) + b] = 0.95       # right site (cR = b)
-    return gp, q.astype(np.uint8), sprob
+    hi = np.concatenate([p_off[:-1] + a, p_off[:-1] + (r + 8) + b])   # left site cL = a, right site cR = b
+    if not sprob:
+        return gp, q.astype(np.uint8), (int(p_off[-1]), hi)
+    sp = rng.random(int(p_off[-1])) * 0.3
+    sp[hi] = 0.95
+    return gp, q.astype(np.uint8), sp
 
 
-def make_stage2(genome, layout, n, rng, exons=5, exlen=400, pad=1000):
-    """Stage-2 seeding calls, one per 2-kb read: 5 exons x 400 nt cut from the genome with
-    log-uniform [80, 20000] introns, 2 % substitutions, half reverse-complemented (seeded on the
-    minus strand), against the window spanning the locus plus 1 kb each side (the gregion).
+def mutate(q, rng, subs, indel):
+    """Reads of equal length (rows of q) with `subs` uniform substitutions and `indel` 1-nt indels (half
+    deletions, half insertions of a random base) per base.  Returns (flat arena, lengths)."""
+    n, L = q.shape
+    q = np.where(rng.random(q.shape) < subs, ACGT[rng.integers(0, 4, size=q.shape, dtype=np.uint8)], q)
+    if indel <= 0:
+        return q.reshape(-1).astype(np.uint8), np.full(n, L, dtype=np.int64)
+    u = rng.random(q.shape)
+    reps = np.where(u < indel / 2, 0, np.where(u < indel, 2, 1)).astype(np.int64)
+    flat = np.repeat(q.reshape(-1), reps.reshape(-1))
+    ends = np.cumsum(reps.reshape(-1)) - 1
+    ins = ends[reps.reshape(-1) == 2]
+    flat[ins] = ACGT[rng.integers(0, 4, size=len(ins), dtype=np.uint8)]
+    return flat.astype(np.uint8), reps.sum(axis=1)
+
+
+def make_stage2(genome, layout, n, rng, exons=5, exlen=400, pad=1000, subs=0.02, indel=0.0):
+    """Stage-2 calls, one per read: `exons` exons x `exlen` nt cut from the genome with log-uniform
+    [80, 20000] introns, substitutions and indels, half reverse-complemented (seeded on the minus
+    strand), against the window spanning the locus plus 1 kb each side (the gregion).
     Returns (gmapdp_oligo_problem array, upper-case query arena)."""
     import gmapdp
     introns = np.exp(rng.uniform(np.log(80), np.log(20000), size=(n, exons - 1))).astype(np.int64)
@@ -231,21 +378,24 @@ def make_stage2(genome, layout, n, rng, exons=5, exlen=400, pad=1000):
                               np.cumsum(exlen + introns, axis=1)], axis=1) + start[:, None]   # (n, exons)
     j = np.arange(exons * exlen)
     src = choff[:, None] + exstart[:, j // exlen] + j % exlen        # universal coordinates, exon by exon
-    q = genome[src]                                                   # (n, 2000)
-    m = rng.random(q.shape) < 0.02
-    q = np.where(m, ACGT[rng.integers(0, 4, size=q.shape, dtype=np.uint8)], q)
+    flat, L = mutate(genome[src], rng, subs, indel)
+    off = np.concatenate([[0], np.cumsum(L)])
     plus = rng.random(n) < 0.5
-    q = np.where(plus[:, None], q, COMPL[q[:, ::-1]]).astype(np.uint8)
+    qpid = np.repeat(np.arange(n), L)
+    k = np.arange(off[-1]) - off[qpid]
+    rc = ~plus[qpid]
+    q = flat[np.where(rc, off[qpid] + L[qpid] - 1 - k, off[qpid] + k)]
+    q = np.where(rc, COMPL[q], q).astype(np.uint8)
     probs = np.zeros(n, dtype=gmapdp.OLIGO_PROBLEM_DTYPE)
-    probs["qoff"] = np.arange(n) * q.shape[1]
-    probs["querylength"] = q.shape[1]
+    probs["qoff"] = off[:-1]
+    probs["querylength"] = L
     probs["chrstart"] = start - pad
     probs["chrend"] = start + span + pad
     probs["chroffset"] = choff
     probs["chrhigh"] = chrhigh
     probs["plusp"] = plus
     probs["minor"] = 0
-    return probs, q.reshape(-1)
+    return probs, q
 
 
 def make_microexon(gp, n, rng):
@@ -265,22 +415,66 @@ def make_microexon(gp, n, rng):
     return mp
 
 
-def make_reads(genome, layout, reads, seed, site_seed=23):
-    """The per-read call stream of `reads` reads: dict of descriptor arrays and arenas.  Genome gaps
-    plant their intron motifs first (in place), then every other sub-problem is cut."""
+def block_seeds(b):
+    """(read seed, intron-site seed) of block b of the read stream"""
+    return 1000 + 7919 * b, 23 + b
+
+
+def make_reads(genome, layout, reads, seed, site_seed=23, shape=CDNA2K, plant=True, sprob=True):
+    """The per-read call stream of `reads` reads of `shape`: dict of descriptor arrays and arenas.
+    With `plant`, genome gaps plant their intron motifs first (in place), then every other sub-problem
+    is cut."""
     rng = np.random.default_rng(seed)
-    ng = int(round(reads * GENOME_PER_READ))
+    ng = int(round(reads * shape.genome))
     # intron sites are rank-independent (site_seed), so every rank plants the same genome
-    gp, gq, sprob = make_genome_gaps(genome, layout, ng, np.random.default_rng(seed + 1), site_seed=site_seed)
-    ns = int(round(reads * SINGLE_PER_READ))
-    n5 = int(round(reads * END5_PER_READ))
-    n3 = int(round(reads * END3_PER_READ))
-    sp, sq = make_single(genome, layout, ns, rng)
+    gp, gq, sp = make_genome_gaps(genome, layout, ng, np.random.default_rng(seed + 1), site_seed=site_seed,
+                                  plant=plant, sprob=sprob)
+    ns = int(round(reads * shape.single))
+    n5 = int(round(reads * shape.end5))
+    n3 = int(round(reads * shape.end3))
+    sp_, sq = make_single(genome, layout, ns, rng)
     ep, eq = make_end(genome, layout, n5, n3, rng)
     ep["qoff"] += len(sq)
     gp["qoff"] += len(sq) + len(eq)
     q = np.concatenate([sq, eq, gq])
-    op, oq = make_stage2(genome, layout, reads, np.random.default_rng(seed + 3))
-    mp = make_microexon(gp, int(round(reads * MICROEXON_PER_READ)), np.random.default_rng(seed + 4))
-    return {"single": sp, "end": ep, "genome": gp, "q": q, "sprob": sprob, "oligo": op, "oq": oq,
-            "microexon": mp, "reads": reads}
+    op, oq = make_stage2(genome, layout, reads, np.random.default_rng(seed + 3), exons=shape.exons,
+                         exlen=shape.exlen, subs=shape.subs, indel=shape.indel)
+    mp = make_microexon(gp, int(round(reads * shape.microexon)), np.random.default_rng(seed + 4))
+    out = {"single": sp_, "end": ep, "genome": gp, "q": q, "oligo": op, "oq": oq, "microexon": mp,
+           "reads": reads}
+    if sprob:
+        out["sprob"] = sp
+    else:
+        out["sprob_len"], out["sprob_hi"] = sp
+    return out
+
+
+def plant_stream(genome, layout, reads, blocks, shape=CDNA2K):
+    """Plant the intron sites of every block of the stream, in block order (every rank does the same,
+    so every rank holds the same genome)."""
+    for b in blocks:
+        plant_sites(genome, genome_gap_sites(layout, int(round(reads * shape.genome)), block_seeds(b)[1]))
+
+
+def _block_worker(args):
+    genome, layout, reads, b, shape, sprob = _POOL_STATE[0], _POOL_STATE[1], args[0], args[1], args[2], args[3]
+    seed, site_seed = block_seeds(b)
+    return make_reads(genome, layout, reads, seed, site_seed=site_seed, shape=shape, plant=False, sprob=sprob)
+
+
+_POOL_STATE = [None, None]
+
+
+def make_blocks(genome, layout, reads, blocks, shape=CDNA2K, sprob=True, workers=1):
+    """The call streams of `blocks` (the genome already planted by plant_stream), generated in
+    `workers` forked processes (the genome is shared copy-on-write; call before any GPU work)."""
+    _POOL_STATE[0], _POOL_STATE[1] = genome, layout
+    jobs = [(reads, b, shape, sprob) for b in blocks]
+    try:
+        if workers <= 1 or len(blocks) <= 1:
+            return [_block_worker(j) for j in jobs]
+        import multiprocessing as mp
+        with mp.get_context("fork").Pool(min(workers, len(blocks))) as pool:
+            return pool.map(_block_worker, jobs)
+    finally:
+        _POOL_STATE[0] = _POOL_STATE[1] = None

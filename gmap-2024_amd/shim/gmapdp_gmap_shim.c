@@ -171,6 +171,10 @@ __wrap_Dynprog_end_setup (Univcoord_T *splicesites_in, Splicetype_T *splicetypes
                           int nsplicesites_in, Trieoffset_T *trieoffsets_obs_in, Triecontent_T *triecontents_obs_in,
                           Trieoffset_T *trieoffsets_max_in, Triecontent_T *triecontents_max_in,
                           int user_open_in, int user_extend_in, bool user_dynprog_p_in) {
+  /* Known splice sites (-s): GMAP then calls Dynprog_end5/3_known and _splicejunction
+     (dynprog_end.c:1653-3009), which the engine does not implement; refused at setup, before any read
+     runs, so that no reference CPU code executes inside the product */
+  if (nsplicesites_in > 0) shim_refuse("known splice sites (-s: Dynprog_end5/3_known, _splicejunction)");
   __real_Dynprog_end_setup(splicesites_in, splicetypes_in, splicedists_in, nsplicesites_in, trieoffsets_obs_in,
                            triecontents_obs_in, trieoffsets_max_in, triecontents_max_in, user_open_in,
                            user_extend_in, user_dynprog_p_in);
@@ -1227,7 +1231,16 @@ __wrap_Stage2_compute (char *queryseq_ptr, char *queryuc_ptr, int querylength, i
   major = Oligoindex_array_elt(oligoindices, 0);
   if (major->indexsize != 8 || major->diag_lookback != 120 || major->suffnconsecutive != 20)
     shim_refuse("an oligoindex other than GMAP's major 8-mer index");
-  if (querylength <= 8) shim_refuse("Stage2_compute on a query of 8 nt or less");
+  /* Below 8 nt the query holds no 8-mer: Oligoindex_get_mappings finds no position, totalpositions is 0
+     and the reference returns NULL (stage2.c:6524).  At exactly 8 nt the tally runs against the previous
+     query's inquery flags (Oligoindex_set_inquery returns early, oligoindex_hr.c:33478), a state the
+     engine does not keep: refused. */
+  if (querylength < 8) return NULL;
+  if (querylength == 8) shim_refuse("Stage2_compute on a query of exactly 8 nt");
+  /* the chaining kernels keep Chrpos_T differences in 32-bit registers: checked here, on the calling
+     thread, so that a refusal names its own call and never fails another thread's batch */
+  if (chrend >= 0x80000000U || chrstart >= 0x80000000U)
+    shim_refuse("Stage2_compute at chromosome positions past 2^31");
   r = shim_request(K_STAGE2);
   p = &r->p.s2;
   p->querylength = querylength;
