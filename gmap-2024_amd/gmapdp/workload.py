@@ -49,10 +49,14 @@ WHEAT17 = [("chr" + c, int(round(m * 1e6 * 17e9 / (sum(x for _, x in _WHEAT) * 1
 class Shape:
     """Read shape and per-read call mix of one BASELINE config."""
 
-    def __init__(self, name, exons, exlen, subs, indel, single, end5, end3, genome, microexon, source):
+    def __init__(self, name, exons, exlen, subs, indel, single, end5, end3, genome, microexon, source,
+                 single_indel=0.15, single_dmean=0.0):
         self.name, self.exons, self.exlen, self.subs, self.indel = name, exons, exlen, subs, indel
         self.single, self.end5, self.end3, self.genome, self.microexon = single, end5, end3, genome, microexon
         self.source = source
+        # single gaps whose query and genome lengths differ: a fraction, and (single_dmean > 0) the mean of
+        # an exponential genome-minus-query excess; otherwise a uniform +-1..3 nt indel
+        self.single_indel, self.single_dmean = single_indel, single_dmean
 
     @property
     def readlength(self):
@@ -61,10 +65,14 @@ class Shape:
 
 # configs[2]: 2-kb cDNA, 5 x 400 nt, 2 % substitutions; call mix from SURVEY App. B (nosimd instrumentation)
 CDNA2K = Shape("cdna2k", 5, 400, 0.02, 0.0, 43.7, 7.1, 6.5, 49.4, 25.6, "SURVEY App. B")
-# configs[4]: 5-kb Iso-Seq-style reads, 10 x 500 nt, 1 % substitutions + 1 % indels; the call mix is
-# measured by oracle/callmix.c (tools/callmix.py) -- see ISOSEQ_MIX below
-ISOSEQ5K = Shape("isoseq5k", 10, 500, 0.01, 0.01, 43.7 * 2.5, 7.1, 6.5, 49.4 * 9 / 4, 25.6 * 9 / 4,
-                 "scaled from SURVEY App. B (per kb / per intron)")
+# configs[4]: 5-kb Iso-Seq-style reads, 10 x 500 nt, 1 % substitutions + 1 % indels.  Call mix measured
+# with the reference's own gmap on 200 reads of that shape (oracle/callmix.c, tools/callmix.py,
+# profiles/r03_callmix/callmix.json): per read 285.1 single gaps (91 % with query and genome lengths
+# differing, genome longer by 22 nt on average), 4.66 end5, 4.05 end3, 77.4 genome gaps, 36.95 microexon
+# calls; Stage2_compute once per read over the read's gregion, as configs[2]
+ISOSEQ5K = Shape("isoseq5k", 10, 500, 0.01, 0.01, 285.1, 4.66, 4.05, 77.4, 36.95,
+                 "measured: reference gmap on 200 reads of this shape (profiles/r03_callmix/callmix.json)",
+                 single_indel=0.91, single_dmean=22.0)
 
 SINGLE_PER_READ = CDNA2K.single        # Dynprog_single_gap calls per 2-kb read (nosimd)
 END5_PER_READ = CDNA2K.end5            # Dynprog_end5_gap
@@ -184,12 +192,19 @@ def genomic_chars(genome, pos, watson, chroff, chrhigh):
     return np.where(watson, ch, COMPL[ch])
 
 
-def make_single(genome, layout, n, rng):
+def make_single(genome, layout, n, rng, shape=None):
     """Dynprog_single_gap sub-problems (stage3.c:9081): query slices with 2 % substitutions and
-    occasional 1-3 nt indels, extraband 6, wide band."""
+    occasional 1-3 nt indels (or, for shapes with single_dmean, a genome-minus-query excess drawn from an
+    exponential), extraband 6, wide band."""
     import gmapdp
+    shape = shape or CDNA2K
     g = np.clip(rng.gamma(3.0, 40.0, size=n).astype(np.int64), 1, 640)
-    d = np.where(rng.random(n) < 0.15, rng.integers(-3, 4, size=n), 0)
+    if shape.single_dmean > 0:
+        d = -np.rint(rng.exponential(shape.single_dmean, size=n)).astype(np.int64) - 1
+        d = np.where(rng.random(n) < shape.single_indel, d, 0)
+        d = np.maximum(d, 1 - g)
+    else:
+        d = np.where(rng.random(n) < shape.single_indel, rng.integers(-3, 4, size=n), 0)
     d = np.where(g + d < 1, 0, d)
     r = np.clip(g + d, 1, 660)
     d = r - g
@@ -432,7 +447,7 @@ def make_reads(genome, layout, reads, seed, site_seed=23, shape=CDNA2K, plant=Tr
     ns = int(round(reads * shape.single))
     n5 = int(round(reads * shape.end5))
     n3 = int(round(reads * shape.end3))
-    sp_, sq = make_single(genome, layout, ns, rng)
+    sp_, sq = make_single(genome, layout, ns, rng, shape)
     ep, eq = make_end(genome, layout, n5, n3, rng)
     ep["qoff"] += len(sq)
     gp["qoff"] += len(sq) + len(eq)

@@ -1,0 +1,165 @@
+/* oracle/callmix.c -- MEASUREMENT INFRASTRUCTURE ONLY (never linked into the product).
+ *
+ * Records the stream of calls GMAP's own per-read pipeline makes into the hot path, so that the
+ * synthetic bench workload (gmap-2024_amd/gmapdp/workload.py) can restate its per-read call mix and
+ * sub-problem sizes for a read shape (BASELINE configs[4]: 5-kb Iso-Seq reads) from a measurement
+ * instead of a guess.  Linked into the UNMODIFIED reference gmap program (oracle/ref.mk:
+ * _ref/gmap_callmix) with ld --wrap around the entry points; every wrapper appends one line to
+ * $GMAPDP_CALLMIX_LOG and calls the reference's own function (__real_), so the program's output is
+ * the reference's.  Line formats (tools/callmix.py parses them):
+ *   S rlength glength extraband widebandp            Dynprog_single_gap   (dynprog_single.c:429)
+ *   E5 / E3 rlength glength extraband endalign       Dynprog_end5/3_gap    (dynprog_end.c:1294/1924)
+ *   G rlength glengthL glengthR extraband finalp     Dynprog_genome_gap    (dynprog_genome.c:3288)
+ *   C rlengthL rlengthR glength                      Dynprog_cdna_gap      (dynprog_cdna.c:787)
+ *   M rlength intronlength                           Dynprog_microexon_int (dynprog_single.c:900)
+ *   T querylength chrend-chrstart                    Stage2_compute        (stage2.c:6325)
+ */
+#ifdef HAVE_CONFIG_H
+#include "config.h"
+#endif
+#include <stdio.h>
+#include <stdlib.h>
+#include <pthread.h>
+
+#include "gmapdp_dynprog.h"
+
+extern List_T __real_Dynprog_single_gap(int *, int *, int *, int *, int *, int *, Dynprog_T, char *, char *, int, int,
+                                        int, int, Univcoord_T, Univcoord_T, bool, int, bool, Genome_T, Genome_T,
+                                        Pairpool_T, int, bool, double);
+extern List_T __real_Dynprog_end5_gap(int *, int *, int *, int *, int *, int *, Dynprog_T, char *, char *, int, int,
+                                      int, int, Univcoord_T, Univcoord_T, bool, int, bool, Genome_T, Genome_T,
+                                      Pairpool_T, int, double, Endalign_T, bool);
+extern List_T __real_Dynprog_end3_gap(int *, int *, int *, int *, int *, int *, Dynprog_T, char *, char *, int, int,
+                                      int, int, Univcoord_T, Univcoord_T, bool, int, bool, Genome_T, Genome_T,
+                                      Pairpool_T, int, double, Endalign_T, bool);
+extern List_T __real_Dynprog_genome_gap(int *, int *, int *, double *, double *, int *, int *, int *, int *, int *,
+                                        int *, int *, Dynprog_T, Dynprog_T, char *, char *, int, int, int, int, int,
+                                        int, Chrnum_T, Univcoord_T, Univcoord_T, int, bool, int, bool, Genome_T,
+                                        Genome_T, Pairpool_T, int, double, int, bool, bool);
+extern List_T __real_Dynprog_cdna_gap(int *, int *, bool *, Dynprog_T, Dynprog_T, char *, char *, char *, char *, int,
+                                      int, int, int, int, int, Univcoord_T, Univcoord_T, bool, int, bool, Genome_T,
+                                      Genome_T, Pairpool_T, int, double);
+extern List_T __real_Dynprog_microexon_int(double *, double *, int *, int *, char *, char *, int, int, int, int, int,
+                                           char *, char *, Univcoord_T, Univcoord_T, bool, int, Genome_T, Genome_T,
+                                           Pairpool_T);
+extern List_T __real_Stage2_compute(char *, char *, int, int, Chrpos_T, Chrpos_T, Univcoord_T, Univcoord_T, bool, int,
+                                    Stage2_alloc_T, double, Oligoindex_array_T, Genome_T, Genome_T, Pairpool_T,
+                                    Diagpool_T, Cellpool_T, bool, bool, bool, int, Stopwatch_T, bool);
+
+static pthread_mutex_t cm_lock = PTHREAD_MUTEX_INITIALIZER;
+static FILE *cm_out = NULL;
+
+static void
+cm_log (const char *fmt, int a, int b, int c, int d, int e) {
+  pthread_mutex_lock(&cm_lock);
+  if (cm_out == NULL) {
+    const char *path = getenv("GMAPDP_CALLMIX_LOG");
+    cm_out = fopen(path ? path : "callmix.log", "w");
+  }
+  if (cm_out) fprintf(cm_out, fmt, a, b, c, d, e);
+  pthread_mutex_unlock(&cm_lock);
+}
+
+__attribute__((destructor)) static void
+cm_close (void) {
+  if (cm_out) fclose(cm_out);
+}
+
+List_T
+__wrap_Dynprog_single_gap (int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches, int *nopens,
+                           int *nindels, Dynprog_T dynprog, char *sequence1, char *sequenceuc1, int length1,
+                           int length2, int offset1, int offset2, Univcoord_T chroffset, Univcoord_T chrhigh,
+                           bool watsonp, int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
+                           Pairpool_T pairpool, int extraband_single, bool widebandp, double defect_rate) {
+  cm_log("S %d %d %d %d%.0d\n", length1, length2, extraband_single, widebandp ? 1 : 0, 0);
+  return __real_Dynprog_single_gap(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels, dynprog,
+                                   sequence1, sequenceuc1, length1, length2, offset1, offset2, chroffset, chrhigh,
+                                   watsonp, genestrand, jump_late_p, genome, genomealt, pairpool, extraband_single,
+                                   widebandp, defect_rate);
+}
+
+List_T
+__wrap_Dynprog_end5_gap (int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches, int *nopens,
+                         int *nindels, Dynprog_T dynprog, char *revsequence1, char *revsequenceuc1, int length1,
+                         int length2, int revoffset1, int revoffset2, Univcoord_T chroffset, Univcoord_T chrhigh,
+                         bool watsonp, int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
+                         Pairpool_T pairpool, int extraband_end, double defect_rate, Endalign_T endalign,
+                         bool require_pos_score_p) {
+  cm_log("E5 %d %d %d %d%.0d\n", length1, length2, extraband_end, (int) endalign, 0);
+  return __real_Dynprog_end5_gap(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels, dynprog,
+                                 revsequence1, revsequenceuc1, length1, length2, revoffset1, revoffset2, chroffset,
+                                 chrhigh, watsonp, genestrand, jump_late_p, genome, genomealt, pairpool, extraband_end,
+                                 defect_rate, endalign, require_pos_score_p);
+}
+
+List_T
+__wrap_Dynprog_end3_gap (int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches, int *nopens,
+                         int *nindels, Dynprog_T dynprog, char *sequence1, char *sequenceuc1, int length1,
+                         int length2, int offset1, int offset2, Univcoord_T chroffset, Univcoord_T chrhigh,
+                         bool watsonp, int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
+                         Pairpool_T pairpool, int extraband_end, double defect_rate, Endalign_T endalign,
+                         bool require_pos_score_p) {
+  cm_log("E3 %d %d %d %d%.0d\n", length1, length2, extraband_end, (int) endalign, 0);
+  return __real_Dynprog_end3_gap(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels, dynprog,
+                                 sequence1, sequenceuc1, length1, length2, offset1, offset2, chroffset, chrhigh,
+                                 watsonp, genestrand, jump_late_p, genome, genomealt, pairpool, extraband_end,
+                                 defect_rate, endalign, require_pos_score_p);
+}
+
+List_T
+__wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_rightgenomepos, double *left_prob,
+                           double *right_prob, int *traceback_score, int *nmatches, int *nmismatches, int *nopens,
+                           int *nindels, int *exonhead, int *introntype, Dynprog_T dynprogL, Dynprog_T dynprogR,
+                           char *rsequence, char *rsequenceuc, int rlength, int glengthL, int glengthR, int roffset,
+                           int goffsetL, int rev_goffsetR, Chrnum_T chrnum, Univcoord_T chroffset,
+                           Univcoord_T chrhigh, int cdna_direction, bool watsonp, int genestrand, bool jump_late_p,
+                           Genome_T genome, Genome_T genomealt, Pairpool_T pairpool, int extraband_paired,
+                           double defect_rate, int maxpeelback, bool halfp, bool finalp) {
+  cm_log("G %d %d %d %d %d\n", rlength, glengthL, glengthR, extraband_paired, finalp ? 1 : 0);
+  return __real_Dynprog_genome_gap(dynprogindex, new_leftgenomepos, new_rightgenomepos, left_prob, right_prob,
+                                   traceback_score, nmatches, nmismatches, nopens, nindels, exonhead, introntype,
+                                   dynprogL, dynprogR, rsequence, rsequenceuc, rlength, glengthL, glengthR, roffset,
+                                   goffsetL, rev_goffsetR, chrnum, chroffset, chrhigh, cdna_direction, watsonp,
+                                   genestrand, jump_late_p, genome, genomealt, pairpool, extraband_paired,
+                                   defect_rate, maxpeelback, halfp, finalp);
+}
+
+List_T
+__wrap_Dynprog_cdna_gap (int *dynprogindex, int *traceback_score, bool *incompletep, Dynprog_T dynprogL,
+                         Dynprog_T dynprogR, char *rsequenceL, char *rsequence_ucL, char *rev_rsequenceR,
+                         char *rev_rsequence_ucR, int rlengthL, int rlengthR, int glength, int roffsetL,
+                         int rev_roffsetR, int goffset, Univcoord_T chroffset, Univcoord_T chrhigh, bool watsonp,
+                         int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
+                         Pairpool_T pairpool, int extraband_paired, double defect_rate) {
+  cm_log("C %d %d %d%.0d%.0d\n", rlengthL, rlengthR, glength, 0, 0);
+  return __real_Dynprog_cdna_gap(dynprogindex, traceback_score, incompletep, dynprogL, dynprogR, rsequenceL,
+                                 rsequence_ucL, rev_rsequenceR, rev_rsequence_ucR, rlengthL, rlengthR, glength,
+                                 roffsetL, rev_roffsetR, goffset, chroffset, chrhigh, watsonp, genestrand,
+                                 jump_late_p, genome, genomealt, pairpool, extraband_paired, defect_rate);
+}
+
+List_T
+__wrap_Dynprog_microexon_int (double *bestprob2, double *bestprob3, int *dynprogindex, int *microintrontype,
+                              char *rsequence, char *rsequenceuc, int rlength, int roffset, int goffsetL,
+                              int rev_goffsetR, int cdna_direction, char *queryseq, char *queryuc,
+                              Univcoord_T chroffset, Univcoord_T chrhigh, bool watsonp, int genestrand,
+                              Genome_T genome, Genome_T genomealt, Pairpool_T pairpool) {
+  cm_log("M %d %d%.0d%.0d%.0d\n", rlength, rev_goffsetR - goffsetL + 1, 0, 0, 0);
+  return __real_Dynprog_microexon_int(bestprob2, bestprob3, dynprogindex, microintrontype, rsequence, rsequenceuc,
+                                      rlength, roffset, goffsetL, rev_goffsetR, cdna_direction, queryseq, queryuc,
+                                      chroffset, chrhigh, watsonp, genestrand, genome, genomealt, pairpool);
+}
+
+List_T
+__wrap_Stage2_compute (char *queryseq_ptr, char *queryuc_ptr, int querylength, int query_offset, Chrpos_T chrstart,
+                       Chrpos_T chrend, Univcoord_T chroffset, Univcoord_T chrhigh, bool plusp, int genestrand,
+                       Stage2_alloc_T stage2_alloc, double proceed_pctcoverage, Oligoindex_array_T oligoindices,
+                       Genome_T genome, Genome_T genomealt, Pairpool_T pairpool, Diagpool_T diagpool,
+                       Cellpool_T cellpool, bool localp, bool skip_repetitive_p, bool favor_right_p,
+                       int max_nalignments, Stopwatch_T stopwatch, bool diag_debug) {
+  cm_log("T %d %d%.0d%.0d%.0d\n", querylength, (int) (chrend - chrstart), 0, 0, 0);
+  return __real_Stage2_compute(queryseq_ptr, queryuc_ptr, querylength, query_offset, chrstart, chrend, chroffset,
+                               chrhigh, plusp, genestrand, stage2_alloc, proceed_pctcoverage, oligoindices, genome,
+                               genomealt, pairpool, diagpool, cellpool, localp, skip_repetitive_p, favor_right_p,
+                               max_nalignments, stopwatch, diag_debug);
+}

@@ -163,7 +163,18 @@ $(OUT)/gpushim_$(1)/gmapdp_gmap_shim.o: $(SHIM_SRC) ../include/gmapdp.h
 endef
 $(foreach v,$(PROG_VARIANTS),$(eval $(call prog_rules,$(v))))
 
-programs: $(foreach v,$(PROG_VARIANTS),$(OUT)/gmap_$(v)) \
+programs: $(foreach v,$(PROG_VARIANTS),$(OUT)/gmap_$(v)) $(OUT)/gmap_callmix \
           $(if $(wildcard $(GMAPDP_LIB)/libgmapdp.so),$(foreach v,$(PROG_VARIANTS),$(OUT)/gmap_gpu_$(v)))
+
+# The unmodified nosimd gmap with the hot-path entry points counted (callmix.c: one log line per call,
+# then the reference's own function): the measured per-read call mix of a read shape (tools/callmix.py)
+CALLMIX := Dynprog_single_gap Dynprog_end5_gap Dynprog_end3_gap Dynprog_genome_gap Dynprog_cdna_gap \
+           Dynprog_microexon_int Stage2_compute
+$(OUT)/callmix/callmix.o: callmix.c ../include/gmapdp_dynprog.h
+	@mkdir -p $(dir $@)
+	$(CC) $(BASEFLAGS) -DHAVE_CONFIG_H -I../include -c $< -o $@
+
+$(OUT)/gmap_callmix: $(PROGOBJS_nosimd) $(OUT)/callmix/callmix.o
+	$(CC) -pthread -s $(foreach w,$(CALLMIX),-Wl,--wrap=$(w)) -o $@ $^ -lz -lm
 
 .PHONY: all programs
