@@ -173,6 +173,8 @@ def rocprof_name(kind, R, dl, lds=0):
         return "gmapdp::uxe_kernel<%d>" % R
     if kind == 5:
         return "gmapdp::uxg_kernel<%d>" % R
+    if R == 1:  # bands <= 64: gg2_kernel<DIRS_LDS> (gg2_kernel.hip)
+        return "gmapdp::gg2_kernel<%s>" % ("true" if dl else "false")
     return "gmapdp::gg_kernel<%d, %s>" % (R, "true" if dl else "false")
 
 
@@ -283,7 +285,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--reads", type=int, default=10000, help="reads per step per GPU (one block)")
+    ap.add_argument("--reads", type=int, default=None,
+                    help="reads per step per GPU (one block; default 10000, 2000 for --config 4's 5-kb reads)")
     ap.add_argument("--batches", type=int, default=8, help="distinct read blocks per rank, cycled over the steps")
     ap.add_argument("--config", type=int, default=2, choices=[2, 4], help="BASELINE.json configs index")
     ap.add_argument("--genome", default="grch38", choices=["grch38", "chr22"], help="configs[2] genome layout")
@@ -292,6 +295,8 @@ def main():
     ap.add_argument("--dry-run", action="store_true", help="CPU only: launcher, gloo process group, sharding")
     args = ap.parse_args()
 
+    if args.reads is None:
+        args.reads = 2000 if args.config == 4 else 10000
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
