@@ -263,6 +263,8 @@ struct gmapdp_ctx {
   uint32_t* d_genome = nullptr;
   uint64_t genome_words = 0;
   uint64_t genome_length = 0;
+  bool genome_owned = true;  // false: another context's HBM genome (gmapdp_share_genome)
+  bool one_stream = false;   // GMAPDP_CTX_ONE_STREAM: no side streams (callers that run many contexts)
   DevBuf probs, order, qseq, qseq_uc, results, pairs, gdirs;
   DevBuf din, dout;    // run_batch: all inputs / all outputs of one synchronous batch
   HostBuf hin, hout;   // their pinned host images
@@ -336,6 +338,11 @@ void gmapdp_compute_bands(int* lband, int* uband, int rlength, int glength, int 
 const char* gmapdp_last_error(gmapdp_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
 int gmapdp_create(gmapdp_ctx** out, int device, int mode, int user_open, int user_extend, int user_dynprog_p) {
+  return gmapdp_create_ex(out, device, mode, user_open, user_extend, user_dynprog_p, 0);
+}
+
+int gmapdp_create_ex(gmapdp_ctx** out, int device, int mode, int user_open, int user_extend, int user_dynprog_p,
+                     int flags) {
   if (!out || mode < 0 || mode > 6) return GMAPDP_EINVAL;
   *out = nullptr;
   int ndev = 0;
@@ -346,13 +353,24 @@ int gmapdp_create(gmapdp_ctx** out, int device, int mode, int user_open, int use
   ctx->user_open = user_open;
   ctx->user_extend = user_extend;
   ctx->user_dynprog_p = user_dynprog_p;
+  ctx->one_stream = (flags & GMAPDP_CTX_ONE_STREAM) != 0;
   hipError_t e = hipSetDevice(device);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
-  for (int i = 0; i < gmapdp_ctx::kAux && e == hipSuccess; i++) {
+  int prio_least = 0, prio_greatest = 0;
+  if (e == hipSuccess && (flags & (GMAPDP_CTX_PRIO_HIGH | GMAPDP_CTX_PRIO_LOW)))
+    e = hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
+  if (e == hipSuccess) {
+    if (flags & GMAPDP_CTX_PRIO_HIGH)
+      e = hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_greatest);
+    else if (flags & GMAPDP_CTX_PRIO_LOW)
+      e = hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_least);
+    else
+      e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  }
+  for (int i = 0; i < gmapdp_ctx::kAux && e == hipSuccess && !ctx->one_stream; i++) {
     e = hipStreamCreateWithFlags(&ctx->aux[i], hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join[i], hipEventDisableTiming);
   }
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
+  if (e == hipSuccess && !ctx->one_stream) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
   ctx->tables = new Tables();
   build_tables(*ctx->tables, mode);
   if (e == hipSuccess) e = hipMalloc(&ctx->d_sc, sizeof(ctx->tables->sc));
@@ -376,7 +394,7 @@ void gmapdp_destroy(gmapdp_ctx* ctx) {
   if (ctx->d_sc) (void)hipFree(ctx->d_sc);
   if (ctx->d_cs) (void)hipFree(ctx->d_cs);
   if (ctx->d_isc) (void)hipFree(ctx->d_isc);
-  if (ctx->d_genome) (void)hipFree(ctx->d_genome);
+  if (ctx->d_genome && ctx->genome_owned) (void)hipFree(ctx->d_genome);
   for (int i = 0; i < gmapdp_ctx::kAux; i++) {
     if (ctx->aux[i]) (void)hipStreamSynchronize(ctx->aux[i]);
     if (ctx->aux[i]) (void)hipStreamDestroy(ctx->aux[i]);
@@ -440,14 +458,27 @@ int gmapdp_set_genome(gmapdp_ctx* ctx, const uint32_t* blocks, size_t nwords, ui
   if (!ctx || !blocks || nwords < (size_t)((length + 31) / 32) * 3) return GMAPDP_EINVAL;
   // coordinates are 64-bit (gmapdp_coord_t): gmapl genomes past 2^32 nt are supported
   (void)hipSetDevice(ctx->device);
-  if (ctx->d_genome) (void)hipFree(ctx->d_genome);
+  if (ctx->d_genome && ctx->genome_owned) (void)hipFree(ctx->d_genome);
   ctx->d_genome = nullptr;
+  ctx->genome_owned = true;
   hipError_t e = hipMalloc(&ctx->d_genome, nwords * sizeof(uint32_t));
   if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "hipMalloc genome: %s", e);
   e = hipMemcpy(ctx->d_genome, blocks, nwords * sizeof(uint32_t), hipMemcpyHostToDevice);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "genome upload: %s", e);
   ctx->genome_words = nwords;
   ctx->genome_length = length;
+  return GMAPDP_OK;
+}
+
+int gmapdp_share_genome(gmapdp_ctx* ctx, const gmapdp_ctx* owner) {
+  if (!ctx || !owner || ctx == owner || ctx->device != owner->device) return GMAPDP_EINVAL;
+  if (!owner->d_genome) return GMAPDP_ENOGENOME;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->d_genome && ctx->genome_owned) (void)hipFree(ctx->d_genome);
+  ctx->d_genome = owner->d_genome;
+  ctx->genome_words = owner->genome_words;
+  ctx->genome_length = owner->genome_length;
+  ctx->genome_owned = false;
   return GMAPDP_OK;
 }
 
@@ -514,6 +545,14 @@ static size_t gg_lds_dirs_max() {
 }
 // gg2_kernel (bands <= 64): its packed direction words stay in LDS while the workgroup's LDS stays
 // within this (GMAPDP_GG2_LDS_MAX overrides it); larger problems write them to the global scratch.
+static size_t latency_batch() {
+  static const size_t v = env_size("GMAPDP_LATENCY_BATCH", 1024);
+  return v;
+}
+static bool gg2_enabled() {  // GMAPDP_GG2=0 routes bands <= 64 to gg_kernel<1> instead (experiments)
+  static const bool v = env_size("GMAPDP_GG2", 1) != 0;
+  return v;
+}
 static size_t gg2_lds_max() {
   static const size_t v = env_size("GMAPDP_GG2_LDS_MAX", 24 * 1024);
   return v;
@@ -764,6 +803,19 @@ static int convert_genome(gmapdp_ctx* ctx, const gmapdp_genome_problem& p, gmapd
 static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
   std::map<std::tuple<int, int, int, size_t>, std::vector<int>> classes;  // (kind, R, dirs_lds, lds bucket)
   size_t pair_off = 0, gdirs_off = 0;
+  // Latency mode (small batches: the GMAP drop-in's dispatcher batches): one launch class per (kind, R,
+  // direction placement) with the LDS of its largest member, and no packed narrow-band kernels, so a
+  // batch is a few launches whose latencies do not add up class after class.
+  const bool latency = plan.dev.size() + plan.gdev.size() <= latency_batch();
+  std::vector<size_t> need(plan.dev.size(), 0), gneed(plan.gdev.size(), 0);
+  auto add = [&](int kind, int R, int dl, size_t bucket, size_t s) {
+    need[s] = bucket;
+    classes[std::make_tuple(kind, R, dl, latency ? (size_t)0 : bucket)].push_back((int)s);
+  };
+  auto gadd = [&](int kind, int R, int dl, size_t bucket, size_t s) {
+    gneed[s] = bucket;
+    classes[std::make_tuple(kind, R, dl, latency ? (size_t)0 : bucket)].push_back((int)s);
+  };
   for (size_t s = 0; s < plan.dev.size(); s++) {
     DevProblem& d = plan.dev[s];
     d.pair_offset = (int32_t)pair_off;
@@ -777,7 +829,7 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
       if (lds > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
       d.dirs_offset = (int64_t)gdirs_off;
       gdirs_off += (scratch_bytes_uxe(d.rlength, d.glength, d.lband, d.uband, B) + 255) & ~(size_t)255;
-      classes[std::make_tuple((int)PlanCore::kUxe, B, 0, gg_lds_bucket(lds))].push_back((int)s);
+      add((int)PlanCore::kUxe, B, 0, gg_lds_bucket(lds), s);
       continue;
     }
     if (d.flags & kFSimd) {
@@ -787,18 +839,18 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
       const int B = (d.rlength < use8p[d.mismatchtype] && d.glength < use8p[d.mismatchtype]) ? 32 : 16;
       const size_t slot = gg_lds_bucket(lds_slot_sx(d.rlength, d.glength, B));
       if (slot * (64 / B) > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
-      classes[std::make_tuple((int)PlanCore::kSx, B, 0, slot)].push_back((int)s);
+      add((int)PlanCore::kSx, B, 0, slot, s);
       continue;
     }
     if (d.open > 0 && !nofill) return bad(ctx, "positive gap-open penalty is not supported by the scan formulation");
     if (d.lband < 0 || d.uband < 0) return bad(ctx, "negative band");
     const int W = d.lband + d.uband + 1;
     d.dirs_offset = 0;
-    if (nofill || W <= 32) {  // narrow band: pack 64/S problems per wave
+    if (!latency && (nofill || W <= 32)) {  // narrow band: pack 64/S problems per wave
       const int S = (nofill || W <= 16) ? 16 : 32;
       const size_t slot = slot_bucket(lds_slot_dpx(d.rlength, d.glength));
       if (slot && slot * (64 / S) + lds_dirs_dpx(d.glength) <= kLdsBudget) {
-        classes[std::make_tuple((int)PlanCore::kDpx, S, 1, slot)].push_back((int)s);
+        add((int)PlanCore::kDpx, S, 1, slot, s);
         continue;
       }
     }
@@ -815,7 +867,7 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
       }
     }
     if (lds > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
-    classes[std::make_tuple((int)PlanCore::kDp, R, dirs_lds ? 1 : 0, lds_bucket(lds))].push_back((int)s);
+    add((int)PlanCore::kDp, R, dirs_lds ? 1 : 0, lds_bucket(lds), s);
   }
   for (size_t s = 0; s < plan.gdev.size(); s++) {
     DevGenomeProblem& d = plan.gdev[s];
@@ -831,7 +883,7 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
       if (lds > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
       d.dirs_offset = (int64_t)gdirs_off;
       gdirs_off += (scratch_bytes_uxg(d.rlength, d.glengthL, d.glengthR, d.lbandL, B) + 255) & ~(size_t)255;
-      classes[std::make_tuple((int)PlanCore::kUxg, B, 0, gg_lds_bucket(lds))].push_back((int)s);
+      gadd((int)PlanCore::kUxg, B, 0, gg_lds_bucket(lds), s);
       continue;
     }
     if (d.open > 0) return bad(ctx, "positive gap-open penalty is not supported by the scan formulation");
@@ -847,19 +899,19 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
       }
       d.dirs_offset = (int64_t)gdirs_off;
       gdirs_off += (scratch_bytes_ggp(d.rlength, d.glengthL, d.glengthR) + 255) & ~(size_t)255;
-      classes[std::make_tuple((int)PlanCore::kGgp, RR, 0, (size_t)S)].push_back((int)s);
+      gadd((int)PlanCore::kGgp, RR, 0, (size_t)S, s);
       continue;
     }
     const int R = pick_R(std::max(WL, WR));
     if (R > kMaxR) return bad(ctx, "band wider than 4096");
-    if (R == 1) {  // gg2_kernel: operands fetched a column ahead, packed direction words
+    if (R == 1 && gg2_enabled()) {  // gg2_kernel: operands fetched a column ahead, packed direction words
       size_t lds = lds_bytes_gg2(d.rlength, d.glengthL, d.glengthR, WL, WR, true);
       const bool dirs_lds = lds <= gg2_lds_max();
       if (!dirs_lds) lds = lds_bytes_gg2(d.rlength, d.glengthL, d.glengthR, WL, WR, false);
       d.dirs_offset = (int64_t)gdirs_off;
       gdirs_off += (scratch_bytes_gg2(d.glengthL, d.glengthR, WL, WR, dirs_lds) + 255) & ~(size_t)255;
       if (lds > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
-      classes[std::make_tuple((int)PlanCore::kGenomeGap, 1, dirs_lds ? 1 : 0, gg_lds_bucket(lds))].push_back((int)s);
+      gadd((int)PlanCore::kGenomeGap, 1, dirs_lds ? 1 : 0, gg_lds_bucket(lds), s);
       continue;
     }
     size_t lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, true);
@@ -868,7 +920,7 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     d.dirs_offset = (int64_t)gdirs_off;  // bridge candidates (+ direction planes) in global scratch
     gdirs_off += (scratch_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, dirs_lds) + 255) & ~(size_t)255;
     if (lds > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
-    classes[std::make_tuple((int)PlanCore::kGenomeGap, R, dirs_lds ? 1 : 0, gg_lds_bucket(lds))].push_back((int)s);
+    gadd((int)PlanCore::kGenomeGap, R, dirs_lds ? 1 : 0, gg_lds_bucket(lds), s);
   }
   for (auto& kv : classes) {
     PlanCore::Launch L;
@@ -879,6 +931,12 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     L.count = (int)kv.second.size();
     // longest problems first, so the tail of the launch is short work
     std::vector<int> ids = kv.second;
+    if (latency) {  // the class's LDS: its largest member's
+      const bool g = L.kind == PlanCore::kGenomeGap || L.kind == PlanCore::kUxg || L.kind == PlanCore::kGgp;
+      size_t m = 0;
+      for (int id : ids) m = std::max(m, g ? gneed[id] : need[id]);
+      L.lds = m;
+    }
     if (L.kind != PlanCore::kGenomeGap && L.kind != PlanCore::kUxg && L.kind != PlanCore::kGgp) {
       std::stable_sort(ids.begin(), ids.end(), [&](int a, int b) {
         return (size_t)plan.dev[a].glength * (plan.dev[a].lband + plan.dev[a].uband + 1) >
@@ -1077,7 +1135,7 @@ static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, cons
     return launch_ggp((int)L.lds, L.R, L.count, stream, a.d_gprobs, a.d_gorder + L.first, ctx->d_genome,
                       ctx->genome_words, a.d_q, a.d_quc, a.d_sprob, ctx->d_sc, ctx->d_cs, ctx->d_isc, a.d_gresults,
                       a.d_pairs, (unsigned char*)ctx->gdirs.p);
-  if (L.R == 1)
+  if (L.R == 1 && gg2_enabled())
     return launch_gg2(L.dirs_lds, L.count, L.lds, stream, a.d_gprobs, a.d_gorder + L.first, ctx->d_genome,
                       ctx->genome_words, a.d_q, a.d_quc, a.d_sprob, ctx->d_sc, ctx->d_cs, ctx->d_isc, a.d_gresults,
                       a.d_pairs, (unsigned char*)ctx->gdirs.p);
@@ -1095,7 +1153,7 @@ static int run_plan(gmapdp_ctx* ctx, const PlanCore& plan, const RunArgs& a, hip
   // its assigned stream; join: `stream` waits for the side streams.  A small batch (the drop-in's
   // dispatcher batches) runs on `stream` alone: a process has few hardware queues (GPU_MAX_HW_QUEUES)
   // and several dispatcher contexts share them.
-  const bool one_stream = plan.dev.size() + plan.gdev.size() < 2048;
+  const bool one_stream = ctx->one_stream || plan.dev.size() + plan.gdev.size() < 2048;
   hipError_t e = one_stream ? hipSuccess : hipEventRecord(ctx->ev_fork, stream);
   bool used[gmapdp_ctx::kAux] = {false, false, false};
   for (size_t li = 0; li < plan.launches.size() && e == hipSuccess; li++) {
@@ -1253,7 +1311,8 @@ size_t gmapdp_genome_prob_entries(const gmapdp_genome_problem* problems, int n) 
 }
 
 // The Maxent_hr_*_prob call of each probability entry (bridge_intron_gap_site_level,
-// dynprog_genome.c:2573-2660; get_splicesite_probs :332-401).  Univcoord_T is 32-bit.
+// dynprog_genome.c:2573-2660; get_splicesite_probs :332-401).  Positions are 64-bit universal
+// coordinates (gmapdp_coord_t), as gmapl's Univcoord_T.
 int gmapdp_genome_splice_sites(const gmapdp_genome_problem* problems, int n, gmapdp_coord_t* positions, uint8_t* models,
                                size_t nentries) {
   if (n < 0 || (n && (!problems || !positions || !models))) return GMAPDP_EINVAL;

@@ -18,6 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GMAPDP_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libgmapdp.so")
 
 WATSON, JUMP_LATE, WIDEBAND = 0x1, 0x2, 0x4
+CTX_ONE_STREAM, CTX_PRIO_HIGH, CTX_PRIO_LOW = 0x1, 0x2, 0x4  # gmapdp_create_ex flags
 SIMD = 0x40  # GMAPDP_SIMD: the reference's SIMD builds' semantics (every problem family)
 HALFP, FINALP = 0x8, 0x10
 UNSET = -2147483648
@@ -161,6 +162,8 @@ def load_library(path=LIB_PATH):
     sig = {
         "gmapdp_create": (C.c_int, [P(C.c_void_p), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
         "gmapdp_destroy": (None, [C.c_void_p]),
+        "gmapdp_create_ex": (C.c_int, [P(C.c_void_p), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
+        "gmapdp_share_genome": (C.c_int, [C.c_void_p, C.c_void_p]),
         "gmapdp_genome_words": (C.c_size_t, [C.c_uint64]),
         "gmapdp_debug_stage2_scratch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
         "gmapdp_stage2_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_char_p, C.c_char_p, C.c_size_t,
@@ -315,10 +318,11 @@ def genome_splice_sites(probs):
 class Engine:
     """One Dynprog engine context on one GPU (mirrors a GMAP worker's Dynprog_T)."""
 
-    def __init__(self, device=0, mode=0, user_open=0, user_extend=0, user_dynprog_p=False):
+    def __init__(self, device=0, mode=0, user_open=0, user_extend=0, user_dynprog_p=False, flags=0):
         self.lib = load_library()
         h = C.c_void_p()
-        rc = self.lib.gmapdp_create(C.byref(h), device, mode, user_open, user_extend, int(bool(user_dynprog_p)))
+        rc = self.lib.gmapdp_create_ex(C.byref(h), device, mode, user_open, user_extend, int(bool(user_dynprog_p)),
+                                       flags)
         if rc:
             raise GmapdpError("gmapdp_create failed (%d): no usable HIP device %d?" % (rc, device))
         self.h = h
@@ -338,6 +342,11 @@ class Engine:
     def _check(self, rc, what):
         if rc:
             raise GmapdpError("%s failed (%d): %s" % (what, rc, self.lib.gmapdp_last_error(self.h).decode()))
+
+    def share_genome(self, owner):
+        """Use `owner`'s HBM genome (gmapdp_share_genome); `owner` must stay open meanwhile."""
+        self._check(self.lib.gmapdp_share_genome(self.h, owner.h), "gmapdp_share_genome")
+        self.genome_length = owner.genome_length
 
     def set_genome(self, seq: bytes = None, blocks: np.ndarray = None, length: int = None):
         if blocks is None:

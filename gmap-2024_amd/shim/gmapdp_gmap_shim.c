@@ -30,9 +30,10 @@
  *
  * Batching.  GMAP's worker threads (gmap.c:4867) each issue their calls one at a time and wait for
  * the answer (the API is synchronous).  Here a call becomes a request on a process-wide queue and the
- * calling thread sleeps on it.  GMAPDP_SHIM_DISPATCHERS (default 4) dispatcher threads each own an
- * engine context (its own streams and HBM copy of the genome), so that many batches are in flight;
- * stage-2 calls have their own queue and GMAPDP_SHIM_STAGE2_DISPATCHERS (default 2) dispatchers;
+ * calling thread sleeps on it.  GMAPDP_SHIM_DISPATCHERS (default 3) dispatcher threads each own an
+ * engine context with one high-priority stream (the genome is uploaded to HBM once and shared), so
+ * that several batches are in flight; stage-2 calls have their own queue and
+ * GMAPDP_SHIM_STAGE2_DISPATCHERS (default 1) dispatchers on low-priority streams;
  * a free dispatcher takes every request queued meanwhile and runs them together: all single / end /
  * genome gaps in one gmapdp_dynprog_batch, cDNA gaps and stage-2 seeding in their own batches.  The
  * callers then build their List_T from their own results in their own Pairpool.  With many worker
@@ -197,7 +198,16 @@ shim_check_call (Genome_T genome, Genome_T genomealt, Dynprog_T dynprog) {
     shim_refuse("a Dynprog_T with non-default maximum lengths");
 }
 
-/* The engine context with `genome` resident in HBM (dispatcher thread only). */
+/* The engine context with `genome` resident in HBM (dispatcher thread only).  Every dispatcher owns a
+   context with a single stream -- DP dispatchers at the device's highest stream priority, stage-2
+   dispatchers at its lowest -- so that dispatchers x 1 streams fit the process's hardware queues
+   (GPU_MAX_HW_QUEUES) and a DP batch never queues behind a stage-2 sweep.  The genome is uploaded to
+   HBM once, by the first dispatcher that needs it; the others share that copy (gmapdp_share_genome). */
+static __thread int shim_qi = 0;            /* the dispatcher's queue: 0 Dynprog_*, 1 stage 2 */
+static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
+static gmapdp_ctx *g_owner = NULL;          /* the context holding the HBM genome */
+static Genome_T g_owner_genome = NULL;
+
 static gmapdp_ctx *
 shim_context (Genome_T genome) {
   const char *dev;
@@ -205,14 +215,26 @@ shim_context (Genome_T genome) {
   size_t nwords;
   if (shim_ctx == NULL) {
     dev = getenv("GMAPDP_DEVICE");
-    shim_check(gmapdp_create(&shim_ctx, dev ? atoi(dev) : 0, shim_mode, shim_user_open, shim_user_extend,
-                             shim_user_dynprog_p), "gmapdp_create");
+    shim_check(gmapdp_create_ex(&shim_ctx, dev ? atoi(dev) : 0, shim_mode, shim_user_open, shim_user_extend,
+                                shim_user_dynprog_p,
+                                GMAPDP_CTX_ONE_STREAM | (shim_qi == 0 ? GMAPDP_CTX_PRIO_HIGH : GMAPDP_CTX_PRIO_LOW)),
+               "gmapdp_create_ex");
   }
   if (genome != shim_genome) {
-    length = (uint64_t) Genome_genomelength(genome);
-    nwords = gmapdp_genome_words(length);
-    shim_check(gmapdp_set_genome(shim_ctx, (const uint32_t *) Genome_blocks(genome), nwords, length),
-               "gmapdp_set_genome");
+    pthread_mutex_lock(&g_lock);
+    if (g_owner != NULL && g_owner_genome == genome) {
+      if (g_owner != shim_ctx) shim_check(gmapdp_share_genome(shim_ctx, g_owner), "gmapdp_share_genome");
+    } else if (g_owner == NULL) {
+      length = (uint64_t) Genome_genomelength(genome);
+      nwords = gmapdp_genome_words(length);
+      shim_check(gmapdp_set_genome(shim_ctx, (const uint32_t *) Genome_blocks(genome), nwords, length),
+                 "gmapdp_set_genome");
+      g_owner = shim_ctx;
+      g_owner_genome = genome;
+    } else {
+      shim_refuse("a second genome in one process");
+    }
+    pthread_mutex_unlock(&g_lock);
     shim_genome = genome;
   }
   return shim_ctx;
@@ -308,6 +330,7 @@ static void *
 shim_dispatch (void *arg) {
   shim_req *batch, *r, *next;
   const int qi = (int) (intptr_t) arg;
+  shim_qi = qi;
   for (;;) {
     pthread_mutex_lock(&q_lock);
     while (q_head[qi] == NULL) pthread_cond_wait(&q_cond[qi], &q_lock);
@@ -338,11 +361,12 @@ shim_submit (shim_req *r) {
   if (!dispatcher_started) {
     st = getenv("GMAPDP_SHIM_STATS");
     if (st != NULL && st[0] == '1') atexit(shim_print_stats);
+    /* 3 + 1 streams: HIP's default of four hardware queues per process, one per dispatcher */
     st = getenv("GMAPDP_SHIM_DISPATCHERS");
-    nd = st != NULL ? atoi(st) : 4;
+    nd = st != NULL ? atoi(st) : 3;
     if (nd < 1) nd = 1;
     st = getenv("GMAPDP_SHIM_STAGE2_DISPATCHERS");
-    nd2 = st != NULL ? atoi(st) : 2;
+    nd2 = st != NULL ? atoi(st) : 1;
     if (nd2 < 1) nd2 = 1;
     pthread_attr_init(&attr);
     pthread_attr_setdetachstate(&attr, PTHREAD_CREATE_DETACHED);

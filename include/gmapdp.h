@@ -46,7 +46,12 @@
  * scratch buffers, fork/join events and side streams) and every plan created on
  * it must be used by one host thread at a time, and a plan must not run on two
  * streams at once (its pool counter and the context scratch are shared).  Use
- * one context per thread, or serialise (the GMAP shim does the latter).
+ * one context per thread, or serialise.  The GMAP shim gives each of its
+ * dispatcher threads its own context (gmapdp_create_ex: one stream each, DP
+ * dispatchers at high priority, stage-2 dispatchers at low priority) and
+ * uploads the genome to HBM once: the other contexts share that copy
+ * (gmapdp_share_genome), so GRCh38 costs 1.16 GB of HBM and a 17-Gnt genome
+ * 6.4 GB whatever the number of dispatchers.
  */
 #ifndef GMAPDP_H
 #define GMAPDP_H
@@ -534,6 +539,18 @@ void gmapdp_stage2_plan_destroy (gmapdp_stage2_plan *plan);
 int gmapdp_create (gmapdp_ctx **ctx, int device, int mode,
                    int user_open, int user_extend, int user_dynprog_p);
 void gmapdp_destroy (gmapdp_ctx *ctx);
+/* gmapdp_create with flags, for callers that run several contexts at once (the GMAP drop-in's
+ * dispatcher threads): GMAPDP_CTX_ONE_STREAM creates no side streams (a process has few hardware
+ * queues, GPU_MAX_HW_QUEUES, and streams beyond them share one and serialise); GMAPDP_CTX_PRIO_HIGH /
+ * _LOW create the context's stream at the device's highest / lowest priority. */
+#define GMAPDP_CTX_ONE_STREAM 0x1
+#define GMAPDP_CTX_PRIO_HIGH  0x2
+#define GMAPDP_CTX_PRIO_LOW   0x4
+int gmapdp_create_ex (gmapdp_ctx **ctx, int device, int mode, int user_open, int user_extend, int user_dynprog_p,
+                      int flags);
+/* Use `owner`'s HBM-resident genome in `ctx` (no copy; same device).  `owner` must outlive every
+ * context sharing its genome and keep that genome until they are done. */
+int gmapdp_share_genome (gmapdp_ctx *ctx, const gmapdp_ctx *owner);
 
 /* Words needed for a packed genome of `length` nt ((len+31)/32*3 + 4). */
 size_t gmapdp_genome_words (uint64_t length);
