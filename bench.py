@@ -173,8 +173,6 @@ def rocprof_name(kind, R, dl, lds=0):
         return "gmapdp::uxe_kernel<%d>" % R
     if kind == 5:
         return "gmapdp::uxg_kernel<%d>" % R
-    if R == 1:  # bands <= 64: gg2_kernel<DIRS_LDS> (gg2_kernel.hip)
-        return "gmapdp::gg2_kernel<%s>" % ("true" if dl else "false")
     return "gmapdp::gg_kernel<%d, %s>" % (R, "true" if dl else "false")
 
 

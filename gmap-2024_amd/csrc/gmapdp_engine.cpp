@@ -44,13 +44,6 @@ hipError_t launch_dpx(int S, int nproblems, int slot, int dirs_bytes, unsigned c
 size_t lds_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds);
 size_t scratch_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds);
 size_t scratch_bytes_ggp(int rlength, int glengthL, int glengthR);
-size_t lds_bytes_gg2(int rlength, int glengthL, int glengthR, int WL, int WR, bool dirs_lds);
-size_t scratch_bytes_gg2(int glengthL, int glengthR, int WL, int WR, bool dirs_lds);
-hipError_t launch_gg2(bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevGenomeProblem* probs,
-                      const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
-                      const char* qseq_uc, const double* sprob, const int8_t* sctab, const uint8_t* constab,
-                      const int8_t* isctab, gmapdp_genome_result* results, gmapdp_pair* pairs,
-                      unsigned char* gscratch);
 size_t chunk_bytes_ggp(int gmax, int S, int R);
 hipError_t launch_ggp(int S, int R, int count, hipStream_t stream, const DevGenomeProblem* probs, const int* order,
                       const uint32_t* blocks, uint64_t nwords, const char* qseq, const char* qseq_uc,
@@ -543,18 +536,10 @@ static size_t gg_lds_dirs_max() {
   static const size_t v = env_size("GMAPDP_GG_LDS_DIRS_MAX", 0);
   return v;
 }
-// gg2_kernel (bands <= 64): its packed direction words stay in LDS while the workgroup's LDS stays
-// within this (GMAPDP_GG2_LDS_MAX overrides it); larger problems write them to the global scratch.
+// Batches of at most this many problems are planned for latency (classify); GMAPDP_LATENCY_BATCH
+// overrides it.
 static size_t latency_batch() {
   static const size_t v = env_size("GMAPDP_LATENCY_BATCH", 1024);
-  return v;
-}
-static bool gg2_enabled() {  // GMAPDP_GG2=0 routes bands <= 64 to gg_kernel<1> instead (experiments)
-  static const bool v = env_size("GMAPDP_GG2", 1) != 0;
-  return v;
-}
-static size_t gg2_lds_max() {
-  static const size_t v = env_size("GMAPDP_GG2_LDS_MAX", 24 * 1024);
   return v;
 }
 
@@ -904,16 +889,6 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     }
     const int R = pick_R(std::max(WL, WR));
     if (R > kMaxR) return bad(ctx, "band wider than 4096");
-    if (R == 1 && gg2_enabled()) {  // gg2_kernel: operands fetched a column ahead, packed direction words
-      size_t lds = lds_bytes_gg2(d.rlength, d.glengthL, d.glengthR, WL, WR, true);
-      const bool dirs_lds = lds <= gg2_lds_max();
-      if (!dirs_lds) lds = lds_bytes_gg2(d.rlength, d.glengthL, d.glengthR, WL, WR, false);
-      d.dirs_offset = (int64_t)gdirs_off;
-      gdirs_off += (scratch_bytes_gg2(d.glengthL, d.glengthR, WL, WR, dirs_lds) + 255) & ~(size_t)255;
-      if (lds > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
-      gadd((int)PlanCore::kGenomeGap, 1, dirs_lds ? 1 : 0, gg_lds_bucket(lds), s);
-      continue;
-    }
     size_t lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, true);
     const bool dirs_lds = lds <= gg_lds_dirs_max();
     if (!dirs_lds) lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, false);
@@ -1133,10 +1108,6 @@ static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, cons
   if (!a.d_gresults || !a.d_sprob) return hipErrorInvalidValue;
   if (L.kind == PlanCore::kGgp)
     return launch_ggp((int)L.lds, L.R, L.count, stream, a.d_gprobs, a.d_gorder + L.first, ctx->d_genome,
-                      ctx->genome_words, a.d_q, a.d_quc, a.d_sprob, ctx->d_sc, ctx->d_cs, ctx->d_isc, a.d_gresults,
-                      a.d_pairs, (unsigned char*)ctx->gdirs.p);
-  if (L.R == 1 && gg2_enabled())
-    return launch_gg2(L.dirs_lds, L.count, L.lds, stream, a.d_gprobs, a.d_gorder + L.first, ctx->d_genome,
                       ctx->genome_words, a.d_q, a.d_quc, a.d_sprob, ctx->d_sc, ctx->d_cs, ctx->d_isc, a.d_gresults,
                       a.d_pairs, (unsigned char*)ctx->gdirs.p);
   return launch_gg(L.R, L.dirs_lds, L.count, L.lds, stream, a.d_gprobs, a.d_gorder + L.first, ctx->d_genome,

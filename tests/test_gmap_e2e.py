@@ -131,6 +131,23 @@ def test_gpu_gmap_worker_threads(threads):
     assert st["batches"] > 0 and (threads < 8 or st["mean_batch"] > 1.5), st
 
 
+@pytest.mark.gpu
+def test_gpu_gmap_parts(monkeypatch):
+    """configs[3]'s sharding (tools/multi_gmap.py): three GMAP drop-in processes on the one GPU, each with
+    the reads --part=i/3 gives it, outputs merged in input order: identical to the single-process
+    reference output, and every copy ran its calls on the engine."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import multi_gmap
+    monkeypatch.setenv("GMAPDP_SHIM_STATS", "1")
+    rc, out, errs, _ = multi_gmap.run(3, 1, [_exe("gmap_gpu_nosimd"), "-t", "8", "-O"] + E2E_ARGS[:-1],
+                                      E2E_ARGS[-1], cwd=GOLD)
+    assert rc == 0, errs
+    assert out == _read("e2e_nosimd.sam")
+    for err in errs:
+        assert _stats(err)["Dynprog_single_gap"] > 0
+
+
 # ---- gmapl (LARGE_GENOMES, 64-bit Univcoord_T): the nosimd semantics, the same fixtures ----
 
 def test_reference_gmapl_reproduces_fixtures():

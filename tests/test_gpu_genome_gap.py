@@ -125,22 +125,3 @@ def test_gpu_genome_gap_every_packed_band_class(engine):
     d = _first_diff(got, exp)
     assert d is None, _msg(probs, d, "oracle")
 
-
-def test_gpu_genome_gap_global_dirs_variant():
-    """gg2_kernel keeps its packed direction words in LDS below a size threshold and in the global
-    scratch above it; with the threshold at 1 byte every band-<=64 problem takes the global variant.
-    Runs in a child process (the threshold is read once per process): golden parity must hold."""
-    import subprocess
-    import sys
-    code = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
-            "import test_gpu_genome_gap as T, gmapdp\n"
-            "e = gmapdp.Engine(0)\n"
-            "g, probs, outs = T._golden()\n"
-            "e.set_genome(g)\n"
-            "got = e.genome_gap_batch(probs, [(p['probsL'], p['probsR']) for p in probs])\n"
-            "d = T._first_diff(got, outs['ref_nosimd'])\n"
-            "assert d is None, T._msg(probs, d, 'ref')\n"
-            "print('ok', len(probs))\n" % (os.path.join(os.path.dirname(HERE), "gmap-2024_amd"), HERE))
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240,
-                       env=dict(os.environ, GMAPDP_GG2_LDS_MAX="1"))
-    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]

@@ -13,8 +13,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gmap-2024_amd"))
-VARIANTS = {"gg_kernel": {"GMAPDP_GG2": "0"}, "gg2_lds24k": {"GMAPDP_GG2_LDS_MAX": str(24 * 1024)},
-            "gg2_global": {"GMAPDP_GG2_LDS_MAX": "1"}, "gg2_lds64k": {"GMAPDP_GG2_LDS_MAX": str(64 * 1024)}}
+VARIANTS = {"gg_kernel": {}, "gg_kernel_lds_dirs": {"GMAPDP_GG_LDS_DIRS_MAX": str(48 * 1024)},
+            "ggp_packed": {"GMAPDP_GGP": "1"}}
 
 
 def child(reads, reps):
