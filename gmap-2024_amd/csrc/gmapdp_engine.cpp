@@ -463,6 +463,53 @@ int gmapdp_set_genome(gmapdp_ctx* ctx, const uint32_t* blocks, size_t nwords, ui
   return GMAPDP_OK;
 }
 
+struct gmapdp_dgenome {
+  int device = 0;
+  uint32_t* d = nullptr;
+  uint64_t words = 0, length = 0;
+};
+
+int gmapdp_dgenome_create(int device, const uint32_t* blocks, size_t nwords, uint64_t length, gmapdp_dgenome** out) {
+  if (!out || !blocks || nwords < (size_t)((length + 31) / 32) * 3) return GMAPDP_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return GMAPDP_ENODEV;
+  if (hipSetDevice(device) != hipSuccess) return GMAPDP_ENODEV;
+  gmapdp_dgenome* g = new gmapdp_dgenome();
+  g->device = device;
+  if (hipMalloc(&g->d, nwords * sizeof(uint32_t)) != hipSuccess) {
+    delete g;
+    return GMAPDP_ENOMEM;
+  }
+  if (hipMemcpy(g->d, blocks, nwords * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(g->d);
+    delete g;
+    return GMAPDP_ENOMEM;
+  }
+  g->words = nwords;
+  g->length = length;
+  *out = g;
+  return GMAPDP_OK;
+}
+
+void gmapdp_dgenome_destroy(gmapdp_dgenome* g) {
+  if (!g) return;
+  (void)hipSetDevice(g->device);
+  if (g->d) (void)hipFree(g->d);
+  delete g;
+}
+
+int gmapdp_use_dgenome(gmapdp_ctx* ctx, const gmapdp_dgenome* g) {
+  if (!ctx || !g || ctx->device != g->device) return GMAPDP_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->d_genome && ctx->genome_owned) (void)hipFree(ctx->d_genome);
+  ctx->d_genome = g->d;
+  ctx->genome_words = g->words;
+  ctx->genome_length = g->length;
+  ctx->genome_owned = false;
+  return GMAPDP_OK;
+}
+
 int gmapdp_share_genome(gmapdp_ctx* ctx, const gmapdp_ctx* owner) {
   if (!ctx || !owner || ctx == owner || ctx->device != owner->device) return GMAPDP_EINVAL;
   if (!owner->d_genome) return GMAPDP_ENOGENOME;

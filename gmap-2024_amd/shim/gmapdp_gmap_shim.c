@@ -200,41 +200,51 @@ shim_check_call (Genome_T genome, Genome_T genomealt, Dynprog_T dynprog) {
 
 /* The engine context with `genome` resident in HBM (dispatcher thread only).  Every dispatcher owns a
    context with a single stream -- DP dispatchers at the device's highest stream priority, stage-2
-   dispatchers at its lowest -- so that dispatchers x 1 streams fit the process's hardware queues
-   (GPU_MAX_HW_QUEUES) and a DP batch never queues behind a stage-2 sweep.  The genome is uploaded to
-   HBM once, by the first dispatcher that needs it; the others share that copy (gmapdp_share_genome). */
+   dispatchers at its lowest -- so that the dispatchers' streams fit the process's hardware queues
+   (GPU_MAX_HW_QUEUES) and a DP batch never queues behind a stage-2 sweep.  Each GMAP genome (a Genome_T;
+   a -g run over a multi-sequence file has several) is uploaded to HBM once, as a device genome every
+   dispatcher context reads (gmapdp_dgenome_create / gmapdp_use_dgenome). */
 static __thread int shim_qi = 0;            /* the dispatcher's queue: 0 Dynprog_*, 1 stage 2 */
+typedef struct shim_dgenome {
+  Genome_T genome;
+  gmapdp_dgenome *dg;
+  struct shim_dgenome *next;
+} shim_dgenome;
 static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
-static gmapdp_ctx *g_owner = NULL;          /* the context holding the HBM genome */
-static Genome_T g_owner_genome = NULL;
+static shim_dgenome *g_genomes = NULL;
+
+static int
+shim_device (void) {
+  const char *dev = getenv("GMAPDP_DEVICE");
+  return dev ? atoi(dev) : 0;
+}
 
 static gmapdp_ctx *
 shim_context (Genome_T genome) {
-  const char *dev;
+  shim_dgenome *e;
   uint64_t length;
   size_t nwords;
-  if (shim_ctx == NULL) {
-    dev = getenv("GMAPDP_DEVICE");
-    shim_check(gmapdp_create_ex(&shim_ctx, dev ? atoi(dev) : 0, shim_mode, shim_user_open, shim_user_extend,
+  if (shim_ctx == NULL)
+    shim_check(gmapdp_create_ex(&shim_ctx, shim_device(), shim_mode, shim_user_open, shim_user_extend,
                                 shim_user_dynprog_p,
                                 GMAPDP_CTX_ONE_STREAM | (shim_qi == 0 ? GMAPDP_CTX_PRIO_HIGH : GMAPDP_CTX_PRIO_LOW)),
                "gmapdp_create_ex");
-  }
   if (genome != shim_genome) {
     pthread_mutex_lock(&g_lock);
-    if (g_owner != NULL && g_owner_genome == genome) {
-      if (g_owner != shim_ctx) shim_check(gmapdp_share_genome(shim_ctx, g_owner), "gmapdp_share_genome");
-    } else if (g_owner == NULL) {
+    for (e = g_genomes; e != NULL && e->genome != genome; e = e->next) ;
+    if (e == NULL) {
+      e = (shim_dgenome *) calloc(1, sizeof(shim_dgenome));
+      if (e == NULL) shim_refuse("host memory for a genome record (out of memory)");
       length = (uint64_t) Genome_genomelength(genome);
       nwords = gmapdp_genome_words(length);
-      shim_check(gmapdp_set_genome(shim_ctx, (const uint32_t *) Genome_blocks(genome), nwords, length),
-                 "gmapdp_set_genome");
-      g_owner = shim_ctx;
-      g_owner_genome = genome;
-    } else {
-      shim_refuse("a second genome in one process");
+      shim_check(gmapdp_dgenome_create(shim_device(), (const uint32_t *) Genome_blocks(genome), nwords, length,
+                                       &e->dg), "gmapdp_dgenome_create");
+      e->genome = genome;
+      e->next = g_genomes;
+      g_genomes = e;
     }
     pthread_mutex_unlock(&g_lock);
+    shim_check(gmapdp_use_dgenome(shim_ctx, e->dg), "gmapdp_use_dgenome");
     shim_genome = genome;
   }
   return shim_ctx;
@@ -337,14 +347,26 @@ shim_dispatch (void *arg) {
     batch = q_head[qi];
     q_head[qi] = q_tail[qi] = NULL;
     pthread_mutex_unlock(&q_lock);
-    shim_run(batch);
-    pthread_mutex_lock(&q_lock);
-    for (r = batch; r != NULL; r = next) {
-      next = r->next;
-      r->done = 1;
-      pthread_cond_signal(&r->cv);
+    /* one engine batch per genome (requests keep their queue order within a genome) */
+    while (batch != NULL) {
+      shim_req *same = NULL, **st = &same, *rest = NULL, **rt = &rest;
+      Genome_T g = batch->genome;
+      for (r = batch; r != NULL; r = next) {
+        next = r->next;
+        r->next = NULL;
+        if (r->genome == g) { *st = r; st = &r->next; }
+        else { *rt = r; rt = &r->next; }
+      }
+      shim_run(same);
+      pthread_mutex_lock(&q_lock);
+      for (r = same; r != NULL; r = next) {
+        next = r->next;
+        r->done = 1;
+        pthread_cond_signal(&r->cv);
+      }
+      pthread_mutex_unlock(&q_lock);
+      batch = rest;
     }
-    pthread_mutex_unlock(&q_lock);
   }
   return NULL;
 }
@@ -437,8 +459,7 @@ shim_run (shim_req *batch) {
   Genome_T genome = NULL;
   for (r = batch; r != NULL; r = r->next) {
     n++;
-    if (genome == NULL) genome = r->genome;
-    else if (r->genome != genome) shim_refuse("two genomes in one process");
+    if (genome == NULL) genome = r->genome;  /* shim_dispatch hands over one genome's requests */
     switch (r->kind) {
     case K_SINGLE: GROW(D.rs, D.rscap, ns + 1); D.rs[ns++] = r; break;
     case K_END: GROW(D.re, D.recap, ne + 1); D.re[ne++] = r; break;

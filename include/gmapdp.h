@@ -551,6 +551,14 @@ int gmapdp_create_ex (gmapdp_ctx **ctx, int device, int mode, int user_open, int
 /* Use `owner`'s HBM-resident genome in `ctx` (no copy; same device).  `owner` must outlive every
  * context sharing its genome and keep that genome until they are done. */
 int gmapdp_share_genome (gmapdp_ctx *ctx, const gmapdp_ctx *owner);
+/* A packed genome resident in one device's HBM, independent of any context: upload once, then let any
+ * number of contexts read it (gmapdp_use_dgenome; no copy).  The drop-in keeps one per GMAP Genome_T
+ * (a -g run over a multi-sequence file has several).  Destroy it only after every context using it is
+ * done with it. */
+typedef struct gmapdp_dgenome gmapdp_dgenome;
+int gmapdp_dgenome_create (int device, const uint32_t *blocks, size_t nwords, uint64_t length, gmapdp_dgenome **g);
+void gmapdp_dgenome_destroy (gmapdp_dgenome *g);
+int gmapdp_use_dgenome (gmapdp_ctx *ctx, const gmapdp_dgenome *g);
 
 /* Words needed for a packed genome of `length` nt ((len+31)/32*3 + 4). */
 size_t gmapdp_genome_words (uint64_t length);
