@@ -106,6 +106,7 @@ static const char *const shim_stat_name[ST_N] = {"Dynprog_single_gap", "Dynprog_
 static unsigned long shim_stats[ST_N];
 
 static unsigned long shim_batches, shim_batched;
+static FILE *shim_trace = NULL;  /* GMAPDP_SHIM_TRACE: per-batch record (diagnostics) */
 static double shim_secs[4];  /* dispatcher wall time in the DP, cDNA, seeding and Stage2_compute batches */
 
 #include <time.h>
@@ -383,6 +384,8 @@ shim_submit (shim_req *r) {
   if (!dispatcher_started) {
     st = getenv("GMAPDP_SHIM_STATS");
     if (st != NULL && st[0] == '1') atexit(shim_print_stats);
+    st = getenv("GMAPDP_SHIM_TRACE");
+    if (st != NULL && st[0] != '\0') shim_trace = fopen(st, "w");
     /* 3 + 1 streams: HIP's default of four hardware queues per process, one per dispatcher */
     st = getenv("GMAPDP_SHIM_DISPATCHERS");
     nd = st != NULL ? atoi(st) : 3;
@@ -751,6 +754,14 @@ shim_run (shim_req *batch) {
   td[3] = shim_now() - t1;
   pthread_mutex_lock(&q_lock);
   for (i = 0; i < 4; i++) shim_secs[i] += td[i];
+  if (shim_trace != NULL) {  /* GMAPDP_SHIM_TRACE=<file>: one line per dispatcher batch */
+    int gmax = 0;
+    for (i = 0; i < ns; i++) gmax = D.s[i].glength > gmax ? D.s[i].glength : gmax;
+    for (i = 0; i < ne; i++) gmax = D.e[i].glength > gmax ? D.e[i].glength : gmax;
+    for (i = 0; i < ng; i++) gmax = D.g[i].glengthL > gmax ? D.g[i].glengthL : gmax;
+    fprintf(shim_trace, "%d %.6f %zu %zu %zu %zu %zu %zu %zu %d %.6f %.6f %.6f %.6f\n", shim_qi, shim_now(), ns, ne, ng,
+            nc, nxs, nxf, n2, gmax, td[0], td[1], td[2], td[3]);
+  }
   pthread_mutex_unlock(&q_lock);
 }
 

@@ -27,7 +27,8 @@ def main():
     ap.add_argument("--threads", default="1,16")
     ap.add_argument("--build", default="nosimd", choices=["nosimd", "avx2"])
     ap.add_argument("--gpu-threads", default=None, help="thread counts for the GPU program (default: --threads)")
-    ap.add_argument("--dispatchers", type=int, default=4, help="GMAPDP_SHIM_DISPATCHERS")
+    ap.add_argument("--dispatchers", type=int, default=3, help="GMAPDP_SHIM_DISPATCHERS")
+    ap.add_argument("--trace", default=None, help="directory for the shim's per-batch traces (GMAPDP_SHIM_TRACE)")
     a = ap.parse_args()
     import make_e2e as M
     genome = list(M.synth_genome())
@@ -49,6 +50,9 @@ def main():
     for prog, t in runs:
         if True:
             env = dict(os.environ, GMAPDP_SHIM_STATS="1", GMAPDP_SHIM_DISPATCHERS=str(a.dispatchers))
+            if a.trace and "gpu" in prog:
+                os.makedirs(a.trace, exist_ok=True)
+                env["GMAPDP_SHIM_TRACE"] = os.path.abspath(os.path.join(a.trace, "trace_t%d.txt" % t))
             args = [os.path.join(ref, prog), "-t", str(t), "-O", "-g", "g.fa", "-f", "samse", "--no-sam-headers",
                     "r.fa"]
             t0 = time.perf_counter()
