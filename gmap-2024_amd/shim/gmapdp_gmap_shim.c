@@ -205,7 +205,7 @@ shim_check_call (Genome_T genome, Genome_T genomealt, Dynprog_T dynprog) {
    (GPU_MAX_HW_QUEUES) and a DP batch never queues behind a stage-2 sweep.  Each GMAP genome (a Genome_T;
    a -g run over a multi-sequence file has several) is uploaded to HBM once, as a device genome every
    dispatcher context reads (gmapdp_dgenome_create / gmapdp_use_dgenome). */
-static __thread int shim_qi = 0;            /* the dispatcher's queue: 0 Dynprog_*, 1 stage 2 */
+static __thread int shim_qi = 0;            /* the dispatcher's queue: 0 Dynprog_*, 1 stage 2, 2 long fills */
 typedef struct shim_dgenome {
   Genome_T genome;
   gmapdp_dgenome *dg;
@@ -228,7 +228,7 @@ shim_context (Genome_T genome) {
   if (shim_ctx == NULL)
     shim_check(gmapdp_create_ex(&shim_ctx, shim_device(), shim_mode, shim_user_open, shim_user_extend,
                                 shim_user_dynprog_p,
-                                GMAPDP_CTX_ONE_STREAM | (shim_qi == 0 ? GMAPDP_CTX_PRIO_HIGH : GMAPDP_CTX_PRIO_LOW)),
+                                GMAPDP_CTX_ONE_STREAM | (shim_qi != 1 ? GMAPDP_CTX_PRIO_HIGH : GMAPDP_CTX_PRIO_LOW)),
                "gmapdp_create_ex");
   if (genome != shim_genome) {
     pthread_mutex_lock(&g_lock);
@@ -294,6 +294,7 @@ typedef struct shim_req {
   double *mxp;                  /* the caller's MaxEnt probabilities of its candidates (2 per candidate) */
   size_t mxccap, mxpcap;
   int done;
+  int longp;                    /* a long fill: queue 2 */
   pthread_cond_t cv;
   struct shim_req *next;
 } shim_req;
@@ -301,8 +302,19 @@ typedef struct shim_req {
 /* Two queues: 0 for the Dynprog_* calls (short, ~150 per read), 1 for stage 2 (one long call per
    read), so that a stage-2 batch never holds back the DP calls queued behind it. */
 static pthread_mutex_t q_lock = PTHREAD_MUTEX_INITIALIZER;
-static pthread_cond_t q_cond[2] = {PTHREAD_COND_INITIALIZER, PTHREAD_COND_INITIALIZER};
-static shim_req *q_head[2] = {NULL, NULL}, *q_tail[2] = {NULL, NULL};
+static pthread_cond_t q_cond[3] = {PTHREAD_COND_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_COND_INITIALIZER};
+static shim_req *q_head[3] = {NULL, NULL, NULL}, *q_tail[3] = {NULL, NULL, NULL};
+/* Queue 2: Dynprog_* calls whose fill is long (shim_cost above GMAPDP_SHIM_LONG_COST, default 400 band-word
+   columns: end gaps against up to 2000 genome columns, wide bands).  A batch lasts as long as its longest
+   fill, so these get their own dispatcher and never hold back the short calls that are most of a read. */
+static long shim_long_cost = 400;
+
+/* band-word columns of a banded fill: columns x ceil(band width / 64) (Dynprog_compute_bands, wide band) */
+static long
+shim_cost (int rlength, int glength, int extraband) {
+  long g = glength > 2000 ? 2000 : glength, w = (long) abs(glength - rlength) + 2L * extraband + 1L;
+  return g < 0 ? 0 : g * ((w + 63) / 64);
+}
 static int dispatcher_started = 0;
 static __thread shim_req *tl_req = NULL;
 
@@ -327,6 +339,7 @@ shim_request (int kind) {
     tl_req = r;
   }
   r->kind = kind;
+  r->longp = 0;
   r->q = r->quc = NULL;
   r->qlen = 0;
   r->probs = NULL;
@@ -378,25 +391,30 @@ shim_submit (shim_req *r) {
   pthread_t th;
   pthread_attr_t attr;
   const char *st;
-  int nd, nd2, k;
-  const int qi = r->kind >= K_OLIGO ? 1 : 0;
+  int nd, nd2, nl, k;
+  const int qi = r->kind >= K_OLIGO ? 1 : (r->longp ? 2 : 0);
   pthread_mutex_lock(&q_lock);
   if (!dispatcher_started) {
     st = getenv("GMAPDP_SHIM_STATS");
     if (st != NULL && st[0] == '1') atexit(shim_print_stats);
     st = getenv("GMAPDP_SHIM_TRACE");
     if (st != NULL && st[0] != '\0') shim_trace = fopen(st, "w");
-    /* 3 + 1 streams: HIP's default of four hardware queues per process, one per dispatcher */
+    /* 2 + 1 + 1 streams: HIP's default of four hardware queues per process, one per dispatcher */
     st = getenv("GMAPDP_SHIM_DISPATCHERS");
-    nd = st != NULL ? atoi(st) : 3;
+    nd = st != NULL ? atoi(st) : 2;
     if (nd < 1) nd = 1;
+    st = getenv("GMAPDP_SHIM_LONG_DISPATCHERS");
+    nl = st != NULL ? atoi(st) : 1;
+    if (nl < 1) nl = 1;
     st = getenv("GMAPDP_SHIM_STAGE2_DISPATCHERS");
     nd2 = st != NULL ? atoi(st) : 1;
     if (nd2 < 1) nd2 = 1;
+    st = getenv("GMAPDP_SHIM_LONG_COST");
+    if (st != NULL) shim_long_cost = atol(st);
     pthread_attr_init(&attr);
     pthread_attr_setdetachstate(&attr, PTHREAD_CREATE_DETACHED);
-    for (k = 0; k < nd + nd2; k++)
-      if (pthread_create(&th, &attr, shim_dispatch, (void *) (intptr_t) (k < nd ? 0 : 1)) != 0)
+    for (k = 0; k < nd + nl + nd2; k++)
+      if (pthread_create(&th, &attr, shim_dispatch, (void *) (intptr_t) (k < nd ? 0 : (k < nd + nl ? 2 : 1))) != 0)
         shim_refuse("a dispatcher thread (pthread_create)");
     pthread_attr_destroy(&attr);
     dispatcher_started = 1;
@@ -822,6 +840,7 @@ __wrap_Dynprog_single_gap (int *dynprogindex, int *finalscore, int *nmatches, in
   r->q = sequence1;
   r->quc = sequenceuc1;
   r->qlen = length1 > 0 ? (size_t) length1 : 0;
+  r->longp = shim_cost(length1, length2, extraband_single) > shim_long_cost;
   GROW(r->pairs, r->pcap, gmapdp_single_pair_capacity(p, 1) + 1);
   shim_submit(r);
   shim_count(ST_SINGLE);
@@ -866,6 +885,7 @@ shim_end_gap (int end3p, int *dynprogindex, int *finalscore, int *nmatches, int 
   r->q = (end3p || length1 <= 0) ? seq : seq - (length1 - 1);
   r->quc = (end3p || length1 <= 0) ? sequc : sequc - (length1 - 1);
   r->qlen = length1 > 0 ? (size_t) length1 : 0;
+  r->longp = shim_cost(length1 > 660 ? 660 : length1, length2, extraband_end) > shim_long_cost;
   GROW(r->pairs, r->pcap, gmapdp_end_pair_capacity(p, 1) + 1);
   shim_submit(r);
   shim_count(end3p ? ST_END3 : ST_END5);
@@ -980,6 +1000,7 @@ __wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_r
   r->qlen = rlength > 0 ? (size_t) rlength : 0;
   r->probs = r->pbuf;
   r->nprobs = m;
+  r->longp = 2 * shim_cost(rlength, glengthL > glengthR ? glengthL : glengthR, extraband_paired) > shim_long_cost;
   GROW(r->pairs, r->pcap, gmapdp_genome_pair_capacity(p, 1) + 1);
   shim_submit(r);
   shim_count(ST_GENOME);

@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--threads", default="1,16")
     ap.add_argument("--build", default="nosimd", choices=["nosimd", "avx2"])
     ap.add_argument("--gpu-threads", default=None, help="thread counts for the GPU program (default: --threads)")
-    ap.add_argument("--dispatchers", type=int, default=3, help="GMAPDP_SHIM_DISPATCHERS")
+    ap.add_argument("--dispatchers", type=int, default=2, help="GMAPDP_SHIM_DISPATCHERS")
     ap.add_argument("--trace", default=None, help="directory for the shim's per-batch traces (GMAPDP_SHIM_TRACE)")
     a = ap.parse_args()
     import make_e2e as M
