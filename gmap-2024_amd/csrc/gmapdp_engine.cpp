@@ -200,8 +200,10 @@ struct DevBuf {
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
+    // doubling: a hipFree waits for the whole device (every stream of every context), so a buffer
+    // should grow a handful of times per process, not per batch
     size_t want = std::max(bytes, (size_t)4096);
-    want = want + want / 4;
+    want = want + want;
     hipError_t e = hipMalloc(&p, want);
     if (e == hipSuccess) cap = want;
     return e;
@@ -222,7 +224,7 @@ struct HostBuf {
     p = nullptr;
     cap = 0;
     size_t want = std::max(bytes, (size_t)65536);
-    want = want + want / 4;
+    want = want + want;
     hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
     if (e == hipSuccess) cap = want;
     return e;
@@ -461,6 +463,35 @@ int gmapdp_set_genome(gmapdp_ctx* ctx, const uint32_t* blocks, size_t nwords, ui
   ctx->genome_words = nwords;
   ctx->genome_length = length;
   return GMAPDP_OK;
+}
+
+int gmapdp_reserve(gmapdp_ctx* ctx, size_t bytes, int what) {
+  if (!ctx) return GMAPDP_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  hipError_t e = hipSuccess;
+  auto dev = [&](DevBuf& b, size_t n) { if (e == hipSuccess) e = b.ensure(n); };
+  auto host = [&](HostBuf& b, size_t n) { if (e == hipSuccess) e = b.ensure(n); };
+  if (what & GMAPDP_RESERVE_DP) {
+    host(ctx->hin, bytes);
+    host(ctx->hout, bytes);
+    dev(ctx->din, bytes);
+    dev(ctx->dout, bytes);
+    dev(ctx->gdirs, 4 * bytes);
+  }
+  if (what & GMAPDP_RESERVE_AUX) {
+    for (DevBuf* b : {&ctx->mxprobs, &ctx->mxres, &ctx->mxcands, &ctx->mxcnt, &ctx->mxdirect, &ctx->mxprobs2,
+                      &ctx->mxpairs, &ctx->cprobs, &ctx->corder, &ctx->cresults, &ctx->cscratch, &ctx->qseq_uc})
+      dev(*b, bytes);
+  }
+  if (what & GMAPDP_RESERVE_STAGE2) {
+    for (DevBuf* b : {&ctx->oprobs, &ctx->oresults, &ctx->oscratch, &ctx->onpos, &ctx->omap, &ctx->otable, &ctx->odiag,
+                      &ctx->opool, &ctx->opoolctr, &ctx->qseq_uc, &ctx->s2probs, &ctx->s2results, &ctx->s2counters,
+                      &ctx->s2paths, &ctx->s2pairs, &ctx->s2qseq})
+      dev(*b, bytes);
+    dev(ctx->s2scratch, 4 * bytes);
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  return e == hipSuccess ? GMAPDP_OK : fail(ctx, GMAPDP_ENOMEM, "reserve: %s", e);
 }
 
 struct gmapdp_dgenome {

@@ -167,6 +167,7 @@ def load_library(path=LIB_PATH):
         "gmapdp_dgenome_create": (C.c_int, [C.c_int, C.c_void_p, C.c_size_t, C.c_uint64, P(C.c_void_p)]),
         "gmapdp_dgenome_destroy": (None, [C.c_void_p]),
         "gmapdp_use_dgenome": (C.c_int, [C.c_void_p, C.c_void_p]),
+        "gmapdp_reserve": (C.c_int, [C.c_void_p, C.c_size_t, C.c_int]),
         "gmapdp_genome_words": (C.c_size_t, [C.c_uint64]),
         "gmapdp_debug_stage2_scratch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
         "gmapdp_stage2_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_char_p, C.c_char_p, C.c_size_t,

@@ -205,6 +205,7 @@ shim_check_call (Genome_T genome, Genome_T genomealt, Dynprog_T dynprog) {
    (GPU_MAX_HW_QUEUES) and a DP batch never queues behind a stage-2 sweep.  Each GMAP genome (a Genome_T;
    a -g run over a multi-sequence file has several) is uploaded to HBM once, as a device genome every
    dispatcher context reads (gmapdp_dgenome_create / gmapdp_use_dgenome). */
+static __thread int shim_reserved = 0;
 static __thread int shim_qi = 0;            /* the dispatcher's queue: 0 Dynprog_*, 1 stage 2, 2 long fills */
 typedef struct shim_dgenome {
   Genome_T genome;
@@ -230,6 +231,12 @@ shim_context (Genome_T genome) {
                                 shim_user_dynprog_p,
                                 GMAPDP_CTX_ONE_STREAM | (shim_qi != 1 ? GMAPDP_CTX_PRIO_HIGH : GMAPDP_CTX_PRIO_LOW)),
                "gmapdp_create_ex");
+  if (!shim_reserved) {  /* staging and scratch sized up front: growing them later stalls the device */
+    shim_check(gmapdp_reserve(shim_ctx, shim_qi == 1 ? (size_t) 64 << 20 : (size_t) 16 << 20,
+                              shim_qi == 1 ? GMAPDP_RESERVE_STAGE2 : GMAPDP_RESERVE_DP | GMAPDP_RESERVE_AUX),
+               "gmapdp_reserve");
+    shim_reserved = 1;
+  }
   if (genome != shim_genome) {
     pthread_mutex_lock(&g_lock);
     for (e = g_genomes; e != NULL && e->genome != genome; e = e->next) ;

@@ -555,6 +555,15 @@ int gmapdp_share_genome (gmapdp_ctx *ctx, const gmapdp_ctx *owner);
  * number of contexts read it (gmapdp_use_dgenome; no copy).  The drop-in keeps one per GMAP Genome_T
  * (a -g run over a multi-sequence file has several).  Destroy it only after every context using it is
  * done with it. */
+/* Grow the context's staging and scratch buffers to `bytes` each (4x for the direction and chaining
+ * scratch) now, so that a long-running caller does not grow them later: a buffer's growth frees the old
+ * one, and hipFree waits for the whole device, stalling every context's streams.  what: GMAPDP_RESERVE_DP
+ * (single / end / genome-gap batches), _AUX (microexon and cDNA-gap batches), _STAGE2 (Stage2_compute and
+ * seeding batches). */
+#define GMAPDP_RESERVE_DP     0x1
+#define GMAPDP_RESERVE_AUX    0x2
+#define GMAPDP_RESERVE_STAGE2 0x4
+int gmapdp_reserve (gmapdp_ctx *ctx, size_t bytes, int what);
 typedef struct gmapdp_dgenome gmapdp_dgenome;
 int gmapdp_dgenome_create (int device, const uint32_t *blocks, size_t nwords, uint64_t length, gmapdp_dgenome **g);
 void gmapdp_dgenome_destroy (gmapdp_dgenome *g);
