@@ -406,15 +406,18 @@ shim_submit (shim_req *r) {
     if (st != NULL && st[0] == '1') atexit(shim_print_stats);
     st = getenv("GMAPDP_SHIM_TRACE");
     if (st != NULL && st[0] != '\0') shim_trace = fopen(st, "w");
-    /* 2 + 1 + 1 streams: HIP's default of four hardware queues per process, one per dispatcher */
+    /* One hardware queue per dispatcher stream: 3 short + 3 long + 2 stage-2 dispatchers on 8 queues.
+       HIP reads GPU_MAX_HW_QUEUES (default 4) when the process first touches the GPU, which is later,
+       in a dispatcher; a value the user set is kept. */
+    setenv("GPU_MAX_HW_QUEUES", "8", 0);
     st = getenv("GMAPDP_SHIM_DISPATCHERS");
-    nd = st != NULL ? atoi(st) : 2;
+    nd = st != NULL ? atoi(st) : 3;
     if (nd < 1) nd = 1;
     st = getenv("GMAPDP_SHIM_LONG_DISPATCHERS");
-    nl = st != NULL ? atoi(st) : 1;
+    nl = st != NULL ? atoi(st) : 3;
     if (nl < 1) nl = 1;
     st = getenv("GMAPDP_SHIM_STAGE2_DISPATCHERS");
-    nd2 = st != NULL ? atoi(st) : 1;
+    nd2 = st != NULL ? atoi(st) : 2;
     if (nd2 < 1) nd2 = 1;
     st = getenv("GMAPDP_SHIM_LONG_COST");
     if (st != NULL) shim_long_cost = atol(st);

@@ -12,6 +12,7 @@ shim's call counts.
 import argparse
 import json
 import os
+import resource
 import subprocess
 import sys
 import tempfile
@@ -27,7 +28,7 @@ def main():
     ap.add_argument("--threads", default="1,16")
     ap.add_argument("--build", default="nosimd", choices=["nosimd", "avx2"])
     ap.add_argument("--gpu-threads", default=None, help="thread counts for the GPU program (default: --threads)")
-    ap.add_argument("--dispatchers", type=int, default=2, help="GMAPDP_SHIM_DISPATCHERS")
+    ap.add_argument("--dispatchers", type=int, default=3, help="GMAPDP_SHIM_DISPATCHERS")
     ap.add_argument("--trace", default=None, help="directory for the shim's per-batch traces (GMAPDP_SHIM_TRACE)")
     a = ap.parse_args()
     import make_e2e as M
@@ -56,13 +57,17 @@ def main():
             args = [os.path.join(ref, prog), "-t", str(t), "-O", "-g", "g.fa", "-f", "samse", "--no-sam-headers",
                     "r.fa"]
             t0 = time.perf_counter()
+            ru0 = resource.getrusage(resource.RUSAGE_CHILDREN)
             r = subprocess.run(args, cwd=tmp, env=env, capture_output=True, text=True, timeout=1500)
             dt = time.perf_counter() - t0
+            ru1 = resource.getrusage(resource.RUSAGE_CHILDREN)
+            cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
             if r.returncode != 0:
                 raise SystemExit("%s failed: %s" % (prog, r.stderr[-2000:]))
             sams[(prog, t)] = r.stdout
             stats = [l for l in r.stderr.splitlines() if l.startswith("gmapdp shim calls")]
             out["runs"].append({"program": prog, "threads": t, "seconds": dt, "reads_per_s": a.reads / dt,
+                                "cpu_seconds": cpu, "cpu_cores_busy": cpu / dt,
                                 "shim_calls": stats[0] if stats else None})
             print(json.dumps(out["runs"][-1]), file=sys.stderr, flush=True)
     base = sams[("gmap_%s" % a.build, min(cpu_t))]
