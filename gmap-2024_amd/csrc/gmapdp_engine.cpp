@@ -260,6 +260,7 @@ struct gmapdp_ctx {
   uint64_t genome_length = 0;
   bool genome_owned = true;  // false: another context's HBM genome (gmapdp_share_genome)
   bool one_stream = false;   // GMAPDP_CTX_ONE_STREAM: no side streams (callers that run many contexts)
+  hipEvent_t ev_block = nullptr;  // GMAPDP_CTX_BLOCKING_SYNC: batch completion waited on without spinning
   DevBuf probs, order, qseq, qseq_uc, results, pairs, gdirs;
   DevBuf din, dout;    // run_batch: all inputs / all outputs of one synchronous batch
   HostBuf hin, hout;   // their pinned host images
@@ -270,6 +271,15 @@ struct gmapdp_ctx {
   DevBuf mxprobs, mxres, mxcands, mxcnt, mxdirect, mxprobs2, mxpairs;  // Dynprog_microexon_int batches
   std::string err;
 };
+
+// Wait for `s`: spinning (hipStreamSynchronize) by default; with GMAPDP_CTX_BLOCKING_SYNC the thread
+// sleeps on a blocking-sync event instead, so that callers running many dispatcher threads next to
+// their own compute threads (the GMAP drop-in) do not burn a core per waiting dispatcher.
+static hipError_t ctx_sync(gmapdp_ctx* ctx, hipStream_t s) {
+  if (!ctx->ev_block) return hipStreamSynchronize(s);
+  hipError_t e = hipEventRecord(ctx->ev_block, s);
+  return e == hipSuccess ? hipEventSynchronize(ctx->ev_block) : e;
+}
 
 // A batch resolved on the host: GPU problems grouped into launch classes.
 struct PlanCore {
@@ -366,6 +376,8 @@ int gmapdp_create_ex(gmapdp_ctx** out, int device, int mode, int user_open, int 
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join[i], hipEventDisableTiming);
   }
   if (e == hipSuccess && !ctx->one_stream) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
+  if (e == hipSuccess && (flags & GMAPDP_CTX_BLOCKING_SYNC))
+    e = hipEventCreateWithFlags(&ctx->ev_block, hipEventDisableTiming | hipEventBlockingSync);
   ctx->tables = new Tables();
   build_tables(*ctx->tables, mode);
   if (e == hipSuccess) e = hipMalloc(&ctx->d_sc, sizeof(ctx->tables->sc));
@@ -385,7 +397,7 @@ int gmapdp_create_ex(gmapdp_ctx** out, int device, int mode, int user_open, int 
 void gmapdp_destroy(gmapdp_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->stream) (void)ctx_sync(ctx, ctx->stream);
   if (ctx->d_sc) (void)hipFree(ctx->d_sc);
   if (ctx->d_cs) (void)hipFree(ctx->d_cs);
   if (ctx->d_isc) (void)hipFree(ctx->d_isc);
@@ -396,6 +408,7 @@ void gmapdp_destroy(gmapdp_ctx* ctx) {
     if (ctx->ev_join[i]) (void)hipEventDestroy(ctx->ev_join[i]);
   }
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+  if (ctx->ev_block) (void)hipEventDestroy(ctx->ev_block);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx->tables;
   delete ctx;
@@ -1305,7 +1318,7 @@ static int run_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int 
   rc = run_plan(ctx, plan, a, s);
   if (rc) return rc;
   e = hipMemcpyAsync(hout, dout, out_bytes, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess) e = ctx_sync(ctx, s);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "dp execution: %s", e);
   const gmapdp_result* dres = (const gmapdp_result*)(hout + r_res);
   const gmapdp_genome_result* gres = (const gmapdp_genome_result*)(hout + r_gres);
@@ -1608,7 +1621,7 @@ int gmapdp_cdna_gap_batch(gmapdp_ctx* ctx, const gmapdp_cdna_problem* problems, 
   e = hipMemcpyAsync(dres.data(), ctx->cresults.p, sizeof(gmapdp_cdna_result) * ndev, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess && pairs)
     e = hipMemcpyAsync(pairs, ctx->pairs.p, sizeof(gmapdp_pair) * pair_off, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess) e = ctx_sync(ctx, s);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "cdna execution: %s", e);
   for (int d = 0; d < ndev; d++) results[dev_problem[d]] = dres[d];
   return GMAPDP_OK;
@@ -2048,7 +2061,7 @@ int gmapdp_oligo_mappings_batch(gmapdp_ctx* ctx, const gmapdp_oligo_problem* pro
                              (int32_t*)ctx->onpos.p, (int32_t*)ctx->omap.p, (uint32_t*)ctx->otable.p,
                              (int32_t*)ctx->odiag.p, nullptr);
   if (rc) {
-    (void)hipStreamSynchronize(s);
+    (void)ctx_sync(ctx, s);
     oligo_plan_free(plan);
     return rc;
   }
@@ -2059,7 +2072,7 @@ int gmapdp_oligo_mappings_batch(gmapdp_ctx* ctx, const gmapdp_oligo_problem* pro
     e = hipMemcpyAsync(positions, ctx->otable.p, sizeof(uint32_t) * toff, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess && doff)
     e = hipMemcpyAsync(diagonals, ctx->odiag.p, 4 * sizeof(int32_t) * doff, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess) e = ctx_sync(ctx, s);
   oligo_plan_free(plan);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "oligo execution: %s", e);
   return GMAPDP_OK;
@@ -2135,14 +2148,14 @@ extern "C" int gmapdp_stage2_batch(gmapdp_ctx* ctx, const gmapdp_stage2_problem*
                              (int32_t*)ctx->onpos.p, (int32_t*)ctx->omap.p, (uint32_t*)ctx->otable.p,
                              (int32_t*)ctx->odiag.p, nullptr);
   if (rc) {
-    (void)hipStreamSynchronize(s);
+    (void)ctx_sync(ctx, s);
     oligo_plan_free(plan);
     return rc;
   }
   // the chaining scratch is sized exactly from the seeding (totalpositions, ndiagonals per call)
   std::vector<gmapdp_oligo_result> ores(n);
   e = hipMemcpyAsync(ores.data(), ctx->oresults.p, sizeof(gmapdp_oligo_result) * n, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess) e = ctx_sync(ctx, s);
   oligo_plan_free(plan);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "stage-2 seeding: %s", e);
   size_t scratch = 0, qsum = 0;
@@ -2171,7 +2184,7 @@ extern "C" int gmapdp_stage2_batch(gmapdp_ctx* ctx, const gmapdp_stage2_problem*
     if (e == hipSuccess)
       e = hipMemcpyAsync(results, ctx->s2results.p, sizeof(gmapdp_stage2_result) * n, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipMemcpyAsync(cnt, ctx->s2counters.p, sizeof(cnt), hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = ctx_sync(ctx, s);
     if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "stage-2 chaining: %s", e);
     bool overflow = false;
     for (int i = 0; i < n; i++) {
@@ -2185,7 +2198,7 @@ extern "C" int gmapdp_stage2_batch(gmapdp_ctx* ctx, const gmapdp_stage2_problem*
       if (cnt[1]) e = hipMemcpyAsync(paths, ctx->s2paths.p, sizeof(gmapdp_path) * cnt[1], hipMemcpyDeviceToHost, s);
       if (e == hipSuccess && cnt[2])
         e = hipMemcpyAsync(pairs, ctx->s2pairs.p, sizeof(gmapdp_path_pair) * cnt[2], hipMemcpyDeviceToHost, s);
-      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e == hipSuccess) e = ctx_sync(ctx, s);
       if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "stage-2 copy-out: %s", e);
       return GMAPDP_OK;
     }
@@ -2251,7 +2264,7 @@ extern "C" int gmapdp_microexon_search(gmapdp_ctx* ctx, const gmapdp_microexon_p
     if (e == hipSuccess)
       e = hipMemcpyAsync(results, ctx->mxres.p, sizeof(gmapdp_microexon_result) * n, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipMemcpyAsync(&cnt, ctx->mxcnt.p, sizeof(cnt), hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = ctx_sync(ctx, s);
     if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "microexon search: %s", e);
     bool regrow = false;
     for (int i = 0; i < n; i++) regrow |= results[i].cand_offset == -2;
@@ -2277,7 +2290,7 @@ extern "C" int gmapdp_microexon_search(gmapdp_ctx* ctx, const gmapdp_microexon_p
       e = keep.ensure(sizeof(gmapdp_microexon_candidate) * std::max<size_t>(total, 1));
       if (e == hipSuccess && cnt)
         e = hipMemcpyAsync(keep.p, ctx->mxcands.p, sizeof(gmapdp_microexon_candidate) * cnt, hipMemcpyDeviceToDevice, s);
-      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e == hipSuccess) e = ctx_sync(ctx, s);
       if (e == hipSuccess) std::swap(keep.p, ctx->mxcands.p), std::swap(keep.cap, ctx->mxcands.cap);
     }
     if (e == hipSuccess) e = ctx->mxdirect.ensure(sizeof(int64_t) * n);
@@ -2290,14 +2303,14 @@ extern "C" int gmapdp_microexon_search(gmapdp_ctx* ctx, const gmapdp_microexon_p
                            total, (unsigned long long*)ctx->mxcnt.p, (const int64_t*)ctx->mxdirect.p);
     if (e == hipSuccess)
       e = hipMemcpyAsync(results, ctx->mxres.p, sizeof(gmapdp_microexon_result) * n, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = ctx_sync(ctx, s);
     if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "microexon search (large): %s", e);
   }
   if (cands_needed) *cands_needed = total;
   if (total > cand_capacity || (total && !candidates)) return GMAPDP_ESPACE;
   if (total) e = hipMemcpyAsync(candidates, ctx->mxcands.p, sizeof(gmapdp_microexon_candidate) * total,
                                 hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess) e = ctx_sync(ctx, s);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "microexon candidates: %s", e);
   return GMAPDP_OK;
 }
@@ -2342,7 +2355,7 @@ extern "C" int gmapdp_microexon_finish(gmapdp_ctx* ctx, const gmapdp_microexon_p
   if (e == hipSuccess)
     e = hipMemcpyAsync(results, ctx->mxres.p, sizeof(gmapdp_microexon_result) * n, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipMemcpyAsync(pairs, ctx->mxpairs.p, sizeof(gmapdp_pair) * poff, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess) e = ctx_sync(ctx, s);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "microexon finish: %s", e);
   return GMAPDP_OK;
 }
@@ -2539,7 +2552,7 @@ int gmapdp_stage2_plan_create(gmapdp_ctx* ctx, const gmapdp_stage2_problem* prob
   std::vector<gmapdp_oligo_result> ores(n);
   if (!rc) {
     e = hipMemcpyAsync(ores.data(), P->d_ores, sizeof(gmapdp_oligo_result) * n, hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = ctx_sync(ctx, ctx->stream);
     if (e != hipSuccess) rc = fail(ctx, GMAPDP_ELAUNCH, "stage-2 plan seeding: %s", e);
   }
   if (rc) {

@@ -229,7 +229,8 @@ shim_context (Genome_T genome) {
   if (shim_ctx == NULL)
     shim_check(gmapdp_create_ex(&shim_ctx, shim_device(), shim_mode, shim_user_open, shim_user_extend,
                                 shim_user_dynprog_p,
-                                GMAPDP_CTX_ONE_STREAM | (shim_qi != 1 ? GMAPDP_CTX_PRIO_HIGH : GMAPDP_CTX_PRIO_LOW)),
+                                GMAPDP_CTX_ONE_STREAM | GMAPDP_CTX_BLOCKING_SYNC |
+                                    (shim_qi != 1 ? GMAPDP_CTX_PRIO_HIGH : GMAPDP_CTX_PRIO_LOW)),
                "gmapdp_create_ex");
   if (!shim_reserved) {  /* staging and scratch sized up front: growing them later stalls the device */
     shim_check(gmapdp_reserve(shim_ctx, shim_qi == 1 ? (size_t) 64 << 20 : (size_t) 16 << 20,

@@ -542,10 +542,12 @@ void gmapdp_destroy (gmapdp_ctx *ctx);
 /* gmapdp_create with flags, for callers that run several contexts at once (the GMAP drop-in's
  * dispatcher threads): GMAPDP_CTX_ONE_STREAM creates no side streams (a process has few hardware
  * queues, GPU_MAX_HW_QUEUES, and streams beyond them share one and serialise); GMAPDP_CTX_PRIO_HIGH /
- * _LOW create the context's stream at the device's highest / lowest priority. */
+ * _LOW create the context's stream at the device's highest / lowest priority; GMAPDP_CTX_BLOCKING_SYNC
+ * makes the synchronous batch calls wait without spinning. */
 #define GMAPDP_CTX_ONE_STREAM 0x1
 #define GMAPDP_CTX_PRIO_HIGH  0x2
 #define GMAPDP_CTX_PRIO_LOW   0x4
+#define GMAPDP_CTX_BLOCKING_SYNC 0x8  /* batch calls sleep on a blocking-sync event instead of spinning */
 int gmapdp_create_ex (gmapdp_ctx **ctx, int device, int mode, int user_open, int user_extend, int user_dynprog_p,
                       int flags);
 /* Use `owner`'s HBM-resident genome in `ctx` (no copy; same device).  `owner` must outlive every

@@ -68,7 +68,7 @@ def test_shared_genome_context(engine):
     rng = random.Random(808)
     g = random_genome(rng, 40000)
     engine.set_genome(g)
-    other = gmapdp.Engine(0, flags=gmapdp.CTX_ONE_STREAM | gmapdp.CTX_PRIO_LOW)
+    other = gmapdp.Engine(0, flags=gmapdp.CTX_ONE_STREAM | gmapdp.CTX_PRIO_LOW | gmapdp.CTX_BLOCKING_SYNC)
     try:
         other.share_genome(engine)
         probs = [single_gap_problem(rng, g) for _ in range(300)]
