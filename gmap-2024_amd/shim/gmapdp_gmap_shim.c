@@ -40,6 +40,9 @@
  * threads per GPU (gmap -t N, N well above the core count: the workers mostly wait) one launch set
  * carries many reads' calls.  GMAPDP_SHIM_STATS=1 prints the call counts and the mean batch size.
  */
+#ifndef _GNU_SOURCE
+#define _GNU_SOURCE
+#endif
 #ifdef HAVE_CONFIG_H
 #include "config.h"
 #endif
@@ -362,7 +365,10 @@ static void *
 shim_dispatch (void *arg) {
   shim_req *batch, *r, *next;
   const int qi = (int) (intptr_t) arg;
+  char name[16];
   shim_qi = qi;
+  snprintf(name, sizeof(name), "gmapdp-q%d", qi);
+  pthread_setname_np(pthread_self(), name);  /* per-thread CPU accounting (tools/thread_cpu.py) */
   for (;;) {
     pthread_mutex_lock(&q_lock);
     while (q_head[qi] == NULL) pthread_cond_wait(&q_cond[qi], &q_lock);
