@@ -165,6 +165,8 @@ def rocprof_name(kind, R, dl, lds=0):
                 % (lds, R, lds, R))
     if kind == 0:
         return "gmapdp::dp_kernel<%d, %s>" % (R, "true" if dl else "false")
+    if kind == 7:  # lanes over query rows (bands wider than the query)
+        return "gmapdp::dpr_kernel<%d, %s>" % (R, "true" if dl else "false")
     if kind == 2:  # dpx_kernel<S, GD>: GD = direction words in global scratch
         return "gmapdp::dpx_kernel<%d, %s>" % (R, "false" if dl else "true")
     if kind == 3:

@@ -569,6 +569,154 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
   }
 }
 
+// ---- row-major fill: the same recurrence with lanes over query rows ----
+// For a band much wider than the query (a short query against a long genome segment: the stage-3
+// single gaps across ~2000-nt genomic gaps), the band layout above spends R = W/64 words per lane on
+// a column that holds at most rlength + 1 live cells.  Here lane L owns rows r = L*R + i
+// (64*R >= rlength + 1), so a column costs R words however wide the band is.  The inputs swap
+// places: the horizontal (E) input is the same register one column back, the diagonal one is row
+// r - 1 (the register below, or DPP wave_shr:1 from the previous lane); the F chain is the same
+// max-plus scan.  Cells outside the band (k = r - c + uband outside [0, W)) are not computed and
+// read back as NEG_INFINITY, exactly as the band layout's edges.  Direction words: bit r / R of
+// word r % R (RowDirs).  No bridge carry, no stored scores (single and end gaps only).
+template <int R>
+__device__ __forceinline__ void fill_rows(int lane, int rlen, int glen, int lband, int uband, int open, int ext,
+                                          int late, int track, const int8_t* sc, int srow, const uint8_t* gcl,
+                                          uint64_t* dirs, int& bestr, int& bestc) {
+  const int sat = kNegInf32;
+  const int binit = (track == 2) ? kNegInf32 : 0;
+  int Hs[R], E[R], bv[R], bcol[R], rext[R];
+#pragma unroll
+  for (int i = 0; i < R; i++) {  // column 0 (dynprog.c:1331-1369)
+    const int r = lane * R + i;
+    int v = kNegInf32;
+    if (r <= rlen) v = (r == 0) ? 0 : (r <= lband ? open + r * ext : kNegInf32);
+    Hs[i] = v;
+    E[i] = kNegInf32;
+    bv[i] = binit;
+    bcol[i] = 0;
+    rext[i] = r * ext;
+  }
+  int rtop_ext = -uband * ext;  // (c - uband) * ext
+  int oce = open;               // open + c * ext
+  for (int c = 1; c <= glen; c++) {
+    const int gi = __builtin_amdgcn_readfirstlane(gcl[c]);
+    const int rtop = c - uband;
+    const int rlo = rtop < 1 ? 1 : rtop;
+    const int rhigh = (c + lband) < rlen ? (c + lband) : rlen;
+    rtop_ext += ext;
+    oce += ext;
+    const int L0 = (c == 1) ? (kNegInf32 - open + 1) : (c <= uband ? oce : kNegInf32);
+    const int row0 = (c <= uband) ? oce : kNegInf32;
+    const int8_t* scg = sc + gi * srow;
+    // diagonal input: row r - 1, previous column
+    int Hd[R];
+    Hd[0] = dpp_wave_shr1(Hs[R - 1], kNegInf32);
+#pragma unroll
+    for (int i = 1; i < R; i++) Hd[i] = Hs[i - 1];
+    int Hp[R], En[R], A[R];
+    bool valid[R], eb[R], hb[R];
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+      const int r = lane * R + i;
+      valid[i] = (r >= rlo) & (r <= rhigh);
+      const int s = scg[min(r, rlen + 1)];
+      const int es = Hs[i] + open;  // Egap from the same row (dynprog.c:1518-1524)
+      eb[i] = E[i] > es - late;
+      En[i] = max(E[i], es) + ext;
+      const int dg = Hd[i] + s;
+      hb[i] = En[i] > dg - late;
+      Hp[i] = max(En[i], dg);
+      A[i] = valid[i] ? Hp[i] + open - rext[i] : kSent;
+    }
+    int pre[R];
+    pre[0] = A[0];
+#pragma unroll
+    for (int i = 1; i < R; i++) pre[i] = max(pre[i - 1], A[i]);
+    const int X = dpp_wave_shr1(wave_scan_max(pre[R - 1]), kSent);
+    const int init = max(kNegInf32, L0 + open) - ((rtop > 1) ? rtop_ext - ext : 0);  // (rlo - 1) * ext
+    int F[R], Hun[R];
+    bool vb[R];
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+      const int ex = (i == 0) ? X : max(X, pre[i - 1]);
+      F[i] = rext[i] + max(init, ex);
+      vb[i] = F[i] > Hp[i] - late;
+      Hun[i] = max(F[i], Hp[i]);
+    }
+    const int Fup = dpp_wave_shr1(F[R - 1], kNegInf32);
+    const int Hup = dpp_wave_shr1(Hun[R - 1], kNegInf32);
+    uint64_t mH[R], mV[R], mE[R], mF[R];
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+      const int r = lane * R + i;
+      const bool top = r == rlo;
+      const int fprev = top ? kNegInf32 : ((i == 0) ? Fup : F[i - 1]);
+      const int hprev = top ? L0 : ((i == 0) ? Hup : Hun[i - 1]);
+      const bool fb = fprev > hprev + open - late;
+      const uint64_t mvalid = ballot(valid[i]);
+      mV[i] = ballot(vb[i]) & mvalid;
+      mH[i] = ballot(hb[i]) & ~mV[i] & mvalid;
+      mE[i] = ballot(eb[i]) & mvalid;
+      mF[i] = ballot(fb) & mvalid;
+      const int Hc = max(Hun[i], sat);
+      // band offset 0 keeps its unclamped value: its only reader is the next band-top cell's diagonal
+      Hs[i] = valid[i] ? ((r == rtop) ? Hun[i] : Hc) : ((r == 0) ? row0 : kNegInf32);
+      E[i] = valid[i] ? En[i] : kNegInf32;
+      const bool cand = valid[i] & ((track == 1) | ((track == 2) & (r == rlen))) & (Hc > bv[i] - late);
+      bv[i] = cand ? Hc : bv[i];
+      bcol[i] = cand ? c : bcol[i];
+    }
+    if (lane == 0) {
+      uint64_t* dcol = dirs + (size_t)c * 4 * R;
+#pragma unroll
+      for (int i = 0; i < R; i++) {
+        dcol[0 * R + i] = mH[i];
+        dcol[1 * R + i] = mV[i];
+        dcol[2 * R + i] = mE[i];
+        dcol[3 * R + i] = mF[i];
+      }
+    }
+  }
+  if (track) {  // as fill_band: the max (score, r, c) key is the reference's scan-order choice
+    uint64_t key = 0;
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+      if (bcol[i] > 0) {
+        const int r = lane * R + i;
+        const uint32_t rk = late ? (uint32_t)r : 4095u - (uint32_t)r;
+        const uint32_t ck = late ? (uint32_t)bcol[i] : 4095u - (uint32_t)bcol[i];
+        const uint64_t kk = ((uint64_t)(uint32_t)(bv[i] + (1 << 30)) << 24) | ((uint64_t)rk << 12) | ck;
+        key = kk > key ? kk : key;
+      }
+    }
+    key = wave_max_u64(key);
+    if (key == 0) {
+      bestr = (track == 2) ? rlen : 0;
+      bestc = 0;
+    } else {
+      const uint32_t rk = (uint32_t)(key >> 12) & 4095u, ck = (uint32_t)key & 4095u;
+      bestr = late ? (int)rk : 4095 - (int)rk;
+      bestc = late ? (int)ck : 4095 - (int)ck;
+    }
+  } else {
+    bestr = rlen;
+    bestc = glen;
+  }
+}
+
+// direction bits of fill_rows: row r in word r % R at bit r / R; cells outside the band read DIAG
+template <int R>
+struct RowDirs {
+  const uint64_t* dirs;
+  int W, uband;
+  __device__ uint32_t operator()(int c, int t, int r) const {
+    const int k = r - c + uband;
+    if (k < 0 || k >= W || r < 0) return 0u;
+    return (uint32_t)(dirs[((size_t)c * 4 + t) * R + (r % R)] >> (r / R)) & 1u;
+  }
+};
+
 // ---- wave-cooperative traceback (Dynprog_traceback_std, dynprog.c:1796-1948) ----
 // Emits the reference's push order into out[t.count ...].  `dir(c, t, r)` is the direction bit
 // t (0 nogap=HORIZ, 1 nogap=VERT, 2 Egap=HORIZ, 3 Fgap=VERT) of cell (r, c), 0 (DIAG) for

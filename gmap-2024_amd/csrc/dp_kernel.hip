@@ -68,8 +68,10 @@ extern "C" int gmapdp_debug_gg_marks(unsigned long long* out) {
   } while (0)
 #endif
 
-template <int R, bool DIRS_LDS>
-__global__ __launch_bounds__(64) void dp_kernel(
+// ROWS: lanes over query rows (fill_rows, R = row words) instead of band offsets, for bands much
+// wider than the query; dpr_kernel below.
+template <int R, bool DIRS_LDS, bool ROWS>
+__device__ __forceinline__ void dp_body(
     const DevProblem* __restrict__ probs, const int* __restrict__ order,
     const uint32_t* __restrict__ blocks, uint64_t nwords,
     const char* __restrict__ qseq, const char* __restrict__ qseq_uc,
@@ -167,8 +169,11 @@ __global__ __launch_bounds__(64) void dp_kernel(
 
   if (!(is_end && endalign == kQueryendNogaps)) {
     const int track = !is_end ? 0 : ((endalign == kQueryendIndels) ? 2 : 1);
-    fill_band<R, false>(lane, rlen, glen, lband, uband, P.open, P.extend, late, track, sc, srow, gcl, dirs,
-                        nullptr, bestr, bestc);
+    if constexpr (ROWS)
+      fill_rows<R>(lane, rlen, glen, lband, uband, P.open, P.extend, late, track, sc, srow, gcl, dirs, bestr, bestc);
+    else
+      fill_band<R, false>(lane, rlen, glen, lband, uband, P.open, P.extend, late, track, sc, srow, gcl, dirs,
+                          nullptr, bestr, bestc);
     if (DIRS_LDS) __syncthreads();
     else __threadfence_block();
   } else {
@@ -179,8 +184,12 @@ __global__ __launch_bounds__(64) void dp_kernel(
   if (is_end && endalign == kQueryendNogaps) {
     emit_diag(lane, bestr, bestc, bestr, G, q, quc, gch, cons, out, t);  // traceback_nogaps
   } else if (!skip) {
-    traceback_band<R>(lane, dirs, W, uband, bestr, bestc, G, q, quc, gch, cons, watson, P.chroffset, P.chrhigh,
-                      blocks, nwords, out, t);
+    if constexpr (ROWS)
+      traceback_walk(lane, RowDirs<R>{dirs, W, uband}, bestr, bestc, G, q, quc, gch, cons, watson, P.chroffset,
+                     P.chrhigh, blocks, nwords, out, t);
+    else
+      traceback_band<R>(lane, dirs, W, uband, bestr, bestc, G, q, quc, gch, cons, watson, P.chroffset, P.chrhigh,
+                        blocks, nwords, out, t);
   }
 
   int score = t.score + t.nmatches * kMatch + t.nmismatches * kMismatch;
@@ -209,6 +218,21 @@ __global__ __launch_bounds__(64) void dp_kernel(
     results[pid] = res;
   }
 }
+
+#define GMAPDP_DP_ARGS                                                                                  \
+  const DevProblem *__restrict__ probs, const int *__restrict__ order, const uint32_t *__restrict__ blocks, \
+      uint64_t nwords, const char *__restrict__ qseq, const char *__restrict__ qseq_uc,                  \
+      const int8_t *__restrict__ sctab, const uint8_t *__restrict__ constab,                             \
+      gmapdp_result *__restrict__ results, gmapdp_pair *__restrict__ pairs, uint64_t *__restrict__ gdirs
+template <int R, bool DIRS_LDS>
+__global__ __launch_bounds__(64) void dp_kernel(GMAPDP_DP_ARGS) {
+  dp_body<R, DIRS_LDS, false>(probs, order, blocks, nwords, qseq, qseq_uc, sctab, constab, results, pairs, gdirs);
+}
+template <int R, bool DIRS_LDS>
+__global__ __launch_bounds__(64) void dpr_kernel(GMAPDP_DP_ARGS) {
+  dp_body<R, DIRS_LDS, true>(probs, order, blocks, nwords, qseq, qseq_uc, sctab, constab, results, pairs, gdirs);
+}
+#undef GMAPDP_DP_ARGS
 
 // ===========================================================================
 // dpx_kernel<S>: Dynprog_single_gap / Dynprog_end{5,3}_gap for narrow bands,
@@ -940,33 +964,52 @@ __global__ __launch_bounds__(128) void gg_kernel(
 }
 
 // ---- host-side launch table ----
-template <int R, bool D>
-static void* kptr() { return reinterpret_cast<void*>(&dp_kernel<R, D>); }
+template <int R, bool D, bool ROWS>
+static void* kptr() {
+  if constexpr (ROWS) return reinterpret_cast<void*>(&dpr_kernel<R, D>);
+  else return reinterpret_cast<void*>(&dp_kernel<R, D>);
+}
 
 size_t lds_bytes_dp(int rlength, int glength, int R, bool dirs_lds) {
   return carve_dp(rlength, glength, R, dirs_lds).total;
 }
 
-hipError_t launch_dp(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevProblem* probs,
-                     const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
-                     const char* qseq_uc, const int8_t* sctab, const uint8_t* constab, gmapdp_result* results,
-                     gmapdp_pair* pairs, uint64_t* gdirs) {
+hipError_t launch_dp(int R, bool dirs_lds, bool rows, int nblocks, size_t lds, hipStream_t stream,
+                     const DevProblem* probs, const int* order, const uint32_t* blocks, uint64_t nwords,
+                     const char* qseq, const char* qseq_uc, const int8_t* sctab, const uint8_t* constab,
+                     gmapdp_result* results, gmapdp_pair* pairs, uint64_t* gdirs) {
   void* fn = nullptr;
 #define GMAPDP_CASE(RR)                                          \
   case RR:                                                       \
-    fn = dirs_lds ? kptr<RR, true>() : kptr<RR, false>();        \
+    fn = dirs_lds ? kptr<RR, true, false>() : kptr<RR, false, false>();        \
     break;
-  switch (R) {
-    GMAPDP_CASE(1)
-    GMAPDP_CASE(2)
-    GMAPDP_CASE(4)
-    GMAPDP_CASE(8)
-    GMAPDP_CASE(16)
-    GMAPDP_CASE(32)
-    GMAPDP_CASE(64)
-    default: return hipErrorInvalidValue;
+#define GMAPDP_RCASE(RR)                                         \
+  case RR:                                                       \
+    fn = dirs_lds ? kptr<RR, true, true>() : kptr<RR, false, true>();        \
+    break;
+  if (rows) {
+    switch (R) {  // 64 * 16 rows >= GMAPDP_MAX_RLENGTH + 1
+      GMAPDP_RCASE(1)
+      GMAPDP_RCASE(2)
+      GMAPDP_RCASE(4)
+      GMAPDP_RCASE(8)
+      GMAPDP_RCASE(16)
+      default: return hipErrorInvalidValue;
+    }
+  } else {
+    switch (R) {
+      GMAPDP_CASE(1)
+      GMAPDP_CASE(2)
+      GMAPDP_CASE(4)
+      GMAPDP_CASE(8)
+      GMAPDP_CASE(16)
+      GMAPDP_CASE(32)
+      GMAPDP_CASE(64)
+      default: return hipErrorInvalidValue;
+    }
   }
 #undef GMAPDP_CASE
+#undef GMAPDP_RCASE
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;

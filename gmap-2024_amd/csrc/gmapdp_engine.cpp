@@ -9,6 +9,7 @@
 //                                 NULL cases, segment orientation, bands per endalign)
 //   Compress_create_blocks_comp   compress-write.c:754  (.genomecomp packing)
 #include <hip/hip_runtime.h>
+#include <time.h>
 
 #include <algorithm>
 #include <cctype>
@@ -25,10 +26,10 @@
 
 namespace gmapdp {
 size_t lds_bytes_dp(int rlength, int glength, int R, bool dirs_lds);
-hipError_t launch_dp(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevProblem* probs,
-                     const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
-                     const char* qseq_uc, const int8_t* sctab, const uint8_t* constab, gmapdp_result* results,
-                     gmapdp_pair* pairs, uint64_t* gdirs);
+hipError_t launch_dp(int R, bool dirs_lds, bool rows, int nblocks, size_t lds, hipStream_t stream,
+                     const DevProblem* probs, const int* order, const uint32_t* blocks, uint64_t nwords,
+                     const char* qseq, const char* qseq_uc, const int8_t* sctab, const uint8_t* constab,
+                     gmapdp_result* results, gmapdp_pair* pairs, uint64_t* gdirs);
 size_t lds_slot_dpx(int rlength, int glength);
 size_t lds_dirs_dpx(int gmax);
 size_t lds_slot_sx(int rlength, int glength, int B);
@@ -260,7 +261,8 @@ struct gmapdp_ctx {
   uint64_t genome_length = 0;
   bool genome_owned = true;  // false: another context's HBM genome (gmapdp_share_genome)
   bool one_stream = false;   // GMAPDP_CTX_ONE_STREAM: no side streams (callers that run many contexts)
-  hipEvent_t ev_block = nullptr;  // GMAPDP_CTX_BLOCKING_SYNC: batch completion waited on without spinning
+  hipEvent_t ev_block = nullptr;  // GMAPDP_CTX_BLOCKING_SYNC / _POLL_SYNC: batch completion waited on without spinning
+  bool poll = false;              // GMAPDP_CTX_POLL_SYNC: ev_block is polled with sleeps in between
   DevBuf probs, order, qseq, qseq_uc, results, pairs, gdirs;
   DevBuf din, dout;    // run_batch: all inputs / all outputs of one synchronous batch
   HostBuf hin, hout;   // their pinned host images
@@ -275,10 +277,23 @@ struct gmapdp_ctx {
 // Wait for `s`: spinning (hipStreamSynchronize) by default; with GMAPDP_CTX_BLOCKING_SYNC the thread
 // sleeps on a blocking-sync event instead, so that callers running many dispatcher threads next to
 // their own compute threads (the GMAP drop-in) do not burn a core per waiting dispatcher.
+// With GMAPDP_CTX_POLL_SYNC it polls an event every GMAPDP_POLL_US microseconds (default 20) and
+// sleeps in between: the waiting thread gives its core to the caller's threads but still sees the
+// batch end within a poll period (a blocking-sync wake-up measured slower).
+static long poll_ns() {
+  static const long v = (getenv("GMAPDP_POLL_US") ? atol(getenv("GMAPDP_POLL_US")) : 20L) * 1000L;
+  return v;
+}
 static hipError_t ctx_sync(gmapdp_ctx* ctx, hipStream_t s) {
   if (!ctx->ev_block) return hipStreamSynchronize(s);
   hipError_t e = hipEventRecord(ctx->ev_block, s);
-  return e == hipSuccess ? hipEventSynchronize(ctx->ev_block) : e;
+  if (e != hipSuccess || !ctx->poll) return e == hipSuccess ? hipEventSynchronize(ctx->ev_block) : e;
+  const struct timespec ts = {0, poll_ns()};
+  for (;;) {
+    e = hipEventQuery(ctx->ev_block);
+    if (e != hipErrorNotReady) return e;
+    nanosleep(&ts, nullptr);
+  }
 }
 
 // A batch resolved on the host: GPU problems grouped into launch classes.
@@ -292,8 +307,8 @@ struct PlanCore {
   // kDpx: 64/S narrow problems per wave, R = S; kSx: SIMD-build single gaps, 64/B problems per wave,
   // R = B; kUxe / kUxg: SIMD-build end / genome gaps (triangle fills), one wave per problem, R = B
   // kGgp: Dynprog_genome_gap packed 64/S problems per wave (ggp_kernel.hip), R = cells per lane,
-  // lds = S
-  enum Kind { kDp = 0, kGenomeGap = 1, kDpx = 2, kSx = 3, kUxe = 4, kUxg = 5, kGgp = 6 };
+  // lds = S; kDpRows: dp_kernel's recurrence with lanes over query rows (dpr_kernel), R = row words
+  enum Kind { kDp = 0, kGenomeGap = 1, kDpx = 2, kSx = 3, kUxe = 4, kUxg = 5, kGgp = 6, kDpRows = 7 };
   struct Launch {
     int kind;
     int R;           // band words per lane (kDp, kGenomeGap) or segment width S (kDpx)
@@ -376,8 +391,12 @@ int gmapdp_create_ex(gmapdp_ctx** out, int device, int mode, int user_open, int 
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join[i], hipEventDisableTiming);
   }
   if (e == hipSuccess && !ctx->one_stream) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
-  if (e == hipSuccess && (flags & GMAPDP_CTX_BLOCKING_SYNC))
+  if (e == hipSuccess && (flags & GMAPDP_CTX_POLL_SYNC)) {
+    e = hipEventCreateWithFlags(&ctx->ev_block, hipEventDisableTiming);
+    ctx->poll = true;
+  } else if (e == hipSuccess && (flags & GMAPDP_CTX_BLOCKING_SYNC)) {
     e = hipEventCreateWithFlags(&ctx->ev_block, hipEventDisableTiming | hipEventBlockingSync);
+  }
   ctx->tables = new Tables();
   build_tables(*ctx->tables, mode);
   if (e == hipSuccess) e = hipMalloc(&ctx->d_sc, sizeof(ctx->tables->sc));
@@ -625,6 +644,11 @@ static bool ggp_s8() {
 }
 static size_t gg_lds_dirs_max() {
   static const size_t v = env_size("GMAPDP_GG_LDS_DIRS_MAX", 0);
+  return v;
+}
+// GMAPDP_DP_ROWS=0 keeps every single / end gap in the band layout (experiments, tests)
+static bool rows_disabled() {
+  static const bool v = env_size("GMAPDP_DP_ROWS", 1) == 0;
   return v;
 }
 // Batches of at most this many problems are planned for latency (classify); GMAPDP_LATENCY_BATCH
@@ -930,8 +954,12 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
         continue;
       }
     }
-    const int R = nofill ? 1 : pick_R(W);
+    int R = nofill ? 1 : pick_R(W);
     if (R > kMaxR) return bad(ctx, "band wider than 4096");
+    // a band wider than the query: lanes over the query's rows cost fewer words per column
+    const int Rrows = pick_R(d.rlength + 1);
+    const bool rows = !nofill && Rrows < R && !rows_disabled();
+    if (rows) R = Rrows;
     size_t lds = lds_bytes_dp(d.rlength, d.glength, R, !nofill);
     bool dirs_lds = !nofill && lds <= kLdsBudget;
     d.dirs_offset = 0;
@@ -943,7 +971,7 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
       }
     }
     if (lds > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
-    add((int)PlanCore::kDp, R, dirs_lds ? 1 : 0, lds_bucket(lds), s);
+    add((int)(rows ? PlanCore::kDpRows : PlanCore::kDp), R, dirs_lds ? 1 : 0, lds_bucket(lds), s);
   }
   for (size_t s = 0; s < plan.gdev.size(); s++) {
     DevGenomeProblem& d = plan.gdev[s];
@@ -1192,8 +1220,9 @@ static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, cons
                       L.dirs_lds ? nullptr : (unsigned char*)ctx->gdirs.p + L.gdirs_offset, stream, a.d_probs,
                       a.d_order + L.first, ctx->d_genome, ctx->genome_words, a.d_q, a.d_quc, ctx->d_sc, ctx->d_cs,
                       a.d_results, a.d_pairs);
-  if (L.kind == PlanCore::kDp)
-    return launch_dp(L.R, L.dirs_lds, L.count, L.lds, stream, a.d_probs, a.d_order + L.first, ctx->d_genome,
+  if (L.kind == PlanCore::kDp || L.kind == PlanCore::kDpRows)
+    return launch_dp(L.R, L.dirs_lds, L.kind == PlanCore::kDpRows, L.count, L.lds, stream, a.d_probs,
+                     a.d_order + L.first, ctx->d_genome,
                      ctx->genome_words, a.d_q, a.d_quc, ctx->d_sc, ctx->d_cs, a.d_results, a.d_pairs,
                      (uint64_t*)ctx->gdirs.p);
   if (!a.d_gresults || !a.d_sprob) return hipErrorInvalidValue;

@@ -18,7 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GMAPDP_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libgmapdp.so")
 
 WATSON, JUMP_LATE, WIDEBAND = 0x1, 0x2, 0x4
-CTX_ONE_STREAM, CTX_PRIO_HIGH, CTX_PRIO_LOW, CTX_BLOCKING_SYNC = 0x1, 0x2, 0x4, 0x8  # gmapdp_create_ex flags
+CTX_ONE_STREAM, CTX_PRIO_HIGH, CTX_PRIO_LOW, CTX_BLOCKING_SYNC, CTX_POLL_SYNC = 0x1, 0x2, 0x4, 0x8, 0x10  # create_ex flags
 SIMD = 0x40  # GMAPDP_SIMD: the reference's SIMD builds' semantics (every problem family)
 HALFP, FINALP = 0x8, 0x10
 UNSET = -2147483648

@@ -50,6 +50,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <pthread.h>
+#include <sys/prctl.h>
 
 #include "bool.h"
 #include "list.h"
@@ -209,6 +210,7 @@ shim_check_call (Genome_T genome, Genome_T genomealt, Dynprog_T dynprog) {
    a -g run over a multi-sequence file has several) is uploaded to HBM once, as a device genome every
    dispatcher context reads (gmapdp_dgenome_create / gmapdp_use_dgenome). */
 static __thread int shim_reserved = 0;
+static int shim_oligo_queue = 2;            /* the queue of stage 3's oligoindex calls (GMAPDP_SHIM_OLIGO_QUEUE) */
 static __thread int shim_qi = 0;            /* the dispatcher's queue: 0 Dynprog_*, 1 stage 2, 2 long fills */
 typedef struct shim_dgenome {
   Genome_T genome;
@@ -229,15 +231,22 @@ shim_context (Genome_T genome) {
   shim_dgenome *e;
   uint64_t length;
   size_t nwords;
-  if (shim_ctx == NULL)
+  if (shim_ctx == NULL) {
+    /* GMAPDP_SHIM_BLOCKING=1: the dispatchers wait on blocking-sync events instead of spinning (measured
+       slower end to end: the wake-up adds to every batch, and the HIP wait still spins at first) */
+    const char *blk = getenv("GMAPDP_SHIM_BLOCKING"), *poll = getenv("GMAPDP_SHIM_POLL");
+    const int wait = blk != NULL && blk[0] == '1' ? GMAPDP_CTX_BLOCKING_SYNC
+                     : (poll != NULL && poll[0] == '1' ? GMAPDP_CTX_POLL_SYNC : 0);
     shim_check(gmapdp_create_ex(&shim_ctx, shim_device(), shim_mode, shim_user_open, shim_user_extend,
-                                shim_user_dynprog_p,
-                                GMAPDP_CTX_ONE_STREAM | GMAPDP_CTX_BLOCKING_SYNC |
+                                shim_user_dynprog_p, GMAPDP_CTX_ONE_STREAM | wait |
                                     (shim_qi != 1 ? GMAPDP_CTX_PRIO_HIGH : GMAPDP_CTX_PRIO_LOW)),
                "gmapdp_create_ex");
+  }
   if (!shim_reserved) {  /* staging and scratch sized up front: growing them later stalls the device */
     shim_check(gmapdp_reserve(shim_ctx, shim_qi == 1 ? (size_t) 64 << 20 : (size_t) 16 << 20,
-                              shim_qi == 1 ? GMAPDP_RESERVE_STAGE2 : GMAPDP_RESERVE_DP | GMAPDP_RESERVE_AUX),
+                              shim_qi == 1 ? GMAPDP_RESERVE_STAGE2
+                                           : GMAPDP_RESERVE_DP | GMAPDP_RESERVE_AUX |
+                                                 (shim_qi == shim_oligo_queue ? GMAPDP_RESERVE_STAGE2 : 0)),
                "gmapdp_reserve");
     shim_reserved = 1;
   }
@@ -306,12 +315,15 @@ typedef struct shim_req {
   size_t mxccap, mxpcap;
   int done;
   int longp;                    /* a long fill: queue 2 */
+  long cost;                    /* shim_cost of the fill (diagnostics) */
+  pthread_mutex_t mtx;          /* guards done (the calling thread sleeps on cv) */
   pthread_cond_t cv;
   struct shim_req *next;
 } shim_req;
 
-/* Two queues: 0 for the Dynprog_* calls (short, ~150 per read), 1 for stage 2 (one long call per
-   read), so that a stage-2 batch never holds back the DP calls queued behind it. */
+/* Three queues: 0 for the short Dynprog_* calls (~250 per read), 1 for Stage2_compute (two ~10-ms
+   batches per read), 2 for the long fills and stage 3's oligoindex calls, so that no call waits
+   behind a batch far longer than its own work. */
 static pthread_mutex_t q_lock = PTHREAD_MUTEX_INITIALIZER;
 static pthread_cond_t q_cond[3] = {PTHREAD_COND_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_COND_INITIALIZER};
 static shim_req *q_head[3] = {NULL, NULL, NULL}, *q_tail[3] = {NULL, NULL, NULL};
@@ -347,10 +359,12 @@ shim_request (int kind) {
     r = (shim_req *) calloc(1, sizeof(shim_req));
     if (r == NULL) shim_refuse("host memory for a request (out of memory)");
     pthread_cond_init(&r->cv, NULL);
+    pthread_mutex_init(&r->mtx, NULL);
     tl_req = r;
   }
   r->kind = kind;
   r->longp = 0;
+  r->cost = 0;
   r->q = r->quc = NULL;
   r->qlen = 0;
   r->probs = NULL;
@@ -369,6 +383,7 @@ shim_dispatch (void *arg) {
   shim_qi = qi;
   snprintf(name, sizeof(name), "gmapdp-q%d", qi);
   pthread_setname_np(pthread_self(), name);  /* per-thread CPU accounting (tools/thread_cpu.py) */
+  prctl(PR_SET_TIMERSLACK, 2000UL, 0, 0, 0);  /* GMAPDP_SHIM_POLL: short sleeps between completion polls */
   for (;;) {
     pthread_mutex_lock(&q_lock);
     while (q_head[qi] == NULL) pthread_cond_wait(&q_cond[qi], &q_lock);
@@ -386,13 +401,14 @@ shim_dispatch (void *arg) {
         else { *rt = r; rt = &r->next; }
       }
       shim_run(same);
-      pthread_mutex_lock(&q_lock);
+      /* wake each caller under its own request's lock: no herd on the queue lock */
       for (r = same; r != NULL; r = next) {
         next = r->next;
+        pthread_mutex_lock(&r->mtx);
         r->done = 1;
         pthread_cond_signal(&r->cv);
+        pthread_mutex_unlock(&r->mtx);
       }
-      pthread_mutex_unlock(&q_lock);
       batch = rest;
     }
   }
@@ -406,26 +422,27 @@ shim_submit (shim_req *r) {
   pthread_attr_t attr;
   const char *st;
   int nd, nd2, nl, k;
-  const int qi = r->kind >= K_OLIGO ? 1 : (r->longp ? 2 : 0);
+  int qi;
   pthread_mutex_lock(&q_lock);
   if (!dispatcher_started) {
     st = getenv("GMAPDP_SHIM_STATS");
     if (st != NULL && st[0] == '1') atexit(shim_print_stats);
     st = getenv("GMAPDP_SHIM_TRACE");
     if (st != NULL && st[0] != '\0') shim_trace = fopen(st, "w");
-    /* One hardware queue per dispatcher stream: 3 short + 3 long + 2 stage-2 dispatchers on 8 queues.
-       HIP reads GPU_MAX_HW_QUEUES (default 4) when the process first touches the GPU, which is later,
-       in a dispatcher; a value the user set is kept. */
-    setenv("GPU_MAX_HW_QUEUES", "8", 0);
+    /* 2 short + 1 long + 2 stage-2 dispatchers, one stream each, on HIP's default 4 hardware queues
+       (GPU_MAX_HW_QUEUES): measured end to end, more queues or dispatchers made every batch slower
+       (tools/e2e_timing.py --configs, profiles/r03_e2e). */
     st = getenv("GMAPDP_SHIM_DISPATCHERS");
-    nd = st != NULL ? atoi(st) : 3;
+    nd = st != NULL ? atoi(st) : 2;
     if (nd < 1) nd = 1;
     st = getenv("GMAPDP_SHIM_LONG_DISPATCHERS");
-    nl = st != NULL ? atoi(st) : 3;
+    nl = st != NULL ? atoi(st) : 1;
     if (nl < 1) nl = 1;
     st = getenv("GMAPDP_SHIM_STAGE2_DISPATCHERS");
     nd2 = st != NULL ? atoi(st) : 2;
     if (nd2 < 1) nd2 = 1;
+    st = getenv("GMAPDP_SHIM_OLIGO_QUEUE");
+    if (st != NULL && atoi(st) >= 0 && atoi(st) <= 2) shim_oligo_queue = atoi(st);
     st = getenv("GMAPDP_SHIM_LONG_COST");
     if (st != NULL) shim_long_cost = atol(st);
     pthread_attr_init(&attr);
@@ -436,14 +453,17 @@ shim_submit (shim_req *r) {
     pthread_attr_destroy(&attr);
     dispatcher_started = 1;
   }
+  qi = r->kind == K_STAGE2 ? 1 : (r->kind == K_OLIGO ? shim_oligo_queue : (r->longp ? 2 : 0));
   r->done = 0;
   r->next = NULL;
   if (q_tail[qi] != NULL) q_tail[qi]->next = r;
   else q_head[qi] = r;
   q_tail[qi] = r;
   pthread_cond_signal(&q_cond[qi]);
-  while (!r->done) pthread_cond_wait(&r->cv, &q_lock);
   pthread_mutex_unlock(&q_lock);
+  pthread_mutex_lock(&r->mtx);
+  while (!r->done) pthread_cond_wait(&r->cv, &r->mtx);
+  pthread_mutex_unlock(&r->mtx);
 }
 
 /* dispatcher-owned staging, grown as needed */
@@ -790,12 +810,20 @@ shim_run (shim_req *batch) {
   pthread_mutex_lock(&q_lock);
   for (i = 0; i < 4; i++) shim_secs[i] += td[i];
   if (shim_trace != NULL) {  /* GMAPDP_SHIM_TRACE=<file>: one line per dispatcher batch */
-    int gmax = 0;
+    int gmax = 0, mk = -1, mr = 0, mg = 0;
+    long mc = -1;
     for (i = 0; i < ns; i++) gmax = D.s[i].glength > gmax ? D.s[i].glength : gmax;
     for (i = 0; i < ne; i++) gmax = D.e[i].glength > gmax ? D.e[i].glength : gmax;
     for (i = 0; i < ng; i++) gmax = D.g[i].glengthL > gmax ? D.g[i].glengthL : gmax;
-    fprintf(shim_trace, "%d %.6f %zu %zu %zu %zu %zu %zu %zu %d %.6f %.6f %.6f %.6f\n", shim_qi, shim_now(), ns, ne, ng,
-            nc, nxs, nxf, n2, gmax, td[0], td[1], td[2], td[3]);
+    for (r = batch; r != NULL; r = r->next)  /* the costliest fill: kind, rlength, glength, cost */
+      if (r->cost > mc && r->kind <= K_GENOME) {
+        mc = r->cost;
+        mk = r->kind;
+        mr = r->kind == K_SINGLE ? r->p.s.rlength : (r->kind == K_END ? r->p.e.rlength : r->p.g.rlength);
+        mg = r->kind == K_SINGLE ? r->p.s.glength : (r->kind == K_END ? r->p.e.glength : r->p.g.glengthL);
+      }
+    fprintf(shim_trace, "%d %.6f %zu %zu %zu %zu %zu %zu %zu %d %.6f %.6f %.6f %.6f %d %d %d %ld\n", shim_qi, shim_now(),
+            ns, ne, ng, nc, nxs, nxf, n2, gmax, td[0], td[1], td[2], td[3], mk, mr, mg, mc);
   }
   pthread_mutex_unlock(&q_lock);
 }
@@ -857,7 +885,9 @@ __wrap_Dynprog_single_gap (int *dynprogindex, int *finalscore, int *nmatches, in
   r->q = sequence1;
   r->quc = sequenceuc1;
   r->qlen = length1 > 0 ? (size_t) length1 : 0;
-  r->longp = shim_cost(length1, length2, extraband_single) > shim_long_cost;
+  /* a call past the size guard (dynprog_single.c:509-521) is answered without a fill */
+  r->cost = length1 > GMAPDP_MAX_RLENGTH || length2 > GMAPDP_MAX_GLENGTH ? 0 : shim_cost(length1, length2, extraband_single);
+  r->longp = r->cost > shim_long_cost;
   GROW(r->pairs, r->pcap, gmapdp_single_pair_capacity(p, 1) + 1);
   shim_submit(r);
   shim_count(ST_SINGLE);
@@ -902,7 +932,8 @@ shim_end_gap (int end3p, int *dynprogindex, int *finalscore, int *nmatches, int 
   r->q = (end3p || length1 <= 0) ? seq : seq - (length1 - 1);
   r->quc = (end3p || length1 <= 0) ? sequc : sequc - (length1 - 1);
   r->qlen = length1 > 0 ? (size_t) length1 : 0;
-  r->longp = shim_cost(length1 > 660 ? 660 : length1, length2, extraband_end) > shim_long_cost;
+  r->cost = shim_cost(length1 > 660 ? 660 : length1, length2, extraband_end);
+  r->longp = r->cost > shim_long_cost;
   GROW(r->pairs, r->pcap, gmapdp_end_pair_capacity(p, 1) + 1);
   shim_submit(r);
   shim_count(end3p ? ST_END3 : ST_END5);
@@ -1017,7 +1048,8 @@ __wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_r
   r->qlen = rlength > 0 ? (size_t) rlength : 0;
   r->probs = r->pbuf;
   r->nprobs = m;
-  r->longp = 2 * shim_cost(rlength, glengthL > glengthR ? glengthL : glengthR, extraband_paired) > shim_long_cost;
+  r->cost = m == 0 ? 0 : 2 * shim_cost(rlength, glengthL > glengthR ? glengthL : glengthR, extraband_paired);
+  r->longp = r->cost > shim_long_cost;
   GROW(r->pairs, r->pcap, gmapdp_genome_pair_capacity(p, 1) + 1);
   shim_submit(r);
   shim_count(ST_GENOME);

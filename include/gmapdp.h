@@ -543,11 +543,13 @@ void gmapdp_destroy (gmapdp_ctx *ctx);
  * dispatcher threads): GMAPDP_CTX_ONE_STREAM creates no side streams (a process has few hardware
  * queues, GPU_MAX_HW_QUEUES, and streams beyond them share one and serialise); GMAPDP_CTX_PRIO_HIGH /
  * _LOW create the context's stream at the device's highest / lowest priority; GMAPDP_CTX_BLOCKING_SYNC
- * makes the synchronous batch calls wait without spinning. */
+ * makes the synchronous batch calls wait without spinning; GMAPDP_CTX_POLL_SYNC makes them poll the
+ * batch's completion every GMAPDP_POLL_US microseconds (default 20) and sleep in between. */
 #define GMAPDP_CTX_ONE_STREAM 0x1
 #define GMAPDP_CTX_PRIO_HIGH  0x2
 #define GMAPDP_CTX_PRIO_LOW   0x4
 #define GMAPDP_CTX_BLOCKING_SYNC 0x8  /* batch calls sleep on a blocking-sync event instead of spinning */
+#define GMAPDP_CTX_POLL_SYNC 0x10     /* batch calls poll their completion, sleeping between polls */
 int gmapdp_create_ex (gmapdp_ctx **ctx, int device, int mode, int user_open, int user_extend, int user_dynprog_p,
                       int flags);
 /* Use `owner`'s HBM-resident genome in `ctx` (no copy; same device).  `owner` must outlive every

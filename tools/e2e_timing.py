@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--gpu-threads", default=None, help="thread counts for the GPU program (default: --threads)")
     ap.add_argument("--dispatchers", type=int, default=3, help="GMAPDP_SHIM_DISPATCHERS")
     ap.add_argument("--trace", default=None, help="directory for the shim's per-batch traces (GMAPDP_SHIM_TRACE)")
+    ap.add_argument("--configs", default="default:",
+                    help="shim configurations for the GPU runs, 'name:VAR=V,VAR=V;name2:...' (environment overrides)")
+    ap.add_argument("--skip-cpu", action="store_true")
     a = ap.parse_args()
     import make_e2e as M
     genome = list(M.synth_genome())
@@ -46,14 +49,20 @@ def main():
     sams = {}
     cpu_t = [int(x) for x in a.threads.split(",")]
     gpu_t = [int(x) for x in (a.gpu_threads or a.threads).split(",")]
-    runs = [("gmap_%s" % a.build, t) for t in cpu_t] + [("gmap_gpu_%s" % a.build, t) for t in gpu_t]
+    configs = []
+    for c in a.configs.split(";"):
+        name, _, kv = c.partition(":")
+        configs.append((name, dict(x.split("=", 1) for x in kv.split(",") if x)))
+    runs = [] if a.skip_cpu else [("gmap_%s" % a.build, t, "cpu", {}) for t in cpu_t]
+    runs += [("gmap_gpu_%s" % a.build, t, name, cenv) for name, cenv in configs for t in gpu_t]
     out["dispatchers"] = a.dispatchers
-    for prog, t in runs:
+    for prog, t, cname, cenv in runs:
         if True:
             env = dict(os.environ, GMAPDP_SHIM_STATS="1", GMAPDP_SHIM_DISPATCHERS=str(a.dispatchers))
+            env.update(cenv)
             if a.trace and "gpu" in prog:
                 os.makedirs(a.trace, exist_ok=True)
-                env["GMAPDP_SHIM_TRACE"] = os.path.abspath(os.path.join(a.trace, "trace_t%d.txt" % t))
+                env["GMAPDP_SHIM_TRACE"] = os.path.abspath(os.path.join(a.trace, "trace_%s_t%d.txt" % (cname, t)))
             args = [os.path.join(ref, prog), "-t", str(t), "-O", "-g", "g.fa", "-f", "samse", "--no-sam-headers",
                     "r.fa"]
             t0 = time.perf_counter()
@@ -64,13 +73,13 @@ def main():
             cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
             if r.returncode != 0:
                 raise SystemExit("%s failed: %s" % (prog, r.stderr[-2000:]))
-            sams[(prog, t)] = r.stdout
+            sams[(prog, t, cname)] = r.stdout
             stats = [l for l in r.stderr.splitlines() if l.startswith("gmapdp shim calls")]
-            out["runs"].append({"program": prog, "threads": t, "seconds": dt, "reads_per_s": a.reads / dt,
+            out["runs"].append({"program": prog, "threads": t, "config": cname, "env": cenv, "seconds": dt, "reads_per_s": a.reads / dt,
                                 "cpu_seconds": cpu, "cpu_cores_busy": cpu / dt,
                                 "shim_calls": stats[0] if stats else None})
             print(json.dumps(out["runs"][-1]), file=sys.stderr, flush=True)
-    base = sams[("gmap_%s" % a.build, min(cpu_t))]
+    base = next(iter(sams.values())) if a.skip_cpu else sams[("gmap_%s" % a.build, min(cpu_t), "cpu")]
     out["outputs_identical"] = all(v == base for v in sams.values())
     print(json.dumps(out))
 
