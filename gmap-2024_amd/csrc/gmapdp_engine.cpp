@@ -277,11 +277,11 @@ struct gmapdp_ctx {
 // Wait for `s`: spinning (hipStreamSynchronize) by default; with GMAPDP_CTX_BLOCKING_SYNC the thread
 // sleeps on a blocking-sync event instead, so that callers running many dispatcher threads next to
 // their own compute threads (the GMAP drop-in) do not burn a core per waiting dispatcher.
-// With GMAPDP_CTX_POLL_SYNC it polls an event every GMAPDP_POLL_US microseconds (default 20) and
+// With GMAPDP_CTX_POLL_SYNC it polls an event every GMAPDP_POLL_US microseconds (default 10) and
 // sleeps in between: the waiting thread gives its core to the caller's threads but still sees the
 // batch end within a poll period (a blocking-sync wake-up measured slower).
 static long poll_ns() {
-  static const long v = (getenv("GMAPDP_POLL_US") ? atol(getenv("GMAPDP_POLL_US")) : 20L) * 1000L;
+  static const long v = (getenv("GMAPDP_POLL_US") ? atol(getenv("GMAPDP_POLL_US")) : 10L) * 1000L;
   return v;
 }
 static hipError_t ctx_sync(gmapdp_ctx* ctx, hipStream_t s) {
@@ -2387,6 +2387,187 @@ extern "C" int gmapdp_microexon_finish(gmapdp_ctx* ctx, const gmapdp_microexon_p
   if (e == hipSuccess) e = ctx_sync(ctx, s);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "microexon finish: %s", e);
   return GMAPDP_OK;
+}
+
+// The drop-in's dispatcher batch in one round trip (gmapdp_mixed_batch).  One pinned host image and
+// one device image hold [inputs | outputs]: the DP descriptors and launch orders, the query arena,
+// the splice probabilities, the microexon searches and finishes (the finishes' results, which their
+// kernel updates in place, are the last input section), then the DP results and pairs, the searches'
+// results and candidate pool, the finishes' pairs.  One copy up, the kernels, one copy down from
+// the finishes' results to the end, one wait.  A search that overflows the pool (a result with
+// cand_offset -2) or holds more candidates than its LDS (-1) is rerun by gmapdp_microexon_search.
+extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char* qseq_uc, size_t qbytes,
+                                  gmapdp_mixed* m) {
+  if (!ctx || !m) return GMAPDP_EINVAL;
+  const int nsingle = m->nsingle, nend = m->nend, ngenome = m->ngenome, nxs = m->nsearch, nxf = m->nfinish;
+  if (nsingle < 0 || nend < 0 || ngenome < 0 || nxs < 0 || nxf < 0) return GMAPDP_EINVAL;
+  if ((nsingle && !m->singles) || (nend && !m->ends) || (ngenome && !m->genomes) ||
+      (nsingle + nend && !m->results) || (ngenome && !m->genome_results) || (nxs && (!m->searches || !m->search_results)) ||
+      (nxf && (!m->finishes || !m->finish_results)))
+    return GMAPDP_EINVAL;
+  m->candidates_needed = 0;
+  if (!ctx->d_genome) return GMAPDP_ENOGENOME;
+  if (nsingle + nend + ngenome + nxs + nxf == 0) return GMAPDP_OK;
+  if (!qseq || !qseq_uc) return GMAPDP_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  // ---- DP plan (as run_batch) ----
+  PlanCore plan;
+  if (nsingle + nend + ngenome) {
+    int rc = build_plan(ctx, m->singles, nsingle, m->ends, nend, m->genomes, ngenome, m->results, m->genome_results,
+                        plan);
+    if (rc) return rc;
+    if (plan.pair_capacity > m->pair_capacity || (plan.pair_capacity && !m->pairs)) return bad(ctx, "pair arena too small");
+    for (size_t s = 0; s < plan.dev.size(); s++) {
+      const int i = plan.dev_problem[s];
+      const long lo = i < nsingle ? m->singles[i].qoff : m->ends[i - nsingle].qoff;
+      const long len = i < nsingle ? m->singles[i].rlength : m->ends[i - nsingle].rlength;
+      if (lo < 0 || (size_t)(lo + len) > qbytes) return bad(ctx, "query slice outside the query arena");
+    }
+    for (size_t s = 0; s < plan.gdev.size(); s++) {
+      const gmapdp_genome_problem& g = m->genomes[plan.gdev_problem[s]];
+      if (g.qoff < 0 || (size_t)((long)g.qoff + g.rlength) > qbytes) return bad(ctx, "query slice outside the query arena");
+      if (!m->splice_probs || g.prob_offset < 0 ||
+          (size_t)g.prob_offset + (size_t)g.glengthL + (size_t)g.glengthR > m->nprobs)
+        return bad(ctx, "splice probabilities outside the probability arena");
+    }
+  }
+  const int ndev = (int)plan.dev.size(), ngdev = (int)plan.gdev.size();
+  // ---- microexon sections (as gmapdp_microexon_search / _finish) ----
+  for (int i = 0; i < nxs; i++) {
+    const gmapdp_microexon_problem& p = m->searches[i];
+    if (p.rlength < 0 || p.qoff < 0 || (size_t)p.qoff + (size_t)p.rlength > qbytes)
+      return bad(ctx, "microexon: query slice outside the query arena");
+  }
+  std::vector<gmapdp_microexon_result> fres(m->finish_results, m->finish_results + nxf);
+  size_t fpoff = 0;
+  for (int i = 0; i < nxf; i++) {
+    const gmapdp_microexon_problem& p = m->finishes[i];
+    if (p.rlength < 0 || p.qoff < 0 || (size_t)p.qoff + (size_t)p.rlength > qbytes)
+      return bad(ctx, "microexon: query slice outside the query arena");
+    if (fres[i].ncandidates < 0 ||
+        (fres[i].ncandidates > 0 && (fres[i].cand_offset < 0 ||
+                                     (size_t)fres[i].cand_offset + fres[i].ncandidates > m->nfinish_candidates)))
+      return bad(ctx, "microexon: candidates outside the candidate array");
+    fres[i].pair_offset = (int64_t)fpoff;
+    fpoff += (size_t)std::max(p.rlength, 0) + 2;
+  }
+  if (nxf && (fpoff > m->finish_pair_capacity || !m->finish_pairs)) return bad(ctx, "microexon: pair arena too small");
+  if (m->nfinish_candidates && (!m->finish_candidates || !m->finish_probs)) return GMAPDP_EINVAL;
+  const size_t nfc = nxf ? m->nfinish_candidates : 0;
+  const size_t pool = nxs ? std::max<size_t>(4096, 16 * (size_t)nxs) : 0;  // search candidates
+  // ---- one image: inputs, then outputs ----
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t o = 0;
+  const size_t o_probs = o;   o += al(sizeof(DevProblem) * ndev);
+  const size_t o_order = o;   o += al(sizeof(int) * ndev);
+  const size_t o_gprobs = o;  o += al(sizeof(DevGenomeProblem) * ngdev);
+  const size_t o_gorder = o;  o += al(sizeof(int) * ngdev);
+  const size_t nsp = ngdev ? m->nprobs : 0;
+  const size_t o_sprob = o;   o += al(sizeof(double) * nsp);
+  const size_t o_q = o;       o += al(qbytes);
+  const size_t o_quc = o;     o += al(qbytes);
+  const size_t o_xs = o;      o += al(sizeof(gmapdp_microexon_problem) * nxs);
+  const size_t o_xcnt = o;    o += al(sizeof(unsigned long long));
+  const size_t o_xf = o;      o += al(sizeof(gmapdp_microexon_problem) * nxf);
+  const size_t o_xfc = o;     o += al(sizeof(gmapdp_microexon_candidate) * nfc);
+  const size_t o_xfp = o;     o += al(sizeof(double) * 2 * nfc);
+  const size_t o_xfres = o;   o += al(sizeof(gmapdp_microexon_result) * nxf);  // in and out
+  const size_t in_bytes = o_xfres + sizeof(gmapdp_microexon_result) * nxf;
+  const size_t r_res = o;     o += al(sizeof(gmapdp_result) * ndev);
+  const size_t r_gres = o;    o += al(sizeof(gmapdp_genome_result) * ngdev);
+  const size_t r_pairs = o;   o += al(sizeof(gmapdp_pair) * plan.pair_capacity);
+  const size_t r_xsres = o;   o += al(sizeof(gmapdp_microexon_result) * nxs);
+  const size_t r_xcand = o;   o += al(sizeof(gmapdp_microexon_candidate) * pool);
+  const size_t r_xfpairs = o; o += al(sizeof(gmapdp_pair) * fpoff);
+  const size_t total = o;
+  hipError_t e = ctx->hin.ensure(total);
+  if (e == hipSuccess) e = ctx->din.ensure(total);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "batch buffers: %s", e);
+  unsigned char* h = (unsigned char*)ctx->hin.p;
+  unsigned char* d = (unsigned char*)ctx->din.p;
+  if (ndev) {
+    std::memcpy(h + o_probs, plan.dev.data(), sizeof(DevProblem) * ndev);
+    std::memcpy(h + o_order, plan.order.data(), sizeof(int) * ndev);
+  }
+  if (ngdev) {
+    std::memcpy(h + o_gprobs, plan.gdev.data(), sizeof(DevGenomeProblem) * ngdev);
+    std::memcpy(h + o_gorder, plan.gorder.data(), sizeof(int) * ngdev);
+    std::memcpy(h + o_sprob, m->splice_probs, sizeof(double) * nsp);
+  }
+  std::memcpy(h + o_q, qseq, qbytes);
+  std::memcpy(h + o_quc, qseq_uc, qbytes);
+  if (nxs) std::memcpy(h + o_xs, m->searches, sizeof(gmapdp_microexon_problem) * nxs);
+  std::memset(h + o_xcnt, 0, sizeof(unsigned long long));
+  if (nxf) {
+    std::memcpy(h + o_xf, m->finishes, sizeof(gmapdp_microexon_problem) * nxf);
+    std::memcpy(h + o_xfres, fres.data(), sizeof(gmapdp_microexon_result) * nxf);
+  }
+  if (nfc) {
+    std::memcpy(h + o_xfc, m->finish_candidates, sizeof(gmapdp_microexon_candidate) * nfc);
+    std::memcpy(h + o_xfp, m->finish_probs, sizeof(double) * 2 * nfc);
+  }
+  hipStream_t s = ctx->stream;
+  e = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "upload: %s", e);
+  if (ndev + ngdev) {
+    RunArgs a;
+    a.d_probs = (const DevProblem*)(d + o_probs);
+    a.d_order = (const int*)(d + o_order);
+    a.d_gprobs = (const DevGenomeProblem*)(d + o_gprobs);
+    a.d_gorder = (const int*)(d + o_gorder);
+    a.d_q = (const char*)(d + o_q);
+    a.d_quc = (const char*)(d + o_quc);
+    a.d_sprob = (const double*)(d + o_sprob);
+    a.d_results = (gmapdp_result*)(d + r_res);
+    a.d_gresults = (gmapdp_genome_result*)(d + r_gres);
+    a.d_pairs = (gmapdp_pair*)(d + r_pairs);
+    const int rc = run_plan(ctx, plan, a, s);
+    if (rc) return rc;
+  }
+  if (nxs)
+    e = launch_mx_search(nxs, s, (const gmapdp_microexon_problem*)(d + o_xs), ctx->d_genome, ctx->genome_words,
+                         (const char*)(d + o_q), (const char*)(d + o_quc), (gmapdp_microexon_result*)(d + r_xsres),
+                         (gmapdp_microexon_candidate*)(d + r_xcand), pool, (unsigned long long*)(d + o_xcnt), nullptr);
+  if (e == hipSuccess && nxf)
+    e = launch_mx_finish(nxf, s, (const gmapdp_microexon_problem*)(d + o_xf), ctx->d_genome, ctx->genome_words,
+                         (const char*)(d + o_q), (const char*)(d + o_quc), ctx->d_cs,
+                         (const gmapdp_microexon_candidate*)(d + o_xfc), (const double*)(d + o_xfp),
+                         (gmapdp_microexon_result*)(d + o_xfres), (gmapdp_pair*)(d + r_xfpairs), nullptr);
+  if (e == hipSuccess) e = hipMemcpyAsync(h + o_xfres, d + o_xfres, total - o_xfres, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = ctx_sync(ctx, s);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "mixed batch: %s", e);
+  // ---- unpack ----
+  const gmapdp_result* dres = (const gmapdp_result*)(h + r_res);
+  const gmapdp_genome_result* gres = (const gmapdp_genome_result*)(h + r_gres);
+  if (plan.pair_capacity) std::memcpy(m->pairs, h + r_pairs, sizeof(gmapdp_pair) * plan.pair_capacity);
+  for (int k = 0; k < ndev; k++) m->results[plan.dev_problem[k]] = dres[k];
+  for (int k = 0; k < ngdev; k++) m->genome_results[plan.gdev_problem[k]] = gres[k];
+  if (nxf) {
+    std::memcpy(m->finish_results, h + o_xfres, sizeof(gmapdp_microexon_result) * nxf);
+    std::memcpy(m->finish_pairs, h + r_xfpairs, sizeof(gmapdp_pair) * fpoff);
+  }
+  int rc = GMAPDP_OK;
+  if (nxs) {
+    const gmapdp_microexon_result* xr = (const gmapdp_microexon_result*)(h + r_xsres);
+    bool rerun = false;
+    size_t used = 0;
+    for (int i = 0; i < nxs; i++) {
+      rerun |= xr[i].cand_offset < 0 && xr[i].ncandidates > 0;  // -2: pool overflow, -1: past the LDS list
+      if (xr[i].cand_offset >= 0) used = std::max(used, (size_t)xr[i].cand_offset + (size_t)xr[i].ncandidates);
+    }
+    if (rerun) {
+      size_t need = 0;
+      rc = gmapdp_microexon_search(ctx, m->searches, nxs, qseq, qseq_uc, qbytes, m->search_results, m->candidates,
+                                   m->candidate_capacity, &need);
+      m->candidates_needed = need;
+    } else {
+      std::memcpy(m->search_results, xr, sizeof(gmapdp_microexon_result) * nxs);
+      m->candidates_needed = used;
+      if (used > m->candidate_capacity || (used && !m->candidates)) rc = GMAPDP_ESPACE;
+      else if (used) std::memcpy(m->candidates, h + r_xcand, sizeof(gmapdp_microexon_candidate) * used);
+    }
+  }
+  return rc;
 }
 
 // Device-resident microexon plan (bench / pipelined callers): the search is run once at plan time to

@@ -232,11 +232,13 @@ shim_context (Genome_T genome) {
   uint64_t length;
   size_t nwords;
   if (shim_ctx == NULL) {
-    /* GMAPDP_SHIM_BLOCKING=1: the dispatchers wait on blocking-sync events instead of spinning (measured
-       slower end to end: the wake-up adds to every batch, and the HIP wait still spins at first) */
+    /* How a dispatcher waits for its batch: by default it polls the batch's completion every
+       GMAPDP_POLL_US (10) microseconds and sleeps in between (GMAPDP_CTX_POLL_SYNC), which leaves the
+       cores to GMAP's workers; GMAPDP_SHIM_POLL=0 spins in HIP's wait, GMAPDP_SHIM_BLOCKING=1 sleeps on
+       a blocking-sync event (both measured slower end to end, profiles/r03_e2e). */
     const char *blk = getenv("GMAPDP_SHIM_BLOCKING"), *poll = getenv("GMAPDP_SHIM_POLL");
     const int wait = blk != NULL && blk[0] == '1' ? GMAPDP_CTX_BLOCKING_SYNC
-                     : (poll != NULL && poll[0] == '1' ? GMAPDP_CTX_POLL_SYNC : 0);
+                     : (poll != NULL && poll[0] == '0' ? 0 : GMAPDP_CTX_POLL_SYNC);
     shim_check(gmapdp_create_ex(&shim_ctx, shim_device(), shim_mode, shim_user_open, shim_user_extend,
                                 shim_user_dynprog_p, GMAPDP_CTX_ONE_STREAM | wait |
                                     (shim_qi != 1 ? GMAPDP_CTX_PRIO_HIGH : GMAPDP_CTX_PRIO_LOW)),
@@ -476,11 +478,12 @@ typedef struct {
   gmapdp_stage2_problem *s2;
   shim_req **rs, **re, **rg, **rc, **ro, **r2, **rxs, **rxf;
   size_t scap, ecap, gcap, ccap, ocap, s2cap, rscap, recap, rgcap, rccap, rocap, r2cap, rxscap, rxfcap;
-  gmapdp_microexon_problem *mx;
-  gmapdp_microexon_result *mxres;
-  gmapdp_microexon_candidate *mxc;
+  gmapdp_microexon_problem *mx, *mxf;        /* searches, finishes */
+  gmapdp_microexon_result *mxres, *mxfres;
+  gmapdp_microexon_candidate *mxc, *mxsc;     /* the finishes' candidates, the searches' candidates */
   double *mxp;
-  size_t mxcap, mxrescap, mxccap, mxpcap;
+  gmapdp_pair *mxpairs;
+  size_t mxcap, mxfcap, mxrescap, mxfrescap, mxccap, mxsccap, mxpcap, mxpaircap;
   char *q, *quc;
   size_t qcap, quccap;
   double *pr;
@@ -535,23 +538,39 @@ shim_run (shim_req *batch) {
   shim_batched += n;
   pthread_mutex_unlock(&q_lock);
 
-  /* single, end and genome gaps: one batch over one query arena */
+  /* single, end and genome gaps and the microexon searches / finishes: one round trip over one query
+     arena (gmapdp_mixed_batch) */
   t0 = shim_now();
-  if (ns + ne + ng > 0) {
+  if (ns + ne + ng + nxs + nxf > 0) {
+    gmapdp_mixed M;
+    size_t nct = 0, xcap;
+    int rc;
+    memset(&M, 0, sizeof(M));
     qb = 0;
     pb = 0;
     GROW(D.s, D.scap, ns + 1);
     GROW(D.e, D.ecap, ne + 1);
     GROW(D.g, D.gcap, ng + 1);
+    GROW(D.mx, D.mxcap, nxs + 1);
+    GROW(D.mxf, D.mxfcap, nxf + 1);
+    GROW(D.mxres, D.mxrescap, nxs + 1);
+    GROW(D.mxfres, D.mxfrescap, nxf + 1);
     for (i = 0; i < ns; i++) qb += D.rs[i]->qlen;
     for (i = 0; i < ne; i++) qb += D.re[i]->qlen;
     for (i = 0; i < ng; i++) {
       qb += D.rg[i]->qlen;
       pb += D.rg[i]->nprobs;
     }
+    for (i = 0; i < nxs; i++) qb += D.rxs[i]->qlen;
+    for (i = 0; i < nxf; i++) {
+      qb += D.rxf[i]->qlen;
+      nct += (size_t) D.rxf[i]->mxr.ncandidates;
+    }
     GROW(D.q, D.qcap, qb + 1);
     GROW(D.quc, D.quccap, qb + 1);
     GROW(D.pr, D.prcap, pb + 1);
+    GROW(D.mxc, D.mxccap, nct + 1);
+    GROW(D.mxp, D.mxpcap, 2 * nct + 2);
     qb = 0;
     pb = 0;
 #define STAGE(R, P)                                            \
@@ -578,14 +597,65 @@ shim_run (shim_req *batch) {
       if (D.rg[i]->nprobs) memcpy(D.pr + pb, D.rg[i]->probs, D.rg[i]->nprobs * sizeof(double));
       pb += D.rg[i]->nprobs;
     }
+    for (i = 0; i < nxs; i++) {
+      D.mx[i] = D.rxs[i]->p.mx;
+      STAGE(D.rxs[i], D.mx[i]);
+    }
+    nct = 0;
+    for (i = 0; i < nxf; i++) {
+      r = D.rxf[i];
+      D.mxf[i] = r->p.mx;
+      STAGE(r, D.mxf[i]);
+      D.mxfres[i] = r->mxr;
+      D.mxfres[i].cand_offset = (int64_t) nct;
+      if (r->mxr.ncandidates > 0) {
+        memcpy(D.mxc + nct, r->mxc, (size_t) r->mxr.ncandidates * sizeof(gmapdp_microexon_candidate));
+        memcpy(D.mxp + 2 * nct, r->mxp, 2 * (size_t) r->mxr.ncandidates * sizeof(double));
+      }
+      nct += (size_t) r->mxr.ncandidates;
+    }
 #undef STAGE
     cap = gmapdp_single_pair_capacity(D.s, (int) ns) + gmapdp_end_pair_capacity(D.e, (int) ne) +
           gmapdp_genome_pair_capacity(D.g, (int) ng);
     GROW(D.pairs, D.paircap, cap + 1);
     GROW(D.res, D.rescap, ns + ne + 1);
     GROW(D.gres, D.grescap, ng + 1);
-    shim_check(gmapdp_dynprog_batch(shim_ctx, D.s, (int) ns, D.e, (int) ne, D.g, (int) ng, D.q, D.quc, qb, D.pr, pb,
-                                    D.res, D.gres, D.pairs, cap), "gmapdp_dynprog_batch");
+    xcap = gmapdp_microexon_pair_capacity(D.mxf, (int) nxf);
+    GROW(D.mxpairs, D.mxpaircap, xcap + 1);
+    GROW(D.mxsc, D.mxsccap, 8 * nxs + 64);
+    M.singles = D.s;
+    M.nsingle = (int) ns;
+    M.ends = D.e;
+    M.nend = (int) ne;
+    M.genomes = D.g;
+    M.ngenome = (int) ng;
+    M.splice_probs = D.pr;
+    M.nprobs = pb;
+    M.results = D.res;
+    M.genome_results = D.gres;
+    M.pairs = D.pairs;
+    M.pair_capacity = cap;
+    M.searches = D.mx;
+    M.nsearch = (int) nxs;
+    M.search_results = D.mxres;
+    M.finishes = D.mxf;
+    M.nfinish = (int) nxf;
+    M.finish_candidates = D.mxc;
+    M.finish_probs = D.mxp;
+    M.nfinish_candidates = nct;
+    M.finish_results = D.mxfres;
+    M.finish_pairs = D.mxpairs;
+    M.finish_pair_capacity = xcap;
+    M.candidates = D.mxsc;
+    M.candidate_capacity = D.mxsccap;
+    rc = gmapdp_mixed_batch(shim_ctx, D.q, D.quc, qb, &M);
+    while (rc == GMAPDP_ESPACE) {  /* (rare) the searches found more candidates than D.mxsc holds */
+      size_t need = M.candidates_needed;
+      GROW(D.mxsc, D.mxsccap, need + 64);
+      rc = gmapdp_microexon_search(shim_ctx, D.mx, (int) nxs, D.q, D.quc, qb, D.mxres, D.mxsc, D.mxsccap, &need);
+      M.candidates_needed = need;
+    }
+    shim_check(rc, "gmapdp_mixed_batch");
     for (i = 0; i < ns; i++) {
       r = D.rs[i];
       r->r = D.res[i];
@@ -604,8 +674,21 @@ shim_run (shim_req *batch) {
       shim_copy_pairs(r, D.pairs + r->gr.pair_offset, r->gr.npairs);
       r->gr.pair_offset = 0;
     }
+    for (i = 0; i < nxs; i++) {
+      r = D.rxs[i];
+      r->mxr = D.mxres[i];
+      GROW(r->mxc, r->mxccap, (size_t) r->mxr.ncandidates + 1);
+      if (r->mxr.ncandidates > 0)
+        memcpy(r->mxc, D.mxsc + r->mxr.cand_offset, (size_t) r->mxr.ncandidates * sizeof(gmapdp_microexon_candidate));
+      r->mxr.cand_offset = 0;
+    }
+    for (i = 0; i < nxf; i++) {
+      r = D.rxf[i];
+      r->mxr = D.mxfres[i];
+      if (r->mxr.npairs > 0) shim_copy_pairs(r, D.mxpairs + r->mxr.pair_offset, r->mxr.npairs);
+      r->mxr.pair_offset = 0;
+    }
   }
-
   t1 = shim_now();
   td[0] = t1 - t0;
   /* cDNA gaps (rare): their own batch, each problem's arena span copied whole */
@@ -635,84 +718,6 @@ shim_run (shim_req *batch) {
       r->cr = D.cres[i];
       shim_copy_pairs(r, D.pairs + r->cr.pair_offset, r->cr.npairs);
       r->cr.pair_offset = 0;
-    }
-  }
-
-  /* Dynprog_microexon_int: the candidate searches, then the choices of calls whose MaxEnt is done */
-  if (nxs > 0) {
-    size_t need = 0;
-    int rc;
-    GROW(D.mx, D.mxcap, nxs + 1);
-    GROW(D.mxres, D.mxrescap, nxs + 1);
-    qb = 0;
-    for (i = 0; i < nxs; i++) qb += D.rxs[i]->qlen;
-    GROW(D.q, D.qcap, qb + 1);
-    GROW(D.quc, D.quccap, qb + 1);
-    qb = 0;
-    for (i = 0; i < nxs; i++) {
-      r = D.rxs[i];
-      D.mx[i] = r->p.mx;
-      D.mx[i].qoff = (int32_t) qb;
-      memcpy(D.q + qb, r->q, r->qlen);
-      memcpy(D.quc + qb, r->quc, r->qlen);
-      qb += r->qlen;
-    }
-    GROW(D.mxc, D.mxccap, 8 * nxs + 64);
-    for (;;) {
-      rc = gmapdp_microexon_search(shim_ctx, D.mx, (int) nxs, D.q, D.quc, qb, D.mxres, D.mxc, D.mxccap, &need);
-      if (rc != GMAPDP_ESPACE) break;
-      GROW(D.mxc, D.mxccap, need + 64);
-    }
-    shim_check(rc, "gmapdp_microexon_search");
-    for (i = 0; i < nxs; i++) {
-      r = D.rxs[i];
-      r->mxr = D.mxres[i];
-      GROW(r->mxc, r->mxccap, (size_t) r->mxr.ncandidates + 1);
-      if (r->mxr.ncandidates > 0)
-        memcpy(r->mxc, D.mxc + r->mxr.cand_offset, (size_t) r->mxr.ncandidates * sizeof(gmapdp_microexon_candidate));
-      r->mxr.cand_offset = 0;
-    }
-  }
-  if (nxf > 0) {
-    size_t nct = 0, poff = 0;
-    GROW(D.mx, D.mxcap, nxf + 1);
-    GROW(D.mxres, D.mxrescap, nxf + 1);
-    qb = 0;
-    for (i = 0; i < nxf; i++) {
-      qb += D.rxf[i]->qlen;
-      nct += (size_t) D.rxf[i]->mxr.ncandidates;
-    }
-    GROW(D.q, D.qcap, qb + 1);
-    GROW(D.quc, D.quccap, qb + 1);
-    GROW(D.mxc, D.mxccap, nct + 1);
-    GROW(D.mxp, D.mxpcap, 2 * nct + 2);
-    qb = 0;
-    nct = 0;
-    for (i = 0; i < nxf; i++) {
-      r = D.rxf[i];
-      D.mx[i] = r->p.mx;
-      D.mx[i].qoff = (int32_t) qb;
-      memcpy(D.q + qb, r->q, r->qlen);
-      memcpy(D.quc + qb, r->quc, r->qlen);
-      qb += r->qlen;
-      D.mxres[i] = r->mxr;
-      D.mxres[i].cand_offset = (int64_t) nct;
-      if (r->mxr.ncandidates > 0) {
-        memcpy(D.mxc + nct, r->mxc, (size_t) r->mxr.ncandidates * sizeof(gmapdp_microexon_candidate));
-        memcpy(D.mxp + 2 * nct, r->mxp, 2 * (size_t) r->mxr.ncandidates * sizeof(double));
-      }
-      nct += (size_t) r->mxr.ncandidates;
-    }
-    cap = gmapdp_microexon_pair_capacity(D.mx, (int) nxf);
-    GROW(D.pairs, D.paircap, cap + 1);
-    shim_check(gmapdp_microexon_finish(shim_ctx, D.mx, (int) nxf, D.q, D.quc, qb, D.mxc, D.mxp, nct, D.mxres,
-                                       D.pairs, cap), "gmapdp_microexon_finish");
-    for (i = 0; i < nxf; i++) {
-      r = D.rxf[i];
-      r->mxr = D.mxres[i];
-      if (r->mxr.npairs > 0) shim_copy_pairs(r, D.pairs + r->mxr.pair_offset, r->mxr.npairs);
-      r->mxr.pair_offset = 0;
-      (void) poff;
     }
   }
 

@@ -377,6 +377,32 @@ int gmapdp_microexon_finish (gmapdp_ctx *ctx, const gmapdp_microexon_problem *pr
                              gmapdp_microexon_result *results, gmapdp_pair *pairs, size_t pair_capacity);
 size_t gmapdp_microexon_pair_capacity (const gmapdp_microexon_problem *problems, int n);
 
+/* The GMAP drop-in's dispatcher batch in ONE round trip: gmapdp_dynprog_batch's calls,
+ * gmapdp_microexon_search's calls and gmapdp_microexon_finish's calls (of other, earlier searches)
+ * over one query arena -- one host-to-device copy, the kernels on the context's stream, one
+ * device-to-host copy, one wait.  Each section means what the separate entry point's arguments
+ * mean; a section with n = 0 is skipped.  The rare search that overflows the candidate pool is
+ * rerun as gmapdp_microexon_search would (extra round trips).  GMAPDP_ESPACE: candidate_capacity or
+ * finish_pair_capacity too small (*candidates_needed holds the size required); everything else is
+ * then still filled in. */
+typedef struct {
+  const gmapdp_single_problem *singles; int nsingle;
+  const gmapdp_end_problem *ends; int nend;
+  const gmapdp_genome_problem *genomes; int ngenome;
+  const double *splice_probs; size_t nprobs;
+  gmapdp_result *results;                    /* nsingle + nend */
+  gmapdp_genome_result *genome_results;      /* ngenome */
+  gmapdp_pair *pairs; size_t pair_capacity;
+  const gmapdp_microexon_problem *searches; int nsearch;
+  gmapdp_microexon_result *search_results;   /* nsearch */
+  gmapdp_microexon_candidate *candidates; size_t candidate_capacity; size_t candidates_needed;
+  const gmapdp_microexon_problem *finishes; int nfinish;
+  const gmapdp_microexon_candidate *finish_candidates; const double *finish_probs; size_t nfinish_candidates;
+  gmapdp_microexon_result *finish_results;   /* in: the searches' results; out: the choices */
+  gmapdp_pair *finish_pairs; size_t finish_pair_capacity;
+} gmapdp_mixed;
+int gmapdp_mixed_batch (gmapdp_ctx *ctx, const char *qseq, const char *qseq_uc, size_t qbytes, gmapdp_mixed *m);
+
 /* Device-resident microexon plan (the bench's path): descriptors uploaded once; the search is run at
  * plan time to size each call's candidate region, so gmapdp_microexon_plan_run writes candidates to
  * fixed regions (call i's at the prefix sum of the earlier calls' counts, device array
@@ -544,7 +570,7 @@ void gmapdp_destroy (gmapdp_ctx *ctx);
  * queues, GPU_MAX_HW_QUEUES, and streams beyond them share one and serialise); GMAPDP_CTX_PRIO_HIGH /
  * _LOW create the context's stream at the device's highest / lowest priority; GMAPDP_CTX_BLOCKING_SYNC
  * makes the synchronous batch calls wait without spinning; GMAPDP_CTX_POLL_SYNC makes them poll the
- * batch's completion every GMAPDP_POLL_US microseconds (default 20) and sleep in between. */
+ * batch's completion every GMAPDP_POLL_US microseconds (default 10) and sleep in between. */
 #define GMAPDP_CTX_ONE_STREAM 0x1
 #define GMAPDP_CTX_PRIO_HIGH  0x2
 #define GMAPDP_CTX_PRIO_LOW   0x4
