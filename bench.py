@@ -178,6 +178,58 @@ def rocprof_name(kind, R, dl, lds=0):
     return "gmapdp::gg_kernel<%d, %s>" % (R, "true" if dl else "false")
 
 
+def latest_e2e():
+    """The newest committed GMAP end-to-end record (tools/e2e_timing.py, profiles/*/e2e.json): the unmodified
+    gmap and the drop-in on the same reads and host cores."""
+    import glob
+    best = None
+    for path in glob.glob(os.path.join(ROOT, "profiles", "*", "e2e.json")):
+        try:
+            d = json.load(open(path))
+            runs = d["runs"]
+        except (OSError, ValueError, KeyError):
+            continue
+        cpu = [r for r in runs if "gpu" not in r["program"]]
+        gpu = [r for r in runs if "gpu" in r["program"]]
+        if not cpu or not gpu:
+            continue
+        rec = {"source": os.path.relpath(path, ROOT), "reads": d.get("reads"),
+               "cpu_gmap_reads_per_s": max(r["reads_per_s"] for r in cpu),
+               "cpu_gmap_threads": max(cpu, key=lambda r: r["reads_per_s"])["threads"],
+               "drop_in_reads_per_s": max(r["reads_per_s"] for r in gpu),
+               "drop_in_threads": max(gpu, key=lambda r: r["reads_per_s"])["threads"],
+               "outputs_identical": d.get("outputs_identical"), "mtime": os.path.getmtime(path)}
+        if best is None or rec["mtime"] > best["mtime"]:
+            best = rec
+    if best:
+        best.pop("mtime")
+    return best
+
+
+def like_for_like(out, pcie_ms, up, down):
+    """The headline next to what it leaves out: the step's own host-to-device and device-to-host copies,
+    the host MaxEnt the drop-in evaluates for the genome gaps (the bench takes the probabilities as
+    device inputs), and GMAP end to end through the drop-in."""
+    v = out["value"]
+    ms = out["ms_per_step"]
+    reads = out["config"]["reads_per_step_per_gpu"]
+    with_pcie = reads / ((ms + pcie_ms) * 1e-3) * out["n_gpus"]
+    cb = out.get("cpu_baseline") or {}
+    hm = (cb.get("host_maxent") or {}).get("reads_per_s")
+    pipe = min(with_pcie, hm) if hm else None
+    cpu = cb.get("value")
+    return {"pcie_ms_per_step": pcie_ms, "pcie_bytes_up": up, "pcie_bytes_down": down,
+            "reads_per_s_incl_pcie": with_pcie,
+            "host_maxent_reads_per_s": hm, "host_maxent_cores": cb.get("cores"),
+            "pipeline_bound_reads_per_s": pipe,
+            "ratio_vs_cpu": v / cpu if cpu else None,
+            "ratio_vs_cpu_incl_pcie_and_host_maxent": pipe / cpu if pipe and cpu else None,
+            "drop_in_end_to_end": latest_e2e(),
+            "note": "copies measured serially after the step (not overlapped); host MaxEnt on the CPU baseline's "
+                    "cores, as the drop-in evaluates it; the end-to-end record is GMAP's own program on the same "
+                    "reads and cores (tools/e2e_timing.py)"}
+
+
 def cpu_baselines():
     """tools/cpu_baseline.py as a child process (the reference's own objects, all usable host cores,
     AVX2 and nosimd builds); {build: result or None}."""
@@ -612,6 +664,31 @@ def main():
     valu = pmc["sq_SQ_INSTS_VALU_sum_avg"] if pmc else None
     prof_ms = pmc["avg_duration_ns"] / 1e6 if pmc and pmc.get("avg_duration_ns") else None
 
+    # ---- PCIe: one block's inputs up and outputs down through pinned host memory (outside the step) ----
+    b = B[0]
+    d = b["d"]
+    up = (d["q"].nbytes + d["oq"].nbytes + sum(d[k].nbytes for k in ("single", "end", "genome", "oligo", "microexon"))
+          + 8 * max(d["sprob_len"], 1) + 16 * b["ncands"])
+    # the outputs as produced: results, the DP and microexon pairs, the stage-2 results and path pairs
+    down = int(32 * b["ngpu"] + 72 * b["nggpu"] + 16 * checks["pairs"] / len(B) + 32 * args.reads
+               + 20 * checks["stage2_path_pairs"] / len(B))
+    h_up = torch.empty(up, dtype=torch.uint8, pin_memory=True)
+    h_down = torch.empty(down, dtype=torch.uint8, pin_memory=True)
+    g_up = torch.empty(up, dtype=torch.uint8, device=dev)
+    g_down = torch.empty(down, dtype=torch.uint8, device=dev)
+    pcie_ms = []
+    with torch.cuda.stream(stream):
+        for _ in range(4):
+            e0, e1 = mk()
+            e0.record(stream)
+            g_up.copy_(h_up, non_blocking=True)
+            h_down.copy_(g_down, non_blocking=True)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            pcie_ms.append(e0.elapsed_time(e1))
+    pcie_ms = float(np.median(pcie_ms[1:]))
+    del h_up, h_down, g_up, g_down
+
     ms_step = elapsed / args.steps * 1e3
     reads_total = args.reads * world * args.steps
     nsub = {k: int(np.mean([len(b["d"][k]) for b in B])) for k in ("oligo", "single", "end", "genome", "microexon")}
@@ -702,6 +779,7 @@ def main():
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:
+        out["like_for_like"] = like_for_like(out, pcie_ms, up, down)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

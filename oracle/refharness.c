@@ -398,6 +398,14 @@ refh_maxent (int model, unsigned int splicesitepos, unsigned int chroffset) {
   }
 }
 
+/* n evaluations in one call (measurement: the host MaxEnt work the GMAP drop-in does per genome gap,
+   timed without a foreign-call transition per position) */
+void
+refh_maxent_batch (const int *models, const unsigned int *positions, unsigned int chroffset, int n, double *out) {
+  int i;
+  for (i = 0; i < n; i++) out[i] = refh_maxent(models[i], positions[i], chroffset);
+}
+
 /* CPU baseline loop over include/gmapdp.h's gmapdp_genome_problem layout
    (restated). */
 typedef struct {

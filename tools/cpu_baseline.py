@@ -82,7 +82,45 @@ def worker(args):
     fams = [("single", lib.refh_single_gap_batch, ref_layout(d["single"]), W.SINGLE_PER_READ),
             ("end", lib.refh_end_gap_batch, ref_layout(d["end"]), W.END5_PER_READ + W.END3_PER_READ),
             ("genome", lib.refh_genome_gap_batch, ref_layout(d["genome"]), W.GENOME_PER_READ)]
-    t = {k: 0.0 for k in ("single", "end", "genome", "oligo", "microexon")}
+    # The host MaxEnt work the GMAP drop-in does for a genome gap (gmapdp_genome_splice_sites: every
+    # position of both sides but each side's last, the reference's own Maxent_hr_*_prob; none for the
+    # calls the engine answers before reading them) -- the GPU bench takes these as device inputs.
+    g = d["genome"]
+    fm_b = lib.refh_maxent_batch
+    fm_b.restype = None
+    fm_b.argtypes = [C.c_void_p, C.c_void_p, C.c_uint, C.c_int, C.c_void_p]
+    mx_models, mx_pos, mx_off = [], [], [0]
+    for p in g:
+        gl, gr, r = int(p["glengthL"]), int(p["glengthR"]), int(p["rlength"])
+        if r > 1 and r <= 660 and 0 < gl <= 2000 and 0 < gr <= 2000:
+            watson, sense = bool(int(p["flags"]) & 1), int(p["cdna_direction"]) > 0
+            lo, ro, co, ch = int(p["goffsetL"]), int(p["rev_goffsetR"]), int(p["chroffset"]), int(p["chrhigh"])
+            cl, cr = np.arange(gl - 1), np.arange(gr - 1)
+            if watson:
+                mx_pos += [co + lo + cl, co + ro - cr + 1]
+                mx_models += [np.full(gl - 1, 0 if sense else 3), np.full(gr - 1, 1 if sense else 2)]
+            else:
+                mx_pos += [ch - lo - cl + 1, ch - ro + cr]
+                mx_models += [np.full(gl - 1, 2 if sense else 1), np.full(gr - 1, 3 if sense else 0)]
+            mx_off.append(mx_off[-1] + gl + gr - 2)
+        else:
+            mx_off.append(mx_off[-1])
+    mx_models = np.ascontiguousarray(np.concatenate(mx_models).astype(np.int32)) if mx_models else np.zeros(1, np.int32)
+    mx_pos = np.ascontiguousarray(np.concatenate(mx_pos).astype(np.uint32)) if mx_pos else np.zeros(1, np.uint32)
+    mx_out = np.zeros(max(len(mx_pos), 1), dtype=np.float64)
+    # every call's arguments sliced before its timed region (no Python slicing inside t0..t1)
+    oligo_args = []
+    for p in d["oligo"]:
+        o, ql = int(p["qoff"]), int(p["querylength"])
+        oligo_args.append((oq[o:o + ql], ql, int(p["chrstart"]), int(p["chrend"]), int(p["chroffset"]),
+                           int(p["chrhigh"]), int(p["plusp"])))
+    micro_args = []
+    for m in d["microexon"]:
+        mo, ml = int(m["qoff"]), int(m["rlength"])
+        micro_args.append((qb[mo:mo + ml], ml, int(m["roffset"]), int(m["goffsetL"]), int(m["rev_goffsetR"]),
+                           int(m["cdna_direction"]), int(m["chroffset"]), int(m["chrhigh"]), int(m["watsonp"]),
+                           int(m["genestrand"]), int(m["dynprogindex"])))
+    t = {k: 0.0 for k in ("single", "end", "genome", "oligo", "microexon", "host_maxent")}
     n = {k: 0 for k in t}
     t_start = time.perf_counter()
     # one read's worth of calls per round, so every family is sampled in proportion
@@ -94,22 +132,23 @@ def worker(args):
             t0 = time.perf_counter()
             f(a.ctypes.data, k, qb, qb)
             t[name] += time.perf_counter() - t0
+            if name == "genome":  # the same k calls' host MaxEnt, as the drop-in evaluates it
+                a0, a1 = mx_off[i], mx_off[i + k]
+                pm, pp, po = mx_models[a0:].ctypes.data, mx_pos[a0:].ctypes.data, mx_out.ctypes.data
+                t0 = time.perf_counter()
+                fm_b(pm, pp, 0, a1 - a0, po)
+                t["host_maxent"] += time.perf_counter() - t0
+                n["host_maxent"] += k
             n[name] += k
-        p = d["oligo"][n["oligo"] % len(d["oligo"])]
-        o, ql = int(p["qoff"]), int(p["querylength"])
+        qs, ql, c0, c1, co, ch, pl = oligo_args[n["oligo"] % len(oligo_args)]
         t0 = time.perf_counter()
-        fo(oq[o:o + ql], oq[o:o + ql], ql, int(p["chrstart"]), int(p["chrend"]), int(p["chroffset"]),
-           int(p["chrhigh"]), int(p["plusp"]), 1, 500000, sc.ctypes.data, paths.ctypes.data, 1024,
-           pairs.ctypes.data, cap)
+        fo(qs, qs, ql, c0, c1, co, ch, pl, 1, 500000, sc.ctypes.data, paths.ctypes.data, 1024, pairs.ctypes.data, cap)
         t["oligo"] += time.perf_counter() - t0
         n["oligo"] += 1
         for _ in range(int(round(W.MICROEXON_PER_READ))):
-            m = d["microexon"][n["microexon"] % len(d["microexon"])]
-            mo, ml = int(m["qoff"]), int(m["rlength"])
+            ma = micro_args[n["microexon"] % len(micro_args)]
             t0 = time.perf_counter()
-            fm(qb[mo:mo + ml], qb[mo:mo + ml], ml, int(m["roffset"]), int(m["goffsetL"]), int(m["rev_goffsetR"]),
-               int(m["cdna_direction"]), int(m["chroffset"]), int(m["chrhigh"]), int(m["watsonp"]),
-               int(m["genestrand"]), int(m["dynprogindex"]), msc.ctypes.data, mds.ctypes.data, pairs.ctypes.data, cap)
+            fm(ma[0], ma[0], *ma[1:], msc.ctypes.data, mds.ctypes.data, pairs.ctypes.data, cap)
             t["microexon"] += time.perf_counter() - t0
             n["microexon"] += 1
     per_call = {k: t[k] / max(n[k], 1) for k in t}
@@ -117,7 +156,8 @@ def worker(args):
                     + W.GENOME_PER_READ * per_call["genome"] + W.STAGE2_PER_READ * per_call["oligo"]
                     + W.MICROEXON_PER_READ * per_call["microexon"])
     return {"reads_per_s": 1.0 / sec_per_read, "calls": n, "seconds": t, "per_call_us":
-            {k: v * 1e6 for k, v in per_call.items()}}
+            {k: v * 1e6 for k, v in per_call.items()},
+            "host_maxent_reads_per_s": 1.0 / max(W.GENOME_PER_READ * per_call["host_maxent"], 1e-12)}
 
 
 def main():
@@ -131,16 +171,26 @@ def main():
     if not os.path.exists(so):
         print(json.dumps(None))
         return
-    cores = a.cores or min(16, len(os.sched_getaffinity(0)))
+    # at most 16 workers: the GPU box allots one MI355X job 16 host cores (os.cpu_count() there shows
+    # the whole machine), and the GPU drop-in is measured on the same 16
+    host_cpus = len(os.sched_getaffinity(0))
+    cores = a.cores or min(16, host_cpus)
     with mp.get_context("fork").Pool(cores) as pool:
         res = pool.map(worker, [(w, a.build, a.budget, a.reads) for w in range(cores)])
+    from gmapdp.workload import GENOME_PER_READ as genome_per_read
     total = sum(r["reads_per_s"] for r in res)
+    maxent_total = sum(r["host_maxent_reads_per_s"] for r in res)
     calls = {k: sum(r["calls"][k] for r in res) for k in res[0]["calls"]}
     per_call = {k: float(np.mean([r["per_call_us"][k] for r in res])) for k in res[0]["per_call_us"]}
     print(json.dumps({
         "value": total, "unit": "reads/s", "cores": cores, "kind": "reference",
         "build": "gmap.%s objects (oracle/_ref/librefdp_%s.so)" % (a.build, a.build),
-        "cpu_model": cpu_model(), "per_core_reads_per_s": total / cores, "per_call_us": per_call,
+        "cpu_model": cpu_model(), "host_cpus_visible": host_cpus, "os_cpu_count": os.cpu_count(),
+        "per_core_reads_per_s": total / cores, "per_call_us": per_call,
+        "host_maxent": {"reads_per_s": maxent_total, "per_read_us": per_call["host_maxent"] * genome_per_read,
+                        "note": "the drop-in's host MaxEnt (every splice-site position of every genome gap the engine "
+                                "fills, reference Maxent_hr_*_prob) on the same cores: the ceiling it puts on a "
+                                "pipeline that feeds the GPU bench's calls from host probabilities"},
         "sample": "%d worker processes x %.0f s of timed reference calls (%s) on the configs[2] per-read mix "
                   "(1 Stage2_compute call + %.1f single + %.1f end + %.1f genome-gap + %.1f microexon calls per read) "
                   "cut from a chr22-length i.i.d. genome; per-read time composed from per-call averages"
