@@ -1213,6 +1213,63 @@ static __thread struct {
   Genome_T genome;
 } shim_tally;
 
+/* Oligoindex_set_inquery (oligoindex_hr.c:33454) resets an oligoindex's inquery flags and marks the
+   query's 8-mers only for queries longer than 8 nt; a shorter query's tally and lookups run against the
+   flags of the last longer query on that oligoindex (they are never cleared between queries,
+   Oligoindex_untally :33994).  The shim keeps that set per oligoindex (each GMAP worker thread owns
+   its oligoindices) so that an 8-nt lookup answers as the reference's does. */
+typedef struct {
+  const void *oligoindex;
+  uint32_t bits[2048];  /* 65536 8-mers */
+} shim_inquery;
+static __thread shim_inquery *shim_inq = NULL;
+static __thread int shim_ninq = 0;
+
+static shim_inquery *
+shim_inquery_of (const void *oligoindex, int create) {
+  int i;
+  for (i = 0; i < shim_ninq; i++)
+    if (shim_inq[i].oligoindex == oligoindex) return &shim_inq[i];
+  if (!create) return NULL;
+  shim_inq = (shim_inquery *) realloc(shim_inq, (size_t) (shim_ninq + 1) * sizeof(shim_inquery));
+  if (shim_inq == NULL) shim_refuse("host memory for oligoindex state (out of memory)");
+  memset(&shim_inq[shim_ninq], 0, sizeof(shim_inquery));
+  shim_inq[shim_ninq].oligoindex = oligoindex;
+  return &shim_inq[shim_ninq++];
+}
+
+/* the 8-mer following the encoding of set_inquery (A C G T = 0 1 2 3; other characters restart) */
+static void
+shim_set_inquery (const void *oligoindex, const char *queryuc, int querystart, int queryend) {
+  shim_inquery *e;
+  uint32_t oligo = 0;
+  int i, in_counter = 0, c;
+  if (queryend - querystart <= 8) return;  /* the flags stay as the last longer query left them */
+  e = shim_inquery_of(oligoindex, 1);
+  memset(e->bits, 0, sizeof(e->bits));
+  for (i = querystart; i < queryend; i++) {
+    in_counter++;
+    switch (queryuc[i]) {
+    case 'A': c = 0; break;
+    case 'C': c = 1; break;
+    case 'G': c = 2; break;
+    case 'T': c = 3; break;
+    default: c = -1; break;
+    }
+    if (c < 0) {
+      oligo = 0;
+      in_counter = 0;
+      continue;
+    }
+    oligo = (oligo << 2) | (uint32_t) c;
+    if (in_counter == 8) {
+      const uint32_t m = oligo & 0xFFFFu;
+      e->bits[m >> 5] |= 1u << (m & 31);
+      in_counter--;
+    }
+  }
+}
+
 void
 __wrap_Oligoindex_hr_tally (Oligoindex_T this, Univcoord_T mappingstart, Univcoord_T mappingend, bool plusp,
                             char *queryuc_ptr, int querystart, int queryend, Chrpos_T chrpos, Genome_T genome,
@@ -1229,6 +1286,7 @@ __wrap_Oligoindex_hr_tally (Oligoindex_T this, Univcoord_T mappingstart, Univcoo
   shim_tally.querystart = querystart;
   shim_tally.queryend = queryend;
   shim_tally.genome = genome;
+  shim_set_inquery(this, queryuc_ptr, querystart, queryend);
   this->table = NULL;
 }
 
@@ -1252,6 +1310,68 @@ __wrap_Oligoindex_get_mappings (List_T diagonals, bool *coveredp, Chrpos_T **map
   if (*totalpositions != 0 || *maxnconsecutive != 0) shim_refuse("a second oligoindex source (coverage loop)");
   for (q = 0; q < querylength; q++)
     if (coveredp[q]) shim_refuse("stage-2 seeding with covered query positions");
+  if (chrend <= chrstart) return diagonals;  /* :34157, before anything is written */
+  if (querylength <= 8) {
+    /* At most one 8-mer (querypos 0): lookups answer from the table that the tally built over the
+       last longer query's 8-mers (shim_set_inquery).  Below 8 nt, or an 8-mer outside that set, there
+       is no hit and nothing but oned_matrix_p is written (:34208-34305). */
+    shim_inquery *e = shim_inquery_of(this, 0);
+    uint32_t x = 0;
+    int full = querylength == 8;
+    for (q = 0; q < querylength && full; q++) {
+      switch (queryuc_ptr[q]) {
+      case 'A': x = x << 2; break;
+      case 'C': x = (x << 2) | 1u; break;
+      case 'G': x = (x << 2) | 2u; break;
+      case 'T': x = (x << 2) | 3u; break;
+      default: full = 0; break;
+      }
+    }
+    *oned_matrix_p = true;
+    if (!full) return diagonals;
+    if (e == NULL || !((e->bits[x >> 5] >> (x & 31)) & 1u)) {  /* lookup: nhits 0 */
+      npositions[0] = 0;
+      mappings[0] = NULL;
+      return diagonals;
+    }
+    /* the 8-mer is in the table: its positions in the window are the engine's answer for the query
+       "8-mer" + 'N' (one distinct 8-mer; a single query position makes no consecutive run, so no
+       diagonal and maxnconsecutive 0) */
+    {
+      static __thread char q9[9];
+      memcpy(q9, queryuc_ptr, 8);
+      q9[8] = 'N';
+      r = shim_request(K_OLIGO);
+      p = &r->p.o;
+      p->querylength = 9;
+      p->chrstart = chrstart;
+      p->chrend = chrend;
+      p->chroffset = shim_coord(chroffset);
+      p->chrhigh = shim_coord(chrhigh);
+      p->plusp = plusp ? 1 : 0;
+      p->minor = this->diag_lookback == 60 ? 1 : 0;
+      r->genome = shim_tally.genome;
+      r->q = r->quc = q9;
+      r->qlen = 9;
+      r->tabn = gmapdp_oligo_positions_capacity(p, 1);
+      dc = gmapdp_oligo_diagonal_capacity(p, 1);
+      GROW(r->np, r->npcap, r->qlen + 1);
+      GROW(r->mp, r->mpcap, r->qlen + 1);
+      GROW(r->pos, r->poscap, r->tabn + 1);
+      GROW(r->dg, r->dgcap, 4 * dc + 4);
+      shim_submit(r);
+      shim_count(ST_OLIGO);
+      this->table = NULL;
+      if (r->tabn > 0) {
+        this->table = (Chrpos_T *) MALLOC(r->tabn * sizeof(Chrpos_T));
+        memcpy(this->table, r->pos, r->tabn * sizeof(Chrpos_T));
+      }
+      npositions[0] = r->np[0];
+      mappings[0] = r->np[0] > 0 ? &this->table[r->mp[0]] : NULL;
+      *totalpositions = r->orr.totalpositions;
+      return diagonals;
+    }
+  }
   r = shim_request(K_OLIGO);
   p = &r->p.o;
   p->querylength = querylength;
@@ -1368,6 +1488,7 @@ __wrap_Stage2_compute (char *queryseq_ptr, char *queryuc_ptr, int querylength, i
      engine does not keep: refused. */
   if (querylength < 8) return NULL;
   if (querylength == 8) shim_refuse("Stage2_compute on a query of exactly 8 nt");
+  shim_set_inquery(major, queryuc_ptr, 0, querylength);  /* the tally inside Stage2_compute sets them */
   /* the chaining kernels keep Chrpos_T differences in 32-bit registers: checked here, on the calling
      thread, so that a refusal names its own call and never fails another thread's batch */
   if (chrend >= 0x80000000U || chrstart >= 0x80000000U)

@@ -13,6 +13,8 @@
  *   C rlengthL rlengthR glength                      Dynprog_cdna_gap      (dynprog_cdna.c:787)
  *   M rlength intronlength                           Dynprog_microexon_int (dynprog_single.c:900)
  *   T querylength chrend-chrstart                    Stage2_compute        (stage2.c:6325)
+ *   O querylength chrend-chrstart                    Oligoindex_get_mappings (oligoindex_hr.c:34127; stage 3's
+ *                                                    own oligoindex calls, outside Stage2_compute)
  */
 #ifdef HAVE_CONFIG_H
 #include "config.h"
@@ -162,4 +164,19 @@ __wrap_Stage2_compute (char *queryseq_ptr, char *queryuc_ptr, int querylength, i
                                chrhigh, plusp, genestrand, stage2_alloc, proceed_pctcoverage, oligoindices, genome,
                                genomealt, pairpool, diagpool, cellpool, localp, skip_repetitive_p, favor_right_p,
                                max_nalignments, stopwatch, diag_debug);
+}
+
+extern List_T __real_Oligoindex_get_mappings(List_T, bool *, Chrpos_T **, int *, int *, bool *, int *,
+                                             Oligoindex_array_T, Oligoindex_T, char *, int, int, int, Chrpos_T,
+                                             Chrpos_T, Univcoord_T, Univcoord_T, bool, Diagpool_T);
+List_T
+__wrap_Oligoindex_get_mappings (List_T diagonals, bool *coveredp, Chrpos_T **mappings, int *npositions,
+                                int *totalpositions, bool *oned_matrix_p, int *maxnconsecutive,
+                                Oligoindex_array_T array, Oligoindex_T this, char *queryuc_ptr, int querystart,
+                                int queryend, int querylength, Chrpos_T chrstart, Chrpos_T chrend,
+                                Univcoord_T chroffset, Univcoord_T chrhigh, bool plusp, Diagpool_T diagpool) {
+  cm_log("O %d %d%.0d%.0d%.0d\n", querylength, (int) (chrend - chrstart), 0, 0, 0);
+  return __real_Oligoindex_get_mappings(diagonals, coveredp, mappings, npositions, totalpositions, oned_matrix_p,
+                                        maxnconsecutive, array, this, queryuc_ptr, querystart, queryend, querylength,
+                                        chrstart, chrend, chroffset, chrhigh, plusp, diagpool);
 }

@@ -169,7 +169,7 @@ programs: $(foreach v,$(PROG_VARIANTS),$(OUT)/gmap_$(v)) $(OUT)/gmap_callmix \
 # The unmodified nosimd gmap with the hot-path entry points counted (callmix.c: one log line per call,
 # then the reference's own function): the measured per-read call mix of a read shape (tools/callmix.py)
 CALLMIX := Dynprog_single_gap Dynprog_end5_gap Dynprog_end3_gap Dynprog_genome_gap Dynprog_cdna_gap \
-           Dynprog_microexon_int Stage2_compute
+           Dynprog_microexon_int Stage2_compute Oligoindex_get_mappings
 $(OUT)/callmix/callmix.o: callmix.c ../include/gmapdp_dynprog.h
 	@mkdir -p $(dir $@)
 	$(CC) $(BASEFLAGS) -DHAVE_CONFIG_H -I../include -c $< -o $@

@@ -19,6 +19,10 @@ Outputs (data only):
   e2e_avx2.sam           the same with the AVX2 build (SIMD-build DP semantics)
   cdna2_genetest2_*.txt  `gmap -g genetest2.fa cdna2.fa` (BASELINE configs[0] inputs; the bundled
                          cdna.fa is empty) in default output format, both builds
+  e2e_short_genome.fa, e2e_short_reads.fa, e2e_short_{nosimd,avx2}.sam
+                         reads whose stage 3 makes Oligoindex_get_mappings calls on 8-nt queries
+                         (SHORT_OLIGO_READS, found with oracle/_ref/gmap_callmix), and the reference
+                         program's outputs on them
 """
 import math
 import os
@@ -84,11 +88,22 @@ def write_fasta(path, records, width=60):
                 f.write(seq[k:k + width] + "\n")
 
 
+# reads of the 30 000-read stream (tools/e2e_inputs.py /dir 30000: the segment with all 30 000 reads'
+# junctions planted) whose stage 3 queries an oligoindex with 8 nt -- the reference answers from the
+# previous longer query's 8-mer flags (Oligoindex_set_inquery :33478); read 15135 makes two such calls
+SHORT_OLIGO_READS = (15135,)
+SHORT_STREAM = 30000
+
+
 def make_inputs():
     g = list(synth_genome())
     reads = [synth_read(g, i) for i in range(NREADS)]
     write_fasta(os.path.join(HERE, "e2e_genome.fa"), [("synseg", "".join(g))])
     write_fasta(os.path.join(HERE, "e2e_reads.fa"), reads)
+    g2 = list(synth_genome())
+    short = [r for i, r in ((i, synth_read(g2, i)) for i in range(SHORT_STREAM)) if i in SHORT_OLIGO_READS]
+    write_fasta(os.path.join(HERE, "e2e_short_genome.fa"), [("synseg", "".join(g2))])
+    write_fasta(os.path.join(HERE, "e2e_short_reads.fa"), short)
 
 
 def run_gmap(binary, args, out):
@@ -103,6 +118,8 @@ def main():
         run_gmap(exe, ["-g", "e2e_genome.fa", "-f", "samse", "--no-sam-headers", "e2e_reads.fa"],
                  os.path.join(HERE, "e2e_%s.sam" % v))
         run_gmap(exe, ["-g", "genetest2.fa", "cdna2.fa"], os.path.join(HERE, "cdna2_genetest2_%s.txt" % v))
+        run_gmap(exe, ["-g", "e2e_short_genome.fa", "-f", "samse", "--no-sam-headers", "e2e_short_reads.fa"],
+                 os.path.join(HERE, "e2e_short_%s.sam" % v))
     print("wrote e2e fixtures in", HERE)
 
 

@@ -13,6 +13,7 @@ Fixtures (tests/golden/, data only):
   align.test.ok       the reference's own golden (tests/align.test.in:9: gmap -A -g ss.chr17test ss.her2)
   cdna2_genetest2_*   `gmap -g genetest2.fa cdna2.fa` (BASELINE configs[0] inputs), both builds
   e2e_{nosimd,avx2}.sam  200 synthetic 2-kb spliced reads vs a 300-kb segment (make_e2e.py), both builds
+  e2e_short_*            a read of the same stream whose stage 3 makes 8-nt oligoindex queries
 """
 import os
 import re
@@ -116,6 +117,25 @@ def test_gpu_gmap_synthetic_reads(build):
     for k in ("Dynprog_single_gap", "Dynprog_genome_gap", "Dynprog_end5_gap", "Dynprog_end3_gap",
               "Stage2_compute", "Dynprog_microexon_int"):
         assert st[k] > 0, st
+
+
+SHORT_ARGS = ["-g", "e2e_short_genome.fa", "-f", "samse", "--no-sam-headers", "e2e_short_reads.fa"]
+
+
+@pytest.mark.parametrize("build", BUILDS)
+def test_reference_gmap_reproduces_short_oligo_fixture(build):
+    assert _run(_exe("gmap_" + build), SHORT_ARGS)[0] == _read("e2e_short_%s.sam" % build)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("build", BUILDS)
+def test_gpu_gmap_short_oligoindex_queries(build):
+    """A read whose stage 3 queries an oligoindex with 8 nt (make_e2e.SHORT_OLIGO_READS): the reference
+    answers from the previous longer query's 8-mer flags (Oligoindex_set_inquery returns early), which
+    the shim tracks per oligoindex; the output equals the reference program's."""
+    out, err = _run(_exe("gmap_gpu_" + build), SHORT_ARGS, env={"GMAPDP_SHIM_STATS": "1"})
+    assert out == _read("e2e_short_%s.sam" % build)
+    assert _stats(err)["Oligoindex_get_mappings"] > 0
 
 
 @pytest.mark.gpu
