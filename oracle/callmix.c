@@ -22,6 +22,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <pthread.h>
+#include <time.h>
+#include <sys/resource.h>
 
 #include "gmapdp_dynprog.h"
 
@@ -62,9 +64,51 @@ cm_log (const char *fmt, int a, int b, int c, int d, int e) {
   pthread_mutex_unlock(&cm_lock);
 }
 
+/* GMAPDP_CALLMIX_TIME=1: thread CPU time inside the hot-path entry points (outermost call only: time
+   Stage2_compute spends in its own Oligoindex_get_mappings counts as Stage2_compute), printed at exit
+   next to the process's total CPU time -- the share of GMAP's CPU time the drop-in can take over */
+static double cm_secs[8];
+static __thread int cm_depth = 0;
+static double
+cm_now (void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return (double) ts.tv_sec + 1e-9 * (double) ts.tv_nsec;
+}
+static double
+cm_begin (void) {
+  return cm_depth++ == 0 ? cm_now() : 0.0;
+}
+static void
+cm_end (int k, double t0) {
+  if (--cm_depth == 0) {
+    const double dt = cm_now() - t0;
+    pthread_mutex_lock(&cm_lock);
+    cm_secs[k] += dt;
+    pthread_mutex_unlock(&cm_lock);
+  }
+}
+
 __attribute__((destructor)) static void
 cm_close (void) {
+  static const char *const names[8] = {"single", "end5", "end3", "genome", "cdna", "microexon", "stage2",
+                                       "oligoindex"};
+  const char *t = getenv("GMAPDP_CALLMIX_TIME");
   if (cm_out) fclose(cm_out);
+  if (t != NULL && t[0] == '1') {
+    struct rusage ru;
+    double tot = 0.0;
+    int k;
+    getrusage(RUSAGE_SELF, &ru);
+    fprintf(stderr, "callmix cpu_s:");
+    for (k = 0; k < 8; k++) {
+      fprintf(stderr, " %s=%.3f", names[k], cm_secs[k]);
+      tot += cm_secs[k];
+    }
+    fprintf(stderr, " hot_path=%.3f process=%.3f\n", tot,
+            (double) ru.ru_utime.tv_sec + 1e-6 * ru.ru_utime.tv_usec + (double) ru.ru_stime.tv_sec +
+                1e-6 * ru.ru_stime.tv_usec);
+  }
 }
 
 List_T
@@ -74,10 +118,15 @@ __wrap_Dynprog_single_gap (int *dynprogindex, int *finalscore, int *nmatches, in
                            bool watsonp, int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
                            Pairpool_T pairpool, int extraband_single, bool widebandp, double defect_rate) {
   cm_log("S %d %d %d %d%.0d\n", length1, length2, extraband_single, widebandp ? 1 : 0, 0);
-  return __real_Dynprog_single_gap(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels, dynprog,
+  {
+    const double t0_ = cm_begin();
+    List_T r_ = __real_Dynprog_single_gap(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels, dynprog,
                                    sequence1, sequenceuc1, length1, length2, offset1, offset2, chroffset, chrhigh,
                                    watsonp, genestrand, jump_late_p, genome, genomealt, pairpool, extraband_single,
                                    widebandp, defect_rate);
+    cm_end(0, t0_);
+    return r_;
+  }
 }
 
 List_T
@@ -88,10 +137,15 @@ __wrap_Dynprog_end5_gap (int *dynprogindex, int *finalscore, int *nmatches, int 
                          Pairpool_T pairpool, int extraband_end, double defect_rate, Endalign_T endalign,
                          bool require_pos_score_p) {
   cm_log("E5 %d %d %d %d%.0d\n", length1, length2, extraband_end, (int) endalign, 0);
-  return __real_Dynprog_end5_gap(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels, dynprog,
+  {
+    const double t0_ = cm_begin();
+    List_T r_ = __real_Dynprog_end5_gap(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels, dynprog,
                                  revsequence1, revsequenceuc1, length1, length2, revoffset1, revoffset2, chroffset,
                                  chrhigh, watsonp, genestrand, jump_late_p, genome, genomealt, pairpool, extraband_end,
                                  defect_rate, endalign, require_pos_score_p);
+    cm_end(1, t0_);
+    return r_;
+  }
 }
 
 List_T
@@ -102,10 +156,15 @@ __wrap_Dynprog_end3_gap (int *dynprogindex, int *finalscore, int *nmatches, int 
                          Pairpool_T pairpool, int extraband_end, double defect_rate, Endalign_T endalign,
                          bool require_pos_score_p) {
   cm_log("E3 %d %d %d %d%.0d\n", length1, length2, extraband_end, (int) endalign, 0);
-  return __real_Dynprog_end3_gap(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels, dynprog,
+  {
+    const double t0_ = cm_begin();
+    List_T r_ = __real_Dynprog_end3_gap(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels, dynprog,
                                  sequence1, sequenceuc1, length1, length2, offset1, offset2, chroffset, chrhigh,
                                  watsonp, genestrand, jump_late_p, genome, genomealt, pairpool, extraband_end,
                                  defect_rate, endalign, require_pos_score_p);
+    cm_end(2, t0_);
+    return r_;
+  }
 }
 
 List_T
@@ -118,12 +177,17 @@ __wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_r
                            Genome_T genome, Genome_T genomealt, Pairpool_T pairpool, int extraband_paired,
                            double defect_rate, int maxpeelback, bool halfp, bool finalp) {
   cm_log("G %d %d %d %d %d\n", rlength, glengthL, glengthR, extraband_paired, finalp ? 1 : 0);
-  return __real_Dynprog_genome_gap(dynprogindex, new_leftgenomepos, new_rightgenomepos, left_prob, right_prob,
+  {
+    const double t0_ = cm_begin();
+    List_T r_ = __real_Dynprog_genome_gap(dynprogindex, new_leftgenomepos, new_rightgenomepos, left_prob, right_prob,
                                    traceback_score, nmatches, nmismatches, nopens, nindels, exonhead, introntype,
                                    dynprogL, dynprogR, rsequence, rsequenceuc, rlength, glengthL, glengthR, roffset,
                                    goffsetL, rev_goffsetR, chrnum, chroffset, chrhigh, cdna_direction, watsonp,
                                    genestrand, jump_late_p, genome, genomealt, pairpool, extraband_paired,
                                    defect_rate, maxpeelback, halfp, finalp);
+    cm_end(3, t0_);
+    return r_;
+  }
 }
 
 List_T
@@ -134,10 +198,15 @@ __wrap_Dynprog_cdna_gap (int *dynprogindex, int *traceback_score, bool *incomple
                          int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
                          Pairpool_T pairpool, int extraband_paired, double defect_rate) {
   cm_log("C %d %d %d%.0d%.0d\n", rlengthL, rlengthR, glength, 0, 0);
-  return __real_Dynprog_cdna_gap(dynprogindex, traceback_score, incompletep, dynprogL, dynprogR, rsequenceL,
+  {
+    const double t0_ = cm_begin();
+    List_T r_ = __real_Dynprog_cdna_gap(dynprogindex, traceback_score, incompletep, dynprogL, dynprogR, rsequenceL,
                                  rsequence_ucL, rev_rsequenceR, rev_rsequence_ucR, rlengthL, rlengthR, glength,
                                  roffsetL, rev_roffsetR, goffset, chroffset, chrhigh, watsonp, genestrand,
                                  jump_late_p, genome, genomealt, pairpool, extraband_paired, defect_rate);
+    cm_end(4, t0_);
+    return r_;
+  }
 }
 
 List_T
@@ -147,9 +216,14 @@ __wrap_Dynprog_microexon_int (double *bestprob2, double *bestprob3, int *dynprog
                               Univcoord_T chroffset, Univcoord_T chrhigh, bool watsonp, int genestrand,
                               Genome_T genome, Genome_T genomealt, Pairpool_T pairpool) {
   cm_log("M %d %d%.0d%.0d%.0d\n", rlength, rev_goffsetR - goffsetL + 1, 0, 0, 0);
-  return __real_Dynprog_microexon_int(bestprob2, bestprob3, dynprogindex, microintrontype, rsequence, rsequenceuc,
+  {
+    const double t0_ = cm_begin();
+    List_T r_ = __real_Dynprog_microexon_int(bestprob2, bestprob3, dynprogindex, microintrontype, rsequence, rsequenceuc,
                                       rlength, roffset, goffsetL, rev_goffsetR, cdna_direction, queryseq, queryuc,
                                       chroffset, chrhigh, watsonp, genestrand, genome, genomealt, pairpool);
+    cm_end(5, t0_);
+    return r_;
+  }
 }
 
 List_T
@@ -160,10 +234,15 @@ __wrap_Stage2_compute (char *queryseq_ptr, char *queryuc_ptr, int querylength, i
                        Cellpool_T cellpool, bool localp, bool skip_repetitive_p, bool favor_right_p,
                        int max_nalignments, Stopwatch_T stopwatch, bool diag_debug) {
   cm_log("T %d %d%.0d%.0d%.0d\n", querylength, (int) (chrend - chrstart), 0, 0, 0);
-  return __real_Stage2_compute(queryseq_ptr, queryuc_ptr, querylength, query_offset, chrstart, chrend, chroffset,
+  {
+    const double t0_ = cm_begin();
+    List_T r_ = __real_Stage2_compute(queryseq_ptr, queryuc_ptr, querylength, query_offset, chrstart, chrend, chroffset,
                                chrhigh, plusp, genestrand, stage2_alloc, proceed_pctcoverage, oligoindices, genome,
                                genomealt, pairpool, diagpool, cellpool, localp, skip_repetitive_p, favor_right_p,
                                max_nalignments, stopwatch, diag_debug);
+    cm_end(6, t0_);
+    return r_;
+  }
 }
 
 extern List_T __real_Oligoindex_get_mappings(List_T, bool *, Chrpos_T **, int *, int *, bool *, int *,
@@ -176,7 +255,12 @@ __wrap_Oligoindex_get_mappings (List_T diagonals, bool *coveredp, Chrpos_T **map
                                 int queryend, int querylength, Chrpos_T chrstart, Chrpos_T chrend,
                                 Univcoord_T chroffset, Univcoord_T chrhigh, bool plusp, Diagpool_T diagpool) {
   cm_log("O %d %d%.0d%.0d%.0d\n", querylength, (int) (chrend - chrstart), 0, 0, 0);
-  return __real_Oligoindex_get_mappings(diagonals, coveredp, mappings, npositions, totalpositions, oned_matrix_p,
+  {
+    const double t0_ = cm_begin();
+    List_T r_ = __real_Oligoindex_get_mappings(diagonals, coveredp, mappings, npositions, totalpositions, oned_matrix_p,
                                         maxnconsecutive, array, this, queryuc_ptr, querystart, queryend, querylength,
                                         chrstart, chrend, chroffset, chrhigh, plusp, diagpool);
+    cm_end(7, t0_);
+    return r_;
+  }
 }
