@@ -160,9 +160,6 @@ def pmc_entry(key):
 
 def rocprof_name(kind, R, dl, lds=0):
     """The rocprofv3 kernel name(s) of a DP launch class ('+'-joined when a class is several kernels)."""
-    if kind == 6:  # packed genome gaps: prep + fill<S, R> + tail<S, R> (ggp_kernel.hip), lds = S
-        return ("gmapdp::ggp_prep_kernel+gmapdp::ggp_fill_kernel<%d, %d>+gmapdp::ggp_tail_kernel<%d, %d>"
-                % (lds, R, lds, R))
     if kind == 0:
         return "gmapdp::dp_kernel<%d, %s>" % (R, "true" if dl else "false")
     if kind == 7:  # lanes over query rows (bands wider than the query)

@@ -44,12 +44,6 @@ hipError_t launch_dpx(int S, int nproblems, int slot, int dirs_bytes, unsigned c
                       gmapdp_result* results, gmapdp_pair* pairs);
 size_t lds_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds);
 size_t scratch_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds);
-size_t scratch_bytes_ggp(int rlength, int glengthL, int glengthR);
-size_t chunk_bytes_ggp(int gmax, int S, int R);
-hipError_t launch_ggp(int S, int R, int count, hipStream_t stream, const DevGenomeProblem* probs, const int* order,
-                      const uint32_t* blocks, uint64_t nwords, const char* qseq, const char* qseq_uc,
-                      const double* sprob, const int8_t* sctab, const uint8_t* constab, const int8_t* isctab,
-                      gmapdp_genome_result* results, gmapdp_pair* pairs, unsigned char* gscratch);
 hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevGenomeProblem* probs,
                      const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
                      const char* qseq_uc, const double* sprob, const int8_t* sctab, const uint8_t* constab,
@@ -306,9 +300,8 @@ struct PlanCore {
   std::vector<int> gdev_problem;     // gdev slot -> genome problem index
   // kDpx: 64/S narrow problems per wave, R = S; kSx: SIMD-build single gaps, 64/B problems per wave,
   // R = B; kUxe / kUxg: SIMD-build end / genome gaps (triangle fills), one wave per problem, R = B
-  // kGgp: Dynprog_genome_gap packed 64/S problems per wave (ggp_kernel.hip), R = cells per lane,
-  // lds = S; kDpRows: dp_kernel's recurrence with lanes over query rows (dpr_kernel), R = row words
-  enum Kind { kDp = 0, kGenomeGap = 1, kDpx = 2, kSx = 3, kUxe = 4, kUxg = 5, kGgp = 6, kDpRows = 7 };
+  // kDpRows: dp_kernel's recurrence with lanes over query rows (dpr_kernel), R = row words
+  enum Kind { kDp = 0, kGenomeGap = 1, kDpx = 2, kSx = 3, kUxe = 4, kUxg = 5, kDpRows = 7 };
   struct Launch {
     int kind;
     int R;           // band words per lane (kDp, kGenomeGap) or segment width S (kDpx)
@@ -631,17 +624,6 @@ static size_t env_size(const char* name, size_t dflt) {
 // genome-gap direction planes stay in LDS while the workgroup's LDS stays within this; by default
 // they always go to the L2-resident scratch, which measured fastest (more problems per CU).
 // GMAPDP_GG_LDS_DIRS_MAX overrides it, for experiments.
-// GMAPDP_GGP=1 routes nosimd genome gaps with bands <= 64 to the packed ggp kernels (ggp_kernel.hip)
-// instead of gg_kernel.  Opt-in: bit-exact (tests/test_gpu_ggp.py) but not yet faster on the bench
-// (16.9 vs 14.3 ms, the group fill is latency-bound at 2 waves/SIMD).
-static bool ggp_enabled() {
-  static const bool v = env_size("GMAPDP_GGP", 0) != 0;
-  return v;
-}
-static bool ggp_s8() {
-  static const bool v = env_size("GMAPDP_GGP_S", 16) == 8;
-  return v;
-}
 static size_t gg_lds_dirs_max() {
   static const size_t v = env_size("GMAPDP_GG_LDS_DIRS_MAX", 0);
   return v;
@@ -992,20 +974,6 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     }
     if (d.open > 0) return bad(ctx, "positive gap-open penalty is not supported by the scan formulation");
     const int WL = d.lbandL + d.ubandL + 1, WR = d.lbandL + d.ubandR + 1;
-    if (ggp_enabled() && std::max(WL, WR) <= 64) {
-      // S-lane groups, R band offsets per lane (W <= S*R): GMAPDP_GGP_S = 16 (default; W <= 48: 16 x 3)
-      // or 8 (W <= 40: 8 x 5, <= 48: 8 x 6); W <= 64: 16 x 4
-      const int Wm = std::max(WL, WR);
-      int S = 16, RR = Wm <= 48 ? 3 : 4;
-      if (ggp_s8() && Wm <= 48) {
-        S = 8;
-        RR = Wm <= 40 ? 5 : 6;
-      }
-      d.dirs_offset = (int64_t)gdirs_off;
-      gdirs_off += (scratch_bytes_ggp(d.rlength, d.glengthL, d.glengthR) + 255) & ~(size_t)255;
-      gadd((int)PlanCore::kGgp, RR, 0, (size_t)S, s);
-      continue;
-    }
     const int R = pick_R(std::max(WL, WR));
     if (R > kMaxR) return bad(ctx, "band wider than 4096");
     size_t lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, true);
@@ -1026,12 +994,12 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     // longest problems first, so the tail of the launch is short work
     std::vector<int> ids = kv.second;
     if (latency) {  // the class's LDS: its largest member's
-      const bool g = L.kind == PlanCore::kGenomeGap || L.kind == PlanCore::kUxg || L.kind == PlanCore::kGgp;
+      const bool g = L.kind == PlanCore::kGenomeGap || L.kind == PlanCore::kUxg;
       size_t m = 0;
       for (int id : ids) m = std::max(m, g ? gneed[id] : need[id]);
       L.lds = m;
     }
-    if (L.kind != PlanCore::kGenomeGap && L.kind != PlanCore::kUxg && L.kind != PlanCore::kGgp) {
+    if (L.kind != PlanCore::kGenomeGap && L.kind != PlanCore::kUxg) {
       std::stable_sort(ids.begin(), ids.end(), [&](int a, int b) {
         return (size_t)plan.dev[a].glength * (plan.dev[a].lband + plan.dev[a].uband + 1) >
                (size_t)plan.dev[b].glength * (plan.dev[b].lband + plan.dev[b].uband + 1);
@@ -1046,15 +1014,6 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
       std::stable_sort(ids.begin(), ids.end(), [&](int a, int b) { return work(a) > work(b); });
       L.first = (int)plan.gorder.size();
       plan.gorder.insert(plan.gorder.end(), ids.begin(), ids.end());
-      if (L.kind == PlanCore::kGgp) {  // each fill chunk's direction-ballot region (every member carries it)
-        for (size_t f = 0; f < ids.size(); f += kGgpChunk) {
-          const size_t e = std::min(ids.size(), f + (size_t)kGgpChunk);
-          int gmax = 0;
-          for (size_t k = f; k < e; k++) gmax = std::max(gmax, std::max(plan.gdev[ids[k]].glengthL, plan.gdev[ids[k]].glengthR));
-          for (size_t k = f; k < e; k++) plan.gdev[ids[k]].aux_offset = (int64_t)gdirs_off;
-          gdirs_off += (chunk_bytes_ggp(gmax, (int)L.lds, L.R) + 255) & ~(size_t)255;
-        }
-      }
     }
     // work estimate: fill wave-columns (a packed wave fills 64/S problems at once)
     L.work = 0.0;
@@ -1089,9 +1048,6 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
       if (L.kind == PlanCore::kGenomeGap) {
         const DevGenomeProblem& d = plan.gdev[id];
         L.work += (double)std::max(d.glengthL, d.glengthR) * L.R + d.rlength;
-      } else if (L.kind == PlanCore::kGgp) {  // 64/S problems per wave fill side by side
-        const DevGenomeProblem& d = plan.gdev[id];
-        L.work += (double)(d.glengthL + d.glengthR) * L.R * (double)L.lds / 64.0 + 0.5 * d.rlength;
       } else if (L.kind == PlanCore::kUxg) {
         const DevGenomeProblem& d = plan.gdev[id];
         L.work += (double)(d.glengthL + d.glengthR + 2 * d.rlength) + 4.0 * d.rlength;
@@ -1226,10 +1182,6 @@ static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, cons
                      ctx->genome_words, a.d_q, a.d_quc, ctx->d_sc, ctx->d_cs, a.d_results, a.d_pairs,
                      (uint64_t*)ctx->gdirs.p);
   if (!a.d_gresults || !a.d_sprob) return hipErrorInvalidValue;
-  if (L.kind == PlanCore::kGgp)
-    return launch_ggp((int)L.lds, L.R, L.count, stream, a.d_gprobs, a.d_gorder + L.first, ctx->d_genome,
-                      ctx->genome_words, a.d_q, a.d_quc, a.d_sprob, ctx->d_sc, ctx->d_cs, ctx->d_isc, a.d_gresults,
-                      a.d_pairs, (unsigned char*)ctx->gdirs.p);
   return launch_gg(L.R, L.dirs_lds, L.count, L.lds, stream, a.d_gprobs, a.d_gorder + L.first, ctx->d_genome,
                    ctx->genome_words, a.d_q, a.d_quc, a.d_sprob, ctx->d_sc, ctx->d_cs, ctx->d_isc, a.d_gresults,
                    a.d_pairs, (unsigned char*)ctx->gdirs.p);
@@ -1792,7 +1744,7 @@ int gmapdp_plan_launch_members(const gmapdp_plan* plan, int li, int* problem_ind
   if (!plan || li < 0 || li >= (int)plan->in.launches.size() || !problem_indices) return GMAPDP_EINVAL;
   const auto& L = plan->in.launches[li];
   for (int k = 0; k < L.count; k++) {
-    const bool genome = L.kind == PlanCore::kGenomeGap || L.kind == PlanCore::kUxg || L.kind == PlanCore::kGgp;
+    const bool genome = L.kind == PlanCore::kGenomeGap || L.kind == PlanCore::kUxg;
     if (!genome) problem_indices[k] = plan->in.dev_problem[plan->in.order[L.first + k]];
     else problem_indices[k] = plan->nsingle + plan->nend + plan->in.gdev_problem[plan->in.gorder[L.first + k]];
   }

@@ -95,11 +95,8 @@ struct DevGenomeProblem {
   int32_t pad_;
   int64_t prob_offset;    // left probabilities at [prob_offset, +glengthL), right ones follow
   int64_t dirs_offset;    // byte offset into the global scratch (global-dirs classes)
-  int64_t aux_offset;     // packed genome gaps (ggp): the problem's chunk's direction-ballot region
+  int64_t reserved_;      // keeps the descriptor at 128 B
 };
-// Packed genome gaps (ggp_kernel.hip): one fill workgroup takes kGgpChunk consecutive members of its
-// launch class and fills the ones genome_gap_simple left, 64/S at a time.
-constexpr int kGgpChunk = 32;
 
 // DevCdnaProblem.flags (kFWatson / kFLate as above)
 constexpr int32_t kCSegLeft = 0x100;    // gsequence via Genome_get_segment_left (minus strand)

@@ -99,7 +99,7 @@ def test_gpu_genome_gap_domain_check(engine):
 
 
 def test_gpu_genome_gap_every_packed_band_class(engine):
-    """Band widths across every packed class (ggp_kernel.hip: W <= 40, <= 48, <= 64) and past it
+    """Band widths from narrow (W <= 40, <= 48, <= 64) to wide
     (gg_kernel), with glength - rlength from 1 to 12: engine vs oracle."""
     rng = random.Random(4711)
     g = bytearray(random_genome(rng, 150000))

@@ -14,7 +14,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gmap-2024_amd"))
 VARIANTS = {"gg_kernel": {}, "gg_kernel_lds_dirs": {"GMAPDP_GG_LDS_DIRS_MAX": str(48 * 1024)},
-            "ggp_packed": {"GMAPDP_GGP": "1"}}
+            # an earlier build of the library kept under gmap-2024_amd/lib_base (A/B of a kernel change)
+            "lib_base": {"GMAPDP_LIB": os.path.join(ROOT, "gmap-2024_amd", "lib_base", "libgmapdp.so")}}
 
 
 def child(reads, reps):
