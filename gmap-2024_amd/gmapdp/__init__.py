@@ -147,6 +147,19 @@ MICROEXON_PROBLEM_DTYPE = _struct_dtype(MicroexonProblem)
 MICROEXON_CANDIDATE_DTYPE = _struct_dtype(MicroexonCandidate)
 END_PROBLEM_DTYPE = _struct_dtype(EndProblem)
 
+
+class Mixed(C.Structure):
+    """gmapdp_mixed (include/gmapdp.h): the drop-in's one-round-trip dispatcher batch."""
+    _fields_ = [("singles", C.c_void_p), ("nsingle", C.c_int), ("ends", C.c_void_p), ("nend", C.c_int),
+                ("genomes", C.c_void_p), ("ngenome", C.c_int), ("splice_probs", C.c_void_p), ("nprobs", C.c_size_t),
+                ("results", C.c_void_p), ("genome_results", C.c_void_p), ("pairs", C.c_void_p),
+                ("pair_capacity", C.c_size_t), ("searches", C.c_void_p), ("nsearch", C.c_int),
+                ("search_results", C.c_void_p), ("candidates", C.c_void_p), ("candidate_capacity", C.c_size_t),
+                ("candidates_needed", C.c_size_t), ("finishes", C.c_void_p), ("nfinish", C.c_int),
+                ("finish_candidates", C.c_void_p), ("finish_probs", C.c_void_p), ("nfinish_candidates", C.c_size_t),
+                ("finish_results", C.c_void_p), ("finish_pairs", C.c_void_p), ("finish_pair_capacity", C.c_size_t)]
+
+
 _lib = None
 
 
@@ -245,6 +258,7 @@ def load_library(path=LIB_PATH):
                                               C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
                                               C.c_size_t]),
         "gmapdp_microexon_pair_capacity": (C.c_size_t, [C.c_void_p, C.c_int]),
+        "gmapdp_mixed_batch": (C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p, C.c_size_t, P(Mixed)]),
         "gmapdp_microexon_plan_create": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                                    C.c_size_t, P(C.c_void_p)]),
         "gmapdp_microexon_plan_candidates": (C.c_size_t, [C.c_void_p]),
@@ -632,6 +646,45 @@ class Engine:
                 lists.append(lst)
             out.append((int(r["nresults"]), lists))
         return out
+
+    # -- the drop-in's dispatcher batch (gmapdp_mixed_batch) ---------------------------------------
+    def mixed_batch_raw(self, qbuf, qucbuf, singles=None, ends=None, genomes=None, splice_probs=None,
+                        searches=None, finishes=None, finish_cands=None, finish_probs=None, finish_results=None,
+                        candidate_capacity=None):
+        """One gmapdp_mixed_batch call over one query arena (every section's qoff indexes qbuf).  Returns
+        (return code, outputs: results, genome_results, pairs, search_results, candidates,
+        candidates_needed, finish_results, finish_pairs) -- the caller checks the code (GMAPDP_ESPACE
+        still fills the other sections)."""
+        def arr(a, dt):
+            return np.zeros(0, dtype=dt) if a is None else np.ascontiguousarray(a, dtype=dt)
+        S, E = arr(singles, PROBLEM_DTYPE), arr(ends, END_PROBLEM_DTYPE)
+        G = arr(genomes, GENOME_PROBLEM_DTYPE)
+        XS, XF = arr(searches, MICROEXON_PROBLEM_DTYPE), arr(finishes, MICROEXON_PROBLEM_DTYPE)
+        sp = arr(splice_probs, np.float64)
+        fc, fp = arr(finish_cands, MICROEXON_CANDIDATE_DTYPE), arr(finish_probs, np.float64)
+        fr = arr(finish_results, MICROEXON_RESULT_DTYPE).copy()
+        lib = self.lib
+        cap = (lib.gmapdp_single_pair_capacity(S.ctypes.data, len(S)) + lib.gmapdp_end_pair_capacity(E.ctypes.data, len(E))
+               + lib.gmapdp_genome_pair_capacity(G.ctypes.data, len(G)))
+        ccap = 16 * len(XS) + 4096 if candidate_capacity is None else candidate_capacity
+        out = dict(results=np.zeros(max(1, len(S) + len(E)), dtype=RESULT_DTYPE),
+                   genome_results=np.zeros(max(1, len(G)), dtype=GENOME_RESULT_DTYPE),
+                   pairs=np.zeros(max(1, cap), dtype=PAIR_DTYPE),
+                   search_results=np.zeros(max(1, len(XS)), dtype=MICROEXON_RESULT_DTYPE),
+                   candidates=np.zeros(max(1, ccap), dtype=MICROEXON_CANDIDATE_DTYPE), finish_results=fr,
+                   finish_pairs=np.zeros(max(1, lib.gmapdp_microexon_pair_capacity(XF.ctypes.data, len(XF))),
+                                         dtype=PAIR_DTYPE))
+        m = Mixed(singles=S.ctypes.data, nsingle=len(S), ends=E.ctypes.data, nend=len(E), genomes=G.ctypes.data,
+                  ngenome=len(G), splice_probs=sp.ctypes.data, nprobs=len(sp), results=out["results"].ctypes.data,
+                  genome_results=out["genome_results"].ctypes.data, pairs=out["pairs"].ctypes.data,
+                  pair_capacity=cap, searches=XS.ctypes.data, nsearch=len(XS),
+                  search_results=out["search_results"].ctypes.data, candidates=out["candidates"].ctypes.data,
+                  candidate_capacity=ccap, finishes=XF.ctypes.data, nfinish=len(XF), finish_candidates=fc.ctypes.data,
+                  finish_probs=fp.ctypes.data, nfinish_candidates=len(fc), finish_results=fr.ctypes.data,
+                  finish_pairs=out["finish_pairs"].ctypes.data, finish_pair_capacity=len(out["finish_pairs"]))
+        rc = lib.gmapdp_mixed_batch(self.h, qbuf, qucbuf, len(qbuf), C.byref(m))
+        out["candidates_needed"] = int(m.candidates_needed)
+        return rc, out
 
 
 def decode_genome_results(results, pairs, dynprogindices):

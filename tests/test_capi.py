@@ -111,6 +111,20 @@ def test_struct_layouts_match_the_c_header(tmp_path):
     assert gmapdp.OLIGO_PROBLEM_DTYPE.itemsize == sizes[8] and gmapdp.OLIGO_RESULT_DTYPE.itemsize == sizes[9]
 
 
+def test_mixed_struct_layout_matches_the_c_header(tmp_path):
+    """gmapdp_mixed (the drop-in's one-round-trip batch): every field's offset and the size."""
+    import subprocess
+    names = [f for f, _ in gmapdp.Mixed._fields_]
+    src = tmp_path / "mixed.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "gmapdp.h"\nint main(void) {\n' +
+                   "".join('printf("%%zu\\n", offsetof(gmapdp_mixed, %s));\n' % f for f in names) +
+                   'printf("%zu\\n", sizeof(gmapdp_mixed));\nreturn 0; }\n')
+    exe = tmp_path / "mixed"
+    subprocess.run(["gcc", "-I", os.path.join(os.path.dirname(HERE), "include"), str(src), "-o", str(exe)], check=True)
+    out = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    assert out == [getattr(gmapdp.Mixed, f).offset for f in names] + [C.sizeof(gmapdp.Mixed)]
+
+
 def test_genome_splice_sites_match_oracle():
     """gmapdp_genome_splice_sites (host-only) lists the same Maxent_hr_*_prob calls as the oracle's
     restatement of dynprog_genome.c:2573-2660."""
