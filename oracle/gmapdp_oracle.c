@@ -1192,6 +1192,166 @@ orc_end_gap (int end3p, const char *qbuf, const char *qucbuf, int qpos, int rlen
 }
 
 /* ---------------------------------------------------------------------------
+ * Dynprog_end5_splicejunction / Dynprog_end3_splicejunction (dynprog_end.c:1653 /
+ * 2249), nosimd build: the end-gap fill (Dynprog_standard, ENDQ, END penalties,
+ * wide band) against the caller's junction string instead of the genome,
+ * find_best_endpoint_to_queryend_indels_std, and -- when the best score is not
+ * negative -- traceback_local_std (:1138) twice: the far piece (columns past
+ * contlength, genome positions from goffset_far), the known-splice gap holder,
+ * then the anchor piece (goffset_anchor).  Genome skips take their characters
+ * from the junction string (Pairpool_add_genomeskip with a genomesequence,
+ * pairpool.c:1145).  scalars[0..7] = dynprogindex(after), traceback_score,
+ * missscore, nmatches, nmismatches, nopens, nindels, index of the known gap
+ * holder in the returned list (-1: none); out-parameters the reference leaves
+ * unwritten stay ORC_UNSET.
+ * ------------------------------------------------------------------------- */
+#define ORC_UNSET_SJ (-2147483647 - 1)
+
+/* Pairpool_add_genomeskip with the junction string as genomesequence */
+static int
+add_genomeskip_seq (PairSink *s, int r, int c, int dist, const char *gsequence, int queryoffset, int genomeoffset,
+                    int revp, int dpi) {
+  int j, querycoord = r - 1, left = c - dist, right = c - 1, t, genomecoord, step;
+  if (revp) { querycoord = -querycoord; t = left; left = -right; right = -t; step = +1; } else { step = -1; }
+  if (dist >= MICROINTRON_LENGTH) {
+    sink_gapholder(s, 0, dist);
+    return 0;
+  }
+  genomecoord = revp ? left : right;
+  for (j = 0; j < dist; j++) {
+    sink_push(s, queryoffset + querycoord, genomeoffset + genomecoord, ' ', INDEL_COMP, gsequence[genomecoord],
+              gsequence[genomecoord], dpi);
+    genomecoord += step;
+  }
+  return 1;
+}
+
+/* One gap step of traceback_local_std at cell (r, c): nothing on DIAG, else the E or F chain
+   (the reference's `c > 1` / `r > 1` guards) and its records. */
+static void
+local_gap (PairSink *s, Tally *t, const signed char *dirs, int rlength, int glength, int *rp, int *cp,
+           const char *rsequence, const char *gsequence, int queryoffset, int genomeoffset, int revp, int dpi) {
+  size_t plane = (size_t) (glength + 1) * (size_t) (rlength + 1);
+  const signed char *dnogap = dirs, *dE = dirs + plane, *dF = dirs + 2 * plane;
+  int r = *rp, c = *cp, dist = 1;
+  signed char dir = dnogap[IDX(c, r)];
+  if (dir == DIAG) return;
+  if (dir == HORIZ) {
+    while (c > 1 && dE[IDX(c, r)] != DIAG) { dist++; c--; }
+    c--;
+    if (add_genomeskip_seq(s, r, c + dist, dist, gsequence, queryoffset, genomeoffset, revp, dpi)) {
+      t->score += TOPEN + dist * TINDEL;
+      t->nopens += 1;
+      t->nindels += dist;
+    }
+  } else {
+    while (r > 1 && dF[IDX(c, r)] != DIAG) { dist++; r--; }
+    r--;
+    add_queryskip(s, r + dist, c, dist, rsequence, queryoffset, genomeoffset, revp, dpi);
+    t->score += QOPEN + dist * QINDEL;
+    t->nopens += 1;
+    t->nindels += dist;
+  }
+  *rp = r;
+  *cp = c;
+}
+
+/* traceback_local_std (dynprog_end.c:1138): stops once the column reaches endc (or the row 0) */
+static void
+traceback_local (PairSink *s, Tally *t, const signed char *dirs, int rlength, int glength, int *rp, int *cp, int endc,
+                 const char *rsequence, const char *rsequenceuc, const char *gsequence, int queryoffset,
+                 int genomeoffset, int revp, int genestrand, int dpi) {
+  int querycoord, genomecoord;
+  char c1, c1_uc, c2;
+  if (*cp > endc)
+    local_gap(s, t, dirs, rlength, glength, rp, cp, rsequence, gsequence, queryoffset, genomeoffset, revp, dpi);
+  while (*rp > 0 && *cp > endc) {
+    querycoord = *rp - 1;
+    genomecoord = *cp - 1;
+    if (revp) { querycoord = -querycoord; genomecoord = -genomecoord; }
+    c1 = rsequence[querycoord];
+    c1_uc = rsequenceuc[querycoord];
+    c2 = gsequence[genomecoord];
+    if (c1_uc == c2) {
+      t->score += MATCH; t->nmatches += 1;
+      sink_push(s, queryoffset + querycoord, genomeoffset + genomecoord, c1, DYNPROG_MATCH_COMP, c2, c2, dpi);
+    } else if (consistent[genestrand][(unsigned char) c1_uc][(unsigned char) c2]) {
+      t->score += MATCH; t->nmatches += 1;
+      sink_push(s, queryoffset + querycoord, genomeoffset + genomecoord, c1, AMBIGUOUS_COMP, c2, c2, dpi);
+    } else {
+      t->score += MISMATCH; t->nmismatches += 1;
+      sink_push(s, queryoffset + querycoord, genomeoffset + genomecoord, c1, MISMATCH_COMP, c2, c2, dpi);
+    }
+    (*rp)--;
+    (*cp)--;
+    if (!(*rp == 0 && *cp == 0))
+      local_gap(s, t, dirs, rlength, glength, rp, cp, rsequence, gsequence, queryoffset, genomeoffset, revp, dpi);
+  }
+}
+
+int
+orc_end_splicejunction (int end3p, const char *qbuf, const char *qucbuf, int qpos, const char *jbuf, int jpos,
+                        int rlength, int glength, int roffset, int goffset_anchor, int goffset_far, int genestrand,
+                        int jump_late_p, int extraband_end, double defect_rate, int contlength, int dynprogindex,
+                        int *scalars, OrcPair *out, int max_pairs) {
+  const char *rsequence = qbuf + qpos, *rsequenceuc = qucbuf + qpos, *gseq = jbuf + jpos;
+  int open, extend, lband, uband, bestr, bestc, finalscore, n, i, first, known, revp = !end3p;
+  int late = end3p ? jump_late_p : !jump_late_p;
+  int *matrix;
+  signed char *dirs;
+  PairSink sink = {out, 0, max_pairs};
+  Tally t = {0, 0, 0, 0, 0};
+
+  if (g_user_dynprog_p) { open = g_user_open; extend = g_user_extend; }
+  else if (defect_rate < DEFECT_HIGHQ) { open = END_OPEN_HIGHQ; extend = END_EXTEND; }
+  else if (defect_rate < DEFECT_MEDQ) { open = END_OPEN_MEDQ; extend = END_EXTEND; }
+  else { open = END_OPEN_LOWQ; extend = END_EXTEND; }
+
+  scalars[0] = dynprogindex;
+  for (i = 1; i < 7; i++) scalars[i] = ORC_UNSET_SJ;
+  scalars[7] = -1;
+  if (rlength <= 0 || rlength > ORC_MAX_RLENGTH || glength <= 0 || glength > ORC_MAX_GLENGTH) {
+    scalars[1] = scalars[3] = scalars[4] = scalars[5] = scalars[6] = 0;
+    scalars[2] = -100;
+    return -1;
+  }
+  compute_bands(&lband, &uband, rlength, glength, extraband_end, 1);
+  matrix = (int *) malloc((size_t) (glength + 1) * (rlength + 1) * sizeof(int));
+  dirs = (signed char *) malloc((size_t) 3 * (glength + 1) * (rlength + 1));
+  /* end3 scores the upper-cased query, end5 the query as given (as the end gaps) */
+  orc_standard_fill(end3p ? rsequenceuc : rsequence, gseq, gseq, rlength, glength, ENDQ, open, extend, lband, uband,
+                    late, revp, NEG_INFINITY_32, 1, 1, matrix, dirs);
+  find_best_endpoint_to_queryend_indels_std(&finalscore, &bestr, &bestc, matrix, rlength, glength, lband, uband, late);
+  if (finalscore < 0) {
+    free(matrix); free(dirs);
+    return -1;  /* "Need a reasonable alignment to call a splice": nothing written */
+  }
+  traceback_local(&sink, &t, dirs, rlength, glength, &bestr, &bestc, contlength, rsequence, rsequenceuc, gseq,
+                  roffset, goffset_far, revp, genestrand, dynprogindex);
+  known = sink.n;
+  sink_gapholder(&sink, 0, end3p ? goffset_far - goffset_anchor : goffset_anchor - goffset_far);
+  traceback_local(&sink, &t, dirs, rlength, glength, &bestr, &bestc, 0, rsequence, rsequenceuc, gseq,
+                  roffset, goffset_anchor, revp, genestrand, dynprogindex);
+  free(matrix); free(dirs);
+
+  scalars[0] = dynprogindex + (dynprogindex > 0 ? +1 : -1);
+  scalars[1] = t.score; scalars[2] = t.score - rlength * FULLMATCH;
+  scalars[3] = t.nmatches; scalars[4] = t.nmismatches; scalars[5] = t.nopens; scalars[6] = t.nindels;
+  /* push order == List_reverse(pairs); INDEL pairs at its head (the far end) dropped */
+  n = sink.n < max_pairs ? sink.n : max_pairs;
+  for (first = 0; first < n && out[first].comp == INDEL_COMP; first++) ;
+  for (i = first; i < n; i++) out[i - first] = out[i];
+  n -= first;
+  known -= first;
+  if (!end3p) {
+    reverse_pairs(out, n); /* end5 returns List_reverse once more */
+    known = n - 1 - known;
+  }
+  scalars[7] = known;
+  return n;
+}
+
+/* ---------------------------------------------------------------------------
  * Dynprog_genome_gap (dynprog_genome.c:3288-3901), nosimd build, no splicing
  * IIT (Dynprog_genome_setup with splicing_iit NULL: get_known_splicesites
  * :405 adds nothing, so left_known/right_known stay 0 and

@@ -57,6 +57,17 @@ int orc_end_gap (int end3p, const char *qbuf, const char *qucbuf, int qpos, int 
                  int endalign, int require_pos_score_p, int dynprogindex, int *scalars, OrcPair *out,
                  int max_pairs);
 
+/* Dynprog_end5_splicejunction (end3p = 0) / Dynprog_end3_splicejunction (end3p = 1)
+   (dynprog_end.c:1653/2249), nosimd semantics.  (rev_)rsequence = qbuf + qpos as for orc_end_gap;
+   the junction string (rev_)gsequence = jbuf + jpos (end5: its LAST character).
+   scalars[0..7] = dynprogindex(after), traceback_score, missscore, nmatches, nmismatches, nopens,
+   nindels, list index of the known-splice gap holder (-1 none); unwritten ones are INT_MIN.
+   Returns npairs or -1 for NULL. */
+int orc_end_splicejunction (int end3p, const char *qbuf, const char *qucbuf, int qpos, const char *jbuf, int jpos,
+                            int rlength, int glength, int roffset, int goffset_anchor, int goffset_far,
+                            int genestrand, int jump_late_p, int extraband_end, double defect_rate, int contlength,
+                            int dynprogindex, int *scalars, OrcPair *out, int max_pairs);
+
 /* Genome_get_segment_right / _left (genome.c:11023/11079) over the oracle
    genome (no alternate genome: segmentalt = segment). */
 int orc_get_segment (int rightp, unsigned int pos, int length, unsigned int chrbound, int revcomp,

@@ -303,6 +303,44 @@ refh_end_gap (int end3p, const char *qbuf, const char *qucbuf, int qpos, int rle
   return n;
 }
 
+/* Dynprog_end5_splicejunction / Dynprog_end3_splicejunction (dynprog_end.c:1653/2249) with the
+   junction string (rev_)gsequence = jbuf + jpos passed as both gsequence and gsequence_alt.
+   scalars[0..7] = dynprogindex(after), traceback_score, missscore, nmatches, nmismatches, nopens,
+   nindels, list index of the Pair_T with knowngapp (-1 none); the out-parameters start at INT_MIN so
+   that unwritten ones show.  chroffset/chrhigh/watsonp only feed the reference's debug paths. */
+int
+refh_end_splicejunction (int end3p, const char *qbuf, const char *qucbuf, int qpos, const char *jbuf, int jpos,
+                         int rlength, int glength, int roffset, int goffset_anchor, int goffset_far, int genestrand,
+                         int jump_late_p, int extraband_end, double defect_rate, int contlength, int dynprogindex,
+                         int *scalars, RefPair *out, int max_pairs) {
+  List_T pairs, p;
+  int score = -2147483647 - 1, missscore = score, nmatches = score, nmismatches = score, nopens = score;
+  int nindels = score, n, known = -1;
+  char *rsequence = (char *) qbuf + qpos, *rsequenceuc = (char *) qucbuf + qpos, *gseq = (char *) jbuf + jpos;
+
+  Pairpool_reset(pairpool);
+  if (end3p) {
+    pairs = Dynprog_end3_splicejunction(&dynprogindex, &score, &missscore, &nmatches, &nmismatches, &nopens, &nindels,
+                                        dynprogR, rsequence, rsequenceuc, gseq, gseq, rlength, glength, roffset,
+                                        goffset_anchor, goffset_far, /*chroffset*/0, /*chrhigh*/0, /*watsonp*/true,
+                                        genestrand, jump_late_p ? true : false, genome, genome, pairpool,
+                                        extraband_end, defect_rate, contlength);
+  } else {
+    pairs = Dynprog_end5_splicejunction(&dynprogindex, &score, &missscore, &nmatches, &nmismatches, &nopens, &nindels,
+                                        dynprogL, rsequence, rsequenceuc, gseq, gseq, rlength, glength, roffset,
+                                        goffset_anchor, goffset_far, /*chroffset*/0, /*chrhigh*/0, /*watsonp*/true,
+                                        genestrand, jump_late_p ? true : false, genome, genome, pairpool,
+                                        extraband_end, defect_rate, contlength);
+  }
+  scalars[0] = dynprogindex; scalars[1] = score; scalars[2] = missscore; scalars[3] = nmatches;
+  scalars[4] = nmismatches; scalars[5] = nopens; scalars[6] = nindels;
+  for (n = 0, p = pairs; p != NULL; p = List_next(p), n++)
+    if (((Pair_T) List_head(p))->knowngapp && known < 0) known = n;
+  scalars[7] = known;
+  if (pairs == NULL) return -1;
+  return flatten(pairs, out, max_pairs);
+}
+
 /* Dynprog_genome_gap (dynprog_genome.c:3288).  flags: 1 watsonp, 2 jump_late_p,
    8 halfp, 16 finalp.  scalars[0..9] = dynprogindex(after), traceback_score,
    nmatches, nmismatches, nopens, nindels, new_leftgenomepos,

@@ -889,3 +889,78 @@ def microexon_problem(rng, genome: bytearray, edge=False, at=None):
     return dict(q=q, quc=quc, rlength=len(q), roffset=roffset, goffsetL=goffsetL,
                 rev_goffsetR=goffsetL + span - 1, cdna_direction=cdna_direction, chroffset=chroffset,
                 chrhigh=chrhigh, watsonp=int(watsonp), genestrand=0, dynprogindex=rng.choice([1, 5, -1, -7]))
+
+
+# ---------------------------------------------------------------------------
+# Dynprog_end5_splicejunction / Dynprog_end3_splicejunction (dynprog_end.c:1653/2249)
+# ---------------------------------------------------------------------------
+_SJ_ARGS = [C.c_int, C.c_char_p, C.c_char_p, C.c_int, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+            C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(Pair),
+            C.c_int]
+
+
+def _end_splicejunction(self, p):
+    """((dynprogindex, traceback_score, missscore, nmatches, nmismatches, nopens, nindels, known_index),
+    pairs-or-None); scalars the reference leaves unwritten are INT_MIN."""
+    self._before_call()
+    f = getattr(self.lib, self.prefix + "end_splicejunction")
+    f.argtypes = _SJ_ARGS
+    f.restype = C.c_int
+    scal = (C.c_int * 8)()
+    q, quc, j = p["q"] or b"A", p["quc"] or b"A", p["j"] or b"A"
+    qpos = 0 if p["end3p"] else len(q) - 1
+    jpos = 0 if p["end3p"] else len(j) - 1
+    n = f(p["end3p"], q, quc, qpos, j, jpos, p["rlength"], p["glength"], p["roffset"], p["goffset_anchor"],
+          p["goffset_far"], p["genestrand"], p["jump_late_p"], p["extraband"], p["defect_rate"], p["contlength"],
+          p["dynprogindex"], scal, self._pairs, MAXPAIRS)
+    assert n <= MAXPAIRS
+    return tuple(scal), (None if n < 0 else [self._pairs[i].key() for i in range(n)])
+
+
+Oracle.end_splicejunction = _end_splicejunction
+Ref.end_splicejunction = _end_splicejunction
+
+
+def splicejunction_problem(rng, genome: bytes, edge=False):
+    """One Splicetrie_solve_end5/end3-shaped call (splicetrie.c via Dynprog_end5/3_known,
+    dynprog_end.c:2748/3009): the read end beyond the anchor (rlength), a junction string of glength >=
+    rlength built as the reference builds it (Dynprog_make_splicejunction_5/3 + make_contjunction_5/3):
+    the contlength characters next to the anchor and the far exon's piece, mostly a real splice of the
+    read end (mutated), sometimes random.  end5 strings are given in genome order with the anchor side
+    LAST (rev_gsequence points at the last character); end3 strings with the anchor side first."""
+    end3p = rng.random() < 0.5
+    rlength = max(1, int(rng.gammavariate(1.5, 12))) if not edge else rng.choice([1, 2, 3, rng.randint(40, 700)])
+    glength = rlength + rng.choice([0, 0, 1, 3, 10, 25]) if rng.random() < 0.9 else rng.randint(1, 2100)
+    contlength = rng.randint(0, max(0, min(rlength, glength) - 1))
+    if edge and rng.random() < 0.3:
+        contlength = rng.choice([0, max(0, rlength - 1), rlength + 2])
+    a = rng.randint(0, len(genome) - 2 * glength - 10) if len(genome) > 2 * glength + 10 else 0
+    b = rng.randint(0, len(genome) - glength - 1) if len(genome) > glength + 1 else 0
+    prox = genome[a:a + contlength]
+    dist = genome[b:b + max(0, glength - contlength)]
+    j = (dist + prox) if not end3p else (prox + dist)
+    j = j[:glength].ljust(glength, b"A")
+    mode = rng.random()
+    if mode < 0.7:  # the read end follows the junction
+        piece = j[-rlength:] if not end3p else j[:rlength]
+        q, quc = mutate(rng, piece, sub=rng.choice([0.0, 0.02, 0.06, 0.15]), indel=rng.choice([0.0, 0.0, 0.03]))
+        q, quc = (q or b"A"), (quc or b"A")
+        if len(q) > rlength:
+            q, quc = (q[-rlength:], quc[-rlength:]) if not end3p else (q[:rlength], quc[:rlength])
+        while len(q) < rlength:
+            ch = bytes([rng.choice(b"ACGT")])
+            q, quc = (ch + q, ch + quc) if not end3p else (q + ch, quc + ch)
+    else:
+        q = bytes(rng.choice(b"ACGTacgtN") for _ in range(rlength))
+        quc = q.upper()
+    j = bytes(c if c in b"ACGTN" else ord("N") for c in j)
+    roffset = rng.randint(0, 3000) if not edge else rng.choice([0, 1, rng.randint(0, 3000)])
+    if not end3p:
+        roffset = max(roffset, rlength - 1) if rng.random() < 0.9 else roffset
+    ga = rng.randint(0, 200000) if not edge else rng.choice([0, 3, rng.randint(0, 200000)])
+    gf = rng.randint(0, 200000)
+    return dict(end3p=int(end3p), q=q, quc=quc, j=j, rlength=rlength, glength=glength, roffset=roffset,
+                goffset_anchor=ga, goffset_far=gf, genestrand=0,
+                jump_late_p=rng.randint(0, 1), extraband=rng.choice([3, 6, 10, 10, 10, 14]),
+                defect_rate=rng.choice([0.001, 0.005, 0.02, 0.05]), contlength=contlength,
+                dynprogindex=rng.choice([1, 5, -1, -7]))

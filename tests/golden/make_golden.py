@@ -27,6 +27,10 @@ and the reference's outputs.
                          simd_domain below); halfp genome gaps from the --enable-alloca AVX2 build
   stage2_golden.npz      Stage2_compute (stage2.c:6325): seeding, chaining, convert_to_nucleotides,
                          filter_unique (python tests/golden/make_golden.py stage2)
+  splicejunction_golden.npz
+                         Dynprog_end5_splicejunction / Dynprog_end3_splicejunction (dynprog_end.c:1653/2249),
+                         the known-splice end fills Splicetrie_solve_end5/end3 issue with -s
+                         (python tests/golden/make_golden.py splicejunction)
   oligo_golden.npz       stage-2 seeding: Oligoindex_hr_tally + Oligoindex_get_mappings
                          (oligoindex_hr.c:33849/34127) as Stage2_compute runs them for GMAP
                          (python tests/golden/make_golden.py oligo)
@@ -415,6 +419,42 @@ def load_microexon(path):
     return z["genome"].tobytes(), probs, cands, cprobs, outs
 
 
+SJ_PARAMS = ["end3p", "rlength", "glength", "roffset", "goffset_anchor", "goffset_far", "genestrand", "jump_late_p",
+             "extraband", "contlength", "dynprogindex"]
+
+
+def splicejunction_problems(seed=2031, n_typical=1200, n_edge=400, genome_len=60000):
+    from dpbind import splicejunction_problem
+    rng = random.Random(seed)
+    g = random_genome(rng, genome_len)
+    probs = [splicejunction_problem(rng, g) for _ in range(n_typical)]
+    probs += [splicejunction_problem(rng, g, edge=True) for _ in range(n_edge)]
+    return g, probs
+
+
+def main_splicejunction():
+    g, probs = splicejunction_problems()
+    ref = Ref("nosimd")
+    ref.set_genome(g)
+    outputs = {"ref_nosimd": [ref.end_splicejunction(p) for p in probs]}
+    d = pack(g, probs, outputs, SJ_PARAMS)
+    d["jlen"] = np.array([len(p["j"]) for p in probs], dtype=np.int32)
+    d["jbuf"] = np.frombuffer(b"".join(p["j"] for p in probs), dtype=np.uint8)
+    out = os.path.join(HERE, "splicejunction_golden.npz")
+    np.savez_compressed(out, **d)
+    print("wrote %s: %d problems, %d NULL" % (out, len(probs), sum(o[1] is None for o in outputs["ref_nosimd"])))
+
+
+def load_splicejunction(path):
+    g, probs, outs = load(path)
+    z = np.load(path, allow_pickle=False)
+    joff = np.concatenate([[0], np.cumsum(z["jlen"])])
+    jb = z["jbuf"].tobytes()
+    for i, p in enumerate(probs):
+        p["j"] = jb[joff[i]:joff[i + 1]]
+    return g, probs, outs
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "simd":
         main_simd()
@@ -426,5 +466,7 @@ if __name__ == "__main__":
         main_stage2()
     elif len(sys.argv) > 1 and sys.argv[1] == "microexon":
         main_microexon()
+    elif len(sys.argv) > 1 and sys.argv[1] == "splicejunction":
+        main_splicejunction()
     else:
         main()

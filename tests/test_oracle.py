@@ -477,3 +477,57 @@ def test_oracle_microexon_vs_reference_random():
             cp = microexon_probs(ref, orc.microexon_candidates(p), p["chroffset"])
             a, b = ref.microexon_int(p), orc.microexon_int(p, cp)
             assert a == b, "seed %d problem %d: reference %s vs oracle %s" % (seed, i, a[:2], b[:2])
+
+
+# ---------------------------------------------------------------------------
+# Dynprog_end5_splicejunction / Dynprog_end3_splicejunction
+# ---------------------------------------------------------------------------
+def _golden_sj():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(HERE, "golden", "make_golden.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m.load_splicejunction(os.path.join(HERE, "golden", "splicejunction_golden.npz"))
+
+
+def test_oracle_splicejunction_matches_golden(oracle):
+    g, probs, outs = _golden_sj()
+    oracle.set_genome(g)
+    exp = outs["ref_nosimd"]
+    assert len(probs) == len(exp) == 1600
+    bad = [i for i, p in enumerate(probs) if oracle.end_splicejunction(p) != exp[i]]
+    assert bad == [], "oracle differs from the reference splice-junction golden on %d problems (first %s)" % (
+        len(bad), bad[:5])
+
+
+def test_splicejunction_golden_covers_every_branch():
+    g, probs, outs = _golden_sj()
+    exp = outs["ref_nosimd"]
+    unset = -2147483648
+    kinds = set()
+    for p, (s, pairs) in zip(probs, exp):
+        if pairs is None:
+            kinds.add((p["end3p"], "guard" if s[2] == -100 else "negative"))
+            assert s[2] == -100 or s[1] == unset  # the reference writes nothing on a negative best score
+        else:
+            kinds.add((p["end3p"], "pairs"))
+            assert 0 <= s[7] < len(pairs) and pairs[s[7]][0] == -1  # the known gap holder
+            kinds.add((p["end3p"], "gapholder_only" if len(pairs) == 1 else "both"))
+    for end3p in (0, 1):
+        for k in ("guard", "negative", "pairs", "both"):
+            assert (end3p, k) in kinds, (end3p, k)
+    assert any(p["contlength"] == 0 for p in probs) and any(p["contlength"] >= p["rlength"] for p in probs)
+
+
+@pytest.mark.skipif(not ref_available("nosimd"), reason="reference objects (oracle/_ref) not built here")
+def test_oracle_splicejunction_vs_reference_random(oracle):
+    from dpbind import splicejunction_problem
+    ref = Ref("nosimd")
+    rng = random.Random(4343)
+    g = random_genome(rng, 200000)
+    ref.set_genome(g)
+    oracle.set_genome(g)
+    bad = [i for i in range(3000)
+           for p in [splicejunction_problem(rng, g, edge=(i % 6 == 0))]
+           if ref.end_splicejunction(p) != oracle.end_splicejunction(p)]
+    assert bad == []
