@@ -345,7 +345,7 @@ template <int R, bool CARRY, int S = 64, bool PK = (S < 64), bool STORE = false>
 __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lband, int uband, int open, int ext,
                                           int late, int track, const int8_t* sc, int srow, const uint8_t* gcl,
                                           uint64_t* dirs, const BridgeCarry* bc_, int& bestr, int& bestc,
-                                          int gmax = 0, int* smat = nullptr) {
+                                          int gmax = 0, int* smat = nullptr, int* best_score = nullptr) {
   static_assert(S == 64 || (R == 1 && !CARRY), "segmented fills are single-word, no bridge carry");
   static_assert(!STORE || S == 64, "score matrices are stored by whole-wave fills only");
   const int lk = (S == 64) ? lane : (lane & (S - 1));  // lane within the segment
@@ -555,6 +555,9 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
       }
     }
     key = seg_max_u64<S>(key);
+    // the endpoint's score (find_best_endpoint_to_queryend_indels_std's *finalscore; NEG_INFINITY_32
+    // when no cell of the scanned row beat the initial value)
+    if (best_score) *best_score = key ? (int)(uint32_t)(key >> 24) - (1 << 30) : kNegInf32;
     if (key == 0) {
       bestr = (track == 2) ? rlen : 0;
       bestc = 0;
@@ -800,6 +803,113 @@ __device__ __forceinline__ void traceback_band(int lane, const WORD* dirs, int W
                                                uint64_t nwords, gmapdp_pair* out, Tally& t, int bitoff = 0) {
   const BandDirs<R, WORD> d{dirs, W, uband, bitoff};
   traceback_walk(lane, d, r, c, G, q, quc, gch, cons, watson, chroffset, chrhigh, blocks, nwords, out, t);
+}
+
+// Genome skip whose characters come from the problem's own genome string (Pairpool_add_genomeskip with a
+// genomesequence, pairpool.c:1145-1154): column cc's character is gch[cc].
+template <typename GV>
+__device__ __forceinline__ void emit_genomeskip_seq(int lane, int r, int cs, int dist, const Geo& G, const GV& gch,
+                                                    gmapdp_pair* out, Tally& t) {
+  if (dist >= kMicrointronLength) {
+    if (lane == 0) put_pair(out, t.count, -1, -1, dist, ' ', ' ', ' ', ' ');
+    t.count += 1;
+    t.seen = true;
+    return;
+  }
+  const int qp = G.qpos(r);
+  for (int base = 0; base < dist; base += 64) {
+    const int j = base + lane;
+    const bool active = j < dist;
+    const int gp = G.gpos(cs - j);
+    const bool good = active && qp >= 0 && gp >= 0;
+    const uint64_t mgood = ballot(good);
+    if (good) {
+      const char c2 = gch[cs - j];
+      put_pair(out, t.count + lanes_below(mgood, lane), qp, gp, 0, ' ', '-', c2, c2);
+    }
+    const int nw = __popcll(mgood);
+    t.count += nw;
+    if (!t.seen) t.lead += nw;
+  }
+  t.score += kTopen + dist * kTindel;
+  t.nopens += 1;
+  t.nindels += dist;
+}
+
+// ---- traceback_local_std (dynprog_end.c:1138-1289) ----
+// The splice-junction end gaps trace back in two pieces: from the endpoint until the column reaches
+// `endc` (the far exon's piece of the junction string), then -- after the caller's gap holder -- on
+// to column 0.  Differences from Dynprog_traceback_std that this restates:
+//  * a gap step is taken at the start cell and after every diagonal step, whatever `endc` is (so an
+//    E chain may cross `endc`), and the walk continues only while r > 0 and c > endc;
+//  * the boundary cells are walked too: row 0 (nogap = HORIZ for c <= uband, dynprog.c:1304-1309)
+//    is a genome skip to column 0, column 0 (nogap = VERT for r <= lband) a query skip to row 0;
+//    outside the band they are DIAG (Directions32_alloc clears them, dynprog.c:497);
+//  * genome skips take their characters from the genome string.
+// Every walk here is wave-cooperative as in traceback_walk: a run is found with one ballot over 64
+// candidate cells.
+template <typename DA, typename QV, typename GV>
+__device__ __forceinline__ void traceback_local(int lane, const DA& dir, int& r, int& c, int endc, int lband,
+                                                int uband, const Geo& G, const QV& q, const QV& quc, const GV& gch,
+                                                const uint8_t* __restrict__ cons, gmapdp_pair* out, Tally& t) {
+  auto gap = [&]() {
+    if (r == 0) {
+      if (c <= uband) {
+        emit_genomeskip_seq(lane, 0, c, c, G, gch, out, t);
+        c = 0;
+      }
+      return;
+    }
+    if (c == 0) {
+      if (r <= lband) {
+        emit_queryskip(lane, r, 0, r, G, q, out, t);
+        r = 0;
+      }
+      return;
+    }
+    const uint32_t isV = dir(c, 1, r);
+    const uint32_t isH = dir(c, 0, r);
+    if (!isV && isH) {
+      int n = 0;
+      for (int base = 0;; base += 64) {
+        const int j = base + lane;
+        const bool cont = (c - j >= 1) && dir(c - j, 2, r);
+        const uint64_t stop = ~ballot(cont);
+        if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
+      }
+      const int dist = n + 1;
+      const int c_end = (c - n - 1) > 0 ? (c - n - 1) : 0;
+      emit_genomeskip_seq(lane, r, c_end + dist, dist, G, gch, out, t);
+      c = c_end;
+    } else if (isV) {
+      int n = 0;
+      for (int base = 0;; base += 64) {
+        const int j = base + lane;
+        const bool cont = (r - j >= 1) && dir(c, 3, r - j);
+        const uint64_t stop = ~ballot(cont);
+        if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
+      }
+      const int dist = n + 1;
+      const int r_end = (r - n - 1) > 0 ? (r - n - 1) : 0;
+      emit_queryskip(lane, r_end + dist, c, dist, G, q, out, t);
+      r = r_end;
+    }
+  };
+  if (c > endc) gap();
+  while (r > 0 && c > endc) {
+    // diagonal run: the walk goes on from cell j >= 1 while it is inside (r > 0, c > endc) and DIAG
+    int n = 0;
+    for (int base = 0;; base += 64) {
+      const int j = base + lane;
+      const bool cont = (j == 0) || ((r - j >= 1) && (c - j > endc) && !dir(c - j, 0, r - j) && !dir(c - j, 1, r - j));
+      const uint64_t stop = ~ballot(cont);
+      if (stop) { n = base + __ffsll((long long)stop) - 1; break; }
+    }
+    emit_diag(lane, r, c, n, G, q, quc, gch, cons, out, t);
+    r -= n;
+    c -= n;
+    if (!(r == 0 && c == 0)) gap();
+  }
 }
 
 // reverse out[0..n) in place (List_reverse of an already emitted run)

@@ -49,6 +49,10 @@ hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
                      const char* qseq_uc, const double* sprob, const int8_t* sctab, const uint8_t* constab,
                      const int8_t* isctab, gmapdp_genome_result* results, gmapdp_pair* pairs,
                      unsigned char* gscratch);
+size_t lds_bytes_sj(int rlength, int glength, int R, bool dirs_lds);
+hipError_t launch_sj(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevSjProblem* probs,
+                     const int* order, const char* qseq, const char* qseq_uc, const char* jseq, const int8_t* sctab,
+                     const uint8_t* constab, gmapdp_sj_result* results, gmapdp_pair* pairs, uint64_t* gdirs);
 size_t lds_bytes_uxe(int rlength, int glength, int B);
 size_t scratch_bytes_uxe(int rlength, int glength, int lband, int uband, int B);
 size_t lds_bytes_uxg(int rlength, int glengthL, int glengthR, int B);
@@ -262,6 +266,7 @@ struct gmapdp_ctx {
   HostBuf hin, hout;   // their pinned host images
   DevBuf gprobs, gorder, sprob, gresults;
   DevBuf cprobs, corder, cresults, cscratch;  // Dynprog_cdna_gap batches
+  DevBuf sjprobs, sjorder, sjresults, sjseq, sjdirs;  // Dynprog_end5/3_splicejunction batches
   DevBuf oprobs, oresults, oscratch, onpos, omap, otable, odiag, opool, opoolctr;  // stage-2 seeding batches
   DevBuf s2probs, s2results, s2scratch, s2counters, s2paths, s2pairs, s2qseq;  // Stage2_compute batches
   DevBuf mxprobs, mxres, mxcands, mxcnt, mxdirect, mxprobs2, mxpairs;  // Dynprog_microexon_int batches
@@ -1604,6 +1609,182 @@ int gmapdp_cdna_gap_batch(gmapdp_ctx* ctx, const gmapdp_cdna_problem* problems, 
     e = hipMemcpyAsync(pairs, ctx->pairs.p, sizeof(gmapdp_pair) * pair_off, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = ctx_sync(ctx, s);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "cdna execution: %s", e);
+  for (int d = 0; d < ndev; d++) results[dev_problem[d]] = dres[d];
+  return GMAPDP_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Dynprog_end5/3_splicejunction (dynprog_end.c:1653-1919 / 2249-2498)
+// ---------------------------------------------------------------------------
+static size_t sj_capacity_one(const gmapdp_sj_problem& p) {
+  // every traceback step emits at most one record per row or column, plus the known gap holder
+  return (size_t)std::max(p.rlength, 0) + (size_t)std::max(p.glength, 0) + 2;
+}
+
+// Prologue of the splice-junction end gaps: returns 1 if the problem runs on the GPU.
+static int convert_sj(gmapdp_ctx* ctx, const gmapdp_sj_problem& p, size_t qbytes, const char* jseq, size_t jbytes,
+                      gmapdp_sj_result& res, DevSjProblem& d, int* err) {
+  *err = 0;
+  res.npairs = 0;
+  res.pair_offset = 0;
+  res.known_index = -1;
+  res.dynprogindex = p.dynprogindex;
+  if (p.flags & GMAPDP_SIMD) {
+    *err = bad(ctx, "splice-junction end gaps are built in nosimd semantics only");
+    return 0;
+  }
+  if (p.rlength <= 0 || p.rlength > GMAPDP_MAX_RLENGTH || p.glength <= 0 || p.glength > GMAPDP_MAX_GLENGTH) {
+    res.traceback_score = 0;  // size guard (dynprog_end.c:1707-1722)
+    res.nmatches = res.nmismatches = res.nopens = res.nindels = 0;
+    res.missscore = -100;
+    return 0;
+  }
+  const bool end3 = p.end3p != 0;
+  if (p.qoff < 0 || (size_t)p.qoff + (size_t)p.rlength > qbytes || p.joff < 0 ||
+      (size_t)p.joff + (size_t)p.glength > jbytes) {
+    *err = bad(ctx, "splice-junction problem outside its query or junction arena");
+    return 0;
+  }
+  for (int i = 0; i < p.glength; i++) {
+    const char c = jseq[p.joff + i];
+    if (c != 'A' && c != 'C' && c != 'G' && c != 'T' && c != 'N') {
+      *err = bad(ctx, "junction characters must be A C G T or N");
+      return 0;
+    }
+  }
+  std::memset(&d, 0, sizeof(d));
+  d.rlength = p.rlength;
+  d.glength = p.glength;
+  d.roffset = p.roffset;
+  d.goffset_anchor = p.goffset_anchor;
+  d.goffset_far = p.goffset_far;
+  d.contlength = p.contlength;
+  d.end3p = end3 ? 1 : 0;
+  d.genestrand = p.genestrand;
+  d.dynprogindex = p.dynprogindex;
+  const bool jl = p.flags & GMAPDP_JUMP_LATE;
+  if (end3) {
+    d.qbase = p.qoff;
+    d.jbase = p.joff;
+    d.late = jl ? 1 : 0;
+    d.known_jump = p.goffset_far - p.goffset_anchor;
+  } else {
+    d.qbase = p.qoff + p.rlength - 1;  // rev_rsequence / rev_gsequence: the slices' last characters
+    d.jbase = p.joff + p.glength - 1;
+    d.late = jl ? 0 : 1;               // "for revp true" !jump_late_p (dynprog_end.c:1792)
+    d.known_jump = p.goffset_anchor - p.goffset_far;
+  }
+  const double dr = p.defect_rate;
+  if (ctx->user_dynprog_p) {
+    d.open = ctx->user_open;
+    d.extend = ctx->user_extend;
+  } else {
+    d.open = dr < 0.003 ? -10 : (dr < 0.014 ? -8 : -6);  // END_OPEN_HIGHQ/MEDQ/LOWQ
+    d.extend = -2;                                        // END_EXTEND_*
+  }
+  if (d.open > 0) {
+    *err = bad(ctx, "positive gap-open penalty is not supported by the scan formulation");
+    return 0;
+  }
+  gmapdp_compute_bands(&d.lband, &d.uband, p.rlength, p.glength, p.extraband, /*widebandp*/ 1);
+  if (d.lband < 0 || d.uband < 0) {
+    *err = bad(ctx, "negative band");
+    return 0;
+  }
+  return 1;
+}
+
+extern "C" {
+
+size_t gmapdp_sj_pair_capacity(const gmapdp_sj_problem* problems, int n) {
+  size_t cap = 0;
+  for (int i = 0; i < n; i++) cap += sj_capacity_one(problems[i]);
+  return cap;
+}
+
+int gmapdp_end_splicejunction_batch(gmapdp_ctx* ctx, const gmapdp_sj_problem* problems, int n, const char* qseq,
+                                    const char* qseq_uc, size_t qbytes, const char* jseq, size_t jbytes,
+                                    gmapdp_sj_result* results, gmapdp_pair* pairs, size_t pair_capacity) {
+  if (!ctx || n < 0 || (n > 0 && (!problems || !results))) return GMAPDP_EINVAL;
+  if (n == 0) return GMAPDP_OK;
+  (void)hipSetDevice(ctx->device);
+  std::vector<DevSjProblem> dev;
+  std::vector<int> dev_problem;
+  std::map<std::pair<int, int>, std::vector<int>> classes;  // (R, dirs in LDS) -> device slots
+  size_t pair_off = 0, dirs_off = 0;
+  for (int i = 0; i < n; i++) {
+    DevSjProblem d;
+    int err = 0;
+    if (!convert_sj(ctx, problems[i], qbytes, jseq, jbytes, results[i], d, &err)) {
+      if (err) return err;
+      continue;
+    }
+    const int W = d.lband + d.uband + 1;
+    const int R = pick_R(W);
+    if (R > kMaxR) return bad(ctx, "splice-junction band wider than 4096 cells");
+    const bool dirs_lds = lds_bytes_sj(d.rlength, d.glength, R, true) <= kLdsBudget;
+    if (!dirs_lds) {
+      if (lds_bytes_sj(d.rlength, d.glength, R, false) > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
+      d.dirs_offset = (int64_t)dirs_off;
+      dirs_off += align_up((size_t)(d.glength + 1) * 4 * R * 8, 256);
+    }
+    d.pair_offset = (int32_t)pair_off;
+    pair_off += sj_capacity_one(problems[i]);
+    classes[{R, dirs_lds ? 1 : 0}].push_back((int)dev.size());
+    dev.push_back(d);
+    dev_problem.push_back(i);
+  }
+  if (pair_off > pair_capacity) return bad(ctx, "pair arena too small");
+  const int ndev = (int)dev.size();
+  if (ndev == 0) return GMAPDP_OK;
+  std::vector<int> order;
+  order.reserve(ndev);
+  struct CL {
+    int R;
+    bool dirs_lds;
+    int first, count;
+    size_t lds;
+  };
+  std::vector<CL> launches;
+  for (auto& kv : classes) {
+    CL L{kv.first.first, kv.first.second != 0, (int)order.size(), (int)kv.second.size(), 0};
+    for (int s : kv.second) {
+      L.lds = std::max(L.lds, lds_bytes_sj(dev[s].rlength, dev[s].glength, L.R, L.dirs_lds));
+      order.push_back(s);
+    }
+    launches.push_back(L);
+  }
+  hipError_t e = ctx->sjprobs.ensure(sizeof(DevSjProblem) * ndev);
+  if (e == hipSuccess) e = ctx->sjorder.ensure(sizeof(int) * ndev);
+  if (e == hipSuccess) e = ctx->sjresults.ensure(sizeof(gmapdp_sj_result) * ndev);
+  if (e == hipSuccess) e = ctx->sjdirs.ensure(std::max<size_t>(dirs_off, 256));
+  if (e == hipSuccess) e = ctx->sjseq.ensure(jbytes);
+  if (e == hipSuccess) e = ctx->qseq.ensure(qbytes);
+  if (e == hipSuccess) e = ctx->qseq_uc.ensure(qbytes);
+  if (e == hipSuccess) e = ctx->pairs.ensure(sizeof(gmapdp_pair) * std::max<size_t>(pair_off, 1));
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "device buffers: %s", e);
+  hipStream_t s = ctx->stream;
+  e = hipMemcpyAsync(ctx->sjprobs.p, dev.data(), sizeof(DevSjProblem) * ndev, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(ctx->sjorder.p, order.data(), sizeof(int) * ndev, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(ctx->qseq.p, qseq, qbytes, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(ctx->qseq_uc.p, qseq_uc, qbytes, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(ctx->sjseq.p, jseq, jbytes, hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "upload: %s", e);
+  for (const CL& L : launches) {
+    e = launch_sj(L.R, L.dirs_lds, L.count, L.lds, s, (const DevSjProblem*)ctx->sjprobs.p,
+                  (const int*)ctx->sjorder.p + L.first, (const char*)ctx->qseq.p, (const char*)ctx->qseq_uc.p,
+                  (const char*)ctx->sjseq.p, ctx->d_sc, ctx->d_cs, (gmapdp_sj_result*)ctx->sjresults.p,
+                  (gmapdp_pair*)ctx->pairs.p, (uint64_t*)ctx->sjdirs.p);
+    if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "splice-junction launch: %s", e);
+  }
+  std::vector<gmapdp_sj_result> dres(ndev);
+  e = hipMemcpyAsync(dres.data(), ctx->sjresults.p, sizeof(gmapdp_sj_result) * ndev, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess && pairs)
+    e = hipMemcpyAsync(pairs, ctx->pairs.p, sizeof(gmapdp_pair) * pair_off, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = ctx_sync(ctx, s);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "splice-junction execution: %s", e);
   for (int d = 0; d < ndev; d++) results[dev_problem[d]] = dres[d];
   return GMAPDP_OK;
 }

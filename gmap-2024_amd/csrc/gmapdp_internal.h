@@ -133,6 +133,33 @@ struct DevCdnaProblem {
   int64_t scratch_offset; // byte offset of the problem's region of the global scratch
 };
 
+// Dynprog_end5/3_splicejunction descriptor (dynprog_end.c:1653/2249).  Columns come from the batch's
+// junction arena: column c is jseq[jbase + sgn*(c-1)] (sgn -1 for end5, whose rev_gsequence points at
+// the junction's last character).
+constexpr int kMismatchEndQ = 3;        // Mismatchtype_T ENDQ: the score-table slice of the end gaps
+constexpr int kFullMatch = 3;           // FULLMATCH (dynprog.h:43)
+struct DevSjProblem {
+  int32_t qbase;          // arena index of the query character of DP row 1
+  int32_t jbase;          // junction-arena index of the character of DP column 1
+  int32_t rlength;
+  int32_t glength;
+  int32_t roffset;        // (rev_)roffset
+  int32_t goffset_anchor; // (rev_)goffset_anchor: genome positions of the anchor piece
+  int32_t goffset_far;    // (rev_)goffset_far: genome positions of the far exon's piece
+  int32_t known_jump;     // genomejump of the known-splice gap holder
+  int32_t contlength;     // endc of the far piece's traceback
+  int32_t lband;
+  int32_t uband;
+  int32_t open;
+  int32_t extend;
+  int32_t late;           // tie rule of the fill and the endpoint scan (end5: !jump_late_p)
+  int32_t end3p;
+  int32_t genestrand;
+  int32_t dynprogindex;
+  int32_t pair_offset;
+  int64_t dirs_offset;    // byte offset into the global direction scratch (!DIRS_LDS classes)
+};
+
 // Stage-2 seeding descriptor (Oligoindex_hr_tally + Oligoindex_get_mappings, oligoindex_hr.c:33849/34127)
 struct DevOligoProblem {
   int32_t qoff;           // arena index of queryuc_ptr[0]

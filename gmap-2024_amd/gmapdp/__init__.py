@@ -81,6 +81,17 @@ class CdnaResult(C.Structure):
                 ("gap_queryjump", C.c_int32), ("pad_", C.c_int32)]
 
 
+class SjProblem(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("qoff", "joff", "rlength", "glength", "roffset", "goffset_anchor",
+                                         "goffset_far", "contlength", "flags", "genestrand", "extraband", "end3p",
+                                         "dynprogindex", "pad_")] + [("defect_rate", C.c_double)]
+
+
+class SjResult(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("npairs", "pair_offset", "traceback_score", "missscore", "nmatches",
+                                         "nmismatches", "nopens", "nindels", "dynprogindex", "known_index")]
+
+
 class OligoProblem(C.Structure):
     _fields_ = [("qoff", C.c_int32), ("querylength", C.c_int32), ("chrstart", C.c_uint32), ("chrend", C.c_uint32),
                 ("chroffset", C.c_uint64), ("chrhigh", C.c_uint64), ("plusp", C.c_int32), ("minor", C.c_int32)]
@@ -131,6 +142,8 @@ GENOME_PROBLEM_DTYPE = _struct_dtype(GenomeProblem)
 GENOME_RESULT_DTYPE = _struct_dtype(GenomeResult)
 CDNA_PROBLEM_DTYPE = _struct_dtype(CdnaProblem)
 CDNA_RESULT_DTYPE = _struct_dtype(CdnaResult)
+SJ_PROBLEM_DTYPE = _struct_dtype(SjProblem)
+SJ_RESULT_DTYPE = _struct_dtype(SjResult)
 OLIGO_PROBLEM_DTYPE = _struct_dtype(OligoProblem)
 OLIGO_RESULT_DTYPE = _struct_dtype(OligoResult)
 STAGE2_PROBLEM_DTYPE = _struct_dtype(Stage2Problem)
@@ -222,6 +235,10 @@ def load_library(path=LIB_PATH):
         "gmapdp_cdna_gap_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t,
                                             C.c_void_p, C.c_void_p, C.c_size_t]),
         "gmapdp_cdna_pair_capacity": (C.c_size_t, [C.c_void_p, C.c_int]),
+        "gmapdp_end_splicejunction_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                                      C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
+                                                      C.c_size_t]),
+        "gmapdp_sj_pair_capacity": (C.c_size_t, [C.c_void_p, C.c_int]),
         "gmapdp_oligo_mappings_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_size_t,
                                                   C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
                                                   C.c_void_p, C.c_size_t]),
@@ -461,6 +478,52 @@ class Engine:
         self._check(rc, "gmapdp_end_gap_batch")
         return decode_results(results, pairs, [p["dynprogindex"] for p in calls])
 
+
+    # -- batched Dynprog_end5/3_splicejunction --------------------------------
+    @staticmethod
+    def build_sj_batch(calls):
+        """calls: dicts with the Dynprog_end{5,3}_splicejunction arguments (end3p, q, quc, j, rlength, glength,
+        roffset, goffset_anchor, goffset_far, contlength, genestrand, jump_late_p, extraband, defect_rate,
+        dynprogindex); q/quc is the query slice and j the junction string the reference reads (end5: both
+        rev pointers are the slices' last characters)."""
+        calls = list(calls)
+        probs = np.zeros(len(calls), dtype=SJ_PROBLEM_DTYPE)
+        qparts, qucparts, jparts, off, joff = [], [], [], 0, 0
+        for i, p in enumerate(calls):
+            probs[i]["qoff"] = off
+            probs[i]["joff"] = joff
+            for k in ("rlength", "glength", "roffset", "goffset_anchor", "goffset_far", "contlength", "genestrand",
+                      "end3p", "dynprogindex", "defect_rate"):
+                probs[i][k] = p[k]
+            probs[i]["extraband"] = p["extraband"]
+            probs[i]["flags"] = (JUMP_LATE if p["jump_late_p"] else 0) | (SIMD if p.get("simd") else 0)
+            qparts.append(p["q"])
+            qucparts.append(p["quc"])
+            jparts.append(p["j"])
+            off += len(p["q"])
+            joff += len(p["j"])
+        return probs, (b"".join(qparts) or b"\0"), (b"".join(qucparts) or b"\0"), (b"".join(jparts) or b"\0")
+
+    def end_splicejunction_batch(self, calls):
+        """Per call ((dynprogindex, traceback_score, missscore, nmatches, nmismatches, nopens, nindels,
+        known_index), pairs-or-None), as the oracle's end_splicejunction."""
+        calls = list(calls)
+        probs, qbuf, qucbuf, jbuf = self.build_sj_batch(calls)
+        n = len(probs)
+        results = np.zeros(n, dtype=SJ_RESULT_DTYPE)
+        cap = self.lib.gmapdp_sj_pair_capacity(probs.ctypes.data, n)
+        pairs = np.zeros(max(cap, 1), dtype=PAIR_DTYPE)
+        rc = self.lib.gmapdp_end_splicejunction_batch(self.h, probs.ctypes.data, n, qbuf, qucbuf, len(qbuf), jbuf,
+                                                      len(jbuf), results.ctypes.data, pairs.ctypes.data, cap)
+        self._check(rc, "gmapdp_end_splicejunction_batch")
+        out = []
+        for i, res in enumerate(results):
+            scal = tuple(int(res[k]) for k in ("dynprogindex", "traceback_score", "missscore", "nmatches",
+                                                "nmismatches", "nopens", "nindels", "known_index"))
+            n_ = int(res["npairs"])
+            out.append((scal, None if n_ == 0 else
+                        decode_pairs(pairs, int(res["pair_offset"]), n_, calls[i]["dynprogindex"])))
+        return out
 
     # -- batched Dynprog_genome_gap -------------------------------------------
     def genome_gap_batch_raw(self, probs, qbuf, qucbuf, splice_probs):

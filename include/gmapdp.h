@@ -25,6 +25,8 @@
  *                            inputs (mixed single + end batches)
  *   gmapdp_compute_bands     Dynprog_compute_bands (dynprog.c:1247)
  *   gmapdp_cdna_gap_batch    Dynprog_cdna_gap (dynprog_cdna.c:787)
+ *   gmapdp_end_splicejunction_batch  Dynprog_end5/3_splicejunction (dynprog_end.c:1653/2249), the
+ *                            known-splice-site end alignments of Dynprog_end5/3_known (:2748/3009)
  *   gmapdp_oligo_mappings_batch  stage-2 seeding: Oligoindex_hr_tally + Oligoindex_get_mappings
  *                            (oligoindex_hr.c:33849/34127) as Stage2_compute calls them (stage2.c:6480-6495)
  *   gmapdp_stage2_batch      Stage2_compute (stage2.c:6325) as GMAP calls it (gmap.c:1208): the
@@ -319,6 +321,56 @@ int gmapdp_cdna_gap_batch (gmapdp_ctx *ctx, const gmapdp_cdna_problem *problems,
                            const char *qseq, const char *qseq_uc, size_t qbytes,
                            gmapdp_cdna_result *results, gmapdp_pair *pairs, size_t pair_capacity);
 size_t gmapdp_cdna_pair_capacity (const gmapdp_cdna_problem *problems, int n);
+
+/* One Dynprog_end5_splicejunction (end3p = 0, dynprog_end.c:1653) or Dynprog_end3_splicejunction
+ * (end3p = 1, dynprog_end.c:2249) call: the known-splice-site end alignment Splicetrie_solve_end5/3
+ * (splicetrie.c) run for each candidate far exon.  The query slice is qseq[qoff .. qoff+rlength) as
+ * for an end-gap problem: end5's rev_rsequence points at its LAST character.  The junction string
+ * (the caller's splicejunction buffer, built by Dynprog_make_splicejunction_5/3) is
+ * jseq[joff .. joff+glength) in string order: end5's rev_gsequence points at its last character,
+ * end3's gsequence at its first.  Junction characters must be A C G T or N.  Nosimd semantics
+ * (Dynprog_standard + traceback_local_std); GMAPDP_SIMD is GMAPDP_EINVAL. */
+typedef struct {
+  int32_t qoff;
+  int32_t joff;
+  int32_t rlength;
+  int32_t glength;
+  int32_t roffset;          /* (rev_)roffset */
+  int32_t goffset_anchor;   /* (rev_)goffset_anchor */
+  int32_t goffset_far;      /* (rev_)goffset_far */
+  int32_t contlength;
+  int32_t flags;            /* GMAPDP_JUMP_LATE */
+  int32_t genestrand;
+  int32_t extraband;        /* extraband_end */
+  int32_t end3p;
+  int32_t dynprogindex;
+  int32_t pad_;
+  double defect_rate;
+} gmapdp_sj_problem;
+
+/* Out-parameters of the splice-junction end gaps.  NULL (npairs 0) with the size guard's values
+ * (traceback_score 0, missscore -100, counters 0) for lengths outside 1..660 x 1..2000; NULL with
+ * everything but dynprogindex GMAPDP_UNSET when the best endpoint scores below 0 (the reference
+ * writes nothing then).  Otherwise the list's pairs[known_index] is the known-splice gap holder
+ * (Pairpool_push_gapholder with knownp = true, jump = its genomejump). */
+typedef struct {
+  int32_t npairs;
+  int32_t pair_offset;
+  int32_t traceback_score;
+  int32_t missscore;
+  int32_t nmatches;
+  int32_t nmismatches;
+  int32_t nopens;
+  int32_t nindels;
+  int32_t dynprogindex;
+  int32_t known_index;      /* -1 for NULL */
+} gmapdp_sj_result;
+
+int gmapdp_end_splicejunction_batch (gmapdp_ctx *ctx, const gmapdp_sj_problem *problems, int n,
+                                     const char *qseq, const char *qseq_uc, size_t qbytes,
+                                     const char *jseq, size_t jbytes,
+                                     gmapdp_sj_result *results, gmapdp_pair *pairs, size_t pair_capacity);
+size_t gmapdp_sj_pair_capacity (const gmapdp_sj_problem *problems, int n);
 
 /* Dynprog_microexon_int (dynprog_single.c:900, replaced at stage3.c:9664): the
  * microexon search inside an intron, in two steps because the reference scores each candidate with the
