@@ -69,6 +69,8 @@
 #include "cellpool.h"
 #include "stopwatch.h"
 #include "stage2.h"
+#include "splicetrie.h"
+#include "complement.h"
 #include "mem.h"
 
 #include "gmapdp.h"
@@ -102,11 +104,14 @@ static int shim_homopolymerp = 0, shim_splicing_iit = 0;
 
 /* Calls that reached the engine, per wrapped entry point (printed at exit with GMAPDP_SHIM_STATS=1;
    tests use it to prove the pipeline really ran on the GPU). */
-enum { ST_SINGLE, ST_END5, ST_END3, ST_GENOME, ST_CDNA, ST_OLIGO, ST_STAGE2, ST_MICROEXON, ST_N };
+enum { ST_SINGLE, ST_END5, ST_END3, ST_GENOME, ST_CDNA, ST_OLIGO, ST_STAGE2, ST_MICROEXON, ST_SJ5, ST_SJ3,
+       ST_KNOWN5, ST_KNOWN3, ST_N };
 static const char *const shim_stat_name[ST_N] = {"Dynprog_single_gap", "Dynprog_end5_gap", "Dynprog_end3_gap",
                                                  "Dynprog_genome_gap", "Dynprog_cdna_gap",
                                                  "Oligoindex_get_mappings", "Stage2_compute",
-                                                 "Dynprog_microexon_int"};
+                                                 "Dynprog_microexon_int", "Dynprog_end5_splicejunction",
+                                                 "Dynprog_end3_splicejunction", "Dynprog_end5_known",
+                                                 "Dynprog_end3_known"};
 static unsigned long shim_stats[ST_N];
 
 static unsigned long shim_batches, shim_batched;
@@ -172,15 +177,34 @@ __wrap_Dynprog_single_setup (int user_open_in, int user_extend_in, bool user_dyn
   shim_homopolymerp = homopolymerp_in ? 1 : 0;
 }
 
+/* Known splice sites (-s), as Dynprog_end_setup records them (dynprog_end.c:119-141): the sites sorted by
+   position with their types, and the observed / max-distance splice tries that Splicetrie_solve_end5/3
+   (splicetrie.c) walk.  Dynprog_end5/3_known below restate their orchestration over these. */
+static Univcoord_T *shim_splicesites = NULL;
+static Splicetype_T *shim_splicetypes = NULL;
+static int shim_nsplicesites = 0;
+static Trieoffset_T *shim_trieoffsets_obs = NULL, *shim_trieoffsets_max = NULL;
+static Triecontent_T *shim_triecontents_obs = NULL, *shim_triecontents_max = NULL;
+
 void
 __wrap_Dynprog_end_setup (Univcoord_T *splicesites_in, Splicetype_T *splicetypes_in, Chrpos_T *splicedists_in,
                           int nsplicesites_in, Trieoffset_T *trieoffsets_obs_in, Triecontent_T *triecontents_obs_in,
                           Trieoffset_T *trieoffsets_max_in, Triecontent_T *triecontents_max_in,
                           int user_open_in, int user_extend_in, bool user_dynprog_p_in) {
-  /* Known splice sites (-s): GMAP then calls Dynprog_end5/3_known and _splicejunction
-     (dynprog_end.c:1653-3009), which the engine does not implement; refused at setup, before any read
-     runs, so that no reference CPU code executes inside the product */
-  if (nsplicesites_in > 0) shim_refuse("known splice sites (-s: Dynprog_end5/3_known, _splicejunction)");
+#ifdef HAVE_SSE2
+  /* the splice-junction end gaps (dynprog_end.c:1653/2249) are built in nosimd semantics only: a SIMD
+     build with known splice sites is refused at setup, before any read runs, so that no reference CPU
+     DP executes inside the product */
+  if (nsplicesites_in > 0)
+    shim_refuse("known splice sites (-s) in a SIMD build (the splice-junction end gaps are nosimd only)");
+#endif
+  shim_splicesites = splicesites_in;
+  shim_splicetypes = splicetypes_in;
+  shim_nsplicesites = nsplicesites_in;
+  shim_trieoffsets_obs = trieoffsets_obs_in;
+  shim_triecontents_obs = triecontents_obs_in;
+  shim_trieoffsets_max = trieoffsets_max_in;
+  shim_triecontents_max = triecontents_max_in;
   __real_Dynprog_end_setup(splicesites_in, splicetypes_in, splicedists_in, nsplicesites_in, trieoffsets_obs_in,
                            triecontents_obs_in, trieoffsets_max_in, triecontents_max_in, user_open_in,
                            user_extend_in, user_dynprog_p_in);
@@ -274,7 +298,7 @@ shim_context (Genome_T genome) {
 }
 
 /* ---- requests and the dispatcher ---- */
-enum { K_SINGLE, K_END, K_GENOME, K_CDNA, K_MXS, K_MXF, K_OLIGO, K_STAGE2 };  /* K_MXS / K_MXF: microexon
+enum { K_SINGLE, K_END, K_GENOME, K_CDNA, K_MXS, K_MXF, K_OLIGO, K_STAGE2, K_SJ };  /* K_MXS / K_MXF: microexon
                                                                                    search / finish */
 
 typedef struct shim_req {
@@ -288,15 +312,19 @@ typedef struct shim_req {
     gmapdp_oligo_problem o;
     gmapdp_stage2_problem s2;
     gmapdp_microexon_problem mx;
+    gmapdp_sj_problem sj;
   } p;                          /* qoff / prob_offset relative to q and probs below */
   const char *q, *quc;          /* the query slice (borrowed: the caller waits) */
   size_t qlen;
+  const char *j;                /* splice-junction end gaps: the junction string (borrowed) */
+  size_t jlen;
   const double *probs;          /* genome gaps: the splice probabilities */
   size_t nprobs;
   /* outputs, filled by the dispatcher (pair_offset / table_offset / diag_offset rebased to 0) */
   gmapdp_result r;
   gmapdp_genome_result gr;
   gmapdp_cdna_result cr;
+  gmapdp_sj_result sjr;
   gmapdp_oligo_result orr;
   gmapdp_stage2_result s2r;     /* path_offset rebased to 0, pair_offset of each path to the request's pairs */
   /* per-thread buffers (grown by the caller before submitting) */
@@ -371,6 +399,8 @@ shim_request (int kind) {
   r->qlen = 0;
   r->probs = NULL;
   r->nprobs = 0;
+  r->j = NULL;
+  r->jlen = 0;
   memset(&r->p, 0, sizeof(r->p));
   return r;
 }
@@ -476,8 +506,12 @@ typedef struct {
   gmapdp_cdna_problem *c;
   gmapdp_oligo_problem *o;
   gmapdp_stage2_problem *s2;
-  shim_req **rs, **re, **rg, **rc, **ro, **r2, **rxs, **rxf;
-  size_t scap, ecap, gcap, ccap, ocap, s2cap, rscap, recap, rgcap, rccap, rocap, r2cap, rxscap, rxfcap;
+  gmapdp_sj_problem *sj;
+  gmapdp_sj_result *sjres;
+  char *jq;
+  size_t sjcap, sjrescap, jqcap;
+  shim_req **rs, **re, **rg, **rc, **ro, **r2, **rxs, **rxf, **rsj;
+  size_t scap, ecap, gcap, ccap, ocap, s2cap, rscap, recap, rgcap, rccap, rocap, r2cap, rxscap, rxfcap, rsjcap;
   gmapdp_microexon_problem *mx, *mxf;        /* searches, finishes */
   gmapdp_microexon_result *mxres, *mxfres;
   gmapdp_microexon_candidate *mxc, *mxsc;     /* the finishes' candidates, the searches' candidates */
@@ -515,7 +549,7 @@ shim_copy_pairs (shim_req *r, const gmapdp_pair *src, int n) {
 static void
 shim_run (shim_req *batch) {
   shim_req *r;
-  size_t ns = 0, ne = 0, ng = 0, nc = 0, no = 0, n2 = 0, nxs = 0, nxf = 0, n = 0, qb = 0, pb = 0, cap, i;
+  size_t ns = 0, ne = 0, ng = 0, nc = 0, no = 0, n2 = 0, nxs = 0, nxf = 0, nsj = 0, n = 0, qb = 0, pb = 0, cap, i;
   double t0, t1, td[4];
   Genome_T genome = NULL;
   for (r = batch; r != NULL; r = r->next) {
@@ -529,6 +563,7 @@ shim_run (shim_req *batch) {
     case K_STAGE2: GROW(D.r2, D.r2cap, n2 + 1); D.r2[n2++] = r; break;
     case K_MXS: GROW(D.rxs, D.rxscap, nxs + 1); D.rxs[nxs++] = r; break;
     case K_MXF: GROW(D.rxf, D.rxfcap, nxf + 1); D.rxf[nxf++] = r; break;
+    case K_SJ: GROW(D.rsj, D.rsjcap, nsj + 1); D.rsj[nsj++] = r; break;
     default: GROW(D.ro, D.rocap, no + 1); D.ro[no++] = r; break;
     }
   }
@@ -718,6 +753,44 @@ shim_run (shim_req *batch) {
       r->cr = D.cres[i];
       shim_copy_pairs(r, D.pairs + r->cr.pair_offset, r->cr.npairs);
       r->cr.pair_offset = 0;
+    }
+  }
+  /* splice-junction end gaps (known splice sites, -s): their own batch over a query and a junction arena */
+  if (nsj > 0) {
+    size_t jb = 0;
+    GROW(D.sj, D.sjcap, nsj + 1);
+    qb = 0;
+    for (i = 0; i < nsj; i++) {
+      qb += D.rsj[i]->qlen;
+      jb += D.rsj[i]->jlen;
+    }
+    GROW(D.q, D.qcap, qb + 1);
+    GROW(D.quc, D.quccap, qb + 1);
+    GROW(D.jq, D.jqcap, jb + 1);
+    qb = jb = 0;
+    for (i = 0; i < nsj; i++) {
+      r = D.rsj[i];
+      D.sj[i] = r->p.sj;
+      D.sj[i].qoff = (int32_t) qb;
+      D.sj[i].joff = (int32_t) jb;
+      if (r->qlen) {
+        memcpy(D.q + qb, r->q, r->qlen);
+        memcpy(D.quc + qb, r->quc, r->qlen);
+      }
+      if (r->jlen) memcpy(D.jq + jb, r->j, r->jlen);
+      qb += r->qlen;
+      jb += r->jlen;
+    }
+    cap = gmapdp_sj_pair_capacity(D.sj, (int) nsj);
+    GROW(D.pairs, D.paircap, cap + 1);
+    GROW(D.sjres, D.sjrescap, nsj + 1);
+    shim_check(gmapdp_end_splicejunction_batch(shim_ctx, D.sj, (int) nsj, D.q, D.quc, qb, D.jq, jb, D.sjres,
+                                               D.pairs, cap), "gmapdp_end_splicejunction_batch");
+    for (i = 0; i < nsj; i++) {
+      r = D.rsj[i];
+      r->sjr = D.sjres[i];
+      shim_copy_pairs(r, D.pairs + r->sjr.pair_offset, r->sjr.npairs);
+      r->sjr.pair_offset = 0;
     }
   }
 
@@ -976,6 +1049,363 @@ __wrap_Dynprog_end3_gap (int *dynprogindex, int *finalscore, int *nmatches, int 
                       sequenceuc1, length1, length2, offset1, offset2, chroffset, chrhigh, watsonp, genestrand,
                       jump_late_p, genome, genomealt, pairpool, extraband_end, defect_rate, endalign,
                       require_pos_score_p);
+}
+
+/* ---- known splice sites (-s): Dynprog_end5/3_splicejunction, Dynprog_end5/3_known ---- */
+
+/* The engine's records -> the reference's List_T; the gap holder at known_index is the known splice
+   (Pairpool_push_gapholder with knownp, dynprog_end.c:1888/2484), other gap holders are not. */
+static List_T
+shim_list_known (const gmapdp_pair *pairs, int n, int dynprogindex, int known_index, Pairpool_T pairpool) {
+  List_T list = NULL;
+  int i;
+  for (i = n - 1; i >= 0; i--) {
+    const gmapdp_pair *p = &pairs[i];
+    if (p->querypos == -1 && p->genomepos == -1)
+      list = Pairpool_push_gapholder(list, pairpool, /*queryjump*/0, p->jump, /*leftpair*/NULL, /*rightpair*/NULL,
+                                     /*knownp*/i == known_index);
+    else
+      list = Pairpool_push(list, pairpool, p->querypos, p->genomepos, p->cdna, p->comp, p->genome, p->genomealt,
+                           dynprogindex);
+  }
+  return list;
+}
+
+/* Dynprog_end5_splicejunction (end3p 0) / Dynprog_end3_splicejunction (end3p 1): one request on the DP
+   queue; the junction string travels with the query (gmapdp_end_splicejunction_batch). */
+static List_T
+shim_splicejunction (int end3p, int *dynprogindex, int *finalscore, int *missscore, int *nmatches, int *nmismatches,
+                     int *nopens, int *nindels, Dynprog_T dynprog, char *seq, char *sequc, char *gseq, char *gseq_alt,
+                     int length1, int length2, int offset1, int offset2_anchor, int offset2_far, int genestrand,
+                     bool jump_late_p, Genome_T genome, Genome_T genomealt, Pairpool_T pairpool, int extraband_end,
+                     double defect_rate, int contlength) {
+  shim_req *r;
+  gmapdp_sj_problem *p;
+  List_T list;
+  const int inside = length1 > 0 && length1 <= GMAPDP_MAX_RLENGTH && length2 > 0 && length2 <= GMAPDP_MAX_GLENGTH;
+  shim_check_call(genome, genomealt, dynprog);
+  /* end5's rev pointers are the slices' LAST characters (dynprog_end.c:1653) */
+  const char *q = (end3p || !inside) ? seq : seq - (length1 - 1);
+  const char *quc = (end3p || !inside) ? sequc : sequc - (length1 - 1);
+  const char *j = (end3p || !inside) ? gseq : gseq - (length2 - 1);
+  const char *j_alt = (end3p || !inside) ? gseq_alt : gseq_alt - (length2 - 1);
+  if (inside && gseq_alt != NULL && j_alt != j && memcmp(j_alt, j, (size_t) length2) != 0)
+    shim_refuse("a splice junction whose alternate-allele string differs (genomealt)");
+  r = shim_request(K_SJ);
+  p = &r->p.sj;
+  p->rlength = length1;
+  p->glength = length2;
+  p->roffset = offset1;
+  p->goffset_anchor = offset2_anchor;
+  p->goffset_far = offset2_far;
+  p->contlength = contlength;
+  p->flags = jump_late_p ? GMAPDP_JUMP_LATE : 0;
+  p->genestrand = genestrand;
+  p->extraband = extraband_end;
+  p->end3p = end3p;
+  p->dynprogindex = *dynprogindex;
+  p->defect_rate = defect_rate;
+  r->genome = genome;
+  r->q = q;
+  r->quc = quc;
+  r->qlen = inside ? (size_t) length1 : 0;
+  r->j = j;
+  r->jlen = inside ? (size_t) length2 : 0;
+  r->cost = inside ? shim_cost(length1, length2, extraband_end) : 0;
+  r->longp = r->cost > shim_long_cost;
+  GROW(r->pairs, r->pcap, gmapdp_sj_pair_capacity(p, 1) + 1);
+  shim_submit(r);
+  shim_count(end3p ? ST_SJ3 : ST_SJ5);
+  list = shim_list_known(r->pairs, r->sjr.npairs, p->dynprogindex, r->sjr.known_index, pairpool);
+  /* a negative best endpoint leaves every out-parameter as it was (dynprog_end.c:1798-1800) */
+  *dynprogindex = r->sjr.dynprogindex;
+  if (r->sjr.traceback_score != GMAPDP_UNSET) *finalscore = r->sjr.traceback_score;
+  if (r->sjr.missscore != GMAPDP_UNSET) *missscore = r->sjr.missscore;
+  if (r->sjr.nmatches != GMAPDP_UNSET) *nmatches = r->sjr.nmatches;
+  if (r->sjr.nmismatches != GMAPDP_UNSET) *nmismatches = r->sjr.nmismatches;
+  if (r->sjr.nopens != GMAPDP_UNSET) *nopens = r->sjr.nopens;
+  if (r->sjr.nindels != GMAPDP_UNSET) *nindels = r->sjr.nindels;
+  return list;
+}
+
+List_T
+__wrap_Dynprog_end5_splicejunction (int *dynprogindex, int *finalscore, int *missscore, int *nmatches,
+                                    int *nmismatches, int *nopens, int *nindels, Dynprog_T dynprog,
+                                    char *rev_rsequence, char *rev_rsequenceuc, char *rev_gsequence,
+                                    char *rev_gsequence_alt, int length1, int length2, int revoffset1,
+                                    int revoffset2_anchor, int revoffset2_far, Univcoord_T chroffset,
+                                    Univcoord_T chrhigh, bool watsonp, int genestrand, bool jump_late_p,
+                                    Genome_T genome, Genome_T genomealt, Pairpool_T pairpool, int extraband_end,
+                                    double defect_rate, int contlength) {
+  (void) chroffset;  /* genome skips take their characters from the junction string */
+  (void) chrhigh;
+  (void) watsonp;
+  return shim_splicejunction(0, dynprogindex, finalscore, missscore, nmatches, nmismatches, nopens, nindels, dynprog,
+                             rev_rsequence, rev_rsequenceuc, rev_gsequence, rev_gsequence_alt, length1, length2,
+                             revoffset1, revoffset2_anchor, revoffset2_far, genestrand, jump_late_p, genome, genomealt,
+                             pairpool, extraband_end, defect_rate, contlength);
+}
+
+List_T
+__wrap_Dynprog_end3_splicejunction (int *dynprogindex, int *finalscore, int *missscore, int *nmatches,
+                                    int *nmismatches, int *nopens, int *nindels, Dynprog_T dynprog, char *rsequence,
+                                    char *rsequenceuc, char *gsequence, char *gsequence_alt, int length1,
+                                    int length2, int offset1, int offset2_anchor, int offset2_far,
+                                    Univcoord_T chroffset, Univcoord_T chrhigh, bool watsonp, int genestrand,
+                                    bool jump_late_p, Genome_T genome, Genome_T genomealt, Pairpool_T pairpool,
+                                    int extraband_end, double defect_rate, int contlength) {
+  (void) chroffset;
+  (void) chrhigh;
+  (void) watsonp;
+  return shim_splicejunction(1, dynprogindex, finalscore, missscore, nmatches, nmismatches, nopens, nindels, dynprog,
+                             rsequence, rsequenceuc, gsequence, gsequence_alt, length1, length2, offset1,
+                             offset2_anchor, offset2_far, genestrand, jump_late_p, genome, genomealt, pairpool,
+                             extraband_end, defect_rate, contlength);
+}
+
+/* binary_search (dynprog_end.c:2722): the first site at or above goal in positions[lowi, highi) */
+static int
+shim_site_search (int lowi, int highi, const Univcoord_T *positions, Univcoord_T goal) {
+  int middlei;
+  while (lowi < highi) {
+    middlei = lowi + ((highi - lowi) / 2);
+    if (goal < positions[middlei]) highi = middlei;
+    else if (goal > positions[middlei]) lowi = middlei + 1;
+    else return middlei;
+  }
+  return highi;
+}
+
+static const char shim_compl[128] = COMPLEMENT_LC;
+
+/* make_complement_inplace (dynprog_end.c:2501) */
+static void
+shim_revcomp_inplace (char *s, int length) {
+  int i, k;
+  char t;
+  for (i = 0, k = length - 1; i < k; i++, k--) {
+    t = shim_compl[(int) s[i]];
+    s[i] = shim_compl[(int) s[k]];
+    s[k] = t;
+  }
+  if (i == k) s[i] = shim_compl[(int) s[i]];
+}
+
+/* make_contjunction_5 / _3 (dynprog_end.c:2519 / 2620): the contlength characters next to the anchor
+   site, at the junction's end (5') or start (3'), reverse-complemented on the minus strand */
+static void
+shim_contjunction (int end3p, char *sj, char *sj_alt, Univcoord_T splicecoord, int splicelength, int contlength,
+                   Splicetype_T anchor_splicetype, Genome_T genome, Genome_T genomealt, bool watsonp) {
+  char *prox = end3p ? sj : sj + splicelength, *prox_alt = end3p ? sj_alt : sj_alt + splicelength;
+  int before;  /* the piece ends at the site (else starts there) */
+  if (anchor_splicetype == ACCEPTOR || anchor_splicetype == ANTIDONOR) before = 0;
+  else if (anchor_splicetype == ANTIACCEPTOR || anchor_splicetype == DONOR) before = 1;
+  else shim_refuse("an unexpected anchor splice type");
+  Genome_fill_buffer_blocks_noterm(genome, genomealt, before ? splicecoord - contlength : splicecoord,
+                                   (Chrpos_T) contlength, prox, prox_alt);
+  if (watsonp == false) {
+    shim_revcomp_inplace(prox, contlength);
+    shim_revcomp_inplace(prox_alt, contlength);
+  }
+}
+
+/* Dynprog_end5_known (end3p 0, dynprog_end.c:2748-3005) / Dynprog_end3_known (end3p 1, :3009-3266):
+   restated over the engine.  The straight end gap (QUERYEND_NOGAPS, then BEST_LOCAL when no splice wins)
+   runs through the engine's Dynprog_end5/3_gap; every anchor site of the right type in the read end's
+   span builds its half of the junction and hands it to the reference's Splicetrie_solve_end5/3
+   (splicetrie.c, the trie walk over the far sites), whose Dynprog_end5/3_splicejunction calls land on
+   the engine through the wraps above. */
+static List_T
+shim_known (int end3p, bool *knownsplicep, int *dynprogindex, int *finalscore, int *ambig_end_length,
+            Splicetype_T *ambig_splicetype, int *nmatches, int *nmismatches, int *nopens, int *nindels,
+            Dynprog_T dynprog, char *seq, char *sequc, int rlength, int glength, int roffset, int goffset,
+            int querylength, Univcoord_T chroffset, Univcoord_T chrhigh, Univcoord_T knownsplice_limit_low,
+            Univcoord_T knownsplice_limit_high, int cdna_direction, bool watsonp, int genestrand, bool jump_late_p,
+            Genome_T genome, Genome_T genomealt, Pairpool_T pairpool, int extraband_end, double defect_rate) {
+  List_T best_pairs = NULL, orig_pairs;
+  Pair_T pair;
+  Univcoord_T low, high, far_limit_low, far_limit_high;
+  Splicetype_T anchor_splicetype = DONOR, far_splicetype = DONOR;
+  int contlength, splicelength, j, orig_score, threshold_miss_score, perfect_score, obsmax_penalty;
+  char *sj, *sj_alt;
+
+  shim_count(end3p ? ST_KNOWN3 : ST_KNOWN5);
+  *ambig_end_length = 0;
+  if (rlength <= 0 || glength <= 0) {
+    *finalscore = 0;
+    *knownsplicep = false;
+    return (List_T) NULL;
+  }
+  perfect_score = rlength * FULLMATCH;
+
+  /* without splicing, all the way to the query end */
+  best_pairs = end3p ? __wrap_Dynprog_end3_gap(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels,
+                                               dynprog, seq, sequc, rlength, glength, roffset, goffset, chroffset,
+                                               chrhigh, watsonp, genestrand, jump_late_p, genome, genomealt,
+                                               pairpool, extraband_end, defect_rate, QUERYEND_NOGAPS, true)
+                     : __wrap_Dynprog_end5_gap(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels,
+                                               dynprog, seq, sequc, rlength, glength, roffset, goffset, chroffset,
+                                               chrhigh, watsonp, genestrand, jump_late_p, genome, genomealt,
+                                               pairpool, extraband_end, defect_rate, QUERYEND_NOGAPS, true);
+  if (*finalscore <= 0) {
+    orig_score = 0;
+    orig_pairs = best_pairs = (List_T) NULL;
+  } else {
+    orig_score = *finalscore;
+    orig_pairs = best_pairs;
+  }
+  threshold_miss_score = orig_score - perfect_score;
+  if (threshold_miss_score < -2 * FULLMATCH) threshold_miss_score = -2 * FULLMATCH;  /* <= 2 mismatches */
+  *knownsplicep = false;
+
+  if (threshold_miss_score < 0 && glength > 0) {
+    sj = (char *) malloc((size_t) glength + 1);
+    sj_alt = (char *) malloc((size_t) glength + 1);
+    if (sj == NULL || sj_alt == NULL) shim_refuse("host memory for a splice junction (out of memory)");
+    if (!end3p) {
+      if (watsonp == true) {
+        low = chroffset + goffset - rlength + 2;
+        high = chroffset + goffset + 1;
+        anchor_splicetype = cdna_direction > 0 ? ACCEPTOR : ANTIDONOR;
+        far_splicetype = cdna_direction > 0 ? DONOR : ANTIACCEPTOR;
+      } else {
+        low = chrhigh - goffset;
+        high = chrhigh - (goffset - rlength) - 1;
+        anchor_splicetype = cdna_direction > 0 ? ANTIACCEPTOR : DONOR;
+        far_splicetype = cdna_direction > 0 ? ANTIDONOR : ACCEPTOR;
+      }
+    } else {
+      if (watsonp == true) {
+        low = chroffset + goffset;
+        high = chroffset + goffset + rlength - 1;
+        anchor_splicetype = cdna_direction > 0 ? DONOR : ANTIACCEPTOR;
+        far_splicetype = cdna_direction > 0 ? ACCEPTOR : ANTIDONOR;
+      } else {
+        low = chrhigh - (goffset + rlength) + 2;
+        high = chrhigh - goffset + 1;
+        anchor_splicetype = cdna_direction > 0 ? ANTIDONOR : ACCEPTOR;
+        far_splicetype = cdna_direction > 0 ? ANTIACCEPTOR : DONOR;
+      }
+    }
+    far_limit_low = knownsplice_limit_low;
+    far_limit_high = knownsplice_limit_high;
+    j = shim_site_search(0, shim_nsplicesites, shim_splicesites, low);
+    while (j < shim_nsplicesites && shim_splicesites[j] <= high) {
+      if (shim_splicetypes[j] == anchor_splicetype) {
+        /* 5': the anchor piece runs from the site to the read end's genomic end; 3': from its start */
+        if (!end3p) contlength = watsonp ? (int) (high - shim_splicesites[j]) : (int) (shim_splicesites[j] - low);
+        else contlength = watsonp ? (int) (shim_splicesites[j] - low) : (int) (high - shim_splicesites[j]);
+        splicelength = glength - contlength;
+        shim_contjunction(end3p, sj, sj_alt, shim_splicesites[j], splicelength, contlength, anchor_splicetype, genome,
+                          genomealt, watsonp);
+        if (watsonp == (end3p ? true : false)) far_limit_low = shim_splicesites[j];  /* 3' watson / 5' crick */
+        else far_limit_high = shim_splicesites[j];                                  /* 5' watson / 3' crick */
+        obsmax_penalty = 0;
+        if (shim_trieoffsets_obs != NULL) {
+          best_pairs = end3p
+              ? Splicetrie_solve_end3(best_pairs, shim_triecontents_obs, shim_trieoffsets_obs, j, far_limit_low,
+                                      far_limit_high, finalscore, nmatches, nmismatches, nopens, nindels, knownsplicep,
+                                      ambig_end_length, &threshold_miss_score, /*obsmax_penalty*/0, perfect_score,
+                                      shim_splicesites[j], sj, sj_alt, splicelength, contlength, far_splicetype,
+                                      chroffset, chrhigh, dynprogindex, dynprog, seq, sequc, rlength, glength, roffset,
+                                      goffset, cdna_direction, watsonp, genestrand, jump_late_p, genome, genomealt,
+                                      pairpool, extraband_end, defect_rate)
+              : Splicetrie_solve_end5(best_pairs, shim_triecontents_obs, shim_trieoffsets_obs, j, far_limit_low,
+                                      far_limit_high, finalscore, nmatches, nmismatches, nopens, nindels, knownsplicep,
+                                      ambig_end_length, &threshold_miss_score, /*obsmax_penalty*/0, perfect_score,
+                                      shim_splicesites[j], sj, sj_alt, splicelength, contlength, far_splicetype,
+                                      chroffset, chrhigh, dynprogindex, dynprog, seq, sequc, rlength, glength, roffset,
+                                      goffset, cdna_direction, watsonp, genestrand, jump_late_p, genome, genomealt,
+                                      pairpool, extraband_end, defect_rate);
+          obsmax_penalty += FULLMATCH;
+        }
+        if (threshold_miss_score + obsmax_penalty < 0 && shim_trieoffsets_max != NULL) {
+          best_pairs = end3p
+              ? Splicetrie_solve_end3(best_pairs, shim_triecontents_max, shim_trieoffsets_max, j, far_limit_low,
+                                      far_limit_high, finalscore, nmatches, nmismatches, nopens, nindels, knownsplicep,
+                                      ambig_end_length, &threshold_miss_score, obsmax_penalty, perfect_score,
+                                      shim_splicesites[j], sj, sj_alt, splicelength, contlength, far_splicetype,
+                                      chroffset, chrhigh, dynprogindex, dynprog, seq, sequc, rlength, glength, roffset,
+                                      goffset, cdna_direction, watsonp, genestrand, jump_late_p, genome, genomealt,
+                                      pairpool, extraband_end, defect_rate)
+              : Splicetrie_solve_end5(best_pairs, shim_triecontents_max, shim_trieoffsets_max, j, far_limit_low,
+                                      far_limit_high, finalscore, nmatches, nmismatches, nopens, nindels, knownsplicep,
+                                      ambig_end_length, &threshold_miss_score, obsmax_penalty, perfect_score,
+                                      shim_splicesites[j], sj, sj_alt, splicelength, contlength, far_splicetype,
+                                      chroffset, chrhigh, dynprogindex, dynprog, seq, sequc, rlength, glength, roffset,
+                                      goffset, cdna_direction, watsonp, genestrand, jump_late_p, genome, genomealt,
+                                      pairpool, extraband_end, defect_rate);
+        }
+      }
+      j++;
+    }
+    free(sj_alt);
+    free(sj);
+  }
+
+  if (best_pairs == NULL) {
+    if (*ambig_end_length == 0) {
+      /* not to the query end this time: the best local end (chopped to the Dynprog_T's limits) */
+      if (rlength > dynprog->max_rlength) rlength = dynprog->max_rlength;
+      if (glength > dynprog->max_glength) glength = dynprog->max_glength;
+      orig_pairs = end3p ? __wrap_Dynprog_end3_gap(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels,
+                                                   dynprog, seq, sequc, rlength, glength, roffset, goffset, chroffset,
+                                                   chrhigh, watsonp, genestrand, jump_late_p, genome, genomealt,
+                                                   pairpool, extraband_end, defect_rate, BEST_LOCAL, false)
+                         : __wrap_Dynprog_end5_gap(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels,
+                                                   dynprog, seq, sequc, rlength, glength, roffset, goffset, chroffset,
+                                                   chrhigh, watsonp, genestrand, jump_late_p, genome, genomealt,
+                                                   pairpool, extraband_end, defect_rate, BEST_LOCAL, false);
+      *knownsplicep = false;
+      return orig_pairs;
+    }
+    /* an ambiguous splice: the straight alignment truncated before the ambiguous part */
+    *ambig_splicetype = anchor_splicetype;
+    if (!end3p) {
+      orig_pairs = List_reverse(orig_pairs);  /* querypos is decreasing */
+      while (orig_pairs != NULL && ((Pair_T) orig_pairs->first)->querypos < *ambig_end_length)
+        orig_pairs = Pairpool_pop(orig_pairs, &pair);
+      orig_pairs = List_reverse(orig_pairs);
+    } else {
+      while (orig_pairs != NULL && ((Pair_T) orig_pairs->first)->querypos >= querylength - *ambig_end_length)
+        orig_pairs = Pairpool_pop(orig_pairs, &pair);
+    }
+    *knownsplicep = false;
+    *finalscore = orig_score;
+    return orig_pairs;
+  }
+  *ambig_end_length = 0;
+  if (*knownsplicep == true) return end3p ? Pair_protect_end3(best_pairs) : Pair_protect_end5(best_pairs);
+  return best_pairs;
+}
+
+List_T
+__wrap_Dynprog_end5_known (bool *knownsplicep, int *dynprogindex, int *finalscore, int *ambig_end_length,
+                           Splicetype_T *ambig_splicetype, int *nmatches, int *nmismatches, int *nopens, int *nindels,
+                           Dynprog_T dynprog, char *revsequence1, char *revsequenceuc1, int length1, int length2,
+                           int revoffset1, int revoffset2, Univcoord_T chroffset, Univcoord_T chrhigh,
+                           Univcoord_T knownsplice_limit_low, Univcoord_T knownsplice_limit_high, int cdna_direction,
+                           bool watsonp, int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
+                           Pairpool_T pairpool, int extraband_end, double defect_rate) {
+  return shim_known(0, knownsplicep, dynprogindex, finalscore, ambig_end_length, ambig_splicetype, nmatches,
+                    nmismatches, nopens, nindels, dynprog, revsequence1, revsequenceuc1, length1, length2, revoffset1,
+                    revoffset2, /*querylength*/0, chroffset, chrhigh, knownsplice_limit_low, knownsplice_limit_high,
+                    cdna_direction, watsonp, genestrand, jump_late_p, genome, genomealt, pairpool, extraband_end,
+                    defect_rate);
+}
+
+List_T
+__wrap_Dynprog_end3_known (bool *knownsplicep, int *dynprogindex, int *finalscore, int *ambig_end_length,
+                           Splicetype_T *ambig_splicetype, int *nmatches, int *nmismatches, int *nopens, int *nindels,
+                           Dynprog_T dynprog, char *sequence1, char *sequenceuc1, int length1, int length2, int offset1,
+                           int offset2, int querylength, Univcoord_T chroffset, Univcoord_T chrhigh,
+                           Univcoord_T knownsplice_limit_low, Univcoord_T knownsplice_limit_high, int cdna_direction,
+                           bool watsonp, int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
+                           Pairpool_T pairpool, int extraband_end, double defect_rate) {
+  return shim_known(1, knownsplicep, dynprogindex, finalscore, ambig_end_length, ambig_splicetype, nmatches,
+                    nmismatches, nopens, nindels, dynprog, sequence1, sequenceuc1, length1, length2, offset1, offset2,
+                    querylength, chroffset, chrhigh, knownsplice_limit_low, knownsplice_limit_high, cdna_direction,
+                    watsonp, genestrand, jump_late_p, genome, genomealt, pairpool, extraband_end, defect_rate);
 }
 
 /* Maxent_hr_*_prob of one splice-site entry (the host's MaxEnt models, maxent_hr.c) */

@@ -111,10 +111,18 @@ endef
 
 $(foreach v,$(VARIANTS),$(eval $(call variant_rules,$(v))))
 
+# iit_store (src/Makefile.am IIT_STORE_FILES), the reference's own IIT writer: it builds the known
+# splice-site file of the `gmap -s` end-to-end test (tests/golden/make_e2e.py) from a text list.
+IIT_STORE_C := except.c assert.c mem.c intlist.c list.c littleendian.c bigendian.c univinterval.c interval.c \
+  uintlist.c stopwatch.c semaphore.c access.c doublelist.c iit-write-univ.c iit-write.c tableint.c table.c \
+  chrom.c bzip2.c getline.c getopt.c getopt1.c iit_store.c
+$(OUT)/iit_store: $(patsubst %.c,$(OUT)/nosimd/%.o,$(IIT_STORE_C))
+	$(CC) -pthread -o $@ $^ -lz -lm
+
 SHIM_SRC   := ../gmap-2024_amd/shim/gmapdp_gmap_shim.c
 GMAPDP_LIB := ../gmap-2024_amd/lib
 
-all: programs $(foreach v,$(VARIANTS),$(OUT)/librefdp_$(v).so) \
+all: programs $(OUT)/iit_store $(foreach v,$(VARIANTS),$(OUT)/librefdp_$(v).so) \
      $(if $(wildcard $(GMAPDP_LIB)/libgmapdp.so),$(OUT)/librefdp_gpushim.so $(OUT)/librefdp_gpushim_avx2.so)
 
 # The drop-in check: the same nosimd reference objects, with Dynprog_init / _*_setup /
@@ -123,7 +131,8 @@ all: programs $(foreach v,$(VARIANTS),$(OUT)/librefdp_$(v).so) \
 # build would) and libgmapdp.so.  Tests call it through the same refh_* entry points.
 WRAPPED    := Dynprog_init Dynprog_single_setup Dynprog_end_setup Dynprog_genome_setup \
               Dynprog_single_gap Dynprog_end5_gap Dynprog_end3_gap Dynprog_genome_gap Dynprog_cdna_gap \
-              Dynprog_microexon_int Oligoindex_hr_tally Oligoindex_get_mappings Stage2_setup Stage2_compute
+              Dynprog_microexon_int Oligoindex_hr_tally Oligoindex_get_mappings Stage2_setup Stage2_compute \
+              Dynprog_end5_splicejunction Dynprog_end3_splicejunction Dynprog_end5_known Dynprog_end3_known
 
 $(OUT)/gpushim/gmapdp_gmap_shim.o: $(SHIM_SRC) ../include/gmapdp.h
 	@mkdir -p $(dir $@)

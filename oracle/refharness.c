@@ -341,6 +341,55 @@ refh_end_splicejunction (int end3p, const char *qbuf, const char *qucbuf, int qp
   return flatten(pairs, out, max_pairs);
 }
 
+/* Dynprog_end5_known / Dynprog_end3_known (dynprog_end.c:2748/3009) over a known-site list given here
+   (Dynprog_end_setup with the sites and types, no splice tries: trieoffsets NULL, as gmap.c sets them
+   up when the tries are empty), then the list reset to none.  types: Splicetype_T values (types.h:130).
+   scalars[0..8] = dynprogindex(after), finalscore, ambig_end_length, ambig_splicetype, nmatches,
+   nmismatches, nopens, nindels, knownsplicep; unwritten ones stay INT_MIN. */
+int
+refh_end_known (int end3p, const unsigned int *sites, const int *types, int nsites, const char *qbuf,
+                const char *qucbuf, int qpos, int rlength, int glength, int roffset, int goffset, int querylength,
+                unsigned int chroffset, unsigned int chrhigh, unsigned int limit_low, unsigned int limit_high,
+                int cdna_direction, int watsonp, int genestrand, int jump_late_p, int extraband_end,
+                double defect_rate, int dynprogindex, int *scalars, RefPair *out, int max_pairs) {
+  List_T pairs;
+  Univcoord_T *usites = (Univcoord_T *) calloc(nsites + 1, sizeof(Univcoord_T));
+  Splicetype_T *utypes = (Splicetype_T *) calloc(nsites + 1, sizeof(Splicetype_T));
+  int score = -2147483647 - 1, ambig_end_length = score, nmatches = score, nmismatches = score, nopens = score;
+  int nindels = score, i;
+  Splicetype_T ambig_splicetype = (Splicetype_T) score;
+  bool knownsplicep = false;
+  char *rsequence = (char *) qbuf + qpos, *rsequenceuc = (char *) qucbuf + qpos;
+
+  for (i = 0; i < nsites; i++) {
+    usites[i] = (Univcoord_T) sites[i];
+    utypes[i] = (Splicetype_T) types[i];
+  }
+  Dynprog_end_setup(usites, utypes, /*splicedists*/NULL, nsites, NULL, NULL, NULL, NULL, 0, 0, false);
+  Pairpool_reset(pairpool);
+  if (end3p) {
+    pairs = Dynprog_end3_known(&knownsplicep, &dynprogindex, &score, &ambig_end_length, &ambig_splicetype, &nmatches,
+                               &nmismatches, &nopens, &nindels, dynprogR, rsequence, rsequenceuc, rlength, glength,
+                               roffset, goffset, querylength, chroffset, chrhigh, limit_low, limit_high,
+                               cdna_direction, watsonp ? true : false, genestrand, jump_late_p ? true : false,
+                               genome, genome, pairpool, extraband_end, defect_rate);
+  } else {
+    pairs = Dynprog_end5_known(&knownsplicep, &dynprogindex, &score, &ambig_end_length, &ambig_splicetype, &nmatches,
+                               &nmismatches, &nopens, &nindels, dynprogL, rsequence, rsequenceuc, rlength, glength,
+                               roffset, goffset, chroffset, chrhigh, limit_low, limit_high, cdna_direction,
+                               watsonp ? true : false, genestrand, jump_late_p ? true : false, genome, genome,
+                               pairpool, extraband_end, defect_rate);
+  }
+  Dynprog_end_setup(NULL, NULL, NULL, 0, NULL, NULL, NULL, NULL, 0, 0, false);
+  free(usites);
+  free(utypes);
+  scalars[0] = dynprogindex; scalars[1] = score; scalars[2] = ambig_end_length; scalars[3] = (int) ambig_splicetype;
+  scalars[4] = nmatches; scalars[5] = nmismatches; scalars[6] = nopens; scalars[7] = nindels;
+  scalars[8] = knownsplicep ? 1 : 0;
+  if (pairs == NULL) return -1;
+  return flatten(pairs, out, max_pairs);
+}
+
 /* Dynprog_genome_gap (dynprog_genome.c:3288).  flags: 1 watsonp, 2 jump_late_p,
    8 halfp, 16 finalp.  scalars[0..9] = dynprogindex(after), traceback_score,
    nmatches, nmismatches, nopens, nindels, new_leftgenomepos,

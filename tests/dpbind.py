@@ -964,3 +964,59 @@ def splicejunction_problem(rng, genome: bytes, edge=False):
                 jump_late_p=rng.randint(0, 1), extraband=rng.choice([3, 6, 10, 10, 10, 14]),
                 defect_rate=rng.choice([0.001, 0.005, 0.02, 0.05]), contlength=contlength,
                 dynprogindex=rng.choice([1, 5, -1, -7]))
+
+
+# ---------------------------------------------------------------------------
+# Dynprog_end5_known / Dynprog_end3_known (dynprog_end.c:2748/3009), reference harness only
+# ---------------------------------------------------------------------------
+_KNOWN_ARGS = [C.c_int, C.POINTER(C.c_uint), C.POINTER(C.c_int), C.c_int, C.c_char_p, C.c_char_p, C.c_int,
+               C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint, C.c_uint, C.c_uint, C.c_uint, C.c_int,
+               C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int, C.POINTER(C.c_int), C.POINTER(Pair),
+               C.c_int]
+SPLICETYPES = {"donor": 1, "antidonor": 2, "acceptor": 3, "antiacceptor": 4}  # types.h:130
+
+
+def _end_known(self, p):
+    """((dynprogindex, finalscore, ambig_end_length, ambig_splicetype, nmatches, nmismatches, nopens, nindels,
+    knownsplicep), pairs-or-None) of one Dynprog_end{5,3}_known call over p["sites"] / p["types"]."""
+    self._before_call()
+    f = self.lib.refh_end_known
+    f.argtypes = _KNOWN_ARGS
+    f.restype = C.c_int
+    scal = (C.c_int * 9)()
+    ns = len(p["sites"])
+    sites = (C.c_uint * max(1, ns))(*p["sites"])
+    types = (C.c_int * max(1, ns))(*p["types"])
+    qpos = 0 if p["end3p"] else len(p["q"]) - 1
+    n = f(p["end3p"], sites, types, ns, p["q"], p["quc"], qpos, p["rlength"], p["glength"], p["roffset"],
+          p["goffset"], p["querylength"], p["chroffset"], p["chrhigh"], p["limit_low"], p["limit_high"],
+          p["cdna_direction"], p["watsonp"], p["genestrand"], p["jump_late_p"], p["extraband"], p["defect_rate"],
+          p["dynprogindex"], scal, self._pairs, MAXPAIRS)
+    assert n <= MAXPAIRS
+    return tuple(scal), (None if n < 0 else [self._pairs[i].key() for i in range(n)])
+
+
+Ref.end_known = _end_known
+
+
+def end_known_problem(rng, genome: bytes):
+    """One Dynprog_end5/3_known call shaped as stage 3 makes it with -s (glength >= rlength, the read end
+    beyond the anchor) over a sorted list of known sites, some inside the end's genomic span with the
+    anchor type the call looks for."""
+    p = end_gap_problem(rng, genome)
+    p["glength"] = max(p["glength"], p["rlength"])  # dynprog_end.c:2773 asserts glength >= rlength
+    end3p = p["end3p"]
+    gl = len(genome)
+    p["querylength"] = p["roffset"] + p["rlength"] + rng.randint(0, 50)
+    p["cdna_direction"] = rng.choice([1, -1])
+    p["limit_low"], p["limit_high"] = p["chroffset"], p["chrhigh"]
+    # the end's genomic span in chromosome coordinates (either strand)
+    lo = p["goffset"] - p["rlength"] if not end3p else p["goffset"]
+    if not p["watsonp"]:
+        lo = p["chrhigh"] - p["chroffset"] - lo - p["rlength"]
+    lo += p["chroffset"]
+    sites = sorted(set(max(1, rng.randint(lo - 5, lo + p["rlength"] + 5)) for _ in range(rng.randint(0, 6))) |
+                   set(rng.randint(1, gl - 1) for _ in range(rng.randint(0, 6))))
+    p["sites"] = sites
+    p["types"] = [rng.choice([1, 2, 3, 4]) for _ in sites]
+    return p

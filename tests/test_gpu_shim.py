@@ -150,3 +150,36 @@ def test_shim_microexon_int(build):
     bad = [i for i, p in enumerate(probs) if shim.microexon_int(p) != exp[i]]
     assert bad == []
     assert sum(e[2] is not None for e in exp) > 100
+
+
+def test_shim_splicejunction(impls):
+    """Dynprog_end5/3_splicejunction through the drop-in: the Pair_T lists, the
+    known-splice gap holder (knowngapp) and every out-parameter, written or not, as the reference's."""
+    from dpbind import splicejunction_problem
+    ref, _, shim = impls
+    rng = random.Random(5353)
+    g = random_genome(rng, 120000)
+    ref.set_genome(g)
+    shim.set_genome(g)
+    bad = [i for i in range(800)
+           for p in [splicejunction_problem(rng, g, edge=(i % 5 == 0))]
+           if shim.end_splicejunction(p) != ref.end_splicejunction(p)]
+    assert bad == []
+
+
+def test_shim_end_known(impls):
+    """Dynprog_end5/3_known through the drop-in: the shim's restatement of the
+    known-site orchestration (the straight QUERYEND_NOGAPS end gap, the anchor-site scan, the BEST_LOCAL
+    fallback) on the engine, against the reference's own function, over sorted known-site lists
+    (no splice tries: the trie walk itself is the reference's Splicetrie_solve_end5/3, whose
+    splice-junction calls test_shim_splicejunction pins)."""
+    from dpbind import end_known_problem
+    ref, _, shim = impls
+    rng = random.Random(7171)
+    g = random_genome(rng, 60000)
+    ref.set_genome(g)
+    shim.set_genome(g)
+    bad = [i for i in range(600)
+           for p in [end_known_problem(rng, g)]
+           if shim.end_known(p) != ref.end_known(p)]
+    assert bad == []
