@@ -1092,7 +1092,11 @@ __device__ inline bool gg_simple_wave(int lane, const DevGenomeProblem& P, int p
                                const uint8_t* gclR, const GClassView& gchL, const GClassView& gchR,
                                const uint8_t* ldi, const uint8_t* rdi, const double* pL, const double* pR,
                                int* diagL, int* diagR, gmapdp_pair* out, gmapdp_genome_result& res,
-                               gmapdp_genome_result* __restrict__ results) {
+                               gmapdp_genome_result* __restrict__ results, const uint8_t* __restrict__ ks = nullptr,
+                               const double* __restrict__ raw = nullptr) {
+  // ks: genome_gap_simple's own known-site flags (left [0, rlength], right after them; nullptr: none),
+  // raw: the MaxEnt probabilities (left [0, glengthL), right after them) that get_splicesite_probs
+  // returns for an unknown site (dynprog_genome.c:3045-3049, 3118-3119, 3171)
   const int rlen = P.rlength;
   const int8_t* sct = sctab + (size_t)P.mismatchtype * 128 * kNClass;
   const int8_t* iscp = isctab + (size_t)P.iclass * 128;  // prelim array (:3032)
@@ -1122,8 +1126,9 @@ __device__ inline bool gg_simple_wave(int lane, const DevGenomeProblem& P, int p
   for (int rL = lane + 1; rL <= rlen - 1; rL += 64) {
     const int rR = rlen - rL;
     const int it = ldi[rL] & rdi[rR];
-    const int score = diagL[rL] + iscp[it] + diagR[rR];
-    if (it != 0 && score >= 0) {
+    const int kl = (ks && ks[rL]) ? kKnownReward : 0, kr = (ks && ks[rlen + 1 + rR]) ? kKnownReward : 0;
+    const int score = diagL[rL] + kl + iscp[it] + kr + diagR[rR];
+    if ((it != 0 || kl != 0 || kr != 0) && score >= 0) {
       const uint64_t kk = ((uint64_t)(uint32_t)score << 32) | (uint32_t)rL;
       key = kk > key ? kk : key;
     }
@@ -1136,8 +1141,13 @@ __device__ inline bool gg_simple_wave(int lane, const DevGenomeProblem& P, int p
   res.introntype = it;
   const int finalscore = halfp ? bestscore - scoreI / 2 : bestscore;
   if (finalscore <= 0) return false;
-  res.left_prob = pL[bestrL];
-  res.right_prob = pR[bestrR];
+  if (ks) {
+    res.left_prob = ks[bestrL] ? 1.0 : raw[bestrL];
+    res.right_prob = ks[rlen + 1 + bestrR] ? 1.0 : raw[P.glengthL + bestrR];
+  } else {
+    res.left_prob = pL[bestrL];
+    res.right_prob = pR[bestrR];
+  }
   if (!(res.left_prob >= 0.90 && res.right_prob >= 0.90)) return false;
   Tally t = {0, 0, 0, 0, 0, 0, 0, false};
   // list = reverse of the push order (no List_reverse): R diagonal r = 1..bestrR, gap, L r = bestrL..1

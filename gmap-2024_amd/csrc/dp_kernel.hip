@@ -690,7 +690,7 @@ __global__ __launch_bounds__(128) void gg_kernel(
     const char* __restrict__ qseq, const char* __restrict__ qseq_uc, const double* __restrict__ sprob,
     const int8_t* __restrict__ sctab, const uint8_t* __restrict__ constab, const int8_t* __restrict__ isctab,
     gmapdp_genome_result* __restrict__ results, gmapdp_pair* __restrict__ pairs,
-    unsigned char* __restrict__ gscratch) {
+    unsigned char* __restrict__ gscratch, const uint8_t* __restrict__ known) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -734,6 +734,8 @@ __global__ __launch_bounds__(128) void gg_kernel(
   const Geo GL{P.roffset, P.goffsetL, 1};
   const Geo GR{rev_roffset, P.rev_goffsetR, -1};
   const bool halfp = flags & kGHalf;
+  const bool kn = flags & kGKnown;  // known splice sites (get_known_splicesites, dynprog_genome.c:405)
+  const uint8_t* kb = kn ? known + P.known_offset : nullptr;
 
   // ---- stage (both waves): per query row the 4-bit score word in both DP orders, both genome
   //      segments as classes, dinucleotide codes, the splice probabilities, the intron scores ----
@@ -754,13 +756,14 @@ __global__ __launch_bounds__(128) void gg_kernel(
     const char c2 = segment_nt(blocks, nwords, (uint32_t)i, (uint32_t)gL, P.segposL, P.segboundL,
                                flags & kGSegLLeft, flags & kGSegLRc);
     gclL[i + 1] = gclass(c2);
-    pL[i] = sprob[P.prob_offset + i];
+    // a known site has probability 1.0 in the bridge (dynprog_genome.c:2577-2578)
+    pL[i] = (kn && kb[i]) ? 1.0 : sprob[P.prob_offset + i];
   }
   for (int i = tid; i < gR; i += 128) {
     const char c2 = segment_nt(blocks, nwords, (uint32_t)i, (uint32_t)gR, P.segposR, P.segboundR,
                                flags & kGSegRLeft, flags & kGSegRRc);
     gclR[gR - i] = gclass(c2);  // rev_gsequenceR[1-c] = segment[glengthR-c]
-    pR[i] = sprob[P.prob_offset + gL + i];
+    pR[i] = (kn && kb[gL + i]) ? 1.0 : sprob[P.prob_offset + gL + i];
   }
   if (tid < 64) isc[tid] = isctab[(size_t)P.iclass * 128 + ((flags & kGFinal) ? 64 : 0) + tid];
   if (tid == 0) *done = 0;
@@ -788,7 +791,8 @@ __global__ __launch_bounds__(128) void gg_kernel(
   if (flags & kGSimple) {
     if (wave == 0) {
       const bool ok = gg_simple_wave(lane, P, pid, sctab, isctab, cons, qL, qucL, qR, qucR, gclL, gclR, gchL, gchR,
-                                     ldi, rdi, pL, pR, diagL, diagR, out, res, results);
+                                     ldi, rdi, pL, pR, diagL, diagR, out, res, results,
+                                     kn ? kb + gL + gR : nullptr, sprob + P.prob_offset);
       if (lane == 0) *done = ok ? 1 : 0;
     }
     __syncthreads();
@@ -1079,7 +1083,7 @@ hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
                      const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
                      const char* qseq_uc, const double* sprob, const int8_t* sctab, const uint8_t* constab,
                      const int8_t* isctab, gmapdp_genome_result* results, gmapdp_pair* pairs,
-                     unsigned char* gscratch) {
+                     unsigned char* gscratch, const uint8_t* known) {
   void* fn = nullptr;
 #define GMAPDP_CASE(RR)                                          \
   case RR:                                                       \
@@ -1102,7 +1106,7 @@ hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
   }
   void* args[] = {(void*)&probs, (void*)&order, (void*)&blocks, (void*)&nwords, (void*)&qseq, (void*)&qseq_uc,
                   (void*)&sprob, (void*)&sctab, (void*)&constab, (void*)&isctab, (void*)&results, (void*)&pairs,
-                  (void*)&gscratch};
+                  (void*)&gscratch, (void*)&known};
   return hipLaunchKernel(fn, dim3(nblocks), dim3(128), args, lds, stream);
 }
 

@@ -48,7 +48,7 @@ hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
                      const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
                      const char* qseq_uc, const double* sprob, const int8_t* sctab, const uint8_t* constab,
                      const int8_t* isctab, gmapdp_genome_result* results, gmapdp_pair* pairs,
-                     unsigned char* gscratch);
+                     unsigned char* gscratch, const uint8_t* known);
 size_t lds_bytes_sj(int rlength, int glength, int R, bool dirs_lds);
 hipError_t launch_sj(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevSjProblem* probs,
                      const int* order, const char* qseq, const char* qseq_uc, const char* jseq, const int8_t* sctab,
@@ -862,6 +862,18 @@ static int convert_genome(gmapdp_ctx* ctx, const gmapdp_genome_problem& p, gmapd
             ((p.flags & GMAPDP_HALFP) ? kGHalf : 0) | ((p.flags & GMAPDP_FINALP) ? kGFinal : 0);
   if (!(p.flags & GMAPDP_FINALP) && dr < 0.014) d.flags |= kGSimple;  // :3479
   if (p.flags & GMAPDP_SIMD) d.flags |= kGSimd;
+  if (p.flags & GMAPDP_KNOWN_SITES) {
+    if (p.flags & GMAPDP_SIMD) {
+      *err = bad(ctx, "known splice sites are built in nosimd semantics only");
+      return 0;
+    }
+    if (p.known_offset < 0) {
+      *err = bad(ctx, "negative known_offset");
+      return 0;
+    }
+    d.flags |= kGKnown;
+    d.known_offset = p.known_offset;
+  }
   if (watson) {
     d.segposL = p.chroffset + (uint64_t)(int64_t)p.goffsetL;  // Genome_get_segment_right(left, chrhigh)
     d.segboundL = p.chrhigh;
@@ -1158,6 +1170,7 @@ struct RunArgs {
   gmapdp_result* d_results;
   gmapdp_genome_result* d_gresults;
   gmapdp_pair* d_pairs;
+  const uint8_t* d_known = nullptr;  // known-site arena (GMAPDP_KNOWN_SITES genome gaps)
 };
 
 static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, const RunArgs& a, hipStream_t stream) {
@@ -1189,7 +1202,7 @@ static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, cons
   if (!a.d_gresults || !a.d_sprob) return hipErrorInvalidValue;
   return launch_gg(L.R, L.dirs_lds, L.count, L.lds, stream, a.d_gprobs, a.d_gorder + L.first, ctx->d_genome,
                    ctx->genome_words, a.d_q, a.d_quc, a.d_sprob, ctx->d_sc, ctx->d_cs, ctx->d_isc, a.d_gresults,
-                   a.d_pairs, (unsigned char*)ctx->gdirs.p);
+                   a.d_pairs, (unsigned char*)ctx->gdirs.p, a.d_known);
 }
 
 static int run_plan(gmapdp_ctx* ctx, const PlanCore& plan, const RunArgs& a, hipStream_t stream) {
@@ -1228,7 +1241,7 @@ static int run_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int 
                      const gmapdp_end_problem* ends, int nend, const gmapdp_genome_problem* genomes, int ngenome,
                      const char* qseq, const char* qseq_uc, size_t qbytes, const double* sprob, size_t nsprob,
                      gmapdp_result* results, gmapdp_genome_result* gresults, gmapdp_pair* pairs,
-                     size_t pair_capacity) {
+                     size_t pair_capacity, const uint8_t* known = nullptr, size_t nknown = 0) {
   const int n = nsingle + nend;
   if (!ctx || n < 0 || ngenome < 0 || (n && !results) || (ngenome && !gresults)) return GMAPDP_EINVAL;
   if (!ctx->d_genome) return GMAPDP_ENOGENOME;
@@ -1250,9 +1263,13 @@ static int run_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int 
       return bad(ctx, "query slice outside the query arena");
     if (!sprob || g.prob_offset < 0 || (size_t)g.prob_offset + (size_t)g.glengthL + (size_t)g.glengthR > nsprob)
       return bad(ctx, "splice probabilities outside the probability arena");
+    if ((g.flags & GMAPDP_KNOWN_SITES) &&
+        (!known || (size_t)g.known_offset + gmapdp_genome_known_bytes(&g) > nknown))
+      return bad(ctx, "known-site flags outside the known-site arena");
   }
   const int ndev = (int)plan.dev.size(), ngdev = (int)plan.gdev.size();
   if (ndev + ngdev == 0) return GMAPDP_OK;
+  const size_t nkn = (ngdev && known) ? nknown : 0;
   // one pinned image of every input and one of every output: a single copy each way
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t o_probs = 0;
@@ -1262,7 +1279,8 @@ static int run_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int 
   const size_t o_sprob = o_gorder + al(sizeof(int) * ngdev);
   const size_t o_q = o_sprob + al(ngdev ? sizeof(double) * nsprob : 0);
   const size_t o_quc = o_q + al(qbytes);
-  const size_t in_bytes = o_quc + al(qbytes);
+  const size_t o_known = o_quc + al(qbytes);
+  const size_t in_bytes = o_known + al(nkn);
   const size_t r_res = 0;
   const size_t r_gres = r_res + al(sizeof(gmapdp_result) * ndev);
   const size_t r_pairs = r_gres + al(sizeof(gmapdp_genome_result) * ngdev);
@@ -1284,6 +1302,7 @@ static int run_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int 
     std::memcpy(hin + o_gprobs, plan.gdev.data(), sizeof(DevGenomeProblem) * ngdev);
     std::memcpy(hin + o_gorder, plan.gorder.data(), sizeof(int) * ngdev);
     std::memcpy(hin + o_sprob, sprob, sizeof(double) * nsprob);
+    if (nkn) std::memcpy(hin + o_known, known, nkn);
   }
   std::memcpy(hin + o_q, qseq, qbytes);
   std::memcpy(hin + o_quc, qseq_uc, qbytes);
@@ -1301,6 +1320,7 @@ static int run_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int 
   a.d_results = (gmapdp_result*)(dout + r_res);
   a.d_gresults = (gmapdp_genome_result*)(dout + r_gres);
   a.d_pairs = (gmapdp_pair*)(dout + r_pairs);
+  a.d_known = nkn ? (const uint8_t*)(din + o_known) : nullptr;
   rc = run_plan(ctx, plan, a, s);
   if (rc) return rc;
   e = hipMemcpyAsync(hout, dout, out_bytes, hipMemcpyDeviceToHost, s);
@@ -1419,6 +1439,19 @@ int gmapdp_genome_gap_batch(gmapdp_ctx* ctx, const gmapdp_genome_problem* proble
   if (n > 0 && !problems) return GMAPDP_EINVAL;
   return run_batch(ctx, nullptr, 0, nullptr, 0, problems, n, qseq, qseq_uc, qbytes, splice_probs, nprobs, nullptr,
                    results, pairs, pair_capacity);
+}
+
+int gmapdp_genome_gap_batch_known(gmapdp_ctx* ctx, const gmapdp_genome_problem* problems, int n, const char* qseq,
+                                  const char* qseq_uc, size_t qbytes, const double* splice_probs, size_t nprobs,
+                                  const uint8_t* known_sites, size_t nknown, gmapdp_genome_result* results,
+                                  gmapdp_pair* pairs, size_t pair_capacity) {
+  if (n > 0 && !problems) return GMAPDP_EINVAL;
+  return run_batch(ctx, nullptr, 0, nullptr, 0, problems, n, qseq, qseq_uc, qbytes, splice_probs, nprobs, nullptr,
+                   results, pairs, pair_capacity, known_sites, nknown);
+}
+
+size_t gmapdp_genome_known_bytes(const gmapdp_genome_problem* p) {
+  return (size_t)std::max(p->glengthL, 0) + (size_t)std::max(p->glengthR, 0) + 2 * (size_t)(std::max(p->rlength, 0) + 1);
 }
 
 int gmapdp_dynprog_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int nsingle,
@@ -1849,6 +1882,11 @@ int gmapdp_plan_create_all(gmapdp_ctx* ctx, const gmapdp_single_problem* singles
     delete p;
     return rc;
   }
+  for (const DevGenomeProblem& g : p->in.gdev)
+    if (g.flags & kGKnown) {  // the plan binds no known-site arena
+      delete p;
+      return bad(ctx, "GMAPDP_KNOWN_SITES genome gaps go through the synchronous batches, not plans");
+    }
   const size_t nd = p->in.dev.size(), ng = p->in.gdev.size();
   hipError_t e = hipMalloc(&p->d_probs, sizeof(DevProblem) * std::max<size_t>(nd, 1));
   if (e == hipSuccess) e = hipMalloc(&p->d_order, sizeof(int) * std::max<size_t>(nd, 1));
@@ -2562,6 +2600,9 @@ extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char*
       if (!m->splice_probs || g.prob_offset < 0 ||
           (size_t)g.prob_offset + (size_t)g.glengthL + (size_t)g.glengthR > m->nprobs)
         return bad(ctx, "splice probabilities outside the probability arena");
+      if ((g.flags & GMAPDP_KNOWN_SITES) &&
+          (!m->known_sites || (size_t)g.known_offset + gmapdp_genome_known_bytes(&g) > m->nknown))
+        return bad(ctx, "known-site flags outside the known-site arena");
     }
   }
   const int ndev = (int)plan.dev.size(), ngdev = (int)plan.gdev.size();
@@ -2597,6 +2638,8 @@ extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char*
   const size_t o_gorder = o;  o += al(sizeof(int) * ngdev);
   const size_t nsp = ngdev ? m->nprobs : 0;
   const size_t o_sprob = o;   o += al(sizeof(double) * nsp);
+  const size_t nkn = (ngdev && m->known_sites) ? m->nknown : 0;
+  const size_t o_known = o;   o += al(nkn);
   const size_t o_q = o;       o += al(qbytes);
   const size_t o_quc = o;     o += al(qbytes);
   const size_t o_xs = o;      o += al(sizeof(gmapdp_microexon_problem) * nxs);
@@ -2626,6 +2669,7 @@ extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char*
     std::memcpy(h + o_gprobs, plan.gdev.data(), sizeof(DevGenomeProblem) * ngdev);
     std::memcpy(h + o_gorder, plan.gorder.data(), sizeof(int) * ngdev);
     std::memcpy(h + o_sprob, m->splice_probs, sizeof(double) * nsp);
+    if (nkn) std::memcpy(h + o_known, m->known_sites, nkn);
   }
   std::memcpy(h + o_q, qseq, qbytes);
   std::memcpy(h + o_quc, qseq_uc, qbytes);
@@ -2651,6 +2695,7 @@ extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char*
     a.d_q = (const char*)(d + o_q);
     a.d_quc = (const char*)(d + o_quc);
     a.d_sprob = (const double*)(d + o_sprob);
+    a.d_known = nkn ? (const uint8_t*)(d + o_known) : nullptr;
     a.d_results = (gmapdp_result*)(d + r_res);
     a.d_gresults = (gmapdp_genome_result*)(d + r_gres);
     a.d_pairs = (gmapdp_pair*)(d + r_pairs);

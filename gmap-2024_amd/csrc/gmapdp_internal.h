@@ -65,6 +65,8 @@ constexpr int32_t kGSegLRc = 0x1000;
 constexpr int32_t kGSegRLeft = 0x2000;  // rev_gsequenceR via Genome_get_segment_left (plus strand)
 constexpr int32_t kGSegRRc = 0x4000;
 constexpr int32_t kGSimd = 0x8000;      // SIMD-build semantics (triangle fills, uxg_kernel)
+constexpr int32_t kGKnown = 0x10000;    // known splice sites: flags at known_offset (GMAPDP_KNOWN_SITES)
+constexpr int kKnownReward = 20;        // KNOWN_SPLICESITE_REWARD (dynprog_genome.c:118)
 constexpr int32_t kUnset = (int32_t)0x80000000;  // out-parameter the reference leaves unwritten
 
 // Dynprog_genome_gap descriptor (dynprog_genome.c:3288): two fills share the
@@ -92,7 +94,7 @@ struct DevGenomeProblem {
   int32_t genestrand;
   int32_t dynprogindex;
   int32_t pair_offset;
-  int32_t pad_;
+  int32_t known_offset;   // kGKnown: bridge flags at [known_offset, +glengthL+glengthR), simple's follow
   int64_t prob_offset;    // left probabilities at [prob_offset, +glengthL), right ones follow
   int64_t dirs_offset;    // byte offset into the global scratch (global-dirs classes)
   int64_t reserved_;      // keeps the descriptor at 128 B

@@ -55,7 +55,7 @@ class GenomeProblem(C.Structure):
                 ("roffset", C.c_int32), ("goffsetL", C.c_int32), ("rev_goffsetR", C.c_int32),
                 ("chroffset", C.c_uint64), ("chrhigh", C.c_uint64), ("flags", C.c_int32),
                 ("cdna_direction", C.c_int32), ("genestrand", C.c_int32), ("extraband", C.c_int32),
-                ("maxpeelback", C.c_int32), ("dynprogindex", C.c_int32), ("pad_", C.c_int32),
+                ("maxpeelback", C.c_int32), ("dynprogindex", C.c_int32), ("known_offset", C.c_int32),
                 ("defect_rate", C.c_double), ("prob_offset", C.c_int64)]
 
 
@@ -170,7 +170,8 @@ class Mixed(C.Structure):
                 ("search_results", C.c_void_p), ("candidates", C.c_void_p), ("candidate_capacity", C.c_size_t),
                 ("candidates_needed", C.c_size_t), ("finishes", C.c_void_p), ("nfinish", C.c_int),
                 ("finish_candidates", C.c_void_p), ("finish_probs", C.c_void_p), ("nfinish_candidates", C.c_size_t),
-                ("finish_results", C.c_void_p), ("finish_pairs", C.c_void_p), ("finish_pair_capacity", C.c_size_t)]
+                ("finish_results", C.c_void_p), ("finish_pairs", C.c_void_p), ("finish_pair_capacity", C.c_size_t),
+                ("known_sites", C.c_void_p), ("nknown", C.c_size_t)]
 
 
 _lib = None
@@ -229,6 +230,10 @@ def load_library(path=LIB_PATH):
                                               C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
                                               C.c_size_t]),
         "gmapdp_genome_pair_capacity": (C.c_size_t, [C.c_void_p, C.c_int]),
+        "gmapdp_genome_gap_batch_known": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                                    C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                                    C.c_void_p, C.c_void_p, C.c_size_t]),
+        "gmapdp_genome_known_bytes": (C.c_size_t, [C.c_void_p]),
         "gmapdp_dynprog_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
                                            C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p,
                                            C.c_void_p, C.c_void_p, C.c_size_t]),

@@ -70,6 +70,7 @@
 #include "stopwatch.h"
 #include "stage2.h"
 #include "splicetrie.h"
+#include "iit-read.h"
 #include "complement.h"
 #include "mem.h"
 
@@ -210,13 +211,73 @@ __wrap_Dynprog_end_setup (Univcoord_T *splicesites_in, Splicetype_T *splicetypes
                            user_extend_in, user_dynprog_p_in);
 }
 
+/* The splicing IIT of -s as Dynprog_genome_setup records it (dynprog_genome.c:192-214): the genome
+   gaps look their window's known sites up in it (get_known_splicesites, :405, restated below). */
+static IIT_T shim_siit = NULL;
+static int *shim_siit_cross = NULL;
+static int shim_donor_typeint = -1, shim_acceptor_typeint = -1;
+
 void
 __wrap_Dynprog_genome_setup (bool novelsplicingp_in, IIT_T splicing_iit_in, int *splicing_divint_crosstable_in,
                              int donor_typeint_in, int acceptor_typeint_in, int user_open_in, int user_extend_in,
                              bool user_dynprog_p_in) {
+  if (splicing_iit_in != NULL) {
+#ifdef HAVE_SSE2
+    shim_refuse("a splicing IIT (-s) in a SIMD build (known splice sites are built in nosimd semantics only)");
+#endif
+    /* an introns file (no donor/acceptor types: intron-level bridging, dynprog_genome.c:2944) and
+       known-only splicing (novel splicing off: genome_gap_simple then requires known sites, :3157) are
+       not built */
+    if (donor_typeint_in < 0 || acceptor_typeint_in < 0)
+      shim_refuse("a known-introns file (-s without donor/acceptor tags: intron-level bridging)");
+    if (!novelsplicingp_in) shim_refuse("known splice sites with novel splicing off");
+  }
   __real_Dynprog_genome_setup(novelsplicingp_in, splicing_iit_in, splicing_divint_crosstable_in, donor_typeint_in,
                               acceptor_typeint_in, user_open_in, user_extend_in, user_dynprog_p_in);
   shim_splicing_iit = splicing_iit_in != NULL;
+  shim_siit = splicing_iit_in;
+  shim_siit_cross = splicing_divint_crosstable_in;
+  shim_donor_typeint = donor_typeint_in;
+  shim_acceptor_typeint = acceptor_typeint_in;
+}
+
+/* get_known_splicesites (dynprog_genome.c:405-510), splice-site level: flags (1 = known) at the
+   positions of left_known[0, glengthL] / right_known[0, glengthR] that the reference sets to
+   KNOWN_SPLICESITE_REWARD.  The same IIT queries over the same (Chrpos_T) ranges. */
+static void
+shim_mark_sites (uint8_t *known, int index_sign, int index_base, Chrpos_T x, Chrpos_T y, int typeint, int sign,
+                 Chrnum_T chrnum) {
+  int *matches, nmatches, i;
+  matches = IIT_get_typed_signed_with_divno(&nmatches, shim_siit, shim_siit_cross[chrnum], x, y, typeint, sign,
+                                            /*sortp*/false);
+  for (i = 0; i < nmatches; i++) {
+    const int pos = (int) IIT_interval_low(shim_siit, matches[i]);
+    known[index_sign > 0 ? pos - index_base : index_base - pos] = 1;
+  }
+  FREE(matches);
+}
+
+static void
+shim_known_sites (uint8_t *left_known, uint8_t *right_known, int glengthL, int glengthR, int leftoffset,
+                  int rightoffset, int cdna_direction, bool watsonp, Chrnum_T chrnum, Univcoord_T chroffset,
+                  Univcoord_T chrhigh) {
+  const int span = (int) (chrhigh - chroffset);
+  const int ldonor = cdna_direction > 0 ? shim_donor_typeint : shim_acceptor_typeint;
+  const int racceptor = cdna_direction > 0 ? shim_acceptor_typeint : shim_donor_typeint;
+  if (watsonp) {
+    const int sign = cdna_direction > 0 ? +1 : -1;
+    /* left: splicesitepos = leftoffset + cL; right: splicesitepos = rightoffset - cR + 1 */
+    shim_mark_sites(left_known, +1, leftoffset, leftoffset + 1, leftoffset + glengthL - 2, ldonor, sign, chrnum);
+    shim_mark_sites(right_known, -1, rightoffset + 1, rightoffset - glengthR + 4, rightoffset + 1, racceptor, sign,
+                    chrnum);
+  } else {
+    const int sign = cdna_direction > 0 ? -1 : +1;
+    /* left: splicesitepos = span - leftoffset - cL + 1; right: splicesitepos = span - rightoffset + cR */
+    shim_mark_sites(left_known, -1, span - leftoffset + 1, span - leftoffset - glengthL + 4, span - leftoffset + 1,
+                    ldonor, sign, chrnum);
+    shim_mark_sites(right_known, +1, span - rightoffset, span - rightoffset + 1, span - rightoffset + glengthR - 2,
+                    racceptor, sign, chrnum);
+  }
 }
 
 /* Refusals that depend on the caller's Dynprog_T / genomes (checked on the calling thread). */
@@ -318,6 +379,8 @@ typedef struct shim_req {
   size_t qlen;
   const char *j;                /* splice-junction end gaps: the junction string (borrowed) */
   size_t jlen;
+  uint8_t *known;               /* genome gaps with known splice sites: the flags (gmapdp_genome_known_bytes) */
+  size_t nknown, knowncap;
   const double *probs;          /* genome gaps: the splice probabilities */
   size_t nprobs;
   /* outputs, filled by the dispatcher (pair_offset / table_offset / diag_offset rebased to 0) */
@@ -401,6 +464,7 @@ shim_request (int kind) {
   r->nprobs = 0;
   r->j = NULL;
   r->jlen = 0;
+  r->nknown = 0;
   memset(&r->p, 0, sizeof(r->p));
   return r;
 }
@@ -510,6 +574,8 @@ typedef struct {
   gmapdp_sj_result *sjres;
   char *jq;
   size_t sjcap, sjrescap, jqcap;
+  uint8_t *kn;
+  size_t kncap;
   shim_req **rs, **re, **rg, **rc, **ro, **r2, **rxs, **rxf, **rsj;
   size_t scap, ecap, gcap, ccap, ocap, s2cap, rscap, recap, rgcap, rccap, rocap, r2cap, rxscap, rxfcap, rsjcap;
   gmapdp_microexon_problem *mx, *mxf;        /* searches, finishes */
@@ -592,10 +658,14 @@ shim_run (shim_req *batch) {
     GROW(D.mxfres, D.mxfrescap, nxf + 1);
     for (i = 0; i < ns; i++) qb += D.rs[i]->qlen;
     for (i = 0; i < ne; i++) qb += D.re[i]->qlen;
+    size_t kb = 0;
     for (i = 0; i < ng; i++) {
       qb += D.rg[i]->qlen;
       pb += D.rg[i]->nprobs;
+      kb += D.rg[i]->nknown;
     }
+    GROW(D.kn, D.kncap, kb + 1);
+    kb = 0;
     for (i = 0; i < nxs; i++) qb += D.rxs[i]->qlen;
     for (i = 0; i < nxf; i++) {
       qb += D.rxf[i]->qlen;
@@ -631,6 +701,11 @@ shim_run (shim_req *batch) {
       D.g[i].prob_offset = (int64_t) pb;
       if (D.rg[i]->nprobs) memcpy(D.pr + pb, D.rg[i]->probs, D.rg[i]->nprobs * sizeof(double));
       pb += D.rg[i]->nprobs;
+      if (D.rg[i]->nknown) {
+        D.g[i].known_offset = (int32_t) kb;
+        memcpy(D.kn + kb, D.rg[i]->known, D.rg[i]->nknown);
+        kb += D.rg[i]->nknown;
+      }
     }
     for (i = 0; i < nxs; i++) {
       D.mx[i] = D.rxs[i]->p.mx;
@@ -683,6 +758,8 @@ shim_run (shim_req *batch) {
     M.finish_pair_capacity = xcap;
     M.candidates = D.mxsc;
     M.candidate_capacity = D.mxsccap;
+    M.known_sites = kb ? D.kn : NULL;
+    M.nknown = kb;
     rc = gmapdp_mixed_batch(shim_ctx, D.q, D.quc, qb, &M);
     while (rc == GMAPDP_ESPACE) {  /* (rare) the searches found more candidates than D.mxsc holds */
       size_t need = M.candidates_needed;
@@ -1436,8 +1513,6 @@ __wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_r
   static __thread uint8_t *model = NULL;
   static __thread size_t poscap = 0, modelcap = 0;
   List_T list;
-  (void) chrnum;
-  if (shim_splicing_iit) shim_refuse("known splice sites (a splicing IIT) in Dynprog_genome_gap");
   shim_check_call(genome, genomealt, dynprogL);
   shim_check_call(genome, genomealt, dynprogR);
   r = shim_request(K_GENOME);
@@ -1476,6 +1551,20 @@ __wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_r
     for (i = 0; i < m; i++)
       if (i != (size_t) glengthL - 1 && i != m - 1)
         r->pbuf[i] = shim_maxent(genome, genomealt, model[i], pos[i], chroffset);
+    if (shim_siit != NULL) {
+      /* known splice sites: the bridge's flags over the two windows and genome_gap_simple's over
+         rlength (dynprog_genome.c:2938-2942, 3045-3049); the probabilities stay MaxEnt's */
+      const size_t nk = gmapdp_genome_known_bytes(p);
+      GROW(r->known, r->knowncap, nk);
+      memset(r->known, 0, nk);
+      shim_known_sites(r->known, r->known + glengthL, glengthL, glengthR, goffsetL, rev_goffsetR, cdna_direction,
+                       watsonp, chrnum, chroffset, chrhigh);
+      shim_known_sites(r->known + glengthL + glengthR, r->known + glengthL + glengthR + rlength + 1, rlength, rlength,
+                       goffsetL, rev_goffsetR, cdna_direction, watsonp, chrnum, chroffset, chrhigh);
+      p->flags |= GMAPDP_KNOWN_SITES;
+      p->known_offset = 0;
+      r->nknown = nk;
+    }
   }
   r->genome = genome;
   r->q = rsequence;

@@ -177,6 +177,16 @@ typedef struct {
 /* Dynprog_genome_gap flags (in addition to GMAPDP_WATSON / GMAPDP_JUMP_LATE) */
 #define GMAPDP_HALFP   0x8
 #define GMAPDP_FINALP  0x10
+/* Known splice sites (gmap -s with a splice-site file: Dynprog_genome_setup with a splicing IIT and
+ * donor/acceptor types, novel splicing on; get_known_splicesites, dynprog_genome.c:405).  The problem's
+ * flags per position are in the batch's known-site arena at known_offset (one byte each, 0 or 1):
+ *   [0, glengthL)                        the bridge's left_known (dynprog_genome.c:2938-2942)
+ *   [glengthL, glengthL + glengthR)      its right_known
+ *   then rlength + 1 bytes, then rlength + 1 bytes: genome_gap_simple's left_known / right_known
+ *   (:3045-3049, queried with glength = rlength)
+ * A known position scores KNOWN_SPLICESITE_REWARD in genome_gap_simple and has probability 1.0; the
+ * probability arena then holds the MaxEnt values at every position (known or not).  Nosimd only. */
+#define GMAPDP_KNOWN_SITES 0x80
 
 /* One Dynprog_genome_gap call (dynprog_genome.c:3288 argument list).  The
  * query slice is qseq[qoff .. qoff+rlength) (rsequence / rsequenceuc).
@@ -210,7 +220,7 @@ typedef struct {
   int32_t extraband;      /* extraband_paired (+ peeled indels, stage3.c:9538) */
   int32_t maxpeelback;
   int32_t dynprogindex;
-  int32_t pad_;
+  int32_t known_offset;   /* with GMAPDP_KNOWN_SITES: the problem's first byte in the known-site arena */
   double defect_rate;
   int64_t prob_offset;
 } gmapdp_genome_problem;
@@ -262,6 +272,14 @@ int gmapdp_genome_gap_batch (gmapdp_ctx *ctx, const gmapdp_genome_problem *probl
                              const char *qseq, const char *qseq_uc, size_t qbytes,
                              const double *splice_probs, size_t nprobs,
                              gmapdp_genome_result *results, gmapdp_pair *pairs, size_t pair_capacity);
+/* The same with the known-site arena (nknown bytes) of GMAPDP_KNOWN_SITES problems. */
+int gmapdp_genome_gap_batch_known (gmapdp_ctx *ctx, const gmapdp_genome_problem *problems, int n,
+                                   const char *qseq, const char *qseq_uc, size_t qbytes,
+                                   const double *splice_probs, size_t nprobs, const uint8_t *known_sites,
+                                   size_t nknown, gmapdp_genome_result *results, gmapdp_pair *pairs,
+                                   size_t pair_capacity);
+/* Bytes of the problem's region of the known-site arena: glengthL + glengthR + 2 * (rlength + 1). */
+size_t gmapdp_genome_known_bytes (const gmapdp_genome_problem *problem);
 size_t gmapdp_genome_pair_capacity (const gmapdp_genome_problem *problems, int n);
 
 /* Dynprog_single_gap + Dynprog_end5/3_gap + Dynprog_genome_gap calls of many callers in one
@@ -452,6 +470,7 @@ typedef struct {
   const gmapdp_microexon_candidate *finish_candidates; const double *finish_probs; size_t nfinish_candidates;
   gmapdp_microexon_result *finish_results;   /* in: the searches' results; out: the choices */
   gmapdp_pair *finish_pairs; size_t finish_pair_capacity;
+  const uint8_t *known_sites; size_t nknown; /* GMAPDP_KNOWN_SITES genome gaps' arena (else NULL, 0) */
 } gmapdp_mixed;
 int gmapdp_mixed_batch (gmapdp_ctx *ctx, const char *qseq, const char *qseq_uc, size_t qbytes, gmapdp_mixed *m);
 

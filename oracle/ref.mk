@@ -119,6 +119,25 @@ IIT_STORE_C := except.c assert.c mem.c intlist.c list.c littleendian.c bigendian
 $(OUT)/iit_store: $(patsubst %.c,$(OUT)/nosimd/%.o,$(IIT_STORE_C))
 	$(CC) -pthread -o $@ $^ -lz -lm
 
+# gmapindex (src/Makefile.am GMAPINDEX_FILES, built with -DUTILITYP=1 as gmapindex_CFLAGS says) and
+# the reference's gmap_build / fa_coords / gmap_process perl scripts (util/) make the small indexed
+# genome of the `gmap -d` / `gmap -d -s` end-to-end fixtures (tests/golden/make_index.py).
+FLAGS_util := -DUTILITYP=1
+$(eval $(call variant_rules,util))
+GMAPINDEX_C := except.c assert.c mem.c intlist.c list.c littleendian.c bigendian.c univinterval.c interval.c \
+  uintlist.c stopwatch.c semaphore.c access.c filestring.c iit-read-univ.c iit-write-univ.c iit-read.c md5.c \
+  bzip2.c fopen.c sequence.c genome.c genomicpos.c compress-write.c genome-write.c compress.c popcount.c \
+  bitpack64-read.c bitpack64-readtwo.c bitpack64-access.c bitpack64-incr.c bitpack64-write.c indexdb.c \
+  indexdb-write.c saca-k.c localdb-write.c table.c tableuint.c tableuint8.c tableint.c bytecoding.c \
+  sarray-write.c chrom.c segmentpos.c uint8list.c parserange.c getline.c gmapindex.c
+$(OUT)/bin/gmapindex: $(patsubst %.c,$(OUT)/util/%.o,$(GMAPINDEX_C))
+	@mkdir -p $(dir $@)
+	$(CC) -pthread -o $@ $^ -lz -lm
+$(OUT)/bin/iit_store: $(OUT)/iit_store
+	@mkdir -p $(dir $@)
+	cp $< $@
+index_tools: $(OUT)/bin/gmapindex $(OUT)/bin/iit_store
+
 SHIM_SRC   := ../gmap-2024_amd/shim/gmapdp_gmap_shim.c
 GMAPDP_LIB := ../gmap-2024_amd/lib
 

@@ -190,3 +190,65 @@ def test_gpu_gmapl_end_to_end():
     st = _stats(err)
     for k in ("Dynprog_single_gap", "Dynprog_genome_gap", "Stage2_compute", "Dynprog_microexon_int"):
         assert st[k] > 0, st
+
+
+# ---- indexed genome (-d: stage 1, two chromosomes) and known splice sites (-s) ----
+# tests/golden/idx (make_index.py): a two-chromosome index built by the reference's gmap_build /
+# gmapindex, 160 reads (120 with 10-30-nt terminal exons), the known sites as the reference program
+# reports them for the full-length transcripts (iit_store), and the reference program's SAM.
+IDX_ARGS = ["-D", "idx/db", "-d", "e2eidx", "-f", "samse", "--no-sam-headers", "idx/sj_reads.fa"]
+SITES_ARGS = ["-s", "idx/db/e2eidx/e2eidx.maps/e2esites.iit"] + IDX_ARGS
+
+
+def test_reference_gmap_indexed_reproduces_fixtures():
+    exe = _exe("gmap_nosimd")
+    assert _run(exe, IDX_ARGS)[0] == _read("idx/d_nosimd.sam")
+    assert _run(exe, SITES_ARGS)[0] == _read("idx/ds_nosimd.sam")
+
+
+def test_known_sites_fixture_differs_from_plain():
+    """the known sites matter: -s recovers short terminal exons on many reads"""
+    a, b = _read("idx/d_nosimd.sam").splitlines(), _read("idx/ds_nosimd.sam").splitlines()
+    assert len(a) == len(b) == 160
+    assert sum(1 for x, y in zip(a, b) if x != y) >= 20
+
+
+def _same_sam(out, fixture):
+    exp = _read(fixture).splitlines()
+    got = out.splitlines()
+    bad = [i for i, (x, y) in enumerate(zip(got, exp)) if x != y]
+    assert len(got) == len(exp) and not bad, "reads differing: %s" % bad[:10]
+
+
+@pytest.mark.gpu
+def test_gpu_gmap_indexed_genome():
+    """`gmap -d` (stage 1 over a two-chromosome index, then stages 2-3) through the drop-in: SAM identical
+    to the reference program's."""
+    out, err = _run(_exe("gmap_gpu_nosimd"), IDX_ARGS, env={"GMAPDP_SHIM_STATS": "1"})
+    _same_sam(out, "idx/d_nosimd.sam")
+    st = _stats(err)
+    assert st["Stage2_compute"] > 0 and st["Dynprog_genome_gap"] > 0, st
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads", [1, 16])
+def test_gpu_gmap_known_splice_sites(threads):
+    """`gmap -d -s`: Dynprog_end5/3_known restated in the shim, the splice-trie walk's
+    Dynprog_end5/3_splicejunction calls on the engine; SAM identical to the reference program's."""
+    args = SITES_ARGS if threads == 1 else ["-t", str(threads), "-O"] + SITES_ARGS
+    out, err = _run(_exe("gmap_gpu_nosimd"), args, env={"GMAPDP_SHIM_STATS": "1"})
+    _same_sam(out, "idx/ds_nosimd.sam")
+    st = _stats(err)
+    for k in ("Dynprog_end5_known", "Dynprog_end3_known", "Dynprog_end5_splicejunction",
+              "Dynprog_end3_splicejunction"):
+        assert st[k] > 0, st
+
+
+@pytest.mark.gpu
+def test_gpu_gmap_known_sites_refused_in_simd_build():
+    """The splice-junction kernels are nosimd semantics: a SIMD drop-in build refuses -s at setup,
+    before any read, instead of running the reference's CPU DP."""
+    exe = _exe("gmap_gpu_avx2")
+    r = subprocess.run([exe] + SITES_ARGS, cwd=GOLD, capture_output=True, timeout=120)
+    assert r.returncode != 0 and b"known splice sites (-s) in a SIMD build" in r.stderr
+    assert r.stdout == b""
