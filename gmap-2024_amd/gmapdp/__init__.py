@@ -21,6 +21,7 @@ WATSON, JUMP_LATE, WIDEBAND = 0x1, 0x2, 0x4
 CTX_ONE_STREAM, CTX_PRIO_HIGH, CTX_PRIO_LOW, CTX_BLOCKING_SYNC, CTX_POLL_SYNC = 0x1, 0x2, 0x4, 0x8, 0x10  # create_ex flags
 SIMD = 0x40  # GMAPDP_SIMD: the reference's SIMD builds' semantics (every problem family)
 HALFP, FINALP = 0x8, 0x10
+KNOWN_SITES = 0x80  # GMAPDP_KNOWN_SITES: known splice sites of a genome gap (gmap -s)
 UNSET = -2147483648
 NEG_INFINITY_32 = -32768
 MAX_RLENGTH, MAX_GLENGTH = 660, 2000
@@ -557,6 +558,36 @@ class Engine:
             arena[o:o + len(lp)] = lp
             arena[o + len(lp):o + len(lp) + len(rp)] = rp
         results, pairs = self.genome_gap_batch_raw(probs, qbuf, qucbuf, arena[:m])
+        return decode_genome_results(results, pairs, [p["dynprogindex"] for p in calls])
+
+    def genome_gap_batch_known(self, calls, splice_probs, known):
+        """genome_gap_batch with known splice sites (GMAPDP_KNOWN_SITES): known[i] is call i's flag bytes
+        in the include/gmapdp.h layout (bridge left, bridge right, simple left, simple right), or None."""
+        calls = list(calls)
+        probs, qbuf, qucbuf, m = build_genome_batch(calls)
+        arena = np.zeros(max(m, 1))
+        for i, (lp, rp) in enumerate(splice_probs):
+            o = int(probs[i]["prob_offset"])
+            arena[o:o + len(lp)] = lp
+            arena[o + len(lp):o + len(lp) + len(rp)] = rp
+        kparts, ko = [], 0
+        for i, k in enumerate(known):
+            if k is None:
+                continue
+            probs[i]["flags"] |= KNOWN_SITES
+            probs[i]["known_offset"] = ko
+            kparts.append(bytes(k))
+            ko += len(k)
+        kb = np.frombuffer(b"".join(kparts) or b"\0", dtype=np.uint8).copy()
+        n = len(probs)
+        results = np.zeros(n, dtype=GENOME_RESULT_DTYPE)
+        cap = self.lib.gmapdp_genome_pair_capacity(probs.ctypes.data, n)
+        pairs = np.zeros(max(cap, 1), dtype=PAIR_DTYPE)
+        sp = np.ascontiguousarray(arena[:max(m, 1)])
+        rc = self.lib.gmapdp_genome_gap_batch_known(self.h, probs.ctypes.data, n, qbuf, qucbuf, len(qbuf),
+                                                    sp.ctypes.data, m, kb.ctypes.data, ko, results.ctypes.data,
+                                                    pairs.ctypes.data, cap)
+        self._check(rc, "gmapdp_genome_gap_batch_known")
         return decode_genome_results(results, pairs, [p["dynprogindex"] for p in calls])
 
     # -- batched Dynprog_cdna_gap ---------------------------------------------

@@ -1504,14 +1504,24 @@ simple_push (PairSink *s, GGOut *o, char c1, char c1_uc, char c2, int querypos, 
   }
 }
 
+/* Known splice sites (gmap -s, get_known_splicesites dynprog_genome.c:405) for the next orc_genome_gap
+   call, as flags in the engine's layout (include/gmapdp.h GMAPDP_KNOWN_SITES): the bridge's left_known
+   [0, glengthL) and right_known [glengthL, +glengthR), then genome_gap_simple's left / right_known over
+   rlength + 1 each.  A known site has probability 1.0 (:2577, 339) and scores KNOWN_SPLICESITE_REWARD
+   in genome_gap_simple (:3118).  NULL: none (the default). */
+#define KNOWN_SPLICESITE_REWARD 20
+static const unsigned char *g_known = NULL;
+void orc_set_known (const unsigned char *known) { g_known = known; }
+
 /* genome_gap_simple (dynprog_genome.c:3006-3280).  Returns the number of pairs
-   (reference list order) or -1 when it declines. */
+   (reference list order) or -1 when it declines.  ks: its known-site flags (left [0, rlength],
+   right after them) or NULL. */
 static int
 genome_gap_simple (PairSink *s, GGOut *o, const char *rsequence, const char *rsequenceuc,
                    const char *rev_rsequence, const char *rev_rsequenceuc, int rlength, const char *gL,
                    const char *revR, int roffset, int rev_roffset, int leftoffset, int rightoffset,
                    int mismatchtype, int dirclass, const double *left_probs, const double *right_probs,
-                   int genestrand, int dpi, int halfp) {
+                   int genestrand, int dpi, int halfp, const unsigned char *ks) {
   const int *isc = intron_score[dirclass][0];  /* assumes finalp false (:3032) */
   short (*pd)[128] = pairdistance[mismatchtype];
   int scoreL = 0, scoreR = 0, bestscore = 0, bestscoreI = 0, bestrL = -1, bestrR = -1;
@@ -1522,7 +1532,9 @@ genome_gap_simple (PairSink *s, GGOut *o, const char *rsequence, const char *rse
     scoreL += pd[(unsigned char) rsequenceuc[rL - 1]][(unsigned char) gL[rL - 1]];
     introntype = left_dinucl(gL[rL], gL[rL + 1]) & right_dinucl(revR[-rR - 1], revR[-rR]);
     scoreI = isc[introntype];
-    if (introntype != 0 && (score = scoreL + scoreI + scoreR) >= bestscore) {  /* >= : jump late */
+    const int kl = (ks && ks[rL]) ? KNOWN_SPLICESITE_REWARD : 0;
+    const int kr = (ks && ks[rlength + 1 + rR]) ? KNOWN_SPLICESITE_REWARD : 0;
+    if ((introntype != 0 || kl > 0 || kr > 0) && (score = scoreL + kl + scoreI + kr + scoreR) >= bestscore) {
       bestscore = score;
       bestscoreI = scoreI;
       bestrL = rL;
@@ -1534,8 +1546,8 @@ genome_gap_simple (PairSink *s, GGOut *o, const char *rsequence, const char *rse
   finalscore = halfp ? bestscore - bestscoreI / 2 : bestscore;
   o->score = o->nmatches = o->nmismatches = 0;
   if (finalscore <= 0) return -1;
-  o->left_prob = left_probs[bestrL];
-  o->right_prob = right_probs[bestrR];
+  o->left_prob = (ks && ks[bestrL]) ? 1.0 : left_probs[bestrL];  /* get_splicesite_probs (:339) */
+  o->right_prob = (ks && ks[rlength + 1 + bestrR]) ? 1.0 : right_probs[bestrR];
   if (o->left_prob < 0.90 || o->right_prob < 0.90) return -1;
 
   for (r = 1; r <= bestrL; r++)
@@ -1875,7 +1887,8 @@ orc_genome_gap (const char *rsequence, const char *rsequenceuc, int rlength, int
   if (!finalp && defect_rate < DEFECT_MEDQ) {
     n = genome_gap_simple(&sink, &o, rsequence, rsequenceuc, rev_rsequence, rev_rsequenceuc, rlength, gL, revR,
                           roffset, rev_roffset, goffsetL, rev_goffsetR, mismatchtype, dirclass, left_probs,
-                          right_probs, genestrand, dynprogindex, halfp);
+                          right_probs, genestrand, dynprogindex, halfp,
+                          g_known ? g_known + glengthL + glengthR : NULL);
     if (n >= 0) {
       o.dpi = dynprogindex + (dynprogindex > 0 ? +1 : -1);
       free(gL); free(gLa); free(gR); free(gRa);
@@ -1944,6 +1957,17 @@ orc_genome_gap (const char *rsequence, const char *rsequenceuc, int rlength, int
   orc_standard_fill(rev_rsequence, revR, revR, rlength, glengthR, mismatchtype, open, extend, lbandL, ubandR,
                     !jump_late_p, /*revp*/1, NEG_INFINITY_32, 1, 1, matrixR, dirsR);
 
+  /* known sites: probability 1.0 in the bridge (dynprog_genome.c:2577-2652) */
+  double *lpk = NULL, *rpk = NULL;
+  if (g_known) {
+    int c;
+    lpk = (double *) malloc((glengthL + 1) * sizeof(double));
+    rpk = (double *) malloc((glengthR + 1) * sizeof(double));
+    for (c = 0; c < glengthL; c++) lpk[c] = g_known[c] ? 1.0 : left_probs[c];
+    for (c = 0; c < glengthR; c++) rpk[c] = g_known[glengthL + c] ? 1.0 : right_probs[c];
+    left_probs = lpk;
+    right_probs = rpk;
+  }
   /* bridge_intron_gap's own bands (:2924-2928) */
   finalscore = bridge_site_level(&bestrL, &bestrR, &bestcL, &bestcR, matrixL, matrixR, gL, revR, rlength,
                                  glengthL, glengthR, dirclass, finalp, halfp,
@@ -1971,6 +1995,7 @@ orc_genome_gap (const char *rsequence, const char *rsequenceuc, int rlength, int
   /* returned list: List_reverse of [reverse(TL) G TR] = reverse(TR) G TL, which is the sink order */
   free(matrixL); free(dirsL); free(matrixR); free(dirsR);
   free(gL); free(gLa); free(gR); free(gRa);
+  free(lpk); free(rpk);
   gg_scalars(&o, scalars, dscalars);
   return n;
 }

@@ -89,6 +89,9 @@ int orc_standard_fill (const char *rsequence, const char *gsequence, const char 
    nmismatches, nopens, nindels, new_leftgenomepos, new_rightgenomepos,
    exonhead, introntype (INT_MIN where the reference leaves an out-parameter
    unwritten); dscalars[0..1] = left_prob, right_prob. */
+/* Known-site flags (GMAPDP_KNOWN_SITES layout) for the following orc_genome_gap calls; NULL: none. */
+void orc_set_known (const unsigned char *known);
+
 int orc_genome_gap (const char *rsequence, const char *rsequenceuc, int rlength, int glengthL, int glengthR,
                     int roffset, int goffsetL, int rev_goffsetR, unsigned int chroffset, unsigned int chrhigh,
                     int cdna_direction, int flags, int genestrand, int extraband_paired, double defect_rate,

@@ -1020,3 +1020,32 @@ def end_known_problem(rng, genome: bytes):
     p["sites"] = sites
     p["types"] = [rng.choice([1, 2, 3, 4]) for _ in sites]
     return p
+
+
+def _orc_genome_gap_known(self, p, probsL, probsR, known):
+    """orc_genome_gap with known-site flags (GMAPDP_KNOWN_SITES layout bytes, or None)."""
+    self.lib.orc_set_known.argtypes = [C.c_char_p]
+    keep = C.create_string_buffer(bytes(known), len(known)) if known is not None else None
+    self.lib.orc_set_known(keep)
+    try:
+        return self.genome_gap(p, probsL, probsR)
+    finally:
+        self.lib.orc_set_known(None)
+
+
+Oracle.genome_gap_known = _orc_genome_gap_known
+
+
+def random_known_flags(rng, p, density=0.03):
+    """Known-site flags for a genome-gap call in the engine's layout: sparse random flags for the bridge's
+    windows and genome_gap_simple's rlength windows, set where the reference's IIT ranges can set them
+    (left [1, glength-2], right [0, glength-3] on the plus strand; mirrored on the minus strand)."""
+    gL, gR, r = p["glengthL"], p["glengthR"], p["rlength"]
+    watson = p["flags"] & 1
+
+    def side(n, left):
+        lo, hi = (1, n - 2) if (left == bool(watson)) else (0, n - 3)
+        return bytes(1 if (lo <= i <= hi and rng.random() < density) else 0 for i in range(n))
+
+    out = side(gL, True) + side(gR, False) + side(r + 1, True) + side(r + 1, False)
+    return out

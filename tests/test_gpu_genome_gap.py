@@ -125,3 +125,31 @@ def test_gpu_genome_gap_every_packed_band_class(engine):
     d = _first_diff(got, exp)
     assert d is None, _msg(probs, d, "oracle")
 
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_gpu_genome_gap_known_sites_match_oracle(engine, seed):
+    """Known splice sites (gmap -s, GMAPDP_KNOWN_SITES): probability 1.0 at a known site in the bridge and
+    in genome_gap_simple's probability test, KNOWN_SPLICESITE_REWARD in genome_gap_simple's score and
+    candidate test (dynprog_genome.c:2577-2652, 3118-3119, 339-372); calls without flags in the same batch
+    stay as they were."""
+    from dpbind import random_known_flags
+    rng = random.Random(7100 + seed)
+    g = bytearray(random_genome(rng, 120000))
+    probs = [genome_gap_problem(rng, g, edge=(i % 5 == 0)) for i in range(3000)]
+    for p in probs[::2]:
+        p["defect_rate"] = 0.001  # genome_gap_simple runs first (:3479)
+    g = bytes(g)
+    engine.set_genome(g)
+    orc = Oracle()
+    orc.set_genome(g)
+    sp = [_synthetic_probs(rng, p) for p in probs]
+    known = [None if i % 7 == 0 else random_known_flags(rng, p, density=rng.choice([0.01, 0.05, 0.2]))
+             for i, p in enumerate(probs)]
+    got = engine.genome_gap_batch_known(probs, sp, known)
+    exp = [orc.genome_gap_known(p, lp, rp, k) for p, (lp, rp), k in zip(probs, sp, known)]
+    d = _first_diff(got, exp)
+    assert d is None, _msg(probs, d, "oracle")
+    # the flags changed results (rewarded simple-path splices, bridges on known sites)
+    plain = [orc.genome_gap(p, lp, rp) for p, (lp, rp) in zip(probs, sp)]
+    assert sum(1 for a, b in zip(exp, plain) if a != b) > 50
