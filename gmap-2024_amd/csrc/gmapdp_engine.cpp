@@ -50,6 +50,9 @@ hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
                      const int8_t* isctab, gmapdp_genome_result* results, gmapdp_pair* pairs,
                      unsigned char* gscratch, const uint8_t* known);
 size_t lds_bytes_sj(int rlength, int glength, int R, bool dirs_lds);
+hipError_t launch_usj(int B, int nblocks, size_t lds, hipStream_t stream, const DevSjProblem* probs, const int* order,
+                      unsigned char* gscratch, const char* qseq, const char* qseq_uc, const char* jseq,
+                      const int8_t* sctab, const uint8_t* constab, gmapdp_sj_result* results, gmapdp_pair* pairs);
 hipError_t launch_sj(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevSjProblem* probs,
                      const int* order, const char* qseq, const char* qseq_uc, const char* jseq, const int8_t* sctab,
                      const uint8_t* constab, gmapdp_sj_result* results, gmapdp_pair* pairs, uint64_t* gdirs);
@@ -65,7 +68,7 @@ hipError_t launch_uxg(int B, int nproblems, size_t lds, hipStream_t stream, cons
                       const int* order, unsigned char* gscratch, const uint32_t* blocks, uint64_t nwords,
                       const char* qseq, const char* qseq_uc, const double* sprob, const int8_t* sctab,
                       const uint8_t* constab, const int8_t* isctab, gmapdp_genome_result* results,
-                      gmapdp_pair* pairs);
+                      gmapdp_pair* pairs, const uint8_t* known);
 size_t lds_bytes_cg(int rlength, int glength, bool simd, int RB);
 size_t scratch_bytes_cg(int rlength, int glength, int lband, int uband, bool simd, int RB);
 hipError_t launch_cg(bool simd, int RB, int nproblems, size_t lds, hipStream_t stream, const DevCdnaProblem* probs,
@@ -863,10 +866,6 @@ static int convert_genome(gmapdp_ctx* ctx, const gmapdp_genome_problem& p, gmapd
   if (!(p.flags & GMAPDP_FINALP) && dr < 0.014) d.flags |= kGSimple;  // :3479
   if (p.flags & GMAPDP_SIMD) d.flags |= kGSimd;
   if (p.flags & GMAPDP_KNOWN_SITES) {
-    if (p.flags & GMAPDP_SIMD) {
-      *err = bad(ctx, "known splice sites are built in nosimd semantics only");
-      return 0;
-    }
     if (p.known_offset < 0) {
       *err = bad(ctx, "negative known_offset");
       return 0;
@@ -1183,7 +1182,7 @@ static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, cons
     if (!a.d_gresults || !a.d_sprob) return hipErrorInvalidValue;
     return launch_uxg(L.R, L.count, L.lds, stream, a.d_gprobs, a.d_gorder + L.first, (unsigned char*)ctx->gdirs.p,
                       ctx->d_genome, ctx->genome_words, a.d_q, a.d_quc, a.d_sprob, ctx->d_sc, ctx->d_cs, ctx->d_isc,
-                      a.d_gresults, a.d_pairs);
+                      a.d_gresults, a.d_pairs, a.d_known);
   }
   if (L.kind == PlanCore::kSx)
     return launch_sx(L.R, L.count, (int)L.lds, (long long)L.extra, (unsigned char*)ctx->gdirs.p + L.gdirs_offset,
@@ -1664,10 +1663,6 @@ static int convert_sj(gmapdp_ctx* ctx, const gmapdp_sj_problem& p, size_t qbytes
   res.pair_offset = 0;
   res.known_index = -1;
   res.dynprogindex = p.dynprogindex;
-  if (p.flags & GMAPDP_SIMD) {
-    *err = bad(ctx, "splice-junction end gaps are built in nosimd semantics only");
-    return 0;
-  }
   if (p.rlength <= 0 || p.rlength > GMAPDP_MAX_RLENGTH || p.glength <= 0 || p.glength > GMAPDP_MAX_GLENGTH) {
     res.traceback_score = 0;  // size guard (dynprog_end.c:1707-1722)
     res.nmatches = res.nmismatches = res.nopens = res.nindels = 0;
@@ -1726,6 +1721,15 @@ static int convert_sj(gmapdp_ctx* ctx, const gmapdp_sj_problem& p, size_t qbytes
     *err = bad(ctx, "negative band");
     return 0;
   }
+  if (p.flags & GMAPDP_SIMD) {
+    // the SIMD builds' endpoint scan reads lower[rlength][c] for c < rlength, past glength when
+    // rlength > glength + 1 (uninitialised scores there; Splicetrie passes glength >= rlength)
+    if (p.rlength > p.glength + 1) {
+      *err = bad(ctx, "GMAPDP_SIMD splice junction with rlength > glength + 1");
+      return 0;
+    }
+    d.simd = 1;
+  }
   return 1;
 }
 
@@ -1752,6 +1756,17 @@ int gmapdp_end_splicejunction_batch(gmapdp_ctx* ctx, const gmapdp_sj_problem* pr
     int err = 0;
     if (!convert_sj(ctx, problems[i], qbytes, jseq, jbytes, results[i], d, &err)) {
       if (err) return err;
+      continue;
+    }
+    d.pair_offset = (int32_t)pair_off;
+    if (d.simd) {  // 8-bit triangles when either length is below use8p_size[ENDQ] (dynprog_end.c:1743)
+      const int B = (d.rlength < kUse8pSize[kEndQ] || d.glength < kUse8pSize[kEndQ]) ? 32 : 16;
+      d.dirs_offset = (int64_t)dirs_off;
+      dirs_off += align_up(scratch_bytes_uxe(d.rlength, d.glength, d.lband, d.uband, B), 256);
+      pair_off += sj_capacity_one(problems[i]);
+      classes[{-B, 0}].push_back((int)dev.size());
+      dev.push_back(d);
+      dev_problem.push_back(i);
       continue;
     }
     const int W = d.lband + d.uband + 1;
@@ -1784,9 +1799,11 @@ int gmapdp_end_splicejunction_batch(gmapdp_ctx* ctx, const gmapdp_sj_problem* pr
   for (auto& kv : classes) {
     CL L{kv.first.first, kv.first.second != 0, (int)order.size(), (int)kv.second.size(), 0};
     for (int s : kv.second) {
-      L.lds = std::max(L.lds, lds_bytes_sj(dev[s].rlength, dev[s].glength, L.R, L.dirs_lds));
+      L.lds = std::max(L.lds, L.R < 0 ? lds_bytes_uxe(dev[s].rlength, dev[s].glength, -L.R)
+                                      : lds_bytes_sj(dev[s].rlength, dev[s].glength, L.R, L.dirs_lds));
       order.push_back(s);
     }
+    if (L.lds > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
     launches.push_back(L);
   }
   hipError_t e = ctx->sjprobs.ensure(sizeof(DevSjProblem) * ndev);
@@ -1806,10 +1823,16 @@ int gmapdp_end_splicejunction_batch(gmapdp_ctx* ctx, const gmapdp_sj_problem* pr
   if (e == hipSuccess) e = hipMemcpyAsync(ctx->sjseq.p, jseq, jbytes, hipMemcpyHostToDevice, s);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "upload: %s", e);
   for (const CL& L : launches) {
-    e = launch_sj(L.R, L.dirs_lds, L.count, L.lds, s, (const DevSjProblem*)ctx->sjprobs.p,
-                  (const int*)ctx->sjorder.p + L.first, (const char*)ctx->qseq.p, (const char*)ctx->qseq_uc.p,
-                  (const char*)ctx->sjseq.p, ctx->d_sc, ctx->d_cs, (gmapdp_sj_result*)ctx->sjresults.p,
-                  (gmapdp_pair*)ctx->pairs.p, (uint64_t*)ctx->sjdirs.p);
+    if (L.R < 0)  // SIMD-build semantics: key -B
+      e = launch_usj(-L.R, L.count, L.lds, s, (const DevSjProblem*)ctx->sjprobs.p, (const int*)ctx->sjorder.p + L.first,
+                     (unsigned char*)ctx->sjdirs.p, (const char*)ctx->qseq.p, (const char*)ctx->qseq_uc.p,
+                     (const char*)ctx->sjseq.p, ctx->d_sc, ctx->d_cs, (gmapdp_sj_result*)ctx->sjresults.p,
+                     (gmapdp_pair*)ctx->pairs.p);
+    else
+      e = launch_sj(L.R, L.dirs_lds, L.count, L.lds, s, (const DevSjProblem*)ctx->sjprobs.p,
+                    (const int*)ctx->sjorder.p + L.first, (const char*)ctx->qseq.p, (const char*)ctx->qseq_uc.p,
+                    (const char*)ctx->sjseq.p, ctx->d_sc, ctx->d_cs, (gmapdp_sj_result*)ctx->sjresults.p,
+                    (gmapdp_pair*)ctx->pairs.p, (uint64_t*)ctx->sjdirs.p);
     if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "splice-junction launch: %s", e);
   }
   std::vector<gmapdp_sj_result> dres(ndev);

@@ -159,7 +159,8 @@ struct DevSjProblem {
   int32_t genestrand;
   int32_t dynprogindex;
   int32_t pair_offset;
-  int64_t dirs_offset;    // byte offset into the global direction scratch (!DIRS_LDS classes)
+  int32_t simd;           // SIMD-build semantics (usj_kernel)
+  int64_t dirs_offset;    // byte offset into the global direction scratch (!DIRS_LDS / usj classes)
 };
 
 // Stage-2 seeding descriptor (Oligoindex_hr_tally + Oligoindex_get_mappings, oligoindex_hr.c:33849/34127)

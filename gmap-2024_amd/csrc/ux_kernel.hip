@@ -147,7 +147,7 @@ __global__ __launch_bounds__(64) void uxg_kernel(
     const uint32_t* __restrict__ blocks, uint64_t nwords, const char* __restrict__ qseq,
     const char* __restrict__ qseq_uc, const double* __restrict__ sprob, const int8_t* __restrict__ sctab,
     const uint8_t* __restrict__ constab, const int8_t* __restrict__ isctab,
-    gmapdp_genome_result* __restrict__ results, gmapdp_pair* __restrict__ pairs) {
+    gmapdp_genome_result* __restrict__ results, gmapdp_pair* __restrict__ pairs, const uint8_t* __restrict__ known) {
   constexpr int NEG = (B == 32) ? -128 : -32768;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x;
@@ -158,6 +158,7 @@ __global__ __launch_bounds__(64) void uxg_kernel(
   const bool watson = flags & kFWatson;
   const int eb = P.lbandL;  // extraband_paired: lbandL = lbandR (Dynprog_compute_bands, glength > rlength)
   const int ubandL = P.ubandL, ubandR = P.ubandR;
+  const uint8_t* kb = (flags & kGKnown) ? known + P.known_offset : nullptr;  // known splice sites
   const CarveUxg cv = carve_uxg<B>(rlen, gL, gR);
   double* pL = reinterpret_cast<double*>(smem + cv.pL);
   double* pR = reinterpret_cast<double*>(smem + cv.pR);
@@ -186,13 +187,13 @@ __global__ __launch_bounds__(64) void uxg_kernel(
     const char c2 = segment_nt(blocks, nwords, (uint32_t)i, (uint32_t)gL, P.segposL, P.segboundL,
                                flags & kGSegLLeft, flags & kGSegLRc);
     gclL[i + 1] = gclass(c2);
-    pL[i] = sprob[P.prob_offset + i];
+    pL[i] = (kb && kb[i]) ? 1.0 : sprob[P.prob_offset + i];  // known sites: 1.0 (dynprog_genome.c:978)
   }
   for (int i = lane; i < gR; i += 64) {
     const char c2 = segment_nt(blocks, nwords, (uint32_t)i, (uint32_t)gR, P.segposR, P.segboundR,
                                flags & kGSegRLeft, flags & kGSegRRc);
     gclR[gR - i] = gclass(c2);  // rev_gsequenceR[1-c] = segment[glengthR-c]
-    pR[i] = sprob[P.prob_offset + gL + i];
+    pR[i] = (kb && kb[gL + i]) ? 1.0 : sprob[P.prob_offset + gL + i];
   }
   isc[lane] = isctab[(size_t)P.iclass * 128 + ((flags & kGFinal) ? 64 : 0) + lane];
   __syncthreads();
@@ -217,7 +218,8 @@ __global__ __launch_bounds__(64) void uxg_kernel(
 
   // ---- 1. genome_gap_simple (dynprog_genome.c:3479-3498), before the SIMD branch ----
   if ((flags & kGSimple) && gg_simple_wave(lane, P, pid, sctab, isctab, cons, qL, qucL, qR, qucR, gclL, gclR, gchL,
-                                           gchR, ldi, rdi, pL, pR, diagL, diagR, out, res, results))
+                                           gchR, ldi, rdi, pL, pR, diagL, diagR, out, res, results,
+                                           kb ? kb + gL + gR : nullptr, sprob + P.prob_offset))
     return;
 
   // ---- 2. the four triangles (:3510-3547 / :3655-3689); the R side runs with !jump_late_p ----
@@ -417,7 +419,7 @@ hipError_t launch_uxg(int B, int nproblems, size_t lds, hipStream_t stream, cons
                       const int* order, unsigned char* gscratch, const uint32_t* blocks, uint64_t nwords,
                       const char* qseq, const char* qseq_uc, const double* sprob, const int8_t* sctab,
                       const uint8_t* constab, const int8_t* isctab, gmapdp_genome_result* results,
-                      gmapdp_pair* pairs) {
+                      gmapdp_pair* pairs, const uint8_t* known) {
   if (B != 16 && B != 32) return hipErrorInvalidValue;
   void* fn = (B == 16) ? reinterpret_cast<void*>(&uxg_kernel<16>) : reinterpret_cast<void*>(&uxg_kernel<32>);
   if (lds > 64 * 1024) {
@@ -426,7 +428,7 @@ hipError_t launch_uxg(int B, int nproblems, size_t lds, hipStream_t stream, cons
   }
   void* args[] = {(void*)&probs, (void*)&order, (void*)&gscratch, (void*)&blocks, (void*)&nwords, (void*)&qseq,
                   (void*)&qseq_uc, (void*)&sprob, (void*)&sctab, (void*)&constab, (void*)&isctab, (void*)&results,
-                  (void*)&pairs};
+                  (void*)&pairs, (void*)&known};
   return hipLaunchKernel(fn, dim3(nproblems), dim3(64), args, lds, stream);
 }
 

@@ -192,13 +192,6 @@ __wrap_Dynprog_end_setup (Univcoord_T *splicesites_in, Splicetype_T *splicetypes
                           int nsplicesites_in, Trieoffset_T *trieoffsets_obs_in, Triecontent_T *triecontents_obs_in,
                           Trieoffset_T *trieoffsets_max_in, Triecontent_T *triecontents_max_in,
                           int user_open_in, int user_extend_in, bool user_dynprog_p_in) {
-#ifdef HAVE_SSE2
-  /* the splice-junction end gaps (dynprog_end.c:1653/2249) are built in nosimd semantics only: a SIMD
-     build with known splice sites is refused at setup, before any read runs, so that no reference CPU
-     DP executes inside the product */
-  if (nsplicesites_in > 0)
-    shim_refuse("known splice sites (-s) in a SIMD build (the splice-junction end gaps are nosimd only)");
-#endif
   shim_splicesites = splicesites_in;
   shim_splicetypes = splicetypes_in;
   shim_nsplicesites = nsplicesites_in;
@@ -222,9 +215,6 @@ __wrap_Dynprog_genome_setup (bool novelsplicingp_in, IIT_T splicing_iit_in, int 
                              int donor_typeint_in, int acceptor_typeint_in, int user_open_in, int user_extend_in,
                              bool user_dynprog_p_in) {
   if (splicing_iit_in != NULL) {
-#ifdef HAVE_SSE2
-    shim_refuse("a splicing IIT (-s) in a SIMD build (known splice sites are built in nosimd semantics only)");
-#endif
     /* an introns file (no donor/acceptor types: intron-level bridging, dynprog_genome.c:2944) and
        known-only splicing (novel splicing off: genome_gap_simple then requires known sites, :3157) are
        not built */
@@ -1176,7 +1166,7 @@ shim_splicejunction (int end3p, int *dynprogindex, int *finalscore, int *misssco
   p->goffset_anchor = offset2_anchor;
   p->goffset_far = offset2_far;
   p->contlength = contlength;
-  p->flags = jump_late_p ? GMAPDP_JUMP_LATE : 0;
+  p->flags = (jump_late_p ? GMAPDP_JUMP_LATE : 0) | SHIM_SIMD;
   p->genestrand = genestrand;
   p->extraband = extraband_end;
   p->end3p = end3p;

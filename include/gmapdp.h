@@ -185,7 +185,8 @@ typedef struct {
  *   then rlength + 1 bytes, then rlength + 1 bytes: genome_gap_simple's left_known / right_known
  *   (:3045-3049, queried with glength = rlength)
  * A known position scores KNOWN_SPLICESITE_REWARD in genome_gap_simple and has probability 1.0; the
- * probability arena then holds the MaxEnt values at every position (known or not).  Nosimd only. */
+ * probability arena then holds the MaxEnt values at every position (known or not).  Both builds'
+ * semantics (with GMAPDP_SIMD the SIMD bridge reads the same flags). */
 #define GMAPDP_KNOWN_SITES 0x80
 
 /* One Dynprog_genome_gap call (dynprog_genome.c:3288 argument list).  The
@@ -347,7 +348,9 @@ size_t gmapdp_cdna_pair_capacity (const gmapdp_cdna_problem *problems, int n);
  * (the caller's splicejunction buffer, built by Dynprog_make_splicejunction_5/3) is
  * jseq[joff .. joff+glength) in string order: end5's rev_gsequence points at its last character,
  * end3's gsequence at its first.  Junction characters must be A C G T or N.  Nosimd semantics
- * (Dynprog_standard + traceback_local_std); GMAPDP_SIMD is GMAPDP_EINVAL. */
+ * (Dynprog_standard + traceback_local_std), or with GMAPDP_SIMD the SIMD builds' (the
+ * Dynprog_simd_8/16_upper/_lower triangles + traceback_local_8/16_upper/_lower; rlength > glength + 1
+ * is then GMAPDP_EINVAL, as for the SIMD end gaps). */
 typedef struct {
   int32_t qoff;
   int32_t joff;

@@ -1898,6 +1898,17 @@ orc_genome_gap (const char *rsequence, const char *rsequenceuc, int rlength, int
     sink.n = 0;
   }
 
+  /* known sites: probability 1.0 in the bridge of either build (dynprog_genome.c:2577-2652, 978-1053) */
+  double *lpk = NULL, *rpk = NULL;
+  if (g_known) {
+    int c;
+    lpk = (double *) malloc((glengthL + 1) * sizeof(double));
+    rpk = (double *) malloc((glengthR + 1) * sizeof(double));
+    for (c = 0; c < glengthL; c++) lpk[c] = g_known[c] ? 1.0 : left_probs[c];
+    for (c = 0; c < glengthR; c++) rpk[c] = g_known[glengthL + c] ? 1.0 : right_probs[c];
+    left_probs = lpk;
+    right_probs = rpk;
+  }
   if (g_simd) {
     /* dynprog_genome.c:3501-3795: 8-bit triangles when rlength or both glengths are below use8p_size */
     int bits = (rlength < use8p_size[mismatchtype] ||
@@ -1940,6 +1951,7 @@ orc_genome_gap (const char *rsequence, const char *rsequenceuc, int rlength, int
       n = gg_finish(&sink, &t, &o, out, max_pairs, dynprogindex);
     }
     free(mL); free(mR); free(dL); free(dR);
+    free(lpk); free(rpk);
     free(gL); free(gLa); free(gR); free(gRa);
     gg_scalars(&o, scalars, dscalars);
     return n;
@@ -1957,17 +1969,6 @@ orc_genome_gap (const char *rsequence, const char *rsequenceuc, int rlength, int
   orc_standard_fill(rev_rsequence, revR, revR, rlength, glengthR, mismatchtype, open, extend, lbandL, ubandR,
                     !jump_late_p, /*revp*/1, NEG_INFINITY_32, 1, 1, matrixR, dirsR);
 
-  /* known sites: probability 1.0 in the bridge (dynprog_genome.c:2577-2652) */
-  double *lpk = NULL, *rpk = NULL;
-  if (g_known) {
-    int c;
-    lpk = (double *) malloc((glengthL + 1) * sizeof(double));
-    rpk = (double *) malloc((glengthR + 1) * sizeof(double));
-    for (c = 0; c < glengthL; c++) lpk[c] = g_known[c] ? 1.0 : left_probs[c];
-    for (c = 0; c < glengthR; c++) rpk[c] = g_known[glengthL + c] ? 1.0 : right_probs[c];
-    left_probs = lpk;
-    right_probs = rpk;
-  }
   /* bridge_intron_gap's own bands (:2924-2928) */
   finalscore = bridge_site_level(&bestrL, &bestrR, &bestcL, &bestcR, matrixL, matrixR, gL, revR, rlength,
                                  glengthL, glengthR, dirclass, finalp, halfp,

@@ -20,8 +20,8 @@ Outputs (data only), under tests/golden/idx/:
                              not read them)
   db/e2eidx/e2eidx.maps/e2esites.iit   the known splice sites (iit_store)
   sj_reads.fa                the reads
-  d_nosimd.sam               `gmap_nosimd -D db -d e2eidx -f samse --no-sam-headers sj_reads.fa`
-  ds_nosimd.sam              the same with `-s db/e2eidx/e2eidx.maps/e2esites.iit`
+  d_{nosimd,avx2}.sam        `gmap_<build> -D db -d e2eidx -f samse --no-sam-headers sj_reads.fa`
+  ds_{nosimd,avx2}.sam       the same with `-s db/e2eidx/e2eidx.maps/e2esites.iit`
 """
 import os
 import random
@@ -132,9 +132,11 @@ def main():
     base = ["-D", "db", "-d", "e2eidx", "-f", "samse", "--no-sam-headers", "sj_reads.fa"]
     # -s takes the .iit path: a bare name that is not a local file makes gmap.c:6318 call strlen on a NULL
     # user_splicingdir (the reference crashes)
-    for name, extra in (("d_nosimd.sam", []), ("ds_nosimd.sam", ["-s", SITES])):
-        with open(os.path.join(OUT, name), "w") as f:
-            subprocess.run([gmap] + extra + base, stdout=f, stderr=subprocess.DEVNULL, check=True, cwd=OUT)
+    for build in ("nosimd", "avx2"):
+        exe = os.path.join(REF, "gmap_" + build)
+        for name, extra in (("d_%s.sam" % build, []), ("ds_%s.sam" % build, ["-s", SITES])):
+            with open(os.path.join(OUT, name), "w") as f:
+                subprocess.run([exe] + extra + base, stdout=f, stderr=subprocess.DEVNULL, check=True, cwd=OUT)
     a = open(os.path.join(OUT, "d_nosimd.sam")).read().splitlines()
     b = open(os.path.join(OUT, "ds_nosimd.sam")).read().splitlines()
     print("wrote %s: %d reads, %d known-site lines, %d SAM lines differ with -s" % (

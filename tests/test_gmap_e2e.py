@@ -200,10 +200,11 @@ IDX_ARGS = ["-D", "idx/db", "-d", "e2eidx", "-f", "samse", "--no-sam-headers", "
 SITES_ARGS = ["-s", "idx/db/e2eidx/e2eidx.maps/e2esites.iit"] + IDX_ARGS
 
 
-def test_reference_gmap_indexed_reproduces_fixtures():
-    exe = _exe("gmap_nosimd")
-    assert _run(exe, IDX_ARGS)[0] == _read("idx/d_nosimd.sam")
-    assert _run(exe, SITES_ARGS)[0] == _read("idx/ds_nosimd.sam")
+@pytest.mark.parametrize("build", BUILDS)
+def test_reference_gmap_indexed_reproduces_fixtures(build):
+    exe = _exe("gmap_" + build)
+    assert _run(exe, IDX_ARGS)[0] == _read("idx/d_%s.sam" % build)
+    assert _run(exe, SITES_ARGS)[0] == _read("idx/ds_%s.sam" % build)
 
 
 def test_known_sites_fixture_differs_from_plain():
@@ -221,34 +222,26 @@ def _same_sam(out, fixture):
 
 
 @pytest.mark.gpu
-def test_gpu_gmap_indexed_genome():
+@pytest.mark.parametrize("build", BUILDS)
+def test_gpu_gmap_indexed_genome(build):
     """`gmap -d` (stage 1 over a two-chromosome index, then stages 2-3) through the drop-in: SAM identical
     to the reference program's."""
-    out, err = _run(_exe("gmap_gpu_nosimd"), IDX_ARGS, env={"GMAPDP_SHIM_STATS": "1"})
-    _same_sam(out, "idx/d_nosimd.sam")
+    out, err = _run(_exe("gmap_gpu_" + build), IDX_ARGS, env={"GMAPDP_SHIM_STATS": "1"})
+    _same_sam(out, "idx/d_%s.sam" % build)
     st = _stats(err)
     assert st["Stage2_compute"] > 0 and st["Dynprog_genome_gap"] > 0, st
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("threads", [1, 16])
-def test_gpu_gmap_known_splice_sites(threads):
+@pytest.mark.parametrize("build,threads", [("nosimd", 1), ("nosimd", 16), ("avx2", 1), ("avx2", 16)])
+def test_gpu_gmap_known_splice_sites(build, threads):
     """`gmap -d -s`: Dynprog_end5/3_known restated in the shim, the splice-trie walk's
-    Dynprog_end5/3_splicejunction calls on the engine; SAM identical to the reference program's."""
+    Dynprog_end5/3_splicejunction calls and the known-site genome gaps on the engine, in both builds'
+    semantics; SAM identical to the reference program's."""
     args = SITES_ARGS if threads == 1 else ["-t", str(threads), "-O"] + SITES_ARGS
-    out, err = _run(_exe("gmap_gpu_nosimd"), args, env={"GMAPDP_SHIM_STATS": "1"})
-    _same_sam(out, "idx/ds_nosimd.sam")
+    out, err = _run(_exe("gmap_gpu_" + build), args, env={"GMAPDP_SHIM_STATS": "1"})
+    _same_sam(out, "idx/ds_%s.sam" % build)
     st = _stats(err)
     for k in ("Dynprog_end5_known", "Dynprog_end3_known", "Dynprog_end5_splicejunction",
-              "Dynprog_end3_splicejunction"):
+              "Dynprog_end3_splicejunction", "Dynprog_genome_gap"):
         assert st[k] > 0, st
-
-
-@pytest.mark.gpu
-def test_gpu_gmap_known_sites_refused_in_simd_build():
-    """The splice-junction kernels are nosimd semantics: a SIMD drop-in build refuses -s at setup,
-    before any read, instead of running the reference's CPU DP."""
-    exe = _exe("gmap_gpu_avx2")
-    r = subprocess.run([exe] + SITES_ARGS, cwd=GOLD, capture_output=True, timeout=120)
-    assert r.returncode != 0 and b"(-s) in a SIMD build" in r.stderr
-    assert r.stdout == b""

@@ -153,3 +153,26 @@ def test_gpu_genome_gap_known_sites_match_oracle(engine, seed):
     # the flags changed results (rewarded simple-path splices, bridges on known sites)
     plain = [orc.genome_gap(p, lp, rp) for p, (lp, rp) in zip(probs, sp)]
     assert sum(1 for a, b in zip(exp, plain) if a != b) > 50
+
+
+def test_gpu_genome_gap_known_sites_simd_match_oracle(engine):
+    """Known splice sites in the SIMD builds' genome gap (uxg_kernel): the same flags, the SIMD bridge."""
+    from dpbind import random_known_flags
+    rng = random.Random(7300)
+    g = bytearray(random_genome(rng, 120000))
+    probs = [genome_gap_problem(rng, g, edge=(i % 5 == 0)) for i in range(1500)]
+    for i, p in enumerate(probs):
+        p["simd"] = True
+        if i % 2:
+            p["defect_rate"] = 0.001
+    g = bytes(g)
+    engine.set_genome(g)
+    orc = Oracle(simd=True)
+    orc.set_genome(g)
+    sp = [_synthetic_probs(rng, p) for p in probs]
+    known = [None if i % 7 == 0 else random_known_flags(rng, p, density=rng.choice([0.01, 0.05, 0.2]))
+             for i, p in enumerate(probs)]
+    got = engine.genome_gap_batch_known(probs, sp, known)
+    exp = [orc.genome_gap_known(p, lp, rp, k) for p, (lp, rp), k in zip(probs, sp, known)]
+    d = _first_diff(got, exp)
+    assert d is None, _msg(probs, d, "oracle")

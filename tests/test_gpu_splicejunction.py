@@ -107,3 +107,25 @@ def test_gpu_splicejunction_matches_reference_objects(engine):
     exp = [ref.end_splicejunction(p) for p in probs]
     d = _first_diff(got, exp)
     assert d is None, "problem %d (%s): gpu %s vs ref %s" % (d[0], _desc(probs[d[0]]), d[1], d[2])
+
+
+@pytest.mark.skipif(not ref_available("avx2"), reason="reference objects did not travel")
+def test_gpu_splicejunction_simd_matches_reference_objects(engine):
+    """The SIMD builds' Dynprog_end5/3_splicejunction (usj_kernel: the 8/16-bit triangles,
+    find_best_endpoint_to_queryend_indels_8/16, traceback_local_8/16_upper/_lower) against the AVX2
+    objects, inside the domain Splicetrie calls them in (glength >= rlength - 1)."""
+    rng = random.Random(9393)
+    g = random_genome(rng, 200000)
+    ref = Ref("avx2")
+    ref.set_genome(g)
+    probs = []
+    while len(probs) < 2500:
+        p = splicejunction_problem(rng, g, edge=(len(probs) % 5 == 0))
+        if p["rlength"] <= p["glength"] + 1:
+            p["simd"] = True
+            probs.append(p)
+    got = engine.end_splicejunction_batch(probs)
+    exp = [ref.end_splicejunction(p) for p in probs]
+    d = _first_diff(got, exp)
+    assert d is None, "problem %d (%s): gpu %s vs ref %s" % (d[0], _desc(probs[d[0]]), d[1], d[2])
+    assert sum(1 for s, pairs in exp if pairs is not None) > 500
