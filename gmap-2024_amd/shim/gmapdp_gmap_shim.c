@@ -7,7 +7,9 @@
  *   -Wl,--wrap=Dynprog_genome_setup,--wrap=Dynprog_single_gap,--wrap=Dynprog_end5_gap,
  *   -Wl,--wrap=Dynprog_end3_gap,--wrap=Dynprog_genome_gap,--wrap=Dynprog_cdna_gap
  *   -Wl,--wrap=Oligoindex_hr_tally,--wrap=Oligoindex_get_mappings
- *   -Wl,--wrap=Stage2_setup,--wrap=Stage2_compute  -lgmapdp
+ *   -Wl,--wrap=Stage2_setup,--wrap=Stage2_compute
+ *   -Wl,--wrap=Dynprog_end5_splicejunction,--wrap=Dynprog_end3_splicejunction
+ *   -Wl,--wrap=Dynprog_end5_known,--wrap=Dynprog_end3_known  -lgmapdp
  *
  * so that every call GMAP's stage 3 makes to these functions (stage3.c:9081,
  * 9275, 9510, 9531, 10244-10600, ...), and GMAP's per-read Stage2_compute (gmap.c:1208, 1323: seeding
@@ -15,8 +17,11 @@
  * (dynprog_single.h:22, dynprog_end.h:25/47, dynprog_genome.h:24, dynprog_cdna.h:12) and returns
  * the reference's List_T of Pair_T built in the caller's Pairpool
  * (Pairpool_push / Pairpool_push_gapholder, pairpool.c:180/375).  The setup
- * functions are wrapped only to learn Mode_T and the user gap penalties; the
- * reference's own setup still runs.  See INTEGRATION.md.
+ * functions are wrapped only to learn Mode_T, the user gap penalties and, with known splice sites
+ * (-s), the site list, the splice tries and the splicing IIT; the reference's own setup still runs.
+ * With -s, Dynprog_end5/3_known are restated here over the engine (the reference's
+ * Splicetrie_solve_end5/3 walks the tries and its splice-junction calls land on the engine too), and
+ * the genome gaps carry their windows' known sites.  See INTEGRATION.md.
  *
  * Semantics follow the GMAP build the shim is compiled into: a SIMD build
  * (HAVE_SSE2: gmap.sse42 / .avx2 / .avx512, dynprog_simd.c) gets GMAPDP_SIMD on
