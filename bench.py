@@ -606,7 +606,7 @@ def main():
         for li in range(len(b["names"])):
             m = np.zeros(b["info"][li][2], dtype=np.int32)
             lib.gmapdp_plan_launch_members(b["plan"], li, m.ctypes.data)
-            if b["kinds"][li] in (0, 2, 3, 4):
+            if b["kinds"][li] not in (1, 5):  # every class but the genome-gap kernels (gg, uxg)
                 b["bytes"].append(algorithmic_bytes(rl[m], gl[m], npairs[m], desc[m]))
                 b["cells"].append(None)
             else:

@@ -731,7 +731,9 @@ int gmapdp_plan_genome_gpu_problems (const gmapdp_plan *plan);
 int gmapdp_plan_genome_dev_index (const gmapdp_plan *plan, int j);
 /* 0: Dynprog_single_gap / end-gap kernel (one problem per wave), 1: Dynprog_genome_gap
  * kernel, 2: packed single/end-gap kernel (64/S narrow-band problems per wave; for these
- * gmapdp_plan_launch_info reports R = S and lds = the per-problem LDS slot) */
+ * gmapdp_plan_launch_info reports R = S and lds = the per-problem LDS slot), 3: SIMD-build
+ * single gaps (sx), 4: SIMD-build end gaps (uxe), 5: SIMD-build genome gaps (uxg),
+ * 7: single/end gaps whose band is wider than the query (lanes over query rows) */
 int gmapdp_plan_launch_kind (const gmapdp_plan *plan, int li);
 size_t gmapdp_plan_pair_capacity (const gmapdp_plan *plan);
 int gmapdp_plan_gpu_problems (const gmapdp_plan *plan);

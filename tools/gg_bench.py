@@ -2,7 +2,9 @@
 once and their launch classes run alone on one stream, timed with HIP events; variants are selected
 through the engine's environment switches, one child process each (they are read once per process).
 
-  python tools/gg_bench.py [--reads 10000] [--reps 5]
+  python tools/gg_bench.py [--reads 10000] [--reps 5] [--simd]
+
+--simd times the SIMD builds' genome gaps (uxg_kernel) on the same block.
 """
 import argparse
 import ctypes as C
@@ -18,7 +20,16 @@ VARIANTS = {"gg_kernel": {}, "gg_kernel_lds_dirs": {"GMAPDP_GG_LDS_DIRS_MAX": st
             "lib_base": {"GMAPDP_LIB": os.path.join(ROOT, "gmap-2024_amd", "lib_base", "libgmapdp.so")}}
 
 
-def child(reads, reps):
+def variant_env(v):
+    """A named variant, or lib_<x>: a build kept under gmap-2024_amd/lib_<x> (A/B of a kernel change)."""
+    if v in VARIANTS:
+        return VARIANTS[v]
+    if v.startswith("lib_"):
+        return {"GMAPDP_LIB": os.path.join(ROOT, "gmap-2024_amd", v, "libgmapdp.so")}
+    raise SystemExit("unknown variant " + v)
+
+
+def child(reads, reps, simd):
     import numpy as np
     import torch
     import gmapdp
@@ -31,6 +42,8 @@ def child(reads, reps):
     eng.set_genome(blocks=g.blocks, length=g.length)
     lib = eng.lib
     gp = d["genome"]
+    if simd:
+        gp["flags"] |= gmapdp.SIMD
     dev = torch.device("cuda", 0)
     d_q = torch.from_numpy(d["q"]).to(dev)
     d_sp = torch.from_numpy(d["sprob"]).to(dev)
@@ -73,16 +86,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reads", type=int, default=10000)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--simd", action="store_true")
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--variants", default=",".join(VARIANTS))
     a = ap.parse_args()
     if a.child:
-        return child(a.reads, a.reps)
+        return child(a.reads, a.reps, a.simd)
     res = {}
     for v in a.variants.split(","):
         r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "--reads", str(a.reads), "--reps",
-                            str(a.reps)], capture_output=True, text=True, timeout=300,
-                           env=dict(os.environ, **VARIANTS[v]))
+                            str(a.reps)] + (["--simd"] if a.simd else []), capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, **variant_env(v)))
         if r.returncode != 0:
             res[v] = {"error": r.stderr[-1500:]}
             break
