@@ -26,20 +26,21 @@ struct UxView {
   const uint64_t* wd;
   const int16_t* ws;
   int seg, B, t0, nrow, ncol, band, upper;
+  int lgB;  // log2(B): B is 16 or 32, so blocks are shifts, not divisions
   __device__ int step(int i, int x) const {  // -1 where no block of the fill wrote
     if (i < 0 || i > nrow || x < 0) return -1;
-    const int k = i / B, lo = k * B, hi = min(lo + B - 1, nrow);
+    const int k = i >> lgB, lo = k << lgB, hi = min(lo + B - 1, nrow);
     if (x < lo || x > min(hi + band, ncol)) return -1;
     return t0 + k * (B + band) + (x - lo);
   }
   __device__ uint32_t bit(int i, int x, int plane) const {
     const int s = step(i, x);
     if (s < 0) return 0u;
-    return (uint32_t)(wd[2 * (size_t)s + plane] >> (seg * B + (i % B))) & 1u;
+    return (uint32_t)(wd[2 * (size_t)s + plane] >> (seg * B + (i & (B - 1)))) & 1u;
   }
   __device__ int score(int i, int x) const {
     const int s = step(i, x);
-    return s < 0 ? 0 : (int)ws[(size_t)s * 64 + seg * B + (i % B)];
+    return s < 0 ? 0 : (int)ws[(size_t)s * 64 + seg * B + (i & (B - 1))];
   }
   __device__ int cell(int r, int c) const { return upper ? score(r, c) : score(c, r); }
   // traceback_walk's view: t 0 nogap=HORIZ, 1 nogap=VERT, 2 Egap=HORIZ, 3 Fgap=VERT
@@ -209,7 +210,7 @@ __device__ __forceinline__ UxFill ux_fill(unsigned char* smem, const CarveUx& cv
 
 __device__ __forceinline__ UxView ux_view(const uint64_t* wd, const int16_t* ws, int seg, int B, const UxFill& f,
                                           bool upper) {
-  return UxView{wd, ws, seg, B, f.t0, f.nrow, f.ncol, f.band, upper ? 1 : 0};
+  return UxView{wd, ws, seg, B, f.t0, f.nrow, f.ncol, f.band, upper ? 1 : 0, B == 32 ? 5 : 4};
 }
 
 }  // namespace gmapdp

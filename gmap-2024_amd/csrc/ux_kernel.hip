@@ -80,14 +80,33 @@ __global__ __launch_bounds__(64) void uxe_kernel(
   const bool indels = P.endalign == kQueryendIndels;
   const int init = indels ? NEG : 0;
   uint64_t key = 0;
-  for (int r = indels ? rlen : 1; r <= rlen; r++) {
-    const int clo = max(1, r - P.lband), chigh = min(r + P.uband, glen), cend = max(r - 1, chigh);
-    for (int c = clo + lane; c <= cend; c += 64) {
-      const int s = (c < r) ? VL.cell(r, c) : VU.cell(r, c);
-      if (late ? (s >= init) : (s > init)) {
-        const uint32_t ord = ((uint32_t)r << 12) | (uint32_t)c;
-        const uint64_t kk = ((uint64_t)(uint32_t)(s + (1 << 30)) << 24) | (late ? ord : 0xffffffu - ord);
-        key = kk > key ? kk : key;
+  auto take = [&](int r, int c, int s) {
+    if (late ? (s >= init) : (s > init)) {
+      const uint32_t ord = ((uint32_t)r << 12) | (uint32_t)c;
+      const uint64_t kk = ((uint64_t)(uint32_t)(s + (1 << 30)) << 24) | (late ? ord : 0xffffffu - ord);
+      key = kk > key ? kk : key;
+    }
+  };
+  if (indels) {  // one row
+    const int r = rlen, clo = max(1, r - P.lband), cend = max(r - 1, min(r + P.uband, glen));
+    for (int c = clo + lane; c <= cend; c += 64) take(r, c, (c < r) ? VL.cell(r, c) : VU.cell(r, c));
+  } else {
+    // the key is a total order, so the cells go in any order: the lower cells (c < r) of a row lie
+    // in one step of the lower fill; the upper ones are read by row blocks of the upper fill, lane
+    // = (row in the block, column group), B consecutive rows of one step per load
+    for (int r = 1; r <= rlen; r++) {
+      for (int c = max(1, r - P.lband) + lane; c < r; c += 64) take(r, c, VL.cell(r, c));
+    }
+    constexpr int NSEG = 64 / B;
+    const int i = lane & (B - 1), g = lane / B;
+    for (int lo = 0; lo <= rlen; lo += B) {
+      const int r = lo + i;
+      const bool row = r >= 1 && r <= rlen;
+      const int cu = row ? max(max(1, r - P.lband), r) : 1, ce = row ? max(r - 1, min(r + P.uband, glen)) : 0;
+      const int xend = min(lo + B - 1 + P.uband, glen);
+      for (int x0 = lo; x0 <= xend; x0 += NSEG) {
+        const int c = x0 + g;
+        if (c >= cu && c <= ce) take(r, c, VU.cell(r, c));
       }
     }
   }
@@ -246,44 +265,103 @@ __global__ __launch_bounds__(64) void uxg_kernel(
   double wp = 0.0;
   int ds = NEG, drL = 0x7fffffff;  // best dinucleotide (A) candidate: max prob, earliest
   double dp = 0.0;
-  for (int rL = 1; rL < rlen; rL++) {
+  // The candidates go in any order: the rule is a total order on (score, prob, scan order), and
+  // the A candidates' dinucleotide first-max rule holds per lane (a lane's rows ascend) and in the
+  // merge (earliest row wins ties).  Every cell is read where its fill stored it side by side:
+  // the upper-triangle cells by row blocks of the upper fill (lane = row in the block, column
+  // group), the lower-triangle cells by column blocks of the lower fill (lane = column in the
+  // block, row group), so one load reads B consecutive lanes of one step (32-64 B).  The
+  // diagonal cells, one per row and side, are staged in LDS first (the fills' block-row buffers
+  // are free by now).
+  auto take = [&](int s, double pr, int ordv, int rL, int cL, int cR) {
+    if (s > ws_ || (s == ws_ && (pr > wp || (pr == wp && ordv < word)))) {
+      ws_ = s; wp = pr; wrL = rL; wcL = cL; wcR = cR; word = ordv;
+    }
+  };
+  int* dgL = reinterpret_cast<int*>(smem + cv.L.bufU);  // 4 (gL + 1) >= 4 (rlen + 1) bytes
+  int* dgR = reinterpret_cast<int*>(smem + cv.R.bufU);
+  for (int r = lane; r <= rlen; r += 64) {
+    dgL[r] = VLu.cell(r, r);
+    dgR[r] = VRu.cell(r, r);
+  }
+  __syncthreads();
+  // A: cL = rL, cR = rR
+  for (int rL = 1 + lane; rL < rlen; rL += 64) {
     const int rR = rlen - rL;
-    const int cloL = max(1, rL - eb), chighL = min(rL + ubandL, gL - 1);
-    const int cloR = max(1, rR - eb), chighR = min(rR + ubandR, gR - 1);
-    const int dL = VLu.cell(rL, rL), dR = VRu.cell(rR, rR);
-    // B: cL = rL; lower cR in [cloR, e), upper cR in [e + 1, min(chighR, lim))
-    const int limB = rdist - rL;
-    const int eB = max(cloR, min(rR, limB));
-    const int nBl = eB - cloR, nBu = max(0, min(chighR, limB) - (eB + 1));
-    // C: cR = rR; lower cL in [cloL, e), upper cL in [e + 1, min(chighL, lim))
-    const int limC = rdist - rR;
-    const int eC = max(cloL, min(rL, limC));
-    const int nCl = eC - cloL, nCu = max(0, min(chighL, limC) - (eC + 1));
-    const int n = 1 + nBl + nBu + nCl + nCu;
-    for (int j = lane; j < n; j += 64) {
-      int cL, cR, sL, sR, part;
-      if (j == 0) {
-        cL = rL; cR = rR; sL = dL; sR = dR; part = 0;
-      } else if (j < 1 + nBl) {
-        cL = rL; cR = cloR + (j - 1); sL = dL; sR = VRl.cell(rR, cR); part = 1;
-      } else if (j < 1 + nBl + nBu) {
-        cL = rL; cR = eB + 1 + (j - 1 - nBl); sL = dL; sR = VRu.cell(rR, cR); part = 1;
-      } else if (j < 1 + nBl + nBu + nCl) {
-        cR = rR; cL = cloL + (j - 1 - nBl - nBu); sR = dR; sL = VLl.cell(rL, cL); part = 2;
-      } else {
-        cR = rR; cL = eC + 1 + (j - 1 - nBl - nBu - nCl); sR = dR; sL = VLu.cell(rL, cL); part = 2;
+    const int sI = isc[ldi[rL] & rdi[rR]];
+    const int s = dgL[rL] + sI + dgR[rR];
+    const double pr = pL[rL] + pR[rR];
+    take(s, pr, (rL << 14) | rL, rL, rL, rR);
+    if (sI > 0 && pr > dp) {  // first max of this lane's rows
+      dp = pr;
+      ds = s;
+      drL = rL;
+    }
+  }
+  {
+    const int i = lane & (B - 1), g = lane / B;
+    // B lower: cL = rL, cR in [cloR, eB) (cR < rR): column blocks of VRl, rows rR = x
+    for (int lo = 0; lo < rlen; lo += B) {
+      const int cR = lo + i;
+      const int xend = min(lo + B - 1 + eb, rlen - 1);
+      for (int x0 = lo + 1; x0 <= xend; x0 += NSEG) {
+        const int rR = x0 + g, rL = rlen - rR;
+        if (cR < 1 || rR > rlen - 1) continue;
+        const int cloR = max(1, rR - eb), eB = max(cloR, min(rR, rdist - rL));
+        if (cR >= cloR && cR < eB) {
+          const int sI = isc[ldi[rL] & rdi[cR]];
+          take(dgL[rL] + sI + VRl.cell(rR, cR), pL[rL] + pR[cR], (rL << 14) | (1 << 12) | cR, rL, rL, cR);
+        }
       }
-      const int sI = isc[ldi[cL] & rdi[cR]];
-      const int s = sL + sI + sR;
-      const double pr = pL[cL] + pR[cR];
-      const int ordv = (rL << 14) | (part << 12) | (part == 1 ? cR : cL);
-      if (s > ws_ || (s == ws_ && (pr > wp || (pr == wp && ordv < word)))) {
-        ws_ = s; wp = pr; wrL = rL; wcL = cL; wcR = cR; word = ordv;
+    }
+    // C lower: cR = rR, cL in [cloL, eC) (cL < rL): column blocks of VLl, rows rL = x
+    for (int lo = 0; lo < rlen; lo += B) {
+      const int cL = lo + i;
+      const int xend = min(lo + B - 1 + eb, rlen - 1);
+      for (int x0 = lo + 1; x0 <= xend; x0 += NSEG) {
+        const int rL = x0 + g, rR = rlen - rL;
+        if (cL < 1 || rL > rlen - 1) continue;
+        const int cloL = max(1, rL - eb), eC = max(cloL, min(rL, rdist - rR));
+        if (cL >= cloL && cL < eC) {
+          const int sI = isc[ldi[cL] & rdi[rR]];
+          take(VLl.cell(rL, cL) + sI + dgR[rR], pL[cL] + pR[rR], (rL << 14) | (2 << 12) | cL, rL, cL, rR);
+        }
       }
-      if (part == 0 && sI > 0 && pr > dp) {  // rows run in order in every lane: first max kept
-        dp = pr;
-        ds = s;
-        drL = rL;
+    }
+    // C upper: cR = rR, cL in [eC + 1, min(chighL, rdist - rR)): row blocks of VLu
+    for (int lo = 0; lo < rlen; lo += B) {
+      const int rL = lo + i, rR = rlen - rL;
+      int cu = 0, ce = 0;
+      if (rL >= 1 && rL < rlen) {
+        const int limC = rdist - rR;
+        cu = max(max(1, rL - eb), min(rL, limC)) + 1;
+        ce = min(min(rL + ubandL, gL - 1), limC);
+      }
+      const int xend = min(lo + B - 1 + ubandL, gL - 1);
+      for (int x0 = lo + 1; x0 < xend; x0 += NSEG) {
+        const int cL = x0 + g;
+        if (cL >= cu && cL < ce) {
+          const int sI = isc[ldi[cL] & rdi[rR]];
+          take(VLu.cell(rL, cL) + sI + dgR[rR], pL[cL] + pR[rR], (rL << 14) | (2 << 12) | cL, rL, cL, rR);
+        }
+      }
+    }
+    // B upper: cL = rL, cR in [eB + 1, min(chighR, rdist - rL)): row blocks of VRu
+    for (int lo = 0; lo < rlen; lo += B) {
+      const int rR = lo + i, rL = rlen - rR;
+      int cu = 0, ce = 0;
+      if (rR >= 1 && rR < rlen) {
+        const int limB = rdist - rL;
+        cu = max(max(1, rR - eb), min(rR, limB)) + 1;
+        ce = min(min(rR + ubandR, gR - 1), limB);
+      }
+      const int xend = min(lo + B - 1 + ubandR, gR - 1);
+      for (int x0 = lo + 1; x0 < xend; x0 += NSEG) {
+        const int cR = x0 + g;
+        if (cR >= cu && cR < ce) {
+          const int sI = isc[ldi[rL] & rdi[cR]];
+          take(dgL[rL] + sI + VRu.cell(rR, cR), pL[rL] + pR[cR], (rL << 14) | (1 << 12) | cR, rL, rL, cR);
+        }
       }
     }
   }
