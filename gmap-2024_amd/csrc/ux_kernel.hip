@@ -91,14 +91,19 @@ __global__ __launch_bounds__(64) void uxe_kernel(
     const int r = rlen, clo = max(1, r - P.lband), cend = max(r - 1, min(r + P.uband, glen));
     for (int c = clo + lane; c <= cend; c += 64) take(r, c, (c < r) ? VL.cell(r, c) : VU.cell(r, c));
   } else {
-    // the key is a total order, so the cells go in any order: the lower cells (c < r) of a row lie
-    // in one step of the lower fill; the upper ones are read by row blocks of the upper fill, lane
-    // = (row in the block, column group), B consecutive rows of one step per load
-    for (int r = 1; r <= rlen; r++) {
-      for (int c = max(1, r - P.lband) + lane; c < r; c += 64) take(r, c, VL.cell(r, c));
-    }
+    // the key is a total order, so the cells go in any order: the lower cells (c < r) by column
+    // blocks of the lower fill, the upper ones by row blocks of the upper fill, lane = (row or
+    // column in the block, group), B consecutive lanes of one step per load
     constexpr int NSEG = 64 / B;
     const int i = lane & (B - 1), g = lane / B;
+    for (int lo = 0; lo < rlen; lo += B) {  // lower cells by column blocks: c = lo + i, rows r = x
+      const int c = lo + i;
+      const int xend = min(lo + B - 1 + P.lband, rlen);
+      for (int x0 = lo + 1; x0 <= xend; x0 += NSEG) {
+        const int r = x0 + g;
+        if (c >= 1 && r <= rlen && c < r && c >= r - P.lband) take(r, c, VL.cell(r, c));
+      }
+    }
     for (int lo = 0; lo <= rlen; lo += B) {
       const int r = lo + i;
       const bool row = r >= 1 && r <= rlen;
