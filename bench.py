@@ -139,23 +139,52 @@ def genome_cells(gp, g_fills):
 # ---------------------------------------------------------------------------------------------------
 # committed profiles (profiles/*): PMC traffic, VALU instructions, rocprof average duration
 # ---------------------------------------------------------------------------------------------------
-def pmc_entry(key):
-    """The newest committed PMC summary's record of kernel `key` ('+'-joined names are summed), or
-    (None, None)."""
+def profile_record(kind, name):
+    """The committed record of `kind` the bench line cites: the one profiles/current.json names, else the
+    newest by the "recorded" time the writing tool stored in it (tools/pmc_summary.py, tools/e2e_timing.py);
+    records without one rank oldest.  Never by path name or file mtime (a checkout sets mtimes in checkout
+    order).  Returns (parsed json, path relative to ROOT) or (None, None)."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")), reverse=True):
+    try:
+        cur = json.load(open(os.path.join(ROOT, "profiles", "current.json"))).get(kind)
+    except (OSError, ValueError):
+        cur = None
+    paths = [os.path.join(ROOT, cur)] if cur else glob.glob(os.path.join(ROOT, "profiles", "*", name))
+    best = None
+    for path in paths:
         try:
-            ks = json.load(open(path))["kernels"]
-        except (OSError, ValueError, KeyError):
+            d = json.load(open(path))
+        except (OSError, ValueError):
             continue
-        parts = key.split("+")
-        if all(p in ks for p in parts):
-            rec = {}
-            for f in ("hbm_bytes_per_dispatch", "sq_SQ_INSTS_VALU_sum_avg", "avg_duration_ns"):
-                vals = [ks[p].get(f) for p in parts]
-                rec[f] = None if any(v is None for v in vals) else sum(vals)
-            return rec, os.path.relpath(path, ROOT)
-    return None, None
+        key = d.get("recorded") or ""
+        if best is None or key > best[0]:
+            best = (key, d, os.path.relpath(path, ROOT))
+    return (best[1], best[2]) if best else (None, None)
+
+
+def pmc_entry(key):
+    """The cited PMC summary's record of kernel `key` ('+'-joined names are summed), or (None, None)."""
+    d, src = profile_record("pmc_summary", "pmc_summary.json")
+    if not d:
+        return None, None
+    ks = d.get("kernels", {})
+    parts = key.split("+")
+    if not all(p in ks for p in parts):
+        return None, src
+    rec = {}
+    for f in ("hbm_bytes_per_dispatch", "sq_SQ_INSTS_VALU_sum_avg", "avg_duration_ns"):
+        vals = [ks[p].get(f) for p in parts]
+        rec[f] = None if any(v is None for v in vals) else sum(vals)
+    return rec, src
+
+
+def iso_entry(key):
+    """The cited rocprofv3 --kernel-trace --stats record of `bench.py --iso-kernel <key>` (the dominant
+    kernel's launches run alone, tools/pmc_summary.py --iso): {avg_duration_ns, dispatches, ...}."""
+    d, src = profile_record("iso_summary", "iso_summary.json")
+    if not d or d.get("kernel") != key:
+        return None, src
+    return d, src
 
 
 def rocprof_name(kind, R, dl, lds=0):
@@ -176,31 +205,23 @@ def rocprof_name(kind, R, dl, lds=0):
 
 
 def latest_e2e():
-    """The newest committed GMAP end-to-end record (tools/e2e_timing.py, profiles/*/e2e.json): the unmodified
-    gmap and the drop-in on the same reads and host cores."""
-    import glob
-    best = None
-    for path in glob.glob(os.path.join(ROOT, "profiles", "*", "e2e.json")):
-        try:
-            d = json.load(open(path))
-            runs = d["runs"]
-        except (OSError, ValueError, KeyError):
-            continue
-        cpu = [r for r in runs if "gpu" not in r["program"]]
-        gpu = [r for r in runs if "gpu" in r["program"]]
-        if not cpu or not gpu:
-            continue
-        rec = {"source": os.path.relpath(path, ROOT), "reads": d.get("reads"),
-               "cpu_gmap_reads_per_s": max(r["reads_per_s"] for r in cpu),
-               "cpu_gmap_threads": max(cpu, key=lambda r: r["reads_per_s"])["threads"],
-               "drop_in_reads_per_s": max(r["reads_per_s"] for r in gpu),
-               "drop_in_threads": max(gpu, key=lambda r: r["reads_per_s"])["threads"],
-               "outputs_identical": d.get("outputs_identical"), "mtime": os.path.getmtime(path)}
-        if best is None or rec["mtime"] > best["mtime"]:
-            best = rec
-    if best:
-        best.pop("mtime")
-    return best
+    """The cited GMAP end-to-end record (tools/e2e_timing.py, profiles/*/e2e.json; profile_record's rule):
+    the unmodified gmap and the drop-in on the same reads and host cores."""
+    d, src = profile_record("e2e", "e2e.json")
+    try:
+        runs = d["runs"]
+    except (TypeError, KeyError):
+        return None
+    cpu = [r for r in runs if "gpu" not in r["program"]]
+    gpu = [r for r in runs if "gpu" in r["program"]]
+    if not cpu or not gpu:
+        return None
+    return {"source": src, "recorded": d.get("recorded"), "reads": d.get("reads"),
+            "cpu_gmap_reads_per_s": max(r["reads_per_s"] for r in cpu),
+            "cpu_gmap_threads": max(cpu, key=lambda r: r["reads_per_s"])["threads"],
+            "drop_in_reads_per_s": max(r["reads_per_s"] for r in gpu),
+            "drop_in_threads": max(gpu, key=lambda r: r["reads_per_s"])["threads"],
+            "outputs_identical": d.get("outputs_identical")}
 
 
 def like_for_like(out, pcie_ms, up, down):
@@ -342,6 +363,11 @@ def main():
     ap.add_argument("--simd", action="store_true", help="the SIMD builds' semantics (gmap.avx2: sx/uxe/uxg kernels)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dry-run", action="store_true", help="CPU only: launcher, gloo process group, sharding")
+    ap.add_argument("--iso-kernel", default=None,
+                    help="profiling mode: run only this kernel template's launch classes, one launch at a time on one "
+                         "stream (what the line's roofline times), print their timing and exit; run under rocprofv3 "
+                         "--kernel-trace --stats for the committed isolated average (tools/profile.sh iso)")
+    ap.add_argument("--iso-reps", type=int, default=3)
     args = ap.parse_args()
 
     if args.reads is None:
@@ -521,6 +547,71 @@ def main():
 
     mk = lambda: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))  # noqa: E731
 
+    def class_outputs(b, res, gres):
+        """Per problem of block b: pairs emitted (single/end, genome), genome_gap_simple answered, and the
+        genome gaps that ran both fills, from the results the launches left in res / gres."""
+        d = b["d"]
+        ns, ne, ng = b["ns"], b["ne"], b["ng"]
+        nprob = ns + ne
+        dev_index = np.array([lib.gmapdp_plan_dev_index(b["plan"], i) for i in range(nprob)], dtype=np.int64)
+        gdev_index = np.array([lib.gmapdp_plan_genome_dev_index(b["plan"], j) for j in range(ng)], dtype=np.int64)
+        npairs = np.zeros(nprob, dtype=np.int64)
+        npairs[dev_index >= 0] = res["npairs"][dev_index[dev_index >= 0]]
+        gnp = np.zeros(ng, dtype=np.int64)
+        gsel = gdev_index >= 0
+        gnp[gsel] = gres["npairs"][gdev_index[gsel]]
+        # genome_gap_simple answered (dynprog_genome.c:3479): its result sets exonhead = new_rightgenomepos
+        gsimple = np.zeros(ng, dtype=bool)
+        gr = gres[gdev_index[gsel]]
+        gsimple[gsel] = (gr["npairs"] > 0) & (gr["exonhead"] == gr["new_rightgenomepos"])
+        _ = d
+        return npairs, gnp, gsimple, gsel & ~gsimple
+
+    def class_bytes(b, li, npairs, gnp, g_fills):
+        """Algorithmic bytes and banded cells (genome-gap classes) of launch class li."""
+        d = b["d"]
+        sp, ep, gp = d["single"], d["end"], d["genome"]
+        ns, ne = b["ns"], b["ne"]
+        nprob = ns + ne
+        m = np.zeros(b["info"][li][2], dtype=np.int32)
+        lib.gmapdp_plan_launch_members(b["plan"], li, m.ctypes.data)
+        if b["kinds"][li] not in (1, 5):  # every class but the genome-gap kernels (gg, uxg)
+            rl = np.concatenate([sp["rlength"], np.minimum(ep["rlength"], 660)]).astype(np.int64)
+            gl = np.concatenate([sp["glength"], np.minimum(ep["glength"], 2000)]).astype(np.int64)
+            desc = np.concatenate([np.full(ns, gmapdp.PROBLEM_DTYPE.itemsize),
+                                   np.full(ne, gmapdp.END_PROBLEM_DTYPE.itemsize)])
+            return algorithmic_bytes(rl[m], gl[m], npairs[m], desc[m]), None
+        j = m - nprob
+        return genome_algorithmic_bytes(gp[j], gnp[j]), int(genome_cells(gp[j], g_fills[j]).sum())
+
+    def fetch_results(b):
+        res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=gmapdp.RESULT_DTYPE)[:b["ngpu"]]
+        gres = np.frombuffer(d_gres.cpu().numpy().tobytes(), dtype=gmapdp.GENOME_RESULT_DTYPE)[:b["nggpu"]]
+        return res, gres
+
+    def iso_launches(name, reps, with_bytes):
+        """Every launch class of kernel `name`, one launch at a time on one stream, HIP events around each
+        (on the stream it runs on); per dispatch: (ms, algorithmic bytes, cells)."""
+        out = []
+        with torch.cuda.stream(stream):
+            for rep in range(reps):
+                for b in B:
+                    for li, nm in enumerate(b["names"]):
+                        if nm != name:
+                            continue
+                        e0, e1 = mk()
+                        e0.record(stream)
+                        launch(b, li, stream)
+                        e1.record(stream)
+                        torch.cuda.synchronize()
+                        if with_bytes and rep == 0:
+                            npairs, gnp, _, g_fills = class_outputs(b, *fetch_results(b))
+                            b.setdefault("iso_bytes", {})[li] = class_bytes(b, li, npairs, gnp, g_fills)
+                        nbytes, cells = b["iso_bytes"][li] if with_bytes else (b["bytes"][li], b["cells"][li])
+                        out.append((e0.elapsed_time(e1), nbytes, cells or 0))
+        return out
+
+
     def timed(steps, warmup, **kw):
         with torch.cuda.stream(stream):
             for k in range(warmup):
@@ -541,6 +632,23 @@ def main():
         if world > 1:
             elapsed = shard.max_over_ranks(elapsed, dist, device=dev)
         return elapsed, evs
+
+    if args.iso_kernel:
+        if not any(args.iso_kernel in b["names"] for b in B):
+            raise SystemExit("bench: no launch class of %s in this workload" % args.iso_kernel)
+        rows = iso_launches(args.iso_kernel, args.iso_reps, True)
+        ms = [r[0] for r in rows]
+        nbytes = float(np.mean([r[1] for r in rows]))
+        if rank == 0:
+            print(json.dumps({"iso_kernel": args.iso_kernel, "dispatches": len(rows), "ms_per_launch": float(np.mean(ms)),
+                              "ms_min": min(ms), "ms_max": max(ms), "algorithmic_bytes_per_launch": nbytes,
+                              "achieved_gbs": nbytes / (np.mean(ms) * 1e-3) / 1e9,
+                              "cells_per_launch": float(np.mean([r[2] for r in rows]))}), flush=True)
+        for b in B:
+            lib.gmapdp_plan_destroy(b["plan"])
+            lib.gmapdp_stage2_plan_destroy(b["oplan"])
+            lib.gmapdp_microexon_plan_destroy(b["mplan"])
+        return
 
     # every block once before anything is timed: the context's grow-only scratch reaches its size
     with torch.cuda.stream(stream):
@@ -575,44 +683,16 @@ def main():
         torch.cuda.synchronize()
         d = b["d"]
         sp, ep, gp, op, mp = d["single"], d["end"], d["genome"], d["oligo"], d["microexon"]
-        ns, ne, ng = b["ns"], b["ne"], b["ng"]
-        res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=gmapdp.RESULT_DTYPE)[:b["ngpu"]]
-        gres = np.frombuffer(d_gres.cpu().numpy().tobytes(), dtype=gmapdp.GENOME_RESULT_DTYPE)[:b["nggpu"]]
+        res, gres = fetch_results(b)
         s2res = np.frombuffer(d_s2res.cpu().numpy().tobytes(), dtype=gmapdp.STAGE2_RESULT_DTYPE)[:len(op)]
         mres = np.frombuffer(d_mres.cpu().numpy().tobytes(), dtype=gmapdp.MICROEXON_RESULT_DTYPE)[:len(mp)]
         # size-independent invariants of the step's outputs (the oracle parity of this same workload is
         # tests/test_gpu_bench_workload.py)
         assert np.all(res["npairs"] >= 0) and np.all(gres["npairs"] >= 0) and np.all(s2res["status"] >= 0)
         assert np.all(mres["ncandidates"] >= 0) and np.all(mres["cand_offset"] >= 0)
-        nprob = ns + ne
-        dev_index = np.array([lib.gmapdp_plan_dev_index(b["plan"], i) for i in range(nprob)])
-        gdev_index = np.array([lib.gmapdp_plan_genome_dev_index(b["plan"], j) for j in range(ng)])
-        npairs = np.zeros(nprob, dtype=np.int64)
-        npairs[dev_index >= 0] = res["npairs"][dev_index[dev_index >= 0]]
-        gnp = np.zeros(ng, dtype=np.int64)
-        gsel = gdev_index >= 0
-        gnp[gsel] = gres["npairs"][gdev_index[gsel]]
-        # genome_gap_simple answered (dynprog_genome.c:3479): its result sets exonhead = new_rightgenomepos
-        gsimple = np.zeros(ng, dtype=bool)
-        gr = gres[gdev_index[gsel]]
-        gsimple[gsel] = (gr["npairs"] > 0) & (gr["exonhead"] == gr["new_rightgenomepos"])
-        g_fills = gsel & ~gsimple
-        b["gcells"] = genome_cells(gp, g_fills)
+        npairs, gnp, gsimple, g_fills = class_outputs(b, res, gres)
         cells_total += dp_cells(sp, ep, gp, g_fills)
-        rl = np.concatenate([sp["rlength"], np.minimum(ep["rlength"], 660)]).astype(np.int64)
-        gl = np.concatenate([sp["glength"], np.minimum(ep["glength"], 2000)]).astype(np.int64)
-        desc = np.concatenate([np.full(ns, gmapdp.PROBLEM_DTYPE.itemsize), np.full(ne, gmapdp.END_PROBLEM_DTYPE.itemsize)])
-        b["bytes"], b["cells"] = [], []
-        for li in range(len(b["names"])):
-            m = np.zeros(b["info"][li][2], dtype=np.int32)
-            lib.gmapdp_plan_launch_members(b["plan"], li, m.ctypes.data)
-            if b["kinds"][li] not in (1, 5):  # every class but the genome-gap kernels (gg, uxg)
-                b["bytes"].append(algorithmic_bytes(rl[m], gl[m], npairs[m], desc[m]))
-                b["cells"].append(None)
-            else:
-                j = m - nprob
-                b["bytes"].append(genome_algorithmic_bytes(gp[j], gnp[j]))
-                b["cells"].append(int(b["gcells"][j].sum()))
+        b["bytes"], b["cells"] = zip(*[class_bytes(b, li, npairs, gnp, g_fills) for li in range(len(b["names"]))])
         b["chain_bytes"] = chain_algorithmic_bytes(op, s2res)
         checks["pairs"] += int(npairs.sum() + gnp.sum())
         checks["genome_gaps_bridged"] += int((gnp > 0).sum())
@@ -635,23 +715,11 @@ def main():
     dms, dn, dbytes = per_kernel[dominant]
 
     # ---- the dominant kernel alone (its launches of every block, one at a time on one stream) ----
-    iso_ms, iso_n, iso_bytes, iso_cells = 0.0, 0, 0, 0
-    reps = 3
-    with torch.cuda.stream(stream):
-        for _ in range(reps):
-            for b in B:
-                for li, name in enumerate(b["names"]):
-                    if name != dominant:
-                        continue
-                    e0, e1 = mk()
-                    e0.record(stream)
-                    launch(b, li, stream)
-                    e1.record(stream)
-                    torch.cuda.synchronize()
-                    iso_ms += e0.elapsed_time(e1)
-                    iso_n += 1
-                    iso_bytes += b["bytes"][li]
-                    iso_cells += b["cells"][li] or 0
+    rows = iso_launches(dominant, 3, False)
+    iso_n = len(rows)
+    iso_ms = sum(r[0] for r in rows)
+    iso_bytes = sum(r[1] for r in rows)
+    iso_cells = sum(r[2] for r in rows)
     kms = iso_ms / iso_n
     kbytes = iso_bytes / iso_n
     kcells = iso_cells / iso_n
@@ -660,6 +728,8 @@ def main():
     traffic = pmc["hbm_bytes_per_dispatch"] if pmc else None
     valu = pmc["sq_SQ_INSTS_VALU_sum_avg"] if pmc else None
     prof_ms = pmc["avg_duration_ns"] / 1e6 if pmc and pmc.get("avg_duration_ns") else None
+    iso, isrc = iso_entry(dominant)
+    iso_prof_ms = iso["avg_duration_ns"] / 1e6 if iso else None
 
     # ---- PCIe: one block's inputs up and outputs down through pinned host memory (outside the step) ----
     b = B[0]
@@ -728,6 +798,16 @@ def main():
                                "dispatches, after the timed region); in the timed steps, which share the CUs "
                                "four streams wide, its launches average %.3f ms" % (iso_n, dms / dn),
                      "kernel_ms_per_launch_in_step": dms / dn, "rocprof_avg_ms_committed": prof_ms,
+                     "rocprof_isolated": {"source": isrc, "avg_ms": iso_prof_ms,
+                                          "dispatches": iso["dispatches"] if iso else None,
+                                          "algorithmic_bytes_per_launch": iso.get("algorithmic_bytes_per_launch")
+                                          if iso else None,
+                                          "frac": (iso["algorithmic_bytes_per_launch"] / (iso_prof_ms * 1e-3) / 1e9
+                                                   / HBM_PEAK_GBS) if iso and iso.get("algorithmic_bytes_per_launch")
+                                          else None,
+                                          "live_over_rocprof": kms / iso_prof_ms if iso_prof_ms else None,
+                                          "note": "rocprofv3 --kernel-trace --stats of `bench.py --iso-kernel <kernel>` "
+                                                  "(the same isolated launches this line times with HIP events)"},
                      "step_algorithmic_gbs": sum(e[2] for e in per_kernel.values()) / args.steps
                                              / (ms_step * 1e-3) / 1e9,
                      "valu": {"insts_per_launch": valu,

@@ -254,6 +254,7 @@ struct S2W {
   uint32_t maxintronlen;
 #ifdef GMAPDP_OI_TIMING
   unsigned long long n_cand = 0, n_fast = 0, n_slow = 0, n_multi = 0;  // candidates, fast/multi windows, slow evals
+  unsigned long long n_runs = 0, n_runpos = 0, n_onepos = 0, n_multpos = 0;  // runs, their members, other positions
 #define S2_TALLY(f, v) (W.f += (v))
 #else
 #define S2_TALLY(f, v) (void)0
@@ -885,6 +886,40 @@ __device__ __forceinline__ void s2_mult(S2W& W, int q, int offq, int low, int hi
   wave_sync();
 }
 
+// the members of a run (s2_sweep): lane = query position cb + lane, members Mm; links, active lists and
+// ring slots (its own function: the sweep's register budget is full)
+struct S2Run {
+  int score, consec, tracei, root, hit, q, cb, pushed, np;
+};
+__device__ __forceinline__ void s2_run_write(S2Hit* hits, int* alist, int lane, int off, uint32_t map, int qq,
+                                                       S2Run L, uint64_t Mm) {
+  if (!((Mm >> lane) & 1ull)) return;
+  const uint64_t below = Mm & ((1ull << lane) - 1ull);
+  const int r = __popcll(below);
+  const int pl = below ? 63 - __clzll((long long)below) : -1;  // the previous member's lane
+  const int dq = qq - L.q;
+  S2Hit& x = hits[off];
+  x.consec = L.consec + dq;
+  x.root = L.root;
+  x.fpos = pl >= 0 ? L.cb + pl : L.q;
+  x.fhit = pl >= 0 ? 0 : L.hit;
+  x.tracei = L.tracei;
+  x.score = L.score + dq;
+  alist[off] = 0;
+  const int sl = (L.pushed + r) & (kS2Ring - 1);
+  s2_ring.map[sl] = map;
+  s2_ring.score[sl] = L.score + dq;
+  s2_ring.consec[sl] = L.consec + dq;
+  s2_ring.tracei[sl] = L.tracei;
+  s2_ring.root[sl] = L.root;
+  s2_ring.hit[sl] = 0;
+  const int ms = (L.np + r) & (kS2Meta - 1);
+  s2_ring.eq[ms] = qq;
+  s2_ring.en[ms] = 1;
+  s2_ring.eoff[ms] = off;
+  s2_ring.estart[ms] = L.pushed + r;
+}
+
 // the sweep (stage2.c:3746-4080)
 __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, const uint32_t* minact, const uint32_t* maxact,
                          int qstart, int qend) {
@@ -937,6 +972,57 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
       m_map0 = m_n > 0 ? W.hits[m_off].map : 0u;
     }
     const int j = q - cb;
+    // A run on the last processed entry's diagonal.  When that entry has one active hit whose consecutive
+    // count reaches ENOUGH_CONSECUTIVE by the next position on its diagonal, every following position
+    // whose only hit in the active range sits on that diagonal takes section A's link (stage2.c:1126-1168)
+    // and skips section D (:1191): score and consec grow by the query distance, root and tracei carry
+    // over, the link points at the previous such position, the hit stays active (score > 0), and the
+    // grand lookback (:3983) does not apply (the link has a predecessor).  Positions without hits in
+    // between change nothing (they are not processed entries).  So the chunk's run of such positions is
+    // written lane-parallel in one step: links, active lists, the ring, the grand best.
+    if (last.n == 1 && last.inring && nskipped <= kS2MaxSkipped) {
+      const int ls = last.start & (kS2Ring - 1);
+      const uint32_t lmap = s2_u(s2_ring.map[ls]);
+      const int lcons = s2_u(s2_ring.consec[ls]);
+      const uint32_t dg = lmap - (uint32_t)last.q;
+      const int qq = cb + lane;
+      const bool one = m_n == 1 && m_map0 >= m_min && m_map0 <= m_max && m_map0 - (uint32_t)qq == dg;
+      const uint64_t from_j = ~0ull << j;
+      const uint64_t notE = ~ballot(qq <= qend && (m_n <= 0 || one)) & from_j;
+      const int stop = notE ? __ffsll((long long)notE) - 1 : 64;
+      const uint64_t inrun = stop >= 64 ? from_j : (from_j & ((1ull << stop) - 1ull));
+      const uint64_t Mm = ballot(one) & inrun;
+      if (Mm && lcons + (cb + __ffsll((long long)Mm) - 1 - last.q) >= kS2EnoughConsec) {
+        const int lscore = s2_u(s2_ring.score[ls]), ltr = s2_u(s2_ring.tracei[ls]), lroot = s2_u(s2_ring.root[ls]),
+                  lhit = s2_u(s2_ring.hit[ls]);
+        s2_run_write(W.hits, W.alist, lane, m_off, m_map0, qq, {lscore, lcons, ltr, lroot, lhit, last.q, cb, W.pushed, np}, Mm);
+        if ((inrun >> lane) & 1ull) W.actn[qq] = (int)((Mm >> lane) & 1ull);
+        const int cnt = __popcll(Mm);
+        S2_TALLY(n_runs, 1);
+        S2_TALLY(n_runpos, cnt);
+        const int ll = 63 - __clzll((long long)Mm);
+        const int lq = cb + ll;
+        const int lsc = lscore + (lq - last.q);
+        if (lsc >= grand_score) {  // consec >= ENOUGH_CONSECUTIVE > EXON_DEFN
+          grand_score = lsc;
+          grand_q = lq;
+          grand_hit = 0;
+          grand_map = (uint32_t)__builtin_amdgcn_readlane((int)m_map0, ll);
+        }
+        const int loff = __builtin_amdgcn_readlane(m_off, ll);
+        W.pushed += cnt;
+        np += cnt;
+        last = s2_mkentry(W, lq, 1, loff, W.pushed - 1);
+        nskipped = 0;
+        min_hits = 1000000;
+        specific_q = -1;
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __builtin_amdgcn_wave_barrier();
+        S2_TACC(t_one);
+        q = cb + stop;
+        continue;
+      }
+    }
     const int n = __builtin_amdgcn_readlane(m_n, j);
     const int offq = __builtin_amdgcn_readlane(m_off, j);
     const uint32_t mn = (uint32_t)__builtin_amdgcn_readlane((int)m_min, j);
@@ -1250,6 +1336,7 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
       }
     }
     if (high - low == 1) S2_TACC(t_one); else S2_TACC(t_mult);
+    if (high - low == 1) S2_TALLY(n_onepos, 1); else if (high - low > 1) S2_TALLY(n_multpos, 1);
     if (lane == 0) W.actn[q] = nact;
     if ((q == cb + j ? n : npos(q)) > 0) {  // the prefetched count unless the MAX_SKIPPED jump moved q
       const bool ringed = high - low <= kS2Ring;
@@ -1281,7 +1368,13 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
   S2_COUNT(13, W.n_cand);
   S2_COUNT(14, W.n_fast);
   S2_COUNT(15, W.n_slow);
-  if (threadIdx.x == 0) atomicAdd(&g_s2_marks[1][15], W.n_multi);
+  if (threadIdx.x == 0) {
+    atomicAdd(&g_s2_marks[1][15], W.n_multi);
+    atomicAdd(&g_s2_marks[1][8], W.n_runs);
+    atomicAdd(&g_s2_marks[1][9], W.n_runpos);
+    atomicAdd(&g_s2_marks[1][10], W.n_onepos);
+    atomicAdd(&g_s2_marks[1][11], W.n_multpos);
+  }
 #endif
 }
 
@@ -1698,7 +1791,7 @@ __global__ __launch_bounds__(64) void s2a_kernel(
 }
 
 // the lookback sweep (align_compute_scores_lookback) of the calls s2a_kernel left chained
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void s2b_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void s2b_kernel(
     const DevStage2Problem* __restrict__ probs, const uint32_t* __restrict__ blocks, uint64_t nwords,
     const char* __restrict__ qseq, const char* __restrict__ quc, const gmapdp_oligo_result* __restrict__ ores,
     const int32_t* __restrict__ npos_all, const int32_t* __restrict__ map_all, const uint32_t* __restrict__ table_all,

@@ -81,6 +81,7 @@ def main():
             print(json.dumps(out["runs"][-1]), file=sys.stderr, flush=True)
     base = next(iter(sams.values())) if a.skip_cpu else sams[("gmap_%s" % a.build, min(cpu_t), "cpu")]
     out["outputs_identical"] = all(v == base for v in sams.values())
+    out["recorded"] = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())  # bench.py selects records by this
     print(json.dumps(out))
 
 

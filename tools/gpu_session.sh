@@ -1,0 +1,36 @@
+#!/bin/bash
+# One GPU-box session (gpurun -- 'bash tools/gpu_session.sh <tag> <steps...>'): each step under its own time
+# limit, the session ends at the first failure.  Outputs under gpurun_out/<tag>/.
+#   tests          the whole -m gpu suite
+#   tests:<k>      the -m gpu tests matching -k <k>
+#   bench:<lib>    bench.py --steps 20 --no-cpu-baseline with gmap-2024_amd/<lib>/libgmapdp.so
+#   benchfull      bench.py as the driver runs it (CPU baseline included)
+#   simd:<lib>     bench.py --simd;  c4:<lib>  bench.py --config 4
+#   iso:<kernel>   tools/profile.sh <tag>_iso iso <kernel>  (the dominant kernel's launches alone)
+#   prof           tools/profile.sh <tag>  (kernel stats + PMC passes of the bench step)
+#   smoke          __graft_entry__.smoke()
+#   e2e:<b>:<n>    tools/e2e_timing.py --build <b> --reads <n> (gmap -t 16 vs the drop-in at -t 512)
+#   s2timing       tools/oi_timing.py s2 (the GMAPDP_OI_TIMING build: stage-2 sweep phases and counts)
+set -o pipefail
+TAG=$1
+shift
+O=gpurun_out/$TAG
+mkdir -p $O
+for S in "$@"; do
+  echo "[session] $S $(date +%T)"
+  case "$S" in
+    tests) timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $O/gputest.txt 2>&1 || exit 11 ;;
+    tests:*) timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu -k "${S#tests:}" tests > $O/gputest_k.txt 2>&1 || exit 12 ;;
+    bench:*) L=${S#bench:}; GMAPDP_LIB=$PWD/gmap-2024_amd/$L/libgmapdp.so timeout -k 10 400 python bench.py --steps 20 --no-cpu-baseline > $O/bench_$L.json 2> $O/bench_$L.err || exit 13 ;;
+    simd:*) L=${S#simd:}; GMAPDP_LIB=$PWD/gmap-2024_amd/$L/libgmapdp.so timeout -k 10 400 python bench.py --steps 20 --simd --no-cpu-baseline > $O/simd_$L.json 2> $O/simd_$L.err || exit 14 ;;
+    c4:*) L=${S#c4:}; GMAPDP_LIB=$PWD/gmap-2024_amd/$L/libgmapdp.so timeout -k 10 600 python bench.py --steps 10 --config 4 --no-cpu-baseline > $O/c4_$L.json 2> $O/c4_$L.err || exit 15 ;;
+    benchfull) timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err || exit 16 ;;
+    iso:*) bash tools/profile.sh ${TAG}_iso iso "${S#iso:}" > $O/prof_iso.txt 2>&1 || exit 17 ;;
+    prof) bash tools/profile.sh $TAG > $O/prof.txt 2>&1 || exit 18 ;;
+    e2e:*) IFS=: read -r _ B N <<< "$S"; timeout -k 10 900 python tools/e2e_timing.py --build $B --reads $N --threads 16 --gpu-threads 512 > $O/e2e_${B}_$N.json 2> $O/e2e_${B}_$N.err || exit 20 ;;
+    s2timing) timeout -k 10 300 python tools/oi_timing.py s2 > $O/s2timing.json 2> $O/s2timing.err || exit 21 ;;
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || exit 19 ;;
+    *) echo "unknown step $S"; exit 2 ;;
+  esac
+done
+echo "[session] ok $(date +%T)"

@@ -92,6 +92,10 @@ def main_s2(reads=10000):
              "per_wave_fast_windows": float(marks[14]) / max(int(c[0]), 1),
              "per_wave_slow_entry_evals": float(marks[15]) / max(int(c[0]), 1),
              "per_wave_multi_windows": float(marks[31]) / max(int(c[0]), 1),
+             "per_wave_runs": float(marks[24]) / max(int(c[0]), 1),
+             "per_wave_run_positions": float(marks[25]) / max(int(c[0]), 1),
+             "per_wave_one_hit_positions": float(marks[26]) / max(int(c[0]), 1),
+             "per_wave_multi_hit_positions": float(marks[27]) / max(int(c[0]), 1),
              "slowest": [[float(us[i]), int(npq[i]), int(nh[i])] for i in np.argsort(-us)[:8]]}
     print(json.dumps({"waves": [int(x) for x in c[:8]], "phases": {n: round(d / tot, 4) for n, d in zip(S2_PHASES, dur)},
                       "mean_wave_us": tot / 1e2 / max(int(c[0]), 1), "status": np.bincount(res["status"] + 3).tolist(),

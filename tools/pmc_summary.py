@@ -16,6 +16,7 @@ import os
 import re
 import shutil
 import sys
+import time
 from collections import defaultdict
 
 
@@ -47,7 +48,7 @@ def find(root, sub, name):
     return None
 
 
-def main(src, dst):
+def main(src, dst, iso=False):
     os.makedirs(dst, exist_ok=True)
     stats = find(src, "stats", "run_kernel_stats.csv")
     kern = {}
@@ -82,7 +83,10 @@ def main(src, dst):
     for e in kern.values():
         if "fetch_size_kb_avg" in e and "write_size_kb_avg" in e:
             e["hbm_bytes_per_dispatch"] = (2 * e["fetch_size_kb_avg"] + e["write_size_kb_avg"]) * 1024
+    if iso:
+        return write_iso(src, dst, kern)
     summary = {
+        "recorded": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),  # bench.py selects summaries by this
         "command": "python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline (under rocprofv3, tools/profile.sh)",
         "hbm_bytes_rule": "2*FETCH_SIZE + WRITE_SIZE, KB -> bytes x1024 (MI355X_MICROARCH.md HBM: gfx950 "
                           "FETCH_SIZE counts half of wide reads)",
@@ -95,5 +99,33 @@ def main(src, dst):
     print("wrote", dst, "kernels:", ", ".join(kern))
 
 
+def write_iso(src, dst, kern):
+    """iso_summary.json: the rocprofv3 record of `bench.py --iso-kernel K` (K's launch classes run alone, one
+    launch at a time) -- the average duration the bench line's roofline cites, the bench's own HIP-event
+    timing and algorithmic bytes of the same launches, and that kernel's counters (per dispatch)."""
+    bench = {}
+    try:
+        bench = json.loads(open(os.path.join(src, "iso_bench.json")).read().strip().splitlines()[-1])
+    except (OSError, ValueError, IndexError):
+        pass
+    k = bench.get("iso_kernel")
+    e = kern.get(k, {}) if k else {}
+    out = {"recorded": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
+           "command": "rocprofv3 --kernel-trace --stats -- python3 bench.py --iso-kernel '%s' --iso-reps 3 "
+                      "(tools/profile.sh <tag> iso)" % k,
+           "kernel": k, "dispatches": e.get("dispatches"), "avg_duration_ns": e.get("avg_duration_ns"),
+           "algorithmic_bytes_per_launch": bench.get("algorithmic_bytes_per_launch"),
+           "bench_hip_event_ms_per_launch": bench.get("ms_per_launch"),
+           "hbm_rule": "2*FETCH_SIZE + WRITE_SIZE, KB -> bytes x1024 (MI355X_MICROARCH.md)",
+           "counters": e, "other_kernels": {n: v for n, v in kern.items() if n != k}}
+    if out["avg_duration_ns"] and out["algorithmic_bytes_per_launch"]:
+        out["achieved_gbs"] = out["algorithmic_bytes_per_launch"] / out["avg_duration_ns"]
+        out["frac_of_8tbs"] = out["achieved_gbs"] / 8000.0
+    with open(os.path.join(dst, "iso_summary.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print("wrote", os.path.join(dst, "iso_summary.json"), "kernel:", k)
+
+
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    args = [a for a in sys.argv[1:] if a != "--iso"]
+    main(args[0], args[1], iso="--iso" in sys.argv[1:])
