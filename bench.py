@@ -12,8 +12,9 @@ Workload (gmap-2024_amd/gmapdp/workload.py):
   * configs[4] (--config 4; gmapl, "500k 5-kb Iso-Seq-style reads vs 17-Gb wheat genome"): 5-kb reads of
     10 exons with 1 % substitutions + 1 % indels against a 17-Gnt wheat-layout genome (6.4 GB packed,
     universal coordinates past 2^32), the per-read call mix of that read shape (workload.ISOSEQ5K).
-The splice probabilities of the genome gaps and the MaxEnt scores between the microexon search and its
-choice are synthetic device inputs (the engine takes MaxEnt as an input).
+The splice probabilities of the genome gaps and the microexon candidates' sites are GMAP's MaxEnt models
+evaluated by the engine on the device inside the step (gmapdp_plan_bind_genome_maxent, the microexon plan
+with device probabilities); the genome-gap introns carry strong planted splice sites.
 
 Read stream: blocks of --reads reads, each generated from its own seeds; rank r of N takes the blocks
 b % N == r (GMAP's --part=r/N rule, inbuffer.c:283, per block) and cycles through --batches of them, so
@@ -60,8 +61,14 @@ T_START = time.perf_counter()
 def progress(msg):
     """a progress line on stderr (stdout carries only the result line)"""
     r = os.environ.get("RANK")
-    print("[bench%s %.0fs] %s" % ("" if r is None else " r" + r, time.perf_counter() - T_START, msg),
-          file=sys.stderr, flush=True)
+    err_line("[bench%s %.0fs] %s" % ("" if r is None else " r" + r, time.perf_counter() - T_START, msg))
+
+
+def err_line(text):
+    """One stderr line in ONE write: the ranks share the pipe, and print's separate newline write could let
+    another rank's line land in the middle of this one."""
+    sys.stderr.write(text + "\n")
+    sys.stderr.flush()
 
 
 # ---------------------------------------------------------------------------------------------------
@@ -225,27 +232,22 @@ def latest_e2e():
 
 
 def like_for_like(out, pcie_ms, up, down):
-    """The headline next to what it leaves out: the step's own host-to-device and device-to-host copies,
-    the host MaxEnt the drop-in evaluates for the genome gaps (the bench takes the probabilities as
-    device inputs), and GMAP end to end through the drop-in."""
+    """The headline next to what it leaves out: the step's own host-to-device and device-to-host copies and
+    GMAP end to end through the drop-in.  MaxEnt is in the step (device), as it is in the CPU baseline's
+    reference objects."""
     v = out["value"]
     ms = out["ms_per_step"]
     reads = out["config"]["reads_per_step_per_gpu"]
     with_pcie = reads / ((ms + pcie_ms) * 1e-3) * out["n_gpus"]
     cb = out.get("cpu_baseline") or {}
-    hm = (cb.get("host_maxent") or {}).get("reads_per_s")
-    pipe = min(with_pcie, hm) if hm else None
     cpu = cb.get("value")
     return {"pcie_ms_per_step": pcie_ms, "pcie_bytes_up": up, "pcie_bytes_down": down,
             "reads_per_s_incl_pcie": with_pcie,
-            "host_maxent_reads_per_s": hm, "host_maxent_cores": cb.get("cores"),
-            "pipeline_bound_reads_per_s": pipe,
             "ratio_vs_cpu": v / cpu if cpu else None,
-            "ratio_vs_cpu_incl_pcie_and_host_maxent": pipe / cpu if pipe and cpu else None,
+            "ratio_vs_cpu_incl_pcie": with_pcie / cpu if cpu else None,
             "drop_in_end_to_end": latest_e2e(),
-            "note": "copies measured serially after the step (not overlapped); host MaxEnt on the CPU baseline's "
-                    "cores, as the drop-in evaluates it; the end-to-end record is GMAP's own program on the same "
-                    "reads and cores (tools/e2e_timing.py)"}
+            "note": "copies measured serially after the step (not overlapped); the end-to-end record is GMAP's own "
+                    "program on the same reads and cores (tools/e2e_timing.py)"}
 
 
 def cpu_baselines():
@@ -341,7 +343,7 @@ def dry_run(args, rank, world):
     rank_line = {"rank": rank, "world_size": dist.get_world_size() if world > 1 else 1,
                  "backend": dist.get_backend() if world > 1 else None, "blocks": mine,
                  "stage2_calls": [int(len(d["oligo"])) for d in data]}
-    print(json.dumps({"rank_line": rank_line}), file=sys.stderr, flush=True)
+    err_line(json.dumps({"rank_line": rank_line}))
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": world, "config": gname, "shard": rec,
                           "genome_digest": digest.hex(), "setup_s": t_gen}))
@@ -414,10 +416,8 @@ def main():
         blk = {"id": bi, "d": d, "ns": len(sp), "ne": len(ep), "ng": len(gp)}
         blk["d_q"] = torch.from_numpy(d["q"]).to(dev)
         blk["d_oq"] = torch.from_numpy(d["oq"]).to(dev)
-        gen.manual_seed(5000 + bi)
-        sprob = torch.rand(max(d["sprob_len"], 1), dtype=torch.float64, device=dev, generator=gen) * 0.3
-        sprob[torch.from_numpy(d["sprob_hi"]).to(dev)] = 0.95
-        blk["d_sprob"] = sprob
+        # the genome gaps' splice-probability arena: scratch the device MaxEnt fills in the step
+        blk["d_sprob"] = torch.zeros(max(d["sprob_len"], 1), dtype=torch.float64, device=dev)
         nprob = len(sp) + len(ep)
         blk["host_res"] = np.zeros(nprob, dtype=gmapdp.RESULT_DTYPE)
         blk["host_gres"] = np.zeros(max(len(gp), 1), dtype=gmapdp.GENOME_RESULT_DTYPE)
@@ -449,8 +449,6 @@ def main():
                    "gmapdp_microexon_plan_create")
         blk["mplan"] = mplan
         blk["ncands"] = lib.gmapdp_microexon_plan_candidates(mplan)
-        gen.manual_seed(7700 + bi)
-        blk["d_mxp"] = torch.rand(max(2 * blk["ncands"], 2), dtype=torch.float64, device=dev, generator=gen)
         blk["ngpu"], blk["nggpu"] = lib.gmapdp_plan_gpu_problems(plan), lib.gmapdp_plan_genome_gpu_problems(plan)
         blk["cap"] = lib.gmapdp_plan_pair_capacity(plan)
         blk["mcap"] = lib.gmapdp_microexon_plan_pair_capacity(mplan)
@@ -474,8 +472,8 @@ def main():
                          dtype=torch.uint8, device=dev)
     d_mpairs = torch.empty(max(mx("mcap"), 1) * 16, dtype=torch.uint8, device=dev)
     for b in B:
-        eng._check(lib.gmapdp_plan_bind_genome(b["plan"], C.c_void_p(b["d_sprob"].data_ptr()),
-                                               C.c_void_p(d_gres.data_ptr())), "gmapdp_plan_bind_genome")
+        eng._check(lib.gmapdp_plan_bind_genome_maxent(eng.h, b["plan"], C.c_void_p(b["d_sprob"].data_ptr()),
+                                                      C.c_void_p(d_gres.data_ptr())), "gmapdp_plan_bind_genome_maxent")
     progress("plans ready (%d blocks, %.2f s DP plans, %.2f s stage-2 plans)" % (len(B), t_plan, t_oplan))
 
     # Streams: stage 2 on its own stream, the DP launch classes on the engine's schedule (0 = main,
@@ -501,7 +499,7 @@ def main():
 
     def mrun(b, s, what):
         eng._check(lib.gmapdp_microexon_plan_run(eng.h, b["mplan"], C.c_void_p(b["d_q"].data_ptr()),
-                                                 C.c_void_p(b["d_q"].data_ptr()), C.c_void_p(b["d_mxp"].data_ptr()),
+                                                 C.c_void_p(b["d_q"].data_ptr()), None,
                                                  C.c_void_p(d_mres.data_ptr()), C.c_void_p(d_mpairs.data_ptr()),
                                                  what, C.c_void_p(s.cuda_stream)), "gmapdp_microexon_plan_run")
 
@@ -734,8 +732,8 @@ def main():
     # ---- PCIe: one block's inputs up and outputs down through pinned host memory (outside the step) ----
     b = B[0]
     d = b["d"]
-    up = (d["q"].nbytes + d["oq"].nbytes + sum(d[k].nbytes for k in ("single", "end", "genome", "oligo", "microexon"))
-          + 8 * max(d["sprob_len"], 1) + 16 * b["ncands"])
+    # (the splice and microexon probabilities are computed on the device: no probability crosses PCIe)
+    up = d["q"].nbytes + d["oq"].nbytes + sum(d[k].nbytes for k in ("single", "end", "genome", "oligo", "microexon"))
     # the outputs as produced: results, the DP and microexon pairs, the stage-2 results and path pairs
     down = int(32 * b["ngpu"] + 72 * b["nggpu"] + 16 * checks["pairs"] / len(B) + 32 * args.reads
                + 20 * checks["stage2_path_pairs"] / len(B))
@@ -841,7 +839,7 @@ def main():
     rank_line = {"rank": rank, "world_size": dist.get_world_size() if world > 1 else 1,
                  "backend": dist.get_backend() if world > 1 else None, "device": local,
                  "blocks": mine, "ms_per_step_local": ms_step}
-    print(json.dumps({"rank_line": rank_line}), file=sys.stderr, flush=True)
+    err_line(json.dumps({"rank_line": rank_line}))
     for b in B:
         lib.gmapdp_plan_destroy(b["plan"])
         lib.gmapdp_stage2_plan_destroy(b["oplan"])

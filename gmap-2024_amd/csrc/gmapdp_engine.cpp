@@ -8,6 +8,7 @@
 //   Dynprog_end5/3_gap prologues  dynprog_end.c:1333-1411 / 1962-2027 (penalties, chopping,
 //                                 NULL cases, segment orientation, bands per endalign)
 //   Compress_create_blocks_comp   compress-write.c:754  (.genomecomp packing)
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <time.h>
 
@@ -17,11 +18,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <tuple>
 #include <vector>
 
 #include "gmapdp_internal.h"
+#include "me_device.h"
 #include "../../include/gmapdp.h"
 
 namespace gmapdp {
@@ -96,8 +99,13 @@ hipError_t launch_mx_search(int n, hipStream_t s, const gmapdp_microexon_problem
                             const int64_t* direct);
 hipError_t launch_mx_finish(int n, hipStream_t s, const gmapdp_microexon_problem* probs, const uint32_t* blocks,
                             uint64_t nwords, const char* qseq, const char* qseq_uc, const uint8_t* constab,
-                            const gmapdp_microexon_candidate* cands, const double* cand_probs,
+                            const gmapdp_microexon_candidate* cands, const double* cand_probs, const double* metab,
                             gmapdp_microexon_result* results, gmapdp_pair* pairs, const int64_t* poff);
+hipError_t launch_me_sites(long long n, hipStream_t s, const uint32_t* blocks, uint64_t nwords, const double* T,
+                           const gmapdp_coord_t* pos, const uint8_t* models, const gmapdp_coord_t* chroffsets,
+                           double* out);
+hipError_t launch_me_gap(int n, hipStream_t s, const DevGenomeProblem* probs, const int* order,
+                         const uint32_t* blocks, uint64_t nwords, const double* T, double* sprob);
 static const int kUse8pSize[4] = {41, 63, 127, 24};  // use8p_size (dynprog.c:1022-1025)
 
 // ---------------------------------------------------------------------------
@@ -584,6 +592,112 @@ int gmapdp_share_genome(gmapdp_ctx* ctx, const gmapdp_ctx* owner) {
   ctx->genome_length = owner->genome_length;
   ctx->genome_owned = false;
   return GMAPDP_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Device MaxEnt (me_device.h): the reference's model tables (maxent_hr.c:25-24660), as
+// tools/make_maxent_tables.py writes them, loaded once per process and uploaded once per device.
+// ---------------------------------------------------------------------------
+static std::mutex g_me_mu;
+static std::vector<double> g_me_host;
+static std::string g_me_path, g_me_err;
+static double* g_me_dev[64];
+
+static std::string me_path() {
+  if (const char* e = getenv("GMAPDP_MAXENT_TABLES")) return e;
+  Dl_info info;
+  if (dladdr((void*)&gmapdp_genome_words, &info) && info.dli_fname) {
+    const std::string so = info.dli_fname;
+    const size_t k = so.rfind('/');
+    return (k == std::string::npos ? std::string(".") : so.substr(0, k)) + "/maxent_hr_tables.bin";
+  }
+  return "maxent_hr_tables.bin";
+}
+
+static bool me_load_host_locked() {
+  if (!g_me_host.empty()) return true;
+  g_me_path = me_path();
+  FILE* f = std::fopen(g_me_path.c_str(), "rb");
+  if (!f) {
+    g_me_err = "maxent tables: cannot open " + g_me_path + " (tools/make_maxent_tables.py writes it)";
+    return false;
+  }
+  char magic[8];
+  uint32_t hdr[2];
+  bool ok = std::fread(magic, 1, 8, f) == 8 && std::memcmp(magic, "GMDPMXT1", 8) == 0 &&
+            std::fread(hdr, 4, 2, f) == 2 && hdr[0] == 16;
+  std::vector<double> all(kMeTotal);
+  for (int t = 0; ok && t < 16; t++) {
+    char name[32];
+    uint32_t h[2];
+    ok = std::fread(name, 1, 32, f) == 32 && std::fread(h, 4, 2, f) == 2 && (int)h[0] == kMeEntries[t] &&
+         std::fread(all.data() + me_offset(t), sizeof(double), h[0], f) == h[0];
+  }
+  std::fclose(f);
+  if (!ok) {
+    g_me_err = "maxent tables: " + g_me_path + " is not a tools/make_maxent_tables.py table file";
+    return false;
+  }
+  g_me_host.swap(all);
+  return true;
+}
+
+// the device copy of the tables for ctx's device, or nullptr with ctx->err set
+static const double* me_tables(gmapdp_ctx* ctx) {
+  std::lock_guard<std::mutex> lk(g_me_mu);
+  if (!me_load_host_locked()) {
+    ctx->err = g_me_err;
+    return nullptr;
+  }
+  if (ctx->device < 0 || ctx->device >= 64) return nullptr;
+  if (!g_me_dev[ctx->device]) {
+    double* d = nullptr;
+    hipError_t e = hipMalloc(&d, sizeof(double) * kMeTotal);
+    if (e == hipSuccess) e = hipMemcpy(d, g_me_host.data(), sizeof(double) * kMeTotal, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      if (d) (void)hipFree(d);
+      ctx->err = std::string("maxent tables upload: ") + hipGetErrorString(e);
+      return nullptr;
+    }
+    g_me_dev[ctx->device] = d;
+  }
+  return g_me_dev[ctx->device];
+}
+
+extern "C" {
+
+int gmapdp_maxent_available(char* path, size_t path_bytes) {
+  std::lock_guard<std::mutex> lk(g_me_mu);
+  const bool ok = me_load_host_locked();
+  if (path && path_bytes) std::snprintf(path, path_bytes, "%s", g_me_path.c_str());
+  return ok ? 1 : 0;
+}
+
+int gmapdp_maxent_sites(gmapdp_ctx* ctx, const gmapdp_coord_t* positions, const uint8_t* models,
+                        const gmapdp_coord_t* chroffsets, size_t n, double* out) {
+  if (!ctx || (n && (!positions || !models || !chroffsets || !out))) return GMAPDP_EINVAL;
+  if (!ctx->d_genome) return GMAPDP_ENOGENOME;
+  if (n == 0) return GMAPDP_OK;
+  (void)hipSetDevice(ctx->device);
+  const double* T = me_tables(ctx);
+  if (!T) return GMAPDP_EINVAL;
+  const size_t o_pos = 0, o_chr = o_pos + 8 * n, o_mod = o_chr + 8 * n, in_bytes = o_mod + n;
+  hipError_t e = ctx->din.ensure(in_bytes);
+  if (e == hipSuccess) e = ctx->dout.ensure(8 * n);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "maxent buffers: %s", e);
+  unsigned char* din = (unsigned char*)ctx->din.p;
+  hipStream_t s = ctx->stream;
+  e = hipMemcpyAsync(din + o_pos, positions, 8 * n, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(din + o_chr, chroffsets, 8 * n, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(din + o_mod, models, n, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess)
+    e = launch_me_sites((long long)n, s, ctx->d_genome, ctx->genome_words, T, (const gmapdp_coord_t*)(din + o_pos),
+                        din + o_mod, (const gmapdp_coord_t*)(din + o_chr), (double*)ctx->dout.p);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, ctx->dout.p, 8 * n, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = ctx_sync(ctx, s);
+  return e == hipSuccess ? GMAPDP_OK : fail(ctx, GMAPDP_ELAUNCH, "maxent: %s", e);
 }
 
 }  // extern "C"
@@ -1170,7 +1284,16 @@ struct RunArgs {
   gmapdp_genome_result* d_gresults;
   gmapdp_pair* d_pairs;
   const uint8_t* d_known = nullptr;  // known-site arena (GMAPDP_KNOWN_SITES genome gaps)
+  // device MaxEnt: each genome-gap class first fills its problems' entries of d_sprob (me_gap_kernel)
+  const double* d_metab = nullptr;
 };
+
+// me_gap_kernel over a genome-gap launch class's problems, on the class's stream
+static hipError_t launch_class_maxent(gmapdp_ctx* ctx, const PlanCore::Launch& L, const RunArgs& a, hipStream_t s) {
+  if (!a.d_metab) return hipSuccess;
+  return launch_me_gap(L.count, s, a.d_gprobs, a.d_gorder + L.first, ctx->d_genome, ctx->genome_words, a.d_metab,
+                       const_cast<double*>(a.d_sprob));
+}
 
 static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, const RunArgs& a, hipStream_t stream) {
   const auto& L = plan.launches[li];
@@ -1180,6 +1303,8 @@ static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, cons
                       a.d_pairs);
   if (L.kind == PlanCore::kUxg) {
     if (!a.d_gresults || !a.d_sprob) return hipErrorInvalidValue;
+    const hipError_t e = launch_class_maxent(ctx, L, a, stream);
+    if (e != hipSuccess) return e;
     return launch_uxg(L.R, L.count, L.lds, stream, a.d_gprobs, a.d_gorder + L.first, (unsigned char*)ctx->gdirs.p,
                       ctx->d_genome, ctx->genome_words, a.d_q, a.d_quc, a.d_sprob, ctx->d_sc, ctx->d_cs, ctx->d_isc,
                       a.d_gresults, a.d_pairs, a.d_known);
@@ -1199,6 +1324,8 @@ static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, cons
                      ctx->genome_words, a.d_q, a.d_quc, ctx->d_sc, ctx->d_cs, a.d_results, a.d_pairs,
                      (uint64_t*)ctx->gdirs.p);
   if (!a.d_gresults || !a.d_sprob) return hipErrorInvalidValue;
+  const hipError_t e = launch_class_maxent(ctx, L, a, stream);
+  if (e != hipSuccess) return e;
   return launch_gg(L.R, L.dirs_lds, L.count, L.lds, stream, a.d_gprobs, a.d_gorder + L.first, ctx->d_genome,
                    ctx->genome_words, a.d_q, a.d_quc, a.d_sprob, ctx->d_sc, ctx->d_cs, ctx->d_isc, a.d_gresults,
                    a.d_pairs, (unsigned char*)ctx->gdirs.p, a.d_known);
@@ -1256,11 +1383,18 @@ static int run_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int 
     const long len = i < nsingle ? singles[i].rlength : ends[i - nsingle].rlength;
     if (lo < 0 || (size_t)(lo + len) > qbytes) return bad(ctx, "query slice outside the query arena");
   }
+  // splice_probs == NULL: the probability entries are evaluated on the device (me_gap_kernel)
+  const bool dev_me = !sprob && !plan.gdev.empty();
+  const double* metab = nullptr;
+  if (dev_me) {
+    nsprob = std::max(nsprob, gmapdp_genome_prob_entries(genomes, ngenome));
+    if (!(metab = me_tables(ctx))) return GMAPDP_EINVAL;
+  }
   for (size_t s = 0; s < plan.gdev.size(); s++) {
     const gmapdp_genome_problem& g = genomes[plan.gdev_problem[s]];
     if (g.qoff < 0 || (size_t)((long)g.qoff + g.rlength) > qbytes)
       return bad(ctx, "query slice outside the query arena");
-    if (!sprob || g.prob_offset < 0 || (size_t)g.prob_offset + (size_t)g.glengthL + (size_t)g.glengthR > nsprob)
+    if (g.prob_offset < 0 || (size_t)g.prob_offset + (size_t)g.glengthL + (size_t)g.glengthR > nsprob)
       return bad(ctx, "splice probabilities outside the probability arena");
     if ((g.flags & GMAPDP_KNOWN_SITES) &&
         (!known || (size_t)g.known_offset + gmapdp_genome_known_bytes(&g) > nknown))
@@ -1276,7 +1410,7 @@ static int run_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int 
   const size_t o_gprobs = o_order + al(sizeof(int) * ndev);
   const size_t o_gorder = o_gprobs + al(sizeof(DevGenomeProblem) * ngdev);
   const size_t o_sprob = o_gorder + al(sizeof(int) * ngdev);
-  const size_t o_q = o_sprob + al(ngdev ? sizeof(double) * nsprob : 0);
+  const size_t o_q = o_sprob + al(ngdev && !dev_me ? sizeof(double) * nsprob : 0);
   const size_t o_quc = o_q + al(qbytes);
   const size_t o_known = o_quc + al(qbytes);
   const size_t in_bytes = o_known + al(nkn);
@@ -1288,6 +1422,7 @@ static int run_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int 
   if (e == hipSuccess) e = ctx->din.ensure(in_bytes);
   if (e == hipSuccess) e = ctx->hout.ensure(out_bytes);
   if (e == hipSuccess) e = ctx->dout.ensure(out_bytes);
+  if (e == hipSuccess && dev_me) e = ctx->sprob.ensure(sizeof(double) * nsprob);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "batch buffers: %s", e);
   unsigned char* hin = (unsigned char*)ctx->hin.p;
   unsigned char* din = (unsigned char*)ctx->din.p;
@@ -1300,7 +1435,7 @@ static int run_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int 
   if (ngdev) {
     std::memcpy(hin + o_gprobs, plan.gdev.data(), sizeof(DevGenomeProblem) * ngdev);
     std::memcpy(hin + o_gorder, plan.gorder.data(), sizeof(int) * ngdev);
-    std::memcpy(hin + o_sprob, sprob, sizeof(double) * nsprob);
+    if (!dev_me) std::memcpy(hin + o_sprob, sprob, sizeof(double) * nsprob);
     if (nkn) std::memcpy(hin + o_known, known, nkn);
   }
   std::memcpy(hin + o_q, qseq, qbytes);
@@ -1315,7 +1450,8 @@ static int run_batch(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int 
   a.d_gorder = (const int*)(din + o_gorder);
   a.d_q = (const char*)(din + o_q);
   a.d_quc = (const char*)(din + o_quc);
-  a.d_sprob = (const double*)(din + o_sprob);
+  a.d_sprob = dev_me ? (const double*)ctx->sprob.p : (const double*)(din + o_sprob);
+  a.d_metab = metab;
   a.d_results = (gmapdp_result*)(dout + r_res);
   a.d_gresults = (gmapdp_genome_result*)(dout + r_gres);
   a.d_pairs = (gmapdp_pair*)(dout + r_pairs);
@@ -1860,6 +1996,7 @@ struct gmapdp_plan {
   int* d_gorder = nullptr;
   const double* d_sprob = nullptr;            // bound by gmapdp_plan_bind_genome
   gmapdp_genome_result* d_gresults = nullptr;
+  const double* d_metab = nullptr;            // gmapdp_plan_bind_genome_maxent: each genome-gap class fills d_sprob
 };
 
 static void plan_free(gmapdp_plan* p) {
@@ -1880,6 +2017,7 @@ static RunArgs plan_args(const gmapdp_plan* plan, const char* d_qseq, const char
   a.d_q = d_qseq;
   a.d_quc = d_qseq_uc;
   a.d_sprob = plan->d_sprob;
+  a.d_metab = plan->d_metab;
   a.d_results = d_results;
   a.d_gresults = plan->d_gresults;
   a.d_pairs = d_pairs;
@@ -1943,6 +2081,19 @@ int gmapdp_plan_bind_genome(gmapdp_plan* plan, const double* d_splice_probs, gma
   if (!plan) return GMAPDP_EINVAL;
   plan->d_sprob = d_splice_probs;
   plan->d_gresults = d_genome_results;
+  plan->d_metab = nullptr;
+  return GMAPDP_OK;
+}
+
+int gmapdp_plan_bind_genome_maxent(gmapdp_ctx* ctx, gmapdp_plan* plan, double* d_splice_probs,
+                                   gmapdp_genome_result* d_genome_results) {
+  if (!ctx || !plan || !d_splice_probs) return GMAPDP_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  const double* T = me_tables(ctx);
+  if (!T) return GMAPDP_EINVAL;
+  plan->d_sprob = d_splice_probs;
+  plan->d_gresults = d_genome_results;
+  plan->d_metab = T;
   return GMAPDP_OK;
 }
 
@@ -2546,7 +2697,7 @@ extern "C" int gmapdp_microexon_finish(gmapdp_ctx* ctx, const gmapdp_microexon_p
   if (!ctx || n < 0 || (n > 0 && (!problems || !results || !qseq || !qseq_uc))) return GMAPDP_EINVAL;
   if (!ctx->d_genome) return GMAPDP_ENOGENOME;
   if (n == 0) return GMAPDP_OK;
-  if (ncands && (!candidates || !cand_probs)) return GMAPDP_EINVAL;
+  if (ncands && !candidates) return GMAPDP_EINVAL;
   size_t poff = 0;
   std::vector<gmapdp_microexon_result> res(results, results + n);
   for (int i = 0; i < n; i++) {
@@ -2558,6 +2709,9 @@ extern "C" int gmapdp_microexon_finish(gmapdp_ctx* ctx, const gmapdp_microexon_p
   }
   if (poff > pair_capacity || !pairs) return bad(ctx, "microexon: pair arena too small");
   (void)hipSetDevice(ctx->device);
+  // cand_probs NULL: the finish kernel evaluates the candidates' MaxEnt sites on the device
+  const double* metab = nullptr;
+  if (!cand_probs && !(metab = me_tables(ctx))) return GMAPDP_EINVAL;
   int rc = mx_upload(ctx, problems, n, qseq, qseq_uc, qbytes);
   if (rc) return rc;
   hipStream_t s = ctx->stream;
@@ -2566,14 +2720,15 @@ extern "C" int gmapdp_microexon_finish(gmapdp_ctx* ctx, const gmapdp_microexon_p
   if (e == hipSuccess) e = ctx->mxpairs.ensure(sizeof(gmapdp_pair) * std::max<size_t>(poff, 1));
   if (e == hipSuccess && ncands)
     e = hipMemcpyAsync(ctx->mxcands.p, candidates, sizeof(gmapdp_microexon_candidate) * ncands, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && ncands)
+  if (e == hipSuccess && ncands && cand_probs)
     e = hipMemcpyAsync(ctx->mxprobs2.p, cand_probs, sizeof(double) * 2 * ncands, hipMemcpyHostToDevice, s);
   if (e == hipSuccess)
     e = hipMemcpyAsync(ctx->mxres.p, res.data(), sizeof(gmapdp_microexon_result) * n, hipMemcpyHostToDevice, s);
   if (e == hipSuccess)
     e = launch_mx_finish(n, s, (const gmapdp_microexon_problem*)ctx->mxprobs.p, ctx->d_genome, ctx->genome_words,
                          (const char*)ctx->qseq.p, (const char*)ctx->qseq_uc.p, ctx->d_cs,
-                         (const gmapdp_microexon_candidate*)ctx->mxcands.p, (const double*)ctx->mxprobs2.p,
+                         (const gmapdp_microexon_candidate*)ctx->mxcands.p,
+                         cand_probs ? (const double*)ctx->mxprobs2.p : nullptr, metab,
                          (gmapdp_microexon_result*)ctx->mxres.p, (gmapdp_pair*)ctx->mxpairs.p, nullptr);
   if (e == hipSuccess)
     e = hipMemcpyAsync(results, ctx->mxres.p, sizeof(gmapdp_microexon_result) * n, hipMemcpyDeviceToHost, s);
@@ -2584,28 +2739,33 @@ extern "C" int gmapdp_microexon_finish(gmapdp_ctx* ctx, const gmapdp_microexon_p
 }
 
 // The drop-in's dispatcher batch in one round trip (gmapdp_mixed_batch).  One pinned host image and
-// one device image hold [inputs | outputs]: the DP descriptors and launch orders, the query arena,
-// the splice probabilities, the microexon searches and finishes (the finishes' results, which their
-// kernel updates in place, are the last input section), then the DP results and pairs, the searches'
-// results and candidate pool, the finishes' pairs.  One copy up, the kernels, one copy down from
-// the finishes' results to the end, one wait.  A search that overflows the pool (a result with
-// cand_offset -2) or holds more candidates than its LDS (-1) is rerun by gmapdp_microexon_search.
+// one device image hold [inputs | outputs | device-only scratch]: the DP descriptors and launch orders,
+// the query arena, the splice probabilities (unless the device evaluates them), the microexon
+// searches, finishes and whole calls (the finishes' results, which their kernel updates in place, are
+// the last input section), then the DP results and pairs, the searches' results and candidate pool,
+// the finishes' and whole calls' results and pairs, then the whole calls' candidate pool (never copied).
+// One copy up, the kernels, one copy down of the outputs, one wait.  A search that overflows the pool (a
+// result with cand_offset -2) or holds more candidates than its LDS (-1) is rerun by
+// gmapdp_microexon_search (a whole call then also by gmapdp_microexon_finish).
 extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char* qseq_uc, size_t qbytes,
                                   gmapdp_mixed* m) {
   if (!ctx || !m) return GMAPDP_EINVAL;
   const int nsingle = m->nsingle, nend = m->nend, ngenome = m->ngenome, nxs = m->nsearch, nxf = m->nfinish;
-  if (nsingle < 0 || nend < 0 || ngenome < 0 || nxs < 0 || nxf < 0) return GMAPDP_EINVAL;
+  const int nxw = m->nwhole;
+  if (nsingle < 0 || nend < 0 || ngenome < 0 || nxs < 0 || nxf < 0 || nxw < 0) return GMAPDP_EINVAL;
   if ((nsingle && !m->singles) || (nend && !m->ends) || (ngenome && !m->genomes) ||
       (nsingle + nend && !m->results) || (ngenome && !m->genome_results) || (nxs && (!m->searches || !m->search_results)) ||
-      (nxf && (!m->finishes || !m->finish_results)))
+      (nxf && (!m->finishes || !m->finish_results)) || (nxw && (!m->wholes || !m->whole_results)))
     return GMAPDP_EINVAL;
   m->candidates_needed = 0;
   if (!ctx->d_genome) return GMAPDP_ENOGENOME;
-  if (nsingle + nend + ngenome + nxs + nxf == 0) return GMAPDP_OK;
+  if (nsingle + nend + ngenome + nxs + nxf + nxw == 0) return GMAPDP_OK;
   if (!qseq || !qseq_uc) return GMAPDP_EINVAL;
   (void)hipSetDevice(ctx->device);
   // ---- DP plan (as run_batch) ----
   PlanCore plan;
+  size_t nsp = 0;
+  bool dev_me = false;
   if (nsingle + nend + ngenome) {
     int rc = build_plan(ctx, m->singles, nsingle, m->ends, nend, m->genomes, ngenome, m->results, m->genome_results,
                         plan);
@@ -2617,11 +2777,12 @@ extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char*
       const long len = i < nsingle ? m->singles[i].rlength : m->ends[i - nsingle].rlength;
       if (lo < 0 || (size_t)(lo + len) > qbytes) return bad(ctx, "query slice outside the query arena");
     }
+    dev_me = !m->splice_probs && !plan.gdev.empty();
+    nsp = plan.gdev.empty() ? 0 : dev_me ? std::max(m->nprobs, gmapdp_genome_prob_entries(m->genomes, ngenome)) : m->nprobs;
     for (size_t s = 0; s < plan.gdev.size(); s++) {
       const gmapdp_genome_problem& g = m->genomes[plan.gdev_problem[s]];
       if (g.qoff < 0 || (size_t)((long)g.qoff + g.rlength) > qbytes) return bad(ctx, "query slice outside the query arena");
-      if (!m->splice_probs || g.prob_offset < 0 ||
-          (size_t)g.prob_offset + (size_t)g.glengthL + (size_t)g.glengthR > m->nprobs)
+      if (g.prob_offset < 0 || (size_t)g.prob_offset + (size_t)g.glengthL + (size_t)g.glengthR > nsp)
         return bad(ctx, "splice probabilities outside the probability arena");
       if ((g.flags & GMAPDP_KNOWN_SITES) &&
           (!m->known_sites || (size_t)g.known_offset + gmapdp_genome_known_bytes(&g) > m->nknown))
@@ -2649,27 +2810,42 @@ extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char*
     fpoff += (size_t)std::max(p.rlength, 0) + 2;
   }
   if (nxf && (fpoff > m->finish_pair_capacity || !m->finish_pairs)) return bad(ctx, "microexon: pair arena too small");
-  if (m->nfinish_candidates && (!m->finish_candidates || !m->finish_probs)) return GMAPDP_EINVAL;
+  if (m->nfinish_candidates && !m->finish_candidates) return GMAPDP_EINVAL;
+  std::vector<int64_t> wpoff(nxw);
+  size_t wpairs = 0;
+  for (int i = 0; i < nxw; i++) {
+    const gmapdp_microexon_problem& p = m->wholes[i];
+    if (p.rlength < 0 || p.qoff < 0 || (size_t)p.qoff + (size_t)p.rlength > qbytes)
+      return bad(ctx, "microexon: query slice outside the query arena");
+    wpoff[i] = (int64_t)wpairs;
+    wpairs += (size_t)p.rlength + 2;
+  }
+  if (nxw && (wpairs > m->whole_pair_capacity || !m->whole_pairs)) return bad(ctx, "microexon: whole-call pair arena too small");
+  const bool fdev_me = nxf && !m->finish_probs;
+  const double* metab = nullptr;
+  if ((dev_me || fdev_me || nxw) && !(metab = me_tables(ctx))) return GMAPDP_EINVAL;
   const size_t nfc = nxf ? m->nfinish_candidates : 0;
-  const size_t pool = nxs ? std::max<size_t>(4096, 16 * (size_t)nxs) : 0;  // search candidates
-  // ---- one image: inputs, then outputs ----
+  const size_t pool = nxs ? std::max<size_t>(4096, 16 * (size_t)nxs) : 0;   // search candidates
+  const size_t wpool = nxw ? std::max<size_t>(4096, 16 * (size_t)nxw) : 0;  // whole calls' candidates
+  // ---- one image: inputs, then outputs, then device-only scratch ----
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   size_t o = 0;
   const size_t o_probs = o;   o += al(sizeof(DevProblem) * ndev);
   const size_t o_order = o;   o += al(sizeof(int) * ndev);
   const size_t o_gprobs = o;  o += al(sizeof(DevGenomeProblem) * ngdev);
   const size_t o_gorder = o;  o += al(sizeof(int) * ngdev);
-  const size_t nsp = ngdev ? m->nprobs : 0;
-  const size_t o_sprob = o;   o += al(sizeof(double) * nsp);
+  const size_t o_sprob = o;   o += al(dev_me ? 0 : sizeof(double) * nsp);
   const size_t nkn = (ngdev && m->known_sites) ? m->nknown : 0;
   const size_t o_known = o;   o += al(nkn);
   const size_t o_q = o;       o += al(qbytes);
   const size_t o_quc = o;     o += al(qbytes);
   const size_t o_xs = o;      o += al(sizeof(gmapdp_microexon_problem) * nxs);
-  const size_t o_xcnt = o;    o += al(sizeof(unsigned long long));
+  const size_t o_xcnt = o;    o += al(2 * sizeof(unsigned long long));  // search pool, whole-call pool
   const size_t o_xf = o;      o += al(sizeof(gmapdp_microexon_problem) * nxf);
   const size_t o_xfc = o;     o += al(sizeof(gmapdp_microexon_candidate) * nfc);
-  const size_t o_xfp = o;     o += al(sizeof(double) * 2 * nfc);
+  const size_t o_xfp = o;     o += al(fdev_me ? 0 : sizeof(double) * 2 * nfc);
+  const size_t o_xw = o;      o += al(sizeof(gmapdp_microexon_problem) * nxw);
+  const size_t o_xwpoff = o;  o += al(sizeof(int64_t) * nxw);
   const size_t o_xfres = o;   o += al(sizeof(gmapdp_microexon_result) * nxf);  // in and out
   const size_t in_bytes = o_xfres + sizeof(gmapdp_microexon_result) * nxf;
   const size_t r_res = o;     o += al(sizeof(gmapdp_result) * ndev);
@@ -2678,9 +2854,14 @@ extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char*
   const size_t r_xsres = o;   o += al(sizeof(gmapdp_microexon_result) * nxs);
   const size_t r_xcand = o;   o += al(sizeof(gmapdp_microexon_candidate) * pool);
   const size_t r_xfpairs = o; o += al(sizeof(gmapdp_pair) * fpoff);
+  const size_t r_xwres = o;   o += al(sizeof(gmapdp_microexon_result) * nxw);
+  const size_t r_xwpairs = o; o += al(sizeof(gmapdp_pair) * wpairs);
+  const size_t out_end = o;
+  const size_t s_xwcand = o;  o += al(sizeof(gmapdp_microexon_candidate) * wpool);
   const size_t total = o;
-  hipError_t e = ctx->hin.ensure(total);
+  hipError_t e = ctx->hin.ensure(out_end);
   if (e == hipSuccess) e = ctx->din.ensure(total);
+  if (e == hipSuccess && dev_me) e = ctx->sprob.ensure(sizeof(double) * nsp);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "batch buffers: %s", e);
   unsigned char* h = (unsigned char*)ctx->hin.p;
   unsigned char* d = (unsigned char*)ctx->din.p;
@@ -2691,20 +2872,24 @@ extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char*
   if (ngdev) {
     std::memcpy(h + o_gprobs, plan.gdev.data(), sizeof(DevGenomeProblem) * ngdev);
     std::memcpy(h + o_gorder, plan.gorder.data(), sizeof(int) * ngdev);
-    std::memcpy(h + o_sprob, m->splice_probs, sizeof(double) * nsp);
+    if (!dev_me) std::memcpy(h + o_sprob, m->splice_probs, sizeof(double) * nsp);
     if (nkn) std::memcpy(h + o_known, m->known_sites, nkn);
   }
   std::memcpy(h + o_q, qseq, qbytes);
   std::memcpy(h + o_quc, qseq_uc, qbytes);
   if (nxs) std::memcpy(h + o_xs, m->searches, sizeof(gmapdp_microexon_problem) * nxs);
-  std::memset(h + o_xcnt, 0, sizeof(unsigned long long));
+  std::memset(h + o_xcnt, 0, 2 * sizeof(unsigned long long));
   if (nxf) {
     std::memcpy(h + o_xf, m->finishes, sizeof(gmapdp_microexon_problem) * nxf);
     std::memcpy(h + o_xfres, fres.data(), sizeof(gmapdp_microexon_result) * nxf);
   }
   if (nfc) {
     std::memcpy(h + o_xfc, m->finish_candidates, sizeof(gmapdp_microexon_candidate) * nfc);
-    std::memcpy(h + o_xfp, m->finish_probs, sizeof(double) * 2 * nfc);
+    if (!fdev_me) std::memcpy(h + o_xfp, m->finish_probs, sizeof(double) * 2 * nfc);
+  }
+  if (nxw) {
+    std::memcpy(h + o_xw, m->wholes, sizeof(gmapdp_microexon_problem) * nxw);
+    std::memcpy(h + o_xwpoff, wpoff.data(), sizeof(int64_t) * nxw);
   }
   hipStream_t s = ctx->stream;
   e = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s);
@@ -2717,7 +2902,8 @@ extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char*
     a.d_gorder = (const int*)(d + o_gorder);
     a.d_q = (const char*)(d + o_q);
     a.d_quc = (const char*)(d + o_quc);
-    a.d_sprob = (const double*)(d + o_sprob);
+    a.d_sprob = dev_me ? (const double*)ctx->sprob.p : (const double*)(d + o_sprob);
+    a.d_metab = dev_me ? metab : nullptr;
     a.d_known = nkn ? (const uint8_t*)(d + o_known) : nullptr;
     a.d_results = (gmapdp_result*)(d + r_res);
     a.d_gresults = (gmapdp_genome_result*)(d + r_gres);
@@ -2725,16 +2911,28 @@ extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char*
     const int rc = run_plan(ctx, plan, a, s);
     if (rc) return rc;
   }
+  unsigned long long* cnt = (unsigned long long*)(d + o_xcnt);
   if (nxs)
     e = launch_mx_search(nxs, s, (const gmapdp_microexon_problem*)(d + o_xs), ctx->d_genome, ctx->genome_words,
                          (const char*)(d + o_q), (const char*)(d + o_quc), (gmapdp_microexon_result*)(d + r_xsres),
-                         (gmapdp_microexon_candidate*)(d + r_xcand), pool, (unsigned long long*)(d + o_xcnt), nullptr);
+                         (gmapdp_microexon_candidate*)(d + r_xcand), pool, cnt, nullptr);
   if (e == hipSuccess && nxf)
     e = launch_mx_finish(nxf, s, (const gmapdp_microexon_problem*)(d + o_xf), ctx->d_genome, ctx->genome_words,
                          (const char*)(d + o_q), (const char*)(d + o_quc), ctx->d_cs,
-                         (const gmapdp_microexon_candidate*)(d + o_xfc), (const double*)(d + o_xfp),
-                         (gmapdp_microexon_result*)(d + o_xfres), (gmapdp_pair*)(d + r_xfpairs), nullptr);
-  if (e == hipSuccess) e = hipMemcpyAsync(h + o_xfres, d + o_xfres, total - o_xfres, hipMemcpyDeviceToHost, s);
+                         (const gmapdp_microexon_candidate*)(d + o_xfc), fdev_me ? nullptr : (const double*)(d + o_xfp),
+                         fdev_me ? metab : nullptr, (gmapdp_microexon_result*)(d + o_xfres),
+                         (gmapdp_pair*)(d + r_xfpairs), nullptr);
+  if (e == hipSuccess && nxw)
+    e = launch_mx_search(nxw, s, (const gmapdp_microexon_problem*)(d + o_xw), ctx->d_genome, ctx->genome_words,
+                         (const char*)(d + o_q), (const char*)(d + o_quc), (gmapdp_microexon_result*)(d + r_xwres),
+                         (gmapdp_microexon_candidate*)(d + s_xwcand), wpool, cnt + 1, nullptr);
+  if (e == hipSuccess && nxw)
+    e = launch_mx_finish(nxw, s, (const gmapdp_microexon_problem*)(d + o_xw), ctx->d_genome, ctx->genome_words,
+                         (const char*)(d + o_q), (const char*)(d + o_quc), ctx->d_cs,
+                         (const gmapdp_microexon_candidate*)(d + s_xwcand), nullptr, metab,
+                         (gmapdp_microexon_result*)(d + r_xwres), (gmapdp_pair*)(d + r_xwpairs),
+                         (const int64_t*)(d + o_xwpoff));
+  if (e == hipSuccess) e = hipMemcpyAsync(h + o_xfres, d + o_xfres, out_end - o_xfres, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = ctx_sync(ctx, s);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "mixed batch: %s", e);
   // ---- unpack ----
@@ -2747,6 +2945,11 @@ extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char*
     std::memcpy(m->finish_results, h + o_xfres, sizeof(gmapdp_microexon_result) * nxf);
     std::memcpy(m->finish_pairs, h + r_xfpairs, sizeof(gmapdp_pair) * fpoff);
   }
+  if (nxw) {
+    std::memcpy(m->whole_results, h + r_xwres, sizeof(gmapdp_microexon_result) * nxw);
+    std::memcpy(m->whole_pairs, h + r_xwpairs, sizeof(gmapdp_pair) * wpairs);
+  }
+  // (the buffers of the reruns below are the context's own; the image above is consumed)
   int rc = GMAPDP_OK;
   if (nxs) {
     const gmapdp_microexon_result* xr = (const gmapdp_microexon_result*)(h + r_xsres);
@@ -2766,6 +2969,36 @@ extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char*
       m->candidates_needed = used;
       if (used > m->candidate_capacity || (used && !m->candidates)) rc = GMAPDP_ESPACE;
       else if (used) std::memcpy(m->candidates, h + r_xcand, sizeof(gmapdp_microexon_candidate) * used);
+    }
+  }
+  // whole calls whose candidates did not fit (finish left npairs -2): search + finish again, alone
+  std::vector<int> redo;
+  for (int i = 0; i < nxw; i++)
+    if (m->whole_results[i].npairs == -2) redo.push_back(i);
+  if (!redo.empty() && rc == GMAPDP_OK) {
+    std::vector<gmapdp_microexon_problem> P(redo.size());
+    for (size_t k = 0; k < redo.size(); k++) P[k] = m->wholes[redo[k]];
+    const int nr = (int)redo.size();
+    std::vector<gmapdp_microexon_result> R(nr);
+    size_t need = 0;
+    std::vector<gmapdp_microexon_candidate> C(4096);
+    int r2 = gmapdp_microexon_search(ctx, P.data(), nr, qseq, qseq_uc, qbytes, R.data(), C.data(), C.size(), &need);
+    if (r2 == GMAPDP_ESPACE) {
+      C.resize(need);
+      r2 = gmapdp_microexon_search(ctx, P.data(), nr, qseq, qseq_uc, qbytes, R.data(), C.data(), C.size(), &need);
+    }
+    std::vector<gmapdp_pair> pp(gmapdp_microexon_pair_capacity(P.data(), nr));
+    if (r2 == GMAPDP_OK)
+      r2 = gmapdp_microexon_finish(ctx, P.data(), nr, qseq, qseq_uc, qbytes, C.data(), nullptr, need, R.data(), pp.data(),
+                                   pp.size());
+    if (r2 != GMAPDP_OK) return r2;
+    for (int k = 0; k < nr; k++) {
+      const int i = redo[k];
+      gmapdp_microexon_result x = R[k];
+      x.pair_offset = wpoff[i];
+      if (x.npairs > 0)
+        std::memcpy(m->whole_pairs + wpoff[i], pp.data() + R[k].pair_offset, sizeof(gmapdp_pair) * (size_t)x.npairs);
+      m->whole_results[i] = x;
     }
   }
   return rc;
@@ -2841,8 +3074,11 @@ extern "C" int gmapdp_microexon_plan_run(gmapdp_ctx* ctx, const gmapdp_microexon
                                          void* stream) {
   if (!ctx || !plan || !d_results) return GMAPDP_EINVAL;
   if (plan->n == 0) return GMAPDP_OK;
-  if ((what & 2) && ((plan->ncands && !d_cand_probs) || !d_pairs)) return GMAPDP_EINVAL;
+  if ((what & 2) && !d_pairs) return GMAPDP_EINVAL;
   (void)hipSetDevice(ctx->device);
+  // d_cand_probs NULL: the finish evaluates the candidates' MaxEnt sites on the device
+  const double* metab = nullptr;
+  if ((what & 2) && !d_cand_probs && !(metab = me_tables(ctx))) return GMAPDP_EINVAL;
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   hipError_t e = hipSuccess;
   if (what & 1)
@@ -2850,7 +3086,7 @@ extern "C" int gmapdp_microexon_plan_run(gmapdp_ctx* ctx, const gmapdp_microexon
                          d_results, plan->d_cands, plan->ncands, plan->d_counter, plan->d_direct);
   if (e == hipSuccess && (what & 2))
     e = launch_mx_finish(plan->n, s, plan->d_probs, ctx->d_genome, ctx->genome_words, d_qseq, d_qseq_uc, ctx->d_cs,
-                         plan->d_cands, d_cand_probs, d_results, d_pairs, plan->d_poff);
+                         plan->d_cands, d_cand_probs, metab, d_results, d_pairs, plan->d_poff);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "microexon plan launch: %s", e);
   return GMAPDP_OK;
 }

@@ -19,6 +19,7 @@
 //   candidates in order, then make_microexon_pairs_double (:683) with every record placed by a ballot
 //   rank (Pairpool_push drops negative positions, pairpool.c:188) in List_T order.
 #include "dp_device.h"
+#include "me_device.h"
 
 namespace gmapdp {
 
@@ -198,6 +199,7 @@ __global__ __launch_bounds__(64) void mx_finish_kernel(const gmapdp_microexon_pr
                                                        const uint8_t* __restrict__ constab,
                                                        const gmapdp_microexon_candidate* __restrict__ cands,
                                                        const double* __restrict__ cand_probs,
+                                                       const double* __restrict__ metab,
                                                        gmapdp_microexon_result* __restrict__ results,
                                                        gmapdp_pair* __restrict__ pairs,
                                                        const int64_t* __restrict__ poff) {
@@ -207,6 +209,11 @@ __global__ __launch_bounds__(64) void mx_finish_kernel(const gmapdp_microexon_pr
   const gmapdp_microexon_problem P = probs[pi];
   gmapdp_microexon_result R = results[pi];
   if (poff) R.pair_offset = poff[pi];
+  if (R.ncandidates > 0 && R.cand_offset < 0) {  // a search whose candidates are not in the pool: the host reruns it
+    R.npairs = -2;
+    if (lane == 0) results[pi] = R;
+    return;
+  }
   R.dynprogindex = P.dynprogindex;
   R.npairs = -1;
   R.bestprob2 = R.bestprob3 = 0.0;
@@ -214,7 +221,7 @@ __global__ __launch_bounds__(64) void mx_finish_kernel(const gmapdp_microexon_pr
   // the selection (:1147): float sums, strict >, candidates in order
   int best = -1;
   float bestprob = 0.0f, b2 = 0.0f, b3 = 0.0f;
-  if (P.cdna_direction != 0) {
+  if (P.cdna_direction != 0 && cand_probs) {
     for (int k = 0; k < R.ncandidates; k++) {
       const float p2 = (float)cand_probs[2 * (R.cand_offset + k)];
       const float p3 = (float)cand_probs[2 * (R.cand_offset + k) + 1];
@@ -223,6 +230,28 @@ __global__ __launch_bounds__(64) void mx_finish_kernel(const gmapdp_microexon_pr
         b2 = p2;
         b3 = p3;
         bestprob = p2 + p3;
+      }
+    }
+  } else if (P.cdna_direction != 0) {
+    // device MaxEnt (me_device.h): the candidates' Maxent_hr_*_prob (:1120-1144) 64 at a time, one per lane;
+    // the strict > over candidates in order keeps the first maximal sum above the running best
+    for (int base = 0; base < R.ncandidates; base += 64) {
+      const int k = base + lane;
+      float p2 = 0.0f, p3 = 0.0f, sum = -1.0f;
+      if (k < R.ncandidates) {
+        const gmapdp_microexon_candidate C = cands[R.cand_offset + k];
+        p2 = (float)maxent_prob(blocks, nwords, metab, C.model2 & 3, C.pos2, P.chroffset);
+        p3 = (float)maxent_prob(blocks, nwords, metab, C.model3 & 3, C.pos3, P.chroffset);
+        sum = p2 + p3;
+      }
+      float mx = sum;
+      for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+      if (mx > bestprob) {
+        const int j = __ffsll((long long)ballot(sum == mx)) - 1;
+        best = base + j;
+        b2 = __shfl(p2, j, 64);
+        b3 = __shfl(p3, j, 64);
+        bestprob = mx;
       }
     }
   }
@@ -312,11 +341,12 @@ hipError_t launch_mx_search(int n, hipStream_t s, const gmapdp_microexon_problem
 
 hipError_t launch_mx_finish(int n, hipStream_t s, const gmapdp_microexon_problem* probs, const uint32_t* blocks,
                             uint64_t nwords, const char* qseq, const char* qseq_uc, const uint8_t* constab,
-                            const gmapdp_microexon_candidate* cands, const double* cand_probs,
+                            const gmapdp_microexon_candidate* cands, const double* cand_probs, const double* metab,
                             gmapdp_microexon_result* results, gmapdp_pair* pairs, const int64_t* poff) {
   if (n <= 0) return hipSuccess;
+  if (!cand_probs && !metab) return hipErrorInvalidValue;
   hipLaunchKernelGGL(mx_finish_kernel, dim3(n), dim3(64), 0, s, probs, n, blocks, nwords, qseq, qseq_uc, constab,
-                     cands, cand_probs, results, pairs, poff);
+                     cands, cand_probs, metab, results, pairs, poff);
   return hipGetLastError();
 }
 

@@ -18,6 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GMAPDP_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libgmapdp.so")
 
 WATSON, JUMP_LATE, WIDEBAND = 0x1, 0x2, 0x4
+DEVICE = "device"  # splice / candidate probabilities evaluated by the engine's device MaxEnt (a NULL arena)
 CTX_ONE_STREAM, CTX_PRIO_HIGH, CTX_PRIO_LOW, CTX_BLOCKING_SYNC, CTX_POLL_SYNC = 0x1, 0x2, 0x4, 0x8, 0x10  # create_ex flags
 SIMD = 0x40  # GMAPDP_SIMD: the reference's SIMD builds' semantics (every problem family)
 HALFP, FINALP = 0x8, 0x10
@@ -172,7 +173,8 @@ class Mixed(C.Structure):
                 ("candidates_needed", C.c_size_t), ("finishes", C.c_void_p), ("nfinish", C.c_int),
                 ("finish_candidates", C.c_void_p), ("finish_probs", C.c_void_p), ("nfinish_candidates", C.c_size_t),
                 ("finish_results", C.c_void_p), ("finish_pairs", C.c_void_p), ("finish_pair_capacity", C.c_size_t),
-                ("known_sites", C.c_void_p), ("nknown", C.c_size_t)]
+                ("known_sites", C.c_void_p), ("nknown", C.c_size_t), ("wholes", C.c_void_p), ("nwhole", C.c_int),
+                ("whole_results", C.c_void_p), ("whole_pairs", C.c_void_p), ("whole_pair_capacity", C.c_size_t)]
 
 
 _lib = None
@@ -282,6 +284,9 @@ def load_library(path=LIB_PATH):
                                               C.c_size_t]),
         "gmapdp_microexon_pair_capacity": (C.c_size_t, [C.c_void_p, C.c_int]),
         "gmapdp_mixed_batch": (C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p, C.c_size_t, P(Mixed)]),
+        "gmapdp_maxent_available": (C.c_int, [C.c_char_p, C.c_size_t]),
+        "gmapdp_plan_bind_genome_maxent": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+        "gmapdp_maxent_sites": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
         "gmapdp_microexon_plan_create": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                                    C.c_size_t, P(C.c_void_p)]),
         "gmapdp_microexon_plan_candidates": (C.c_size_t, [C.c_void_p]),
@@ -531,17 +536,33 @@ class Engine:
                         decode_pairs(pairs, int(res["pair_offset"]), n_, calls[i]["dynprogindex"])))
         return out
 
+    # -- device MaxEnt (Maxent_hr_*_prob, maxent_hr.c:27357-27652) ------------------------------------
+    def maxent_sites(self, positions, models, chroffsets):
+        """Maxent_hr_<model>_prob(splice_pos, chroffset) per entry on the device (model GMAPDP_MAXENT_*)."""
+        pos = np.ascontiguousarray(positions, dtype=np.uint64)
+        mod = np.ascontiguousarray(models, dtype=np.uint8)
+        chro = np.ascontiguousarray(np.broadcast_to(np.asarray(chroffsets, dtype=np.uint64), pos.shape))
+        out = np.zeros(len(pos), dtype=np.float64)
+        self._check(self.lib.gmapdp_maxent_sites(self.h, pos.ctypes.data, mod.ctypes.data, chro.ctypes.data, len(pos),
+                                                 out.ctypes.data), "gmapdp_maxent_sites")
+        return out
+
     # -- batched Dynprog_genome_gap -------------------------------------------
     def genome_gap_batch_raw(self, probs, qbuf, qucbuf, splice_probs):
+        """splice_probs: the probability arena, or DEVICE (the engine's device MaxEnt: a NULL arena)."""
         n = len(probs)
         results = np.zeros(n, dtype=GENOME_RESULT_DTYPE)
         cap = self.lib.gmapdp_genome_pair_capacity(probs.ctypes.data, n)
         pairs = np.zeros(max(cap, 1), dtype=PAIR_DTYPE)
-        sp = np.ascontiguousarray(splice_probs, dtype=np.float64)
-        if sp.size == 0:
-            sp = np.zeros(1)
-        rc = self.lib.gmapdp_genome_gap_batch(self.h, probs.ctypes.data, n, qbuf, qucbuf, len(qbuf), sp.ctypes.data,
-                                              len(splice_probs), results.ctypes.data, pairs.ctypes.data, cap)
+        if isinstance(splice_probs, str) and splice_probs == DEVICE:
+            sp_ptr, nsp = None, 0
+        else:
+            sp = np.ascontiguousarray(splice_probs, dtype=np.float64)
+            if sp.size == 0:
+                sp = np.zeros(1)
+            sp_ptr, nsp = sp.ctypes.data, len(splice_probs)
+        rc = self.lib.gmapdp_genome_gap_batch(self.h, probs.ctypes.data, n, qbuf, qucbuf, len(qbuf), sp_ptr,
+                                              nsp, results.ctypes.data, pairs.ctypes.data, cap)
         self._check(rc, "gmapdp_genome_gap_batch")
         return results, pairs
 
@@ -552,6 +573,9 @@ class Engine:
         the queryjump)."""
         calls = list(calls)
         probs, qbuf, qucbuf, m = build_genome_batch(calls)
+        if isinstance(splice_probs, str) and splice_probs == DEVICE:
+            results, pairs = self.genome_gap_batch_raw(probs, qbuf, qucbuf, DEVICE)
+            return decode_genome_results(results, pairs, [p["dynprogindex"] for p in calls])
         arena = np.zeros(max(m, 1))
         for i, (lp, rp) in enumerate(splice_probs):
             o = int(probs[i]["prob_offset"])
@@ -565,8 +589,9 @@ class Engine:
         in the include/gmapdp.h layout (bridge left, bridge right, simple left, simple right), or None."""
         calls = list(calls)
         probs, qbuf, qucbuf, m = build_genome_batch(calls)
+        dev = isinstance(splice_probs, str) and splice_probs == DEVICE
         arena = np.zeros(max(m, 1))
-        for i, (lp, rp) in enumerate(splice_probs):
+        for i, (lp, rp) in enumerate([] if dev else splice_probs):
             o = int(probs[i]["prob_offset"])
             arena[o:o + len(lp)] = lp
             arena[o + len(lp):o + len(lp) + len(rp)] = rp
@@ -585,7 +610,8 @@ class Engine:
         pairs = np.zeros(max(cap, 1), dtype=PAIR_DTYPE)
         sp = np.ascontiguousarray(arena[:max(m, 1)])
         rc = self.lib.gmapdp_genome_gap_batch_known(self.h, probs.ctypes.data, n, qbuf, qucbuf, len(qbuf),
-                                                    sp.ctypes.data, m, kb.ctypes.data, ko, results.ctypes.data,
+                                                    None if dev else sp.ctypes.data, m, kb.ctypes.data, ko,
+                                                    results.ctypes.data,
                                                     pairs.ctypes.data, cap)
         self._check(rc, "gmapdp_genome_gap_batch_known")
         return decode_genome_results(results, pairs, [p["dynprogindex"] for p in calls])
@@ -749,7 +775,7 @@ class Engine:
     # -- the drop-in's dispatcher batch (gmapdp_mixed_batch) ---------------------------------------
     def mixed_batch_raw(self, qbuf, qucbuf, singles=None, ends=None, genomes=None, splice_probs=None,
                         searches=None, finishes=None, finish_cands=None, finish_probs=None, finish_results=None,
-                        candidate_capacity=None):
+                        candidate_capacity=None, wholes=None):
         """One gmapdp_mixed_batch call over one query arena (every section's qoff indexes qbuf).  Returns
         (return code, outputs: results, genome_results, pairs, search_results, candidates,
         candidates_needed, finish_results, finish_pairs) -- the caller checks the code (GMAPDP_ESPACE
@@ -759,8 +785,11 @@ class Engine:
         S, E = arr(singles, PROBLEM_DTYPE), arr(ends, END_PROBLEM_DTYPE)
         G = arr(genomes, GENOME_PROBLEM_DTYPE)
         XS, XF = arr(searches, MICROEXON_PROBLEM_DTYPE), arr(finishes, MICROEXON_PROBLEM_DTYPE)
-        sp = arr(splice_probs, np.float64)
-        fc, fp = arr(finish_cands, MICROEXON_CANDIDATE_DTYPE), arr(finish_probs, np.float64)
+        dev_sp = isinstance(splice_probs, str) and splice_probs == DEVICE
+        dev_fp = isinstance(finish_probs, str) and finish_probs == DEVICE
+        sp = arr(None if dev_sp else splice_probs, np.float64)
+        fc, fp = arr(finish_cands, MICROEXON_CANDIDATE_DTYPE), arr(None if dev_fp else finish_probs, np.float64)
+        XW = arr(wholes, MICROEXON_PROBLEM_DTYPE)
         fr = arr(finish_results, MICROEXON_RESULT_DTYPE).copy()
         lib = self.lib
         cap = (lib.gmapdp_single_pair_capacity(S.ctypes.data, len(S)) + lib.gmapdp_end_pair_capacity(E.ctypes.data, len(E))
@@ -772,15 +801,22 @@ class Engine:
                    search_results=np.zeros(max(1, len(XS)), dtype=MICROEXON_RESULT_DTYPE),
                    candidates=np.zeros(max(1, ccap), dtype=MICROEXON_CANDIDATE_DTYPE), finish_results=fr,
                    finish_pairs=np.zeros(max(1, lib.gmapdp_microexon_pair_capacity(XF.ctypes.data, len(XF))),
-                                         dtype=PAIR_DTYPE))
+                                         dtype=PAIR_DTYPE),
+                   whole_results=np.zeros(max(1, len(XW)), dtype=MICROEXON_RESULT_DTYPE),
+                   whole_pairs=np.zeros(max(1, lib.gmapdp_microexon_pair_capacity(XW.ctypes.data, len(XW))),
+                                        dtype=PAIR_DTYPE))
         m = Mixed(singles=S.ctypes.data, nsingle=len(S), ends=E.ctypes.data, nend=len(E), genomes=G.ctypes.data,
-                  ngenome=len(G), splice_probs=sp.ctypes.data, nprobs=len(sp), results=out["results"].ctypes.data,
+                  ngenome=len(G), splice_probs=None if dev_sp else sp.ctypes.data, nprobs=len(sp),
+                  results=out["results"].ctypes.data,
                   genome_results=out["genome_results"].ctypes.data, pairs=out["pairs"].ctypes.data,
                   pair_capacity=cap, searches=XS.ctypes.data, nsearch=len(XS),
                   search_results=out["search_results"].ctypes.data, candidates=out["candidates"].ctypes.data,
                   candidate_capacity=ccap, finishes=XF.ctypes.data, nfinish=len(XF), finish_candidates=fc.ctypes.data,
-                  finish_probs=fp.ctypes.data, nfinish_candidates=len(fc), finish_results=fr.ctypes.data,
-                  finish_pairs=out["finish_pairs"].ctypes.data, finish_pair_capacity=len(out["finish_pairs"]))
+                  finish_probs=None if dev_fp else fp.ctypes.data, nfinish_candidates=len(fc),
+                  finish_results=fr.ctypes.data, finish_pairs=out["finish_pairs"].ctypes.data,
+                  finish_pair_capacity=len(out["finish_pairs"]), wholes=XW.ctypes.data, nwhole=len(XW),
+                  whole_results=out["whole_results"].ctypes.data, whole_pairs=out["whole_pairs"].ctypes.data,
+                  whole_pair_capacity=len(out["whole_pairs"]))
         rc = lib.gmapdp_mixed_batch(self.h, qbuf, qucbuf, len(qbuf), C.byref(m))
         out["candidates_needed"] = int(m.candidates_needed)
         return rc, out
@@ -832,13 +868,14 @@ def _microexon_engine_methods():
         n = len(probs)
         cap = self.lib.gmapdp_microexon_pair_capacity(probs.ctypes.data, n)
         pairs = np.zeros(max(cap, 1), dtype=PAIR_DTYPE)
-        cp = np.ascontiguousarray(cand_probs, dtype=np.float64)
-        if cp.size == 0:
+        dev = isinstance(cand_probs, str) and cand_probs == DEVICE
+        cp = None if dev else np.ascontiguousarray(cand_probs, dtype=np.float64)
+        if cp is not None and cp.size == 0:
             cp = np.zeros(2)
         res = results.copy()
         rc = self.lib.gmapdp_microexon_finish(self.h, probs.ctypes.data, n, qb, qub, len(qb), cands.ctypes.data,
-                                              cp.ctypes.data, len(cands), res.ctypes.data, pairs.ctypes.data,
-                                              len(pairs))
+                                              None if dev else cp.ctypes.data, len(cands), res.ctypes.data,
+                                              pairs.ctypes.data, len(pairs))
         self._check(rc, "gmapdp_microexon_finish")
         return res, pairs
 
@@ -866,6 +903,9 @@ def _microexon_engine_methods():
         calls = list(calls)
         probs, qb, qub = build_microexon_batch(calls)
         results, cands = self.microexon_search_raw(probs, qb, qub)
+        if isinstance(maxent, str) and maxent == DEVICE:
+            res, pairs = self.microexon_finish_raw(probs, qb, qub, cands, DEVICE, results)
+            return decode_microexon(calls, res, pairs)
         cp = np.zeros(2 * len(cands))
         for i, (p, r) in enumerate(zip(calls, results)):
             o = int(r["cand_offset"])
@@ -874,24 +914,39 @@ def _microexon_engine_methods():
                 cp[2 * (o + k)] = maxent(int(c["model2"]), int(c["pos2"]), p["chroffset"])
                 cp[2 * (o + k) + 1] = maxent(int(c["model3"]), int(c["pos3"]), p["chroffset"])
         res, pairs = self.microexon_finish_raw(probs, qb, qub, cands, cp, results)
-        out = []
-        for p, r in zip(calls, res):
-            lst = None
-            if r["npairs"] >= 0:
-                lst = []
-                for rec in pairs[int(r["pair_offset"]):int(r["pair_offset"]) + int(r["npairs"])]:
-                    if rec["querypos"] == -1 and rec["genomepos"] == -1:
-                        lst.append((-1, -1, 0, int(rec["jump"]), 0, b" ", rec["comp"], b" ", b" ", 1))
-                    else:
-                        lst.append((int(rec["querypos"]), int(rec["genomepos"]), 0, 0, p["dynprogindex"], rec["cdna"],
-                                    rec["comp"], rec["genome"], rec["genomealt"], 0))
-            out.append(((int(r["dynprogindex"]), int(r["microintrontype"])),
-                        (float(r["bestprob2"]), float(r["bestprob3"])), lst))
-        return out
+        return decode_microexon(calls, res, pairs)
+
+    def microexon_whole_batch(self, calls):
+        """Dynprog_microexon_int over a batch in ONE gmapdp_mixed_batch round trip (the whole-call section:
+        search, device MaxEnt, choice); the same format as microexon_batch."""
+        calls = list(calls)
+        probs, qb, qub = build_microexon_batch(calls)
+        rc, out = self.mixed_batch_raw(qb, qub, wholes=probs)
+        self._check(rc, "gmapdp_mixed_batch (whole microexon calls)")
+        return decode_microexon(calls, out["whole_results"], out["whole_pairs"])
 
     return dict(build_microexon_batch=staticmethod(build_microexon_batch), microexon_search_raw=microexon_search_raw,
                 microexon_finish_raw=microexon_finish_raw, microexon_candidates=microexon_candidates,
-                microexon_batch=microexon_batch)
+                microexon_batch=microexon_batch, microexon_whole_batch=microexon_whole_batch)
+
+
+def decode_microexon(calls, res, pairs):
+    """Per call ((dynprogindex after, microintrontype), (bestprob2, bestprob3), pairs-or-None), the oracle's
+    format, from gmapdp_microexon_result records and their pairs."""
+    out = []
+    for p, r in zip(calls, res):
+        lst = None
+        if r["npairs"] >= 0:
+            lst = []
+            for rec in pairs[int(r["pair_offset"]):int(r["pair_offset"]) + int(r["npairs"])]:
+                if rec["querypos"] == -1 and rec["genomepos"] == -1:
+                    lst.append((-1, -1, 0, int(rec["jump"]), 0, b" ", rec["comp"], b" ", b" ", 1))
+                else:
+                    lst.append((int(rec["querypos"]), int(rec["genomepos"]), 0, 0, p["dynprogindex"], rec["cdna"],
+                                rec["comp"], rec["genome"], rec["genomealt"], 0))
+        out.append(((int(r["dynprogindex"]), int(r["microintrontype"])),
+                    (float(r["bestprob2"]), float(r["bestprob3"])), lst))
+    return out
 
 
 for _k, _v in _microexon_engine_methods().items():

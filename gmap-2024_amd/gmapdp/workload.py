@@ -306,14 +306,23 @@ def genome_gap_sites(layout, n, site_seed=23):
             "revR": revR}
 
 
+# Splice-site contexts planted around each genome gap's intron (strand sense): the donor's 3 exonic +
+# 6 intronic nt and the acceptor's 20 intronic + 3 exonic nt, strong sites under GMAP's MaxEnt models
+# (Maxent_hr_donor_prob / _acceptor_prob 0.999+, which the engine evaluates on the device in the step),
+# as real introns mostly are; the GT..AG dinucleotides are part of them.
+DONOR_CONTEXT = b"CAGGTAAGT"                    # x - 3 .. x + 5 (x = first intron base)
+ACCEPTOR_CONTEXT = b"CCTTTCTTTTCCTTTTCTAGGTA"   # y - 19 .. y + 3 (y = last intron base)
+
+
 def plant_sites(genome, st):
-    """Write the GT..AG dinucleotides of genome_gap_sites into `genome` (in place)."""
+    """Write the splice-site contexts of genome_gap_sites (GT..AG introns) into `genome` (in place)."""
     watson, choff, chrhigh = st["watson"], st["choff"], st["chrhigh"]
     x, y = st["goffL"] + st["a"], st["revR"] - st["b"]   # first / last intron base, strand coordinates
     idx, ch = [], []
-    for pos, c in ((x, "G"), (x + 1, "T"), (y - 1, "A"), (y, "G")):
+    ctx = [(x + k - 3, c) for k, c in enumerate(DONOR_CONTEXT)] + [(y + k - 19, c) for k, c in enumerate(ACCEPTOR_CONTEXT)]
+    for pos, c in ctx:
         idx.append(np.where(watson, choff + pos, chrhigh - pos))
-        ch.append(np.where(watson, ord(c), COMPL[ord(c)]).astype(np.uint8))
+        ch.append(np.where(watson, c, COMPL[c]).astype(np.uint8))
     genome[np.concatenate(idx)] = np.concatenate(ch)
 
 

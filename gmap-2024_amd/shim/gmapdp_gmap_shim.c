@@ -34,16 +34,24 @@
  * a message and abort() -- there is no silent CPU fallback.
  *
  * Batching.  GMAP's worker threads (gmap.c:4867) each issue their calls one at a time and wait for
- * the answer (the API is synchronous).  Here a call becomes a request on a process-wide queue and the
- * calling thread sleeps on it.  GMAPDP_SHIM_DISPATCHERS (default 3) dispatcher threads each own an
- * engine context with one high-priority stream (the genome is uploaded to HBM once and shared), so
- * that several batches are in flight; stage-2 calls have their own queue and
- * GMAPDP_SHIM_STAGE2_DISPATCHERS (default 1) dispatchers on low-priority streams;
- * a free dispatcher takes every request queued meanwhile and runs them together: all single / end /
- * genome gaps in one gmapdp_dynprog_batch, cDNA gaps and stage-2 seeding in their own batches.  The
- * callers then build their List_T from their own results in their own Pairpool.  With many worker
- * threads per GPU (gmap -t N, N well above the core count: the workers mostly wait) one launch set
- * carries many reads' calls.  GMAPDP_SHIM_STATS=1 prints the call counts and the mean batch size.
+ * the answer (the API is synchronous).  Here a call becomes a request on one of three process-wide queues
+ * and the calling thread sleeps on its own request.  Dispatcher threads each own an engine context with
+ * one stream (the genome is uploaded to HBM once and shared): GMAPDP_SHIM_DISPATCHERS (default 2) on
+ * queue 0, the short Dynprog_* calls (high-priority streams); GMAPDP_SHIM_LONG_DISPATCHERS (default 1) on
+ * queue 2, the long fills and stage 3's oligoindex calls; GMAPDP_SHIM_STAGE2_DISPATCHERS (default 2) on
+ * queue 1, Stage2_compute (low-priority streams).  That is five streams on HIP's default four hardware
+ * queues (GPU_MAX_HW_QUEUES), so two of them share a queue; end to end, four dispatchers (one stage-2)
+ * or more hardware queues measured slower (tools/e2e_timing.py --configs, profiles/r03_e2e).  A free
+ * dispatcher takes every request queued meanwhile and runs them together: single / end / genome gaps and
+ * microexon calls in one gmapdp_mixed_batch (one round trip), cDNA gaps, splice-junction ends and
+ * stage-2 seeding in their own batches.  The callers then build their List_T from their own results in
+ * their own Pairpool.  With many worker threads per GPU (gmap -t N, N well above the core count: the
+ * workers mostly wait) one launch set carries many reads' calls.  GMAPDP_SHIM_STATS=1 prints the call
+ * counts and the mean batch size.
+ *
+ * MaxEnt.  The genome gaps' splice probabilities and the microexon candidates' are evaluated by the
+ * engine on the device (Maxent_hr_*_prob restated over the HBM genome, bit-identical doubles), so a
+ * microexon call is one request; GMAPDP_SHIM_HOST_MAXENT=1 keeps the host's maxent_hr.c instead.
  */
 #ifndef _GNU_SOURCE
 #define _GNU_SOURCE
@@ -168,15 +176,188 @@ shim_check (int rc, const char *what) {
   }
 }
 
+#ifdef GMAPDP_SHIM_OWN
+/* ---- the rest of the Dynprog_* interface, owned here (GMAP links without the six dynprog*.o) ---- */
+
+/* consistent_array (dynprog.c:890) as Dynprog_init fills it (permute_cases / permute_cases_oneway,
+   :904-1004, with PREUC, dynprog.h:165: every case combination of a pair): the (query, genome) characters
+   that count as consistent, per genestrand -- [0] for STANDARD and the stranded modes, [+1] / [+2] for the
+   nonstranded ones.  Only Dynprog_consistent_p reads it; the engine has its own device tables. */
+static bool shim_consistent[3][128][128];
+
+static void
+shim_consistent_mark (int gs, int a, int b) {
+  const int as[2] = {a, a - 'A' + 'a'}, bs[2] = {b, b - 'A' + 'a'};
+  int i, j;
+  for (i = 0; i < 2; i++)
+    for (j = 0; j < 2; j++) shim_consistent[gs][as[i]][bs[j]] = true;
+}
+
+static void
+shim_consistent_pair (int a, int b, Mode_T mode) {  /* permute_cases: both orders */
+  if (mode == STANDARD || mode == CMET_STRANDED || mode == ATOI_STRANDED || mode == TTOC_STRANDED) {
+    shim_consistent_mark(0, a, b);
+    shim_consistent_mark(0, b, a);
+  } else {
+    shim_consistent_mark(1, a, b);
+    shim_consistent_mark(2, a, b);
+    shim_consistent_mark(1, b, a);
+    shim_consistent_mark(2, b, a);
+  }
+}
+
+static void
+shim_init_tables (Mode_T mode) {
+  /* FULLMATCH 'U'/'T', HALFMATCH and AMBIGUOUS IUPAC pairs, and N/N, X/X (dynprog.c:1094-1141) */
+  static const char pairs[][2] = {{'U', 'T'}, {'R', 'A'}, {'R', 'G'}, {'Y', 'T'}, {'Y', 'C'}, {'W', 'A'}, {'W', 'T'},
+                                  {'S', 'G'}, {'S', 'C'}, {'M', 'A'}, {'M', 'C'}, {'K', 'G'}, {'K', 'T'}, {'H', 'A'},
+                                  {'H', 'T'}, {'H', 'C'}, {'B', 'G'}, {'B', 'C'}, {'B', 'T'}, {'V', 'G'}, {'V', 'A'},
+                                  {'V', 'C'}, {'D', 'G'}, {'D', 'A'}, {'D', 'T'}, {'N', 'T'}, {'N', 'C'}, {'N', 'A'},
+                                  {'N', 'G'}, {'X', 'T'}, {'X', 'C'}, {'X', 'A'}, {'X', 'G'}, {'N', 'N'}, {'X', 'X'}};
+  int c;
+  size_t i;
+  memset(shim_consistent, 0, sizeof(shim_consistent));
+  for (c = 'A'; c < 'Z'; c++) shim_consistent_pair(c, c, mode);  /* 'A'..'Y', as :1089 */
+  for (i = 0; i < sizeof(pairs) / sizeof(pairs[0]); i++) shim_consistent_pair(pairs[i][0], pairs[i][1], mode);
+  switch (mode) {  /* the one-way pairs of the bisulfite / RNA-editing modes (:1145-1173) */
+  case STANDARD: break;
+  case CMET_STRANDED: shim_consistent_mark(0, 'T', 'C'); break;
+  case CMET_NONSTRANDED: shim_consistent_mark(1, 'T', 'C'); shim_consistent_mark(2, 'A', 'G'); break;
+  case ATOI_STRANDED: shim_consistent_mark(0, 'G', 'A'); break;
+  case ATOI_NONSTRANDED: shim_consistent_mark(1, 'G', 'A'); shim_consistent_mark(2, 'C', 'T'); break;
+  case TTOC_STRANDED: shim_consistent_mark(0, 'C', 'T'); break;
+  case TTOC_NONSTRANDED: shim_consistent_mark(1, 'C', 'T'); shim_consistent_mark(2, 'G', 'A'); break;
+  default:
+    fprintf(stderr, "Mode %d not recognized\n", mode);
+    exit(9);
+  }
+}
+
+bool
+Dynprog_consistent_p (int c, int g, int g_alt, int genestrand) {  /* dynprog.c:895 */
+  return shim_consistent[genestrand][c][g] || shim_consistent[genestrand][c][g_alt];
+}
+
 void
-__wrap_Dynprog_init (Mode_T mode) {
+Dynprog_term (Mode_T mode) {  /* dynprog.c:1203: the tables are static here */
+  (void) mode;
+}
+
+int
+Dynprog_score (int matches, int mismatches, int qopens, int qindels, int topens, int tindels, double defect_rate,
+               int user_open, int user_extend, bool user_dynprog_p) {  /* dynprog.c:126 */
+  int mismatch, open, extend;
+  if (user_dynprog_p == true) {
+    mismatch = MISMATCH_HIGHQ;
+    open = user_open;
+    extend = user_extend;
+  } else if (defect_rate < DEFECT_HIGHQ) {
+    mismatch = MISMATCH_HIGHQ;
+    open = SINGLE_OPEN_HIGHQ;
+    extend = SINGLE_EXTEND_HIGHQ;
+  } else if (defect_rate < DEFECT_MEDQ) {
+    mismatch = MISMATCH_MEDQ;
+    open = SINGLE_OPEN_MEDQ;
+    extend = SINGLE_EXTEND_MEDQ;
+  } else {
+    mismatch = MISMATCH_LOWQ;
+    open = SINGLE_OPEN_LOWQ;
+    extend = SINGLE_EXTEND_LOWQ;
+  }
+  return FULLMATCH * matches + mismatch * mismatches + open * qopens + extend * qindels + open * topens +
+         extend * tindels;
+}
+
+/* Dynprog_new (dynprog.c:631) as a limits-only handle: compute_maxlengths (:606) sets the two limits the
+   engine checks (shim_check_call); the score and direction arenas the reference allocates per worker
+   (12-17 MB each, three per worker thread) are never touched by the engine, so none are made. */
+Dynprog_T
+Dynprog_new (int maxlookback, int extraquerygap, int maxpeelback, int extramaterial_end, int extramaterial_paired,
+             bool doublep) {
+  Dynprog_T d = (Dynprog_T) calloc(1, sizeof(*d));
+  int max_rlength = maxlookback + maxpeelback, max_glength;
+  (void) doublep;
+  if (d == NULL) {
+    fprintf(stderr, "gmapdp shim: out of memory in Dynprog_new\n");
+    abort();
+  }
+  if (max_rlength < 500) max_rlength = 500;  /* QUERY_MAXLENGTH */
+  max_glength = max_rlength + extraquerygap +
+                (extramaterial_end > extramaterial_paired ? extramaterial_end : extramaterial_paired);
+  if (max_glength < 2000) max_glength = 2000;  /* GENOMIC_MAXLENGTH */
+  d->max_rlength = max_rlength;
+  d->max_glength = max_glength;
+  return d;
+}
+
+void
+Dynprog_free (Dynprog_T *old) {  /* dynprog.c:777 */
+  if (*old) {
+    free(*old);
+    *old = NULL;
+  }
+}
+
+static void shim_revcomp_inplace (char *s, int length);
+
+/* The far piece of a splice junction (Dynprog_make_splicejunction_5 / _3, dynprog_end.c:2569 / 2670):
+   splicelength genome characters that end at the far site (donor / antiacceptor) or start there
+   (acceptor / antidonor), reverse-complemented on the minus strand.  False when the piece would start
+   before the genome. */
+static bool
+shim_splicejunction_far (char *distal, char *distal_alt, Univcoord_T splicecoord, int splicelength,
+                         Splicetype_T far_splicetype, Genome_T genome, Genome_T genomealt, bool watsonp) {
+  if (far_splicetype == ACCEPTOR || far_splicetype == ANTIDONOR) {
+    Genome_fill_buffer_blocks_noterm(genome, genomealt, splicecoord, (Chrpos_T) splicelength, distal, distal_alt);
+  } else if (splicecoord <= (Univcoord_T) splicelength) {
+    return false;
+  } else if (far_splicetype == ANTIACCEPTOR || far_splicetype == DONOR) {
+    Genome_fill_buffer_blocks_noterm(genome, genomealt, splicecoord - splicelength, (Chrpos_T) splicelength, distal,
+                                     distal_alt);
+  } else {
+    fprintf(stderr, "Unexpected far_splicetype value %d\n", far_splicetype);
+    abort();
+  }
+  if (watsonp == false) {
+    shim_revcomp_inplace(distal, splicelength);
+    shim_revcomp_inplace(distal_alt, splicelength);
+  }
+  return true;
+}
+
+bool
+Dynprog_make_splicejunction_5 (char *splicejunction, char *splicejunction_alt, Univcoord_T splicecoord,
+                               int splicelength, int contlength, Splicetype_T far_splicetype, Genome_T genome,
+                               Genome_T genomealt, bool watsonp) {
+  (void) contlength;  /* the far piece leads the 5' junction */
+  return shim_splicejunction_far(splicejunction, splicejunction_alt, splicecoord, splicelength, far_splicetype,
+                                 genome, genomealt, watsonp);
+}
+
+bool
+Dynprog_make_splicejunction_3 (char *splicejunction, char *splicejunction_alt, Univcoord_T splicecoord,
+                               int splicelength, int contlength, Splicetype_T far_splicetype, Genome_T genome,
+                               Genome_T genomealt, bool watsonp) {
+  return shim_splicejunction_far(&splicejunction[contlength], &splicejunction_alt[contlength], splicecoord,
+                                 splicelength, far_splicetype, genome, genomealt, watsonp);
+}
+#endif
+
+void
+GMAPDP_DYNPROG_ENTRY(Dynprog_init) (Mode_T mode) {
+#ifdef GMAPDP_SHIM_OWN
+  shim_init_tables(mode);
+#else
   __real_Dynprog_init(mode);
+#endif
   shim_mode = (int) mode;
 }
 
 void
-__wrap_Dynprog_single_setup (int user_open_in, int user_extend_in, bool user_dynprog_p_in, bool homopolymerp_in) {
+GMAPDP_DYNPROG_ENTRY(Dynprog_single_setup) (int user_open_in, int user_extend_in, bool user_dynprog_p_in, bool homopolymerp_in) {
+#ifndef GMAPDP_SHIM_OWN
   __real_Dynprog_single_setup(user_open_in, user_extend_in, user_dynprog_p_in, homopolymerp_in);
+#endif
   shim_user_open = user_open_in;
   shim_user_extend = user_extend_in;
   shim_user_dynprog_p = user_dynprog_p_in ? 1 : 0;
@@ -193,7 +374,7 @@ static Trieoffset_T *shim_trieoffsets_obs = NULL, *shim_trieoffsets_max = NULL;
 static Triecontent_T *shim_triecontents_obs = NULL, *shim_triecontents_max = NULL;
 
 void
-__wrap_Dynprog_end_setup (Univcoord_T *splicesites_in, Splicetype_T *splicetypes_in, Chrpos_T *splicedists_in,
+GMAPDP_DYNPROG_ENTRY(Dynprog_end_setup) (Univcoord_T *splicesites_in, Splicetype_T *splicetypes_in, Chrpos_T *splicedists_in,
                           int nsplicesites_in, Trieoffset_T *trieoffsets_obs_in, Triecontent_T *triecontents_obs_in,
                           Trieoffset_T *trieoffsets_max_in, Triecontent_T *triecontents_max_in,
                           int user_open_in, int user_extend_in, bool user_dynprog_p_in) {
@@ -204,9 +385,16 @@ __wrap_Dynprog_end_setup (Univcoord_T *splicesites_in, Splicetype_T *splicetypes
   shim_triecontents_obs = triecontents_obs_in;
   shim_trieoffsets_max = trieoffsets_max_in;
   shim_triecontents_max = triecontents_max_in;
+#ifdef GMAPDP_SHIM_OWN
+  (void) splicedists_in;
+  (void) user_open_in;
+  (void) user_extend_in;
+  (void) user_dynprog_p_in;
+#else
   __real_Dynprog_end_setup(splicesites_in, splicetypes_in, splicedists_in, nsplicesites_in, trieoffsets_obs_in,
                            triecontents_obs_in, trieoffsets_max_in, triecontents_max_in, user_open_in,
                            user_extend_in, user_dynprog_p_in);
+#endif
 }
 
 /* The splicing IIT of -s as Dynprog_genome_setup records it (dynprog_genome.c:192-214): the genome
@@ -216,7 +404,7 @@ static int *shim_siit_cross = NULL;
 static int shim_donor_typeint = -1, shim_acceptor_typeint = -1;
 
 void
-__wrap_Dynprog_genome_setup (bool novelsplicingp_in, IIT_T splicing_iit_in, int *splicing_divint_crosstable_in,
+GMAPDP_DYNPROG_ENTRY(Dynprog_genome_setup) (bool novelsplicingp_in, IIT_T splicing_iit_in, int *splicing_divint_crosstable_in,
                              int donor_typeint_in, int acceptor_typeint_in, int user_open_in, int user_extend_in,
                              bool user_dynprog_p_in) {
   if (splicing_iit_in != NULL) {
@@ -227,8 +415,10 @@ __wrap_Dynprog_genome_setup (bool novelsplicingp_in, IIT_T splicing_iit_in, int 
       shim_refuse("a known-introns file (-s without donor/acceptor tags: intron-level bridging)");
     if (!novelsplicingp_in) shim_refuse("known splice sites with novel splicing off");
   }
+#ifndef GMAPDP_SHIM_OWN
   __real_Dynprog_genome_setup(novelsplicingp_in, splicing_iit_in, splicing_divint_crosstable_in, donor_typeint_in,
                               acceptor_typeint_in, user_open_in, user_extend_in, user_dynprog_p_in);
+#endif
   shim_splicing_iit = splicing_iit_in != NULL;
   shim_siit = splicing_iit_in;
   shim_siit_cross = splicing_divint_crosstable_in;
@@ -354,8 +544,21 @@ shim_context (Genome_T genome) {
 }
 
 /* ---- requests and the dispatcher ---- */
-enum { K_SINGLE, K_END, K_GENOME, K_CDNA, K_MXS, K_MXF, K_OLIGO, K_STAGE2, K_SJ };  /* K_MXS / K_MXF: microexon
-                                                                                   search / finish */
+enum { K_SINGLE, K_END, K_GENOME, K_CDNA, K_MXS, K_MXF, K_OLIGO, K_STAGE2, K_SJ, K_MXW };  /* K_MXS / K_MXF: microexon
+                                                                   search / finish; K_MXW: the whole call */
+
+/* MaxEnt splice-site probabilities: on the device (the engine's Maxent_hr_*_prob restatement over its HBM
+   genome, bit-identical doubles; include/gmapdp.h "Device MaxEnt") unless GMAPDP_SHIM_HOST_MAXENT=1, which
+   keeps the host's own maxent_hr.c on the calling thread (two round trips per microexon call). */
+static int shim_host_maxent = -1;
+static int
+shim_use_host_maxent (void) {
+  if (shim_host_maxent < 0) {
+    const char *st = getenv("GMAPDP_SHIM_HOST_MAXENT");
+    shim_host_maxent = st != NULL && st[0] == '1';
+  }
+  return shim_host_maxent;
+}
 
 typedef struct shim_req {
   int kind;
@@ -571,8 +774,12 @@ typedef struct {
   size_t sjcap, sjrescap, jqcap;
   uint8_t *kn;
   size_t kncap;
-  shim_req **rs, **re, **rg, **rc, **ro, **r2, **rxs, **rxf, **rsj;
-  size_t scap, ecap, gcap, ccap, ocap, s2cap, rscap, recap, rgcap, rccap, rocap, r2cap, rxscap, rxfcap, rsjcap;
+  shim_req **rs, **re, **rg, **rc, **ro, **r2, **rxs, **rxf, **rsj, **rxw;
+  size_t scap, ecap, gcap, ccap, ocap, s2cap, rscap, recap, rgcap, rccap, rocap, r2cap, rxscap, rxfcap, rsjcap, rxwcap;
+  gmapdp_microexon_problem *mxw;             /* whole calls */
+  gmapdp_microexon_result *mxwres;
+  gmapdp_pair *mxwpairs;
+  size_t mxwcap, mxwrescap, mxwpaircap;
   gmapdp_microexon_problem *mx, *mxf;        /* searches, finishes */
   gmapdp_microexon_result *mxres, *mxfres;
   gmapdp_microexon_candidate *mxc, *mxsc;     /* the finishes' candidates, the searches' candidates */
@@ -610,7 +817,7 @@ shim_copy_pairs (shim_req *r, const gmapdp_pair *src, int n) {
 static void
 shim_run (shim_req *batch) {
   shim_req *r;
-  size_t ns = 0, ne = 0, ng = 0, nc = 0, no = 0, n2 = 0, nxs = 0, nxf = 0, nsj = 0, n = 0, qb = 0, pb = 0, cap, i;
+  size_t ns = 0, ne = 0, ng = 0, nc = 0, no = 0, n2 = 0, nxs = 0, nxf = 0, nsj = 0, nxw = 0, n = 0, qb = 0, pb = 0, cap, i;
   double t0, t1, td[4];
   Genome_T genome = NULL;
   for (r = batch; r != NULL; r = r->next) {
@@ -625,6 +832,7 @@ shim_run (shim_req *batch) {
     case K_MXS: GROW(D.rxs, D.rxscap, nxs + 1); D.rxs[nxs++] = r; break;
     case K_MXF: GROW(D.rxf, D.rxfcap, nxf + 1); D.rxf[nxf++] = r; break;
     case K_SJ: GROW(D.rsj, D.rsjcap, nsj + 1); D.rsj[nsj++] = r; break;
+    case K_MXW: GROW(D.rxw, D.rxwcap, nxw + 1); D.rxw[nxw++] = r; break;
     default: GROW(D.ro, D.rocap, no + 1); D.ro[no++] = r; break;
     }
   }
@@ -637,9 +845,10 @@ shim_run (shim_req *batch) {
   /* single, end and genome gaps and the microexon searches / finishes: one round trip over one query
      arena (gmapdp_mixed_batch) */
   t0 = shim_now();
-  if (ns + ne + ng + nxs + nxf > 0) {
+  if (ns + ne + ng + nxs + nxf + nxw > 0) {
     gmapdp_mixed M;
-    size_t nct = 0, xcap;
+    size_t nct = 0, xcap, wcap;
+    int dev_probs = 0;
     int rc;
     memset(&M, 0, sizeof(M));
     qb = 0;
@@ -658,7 +867,11 @@ shim_run (shim_req *batch) {
       qb += D.rg[i]->qlen;
       pb += D.rg[i]->nprobs;
       kb += D.rg[i]->nknown;
+      dev_probs |= D.rg[i]->probs == NULL;  /* device MaxEnt (every request of a process alike) */
     }
+    GROW(D.mxw, D.mxwcap, nxw + 1);
+    GROW(D.mxwres, D.mxwrescap, nxw + 1);
+    for (i = 0; i < nxw; i++) qb += D.rxw[i]->qlen;
     GROW(D.kn, D.kncap, kb + 1);
     kb = 0;
     for (i = 0; i < nxs; i++) qb += D.rxs[i]->qlen;
@@ -694,7 +907,7 @@ shim_run (shim_req *batch) {
       D.g[i] = D.rg[i]->p.g;
       STAGE(D.rg[i], D.g[i]);
       D.g[i].prob_offset = (int64_t) pb;
-      if (D.rg[i]->nprobs) memcpy(D.pr + pb, D.rg[i]->probs, D.rg[i]->nprobs * sizeof(double));
+      if (D.rg[i]->nprobs && D.rg[i]->probs) memcpy(D.pr + pb, D.rg[i]->probs, D.rg[i]->nprobs * sizeof(double));
       pb += D.rg[i]->nprobs;
       if (D.rg[i]->nknown) {
         D.g[i].known_offset = (int32_t) kb;
@@ -705,6 +918,10 @@ shim_run (shim_req *batch) {
     for (i = 0; i < nxs; i++) {
       D.mx[i] = D.rxs[i]->p.mx;
       STAGE(D.rxs[i], D.mx[i]);
+    }
+    for (i = 0; i < nxw; i++) {
+      D.mxw[i] = D.rxw[i]->p.mx;
+      STAGE(D.rxw[i], D.mxw[i]);
     }
     nct = 0;
     for (i = 0; i < nxf; i++) {
@@ -728,13 +945,15 @@ shim_run (shim_req *batch) {
     xcap = gmapdp_microexon_pair_capacity(D.mxf, (int) nxf);
     GROW(D.mxpairs, D.mxpaircap, xcap + 1);
     GROW(D.mxsc, D.mxsccap, 8 * nxs + 64);
+    wcap = gmapdp_microexon_pair_capacity(D.mxw, (int) nxw);
+    GROW(D.mxwpairs, D.mxwpaircap, wcap + 1);
     M.singles = D.s;
     M.nsingle = (int) ns;
     M.ends = D.e;
     M.nend = (int) ne;
     M.genomes = D.g;
     M.ngenome = (int) ng;
-    M.splice_probs = D.pr;
+    M.splice_probs = dev_probs ? NULL : D.pr;
     M.nprobs = pb;
     M.results = D.res;
     M.genome_results = D.gres;
@@ -755,6 +974,11 @@ shim_run (shim_req *batch) {
     M.candidate_capacity = D.mxsccap;
     M.known_sites = kb ? D.kn : NULL;
     M.nknown = kb;
+    M.wholes = D.mxw;
+    M.nwhole = (int) nxw;
+    M.whole_results = D.mxwres;
+    M.whole_pairs = D.mxwpairs;
+    M.whole_pair_capacity = wcap;
     rc = gmapdp_mixed_batch(shim_ctx, D.q, D.quc, qb, &M);
     while (rc == GMAPDP_ESPACE) {  /* (rare) the searches found more candidates than D.mxsc holds */
       size_t need = M.candidates_needed;
@@ -793,6 +1017,12 @@ shim_run (shim_req *batch) {
       r = D.rxf[i];
       r->mxr = D.mxfres[i];
       if (r->mxr.npairs > 0) shim_copy_pairs(r, D.mxpairs + r->mxr.pair_offset, r->mxr.npairs);
+      r->mxr.pair_offset = 0;
+    }
+    for (i = 0; i < nxw; i++) {
+      r = D.rxw[i];
+      r->mxr = D.mxwres[i];
+      if (r->mxr.npairs > 0) shim_copy_pairs(r, D.mxwpairs + r->mxr.pair_offset, r->mxr.npairs);
       r->mxr.pair_offset = 0;
     }
   }
@@ -1007,7 +1237,7 @@ shim_list (const gmapdp_pair *pairs, int n, int dynprogindex, int gap_index, int
 }
 
 List_T
-__wrap_Dynprog_single_gap (int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches, int *nopens,
+GMAPDP_DYNPROG_ENTRY(Dynprog_single_gap) (int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches, int *nopens,
                            int *nindels, Dynprog_T dynprog, char *sequence1, char *sequenceuc1, int length1,
                            int length2, int offset1, int offset2, Univcoord_T chroffset, Univcoord_T chrhigh,
                            bool watsonp, int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
@@ -1098,7 +1328,7 @@ shim_end_gap (int end3p, int *dynprogindex, int *finalscore, int *nmatches, int 
 }
 
 List_T
-__wrap_Dynprog_end5_gap (int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches, int *nopens,
+GMAPDP_DYNPROG_ENTRY(Dynprog_end5_gap) (int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches, int *nopens,
                          int *nindels, Dynprog_T dynprog, char *revsequence1, char *revsequenceuc1, int length1,
                          int length2, int revoffset1, int revoffset2, Univcoord_T chroffset, Univcoord_T chrhigh,
                          bool watsonp, int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
@@ -1111,7 +1341,7 @@ __wrap_Dynprog_end5_gap (int *dynprogindex, int *finalscore, int *nmatches, int 
 }
 
 List_T
-__wrap_Dynprog_end3_gap (int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches, int *nopens,
+GMAPDP_DYNPROG_ENTRY(Dynprog_end3_gap) (int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches, int *nopens,
                          int *nindels, Dynprog_T dynprog, char *sequence1, char *sequenceuc1, int length1,
                          int length2, int offset1, int offset2, Univcoord_T chroffset, Univcoord_T chrhigh,
                          bool watsonp, int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
@@ -1201,7 +1431,7 @@ shim_splicejunction (int end3p, int *dynprogindex, int *finalscore, int *misssco
 }
 
 List_T
-__wrap_Dynprog_end5_splicejunction (int *dynprogindex, int *finalscore, int *missscore, int *nmatches,
+GMAPDP_DYNPROG_ENTRY(Dynprog_end5_splicejunction) (int *dynprogindex, int *finalscore, int *missscore, int *nmatches,
                                     int *nmismatches, int *nopens, int *nindels, Dynprog_T dynprog,
                                     char *rev_rsequence, char *rev_rsequenceuc, char *rev_gsequence,
                                     char *rev_gsequence_alt, int length1, int length2, int revoffset1,
@@ -1219,7 +1449,7 @@ __wrap_Dynprog_end5_splicejunction (int *dynprogindex, int *finalscore, int *mis
 }
 
 List_T
-__wrap_Dynprog_end3_splicejunction (int *dynprogindex, int *finalscore, int *missscore, int *nmatches,
+GMAPDP_DYNPROG_ENTRY(Dynprog_end3_splicejunction) (int *dynprogindex, int *finalscore, int *missscore, int *nmatches,
                                     int *nmismatches, int *nopens, int *nindels, Dynprog_T dynprog, char *rsequence,
                                     char *rsequenceuc, char *gsequence, char *gsequence_alt, int length1,
                                     int length2, int offset1, int offset2_anchor, int offset2_far,
@@ -1311,11 +1541,11 @@ shim_known (int end3p, bool *knownsplicep, int *dynprogindex, int *finalscore, i
   perfect_score = rlength * FULLMATCH;
 
   /* without splicing, all the way to the query end */
-  best_pairs = end3p ? __wrap_Dynprog_end3_gap(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels,
+  best_pairs = end3p ? GMAPDP_DYNPROG_ENTRY(Dynprog_end3_gap)(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels,
                                                dynprog, seq, sequc, rlength, glength, roffset, goffset, chroffset,
                                                chrhigh, watsonp, genestrand, jump_late_p, genome, genomealt,
                                                pairpool, extraband_end, defect_rate, QUERYEND_NOGAPS, true)
-                     : __wrap_Dynprog_end5_gap(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels,
+                     : GMAPDP_DYNPROG_ENTRY(Dynprog_end5_gap)(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels,
                                                dynprog, seq, sequc, rlength, glength, roffset, goffset, chroffset,
                                                chrhigh, watsonp, genestrand, jump_late_p, genome, genomealt,
                                                pairpool, extraband_end, defect_rate, QUERYEND_NOGAPS, true);
@@ -1420,11 +1650,11 @@ shim_known (int end3p, bool *knownsplicep, int *dynprogindex, int *finalscore, i
       /* not to the query end this time: the best local end (chopped to the Dynprog_T's limits) */
       if (rlength > dynprog->max_rlength) rlength = dynprog->max_rlength;
       if (glength > dynprog->max_glength) glength = dynprog->max_glength;
-      orig_pairs = end3p ? __wrap_Dynprog_end3_gap(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels,
+      orig_pairs = end3p ? GMAPDP_DYNPROG_ENTRY(Dynprog_end3_gap)(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels,
                                                    dynprog, seq, sequc, rlength, glength, roffset, goffset, chroffset,
                                                    chrhigh, watsonp, genestrand, jump_late_p, genome, genomealt,
                                                    pairpool, extraband_end, defect_rate, BEST_LOCAL, false)
-                         : __wrap_Dynprog_end5_gap(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels,
+                         : GMAPDP_DYNPROG_ENTRY(Dynprog_end5_gap)(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels,
                                                    dynprog, seq, sequc, rlength, glength, roffset, goffset, chroffset,
                                                    chrhigh, watsonp, genestrand, jump_late_p, genome, genomealt,
                                                    pairpool, extraband_end, defect_rate, BEST_LOCAL, false);
@@ -1452,7 +1682,7 @@ shim_known (int end3p, bool *knownsplicep, int *dynprogindex, int *finalscore, i
 }
 
 List_T
-__wrap_Dynprog_end5_known (bool *knownsplicep, int *dynprogindex, int *finalscore, int *ambig_end_length,
+GMAPDP_DYNPROG_ENTRY(Dynprog_end5_known) (bool *knownsplicep, int *dynprogindex, int *finalscore, int *ambig_end_length,
                            Splicetype_T *ambig_splicetype, int *nmatches, int *nmismatches, int *nopens, int *nindels,
                            Dynprog_T dynprog, char *revsequence1, char *revsequenceuc1, int length1, int length2,
                            int revoffset1, int revoffset2, Univcoord_T chroffset, Univcoord_T chrhigh,
@@ -1467,7 +1697,7 @@ __wrap_Dynprog_end5_known (bool *knownsplicep, int *dynprogindex, int *finalscor
 }
 
 List_T
-__wrap_Dynprog_end3_known (bool *knownsplicep, int *dynprogindex, int *finalscore, int *ambig_end_length,
+GMAPDP_DYNPROG_ENTRY(Dynprog_end3_known) (bool *knownsplicep, int *dynprogindex, int *finalscore, int *ambig_end_length,
                            Splicetype_T *ambig_splicetype, int *nmatches, int *nmismatches, int *nopens, int *nindels,
                            Dynprog_T dynprog, char *sequence1, char *sequenceuc1, int length1, int length2, int offset1,
                            int offset2, int querylength, Univcoord_T chroffset, Univcoord_T chrhigh,
@@ -1492,7 +1722,7 @@ shim_maxent (Genome_T genome, Genome_T genomealt, uint8_t model, gmapdp_coord_t 
 }
 
 List_T
-__wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_rightgenomepos, double *left_prob,
+GMAPDP_DYNPROG_ENTRY(Dynprog_genome_gap) (int *dynprogindex, int *new_leftgenomepos, int *new_rightgenomepos, double *left_prob,
                            double *right_prob, int *traceback_score, int *nmatches, int *nmismatches, int *nopens,
                            int *nindels, int *exonhead, int *introntype, Dynprog_T dynprogL, Dynprog_T dynprogR,
                            char *rsequence, char *rsequenceuc, int rlength, int glengthL, int glengthR, int roffset,
@@ -1537,8 +1767,8 @@ __wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_r
       glengthR <= GMAPDP_MAX_GLENGTH && glengthL > 0 && glengthR > 0)
     m = gmapdp_genome_prob_entries(p, 1);
   GROW(r->pbuf, r->pbufcap, m + 1);
-  memset(r->pbuf, 0, (m + 1) * sizeof(double));
-  if (m) {
+  if (m && shim_use_host_maxent()) {
+    memset(r->pbuf, 0, (m + 1) * sizeof(double));
     GROW(pos, poscap, m);
     GROW(model, modelcap, m);
     shim_check(gmapdp_genome_splice_sites(p, 1, pos, model, m), "gmapdp_genome_splice_sites");
@@ -1546,6 +1776,8 @@ __wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_r
     for (i = 0; i < m; i++)
       if (i != (size_t) glengthL - 1 && i != m - 1)
         r->pbuf[i] = shim_maxent(genome, genomealt, model[i], pos[i], chroffset);
+  }
+  if (m) {
     if (shim_siit != NULL) {
       /* known splice sites: the bridge's flags over the two windows and genome_gap_simple's over
          rlength (dynprog_genome.c:2938-2942, 3045-3049); the probabilities stay MaxEnt's */
@@ -1565,7 +1797,7 @@ __wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_r
   r->q = rsequence;
   r->quc = rsequenceuc;
   r->qlen = rlength > 0 ? (size_t) rlength : 0;
-  r->probs = r->pbuf;
+  r->probs = shim_use_host_maxent() ? r->pbuf : NULL;  /* NULL: the engine evaluates them on the device */
   r->nprobs = m;
   r->cost = m == 0 ? 0 : 2 * shim_cost(rlength, glengthL > glengthR ? glengthL : glengthR, extraband_paired);
   r->longp = r->cost > shim_long_cost;
@@ -1591,7 +1823,7 @@ __wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_r
 }
 
 List_T
-__wrap_Dynprog_cdna_gap (int *dynprogindex, int *traceback_score, bool *incompletep, Dynprog_T dynprogL,
+GMAPDP_DYNPROG_ENTRY(Dynprog_cdna_gap) (int *dynprogindex, int *traceback_score, bool *incompletep, Dynprog_T dynprogL,
                          Dynprog_T dynprogR, char *rsequenceL, char *rsequence_ucL, char *rev_rsequenceR,
                          char *rev_rsequence_ucR, int rlengthL, int rlengthR, int glength, int roffsetL,
                          int rev_roffsetR, int goffset, Univcoord_T chroffset, Univcoord_T chrhigh, bool watsonp,
@@ -1647,11 +1879,12 @@ __wrap_Dynprog_cdna_gap (int *dynprogindex, int *traceback_score, bool *incomple
 }
 
 /* ---- Dynprog_microexon_int (dynprog_single.c:900, called at stage3.c:9664) ----
-   Two requests: the GPU lists the candidates, this thread scores them with the host's MaxEnt models (as
-   the reference does, maxent_hr.c), the GPU picks the winner and builds make_microexon_pairs_double's
-   list, which is rebuilt here in the caller's Pairpool with the gap holders' comp set. */
+   One request (K_MXW): the GPU lists the candidates, scores their splice sites with its MaxEnt models,
+   picks the winner and builds make_microexon_pairs_double's list, which is rebuilt here in the caller's
+   Pairpool with the gap holders' comp set.  With GMAPDP_SHIM_HOST_MAXENT=1: two requests, the candidates
+   scored on this thread with the host's maxent_hr.c in between. */
 List_T
-__wrap_Dynprog_microexon_int (double *bestprob2, double *bestprob3, int *dynprogindex, int *microintrontype,
+GMAPDP_DYNPROG_ENTRY(Dynprog_microexon_int) (double *bestprob2, double *bestprob3, int *dynprogindex, int *microintrontype,
                               char *rsequence, char *rsequenceuc, int rlength, int roffset, int goffsetL,
                               int rev_goffsetR, int cdna_direction, char *queryseq, char *queryuc,
                               Univcoord_T chroffset, Univcoord_T chrhigh, bool watsonp, int genestrand,
@@ -1665,7 +1898,7 @@ __wrap_Dynprog_microexon_int (double *bestprob2, double *bestprob3, int *dynprog
   /* make_microexon_pairs_double reads queryseq[roffset + i]; the engine reads the slice */
   if (rsequence != queryseq + roffset || rsequenceuc != queryuc + roffset)
     shim_refuse("Dynprog_microexon_int with rsequence other than queryseq + roffset");
-  r = shim_request(K_MXS);
+  r = shim_request(shim_use_host_maxent() ? K_MXS : K_MXW);
   p = &r->p.mx;
   p->qoff = 0;
   p->rlength = rlength;
@@ -1682,15 +1915,17 @@ __wrap_Dynprog_microexon_int (double *bestprob2, double *bestprob3, int *dynprog
   r->q = rsequence;
   r->quc = rsequenceuc;
   r->qlen = (size_t) (rlength > 0 ? rlength : 0);
-  shim_submit(r);
-  GROW(r->mxp, r->mxpcap, 2 * (size_t) r->mxr.ncandidates + 2);
-  for (k = 0; k < r->mxr.ncandidates; k++) {
-    const gmapdp_microexon_candidate *c = &r->mxc[k];
-    r->mxp[2 * k] = shim_maxent(genome, genomealt, c->model2, c->pos2, chroffset);
-    r->mxp[2 * k + 1] = shim_maxent(genome, genomealt, c->model3, c->pos3, chroffset);
-  }
   GROW(r->pairs, r->pcap, gmapdp_microexon_pair_capacity(p, 1) + 1);
-  r->kind = K_MXF;
+  if (r->kind == K_MXS) {
+    shim_submit(r);
+    GROW(r->mxp, r->mxpcap, 2 * (size_t) r->mxr.ncandidates + 2);
+    for (k = 0; k < r->mxr.ncandidates; k++) {
+      const gmapdp_microexon_candidate *c = &r->mxc[k];
+      r->mxp[2 * k] = shim_maxent(genome, genomealt, c->model2, c->pos2, chroffset);
+      r->mxp[2 * k + 1] = shim_maxent(genome, genomealt, c->model3, c->pos3, chroffset);
+    }
+    r->kind = K_MXF;
+  }
   shim_submit(r);
   shim_count(ST_MICROEXON);
   for (k = r->mxr.npairs - 1; k >= 0; k--) {

@@ -258,6 +258,27 @@ typedef struct {
 #define GMAPDP_MAXENT_ANTIDONOR    2  /* Maxent_hr_antidonor_prob */
 #define GMAPDP_MAXENT_ANTIACCEPTOR 3  /* Maxent_hr_antiacceptor_prob */
 
+/* Device MaxEnt.  The engine evaluates Maxent_hr_{donor,acceptor,antidonor,antiacceptor}_prob
+ * (maxent_hr.c:27357 / 27433 / 27512 / 27586) itself, on the HBM-resident genome, bit-identical doubles
+ * (genomealt == genome, the engine's scope).  The model tables are the reference's constants
+ * (maxent_hr.c:25-24660) as tools/make_maxent_tables.py writes them: maxent_hr_tables.bin next to
+ * libgmapdp.so, or the file GMAPDP_MAXENT_TABLES names; loaded on first use, once per device.
+ *   - genome gaps: pass splice_probs = NULL (gmapdp_genome_gap_batch[_known], gmapdp_dynprog_batch,
+ *     gmapdp_mixed.splice_probs) and the probability entries are computed on the device in the batch's
+ *     stream (nprobs / nsplice_probs still give the arena size, gmapdp_genome_prob_entries);
+ *   - microexons: gmapdp_microexon_finish with cand_probs = NULL (gmapdp_mixed.finish_probs = NULL)
+ *     evaluates the candidates' two sites in the finish kernel; gmapdp_mixed's "whole microexon" section
+ *     runs search and finish in the one round trip;
+ *   - plans: gmapdp_plan_bind_genome_maxent; gmapdp_microexon_plan_run with d_cand_probs = NULL.
+ * Missing tables make these calls fail with GMAPDP_EINVAL ("maxent tables: ...") -- never a host
+ * fallback. */
+/* 1 when the tables load (host only, no device needed), else 0; path: the file used or looked for. */
+int gmapdp_maxent_available (char *path, size_t path_bytes);
+/* out[i] = Maxent_hr_<models[i]>_prob(splice_pos = positions[i], chroffset = chroffsets[i]) on ctx's genome
+ * (synchronous). */
+int gmapdp_maxent_sites (gmapdp_ctx *ctx, const gmapdp_coord_t *positions, const uint8_t *models,
+                         const gmapdp_coord_t *chroffsets, size_t n, double *out);
+
 /* For each problem, write glengthL + glengthR (splicesitepos, model) pairs
  * at the problem's prob_offset: the arguments of the Maxent_hr_*_prob call
  * (with the problem's chroffset) whose result belongs at that entry
@@ -457,7 +478,7 @@ size_t gmapdp_microexon_pair_capacity (const gmapdp_microexon_problem *problems,
  * mean; a section with n = 0 is skipped.  The rare search that overflows the candidate pool is
  * rerun as gmapdp_microexon_search would (extra round trips).  GMAPDP_ESPACE: candidate_capacity or
  * finish_pair_capacity too small (*candidates_needed holds the size required); everything else is
- * then still filled in. */
+ * then still filled in.  splice_probs = NULL / finish_probs = NULL: device MaxEnt (see "Device MaxEnt"). */
 typedef struct {
   const gmapdp_single_problem *singles; int nsingle;
   const gmapdp_end_problem *ends; int nend;
@@ -474,6 +495,13 @@ typedef struct {
   gmapdp_microexon_result *finish_results;   /* in: the searches' results; out: the choices */
   gmapdp_pair *finish_pairs; size_t finish_pair_capacity;
   const uint8_t *known_sites; size_t nknown; /* GMAPDP_KNOWN_SITES genome gaps' arena (else NULL, 0) */
+  /* whole Dynprog_microexon_int calls: the search, the candidates' MaxEnt on the device and the choice,
+   * all in this batch (the candidates stay on the device); whole_results as gmapdp_microexon_finish
+   * leaves them, call i's pairs at the prefix sum of the earlier calls' rlength + 2
+   * (gmapdp_microexon_pair_capacity) */
+  const gmapdp_microexon_problem *wholes; int nwhole;
+  gmapdp_microexon_result *whole_results;
+  gmapdp_pair *whole_pairs; size_t whole_pair_capacity;
 } gmapdp_mixed;
 int gmapdp_mixed_batch (gmapdp_ctx *ctx, const char *qseq, const char *qseq_uc, size_t qbytes, gmapdp_mixed *m);
 
@@ -727,6 +755,10 @@ int gmapdp_plan_create_all (gmapdp_ctx *ctx, const gmapdp_single_problem *single
  * results (indexed by gmapdp_plan_genome_dev_index).  Required before running a plan
  * that has genome-gap problems on the GPU. */
 int gmapdp_plan_bind_genome (gmapdp_plan *plan, const double *d_splice_probs, gmapdp_genome_result *d_genome_results);
+/* The same with device MaxEnt: d_splice_probs (gmapdp_genome_prob_entries doubles) is scratch that each
+ * genome-gap launch class fills for its own problems on its own stream before its fill kernel. */
+int gmapdp_plan_bind_genome_maxent (gmapdp_ctx *ctx, gmapdp_plan *plan, double *d_splice_probs,
+                                    gmapdp_genome_result *d_genome_results);
 int gmapdp_plan_genome_gpu_problems (const gmapdp_plan *plan);
 int gmapdp_plan_genome_dev_index (const gmapdp_plan *plan, int j);
 /* 0: Dynprog_single_gap / end-gap kernel (one problem per wave), 1: Dynprog_genome_gap

@@ -28,6 +28,21 @@
  *                               reference's setup calls (dynprog.c:1008, dynprog_single.c:101,
  *                               dynprog_end.c, dynprog_genome.c:192) and forward them
  *
+ * Owning the whole Dynprog_* interface (SURVEY §8b's unit of replacement): compiled with
+ * -DGMAPDP_SHIM_OWN, the shim defines the reference's 21 exported Dynprog_* symbols under their own
+ * names and GMAP links WITHOUT the six dynprog*.o objects (oracle/ref.mk gmap_gpu_*); only the
+ * stage-2 pair (Stage2_setup / Stage2_compute, Oligoindex_hr_tally / Oligoindex_get_mappings) is still
+ * routed with --wrap, since stage2.o / oligoindex_hr.o stay linked for their other entry points.  The
+ * 21 are the entry points above plus
+ *   Dynprog_new / Dynprog_free  (dynprog.c:631/777)   a limits-only handle: no score/direction arenas
+ *   Dynprog_term                (dynprog.c:1203)
+ *   Dynprog_score               (dynprog.c:126)
+ *   Dynprog_consistent_p        (dynprog.c:895)       over the shim's own consistent table (Dynprog_init)
+ *   Dynprog_end5/3_splicejunction, Dynprog_end5/3_known (dynprog_end.c:1653/2249/2748/3009)
+ *   Dynprog_make_splicejunction_5/3 (dynprog_end.c:2569/2670)
+ * Without GMAPDP_SHIM_OWN the entry points are the __wrap_ names (the link above keeps the reference's
+ * dynprog objects for Dynprog_new/_free/_term/_score/_consistent_p/_make_splicejunction_5/3).
+ *
  * Results are returned as the reference does: a List_T of Pair_T allocated in
  * the caller's Pairpool_T (same order, same fields), the same out-parameters.
  * GMAPDP_DEVICE selects the HIP device (default 0).
@@ -48,28 +63,34 @@
 #include "oligoindex_hr.h"
 #include "stage2.h"
 
-extern void __wrap_Dynprog_init (Mode_T mode);
-extern void __wrap_Dynprog_single_setup (int user_open_in, int user_extend_in, bool user_dynprog_p_in,
+#ifdef GMAPDP_SHIM_OWN
+#define GMAPDP_DYNPROG_ENTRY(name) name
+#else
+#define GMAPDP_DYNPROG_ENTRY(name) __wrap_##name
+#endif
+
+extern void GMAPDP_DYNPROG_ENTRY(Dynprog_init) (Mode_T mode);
+extern void GMAPDP_DYNPROG_ENTRY(Dynprog_single_setup) (int user_open_in, int user_extend_in, bool user_dynprog_p_in,
                                          bool homopolymerp_in);
-extern void __wrap_Dynprog_end_setup (Univcoord_T *splicesites_in, Splicetype_T *splicetypes_in,
+extern void GMAPDP_DYNPROG_ENTRY(Dynprog_end_setup) (Univcoord_T *splicesites_in, Splicetype_T *splicetypes_in,
                                       Chrpos_T *splicedists_in, int nsplicesites_in,
                                       Trieoffset_T *trieoffsets_obs_in, Triecontent_T *triecontents_obs_in,
                                       Trieoffset_T *trieoffsets_max_in, Triecontent_T *triecontents_max_in,
                                       int user_open_in, int user_extend_in, bool user_dynprog_p_in);
-extern void __wrap_Dynprog_genome_setup (bool novelsplicingp_in, IIT_T splicing_iit_in,
+extern void GMAPDP_DYNPROG_ENTRY(Dynprog_genome_setup) (bool novelsplicingp_in, IIT_T splicing_iit_in,
                                          int *splicing_divint_crosstable_in, int donor_typeint_in,
                                          int acceptor_typeint_in, int user_open_in, int user_extend_in,
                                          bool user_dynprog_p_in);
 
 extern List_T
-__wrap_Dynprog_single_gap (int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches, int *nopens,
+GMAPDP_DYNPROG_ENTRY(Dynprog_single_gap) (int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches, int *nopens,
                            int *nindels, Dynprog_T dynprog, char *sequence1, char *sequenceuc1, int length1,
                            int length2, int offset1, int offset2, Univcoord_T chroffset, Univcoord_T chrhigh,
                            bool watsonp, int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
                            Pairpool_T pairpool, int extraband_single, bool widebandp, double defect_rate);
 
 extern List_T
-__wrap_Dynprog_end5_gap (int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches, int *nopens,
+GMAPDP_DYNPROG_ENTRY(Dynprog_end5_gap) (int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches, int *nopens,
                          int *nindels, Dynprog_T dynprog, char *revsequence1, char *revsequenceuc1, int length1,
                          int length2, int revoffset1, int revoffset2, Univcoord_T chroffset, Univcoord_T chrhigh,
                          bool watsonp, int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
@@ -77,7 +98,7 @@ __wrap_Dynprog_end5_gap (int *dynprogindex, int *finalscore, int *nmatches, int 
                          bool require_pos_score_p);
 
 extern List_T
-__wrap_Dynprog_end3_gap (int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches, int *nopens,
+GMAPDP_DYNPROG_ENTRY(Dynprog_end3_gap) (int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches, int *nopens,
                          int *nindels, Dynprog_T dynprog, char *sequence1, char *sequenceuc1, int length1,
                          int length2, int offset1, int offset2, Univcoord_T chroffset, Univcoord_T chrhigh,
                          bool watsonp, int genestrand, bool jump_late_p, Genome_T genome, Genome_T genomealt,
@@ -85,7 +106,7 @@ __wrap_Dynprog_end3_gap (int *dynprogindex, int *finalscore, int *nmatches, int 
                          bool require_pos_score_p);
 
 extern List_T
-__wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_rightgenomepos, double *left_prob,
+GMAPDP_DYNPROG_ENTRY(Dynprog_genome_gap) (int *dynprogindex, int *new_leftgenomepos, int *new_rightgenomepos, double *left_prob,
                            double *right_prob, int *traceback_score, int *nmatches, int *nmismatches, int *nopens,
                            int *nindels, int *exonhead, int *introntype, Dynprog_T dynprogL, Dynprog_T dynprogR,
                            char *rsequence, char *rsequenceuc, int rlength, int glengthL, int glengthR, int roffset,
@@ -95,7 +116,7 @@ __wrap_Dynprog_genome_gap (int *dynprogindex, int *new_leftgenomepos, int *new_r
                            double defect_rate, int maxpeelback, bool halfp, bool finalp);
 
 extern List_T
-__wrap_Dynprog_cdna_gap (int *dynprogindex, int *traceback_score, bool *incompletep, Dynprog_T dynprogL,
+GMAPDP_DYNPROG_ENTRY(Dynprog_cdna_gap) (int *dynprogindex, int *traceback_score, bool *incompletep, Dynprog_T dynprogL,
                          Dynprog_T dynprogR, char *rsequenceL, char *rsequence_ucL, char *rev_rsequenceR,
                          char *rev_rsequence_ucR, int rlengthL, int rlengthR, int glength, int roffsetL,
                          int rev_roffsetR, int goffset, Univcoord_T chroffset, Univcoord_T chrhigh, bool watsonp,
@@ -103,7 +124,7 @@ __wrap_Dynprog_cdna_gap (int *dynprogindex, int *traceback_score, bool *incomple
                          Pairpool_T pairpool, int extraband_paired, double defect_rate);
 
 extern List_T
-__wrap_Dynprog_microexon_int (double *bestprob2, double *bestprob3, int *dynprogindex, int *microintrontype,
+GMAPDP_DYNPROG_ENTRY(Dynprog_microexon_int) (double *bestprob2, double *bestprob3, int *dynprogindex, int *microintrontype,
                               char *rsequence, char *rsequenceuc, int rlength, int roffset, int goffsetL,
                               int rev_goffsetR, int cdna_direction, char *queryseq, char *queryuc,
                               Univcoord_T chroffset, Univcoord_T chrhigh, bool watsonp, int genestrand,

@@ -136,6 +136,13 @@ int orc_microexon_int (const char *rsequence, const char *rsequenceuc, int rleng
 /* The genome set by orc_set_genome. */
 const char *orc_genome_seq (unsigned int *length);
 
+/* maxent_oracle.c: Maxent_hr_*_prob (model GMAPDP_MAXENT_*, maxent_hr.c:27357-27652) over the genome of
+   orc_set_genome, from the tables tools/make_maxent_tables.py wrote (orc_maxent_load: 0 on success). */
+int orc_maxent_load (const char *path);
+double orc_maxent (int model, unsigned long long splice_pos, unsigned long long chroffset);
+void orc_maxent_batch (const int *models, const unsigned long long *positions, unsigned long long chroffset, int n,
+                       double *out);
+
 /* Stage-2 seeding (stage2_oracle.c): Oligoindex_hr_tally + Oligoindex_get_mappings as
    Stage2_compute runs them for GMAP; same arguments and outputs as refh_oligo_mappings
    (oracle/refharness.c).  Returns the positions written, -1 when a capacity is too small, -3 for

@@ -176,22 +176,43 @@ $(OUT)/librefdp_gpushim_avx2.so: $(LIBOBJS_avx2a) $(OUT)/avx2a/refharness.o $(OU
 	  -L$(GMAPDP_LIB) -lgmapdp -Wl,-rpath,'$$ORIGIN/../../gmap-2024_amd/lib' -lz -lm
 
 # ---- the full gmap program (end-to-end oracle) and the same program on the MI355X engine ----
+# gmap_gpu_V owns the whole Dynprog_* interface (SURVEY §8b's unit of replacement): the six dynprog*.o
+# objects are NOT linked; the shim, compiled with -DGMAPDP_SHIM_OWN, defines all 21 Dynprog_* symbols GMAP
+# imports.  Only the stage-2 pair is still routed with --wrap (stage2.o / oligoindex_hr.o stay linked for
+# their other entry points).
+DYNPROG_C   := dynprog.c dynprog_simd.c dynprog_single.c dynprog_genome.c dynprog_cdna.c dynprog_end.c
+WRAPPED_OWN := Oligoindex_hr_tally Oligoindex_get_mappings Stage2_setup Stage2_compute
 PROG_VARIANTS := nosimd avx2 large
 define prog_rules
 $(OUT)/gmap_$(1): $$(PROGOBJS_$(1))
 	$$(CC) -pthread -s -o $$@ $$^ -lz -lm
 
-$(OUT)/gmap_gpu_$(1): $$(PROGOBJS_$(1)) $(OUT)/gpushim_$(1)/gmapdp_gmap_shim.o $(GMAPDP_LIB)/libgmapdp.so
-	$$(CC) -pthread -s $(foreach w,$(WRAPPED),-Wl,--wrap=$(w)) -o $$@ $$(filter %.o,$$^) \
+NODP_$(1) := $$(filter-out $$(patsubst %.c,$(OUT)/$(1)/%.o,$(DYNPROG_C)),$$(PROGOBJS_$(1)))
+
+$(OUT)/gmap_gpu_$(1): $$(NODP_$(1)) $(OUT)/gpushim_own_$(1)/gmapdp_gmap_shim.o $(GMAPDP_LIB)/libgmapdp.so
+	$$(CC) -pthread -s $(foreach w,$(WRAPPED_OWN),-Wl,--wrap=$(w)) -o $$@ $$(filter %.o,$$^) \
 	  -L$(GMAPDP_LIB) -lgmapdp -Wl,-rpath,'$$$$ORIGIN/../../gmap-2024_amd/lib' -lz -lm
 
-$(OUT)/gpushim_$(1)/gmapdp_gmap_shim.o: $(SHIM_SRC) ../include/gmapdp.h
+$(OUT)/gpushim_own_$(1)/gmapdp_gmap_shim.o: $(SHIM_SRC) ../include/gmapdp.h ../include/gmapdp_dynprog.h
 	@mkdir -p $$(dir $$@)
-	$$(CC) $(BASEFLAGS) -DHAVE_CONFIG_H $$(FLAGS_$(1)) -I../include -c $$< -o $$@
+	$$(CC) $(BASEFLAGS) -DHAVE_CONFIG_H -DGMAPDP_SHIM_OWN $$(FLAGS_$(1)) -I../include -c $$< -o $$@
 endef
 $(foreach v,$(PROG_VARIANTS),$(eval $(call prog_rules,$(v))))
 
-programs: $(foreach v,$(PROG_VARIANTS),$(OUT)/gmap_$(v)) $(OUT)/gmap_callmix \
+# own_check (tests/test_shim_own.py): the non-DP Dynprog_* entry points (consistent table, scores, handles)
+# from the reference's dynprog objects and from the owned shim, printed for comparison; no GPU call.
+$(OUT)/nosimd/own_check.o: own_check.c
+	@mkdir -p $(dir $@)
+	$(CC) $(BASEFLAGS) -DHAVE_CONFIG_H -c $< -o $@
+$(OUT)/own_check_ref: $(filter-out $(OUT)/nosimd/gmap.o,$(PROGOBJS_nosimd)) $(OUT)/nosimd/own_check.o
+	$(CC) -pthread -o $@ $^ -lz -lm
+$(OUT)/own_check_shim: $(filter-out $(OUT)/nosimd/gmap.o,$(NODP_nosimd)) $(OUT)/gpushim_own_nosimd/gmapdp_gmap_shim.o \
+                       $(OUT)/nosimd/own_check.o $(GMAPDP_LIB)/libgmapdp.so
+	$(CC) -pthread $(foreach w,$(WRAPPED_OWN),-Wl,--wrap=$(w)) -o $@ $(filter %.o,$^) \
+	  -L$(GMAPDP_LIB) -lgmapdp -Wl,-rpath,'$$ORIGIN/../../gmap-2024_amd/lib' -lz -lm
+own_check: $(OUT)/own_check_ref $(if $(wildcard $(GMAPDP_LIB)/libgmapdp.so),$(OUT)/own_check_shim)
+
+programs: $(foreach v,$(PROG_VARIANTS),$(OUT)/gmap_$(v)) $(OUT)/gmap_callmix own_check \
           $(if $(wildcard $(GMAPDP_LIB)/libgmapdp.so),$(foreach v,$(PROG_VARIANTS),$(OUT)/gmap_gpu_$(v)))
 
 # The unmodified nosimd gmap with the hot-path entry points counted (callmix.c: one log line per call,
@@ -205,4 +226,4 @@ $(OUT)/callmix/callmix.o: callmix.c ../include/gmapdp_dynprog.h
 $(OUT)/gmap_callmix: $(PROGOBJS_nosimd) $(OUT)/callmix/callmix.o
 	$(CC) -pthread -s $(foreach w,$(CALLMIX),-Wl,--wrap=$(w)) -o $@ $^ -lz -lm
 
-.PHONY: all programs
+.PHONY: all programs own_check

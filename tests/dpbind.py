@@ -398,6 +398,33 @@ def _orc_splice_sites(self, p):
 Oracle.genome_gap = _orc_genome_gap
 Oracle.splice_sites = _orc_splice_sites
 
+MAXENT_TABLES = os.path.join(ROOT, "gmap-2024_amd", "lib", "maxent_hr_tables.bin")
+
+
+def _orc_maxent(self, model, pos, chroffset=0):
+    """oracle/maxent_oracle.c: Maxent_hr_<model>_prob over the oracle's genome (tools/make_maxent_tables.py's
+    tables)."""
+    lib = self.lib
+    if not getattr(lib, "_me_ready", False):
+        lib.orc_maxent_load.argtypes = [C.c_char_p]
+        lib.orc_maxent.argtypes = [C.c_int, C.c_ulonglong, C.c_ulonglong]
+        lib.orc_maxent.restype = C.c_double
+        assert lib.orc_maxent_load(MAXENT_TABLES.encode()) == 0, "maxent tables not generated"
+        lib._me_ready = True
+    return lib.orc_maxent(model, pos, chroffset)
+
+
+def oracle_splice_probs(orc, p):
+    """splice_probs with the oracle's MaxEnt restatement instead of the reference's functions."""
+    if p["rlength"] <= 1 or p["rlength"] > 660 or p["glengthL"] > 2000 or p["glengthR"] > 2000:
+        return [0.0] * max(0, p["glengthL"]), [0.0] * max(0, p["glengthR"])
+    sl, sr = orc.splice_sites(p)
+    return ([orc.maxent(m, pos, p["chroffset"]) for pos, m in sl],
+            [orc.maxent(m, pos, p["chroffset"]) for pos, m in sr])
+
+
+Oracle.maxent = _orc_maxent
+
 _COMPL = {ord("A"): ord("T"), ord("C"): ord("G"), ord("G"): ord("C"), ord("T"): ord("A"), ord("N"): ord("N")}
 
 # canonical, GC-AG and AT-AC introns in the cDNA's sense / antisense orientation (intron.h)

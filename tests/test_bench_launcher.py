@@ -44,8 +44,12 @@ def test_bench_launcher_spawns_ranks():
 
 
 def test_bench_under_torchrun():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:  # a free port (a fixed one can be taken)
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
     out, ranks = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                       "--master-addr", "127.0.0.1", "--master-port", "29533", "bench.py", "--gpus", "2", "--dry-run",
+                       "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--dry-run",
                        "--reads", "200", "--batches", "2", "--genome", "chr22"])
     _check(out, ranks, 2, 2, 200)
 
