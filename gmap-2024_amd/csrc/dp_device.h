@@ -516,6 +516,9 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
         }
       }
     }
+#ifdef GMAPDP_GGX_NODIRS
+    if (!CARRY)  // timing experiment only (make variant): the genome-gap fills store no directions
+#endif
     if (lane == 0) {  // one lane stores the column's 4R direction words
       uint64_t* dcol = dirs + (size_t)c * 4 * R;
 #pragma unroll

@@ -683,8 +683,15 @@ __host__ __device__ inline ScratchGG scratch_gg(int rlength, int glengthL, int g
   return sv;
 }
 
+// GMAPDP_GGX_*: timing experiments only (make variant; outputs are garbage): NOSTAGE stages constants
+// instead of loading, NOEMIT ends after the fills, WPE sets amdgpu_waves_per_eu.
+#ifdef GMAPDP_GGX_WPE
+#define GGX_ATTR __attribute__((amdgpu_waves_per_eu(GMAPDP_GGX_WPE)))
+#else
+#define GGX_ATTR
+#endif
 template <int R, bool DIRS_LDS>
-__global__ __launch_bounds__(128) void gg_kernel(
+__global__ __launch_bounds__(128) GGX_ATTR void gg_kernel(
     const DevGenomeProblem* __restrict__ probs, const int* __restrict__ order,
     const uint32_t* __restrict__ blocks, uint64_t nwords,
     const char* __restrict__ qseq, const char* __restrict__ qseq_uc, const double* __restrict__ sprob,
@@ -739,6 +746,17 @@ __global__ __launch_bounds__(128) void gg_kernel(
 
   // ---- stage (both waves): per query row the 4-bit score word in both DP orders, both genome
   //      segments as classes, dinucleotide codes, the splice probabilities, the intron scores ----
+#ifdef GMAPDP_GGX_NOSTAGE
+  for (int i = tid; i < rlen + 2; i += 128) scL[i] = scR[i] = 0x123456;
+  for (int i = tid; i < gL + 2; i += 128) gclL[i] = i & 3;
+  for (int i = tid; i < gR + 2; i += 128) gclR[i] = i & 3;
+  for (int i = tid; i < gL; i += 128) pL[i] = 0.1;
+  for (int i = tid; i < gR; i += 128) pR[i] = 0.1;
+  if (tid < 64) isc[tid] = tid & 7;
+  if (tid == 0) *done = 0;
+  __syncthreads();
+  if (false)
+#endif
   for (int i = tid; i < rlen; i += 128) {
     const char c1 = qseq[P.qbase + i];
     const uint64_t row = *reinterpret_cast<const uint64_t*>(sct + (uint8_t)(c1 & 127) * kNClass);
@@ -748,6 +766,7 @@ __global__ __launch_bounds__(128) void gg_kernel(
     scL[i + 1] = (int32_t)w;
     scR[rlen - i] = (int32_t)w;
   }
+#ifndef GMAPDP_GGX_NOSTAGE
   if (tid < 2) {
     scL[tid ? rlen + 1 : 0] = 0;
     scR[tid ? rlen + 1 : 0] = 0;
@@ -768,6 +787,7 @@ __global__ __launch_bounds__(128) void gg_kernel(
   if (tid < 64) isc[tid] = isctab[(size_t)P.iclass * 128 + ((flags & kGFinal) ? 64 : 0) + tid];
   if (tid == 0) *done = 0;
   __syncthreads();
+#endif
   // leftdi[cL] from gsequenceL[cL], [cL+1]; rightdi[cR] from rev_gsequenceR[-cR-1], [-cR] (:2518-2566)
   for (int c = tid; c <= gL; c += 128) ldi[c] = (c < gL - 1) ? left_dinucl(gchL[c + 1], gchL[c + 2]) : 0;
   for (int c = tid; c <= gR; c += 128) rdi[c] = (c < gR - 1) ? right_dinucl(gchR[c + 2], gchR[c + 1]) : 0;
@@ -821,6 +841,10 @@ __global__ __launch_bounds__(128) void gg_kernel(
   __syncthreads();
   GG_MARK(3);
   if (wave != 0) return;
+#ifdef GMAPDP_GGX_NOEMIT
+  if (lane == 0) results[pid] = res;
+  return;
+#endif
 
   // ---- 3. bridge: per-lane scan of rows rL = lane+1, lane+65, ... (A, B, C per row) ----
   int ws = kNegInf32, wrL = -1, wcL = 0, wcR = 0;  // (NEG_INFINITY_32, 0.0) is the reference's initial state

@@ -531,7 +531,7 @@ int gmapdp_reserve(gmapdp_ctx* ctx, size_t bytes, int what) {
       dev(*b, bytes);
     dev(ctx->s2scratch, 4 * bytes);
   }
-  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);  // this context only: other dispatchers keep running
   return e == hipSuccess ? GMAPDP_OK : fail(ctx, GMAPDP_ENOMEM, "reserve: %s", e);
 }
 
@@ -3205,6 +3205,38 @@ int gmapdp_stage2_plan_create(gmapdp_ctx* ctx, const gmapdp_stage2_problem* prob
   if (rc) {
     stage2_plan_free(P);
     return rc;
+  }
+  // The seeding's arenas were sized from upper bounds (a window's worth of positions and 24 diagonals per
+  // query position: 19 GB for 10 000 5-kb reads).  Re-lay them out from this run's measured use -- the
+  // table holds at most totalpositions entries (one per distinct 8-mer hit, each counted at least once
+  // over the query positions), the diagonal arena exactly ndiagonals records -- so that the plan keeps
+  // only what its runs write; every run of the plan seeds the same way and writes the same amounts.
+  {
+    std::vector<int64_t> toffs(n), doffs(n);
+    size_t t = 0, dd = 0;
+    for (int i = 0; i < n; i++) {
+      toffs[i] = (int64_t)t;
+      doffs[i] = (int64_t)dd;
+      t += std::min<size_t>(oligo_table_cap(op[i]), (size_t)std::max(ores[i].totalpositions, 0));
+      dd += (size_t)std::max(ores[i].ndiagonals, 0);
+    }
+    for (DevOligoProblem& d : P->oplan->ord) {
+      d.table_offset = toffs[d.index];
+      d.diag_offset = doffs[d.index];
+    }
+    (void)hipFree(P->d_table);
+    (void)hipFree(P->d_diag);
+    P->d_table = nullptr;
+    P->d_diag = nullptr;
+    P->oplan->table_cap = t;
+    P->oplan->diag_cap = dd;
+    e = hipMemcpy(P->oplan->d_probs, P->oplan->ord.data(), sizeof(DevOligoProblem) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&P->d_table, sizeof(uint32_t) * std::max<size_t>(t, 1));
+    if (e == hipSuccess) e = hipMalloc(&P->d_diag, 4 * sizeof(int32_t) * std::max<size_t>(dd, 1));
+    if (e != hipSuccess) {
+      stage2_plan_free(P);
+      return fail(ctx, GMAPDP_ENOMEM, "stage-2 plan arenas: %s", e);
+    }
   }
   for (int i = 0; i < n; i++) {
     dp[i].scratch_offset = (int64_t)P->scratch;

@@ -605,6 +605,7 @@ typedef struct shim_req {
   double *mxp;                  /* the caller's MaxEnt probabilities of its candidates (2 per candidate) */
   size_t mxccap, mxpcap;
   int done;
+  struct shim_fiber *fiber;     /* the calling fiber (GMAPDP_SHIM_FIBERS), else NULL: the caller sleeps on cv */
   int longp;                    /* a long fill: queue 2 */
   long cost;                    /* shim_cost of the fill (diagnostics) */
   pthread_mutex_t mtx;          /* guards done (the calling thread sleeps on cv) */
@@ -632,6 +633,199 @@ shim_cost (int rlength, int glength, int extraband) {
 static int dispatcher_started = 0;
 static __thread shim_req *tl_req = NULL;
 
+/* ---- fibers: GMAP's worker threads as user-level contexts (the owned link, GMAPDP_SHIM_OWN) ----
+   GMAP runs one OS thread per worker (gmap.c:6639, worker_thread :4867), and each worker's read makes
+   ~270 serially dependent engine calls; with hundreds of workers per GPU every call was a futex sleep and
+   a scheduler wake-up of one of 512-2 048 threads.  Linked with --wrap=pthread_create,pthread_join,
+   pthread_getspecific,pthread_setspecific, the workers become fibers: GMAPDP_SHIM_FIBER_HOSTS (default 16)
+   OS threads each run their share round-robin, and a fiber's engine call queues its request and switches
+   to the next runnable fiber of its host (swapcontext) instead of sleeping; a dispatcher that finishes a
+   batch makes the callers' fibers runnable again, one wake-up per idle host.  GMAP keeps its per-thread
+   state in pthread keys only (except.c:34-132 exception stacks, gmap.c:4920 the request), which become
+   per-fiber; the output thread (Outbuffer_thread_*) stays an OS thread.  GMAPDP_SHIM_FIBERS=0 turns it
+   off (one OS thread per worker, as before). */
+#ifdef GMAPDP_SHIM_OWN
+#include <ucontext.h>
+#include <sys/mman.h>
+#include "outbuffer.h"
+
+extern int __real_pthread_create (pthread_t *th, const pthread_attr_t *attr, void *(*fn)(void *), void *arg);
+extern int __real_pthread_join (pthread_t th, void **ret);
+extern void *__real_pthread_getspecific (pthread_key_t key);
+extern int __real_pthread_setspecific (pthread_key_t key, const void *value);
+
+#define SHIM_NKEYS 64
+#define SHIM_MAXHOSTS 256
+#define SHIM_FIBER_STACK (8UL << 20)  /* glibc's default thread stack (reserved, touched pages only) */
+
+typedef struct shim_fiber {
+  ucontext_t ctx;
+  struct shim_host *host;
+  void *(*fn) (void *);
+  void *arg, *ret;
+  int finished;                /* 1: returned, 2: its host has left its stack (joinable) */
+  shim_req *req;               /* the fiber's request (tl_req of an OS thread) */
+  void *keys[SHIM_NKEYS];      /* pthread_getspecific / _setspecific values */
+  void *stack;
+  pthread_mutex_t jm;
+  pthread_cond_t jc;
+  struct shim_fiber *next, *all_next;
+} shim_fiber;
+
+typedef struct shim_host {
+  ucontext_t ctx;              /* the scheduler loop's context */
+  pthread_mutex_t mu;
+  pthread_cond_t cv;
+  shim_fiber *head, *tail;     /* runnable fibers */
+} shim_host;
+
+static shim_host shim_hosts[SHIM_MAXHOSTS];
+static int shim_nhosts = 0, shim_nfibers = 0, shim_fiber_mode = -1, shim_fiber_hosts = 16;
+static pthread_mutex_t shim_fiber_lock = PTHREAD_MUTEX_INITIALIZER;
+static shim_fiber *shim_all_fibers = NULL;
+static __thread shim_fiber *cur_fiber = NULL;
+
+static int
+shim_fibers_on (void) {
+  if (shim_fiber_mode < 0) {
+    const char *st = getenv("GMAPDP_SHIM_FIBERS");
+    shim_fiber_mode = !(st != NULL && st[0] == '0');
+    st = getenv("GMAPDP_SHIM_FIBER_HOSTS");
+    if (st != NULL && atoi(st) > 0) shim_fiber_hosts = atoi(st) < SHIM_MAXHOSTS ? atoi(st) : SHIM_MAXHOSTS;
+  }
+  return shim_fiber_mode;
+}
+
+static void
+shim_host_ready (shim_host *h, shim_fiber *f) {
+  pthread_mutex_lock(&h->mu);
+  f->next = NULL;
+  if (h->tail != NULL) h->tail->next = f;
+  else h->head = f;
+  h->tail = f;
+  pthread_cond_signal(&h->cv);
+  pthread_mutex_unlock(&h->mu);
+}
+
+static void *
+shim_host_main (void *arg) {
+  shim_host *h = (shim_host *) arg;
+  shim_fiber *f;
+  pthread_setname_np(pthread_self(), "gmapdp-fibers");
+  for (;;) {
+    pthread_mutex_lock(&h->mu);
+    while (h->head == NULL) pthread_cond_wait(&h->cv, &h->mu);
+    f = h->head;
+    h->head = f->next;
+    if (h->head == NULL) h->tail = NULL;
+    pthread_mutex_unlock(&h->mu);
+    cur_fiber = f;
+    swapcontext(&h->ctx, &f->ctx);  /* runs f until it waits for the engine or returns */
+    cur_fiber = NULL;
+    if (f->finished) {
+      munmap(f->stack, SHIM_FIBER_STACK);
+      pthread_mutex_lock(&f->jm);
+      f->finished = 2;
+      pthread_cond_broadcast(&f->jc);
+      pthread_mutex_unlock(&f->jm);
+    }
+  }
+  return NULL;
+}
+
+static void
+shim_fiber_main (unsigned int lo, unsigned int hi) {
+  shim_fiber *f = (shim_fiber *) (((uintptr_t) hi << 32) | (uintptr_t) lo);
+  f->ret = f->fn(f->arg);
+  f->finished = 1;  /* returning resumes the host (uc_link) */
+}
+
+int
+__wrap_pthread_create (pthread_t *th, const pthread_attr_t *attr, void *(*fn) (void *), void *arg) {
+  shim_fiber *f;
+  pthread_attr_t da;
+  int k;
+  if (!shim_fibers_on() || fn == Outbuffer_thread_ordered || fn == Outbuffer_thread_anyorder)
+    return __real_pthread_create(th, attr, fn, arg);
+  f = (shim_fiber *) calloc(1, sizeof(shim_fiber));
+  if (f == NULL) shim_refuse("host memory for a worker fiber (out of memory)");
+  f->stack = mmap(NULL, SHIM_FIBER_STACK, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE | MAP_STACK,
+                  -1, 0);
+  if (f->stack == MAP_FAILED) shim_refuse("a worker fiber's stack (mmap)");
+  f->fn = fn;
+  f->arg = arg;
+  pthread_mutex_init(&f->jm, NULL);
+  pthread_cond_init(&f->jc, NULL);
+  pthread_mutex_lock(&shim_fiber_lock);
+  k = shim_nfibers++ % shim_fiber_hosts;
+  if (k >= shim_nhosts) {  /* hosts start with their first fiber */
+    pthread_t tid;
+    pthread_mutex_init(&shim_hosts[k].mu, NULL);
+    pthread_cond_init(&shim_hosts[k].cv, NULL);
+    pthread_attr_init(&da);
+    pthread_attr_setdetachstate(&da, PTHREAD_CREATE_DETACHED);
+    if (__real_pthread_create(&tid, &da, shim_host_main, &shim_hosts[k]) != 0)
+      shim_refuse("a fiber host thread (pthread_create)");
+    pthread_attr_destroy(&da);
+    shim_nhosts = k + 1;
+  }
+  f->host = &shim_hosts[k];
+  f->all_next = shim_all_fibers;
+  shim_all_fibers = f;
+  pthread_mutex_unlock(&shim_fiber_lock);
+  getcontext(&f->ctx);
+  f->ctx.uc_stack.ss_sp = f->stack;
+  f->ctx.uc_stack.ss_size = SHIM_FIBER_STACK;
+  f->ctx.uc_link = &f->host->ctx;
+  makecontext(&f->ctx, (void (*)(void)) shim_fiber_main, 2, (unsigned int) (uintptr_t) f,
+              (unsigned int) ((uintptr_t) f >> 32));
+  *th = (pthread_t) f;
+  shim_host_ready(f->host, f);
+  return 0;
+}
+
+int
+__wrap_pthread_join (pthread_t th, void **ret) {
+  shim_fiber *f;
+  pthread_mutex_lock(&shim_fiber_lock);
+  for (f = shim_all_fibers; f != NULL && (pthread_t) f != th; f = f->all_next) ;
+  pthread_mutex_unlock(&shim_fiber_lock);
+  if (f == NULL) return __real_pthread_join(th, ret);
+  pthread_mutex_lock(&f->jm);
+  while (f->finished != 2) pthread_cond_wait(&f->jc, &f->jm);
+  pthread_mutex_unlock(&f->jm);
+  if (ret != NULL) *ret = f->ret;
+  return 0;
+}
+
+void *
+__wrap_pthread_getspecific (pthread_key_t key) {
+  if (cur_fiber != NULL && key < SHIM_NKEYS) return cur_fiber->keys[key];
+  return __real_pthread_getspecific(key);
+}
+
+int
+__wrap_pthread_setspecific (pthread_key_t key, const void *value) {
+  if (cur_fiber != NULL && key < SHIM_NKEYS) {
+    cur_fiber->keys[key] = (void *) value;
+    return 0;
+  }
+  return __real_pthread_setspecific(key, value);
+}
+
+static shim_req **
+shim_req_slot (void) {
+  return cur_fiber != NULL ? &cur_fiber->req : &tl_req;
+}
+#define SHIM_OS_THREAD_CREATE __real_pthread_create
+#else
+static shim_req **
+shim_req_slot (void) {
+  return &tl_req;
+}
+#define SHIM_OS_THREAD_CREATE pthread_create
+#endif
+
 static void *
 shim_grow (void *p, size_t *cap, size_t want, size_t elt) {
   if (want <= *cap && p != NULL) return p;
@@ -645,13 +839,14 @@ shim_grow (void *p, size_t *cap, size_t want, size_t elt) {
 /* the calling thread's request (one outstanding call per thread) */
 static shim_req *
 shim_request (int kind) {
-  shim_req *r = tl_req;
+  shim_req **slot = shim_req_slot();
+  shim_req *r = *slot;
   if (r == NULL) {
     r = (shim_req *) calloc(1, sizeof(shim_req));
     if (r == NULL) shim_refuse("host memory for a request (out of memory)");
     pthread_cond_init(&r->cv, NULL);
     pthread_mutex_init(&r->mtx, NULL);
-    tl_req = r;
+    *slot = r;
   }
   r->kind = kind;
   r->longp = 0;
@@ -698,6 +893,13 @@ shim_dispatch (void *arg) {
       /* wake each caller under its own request's lock: no herd on the queue lock */
       for (r = same; r != NULL; r = next) {
         next = r->next;
+#ifdef GMAPDP_SHIM_OWN
+        if (r->fiber != NULL) {  /* the caller's fiber runs again (r is its own from here on) */
+          r->done = 1;
+          shim_host_ready(r->fiber->host, r->fiber);
+          continue;
+        }
+#endif
         pthread_mutex_lock(&r->mtx);
         r->done = 1;
         pthread_cond_signal(&r->cv);
@@ -742,7 +944,7 @@ shim_submit (shim_req *r) {
     pthread_attr_init(&attr);
     pthread_attr_setdetachstate(&attr, PTHREAD_CREATE_DETACHED);
     for (k = 0; k < nd + nl + nd2; k++)
-      if (pthread_create(&th, &attr, shim_dispatch, (void *) (intptr_t) (k < nd ? 0 : (k < nd + nl ? 2 : 1))) != 0)
+      if (SHIM_OS_THREAD_CREATE(&th, &attr, shim_dispatch, (void *) (intptr_t) (k < nd ? 0 : (k < nd + nl ? 2 : 1))) != 0)
         shim_refuse("a dispatcher thread (pthread_create)");
     pthread_attr_destroy(&attr);
     dispatcher_started = 1;
@@ -750,11 +952,23 @@ shim_submit (shim_req *r) {
   qi = r->kind == K_STAGE2 ? 1 : (r->kind == K_OLIGO ? shim_oligo_queue : (r->longp ? 2 : 0));
   r->done = 0;
   r->next = NULL;
+#ifdef GMAPDP_SHIM_OWN
+  r->fiber = cur_fiber;
+#else
+  r->fiber = NULL;
+#endif
   if (q_tail[qi] != NULL) q_tail[qi]->next = r;
   else q_head[qi] = r;
   q_tail[qi] = r;
   pthread_cond_signal(&q_cond[qi]);
   pthread_mutex_unlock(&q_lock);
+#ifdef GMAPDP_SHIM_OWN
+  if (r->fiber != NULL) {  /* run the host's next fiber; the dispatcher makes this one runnable again */
+    shim_fiber *f = r->fiber;
+    swapcontext(&f->ctx, &f->host->ctx);
+    return;
+  }
+#endif
   pthread_mutex_lock(&r->mtx);
   while (!r->done) pthread_cond_wait(&r->cv, &r->mtx);
   pthread_mutex_unlock(&r->mtx);

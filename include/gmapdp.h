@@ -476,9 +476,10 @@ size_t gmapdp_microexon_pair_capacity (const gmapdp_microexon_problem *problems,
  * over one query arena -- one host-to-device copy, the kernels on the context's stream, one
  * device-to-host copy, one wait.  Each section means what the separate entry point's arguments
  * mean; a section with n = 0 is skipped.  The rare search that overflows the candidate pool is
- * rerun as gmapdp_microexon_search would (extra round trips).  GMAPDP_ESPACE: candidate_capacity or
- * finish_pair_capacity too small (*candidates_needed holds the size required); everything else is
- * then still filled in.  splice_probs = NULL / finish_probs = NULL: device MaxEnt (see "Device MaxEnt"). */
+ * rerun as gmapdp_microexon_search would (extra round trips).  GMAPDP_ESPACE: candidate_capacity too
+ * small (*candidates_needed holds the size required); everything else is then still filled in.  Pair
+ * arenas (pair_capacity, finish_pair_capacity, whole_pair_capacity) are checked up front against
+ * gmapdp_*_pair_capacity of their calls: too small is GMAPDP_EINVAL, nothing run.  splice_probs = NULL / finish_probs = NULL: device MaxEnt (see "Device MaxEnt"). */
 typedef struct {
   const gmapdp_single_problem *singles; int nsingle;
   const gmapdp_end_problem *ends; int nend;

@@ -181,7 +181,8 @@ $(OUT)/librefdp_gpushim_avx2.so: $(LIBOBJS_avx2a) $(OUT)/avx2a/refharness.o $(OU
 # imports.  Only the stage-2 pair is still routed with --wrap (stage2.o / oligoindex_hr.o stay linked for
 # their other entry points).
 DYNPROG_C   := dynprog.c dynprog_simd.c dynprog_single.c dynprog_genome.c dynprog_cdna.c dynprog_end.c
-WRAPPED_OWN := Oligoindex_hr_tally Oligoindex_get_mappings Stage2_setup Stage2_compute
+WRAPPED_OWN := Oligoindex_hr_tally Oligoindex_get_mappings Stage2_setup Stage2_compute \
+               pthread_create pthread_join pthread_getspecific pthread_setspecific
 PROG_VARIANTS := nosimd avx2 large
 define prog_rules
 $(OUT)/gmap_$(1): $$(PROGOBJS_$(1))
@@ -210,7 +211,15 @@ $(OUT)/own_check_shim: $(filter-out $(OUT)/nosimd/gmap.o,$(NODP_nosimd)) $(OUT)/
                        $(OUT)/nosimd/own_check.o $(GMAPDP_LIB)/libgmapdp.so
 	$(CC) -pthread $(foreach w,$(WRAPPED_OWN),-Wl,--wrap=$(w)) -o $@ $(filter %.o,$^) \
 	  -L$(GMAPDP_LIB) -lgmapdp -Wl,-rpath,'$$ORIGIN/../../gmap-2024_amd/lib' -lz -lm
-own_check: $(OUT)/own_check_ref $(if $(wildcard $(GMAPDP_LIB)/libgmapdp.so),$(OUT)/own_check_shim)
+# fiber_check: the drop-in's worker fibers (pthread_* wrapped as in gmap_gpu_*) without a GPU
+$(OUT)/nosimd/fiber_check.o: fiber_check.c
+	@mkdir -p $(dir $@)
+	$(CC) $(BASEFLAGS) -c $< -o $@
+$(OUT)/fiber_check: $(filter-out $(OUT)/nosimd/gmap.o,$(NODP_nosimd)) $(OUT)/gpushim_own_nosimd/gmapdp_gmap_shim.o \
+                    $(OUT)/nosimd/fiber_check.o $(GMAPDP_LIB)/libgmapdp.so
+	$(CC) -pthread $(foreach w,$(WRAPPED_OWN),-Wl,--wrap=$(w)) -o $@ $(filter %.o,$^) \
+	  -L$(GMAPDP_LIB) -lgmapdp -Wl,-rpath,'$$ORIGIN/../../gmap-2024_amd/lib' -lz -lm
+own_check: $(OUT)/own_check_ref $(if $(wildcard $(GMAPDP_LIB)/libgmapdp.so),$(OUT)/own_check_shim $(OUT)/fiber_check)
 
 programs: $(foreach v,$(PROG_VARIANTS),$(OUT)/gmap_$(v)) $(OUT)/gmap_callmix own_check \
           $(if $(wildcard $(GMAPDP_LIB)/libgmapdp.so),$(foreach v,$(PROG_VARIANTS),$(OUT)/gmap_gpu_$(v)))

@@ -5,6 +5,9 @@ universal coordinates -- run on the engine with the whole genome resident in HBM
 every family (Dynprog_single_gap, _end5/3_gap, _genome_gap, _microexon_int, Stage2_compute) is compared
 bit-exactly with the oracle run on the problem's chromosome alone (chroffset 0; outputs are
 chromosome-relative, so only the addresses the kernels compute differ, as in test_gpu_large_coords.py).
+The splice-site probabilities are GMAP's MaxEnt models as the bench computes them: on the device at the
+universal coordinates (gmapdp.DEVICE), against the oracle's restatement on the chromosome alone -- so the
+device MaxEnt is pinned past 2^31 (GRCh38) and past 2^32 (wheat) too.
 
 configs[2]: block 0 of the default bench stream (GRCh38 layout, 3.09 Gnt, 10 000 reads, 8 blocks planted).
 configs[4]: a 2 000-read block of the Iso-Seq stream on the 17-Gnt wheat layout (coordinates past 2^32),
@@ -16,15 +19,10 @@ import pytest
 
 import gmapdp
 from gmapdp import workload as W
-from dpbind import Oracle, call_end, call_single
+from dpbind import Oracle, call_end, call_single, microexon_probs, oracle_splice_probs
 
 pytestmark = pytest.mark.gpu
 TAIL = 8192
-
-
-def _maxent(model, relpos):
-    """a deterministic stand-in for the host's Maxent_hr_*_prob, a function of the chromosome position"""
-    return ((relpos * 2654435761 + 97 * model) % 1000) / 1000.0
 
 
 def _sample(n, frac, rng, allowed=None):
@@ -36,7 +34,7 @@ def _sample(n, frac, rng, allowed=None):
 def _run(layout, shape, reads, nblocks, chroms=None, frac=0.01):
     genome = W.PackedGenome(layout.total, seed=38)
     W.plant_stream(genome, layout, reads, range(nblocks), shape)
-    d = W.make_blocks(genome, layout, reads, [0], shape=shape, sprob=True)[0]
+    d = W.make_blocks(genome, layout, reads, [0], shape=shape, sprob=False)[0]
     eng = gmapdp.Engine(0)
     eng.set_genome(blocks=genome.blocks, length=genome.length)
     rng = np.random.default_rng(77)
@@ -91,14 +89,10 @@ def _run(layout, shape, reads, nblocks, chroms=None, frac=0.01):
     calls = {"single": [single_call(sp[i]) for i in pick["single"]], "end": [end_call(ep[i]) for i in pick["end"]],
              "genome": [genome_call(gp[i]) for i in pick["genome"]], "microexon": [mx_call(mp[i]) for i in pick["microexon"]],
              "oligo": [s2_call(op[i]) for i in pick["oligo"]]}
-    sprobs = [(d["sprob"][int(gp[i]["prob_offset"]):int(gp[i]["prob_offset"]) + int(gp[i]["glengthL"])],
-               d["sprob"][int(gp[i]["prob_offset"]) + int(gp[i]["glengthL"]):
-                          int(gp[i]["prob_offset"]) + int(gp[i]["glengthL"]) + int(gp[i]["glengthR"])])
-              for i in pick["genome"]]
-    # the engine, at universal coordinates
+    # the engine, at universal coordinates (MaxEnt on the device)
     got = {"single": eng.single_gap_batch(calls["single"]), "end": eng.end_gap_batch(calls["end"]),
-           "genome": eng.genome_gap_batch(calls["genome"], [(list(a), list(b)) for a, b in sprobs]),
-           "microexon": eng.microexon_batch(calls["microexon"], lambda m, pos, cho: _maxent(m, pos - cho)),
+           "genome": eng.genome_gap_batch(calls["genome"], gmapdp.DEVICE),
+           "microexon": eng.microexon_batch(calls["microexon"], gmapdp.DEVICE),
            "oligo": eng.stage2_batch(calls["oligo"])}
     eng.close()
     # the oracle, chromosome by chromosome
@@ -117,10 +111,10 @@ def _run(layout, shape, reads, nblocks, chroms=None, frac=0.01):
             elif fam == "end":
                 exp = call_end(orc, c)
             elif fam == "genome":
-                exp = orc.genome_gap(c, list(sprobs[k][0]), list(sprobs[k][1]))
+                exp = orc.genome_gap(c, *oracle_splice_probs(orc, c))
             elif fam == "microexon":
                 cands = orc.microexon_candidates(c) or []
-                exp = orc.microexon_int(c, [x for cd in cands for x in (_maxent(cd[5], cd[4]), _maxent(cd[7], cd[6]))])
+                exp = orc.microexon_int(c, microexon_probs(orc, cands, 0))
             else:
                 exp = orc.stage2_compute(c)
             if got[fam][k] != exp:

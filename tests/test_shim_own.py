@@ -37,3 +37,16 @@ def test_owned_non_dp_entry_points_match_reference():
     rb = subprocess.run([b], capture_output=True, text=True, timeout=60, check=True).stdout
     assert ra.count("consistent mode") == 10 and ra.count("score ") == 54 and ra.count("new ") == 5
     assert ra == rb
+
+
+@pytest.mark.parametrize("fibers", ["1", "0"])
+def test_worker_fibers_without_gpu(fibers):
+    """The drop-in's worker fibers (pthread_create / _join / _getspecific / _setspecific wrapped as in
+    gmap_gpu_*): 300 workers on 5 host threads keep their own pthread-key values, run deep on their own
+    stacks and hand their return values to pthread_join; with GMAPDP_SHIM_FIBERS=0 they are OS threads."""
+    exe = os.path.join(REF, "fiber_check")
+    if not os.path.exists(exe):
+        pytest.skip("fiber_check not built (make -C oracle ref)")
+    env = dict(os.environ, GMAPDP_SHIM_FIBERS=fibers, GMAPDP_SHIM_FIBER_HOSTS="5")
+    r = subprocess.run([exe, "300"], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0 and r.stdout.strip() == "fibers ok 300", (r.stdout, r.stderr[-2000:])

@@ -9,7 +9,9 @@
 #   iso:<kernel>   tools/profile.sh <tag>_iso iso <kernel>  (the dominant kernel's launches alone)
 #   prof           tools/profile.sh <tag>  (kernel stats + PMC passes of the bench step)
 #   smoke          __graft_entry__.smoke()
-#   e2e:<b>:<n>    tools/e2e_timing.py --build <b> --reads <n> (gmap -t 16 vs the drop-in at -t 512)
+#   e2e:<b>:<n>[:<gpu threads>[:<configs>]]  tools/e2e_timing.py --build <b> --reads <n> (gmap -t 16 vs the
+#                  drop-in at -t 512 or the given list; configs as e2e_timing.py --configs)
+#   isot:<lib>     bench.py --iso-kernel $ISO_KERNEL (default gg_kernel<1, false>) with <lib>: HIP-event time per launch
 #   s2timing       tools/oi_timing.py s2 (the GMAPDP_OI_TIMING build: stage-2 sweep phases and counts)
 set -o pipefail
 TAG=$1
@@ -27,7 +29,8 @@ for S in "$@"; do
     benchfull) timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err || exit 16 ;;
     iso:*) bash tools/profile.sh ${TAG}_iso iso "${S#iso:}" > $O/prof_iso.txt 2>&1 || exit 17 ;;
     prof) bash tools/profile.sh $TAG > $O/prof.txt 2>&1 || exit 18 ;;
-    e2e:*) IFS=: read -r _ B N <<< "$S"; timeout -k 10 900 python tools/e2e_timing.py --build $B --reads $N --threads 16 --gpu-threads 512 > $O/e2e_${B}_$N.json 2> $O/e2e_${B}_$N.err || exit 20 ;;
+    e2e:*) IFS=: read -r _ B N T C <<< "$S"; timeout -k 10 900 python tools/e2e_timing.py --build $B --reads $N --threads 16 --gpu-threads ${T:-512} ${C:+--configs "$C"} > $O/e2e_${B}_$N.json 2> $O/e2e_${B}_$N.err || exit 20 ;;
+    isot:*) L=${S#isot:}; GMAPDP_LIB=$PWD/gmap-2024_amd/$L/libgmapdp.so timeout -k 10 300 python bench.py --iso-kernel "${ISO_KERNEL:-gmapdp::gg_kernel<1, false>}" --iso-reps ${ISO_REPS:-3} > $O/isot_$L.json 2> $O/isot_$L.err || exit 22 ;;
     s2timing) timeout -k 10 300 python tools/oi_timing.py s2 > $O/s2timing.json 2> $O/s2timing.err || exit 21 ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || exit 19 ;;
     *) echo "unknown step $S"; exit 2 ;;
