@@ -250,15 +250,15 @@ def like_for_like(out, pcie_ms, up, down):
                     "program on the same reads and cores (tools/e2e_timing.py)"}
 
 
-def cpu_baselines():
+def cpu_baselines(mix):
     """tools/cpu_baseline.py as a child process (the reference's own objects, all usable host cores,
-    AVX2 and nosimd builds); {build: result or None}."""
+    AVX2 and nosimd builds, the bench's call mix); {build: result or None}."""
     out = {}
     for build in ("avx2", "nosimd"):
         progress("CPU baseline (%s build)" % build)
         try:
             r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "cpu_baseline.py"), "--build", build,
-                                "--budget", "10"], capture_output=True, timeout=240, text=True)
+                                "--budget", "10", "--mix", mix], capture_output=True, timeout=240, text=True)
             out[build] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else None
         except (subprocess.TimeoutExpired, ValueError, IndexError):
             out[build] = None
@@ -306,10 +306,11 @@ def launch_ranks(n):
 def config_of(args):
     from gmapdp import workload as W
     if args.config == 4:
-        return W.Layout(W.WHEAT17), W.ISOSEQ5K, "wheat17"
+        return W.Layout(W.WHEAT17), (W.ISOSEQ5K if args.mix == "d" else W.ISOSEQ5K_G), "wheat17"
+    shape = W.SHAPES[args.mix]
     if args.genome == "chr22":
-        return W.Layout(W.CHR22), W.CDNA2K, "chr22"
-    return W.Layout(W.GRCH38), W.CDNA2K, "grch38"
+        return W.Layout(W.CHR22), shape, "chr22"
+    return W.Layout(W.GRCH38), shape, "grch38"
 
 
 def make_stream(args, rank, world):
@@ -363,6 +364,9 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=[2, 4], help="BASELINE.json configs index")
     ap.add_argument("--genome", default="grch38", choices=["grch38", "chr22"], help="configs[2] genome layout")
     ap.add_argument("--simd", action="store_true", help="the SIMD builds' semantics (gmap.avx2: sx/uxe/uxg kernels)")
+    ap.add_argument("--mix", default="d", choices=["d", "appb"],
+                    help="per-read call mix: d = measured with the reference's gmap -d (stage 1 included; 1.585 "
+                         "Stage2_compute calls per read over ~214-kb windows), appb = SURVEY App. B (rounds 1-3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dry-run", action="store_true", help="CPU only: launcher, gloo process group, sharding")
     ap.add_argument("--iso-kernel", default=None,
@@ -772,13 +776,15 @@ def main():
         "data": "synthetic",
         "config": {"workload": "configs[%d]: synthetic %d-nt %s reads (%d exons x %d nt, %g %% subs, %g %% indels) vs a "
                                "%s-layout i.i.d. genome (%d chromosomes, %d nt, universal coordinates to %d): per read "
-                               "1 Stage2_compute call (seeding + chaining) + %.1f Dynprog_single_gap + %.1f "
+                               "%.3g Stage2_compute calls (seeding + chaining, locus +- %d-nt windows) + %.1f "
+                               "Dynprog_single_gap + %.1f "
                                "Dynprog_end5_gap + %.1f Dynprog_end3_gap + %.1f Dynprog_genome_gap + %.1f "
                                "Dynprog_microexon_int (%s semantics); %d distinct blocks of %d reads cycled per rank; "
                                "inputs HBM-resident; host stages 1/3 not in the step"
                                % (args.config, shape.readlength, "Iso-Seq-style" if args.config == 4 else "cDNA",
                                   shape.exons, shape.exlen, 100 * shape.subs, 100 * shape.indel, gname,
-                                  len(layout.lens), layout.total, layout.total - 1, shape.single, shape.end5,
+                                  len(layout.lens), layout.total, layout.total - 1, shape.stage2, shape.pad,
+                                  shape.single, shape.end5,
                                   shape.end3, shape.genome, shape.microexon, "gmap.avx2" if args.simd else "nosimd",
                                   len(B), args.reads),
                    "genome": gname, "reads_per_step_per_gpu": args.reads, "blocks_per_rank": len(B),
@@ -846,7 +852,7 @@ def main():
         lib.gmapdp_microexon_plan_destroy(b["mplan"])
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == 2 and not args.simd:
         progress("CPU baselines")
-        cb = cpu_baselines()
+        cb = cpu_baselines(args.mix)
         # the faster of the reference's two builds is the baseline; the other is kept beside it
         done = sorted((c for c in cb.values() if c), key=lambda c: -c["value"])
         out["cpu_baseline"] = done[0] if done else None

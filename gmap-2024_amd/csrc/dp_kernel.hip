@@ -771,18 +771,63 @@ __global__ __launch_bounds__(128) GGX_ATTR void gg_kernel(
     scL[tid ? rlen + 1 : 0] = 0;
     scR[tid ? rlen + 1 : 0] = 0;
   }
-  for (int i = tid; i < gL; i += 128) {
-    const char c2 = segment_nt(blocks, nwords, (uint32_t)i, (uint32_t)gL, P.segposL, P.segboundL,
-                               flags & kGSegLLeft, flags & kGSegLRc);
-    gclL[i + 1] = gclass(c2);
-    // a known site has probability 1.0 in the bridge (dynprog_genome.c:2577-2578)
-    pL[i] = (kn && kb[i]) ? 1.0 : sprob[P.prob_offset + i];
-  }
-  for (int i = tid; i < gR; i += 128) {
-    const char c2 = segment_nt(blocks, nwords, (uint32_t)i, (uint32_t)gR, P.segposR, P.segboundR,
-                               flags & kGSegRLeft, flags & kGSegRRc);
-    gclR[gR - i] = gclass(c2);  // rev_gsequenceR[1-c] = segment[glengthR-c]
-    pR[i] = (kn && kb[gL + i]) ? 1.0 : sprob[P.prob_offset + gL + i];
+  // Both segments as one index space jj (L: i = jj, R: i = jj - gL), two items per thread per pass with
+  // every load issued before any is used: segment_nt's bounds (Genome_get_segment_right/left) become a
+  // class or a block address, then the flags word and the half word of each block are loaded together.
+  {
+    const int nG = gL + gR;
+    for (int b0 = tid; b0 < nG; b0 += 256) {
+      uint32_t wf[2], wv[2], bit[2];
+      int cls[2];  // kStar / kN decided from the bounds, -1: decode the words
+      double pv[2];
+      bool rcv[2];
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const int jj = b0 + 128 * u;
+        const bool act = jj < nG;
+        const bool rs = jj >= gL;
+        const uint32_t i = (uint32_t)(rs ? jj - gL : jj), L = (uint32_t)(rs ? gR : gL);
+        const uint64_t pos = rs ? P.segposR : P.segposL, bound = rs ? P.segboundR : P.segboundL;
+        const bool left = rs ? (flags & kGSegRLeft) : (flags & kGSegLLeft);
+        rcv[u] = rs ? (flags & kGSegRRc) : (flags & kGSegLRc);
+        const uint64_t j = rcv[u] ? L - 1u - i : i;
+        bool star;
+        uint64_t g;
+        if (!left) {  // Genome_get_segment_right(left = pos, L, chrhigh = bound)
+          star = pos >= bound || (pos + L >= bound && j + (pos + L - bound) >= L);
+          g = pos + j;
+        } else {      // Genome_get_segment_left(right = pos, L, chroffset = bound)
+          star = pos < bound || (pos < bound + L && j < bound + L - pos);
+          g = pos - L + j;
+        }
+        const uint64_t ptr = (g >> 5) * 3u;
+        cls[u] = star ? kStar : (ptr + 2 >= nwords ? kN : -1);  // beyond the allocation: 'N' (decode_nt)
+        const uint64_t pp = (cls[u] < 0 && act) ? ptr : 0;
+        bit[u] = (uint32_t)(g & 31u);
+        wf[u] = blocks[pp + 2];
+        wv[u] = blocks[pp + (bit[u] < 16 ? 1 : 0)];
+        pv[u] = act ? sprob[P.prob_offset + jj] : 0.0;
+        // a known site has probability 1.0 in the bridge (dynprog_genome.c:2577-2578)
+        if (kn && act && kb[jj]) pv[u] = 1.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const int jj = b0 + 128 * u;
+        if (jj >= nG) continue;
+        int c = cls[u];
+        if (c < 0) {
+          const int x = (int)((wv[u] >> (2u * (bit[u] & 15u))) & 3u);
+          c = ((wf[u] >> bit[u]) & 1u) ? kN : (rcv[u] ? 3 - x : x);  // complement of A C G T is 3 - code
+        }
+        if (jj < gL) {
+          gclL[jj + 1] = (uint8_t)c;
+          pL[jj] = pv[u];
+        } else {
+          gclR[gR - (jj - gL)] = (uint8_t)c;  // rev_gsequenceR[1-c] = segment[glengthR-c]
+          pR[jj - gL] = pv[u];
+        }
+      }
+    }
   }
   if (tid < 64) isc[tid] = isctab[(size_t)P.iclass * 128 + ((flags & kGFinal) ? 64 : 0) + tid];
   if (tid == 0) *done = 0;

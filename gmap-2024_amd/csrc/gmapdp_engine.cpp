@@ -80,6 +80,7 @@ hipError_t launch_cg(bool simd, int RB, int nproblems, size_t lds, hipStream_t s
                      gmapdp_cdna_result* results, gmapdp_pair* pairs);
 size_t lds_bytes_oi(int umax, bool wide);
 size_t scratch_bytes_oi(int querylength, uint32_t genomiclength);
+size_t scratch_bytes_oi_fallback(int querylength, uint32_t genomiclength);
 size_t scratch_bytes_s2c(int querylength, int totalpositions, int ndiagonals);
 // the chaining kernels' counters (paths, pairs, ...) followed by their launch order (one int per call)
 inline size_t s2_counters_bytes(int n) { return 4 * sizeof(unsigned long long) + sizeof(int) * (size_t)(n > 0 ? n : 1); }
@@ -2240,17 +2241,22 @@ size_t gmapdp_oligo_diagonal_capacity(const gmapdp_oligo_problem* problems, int 
 
 }  // extern "C"
 
-// A planned stage-2 batch: descriptors (in launch-class order) resident on the device, the launch
-// classes, the per-problem scratch, the output capacities.
+// A planned stage-2 batch: descriptors (in launch-class order) resident on the device, the launches, the
+// scratch, the output capacities.  Launches are chunks of one launch class: each chunk's problems have their
+// scratch regions and event-pool slots laid out from 0, and the chunks run one after another on the stream,
+// so the scratch and the pool are sized for the largest chunk, not for the batch (a 214-kb stage-2 window,
+// as GMAP's stage 1 extends a gregion by 100 kb each side, gregion.c:899, takes 1.7 MB of hit list and
+// 7 MB of sequential-walk states).
 struct gmapdp_oligo_plan {
   int n = 0;
   DevOligoProblem* d_probs = nullptr;
   unsigned char* d_scratch = nullptr;
-  std::vector<std::pair<int, int>> launches;  // (first, count)
-  std::vector<int> umax;  // per launch: 2 * umax + (32-bit counters)
-  size_t table_cap = 0, diag_cap = 0;
-  // get_mappings' event pool (3 slots per hit, shared by the batch through an atomic cursor; a
-  // problem that no longer fits runs the sequential walk in its own scratch instead)
+  std::vector<std::pair<int, int>> launches;  // (first, count) per chunk
+  std::vector<int> umax;                      // per chunk: 2 * umax + (32-bit counters)
+  std::vector<int> keys;                      // per problem in launch order: its class key
+  size_t table_cap = 0, diag_cap = 0, scratch_cap = 0;
+  // get_mappings' event pool (3 slots per hit, shared by a chunk through an atomic cursor; a problem that no
+  // longer fits runs the sequential walk in its fallback region, or reports overflow when it has none)
   uint64_t* d_pool = nullptr;
   unsigned long long* d_pool_counter = nullptr;
   unsigned long long pool_cap = 0;
@@ -2260,6 +2266,9 @@ struct gmapdp_oligo_plan {
   bool borrowed = false;
   std::vector<DevOligoProblem> ord;
 };
+
+static constexpr int kOligoChunkProblems = 4096;
+static constexpr size_t kOligoChunkBytes = size_t(3) << 30;
 
 static void oligo_plan_free(gmapdp_oligo_plan* p) {
   if (!p) return;
@@ -2274,9 +2283,68 @@ static void oligo_plan_free(gmapdp_oligo_plan* p) {
   delete p;
 }
 
-extern "C" {
+// Cut the launch-ordered problems into chunks and lay out each chunk's scratch (main region, then the
+// sequential walk's region when `fallback`) and pool.  slots[i]: pool slots problem i may take.
+static void oligo_layout(gmapdp_oligo_plan* P, const std::vector<size_t>& slots, bool fallback) {
+  P->launches.clear();
+  P->umax.clear();
+  P->scratch_cap = 0;
+  P->pool_cap = 0;
+  size_t cb = 0, cs = 0;
+  int first = 0;
+  auto close = [&](int end) {
+    if (end > first) {
+      P->launches.push_back({first, end - first});
+      P->umax.push_back(P->keys[first]);
+      P->scratch_cap = std::max(P->scratch_cap, cb);
+      P->pool_cap = std::max<unsigned long long>(P->pool_cap, cs);
+    }
+    first = end;
+    cb = cs = 0;
+  };
+  for (int k = 0; k < (int)P->ord.size(); k++) {
+    DevOligoProblem& d = P->ord[k];
+    const uint32_t w = d.chrend > d.chrstart ? d.chrend - d.chrstart : 0;
+    const size_t mb = align_up(scratch_bytes_oi(d.querylength, w), 256);
+    const size_t fb = fallback ? align_up(scratch_bytes_oi_fallback(d.querylength, w), 256) : 0;
+    if (k > first && (P->keys[k] != P->keys[first] || k - first >= kOligoChunkProblems || cb + mb + fb > kOligoChunkBytes))
+      close(k);
+    d.scratch_offset = (int64_t)cb;
+    d.fallback_offset = fallback ? (int64_t)(cb + mb) : -1;
+    cb += mb + fb;
+    cs += slots[d.index];
+  }
+  close((int)P->ord.size());
+}
 
-}  // extern "C"
+static hipError_t oligo_buffers(gmapdp_ctx* ctx, gmapdp_oligo_plan* P) {
+  const int n = P->n;
+  hipError_t e = hipSuccess;
+  if (P->borrowed) {
+    e = ctx->oprobs.ensure(sizeof(DevOligoProblem) * std::max(n, 1));
+    if (e == hipSuccess) e = ctx->oscratch.ensure(std::max<size_t>(P->scratch_cap, 256));
+    if (e == hipSuccess) e = ctx->opool.ensure(sizeof(uint64_t) * std::max<size_t>(P->pool_cap, 1));
+    if (e == hipSuccess) e = ctx->opoolctr.ensure(sizeof(unsigned long long));
+    P->d_probs = (DevOligoProblem*)ctx->oprobs.p;
+    P->d_scratch = (unsigned char*)ctx->oscratch.p;
+    P->d_pool = (uint64_t*)ctx->opool.p;
+    P->d_pool_counter = (unsigned long long*)ctx->opoolctr.p;
+    if (e == hipSuccess && n)
+      e = hipMemcpyAsync(P->d_probs, P->ord.data(), sizeof(DevOligoProblem) * n, hipMemcpyHostToDevice, ctx->stream);
+    return e;
+  }
+  for (void** b : {(void**)&P->d_scratch, (void**)&P->d_pool}) {
+    if (*b) (void)hipFree(*b);
+    *b = nullptr;
+  }
+  if (!P->d_probs) e = hipMalloc(&P->d_probs, sizeof(DevOligoProblem) * std::max(n, 1));
+  if (e == hipSuccess) e = hipMalloc(&P->d_scratch, std::max<size_t>(P->scratch_cap, 256));
+  if (e == hipSuccess) e = hipMalloc(&P->d_pool, sizeof(uint64_t) * std::max<size_t>(P->pool_cap, 1));
+  if (e == hipSuccess && !P->d_pool_counter) e = hipMalloc(&P->d_pool_counter, sizeof(unsigned long long));
+  if (e == hipSuccess && n)
+    e = hipMemcpy(P->d_probs, P->ord.data(), sizeof(DevOligoProblem) * n, hipMemcpyHostToDevice);
+  return e;
+}
 
 static int oligo_plan_build(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problems, int n, const char* qseq_uc,
                             size_t qbytes, gmapdp_oligo_plan** plan, bool borrow) {
@@ -2286,14 +2354,17 @@ static int oligo_plan_build(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problem
   (void)hipSetDevice(ctx->device);
   std::vector<uint32_t> bm(2048, 0u);
   std::vector<DevOligoProblem> dev(n);
-  size_t toff = 0, doff = 0, soff = 0, pslots = 0;
+  std::vector<size_t> slots(n);
+  size_t toff = 0, doff = 0;
   static const int kBuckets[] = {1024, 2048, 4096, 8192, 16384};  // launch classes by LDS
   std::map<int, std::vector<int>> classes;
+  const char* ev = std::getenv("GMAPDP_OLIGO_POOL_SLOTS");  // tests: a small pool forces the sequential walk
   for (int i = 0; i < n; i++) {
     const gmapdp_oligo_problem& p = problems[i];
     if (p.querylength <= 8) return bad(ctx, "stage-2 seeding needs querylength > 8 (Oligoindex_set_inquery)");
     if (p.qoff < 0 || (size_t)p.qoff + (size_t)p.querylength > qbytes) return bad(ctx, "query outside the arena");
-    if (oligo_window(p) > 0) {  // the last 8-mer start's half-word and the one after it (window8)
+    const uint64_t win = oligo_window(p);
+    if (win > 0) {  // the last 8-mer start's half-word and the one after it (window8)
       const uint64_t lpl = (uint64_t)p.chroffset + p.chrend + (p.plusp ? 0 : 1) - 8;
       const uint64_t h = (lpl >> 4) + 1;
       if (3 * (h >> 1) + 1 >= ctx->genome_words) return bad(ctx, "stage-2 window past the genome");
@@ -2317,56 +2388,63 @@ static int oligo_plan_build(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problem
     d.index = i;
     d.table_offset = (int64_t)toff;
     d.diag_offset = (int64_t)doff;
-    d.scratch_offset = (int64_t)soff;
     toff += oligo_table_cap(p);
-    pslots += 3 * std::min<size_t>(oligo_table_cap(p), 2 * (size_t)p.querylength + 256);  // hits ~ query 8-mers
     doff += oligo_diag_cap(p);
-    soff += align_up(scratch_bytes_oi(p.querylength, p.chrend > p.chrstart ? p.chrend - p.chrstart : 0), 256);
+    // hits ~ the query's 8-mers once (the locus) plus the window's random matches (4^-8 per position each)
+    const size_t est = (size_t)p.querylength * (2 + (size_t)(win >> 15)) + 256;
+    slots[i] = 3 * std::min<size_t>(oligo_table_cap(p), est);
     // launch class: (umax, 32-bit counters); 16-bit counters when no count can reach 2^16
-    const int wide = oligo_window(p) >= 65536 ? 1 : 0;
-    classes[2 * umax + wide].push_back(i);
+    classes[2 * umax + (win >= 65536 ? 1 : 0)].push_back(i);
   }
   if (toff > 0x7fffffffull) return bad(ctx, "stage-2 table arena beyond 2^31 entries");
   gmapdp_oligo_plan* P = new gmapdp_oligo_plan();
   P->n = n;
   P->table_cap = toff;
   P->diag_cap = doff;
-  std::vector<DevOligoProblem>& ord = P->ord;
-  ord.reserve(n);
-  for (auto& kv : classes) {
-    P->launches.push_back({(int)ord.size(), (int)kv.second.size()});
-    P->umax.push_back(kv.first);
-    for (int i : kv.second) ord.push_back(dev[i]);
-  }
-  if (const char* ev = std::getenv("GMAPDP_OLIGO_POOL_SLOTS")) pslots = std::strtoull(ev, nullptr, 10);  // tests
-  P->pool_cap = pslots;
-  hipError_t e = hipSuccess;
-  if (borrow) {
-    P->borrowed = true;
-    e = ctx->oprobs.ensure(sizeof(DevOligoProblem) * std::max(n, 1));
-    if (e == hipSuccess) e = ctx->oscratch.ensure(std::max<size_t>(soff, 256));
-    if (e == hipSuccess) e = ctx->opool.ensure(sizeof(uint64_t) * std::max<size_t>(pslots, 1));
-    if (e == hipSuccess) e = ctx->opoolctr.ensure(sizeof(unsigned long long));
-    P->d_probs = (DevOligoProblem*)ctx->oprobs.p;
-    P->d_scratch = (unsigned char*)ctx->oscratch.p;
-    P->d_pool = (uint64_t*)ctx->opool.p;
-    P->d_pool_counter = (unsigned long long*)ctx->opoolctr.p;
-    if (e == hipSuccess && n)
-      e = hipMemcpyAsync(P->d_probs, ord.data(), sizeof(DevOligoProblem) * n, hipMemcpyHostToDevice, ctx->stream);
-  } else {
-    e = hipMalloc(&P->d_probs, sizeof(DevOligoProblem) * std::max(n, 1));
-    if (e == hipSuccess) e = hipMalloc(&P->d_scratch, std::max<size_t>(soff, 256));
-    if (e == hipSuccess) e = hipMalloc(&P->d_pool, sizeof(uint64_t) * std::max<size_t>(pslots, 1));
-    if (e == hipSuccess) e = hipMalloc(&P->d_pool_counter, sizeof(unsigned long long));
-    if (e == hipSuccess && n)
-      e = hipMemcpy(P->d_probs, ord.data(), sizeof(DevOligoProblem) * n, hipMemcpyHostToDevice);
-  }
+  P->borrowed = borrow;
+  P->ord.reserve(n);
+  for (auto& kv : classes)
+    for (int i : kv.second) {
+      P->ord.push_back(dev[i]);
+      P->keys.push_back(kv.first);
+    }
+  oligo_layout(P, slots, true);
+  if (ev) P->pool_cap = std::strtoull(ev, nullptr, 10);  // per chunk
+  const hipError_t e = oligo_buffers(ctx, P);
   if (e != hipSuccess) {
     oligo_plan_free(P);
     return fail(ctx, GMAPDP_ENOMEM, "oligo plan: %s", e);
   }
   *plan = P;
   return GMAPDP_OK;
+}
+
+// After a measured run (the stage-2 plan's sizing run): every arena laid out from what the run wrote.  The
+// table holds at most totalpositions entries per problem (each distinct 8-mer's hits, counted at least once
+// over the query positions), the diagonal arena exactly ndiagonals records, the pool exactly 3 slots per hit
+// (so no problem takes the sequential walk and no fallback region is kept); a rerun seeds the same way.
+static hipError_t oligo_plan_relayout(gmapdp_ctx* ctx, gmapdp_oligo_plan* P, const gmapdp_oligo_problem* problems,
+                                      const gmapdp_oligo_result* ores) {
+  const int n = P->n;
+  std::vector<int64_t> toffs(n), doffs(n);
+  std::vector<size_t> slots(n);
+  size_t t = 0, dd = 0;
+  for (int i = 0; i < n; i++) {
+    toffs[i] = (int64_t)t;
+    doffs[i] = (int64_t)dd;
+    const size_t tp = (size_t)std::max(ores[i].totalpositions, 0);
+    t += std::min<size_t>(oligo_table_cap(problems[i]), tp);
+    dd += (size_t)std::max(ores[i].ndiagonals, 0);
+    slots[i] = 3 * tp;
+  }
+  for (DevOligoProblem& d : P->ord) {
+    d.table_offset = toffs[d.index];
+    d.diag_offset = doffs[d.index];
+  }
+  P->table_cap = t;
+  P->diag_cap = dd;
+  oligo_layout(P, slots, false);
+  return oligo_buffers(ctx, P);
 }
 
 extern "C" {
@@ -2388,9 +2466,10 @@ int gmapdp_oligo_plan_run(gmapdp_ctx* ctx, const gmapdp_oligo_plan* plan, const 
   if (plan->n == 0) return GMAPDP_OK;
   (void)hipSetDevice(ctx->device);
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-  if (hipMemsetAsync(plan->d_pool_counter, 0, sizeof(unsigned long long), s) != hipSuccess)
-    return fail(ctx, GMAPDP_ELAUNCH, "oligo pool reset: %s", hipGetLastError());
   for (size_t li = 0; li < plan->launches.size(); li++) {
+    // the chunks reuse one scratch and one pool, in stream order
+    if (hipMemsetAsync(plan->d_pool_counter, 0, sizeof(unsigned long long), s) != hipSuccess)
+      return fail(ctx, GMAPDP_ELAUNCH, "oligo pool reset: %s", hipGetLastError());
     const int key = plan->umax[li];
     const hipError_t e = launch_oi(key & 1, plan->launches[li].second, lds_bytes_oi(key >> 1, key & 1), s,
                                    plan->d_probs + plan->launches[li].first, ctx->d_genome, d_qseq_uc,
@@ -3207,36 +3286,18 @@ int gmapdp_stage2_plan_create(gmapdp_ctx* ctx, const gmapdp_stage2_problem* prob
     return rc;
   }
   // The seeding's arenas were sized from upper bounds (a window's worth of positions and 24 diagonals per
-  // query position: 19 GB for 10 000 5-kb reads).  Re-lay them out from this run's measured use -- the
-  // table holds at most totalpositions entries (one per distinct 8-mer hit, each counted at least once
-  // over the query positions), the diagonal arena exactly ndiagonals records -- so that the plan keeps
-  // only what its runs write; every run of the plan seeds the same way and writes the same amounts.
-  {
-    std::vector<int64_t> toffs(n), doffs(n);
-    size_t t = 0, dd = 0;
-    for (int i = 0; i < n; i++) {
-      toffs[i] = (int64_t)t;
-      doffs[i] = (int64_t)dd;
-      t += std::min<size_t>(oligo_table_cap(op[i]), (size_t)std::max(ores[i].totalpositions, 0));
-      dd += (size_t)std::max(ores[i].ndiagonals, 0);
-    }
-    for (DevOligoProblem& d : P->oplan->ord) {
-      d.table_offset = toffs[d.index];
-      d.diag_offset = doffs[d.index];
-    }
-    (void)hipFree(P->d_table);
-    (void)hipFree(P->d_diag);
-    P->d_table = nullptr;
-    P->d_diag = nullptr;
-    P->oplan->table_cap = t;
-    P->oplan->diag_cap = dd;
-    e = hipMemcpy(P->oplan->d_probs, P->oplan->ord.data(), sizeof(DevOligoProblem) * n, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&P->d_table, sizeof(uint32_t) * std::max<size_t>(t, 1));
-    if (e == hipSuccess) e = hipMalloc(&P->d_diag, 4 * sizeof(int32_t) * std::max<size_t>(dd, 1));
-    if (e != hipSuccess) {
-      stage2_plan_free(P);
-      return fail(ctx, GMAPDP_ENOMEM, "stage-2 plan arenas: %s", e);
-    }
+  // query position: 19 GB for 10 000 5-kb reads).  Re-lay them out from this run's measured use
+  // (oligo_plan_relayout) so the plan keeps only what its runs write.
+  (void)hipFree(P->d_table);
+  (void)hipFree(P->d_diag);
+  P->d_table = nullptr;
+  P->d_diag = nullptr;
+  e = oligo_plan_relayout(ctx, P->oplan, op.data(), ores.data());
+  if (e == hipSuccess) e = hipMalloc(&P->d_table, sizeof(uint32_t) * std::max<size_t>(P->oplan->table_cap, 1));
+  if (e == hipSuccess) e = hipMalloc(&P->d_diag, 4 * sizeof(int32_t) * std::max<size_t>(P->oplan->diag_cap, 1));
+  if (e != hipSuccess) {
+    stage2_plan_free(P);
+    return fail(ctx, GMAPDP_ENOMEM, "stage-2 plan arenas: %s", e);
   }
   for (int i = 0; i < n; i++) {
     dp[i].scratch_offset = (int64_t)P->scratch;

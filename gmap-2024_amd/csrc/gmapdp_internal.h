@@ -175,7 +175,8 @@ struct DevOligoProblem {
   int32_t index;          // the problem's index in the batch (its result slot)
   int64_t table_offset;   // first entry of the problem's table in the positions arena
   int64_t diag_offset;    // first diagonal record (4 x int32)
-  int64_t scratch_offset; // byte offset of the problem's region of the global scratch
+  int64_t scratch_offset; // byte offset of the problem's region of the global scratch (its launch chunk's)
+  int64_t fallback_offset; // the sequential walk's region in the same scratch, or -1: none (exact pool)
 };
 
 // Stage2_compute descriptor (stage2.c:6325): the seeding problem's results slot plus the chaining

@@ -77,18 +77,28 @@ __device__ __forceinline__ int oligo_id(const uint32_t* bitmap, const uint16_t* 
   return wrank[m >> 5] + __popc(wbits & ((1u << (m & 31)) - 1u));
 }
 
-// per-problem scratch: cum_nohits (querylength + 1 ints), the genomicdiag init flags, the states
+// per-problem scratch: cum_nohits (querylength + 1 ints), the event-pool offset, the window's hit list
 struct ScratchOi {
-  size_t poolbase, initp, states, hits, total;
+  size_t poolbase, hits, total;
 };
 __host__ __device__ inline ScratchOi scratch_oi(int querylength, uint32_t genomiclength) {
-  const size_t nd = (size_t)querylength + genomiclength + 1;
   ScratchOi s;
   s.poolbase = align16(4 * (size_t)(querylength + 1));  // the problem's event-pool offset (or ~0)
-  s.initp = align16(s.poolbase + 8);
-  s.states = align16(s.initp + nd);
-  s.hits = align16(s.states + nd * sizeof(OiState));
+  s.hits = align16(s.poolbase + 8);
   s.total = align16(s.hits + 8 * ((size_t)genomiclength + 2));
+  return s;
+}
+// the sequential walk's region (only when the event pool cannot take the problem): the genomicdiag init
+// flags and states, one per diagonal (querylength + window + 1); DevOligoProblem.fallback_offset
+struct ScratchOiFb {
+  size_t initp, states, total;
+};
+__host__ __device__ inline ScratchOiFb scratch_oi_fb(int querylength, uint32_t genomiclength) {
+  const size_t nd = (size_t)querylength + genomiclength + 1;
+  ScratchOiFb s;
+  s.initp = 0;
+  s.states = align16(nd);
+  s.total = align16(s.states + nd * sizeof(OiState));
   return s;
 }
 
@@ -667,10 +677,20 @@ __global__ __launch_bounds__(64) void oi_map_kernel(
     if (!oi_mappings_sorted(lane, qlen, nq, totalpositions, maxdiag, chrinit, diag_lookback, suffn, npq, mpq, cum,
                             table_all, pool, *reinterpret_cast<const unsigned long long*>(base_s + so.poolbase), hist,
                             evq, good, ngood, maxn)) {
-      // the event pool is full: the sequential walk (per-diagonal states in this problem's scratch)
-      unsigned char* initp = base_s + so.initp;
-      OiState* st = reinterpret_cast<OiState*>(base_s + so.states);
-      for (size_t b = 16 * (size_t)lane; b < so.states - so.initp; b += 16 * 64)
+      // the event pool is full: the sequential walk (per-diagonal states in the problem's fallback region;
+      // a plan sized from a measured run has an exact pool and none: report the overflow instead)
+      if (P.fallback_offset < 0) {
+        if (lane == 0) {
+          results[P.index].maxnconsecutive = 0;
+          results[P.index].ndiagonals = 0;
+          results[P.index].oned_matrix_p = -1;  // Stage2_compute answers GMAPDP overflow (status -2)
+        }
+        return;
+      }
+      const ScratchOiFb fb = scratch_oi_fb(qlen, P.chrend - P.chrstart);
+      unsigned char* initp = scratch + P.fallback_offset + fb.initp;
+      OiState* st = reinterpret_cast<OiState*>(scratch + P.fallback_offset + fb.states);
+      for (size_t b = 16 * (size_t)lane; b < fb.states - fb.initp; b += 16 * 64)
         *reinterpret_cast<uint4*>(initp + b) = make_uint4(0u, 0u, 0u, 0u);
       __threadfence_block();
       int best = -1;  // diagi of each good diagonal goes in field 0 of its record first
@@ -773,6 +793,9 @@ extern "C" int gmapdp_debug_oi_marks(unsigned long long* out) {
 size_t lds_bytes_oi(int umax, bool wide) { return 6 * (size_t)kOiWords + (wide ? 8 : 4) * (size_t)umax; }
 size_t scratch_bytes_oi(int querylength, uint32_t genomiclength) {
   return scratch_oi(querylength, genomiclength).total;
+}
+size_t scratch_bytes_oi_fallback(int querylength, uint32_t genomiclength) {
+  return scratch_oi_fb(querylength, genomiclength).total;
 }
 
 hipError_t launch_oi(bool wide, int nproblems, size_t lds, hipStream_t stream, const DevOligoProblem* probs,

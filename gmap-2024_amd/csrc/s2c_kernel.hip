@@ -1529,7 +1529,8 @@ __global__ __launch_bounds__(64) void s2a_kernel(
   R.path_offset = 0;
   R.npairs = 0;
   S2_MARK(0);
-  if (P.scratch_offset + (unsigned long long)so.total > scratch_cap) {
+  // chaining scratch too small, or the seeding's event pool could not take the call (oned_matrix_p -1)
+  if (P.scratch_offset + (unsigned long long)so.total > scratch_cap || O.oned_matrix_p < 0) {
     if (lane == 0) {
       R.status = kS2Overflow;
       results[P.index] = R;

@@ -25,6 +25,8 @@ size, and rank r of N takes the blocks b with b % N == r (GMAP's --part=r/N rule
 applied per block; gmapdp.shard).  Every rank plants the intron sites of every block of the stream in
 block order, so all ranks hold the same genome.
 """
+import os
+
 import numpy as np
 
 # GRCh38 primary assembly chromosome lengths (chr1..chr22, chrX, chrY)
@@ -50,10 +52,13 @@ class Shape:
     """Read shape and per-read call mix of one BASELINE config."""
 
     def __init__(self, name, exons, exlen, subs, indel, single, end5, end3, genome, microexon, source,
-                 single_indel=0.15, single_dmean=0.0):
+                 single_indel=0.15, single_dmean=0.0, stage2=1.0, pad=1000):
         self.name, self.exons, self.exlen, self.subs, self.indel = name, exons, exlen, subs, indel
         self.single, self.end5, self.end3, self.genome, self.microexon = single, end5, end3, genome, microexon
         self.source = source
+        # Stage2_compute calls per read (above 1: a second call on the same read and nearly the same window,
+        # as gmap -d makes for part of its reads) and the genomic window: the locus plus `pad` nt each side
+        self.stage2, self.pad = stage2, pad
         # single gaps whose query and genome lengths differ: a fraction, and (single_dmean > 0) the mean of
         # an exponential genome-minus-query excess; otherwise a uniform +-1..3 nt indel
         self.single_indel, self.single_dmean = single_indel, single_dmean
@@ -63,22 +68,39 @@ class Shape:
         return self.exons * self.exlen
 
 
-# configs[2]: 2-kb cDNA, 5 x 400 nt, 2 % substitutions; call mix from SURVEY App. B (nosimd instrumentation)
-CDNA2K = Shape("cdna2k", 5, 400, 0.02, 0.0, 43.7, 7.1, 6.5, 49.4, 25.6, "SURVEY App. B")
+# configs[2]: 2-kb cDNA, 5 x 400 nt, 2 % substitutions.  Call mix measured with the reference's own gmap as
+# it runs in production (`gmap -d` over a gmap_build index: stage 1, then stages 2 and 3; tools/callmix.py
+# --index, profiles/r04_callmix/callmix_d.json): per read 21.1 single gaps (2.5 % with query and genome
+# lengths differing, by 80 nt on average), 6.78 end5, 6.38 end3, 49.7 genome gaps, 7.53 microexon calls and
+# 1.585 Stage2_compute calls over windows of 205-232 kb (p10-p90): stage 1 extends each gregion by
+# EXTRA_LONGEND = 100 kb on both sides (gregion.c:27, 899).
+CDNA2K = Shape("cdna2k", 5, 400, 0.02, 0.0, 21.1, 6.78, 6.38, 49.7, 7.53,
+               "measured: reference gmap -d on 200 reads of this shape (profiles/r04_callmix/callmix_d.json)",
+               single_indel=0.025, single_dmean=80.0, stage2=1.585, pad=98000)
+# the same reads with SURVEY App. B's mix (rounds 1-3's headline): one Stage2_compute per read over the
+# locus +- 1 kb, 43.7 single, 7.1 end5, 6.5 end3, 49.4 genome, 25.6 microexon calls
+CDNA2K_APPB = Shape("cdna2k-appb", 5, 400, 0.02, 0.0, 43.7, 7.1, 6.5, 49.4, 25.6, "SURVEY App. B")
 # configs[4]: 5-kb Iso-Seq-style reads, 10 x 500 nt, 1 % substitutions + 1 % indels.  Call mix measured
 # with the reference's own gmap on 200 reads of that shape (oracle/callmix.c, tools/callmix.py,
 # profiles/r03_callmix/callmix.json): per read 285.1 single gaps (91 % with query and genome lengths
 # differing, genome longer by 22 nt on average), 4.66 end5, 4.05 end3, 77.4 genome gaps, 36.95 microexon
 # calls; Stage2_compute once per read over the read's gregion, as configs[2]
-ISOSEQ5K = Shape("isoseq5k", 10, 500, 0.01, 0.01, 285.1, 4.66, 4.05, 77.4, 36.95,
-                 "measured: reference gmap on 200 reads of this shape (profiles/r03_callmix/callmix.json)",
-                 single_indel=0.91, single_dmean=22.0)
+ISOSEQ5K_G = Shape("isoseq5k-g", 10, 500, 0.01, 0.01, 285.1, 4.66, 4.05, 77.4, 36.95,
+                   "measured: reference gmap -g on 200 reads of this shape (profiles/r03_callmix/callmix.json)",
+                   single_indel=0.91, single_dmean=22.0)
+# the same measured with gmap -d (profiles/r04_callmix/callmix_d.json): 584.5 single gaps (96 % lengths
+# differing, by 33 nt), 7.72 end5, 6.79 end3, 148.5 genome gaps, 67.5 microexon calls, 1.69 Stage2_compute
+# calls over 217-263-kb windows
+ISOSEQ5K = Shape("isoseq5k", 10, 500, 0.01, 0.01, 584.5, 7.72, 6.79, 148.5, 67.5,
+                 "measured: reference gmap -d on 200 reads of this shape (profiles/r04_callmix/callmix_d.json)",
+                 single_indel=0.96, single_dmean=33.0, stage2=1.69, pad=110000)
+SHAPES = {"d": CDNA2K, "appb": CDNA2K_APPB}
 
-SINGLE_PER_READ = CDNA2K.single        # Dynprog_single_gap calls per 2-kb read (nosimd)
+SINGLE_PER_READ = CDNA2K.single        # Dynprog_single_gap calls per 2-kb read (gmap -d, nosimd)
 END5_PER_READ = CDNA2K.end5            # Dynprog_end5_gap
 END3_PER_READ = CDNA2K.end3            # Dynprog_end3_gap
 GENOME_PER_READ = CDNA2K.genome        # Dynprog_genome_gap
-STAGE2_PER_READ = 1                    # Stage2_compute seeding calls
+STAGE2_PER_READ = CDNA2K.stage2        # Stage2_compute calls
 MICROEXON_PER_READ = CDNA2K.microexon  # Dynprog_microexon_int
 
 COMPL = np.zeros(256, dtype=np.uint8)
@@ -302,24 +324,45 @@ def genome_gap_sites(layout, n, site_seed=23):
     choff, chrhigh, clen = layout.sample(srng, n, 8000)
     goffL = (srng.random(n) * (clen - 7200)).astype(np.int64) + 100
     revR = goffL + a + intron + b - 1
-    return {"r": r, "a": a, "b": b, "watson": watson, "choff": choff, "chrhigh": chrhigh, "goffL": goffL,
+    don, acc = splice_pool()
+    dctx = srng.integers(0, len(don), size=n)
+    actx = srng.integers(0, len(acc), size=n)
+    return {"dctx": dctx, "actx": actx,
+            "r": r, "a": a, "b": b, "watson": watson, "choff": choff, "chrhigh": chrhigh, "goffL": goffL,
             "revR": revR}
 
 
-# Splice-site contexts planted around each genome gap's intron (strand sense): the donor's 3 exonic +
-# 6 intronic nt and the acceptor's 20 intronic + 3 exonic nt, strong sites under GMAP's MaxEnt models
-# (Maxent_hr_donor_prob / _acceptor_prob 0.999+, which the engine evaluates on the device in the step),
-# as real introns mostly are; the GT..AG dinucleotides are part of them.
-DONOR_CONTEXT = b"CAGGTAAGT"                    # x - 3 .. x + 5 (x = first intron base)
-ACCEPTOR_CONTEXT = b"CCTTTCTTTTCCTTTTCTAGGTA"   # y - 19 .. y + 3 (y = last intron base)
+# Splice-site contexts planted around every genome-gap intron, so that MaxEnt (evaluated on the device in
+# the step) finds strong sites there, as at real introns: a donor context x-3 .. x+5 (x = first intron base)
+# and an acceptor context y-19 .. y+3 (y = last intron base), GT..AG included, each site drawing its own from a
+# pool of distinct contexts that all score >= 0.9 (splice_contexts.txt, tools/make_splice_pool.py).  One fixed
+# context at every site made its 8-mers ~1 per 750 nt of the genome and the stage-2 seeding hits of the reads
+# crossing them about doubled; the pool keeps every 8-mer near the i.i.d. background.
+_SPLICE_POOL = []
+
+
+def splice_pool():
+    """(donor contexts, acceptor contexts) as uint8 arrays of shape (n, 9) and (n, 23)."""
+    if not _SPLICE_POOL:
+        d, a = [], []
+        for line in open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "splice_contexts.txt")):
+            if line.startswith("D "):
+                d.append(line.split()[1])
+            elif line.startswith("A "):
+                a.append(line.split()[1])
+        _SPLICE_POOL.extend([np.frombuffer("".join(d).encode(), dtype=np.uint8).reshape(-1, 9),
+                             np.frombuffer("".join(a).encode(), dtype=np.uint8).reshape(-1, 23)])
+    return _SPLICE_POOL[0], _SPLICE_POOL[1]
 
 
 def plant_sites(genome, st):
     """Write the splice-site contexts of genome_gap_sites (GT..AG introns) into `genome` (in place)."""
     watson, choff, chrhigh = st["watson"], st["choff"], st["chrhigh"]
     x, y = st["goffL"] + st["a"], st["revR"] - st["b"]   # first / last intron base, strand coordinates
+    don, acc = splice_pool()
+    dc, ac = don[st["dctx"]], acc[st["actx"]]
     idx, ch = [], []
-    ctx = [(x + k - 3, c) for k, c in enumerate(DONOR_CONTEXT)] + [(y + k - 19, c) for k, c in enumerate(ACCEPTOR_CONTEXT)]
+    ctx = [(x + k - 3, dc[:, k]) for k in range(9)] + [(y + k - 19, ac[:, k]) for k in range(23)]
     for pos, c in ctx:
         idx.append(np.where(watson, choff + pos, chrhigh - pos))
         ch.append(np.where(watson, c, COMPL[c]).astype(np.uint8))
@@ -388,10 +431,12 @@ def mutate(q, rng, subs, indel):
     return flat.astype(np.uint8), reps.sum(axis=1)
 
 
-def make_stage2(genome, layout, n, rng, exons=5, exlen=400, pad=1000, subs=0.02, indel=0.0):
-    """Stage-2 calls, one per read: `exons` exons x `exlen` nt cut from the genome with log-uniform
+def make_stage2(genome, layout, n, rng, exons=5, exlen=400, pad=1000, subs=0.02, indel=0.0, extra=0.0):
+    """Stage-2 calls of n reads: `exons` exons x `exlen` nt cut from the genome with log-uniform
     [80, 20000] introns, substitutions and indels, half reverse-complemented (seeded on the minus
-    strand), against the window spanning the locus plus 1 kb each side (the gregion).
+    strand), against the window spanning the locus plus `pad` nt each side (the extended gregion); then
+    round(extra * n) second calls, on the first reads again over the window moved 9 nt left and 18 nt
+    shorter (what gmap -d's second calls on a read look like), each with its own copy of the query.
     Returns (gmapdp_oligo_problem array, upper-case query arena)."""
     import gmapdp
     introns = np.exp(rng.uniform(np.log(80), np.log(20000), size=(n, exons - 1))).astype(np.int64)
@@ -419,6 +464,14 @@ def make_stage2(genome, layout, n, rng, exons=5, exlen=400, pad=1000, subs=0.02,
     probs["chrhigh"] = chrhigh
     probs["plusp"] = plus
     probs["minor"] = 0
+    m = int(round(extra * n))
+    if m > 0:
+        dup = probs[:m].copy()
+        dup["qoff"] = len(q) + off[:m]
+        dup["chrstart"] = np.maximum(dup["chrstart"].astype(np.int64) - 9, 0)
+        dup["chrend"] = dup["chrend"].astype(np.int64) - 27
+        q = np.concatenate([q, q[:off[m]]])
+        probs = np.concatenate([probs, dup])
     return probs, q
 
 
@@ -462,7 +515,8 @@ def make_reads(genome, layout, reads, seed, site_seed=23, shape=CDNA2K, plant=Tr
     gp["qoff"] += len(sq) + len(eq)
     q = np.concatenate([sq, eq, gq])
     op, oq = make_stage2(genome, layout, reads, np.random.default_rng(seed + 3), exons=shape.exons,
-                         exlen=shape.exlen, subs=shape.subs, indel=shape.indel)
+                         exlen=shape.exlen, pad=shape.pad, subs=shape.subs, indel=shape.indel,
+                         extra=shape.stage2 - 1.0)
     mp = make_microexon(gp, int(round(reads * shape.microexon)), np.random.default_rng(seed + 4))
     out = {"single": sp_, "end": ep, "genome": gp, "q": q, "oligo": op, "oq": oq, "microexon": mp,
            "reads": reads}

@@ -233,7 +233,6 @@ __wrap_Stage2_compute (char *queryseq_ptr, char *queryuc_ptr, int querylength, i
                        Genome_T genome, Genome_T genomealt, Pairpool_T pairpool, Diagpool_T diagpool,
                        Cellpool_T cellpool, bool localp, bool skip_repetitive_p, bool favor_right_p,
                        int max_nalignments, Stopwatch_T stopwatch, bool diag_debug) {
-  cm_log("T %d %d%.0d%.0d%.0d\n", querylength, (int) (chrend - chrstart), 0, 0, 0);
   {
     const double t0_ = cm_begin();
     List_T r_ = __real_Stage2_compute(queryseq_ptr, queryuc_ptr, querylength, query_offset, chrstart, chrend, chroffset,
@@ -241,6 +240,9 @@ __wrap_Stage2_compute (char *queryseq_ptr, char *queryuc_ptr, int querylength, i
                                genomealt, pairpool, diagpool, cellpool, localp, skip_repetitive_p, favor_right_p,
                                max_nalignments, stopwatch, diag_debug);
     cm_end(6, t0_);
+    /* querylength, window, window start (chrpos), strand, paths returned */
+    cm_log("T %d %d %d %d %d\n", querylength, (int) (chrend - chrstart), (int) chrstart, plusp ? 1 : 0,
+           List_length(r_));
     return r_;
   }
 }

@@ -14,7 +14,7 @@ import random
 import numpy as np
 import pytest
 
-from dpbind import ORACLE_SO, Ref, random_genome, ref_available
+from dpbind import ORACLE_SO, Oracle, Ref, random_genome, ref_available
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TABLES = os.path.join(ROOT, "gmap-2024_amd", "lib", "maxent_hr_tables.bin")
@@ -78,3 +78,25 @@ def test_maxent_table_binary_layout():
     raw = open(TABLES, "rb").read()
     assert raw[:8] == b"GMDPMXT1"
     assert len(raw) == 16 + 16 * 40 + 8 * (12 * 16384 + 4 * 16)
+
+
+def test_bench_splice_pool_is_strong_and_diverse():
+    """The bench plants these contexts at its genome-gap introns (workload.splice_pool): every one is a strong
+    site under MaxEnt (>= 0.9, the oracle restatement), and they are distinct (no 8-mer is planted millions of
+    times, which would inflate stage-2 seeding hits)."""
+    import random
+    from gmapdp import workload as W
+    don, acc = W.splice_pool()
+    assert len(don) > 1000 and len(acc) >= 4096
+    assert len({d.tobytes() for d in don}) == len(don) and len({a.tobytes() for a in acc}) == len(acc)
+    rng = random.Random(3)
+    orc = Oracle()
+    for ctx, model, off in ((don[::7], 0, 3), (acc[::17], 1, 20)):
+        parts, bases, pos = [], [], 0
+        for c in ctx:
+            filler = bytes(rng.choice(b"ACGT") for _ in range(50))
+            parts += [filler, c.tobytes()]
+            bases.append(pos + 50)
+            pos += 50 + len(c)
+        orc.set_genome(b"".join(parts) + b"A" * 64)
+        assert min(orc.maxent(model, b + off, 0) for b in bases) >= 0.9

@@ -10,6 +10,12 @@ method:
 Introns log-uniform [80, 20000] nt with GT..AG planted, half the reads reverse-complemented.
 
   python tools/callmix.py --reads 200 --out profiles/r03_callmix/callmix.json
+
+--index runs GMAP as it runs in production instead (`-d`: stage 1 over a genome index, then stages 2 and
+3): the same segment is indexed by the reference's own gmap_build (util/gmap_build with the gmapindex
+compiled by `make -C oracle -f ref.mk index_tools`), and the reads are mapped against it.
+
+  python tools/callmix.py --index --reads 200 --genome 20000000 --out profiles/r04_callmix/callmix_d.json
 """
 import argparse
 import collections
@@ -81,7 +87,7 @@ def summarize(log, nreads):
              "T": "stage2_compute"}
     for k, name in names.items():
         v = np.array(kinds.get(k, []), dtype=np.int64).reshape(-1, 4 if k in ("S", "E5", "E3") else
-                                                                (5 if k == "G" else (3 if k == "C" else 2)))
+                                                                (5 if k in ("G", "T") else (3 if k == "C" else 2)))
         rec = {"calls": int(len(v)), "per_read": len(v) / nreads}
         if len(v):
             rec["rlength_mean"] = float(v[:, 0].mean())
@@ -98,8 +104,29 @@ def summarize(log, nreads):
                 rec["abs_length_diff_mean"] = float(np.abs(v[:, 0] - v[:, 1]).mean())
             if k == "T":
                 rec["window_mean"] = float(v[:, 1].mean())
+                rec["window_p10_p50_p90_max"] = [int(np.percentile(v[:, 1], x)) for x in (10, 50, 90)] + [int(v[:, 1].max())]
+                rec["plus_frac"] = float(v[:, 3].mean())
+                rec["paths_returned_hist"] = {int(x): int((v[:, 4] == x).sum()) for x in np.unique(v[:, 4])}
         out[name] = rec
     return out
+
+
+REFTREE = "/root/reference"
+BIN = os.path.join(ROOT, "oracle", "_ref", "bin")
+
+
+def build_index(d, gpath, name):
+    """gmap_build (the reference's perl driver with the gmapindex / iit_store compiled from its sources)."""
+    tbin = os.path.join(d, "bin_" + name)
+    os.makedirs(tbin)
+    for t in ("gmapindex", "iit_store"):
+        os.symlink(os.path.join(BIN, t), os.path.join(tbin, t))
+    for t in ("fa_coords", "gmap_process"):
+        os.symlink(os.path.join(REFTREE, "util", t), os.path.join(tbin, t))
+    db = os.path.join(d, "db")
+    subprocess.run(["perl", os.path.join(REFTREE, "util", "gmap_build"), "-B", tbin, "-D", db, "-d", name, gpath],
+                   check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    return ["-D", db, "-d", name]
 
 
 def main():
@@ -107,10 +134,13 @@ def main():
     ap.add_argument("--reads", type=int, default=200)
     ap.add_argument("--genome", type=int, default=2_000_000)
     ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--index", action="store_true", help="gmap -d over a gmap_build index (stage 1 included)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
-    res = {"method": "unmodified reference gmap (nosimd) in user-segment mode (-g) with the hot-path entry points "
-                     "counted (oracle/callmix.c); %d reads per shape on a %d-nt i.i.d. segment" % (a.reads, a.genome),
+    mode = ("indexed-genome mode (-d: stage 1 over a gmap_build index of the segment)" if a.index
+            else "user-segment mode (-g)")
+    res = {"method": "unmodified reference gmap (nosimd) in %s with the hot-path entry points counted "
+                     "(oracle/callmix.c); %d reads per shape on a %d-nt i.i.d. segment" % (mode, a.reads, a.genome),
            "shapes": {}}
     with tempfile.TemporaryDirectory() as d:
         for si, (shape, kw) in enumerate(SHAPES.items()):
@@ -121,7 +151,8 @@ def main():
             write_fasta(gpath, [("seg", genome.tobytes().decode())])
             write_fasta(rpath, reads)
             t0 = time.perf_counter()
-            r = subprocess.run([GMAP, "-g", gpath, "-t", str(a.threads), "-f", "samse", "--no-sam-headers", rpath],
+            src = build_index(d, gpath, shape) if a.index else ["-g", gpath]
+            r = subprocess.run([GMAP] + src + ["-t", str(a.threads), "-f", "samse", "--no-sam-headers", rpath],
                                capture_output=True, text=True, env=dict(os.environ, GMAPDP_CALLMIX_LOG=log))
             if r.returncode != 0:
                 raise SystemExit(r.stderr[-2000:])

@@ -51,11 +51,12 @@ def ref_layout(arr):
 
 
 def worker(args):
-    wid, build, budget, reads = args
+    wid, build, budget, reads, mix = args
     from gmapdp import workload as W
+    shape = W.SHAPES[mix]
     layout = W.Layout(W.CHR22)
     genome = W.make_genome(layout, seed=22)
-    d = W.make_reads(genome, layout, reads, seed=7000 + 17 * wid)
+    d = W.make_reads(genome, layout, reads, seed=7000 + 17 * wid, shape=shape)
     lib = C.CDLL(os.path.join(ROOT, "oracle", "_ref", "librefdp_%s.so" % build))
     lib.refh_init(0, 0, 0)
     lib.refh_set_genome(genome.tobytes(), len(genome))
@@ -79,9 +80,9 @@ def worker(args):
     pairs = np.zeros(cap * 32, dtype=np.uint8)  # RefPair records (oracle/refharness.c)
     paths = np.zeros(2 * 1024, dtype=np.int32)
     sc = np.zeros(8, dtype=np.int32)
-    fams = [("single", lib.refh_single_gap_batch, ref_layout(d["single"]), W.SINGLE_PER_READ),
-            ("end", lib.refh_end_gap_batch, ref_layout(d["end"]), W.END5_PER_READ + W.END3_PER_READ),
-            ("genome", lib.refh_genome_gap_batch, ref_layout(d["genome"]), W.GENOME_PER_READ)]
+    fams = [("single", lib.refh_single_gap_batch, ref_layout(d["single"]), shape.single),
+            ("end", lib.refh_end_gap_batch, ref_layout(d["end"]), shape.end5 + shape.end3),
+            ("genome", lib.refh_genome_gap_batch, ref_layout(d["genome"]), shape.genome)]
     # The host MaxEnt work the GMAP drop-in does for a genome gap (gmapdp_genome_splice_sites: every
     # position of both sides but each side's last, the reference's own Maxent_hr_*_prob; none for the
     # calls the engine answers before reading them) -- the GPU bench takes these as device inputs.
@@ -145,19 +146,19 @@ def worker(args):
         fo(qs, qs, ql, c0, c1, co, ch, pl, 1, 500000, sc.ctypes.data, paths.ctypes.data, 1024, pairs.ctypes.data, cap)
         t["oligo"] += time.perf_counter() - t0
         n["oligo"] += 1
-        for _ in range(int(round(W.MICROEXON_PER_READ))):
+        for _ in range(int(round(shape.microexon))):
             ma = micro_args[n["microexon"] % len(micro_args)]
             t0 = time.perf_counter()
             fm(ma[0], ma[0], *ma[1:], msc.ctypes.data, mds.ctypes.data, pairs.ctypes.data, cap)
             t["microexon"] += time.perf_counter() - t0
             n["microexon"] += 1
     per_call = {k: t[k] / max(n[k], 1) for k in t}
-    sec_per_read = (W.SINGLE_PER_READ * per_call["single"] + (W.END5_PER_READ + W.END3_PER_READ) * per_call["end"]
-                    + W.GENOME_PER_READ * per_call["genome"] + W.STAGE2_PER_READ * per_call["oligo"]
-                    + W.MICROEXON_PER_READ * per_call["microexon"])
+    sec_per_read = (shape.single * per_call["single"] + (shape.end5 + shape.end3) * per_call["end"]
+                    + shape.genome * per_call["genome"] + shape.stage2 * per_call["oligo"]
+                    + shape.microexon * per_call["microexon"])
     return {"reads_per_s": 1.0 / sec_per_read, "calls": n, "seconds": t, "per_call_us":
             {k: v * 1e6 for k, v in per_call.items()},
-            "host_maxent_reads_per_s": 1.0 / max(W.GENOME_PER_READ * per_call["host_maxent"], 1e-12)}
+            "host_maxent_reads_per_s": 1.0 / max(shape.genome * per_call["host_maxent"], 1e-12)}
 
 
 def main():
@@ -166,7 +167,10 @@ def main():
     ap.add_argument("--cores", type=int, default=0, help="worker processes (0: the CPUs this process may use, <= 16)")
     ap.add_argument("--budget", type=float, default=10.0, help="seconds of timed calls per worker")
     ap.add_argument("--reads", type=int, default=200, help="reads generated per worker (the sample is cycled)")
+    ap.add_argument("--mix", default="d", choices=["d", "appb"], help="per-read call mix (workload.SHAPES)")
     a = ap.parse_args()
+    from gmapdp import workload as W
+    shape = W.SHAPES[a.mix]
     so = os.path.join(ROOT, "oracle", "_ref", "librefdp_%s.so" % a.build)
     if not os.path.exists(so):
         print(json.dumps(None))
@@ -176,8 +180,8 @@ def main():
     host_cpus = len(os.sched_getaffinity(0))
     cores = a.cores or min(16, host_cpus)
     with mp.get_context("fork").Pool(cores) as pool:
-        res = pool.map(worker, [(w, a.build, a.budget, a.reads) for w in range(cores)])
-    from gmapdp.workload import GENOME_PER_READ as genome_per_read
+        res = pool.map(worker, [(w, a.build, a.budget, a.reads, a.mix) for w in range(cores)])
+    genome_per_read = shape.genome
     total = sum(r["reads_per_s"] for r in res)
     maxent_total = sum(r["host_maxent_reads_per_s"] for r in res)
     calls = {k: sum(r["calls"][k] for r in res) for k in res[0]["calls"]}
@@ -192,10 +196,11 @@ def main():
                                 "fills, reference Maxent_hr_*_prob) on the same cores: the ceiling it puts on a "
                                 "pipeline that feeds the GPU bench's calls from host probabilities"},
         "sample": "%d worker processes x %.0f s of timed reference calls (%s) on the configs[2] per-read mix "
-                  "(1 Stage2_compute call + %.1f single + %.1f end + %.1f genome-gap + %.1f microexon calls per read) "
-                  "cut from a chr22-length i.i.d. genome; per-read time composed from per-call averages"
-                  % (cores, a.budget, ", ".join("%d %s" % (v, k) for k, v in calls.items()), 43.7, 13.6, 49.4,
-                     25.6)}))
+                  "(%s: %.3g Stage2_compute calls over locus +- %d-nt windows + %.1f single + %.1f end + %.1f "
+                  "genome-gap + %.1f microexon calls per read) cut from a chr22-length i.i.d. genome; per-read time "
+                  "composed from per-call averages"
+                  % (cores, a.budget, ", ".join("%d %s" % (v, k) for k, v in calls.items()), shape.source,
+                     shape.stage2, shape.pad, shape.single, shape.end5 + shape.end3, shape.genome, shape.microexon)}))
 
 
 if __name__ == "__main__":

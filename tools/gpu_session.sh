@@ -4,6 +4,7 @@
 #   tests          the whole -m gpu suite
 #   tests:<k>      the -m gpu tests matching -k <k>
 #   bench:<lib>    bench.py --steps 20 --no-cpu-baseline with gmap-2024_amd/<lib>/libgmapdp.so
+#   bx:<tag>:<args>  bench.py --steps 10 --no-cpu-baseline <args> -> bx_<tag>.json
 #   benchfull      bench.py as the driver runs it (CPU baseline included)
 #   simd:<lib>     bench.py --simd;  c4:<lib>  bench.py --config 4
 #   iso:<kernel>   tools/profile.sh <tag>_iso iso <kernel>  (the dominant kernel's launches alone)
@@ -26,6 +27,7 @@ for S in "$@"; do
     bench:*) L=${S#bench:}; GMAPDP_LIB=$PWD/gmap-2024_amd/$L/libgmapdp.so timeout -k 10 400 python bench.py --steps 20 --no-cpu-baseline > $O/bench_$L.json 2> $O/bench_$L.err || exit 13 ;;
     simd:*) L=${S#simd:}; GMAPDP_LIB=$PWD/gmap-2024_amd/$L/libgmapdp.so timeout -k 10 400 python bench.py --steps 20 --simd --no-cpu-baseline > $O/simd_$L.json 2> $O/simd_$L.err || exit 14 ;;
     c4:*) L=${S#c4:}; GMAPDP_LIB=$PWD/gmap-2024_amd/$L/libgmapdp.so timeout -k 10 600 python bench.py --steps 10 --config 4 --no-cpu-baseline > $O/c4_$L.json 2> $O/c4_$L.err || exit 15 ;;
+    bx:*) X=${S#bx:}; T=${X%%:*}; A=${X#*:}; timeout -k 10 600 python bench.py --steps 10 --no-cpu-baseline $A > $O/bx_$T.json 2> $O/bx_$T.err || exit 23 ;;
     benchfull) timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err || exit 16 ;;
     iso:*) bash tools/profile.sh ${TAG}_iso iso "${S#iso:}" > $O/prof_iso.txt 2>&1 || exit 17 ;;
     prof) bash tools/profile.sh $TAG > $O/prof.txt 2>&1 || exit 18 ;;
