@@ -341,13 +341,32 @@ struct Part {
 // owns bits [j*S, j*S+S) of each word).
 // STORE: also write the stored score of every band cell, smat[c * W + k] (the `matrix` that
 // Dynprog_cdna_gap's bridge reads at arbitrary cells).
-template <int R, bool CARRY, int S = 64, bool PK = (S < 64), bool STORE = false>
+// Direction words packed for a band of W <= 64 lanes (DPK, the genome-gap kernel's LDS planes): per column
+// the low 32 bits of the four ballots (one 16-byte record, dirs[4c + t]) and, in a second region after all
+// columns (hi = dirs + 4 (glen + 1)), the ballots' bits 32.. W-1: gg_dir_nhigh(W) words per column, plane t's
+// bits from bit t * 8 * nhigh.  16 + 4 nhigh bytes per column instead of 32.
+__host__ __device__ inline int gg_dir_nhigh(int W) { return W <= 32 ? 0 : W <= 40 ? 1 : W <= 48 ? 2 : 4; }
+struct PackedDirs {
+  const uint32_t* lo;
+  const uint32_t* hi;
+  int W, uband, nhigh;
+  __device__ uint32_t operator()(int c, int t, int r) const {
+    const int k = r - c + uband;
+    if (k < 0 || k >= W) return 0u;  // outside the band: cleared to DIAG (dynprog.c:498)
+    if (k < 32) return (lo[4 * c + t] >> k) & 1u;
+    const int b = t * 8 * nhigh + (k - 32);
+    return (hi[c * nhigh + (b >> 5)] >> (b & 31)) & 1u;
+  }
+};
+
+template <int R, bool CARRY, int S = 64, bool PK = (S < 64), bool STORE = false, bool DPK = false>
 __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lband, int uband, int open, int ext,
                                           int late, int track, const int8_t* sc, int srow, const uint8_t* gcl,
                                           uint64_t* dirs, const BridgeCarry* bc_, int& bestr, int& bestc,
                                           int gmax = 0, int* smat = nullptr, int* best_score = nullptr) {
   static_assert(S == 64 || (R == 1 && !CARRY), "segmented fills are single-word, no bridge carry");
   static_assert(!STORE || S == 64, "score matrices are stored by whole-wave fills only");
+  static_assert(!DPK || (R == 1 && S == 64), "packed direction words: one-word bands");
   const int lk = (S == 64) ? lane : (lane & (S - 1));  // lane within the segment
   const int cend = (S == 64) ? glen : gmax;
   const int sat = kNegInf32;
@@ -519,6 +538,23 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
 #ifdef GMAPDP_GGX_NODIRS
     if (!CARRY)  // timing experiment only (make variant): the genome-gap fills store no directions
 #endif
+    if constexpr (DPK) {
+      if (lane == 0) {
+        uint32_t* lo = reinterpret_cast<uint32_t*>(dirs);
+        *reinterpret_cast<uint4*>(lo + 4 * c) = make_uint4((uint32_t)mH[0], (uint32_t)mV[0], (uint32_t)mE[0], (uint32_t)mF[0]);
+        const int nh = gg_dir_nhigh(W);
+        uint32_t* hi = lo + 4 * (glen + 1) + nh * c;
+        const uint32_t h0 = (uint32_t)(mH[0] >> 32), h1 = (uint32_t)(mV[0] >> 32), h2 = (uint32_t)(mE[0] >> 32),
+                       h3 = (uint32_t)(mF[0] >> 32);
+        if (nh == 1) {
+          hi[0] = (h0 & 0xffu) | ((h1 & 0xffu) << 8) | ((h2 & 0xffu) << 16) | (h3 << 24);
+        } else if (nh == 2) {
+          *reinterpret_cast<uint2*>(hi) = make_uint2((h0 & 0xffffu) | (h1 << 16), (h2 & 0xffffu) | (h3 << 16));
+        } else if (nh == 4) {
+          *reinterpret_cast<uint4*>(hi) = make_uint4(h0, h1, h2, h3);
+        }
+      }
+    } else
     if (lane == 0) {  // one lane stores the column's 4R direction words
       uint64_t* dcol = dirs + (size_t)c * 4 * R;
 #pragma unroll

@@ -641,11 +641,15 @@ struct ScratchGG {
 };
 
 __host__ __device__ inline size_t gg_dirs_bytes(int glength, int R) { return (size_t)(glength + 1) * 4u * (size_t)R * 8u; }
+// LDS direction planes of a one-word band (PackedDirs): 16 + 4 nhigh bytes per column
+__host__ __device__ inline size_t gg_dirs_bytes_packed(int glength, int W) {
+  return (size_t)(glength + 1) * (16u + 4u * (size_t)gg_dir_nhigh(W));
+}
 
 // LDS: per query row one word of 4-bit scores per side (as the packed kernel), genome classes,
 // dinucleotide codes and splice probabilities per column; the query stays in HBM and genome
 // characters derive from the classes.
-__host__ __device__ inline CarveGG carve_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds) {
+__host__ __device__ inline CarveGG carve_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds, int W = 64) {
   CarveGG cv;
   size_t off = 0;
   cv.pL = off;    off = align16(off + 8u * (size_t)glengthL);
@@ -659,9 +663,9 @@ __host__ __device__ inline CarveGG carve_gg(int rlength, int glengthL, int gleng
   cv.isc = off;   off = align16(off + 64);
   cv.flag = off;  off = align16(off + 4);
   cv.dirsL = cv.dirsR = 0;
-  if (dirs_lds) {
-    cv.dirsL = off; off = align16(off + gg_dirs_bytes(glengthL, R));
-    cv.dirsR = off; off = align16(off + gg_dirs_bytes(glengthR, R));
+  if (dirs_lds) {  // one-word bands keep them packed (W: the wider side's band)
+    cv.dirsL = off; off = align16(off + (R == 1 ? gg_dirs_bytes_packed(glengthL, W) : gg_dirs_bytes(glengthL, R)));
+    cv.dirsR = off; off = align16(off + (R == 1 ? gg_dirs_bytes_packed(glengthR, W) : gg_dirs_bytes(glengthR, R)));
   }
   cv.total = off;
   return cv;
@@ -711,7 +715,8 @@ __global__ __launch_bounds__(128) GGX_ATTR void gg_kernel(
   const int late = (flags & kFLate) ? 1 : 0;
   const int lband = P.lbandL, ubandL = P.ubandL, ubandR = P.ubandR;
   const int WL = lband + ubandL + 1, WR = lband + ubandR + 1;
-  const CarveGG cv = carve_gg(rlen, gL, gR, R, DIRS_LDS);
+  constexpr bool DPK = DIRS_LDS && R == 1;  // packed LDS direction planes (PackedDirs)
+  const CarveGG cv = carve_gg(rlen, gL, gR, R, DIRS_LDS, WL > WR ? WL : WR);
   const ScratchGG sv = scratch_gg(rlen, gL, gR, R, DIRS_LDS);
   unsigned char* gbase = gscratch + P.dirs_offset;
   double* pL = reinterpret_cast<double*>(smem + cv.pL);
@@ -874,12 +879,12 @@ __global__ __launch_bounds__(128) GGX_ATTR void gg_kernel(
     int br, bc;
     if (wave == 0) {
       const BridgeCarry B{ldi, rdi, pL, pR, isc, rdist, partB, diagR};
-      fill_band<R, true, 64, true>(lane, rlen, gR, lband, ubandR, P.open, P.extend, 1 - late, 0,
-                                   reinterpret_cast<const int8_t*>(scR), 0, gclR, dirsR, &B, br, bc);
+      fill_band<R, true, 64, true, false, DPK>(lane, rlen, gR, lband, ubandR, P.open, P.extend, 1 - late, 0,
+                                               reinterpret_cast<const int8_t*>(scR), 0, gclR, dirsR, &B, br, bc);
     } else {
       const BridgeCarry B{rdi, ldi, pR, pL, isc, rdist, partC, diagL};
-      fill_band<R, true, 64, true>(lane, rlen, gL, lband, ubandL, P.open, P.extend, late, 0,
-                                   reinterpret_cast<const int8_t*>(scL), 0, gclL, dirsL, &B, br, bc);
+      fill_band<R, true, 64, true, false, DPK>(lane, rlen, gL, lband, ubandL, P.open, P.extend, late, 0,
+                                               reinterpret_cast<const int8_t*>(scL), 0, gclL, dirsL, &B, br, bc);
     }
   }
   __threadfence_block();
@@ -996,16 +1001,30 @@ __global__ __launch_bounds__(128) GGX_ATTR void gg_kernel(
   const int new_left = P.goffsetL + (bestcL - 1);
   const int new_right = P.rev_goffsetR - (bestcR - 1);
   Tally t = {0, 0, 0, 0, 0, 0, 0, false};
-  traceback_band<R>(lane, dirsR, WR, ubandR, bestrR, bestcR, GR, qR, qucR, gchR, cons, watson, P.chroffset,
-                    P.chrhigh, blocks, nwords, out, t);
+  if constexpr (DPK) {
+    const uint32_t* lo = reinterpret_cast<const uint32_t*>(dirsR);
+    const PackedDirs dR{lo, lo + 4 * (gR + 1), WR, ubandR, gg_dir_nhigh(WR)};
+    traceback_walk(lane, dR, bestrR, bestcR, GR, qR, qucR, gchR, cons, watson, P.chroffset, P.chrhigh, blocks, nwords,
+                   out, t);
+  } else {
+    traceback_band<R>(lane, dirsR, WR, ubandR, bestrR, bestcR, GR, qR, qucR, gchR, cons, watson, P.chroffset,
+                      P.chrhigh, blocks, nwords, out, t);
+  }
   const int nR = t.count;
   reverse_records(lane, out, nR);
   GG_MARK(5);
   const int queryjump = (rev_roffset - bestrR) - (P.roffset + bestrL) + 1;
   if (lane == 0) put_pair(out, nR, -1, -1, new_right - new_left - 1, ' ', ' ', ' ', ' ');
   t.count += 1;
-  traceback_band<R>(lane, dirsL, WL, ubandL, bestrL, bestcL, GL, qL, qucL, gchL, cons, watson, P.chroffset,
-                    P.chrhigh, blocks, nwords, out, t);
+  if constexpr (DPK) {
+    const uint32_t* lo = reinterpret_cast<const uint32_t*>(dirsL);
+    const PackedDirs dL{lo, lo + 4 * (gL + 1), WL, ubandL, gg_dir_nhigh(WL)};
+    traceback_walk(lane, dL, bestrL, bestcL, GL, qL, qucL, gchL, cons, watson, P.chroffset, P.chrhigh, blocks, nwords,
+                   out, t);
+  } else {
+    traceback_band<R>(lane, dirsL, WL, ubandL, bestrL, bestcL, GL, qL, qucL, gchL, cons, watson, P.chroffset,
+                      P.chrhigh, blocks, nwords, out, t);
+  }
   GG_MARK(6);
   int npairs = t.count;
   int score = t.score + t.nmatches * kMatch + t.nmismatches * kMismatch;
@@ -1141,8 +1160,8 @@ hipError_t launch_sx(int B, int nproblems, int slot, long long wave_dirs_bytes, 
 template <int R, bool D>
 static void* gptr() { return reinterpret_cast<void*>(&gg_kernel<R, D>); }
 
-size_t lds_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds) {
-  return carve_gg(rlength, glengthL, glengthR, R, dirs_lds).total;
+size_t lds_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds, int W) {
+  return carve_gg(rlength, glengthL, glengthR, R, dirs_lds, W).total;
 }
 size_t scratch_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds) {
   return scratch_gg(rlength, glengthL, glengthR, R, dirs_lds).total;

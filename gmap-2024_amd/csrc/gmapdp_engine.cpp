@@ -45,7 +45,7 @@ hipError_t launch_dpx(int S, int nproblems, int slot, int dirs_bytes, unsigned c
                       const DevProblem* probs, const int* order, const uint32_t* blocks, uint64_t nwords,
                       const char* qseq, const char* qseq_uc, const int8_t* sctab, const uint8_t* constab,
                       gmapdp_result* results, gmapdp_pair* pairs);
-size_t lds_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds);
+size_t lds_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds, int W);
 size_t scratch_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds);
 hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevGenomeProblem* probs,
                      const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
@@ -747,10 +747,7 @@ static size_t env_size(const char* name, size_t dflt) {
 // genome-gap direction planes stay in LDS while the workgroup's LDS stays within this; by default
 // they always go to the L2-resident scratch, which measured fastest (more problems per CU).
 // GMAPDP_GG_LDS_DIRS_MAX overrides it, for experiments.
-static size_t gg_lds_dirs_max() {
-  static const size_t v = env_size("GMAPDP_GG_LDS_DIRS_MAX", 0);
-  return v;
-}
+static size_t gg_lds_dirs_max() { return env_size("GMAPDP_GG_LDS_DIRS_MAX", 0); }
 // GMAPDP_DP_ROWS=0 keeps every single / end gap in the band layout (experiments, tests)
 static bool rows_disabled() {
   static const bool v = env_size("GMAPDP_DP_ROWS", 1) == 0;
@@ -1107,9 +1104,9 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     const int WL = d.lbandL + d.ubandL + 1, WR = d.lbandL + d.ubandR + 1;
     const int R = pick_R(std::max(WL, WR));
     if (R > kMaxR) return bad(ctx, "band wider than 4096");
-    size_t lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, true);
+    size_t lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, true, std::max(WL, WR));
     const bool dirs_lds = lds <= gg_lds_dirs_max();
-    if (!dirs_lds) lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, false);
+    if (!dirs_lds) lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, false, std::max(WL, WR));
     d.dirs_offset = (int64_t)gdirs_off;  // bridge candidates (+ direction planes) in global scratch
     gdirs_off += (scratch_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, dirs_lds) + 255) & ~(size_t)255;
     if (lds > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
@@ -2284,13 +2281,18 @@ static void oligo_plan_free(gmapdp_oligo_plan* p) {
 }
 
 // Cut the launch-ordered problems into chunks and lay out each chunk's scratch (main region, then the
-// sequential walk's region when `fallback`) and pool.  slots[i]: pool slots problem i may take.
-static void oligo_layout(gmapdp_oligo_plan* P, const std::vector<size_t>& slots, bool fallback) {
+// sequential walk's region when `fallback`) and pool, and the table and diagonal arenas: slots[i], tcap[i],
+// dcap[i] are what problem i may take of each.  `local`: the arenas too restart at 0 in every chunk (a
+// sizing run, whose outputs are only its counts), else they are laid out over the whole plan.
+static void oligo_layout(gmapdp_oligo_plan* P, const std::vector<size_t>& slots, bool fallback,
+                         const std::vector<size_t>& tcap, const std::vector<size_t>& dcap, bool local) {
   P->launches.clear();
   P->umax.clear();
   P->scratch_cap = 0;
   P->pool_cap = 0;
-  size_t cb = 0, cs = 0;
+  P->table_cap = 0;
+  P->diag_cap = 0;
+  size_t cb = 0, cs = 0, ct = 0, cd = 0;
   int first = 0;
   auto close = [&](int end) {
     if (end > first) {
@@ -2298,9 +2300,12 @@ static void oligo_layout(gmapdp_oligo_plan* P, const std::vector<size_t>& slots,
       P->umax.push_back(P->keys[first]);
       P->scratch_cap = std::max(P->scratch_cap, cb);
       P->pool_cap = std::max<unsigned long long>(P->pool_cap, cs);
+      P->table_cap = std::max(P->table_cap, ct);
+      P->diag_cap = std::max(P->diag_cap, cd);
     }
     first = end;
     cb = cs = 0;
+    if (local) ct = cd = 0;
   };
   for (int k = 0; k < (int)P->ord.size(); k++) {
     DevOligoProblem& d = P->ord[k];
@@ -2311,8 +2316,12 @@ static void oligo_layout(gmapdp_oligo_plan* P, const std::vector<size_t>& slots,
       close(k);
     d.scratch_offset = (int64_t)cb;
     d.fallback_offset = fallback ? (int64_t)(cb + mb) : -1;
+    d.table_offset = (int64_t)ct;
+    d.diag_offset = (int64_t)cd;
     cb += mb + fb;
     cs += slots[d.index];
+    ct += tcap[d.index];
+    cd += dcap[d.index];
   }
   close((int)P->ord.size());
 }
@@ -2347,15 +2356,15 @@ static hipError_t oligo_buffers(gmapdp_ctx* ctx, gmapdp_oligo_plan* P) {
 }
 
 static int oligo_plan_build(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problems, int n, const char* qseq_uc,
-                            size_t qbytes, gmapdp_oligo_plan** plan, bool borrow) {
+                            size_t qbytes, gmapdp_oligo_plan** plan, bool borrow, bool sizing = false) {
   if (!ctx || !plan || n < 0 || (n > 0 && (!problems || !qseq_uc))) return GMAPDP_EINVAL;
   *plan = nullptr;
   if (!ctx->d_genome) return GMAPDP_ENOGENOME;
   (void)hipSetDevice(ctx->device);
   std::vector<uint32_t> bm(2048, 0u);
   std::vector<DevOligoProblem> dev(n);
-  std::vector<size_t> slots(n);
-  size_t toff = 0, doff = 0;
+  std::vector<size_t> slots(n), tcap(n), dcap(n);
+  size_t toff = 0;
   static const int kBuckets[] = {1024, 2048, 4096, 8192, 16384};  // launch classes by LDS
   std::map<int, std::vector<int>> classes;
   const char* ev = std::getenv("GMAPDP_OLIGO_POOL_SLOTS");  // tests: a small pool forces the sequential walk
@@ -2386,21 +2395,17 @@ static int oligo_plan_build(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problem
     d.minor = p.minor ? 1 : 0;
     d.umax = umax;
     d.index = i;
-    d.table_offset = (int64_t)toff;
-    d.diag_offset = (int64_t)doff;
-    toff += oligo_table_cap(p);
-    doff += oligo_diag_cap(p);
+    tcap[i] = oligo_table_cap(p);
+    dcap[i] = oligo_diag_cap(p);
+    toff += tcap[i];
     // hits ~ the query's 8-mers once (the locus) plus the window's random matches (4^-8 per position each)
     const size_t est = (size_t)p.querylength * (2 + (size_t)(win >> 15)) + 256;
     slots[i] = 3 * std::min<size_t>(oligo_table_cap(p), est);
     // launch class: (umax, 32-bit counters); 16-bit counters when no count can reach 2^16
     classes[2 * umax + (win >= 65536 ? 1 : 0)].push_back(i);
   }
-  if (toff > 0x7fffffffull) return bad(ctx, "stage-2 table arena beyond 2^31 entries");
   gmapdp_oligo_plan* P = new gmapdp_oligo_plan();
   P->n = n;
-  P->table_cap = toff;
-  P->diag_cap = doff;
   P->borrowed = borrow;
   P->ord.reserve(n);
   for (auto& kv : classes)
@@ -2408,7 +2413,13 @@ static int oligo_plan_build(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problem
       P->ord.push_back(dev[i]);
       P->keys.push_back(kv.first);
     }
-  oligo_layout(P, slots, true);
+  oligo_layout(P, slots, true, tcap, dcap, sizing);
+  // mappings index the table with 32-bit offsets (a sizing run's restart in every chunk)
+  if (P->table_cap > 0x7fffffffull) {
+    oligo_plan_free(P);
+    return bad(ctx, "stage-2 table arena beyond 2^31 entries");
+  }
+  (void)toff;
   if (ev) P->pool_cap = std::strtoull(ev, nullptr, 10);  // per chunk
   const hipError_t e = oligo_buffers(ctx, P);
   if (e != hipSuccess) {
@@ -2426,24 +2437,15 @@ static int oligo_plan_build(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problem
 static hipError_t oligo_plan_relayout(gmapdp_ctx* ctx, gmapdp_oligo_plan* P, const gmapdp_oligo_problem* problems,
                                       const gmapdp_oligo_result* ores) {
   const int n = P->n;
-  std::vector<int64_t> toffs(n), doffs(n);
-  std::vector<size_t> slots(n);
-  size_t t = 0, dd = 0;
+  std::vector<size_t> slots(n), tcap(n), dcap(n);
   for (int i = 0; i < n; i++) {
-    toffs[i] = (int64_t)t;
-    doffs[i] = (int64_t)dd;
     const size_t tp = (size_t)std::max(ores[i].totalpositions, 0);
-    t += std::min<size_t>(oligo_table_cap(problems[i]), tp);
-    dd += (size_t)std::max(ores[i].ndiagonals, 0);
+    tcap[i] = std::min<size_t>(oligo_table_cap(problems[i]), tp);
+    dcap[i] = (size_t)std::max(ores[i].ndiagonals, 0);
     slots[i] = 3 * tp;
   }
-  for (DevOligoProblem& d : P->ord) {
-    d.table_offset = toffs[d.index];
-    d.diag_offset = doffs[d.index];
-  }
-  P->table_cap = t;
-  P->diag_cap = dd;
-  oligo_layout(P, slots, false);
+  oligo_layout(P, slots, false, tcap, dcap, false);
+  if (P->table_cap > 0x7fffffffull) return hipErrorInvalidValue;  // 32-bit mappings
   return oligo_buffers(ctx, P);
 }
 
@@ -3253,7 +3255,7 @@ int gmapdp_stage2_plan_create(gmapdp_ctx* ctx, const gmapdp_stage2_problem* prob
   gmapdp_stage2_plan* P = new gmapdp_stage2_plan();
   P->n = n;
   P->qbytes = qbytes;
-  int rc = gmapdp_oligo_plan_create(ctx, op.data(), n, qseq_uc, qbytes, &P->oplan);
+  int rc = oligo_plan_build(ctx, op.data(), n, qseq_uc, qbytes, &P->oplan, false, /*sizing*/ true);
   if (rc) {
     delete P;
     return rc;

@@ -70,6 +70,31 @@ def test_gpu_genome_gap_matches_oracle_random(engine, seed):
     assert d is None, _msg(probs, d, "oracle")
 
 
+@pytest.mark.parametrize("lds_dirs", ["0", "163840"])
+def test_gpu_genome_gap_direction_planes_global_and_lds(engine, monkeypatch, lds_dirs):
+    """Both placements of the fills' direction planes: L2-resident scratch (4 x 64-bit ballots per column)
+    and LDS (GMAPDP_GG_LDS_DIRS_MAX: one-word bands packed to 16 + 4 nhigh bytes per column, PackedDirs),
+    with bands of every packed width class (W <= 32, <= 40, <= 48, <= 64) and wider ones."""
+    monkeypatch.setenv("GMAPDP_GG_LDS_DIRS_MAX", lds_dirs)
+    rng = random.Random(3100)
+    g = bytearray(random_genome(rng, 120000))
+    probs = []
+    for i in range(2400):
+        p = genome_gap_problem(rng, g, edge=(i % 5 == 0))
+        if i % 3 == 0:  # vary the band: extraband 2..30 (W = |g - r| + 2 extraband + 1)
+            p["extraband"] = rng.randint(2, 30)
+        probs.append(p)
+    g = bytes(g)
+    engine.set_genome(g)
+    orc = Oracle()
+    orc.set_genome(g)
+    sp = [_synthetic_probs(rng, p) for p in probs]
+    got = engine.genome_gap_batch(probs, sp)
+    exp = [orc.genome_gap(p, lp, rp) for p, (lp, rp) in zip(probs, sp)]
+    d = _first_diff(got, exp)
+    assert d is None, _msg(probs, d, "oracle")
+
+
 @pytest.mark.skipif(not ref_available("nosimda"), reason="reference objects did not travel")
 def test_gpu_genome_gap_matches_reference_objects(engine):
     rng = random.Random(79)

@@ -63,7 +63,8 @@ def main_s2(reads=10000):
     genome = W.make_genome(layout, seed=22)
     eng = gmapdp.Engine(0)
     eng.set_genome(genome.tobytes())
-    op, oq = W.make_stage2(genome, layout, reads, np.random.default_rng(3000))
+    sh = W.CDNA2K  # the bench's configs[2] read shape and stage-2 windows (gmap -d: locus +- ~100 kb)
+    op, oq = W.make_stage2(genome, layout, reads, np.random.default_rng(3000), pad=sh.pad, extra=sh.stage2 - 1.0)
     calls = [dict(quc=oq[int(p["qoff"]):int(p["qoff"]) + int(p["querylength"])].tobytes(),
                   **{k: int(p[k]) for k in ("chrstart", "chrend", "chroffset", "chrhigh", "plusp")}) for p in op]
     probs, qb, qub = eng.build_stage2_batch(calls)
@@ -116,7 +117,8 @@ def main():
     genome = W.make_genome(layout, seed=22)
     eng = gmapdp.Engine(0)
     eng.set_genome(genome.tobytes())
-    op, oq = W.make_stage2(genome, layout, n, np.random.default_rng(3000))
+    sh = W.CDNA2K
+    op, oq = W.make_stage2(genome, layout, n, np.random.default_rng(3000), pad=sh.pad, extra=sh.stage2 - 1.0)
     qb = oq.tobytes()
     res = eng.oligo_mappings_batch_raw(op, qb)
     marks = np.zeros(32, dtype=np.uint64)
