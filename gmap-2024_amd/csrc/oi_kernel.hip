@@ -511,25 +511,29 @@ __global__ __launch_bounds__(64) void oi_kernel(
         w0 = half_word(blocks, hb + 64 + lane);
         w1 = half_word(blocks, hb + 64 + lane + 1);
       }
-      int id[16];
+      // membership first (one bitmap word each); the id (rank within the bitmap) only for the ~3 % of
+      // 8-mers that hit, so the rank table is read by the hit lanes alone
       uint32_t hm = 0;
 #pragma unroll
       for (int j = 0; j < 16; j++) {
         const uint64_t p = 16 * h + j;
         const uint32_t x = (uint32_t)(v >> (2 * j)) & 0xFFFFu;
-        bool in;
-        id[j] = oligo_id(bitmap, wrank, P.plusp ? oligo_fwd(x) : (~x & 0xFFFFu), in);
+        const uint32_t m = P.plusp ? oligo_fwd(x) : (~x & 0xFFFFu);
+        const bool in = (bitmap[m >> 5] >> (m & 31)) & 1u;
         if (in && h <= hhi && p >= left && p <= lpl) hm |= 1u << j;
       }
-#pragma unroll
-      for (int j = 0; j < 16; j++)
-        if ((hm >> j) & 1u) count_inc(cnt, id[j]);
       const int c = __popc(hm);
       const int incl = wave_scan_add(lane, c);
       int o = nhits + incl - c;
-#pragma unroll
-      for (int j = 0; j < 16; j++)
-        if ((hm >> j) & 1u) hitlist[o++] = make_uint2((uint32_t)(16 * h + j - left), (uint32_t)id[j]);
+      for (uint32_t r = hm; r; r &= r - 1) {
+        const int j = __ffs(r) - 1;
+        const uint32_t x = (uint32_t)(v >> (2 * j)) & 0xFFFFu;
+        const uint32_t m = P.plusp ? oligo_fwd(x) : (~x & 0xFFFFu);
+        bool in;
+        const int id = oligo_id(bitmap, wrank, m, in);
+        count_inc(cnt, id);
+        hitlist[o++] = make_uint2((uint32_t)(16 * h + j - left), (uint32_t)id);
+      }
       nhits += __builtin_amdgcn_readlane(incl, 63);
     }
   }

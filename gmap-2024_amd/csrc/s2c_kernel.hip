@@ -89,7 +89,7 @@ struct S2Path {
   uint32_t start, end;  // genomepos of the first and last pair of the converted list
 };
 struct S2Scratch {
-  size_t diff, run, off, minact, maxact, first, proc, diags, ord, tmp, hits, cand, keep, paths, pq, ph, sbuf, total;
+  size_t diff, run, off, minact, maxact, first, proc, diags, ord, tmp, hits, cand, keep, paths, pq, ph, sbuf, lk, total;
   int sortn;  // power of two >= every sorted array
 };
 __host__ __device__ inline int s2_pow2(int n) {
@@ -118,7 +118,8 @@ __host__ __device__ inline S2Scratch s2_scratch(int ql, int T, int nd) {
   s.ph = align16(s.pq + 4 * Q);
   s.sortn = s2_pow2((int)(H > D ? H : D));
   s.sbuf = align16(s.ph + 4 * Q);
-  s.total = align16(s.sbuf + 4 * (size_t)s.sortn);
+  s.lk = align16(s.sbuf + 4 * (size_t)s.sortn);  // the walk's link words and maps when they exceed the LDS
+  s.total = align16(s.lk + 8 * H);
   return s;
 }
 
@@ -583,38 +584,38 @@ __device__ __forceinline__ int s2_dloop_fast(S2W& W, const S2Pref& pf, int np, i
       fs = pf.h.score + 1;
     }
   }
-  uint64_t C = ballot(kind != 0);
-  int last_visited = kend;
-  bool stopped = false;
-  S2_TALLY(n_fast, 1);
-  while (C) {
-    const int j = __ffsll((long long)C) - 1;
-    C &= C - 1;
-    S2_TALLY(n_cand, 1);
-    const int fsj = __builtin_amdgcn_readlane(fs, j);
-    if (fsj > b.score) {
-      const S2HV u = s2_bcast(pf.h, j);
-      const int eq = __builtin_amdgcn_readlane(pf.q, j);
-      if (__builtin_amdgcn_readlane(kind, j) == 2) {
-        b.consec = 0;
-        b.tracei = ++W.tracectr;
-      } else {
-        const int g = (int)(position - u.map), qdj = q - eq;
-        const int diff = g > qdj ? g - qdj : qdj - g;
-        b.consec = (diff <= 0) ? u.consec + qdj : 0;
-        b.tracei = u.tracei;
-      }
-      b.root = u.root;
-      b.score = fsj;
-      b.pp = eq;
-      b.ph = u.hit;
-      if (b.consec >= kS2EnoughConsec) {
-        last_visited = j;
-        stopped = true;
-        break;
-      }
-    }
+  // The walk over the candidates in entry order keeps the first strictly better score each time and stops
+  // after an update whose consec reaches ENOUGH_CONSECUTIVE: the updates are the records of a prefix max
+  // seeded with the current score, the walk ends at the first record with such a consec, else the last
+  // record wins (one wave scan instead of a scalar step per candidate).
+  int cons = 0;
+  if (kind == 4) {
+    const int g = (int)(position - pf.h.map);
+    const int diff = g > qd ? g - qd : qd - g;
+    cons = (diff <= 0) ? pf.h.consec + qd : 0;
   }
+  const int fsv = kind != 0 ? fs : INT_MIN;
+  int pm = __shfl_up(wave_incl_max(fsv, kk), 1, 64);
+  if (kk == 0) pm = INT_MIN;
+  pm = max(pm, b.score);
+  const bool rec = kind != 0 && fsv > pm;
+  const uint64_t R = ballot(rec);
+  const uint64_t S = ballot(rec && cons >= kS2EnoughConsec);
+  S2_TALLY(n_fast, 1);
+  S2_TALLY(n_cand, __popcll(R));
+  int w = -1;
+  if (S) w = __ffsll((long long)S) - 1;
+  else if (R) w = 63 - __clzll((long long)R);
+  if (w >= 0) {
+    b.score = __builtin_amdgcn_readlane(fs, w);
+    b.consec = __builtin_amdgcn_readlane(cons, w);
+    b.root = __builtin_amdgcn_readlane(pf.h.root, w);
+    b.pp = __builtin_amdgcn_readlane(pf.q, w);
+    b.ph = __builtin_amdgcn_readlane(pf.h.hit, w);
+    b.tracei = __builtin_amdgcn_readlane(kind, w) == 2 ? ++W.tracectr : __builtin_amdgcn_readlane(pf.h.tracei, w);
+  }
+  const bool stopped = S != 0;
+  const int last_visited = stopped ? w : kend;
   if (use_f && kk <= last_visited && (skip || r1skip)) f = -1;
   if (stopped || kmax < 64) return 1;
   if (V) lt = __builtin_amdgcn_readlane(pf.h.tracei, 63 - __clzll((long long)V));  // every entry leaves its tracei
@@ -891,28 +892,28 @@ __device__ __forceinline__ void s2_mult(S2W& W, int q, int offq, int low, int hi
 struct S2Run {
   int score, consec, tracei, root, hit, q, cb, pushed, np;
 };
-__device__ __forceinline__ void s2_run_write(S2Hit* hits, int* alist, int lane, int off, uint32_t map, int qq,
-                                                       S2Run L, uint64_t Mm) {
+__device__ __forceinline__ void s2_run_write(S2Hit* hits, int* alist, int lane, int off, int hit, int prevhit,
+                                             uint32_t map, int qq, S2Run L, uint64_t Mm) {
   if (!((Mm >> lane) & 1ull)) return;
   const uint64_t below = Mm & ((1ull << lane) - 1ull);
   const int r = __popcll(below);
   const int pl = below ? 63 - __clzll((long long)below) : -1;  // the previous member's lane
   const int dq = qq - L.q;
-  S2Hit& x = hits[off];
+  S2Hit& x = hits[off + hit];
   x.consec = L.consec + dq;
   x.root = L.root;
   x.fpos = pl >= 0 ? L.cb + pl : L.q;
-  x.fhit = pl >= 0 ? 0 : L.hit;
+  x.fhit = pl >= 0 ? prevhit : L.hit;
   x.tracei = L.tracei;
   x.score = L.score + dq;
-  alist[off] = 0;
+  alist[off] = hit;
   const int sl = (L.pushed + r) & (kS2Ring - 1);
   s2_ring.map[sl] = map;
   s2_ring.score[sl] = L.score + dq;
   s2_ring.consec[sl] = L.consec + dq;
   s2_ring.tracei[sl] = L.tracei;
   s2_ring.root[sl] = L.root;
-  s2_ring.hit[sl] = 0;
+  s2_ring.hit[sl] = hit;
   const int ms = (L.np + r) & (kS2Meta - 1);
   s2_ring.eq[ms] = qq;
   s2_ring.en[ms] = 1;
@@ -948,8 +949,10 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
   uint32_t grand_map = 0;
   S2E last = {0, 0, 0, 0, false};
   // per-position metadata for the chunk [cb, cb + 64): npositions, off, minactive, maxactive, first map
-  int cb = -1, m_n = 0, m_off = 0;
-  uint32_t m_min = 0, m_max = 0, m_map0 = 0;
+  // and per position the hits inside [minactive, maxactive]: [m_low, m_high) (the hits ascend in chrpos, so
+  // two binary searches per lane), m_rmap the first of them
+  int cb = -1, m_n = 0, m_off = 0, m_low = 0, m_high = 0;
+  uint32_t m_min = 0, m_max = 0, m_map0 = 0, m_rmap = 0;
 #ifdef GMAPDP_OI_TIMING
   unsigned long long t_one = 0, t_mult = 0, t_tail = 0, t_meta = 0, t0c = 0;
 #define S2_T0() t0c = wall_clock64()
@@ -970,6 +973,28 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
       m_min = qq <= qend ? minact[qq] : 0u;
       m_max = qq <= qend ? maxact[qq] : 0u;
       m_map0 = m_n > 0 ? W.hits[m_off].map : 0u;
+      m_low = m_high = 0;
+      m_rmap = m_map0;
+      if (m_n == 1) {
+        m_low = m_map0 < m_min ? 1 : 0;
+        m_high = (m_low == 0 && m_map0 <= m_max) ? 1 : m_low;
+      } else if (m_n > 1 && qq <= qend) {
+        int lo = m_map0 < m_min ? 1 : 0, hi = m_n;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (W.hits[m_off + mid].map < m_min) lo = mid + 1;
+          else hi = mid;
+        }
+        int lo2 = lo, hi2 = m_n;
+        while (lo2 < hi2) {
+          const int mid = (lo2 + hi2) >> 1;
+          if (W.hits[m_off + mid].map <= m_max) lo2 = mid + 1;
+          else hi2 = mid;
+        }
+        m_low = lo;
+        m_high = lo2 > lo ? lo2 : lo;
+        if (m_high > m_low) m_rmap = W.hits[m_off + m_low].map;
+      }
     }
     const int j = q - cb;
     // A run on the last processed entry's diagonal.  When that entry has one active hit whose consecutive
@@ -986,7 +1011,7 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
       const int lcons = s2_u(s2_ring.consec[ls]);
       const uint32_t dg = lmap - (uint32_t)last.q;
       const int qq = cb + lane;
-      const bool one = m_n == 1 && m_map0 >= m_min && m_map0 <= m_max && m_map0 - (uint32_t)qq == dg;
+      const bool one = qq <= qend && m_high - m_low == 1 && m_rmap - (uint32_t)qq == dg;
       const uint64_t from_j = ~0ull << j;
       const uint64_t notE = ~ballot(qq <= qend && (m_n <= 0 || one)) & from_j;
       const int stop = notE ? __ffsll((long long)notE) - 1 : 64;
@@ -995,7 +1020,10 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
       if (Mm && lcons + (cb + __ffsll((long long)Mm) - 1 - last.q) >= kS2EnoughConsec) {
         const int lscore = s2_u(s2_ring.score[ls]), ltr = s2_u(s2_ring.tracei[ls]), lroot = s2_u(s2_ring.root[ls]),
                   lhit = s2_u(s2_ring.hit[ls]);
-        s2_run_write(W.hits, W.alist, lane, m_off, m_map0, qq, {lscore, lcons, ltr, lroot, lhit, last.q, cb, W.pushed, np}, Mm);
+        const uint64_t mb = Mm & ((1ull << lane) - 1ull);
+        const int prevhit = __shfl(m_low, mb ? 63 - __clzll((long long)mb) : 0, 64);
+        s2_run_write(W.hits, W.alist, lane, m_off, m_low, prevhit, m_rmap, qq,
+                     {lscore, lcons, ltr, lroot, lhit, last.q, cb, W.pushed, np}, Mm);
         if ((inrun >> lane) & 1ull) W.actn[qq] = (int)((Mm >> lane) & 1ull);
         const int cnt = __popcll(Mm);
         S2_TALLY(n_runs, 1);
@@ -1006,8 +1034,8 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
         if (lsc >= grand_score) {  // consec >= ENOUGH_CONSECUTIVE > EXON_DEFN
           grand_score = lsc;
           grand_q = lq;
-          grand_hit = 0;
-          grand_map = (uint32_t)__builtin_amdgcn_readlane((int)m_map0, ll);
+          grand_hit = __builtin_amdgcn_readlane(m_low, ll);
+          grand_map = (uint32_t)__builtin_amdgcn_readlane((int)m_rmap, ll);
         }
         const int loff = __builtin_amdgcn_readlane(m_off, ll);
         W.pushed += cnt;
@@ -1027,22 +1055,9 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
     const int offq = __builtin_amdgcn_readlane(m_off, j);
     const uint32_t mn = (uint32_t)__builtin_amdgcn_readlane((int)m_min, j);
     const uint32_t mx = (uint32_t)__builtin_amdgcn_readlane((int)m_max, j);
-    int low = 0, high = 0;
-    if (n == 1) {
-      const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)m_map0, j);
-      low = m0 < mn ? 1 : 0;
-      high = (low == 0 && m0 <= mx) ? 1 : low;
-    } else if (n > 1) {
-      int cl = 0, ch = 0;
-      for (int c0 = 0; c0 < n; c0 += 64) {
-        const int i = c0 + lane;
-        const uint32_t mp = i < n ? W.hits[offq + i].map : 0u;
-        cl += __popcll(ballot(i < n && mp < mn));
-        ch += __popcll(ballot(i < n && mp <= mx));
-      }
-      low = cl;
-      high = max(cl, ch);
-    }
+    (void)mn;
+    (void)mx;
+    int low = __builtin_amdgcn_readlane(m_low, j), high = __builtin_amdgcn_readlane(m_high, j);
     if (high - low >= kS2MaxNactive && nskipped <= kS2MaxSkipped) {
       if (lane == 0) W.actn[q] = 0;
       nskipped++;
@@ -1069,8 +1084,8 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
     int nact = 0;
     if (high - low == 1) {
       // one hit in the active range (the common case): everything stays in registers and LDS
-      const uint32_t position = (low == 0 && q == cb + j) ? (uint32_t)__builtin_amdgcn_readlane((int)m_map0, j)
-                                                          : W.hits[qoff + low].map;
+      const uint32_t position = (q == cb + j) ? (uint32_t)__builtin_amdgcn_readlane((int)m_rmap, j)
+                                              : W.hits[qoff + low].map;
       S2Best b = s2_one(W, q, position, np, last);
       int best_score = b.score > 0 ? b.score : 0;
       const bool have_best = b.score > 0;
@@ -1148,19 +1163,57 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
           if (B || !(Vm >> 63)) break;
         }
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        // Section A for every hit at once when the last entry's active hits are in the ring: both lists
+        // ascend, so hit i's adjacent hit is the first active one with map + adq >= its position (what
+        // s2_adj's frontier walk finds), by a binary search per lane
+        const bool par_adj = last.n > 0 && last.inring;
+        bool a_found = false;
+        S2HV a_u = {};
         int overall = 0, adjf = last.n > 0 ? 0 : -1;
-        for (int i = 0; i < nh; i++) {
-          const uint32_t position = (uint32_t)__builtin_amdgcn_readlane((int)cm, i);
-          S2HV u;
-          if (s2_adj(W, last, adjf, adq, position, u) && u.consec + adq > overall) overall = u.consec + adq;
+        if (par_adj) {
+          if (lane < nh) {
+            int lo = 0, hi = last.n;
+            while (lo < hi) {
+              const int mid = (lo + hi) >> 1;
+              if (s2_ring.map[(last.start + mid) & (kS2Ring - 1)] + (uint32_t)adq >= cm) hi = mid;
+              else lo = mid + 1;
+            }
+            if (lo < last.n) {
+              const int sl = (last.start + lo) & (kS2Ring - 1);
+              if (s2_ring.map[sl] + (uint32_t)adq == cm) {
+                a_found = true;
+                a_u.map = cm;
+                a_u.score = s2_ring.score[sl];
+                a_u.consec = s2_ring.consec[sl];
+                a_u.tracei = s2_ring.tracei[sl];
+                a_u.root = s2_ring.root[sl];
+                a_u.hit = s2_ring.hit[sl];
+              }
+            }
+          }
+          overall = max(wave_max_i(a_found ? a_u.consec + adq : 0), 0);
+        } else {
+          for (int i = 0; i < nh; i++) {
+            const uint32_t position = (uint32_t)__builtin_amdgcn_readlane((int)cm, i);
+            S2HV u;
+            if (s2_adj(W, last, adjf, adq, position, u) && u.consec + adq > overall) overall = u.consec + adq;
+          }
         }
+        const uint64_t a_mask = ballot(a_found);
         adjf = last.n > 0 ? 0 : -1;
         for (int i = 0; i < nh; i++) {
           const uint32_t position = (uint32_t)__builtin_amdgcn_readlane((int)cm, i);
           S2Best b;
           int maxseen;
           S2HV u;
-          if (s2_adj(W, last, adjf, adq, position, u)) {
+          bool adjacent;
+          if (par_adj) {
+            adjacent = (a_mask >> i) & 1ull;
+            if (adjacent) u = s2_bcast(a_u, i);
+          } else {
+            adjacent = s2_adj(W, last, adjf, adq, position, u);
+          }
+          if (adjacent) {
             b = {u.consec + adq, u.root, last.q, u.hit, u.score + adq, u.tracei};
             maxseen = maxadj;
           } else {
@@ -2024,10 +2077,13 @@ __global__ __launch_bounds__(64) void s2c_kernel(
   S2_MARK(5);
   // ---- traceback_one per selected cell: length and extent of the converted list ----
   // the links go to LDS first (coalesced loads), so the pointer chases run at LDS latency
+  // (in the call's scratch when they do not fit: a 214-kb window's 8 000+ hits, the wave walk then runs at
+  // L2 latency instead of one lane chasing ~2 000 global links per path)
   extern __shared__ uint32_t s2c_lds[];
-  uint32_t* llq = s2c_lds;
-  uint32_t* lmap = s2c_lds + kS2cCap;
-  const bool lds_walk = T <= kS2cCap && nq <= 65536;
+  const bool in_lds = T <= kS2cCap;
+  uint32_t* llq = in_lds ? s2c_lds : reinterpret_cast<uint32_t*>(S + so.lk);
+  uint32_t* lmap = in_lds ? s2c_lds + kS2cCap : reinterpret_cast<uint32_t*>(S + so.lk) + T;
+  const bool lds_walk = T <= (int)kS2NoPred && nq <= 65536;  // link words: 15-bit hit index, 16-bit querypos
   if (lds_walk && npaths > 0) {
     // four hits per lane per step: their loads, then their off[] gathers, overlap
     for (int b0 = lane; b0 < T; b0 += 256) {
@@ -2061,6 +2117,12 @@ __global__ __launch_bounds__(64) void s2c_kernel(
     }
   }
   wave_sync();
+#ifdef GMAPDP_OI_TIMING
+  if (threadIdx.x == 0) {
+    atomicAdd(&g_s2_marks[1][13], (unsigned long long)npaths);
+    atomicAdd(&g_s2_marks[1][14], (unsigned long long)wall_clock64());  // minus mark 5's time: the link table
+  }
+#endif
   // a single selected cell is the single result (Stage2_filter_unique keeps it): its walk records the
   // entries convert_to_nucleotides needs, and the second walk below is skipped
   const bool single = npaths == 1;

@@ -20,6 +20,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 
 def main():
@@ -33,6 +34,7 @@ def main():
     ap.add_argument("--configs", default="default:",
                     help="shim configurations for the GPU runs, 'name:VAR=V,VAR=V;name2:...' (environment overrides)")
     ap.add_argument("--skip-cpu", action="store_true")
+    ap.add_argument("--thread-cpu", action="store_true", help="per-thread-name CPU seconds of each run")
     a = ap.parse_args()
     import make_e2e as M
     genome = list(M.synth_genome())
@@ -67,7 +69,27 @@ def main():
                     "r.fa"]
             t0 = time.perf_counter()
             ru0 = resource.getrusage(resource.RUSAGE_CHILDREN)
-            r = subprocess.run(args, cwd=tmp, env=env, capture_output=True, text=True, timeout=1500)
+            threads = None
+            if a.thread_cpu:  # per-thread-name CPU seconds (fiber hosts, dispatchers, GMAP's own threads)
+                import collections
+                from thread_cpu import sample
+                seen = {}
+                p = subprocess.Popen(args, cwd=tmp, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+                import threading
+                res = {}
+                th = threading.Thread(target=lambda: res.update(zip(("out", "err"), p.communicate())))
+                th.start()
+                while th.is_alive():
+                    sample(p.pid, seen)
+                    time.sleep(0.2)
+                th.join()
+                agg = collections.defaultdict(float)
+                for name, secs in seen.values():
+                    agg[name] += secs
+                threads = {k: round(v, 2) for k, v in sorted(agg.items(), key=lambda kv: -kv[1])}
+                r = subprocess.CompletedProcess(args, p.returncode, res.get("out", ""), res.get("err", ""))
+            else:
+                r = subprocess.run(args, cwd=tmp, env=env, capture_output=True, text=True, timeout=1500)
             dt = time.perf_counter() - t0
             ru1 = resource.getrusage(resource.RUSAGE_CHILDREN)
             cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
@@ -77,7 +99,7 @@ def main():
             stats = [l for l in r.stderr.splitlines() if l.startswith("gmapdp shim calls")]
             out["runs"].append({"program": prog, "threads": t, "config": cname, "env": cenv, "seconds": dt, "reads_per_s": a.reads / dt,
                                 "cpu_seconds": cpu, "cpu_cores_busy": cpu / dt,
-                                "shim_calls": stats[0] if stats else None})
+                                "shim_calls": stats[0] if stats else None, "thread_cpu_s": threads})
             print(json.dumps(out["runs"][-1]), file=sys.stderr, flush=True)
     base = next(iter(sams.values())) if a.skip_cpu else sams[("gmap_%s" % a.build, min(cpu_t), "cpu")]
     out["outputs_identical"] = all(v == base for v in sams.values())

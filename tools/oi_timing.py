@@ -79,6 +79,9 @@ def main_s2(reads=10000):
     tot = sum(dur)
     s2c = {n: round(float(t[b] - t[a]) / 1e2 / max(int(c[0]), 1), 1)
            for n, a, b in (("cells_us", 12, 5), ("traceback_filter_us", 5, 6), ("convert_us", 6, 7))}
+    nw = max(int(c[5]), 1)  # s2c waves that reached the traceback (mark 5)
+    s2c["npaths_per_wave"] = round(float(marks[29]) / nw, 2)
+    s2c["link_table_us"] = round(float(marks[30] - t[5]) / 1e2 / nw, 1)
     cnt = {k: round(float(marks[i]) / 1e2 / max(int(c[0]), 1), 1)
            for k, i in (("sweep_meta_us", 8), ("sweep_one_us", 9), ("sweep_mult_us", 10), ("sweep_tail_us", 11))}
     wv = np.zeros((3, 16384), dtype=np.uint32)
