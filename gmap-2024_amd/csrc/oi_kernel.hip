@@ -499,42 +499,74 @@ __global__ __launch_bounds__(64) void oi_kernel(
   int nhits = 0;
   if (npos > 0) {
     const uint64_t hlo = left >> 4, hhi = lpl >> 4;
-    uint32_t w0 = 0, w1 = 0;
-    if (hlo + lane <= hhi) {
-      w0 = half_word(blocks, hlo + lane);
-      w1 = half_word(blocks, hlo + lane + 1);
+    // a window of ~200 kb is ~200 steps: the half-words of the next kOiAhead steps are in flight, so a
+    // step waits on an L2 / HBM round trip only at the start (one step ahead left every step waiting)
+    constexpr int kOiAhead = 4;
+    uint32_t pw0[kOiAhead], pw1[kOiAhead];
+#pragma unroll
+    for (int a = 0; a < kOiAhead; a++) {
+      const uint64_t hh = hlo + 64 * a + lane;
+      pw0[a] = hh <= hhi ? half_word(blocks, hh) : 0u;
+      pw1[a] = hh <= hhi ? half_word(blocks, hh + 1) : 0u;
     }
-    for (uint64_t hb = hlo; hb <= hhi; hb += 64) {
+    // one step: the lane's 16 8-mer starts of half-word h (v = half-words h, h + 1)
+    auto step = [&](uint64_t hb, uint64_t v) {
       const uint64_t h = hb + lane;
-      const uint64_t v = (uint64_t)w0 | ((uint64_t)w1 << 32);
-      if (hb + 64 + lane <= hhi) {  // prefetch the next step
-        w0 = half_word(blocks, hb + 64 + lane);
-        w1 = half_word(blocks, hb + 64 + lane + 1);
+      // the 8-mer at window offset j as its oligo: plus strand, first nt most significant (the 2-bit groups
+      // of the 32 nt reversed once, then m_j = bits 2 (24 - j) ..); minus strand, the complement as read
+      uint64_t vv;
+      if (P.plusp) {
+        vv = ((v >> 2) & 0x3333333333333333ull) | ((v & 0x3333333333333333ull) << 2);
+        vv = ((vv >> 4) & 0x0F0F0F0F0F0F0F0Full) | ((vv & 0x0F0F0F0F0F0F0F0Full) << 4);
+        vv = __builtin_bswap64(vv);
+      } else {
+        vv = ~v;
+      }
+      auto oligo_at = [&](int j) -> uint32_t {
+        return (uint32_t)(vv >> (P.plusp ? 2 * (24 - j) : 2 * j)) & 0xFFFFu;
+      };
+      // the starts of this half-word inside [left, lpl]: bits jlo .. jhi
+      uint32_t vmask = 0;
+      if (h <= hhi) {
+        const uint64_t p0 = 16 * h;
+        const int jlo = left > p0 ? (int)(left - p0) : 0;
+        const int jhi = lpl < p0 + 15 ? (int)(lpl - p0) : 15;
+        if (jlo <= jhi) vmask = (0xFFFFu >> (15 - jhi)) & (0xFFFFu << jlo);
       }
       // membership first (one bitmap word each); the id (rank within the bitmap) only for the ~3 % of
       // 8-mers that hit, so the rank table is read by the hit lanes alone
       uint32_t hm = 0;
 #pragma unroll
       for (int j = 0; j < 16; j++) {
-        const uint64_t p = 16 * h + j;
-        const uint32_t x = (uint32_t)(v >> (2 * j)) & 0xFFFFu;
-        const uint32_t m = P.plusp ? oligo_fwd(x) : (~x & 0xFFFFu);
-        const bool in = (bitmap[m >> 5] >> (m & 31)) & 1u;
-        if (in && h <= hhi && p >= left && p <= lpl) hm |= 1u << j;
+        const uint32_t m = oligo_at(j);
+        hm |= ((bitmap[m >> 5] >> (m & 31)) & 1u) << j;
       }
+      hm &= vmask;
       const int c = __popc(hm);
       const int incl = wave_scan_add(lane, c);
       int o = nhits + incl - c;
       for (uint32_t r = hm; r; r &= r - 1) {
         const int j = __ffs(r) - 1;
-        const uint32_t x = (uint32_t)(v >> (2 * j)) & 0xFFFFu;
-        const uint32_t m = P.plusp ? oligo_fwd(x) : (~x & 0xFFFFu);
+        const uint32_t m = oligo_at(j);
         bool in;
         const int id = oligo_id(bitmap, wrank, m, in);
         count_inc(cnt, id);
         hitlist[o++] = make_uint2((uint32_t)(16 * h + j - left), (uint32_t)id);
       }
       nhits += __builtin_amdgcn_readlane(incl, 63);
+    };
+    // unrolled by kOiAhead so each slot is a fixed register pair and a step waits for its own loads only
+    for (uint64_t hb0 = hlo; hb0 <= hhi; hb0 += 64 * kOiAhead) {
+#pragma unroll
+      for (int a = 0; a < kOiAhead; a++) {
+        const uint64_t hb = hb0 + 64 * a;
+        if (hb > hhi) break;
+        const uint64_t v = (uint64_t)pw0[a] | ((uint64_t)pw1[a] << 32);
+        const uint64_t hh = hb + 64 * kOiAhead + lane;  // refill the slot with the step kOiAhead ahead
+        pw0[a] = hh <= hhi ? half_word(blocks, hh) : 0u;
+        pw1[a] = hh <= hhi ? half_word(blocks, hh + 1) : 0u;
+        step(hb, v);
+      }
     }
   }
   __syncthreads();

@@ -1934,6 +1934,68 @@ constexpr uint32_t kS2NoPred = 0x7fffu;
 struct S2WalkOut {
   int n, top, bottom;
 };
+// The same walk over the global hit arrays, for calls with more hits than the LDS link table holds (a
+// 214-kb window's random matches: ~4 hits per query position, so a path's nodes are not consecutive hit
+// indices and s2_walk_wave would advance one node per step).  A path mostly follows one diagonal through
+// consecutive query positions, so each step guesses the next 64 nodes there: lane k takes the hit of
+// position q - k with map - k (a binary search in that position's hits, which ascend), and the guesses
+// hold while each one is its predecessor's link (fpos, fhit); the walk goes on from the last holding
+// node's real link.  Same nodes, order and outputs as s2_walk.
+__device__ S2WalkOut s2_walk_diag(const S2Hit* hits, const int* off, int gi, int lane, int* pq, int* ph) {
+  S2WalkOut o = {0, -1, -1};
+  while (gi >= 0 && hits[gi].consec < kS2MinTerminal) {  // prune the 3' end
+    const int fq = hits[gi].fpos;
+    gi = fq >= 0 ? off[fq] + hits[gi].fhit : -1;
+  }
+  while (gi >= 0) {
+    const int qn = s2_u(hits[gi].q);
+    const uint32_t mn = s2_u(hits[gi].map);
+    const int p = qn - lane;
+    int idx = -1;
+    if (lane == 0) {
+      idx = gi;
+    } else if (p >= 0) {
+      const uint32_t target = mn - (uint32_t)lane;
+      int lo = off[p], hi = off[p + 1];
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (hits[mid].map < target) lo = mid + 1;
+        else hi = mid;
+      }
+      if (lo < off[p + 1] && hits[lo].map == target) idx = lo;
+    }
+    int pred = -1;
+    uint32_t mx = 0x80000000u;
+    int qx = 0;
+    if (idx >= 0) {
+      const S2Hit& x = hits[idx];
+      pred = x.fpos >= 0 ? off[x.fpos] + x.fhit : -1;
+      mx = x.map;
+      qx = x.q;
+    }
+    // node k holds when node k - 1 does and node k - 1's link is this guess
+    const int prev_pred = __shfl_up(pred, 1, 64);
+    const bool c = lane == 0 || (idx >= 0 && prev_pred == idx);
+    const uint64_t brk = ballot(!c);
+    const int len = brk ? __ffsll((long long)brk) - 1 : 64;  // nodes 0 .. len-1
+    const bool vis = lane < len && (int)mx >= 0;
+    const uint64_t vm = ballot(vis);
+    if (vis && pq) {
+      const int k = o.n + lanes_below(vm, lane);
+      pq[k] = qx;
+      ph[k] = (int)mx;
+    }
+    if (vm) {
+      const int f = __ffsll((long long)vm) - 1, l = 63 - __clzll((long long)vm);
+      if (o.top < 0) o.top = __builtin_amdgcn_readlane(idx, f);
+      o.bottom = __builtin_amdgcn_readlane(idx, l);
+    }
+    o.n += __popcll(vm);
+    gi = __builtin_amdgcn_readlane(pred, len - 1);
+  }
+  return o;
+}
+
 __device__ S2WalkOut s2_walk_wave(const uint32_t* lql, const uint32_t* map, int gi, int lane, int* pq, int* ph) {
   S2WalkOut o = {0, -1, -1};
   uint32_t w = lql[gi];
@@ -2080,10 +2142,9 @@ __global__ __launch_bounds__(64) void s2c_kernel(
   // (in the call's scratch when they do not fit: a 214-kb window's 8 000+ hits, the wave walk then runs at
   // L2 latency instead of one lane chasing ~2 000 global links per path)
   extern __shared__ uint32_t s2c_lds[];
-  const bool in_lds = T <= kS2cCap;
-  uint32_t* llq = in_lds ? s2c_lds : reinterpret_cast<uint32_t*>(S + so.lk);
-  uint32_t* lmap = in_lds ? s2c_lds + kS2cCap : reinterpret_cast<uint32_t*>(S + so.lk) + T;
-  const bool lds_walk = T <= (int)kS2NoPred && nq <= 65536;  // link words: 15-bit hit index, 16-bit querypos
+  uint32_t* llq = s2c_lds;
+  uint32_t* lmap = s2c_lds + kS2cCap;
+  const bool lds_walk = T <= kS2cCap && nq <= 65536;  // link words: 15-bit hit index, 16-bit querypos
   if (lds_walk && npaths > 0) {
     // four hits per lane per step: their loads, then their off[] gathers, overlap
     for (int b0 = lane; b0 < T; b0 += 256) {
@@ -2129,8 +2190,9 @@ __global__ __launch_bounds__(64) void s2c_kernel(
   for (int p = 0; p < npaths; p++) {
     const int cell = s2_u(cand[p]);
     int n = 0, top = -1, bottom = -1;
-    if (lds_walk) {
-      const S2WalkOut o = s2_walk_wave(llq, lmap, cell, lane, single ? pathq : nullptr, pathh);
+    if (lds_walk || nq <= 65536) {
+      const S2WalkOut o = lds_walk ? s2_walk_wave(llq, lmap, cell, lane, single ? pathq : nullptr, pathh)
+                                   : s2_walk_diag(hits, off, cell, lane, single ? pathq : nullptr, pathh);
       n = o.n;
       top = o.top;
       bottom = o.bottom;
@@ -2210,8 +2272,9 @@ __global__ __launch_bounds__(64) void s2c_kernel(
     if (keep[i]) continue;
     const S2Path x = pth[pord[i]];
     const int n = x.n;
-    if (!single && lds_walk) {  // entries, 3' end first
-      (void)s2_walk_wave(llq, lmap, x.cell, lane, pathq, pathh);
+    if (!single && (lds_walk || nq <= 65536)) {  // entries, 3' end first
+      if (lds_walk) (void)s2_walk_wave(llq, lmap, x.cell, lane, pathq, pathh);
+      else (void)s2_walk_diag(hits, off, x.cell, lane, pathq, pathh);
     } else if (lane == 0 && !single) {
       int e = 0;
       {
