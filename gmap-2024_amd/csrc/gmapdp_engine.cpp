@@ -93,7 +93,8 @@ hipError_t launch_s2c(int nproblems, hipStream_t stream, const DevStage2Problem*
 hipError_t launch_oi(bool wide, int nproblems, size_t lds, hipStream_t stream, const DevOligoProblem* probs,
                      const uint32_t* blocks, const char* quc, unsigned char* scratch, gmapdp_oligo_result* results,
                      int32_t* npos, int32_t* map, uint32_t* table, int32_t* diags, uint64_t* pool,
-                     unsigned long long* pool_counter, unsigned long long pool_cap);
+                     unsigned long long* pool_counter, unsigned long long pool_cap, int32_t* nhits_out);
+size_t scratch_bytes_oi_hits(int querylength, size_t hitcap);
 hipError_t launch_mx_search(int n, hipStream_t s, const gmapdp_microexon_problem* probs, const uint32_t* blocks,
                             uint64_t nwords, const char* qseq, const char* qseq_uc, gmapdp_microexon_result* results,
                             gmapdp_microexon_candidate* cands, unsigned long long cap, unsigned long long* counter,
@@ -2252,6 +2253,7 @@ struct gmapdp_oligo_plan {
   std::vector<int> umax;                      // per chunk: 2 * umax + (32-bit counters)
   std::vector<int> keys;                      // per problem in launch order: its class key
   size_t table_cap = 0, diag_cap = 0, scratch_cap = 0;
+  int32_t* d_nhits = nullptr;                 // sizing runs: each problem's hit-list length
   // get_mappings' event pool (3 slots per hit, shared by a chunk through an atomic cursor; a problem that no
   // longer fits runs the sequential walk in its fallback region, or reports overflow when it has none)
   uint64_t* d_pool = nullptr;
@@ -2264,7 +2266,7 @@ struct gmapdp_oligo_plan {
   std::vector<DevOligoProblem> ord;
 };
 
-static constexpr int kOligoChunkProblems = 4096;
+static constexpr int kOligoChunkProblems = 16384;
 static constexpr size_t kOligoChunkBytes = size_t(3) << 30;
 
 static void oligo_plan_free(gmapdp_oligo_plan* p) {
@@ -2277,6 +2279,7 @@ static void oligo_plan_free(gmapdp_oligo_plan* p) {
   if (p->d_scratch) (void)hipFree(p->d_scratch);
   if (p->d_pool) (void)hipFree(p->d_pool);
   if (p->d_pool_counter) (void)hipFree(p->d_pool_counter);
+  if (p->d_nhits) (void)hipFree(p->d_nhits);
   delete p;
 }
 
@@ -2285,7 +2288,8 @@ static void oligo_plan_free(gmapdp_oligo_plan* p) {
 // dcap[i] are what problem i may take of each.  `local`: the arenas too restart at 0 in every chunk (a
 // sizing run, whose outputs are only its counts), else they are laid out over the whole plan.
 static void oligo_layout(gmapdp_oligo_plan* P, const std::vector<size_t>& slots, bool fallback,
-                         const std::vector<size_t>& tcap, const std::vector<size_t>& dcap, bool local) {
+                         const std::vector<size_t>& tcap, const std::vector<size_t>& dcap, bool local,
+                         const std::vector<size_t>* hcap = nullptr) {
   P->launches.clear();
   P->umax.clear();
   P->scratch_cap = 0;
@@ -2310,7 +2314,8 @@ static void oligo_layout(gmapdp_oligo_plan* P, const std::vector<size_t>& slots,
   for (int k = 0; k < (int)P->ord.size(); k++) {
     DevOligoProblem& d = P->ord[k];
     const uint32_t w = d.chrend > d.chrstart ? d.chrend - d.chrstart : 0;
-    const size_t mb = align_up(scratch_bytes_oi(d.querylength, w), 256);
+    const size_t mb = align_up(hcap ? scratch_bytes_oi_hits(d.querylength, (*hcap)[d.index])
+                                    : scratch_bytes_oi(d.querylength, w), 256);
     const size_t fb = fallback ? align_up(scratch_bytes_oi_fallback(d.querylength, w), 256) : 0;
     if (k > first && (P->keys[k] != P->keys[first] || k - first >= kOligoChunkProblems || cb + mb + fb > kOligoChunkBytes))
       close(k);
@@ -2435,16 +2440,18 @@ static int oligo_plan_build(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problem
 // over the query positions), the diagonal arena exactly ndiagonals records, the pool exactly 3 slots per hit
 // (so no problem takes the sequential walk and no fallback region is kept); a rerun seeds the same way.
 static hipError_t oligo_plan_relayout(gmapdp_ctx* ctx, gmapdp_oligo_plan* P, const gmapdp_oligo_problem* problems,
-                                      const gmapdp_oligo_result* ores) {
+                                      const gmapdp_oligo_result* ores, const int32_t* nhits) {
   const int n = P->n;
-  std::vector<size_t> slots(n), tcap(n), dcap(n);
+  std::vector<size_t> slots(n), tcap(n), dcap(n), hcap(n);
   for (int i = 0; i < n; i++) {
     const size_t tp = (size_t)std::max(ores[i].totalpositions, 0);
     tcap[i] = std::min<size_t>(oligo_table_cap(problems[i]), tp);
     dcap[i] = (size_t)std::max(ores[i].ndiagonals, 0);
     slots[i] = 3 * tp;
+    hcap[i] = (size_t)std::max(nhits[i], 0);
   }
-  oligo_layout(P, slots, false, tcap, dcap, false);
+  // the hit lists sized as measured (a few % of a 214-kb window), so one launch holds most of a plan
+  oligo_layout(P, slots, false, tcap, dcap, false, &hcap);
   if (P->table_cap > 0x7fffffffull) return hipErrorInvalidValue;  // 32-bit mappings
   return oligo_buffers(ctx, P);
 }
@@ -2476,7 +2483,7 @@ int gmapdp_oligo_plan_run(gmapdp_ctx* ctx, const gmapdp_oligo_plan* plan, const 
     const hipError_t e = launch_oi(key & 1, plan->launches[li].second, lds_bytes_oi(key >> 1, key & 1), s,
                                    plan->d_probs + plan->launches[li].first, ctx->d_genome, d_qseq_uc,
                                    plan->d_scratch, d_results, d_npositions, d_mappings, d_positions, d_diagonals,
-                                   plan->d_pool, plan->d_pool_counter, plan->pool_cap);
+                                   plan->d_pool, plan->d_pool_counter, plan->pool_cap, plan->d_nhits);
     if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "oligo launch: %s", e);
   }
   return GMAPDP_OK;
@@ -3268,6 +3275,7 @@ int gmapdp_stage2_plan_create(gmapdp_ctx* ctx, const gmapdp_stage2_problem* prob
   if (e == hipSuccess) e = hipMalloc(&P->d_table, sizeof(uint32_t) * std::max<size_t>(toff, 1));
   if (e == hipSuccess) e = hipMalloc(&P->d_diag, 4 * sizeof(int32_t) * std::max<size_t>(doff, 1));
   if (e == hipSuccess) e = hipMalloc(&P->d_counters, s2_counters_bytes(n));
+  if (e == hipSuccess) e = hipMalloc(&P->oplan->d_nhits, sizeof(int32_t) * n);
   if (e == hipSuccess) e = hipMemcpy(P->d_probs, dp.data(), sizeof(DevStage2Problem) * n, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = ctx->qseq_uc.ensure(qbytes);
   if (e == hipSuccess) e = hipMemcpy(ctx->qseq_uc.p, qseq_uc, qbytes, hipMemcpyHostToDevice);
@@ -3278,8 +3286,11 @@ int gmapdp_stage2_plan_create(gmapdp_ctx* ctx, const gmapdp_stage2_problem* prob
   // size the chaining scratch from one seeding run
   rc = stage2_plan_launch(ctx, P, nullptr, (const char*)ctx->qseq_uc.p, nullptr, ctx->stream, true, false);
   std::vector<gmapdp_oligo_result> ores(n);
+  std::vector<int32_t> nhits(n);
   if (!rc) {
     e = hipMemcpyAsync(ores.data(), P->d_ores, sizeof(gmapdp_oligo_result) * n, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(nhits.data(), P->oplan->d_nhits, sizeof(int32_t) * n, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = ctx_sync(ctx, ctx->stream);
     if (e != hipSuccess) rc = fail(ctx, GMAPDP_ELAUNCH, "stage-2 plan seeding: %s", e);
   }
@@ -3294,7 +3305,9 @@ int gmapdp_stage2_plan_create(gmapdp_ctx* ctx, const gmapdp_stage2_problem* prob
   (void)hipFree(P->d_diag);
   P->d_table = nullptr;
   P->d_diag = nullptr;
-  e = oligo_plan_relayout(ctx, P->oplan, op.data(), ores.data());
+  (void)hipFree(P->oplan->d_nhits);
+  P->oplan->d_nhits = nullptr;
+  e = oligo_plan_relayout(ctx, P->oplan, op.data(), ores.data(), nhits.data());
   if (e == hipSuccess) e = hipMalloc(&P->d_table, sizeof(uint32_t) * std::max<size_t>(P->oplan->table_cap, 1));
   if (e == hipSuccess) e = hipMalloc(&P->d_diag, 4 * sizeof(int32_t) * std::max<size_t>(P->oplan->diag_cap, 1));
   if (e != hipSuccess) {

@@ -423,7 +423,7 @@ __global__ __launch_bounds__(64) void oi_kernel(
     const DevOligoProblem* __restrict__ probs, const uint32_t* __restrict__ blocks, const char* __restrict__ quc_all,
     unsigned char* __restrict__ scratch, gmapdp_oligo_result* __restrict__ results, int32_t* __restrict__ npos_out,
     int32_t* __restrict__ map_out, uint32_t* __restrict__ table_all, unsigned long long* __restrict__ pool_counter,
-    unsigned long long pool_cap) {
+    unsigned long long pool_cap, int32_t* __restrict__ nhits_out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x;
   const DevOligoProblem P = probs[blockIdx.x];
@@ -569,6 +569,7 @@ __global__ __launch_bounds__(64) void oi_kernel(
       }
     }
   }
+  if (nhits_out && lane == 0) nhits_out[P.index] = nhits;  // the hit list's length (a plan's sizing run)
   __syncthreads();
   // Count_T wraps; the table slices follow oligo order
   uint32_t tot = 0;
@@ -830,6 +831,9 @@ size_t lds_bytes_oi(int umax, bool wide) { return 6 * (size_t)kOiWords + (wide ?
 size_t scratch_bytes_oi(int querylength, uint32_t genomiclength) {
   return scratch_oi(querylength, genomiclength).total;
 }
+size_t scratch_bytes_oi_hits(int querylength, size_t hitcap) {  // a measured hit count instead of the window
+  return align16(scratch_oi(querylength, 0).hits + 8 * (hitcap + 2));
+}
 size_t scratch_bytes_oi_fallback(int querylength, uint32_t genomiclength) {
   return scratch_oi_fb(querylength, genomiclength).total;
 }
@@ -837,14 +841,14 @@ size_t scratch_bytes_oi_fallback(int querylength, uint32_t genomiclength) {
 hipError_t launch_oi(bool wide, int nproblems, size_t lds, hipStream_t stream, const DevOligoProblem* probs,
                      const uint32_t* blocks, const char* quc, unsigned char* scratch, gmapdp_oligo_result* results,
                      int32_t* npos, int32_t* map, uint32_t* table, int32_t* diags, uint64_t* pool,
-                     unsigned long long* pool_counter, unsigned long long pool_cap) {
+                     unsigned long long* pool_counter, unsigned long long pool_cap, int32_t* nhits_out) {
   void* fn = wide ? reinterpret_cast<void*>(&oi_kernel<uint32_t>) : reinterpret_cast<void*>(&oi_kernel<uint16_t>);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
   void* args[] = {(void*)&probs, (void*)&blocks, (void*)&quc, (void*)&scratch, (void*)&results, (void*)&npos,
-                  (void*)&map, (void*)&table, (void*)&pool_counter, (void*)&pool_cap};
+                  (void*)&map, (void*)&table, (void*)&pool_counter, (void*)&pool_cap, (void*)&nhits_out};
   hipError_t e = hipLaunchKernel(fn, dim3(nproblems), dim3(64), args, lds, stream);
   if (e != hipSuccess) return e;
   void* margs[] = {(void*)&probs, (void*)&scratch, (void*)&results, (void*)&npos, (void*)&map, (void*)&table,

@@ -475,8 +475,10 @@ struct S2EntryCache {
 struct S2Pref {
   int q = 0, n = 0, off = 0, start = 0;
   S2HV h = {};
-  __device__ __forceinline__ void load(const S2W& W, int np) {
-    const int k = np - 1 - W.lane;
+  __device__ __forceinline__ void load(const S2W& W, int np, int base = 0) {
+    const int k = np - 1 - base - W.lane;  // entry base + lane (0: the newest)
+    q = n = off = start = 0;
+    h = {};
     if (k >= 0) {
       const int s = k & (kS2Meta - 1);
       q = s2_ring.eq[s];
@@ -634,20 +636,30 @@ __device__ __forceinline__ int s2_dloop_fast(S2W& W, const S2Pref& pf, int np, i
 //    consec >= ENOUGH_CONSECUTIVE, else the last record wins (the first lane holding the maximum);
 //  - _mult's frontiers: per visited entry, the first hit past ranges 0-1, or -1.
 // Fresh tracei values are drawn only for the winning range-2 link (values only meet in equality tests).
+// Entries base .. base + 63 (pf loaded at base, lane = entry - base) from last_tr = lt; when their hits
+// number more than 64 the leading entries whose hits fit are taken (a group) and the walk goes on from the
+// next one (return 2, *next = its index, lt = last_tr there).
 // Returns 0 (nothing done) when the window does not fit, else as s2_dloop_fast.
 __device__ __forceinline__ int s2_dloop_multi(S2W& W, const S2Pref& pf, int np, int kmax, int q, uint32_t position,
-                                              S2Best& b, bool range1, bool use_f, int& f, int& lt) {
-  const int kend = kmax < 63 ? kmax : 63;
+                                              S2Best& b, bool range1, bool use_f, int& f, int& lt, int base = 0,
+                                              int* next = nullptr) {
+  const int kend = kmax - base < 63 ? kmax - base : 63;
   const int lane = W.lane;
   const int f0 = use_f ? f : 0;
-  const bool inw = lane <= kend && lane < np && f0 != -1;
-  const bool valid = inw && pf.n > 0;
+  const bool inw0 = lane <= kend && base + lane < np && f0 != -1;
   const bool inring = pf.n <= kS2Ring && pf.start >= W.pushed - kS2Ring;
-  if (ballot(valid && !inring)) return 0;
-  const int c = valid ? max(pf.n - f0, 0) : 0;
+  if (ballot(inw0 && pf.n > 0 && !inring)) return 0;
+  const int c0 = (inw0 && pf.n > 0) ? max(pf.n - f0, 0) : 0;
+  const int incl0 = wave_incl_sum(c0, lane);
+  // the group: the leading entries whose hits fit in the wave
+  const uint64_t over = ballot(incl0 > 64);
+  const int gend = over ? __ffsll((long long)over) - 1 : 64;  // entries [0, gend) of this window
+  if (gend == 0 || (gend <= kend && !next)) return 0;
+  const bool inw = inw0 && lane < gend;
+  const bool valid = inw && pf.n > 0;
+  const int c = valid ? c0 : 0;
   const int incl = wave_incl_sum(c, lane);
   const int total = __builtin_amdgcn_readlane(incl, 63);
-  if (total > 64) return 0;
   S2_TALLY(n_multi, 1);
   s2_uniform(b);
   if (b.consec >= kS2EnoughConsec) return 1;
@@ -687,7 +699,7 @@ __device__ __forceinline__ int s2_dloop_multi(S2W& W, const S2Pref& pf, int np, 
   const int bt = __shfl(v.tracei, nx < eend ? nx : sl, 64);
   // range 0 across entries (scalar): eqm bit s set when the entry starting at lane s meets last_tr == a
   uint64_t eqm = 0, Hm = H;
-  int last_tr = -1;
+  int last_tr = lt;
   while (Hm) {
     const int s0 = __ffsll((long long)Hm) - 1;
     Hm &= Hm - 1ull;
@@ -751,8 +763,15 @@ __device__ __forceinline__ int s2_dloop_multi(S2W& W, const S2Pref& pf, int np, 
     const int g = Gm ? __ffsll((long long)Gm) - 1 : 64;
     if (inw && lane <= stop_e) f = (c > 0 && g < excl + c) ? f0 + (g - excl) : -1;
   }
-  if (S || kmax < 64) return 1;
+  if (S) return 1;
+  if (gend <= kend) {  // the hits of the later entries did not fit this group
+    lt = last_tr;
+    *next = base + gend;
+    return 2;
+  }
+  if (kmax - base < 64) return 1;
   lt = last_tr;
+  if (next) *next = base + 64;
   return 2;
 }
 
@@ -783,13 +802,27 @@ __device__ __forceinline__ S2Best s2_one(S2W& W, int q, uint32_t position, int n
     // the entry that ends the walk (donep): the first beyond nlookback more than lookback + 8 back
     const uint64_t dm = ballot(W.lane < np && W.lane > nlookback && (q - pf.q) - kS2K > lookback);
     const int kmax = dm ? __ffsll((long long)dm) - 1 : (np <= 64 ? np - 1 : 64);
-    int fdummy = 0, lt = -1;
+    int fdummy = 0, lt = -1, from = 0;
     int st = s2_dloop_fast(W, pf, np, kmax, q, position, b, W.splicingp != 0, false, fdummy, lt);
-    if (!st) st = s2_dloop_multi(W, pf, np, kmax, q, position, b, W.splicingp != 0, false, fdummy, lt);
+    if (st == 2) from = 64;
+    if (!st && kmax >= 64) {  // the walk goes past the window (donep decides there): one group at most
+      st = s2_dloop_multi(W, pf, np, kmax, q, position, b, W.splicingp != 0, false, fdummy, lt);
+      if (st == 2) from = 64;
+    } else if (!st) {  // entries with several hits: groups of entries whose hits fit the wave
+      S2Pref pg;
+      for (;;) {
+        const S2Pref& pw = from ? pg : pf;
+        int nb = from;
+        st = s2_dloop_multi(W, pw, np, kmax, q, position, b, W.splicingp != 0, false, fdummy, lt, from, &nb);
+        if (st != 2) break;
+        from = nb;
+        pg.load(W, np, from);
+      }
+    }
     if (st == 1) np = 0;  // done
-    if (st == 2) last_tr = lt;
+    if (st != 1) last_tr = lt;
     S2EntryCache ec;
-    for (int kk = st == 2 ? 64 : 0; kk < np && b.consec < kS2EnoughConsec && !donep; kk++) {
+    for (int kk = from; kk < np && b.consec < kS2EnoughConsec && !donep; kk++) {
       const int eq = kk < kS2Pref ? __builtin_amdgcn_readlane(pf.q, kk) : ec.get(W, np, kk).q;
       if (kk > nlookback && (q - eq) - kS2K > lookback) donep = true;
       int qd;
@@ -1221,19 +1254,37 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
             maxseen = maxnon;
           }
           s2_uniform(b);
-          int st = 0, lt = -1;
+          int st = 0, lt = -1, from = 0;
           if (overall < kS2GreedyConsec) {
             const int kmax = min(min(maxseen, nfr - 1), np - 1);
             const int kend = min(kmax, 63);
             int f = lane <= kend ? s2_fr[lane] : -1;
             st = s2_dloop_fast(W, pf, np, kmax, q, position, b, true, true, f, lt);
-            if (!st) st = s2_dloop_multi(W, pf, np, kmax, q, position, b, true, true, f, lt);
             if (st && lane <= kend) s2_fr[lane] = f;
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            if (st == 2) from = 64;
+            if (!st) {  // groups of entries whose hits fit the wave, from entry 0
+              lt = -1;
+              st = 2;
+            }
+            S2Pref pg;
+            while (st == 2 && from <= kmax) {
+              if (from) pg.load(W, np, from);
+              const S2Pref& pw = from ? pg : pf;
+              const int ke = min(kmax - from, 63);
+              int fg = lane <= ke ? s2_fr[from + lane] : -1;
+              int nb = from;
+              const int r = s2_dloop_multi(W, pw, np, kmax, q, position, b, true, true, fg, lt, from, &nb);
+              if (r && lane <= ke) s2_fr[from + lane] = fg;
+              __atomic_signal_fence(__ATOMIC_SEQ_CST);
+              st = r;
+              if (r == 2) from = nb;
+            }
+            if (st == 2) st = 1;  // every entry up to kmax walked
           }
           if (overall < kS2GreedyConsec && st != 1) {
-            int last_tr = st == 2 ? lt : -1;
-            for (int kk = st == 2 ? 64 : 0; kk < np && b.consec < kS2EnoughConsec && kk <= maxseen && kk < nfr;
+            int last_tr = lt;
+            for (int kk = from; kk < np && b.consec < kS2EnoughConsec && kk <= maxseen && kk < nfr;
                  kk++) {
               const int f = s2_u(s2_fr[kk]);
               if (f != -1) {
@@ -1647,12 +1698,26 @@ __global__ __launch_bounds__(64) void s2a_kernel(
     qstart = 0;
     qend = ql - 1;
   } else {
-    // assign_scores: running sum in query order (sequential, as the reference rounds it)
-    if (lane == 0) {
+    // assign_scores: running sum in query order, sequential as the reference rounds it, but fed from
+    // registers: 64 terms per coalesced load, added one by one in order by every lane alike (the same
+    // IEEE sums), lane j keeping the prefix through term j (one lane walking run[] took a global round trip
+    // per query position)
+    {
       double acc = 0.0;
-      for (int q = 0; q < ql; q++) {
-        acc += run[q];
-        run[q] = acc;
+      for (int cb = 0; cb < ql; cb += 64) {
+        const int q = cb + lane;
+        const double v = q < ql ? run[q] : 0.0;
+        const int2 vi = *reinterpret_cast<const int2*>(&v);
+        double pre = 0.0;
+        const int m = ql - cb < 64 ? ql - cb : 64;
+        for (int j = 0; j < m; j++) {
+          int2 t;
+          t.x = __builtin_amdgcn_readlane(vi.x, j);
+          t.y = __builtin_amdgcn_readlane(vi.y, j);
+          acc += *reinterpret_cast<const double*>(&t);
+          if (lane == j) pre = acc;
+        }
+        if (q < ql) run[q] = pre;
       }
     }
     wave_sync();
