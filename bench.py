@@ -490,10 +490,11 @@ def main():
     ostream = torch.cuda.Stream(dev)
     side_of = lambda k: min(k, len(sides))  # noqa: E731  plan stream k >= 1 -> side index + 1
 
-    def launch(b, li, s):
-        eng._check(lib.gmapdp_plan_run_launch(eng.h, b["plan"], li, C.c_void_p(b["d_q"].data_ptr()),
-                                              C.c_void_p(b["d_q"].data_ptr()), C.c_void_p(d_res.data_ptr()),
-                                              C.c_void_p(d_pairs.data_ptr()), C.c_void_p(s.cuda_stream)),
+    def launch(b, li, s, kernel_only=False):
+        f = lib.gmapdp_plan_run_launch_kernel if kernel_only else lib.gmapdp_plan_run_launch
+        eng._check(f(eng.h, b["plan"], li, C.c_void_p(b["d_q"].data_ptr()),
+                     C.c_void_p(b["d_q"].data_ptr()), C.c_void_p(d_res.data_ptr()),
+                     C.c_void_p(d_pairs.data_ptr()), C.c_void_p(s.cuda_stream)),
                    "gmapdp_plan_run_launch")
 
     def orun(b, s, what):
@@ -601,9 +602,10 @@ def main():
                     for li, nm in enumerate(b["names"]):
                         if nm != name:
                             continue
+                        launch(b, li, stream)  # (the class's MaxEnt prologue, untimed)
                         e0, e1 = mk()
                         e0.record(stream)
-                        launch(b, li, stream)
+                        launch(b, li, stream, kernel_only=True)  # the kernel alone, as rocprof times it
                         e1.record(stream)
                         torch.cuda.synchronize()
                         if with_bytes and rep == 0:

@@ -1294,7 +1294,10 @@ static hipError_t launch_class_maxent(gmapdp_ctx* ctx, const PlanCore::Launch& L
                        const_cast<double*>(a.d_sprob));
 }
 
-static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, const RunArgs& a, hipStream_t stream) {
+// prologue = false: the launch's kernel alone (the MaxEnt prologue of a genome-gap class is skipped; the
+// probabilities a previous full run computed stay in the arena)
+static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, const RunArgs& a, hipStream_t stream,
+                             bool prologue = true) {
   const auto& L = plan.launches[li];
   if (L.kind == PlanCore::kUxe)
     return launch_uxe(L.R, L.count, L.lds, stream, a.d_probs, a.d_order + L.first, (unsigned char*)ctx->gdirs.p,
@@ -1302,7 +1305,7 @@ static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, cons
                       a.d_pairs);
   if (L.kind == PlanCore::kUxg) {
     if (!a.d_gresults || !a.d_sprob) return hipErrorInvalidValue;
-    const hipError_t e = launch_class_maxent(ctx, L, a, stream);
+    const hipError_t e = prologue ? launch_class_maxent(ctx, L, a, stream) : hipSuccess;
     if (e != hipSuccess) return e;
     return launch_uxg(L.R, L.count, L.lds, stream, a.d_gprobs, a.d_gorder + L.first, (unsigned char*)ctx->gdirs.p,
                       ctx->d_genome, ctx->genome_words, a.d_q, a.d_quc, a.d_sprob, ctx->d_sc, ctx->d_cs, ctx->d_isc,
@@ -1323,7 +1326,7 @@ static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, cons
                      ctx->genome_words, a.d_q, a.d_quc, ctx->d_sc, ctx->d_cs, a.d_results, a.d_pairs,
                      (uint64_t*)ctx->gdirs.p);
   if (!a.d_gresults || !a.d_sprob) return hipErrorInvalidValue;
-  const hipError_t e = launch_class_maxent(ctx, L, a, stream);
+  const hipError_t e = prologue ? launch_class_maxent(ctx, L, a, stream) : hipSuccess;
   if (e != hipSuccess) return e;
   return launch_gg(L.R, L.dirs_lds, L.count, L.lds, stream, a.d_gprobs, a.d_gorder + L.first, ctx->d_genome,
                    ctx->genome_words, a.d_q, a.d_quc, a.d_sprob, ctx->d_sc, ctx->d_cs, ctx->d_isc, a.d_gresults,
@@ -2152,8 +2155,9 @@ int gmapdp_plan_run(gmapdp_ctx* ctx, const gmapdp_plan* plan, const char* d_qseq
                   stream ? (hipStream_t)stream : ctx->stream);
 }
 
-int gmapdp_plan_run_launch(gmapdp_ctx* ctx, const gmapdp_plan* plan, int li, const char* d_qseq,
-                           const char* d_qseq_uc, gmapdp_result* d_results, gmapdp_pair* d_pairs, void* stream) {
+static int plan_run_launch(gmapdp_ctx* ctx, const gmapdp_plan* plan, int li, const char* d_qseq,
+                           const char* d_qseq_uc, gmapdp_result* d_results, gmapdp_pair* d_pairs, void* stream,
+                           bool prologue) {
   if (!ctx || !plan || li < 0 || li >= (int)plan->in.launches.size()) return GMAPDP_EINVAL;
   if (!ctx->d_genome) return GMAPDP_ENOGENOME;
   if (plan->in.gdirs_bytes) {
@@ -2161,9 +2165,19 @@ int gmapdp_plan_run_launch(gmapdp_ctx* ctx, const gmapdp_plan* plan, int li, con
     if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "direction scratch: %s", e);
   }
   hipError_t e = launch_one(ctx, plan->in, li, plan_args(plan, d_qseq, d_qseq_uc, d_results, d_pairs),
-                            stream ? (hipStream_t)stream : ctx->stream);
+                            stream ? (hipStream_t)stream : ctx->stream, prologue);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "dp launch: %s", e);
   return GMAPDP_OK;
+}
+
+int gmapdp_plan_run_launch(gmapdp_ctx* ctx, const gmapdp_plan* plan, int li, const char* d_qseq,
+                           const char* d_qseq_uc, gmapdp_result* d_results, gmapdp_pair* d_pairs, void* stream) {
+  return plan_run_launch(ctx, plan, li, d_qseq, d_qseq_uc, d_results, d_pairs, stream, true);
+}
+
+int gmapdp_plan_run_launch_kernel(gmapdp_ctx* ctx, const gmapdp_plan* plan, int li, const char* d_qseq,
+                                  const char* d_qseq_uc, gmapdp_result* d_results, gmapdp_pair* d_pairs, void* stream) {
+  return plan_run_launch(ctx, plan, li, d_qseq, d_qseq_uc, d_results, d_pairs, stream, false);
 }
 
 void gmapdp_plan_destroy(gmapdp_plan* plan) {

@@ -228,6 +228,8 @@ def load_library(path=LIB_PATH):
         "gmapdp_plan_launch_stream": (C.c_int, [C.c_void_p, C.c_int]),
         "gmapdp_plan_run_launch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                              C.c_void_p, C.c_void_p]),
+        "gmapdp_plan_run_launch_kernel": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                                    C.c_void_p, C.c_void_p, C.c_void_p]),
         "gmapdp_stream": (C.c_void_p, [C.c_void_p]),
         "gmapdp_genome_gap_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                               C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,

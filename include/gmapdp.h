@@ -785,6 +785,11 @@ int gmapdp_plan_launch_is_tail (const gmapdp_plan *plan, int li);
 int gmapdp_plan_launch_members (const gmapdp_plan *plan, int li, int *problem_indices);
 int gmapdp_plan_run_launch (gmapdp_ctx *ctx, const gmapdp_plan *plan, int li, const char *d_qseq,
                             const char *d_qseq_uc, gmapdp_result *d_results, gmapdp_pair *d_pairs, void *stream);
+/* The same launch's kernel alone: a genome-gap class's device-MaxEnt prologue is not re-run (the splice
+ * probabilities a previous full run computed stay in the bound arena).  For timing one kernel's launches. */
+int gmapdp_plan_run_launch_kernel (gmapdp_ctx *ctx, const gmapdp_plan *plan, int li, const char *d_qseq,
+                                   const char *d_qseq_uc, gmapdp_result *d_results, gmapdp_pair *d_pairs,
+                                   void *stream);
 void gmapdp_plan_destroy (gmapdp_plan *plan);
 /* The context's HIP stream (hipStream_t). */
 void *gmapdp_stream (gmapdp_ctx *ctx);
