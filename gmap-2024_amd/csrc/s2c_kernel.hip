@@ -89,7 +89,7 @@ struct S2Path {
   uint32_t start, end;  // genomepos of the first and last pair of the converted list
 };
 struct S2Scratch {
-  size_t diff, run, off, minact, maxact, first, proc, diags, ord, tmp, hits, cand, keep, paths, pq, ph, sbuf, lk, total;
+  size_t diff, run, off, minact, maxact, first, proc, diags, ord, tmp, hits, cand, keep, paths, pq, ph, sbuf, total;
   int sortn;  // power of two >= every sorted array
 };
 __host__ __device__ inline int s2_pow2(int n) {
@@ -118,8 +118,7 @@ __host__ __device__ inline S2Scratch s2_scratch(int ql, int T, int nd) {
   s.ph = align16(s.pq + 4 * Q);
   s.sortn = s2_pow2((int)(H > D ? H : D));
   s.sbuf = align16(s.ph + 4 * Q);
-  s.lk = align16(s.sbuf + 4 * (size_t)s.sortn);  // the walk's link words and maps when they exceed the LDS
-  s.total = align16(s.lk + 8 * H);
+  s.total = align16(s.sbuf + 4 * (size_t)s.sortn);
   return s;
 }
 
@@ -2204,8 +2203,7 @@ __global__ __launch_bounds__(64) void s2c_kernel(
   S2_MARK(5);
   // ---- traceback_one per selected cell: length and extent of the converted list ----
   // the links go to LDS first (coalesced loads), so the pointer chases run at LDS latency
-  // (in the call's scratch when they do not fit: a 214-kb window's 8 000+ hits, the wave walk then runs at
-  // L2 latency instead of one lane chasing ~2 000 global links per path)
+  // (past 4 096 hits the walk reads the hit arrays themselves: s2_walk_diag)
   extern __shared__ uint32_t s2c_lds[];
   uint32_t* llq = s2c_lds;
   uint32_t* lmap = s2c_lds + kS2cCap;
