@@ -1872,30 +1872,40 @@ __global__ __launch_bounds__(64) void s2a_kernel(
 
   S2_MARK(2);
   // ---- per-hit arrays: the hits of query position q at hits[off[q] ...] (Linkmatrix_1d_new) ----
+  // 64 positions at a time: their offsets by a prefix scan, then their hits written in hit order, lane l
+  // taking hit base + l (its position the last lane whose offset is <= the hit, a binary search over the
+  // lanes), so each store instruction covers 64 consecutive records
   carry = 0;
+  bool big = false;
   for (int cb = 0; cb < ql; cb += 64) {
     const int q = cb + lane;
     const int v = q < nq ? npq[q] : 0;
     const int incl = carry + wave_incl_sum(v, lane);
-    if (q < ql) off[q] = incl - v;
-    carry = __shfl(incl, 63, 64);
+    const int o = incl - v;
+    if (q < ql) off[q] = o;
+    const int mq = q < nq && v > 0 ? mpq[q] : 0;
+    const int hend = __shfl(incl, 63, 64);
+    for (int base = carry; base < hend; base += 64) {
+      const int h = base + lane;
+      int j = 0;
+#pragma unroll
+      for (int st = 32; st >= 1; st >>= 1) {
+        const int oj = __shfl(o, j + st, 64);
+        if (oj <= h) j += st;
+      }
+      const int oq = __shfl(o, j, 64), mj = __shfl(mq, j, 64);
+      if (h < hend) {
+        S2Hit x;
+        x.map = table_all[mj + (h - oq)];
+        big |= (x.map >= 0x80000000u);
+        x.consec = x.root = x.fpos = x.fhit = x.tracei = x.score = x.active = 0;  // CALLOC
+        x.q = cb + j;
+        hits[h] = x;
+      }
+    }
+    carry = hend;
   }
   if (lane == 0) off[ql] = carry;
-  bool big = false;
-  for (int q = lane; q < nq; q += 64) {
-    const int n = npq[q];
-    if (n <= 0) continue;
-    const uint32_t* src = table_all + mpq[q];
-    S2Hit* dst = hits + off[q];
-    for (int k = 0; k < n; k++) {
-      S2Hit x;
-      x.map = src[k];
-      big |= (x.map >= 0x80000000u);
-      x.consec = x.root = x.fpos = x.fhit = x.tracei = x.score = x.active = 0;  // CALLOC
-      x.q = q;
-      dst[k] = x;
-    }
-  }
   if (ballot(big)) {  // chromosome positions past 2^31: Pairpool_push would drop them (outside the domain)
     if (lane == 0) {
       R.status = kS2Domain;
@@ -1909,7 +1919,10 @@ __global__ __launch_bounds__(64) void s2a_kernel(
 }
 
 // the lookback sweep (align_compute_scores_lookback) of the calls s2a_kernel left chained
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void s2b_kernel(
+#ifndef GMAPDP_S2B_WPE
+#define GMAPDP_S2B_WPE 4  // waves per SIMD the sweep's registers are budgeted for (variants: make variant DEFS=...)
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GMAPDP_S2B_WPE))) void s2b_kernel(
     const DevStage2Problem* __restrict__ probs, const uint32_t* __restrict__ blocks, uint64_t nwords,
     const char* __restrict__ qseq, const char* __restrict__ quc, const gmapdp_oligo_result* __restrict__ ores,
     const int32_t* __restrict__ npos_all, const int32_t* __restrict__ map_all, const uint32_t* __restrict__ table_all,
@@ -2140,19 +2153,36 @@ __global__ __launch_bounds__(64) void s2c_kernel(
   const int qstart = R.diag_querystart, qend = R.diag_queryend;
   // ---- get_cells_fwd + the path loop: cells within FINAL_SCORE_TOLERANCE of the best, each the best
   // of its root position, in (score desc, root asc, querypos desc, hit asc) order ----
+  // one pass over the scores: the hits within the tolerance of the running best (a superset of those
+  // within it of the final best, in hit order) with their scores, then the final best filters them
   const int h0 = off[qstart], h1 = off[qend + 1];
-  int best = 0;
-  for (int gi = h0 + lane; gi < h1; gi += 64) best = max(best, hits[gi].score);
-  best = wave_max_i(best);
-  int ncand = 0;
-  if (best > 0) {
-    for (int cb = h0; cb < h1; cb += 64) {
-      const int gi = cb + lane;
-      const bool c = gi < h1 && hits[gi].score > best - kS2FinalTolerance && hits[gi].score > 0;
-      const uint64_t m = ballot(c);
-      if (c) cand[ncand + lanes_below(m, lane)] = gi;
-      ncand += __popcll(m);
+  int best = 0, ncand = 0;
+  for (int cb = h0; cb < h1; cb += 64) {
+    const int gi = cb + lane;
+    const int sc = gi < h1 ? hits[gi].score : 0;
+    best = max(best, wave_max_i(sc));
+    const bool c = gi < h1 && sc > best - kS2FinalTolerance && sc > 0;
+    const uint64_t m = ballot(c);
+    if (c) {
+      cand[ncand + lanes_below(m, lane)] = gi;
+      keep[ncand + lanes_below(m, lane)] = sc;
     }
+    ncand += __popcll(m);
+  }
+  wave_sync();
+  if (best > 0) {
+    int n2 = 0;
+    for (int cb = 0; cb < ncand; cb += 64) {
+      const int i = cb + lane;
+      const int gi = i < ncand ? cand[i] : 0, sc = i < ncand ? keep[i] : 0;
+      const bool c = i < ncand && sc > best - kS2FinalTolerance;
+      const uint64_t m = ballot(c);
+      if (c) cand[n2 + lanes_below(m, lane)] = gi;  // in place: n2 <= cb, this chunk's loads came first
+      n2 += __popcll(m);
+    }
+    ncand = n2;
+  } else {
+    ncand = 0;
   }
   wave_sync();
   // get_cells_fwd: by (root asc, score desc, querypos desc, hit asc); each root's best cells are the

@@ -197,7 +197,19 @@ $(OUT)/gmap_gpu_$(1): $$(NODP_$(1)) $(OUT)/gpushim_own_$(1)/gmapdp_gmap_shim.o $
 $(OUT)/gpushim_own_$(1)/gmapdp_gmap_shim.o: $(SHIM_SRC) ../include/gmapdp.h ../include/gmapdp_dynprog.h
 	@mkdir -p $$(dir $$@)
 	$$(CC) $(BASEFLAGS) -DHAVE_CONFIG_H -DGMAPDP_SHIM_OWN $$(FLAGS_$(1)) -I../include -c $$< -o $$@
+
+# the same two programs unstripped, with the sampling profiler (tools/pcprof.c, idle unless PCPROF_OUT is set)
+$(OUT)/gmap_prof_$(1): $$(PROGOBJS_$(1)) $(OUT)/pcprof.o
+	$$(CC) -pthread -o $$@ $$^ -lz -lm
+
+$(OUT)/gmap_gpu_prof_$(1): $$(NODP_$(1)) $(OUT)/gpushim_own_$(1)/gmapdp_gmap_shim.o $(OUT)/pcprof.o $(GMAPDP_LIB)/libgmapdp.so
+	$$(CC) -pthread $(foreach w,$(WRAPPED_OWN),-Wl,--wrap=$(w)) -o $$@ $$(filter %.o,$$^) \
+	  -L$(GMAPDP_LIB) -lgmapdp -Wl,-rpath,'$$$$ORIGIN/../../gmap-2024_amd/lib' -lz -lm
 endef
+
+$(OUT)/pcprof.o: ../tools/pcprof.c
+	@mkdir -p $(dir $@)
+	$(CC) -O2 -g -c $< -o $@
 $(foreach v,$(PROG_VARIANTS),$(eval $(call prog_rules,$(v))))
 
 # own_check (tests/test_shim_own.py): the non-DP Dynprog_* entry points (consistent table, scores, handles)
@@ -221,8 +233,8 @@ $(OUT)/fiber_check: $(filter-out $(OUT)/nosimd/gmap.o,$(NODP_nosimd)) $(OUT)/gpu
 	  -L$(GMAPDP_LIB) -lgmapdp -Wl,-rpath,'$$ORIGIN/../../gmap-2024_amd/lib' -lz -lm
 own_check: $(OUT)/own_check_ref $(if $(wildcard $(GMAPDP_LIB)/libgmapdp.so),$(OUT)/own_check_shim $(OUT)/fiber_check)
 
-programs: $(foreach v,$(PROG_VARIANTS),$(OUT)/gmap_$(v)) $(OUT)/gmap_callmix own_check \
-          $(if $(wildcard $(GMAPDP_LIB)/libgmapdp.so),$(foreach v,$(PROG_VARIANTS),$(OUT)/gmap_gpu_$(v)))
+programs: $(foreach v,$(PROG_VARIANTS),$(OUT)/gmap_$(v)) $(OUT)/gmap_callmix own_check $(OUT)/gmap_prof_nosimd \
+          $(if $(wildcard $(GMAPDP_LIB)/libgmapdp.so),$(foreach v,$(PROG_VARIANTS),$(OUT)/gmap_gpu_$(v)) $(OUT)/gmap_gpu_prof_nosimd)
 
 # The unmodified nosimd gmap with the hot-path entry points counted (callmix.c: one log line per call,
 # then the reference's own function): the measured per-read call mix of a read shape (tools/callmix.py)

@@ -35,6 +35,9 @@ def main():
                     help="shim configurations for the GPU runs, 'name:VAR=V,VAR=V;name2:...' (environment overrides)")
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--thread-cpu", action="store_true", help="per-thread-name CPU seconds of each run")
+    ap.add_argument("--prof", default=None,
+                    help="directory for sampled CPU profiles: runs the unstripped gmap_prof_V / gmap_gpu_prof_V "
+                         "programs with tools/pcprof.c's sampler on and resolves them (tools/pcprof.py)")
     a = ap.parse_args()
     import make_e2e as M
     genome = list(M.synth_genome())
@@ -55,8 +58,10 @@ def main():
     for c in a.configs.split(";"):
         name, _, kv = c.partition(":")
         configs.append((name, dict(x.split("=", 1) for x in kv.split(",") if x)))
-    runs = [] if a.skip_cpu else [("gmap_%s" % a.build, t, "cpu", {}) for t in cpu_t]
-    runs += [("gmap_gpu_%s" % a.build, t, name, cenv) for name, cenv in configs for t in gpu_t]
+    pv = "prof_" if a.prof else ""
+    runs = [] if a.skip_cpu else [("gmap_%s%s" % (pv, a.build), t, "cpu", {}) for t in cpu_t]
+    runs += [("gmap_gpu_%s%s" % (pv, a.build), t, name, cenv) for name, cenv in configs for t in gpu_t]
+    profs = []
     out["dispatchers"] = a.dispatchers
     for prog, t, cname, cenv in runs:
         if True:
@@ -65,6 +70,10 @@ def main():
             if a.trace and "gpu" in prog:
                 os.makedirs(a.trace, exist_ok=True)
                 env["GMAPDP_SHIM_TRACE"] = os.path.abspath(os.path.join(a.trace, "trace_%s_t%d.txt" % (cname, t)))
+            if a.prof:
+                os.makedirs(a.prof, exist_ok=True)
+                env["PCPROF_OUT"] = os.path.abspath(os.path.join(a.prof, "pcprof_%s_%s_t%d.txt" % (prog, cname, t)))
+                profs.append(env["PCPROF_OUT"])
             args = [os.path.join(ref, prog), "-t", str(t), "-O", "-g", "g.fa", "-f", "samse", "--no-sam-headers",
                     "r.fa"]
             t0 = time.perf_counter()
@@ -101,10 +110,13 @@ def main():
                                 "cpu_seconds": cpu, "cpu_cores_busy": cpu / dt,
                                 "shim_calls": stats[0] if stats else None, "thread_cpu_s": threads})
             print(json.dumps(out["runs"][-1]), file=sys.stderr, flush=True)
-    base = next(iter(sams.values())) if a.skip_cpu else sams[("gmap_%s" % a.build, min(cpu_t), "cpu")]
+    base = next(iter(sams.values())) if a.skip_cpu else sams[("gmap_%s%s" % (pv, a.build), min(cpu_t), "cpu")]
     out["outputs_identical"] = all(v == base for v in sams.values())
     out["recorded"] = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())  # bench.py selects records by this
     print(json.dumps(out))
+    if profs:
+        subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pcprof.py"), "--json",
+                        os.path.join(a.prof, "pcprof_summary.json")] + profs, check=False, stdout=sys.stderr)
 
 
 if __name__ == "__main__":

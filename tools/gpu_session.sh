@@ -34,6 +34,7 @@ for S in "$@"; do
     e2e:*) IFS=: read -r _ B N T C <<< "$S"; timeout -k 10 900 python tools/e2e_timing.py --build $B --reads $N --threads 16 --gpu-threads ${T:-512} ${C:+--configs "$C"} > $O/e2e_${B}_$N.json 2> $O/e2e_${B}_$N.err || exit 20 ;;
     isot:*) L=${S#isot:}; GMAPDP_LIB=$PWD/gmap-2024_amd/$L/libgmapdp.so timeout -k 10 300 python bench.py --iso-kernel "${ISO_KERNEL:-gmapdp::gg_kernel<1, false>}" --iso-reps ${ISO_REPS:-3} > $O/isot_$L.json 2> $O/isot_$L.err || exit 22 ;;
     oitiming) timeout -k 10 300 python tools/oi_timing.py 5000 > $O/oitiming.json 2> $O/oitiming.err || exit 24 ;;
+    e2eprof:*) IFS=: read -r _ B N T <<< "$S"; timeout -k 10 900 python tools/e2e_timing.py --build $B --reads $N --threads 16 --gpu-threads ${T:-2048} --prof $O/prof_$N > $O/e2eprof_${B}_$N.json 2> $O/e2eprof_${B}_$N.err || exit 26 ;;
     e2ecpu:*) IFS=: read -r _ B N T <<< "$S"; timeout -k 10 900 python tools/e2e_timing.py --build $B --reads $N --threads 16 --gpu-threads ${T:-2048} --thread-cpu > $O/e2ecpu_${B}_$N.json 2> $O/e2ecpu_${B}_$N.err || exit 25 ;;
     s2timing) timeout -k 10 300 python tools/oi_timing.py s2 5000 > $O/s2timing.json 2> $O/s2timing.err || exit 21 ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || exit 19 ;;
