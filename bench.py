@@ -487,7 +487,9 @@ def main():
     # (non-null) streams, so per-launch events time exactly the launches on their stream.
     stream = torch.cuda.Stream(dev)
     sides = [torch.cuda.Stream(dev) for _ in range(2)]
-    ostream = torch.cuda.Stream(dev)
+    # stage 2 (the step's longest chain) may take the high-priority queue: GMAPDP_BENCH_S2_PRIORITY=1
+    s2prio = int(os.environ.get("GMAPDP_BENCH_S2_PRIORITY", "0"))
+    ostream = torch.cuda.Stream(dev, priority=-1) if s2prio else torch.cuda.Stream(dev)
     side_of = lambda k: min(k, len(sides))  # noqa: E731  plan stream k >= 1 -> side index + 1
 
     def launch(b, li, s, kernel_only=False):

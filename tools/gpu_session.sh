@@ -25,6 +25,7 @@ for S in "$@"; do
     tests) timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $O/gputest.txt 2>&1 || exit 11 ;;
     tests:*) timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu -k "${S#tests:}" tests > $O/gputest_k.txt 2>&1 || exit 12 ;;
     bench:*) L=${S#bench:}; GMAPDP_LIB=$PWD/gmap-2024_amd/$L/libgmapdp.so timeout -k 10 400 python bench.py --steps 20 --no-cpu-baseline > $O/bench_$L.json 2> $O/bench_$L.err || exit 13 ;;
+    bp:*) L=${S#bp:}; GMAPDP_BENCH_S2_PRIORITY=1 GMAPDP_LIB=$PWD/gmap-2024_amd/$L/libgmapdp.so timeout -k 10 400 python bench.py --steps 20 --no-cpu-baseline > $O/bp_$L.json 2> $O/bp_$L.err || exit 27 ;;
     simd:*) L=${S#simd:}; GMAPDP_LIB=$PWD/gmap-2024_amd/$L/libgmapdp.so timeout -k 10 400 python bench.py --steps 20 --simd --no-cpu-baseline > $O/simd_$L.json 2> $O/simd_$L.err || exit 14 ;;
     c4:*) L=${S#c4:}; GMAPDP_LIB=$PWD/gmap-2024_amd/$L/libgmapdp.so timeout -k 10 600 python bench.py --steps 10 --config 4 --no-cpu-baseline > $O/c4_$L.json 2> $O/c4_$L.err || exit 15 ;;
     bx:*) X=${S#bx:}; T=${X%%:*}; A=${X#*:}; timeout -k 10 600 python bench.py --steps 10 --no-cpu-baseline $A > $O/bx_$T.json 2> $O/bx_$T.err || exit 23 ;;
