@@ -169,9 +169,11 @@ def profile_record(kind, name):
     return (best[1], best[2]) if best else (None, None)
 
 
-def pmc_entry(key):
-    """The cited PMC summary's record of kernel `key` ('+'-joined names are summed), or (None, None)."""
-    d, src = profile_record("pmc_summary", "pmc_summary.json")
+def pmc_entry(key, kind="pmc_summary"):
+    """The cited PMC summary's record of kernel `key` ('+'-joined names are summed), or (None, None).
+    kind: "pmc_summary" (the nosimd step) or "pmc_summary_simd" (the --simd step), as profiles/current.json
+    names them."""
+    d, src = profile_record(kind, "pmc_summary.json")
     if not d:
         return None, None
     ks = d.get("kernels", {})
@@ -185,10 +187,10 @@ def pmc_entry(key):
     return rec, src
 
 
-def iso_entry(key):
+def iso_entry(key, kind="iso_summary"):
     """The cited rocprofv3 --kernel-trace --stats record of `bench.py --iso-kernel <key>` (the dominant
     kernel's launches run alone, tools/pmc_summary.py --iso): {avg_duration_ns, dispatches, ...}."""
-    d, src = profile_record("iso_summary", "iso_summary.json")
+    d, src = profile_record(kind, "iso_summary.json")
     if not d or d.get("kernel") != key:
         return None, src
     return d, src
@@ -668,7 +670,10 @@ def main():
     progress("headline %.2f ms per step" % (elapsed / args.steps * 1e3))
     half = max(2, args.steps // 4)
     el_dp, _ = timed(half, 1, do_oligo=False)
-    el_o, _ = timed(half, 1, do_dp=False)
+    el_o, evs_o = timed(half, 1, do_dp=False)
+    # stage 2 alone, split at the seeding / chaining boundary (HIP events on its stream)
+    s2_seed_ms = float(np.mean([e["oligo"][0].elapsed_time(e["oligo"][1]) for e in evs_o]))
+    s2_chain_ms = float(np.mean([e["oligo"][1].elapsed_time(e["chain"][1]) for e in evs_o]))
 
     # ---- per-launch times of the timed steps, by kernel template ----
     per_kernel = {}   # name -> [ms total, dispatches, algorithmic bytes total]
@@ -730,11 +735,11 @@ def main():
     kbytes = iso_bytes / iso_n
     kcells = iso_cells / iso_n
     ach = kbytes / (kms * 1e-3) / 1e9
-    pmc, psrc = pmc_entry(dominant)
+    pmc, psrc = pmc_entry(dominant, "pmc_summary_simd" if args.simd else "pmc_summary")
     traffic = pmc["hbm_bytes_per_dispatch"] if pmc else None
     valu = pmc["sq_SQ_INSTS_VALU_sum_avg"] if pmc else None
     prof_ms = pmc["avg_duration_ns"] / 1e6 if pmc and pmc.get("avg_duration_ns") else None
-    iso, isrc = iso_entry(dominant)
+    iso, isrc = iso_entry(dominant, "iso_summary_simd" if args.simd else "iso_summary")
     iso_prof_ms = iso["avg_duration_ns"] / 1e6 if iso else None
 
     # ---- PCIe: one block's inputs up and outputs down through pinned host memory (outside the step) ----
@@ -830,7 +835,8 @@ def main():
                              "required, the VALU issue and algorithmic int-op fractions are the binding bounds "
                              "(BASELINE.md §3(i))"},
         "gcups": cells_total / len(B) * world * args.steps / elapsed / 1e9,
-        "step_split_ms": {"stage2_alone": el_o / half * 1e3, "dynprog_alone": el_dp / half * 1e3,
+        "step_split_ms": {"stage2_alone": el_o / half * 1e3, "stage2_alone_seeding": s2_seed_ms,
+                          "stage2_alone_chaining": s2_chain_ms, "dynprog_alone": el_dp / half * 1e3,
                           "together": ms_step},
         "launch_classes": sorted(({"kernel": n, "dispatches": e[1], "ms_per_step": round(e[0] / args.steps, 4)}
                                   for n, e in per_kernel.items()), key=lambda x: -x["ms_per_step"]),

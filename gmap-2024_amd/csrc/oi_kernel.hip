@@ -133,9 +133,13 @@ __device__ __forceinline__ int seg_scan_min(int lane, int x, int e, int segstart
   return x;
 }
 
+constexpr int kOiHist = 4 * 256;  // = 2 x 512
+
 // Returns false (nothing written) when the shared event pool could not hold this problem's 3 E slots
 // (oi_kernel took them, `base`, with one atomic as it finished).
-// maxdiag bounds every diagi (querylength + genomiclength); hist is 4 x 256 LDS counters.
+// maxdiag bounds every diagi (querylength + genomiclength); hist holds kOiHist LDS counters: the digits
+// are 9 bits wide when maxdiag < 2^18 (2 passes of 512 buckets: a 214-kb window), else 8 bits (at most 4
+// passes of 256).  (More LDS would cost oi_map_kernel a wave per SIMD.)
 __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t maxdiag, uint32_t chrinit,
                                    int lookback, int suffn, const int32_t* __restrict__ npq,
                                    const int32_t* __restrict__ mpq, const int* __restrict__ cum,
@@ -147,9 +151,11 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
   uint64_t* evA = pool + base;                      // events (diagi << 32 | q)
   uint64_t* evB = evA + E;                          // radix-sort ping-pong
   int4* grec = reinterpret_cast<int4*>(evB + E);    // good records (at most E / 2)
-  int npass = 0;                                    // 8-bit digits of the largest possible diagi
-  while (npass < 4 && (maxdiag >> (8 * npass)) != 0) npass++;
-  for (int i = lane; i < 4 * 256; i += 64) hist[i] = 0u;
+  const int db = maxdiag < (1u << 18) ? 9 : 8;       // digit bits
+  const uint32_t dmask = (1u << db) - 1u;
+  int npass = 0;                                    // digits of the largest possible diagi
+  while (npass < 4 && (maxdiag >> (db * npass)) != 0) npass++;
+  for (int i = lane; i < kOiHist; i += 64) hist[i] = 0u;
   __syncthreads();
 
   // Events in query order, hits of one querypos in table (ascending chrpos) order, 256 query
@@ -209,14 +215,14 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
         // one LDS atomic per distinct digit: the hits of a group mostly share a few diagonals, and
         // same-address atomics serialise
         for (int p = 0; p < npass; p++) {
-          const uint32_t dg = (di >> (8 * p)) & 255u;
+          const uint32_t dg = (di >> (db * p)) & dmask;
           uint64_t eq = ballot(v);
 #pragma unroll
-          for (int b = 0; b < 8; b++) {
+          for (int b = 0; b < 9; b++) {  // (bit 8 of an 8-bit digit is 0 in every lane)
             const uint64_t m = ballot((dg >> b) & 1u);
             eq &= ((dg >> b) & 1u) ? m : ~m;
           }
-          if (v && lanes_below(eq, lane) == 0) atomicAdd(&hist[256 * p + dg], (uint32_t)__popcll(eq));
+          if (v && lanes_below(eq, lane) == 0) atomicAdd(&hist[(dmask + 1) * p + dg], (uint32_t)__popcll(eq));
         }
       }
     }
@@ -231,19 +237,20 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
   uint64_t* src = evA;
   uint64_t* dst = evB;
   for (int p = 0; p < npass; p++) {
-    uint32_t* hp = hist + 256 * p;
-    const int shift = 8 * p;
-    uint32_t h4[4], hs = 0;
+    uint32_t* hp = hist + (dmask + 1) * p;
+    const int shift = db * p;
+    const int cpl = (int)(dmask + 1) / 64;  // buckets per lane: 8 or 4
+    uint32_t h8[8], hs = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      h4[k] = hp[4 * lane + k];
-      hs += h4[k];
+    for (int k = 0; k < 8; k++) {
+      h8[k] = k < cpl ? hp[cpl * lane + k] : 0u;
+      hs += h8[k];
     }
     uint32_t at = (uint32_t)wave_scan_add(lane, (int)hs) - hs;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      hp[4 * lane + k] = at;
-      at += h4[k];
+    for (int k = 0; k < 8; k++) {
+      if (k < cpl) hp[cpl * lane + k] = at;
+      at += h8[k];
     }
     __syncthreads();
     // 256 keys per step: their 4 loads and 4 stores each go out together (one memory round trip per
@@ -259,10 +266,10 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const bool v = e0 + 64 * r + lane < E;
-        const uint32_t d = (uint32_t)(key[r] >> (32 + shift)) & 255u;
+        const uint32_t d = (uint32_t)(key[r] >> (32 + shift)) & dmask;
         uint64_t eq = ballot(v);
 #pragma unroll
-        for (int b = 0; b < 8; b++) {
+        for (int b = 0; b < 9; b++) {
           const uint64_t m = ballot((d >> b) & 1u);
           eq &= ((d >> b) & 1u) ? m : ~m;
         }
@@ -684,14 +691,14 @@ __global__ __launch_bounds__(64) void oi_kernel(
 }
 
 // ---- Oligoindex_get_mappings' diagonal state machine, one wave per problem, after oi_kernel ----
-// A kernel of its own: its only LDS is the 1-KB radix histogram, so many more waves share a CU and
-// hide the L2 latency of the event passes than oi_kernel's query tables would allow.
+// A kernel of its own: its only LDS is the radix histogram and the event step's offsets, so many more
+// waves share a CU and hide the L2 latency of the event passes than oi_kernel's query tables would allow.
 __global__ __launch_bounds__(64) void oi_map_kernel(
     const DevOligoProblem* __restrict__ probs, unsigned char* __restrict__ scratch,
     gmapdp_oligo_result* __restrict__ results, const int32_t* __restrict__ npos_out,
     const int32_t* __restrict__ map_out, const uint32_t* __restrict__ table_all, int32_t* __restrict__ diag_all,
     uint64_t* __restrict__ pool) {
-  __shared__ uint32_t hist[4 * 256];
+  __shared__ uint32_t hist[kOiHist];
   __shared__ int evq[2 * 256];
   const int lane = threadIdx.x;
   const DevOligoProblem P = probs[blockIdx.x];

@@ -89,7 +89,7 @@ struct S2Path {
   uint32_t start, end;  // genomepos of the first and last pair of the converted list
 };
 struct S2Scratch {
-  size_t diff, run, off, minact, maxact, first, proc, diags, ord, tmp, hits, cand, keep, paths, pq, ph, sbuf, total;
+  size_t diff, run, off, minact, maxact, first, proc, diags, ord, tmp, hits, cand, keep, paths, pq, ph, lh, sbuf, total;
   int sortn;  // power of two >= every sorted array
 };
 __host__ __device__ inline int s2_pow2(int n) {
@@ -116,8 +116,9 @@ __host__ __device__ inline S2Scratch s2_scratch(int ql, int T, int nd) {
   s.paths = align16(s.keep + 4 * H);
   s.pq = align16(s.paths + sizeof(S2Path) * H);
   s.ph = align16(s.pq + 4 * Q);
+  s.lh = align16(s.ph + 4 * Q);  // the sweep's active range per position: low[Q], high[Q] (s2a_kernel)
   s.sortn = s2_pow2((int)(H > D ? H : D));
-  s.sbuf = align16(s.ph + 4 * Q);
+  s.sbuf = align16(s.lh + 8 * Q);
   s.total = align16(s.sbuf + 4 * (size_t)s.sortn);
   return s;
 }
@@ -954,8 +955,8 @@ __device__ __forceinline__ void s2_run_write(S2Hit* hits, int* alist, int lane, 
 }
 
 // the sweep (stage2.c:3746-4080)
-__device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, const uint32_t* minact, const uint32_t* maxact,
-                         int qstart, int qend) {
+__device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, const int* lowa, const int* higha,
+                                         const uint32_t* rmapa, int qstart, int qend) {
   const int lane = W.lane;
   auto npos = [&](int q) { return q < nq ? npq[q] : 0; };
   int q = 0, np = 0;
@@ -980,11 +981,10 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
       specific_low = 0, specific_high = 0;
   uint32_t grand_map = 0;
   S2E last = {0, 0, 0, 0, false};
-  // per-position metadata for the chunk [cb, cb + 64): npositions, off, minactive, maxactive, first map
-  // and per position the hits inside [minactive, maxactive]: [m_low, m_high) (the hits ascend in chrpos, so
-  // two binary searches per lane), m_rmap the first of them
+  // per-position metadata for the chunk [cb, cb + 64): npositions, off, and the hits inside [minactive,
+  // maxactive]: [m_low, m_high), m_rmap the first of them (s2a_kernel's binary searches)
   int cb = -1, m_n = 0, m_off = 0, m_low = 0, m_high = 0;
-  uint32_t m_min = 0, m_max = 0, m_map0 = 0, m_rmap = 0;
+  uint32_t m_rmap = 0;
 #ifdef GMAPDP_OI_TIMING
   unsigned long long t_one = 0, t_mult = 0, t_tail = 0, t_meta = 0, t0c = 0;
 #define S2_T0() t0c = wall_clock64()
@@ -1000,33 +1000,12 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
     if ((q & ~63) != cb) {
       cb = q & ~63;
       const int qq = cb + lane;
+      const bool in = qq <= qend;
       m_n = qq < nq ? npq[qq] : 0;
       m_off = qq <= qend + 1 ? W.off[qq] : 0;
-      m_min = qq <= qend ? minact[qq] : 0u;
-      m_max = qq <= qend ? maxact[qq] : 0u;
-      m_map0 = m_n > 0 ? W.hits[m_off].map : 0u;
-      m_low = m_high = 0;
-      m_rmap = m_map0;
-      if (m_n == 1) {
-        m_low = m_map0 < m_min ? 1 : 0;
-        m_high = (m_low == 0 && m_map0 <= m_max) ? 1 : m_low;
-      } else if (m_n > 1 && qq <= qend) {
-        int lo = m_map0 < m_min ? 1 : 0, hi = m_n;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (W.hits[m_off + mid].map < m_min) lo = mid + 1;
-          else hi = mid;
-        }
-        int lo2 = lo, hi2 = m_n;
-        while (lo2 < hi2) {
-          const int mid = (lo2 + hi2) >> 1;
-          if (W.hits[m_off + mid].map <= m_max) lo2 = mid + 1;
-          else hi2 = mid;
-        }
-        m_low = lo;
-        m_high = lo2 > lo ? lo2 : lo;
-        if (m_high > m_low) m_rmap = W.hits[m_off + m_low].map;
-      }
+      m_low = in ? lowa[qq] : 0;
+      m_high = in ? higha[qq] : 0;
+      m_rmap = in ? rmapa[qq] : 0u;
     }
     const int j = q - cb;
     // A run on the last processed entry's diagonal.  When that entry has one active hit whose consecutive
@@ -1085,10 +1064,6 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
     }
     const int n = __builtin_amdgcn_readlane(m_n, j);
     const int offq = __builtin_amdgcn_readlane(m_off, j);
-    const uint32_t mn = (uint32_t)__builtin_amdgcn_readlane((int)m_min, j);
-    const uint32_t mx = (uint32_t)__builtin_amdgcn_readlane((int)m_max, j);
-    (void)mn;
-    (void)mx;
     int low = __builtin_amdgcn_readlane(m_low, j), high = __builtin_amdgcn_readlane(m_high, j);
     if (high - low >= kS2MaxNactive && nskipped <= kS2MaxSkipped) {
       if (lane == 0) W.actn[q] = 0;
@@ -1875,8 +1850,19 @@ __global__ __launch_bounds__(64) void s2a_kernel(
   // 64 positions at a time: their offsets by a prefix scan, then their hits written in hit order, lane l
   // taking hit base + l (its position the last lane whose offset is <= the hit, a binary search over the
   // lanes), so each store instruction covers 64 consecutive records
+  //
+  // The same pass gives the sweep its active range per query position (stage2.c:1104-1110, 1488-1494):
+  // the hits of q inside [minactive, maxactive] are [low, high), rmap the first of them.  A position's hits
+  // ascend in chrpos, so low is the first hit with map >= minactive and high the first with
+  // map > max(maxactive, minactive - 1) (the search from low: an empty range when maxactive < minactive),
+  // each written by the one hit lane where the predicate turns true, or by the position's last hit (n)
+  // when it never does.  The sweep's chunk metadata is then one round of independent loads.
+  int* lowa = reinterpret_cast<int*>(S + so.lh);
+  int* higha = lowa + (ql + 1);
+  uint32_t* rmapa = reinterpret_cast<uint32_t*>(diff);  // (the coverage is done with diff)
   carry = 0;
   bool big = false;
+  uint32_t pmap = 0;  // the previous step's last hit (a position's hits may span two steps)
   for (int cb = 0; cb < ql; cb += 64) {
     const int q = cb + lane;
     const int v = q < nq ? npq[q] : 0;
@@ -1884,6 +1870,13 @@ __global__ __launch_bounds__(64) void s2a_kernel(
     const int o = incl - v;
     if (q < ql) off[q] = o;
     const int mq = q < nq && v > 0 ? mpq[q] : 0;
+    const bool act = q <= qend && v > 0;
+    const uint32_t qmn = act ? minact[q] : 0u, qmx0 = act ? maxact[q] : 0u;
+    const uint32_t qmx = (qmn > 0 && qmx0 < qmn - 1) ? qmn - 1 : qmx0;
+    if (q < ql && !act) {
+      lowa[q] = higha[q] = 0;
+      rmapa[q] = 0u;
+    }
     const int hend = __shfl(incl, 63, 64);
     for (int base = carry; base < hend; base += 64) {
       const int h = base + lane;
@@ -1893,15 +1886,34 @@ __global__ __launch_bounds__(64) void s2a_kernel(
         const int oj = __shfl(o, j + st, 64);
         if (oj <= h) j += st;
       }
-      const int oq = __shfl(o, j, 64), mj = __shfl(mq, j, 64);
+      const int oq = __shfl(o, j, 64), mj = __shfl(mq, j, 64), nj = __shfl(v, j, 64);
+      const uint32_t mn = (uint32_t)__shfl((int)qmn, j, 64), mx = (uint32_t)__shfl((int)qmx, j, 64);
+      const bool actj = __shfl(act ? 1 : 0, j, 64) != 0;
+      uint32_t map = 0u;
       if (h < hend) {
         S2Hit x;
-        x.map = table_all[mj + (h - oq)];
+        x.map = map = table_all[mj + (h - oq)];
         big |= (x.map >= 0x80000000u);
         x.consec = x.root = x.fpos = x.fhit = x.tracei = x.score = x.active = 0;  // CALLOC
         x.q = cb + j;
         hits[h] = x;
       }
+      uint32_t prev = (uint32_t)__shfl_up((int)map, 1, 64);
+      if (lane == 0) prev = pmap;
+      if (h < hend && actj) {
+        const int k = h - oq, qj = cb + j;
+        const bool first = k == 0, last = k == nj - 1;
+        if (map >= mn && (first || prev < mn)) {
+          lowa[qj] = k;
+          rmapa[qj] = map <= mx ? map : 0u;
+        } else if (last && map < mn) {
+          lowa[qj] = nj;
+          rmapa[qj] = 0u;
+        }
+        if (map > mx && (first || prev <= mx)) higha[qj] = k;
+        else if (last && map <= mx) higha[qj] = nj;
+      }
+      pmap = (uint32_t)__builtin_amdgcn_readlane((int)map, 63);
     }
     carry = hend;
   }
@@ -1983,7 +1995,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GMAPDP_S2B_W
     W.splicingp = P.splicingp;
     W.lane = lane;
     W.maxintronlen = P.maxintronlen;
-    s2_sweep(W, npq, nq, minact, maxact, qstart, qend);
+    const int* lowa = reinterpret_cast<const int*>(S + so.lh);
+    s2_sweep(W, npq, nq, lowa, lowa + (ql + 1), reinterpret_cast<const uint32_t*>(diff), qstart,
+             qend);  // low / high / rmap (s2a_kernel)
   }
   wave_sync();
 #ifdef GMAPDP_OI_TIMING

@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--trace", default=None, help="directory for the shim's per-batch traces (GMAPDP_SHIM_TRACE)")
     ap.add_argument("--configs", default="default:",
                     help="shim configurations for the GPU runs, 'name:VAR=V,VAR=V;name2:...' (environment overrides)")
+    ap.add_argument("--cpu-configs", default="cpu:",
+                    help="environment configurations for the unmodified program's runs, same syntax (e.g. the same "
+                         "malloc tunables as a GPU configuration, for a like-for-like comparison)")
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--thread-cpu", action="store_true", help="per-thread-name CPU seconds of each run")
     ap.add_argument("--prof", default=None,
@@ -54,12 +57,16 @@ def main():
     sams = {}
     cpu_t = [int(x) for x in a.threads.split(",")]
     gpu_t = [int(x) for x in (a.gpu_threads or a.threads).split(",")]
-    configs = []
-    for c in a.configs.split(";"):
-        name, _, kv = c.partition(":")
-        configs.append((name, dict(x.split("=", 1) for x in kv.split(",") if x)))
+    def parse_configs(spec):
+        out = []
+        for c in spec.split(";"):
+            name, _, kv = c.partition(":")
+            out.append((name, dict(x.split("=", 1) for x in kv.split(",") if x)))
+        return out
+    configs = parse_configs(a.configs)
     pv = "prof_" if a.prof else ""
-    runs = [] if a.skip_cpu else [("gmap_%s%s" % (pv, a.build), t, "cpu", {}) for t in cpu_t]
+    runs = [] if a.skip_cpu else [("gmap_%s%s" % (pv, a.build), t, name, cenv)
+                                  for name, cenv in parse_configs(a.cpu_configs) for t in cpu_t]
     runs += [("gmap_gpu_%s%s" % (pv, a.build), t, name, cenv) for name, cenv in configs for t in gpu_t]
     profs = []
     out["dispatchers"] = a.dispatchers
@@ -110,7 +117,7 @@ def main():
                                 "cpu_seconds": cpu, "cpu_cores_busy": cpu / dt,
                                 "shim_calls": stats[0] if stats else None, "thread_cpu_s": threads})
             print(json.dumps(out["runs"][-1]), file=sys.stderr, flush=True)
-    base = next(iter(sams.values())) if a.skip_cpu else sams[("gmap_%s%s" % (pv, a.build), min(cpu_t), "cpu")]
+    base = next(iter(sams.values())) if a.skip_cpu else next(v for k, v in sams.items() if k[0] == "gmap_%s%s" % (pv, a.build))
     out["outputs_identical"] = all(v == base for v in sams.values())
     out["recorded"] = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())  # bench.py selects records by this
     print(json.dumps(out))

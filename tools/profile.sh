@@ -3,6 +3,8 @@
 # Usage: bash tools/profile.sh <tag>                 -- the bench step (kernel stats + PMC passes)
 #        bash tools/profile.sh <tag> iso <kernel>    -- one kernel's launch classes run alone
 #                                                      (bench.py --iso-kernel: what the line's roofline times)
+#        bash tools/profile.sh <tag> simd            -- the --simd step (gmap.avx2 semantics)
+#        bash tools/profile.sh <tag> isosimd <kernel> -- as iso, in the --simd step
 # Summarise with: python3 tools/pmc_summary.py [--iso] gpurun_out/prof_<tag> profiles/<tag>
 set -o pipefail
 TAG=${1:-r1}
@@ -12,9 +14,11 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 # one process, no forked generator workers (a forked worker ending under rocprofv3 --pmc hung the pass)
 export GMAPDP_BENCH_WORKERS=1
-if [ "$MODE" = iso ]; then
+SIMD=()
+if [ "$MODE" = simd ] || [ "$MODE" = isosimd ]; then SIMD=(--simd); fi
+if [ "$MODE" = iso ] || [ "$MODE" = isosimd ]; then
   KERNEL=$3
-  BENCH=(python3 bench.py --iso-kernel "$KERNEL" --iso-reps 3)
+  BENCH=(python3 bench.py --iso-kernel "$KERNEL" --iso-reps 3 "${SIMD[@]}")
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- "${BENCH[@]}" > $OUT/iso_bench.json 2> $OUT/stats.log || exit 1
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- "${BENCH[@]}" > $OUT/fetch.log 2>&1 || exit 2
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- "${BENCH[@]}" > $OUT/write.log 2>&1 || exit 3
@@ -22,7 +26,7 @@ if [ "$MODE" = iso ]; then
   echo done
   exit 0
 fi
-BENCH=(python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline)
+BENCH=(python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline "${SIMD[@]}")
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- "${BENCH[@]}" > $OUT/stats.log 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- "${BENCH[@]}" > $OUT/fetch.log 2>&1 || exit 2
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- "${BENCH[@]}" > $OUT/write.log 2>&1 || exit 3
