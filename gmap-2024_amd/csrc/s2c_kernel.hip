@@ -74,9 +74,9 @@ __device__ unsigned int g_s2_wave[3][16384];  // per s2b wave: sweep duration (w
 // result status
 constexpr int kS2NoPositions = 0, kS2Coverage = 1, kS2Chained = 2, kS2Overflow = -2, kS2Domain = -3;
 
-struct S2Hit {  // struct Link_T (stage2.c:363) + fwd_scores + active, one per (querypos, hit)
+struct __attribute__((aligned(16))) S2Hit {  // struct Link_T (stage2.c:363) + fwd_scores, one per (querypos, hit)
   uint32_t map;
-  int consec, root, fpos, fhit, tracei, score, active, q;
+  int consec, root, fpos, fhit, tracei, score, q;  // 32 B: s2a's record stores cover whole cache lines
 };
 struct S2Diag {  // struct Diag_T (diagdef.h)
   uint32_t diagonal;
@@ -89,7 +89,8 @@ struct S2Path {
   uint32_t start, end;  // genomepos of the first and last pair of the converted list
 };
 struct S2Scratch {
-  size_t diff, run, off, minact, maxact, first, proc, diags, ord, tmp, hits, cand, keep, paths, pq, ph, lh, sbuf, total;
+  size_t diff, run, off, minact, maxact, first, proc, diags, ord, tmp, hits, maps, cand, keep, paths, pq, ph, lh, sbuf,
+      total;
   int sortn;  // power of two >= every sorted array
 };
 __host__ __device__ inline int s2_pow2(int n) {
@@ -111,7 +112,8 @@ __host__ __device__ inline S2Scratch s2_scratch(int ql, int T, int nd) {
   s.ord = align16(s.diags + sizeof(S2Diag) * D);
   s.tmp = align16(s.ord + 4 * D);
   s.hits = align16(s.tmp + 4 * D);
-  s.cand = align16(s.hits + sizeof(S2Hit) * H);
+  s.maps = align16(s.hits + sizeof(S2Hit) * H);  // the hits' chrpos again, 4 B each (the path walk's searches)
+  s.cand = align16(s.maps + 4 * H);
   s.keep = align16(s.cand + 4 * H);
   s.paths = align16(s.keep + 4 * H);
   s.pq = align16(s.paths + sizeof(S2Path) * H);
@@ -1859,6 +1861,7 @@ __global__ __launch_bounds__(64) void s2a_kernel(
   // when it never does.  The sweep's chunk metadata is then one round of independent loads.
   int* lowa = reinterpret_cast<int*>(S + so.lh);
   int* higha = lowa + (ql + 1);
+  uint32_t* mapsa = reinterpret_cast<uint32_t*>(S + so.maps);
   uint32_t* rmapa = reinterpret_cast<uint32_t*>(diff);  // (the coverage is done with diff)
   carry = 0;
   bool big = false;
@@ -1894,9 +1897,10 @@ __global__ __launch_bounds__(64) void s2a_kernel(
         S2Hit x;
         x.map = map = table_all[mj + (h - oq)];
         big |= (x.map >= 0x80000000u);
-        x.consec = x.root = x.fpos = x.fhit = x.tracei = x.score = x.active = 0;  // CALLOC
+        x.consec = x.root = x.fpos = x.fhit = x.tracei = x.score = 0;  // CALLOC
         x.q = cb + j;
         hits[h] = x;
+        mapsa[h] = map;
       }
       uint32_t prev = (uint32_t)__shfl_up((int)map, 1, 64);
       if (lane == 0) prev = pmap;
@@ -2032,7 +2036,8 @@ struct S2WalkOut {
 // position q - k with map - k (a binary search in that position's hits, which ascend), and the guesses
 // hold while each one is its predecessor's link (fpos, fhit); the walk goes on from the last holding
 // node's real link.  Same nodes, order and outputs as s2_walk.
-__device__ S2WalkOut s2_walk_diag(const S2Hit* hits, const int* off, int gi, int lane, int* pq, int* ph) {
+__device__ S2WalkOut s2_walk_diag(const S2Hit* hits, const uint32_t* maps, const int* off, int gi, int lane, int* pq,
+                                  int* ph) {
   S2WalkOut o = {0, -1, -1};
   while (gi >= 0 && hits[gi].consec < kS2MinTerminal) {  // prune the 3' end
     const int fq = hits[gi].fpos;
@@ -2048,12 +2053,13 @@ __device__ S2WalkOut s2_walk_diag(const S2Hit* hits, const int* off, int gi, int
     } else if (p >= 0) {
       const uint32_t target = mn - (uint32_t)lane;
       int lo = off[p], hi = off[p + 1];
-      while (lo < hi) {
+      const int end = hi;
+      while (lo < hi) {  // (4 B per hit: a step's 64 searches touch ~1 KB, not the 36-B records' ~9 KB)
         const int mid = (lo + hi) >> 1;
-        if (hits[mid].map < target) lo = mid + 1;
+        if (maps[mid] < target) lo = mid + 1;
         else hi = mid;
       }
-      if (lo < off[p + 1] && hits[lo].map == target) idx = lo;
+      if (lo < end && maps[lo] == target) idx = lo;
     }
     int pred = -1;
     uint32_t mx = 0x80000000u;
@@ -2122,7 +2128,11 @@ __device__ S2WalkOut s2_walk_wave(const uint32_t* lql, const uint32_t* map, int 
   }
 }
 
-// cells, traceback_one, Stage2_filter_unique, convert_to_nucleotides
+// cells, traceback_one, Stage2_filter_unique, convert_to_nucleotides.  Two launches over the same order:
+// kLdsWalk = false takes the calls whose link table does not fit LDS (more than kS2cCap hits: every 214-kb
+// window) with no LDS reserved, so 6 waves per SIMD run (32 KB of LDS allowed 5 per CU); kLdsWalk = true
+// takes the rest with the 32-KB link table.
+template <bool kLdsWalk>
 __global__ __launch_bounds__(64) void s2c_kernel(
     const DevStage2Problem* __restrict__ probs, const uint32_t* __restrict__ blocks, uint64_t nwords,
     const char* __restrict__ qseq, const char* __restrict__ quc, const gmapdp_oligo_result* __restrict__ ores,
@@ -2151,6 +2161,7 @@ __global__ __launch_bounds__(64) void s2c_kernel(
   int* ord = reinterpret_cast<int*>(S + so.ord);
   int* tmp = reinterpret_cast<int*>(S + so.tmp);
   S2Hit* hits = reinterpret_cast<S2Hit*>(S + so.hits);
+  const uint32_t* maps = reinterpret_cast<const uint32_t*>(S + so.maps);
   int* cand = reinterpret_cast<int*>(S + so.cand);
   int* keep = reinterpret_cast<int*>(S + so.keep);
   S2Path* pth = reinterpret_cast<S2Path*>(S + so.paths);
@@ -2163,6 +2174,7 @@ __global__ __launch_bounds__(64) void s2c_kernel(
   (void)diag_all; (void)counters; (void)scratch_cap; (void)paths_out; (void)path_cap; (void)pairs_out; (void)pair_cap;
   gmapdp_stage2_result R = results[P.index];
   if (R.status != kS2Chained) return;
+  if ((T <= kS2cCap && nq <= 65536) != kLdsWalk) return;  // the other launch's call
   S2_MARK(12);
   const int qstart = R.diag_querystart, qend = R.diag_queryend;
   // ---- get_cells_fwd + the path loop: cells within FINAL_SCORE_TOLERANCE of the best, each the best
@@ -2251,7 +2263,7 @@ __global__ __launch_bounds__(64) void s2c_kernel(
   extern __shared__ uint32_t s2c_lds[];
   uint32_t* llq = s2c_lds;
   uint32_t* lmap = s2c_lds + kS2cCap;
-  const bool lds_walk = T <= kS2cCap && nq <= 65536;  // link words: 15-bit hit index, 16-bit querypos
+  const bool lds_walk = kLdsWalk;  // T <= kS2cCap && nq <= 65536 (checked above): 15-bit hit index, 16-bit querypos
   if (lds_walk && npaths > 0) {
     // four hits per lane per step: their loads, then their off[] gathers, overlap
     for (int b0 = lane; b0 < T; b0 += 256) {
@@ -2299,7 +2311,7 @@ __global__ __launch_bounds__(64) void s2c_kernel(
     int n = 0, top = -1, bottom = -1;
     if (lds_walk || nq <= 65536) {
       const S2WalkOut o = lds_walk ? s2_walk_wave(llq, lmap, cell, lane, single ? pathq : nullptr, pathh)
-                                   : s2_walk_diag(hits, off, cell, lane, single ? pathq : nullptr, pathh);
+                                   : s2_walk_diag(hits, maps, off, cell, lane, single ? pathq : nullptr, pathh);
       n = o.n;
       top = o.top;
       bottom = o.bottom;
@@ -2381,7 +2393,7 @@ __global__ __launch_bounds__(64) void s2c_kernel(
     const int n = x.n;
     if (!single && (lds_walk || nq <= 65536)) {  // entries, 3' end first
       if (lds_walk) (void)s2_walk_wave(llq, lmap, x.cell, lane, pathq, pathh);
-      else (void)s2_walk_diag(hits, off, x.cell, lane, pathq, pathh);
+      else (void)s2_walk_diag(hits, maps, off, x.cell, lane, pathq, pathh);
     } else if (lane == 0 && !single) {
       int e = 0;
       {
@@ -2539,11 +2551,14 @@ hipError_t launch_s2c(int nproblems, hipStream_t stream, const DevStage2Problem*
     e = hipLaunchKernel(reinterpret_cast<void*>(&s2a_kernel), dim3(nproblems), dim3(64), args, 0, stream);
   if (e == hipSuccess)
     e = hipLaunchKernel(reinterpret_cast<void*>(&s2b_kernel), dim3(nproblems), dim3(64), args, 0, stream);
+  if (e == hipSuccess)  // the heavy calls (first in the order) without LDS, then the rest with the link table
+    e = hipLaunchKernel(reinterpret_cast<void*>(&s2c_kernel<false>), dim3(nproblems), dim3(64), args, 0, stream);
   if (e == hipSuccess)
-    e = hipFuncSetAttribute(reinterpret_cast<void*>(&s2c_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+    e = hipFuncSetAttribute(reinterpret_cast<void*>(&s2c_kernel<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(8 * kS2cCap));
   if (e == hipSuccess)
-    e = hipLaunchKernel(reinterpret_cast<void*>(&s2c_kernel), dim3(nproblems), dim3(64), args, 8 * kS2cCap, stream);
+    e = hipLaunchKernel(reinterpret_cast<void*>(&s2c_kernel<true>), dim3(nproblems), dim3(64), args, 8 * kS2cCap,
+                        stream);
   return e;
 }
 

@@ -32,6 +32,7 @@ for S in "$@"; do
     benchfull) timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err || exit 16 ;;
     iso:*) bash tools/profile.sh ${TAG}_iso iso "${S#iso:}" > $O/prof_iso.txt 2>&1 || exit 17 ;;
     prof) bash tools/profile.sh $TAG > $O/prof.txt 2>&1 || exit 18 ;;
+    profs2) bash tools/profile_s2.sh ${TAG}_s2 > $O/profs2.txt 2>&1 || exit 30 ;;
     profsimd) bash tools/profile.sh ${TAG}_simd simd > $O/profsimd.txt 2>&1 || exit 28 ;;
     isosimd:*) bash tools/profile.sh ${TAG}_isosimd isosimd "${S#isosimd:}" > $O/prof_isosimd.txt 2>&1 || exit 29 ;;
     e2e:*) IFS=: read -r _ B N T C <<< "$S"; timeout -k 10 900 python tools/e2e_timing.py --build $B --reads $N --threads 16 --gpu-threads ${T:-512} ${C:+--configs "$C"} > $O/e2e_${B}_$N.json 2> $O/e2e_${B}_$N.err || exit 20 ;;

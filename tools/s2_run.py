@@ -1,6 +1,7 @@
-"""Runs gmapdp_stage2_batch twice on bench.py's Stage2_compute stream (chr22 layout, --reads reads);
-the driver for rocprofv3 passes over s2c_kernel (tools/profile_s2.sh).  Prints the second run's wall
-time."""
+"""Runs gmapdp_stage2_batch twice on bench.py's Stage2_compute calls (chr22 layout, the configs[2] read
+shape and `gmap -d` windows, locus +- ~100 kb: workload.CDNA2K; `appb` as a second argument: App. B's
+locus +- 1 kb); the driver for rocprofv3 passes over the stage-2 kernels alone (tools/profile_s2.sh).
+Prints the second run's wall time."""
 import os
 import sys
 import time
@@ -13,12 +14,16 @@ import gmapdp  # noqa: E402
 from gmapdp import workload as W  # noqa: E402
 
 
-def main(reads=10000):
+def main(reads=10000, mix="d"):
     layout = W.Layout(W.CHR22)
     genome = W.make_genome(layout, seed=22)
     eng = gmapdp.Engine(0)
     eng.set_genome(genome.tobytes())
-    op, oq = W.make_stage2(genome, layout, reads, np.random.default_rng(3000))
+    if mix == "appb":
+        op, oq = W.make_stage2(genome, layout, reads, np.random.default_rng(3000))
+    else:
+        sh = W.CDNA2K
+        op, oq = W.make_stage2(genome, layout, reads, np.random.default_rng(3000), pad=sh.pad, extra=sh.stage2 - 1.0)
     calls = [dict(quc=oq[int(p["qoff"]):int(p["qoff"]) + int(p["querylength"])].tobytes(),
                   **{k: int(p[k]) for k in ("chrstart", "chrend", "chroffset", "chrhigh", "plusp")}) for p in op]
     probs, qb, qub = eng.build_stage2_batch(calls)
@@ -31,4 +36,4 @@ def main(reads=10000):
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]) if len(sys.argv) > 1 else 10000)
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 10000, sys.argv[2] if len(sys.argv) > 2 else "d")
