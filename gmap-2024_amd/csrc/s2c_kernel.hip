@@ -811,11 +811,10 @@ __device__ __forceinline__ S2Best s2_one(S2W& W, int q, uint32_t position, int n
       st = s2_dloop_multi(W, pf, np, kmax, q, position, b, W.splicingp != 0, false, fdummy, lt);
       if (st == 2) from = 64;
     } else if (!st) {  // entries with several hits: groups of entries whose hits fit the wave
-      S2Pref pg;
+      S2Pref pg = pf;  // (a value, not a reference chosen at run time: that kept both windows in scratch)
       for (;;) {
-        const S2Pref& pw = from ? pg : pf;
         int nb = from;
-        st = s2_dloop_multi(W, pw, np, kmax, q, position, b, W.splicingp != 0, false, fdummy, lt, from, &nb);
+        st = s2_dloop_multi(W, pg, np, kmax, q, position, b, W.splicingp != 0, false, fdummy, lt, from, &nb);
         if (st != 2) break;
         from = nb;
         pg.load(W, np, from);
@@ -1243,10 +1242,10 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
               lt = -1;
               st = 2;
             }
-            S2Pref pg;
+            S2Pref pg = pf;  // (a value: a reference chosen at run time kept both windows in scratch)
             while (st == 2 && from <= kmax) {
               if (from) pg.load(W, np, from);
-              const S2Pref& pw = from ? pg : pf;
+              const S2Pref& pw = pg;
               const int ke = min(kmax - from, 63);
               int fg = lane <= ke ? s2_fr[from + lane] : -1;
               int nb = from;
