@@ -252,15 +252,17 @@ def like_for_like(out, pcie_ms, up, down):
                     "program on the same reads and cores (tools/e2e_timing.py)"}
 
 
-def cpu_baselines(mix):
+def cpu_baselines(mix, config=2):
     """tools/cpu_baseline.py as a child process (the reference's own objects, all usable host cores,
-    AVX2 and nosimd builds, the bench's call mix); {build: result or None}."""
+    AVX2 and nosimd builds, the bench's call mix: configs[1] times the single and end gaps alone);
+    {build: result or None}."""
     out = {}
     for build in ("avx2", "nosimd"):
         progress("CPU baseline (%s build)" % build)
         try:
             r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "cpu_baseline.py"), "--build", build,
-                                "--budget", "10", "--mix", mix], capture_output=True, timeout=240, text=True)
+                                "--budget", "10", "--mix", mix, "--config", str(config)],
+                               capture_output=True, timeout=240, text=True)
             out[build] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else None
         except (subprocess.TimeoutExpired, ValueError, IndexError):
             out[build] = None
@@ -307,6 +309,8 @@ def launch_ranks(n):
 # ---------------------------------------------------------------------------------------------------
 def config_of(args):
     from gmapdp import workload as W
+    if args.config == 1:  # "100k synthetic 2-kb cDNA vs human chr22, Dynprog_single + Dynprog_end only"
+        return W.Layout(W.CHR22), W.SHAPES[args.mix], "chr22"
     if args.config == 4:
         return W.Layout(W.WHEAT17), (W.ISOSEQ5K if args.mix == "d" else W.ISOSEQ5K_G), "wheat17"
     shape = W.SHAPES[args.mix]
@@ -326,6 +330,10 @@ def make_stream(args, rank, world):
     W.plant_stream(genome, layout, args.reads, range(world * args.batches), shape)
     workers = int(os.environ.get("GMAPDP_BENCH_WORKERS", "0")) or max(1, min(args.batches, 16 // world))
     data = W.make_blocks(genome, layout, args.reads, mine, shape=shape, sprob=False, workers=workers)
+    if args.config == 1:  # configs[1] times the single and end gaps alone
+        for d in data:
+            for k in ("genome", "microexon", "oligo"):
+                d[k] = d[k][:0]
     progress("genome (%s, %d nt) and %d blocks of %d reads ready (%.0f s, %d workers)"
              % (gname, layout.total, len(mine), args.reads, time.perf_counter() - t0, workers))
     return layout, shape, gname, genome, mine, data, time.perf_counter() - t0
@@ -362,8 +370,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--reads", type=int, default=None,
                     help="reads per step per GPU (one block; default 10000, 2000 for --config 4's 5-kb reads)")
-    ap.add_argument("--batches", type=int, default=8, help="distinct read blocks per rank, cycled over the steps")
-    ap.add_argument("--config", type=int, default=2, choices=[2, 4], help="BASELINE.json configs index")
+    ap.add_argument("--batches", type=int, default=None,
+                    help="distinct read blocks per rank, cycled over the steps (default 8; 10 for --config 1)")
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 4],
+                    help="BASELINE.json configs index: 1 = chr22, Dynprog_single + Dynprog_end only (10 blocks of "
+                         "10 000 reads: 100 k distinct reads per cycle); 2 = GRCh38, full stage 2 + every Dynprog_* "
+                         "family (default); 4 = gmapl, 5-kb Iso-Seq reads vs a 17-Gnt wheat layout")
     ap.add_argument("--genome", default="grch38", choices=["grch38", "chr22"], help="configs[2] genome layout")
     ap.add_argument("--simd", action="store_true", help="the SIMD builds' semantics (gmap.avx2: sx/uxe/uxg kernels)")
     ap.add_argument("--mix", default="d", choices=["d", "appb"],
@@ -380,6 +392,8 @@ def main():
 
     if args.reads is None:
         args.reads = 2000 if args.config == 4 else 10000
+    if args.batches is None:
+        args.batches = 10 if args.config == 1 else 8
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -442,22 +456,26 @@ def main():
         s2p["splicingp"] = 1
         s2p["maxintronlen"] = 500000
         t0 = time.perf_counter()
-        oplan = C.c_void_p()
-        eng._check(lib.gmapdp_stage2_plan_create(eng.h, s2p.ctypes.data, len(s2p), d["oq"].ctypes.data,
-                                                 d["oq"].ctypes.data, len(d["oq"]), C.byref(oplan)),
-                   "gmapdp_stage2_plan_create")
+        oplan = None
+        if len(s2p):
+            oplan = C.c_void_p()
+            eng._check(lib.gmapdp_stage2_plan_create(eng.h, s2p.ctypes.data, len(s2p), d["oq"].ctypes.data,
+                                                     d["oq"].ctypes.data, len(d["oq"]), C.byref(oplan)),
+                       "gmapdp_stage2_plan_create")
         t_oplan += time.perf_counter() - t0
         blk["oplan"] = oplan
         # Dynprog_microexon_int per read (stage3.c:9664) over genome-gap gaps: search + choice
-        mplan = C.c_void_p()
-        eng._check(lib.gmapdp_microexon_plan_create(eng.h, mp.ctypes.data, len(mp), d["q"].ctypes.data,
-                                                    d["q"].ctypes.data, len(d["q"]), C.byref(mplan)),
-                   "gmapdp_microexon_plan_create")
+        mplan = None
+        if len(mp):
+            mplan = C.c_void_p()
+            eng._check(lib.gmapdp_microexon_plan_create(eng.h, mp.ctypes.data, len(mp), d["q"].ctypes.data,
+                                                        d["q"].ctypes.data, len(d["q"]), C.byref(mplan)),
+                       "gmapdp_microexon_plan_create")
         blk["mplan"] = mplan
-        blk["ncands"] = lib.gmapdp_microexon_plan_candidates(mplan)
+        blk["ncands"] = lib.gmapdp_microexon_plan_candidates(mplan) if mplan else 0
         blk["ngpu"], blk["nggpu"] = lib.gmapdp_plan_gpu_problems(plan), lib.gmapdp_plan_genome_gpu_problems(plan)
         blk["cap"] = lib.gmapdp_plan_pair_capacity(plan)
-        blk["mcap"] = lib.gmapdp_microexon_plan_pair_capacity(mplan)
+        blk["mcap"] = lib.gmapdp_microexon_plan_pair_capacity(mplan) if mplan else 0
         nl = lib.gmapdp_plan_nlaunches(plan)
         blk["info"], blk["kinds"], blk["lstream"] = [], [], []
         for li in range(nl):
@@ -513,6 +531,7 @@ def main():
                                                  what, C.c_void_p(s.cuda_stream)), "gmapdp_microexon_plan_run")
 
     def step(b, do_oligo=True, do_dp=True, ev=None):
+        do_oligo = do_oligo and b["oplan"] is not None
         fork = torch.cuda.Event()
         fork.record(stream)
         used = set()
@@ -544,7 +563,8 @@ def main():
                 used.add(len(sides))
             if ev is not None:
                 ev["mx"][0].record(ms)
-            mrun(b, ms, 3)
+            if b["mplan"] is not None:
+                mrun(b, ms, 3)
             if ev is not None:
                 ev["mx"][1].record(ms)
         for k in used:
@@ -654,8 +674,10 @@ def main():
                               "cells_per_launch": float(np.mean([r[2] for r in rows]))}), flush=True)
         for b in B:
             lib.gmapdp_plan_destroy(b["plan"])
-            lib.gmapdp_stage2_plan_destroy(b["oplan"])
-            lib.gmapdp_microexon_plan_destroy(b["mplan"])
+            if b["oplan"] is not None:
+                lib.gmapdp_stage2_plan_destroy(b["oplan"])
+            if b["mplan"] is not None:
+                lib.gmapdp_microexon_plan_destroy(b["mplan"])
         return
 
     # every block once before anything is timed: the context's grow-only scratch reaches its size
@@ -670,10 +692,13 @@ def main():
     progress("headline %.2f ms per step" % (elapsed / args.steps * 1e3))
     half = max(2, args.steps // 4)
     el_dp, _ = timed(half, 1, do_oligo=False)
-    el_o, evs_o = timed(half, 1, do_dp=False)
-    # stage 2 alone, split at the seeding / chaining boundary (HIP events on its stream)
-    s2_seed_ms = float(np.mean([e["oligo"][0].elapsed_time(e["oligo"][1]) for e in evs_o]))
-    s2_chain_ms = float(np.mean([e["oligo"][1].elapsed_time(e["chain"][1]) for e in evs_o]))
+    has_s2 = all(b["oplan"] is not None for b in B)
+    el_o = s2_seed_ms = s2_chain_ms = None
+    if has_s2:
+        el_o, evs_o = timed(half, 1, do_dp=False)
+        # stage 2 alone, split at the seeding / chaining boundary (HIP events on its stream)
+        s2_seed_ms = float(np.mean([e["oligo"][0].elapsed_time(e["oligo"][1]) for e in evs_o]))
+        s2_chain_ms = float(np.mean([e["oligo"][1].elapsed_time(e["chain"][1]) for e in evs_o]))
 
     # ---- per-launch times of the timed steps, by kernel template ----
     per_kernel = {}   # name -> [ms total, dispatches, algorithmic bytes total]
@@ -718,10 +743,13 @@ def main():
         b = B[k % len(B)]
         for li, name in enumerate(b["names"]):
             add(name, e["dp"][li][0].elapsed_time(e["dp"][li][1]), b["bytes"][li])
-        add("gmapdp::oi_kernel<unsigned short>+gmapdp::oi_map_kernel", e["oligo"][0].elapsed_time(e["oligo"][1]), None)
-        add("gmapdp::s2a_kernel+gmapdp::s2b_kernel+gmapdp::s2c_kernel", e["oligo"][1].elapsed_time(e["chain"][1]),
-            b["chain_bytes"])
-        add("gmapdp::mx_search_kernel+gmapdp::mx_finish_kernel", e["mx"][0].elapsed_time(e["mx"][1]), None)
+        if b["oplan"] is not None:
+            add("gmapdp::oi_kernel<unsigned short>+gmapdp::oi_map_kernel", e["oligo"][0].elapsed_time(e["oligo"][1]),
+                None)
+            add("gmapdp::s2a_kernel+gmapdp::s2b_kernel+gmapdp::s2c_kernel", e["oligo"][1].elapsed_time(e["chain"][1]),
+                b["chain_bytes"])
+        if b["mplan"] is not None:
+            add("gmapdp::mx_search_kernel+gmapdp::mx_finish_kernel", e["mx"][0].elapsed_time(e["mx"][1]), None)
     dominant = max((n for n in per_kernel if per_kernel[n][2] > 0 and "+" not in n), key=lambda n: per_kernel[n][0])
     dms, dn, dbytes = per_kernel[dominant]
 
@@ -770,6 +798,8 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     reads_total = args.reads * world * args.steps
     nsub = {k: int(np.mean([len(b["d"][k]) for b in B])) for k in ("oligo", "single", "end", "genome", "microexon")}
+    nsub_end3 = float(np.mean([int((b["d"]["end"]["end3p"] != 0).sum()) for b in B]))
+    nsub_end5 = nsub["end"] - nsub_end3
     out = {
         "metric": METRIC,
         "value": reads_total / elapsed,
@@ -788,14 +818,16 @@ def main():
                                "%.3g Stage2_compute calls (seeding + chaining, locus +- %d-nt windows) + %.1f "
                                "Dynprog_single_gap + %.1f "
                                "Dynprog_end5_gap + %.1f Dynprog_end3_gap + %.1f Dynprog_genome_gap + %.1f "
-                               "Dynprog_microexon_int (%s semantics); %d distinct blocks of %d reads cycled per rank; "
+                               "Dynprog_microexon_int (%s semantics)%s; %d distinct blocks of %d reads cycled per rank; "
                                "inputs HBM-resident; host stages 1/3 not in the step"
                                % (args.config, shape.readlength, "Iso-Seq-style" if args.config == 4 else "cDNA",
                                   shape.exons, shape.exlen, 100 * shape.subs, 100 * shape.indel, gname,
-                                  len(layout.lens), layout.total, layout.total - 1, shape.stage2, shape.pad,
-                                  shape.single, shape.end5,
-                                  shape.end3, shape.genome, shape.microexon, "gmap.avx2" if args.simd else "nosimd",
-                                  len(B), args.reads),
+                                  len(layout.lens), layout.total, layout.total - 1, nsub["oligo"] / args.reads,
+                                  shape.pad, nsub["single"] / args.reads,
+                                  nsub_end5 / args.reads, nsub_end3 / args.reads, nsub["genome"] / args.reads,
+                                  nsub["microexon"] / args.reads, "gmap.avx2" if args.simd else "nosimd",
+                                  " -- Dynprog_single + Dynprog_end only, as configs[1] names it" if args.config == 1
+                                  else "", len(B), args.reads),
                    "genome": gname, "reads_per_step_per_gpu": args.reads, "blocks_per_rank": len(B),
                    "call_mix_source": shape.source,
                    "subproblems_per_step_per_gpu": {"stage2_compute": nsub["oligo"], "single": nsub["single"],
@@ -835,7 +867,8 @@ def main():
                              "required, the VALU issue and algorithmic int-op fractions are the binding bounds "
                              "(BASELINE.md §3(i))"},
         "gcups": cells_total / len(B) * world * args.steps / elapsed / 1e9,
-        "step_split_ms": {"stage2_alone": el_o / half * 1e3, "stage2_alone_seeding": s2_seed_ms,
+        "step_split_ms": {"stage2_alone": el_o / half * 1e3 if el_o is not None else None,
+                          "stage2_alone_seeding": s2_seed_ms,
                           "stage2_alone_chaining": s2_chain_ms, "dynprog_alone": el_dp / half * 1e3,
                           "together": ms_step},
         "launch_classes": sorted(({"kernel": n, "dispatches": e[1], "ms_per_step": round(e[0] / args.steps, 4)}
@@ -858,11 +891,13 @@ def main():
     err_line(json.dumps({"rank_line": rank_line}))
     for b in B:
         lib.gmapdp_plan_destroy(b["plan"])
-        lib.gmapdp_stage2_plan_destroy(b["oplan"])
-        lib.gmapdp_microexon_plan_destroy(b["mplan"])
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == 2 and not args.simd:
+        if b["oplan"] is not None:
+            lib.gmapdp_stage2_plan_destroy(b["oplan"])
+        if b["mplan"] is not None:
+            lib.gmapdp_microexon_plan_destroy(b["mplan"])
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in (1, 2) and not args.simd:
         progress("CPU baselines")
-        cb = cpu_baselines(args.mix)
+        cb = cpu_baselines(args.mix, args.config)
         # the faster of the reference's two builds is the baseline; the other is kept beside it
         done = sorted((c for c in cb.values() if c), key=lambda c: -c["value"])
         out["cpu_baseline"] = done[0] if done else None

@@ -1012,6 +1012,7 @@ static int convert_genome(gmapdp_ctx* ctx, const gmapdp_genome_problem& p, gmapd
 }
 
 static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
+  const size_t lds_dirs_max = gg_lds_dirs_max();  // read once per plan, not per genome-gap problem
   std::map<std::tuple<int, int, int, size_t>, std::vector<int>> classes;  // (kind, R, dirs_lds, lds bucket)
   size_t pair_off = 0, gdirs_off = 0;
   // Latency mode (small batches: the GMAP drop-in's dispatcher batches): one launch class per (kind, R,
@@ -1106,7 +1107,7 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     const int R = pick_R(std::max(WL, WR));
     if (R > kMaxR) return bad(ctx, "band wider than 4096");
     size_t lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, true, std::max(WL, WR));
-    const bool dirs_lds = lds <= gg_lds_dirs_max();
+    const bool dirs_lds = lds <= lds_dirs_max;
     if (!dirs_lds) lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, false, std::max(WL, WR));
     d.dirs_offset = (int64_t)gdirs_off;  // bridge candidates (+ direction planes) in global scratch
     gdirs_off += (scratch_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, dirs_lds) + 255) & ~(size_t)255;
@@ -2337,6 +2338,10 @@ static void oligo_layout(gmapdp_oligo_plan* P, const std::vector<size_t>& slots,
     d.fallback_offset = fallback ? (int64_t)(cb + mb) : -1;
     d.table_offset = (int64_t)ct;
     d.diag_offset = (int64_t)cd;
+    // (scratch_oi sizes the hit list from the window: one entry per 8-mer start, + 2)
+    d.hit_cap = (uint32_t)std::min<size_t>(hcap ? (*hcap)[d.index] : (size_t)w + 2, 0xffffffffu);
+    d.table_cap = (uint32_t)std::min<size_t>(tcap[d.index], 0xffffffffu);
+    d.diag_cap = (uint32_t)std::min<size_t>(dcap[d.index], 0xffffffffu);
     cb += mb + fb;
     cs += slots[d.index];
     ct += tcap[d.index];
@@ -2433,11 +2438,8 @@ static int oligo_plan_build(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problem
       P->keys.push_back(kv.first);
     }
   oligo_layout(P, slots, true, tcap, dcap, sizing);
-  // mappings index the table with 32-bit offsets (a sizing run's restart in every chunk)
-  if (P->table_cap > 0x7fffffffull) {
-    oligo_plan_free(P);
-    return bad(ctx, "stage-2 table arena beyond 2^31 entries");
-  }
+  // (the kernels' mappings are relative to each problem's table_offset: the arena may pass 2^31 entries;
+  // the public seeding API, whose mappings are absolute 32-bit indexes, checks its own total)
   (void)toff;
   if (ev) P->pool_cap = std::strtoull(ev, nullptr, 10);  // per chunk
   const hipError_t e = oligo_buffers(ctx, P);
@@ -2487,7 +2489,6 @@ static hipError_t oligo_plan_relayout(gmapdp_ctx* ctx, gmapdp_oligo_plan* P, con
   }
   // the hit lists sized as measured (a few % of a 214-kb window), so one launch holds most of a plan
   oligo_layout(P, slots, false, tcap, dcap, false, &hcap);
-  if (P->table_cap > 0x7fffffffull) return hipErrorInvalidValue;  // 32-bit mappings
   return oligo_buffers(ctx, P);
 }
 
@@ -2496,6 +2497,18 @@ extern "C" {
 int gmapdp_oligo_plan_create(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problems, int n, const char* qseq_uc,
                              size_t qbytes, gmapdp_oligo_plan** plan) {
   return oligo_plan_build(ctx, problems, n, qseq_uc, qbytes, plan, false);
+}
+
+// The device mappings are relative to each problem's table_offset; the host-array API hands out absolute
+// 32-bit indexes into `positions` (the reference's mappings[q] pointers), so its table stays below 2^31.
+static void oligo_absolute_mappings(const gmapdp_oligo_problem* problems, int n, const gmapdp_oligo_result* res,
+                                    int32_t* mappings) {
+  for (int i = 0; i < n; i++) {
+    const int32_t t = (int32_t)res[i].table_offset;
+    int32_t* m = mappings + problems[i].qoff;
+    for (int q = 0; q < problems[i].querylength; q++)
+      if (m[q] >= 0) m[q] += t;
+  }
 }
 
 size_t gmapdp_oligo_plan_positions_capacity(const gmapdp_oligo_plan* plan) { return plan ? plan->table_cap : 0; }
@@ -2536,6 +2549,10 @@ int gmapdp_oligo_mappings_batch(gmapdp_ctx* ctx, const gmapdp_oligo_problem* pro
   int rc = oligo_plan_build(ctx, problems, n, qseq_uc, qbytes, &plan, true);
   if (rc) return rc;
   const size_t toff = plan->table_cap, doff = plan->diag_cap;
+  if (toff > 0x7fffffffull) {  // absolute 32-bit mappings
+    oligo_plan_free(plan);
+    return bad(ctx, "stage-2 seeding: table arena beyond 2^31 entries (split the batch)");
+  }
   if (toff > positions_capacity || doff > diagonal_capacity || (toff && !positions) || (doff && !diagonals)) {
     oligo_plan_free(plan);
     return bad(ctx, "positions or diagonal arena too small");
@@ -2572,6 +2589,7 @@ int gmapdp_oligo_mappings_batch(gmapdp_ctx* ctx, const gmapdp_oligo_problem* pro
   if (e == hipSuccess) e = ctx_sync(ctx, s);
   oligo_plan_free(plan);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "oligo execution: %s", e);
+  oligo_absolute_mappings(problems, n, results, mappings);
   return GMAPDP_OK;
 }
 
@@ -3094,11 +3112,12 @@ extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char*
       else if (used) std::memcpy(m->candidates, h + r_xcand, sizeof(gmapdp_microexon_candidate) * used);
     }
   }
-  // whole calls whose candidates did not fit (finish left npairs -2): search + finish again, alone
+  // whole calls whose candidates did not fit (finish left npairs -2): search + finish again, alone -- also
+  // when the searches section ran out of candidate room (GMAPDP_ESPACE leaves every other section filled)
   std::vector<int> redo;
   for (int i = 0; i < nxw; i++)
     if (m->whole_results[i].npairs == -2) redo.push_back(i);
-  if (!redo.empty() && rc == GMAPDP_OK) {
+  if (!redo.empty() && (rc == GMAPDP_OK || rc == GMAPDP_ESPACE)) {
     std::vector<gmapdp_microexon_problem> P(redo.size());
     for (size_t k = 0; k < redo.size(); k++) P[k] = m->wholes[redo[k]];
     const int nr = (int)redo.size();
@@ -3384,6 +3403,40 @@ int gmapdp_stage2_plan_outputs(const gmapdp_stage2_plan* plan, gmapdp_path** d_p
   if (d_pairs) *d_pairs = plan->d_pairs;
   if (d_counters) *d_counters = plan->d_counters;
   if (scratch_bytes) *scratch_bytes = plan->scratch;
+  return GMAPDP_OK;
+}
+
+int gmapdp_stage2_plan_fetch(gmapdp_ctx* ctx, const gmapdp_stage2_plan* plan, const gmapdp_stage2_result* d_results,
+                             void* stream, gmapdp_stage2_result* results, gmapdp_path* paths, size_t path_cap,
+                             gmapdp_path_pair* pairs, size_t pair_cap, size_t* paths_needed, size_t* pairs_needed) {
+  if (!ctx || !plan || !d_results || !results) return GMAPDP_EINVAL;
+  if (paths_needed) *paths_needed = 0;
+  if (pairs_needed) *pairs_needed = 0;
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  unsigned long long cnt[4] = {0, 0, 0, 0};
+  hipError_t e = hipMemcpyAsync(results, d_results, sizeof(gmapdp_stage2_result) * plan->n, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(cnt, plan->d_counters, sizeof(cnt), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = ctx_sync(ctx, s);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "stage-2 plan fetch: %s", e);
+  // the pools' atomics count past their capacity when calls overflow (those report status -2)
+  const size_t np = std::min<size_t>(cnt[1], plan->path_cap), nq = std::min<size_t>(cnt[2], plan->pair_cap);
+  if (paths_needed) *paths_needed = np;
+  if (pairs_needed) *pairs_needed = nq;
+  if (np > path_cap || nq > pair_cap || (np && !paths) || (nq && !pairs)) return GMAPDP_ESPACE;
+  if (np) e = hipMemcpyAsync(paths, plan->d_paths, sizeof(gmapdp_path) * np, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess && nq) e = hipMemcpyAsync(pairs, plan->d_pairs, sizeof(gmapdp_path_pair) * nq, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = ctx_sync(ctx, s);
+  if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "stage-2 plan fetch: %s", e);
+  return GMAPDP_OK;
+}
+
+int gmapdp_stage2_plan_seeding_classes(const gmapdp_stage2_plan* plan, int* n16, int* n32) {
+  if (!plan || !plan->oplan) return GMAPDP_EINVAL;
+  int a = 0, b = 0;
+  for (int k : plan->oplan->keys) (k & 1) ? b++ : a++;
+  if (n16) *n16 = a;
+  if (n32) *n32 = b;
   return GMAPDP_OK;
 }
 

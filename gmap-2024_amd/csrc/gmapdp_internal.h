@@ -173,10 +173,16 @@ struct DevOligoProblem {
   int32_t minor;          // oligoindices_minor (diag_lookback 60, suffnconsecutive 10), else major (120, 20)
   int32_t umax;           // LDS slots for the query's distinct 8-mers (>= their number)
   int32_t index;          // the problem's index in the batch (its result slot)
-  int64_t table_offset;   // first entry of the problem's table in the positions arena
+  int64_t table_offset;   // first entry of the problem's table in the positions arena (the mappings the
+                          // kernels write are relative to it, so the arena may pass 2^31 entries)
   int64_t diag_offset;    // first diagonal record (4 x int32)
   int64_t scratch_offset; // byte offset of the problem's region of the global scratch (its launch chunk's)
   int64_t fallback_offset; // the sequential walk's region in the same scratch, or -1: none (exact pool)
+  // What the layout gave the problem: hit-list entries, table entries, diagonal records.  A run that
+  // needs more (a plan re-laid out from a measured run and then run on another query) reports overflow
+  // (oned_matrix_p -1, Stage2_compute status -2) instead of writing past its slices.
+  uint32_t hit_cap, table_cap, diag_cap;
+  int32_t pad_;
 };
 
 // Stage2_compute descriptor (stage2.c:6325): the seeding problem's results slot plus the chaining

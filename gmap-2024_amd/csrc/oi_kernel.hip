@@ -145,7 +145,7 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
                                    const int32_t* __restrict__ mpq, const int* __restrict__ cum,
                                    const uint32_t* __restrict__ table_all, uint64_t* __restrict__ pool,
                                    unsigned long long base, uint32_t* hist,
-                                   int* evq, int32_t* __restrict__ good, int& ngood_out, int& maxn_out) {
+                                   int* evq, int32_t* __restrict__ good, int gcap, int& ngood_out, int& maxn_out) {
   OI_MARK(9);
   if (base == ~0ull) return false;
   uint64_t* evA = pool + base;                      // events (diagi << 32 | q)
@@ -402,6 +402,7 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
                         (int)(uint32_t)S[eb - bn], (int)(uint32_t)S[eb], bn + 1);
   }
   __threadfence_block();
+  if (ngood > gcap) ngood = -1;  // more good diagonals than the layout gave the problem: overflow
   for (int g = lane; g < ngood; g += 64) {
     const uint64_t k = gkey[g];
     int rank = 0;
@@ -558,7 +559,8 @@ __global__ __launch_bounds__(64) void oi_kernel(
         bool in;
         const int id = oligo_id(bitmap, wrank, m, in);
         count_inc(cnt, id);
-        hitlist[o++] = make_uint2((uint32_t)(16 * h + j - left), (uint32_t)id);
+        if ((uint32_t)o < P.hit_cap) hitlist[o] = make_uint2((uint32_t)(16 * h + j - left), (uint32_t)id);
+        o++;
       }
       nhits += __builtin_amdgcn_readlane(incl, 63);
     };
@@ -592,6 +594,27 @@ __global__ __launch_bounds__(64) void oi_kernel(
   }
   __syncthreads();
   OI_MARK(2);
+  // More hits or table entries than the layout gave the problem (a plan re-laid out from a measured run,
+  // then run on another query), or a 16-bit counter that could wrap: report overflow, as an exhausted
+  // event pool does, with no hits and nothing written past the problem's slices.
+  if ((uint32_t)nhits > P.hit_cap || tot > P.table_cap || (sizeof(CT) == 2 && nhits > 65535)) {
+    for (int i = lane; i < qlen; i += 64) {
+      npq[i] = 0;
+      mpq[i] = -1;
+    }
+    if (lane == 0) {
+      gmapdp_oligo_result res;
+      res.totalpositions = 0;
+      res.maxnconsecutive = 0;
+      res.oned_matrix_p = -1;
+      res.ndiagonals = 0;
+      res.table_offset = P.table_offset;
+      res.diag_offset = P.diag_offset;
+      results[P.index] = res;
+      *reinterpret_cast<unsigned long long*>(base_s + so.poolbase) = ~0ull;
+    }
+    return;
+  }
 
   // ---- pass 2: store in descending chrpos (plus: right to left; minus: left to right) ----
   uint32_t* table = table_all + P.table_offset;
@@ -663,7 +686,7 @@ __global__ __launch_bounds__(64) void oi_kernel(
           const int u = oligo_id(bitmap, wrank, (uint32_t)m, in);
           nh = (int)cnt[u];
           npq[i] = nh;
-          if (nh > 0) mo = (int32_t)(P.table_offset + (uint32_t)offs[u]);
+          if (nh > 0) mo = (int32_t)(uint32_t)offs[u];  // relative to the problem's table
         }
         mpq[i] = mo;
       }
@@ -703,7 +726,9 @@ __global__ __launch_bounds__(64) void oi_map_kernel(
   const int lane = threadIdx.x;
   const DevOligoProblem P = probs[blockIdx.x];
   if (P.chrend <= P.chrstart) return;  // oned_matrix_p stays 0 (oi_kernel wrote the record)
+  if (results[P.index].oned_matrix_p < 0) return;  // oi_kernel reported overflow
   OI_MARK(8);
+  const uint32_t* table = table_all + P.table_offset;  // the mappings are relative to it
   const int qlen = P.querylength;
   const int nq = qlen - kOiK + 1;
   const int32_t* npq = npos_out + P.qoff;
@@ -719,8 +744,8 @@ __global__ __launch_bounds__(64) void oi_map_kernel(
     int ngood = 0, maxn = 0;
     const uint32_t maxdiag = (uint32_t)qlen + (P.chrend - P.chrstart);
     if (!oi_mappings_sorted(lane, qlen, nq, totalpositions, maxdiag, chrinit, diag_lookback, suffn, npq, mpq, cum,
-                            table_all, pool, *reinterpret_cast<const unsigned long long*>(base_s + so.poolbase), hist,
-                            evq, good, ngood, maxn)) {
+                            table, pool, *reinterpret_cast<const unsigned long long*>(base_s + so.poolbase), hist,
+                            evq, good, (int)min(P.diag_cap, 0x7fffffffu), ngood, maxn)) {
       // the event pool is full: the sequential walk (per-diagonal states in the problem's fallback region;
       // a plan sized from a measured run has an exact pool and none: report the overflow instead)
       if (P.fallback_offset < 0) {
@@ -748,7 +773,7 @@ __global__ __launch_bounds__(64) void oi_map_kernel(
           c_nh = npq[qi];
           c_mo = mpq[qi];
           c_cum = cum[qi];
-          if (c_nh > 0) c_h0 = table_all[c_mo];
+          if (c_nh > 0) c_h0 = table[c_mo];
         }
         const int cend = min(64, nq - cb);
         for (int j = 0; j < cend; j++) {
@@ -763,7 +788,7 @@ __global__ __launch_bounds__(64) void oi_map_kernel(
             int reached = 0, nb = 0;
             uint32_t diagi = 0;
             if (h < nh) {
-              diagi = (h == 0 ? h0 : table_all[mo + h]) + (uint32_t)(qlen - q) - chrinit;
+              diagi = (h == 0 ? h0 : table[mo + h]) + (uint32_t)(qlen - q) - chrinit;
               const unsigned char ini = initp[diagi];
               OiState s = st[diagi];  // loaded with the flag; ignored when the flag is clear
               if (!ini) {
@@ -789,7 +814,8 @@ __global__ __launch_bounds__(64) void oi_map_kernel(
             }
             // the good list in lane order; the global best: the first lane reaching the new maximum
             const uint64_t rm = ballot(reached);
-            if (reached) good[4 * (ngood + lanes_below(rm, lane))] = (int32_t)diagi;
+            if (reached && ngood + lanes_below(rm, lane) < (int)min(P.diag_cap, 0x7fffffffu))
+              good[4 * (ngood + lanes_below(rm, lane))] = (int32_t)diagi;
             ngood += __popcll(rm);
             int mx = nb;
   #pragma unroll
@@ -803,10 +829,11 @@ __global__ __launch_bounds__(64) void oi_map_kernel(
         }
       }
       if (ngood == 0 && maxn > 0) {
-        if (lane == 0) good[0] = best;
+        if (lane == 0 && P.diag_cap > 0) good[0] = best;
         ngood = 1;
       }
       __threadfence_block();
+      if ((uint32_t)ngood > P.diag_cap) ngood = -1;  // more diagonals than the layout gave: overflow
       for (int g = lane; g < ngood; g += 64) {
         const int di = good[4 * g];
         const OiState s = st[di];
@@ -817,9 +844,9 @@ __global__ __launch_bounds__(64) void oi_map_kernel(
       }
     }
     if (lane == 0) {
-      results[P.index].maxnconsecutive = maxn;
-      results[P.index].oned_matrix_p = 1;
-      results[P.index].ndiagonals = ngood;
+      results[P.index].maxnconsecutive = ngood < 0 ? 0 : maxn;
+      results[P.index].oned_matrix_p = ngood < 0 ? -1 : 1;
+      results[P.index].ndiagonals = max(ngood, 0);
     }
   }
   OI_MARK(7);

@@ -1894,7 +1894,7 @@ __global__ __launch_bounds__(64) void s2a_kernel(
       uint32_t map = 0u;
       if (h < hend) {
         S2Hit x;
-        x.map = map = table_all[mj + (h - oq)];
+        x.map = map = table_all[O.table_offset + mj + (h - oq)];  // (mappings relative to the call's table)
         big |= (x.map >= 0x80000000u);
         x.consec = x.root = x.fpos = x.fhit = x.tracei = x.score = 0;  // CALLOC
         x.q = cb + j;

@@ -268,6 +268,9 @@ def load_library(path=LIB_PATH):
                                              C.c_void_p]),
         "gmapdp_stage2_plan_outputs": (C.c_int, [C.c_void_p, P(C.c_void_p), P(C.c_void_p), P(C.c_void_p),
                                                  P(C.c_size_t)]),
+        "gmapdp_stage2_plan_fetch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                               C.c_size_t, C.c_void_p, C.c_size_t, P(C.c_size_t), P(C.c_size_t)]),
+        "gmapdp_stage2_plan_seeding_classes": (C.c_int, [C.c_void_p, P(C.c_int), P(C.c_int)]),
         "gmapdp_stage2_plan_destroy": (None, [C.c_void_p]),
         "gmapdp_genome_prob_entries": (C.c_size_t, [C.c_void_p, C.c_int]),
         "gmapdp_genome_splice_sites": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t]),
@@ -304,6 +307,21 @@ def load_library(path=LIB_PATH):
         f.argtypes = args
     _lib = lib
     return lib
+
+
+_HIP = None
+
+
+def _hip():
+    """The HIP runtime (device buffers for the plan APIs' caller-owned device arguments)."""
+    global _HIP
+    if _HIP is None:
+        h = C.CDLL("libamdhip64.so")
+        h.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+        h.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        h.hipFree.argtypes = [C.c_void_p]
+        _HIP = h
+    return _HIP
 
 
 def exported_symbols():
@@ -773,6 +791,54 @@ class Engine:
                 lists.append(lst)
             out.append((int(r["nresults"]), lists))
         return out
+
+    def stage2_plan_raw(self, probs, qbuf, qucbuf, run_qbuf=None, run_qucbuf=None):
+        """The device-resident Stage2_compute plan (bench.py's path): gmapdp_stage2_plan_create on
+        (probs, qbuf, qucbuf) -- its sizing run, the measured re-layout, the 16-bit seeding class --,
+        gmapdp_stage2_plan_run(what = 3) against device copies of the query arenas (run_qbuf /
+        run_qucbuf when given: another query of the same layout), gmapdp_stage2_plan_fetch.  Returns
+        (results, paths, pairs, (calls with 16-bit, with 32-bit seeding counters))."""
+        lib, n = self.lib, len(probs)
+        hip = _hip()
+        plan = C.c_void_p()
+        self._check(lib.gmapdp_stage2_plan_create(self.h, probs.ctypes.data, n, qbuf, qucbuf, len(qucbuf),
+                                                  C.byref(plan)), "gmapdp_stage2_plan_create")
+        bufs = []
+        try:
+            n16, n32 = C.c_int(), C.c_int()
+            self._check(lib.gmapdp_stage2_plan_seeding_classes(plan, C.byref(n16), C.byref(n32)),
+                        "gmapdp_stage2_plan_seeding_classes")
+
+            def dbuf(nbytes, src=None):
+                ptr = C.c_void_p()
+                if hip.hipMalloc(C.byref(ptr), max(nbytes, 16)) != 0:
+                    raise GmapdpError("hipMalloc(%d) failed" % nbytes)
+                bufs.append(ptr)
+                if src is not None and hip.hipMemcpy(ptr, src, nbytes, 1) != 0:  # hipMemcpyHostToDevice
+                    raise GmapdpError("hipMemcpy failed")
+                return ptr
+            rq = qbuf if run_qbuf is None else run_qbuf
+            rqu = qucbuf if run_qucbuf is None else run_qucbuf
+            assert len(rq) == len(qbuf) and len(rqu) == len(qucbuf)
+            d_q, d_quc = dbuf(len(rq), rq), dbuf(len(rqu), rqu)
+            d_res = dbuf(n * STAGE2_RESULT_DTYPE.itemsize)
+            self._check(lib.gmapdp_stage2_plan_run(self.h, plan, d_q, d_quc, d_res, 3, None), "gmapdp_stage2_plan_run")
+            results = np.zeros(n, dtype=STAGE2_RESULT_DTYPE)
+            pn, qn = C.c_size_t(), C.c_size_t()
+            rc = lib.gmapdp_stage2_plan_fetch(self.h, plan, d_res, None, results.ctypes.data, None, 0, None, 0,
+                                              C.byref(pn), C.byref(qn))
+            if rc not in (0, -6):
+                self._check(rc, "gmapdp_stage2_plan_fetch")
+            paths = np.zeros(max(pn.value, 1), dtype=PATH_DTYPE)
+            pairs = np.zeros(max(qn.value, 1), dtype=PATH_PAIR_DTYPE)
+            self._check(lib.gmapdp_stage2_plan_fetch(self.h, plan, d_res, None, results.ctypes.data, paths.ctypes.data,
+                                                     len(paths), pairs.ctypes.data, len(pairs), C.byref(pn),
+                                                     C.byref(qn)), "gmapdp_stage2_plan_fetch")
+            return results, paths[:pn.value], pairs[:qn.value], (n16.value, n32.value)
+        finally:
+            for b in bufs:
+                hip.hipFree(b)
+            lib.gmapdp_stage2_plan_destroy(plan)
 
     # -- the drop-in's dispatcher batch (gmapdp_mixed_batch) ---------------------------------------
     def mixed_batch_raw(self, qbuf, qucbuf, singles=None, ends=None, genomes=None, splice_probs=None,

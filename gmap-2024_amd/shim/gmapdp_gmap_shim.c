@@ -574,6 +574,8 @@ typedef struct shim_req {
     gmapdp_sj_problem sj;
   } p;                          /* qoff / prob_offset relative to q and probs below */
   const char *q, *quc;          /* the query slice (borrowed: the caller waits) */
+  char q9[16], quc9[16];        /* an 8-nt query as the 8-mer + 'N' (owned by the request across the
+                                   caller's yield: another fiber of the same host may make such a call) */
   size_t qlen;
   const char *j;                /* splice-junction end gaps: the junction string (borrowed) */
   size_t jlen;
@@ -798,15 +800,22 @@ __wrap_pthread_join (pthread_t th, void **ret) {
   return 0;
 }
 
+/* GMAP's per-thread state (except.c exception stacks, gmap.c's request key) becomes per fiber.  A key past
+   the table would fall back to the host thread's slot, which every fiber of that host shares: refused
+   instead of mixing the fibers' state silently. */
 void *
 __wrap_pthread_getspecific (pthread_key_t key) {
-  if (cur_fiber != NULL && key < SHIM_NKEYS) return cur_fiber->keys[key];
+  if (cur_fiber != NULL) {
+    if (key >= SHIM_NKEYS) shim_refuse("a pthread key past the fibers' key table (GMAPDP_SHIM_FIBERS=0 runs it)");
+    return cur_fiber->keys[key];
+  }
   return __real_pthread_getspecific(key);
 }
 
 int
 __wrap_pthread_setspecific (pthread_key_t key, const void *value) {
-  if (cur_fiber != NULL && key < SHIM_NKEYS) {
+  if (cur_fiber != NULL) {
+    if (key >= SHIM_NKEYS) shim_refuse("a pthread key past the fibers' key table (GMAPDP_SHIM_FIBERS=0 runs it)");
     cur_fiber->keys[key] = (void *) value;
     return 0;
   }
@@ -2301,10 +2310,9 @@ __wrap_Oligoindex_get_mappings (List_T diagonals, bool *coveredp, Chrpos_T **map
        "8-mer" + 'N' (one distinct 8-mer; a single query position makes no consecutive run, so no
        diagonal and maxnconsecutive 0) */
     {
-      static __thread char q9[9];
-      memcpy(q9, queryuc_ptr, 8);
-      q9[8] = 'N';
       r = shim_request(K_OLIGO);
+      memcpy(r->quc9, queryuc_ptr, 8);
+      r->quc9[8] = 'N';
       p = &r->p.o;
       p->querylength = 9;
       p->chrstart = chrstart;
@@ -2314,7 +2322,7 @@ __wrap_Oligoindex_get_mappings (List_T diagonals, bool *coveredp, Chrpos_T **map
       p->plusp = plusp ? 1 : 0;
       p->minor = this->diag_lookback == 60 ? 1 : 0;
       r->genome = shim_tally.genome;
-      r->q = r->quc = q9;
+      r->q = r->quc = r->quc9;
       r->qlen = 9;
       r->tabn = gmapdp_oligo_positions_capacity(p, 1);
       dc = gmapdp_oligo_diagonal_capacity(p, 1);
@@ -2447,11 +2455,28 @@ __wrap_Stage2_compute (char *queryseq_ptr, char *queryuc_ptr, int querylength, i
     shim_refuse("an oligoindex other than GMAP's major 8-mer index");
   /* Below 8 nt the query holds no 8-mer: Oligoindex_get_mappings finds no position, totalpositions is 0
      and the reference returns NULL (stage2.c:6524).  At exactly 8 nt the tally runs against the previous
-     query's inquery flags (Oligoindex_set_inquery returns early, oligoindex_hr.c:33478), a state the
-     engine does not keep: refused. */
+     longer query's inquery flags (Oligoindex_set_inquery returns early, oligoindex_hr.c:33478; the shim
+     keeps them per oligoindex): a full 8-mer outside them has no hit (NULL again); one inside them has
+     the window positions of that 8-mer alone, which is what the engine computes for the query
+     "8-mer" + 'N' -- one query position with hits, no diagonal, the same chaining and pairs (querypos
+     0..7).  The 9th position never has a hit and lies past every pair. */
   if (querylength < 8) return NULL;
-  if (querylength == 8) shim_refuse("Stage2_compute on a query of exactly 8 nt");
-  shim_set_inquery(major, queryuc_ptr, 0, querylength);  /* the tally inside Stage2_compute sets them */
+  if (querylength == 8) {
+    shim_inquery *e = shim_inquery_of(major, 0);
+    uint32_t x = 0;
+    for (i = 0; i < 8; i++) {
+      switch (queryuc_ptr[i]) {
+      case 'A': x = x << 2; break;
+      case 'C': x = (x << 2) | 1u; break;
+      case 'G': x = (x << 2) | 2u; break;
+      case 'T': x = (x << 2) | 3u; break;
+      default: return NULL;  /* no full 8-mer: no lookup, totalpositions 0 */
+      }
+    }
+    if (e == NULL || !((e->bits[x >> 5] >> (x & 31)) & 1u)) return NULL;  /* not in the stale flags */
+  } else {
+    shim_set_inquery(major, queryuc_ptr, 0, querylength);  /* the tally inside Stage2_compute sets them */
+  }
   /* the chaining kernels keep Chrpos_T differences in 32-bit registers: checked here, on the calling
      thread, so that a refusal names its own call and never fails another thread's batch */
   if (chrend >= 0x80000000U || chrstart >= 0x80000000U)
@@ -2470,6 +2495,15 @@ __wrap_Stage2_compute (char *queryseq_ptr, char *queryuc_ptr, int querylength, i
   r->q = queryseq_ptr;
   r->quc = queryuc_ptr;
   r->qlen = (size_t) querylength;
+  if (querylength == 8) {
+    memcpy(r->q9, queryseq_ptr, 8);
+    memcpy(r->quc9, queryuc_ptr, 8);
+    r->q9[8] = r->quc9[8] = 'N';
+    r->q = r->q9;
+    r->quc = r->quc9;
+    r->qlen = 9;
+    p->querylength = 9;
+  }
   shim_submit(r);
   shim_count(ST_STAGE2);
   /* the results in list order: build from the last (each List_push prepends) */

@@ -549,7 +549,8 @@ typedef struct {
  * diagonals[4 * diag_offset ...]: {diagonal, querystart, queryend, nconsecutive} each.  Per query
  * position q: npositions[qoff + q] (0 without a full 8-mer or without hits) and
  * mappings[qoff + q], the index in `positions` of mappings[q][0] (-1 without hits); the problem's
- * table occupies positions[table_offset ...]. */
+ * table occupies positions[table_offset ...].  The batch's table arena stays below 2^31 entries
+ * (GMAPDP_EINVAL otherwise; split the batch). */
 typedef struct {
   int32_t totalpositions;
   int32_t maxnconsecutive;
@@ -571,7 +572,10 @@ size_t gmapdp_oligo_diagonal_capacity (const gmapdp_oligo_problem *problems, int
  * table / diagonal / scratch offsets; the descriptors are uploaded), then run asynchronously on
  * `stream` (hipStream_t; NULL = the context's stream) against a device-resident upper-case query
  * arena.  d_results has n entries in problem order; d_npositions / d_mappings are indexed like the
- * query arena; d_positions / d_diagonals hold the plan's capacities. */
+ * query arena, and a device mapping is relative to its problem's table: mappings[q][0] is
+ * d_positions[table_offset + d_mappings[qoff + q]] (so the table arena may pass 2^31 entries);
+ * d_positions / d_diagonals hold the plan's capacities.  A problem that needs more hit-list, table or
+ * diagonal room than the layout gave it reports oned_matrix_p = -1 and writes nothing else. */
 typedef struct gmapdp_oligo_plan gmapdp_oligo_plan;
 int gmapdp_oligo_plan_create (gmapdp_ctx *ctx, const gmapdp_oligo_problem *problems, int n, const char *qseq_uc,
                               size_t qbytes, gmapdp_oligo_plan **plan);
@@ -661,6 +665,16 @@ int gmapdp_stage2_plan_run (gmapdp_ctx *ctx, const gmapdp_stage2_plan *plan, con
                             const char *d_qseq_uc, gmapdp_stage2_result *d_results, int what, void *stream);
 int gmapdp_stage2_plan_outputs (const gmapdp_stage2_plan *plan, gmapdp_path **d_paths, gmapdp_path_pair **d_pairs,
                                 unsigned long long **d_counters, size_t *scratch_bytes);
+/* The outputs of a finished gmapdp_stage2_plan_run (chaining) on `stream` (NULL = the context's stream;
+ * synchronised here), in gmapdp_stage2_batch's format: n results copied from d_results, and the path
+ * and pair records into host arenas of path_cap / pair_cap records (GMAPDP_ESPACE with *_needed when
+ * they are too small).  A result with status -2 overflowed the plan's pools or its seeding layout. */
+int gmapdp_stage2_plan_fetch (gmapdp_ctx *ctx, const gmapdp_stage2_plan *plan, const gmapdp_stage2_result *d_results,
+                              void *stream, gmapdp_stage2_result *results, gmapdp_path *paths, size_t path_cap,
+                              gmapdp_path_pair *pairs, size_t pair_cap, size_t *paths_needed, size_t *pairs_needed);
+/* How many of the plan's calls seed with 16-bit and with 32-bit counters (after the plan's sizing run
+ * moved every call with fewer than 2^16 hits to the 16-bit class). */
+int gmapdp_stage2_plan_seeding_classes (const gmapdp_stage2_plan *plan, int *n16, int *n32);
 void gmapdp_stage2_plan_destroy (gmapdp_stage2_plan *plan);
 
 /* Create a context on HIP device `device`.  mode = Mode_T (mode.h:5;

@@ -913,3 +913,99 @@ orc_stage2_compute (const char *queryseq, const char *queryuc, int querylength, 
   if (sink.overflow || nkept > path_cap) return -1;
   return nkept;
 }
+
+/* Test instrumentation (whole-block parity, tests/test_gpu_stage2_plan.py): n orc_stage2_compute calls
+   on the current genome over `nthreads` threads (the restatement keeps no state between calls but the
+   genome, which is only read).  Call i reads qseq / quc at qoff[i]; it writes scalars[8 i ...] = {its
+   return value (nkept, or < 0), npaths, ncovered, status, diag_querystart, diag_queryend, 0, 0},
+   paths[2 (path_cap i + k) ...] = {first record, records} of kept path k, and its pair records from
+   pairs[pair_off[i]] on, pair_off[i + 1] - pair_off[i] at most (else scalars[8 i] = -9), in the engine's
+   gmapdp_path_pair layout
+   (20 B: querypos, genomepos, queryjump, genomejump, cdna, comp, genome, genomealt). */
+#include <pthread.h>
+
+typedef struct {
+  int querypos, genomepos, queryjump, genomejump;
+  char cdna, comp, genome, genomealt;
+} OrcPathPair;
+
+typedef struct {
+  int n;
+  const char *qseq, *quc;
+  const int *qoff, *qlen, *plusp, *splicingp, *maxintronlen;
+  const unsigned int *chrstart, *chrend, *chroffset, *chrhigh;
+  int *scalars, *paths, path_cap;
+  OrcPathPair *pairs;
+  const long *pair_off;
+  int next;
+  pthread_mutex_t lock;
+} S2Batch;
+
+static void *
+s2batch_worker (void *arg) {
+  S2Batch *B = (S2Batch *) arg;
+  int *kp = (int *) malloc(2 * (size_t) B->path_cap * sizeof(int));
+  for (;;) {
+    int i, k, j, r, cap;
+    OrcPair *tmp;
+    pthread_mutex_lock(&B->lock);
+    i = B->next++;
+    pthread_mutex_unlock(&B->lock);
+    if (i >= B->n) break;
+    cap = 64 * B->qlen[i] > (1 << 18) ? 64 * B->qlen[i] : (1 << 18);  /* every traced path's records */
+    tmp = (OrcPair *) malloc((size_t) cap * sizeof(OrcPair));
+    r = orc_stage2_compute(B->qseq + B->qoff[i], B->quc + B->qoff[i], B->qlen[i], B->chrstart[i], B->chrend[i],
+                           B->chroffset[i], B->chrhigh[i], B->plusp[i], B->splicingp[i], B->maxintronlen[i],
+                           B->scalars + 8 * (size_t) i, kp, B->path_cap, tmp, cap);
+    B->scalars[8 * (size_t) i] = r;
+    /* kept paths, their records packed from the call's first pair slot on */
+    {
+      long o = B->pair_off[i];
+      int *pp = B->paths + 2 * (size_t) B->path_cap * i;
+      for (k = 0; r > 0 && k < r; k++) {
+        if (o + kp[2 * k + 1] > B->pair_off[i + 1]) {  /* the call's output slot is too small */
+          B->scalars[8 * (size_t) i] = -9;
+          break;
+        }
+        pp[2 * k] = (int) (o - B->pair_off[i]);
+        pp[2 * k + 1] = kp[2 * k + 1];
+        for (j = 0; j < kp[2 * k + 1]; j++, o++) {
+          const OrcPair *x = &tmp[kp[2 * k] + j];
+          OrcPathPair *y = &B->pairs[o];
+          y->querypos = x->querypos;
+          y->genomepos = x->genomepos;
+          y->queryjump = x->queryjump;
+          y->genomejump = x->genomejump;
+          y->cdna = x->cdna;
+          y->comp = x->comp;
+          y->genome = x->genome;
+          y->genomealt = x->genomealt;
+        }
+      }
+    }
+    free(tmp);
+  }
+  free(kp);
+  return NULL;
+}
+
+int
+orc_stage2_batch (int n, const char *qseq, const char *quc, const int *qoff, const int *qlen,
+                  const unsigned int *chrstart, const unsigned int *chrend, const unsigned int *chroffset,
+                  const unsigned int *chrhigh, const int *plusp, const int *splicingp, const int *maxintronlen,
+                  int *scalars, int *paths, int path_cap, void *pairs, const long *pair_off, int nthreads) {
+  S2Batch B;
+  pthread_t th[64];
+  int t;
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 64) nthreads = 64;
+  B.n = n; B.qseq = qseq; B.quc = quc; B.qoff = qoff; B.qlen = qlen; B.plusp = plusp; B.splicingp = splicingp;
+  B.maxintronlen = maxintronlen; B.chrstart = chrstart; B.chrend = chrend; B.chroffset = chroffset;
+  B.chrhigh = chrhigh; B.scalars = scalars; B.paths = paths; B.path_cap = path_cap;
+  B.pairs = (OrcPathPair *) pairs; B.pair_off = pair_off; B.next = 0;
+  pthread_mutex_init(&B.lock, NULL);
+  for (t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, s2batch_worker, &B);
+  for (t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  pthread_mutex_destroy(&B.lock);
+  return 0;
+}

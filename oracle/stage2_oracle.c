@@ -113,8 +113,16 @@ orc_oligo_mappings (const char *queryuc, int querylength, unsigned int chrstart,
   lpl = (unsigned long long) chroffset + chrend + (plusp ? 0 : 1);
   lpl = lpl < K ? 0 : lpl - K;
   chrpos0 = plusp ? chrstart : (chrhigh - chroffset) - chrend;
-  if (lpl > left)
-    for (p = left; p <= lpl; p++) counts[plusp ? kmer_fwd(p) : kmer_rev(p)] += 1;  /* wraps mod 256 */
+  /* (the 8-mers rolled along the window: kmer_fwd(p + 1) / kmer_rev(p + 1) from p's -- the same values) */
+  if (lpl > left) {
+    m = plusp ? kmer_fwd(left) : kmer_rev(left);
+    for (p = left;; p++) {
+      counts[m] += 1;  /* wraps mod 256 */
+      if (p == lpl) break;
+      m = plusp ? (((m << 2) | (unsigned int) gcode(p + K)) & 0xFFFFu)
+                : ((m >> 2) | ((unsigned int) (3 - gcode(p + K)) << (2 * K - 2)));
+    }
+  }
   for (m = 0; m < OLIGOSPACE; m++) {
     if (!inquery[m]) counts[m] = 0;
     offs[m] = (unsigned int) total;
@@ -124,13 +132,15 @@ orc_oligo_mappings (const char *queryuc, int querylength, unsigned int chrstart,
     table = (unsigned int *) malloc((size_t) total * sizeof(unsigned int));
     memcpy(work, counts, OLIGOSPACE);
     if (plusp) {
+      m = kmer_fwd(lpl);
       for (p = lpl + 1; p-- > left;) {  /* right to left, chrpos descending */
-        m = kmer_fwd(p);
+        if (p < lpl) m = (m >> 2) | ((unsigned int) gcode(p) << (2 * K - 2));  /* kmer_fwd(p) */
         if (work[m]) table[offs[m] + (--work[m])] = chrpos0 + (unsigned int) (p - left);
       }
     } else {
+      m = kmer_rev(left);
       for (p = left; p <= lpl; p++) {   /* left to right, chrpos descending */
-        m = kmer_rev(p);
+        if (p > left) m = (m >> 2) | ((unsigned int) (3 - gcode(p + K - 1)) << (2 * K - 2));  /* kmer_rev(p) */
         if (work[m]) table[offs[m] + (--work[m])] = chrpos0 + (unsigned int) (lpl - p);
       }
     }

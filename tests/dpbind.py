@@ -733,6 +733,67 @@ def _stage2_compute(self, p):
 Ref.stage2_compute = _stage2_compute
 Oracle.stage2_compute = _stage2_compute
 
+S2B_PATHS = 64   # kept paths per call the batch oracle keeps (MAX_NALIGNMENTS is 10; ties may add more)
+
+
+def oracle_stage2_batch(orc, probs, qbuf, qucbuf, nthreads=None):
+    """orc_stage2_batch (the restatement, several threads) over gmapdp.STAGE2_PROBLEM_DTYPE problems on the
+    oracle's current genome (coordinates as given).  Returns (scalars (n, 8): {nkept or < 0, npaths,
+    ncovered, status, diag_querystart, diag_queryend}, paths (n, S2B_PATHS, 2): {first record relative to
+    the call's slot, records}, pairs (PATH_PAIR layout, 20 B), pair_off (n + 1))."""
+    import numpy as np
+    n = len(probs)
+    f = orc.lib.orc_stage2_batch
+    f.restype = C.c_int
+    ql = probs["querylength"].astype(np.int64)
+    pair_off = np.zeros(n + 1, dtype=np.int64)
+    pair_off[1:] = np.cumsum(3 * ql + 256)
+    col = lambda k, dt: np.ascontiguousarray(probs[k], dtype=dt)  # noqa: E731
+    args = [col("qoff", np.int32), col("querylength", np.int32), col("chrstart", np.uint32), col("chrend", np.uint32),
+            col("chroffset", np.uint32), col("chrhigh", np.uint32), col("plusp", np.int32), col("splicingp", np.int32),
+            col("maxintronlen", np.int32)]
+    scal = np.zeros((n, 8), dtype=np.int32)
+    paths = np.zeros((n, S2B_PATHS, 2), dtype=np.int32)
+    pairs = np.zeros(int(pair_off[-1]) * 20 + 20, dtype=np.uint8)
+    nt = nthreads or min(16, os.cpu_count() or 4)
+    f(C.c_int(n), C.c_char_p(qbuf), C.c_char_p(qucbuf), *[C.c_void_p(a.ctypes.data) for a in args],
+      C.c_void_p(scal.ctypes.data), C.c_void_p(paths.ctypes.data), C.c_int(S2B_PATHS), C.c_void_p(pairs.ctypes.data),
+      C.c_void_p(pair_off.ctypes.data), C.c_int(nt))
+    return scal, paths, pairs, pair_off
+
+
+def stage2_mismatches(results, paths, pairs, orc_out, index=None):
+    """Calls whose engine outputs (gmapdp_stage2_batch / plan format: results, path records, 20-B pair
+    records) differ from oracle_stage2_batch's: nresults, npaths, ncovered, status, the Diag_compute_bounds
+    query bounds (status 2) and every kept path's pair records byte for byte.  index[i]: the oracle row of
+    engine call i (default i).  Returns [(engine call, what)]."""
+    import numpy as np
+    scal, opaths, opairs, pair_off = orc_out
+    pb = pairs.view(np.uint8).reshape(-1) if len(pairs) else np.zeros(0, dtype=np.uint8)
+    bad = []
+    for i in range(len(results)):
+        j = i if index is None else index[i]
+        r, o = results[i], scal[j]
+        if int(o[0]) < 0:
+            bad.append((i, "oracle error %d" % o[0]))
+            continue
+        got = (int(r["nresults"]), int(r["npaths"]), int(r["ncovered"]), int(r["status"]))
+        exp = (int(o[0]), int(o[1]), int(o[2]), int(o[3]))
+        if got != exp:
+            bad.append((i, "scalars %s vs %s" % (got, exp)))
+            continue
+        if int(r["status"]) == 2 and (int(r["diag_querystart"]), int(r["diag_queryend"])) != (int(o[4]), int(o[5])):
+            bad.append((i, "query bounds"))
+            continue
+        for k in range(int(r["nresults"])):
+            pr = paths[int(r["path_offset"]) + k]
+            eo, en = int(pr["pair_offset"]), int(pr["npairs"])
+            oo, on = int(pair_off[j]) + int(opaths[j, k, 0]), int(opaths[j, k, 1])
+            if en != on or not np.array_equal(pb[20 * eo:20 * (eo + en)], opairs[20 * oo:20 * (oo + on)]):
+                bad.append((i, "path %d" % k))
+                break
+    return bad
+
 
 def repeat_genome(rng, n, nfrac=0.002):
     """An i.i.d. genome with planted tandem repeats and duplicated segments (many hits per 8-mer,

@@ -23,6 +23,11 @@ Outputs (data only):
                          reads whose stage 3 makes Oligoindex_get_mappings calls on 8-nt queries
                          (SHORT_OLIGO_READS, found with oracle/_ref/gmap_callmix), and the reference
                          program's outputs on them
+  e2e_s8_reads.fa, e2e_s8_{nosimd,avx2}.sam
+                         two reads of e2e_reads.fa with 8-nt reads after each (pieces of the read
+                         before them and random 8-mers): GMAP calls Stage2_compute on each 8-nt read,
+                         whose tally runs against the previous longer query's 8-mer flags
+                         (oligoindex_hr.c:33478); against e2e_genome.fa, single worker (-t 1)
 """
 import math
 import os
@@ -104,6 +109,15 @@ def make_inputs():
     short = [r for i, r in ((i, synth_read(g2, i)) for i in range(SHORT_STREAM)) if i in SHORT_OLIGO_READS]
     write_fasta(os.path.join(HERE, "e2e_short_genome.fa"), [("synseg", "".join(g2))])
     write_fasta(os.path.join(HERE, "e2e_short_reads.fa"), short)
+    rng = random.Random(8)
+    s8 = []
+    for name, seq in reads[:2]:
+        s8.append((name, seq))
+        for k in range(6):
+            i = rng.randrange(0, len(seq) - 8)
+            s8.append(("%s_in%d" % (name, k), seq[i:i + 8]))
+            s8.append(("%s_rand%d" % (name, k), "".join(rng.choice("ACGT") for _ in range(8))))
+    write_fasta(os.path.join(HERE, "e2e_s8_reads.fa"), s8)
 
 
 def run_gmap(binary, args, out):
@@ -120,6 +134,8 @@ def main():
         run_gmap(exe, ["-g", "genetest2.fa", "cdna2.fa"], os.path.join(HERE, "cdna2_genetest2_%s.txt" % v))
         run_gmap(exe, ["-g", "e2e_short_genome.fa", "-f", "samse", "--no-sam-headers", "e2e_short_reads.fa"],
                  os.path.join(HERE, "e2e_short_%s.sam" % v))
+        run_gmap(exe, ["-t", "1", "-g", "e2e_genome.fa", "-f", "samse", "--no-sam-headers", "e2e_s8_reads.fa"],
+                 os.path.join(HERE, "e2e_s8_%s.sam" % v))
     print("wrote e2e fixtures in", HERE)
 
 

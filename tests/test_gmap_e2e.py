@@ -138,6 +138,25 @@ def test_gpu_gmap_short_oligoindex_queries(build):
     assert _stats(err)["Oligoindex_get_mappings"] > 0
 
 
+S8_ARGS = ["-t", "1", "-g", "e2e_genome.fa", "-f", "samse", "--no-sam-headers", "e2e_s8_reads.fa"]
+
+
+@pytest.mark.parametrize("build", BUILDS)
+def test_reference_gmap_reproduces_s8_fixture(build):
+    assert _run(_exe("gmap_" + build), S8_ARGS)[0] == _read("e2e_s8_%s.sam" % build)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("build", BUILDS)
+def test_gpu_gmap_8nt_reads(build):
+    """8-nt reads (make_e2e.py e2e_s8_reads.fa): GMAP calls Stage2_compute on each, against the previous
+    longer query's 8-mer flags; the drop-in answers as the reference does (no refusal) and the output is
+    the reference program's."""
+    out, err = _run(_exe("gmap_gpu_" + build), S8_ARGS, env={"GMAPDP_SHIM_STATS": "1"})
+    assert out == _read("e2e_s8_%s.sam" % build)
+    assert _stats(err)["Stage2_compute"] >= 2
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("threads", [4, 32])
 def test_gpu_gmap_worker_threads(threads):

@@ -9,20 +9,26 @@ The splice-site probabilities are GMAP's MaxEnt models as the bench computes the
 universal coordinates (gmapdp.DEVICE), against the oracle's restatement on the chromosome alone -- so the
 device MaxEnt is pinned past 2^31 (GRCh38) and past 2^32 (wheat) too.
 
-configs[2]: block 0 of the default bench stream (GRCh38 layout, 3.09 Gnt, 10 000 reads, 8 blocks planted).
+configs[2]: block 0 of the default bench stream (GRCh38 layout, 3.09 Gnt, 10 000 reads, 8 blocks planted);
+every one of its Stage2_compute calls through both engine paths (the batch API and the plan bench.py times).
+configs[1]: block 0 of `bench.py --config 1` (chr22, single and end gaps only), a 5 % sample.
 configs[4]: a 2 000-read block of the Iso-Seq stream on the 17-Gnt wheat layout (coordinates past 2^32),
 sampled on its three smallest chromosomes."""
 import random
+import sys
+import time
 
 import numpy as np
 import pytest
 
 import gmapdp
 from gmapdp import workload as W
-from dpbind import Oracle, call_end, call_single, microexon_probs, oracle_splice_probs
+from dpbind import (S2B_PATHS, Oracle, call_end, call_single, microexon_probs, oracle_splice_probs,
+                    oracle_stage2_batch, stage2_mismatches)
 
 pytestmark = pytest.mark.gpu
 TAIL = 8192
+T0 = time.perf_counter()
 
 
 def _sample(n, frac, rng, allowed=None):
@@ -31,10 +37,29 @@ def _sample(n, frac, rng, allowed=None):
     return np.sort(rng.choice(idx, size=min(k, len(idx)), replace=False)) if len(idx) else idx
 
 
-def _run(layout, shape, reads, nblocks, chroms=None, frac=0.01):
+def _progress(msg):
+    sys.stderr.write("[bench-workload %.0fs] %s\n" % (time.perf_counter() - T0, msg))
+    sys.stderr.flush()
+
+
+def _block(layout, shape, reads, nblocks):
     genome = W.PackedGenome(layout.total, seed=38)
+    _progress("genome %d nt" % layout.total)
     W.plant_stream(genome, layout, reads, range(nblocks), shape)
+    _progress("planted")
     d = W.make_blocks(genome, layout, reads, [0], shape=shape, sprob=False)[0]
+    _progress("block 0 generated")
+    return genome, d
+
+
+@pytest.fixture(scope="module")
+def grch38_block0():
+    """bench.py's configs[2] block 0 (the default stream: GRCh38 layout, 10 000 reads, 8 blocks planted)"""
+    return _block(W.Layout(W.GRCH38), W.CDNA2K, 10000, 8)
+
+
+def _run(layout, shape, reads, nblocks, chroms=None, frac=0.01, block=None):
+    genome, d = block if block is not None else _block(layout, shape, reads, nblocks)
     eng = gmapdp.Engine(0)
     eng.set_genome(blocks=genome.blocks, length=genome.length)
     rng = np.random.default_rng(77)
@@ -125,10 +150,88 @@ def _run(layout, shape, reads, nblocks, chroms=None, frac=0.01):
     return sizes, got
 
 
-def test_gpu_bench_configs2_block_sample():
-    sizes, got = _run(W.Layout(W.GRCH38), W.CDNA2K, 10000, 8)
+def test_gpu_bench_configs2_block_sample(grch38_block0):
+    sizes, got = _run(W.Layout(W.GRCH38), W.CDNA2K, 10000, 8, block=grch38_block0)
     assert sizes["single"] > 2000 and sizes["genome"] > 4000 and sizes["oligo"] >= 150
     assert sum(1 for r in got["oligo"] if r[0] > 0) > 0.9 * sizes["oligo"]     # the reads chain
+
+
+def test_gpu_bench_configs1_block_sample():
+    """configs[1] ("100k synthetic 2-kb cDNA vs human chr22, Dynprog_single + Dynprog_end only"): block 0 of
+    `bench.py --config 1` (chr22 layout, 10 000 reads, the 10 blocks of a 100 k-read cycle planted), its
+    single and end gaps only, a 5 % sample against the oracle (dynprog_single.c:429, dynprog_end.c:1294/1924)."""
+    genome, d = _block(W.Layout(W.CHR22), W.CDNA2K, 10000, 10)
+    for k in ("genome", "microexon", "oligo"):  # as bench.py --config 1 strips them
+        d[k] = d[k][:0]
+    sizes, got = _run(W.Layout(W.CHR22), W.CDNA2K, 10000, 10, frac=0.05, block=(genome, d))
+    assert sizes["single"] > 9000 and sizes["end"] > 5000 and sizes["genome"] == sizes["oligo"] == 0
+    assert sum(1 for r in got["single"] if r[1]) > 0.5 * sizes["single"]   # the fills emit pairs
+
+
+def _stage2_problems(d):
+    op = d["oligo"]
+    s2p = np.zeros(len(op), dtype=gmapdp.STAGE2_PROBLEM_DTYPE)
+    for k in ("qoff", "querylength", "chrstart", "chrend", "chroffset", "chrhigh", "plusp"):
+        s2p[k] = op[k]
+    s2p["splicingp"] = 1       # GMAP's defaults, as bench.py passes them
+    s2p["maxintronlen"] = 500000
+    return s2p
+
+
+def _oracle_stage2_block(genome, s2p, q):
+    """orc_stage2_batch over every call, chromosome by chromosome (the oracle holds one chromosome at
+    chroffset 0; the outputs are chromosome-relative)."""
+    orc = Oracle()
+    n = len(s2p)
+    scal = np.zeros((n, 8), dtype=np.int32)
+    paths = np.zeros((n, S2B_PATHS, 2), dtype=np.int32)
+    parts, off, base = [], np.zeros(n + 1, dtype=np.int64), 0
+    for cho in sorted(set(int(x) for x in s2p["chroffset"])):
+        idx = np.nonzero(s2p["chroffset"] == cho)[0]
+        chh = int(s2p["chrhigh"][idx[0]])
+        orc.set_genome(genome.ascii(cho, min(genome.length, chh + TAIL)))
+        sub = s2p[idx].copy()
+        sub["chroffset"] = 0
+        sub["chrhigh"] = chh - cho
+        sc, pa, pr, po = oracle_stage2_batch(orc, sub, q, q)
+        _progress("oracle: %d calls at chroffset %d" % (len(idx), cho))
+        scal[idx], paths[idx] = sc, pa
+        off[idx] = base + po[:-1]
+        parts.append(pr[:20 * int(po[-1])])
+        base += int(po[-1])
+    return scal, paths, np.concatenate(parts), off
+
+
+def test_gpu_bench_configs2_stage2_every_call(grch38_block0):
+    """Every Stage2_compute call of bench block 0 (15 850 calls over ~214-kb windows at GRCh38 coordinates),
+    bit-exact against the oracle through both engine paths:
+      - gmapdp_stage2_batch, the drop-in's synchronous API (its seeding arenas laid out from upper bounds:
+        13.6 GB of table for this block, past 2^31 entries -- the mappings are relative to each call's table);
+      - the device-resident plan bench.py times (gmapdp_stage2_plan_create: the sizing run, the arenas
+        re-laid out from it, the calls with fewer than 2^16 hits moved to the 16-bit seeding counters;
+        gmapdp_stage2_plan_run; gmapdp_stage2_plan_fetch)."""
+    genome, d = grch38_block0
+    s2p = _stage2_problems(d)
+    q = d["oq"].tobytes()
+    exp = _oracle_stage2_block(genome, s2p, q)
+    assert np.all(exp[0][:, 0] >= 0), "oracle errors"
+    eng = gmapdp.Engine(0)
+    eng.set_genome(blocks=genome.blocks, length=genome.length)
+    try:
+        res, paths, pairs = eng.stage2_batch_raw(s2p, q, q)
+        _progress("gmapdp_stage2_batch done")
+        bad = stage2_mismatches(res, paths, pairs, exp)
+        assert not bad, "gmapdp_stage2_batch differs from the oracle on %d of %d calls: %s" % (len(bad), len(s2p), bad[:8])
+        pres, ppaths, ppairs, (n16, n32) = eng.stage2_plan_raw(s2p, q, q)
+        _progress("stage-2 plan done (%d calls 16-bit, %d 32-bit)" % (n16, n32))
+        bad = stage2_mismatches(pres, ppaths, ppairs, exp)
+        assert not bad, "the stage-2 plan differs from the oracle on %d of %d calls: %s" % (len(bad), len(s2p), bad[:8])
+    finally:
+        eng.close()
+    # the bench's configuration: 214-kb windows (>= 2^16 starts) seeded with 16-bit counters after the re-layout
+    win = (s2p["chrend"] - s2p["chrstart"]).astype(np.int64)
+    assert (win >= 65536).mean() > 0.99 and n16 + n32 == len(s2p) and n16 > 0.99 * len(s2p)
+    assert (res["status"] == 2).sum() > 0.9 * len(s2p) and res["nresults"].sum() >= len(s2p)
 
 
 def test_gpu_bench_configs4_block_sample():

@@ -131,6 +131,42 @@ def test_shim_stage2_compute(build):
 
 
 @pytest.mark.parametrize("build", ["nosimd", "avx2"])
+def test_shim_stage2_compute_8nt_queries(build):
+    """Stage2_compute on queries of exactly 8 nt (GMAP makes them for 8-nt reads): the
+    reference's tally keeps the previous longer query's 8-mer flags (Oligoindex_set_inquery returns early,
+    oligoindex_hr.c:33478), so an 8-mer inside them chains its window positions and one outside them gives
+    NULL.  A long query, then 8-nt pieces of it, random 8-mers, a piece with an N and a 7-nt query, on one
+    oligoindex: the shim (which keeps the flags per oligoindex) equals the reference call for call."""
+    from dpbind import random_genome, stage2_problem
+    refv, shimv = ("nosimd", "gpushim") if build == "nosimd" else ("avx2a", "gpushim_avx2")
+    if not (ref_available(refv) and ref_available(shimv)):
+        pytest.skip("reference objects did not travel")
+    ref, shim = Ref(refv), Ref(shimv)
+    rng = random.Random(808)
+    g = random_genome(rng, 200000)
+    ref.set_genome(g)
+    shim.set_genome(g)
+    seq, nonempty = [], 0
+    for _ in range(6):
+        p = stage2_problem(rng, g)
+        q = p["quc"]
+        seq.append(p)
+        for k in range(10):
+            i = rng.randrange(0, len(q) - 8)
+            piece = q[i:i + 8] if k < 6 else bytes(rng.choice(b"ACGT") for _ in range(8))
+            if k == 8:
+                piece = piece[:3] + b"N" + piece[4:]
+            if k == 9:
+                piece = piece[:7]
+            seq.append(dict(p, q=piece.lower() if k % 2 else piece, quc=piece))
+    for i, p in enumerate(seq):
+        a, b = ref.stage2_compute(p), shim.stage2_compute(p)
+        assert a == b, "call %d (%d nt): reference %s vs shim %s" % (i, len(p["quc"]), a[0], b[0])
+        nonempty += len(p["quc"]) == 8 and a[0] > 0
+    assert nonempty >= 6  # 8-mers inside the flags that chain
+
+
+@pytest.mark.parametrize("build", ["nosimd", "avx2"])
 def test_shim_microexon_int(build):
     """Dynprog_microexon_int wrapped (mx_search_kernel, the host's MaxEnt, mx_finish_kernel): the list,
     its gap holders' comp and every out-parameter equal the unmodified reference objects'."""

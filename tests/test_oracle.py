@@ -419,6 +419,30 @@ def test_oracle_stage2_compute_matches_golden():
     assert {p["plusp"] for p in probs} == {0, 1} and {p["splicingp"] for p in probs} == {0, 1}
 
 
+def test_oracle_stage2_batch_matches_single_calls():
+    """orc_stage2_batch (the whole-block checker of tests/test_gpu_bench_workload.py: threads, the engine's
+    20-B pair records) gives what orc_stage2_compute gives call by call, on the golden's calls."""
+    import numpy as np
+    import gmapdp
+    from dpbind import oracle_stage2_batch
+    g, probs, exp = _load_stage2_golden()
+    orc = Oracle()
+    orc.set_genome(g)
+    pr, qb, qub = gmapdp.Engine.build_stage2_batch(probs)
+    scal, paths, pairs, off = oracle_stage2_batch(orc, pr, qb, qub, nthreads=4)
+    rec = np.dtype([("q", "<i4"), ("g", "<i4"), ("qj", "<i4"), ("gj", "<i4"), ("c", "S1"), ("m", "S1"), ("x", "S1"),
+                    ("a", "S1")])
+    pv = pairs[:(len(pairs) // 20) * 20].view(rec)
+    for i, (n, lists) in enumerate(exp):
+        assert int(scal[i, 0]) == n, i
+        for k in range(n):
+            o, m = int(off[i]) + int(paths[i, k, 0]), int(paths[i, k, 1])
+            got = [(int(x["q"]), int(x["g"]), int(x["qj"]), int(x["gj"]), 0, bytes(x["c"]) or b"\0",
+                    bytes(x["m"]) or b"\0", bytes(x["x"]) or b"\0", bytes(x["a"]) or b"\0",
+                    1 if x["q"] == -1 and x["g"] == -1 else 0) for x in pv[o:o + m]]
+            assert got == lists[k], (i, k)
+
+
 @pytest.mark.skipif(not ref_available(), reason="reference objects not built")
 def test_oracle_stage2_compute_vs_reference_random():
     from dpbind import random_genome, repeat_genome, stage2_problem

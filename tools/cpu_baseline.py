@@ -51,7 +51,7 @@ def ref_layout(arr):
 
 
 def worker(args):
-    wid, build, budget, reads, mix = args
+    wid, build, budget, reads, mix, config = args
     from gmapdp import workload as W
     shape = W.SHAPES[mix]
     layout = W.Layout(W.CHR22)
@@ -83,6 +83,8 @@ def worker(args):
     fams = [("single", lib.refh_single_gap_batch, ref_layout(d["single"]), shape.single),
             ("end", lib.refh_end_gap_batch, ref_layout(d["end"]), shape.end5 + shape.end3),
             ("genome", lib.refh_genome_gap_batch, ref_layout(d["genome"]), shape.genome)]
+    if config == 1:  # configs[1]: Dynprog_single + Dynprog_end only
+        fams = fams[:2]
     # The host MaxEnt work the GMAP drop-in does for a genome gap (gmapdp_genome_splice_sites: every
     # position of both sides but each side's last, the reference's own Maxent_hr_*_prob; none for the
     # calls the engine answers before reading them) -- the GPU bench takes these as device inputs.
@@ -141,6 +143,8 @@ def worker(args):
                 t["host_maxent"] += time.perf_counter() - t0
                 n["host_maxent"] += k
             n[name] += k
+        if config == 1:
+            continue
         qs, ql, c0, c1, co, ch, pl = oligo_args[n["oligo"] % len(oligo_args)]
         t0 = time.perf_counter()
         fo(qs, qs, ql, c0, c1, co, ch, pl, 1, 500000, sc.ctypes.data, paths.ctypes.data, 1024, pairs.ctypes.data, cap)
@@ -153,9 +157,10 @@ def worker(args):
             t["microexon"] += time.perf_counter() - t0
             n["microexon"] += 1
     per_call = {k: t[k] / max(n[k], 1) for k in t}
-    sec_per_read = (shape.single * per_call["single"] + (shape.end5 + shape.end3) * per_call["end"]
-                    + shape.genome * per_call["genome"] + shape.stage2 * per_call["oligo"]
-                    + shape.microexon * per_call["microexon"])
+    sec_per_read = shape.single * per_call["single"] + (shape.end5 + shape.end3) * per_call["end"]
+    if config != 1:
+        sec_per_read += (shape.genome * per_call["genome"] + shape.stage2 * per_call["oligo"]
+                         + shape.microexon * per_call["microexon"])
     return {"reads_per_s": 1.0 / sec_per_read, "calls": n, "seconds": t, "per_call_us":
             {k: v * 1e6 for k, v in per_call.items()},
             "host_maxent_reads_per_s": 1.0 / max(shape.genome * per_call["host_maxent"], 1e-12)}
@@ -168,6 +173,8 @@ def main():
     ap.add_argument("--budget", type=float, default=10.0, help="seconds of timed calls per worker")
     ap.add_argument("--reads", type=int, default=200, help="reads generated per worker (the sample is cycled)")
     ap.add_argument("--mix", default="d", choices=["d", "appb"], help="per-read call mix (workload.SHAPES)")
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2],
+                    help="BASELINE configs index: 1 = Dynprog_single + Dynprog_end only; 2 = every family + stage 2")
     a = ap.parse_args()
     from gmapdp import workload as W
     shape = W.SHAPES[a.mix]
@@ -180,7 +187,7 @@ def main():
     host_cpus = len(os.sched_getaffinity(0))
     cores = a.cores or min(16, host_cpus)
     with mp.get_context("fork").Pool(cores) as pool:
-        res = pool.map(worker, [(w, a.build, a.budget, a.reads, a.mix) for w in range(cores)])
+        res = pool.map(worker, [(w, a.build, a.budget, a.reads, a.mix, a.config) for w in range(cores)])
     genome_per_read = shape.genome
     total = sum(r["reads_per_s"] for r in res)
     maxent_total = sum(r["host_maxent_reads_per_s"] for r in res)
@@ -191,16 +198,22 @@ def main():
         "build": "gmap.%s objects (oracle/_ref/librefdp_%s.so)" % (a.build, a.build),
         "cpu_model": cpu_model(), "host_cpus_visible": host_cpus, "os_cpu_count": os.cpu_count(),
         "per_core_reads_per_s": total / cores, "per_call_us": per_call,
-        "host_maxent": {"reads_per_s": maxent_total, "per_read_us": per_call["host_maxent"] * genome_per_read,
+        "host_maxent": None if a.config == 1 else {"reads_per_s": maxent_total, "per_read_us": per_call["host_maxent"] * genome_per_read,
                         "note": "the drop-in's host MaxEnt (every splice-site position of every genome gap the engine "
                                 "fills, reference Maxent_hr_*_prob) on the same cores: the ceiling it puts on a "
                                 "pipeline that feeds the GPU bench's calls from host probabilities"},
-        "sample": "%d worker processes x %.0f s of timed reference calls (%s) on the configs[2] per-read mix "
-                  "(%s: %.3g Stage2_compute calls over locus +- %d-nt windows + %.1f single + %.1f end + %.1f "
-                  "genome-gap + %.1f microexon calls per read) cut from a chr22-length i.i.d. genome; per-read time "
-                  "composed from per-call averages"
-                  % (cores, a.budget, ", ".join("%d %s" % (v, k) for k, v in calls.items()), shape.source,
-                     shape.stage2, shape.pad, shape.single, shape.end5 + shape.end3, shape.genome, shape.microexon)}))
+        "sample": ("%d worker processes x %.0f s of timed reference calls (%s) on the configs[1] per-read mix "
+                   "(%s: %.1f single + %.1f end calls per read, Dynprog_single + Dynprog_end only) cut from a chr22 "
+                   "i.i.d. genome; per-read time composed from per-call averages"
+                   % (cores, a.budget, ", ".join("%d %s" % (v, k) for k, v in calls.items() if v), shape.source,
+                      shape.single, shape.end5 + shape.end3)) if a.config == 1 else
+                  ("%d worker processes x %.0f s of timed reference calls (%s) on the configs[2] per-read mix "
+                   "(%s: %.3g Stage2_compute calls over locus +- %d-nt windows + %.1f single + %.1f end + %.1f "
+                   "genome-gap + %.1f microexon calls per read) cut from a chr22-length i.i.d. genome; per-read time "
+                   "composed from per-call averages"
+                   % (cores, a.budget, ", ".join("%d %s" % (v, k) for k, v in calls.items()), shape.source,
+                      shape.stage2, shape.pad, shape.single, shape.end5 + shape.end3, shape.genome,
+                      shape.microexon))}))
 
 
 if __name__ == "__main__":
