@@ -84,25 +84,48 @@ def algorithmic_bytes(rlength, glength, npairs, desc_bytes):
 
 
 def genome_algorithmic_bytes(gp, npairs):
-    """Dynprog_genome_gap: descriptor (96 B) + query and upper-cased query (2 x rlength) + the packed
-    genome blocks of both segments + 8-B splice probability per column of both segments + result
-    (72 B) + one 16-B record per emitted pair."""
+    """Dynprog_genome_gap with its splice-site MaxEnt (the fused operation gg_kernel runs): descriptor (96 B)
+    + query and upper-cased query (2 x rlength) + the packed genome blocks of both segments + result (72 B)
+    + one 16-B record per emitted pair.  The splice probabilities are computed in the kernel from the same
+    segments and the L2-resident model tables, so they are not counted (no probability arena exists)."""
     r = gp["rlength"].astype(np.int64)
     gL = gp["glengthL"].astype(np.int64)
     gR = gp["glengthR"].astype(np.int64)
-    return int((96 + 2 * r + 12 * ((gL + 62) // 32) + 12 * ((gR + 62) // 32) + 8 * (gL + gR) + 72).sum()
+    return int((96 + 2 * r + 12 * ((gL + 62) // 32) + 12 * ((gR + 62) // 32) + 72).sum()
                + 16 * int(np.asarray(npairs).sum()))
 
 
-def chain_algorithmic_bytes(op, s2res):
-    """Stage-2 chaining per call (s2c_kernel): descriptor (48 B) + seeding result (32 B) + npositions
-    and mappings (8 B per query position) + the query twice (cdna and upper case, 2 B per query
-    position) + the result (32 B) + 16-B path records + 20-B pair records of the kept paths.  The
-    mapping positions (4 B each) are read once; totalpositions is not in the stage-2 result, so
-    they are estimated as one per query position."""
+S2_SEED = "gmapdp::oi_kernel+gmapdp::oi_map_kernel"  # the seeding (Oligoindex_hr_tally + get_mappings)
+# stage-2 kernels timed alone: gmapdp_stage2_plan_run's `what` (1 seeding, 4 s2a, 8 s2b, 16 s2c)
+S2_WHAT = {S2_SEED: 1, "gmapdp::s2a_kernel": 4, "gmapdp::s2b_kernel": 8, "gmapdp::s2c_kernel": 16}
+
+
+def stage2_algorithmic_bytes(op, ores, s2res):
+    """Per stage-2 kernel, the algorithmic bytes of one block's calls: ql = querylength,
+    T = totalpositions (seeding hits kept), nd = ndiagonals, W = window length.
+      seeding: descriptor 48 + query ql + genome blocks 12 x ceil((W + 16) / 32) + npositions and mappings 8 ql
+               + table 4 T + result 32 + diagonals 16 nd
+      s2a:     descriptors 48 + 32 + npositions / mappings 8 ql + diagonals 16 nd + table 4 T + chrpos and
+               score arrays out 8 T + per-position offsets, active bounds and ranges 24 ql + result 32
+      s2b:     per-position metadata 20 ql + the chrpos of every hit 4 T + one 36-B link per query position (the
+               chain; a lower bound: the sweep scores every hit in the active ranges)
+      s2c:     the score array 4 T + the kept paths' walk (32 B per pair) + 20-B pair records + 16-B path records
+               + the query twice 2 ql + result 32"""
     ql = op["querylength"].astype(np.int64)
-    return int((48 + 32 + 8 * ql + 2 * ql + 4 * ql + 32).sum() + 16 * int(s2res["nresults"].sum())
-               + 20 * int(s2res["npairs"].sum()))
+    T = np.maximum(ores["totalpositions"].astype(np.int64), 0)
+    nd = np.maximum(ores["ndiagonals"].astype(np.int64), 0)
+    W = (op["chrend"].astype(np.int64) - op["chrstart"].astype(np.int64)).clip(min=0)
+    npairs = int(s2res["npairs"].sum())
+    return {S2_SEED: int((48 + ql + 12 * ((W + 16 + 31) // 32) + 8 * ql + 4 * T + 32 + 16 * nd).sum()),
+            "gmapdp::s2a_kernel": int((80 + 8 * ql + 16 * nd + 4 * T + 8 * T + 24 * ql + 32).sum()),
+            "gmapdp::s2b_kernel": int((20 * ql + 4 * T + 36 * ql).sum()),
+            "gmapdp::s2c_kernel": int((4 * T + 2 * ql + 32).sum()) + 52 * npairs + 16 * int(s2res["nresults"].sum())}
+
+
+def workload_id(args):
+    """The committed PMC / iso summaries a bench line may cite are the ones of its own workload:
+    c<config>[-appb][-simd] (tools/profile.sh records it)."""
+    return "c%d%s%s" % (args.config, "-appb" if args.mix == "appb" else "", "-simd" if args.simd else "")
 
 
 def band_cells(rlength, glength, lband, uband):
@@ -146,16 +169,20 @@ def genome_cells(gp, g_fills):
 # ---------------------------------------------------------------------------------------------------
 # committed profiles (profiles/*): PMC traffic, VALU instructions, rocprof average duration
 # ---------------------------------------------------------------------------------------------------
-def profile_record(kind, name):
-    """The committed record of `kind` the bench line cites: the one profiles/current.json names, else the
-    newest by the "recorded" time the writing tool stored in it (tools/pmc_summary.py, tools/e2e_timing.py);
-    records without one rank oldest.  Never by path name or file mtime (a checkout sets mtimes in checkout
-    order).  Returns (parsed json, path relative to ROOT) or (None, None)."""
+def profile_record(kind, name, workload):
+    """The committed record of `kind` for `workload` (workload_id) the bench line cites: the one
+    profiles/current.json names for it ({kind: {workload: path}}), else the newest of that workload by the
+    "recorded" time the writing tool stored in it (tools/pmc_summary.py); records without one rank oldest.
+    Never by path name or file mtime (a checkout sets mtimes in checkout order), and never a record of
+    another workload (a summary whose "workload" differs is skipped).  Returns (parsed json, path relative
+    to ROOT) or (None, None)."""
     import glob
     try:
         cur = json.load(open(os.path.join(ROOT, "profiles", "current.json"))).get(kind)
     except (OSError, ValueError):
         cur = None
+    if isinstance(cur, dict):
+        cur = cur.get(workload)
     paths = [os.path.join(ROOT, cur)] if cur else glob.glob(os.path.join(ROOT, "profiles", "*", name))
     best = None
     for path in paths:
@@ -163,34 +190,49 @@ def profile_record(kind, name):
             d = json.load(open(path))
         except (OSError, ValueError):
             continue
+        if workload is not None and d.get("workload") != workload:
+            continue
         key = d.get("recorded") or ""
         if best is None or key > best[0]:
             best = (key, d, os.path.relpath(path, ROOT))
     return (best[1], best[2]) if best else (None, None)
 
 
-def pmc_entry(key, kind="pmc_summary"):
-    """The cited PMC summary's record of kernel `key` ('+'-joined names are summed), or (None, None).
-    kind: "pmc_summary" (the nosimd step) or "pmc_summary_simd" (the --simd step), as profiles/current.json
-    names them."""
-    d, src = profile_record(kind, "pmc_summary.json")
+def pmc_entry(key, workload):
+    """The PMC summary of this workload's step (tools/profile.sh + tools/pmc_summary.py): the record of kernel
+    `key` ('+'-joined names and template instances of one kernel are summed per step), or (None, source)."""
+    d, src = profile_record("pmc_summary", "pmc_summary.json", workload)
     if not d:
         return None, None
     ks = d.get("kernels", {})
-    parts = key.split("+")
-    if not all(p in ks for p in parts):
-        return None, src
     rec = {}
+    parts = key.split("+")
+    # a plain name (gmapdp::s2c_kernel) covers its template instances (s2c_kernel<false>, <true>)
+    members = [[k for k in ks if k == p or (("<" not in p) and k.startswith(p + "<"))] for p in parts]
+    if not all(members):
+        return None, src
     for f in ("hbm_bytes_per_dispatch", "sq_SQ_INSTS_VALU_sum_avg", "avg_duration_ns"):
-        vals = [ks[p].get(f) for p in parts]
-        rec[f] = None if any(v is None for v in vals) else sum(vals)
+        tot = 0.0
+        for m in members:
+            for k in m:
+                v = ks[k].get(f)
+                if v is None:
+                    tot = None
+                    break
+                # per bench launch: a template instance dispatched on fewer blocks counts in proportion
+                disp = ks[k].get("dispatches") or 1
+                ref = max(ks[x].get("dispatches") or 1 for x in m)
+                tot += v * disp / ref
+            if tot is None:
+                break
+        rec[f] = tot
     return rec, src
 
 
-def iso_entry(key, kind="iso_summary"):
-    """The cited rocprofv3 --kernel-trace --stats record of `bench.py --iso-kernel <key>` (the dominant
-    kernel's launches run alone, tools/pmc_summary.py --iso): {avg_duration_ns, dispatches, ...}."""
-    d, src = profile_record(kind, "iso_summary.json")
+def iso_entry(key, workload):
+    """The committed rocprofv3 --kernel-trace --stats record of `bench.py --iso-kernel <key>` on this
+    workload (tools/pmc_summary.py --iso): {avg_duration_ns, dispatches, ...}."""
+    d, src = profile_record("iso_summary", "iso_summary.json", workload)
     if not d or d.get("kernel") != key:
         return None, src
     return d, src
@@ -216,7 +258,7 @@ def rocprof_name(kind, R, dl, lds=0):
 def latest_e2e():
     """The cited GMAP end-to-end record (tools/e2e_timing.py, profiles/*/e2e.json; profile_record's rule):
     the unmodified gmap and the drop-in on the same reads and host cores."""
-    d, src = profile_record("e2e", "e2e.json")
+    d, src = profile_record("e2e", "e2e.json", None)
     try:
         runs = d["runs"]
     except (TypeError, KeyError):
@@ -542,7 +584,14 @@ def main():
             orun(b, ostream, 1)
             if ev is not None:
                 ev["oligo"][1].record(ostream)
-            orun(b, ostream, 2)
+            # the chaining as its three kernels (what 4 / 8 / 16: s2a, the s2b sweep, s2c), events between
+            orun(b, ostream, 4)
+            if ev is not None:
+                ev["s2a"].record(ostream)
+            orun(b, ostream, 8)
+            if ev is not None:
+                ev["s2b"].record(ostream)
+            orun(b, ostream, 16)
             if ev is not None:
                 ev["chain"][1].record(ostream)
         if do_dp:
@@ -618,8 +667,25 @@ def main():
 
     def iso_launches(name, reps, with_bytes):
         """Every launch class of kernel `name`, one launch at a time on one stream, HIP events around each
-        (on the stream it runs on); per dispatch: (ms, algorithmic bytes, cells)."""
+        (on the stream it runs on); per dispatch: (ms, algorithmic bytes, cells).  A stage-2 kernel (S2_WHAT)
+        runs alone over the scratch of a full untimed stage-2 run of the same block."""
         out = []
+        if name in S2_WHAT:
+            with torch.cuda.stream(stream):
+                for rep in range(reps):
+                    for b in B:
+                        if b["oplan"] is None:
+                            continue
+                        orun(b, stream, 3)
+                        e0, e1 = mk()
+                        e0.record(stream)
+                        orun(b, stream, S2_WHAT[name])
+                        e1.record(stream)
+                        torch.cuda.synchronize()
+                        if "s2bytes" not in b:
+                            b["s2bytes"] = stage2_bytes(b)
+                        out.append((e0.elapsed_time(e1), b["s2bytes"][name], 0))
+            return out
         with torch.cuda.stream(stream):
             for rep in range(reps):
                 for b in B:
@@ -645,8 +711,8 @@ def main():
             for k in range(warmup):
                 step(B[k % len(B)], **kw)
             torch.cuda.synchronize()
-            evs = [{"oligo": mk(), "chain": mk(), "mx": mk(), "dp": [mk() for _ in B[k % len(B)]["names"]]}
-                   for k in range(steps)]
+            evs = [{"oligo": mk(), "chain": mk(), "mx": mk(), "s2a": mk()[0], "s2b": mk()[0],
+                    "dp": [mk() for _ in B[k % len(B)]["names"]]} for k in range(steps)]
             if world > 1:
                 dist.barrier()
             torch.cuda.synchronize()
@@ -661,8 +727,22 @@ def main():
             elapsed = shard.max_over_ranks(elapsed, dist, device=dev)
         return elapsed, evs
 
+    def stage2_bytes(b):
+        """Algorithmic bytes of block b's stage-2 kernels, from its last run's seeding and
+        chaining results."""
+        op = b["d"]["oligo"]
+        ores = np.zeros(len(op), dtype=gmapdp.OLIGO_RESULT_DTYPE)
+        eng._check(lib.gmapdp_stage2_plan_seeding_results(eng.h, b["oplan"], C.c_void_p(stream.cuda_stream),
+                                                          ores.ctypes.data), "gmapdp_stage2_plan_seeding_results")
+        torch.cuda.synchronize()
+        s2res = np.frombuffer(d_s2res.cpu().numpy().tobytes(), dtype=gmapdp.STAGE2_RESULT_DTYPE)[:len(op)]
+        return stage2_algorithmic_bytes(op, ores, s2res)
+
     if args.iso_kernel:
-        if not any(args.iso_kernel in b["names"] for b in B):
+        if args.iso_kernel in S2_WHAT:
+            if not all(b["oplan"] is not None for b in B):
+                raise SystemExit("bench: no Stage2_compute calls in this workload")
+        elif not any(args.iso_kernel in b["names"] for b in B):
             raise SystemExit("bench: no launch class of %s in this workload" % args.iso_kernel)
         rows = iso_launches(args.iso_kernel, args.iso_reps, True)
         ms = [r[0] for r in rows]
@@ -729,7 +809,8 @@ def main():
         npairs, gnp, gsimple, g_fills = class_outputs(b, res, gres)
         cells_total += dp_cells(sp, ep, gp, g_fills)
         b["bytes"], b["cells"] = zip(*[class_bytes(b, li, npairs, gnp, g_fills) for li in range(len(b["names"]))])
-        b["chain_bytes"] = chain_algorithmic_bytes(op, s2res)
+        if b["oplan"] is not None:
+            b["s2bytes"] = stage2_bytes(b)
         checks["pairs"] += int(npairs.sum() + gnp.sum())
         checks["genome_gaps_bridged"] += int((gnp > 0).sum())
         checks["genome_gap_simple"] += int(gsimple.sum())
@@ -744,31 +825,53 @@ def main():
         for li, name in enumerate(b["names"]):
             add(name, e["dp"][li][0].elapsed_time(e["dp"][li][1]), b["bytes"][li])
         if b["oplan"] is not None:
-            add("gmapdp::oi_kernel<unsigned short>+gmapdp::oi_map_kernel", e["oligo"][0].elapsed_time(e["oligo"][1]),
-                None)
-            add("gmapdp::s2a_kernel+gmapdp::s2b_kernel+gmapdp::s2c_kernel", e["oligo"][1].elapsed_time(e["chain"][1]),
-                b["chain_bytes"])
+            sb = b["s2bytes"]
+            add(S2_SEED, e["oligo"][0].elapsed_time(e["oligo"][1]), sb[S2_SEED])
+            add("gmapdp::s2a_kernel", e["oligo"][1].elapsed_time(e["s2a"]), sb["gmapdp::s2a_kernel"])
+            add("gmapdp::s2b_kernel", e["s2a"].elapsed_time(e["s2b"]), sb["gmapdp::s2b_kernel"])
+            add("gmapdp::s2c_kernel", e["s2b"].elapsed_time(e["chain"][1]), sb["gmapdp::s2c_kernel"])
         if b["mplan"] is not None:
             add("gmapdp::mx_search_kernel+gmapdp::mx_finish_kernel", e["mx"][0].elapsed_time(e["mx"][1]), None)
-    dominant = max((n for n in per_kernel if per_kernel[n][2] > 0 and "+" not in n), key=lambda n: per_kernel[n][0])
+    # the dominant kernel: the largest in-step time among the single kernels (and the seeding pair)
+    dominant = max((n for n in per_kernel if per_kernel[n][2] > 0), key=lambda n: per_kernel[n][0])
     dms, dn, dbytes = per_kernel[dominant]
+    wl = workload_id(args)
+
+    def kernel_roofline(name, reps):
+        """`name`'s launches alone (every block, one at a time on one stream, HIP events) against its
+        algorithmic bytes, with the committed PMC summary of this workload's step (traffic, VALU)."""
+        rows = iso_launches(name, reps, False)
+        n = len(rows)
+        ms = sum(r[0] for r in rows) / n
+        nbytes = sum(r[1] for r in rows) / n
+        cells = sum(r[2] for r in rows) / n
+        ach = nbytes / (ms * 1e-3) / 1e9
+        pmc, psrc = pmc_entry(name, wl)
+        traffic = pmc["hbm_bytes_per_dispatch"] if pmc else None
+        valu = pmc["sq_SQ_INSTS_VALU_sum_avg"] if pmc else None
+        return {"kernel": name, "dispatches_timed": n, "ms_per_launch": ms, "algorithmic_bytes_per_launch": nbytes,
+                "achieved": ach, "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
+                "traffic_over_algorithmic": traffic / nbytes if traffic and nbytes else None, "traffic_source": psrc,
+                "valu_insts_per_launch": valu,
+                "valu_issue_frac": valu / (VALU_WAVE_INSTR_PEAK * ms * 1e-3) if valu else None,
+                "rocprof_avg_ms_in_step_committed": pmc["avg_duration_ns"] / 1e6 if pmc and pmc.get("avg_duration_ns")
+                else None,
+                "ms_per_launch_in_step": per_kernel[name][0] / per_kernel[name][1] if name in per_kernel else None,
+                "cells_per_launch": cells}
 
     # ---- the dominant kernel alone (its launches of every block, one at a time on one stream) ----
-    rows = iso_launches(dominant, 3, False)
-    iso_n = len(rows)
-    iso_ms = sum(r[0] for r in rows)
-    iso_bytes = sum(r[1] for r in rows)
-    iso_cells = sum(r[2] for r in rows)
-    kms = iso_ms / iso_n
-    kbytes = iso_bytes / iso_n
-    kcells = iso_cells / iso_n
-    ach = kbytes / (kms * 1e-3) / 1e9
-    pmc, psrc = pmc_entry(dominant, "pmc_summary_simd" if args.simd else "pmc_summary")
-    traffic = pmc["hbm_bytes_per_dispatch"] if pmc else None
-    valu = pmc["sq_SQ_INSTS_VALU_sum_avg"] if pmc else None
-    prof_ms = pmc["avg_duration_ns"] / 1e6 if pmc and pmc.get("avg_duration_ns") else None
-    iso, isrc = iso_entry(dominant, "iso_summary_simd" if args.simd else "iso_summary")
+    dom = kernel_roofline(dominant, 3)
+    kms, kbytes, kcells, ach = dom["ms_per_launch"], dom["algorithmic_bytes_per_launch"], dom["cells_per_launch"], \
+        dom["achieved"]
+    traffic, psrc, valu = dom["traffic"], dom["traffic_source"], dom["valu_insts_per_launch"]
+    prof_ms = dom["rocprof_avg_ms_in_step_committed"]
+    iso, isrc = iso_entry(dominant, wl)
     iso_prof_ms = iso["avg_duration_ns"] / 1e6 if iso else None
+    # beside it: the stage-2 kernels (the step's long pole) and the largest DP class
+    others = [n for n in list(S2_WHAT) + [max((n for n in per_kernel if n not in S2_WHAT),
+                                              key=lambda n: per_kernel[n][0], default=None)]
+              if n and n != dominant and n in per_kernel]
+    roofline_others = [kernel_roofline(n, 1) for n in others]
 
     # ---- PCIe: one block's inputs up and outputs down through pinned host memory (outside the step) ----
     b = B[0]
@@ -841,7 +944,8 @@ def main():
                      "kernel_ms_per_launch": kms, "algorithmic_bytes_per_launch": kbytes,
                      "timing": "HIP events around each of the kernel's launches run alone on one stream (%d "
                                "dispatches, after the timed region); in the timed steps, which share the CUs "
-                               "four streams wide, its launches average %.3f ms" % (iso_n, dms / dn),
+                               "four streams wide, its launches average %.3f ms" % (dom["dispatches_timed"], dms / dn),
+                     "traffic_over_algorithmic": dom["traffic_over_algorithmic"], "workload_id": wl,
                      "kernel_ms_per_launch_in_step": dms / dn, "rocprof_avg_ms_committed": prof_ms,
                      "rocprof_isolated": {"source": isrc, "avg_ms": iso_prof_ms,
                                           "dispatches": iso["dispatches"] if iso else None,
@@ -863,9 +967,10 @@ def main():
                                  "frac": OPS_PER_CELL * kcells / (INT_OPS_PEAK * kms * 1e-3) if kcells else None,
                                  "peak_ops_per_s": INT_OPS_PEAK,
                                  "note": "genome-gap fills counted only where genome_gap_simple did not answer"},
-                     "note": "integer VALU/LDS/latency-bound DP (SURVEY §8d); the HBM roofline is reported as "
-                             "required, the VALU issue and algorithmic int-op fractions are the binding bounds "
-                             "(BASELINE.md §3(i))"},
+                     "note": "integer VALU/LDS/latency-bound DP and a serial stage-2 sweep (SURVEY §8d); the HBM "
+                             "roofline is reported as required, the VALU issue fraction (and for DP fills the "
+                             "algorithmic int-op fraction) are the binding bounds (BASELINE.md §3(i))"},
+        "roofline_other_kernels": roofline_others,
         "gcups": cells_total / len(B) * world * args.steps / elapsed / 1e9,
         "step_split_ms": {"stage2_alone": el_o / half * 1e3 if el_o is not None else None,
                           "stage2_alone_seeding": s2_seed_ms,

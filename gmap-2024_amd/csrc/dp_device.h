@@ -8,6 +8,7 @@
 
 #include "gmapdp_internal.h"
 #include "../../include/gmapdp.h"
+#include "me_device.h"
 
 namespace gmapdp {
 
@@ -1132,10 +1133,12 @@ __device__ inline bool gg_simple_wave(int lane, const DevGenomeProblem& P, int p
                                const uint8_t* ldi, const uint8_t* rdi, const double* pL, const double* pR,
                                int* diagL, int* diagR, gmapdp_pair* out, gmapdp_genome_result& res,
                                gmapdp_genome_result* __restrict__ results, const uint8_t* __restrict__ ks = nullptr,
-                               const double* __restrict__ raw = nullptr) {
+                               const double* __restrict__ raw = nullptr, const uint32_t* __restrict__ blocks = nullptr,
+                               uint64_t nwords = 0, const double* __restrict__ metab = nullptr) {
   // ks: genome_gap_simple's own known-site flags (left [0, rlength], right after them; nullptr: none),
   // raw: the MaxEnt probabilities (left [0, glengthL), right after them) that get_splicesite_probs
-  // returns for an unknown site (dynprog_genome.c:3045-3049, 3118-3119, 3171)
+  // returns for an unknown site (dynprog_genome.c:3045-3049, 3118-3119, 3171); raw NULL: evaluated
+  // here from the models (metab) on the genome (blocks)
   const int rlen = P.rlength;
   const int8_t* sct = sctab + (size_t)P.mismatchtype * 128 * kNClass;
   const int8_t* iscp = isctab + (size_t)P.iclass * 128;  // prelim array (:3032)
@@ -1181,8 +1184,9 @@ __device__ inline bool gg_simple_wave(int lane, const DevGenomeProblem& P, int p
   const int finalscore = halfp ? bestscore - scoreI / 2 : bestscore;
   if (finalscore <= 0) return false;
   if (ks) {
-    res.left_prob = ks[bestrL] ? 1.0 : raw[bestrL];
-    res.right_prob = ks[rlen + 1 + bestrR] ? 1.0 : raw[P.glengthL + bestrR];
+    res.left_prob = ks[bestrL] ? 1.0 : raw ? raw[bestrL] : gg_site_prob(P, blocks, nwords, metab, bestrL);
+    res.right_prob = ks[rlen + 1 + bestrR] ? 1.0
+                   : raw ? raw[P.glengthL + bestrR] : gg_site_prob(P, blocks, nwords, metab, P.glengthL + bestrR);
   } else {
     res.left_prob = pL[bestrL];
     res.right_prob = pR[bestrR];

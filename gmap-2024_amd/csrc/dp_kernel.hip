@@ -701,7 +701,9 @@ __global__ __launch_bounds__(128) GGX_ATTR void gg_kernel(
     const char* __restrict__ qseq, const char* __restrict__ qseq_uc, const double* __restrict__ sprob,
     const int8_t* __restrict__ sctab, const uint8_t* __restrict__ constab, const int8_t* __restrict__ isctab,
     gmapdp_genome_result* __restrict__ results, gmapdp_pair* __restrict__ pairs,
-    unsigned char* __restrict__ gscratch, const uint8_t* __restrict__ known) {
+    unsigned char* __restrict__ gscratch, const uint8_t* __restrict__ known, const double* __restrict__ metab) {
+  // sprob NULL: the splice probabilities are GMAP's MaxEnt models (metab) evaluated here while the
+  // segments are staged (no probability arena written by a prologue kernel and read back)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -811,7 +813,7 @@ __global__ __launch_bounds__(128) GGX_ATTR void gg_kernel(
         bit[u] = (uint32_t)(g & 31u);
         wf[u] = blocks[pp + 2];
         wv[u] = blocks[pp + (bit[u] < 16 ? 1 : 0)];
-        pv[u] = act ? sprob[P.prob_offset + jj] : 0.0;
+        pv[u] = !act ? 0.0 : sprob ? sprob[P.prob_offset + jj] : gg_site_prob(P, blocks, nwords, metab, jj);
         // a known site has probability 1.0 in the bridge (dynprog_genome.c:2577-2578)
         if (kn && act && kb[jj]) pv[u] = 1.0;
       }
@@ -862,7 +864,8 @@ __global__ __launch_bounds__(128) GGX_ATTR void gg_kernel(
     if (wave == 0) {
       const bool ok = gg_simple_wave(lane, P, pid, sctab, isctab, cons, qL, qucL, qR, qucR, gclL, gclR, gchL, gchR,
                                      ldi, rdi, pL, pR, diagL, diagR, out, res, results,
-                                     kn ? kb + gL + gR : nullptr, sprob + P.prob_offset);
+                                     kn ? kb + gL + gR : nullptr, sprob ? sprob + P.prob_offset : nullptr, blocks,
+                                     nwords, metab);
       if (lane == 0) *done = ok ? 1 : 0;
     }
     __syncthreads();
@@ -1171,7 +1174,7 @@ hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
                      const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
                      const char* qseq_uc, const double* sprob, const int8_t* sctab, const uint8_t* constab,
                      const int8_t* isctab, gmapdp_genome_result* results, gmapdp_pair* pairs,
-                     unsigned char* gscratch, const uint8_t* known) {
+                     unsigned char* gscratch, const uint8_t* known, const double* metab) {
   void* fn = nullptr;
 #define GMAPDP_CASE(RR)                                          \
   case RR:                                                       \
@@ -1194,7 +1197,7 @@ hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
   }
   void* args[] = {(void*)&probs, (void*)&order, (void*)&blocks, (void*)&nwords, (void*)&qseq, (void*)&qseq_uc,
                   (void*)&sprob, (void*)&sctab, (void*)&constab, (void*)&isctab, (void*)&results, (void*)&pairs,
-                  (void*)&gscratch, (void*)&known};
+                  (void*)&gscratch, (void*)&known, (void*)&metab};
   return hipLaunchKernel(fn, dim3(nblocks), dim3(128), args, lds, stream);
 }
 

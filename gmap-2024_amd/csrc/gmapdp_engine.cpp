@@ -51,7 +51,7 @@ hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t 
                      const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
                      const char* qseq_uc, const double* sprob, const int8_t* sctab, const uint8_t* constab,
                      const int8_t* isctab, gmapdp_genome_result* results, gmapdp_pair* pairs,
-                     unsigned char* gscratch, const uint8_t* known);
+                     unsigned char* gscratch, const uint8_t* known, const double* metab);
 size_t lds_bytes_sj(int rlength, int glength, int R, bool dirs_lds);
 hipError_t launch_usj(int B, int nblocks, size_t lds, hipStream_t stream, const DevSjProblem* probs, const int* order,
                       unsigned char* gscratch, const char* qseq, const char* qseq_uc, const char* jseq,
@@ -89,7 +89,7 @@ hipError_t launch_s2c(int nproblems, hipStream_t stream, const DevStage2Problem*
                       const int32_t* npos, const int32_t* map, const uint32_t* table, const int32_t* diags,
                       unsigned char* scratch, unsigned long long* counters, unsigned long long scratch_cap,
                       gmapdp_stage2_result* results, gmapdp_path* paths, unsigned long long path_cap,
-                      gmapdp_path_pair* pairs, unsigned long long pair_cap);
+                      gmapdp_path_pair* pairs, unsigned long long pair_cap, int phases = 7);
 hipError_t launch_oi(bool wide, int nproblems, size_t lds, hipStream_t stream, const DevOligoProblem* probs,
                      const uint32_t* blocks, const char* quc, unsigned char* scratch, gmapdp_oligo_result* results,
                      int32_t* npos, int32_t* map, uint32_t* table, int32_t* diags, uint64_t* pool,
@@ -1327,11 +1327,11 @@ static hipError_t launch_one(gmapdp_ctx* ctx, const PlanCore& plan, int li, cons
                      ctx->genome_words, a.d_q, a.d_quc, ctx->d_sc, ctx->d_cs, a.d_results, a.d_pairs,
                      (uint64_t*)ctx->gdirs.p);
   if (!a.d_gresults || !a.d_sprob) return hipErrorInvalidValue;
-  const hipError_t e = prologue ? launch_class_maxent(ctx, L, a, stream) : hipSuccess;
-  if (e != hipSuccess) return e;
+  // device MaxEnt: gg_kernel evaluates the models while it stages the segments (no me_gap_kernel prologue,
+  // no probability arena written and read back); host probabilities: read from d_sprob
   return launch_gg(L.R, L.dirs_lds, L.count, L.lds, stream, a.d_gprobs, a.d_gorder + L.first, ctx->d_genome,
-                   ctx->genome_words, a.d_q, a.d_quc, a.d_sprob, ctx->d_sc, ctx->d_cs, ctx->d_isc, a.d_gresults,
-                   a.d_pairs, (unsigned char*)ctx->gdirs.p, a.d_known);
+                   ctx->genome_words, a.d_q, a.d_quc, a.d_metab ? nullptr : a.d_sprob, ctx->d_sc, ctx->d_cs,
+                   ctx->d_isc, a.d_gresults, a.d_pairs, (unsigned char*)ctx->gdirs.p, a.d_known, a.d_metab);
 }
 
 static int run_plan(gmapdp_ctx* ctx, const PlanCore& plan, const RunArgs& a, hipStream_t stream) {
@@ -3275,19 +3275,19 @@ static void stage2_plan_free(gmapdp_stage2_plan* p) {
 }
 
 static int stage2_plan_launch(gmapdp_ctx* ctx, const gmapdp_stage2_plan* P, const char* d_qseq, const char* d_qseq_uc,
-                              gmapdp_stage2_result* d_results, hipStream_t s, bool seed, bool chain) {
+                              gmapdp_stage2_result* d_results, hipStream_t s, bool seed, int chain) {
   if (seed) {
     if (hipMemsetAsync(P->d_npos, 0, sizeof(int32_t) * P->qbytes, s) != hipSuccess)
       return fail(ctx, GMAPDP_ELAUNCH, "stage-2 plan: %s", hipGetLastError());
     int rc = gmapdp_oligo_plan_run(ctx, P->oplan, d_qseq_uc, P->d_ores, P->d_npos, P->d_map, P->d_table, P->d_diag, s);
     if (rc) return rc;
   }
-  if (chain) {
-    if (hipMemsetAsync(P->d_counters, 0, 4 * sizeof(unsigned long long), s) != hipSuccess)
+  if (chain) {  // phases: 1 s2a, 2 s2b, 4 s2c (the pools restart with s2a or s2c)
+    if ((chain & 5) && hipMemsetAsync(P->d_counters, 0, 4 * sizeof(unsigned long long), s) != hipSuccess)
       return fail(ctx, GMAPDP_ELAUNCH, "stage-2 plan: %s", hipGetLastError());
     hipError_t e = launch_s2c(P->n, s, P->d_probs, ctx->d_genome, ctx->genome_words, d_qseq, d_qseq_uc, P->d_ores,
                               P->d_npos, P->d_map, P->d_table, P->d_diag, P->d_scratch, P->d_counters, P->scratch,
-                              d_results, P->d_paths, P->path_cap, P->d_pairs, P->pair_cap);
+                              d_results, P->d_paths, P->path_cap, P->d_pairs, P->pair_cap, chain);
     if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "stage-2 chaining launch: %s", e);
   }
   return GMAPDP_OK;
@@ -3338,7 +3338,7 @@ int gmapdp_stage2_plan_create(gmapdp_ctx* ctx, const gmapdp_stage2_problem* prob
     return fail(ctx, GMAPDP_ENOMEM, "stage-2 plan: %s", e);
   }
   // size the chaining scratch from one seeding run
-  rc = stage2_plan_launch(ctx, P, nullptr, (const char*)ctx->qseq_uc.p, nullptr, ctx->stream, true, false);
+  rc = stage2_plan_launch(ctx, P, nullptr, (const char*)ctx->qseq_uc.p, nullptr, ctx->stream, true, 0);
   std::vector<gmapdp_oligo_result> ores(n);
   std::vector<int32_t> nhits(n);
   if (!rc) {
@@ -3392,8 +3392,20 @@ int gmapdp_stage2_plan_run(gmapdp_ctx* ctx, const gmapdp_stage2_plan* plan, cons
                            gmapdp_stage2_result* d_results, int what, void* stream) {
   if (!ctx || !plan || !d_qseq || !d_qseq_uc || !d_results) return GMAPDP_EINVAL;
   (void)hipSetDevice(ctx->device);
+  // what: 1 seeding, 2 chaining; or one chaining kernel alone over a previous run's scratch: 4 s2a, 8 s2b, 16 s2c
+  const int chain = (what & 2) ? 7 : ((what >> 2) & 7);
   return stage2_plan_launch(ctx, plan, d_qseq, d_qseq_uc, d_results, stream ? (hipStream_t)stream : ctx->stream,
-                            (what & 1) != 0, (what & 2) != 0);
+                            (what & 1) != 0, chain);
+}
+
+int gmapdp_stage2_plan_seeding_results(gmapdp_ctx* ctx, const gmapdp_stage2_plan* plan, void* stream,
+                                       gmapdp_oligo_result* out) {
+  if (!ctx || !plan || !out) return GMAPDP_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  hipError_t e = hipMemcpyAsync(out, plan->d_ores, sizeof(gmapdp_oligo_result) * plan->n, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = ctx_sync(ctx, s);
+  return e == hipSuccess ? GMAPDP_OK : fail(ctx, GMAPDP_ELAUNCH, "stage-2 seeding results: %s", e);
 }
 
 int gmapdp_stage2_plan_outputs(const gmapdp_stage2_plan* plan, gmapdp_path** d_paths, gmapdp_path_pair** d_pairs,

@@ -13,6 +13,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "gmapdp_internal.h"
+
 namespace gmapdp {
 
 // entries of the 16 tables, in tools/make_maxent_tables.py's TABLES order
@@ -67,6 +69,30 @@ __device__ __forceinline__ double maxent_prob(const uint32_t* __restrict__ block
     odds *= T[me_offset(15) + ((W >> 10) & 0x3FFF)];
   }
   return odds / (1.0 + odds);
+}
+
+// The probability bridge_intron_gap_site_level reads for genome-gap entry jj (dynprog_genome.c:2573-2660;
+// me_gap_kernel's layout): left entries cL = jj < glengthL at chroffset + goffsetL + cL (plus strand) or
+// chrhigh - goffsetL - cL + 1, right entries cR = jj - glengthL at chroffset + rev_goffsetR - cR + 1 or
+// chrhigh - rev_goffsetR + cR; donor / acceptor models for cdna_direction > 0 (iclass 0), antiacceptor /
+// antidonor otherwise, mirrored on the minus strand.
+__device__ __forceinline__ double gg_site_prob(const DevGenomeProblem& P, const uint32_t* __restrict__ blocks,
+                                               uint64_t nwords, const double* __restrict__ T, int jj) {
+  const bool watson = P.flags & kFWatson;
+  const bool sense = P.iclass == 0;
+  const uint64_t lo = (uint64_t)(int64_t)P.goffsetL, ro = (uint64_t)(int64_t)P.rev_goffsetR;
+  uint64_t pos;
+  int model;
+  if (jj < P.glengthL) {
+    const uint64_t c = (uint64_t)jj;
+    pos = watson ? P.chroffset + lo + c : P.chrhigh - lo - c + 1u;
+    model = watson ? (sense ? 0 : 3) : (sense ? 2 : 1);
+  } else {
+    const uint64_t c = (uint64_t)(jj - P.glengthL);
+    pos = watson ? P.chroffset + ro - c + 1u : P.chrhigh - ro + c;
+    model = watson ? (sense ? 1 : 2) : (sense ? 3 : 0);
+  }
+  return maxent_prob(blocks, nwords, T, model, pos, P.chroffset);
 }
 #endif
 

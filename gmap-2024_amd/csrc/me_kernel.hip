@@ -30,27 +30,9 @@ __global__ __launch_bounds__(256) void me_gap_kernel(const DevGenomeProblem* __r
   const int k = blockIdx.x;
   if (k >= n) return;
   const DevGenomeProblem P = probs[order ? order[k] : k];
-  const bool watson = P.flags & kFWatson;
-  const bool sense = P.iclass == 0;  // cdna_direction > 0
-  const uint64_t lo = (uint64_t)(int64_t)P.goffsetL, ro = (uint64_t)(int64_t)P.rev_goffsetR;
-  const int ml = watson ? (sense ? 0 : 3) : (sense ? 2 : 1);  // left models
-  const int mr = watson ? (sense ? 1 : 2) : (sense ? 3 : 0);  // right models
   double* out = sprob + P.prob_offset;
   const int total = P.glengthL + P.glengthR;
-  for (int e = threadIdx.x; e < total; e += blockDim.x) {
-    uint64_t pos;
-    int model;
-    if (e < P.glengthL) {
-      const uint64_t c = (uint64_t)e;
-      pos = watson ? P.chroffset + lo + c : P.chrhigh - lo - c + 1u;
-      model = ml;
-    } else {
-      const uint64_t c = (uint64_t)(e - P.glengthL);
-      pos = watson ? P.chroffset + ro - c + 1u : P.chrhigh - ro + c;
-      model = mr;
-    }
-    out[e] = maxent_prob(blocks, nwords, T, model, pos, P.chroffset);
-  }
+  for (int e = threadIdx.x; e < total; e += blockDim.x) out[e] = gg_site_prob(P, blocks, nwords, T, e);
 }
 
 hipError_t launch_me_sites(long long n, hipStream_t s, const uint32_t* blocks, uint64_t nwords, const double* T,

@@ -271,6 +271,7 @@ def load_library(path=LIB_PATH):
         "gmapdp_stage2_plan_fetch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                                C.c_size_t, C.c_void_p, C.c_size_t, P(C.c_size_t), P(C.c_size_t)]),
         "gmapdp_stage2_plan_seeding_classes": (C.c_int, [C.c_void_p, P(C.c_int), P(C.c_int)]),
+        "gmapdp_stage2_plan_seeding_results": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
         "gmapdp_stage2_plan_destroy": (None, [C.c_void_p]),
         "gmapdp_genome_prob_entries": (C.c_size_t, [C.c_void_p, C.c_int]),
         "gmapdp_genome_splice_sites": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t]),

@@ -657,7 +657,8 @@ int gmapdp_stage2_batch (gmapdp_ctx *ctx, const gmapdp_stage2_problem *problems,
  * `stream` against device-resident query arenas.  what: 1 seeding only, 2 chaining only (after a
  * seeding run), 3 both.  d_results: n entries in problem order; paths and pairs stay in the plan's
  * pools (gmapdp_stage2_plan_outputs: device pointers and the counters {scratch, paths, pairs} bytes /
- * records used); a result with status -2 did not fit them. */
+ * records used); a result with status -2 did not fit them.  Profiling: what = 4, 8 or 16 re-runs one
+ * chaining kernel alone (s2a, the s2b sweep, s2c) over the scratch of a previous full run. */
 typedef struct gmapdp_stage2_plan gmapdp_stage2_plan;
 int gmapdp_stage2_plan_create (gmapdp_ctx *ctx, const gmapdp_stage2_problem *problems, int n, const char *qseq,
                                const char *qseq_uc, size_t qbytes, gmapdp_stage2_plan **plan);
@@ -672,6 +673,10 @@ int gmapdp_stage2_plan_outputs (const gmapdp_stage2_plan *plan, gmapdp_path **d_
 int gmapdp_stage2_plan_fetch (gmapdp_ctx *ctx, const gmapdp_stage2_plan *plan, const gmapdp_stage2_result *d_results,
                               void *stream, gmapdp_stage2_result *results, gmapdp_path *paths, size_t path_cap,
                               gmapdp_path_pair *pairs, size_t pair_cap, size_t *paths_needed, size_t *pairs_needed);
+/* The seeding results of the plan's last run (n, problem order; table_offset / diag_offset index the plan's
+ * own arenas), synchronising `stream` (NULL = the context's). */
+int gmapdp_stage2_plan_seeding_results (gmapdp_ctx *ctx, const gmapdp_stage2_plan *plan, void *stream,
+                                        gmapdp_oligo_result *out);
 /* How many of the plan's calls seed with 16-bit and with 32-bit counters (after the plan's sizing run
  * moved every call with fewer than 2^16 hits to the 16-bit class). */
 int gmapdp_stage2_plan_seeding_classes (const gmapdp_stage2_plan *plan, int *n16, int *n32);

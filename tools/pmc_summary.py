@@ -48,6 +48,14 @@ def find(root, sub, name):
     return None
 
 
+def workload_of(src):
+    """the bench workload id tools/profile.sh recorded (bench.py workload_id: c<config>[-appb][-simd])"""
+    try:
+        return open(os.path.join(src, "workload.txt")).read().strip() or None
+    except OSError:
+        return None
+
+
 def main(src, dst, iso=False):
     os.makedirs(dst, exist_ok=True)
     stats = find(src, "stats", "run_kernel_stats.csv")
@@ -87,7 +95,10 @@ def main(src, dst, iso=False):
         return write_iso(src, dst, kern)
     summary = {
         "recorded": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),  # bench.py selects summaries by this
-        "command": "python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline (under rocprofv3, tools/profile.sh)",
+        "workload": workload_of(src),  # ... and only those of its own workload
+        "command": "python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline %s(under rocprofv3, tools/profile.sh)"
+                   % (open(os.path.join(src, "bench_args.txt")).read().strip() + " "
+                      if os.path.exists(os.path.join(src, "bench_args.txt")) else ""),
         "hbm_bytes_rule": "2*FETCH_SIZE + WRITE_SIZE, KB -> bytes x1024 (MI355X_MICROARCH.md HBM: gfx950 "
                           "FETCH_SIZE counts half of wide reads)",
         "kernels": dict(sorted(kern.items(), key=lambda kv: -kv[1].get("total_ms", 0.0))),
@@ -110,7 +121,7 @@ def write_iso(src, dst, kern):
         pass
     k = bench.get("iso_kernel")
     e = kern.get(k, {}) if k else {}
-    out = {"recorded": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
+    out = {"recorded": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()), "workload": workload_of(src),
            "command": "rocprofv3 --kernel-trace --stats -- python3 bench.py --iso-kernel '%s' --iso-reps 3 "
                       "(tools/profile.sh <tag> iso)" % k,
            "kernel": k, "dispatches": e.get("dispatches"), "avg_duration_ns": e.get("avg_duration_ns"),

@@ -5,6 +5,7 @@
 #                                                      (bench.py --iso-kernel: what the line's roofline times)
 #        bash tools/profile.sh <tag> simd            -- the --simd step (gmap.avx2 semantics)
 #        bash tools/profile.sh <tag> isosimd <kernel> -- as iso, in the --simd step
+#        BENCH_ARGS="--config 4" bash tools/profile.sh <tag>  -- another workload (recorded in workload.txt)
 # Summarise with: python3 tools/pmc_summary.py [--iso] gpurun_out/prof_<tag> profiles/<tag>
 set -o pipefail
 TAG=${1:-r1}
@@ -16,6 +17,18 @@ cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 export GMAPDP_BENCH_WORKERS=1
 SIMD=()
 if [ "$MODE" = simd ] || [ "$MODE" = isosimd ]; then SIMD=(--simd); fi
+# further bench.py arguments (the workload: --config 4, --mix appb, ...) and the workload id bench.py
+# matches committed summaries by (bench.py workload_id)
+read -r -a EXTRA <<< "${BENCH_ARGS:-}"
+SIMD+=("${EXTRA[@]}")
+python3 - "${SIMD[@]}" > $OUT/workload.txt <<'PY'
+import sys
+a = sys.argv[1:]
+cfg = a[a.index("--config") + 1] if "--config" in a else "2"
+mix = a[a.index("--mix") + 1] if "--mix" in a else "d"
+print("c%s%s%s" % (cfg, "-appb" if mix == "appb" else "", "-simd" if "--simd" in a else ""))
+PY
+echo "${SIMD[@]}" > $OUT/bench_args.txt
 if [ "$MODE" = iso ] || [ "$MODE" = isosimd ]; then
   KERNEL=$3
   BENCH=(python3 bench.py --iso-kernel "$KERNEL" --iso-reps 3 "${SIMD[@]}")
