@@ -749,6 +749,7 @@ def main():
         nbytes = float(np.mean([r[1] for r in rows]))
         if rank == 0:
             print(json.dumps({"iso_kernel": args.iso_kernel, "dispatches": len(rows), "ms_per_launch": float(np.mean(ms)),
+                              "ms_each": [round(x, 3) for x in ms],
                               "ms_min": min(ms), "ms_max": max(ms), "algorithmic_bytes_per_launch": nbytes,
                               "achieved_gbs": nbytes / (np.mean(ms) * 1e-3) / 1e9,
                               "cells_per_launch": float(np.mean([r[2] for r in rows]))}), flush=True)

@@ -426,14 +426,23 @@ __device__ __forceinline__ void count_inc(CT* cnt, int u) {
   }
 }
 
+// Two waves per problem: both take half of the query's 8-mers and half of the window's pass-1 scan (the
+// long phase: ~200 steps on a 214-kb window) over the same LDS tables; the phases that carry a running
+// value in order (the id ranks, the table layout, pass 2's placement, the per-position mappings) stay
+// on wave 0 between workgroup barriers.  Wave 1 appends its hits from the far end of the hit list (so
+// the two lists meet only when the layout's capacity is exceeded, which is reported as overflow).
+constexpr int kOiWaves = 2;
+
 template <typename CT>
-__global__ __launch_bounds__(64) void oi_kernel(
+__global__ __launch_bounds__(64 * kOiWaves) void oi_kernel(
     const DevOligoProblem* __restrict__ probs, const uint32_t* __restrict__ blocks, const char* __restrict__ quc_all,
     unsigned char* __restrict__ scratch, gmapdp_oligo_result* __restrict__ results, int32_t* __restrict__ npos_out,
     int32_t* __restrict__ map_out, uint32_t* __restrict__ table_all, unsigned long long* __restrict__ pool_counter,
     unsigned long long pool_cap, int32_t* __restrict__ nhits_out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int lane = threadIdx.x;
+  __shared__ int nh_wave[kOiWaves];  // each wave's pass-1 hits
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const DevOligoProblem P = probs[blockIdx.x];
   uint32_t* bitmap = reinterpret_cast<uint32_t*>(smem);                  // 2048 words
   uint16_t* wrank = reinterpret_cast<uint16_t*>(smem + 4 * kOiWords);     // set bits before word w
@@ -445,14 +454,14 @@ __global__ __launch_bounds__(64) void oi_kernel(
   const int nq = qlen - kOiK + 1;  // query positions with a full 8-mer
 
   // ---- the query's 8-mers (Oligoindex_set_inquery) ----
-  for (int w = lane; w < kOiWords; w += 64) bitmap[w] = 0u;
+  for (int w = tid; w < kOiWords; w += 64 * kOiWaves) bitmap[w] = 0u;
   __syncthreads();
   int32_t* npq = npos_out + P.qoff;
   int32_t* mpq = map_out + P.qoff;  // holds each querypos's 8-mer (or -1) until get_mappings
   // 256 query positions per step: one coalesced character load per lane and chunk (5 chunks: the
   // last supplies the 7-character overlap), all issued together; the 8-mer at i takes the codes of
   // lanes i..i+7 of its chunk and the next (ds_bpermute)
-  for (int sb = 0; sb < qlen; sb += 4 * 64) {
+  for (int sb = 4 * 64 * wave; sb < qlen; sb += 4 * 64 * kOiWaves) {
     int ch[5];
 #pragma unroll
     for (int r = 0; r < 5; r++) {
@@ -480,16 +489,16 @@ __global__ __launch_bounds__(64) void oi_kernel(
     }
   }
   __syncthreads();
-  int run = 0;  // ids in oligo order: prefix popcounts over the bitmap words
+  int run = 0;  // ids in oligo order: prefix popcounts over the bitmap words (every wave: U below)
   for (int base = 0; base < kOiWords; base += 64) {
     const int c = __popc(bitmap[base + lane]);
     const int incl = wave_scan_add(lane, c);
-    wrank[base + lane] = (uint16_t)(run + incl - c);
+    if (wave == 0) wrank[base + lane] = (uint16_t)(run + incl - c);
     run += __builtin_amdgcn_readlane(incl, 63);
   }
   const int U = run;  // <= umax (the host counted them)
   OI_MARK(1);
-  for (int u = lane; u < U; u += 64) cnt[u] = 0;
+  for (int u = tid; u < U; u += 64 * kOiWaves) cnt[u] = 0;
   __syncthreads();
 
   // ---- pass 1: counts of the window's query 8-mers ----
@@ -506,7 +515,11 @@ __global__ __launch_bounds__(64) void oi_kernel(
   uint2* hitlist = reinterpret_cast<uint2*>(base_s + so.hits);
   int nhits = 0;
   if (npos > 0) {
-    const uint64_t hlo = left >> 4, hhi = lpl >> 4;
+    // this wave's steps of 64 half-words: wave 0 the first half of the window's, wave 1 the rest
+    const uint64_t hlo0 = left >> 4, hhi0 = lpl >> 4;
+    const uint64_t nsteps = (hhi0 - hlo0) / 64 + 1, half = (nsteps + 1) / 2;
+    const uint64_t hlo = hlo0 + (wave ? 64 * half : 0);
+    const uint64_t hhi = wave ? hhi0 : (hlo0 + 64 * half - 1 < hhi0 ? hlo0 + 64 * half - 1 : hhi0);
     // a window of ~200 kb is ~200 steps: the half-words of the next kOiAhead steps are in flight, so a
     // step waits on an L2 / HBM round trip only at the start (one step ahead left every step waiting)
     constexpr int kOiAhead = 4;
@@ -559,13 +572,16 @@ __global__ __launch_bounds__(64) void oi_kernel(
         bool in;
         const int id = oligo_id(bitmap, wrank, m, in);
         count_inc(cnt, id);
-        if ((uint32_t)o < P.hit_cap) hitlist[o] = make_uint2((uint32_t)(16 * h + j - left), (uint32_t)id);
+        // wave 0 from the start of the list, wave 1 from its end (its k-th hit at hit_cap - 1 - k)
+        if ((uint32_t)o < P.hit_cap)
+          hitlist[wave ? P.hit_cap - 1 - (uint32_t)o : (uint32_t)o] =
+              make_uint2((uint32_t)(16 * h + j - left), (uint32_t)id);
         o++;
       }
       nhits += __builtin_amdgcn_readlane(incl, 63);
     };
     // unrolled by kOiAhead so each slot is a fixed register pair and a step waits for its own loads only
-    for (uint64_t hb0 = hlo; hb0 <= hhi; hb0 += 64 * kOiAhead) {
+    for (uint64_t hb0 = hlo; hlo <= hhi && hb0 <= hhi; hb0 += 64 * kOiAhead) {
 #pragma unroll
       for (int a = 0; a < kOiAhead; a++) {
         const uint64_t hb = hb0 + 64 * a;
@@ -578,31 +594,39 @@ __global__ __launch_bounds__(64) void oi_kernel(
       }
     }
   }
-  if (nhits_out && lane == 0) nhits_out[P.index] = nhits;  // the hit list's length (a plan's sizing run)
+  if (lane == 0) nh_wave[wave] = nhits;
   __syncthreads();
-  // Count_T wraps; the table slices follow oligo order
-  uint32_t tot = 0;
-  for (int base = 0; base < U; base += 64) {
-    const int u = base + lane;
-    const uint32_t c = u < U ? ((uint32_t)cnt[u] & 255u) : 0u;
-    const uint32_t incl = (uint32_t)wave_scan_add(lane, (int)c);
-    if (u < U) {
-      offs[u] = (CT)(tot + incl - c);
-      cnt[u] = (CT)c;
+  const int n0 = nh_wave[0], n1 = nh_wave[1];
+  nhits = n0 + n1;
+  if (nhits_out && tid == 0) nhits_out[P.index] = nhits;  // the hit list's length (a plan's sizing run)
+  // Count_T wraps; the table slices follow oligo order (wave 0; the total to both waves)
+  __shared__ uint32_t tot_s;
+  if (wave == 0) {
+    uint32_t tot = 0;
+    for (int base = 0; base < U; base += 64) {
+      const int u = base + lane;
+      const uint32_t c = u < U ? ((uint32_t)cnt[u] & 255u) : 0u;
+      const uint32_t incl = (uint32_t)wave_scan_add(lane, (int)c);
+      if (u < U) {
+        offs[u] = (CT)(tot + incl - c);
+        cnt[u] = (CT)c;
+      }
+      tot += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     }
-    tot += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    if (lane == 0) tot_s = tot;
   }
   __syncthreads();
+  const uint32_t tot = tot_s;
   OI_MARK(2);
   // More hits or table entries than the layout gave the problem (a plan re-laid out from a measured run,
   // then run on another query), or a 16-bit counter that could wrap: report overflow, as an exhausted
   // event pool does, with no hits and nothing written past the problem's slices.
   if ((uint32_t)nhits > P.hit_cap || tot > P.table_cap || (sizeof(CT) == 2 && nhits > 65535)) {
-    for (int i = lane; i < qlen; i += 64) {
+    for (int i = tid; i < qlen; i += 64 * kOiWaves) {
       npq[i] = 0;
       mpq[i] = -1;
     }
-    if (lane == 0) {
+    if (tid == 0) {
       gmapdp_oligo_result res;
       res.totalpositions = 0;
       res.maxnconsecutive = 0;
@@ -621,12 +645,14 @@ __global__ __launch_bounds__(64) void oi_kernel(
   const uint32_t chrpos0 = P.plusp ? P.chrstart : (P.chrhigh - P.chroffset) - P.chrend;
   const int idbits = U > 1 ? 32 - __clz(U - 1) : 1;
   __threadfence_block();
-  for (int c = 0; c < nhits; c += 64) {
+  for (int c = 0; wave == 0 && c < nhits; c += 64) {
     const int sl = c + lane;  // sl-th hit in store order: plus walks the list backwards
     int id = -1;
     uint32_t k = 0;
     if (sl < nhits) {
-      const uint2 hv = hitlist[P.plusp ? nhits - 1 - sl : sl];
+      // ascending position: wave 0's list, then wave 1's from the list's end backwards
+      const int a = P.plusp ? nhits - 1 - sl : sl;
+      const uint2 hv = hitlist[a < n0 ? (uint32_t)a : P.hit_cap - 1 - (uint32_t)(a - n0)];
       k = hv.x;
       id = (int)hv.y;
     }
@@ -650,9 +676,11 @@ __global__ __launch_bounds__(64) void oi_kernel(
   __syncthreads();
   // the per-id counts again (nhits of lookup, :34074)
   OI_MARK(3);
-  for (int u = lane; u < U; u += 64) cnt[u] = (CT)((u + 1 < U ? (uint32_t)offs[u + 1] : tot) - (uint32_t)offs[u]);
+  for (int u = tid; u < U; u += 64 * kOiWaves)
+    cnt[u] = (CT)((u + 1 < U ? (uint32_t)offs[u + 1] : tot) - (uint32_t)offs[u]);
   __threadfence_block();
   __syncthreads();
+  if (wave) return;  // the rest runs in query order on wave 0
 
   // ---- Oligoindex_get_mappings ----
   gmapdp_oligo_result res;
@@ -883,7 +911,7 @@ hipError_t launch_oi(bool wide, int nproblems, size_t lds, hipStream_t stream, c
   }
   void* args[] = {(void*)&probs, (void*)&blocks, (void*)&quc, (void*)&scratch, (void*)&results, (void*)&npos,
                   (void*)&map, (void*)&table, (void*)&pool_counter, (void*)&pool_cap, (void*)&nhits_out};
-  hipError_t e = hipLaunchKernel(fn, dim3(nproblems), dim3(64), args, lds, stream);
+  hipError_t e = hipLaunchKernel(fn, dim3(nproblems), dim3(64 * kOiWaves), args, lds, stream);
   if (e != hipSuccess) return e;
   void* margs[] = {(void*)&probs, (void*)&scratch, (void*)&results, (void*)&npos, (void*)&map, (void*)&table,
                    (void*)&diags, (void*)&pool};

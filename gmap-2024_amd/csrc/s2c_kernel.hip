@@ -27,6 +27,8 @@
 // run on lane 0 over the problem's L2-resident link arrays.  Scratch and outputs come from batch-wide
 // pools (one atomic per problem); a problem that does not fit reports kS2Overflow and the host reruns
 // the batch with larger pools.
+#include <cstdlib>
+
 #include "dp_device.h"
 #include <climits>
 
@@ -52,6 +54,12 @@ constexpr int kS2cCap = 4096;           // hits of s2c's LDS link table (8 B eac
 #ifdef GMAPDP_OI_TIMING
 __device__ unsigned long long g_s2_marks[2][16];
 __device__ unsigned int g_s2_wave[3][16384];  // per s2b wave: sweep duration (wall-clock ticks), positions, hits
+// s2_one's parts, summed over the waves (wall-clock ticks): adjacent hit, prefetch, fast window, multi
+// windows, the entry-by-entry tail, and their call counts
+__device__ unsigned long long g_s2_sub[2][8];
+#define S2_SUB_DECL() unsigned long long _sub_t0 = 0
+#define S2_SUB_T0() (_sub_t0 = wall_clock64())
+#define S2_SUB(k) (W.sub[k] += wall_clock64() - _sub_t0, W.subn[k]++)
 #define S2_MARK(k)                                                  \
   do {                                                              \
     if (threadIdx.x == 0) {                                         \
@@ -70,6 +78,9 @@ __device__ unsigned int g_s2_wave[3][16384];  // per s2b wave: sweep duration (w
 #define S2_COUNT(k, v) \
   do {                 \
   } while (0)
+#define S2_SUB_DECL() (void)0
+#define S2_SUB_T0() (void)0
+#define S2_SUB(k) (void)0
 #endif
 
 // result status
@@ -267,6 +278,7 @@ struct S2W {
 #ifdef GMAPDP_OI_TIMING
   unsigned long long n_cand = 0, n_fast = 0, n_slow = 0, n_multi = 0;  // candidates, fast/multi windows, slow evals
   unsigned long long n_runs = 0, n_runpos = 0, n_onepos = 0, n_multpos = 0;  // runs, their members, other positions
+  unsigned long long sub[8] = {}, subn[8] = {};  // s2_one's parts (registers; flushed once per wave)
 #define S2_TALLY(f, v) (W.f += (v))
 #else
 #define S2_TALLY(f, v) (void)0
@@ -791,7 +803,9 @@ __device__ __forceinline__ int s2_dloop_multi(S2W& W, const S2Pref& pf, int np, 
 __device__ __forceinline__ S2Best s2_one(S2W& W, int q, uint32_t position, int np, const S2E& last) {
   S2Best b = {kS2K, (int)position, -1, -1, 0, 0};
   int nlookback = kS2Nsufflookback, lookback = kS2Sufflookback;
+  S2_SUB_DECL();
   if (np > 0) {
+    S2_SUB_T0();
     int k = last.n > 0 ? 0 : -1;
     S2HV u;
     if (s2_adj(W, last, k, q - last.q, position, u)) {
@@ -804,18 +818,25 @@ __device__ __forceinline__ S2Best s2_one(S2W& W, int q, uint32_t position, int n
       nlookback = 1;
       lookback = kS2Sufflookback / 2;
     }
+    S2_SUB(0);
   }
   s2_uniform(b);
   bool donep = false;
   int last_tr = -1;
   if (np > 0 && b.consec < kS2EnoughConsec) {
+    S2_SUB_T0();
     S2Pref pf;
     pf.load(W, np);
     // the entry that ends the walk (donep): the first beyond nlookback more than lookback + 8 back
     const uint64_t dm = ballot(W.lane < np && W.lane > nlookback && (q - pf.q) - kS2K > lookback);
     const int kmax = dm ? __ffsll((long long)dm) - 1 : (np <= 64 ? np - 1 : 64);
     int fdummy = 0, lt = -1, from = 0;
-    int st = s2_dloop_fast(W, pf, np, kmax, q, position, b, W.splicingp != 0, false, fdummy, lt);
+    S2_SUB(1);
+    int st;
+    S2_SUB_T0();
+    st = s2_dloop_fast(W, pf, np, kmax, q, position, b, W.splicingp != 0, false, fdummy, lt);
+    S2_SUB(2);
+    S2_SUB_T0();
     if (st == 2) from = 64;
     if (!st && kmax >= 64) {  // the walk goes past the window (donep decides there): one group at most
       st = s2_dloop_multi(W, pf, np, kmax, q, position, b, W.splicingp != 0, false, fdummy, lt);
@@ -830,6 +851,8 @@ __device__ __forceinline__ S2Best s2_one(S2W& W, int q, uint32_t position, int n
         pg.load(W, np, from);
       }
     }
+    S2_SUB(3);
+    S2_SUB_T0();
     if (st == 1) np = 0;  // done
     if (st != 1) last_tr = lt;
     S2EntryCache ec;
@@ -839,6 +862,7 @@ __device__ __forceinline__ S2Best s2_one(S2W& W, int q, uint32_t position, int n
       int qd;
       (void)s2_entry_eval(W, pf, ec, np, kk, 0, q, position, last_tr, b, W.splicingp != 0, &qd);
     }
+    S2_SUB(4);
   }
   s2_uniform(b);
   if (b.pp < 0) {  // localp
@@ -1478,6 +1502,10 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
     atomicAdd(&g_s2_marks[1][9], W.n_runpos);
     atomicAdd(&g_s2_marks[1][10], W.n_onepos);
     atomicAdd(&g_s2_marks[1][11], W.n_multpos);
+    for (int k = 0; k < 8; k++) {
+      atomicAdd(&g_s2_sub[0][k], W.sub[k]);
+      atomicAdd(&g_s2_sub[1][k], W.subn[k]);
+    }
   }
 #endif
 }
@@ -2069,8 +2097,8 @@ struct S2WalkOut {
 // position q - k with map - k (a binary search in that position's hits, which ascend), and the guesses
 // hold while each one is its predecessor's link (fpos, fhit); the walk goes on from the last holding
 // node's real link.  Same nodes, order and outputs as s2_walk.
-__device__ S2WalkOut s2_walk_diag(const S2Hit* hits, const uint32_t* maps, const int* off, int gi, int lane, int* pq,
-                                  int* ph) {
+__device__ S2WalkOut s2_walk_diag(const S2Hit* hits, const uint32_t* maps, const int* scs, const int* off, int gi,
+                                  int lane, int* pq, int* ph) {
   S2WalkOut o = {0, -1, -1};
   while (gi >= 0 && hits[gi].consec < kS2MinTerminal) {  // prune the 3' end
     const int fq = hits[gi].fpos;
@@ -2097,6 +2125,9 @@ __device__ S2WalkOut s2_walk_diag(const S2Hit* hits, const uint32_t* maps, const
     int pred = -1;
     uint32_t mx = 0x80000000u;
     int qx = 0;
+    // a guess the sweep never scored (score 0) is on no path, and its record was never written: it fails
+    // (a path node's link always points at a scored hit, so such a guess could not hold anyway)
+    if (idx >= 0 && lane > 0 && scs[idx] <= 0) idx = -1;
     if (idx >= 0) {
       const S2Hit& x = hits[idx];
       pred = x.fpos >= 0 ? off[x.fpos] + x.fhit : -1;
@@ -2345,7 +2376,7 @@ __global__ __launch_bounds__(64) void s2c_kernel(
     int n = 0, top = -1, bottom = -1;
     if (lds_walk || nq <= 65536) {
       const S2WalkOut o = lds_walk ? s2_walk_wave(llq, lmap, cell, lane, single ? pathq : nullptr, pathh)
-                                   : s2_walk_diag(hits, maps, off, cell, lane, single ? pathq : nullptr, pathh);
+                                   : s2_walk_diag(hits, maps, scs, off, cell, lane, single ? pathq : nullptr, pathh);
       n = o.n;
       top = o.top;
       bottom = o.bottom;
@@ -2427,7 +2458,7 @@ __global__ __launch_bounds__(64) void s2c_kernel(
     const int n = x.n;
     if (!single && (lds_walk || nq <= 65536)) {  // entries, 3' end first
       if (lds_walk) (void)s2_walk_wave(llq, lmap, x.cell, lane, pathq, pathh);
-      else (void)s2_walk_diag(hits, maps, off, x.cell, lane, pathq, pathh);
+      else (void)s2_walk_diag(hits, maps, scs, off, x.cell, lane, pathq, pathh);
     } else if (lane == 0 && !single) {
       int e = 0;
       {
@@ -2555,6 +2586,11 @@ __global__ __launch_bounds__(64) void s2c_kernel(
 }
 
 #ifdef GMAPDP_OI_TIMING
+extern "C" int gmapdp_debug_s2_sub(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_s2_sub), sizeof(g_s2_sub)) != hipSuccess) return 1;
+  static const unsigned long long zero[2][8] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_s2_sub), zero, sizeof(zero)) != hipSuccess;
+}
 extern "C" int gmapdp_debug_s2_waves(unsigned int* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_s2_wave), sizeof(g_s2_wave)) != hipSuccess;
 }
@@ -2588,8 +2624,18 @@ hipError_t launch_s2c(int nproblems, hipStream_t stream, const DevStage2Problem*
     if (e == hipSuccess)
       e = hipLaunchKernel(reinterpret_cast<void*>(&s2a_kernel), dim3(nproblems), dim3(64), args, 0, stream);
   }
-  if (e == hipSuccess && (phases & 2))
-    e = hipLaunchKernel(reinterpret_cast<void*>(&s2b_kernel), dim3(nproblems), dim3(64), args, 0, stream);
+  if (e == hipSuccess && (phases & 2)) {
+    // GMAPDP_S2B_LDS (experiments): extra LDS per sweep wave, to cap its waves per CU
+    static const size_t xlds = [] {
+      const char* v = std::getenv("GMAPDP_S2B_LDS");
+      return v ? (size_t)std::strtoull(v, nullptr, 10) : (size_t)0;
+    }();
+    if (xlds > 64 * 1024)
+      e = hipFuncSetAttribute(reinterpret_cast<void*>(&s2b_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)xlds);
+    if (e == hipSuccess)
+      e = hipLaunchKernel(reinterpret_cast<void*>(&s2b_kernel), dim3(nproblems), dim3(64), args, xlds, stream);
+  }
   if (e == hipSuccess && (phases & 4)) {  // the heavy calls (first in the order) without LDS, then the rest
     e = hipLaunchKernel(reinterpret_cast<void*>(&s2c_kernel<false>), dim3(nproblems), dim3(64), args, 0, stream);
     if (e == hipSuccess)

@@ -59,6 +59,7 @@ def main_s2(reads=10000):
     lib = gmapdp.load_library(os.path.join(ROOT, "gmap-2024_amd", "lib", "libgmapdp_oitiming.so"))
     lib.gmapdp_debug_s2_marks.argtypes = [C.c_void_p]
     lib.gmapdp_debug_s2_waves.argtypes = [C.c_void_p]
+    lib.gmapdp_debug_s2_sub.argtypes = [C.c_void_p]
     layout = W.Layout(W.CHR22)
     genome = W.make_genome(layout, seed=22)
     eng = gmapdp.Engine(0)
@@ -70,10 +71,13 @@ def main_s2(reads=10000):
     probs, qb, qub = eng.build_stage2_batch(calls)
     eng.stage2_batch_raw(probs, qb, qub)
     marks = np.zeros(32, dtype=np.uint64)
+    sub = np.zeros(16, dtype=np.uint64)
     lib.gmapdp_debug_s2_marks(marks.ctypes.data)
+    lib.gmapdp_debug_s2_sub(sub.ctypes.data)
     res, _, _ = eng.stage2_batch_raw(probs, qb, qub)
     torch.cuda.synchronize()
     lib.gmapdp_debug_s2_marks(marks.ctypes.data)
+    lib.gmapdp_debug_s2_sub(sub.ctypes.data)
     t, c = marks[:16].astype(np.float64), marks[16:]
     dur = [float(t[k + 1] - t[k]) for k in range(7)]
     tot = sum(dur)
@@ -103,7 +107,13 @@ def main_s2(reads=10000):
              "slowest": [[float(us[i]), int(npq[i]), int(nh[i])] for i in np.argsort(-us)[:8]]}
     print(json.dumps({"waves": [int(x) for x in c[:8]], "phases": {n: round(d / tot, 4) for n, d in zip(S2_PHASES, dur)},
                       "mean_wave_us": tot / 1e2 / max(int(c[0]), 1), "status": np.bincount(res["status"] + 3).tolist(),
-                      "counts": cnt, "s2c_per_wave": s2c, "s2b_sweep_per_wave": sweep}))
+                      "counts": cnt, "s2c_per_wave": s2c, "s2b_sweep_per_wave": sweep,
+                      "s2_one_parts_us_per_wave": {n: round(float(sub[i]) / 1e2 / max(int(c[0]), 1), 1)
+                                                   for i, n in enumerate(("adjacent", "prefetch", "fast_window",
+                                                                          "multi_windows", "entry_tail"))},
+                      "s2_one_parts_calls_per_wave": {n: round(float(sub[8 + i]) / max(int(c[0]), 1), 1)
+                                                      for i, n in enumerate(("adjacent", "prefetch", "fast_window",
+                                                                             "multi_windows", "entry_tail"))}}))
     eng.close()
 
 
@@ -122,11 +132,14 @@ def main():
     eng.set_genome(genome.tobytes())
     sh = W.CDNA2K
     op, oq = W.make_stage2(genome, layout, n, np.random.default_rng(3000), pad=sh.pad, extra=sh.stage2 - 1.0)
-    qb = oq.tobytes()
-    res = eng.oligo_mappings_batch_raw(op, qb)
+    # the seeding as Stage2_compute runs it (the host-array seeding API keeps its table below 2^31 entries)
+    calls = [dict(quc=oq[int(p["qoff"]):int(p["qoff"]) + int(p["querylength"])].tobytes(),
+                  **{k: int(p[k]) for k in ("chrstart", "chrend", "chroffset", "chrhigh", "plusp")}) for p in op]
+    probs, qb, qub = eng.build_stage2_batch(calls)
+    res = eng.stage2_batch_raw(probs, qb, qub)
     marks = np.zeros(32, dtype=np.uint64)
     lib.gmapdp_debug_oi_marks(marks.ctypes.data)  # clear (includes the first run's warm-up)
-    res = eng.oligo_mappings_batch_raw(op, qb)
+    res = eng.stage2_batch_raw(probs, qb, qub)
     torch.cuda.synchronize()
     lib.gmapdp_debug_oi_marks(marks.ctypes.data)
     t, c = marks[:16].astype(np.float64), marks[16:]
