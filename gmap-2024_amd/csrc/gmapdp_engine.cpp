@@ -83,7 +83,10 @@ size_t scratch_bytes_oi(int querylength, uint32_t genomiclength);
 size_t scratch_bytes_oi_fallback(int querylength, uint32_t genomiclength);
 size_t scratch_bytes_s2c(int querylength, int totalpositions, int ndiagonals);
 // the chaining kernels' counters (paths, pairs, ...) followed by their launch order (one int per call)
-inline size_t s2_counters_bytes(int n) { return 4 * sizeof(unsigned long long) + sizeof(int) * (size_t)(n > 0 ? n : 1); }
+// (then, per launch position, s2a's sweep-work estimate that re-orders the sweep)
+inline size_t s2_counters_bytes(int n) {
+  return 4 * sizeof(unsigned long long) + 2 * sizeof(int) * (size_t)(n > 0 ? n : 1);
+}
 hipError_t launch_s2c(int nproblems, hipStream_t stream, const DevStage2Problem* probs, const uint32_t* blocks,
                       uint64_t nwords, const char* qseq, const char* quc, const gmapdp_oligo_result* ores,
                       const int32_t* npos, const int32_t* map, const uint32_t* table, const int32_t* diags,

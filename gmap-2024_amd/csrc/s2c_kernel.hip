@@ -53,7 +53,7 @@ constexpr int kS2cCap = 4096;           // hits of s2c's LDS link table (8 B eac
 // Phase timing (tools/oi_timing.py s2; the GMAPDP_OI_TIMING variant of the library only)
 #ifdef GMAPDP_OI_TIMING
 __device__ unsigned long long g_s2_marks[2][16];
-__device__ unsigned int g_s2_wave[3][16384];  // per s2b wave: sweep duration (wall-clock ticks), positions, hits
+__device__ unsigned int g_s2_wave[3][16384];  // per call (< 16384): sweep duration (wall-clock ticks), positions, hits
 // s2_one's parts, summed over the waves (wall-clock ticks): adjacent hit, prefetch, fast window, multi
 // windows, the entry-by-entry tail, and their call counts
 __device__ unsigned long long g_s2_sub[2][8];
@@ -1562,9 +1562,13 @@ __device__ __forceinline__ int s2_problem(const unsigned long long* counters) {
 }
 
 constexpr int kS2OrderThreads = 512, kS2OrderPer = 16;  // a tile of 8192 calls: keys held in registers
+// keys NULL: by seeding hits (before s2a); else by s2a's sweep-work estimate per launch position (before
+// the sweep: the hits inside the active ranges, which a spurious far diagonal can multiply several-fold
+// at the same hit count), 64 buckets per doubling.
 __global__ __launch_bounds__(kS2OrderThreads) void s2_order_kernel(const DevStage2Problem* __restrict__ probs, int n,
                                                                    const gmapdp_oligo_result* __restrict__ ores,
-                                                                   unsigned long long* __restrict__ counters) {
+                                                                   unsigned long long* __restrict__ counters,
+                                                                   const int* __restrict__ work) {
   __shared__ int hist[1024];
   __shared__ int wsum[16];
   int* order = reinterpret_cast<int*>(counters + 4);
@@ -1582,8 +1586,14 @@ __global__ __launch_bounds__(kS2OrderThreads) void s2_order_kernel(const DevStag
     }
 #pragma unroll
     for (int j = 0; j < kS2OrderPer; j++) {
-      const int T = idx[j] >= 0 ? ores[idx[j]].totalpositions : 0;
-      key[j] = idx[j] >= 0 ? 1023 - min(max(T, 0) >> 2, 1023) : -1;
+      if (work) {
+        const int i = base + j * kS2OrderThreads + t;
+        const int K = i < n ? max(work[i], 0) : 0;
+        key[j] = idx[j] >= 0 ? 1023 - min((int)(64.0f * __log2f((float)K + 1.0f)), 1023) : -1;
+      } else {
+        const int T = idx[j] >= 0 ? ores[idx[j]].totalpositions : 0;
+        key[j] = idx[j] >= 0 ? 1023 - min(max(T, 0) >> 2, 1023) : -1;
+      }
     }
   };
   for (int base = 0; base < n; base += kTile) {
@@ -1623,7 +1633,11 @@ __global__ __launch_bounds__(64) void s2a_kernel(
     unsigned long long path_cap, gmapdp_path_pair* __restrict__ pairs_out, unsigned long long pair_cap) {
   __shared__ int sh[8];
   const int lane = threadIdx.x;
-  const DevStage2Problem P = probs[s2_problem(counters)];
+  const int pos = s2_problem(counters);
+  const DevStage2Problem P = probs[pos];
+  // the sweep-work estimate of this launch position (s2_order_kernel re-orders the sweep by it)
+  int* work = reinterpret_cast<int*>(counters + 4) + gridDim.x;
+  if (lane == 0) work[pos] = 0;
   const int ql = P.querylength, nq = ql - kS2K + 1;
   const gmapdp_oligo_result O = ores[P.index];
   const int T = O.totalpositions, nd = O.ndiagonals;
@@ -1990,6 +2004,17 @@ __global__ __launch_bounds__(64) void s2a_kernel(
     return;
   }
   wave_sync();
+  // the sweep's work: a position's lookbacks grow with its hits inside [minactive, maxactive] (each one
+  // beyond the first a full lookback); a diagonal far from the others widens those ranges over the gap
+  {
+    int wk = 0;
+    for (int q = qstart + lane; q <= qend; q += 64) {
+      const int d = higha[q] - lowa[q];
+      wk += d > 0 ? 1 + 4 * (d - 1) : 0;
+    }
+    wk = wave_sum_i(wk);
+    if (lane == 0) work[pos] = wk;
+  }
 
   if (lane == 0) results[P.index] = R;  // status 2 with the query bounds: the sweep and the paths follow
 }
@@ -2067,10 +2092,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GMAPDP_S2B_W
   }
   wave_sync();
 #ifdef GMAPDP_OI_TIMING
-  if (lane == 0 && blockIdx.x < 16384) {
-    g_s2_wave[0][blockIdx.x] = (unsigned int)(wall_clock64() - tw0);
-    g_s2_wave[1][blockIdx.x] = (unsigned int)(qend - qstart + 1);
-    g_s2_wave[2][blockIdx.x] = (unsigned int)T;
+  if (lane == 0 && P.index < 16384) {  // by call
+    g_s2_wave[0][P.index] = (unsigned int)(wall_clock64() - tw0);
+    g_s2_wave[1][P.index] = (unsigned int)(qend - qstart + 1);
+    g_s2_wave[2][P.index] = (unsigned int)T;
   }
 #endif
 
@@ -2615,14 +2640,21 @@ hipError_t launch_s2c(int nproblems, hipStream_t stream, const DevStage2Problem*
                   (void*)&npos, (void*)&map, (void*)&table, (void*)&diags, (void*)&scratch, (void*)&counters,
                   (void*)&scratch_cap, (void*)&results, (void*)&paths, (void*)&path_cap, (void*)&pairs,
                   (void*)&pair_cap};
-  void* oargs[] = {(void*)&probs, (void*)&nproblems, (void*)&ores, (void*)&counters};
   // phases (bits): 1 the order + s2a, 2 s2b, 4 s2c; one phase alone re-runs it over the previous run's
   // scratch (the bench's per-kernel timing)
   hipError_t e = hipSuccess;
   if (phases & 1) {
-    e = hipLaunchKernel(reinterpret_cast<void*>(&s2_order_kernel), dim3(1), dim3(kS2OrderThreads), oargs, 0, stream);
+    const int* nowork = nullptr;
+    void* oargs0[] = {(void*)&probs, (void*)&nproblems, (void*)&ores, (void*)&counters, (void*)&nowork};
+    e = hipLaunchKernel(reinterpret_cast<void*>(&s2_order_kernel), dim3(1), dim3(kS2OrderThreads), oargs0, 0, stream);
     if (e == hipSuccess)
       e = hipLaunchKernel(reinterpret_cast<void*>(&s2a_kernel), dim3(nproblems), dim3(64), args, 0, stream);
+    // the sweep (and s2c) heaviest first by s2a's work estimate
+    const int* work = reinterpret_cast<const int*>(counters + 4) + nproblems;
+    void* oargs1[] = {(void*)&probs, (void*)&nproblems, (void*)&ores, (void*)&counters, (void*)&work};
+    if (e == hipSuccess)
+      e = hipLaunchKernel(reinterpret_cast<void*>(&s2_order_kernel), dim3(1), dim3(kS2OrderThreads), oargs1, 0,
+                          stream);
   }
   if (e == hipSuccess && (phases & 2)) {
     // GMAPDP_S2B_LDS (experiments): extra LDS per sweep wave, to cap its waves per CU
