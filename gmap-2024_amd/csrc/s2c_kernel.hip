@@ -671,8 +671,8 @@ __device__ __forceinline__ int s2_dloop_multi(S2W& W, const S2Pref& pf, int np, 
   const int lane = W.lane;
   const int f0 = use_f ? f : 0;
   const bool inw0 = lane <= kend && base + lane < np && f0 != -1;
+  // entries whose hits left the LDS ring (many active hits per entry) are gathered from global memory
   const bool inring = pf.n <= kS2Ring && pf.start >= W.pushed - kS2Ring;
-  if (ballot(inw0 && pf.n > 0 && !inring)) return 0;
   const int c0 = (inw0 && pf.n > 0) ? max(pf.n - f0, 0) : 0;
   const int incl0 = wave_incl_sum(c0, lane);
   // the group: the leading entries whose hits fit in the wave
@@ -702,10 +702,11 @@ __device__ __forceinline__ int s2_dloop_multi(S2W& W, const S2Pref& pf, int np, 
   const int e = __shfl(hd, sl, 64) - 1;
   const int ee = e < 0 ? 0 : e;
   const int eq = __shfl(pf.q, ee, 64), est = __shfl(pf.start, ee, 64), ef = __shfl(f0, ee, 64),
-            ec = __shfl(c, ee, 64);
+            ec = __shfl(c, ee, 64), eoff = __shfl(pf.off, ee, 64), ering = __shfl((int)inring, ee, 64);
   const int k = ef + (lane - sl);
   S2HV v = {};
-  if (act) {
+  if (ballot(act && !ering)) wave_sync();  // this wave's earlier global writes are complete
+  if (act && ering) {
     const int r = (est + k) & (kS2Ring - 1);
     v.map = s2_ring.map[r];
     v.score = s2_ring.score[r];
@@ -713,6 +714,8 @@ __device__ __forceinline__ int s2_dloop_multi(S2W& W, const S2Pref& pf, int np, 
     v.tracei = s2_ring.tracei[r];
     v.root = s2_ring.root[r];
     v.hit = s2_ring.hit[r];
+  } else if (act) {
+    v = s2_load_global(W.hits, W.maps, W.alist, eoff, k);
   }
   const int eend = sl + ec;  // one past the entry's last lane
   const int a = __shfl(v.tracei, sl, 64);
@@ -788,13 +791,12 @@ __device__ __forceinline__ int s2_dloop_multi(S2W& W, const S2Pref& pf, int np, 
     if (inw && lane <= stop_e) f = (c > 0 && g < excl + c) ? f0 + (g - excl) : -1;
   }
   if (S) return 1;
+  lt = last_tr;  // (also at the window's end: a caller whose window stops short of the walk's goes on)
   if (gend <= kend) {  // the hits of the later entries did not fit this group
-    lt = last_tr;
     *next = base + gend;
     return 2;
   }
   if (kmax - base < 64) return 1;
-  lt = last_tr;
   if (next) *next = base + 64;
   return 2;
 }
@@ -838,17 +840,21 @@ __device__ __forceinline__ S2Best s2_one(S2W& W, int q, uint32_t position, int n
     S2_SUB(2);
     S2_SUB_T0();
     if (st == 2) from = 64;
-    if (!st && kmax >= 64) {  // the walk goes past the window (donep decides there): one group at most
-      st = s2_dloop_multi(W, pf, np, kmax, q, position, b, W.splicingp != 0, false, fdummy, lt);
-      if (st == 2) from = 64;
-    } else if (!st) {  // entries with several hits: groups of entries whose hits fit the wave
+    if (!st) {  // entries with several hits: groups of entries whose hits fit the wave
+      // (when the walk goes past the window, donep decides beyond it: the groups stop at entry 63 and a
+      // window walked to its end without a stop goes on from entry 64)
+      const int kg = kmax >= 64 ? 63 : kmax;
       S2Pref pg = pf;  // (a value, not a reference chosen at run time: that kept both windows in scratch)
       for (;;) {
         int nb = from;
-        st = s2_dloop_multi(W, pg, np, kmax, q, position, b, W.splicingp != 0, false, fdummy, lt, from, &nb);
+        st = s2_dloop_multi(W, pg, np, kg, q, position, b, W.splicingp != 0, false, fdummy, lt, from, &nb);
         if (st != 2) break;
         from = nb;
         pg.load(W, np, from);
+      }
+      if (st == 1 && kmax >= 64 && b.consec < kS2EnoughConsec) {  // (a stop leaves consec >= ENOUGH)
+        st = 2;
+        from = 64;
       }
     }
     S2_SUB(3);
@@ -1178,6 +1184,8 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
     } else if (high - low > 1 && high - low <= 64) {
       // several hits (<= 64): lane i holds hit low + i and its link
       const int nh = high - low;
+      S2_SUB_DECL();
+      S2_SUB_T0();
       const uint32_t cm = lane < nh ? W.maps[qoff + low + lane] : 0u;
       S2Best mb = {0, 0, -1, -1, 0, 0};
       if (np == 0) {
@@ -1252,6 +1260,7 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
         }
         const uint64_t a_mask = ballot(a_found);
         adjf = last.n > 0 ? 0 : -1;
+        S2_SUB(6);
         for (int i = 0; i < nh; i++) {
           const uint32_t position = (uint32_t)__builtin_amdgcn_readlane((int)cm, i);
           S2Best b;
@@ -1273,6 +1282,7 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
           }
           s2_uniform(b);
           int st = 0, lt = -1, from = 0;
+          S2_SUB_T0();
           if (overall < kS2GreedyConsec) {
             const int kmax = min(min(maxseen, nfr - 1), np - 1);
             const int kend = min(kmax, 63);
@@ -1300,6 +1310,8 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
             }
             if (st == 2) st = 1;  // every entry up to kmax walked
           }
+          S2_SUB(7);
+          S2_SUB_T0();
           if (overall < kS2GreedyConsec && st != 1) {
             int last_tr = lt;
             for (int kk = from; kk < np && b.consec < kS2EnoughConsec && kk <= maxseen && kk < nfr;
@@ -1313,6 +1325,7 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
               }
             }
           }
+          S2_SUB(5);
           s2_uniform(b);
           if (b.pp < 0) {
             b.tracei = ++W.tracectr;
@@ -1382,7 +1395,10 @@ __device__ __forceinline__ void s2_sweep(S2W& W, const int32_t* npq, int nq, con
     } else {
       int best_score = 0, best_hit = -1, best_fhit = 0, best_consec = 0;
       if (high - low > 1) {
+        S2_SUB_DECL();
+        S2_SUB_T0();
         s2_mult(W, q, qoff, low, high, np, last);
+        S2_SUB(5);
         int bs = 0, bh = -1;
         for (int c0 = low; c0 < high; c0 += 64) {
           const int i = c0 + lane;
@@ -2023,6 +2039,10 @@ __global__ __launch_bounds__(64) void s2a_kernel(
 #ifndef GMAPDP_S2B_WPE
 #define GMAPDP_S2B_WPE 4  // waves per SIMD the sweep's registers are budgeted for (variants: make variant DEFS=...)
 #endif
+// the sweeps launched first (the heaviest, by s2a's work estimate) issue ahead of the light waves that share
+// their SIMD: a heavy call's single-wave latency, not the grid's throughput, ends the launch
+__device__ int g_s2b_prio_n = 256;
+
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GMAPDP_S2B_WPE))) void s2b_kernel(
     const DevStage2Problem* __restrict__ probs, const uint32_t* __restrict__ blocks, uint64_t nwords,
     const char* __restrict__ qseq, const char* __restrict__ quc, const gmapdp_oligo_result* __restrict__ ores,
@@ -2063,6 +2083,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GMAPDP_S2B_W
   (void)diag_all; (void)counters; (void)scratch_cap; (void)paths_out; (void)path_cap; (void)pairs_out; (void)pair_cap;
   const gmapdp_stage2_result R0 = results[P.index];
   if (R0.status != kS2Chained) return;
+  if ((int)blockIdx.x < g_s2b_prio_n) __builtin_amdgcn_s_setprio(2);
   const int qstart = R0.diag_querystart, qend = R0.diag_queryend;
   S2_MARK(3);
 #ifdef GMAPDP_OI_TIMING
@@ -2662,7 +2683,17 @@ hipError_t launch_s2c(int nproblems, hipStream_t stream, const DevStage2Problem*
       const char* v = std::getenv("GMAPDP_S2B_LDS");
       return v ? (size_t)std::strtoull(v, nullptr, 10) : (size_t)0;
     }();
-    if (xlds > 64 * 1024)
+    // GMAPDP_S2B_PRIO (experiments): how many of the first sweeps run at raised priority
+    static const int prio_n = [] {
+      const char* v = std::getenv("GMAPDP_S2B_PRIO");
+      return v ? std::atoi(v) : -1;
+    }();
+    static bool prio_set = false;
+    if (prio_n >= 0 && !prio_set) {
+      e = hipMemcpyToSymbol(HIP_SYMBOL(g_s2b_prio_n), &prio_n, sizeof(int));
+      prio_set = true;
+    }
+    if (e == hipSuccess && xlds > 64 * 1024)
       e = hipFuncSetAttribute(reinterpret_cast<void*>(&s2b_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)xlds);
     if (e == hipSuccess)
