@@ -548,7 +548,8 @@ def main():
     # side list joins its second (the two lightest), where the microexon plan runs too.  Real
     # (non-null) streams, so per-launch events time exactly the launches on their stream.
     stream = torch.cuda.Stream(dev)
-    sides = [torch.cuda.Stream(dev) for _ in range(2)]
+    # GMAPDP_BENCH_SIDES=3 (with GPU_MAX_HW_QUEUES >= 5): each of the plan's side lists on its own stream
+    sides = [torch.cuda.Stream(dev) for _ in range(int(os.environ.get("GMAPDP_BENCH_SIDES", "2")))]
     # stage 2 (the step's longest chain) may take the high-priority queue: GMAPDP_BENCH_S2_PRIORITY=1
     s2prio = int(os.environ.get("GMAPDP_BENCH_S2_PRIORITY", "0"))
     ostream = torch.cuda.Stream(dev, priority=-1) if s2prio else torch.cuda.Stream(dev)

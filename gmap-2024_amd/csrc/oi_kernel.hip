@@ -37,6 +37,8 @@ constexpr int kOiK = 8;
 // is the time spent in phase k.
 #ifdef GMAPDP_OI_TIMING
 __device__ unsigned long long g_oi_marks[2][16];
+// per call (index < 16384): oi_kernel wave 0's and oi_map_kernel's durations (ticks), the events E
+__device__ unsigned int g_oi_wave[3][16384];
 #define OI_MARK(k)                                                 \
   do {                                                             \
     if (threadIdx.x == 0) {                                        \
@@ -135,11 +137,37 @@ __device__ __forceinline__ int seg_scan_min(int lane, int x, int e, int segstart
 
 constexpr int kOiHist = 4 * 256;  // = 2 x 512
 
+// Event keys, ordered by diagi (the sort's digits) then by generation order (query order).  The run test
+// of the reference, q - q_prev >= diag_lookback + cum[q] - cum[q_prev], is (q - cum[q]) - (q_prev -
+// cum[q_prev]) >= diag_lookback: with t = q - cum_nohits[q] carried in the key (querypos < 2^16), the
+// sweep compares two keys and reads no cum_nohits at all (two scattered loads per event otherwise, the
+// L2 request rate being what bounds this kernel).  Past 2^16 query positions the key holds q only and
+// the sweep looks t up.
+struct OiKeyQT {  // diagi << 32 | q << 16 | t
+  __device__ static uint64_t make(uint32_t di, uint32_t q, uint32_t t) {
+    return ((uint64_t)di << 32) | (q << 16) | t;
+  }
+  __device__ static uint32_t di(uint64_t k) { return (uint32_t)(k >> 32); }
+  __device__ static uint32_t q(uint64_t k) { return ((uint32_t)k >> 16); }
+  __device__ static int t(uint64_t k, const int* __restrict__) { return (int)((uint32_t)k & 0xFFFFu); }
+};
+struct OiKeyQ {  // diagi << 32 | q
+  __device__ static uint64_t make(uint32_t di, uint32_t q, uint32_t) { return ((uint64_t)di << 32) | q; }
+  __device__ static uint32_t di(uint64_t k) { return (uint32_t)(k >> 32); }
+  __device__ static uint32_t q(uint64_t k) { return (uint32_t)k; }
+  __device__ static int t(uint64_t k, const int* __restrict__ cum) { return (int)(uint32_t)k - cum[(uint32_t)k]; }
+};
+__device__ __forceinline__ uint64_t readlane64(uint64_t k, int l) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(k >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k, l);
+}
+
 // Returns false (nothing written) when the shared event pool could not hold this problem's 3 E slots
 // (oi_kernel took them, `base`, with one atomic as it finished).
 // maxdiag bounds every diagi (querylength + genomiclength); hist holds kOiHist LDS counters: the digits
 // are 9 bits wide when maxdiag < 2^18 (2 passes of 512 buckets: a 214-kb window), else 8 bits (at most 4
 // passes of 256).  (More LDS would cost oi_map_kernel a wave per SIMD.)
+template <typename KT>
 __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t maxdiag, uint32_t chrinit,
                                    int lookback, int suffn, const int32_t* __restrict__ npq,
                                    const int32_t* __restrict__ mpq, const int* __restrict__ cum,
@@ -148,9 +176,11 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
                                    int* evq, int32_t* __restrict__ good, int gcap, int& ngood_out, int& maxn_out) {
   OI_MARK(9);
   if (base == ~0ull) return false;
-  uint64_t* evA = pool + base;                      // events (diagi << 32 | q)
-  uint64_t* evB = evA + E;                          // radix-sort ping-pong
-  int4* grec = reinterpret_cast<int4*>(evB + E);    // good records (at most E / 2)
+  using K = uint64_t;
+  constexpr K kMax = ~0ull;
+  K* evA = pool + base;                             // events (OiKeyQT / OiKeyQ)
+  K* evB = evA + E;                                 // radix-sort ping-pong
+  int4* grec = reinterpret_cast<int4*>(pool + base + 2 * (size_t)E);  // good records (at most E / 2)
   const int db = maxdiag < (1u << 18) ? 9 : 8;       // digit bits
   const uint32_t dmask = (1u << db) - 1u;
   int npass = 0;                                    // digits of the largest possible diagi
@@ -165,23 +195,27 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
   // radix pass are counted here, so the sort never re-reads the keys to count them.
   int* exo = evq;          // [256] exclusive event offset of each query position of the step
   int* mos = evq + 256;    // [256] its table offset
+  int* cus = evq + 512;    // [256] its cum_nohits
   int eoff = 0;
-  int nh_n[4], mo_n[4];
+  int nh_n[4], mo_n[4], cu_n[4];
 #pragma unroll
   for (int r = 0; r < 4; r++) {
     const int q = 64 * r + lane;
     nh_n[r] = q < nq ? npq[q] : 0;
     mo_n[r] = q < nq ? mpq[q] : 0;
+    cu_n[r] = q < nq ? cum[q] : 0;
   }
   for (int sb = 0; sb < nq; sb += 4 * 64) {
-    int nh[4], mo[4];
+    int nh[4], mo[4], cu[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       nh[r] = max(nh_n[r], 0);
       mo[r] = mo_n[r];
+      cu[r] = cu_n[r];
       const int q = sb + 4 * 64 + 64 * r + lane;
       nh_n[r] = q < nq ? npq[q] : 0;
       mo_n[r] = q < nq ? mpq[q] : 0;
+      cu_n[r] = q < nq ? cum[q] : 0;
     }
     int run = 0;
 #pragma unroll
@@ -189,13 +223,14 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
       const int incl = wave_scan_add(lane, nh[r]);
       exo[64 * r + lane] = run + incl - nh[r];
       mos[64 * r + lane] = mo[r];
+      cus[64 * r + lane] = cu[r];
       run += __builtin_amdgcn_readlane(incl, 63);
     }
     const int T = run;
     __syncthreads();
     for (int g0 = 0; g0 < T; g0 += 4 * 64) {
       uint32_t tv[4];
-      int qv[4];
+      int qv[4], cv[4];
 #pragma unroll
       for (int gi = 0; gi < 4; gi++) {
         const int j = g0 + 64 * gi + lane;
@@ -204,6 +239,7 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
         for (int step = 128; step >= 1; step >>= 1)
           if (exo[l + step] <= j) l += step;
         qv[gi] = sb + l;
+        cv[gi] = cus[l];
         tv[gi] = j < T ? table_all[mos[l] + (j - exo[l])] : 0u;
       }
 #pragma unroll
@@ -211,7 +247,7 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
         const int j = g0 + 64 * gi + lane;
         const bool v = j < T;
         const uint32_t di = tv[gi] + (uint32_t)(qlen - qv[gi]) - chrinit;
-        if (v) evA[eoff + j] = ((uint64_t)di << 32) | (uint32_t)qv[gi];
+        if (v) evA[eoff + j] = KT::make(di, (uint32_t)qv[gi], (uint32_t)(qv[gi] - cv[gi]));
         // one LDS atomic per distinct digit: the hits of a group mostly share a few diagonals, and
         // same-address atomics serialise
         for (int p = 0; p < npass; p++) {
@@ -234,8 +270,8 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
   OI_MARK(5);
 
   // stable LSD radix sort on diagi
-  uint64_t* src = evA;
-  uint64_t* dst = evB;
+  K* src = evA;
+  K* dst = evB;
   for (int p = 0; p < npass; p++) {
     uint32_t* hp = hist + (dmask + 1) * p;
     const int shift = db * p;
@@ -256,7 +292,7 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
     // 256 keys per step: their 4 loads and 4 stores each go out together (one memory round trip per
     // step); the ranks are taken chunk by chunk in order, which keeps the sort stable
     for (int e0 = 0; e0 < E; e0 += 4 * 64) {
-      uint64_t key[4];
+      K key[4];
       uint32_t dpos[4];
 #pragma unroll
       for (int r = 0; r < 4; r++) {
@@ -266,7 +302,7 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const bool v = e0 + 64 * r + lane < E;
-        const uint32_t d = (uint32_t)(key[r] >> (32 + shift)) & dmask;
+        const uint32_t d = (KT::di(key[r]) >> shift) & dmask;
         uint64_t eq = ballot(v);
 #pragma unroll
         for (int b = 0; b < 9; b++) {
@@ -285,11 +321,11 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
         if (e0 + 64 * r + lane < E) dst[dpos[r]] = key[r];
     }
     __threadfence_block();
-    uint64_t* t = src;
+    K* t = src;
     src = dst;
     dst = t;
   }
-  const uint64_t* S = src;
+  const K* S = src;
   __threadfence_block();
   OI_MARK(6);
 
@@ -297,43 +333,41 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
   // diagonal's last event appends its record when it is good.  Per lane, the largest n seen and the
   // smallest (querypos, diagi) event carrying it (the fallback best).  Nothing is stored per event.
   int c_rs = -1, c_ds = -1, c_fs = 0x7fffffff, ngood = 0;
-  uint64_t c_mk = 0, c_key = 0;
+  uint64_t c_mk = 0;
+  K c_key = 0;
   int bm = -1, be = -1;
   uint64_t bkey = ~0ull;
   // 256 events per step: their key loads, then their cum_nohits loads, go out together (two memory
   // round trips per step); the 4 chunks are then scanned in order with the carries
   for (int s0 = 0; s0 < E; s0 += 4 * 64) {
-    uint64_t key[4];
+    K key[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int e = s0 + 64 * r + lane;
-      key[r] = e < E ? S[e] : ~0ull;
+      key[r] = e < E ? S[e] : kMax;
     }
-    const uint64_t after = s0 + 4 * 64 < E ? S[s0 + 4 * 64] : ~0ull;  // the event after this step
-    uint64_t pkey[4];
-    int cq[4], cpq[4];
+    const K after = s0 + 4 * 64 < E ? S[s0 + 4 * 64] : kMax;  // the event after this step
+    K pkey[4];
+    int tq[4], tpq[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-      uint64_t pk = __shfl_up(key[r], 1, 64);
-      if (lane == 0)
-        pk = r == 0 ? c_key
-                    : (((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(key[r - 1] >> 32), 63) << 32) |
-                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key[r - 1], 63));
+      K pk = __shfl_up(key[r], 1, 64);
+      if (lane == 0) pk = r == 0 ? c_key : readlane64(key[r - 1], 63);
       pkey[r] = pk;
       const bool v = s0 + 64 * r + lane < E;
-      cq[r] = v ? cum[(uint32_t)key[r]] : 0;
-      cpq[r] = v ? cum[(uint32_t)pk] : 0;
+      tq[r] = v ? KT::t(key[r], cum) : 0;
+      tpq[r] = v && s0 + 64 * r + lane > 0 ? KT::t(pk, cum) : 0;
     }
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int e0 = s0 + 64 * r;
       const int e = e0 + lane;
       const bool v = e < E;
-      const uint64_t key_r = key[r], pk = pkey[r];
-      const uint32_t d = (uint32_t)(key_r >> 32), q = (uint32_t)key_r;
-      const bool newdiag = v && (e == 0 || (uint32_t)(pk >> 32) != d);
+      const K key_r = key[r], pk = pkey[r];
+      const uint32_t d = KT::di(key_r), q = KT::q(key_r);
+      const bool newdiag = v && (e == 0 || KT::di(pk) != d);
       bool newrun = newdiag;
-      if (v && !newdiag) newrun = (int)(q - (uint32_t)pk) >= lookback + cq[r] - cpq[r];
+      if (v && !newdiag) newrun = tq[r] - tpq[r] >= lookback;
       const int rs = max(wave_scan_max(newrun ? e : -1), c_rs);
       const int ds = max(wave_scan_max(newdiag ? e : -1), c_ds);
       const int n = e - rs;
@@ -343,12 +377,9 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
       int fs = (v && n == suffn) ? e : 0x7fffffff;
       fs = seg_scan_min(lane, fs, e, ds);
       if (ds < e0) fs = min(fs, c_fs);
-      uint64_t nk = __shfl_down(key_r, 1, 64);
-      if (lane == 63)
-        nk = r < 3 ? (((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(key[r + 1] >> 32), 0) << 32) |
-                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key[r + 1], 0))
-                   : after;
-      const bool dend = v && (e + 1 == E || (uint32_t)(nk >> 32) != d);
+      K nk = __shfl_down(key_r, 1, 64);
+      if (lane == 63) nk = r < 3 ? readlane64(key[r + 1], 0) : after;
+      const bool dend = v && (e + 1 == E || KT::di(nk) != d);
       const bool isgood = dend && fs != 0x7fffffff;
       const uint64_t gm = ballot(isgood);
       if (isgood)  // {first event with n == suffn, first event with the maximum, the maximum, diagi}
@@ -367,8 +398,7 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
       c_fs = __builtin_amdgcn_readlane(fs, 63);
       c_mk = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(mk >> 32), 63) << 32) |
              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mk, 63);
-      c_key = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(key_r >> 32), 63) << 32) |
-              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key_r, 63);
+      c_key = readlane64(key_r, 63);
     }
   }
   // the global maximum and the first (querypos, diagi) event carrying it
@@ -391,15 +421,15 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
   }
   __threadfence_block();
   // records and their (querypos, diagi) keys; then the reference's order
-  uint64_t* gkey = (S == evA) ? evB : evA;  // the free sort buffer
+  uint64_t* gkey = (S == evA) ? evB : evA;  // the free sort buffer: the good diagonals' query-order keys
   for (int g = lane; g < ngood; g += 64) {
     const int4 r = grec[g];
     const uint32_t di = (uint32_t)r.w;
     const int eb = r.y, bn = r.z;
-    const uint32_t qreach = r.x >= 0 ? (uint32_t)S[r.x] : 0u;
+    const uint32_t qreach = r.x >= 0 ? KT::q(S[r.x]) : 0u;
     gkey[g] = ((uint64_t)qreach << 32) | di;
     grec[g] = make_int4(di >= (uint32_t)qlen ? (int)(di - (uint32_t)qlen) : (int)((uint32_t)qlen - di),
-                        (int)(uint32_t)S[eb - bn], (int)(uint32_t)S[eb], bn + 1);
+                        (int)KT::q(S[eb - bn]), (int)KT::q(S[eb]), bn + 1);
   }
   __threadfence_block();
   if (ngood > gcap) ngood = -1;  // more good diagonals than the layout gave the problem: overflow
@@ -451,6 +481,9 @@ __global__ __launch_bounds__(64 * kOiWaves) void oi_kernel(
   const char* quc = quc_all + P.qoff;
   const int qlen = P.querylength;
   OI_MARK(0);
+#ifdef GMAPDP_OI_TIMING
+  const unsigned long long oi_t0 = wall_clock64();
+#endif
   const int nq = qlen - kOiK + 1;  // query positions with a full 8-mer
 
   // ---- the query's 8-mers (Oligoindex_set_inquery) ----
@@ -739,6 +772,9 @@ __global__ __launch_bounds__(64 * kOiWaves) void oi_kernel(
     *reinterpret_cast<unsigned long long*>(base_s + so.poolbase) = b;
   }
   OI_MARK(4);
+#ifdef GMAPDP_OI_TIMING
+  if (lane == 0 && P.index < 16384) g_oi_wave[0][P.index] = (unsigned int)(wall_clock64() - oi_t0);
+#endif
 }
 
 // ---- Oligoindex_get_mappings' diagonal state machine, one wave per problem, after oi_kernel ----
@@ -750,12 +786,15 @@ __global__ __launch_bounds__(64) void oi_map_kernel(
     const int32_t* __restrict__ map_out, const uint32_t* __restrict__ table_all, int32_t* __restrict__ diag_all,
     uint64_t* __restrict__ pool) {
   __shared__ uint32_t hist[kOiHist];
-  __shared__ int evq[2 * 256];
+  __shared__ int evq[3 * 256];
   const int lane = threadIdx.x;
   const DevOligoProblem P = probs[blockIdx.x];
   if (P.chrend <= P.chrstart) return;  // oned_matrix_p stays 0 (oi_kernel wrote the record)
   if (results[P.index].oned_matrix_p < 0) return;  // oi_kernel reported overflow
   OI_MARK(8);
+#ifdef GMAPDP_OI_TIMING
+  const unsigned long long om_t0 = wall_clock64();
+#endif
   const uint32_t* table = table_all + P.table_offset;  // the mappings are relative to it
   const int qlen = P.querylength;
   const int nq = qlen - kOiK + 1;
@@ -771,9 +810,15 @@ __global__ __launch_bounds__(64) void oi_map_kernel(
     int32_t* good = diag_all + 4 * P.diag_offset;  // records {diag, best_start, best_end, best_n + 1}
     int ngood = 0, maxn = 0;
     const uint32_t maxdiag = (uint32_t)qlen + (P.chrend - P.chrstart);
-    if (!oi_mappings_sorted(lane, qlen, nq, totalpositions, maxdiag, chrinit, diag_lookback, suffn, npq, mpq, cum,
-                            table, pool, *reinterpret_cast<const unsigned long long*>(base_s + so.poolbase), hist,
-                            evq, good, (int)min(P.diag_cap, 0x7fffffffu), ngood, maxn)) {
+    const unsigned long long pbase = *reinterpret_cast<const unsigned long long*>(base_s + so.poolbase);
+    const int gcap = (int)min(P.diag_cap, 0x7fffffffu);
+    const bool sorted =
+        nq < 65536
+            ? oi_mappings_sorted<OiKeyQT>(lane, qlen, nq, totalpositions, maxdiag, chrinit, diag_lookback, suffn,
+                                           npq, mpq, cum, table, pool, pbase, hist, evq, good, gcap, ngood, maxn)
+            : oi_mappings_sorted<OiKeyQ>(lane, qlen, nq, totalpositions, maxdiag, chrinit, diag_lookback, suffn,
+                                           npq, mpq, cum, table, pool, pbase, hist, evq, good, gcap, ngood, maxn);
+    if (!sorted) {
       // the event pool is full: the sequential walk (per-diagonal states in the problem's fallback region;
       // a plan sized from a measured run has an exact pool and none: report the overflow instead)
       if (P.fallback_offset < 0) {
@@ -878,9 +923,18 @@ __global__ __launch_bounds__(64) void oi_map_kernel(
     }
   }
   OI_MARK(7);
+#ifdef GMAPDP_OI_TIMING
+  if (lane == 0 && P.index < 16384) {
+    g_oi_wave[1][P.index] = (unsigned int)(wall_clock64() - om_t0);
+    g_oi_wave[2][P.index] = (unsigned int)totalpositions;
+  }
+#endif
 }
 
 #ifdef GMAPDP_OI_TIMING
+extern "C" int gmapdp_debug_oi_waves(unsigned int* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_oi_wave), sizeof(g_oi_wave)) != hipSuccess;
+}
 // copies out and clears the marks: [0..15] timestamp sums (100 MHz), [16..31] wave counts
 extern "C" int gmapdp_debug_oi_marks(unsigned long long* out) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_oi_marks), sizeof(g_oi_marks)) != hipSuccess) return 1;

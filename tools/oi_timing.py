@@ -152,6 +152,19 @@ def main():
     out["phases"] = {name: round(d / tot, 4) for name, d in zip(PHASES, dur)}
     out["mean_wave_us"] = {"oi_kernel": sum(dur[:4]) / 1e2 / max(int(c[0]), 1),
                            "oi_map_kernel": sum(dur[4:]) / 1e2 / max(int(c[8]), 1)}
+    if hasattr(lib, "gmapdp_debug_oi_waves"):  # per-call wave durations: the kernels' tails
+        lib.gmapdp_debug_oi_waves.argtypes = [C.c_void_p]
+        wv = np.zeros((3, 16384), dtype=np.uint32)
+        lib.gmapdp_debug_oi_waves(wv.ctypes.data)
+        m = min(len(probs), 16384)
+        for name, row in (("oi_kernel", 0), ("oi_map_kernel", 1)):
+            us = wv[row, :m] / 1e2
+            top = np.argsort(-us)[:8]
+            out["waves_" + name] = {"p50_us": float(np.percentile(us, 50)), "p99_us": float(np.percentile(us, 99)),
+                                    "max_us": float(us.max()),
+                                    "slowest": [[int(i), float(us[i]), int(wv[2, i])] for i in top]}
+        E = wv[2, :m].astype(np.float64)
+        out["events"] = {"p50": float(np.percentile(E, 50)), "p99": float(np.percentile(E, 99)), "max": float(E.max())}
     print(json.dumps(out))
     eng.close()
     del res
