@@ -458,7 +458,8 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", init_method="env://", device_id=dev)
-    eng = gmapdp.Engine(local)
+    # the plans' launch classes over three streams (the caller's and two sides): stage 2 takes the fourth
+    eng = gmapdp.Engine(local, flags=gmapdp.CTX_TWO_SIDES if int(os.environ.get("GMAPDP_BENCH_SIDES", "2")) < 3 else 0)
     if world > 1:
         shard.check_replicated(shard.genome_digest(genome.blocks[::4097]), dist)
     eng.set_genome(blocks=genome.blocks, length=genome.length)
@@ -543,16 +544,18 @@ def main():
     progress("plans ready (%d blocks, %.2f s DP plans, %.2f s stage-2 plans)" % (len(B), t_plan, t_oplan))
 
     # Streams: stage 2 on its own stream, the DP launch classes on the engine's schedule (0 = main,
-    # 1..3 = sides, longest-processing-time first), forked from and joined into main.  The process
-    # has four hardware queues (GPU_MAX_HW_QUEUES, HIP's default), so four streams: the plan's third
-    # side list joins its second (the two lightest), where the microexon plan runs too.  Real
+    # 1..2 = sides, longest-processing-time first over these three: the context is created with
+    # GMAPDP_CTX_TWO_SIDES), forked from and joined into main; the microexon plan runs on the last side.
+    # The process has four hardware queues (GPU_MAX_HW_QUEUES, HIP's default), so four streams.  Real
     # (non-null) streams, so per-launch events time exactly the launches on their stream.
     stream = torch.cuda.Stream(dev)
     # GMAPDP_BENCH_SIDES=3 (with GPU_MAX_HW_QUEUES >= 5): each of the plan's side lists on its own stream
     sides = [torch.cuda.Stream(dev) for _ in range(int(os.environ.get("GMAPDP_BENCH_SIDES", "2")))]
     # stage 2 (the step's longest chain) may take the high-priority queue: GMAPDP_BENCH_S2_PRIORITY=1
     s2prio = int(os.environ.get("GMAPDP_BENCH_S2_PRIORITY", "0"))
-    ostream = torch.cuda.Stream(dev, priority=-1) if s2prio else torch.cuda.Stream(dev)
+    # (=2: only the seeding launch on a high-priority stream, the chaining back on a normal one)
+    ostream = torch.cuda.Stream(dev, priority=-1) if s2prio == 1 else torch.cuda.Stream(dev)
+    sstream = torch.cuda.Stream(dev, priority=-1) if s2prio == 2 else ostream
     side_of = lambda k: min(k, len(sides))  # noqa: E731  plan stream k >= 1 -> side index + 1
 
     def launch(b, li, s, kernel_only=False):
@@ -579,12 +582,14 @@ def main():
         fork.record(stream)
         used = set()
         if do_oligo:
-            ostream.wait_event(fork)
+            sstream.wait_event(fork)
             if ev is not None:
-                ev["oligo"][0].record(ostream)
-            orun(b, ostream, 1)
+                ev["oligo"][0].record(sstream)
+            orun(b, sstream, 1)
             if ev is not None:
-                ev["oligo"][1].record(ostream)
+                ev["oligo"][1].record(sstream)
+            if sstream is not ostream:
+                ostream.wait_stream(sstream)
             # the chaining as its three kernels (what 4 / 8 / 16: s2a, the s2b sweep, s2c), events between
             orun(b, ostream, 4)
             if ev is not None:

@@ -275,6 +275,7 @@ struct gmapdp_ctx {
   uint64_t genome_length = 0;
   bool genome_owned = true;  // false: another context's HBM genome (gmapdp_share_genome)
   bool one_stream = false;   // GMAPDP_CTX_ONE_STREAM: no side streams (callers that run many contexts)
+  int plan_sides = kAux;     // side streams a plan's LPT spreads over (GMAPDP_CTX_TWO_SIDES: 2)
   hipEvent_t ev_block = nullptr;  // GMAPDP_CTX_BLOCKING_SYNC / _POLL_SYNC: batch completion waited on without spinning
   bool poll = false;              // GMAPDP_CTX_POLL_SYNC: ev_block is polled with sleeps in between
   DevBuf probs, order, qseq, qseq_uc, results, pairs, gdirs;
@@ -388,6 +389,7 @@ int gmapdp_create_ex(gmapdp_ctx** out, int device, int mode, int user_open, int 
   ctx->user_extend = user_extend;
   ctx->user_dynprog_p = user_dynprog_p;
   ctx->one_stream = (flags & GMAPDP_CTX_ONE_STREAM) != 0;
+  ctx->plan_sides = (flags & GMAPDP_CTX_TWO_SIDES) ? 2 : gmapdp_ctx::kAux;
   hipError_t e = hipSetDevice(device);
   int prio_least = 0, prio_greatest = 0;
   if (e == hipSuccess && (flags & (GMAPDP_CTX_PRIO_HIGH | GMAPDP_CTX_PRIO_LOW)))
@@ -1213,7 +1215,7 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     double load[1 + gmapdp_ctx::kAux] = {0.0, 0.0, 0.0, 0.0};
     for (int i : idx) {
       int best = 0;
-      for (int k = 1; k <= gmapdp_ctx::kAux; k++)
+      for (int k = 1; k <= ctx->plan_sides; k++)
         if (load[k] < load[best]) best = k;
       plan.launches[i].stream = best;
       load[best] += plan.launches[i].work;

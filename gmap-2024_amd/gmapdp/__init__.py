@@ -20,6 +20,7 @@ LIB_PATH = os.environ.get("GMAPDP_LIB") or os.path.join(os.path.dirname(_HERE), 
 WATSON, JUMP_LATE, WIDEBAND = 0x1, 0x2, 0x4
 DEVICE = "device"  # splice / candidate probabilities evaluated by the engine's device MaxEnt (a NULL arena)
 CTX_ONE_STREAM, CTX_PRIO_HIGH, CTX_PRIO_LOW, CTX_BLOCKING_SYNC, CTX_POLL_SYNC = 0x1, 0x2, 0x4, 0x8, 0x10  # create_ex flags
+CTX_TWO_SIDES = 0x20
 SIMD = 0x40  # GMAPDP_SIMD: the reference's SIMD builds' semantics (every problem family)
 HALFP, FINALP = 0x8, 0x10
 KNOWN_SITES = 0x80  # GMAPDP_KNOWN_SITES: known splice sites of a genome gap (gmap -s)

@@ -698,6 +698,11 @@ void gmapdp_destroy (gmapdp_ctx *ctx);
 #define GMAPDP_CTX_PRIO_LOW   0x4
 #define GMAPDP_CTX_BLOCKING_SYNC 0x8  /* batch calls sleep on a blocking-sync event instead of spinning */
 #define GMAPDP_CTX_POLL_SYNC 0x10     /* batch calls poll their completion, sleeping between polls */
+/* Plans spread their launch classes (longest-processing-time first) over the caller's stream and two
+ * side streams instead of three: for a caller that keeps the process's fourth hardware queue for other
+ * work of its own, e.g. Stage2_compute on its own stream beside the plan (bench.py), so that no stream
+ * receives two of the plan's lists. */
+#define GMAPDP_CTX_TWO_SIDES 0x20
 int gmapdp_create_ex (gmapdp_ctx **ctx, int device, int mode, int user_open, int user_extend, int user_dynprog_p,
                       int flags);
 /* Use `owner`'s HBM-resident genome in `ctx` (no copy; same device).  `owner` must outlive every

@@ -1,5 +1,5 @@
 set -o pipefail
-O=gpurun_out/r05m
+O=gpurun_out/r05y
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 export GMAPDP_BENCH_WORKERS=1
