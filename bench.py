@@ -255,10 +255,10 @@ def rocprof_name(kind, R, dl, lds=0):
     return "gmapdp::gg_kernel<%d, %s>" % (R, "true" if dl else "false")
 
 
-def latest_e2e():
-    """The cited GMAP end-to-end record (tools/e2e_timing.py, profiles/*/e2e.json; profile_record's rule):
-    the unmodified gmap and the drop-in on the same reads and host cores."""
-    d, src = profile_record("e2e", "e2e.json", None)
+def latest_e2e(kind="e2e"):
+    """The cited GMAP end-to-end record (tools/e2e_timing.py, profiles/*/e2e.json, or e2e_avx2.json for the
+    AVX2 builds; profile_record's rule): the unmodified gmap and the drop-in on the same reads and host cores."""
+    d, src = profile_record(kind, kind + ".json", None)
     try:
         runs = d["runs"]
     except (TypeError, KeyError):
@@ -267,7 +267,7 @@ def latest_e2e():
     gpu = [r for r in runs if "gpu" in r["program"]]
     if not cpu or not gpu:
         return None
-    return {"source": src, "recorded": d.get("recorded"), "reads": d.get("reads"),
+    return {"source": src, "recorded": d.get("recorded"), "reads": d.get("reads"), "mode": d.get("mode", "-g"),
             "cpu_gmap_reads_per_s": max(r["reads_per_s"] for r in cpu),
             "cpu_gmap_threads": max(cpu, key=lambda r: r["reads_per_s"])["threads"],
             "drop_in_reads_per_s": max(r["reads_per_s"] for r in gpu),
@@ -290,6 +290,7 @@ def like_for_like(out, pcie_ms, up, down):
             "ratio_vs_cpu": v / cpu if cpu else None,
             "ratio_vs_cpu_incl_pcie": with_pcie / cpu if cpu else None,
             "drop_in_end_to_end": latest_e2e(),
+            "drop_in_end_to_end_avx2": latest_e2e("e2e_avx2"),
             "note": "copies measured serially after the step (not overlapped); the end-to-end record is GMAP's own "
                     "program on the same reads and cores (tools/e2e_timing.py)"}
 

@@ -5,9 +5,11 @@ engine), on the same host cores.  Measurement tool, run on the GPU box:
     python tools/e2e_timing.py --reads 2000 --threads 1,16
 
 Reads are tests/golden/make_e2e.py's synthetic 2-kb spliced reads (5 exons x 400 nt, 2 % subs) against
-its 300-kb segment, in user-segment mode (-g: stage 2 over the whole segment, then stage 3).  Both
-programs' SAM outputs are compared; the JSON line gives reads/s per program and thread count and the
-shim's call counts.
+its 300-kb segment, in user-segment mode (-g: stage 2 over the whole segment, then stage 3).  With
+--index DIR (made by tools/e2e_index.py) the reads are DIR/r.fa and both programs run on DIR's genome
+index (`-D DIR/db -d NAME`: stage 1, then stage 2 over each locus +- 100 kb, then stage 3 -- the mix the
+headline bench restates).  Both programs' SAM outputs are compared; the JSON line gives reads/s per
+program and thread count and the shim's call counts.
 """
 import argparse
 import json
@@ -26,6 +28,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reads", type=int, default=2000)
+    ap.add_argument("--index", default=None, help="tools/e2e_index.py's directory: gmap -d over its index")
     ap.add_argument("--threads", default="1,16")
     ap.add_argument("--build", default="nosimd", choices=["nosimd", "avx2"])
     ap.add_argument("--gpu-threads", default=None, help="thread counts for the GPU program (default: --threads)")
@@ -43,13 +46,30 @@ def main():
                          "programs with tools/pcprof.c's sampler on and resolves them (tools/pcprof.py)")
     a = ap.parse_args()
     import make_e2e as M
-    genome = list(M.synth_genome())
-    reads = [M.synth_read(genome, i) for i in range(a.reads)]
     tmp = tempfile.mkdtemp(prefix="e2e_")
-    M.write_fasta(os.path.join(tmp, "g.fa"), [("synseg", "".join(genome))])
-    M.write_fasta(os.path.join(tmp, "r.fa"), reads)
+    if a.index:
+        idx = os.path.abspath(a.index)
+        meta = json.load(open(os.path.join(idx, "meta.json")))
+        # the first --reads reads of the index's read set
+        with open(os.path.join(idx, "r.fa")) as f, open(os.path.join(tmp, "r.fa"), "w") as g:
+            n = 0
+            for line in f:
+                if line.startswith(">"):
+                    n += 1
+                    if n > a.reads:
+                        break
+                g.write(line)
+        a.reads = min(a.reads, n)
+        gargs = ["-D", os.path.join(idx, "db"), "-d", meta["name"]]
+    else:
+        genome = list(M.synth_genome())
+        reads = [M.synth_read(genome, i) for i in range(a.reads)]
+        M.write_fasta(os.path.join(tmp, "g.fa"), [("synseg", "".join(genome))])
+        M.write_fasta(os.path.join(tmp, "r.fa"), reads)
+        gargs = ["-g", "g.fa"]
     ref = os.path.join(ROOT, "oracle", "_ref")
-    out = {"reads": a.reads, "build": a.build, "cpu_model": None, "runs": []}
+    out = {"reads": a.reads, "build": a.build, "mode": "-d %s" % meta["name"] if a.index else "-g", "cpu_model": None,
+           "runs": []}
     try:
         out["cpu_model"] = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
     except (OSError, StopIteration):
@@ -81,8 +101,7 @@ def main():
                 os.makedirs(a.prof, exist_ok=True)
                 env["PCPROF_OUT"] = os.path.abspath(os.path.join(a.prof, "pcprof_%s_%s_t%d.txt" % (prog, cname, t)))
                 profs.append(env["PCPROF_OUT"])
-            args = [os.path.join(ref, prog), "-t", str(t), "-O", "-g", "g.fa", "-f", "samse", "--no-sam-headers",
-                    "r.fa"]
+            args = [os.path.join(ref, prog), "-t", str(t), "-O"] + gargs + ["-f", "samse", "--no-sam-headers", "r.fa"]
             t0 = time.perf_counter()
             ru0 = resource.getrusage(resource.RUSAGE_CHILDREN)
             threads = None
