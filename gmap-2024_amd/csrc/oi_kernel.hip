@@ -139,28 +139,62 @@ constexpr int kOiHist = 4 * 256;  // = 2 x 512
 
 // Event keys, ordered by diagi (the sort's digits) then by generation order (query order).  The run test
 // of the reference, q - q_prev >= diag_lookback + cum[q] - cum[q_prev], is (q - cum[q]) - (q_prev -
-// cum[q_prev]) >= diag_lookback: with t = q - cum_nohits[q] carried in the key (querypos < 2^16), the
-// sweep compares two keys and reads no cum_nohits at all (two scattered loads per event otherwise, the
-// L2 request rate being what bounds this kernel).  Past 2^16 query positions the key holds q only and
-// the sweep looks t up.
-struct OiKeyQT {  // diagi << 32 | q << 16 | t
-  __device__ static uint64_t make(uint32_t di, uint32_t q, uint32_t t) {
-    return ((uint64_t)di << 32) | (q << 16) | t;
-  }
-  __device__ static uint32_t di(uint64_t k) { return (uint32_t)(k >> 32); }
-  __device__ static uint32_t q(uint64_t k) { return ((uint32_t)k >> 16); }
-  __device__ static int t(uint64_t k, const int* __restrict__) { return (int)((uint32_t)k & 0xFFFFu); }
-};
-struct OiKeyQ {  // diagi << 32 | q
-  __device__ static uint64_t make(uint32_t di, uint32_t q, uint32_t) { return ((uint64_t)di << 32) | q; }
-  __device__ static uint32_t di(uint64_t k) { return (uint32_t)(k >> 32); }
-  __device__ static uint32_t q(uint64_t k) { return (uint32_t)k; }
-  __device__ static int t(uint64_t k, const int* __restrict__ cum) { return (int)(uint32_t)k - cum[(uint32_t)k]; }
-};
+// cum[q_prev]) >= diag_lookback: with t = q - cum_nohits[q] in the key the sweep compares two keys and
+// reads no cum_nohits (two scattered loads per event otherwise).  t rises by one at every query position
+// that has hits (cum_nohits only counts positions without), so on the positions events come from t is
+// strictly increasing in q: (t, diagi) orders events as (q, diagi) does, and q is recovered, for the few
+// events whose querypos the records need, as the first position with q - cum[q] >= t (binary search).
+// So a 2-kb read's 214-kb window takes 32-bit keys (diagi < 2^20 - 1, t < 4096: half the bytes of every
+// event pass and radix scatter, the kernel being bound by that traffic); longer queries or windows keep
+// 64 bits with q (and t below 2^16) inside.
 __device__ __forceinline__ uint64_t readlane64(uint64_t k, int l) {
   return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(k >> 32), l) << 32) |
          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k, l);
 }
+// first query position whose q - cum[q] reaches t (q - cum[q] is non-decreasing)
+__device__ __forceinline__ uint32_t oi_q_of_t(int t, const int* __restrict__ cum, int nq) {
+  int lo = 0, hi = nq - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (mid - cum[mid] >= t) hi = mid;
+    else lo = mid + 1;
+  }
+  return (uint32_t)lo;
+}
+struct OiKeyT32 {  // diagi << 12 | t
+  using K = uint32_t;
+  static constexpr uint32_t kMax = ~0u;
+  __device__ static uint32_t make(uint32_t di, uint32_t, uint32_t t) { return (di << 12) | t; }
+  __device__ static uint32_t di(uint32_t k) { return k >> 12; }
+  __device__ static int t(uint32_t k, const int* __restrict__) { return (int)(k & 0xFFFu); }
+  __device__ static uint32_t ord(uint32_t k) { return k & 0xFFFu; }  // orders events as q does
+  __device__ static uint32_t q(uint32_t k, const int* __restrict__ cum, int nq) {
+    return oi_q_of_t((int)(k & 0xFFFu), cum, nq);
+  }
+  __device__ static uint32_t readlane(uint32_t k, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)k, l); }
+};
+struct OiKeyQT {  // diagi << 32 | q << 16 | t
+  using K = uint64_t;
+  static constexpr uint64_t kMax = ~0ull;
+  __device__ static uint64_t make(uint32_t di, uint32_t q, uint32_t t) {
+    return ((uint64_t)di << 32) | (q << 16) | t;
+  }
+  __device__ static uint32_t di(uint64_t k) { return (uint32_t)(k >> 32); }
+  __device__ static int t(uint64_t k, const int* __restrict__) { return (int)((uint32_t)k & 0xFFFFu); }
+  __device__ static uint32_t ord(uint64_t k) { return (uint32_t)k >> 16; }
+  __device__ static uint32_t q(uint64_t k, const int* __restrict__, int) { return (uint32_t)k >> 16; }
+  __device__ static uint64_t readlane(uint64_t k, int l) { return readlane64(k, l); }
+};
+struct OiKeyQ {  // diagi << 32 | q
+  using K = uint64_t;
+  static constexpr uint64_t kMax = ~0ull;
+  __device__ static uint64_t make(uint32_t di, uint32_t q, uint32_t) { return ((uint64_t)di << 32) | q; }
+  __device__ static uint32_t di(uint64_t k) { return (uint32_t)(k >> 32); }
+  __device__ static int t(uint64_t k, const int* __restrict__ cum) { return (int)(uint32_t)k - cum[(uint32_t)k]; }
+  __device__ static uint32_t ord(uint64_t k) { return (uint32_t)k; }
+  __device__ static uint32_t q(uint64_t k, const int* __restrict__, int) { return (uint32_t)k; }
+  __device__ static uint64_t readlane(uint64_t k, int l) { return readlane64(k, l); }
+};
 
 // Returns false (nothing written) when the shared event pool could not hold this problem's 3 E slots
 // (oi_kernel took them, `base`, with one atomic as it finished).
@@ -176,9 +210,9 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
                                    int* evq, int32_t* __restrict__ good, int gcap, int& ngood_out, int& maxn_out) {
   OI_MARK(9);
   if (base == ~0ull) return false;
-  using K = uint64_t;
-  constexpr K kMax = ~0ull;
-  K* evA = pool + base;                             // events (OiKeyQT / OiKeyQ)
+  using K = typename KT::K;
+  constexpr K kMax = KT::kMax;
+  K* evA = reinterpret_cast<K*>(pool + base);       // events (OiKeyT32 / OiKeyQT / OiKeyQ)
   K* evB = evA + E;                                 // radix-sort ping-pong
   int4* grec = reinterpret_cast<int4*>(pool + base + 2 * (size_t)E);  // good records (at most E / 2)
   const int db = maxdiag < (1u << 18) ? 9 : 8;       // digit bits
@@ -297,7 +331,7 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const int e = e0 + 64 * r + lane;
-        key[r] = e < E ? src[e] : 0ull;
+        key[r] = e < E ? src[e] : (K)0;
       }
 #pragma unroll
       for (int r = 0; r < 4; r++) {
@@ -352,7 +386,7 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       K pk = __shfl_up(key[r], 1, 64);
-      if (lane == 0) pk = r == 0 ? c_key : readlane64(key[r - 1], 63);
+      if (lane == 0) pk = r == 0 ? c_key : KT::readlane(key[r - 1], 63);
       pkey[r] = pk;
       const bool v = s0 + 64 * r + lane < E;
       tq[r] = v ? KT::t(key[r], cum) : 0;
@@ -364,7 +398,7 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
       const int e = e0 + lane;
       const bool v = e < E;
       const K key_r = key[r], pk = pkey[r];
-      const uint32_t d = KT::di(key_r), q = KT::q(key_r);
+      const uint32_t d = KT::di(key_r), q = KT::ord(key_r);  // (q or t: the same order)
       const bool newdiag = v && (e == 0 || KT::di(pk) != d);
       bool newrun = newdiag;
       if (v && !newdiag) newrun = tq[r] - tpq[r] >= lookback;
@@ -378,7 +412,7 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
       fs = seg_scan_min(lane, fs, e, ds);
       if (ds < e0) fs = min(fs, c_fs);
       K nk = __shfl_down(key_r, 1, 64);
-      if (lane == 63) nk = r < 3 ? readlane64(key[r + 1], 0) : after;
+      if (lane == 63) nk = r < 3 ? KT::readlane(key[r + 1], 0) : after;
       const bool dend = v && (e + 1 == E || KT::di(nk) != d);
       const bool isgood = dend && fs != 0x7fffffff;
       const uint64_t gm = ballot(isgood);
@@ -398,7 +432,7 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
       c_fs = __builtin_amdgcn_readlane(fs, 63);
       c_mk = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(mk >> 32), 63) << 32) |
              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mk, 63);
-      c_key = readlane64(key_r, 63);
+      c_key = KT::readlane(key_r, 63);
     }
   }
   // the global maximum and the first (querypos, diagi) event carrying it
@@ -421,15 +455,17 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
   }
   __threadfence_block();
   // records and their (querypos, diagi) keys; then the reference's order
-  uint64_t* gkey = (S == evA) ? evB : evA;  // the free sort buffer: the good diagonals' query-order keys
+  // the good diagonals' query-order keys: the free sort buffer (64-bit events), or the pool's second E
+  // words (32-bit events: both sort buffers sit in the first)
+  uint64_t* gkey = sizeof(K) == 8 ? reinterpret_cast<uint64_t*>(S == evA ? evB : evA) : pool + base + E;
   for (int g = lane; g < ngood; g += 64) {
     const int4 r = grec[g];
     const uint32_t di = (uint32_t)r.w;
     const int eb = r.y, bn = r.z;
-    const uint32_t qreach = r.x >= 0 ? KT::q(S[r.x]) : 0u;
+    const uint32_t qreach = r.x >= 0 ? KT::q(S[r.x], cum, nq) : 0u;
     gkey[g] = ((uint64_t)qreach << 32) | di;
     grec[g] = make_int4(di >= (uint32_t)qlen ? (int)(di - (uint32_t)qlen) : (int)((uint32_t)qlen - di),
-                        (int)KT::q(S[eb - bn]), (int)KT::q(S[eb]), bn + 1);
+                        (int)KT::q(S[eb - bn], cum, nq), (int)KT::q(S[eb], cum, nq), bn + 1);
   }
   __threadfence_block();
   if (ngood > gcap) ngood = -1;  // more good diagonals than the layout gave the problem: overflow
@@ -813,7 +849,10 @@ __global__ __launch_bounds__(64) void oi_map_kernel(
     const unsigned long long pbase = *reinterpret_cast<const unsigned long long*>(base_s + so.poolbase);
     const int gcap = (int)min(P.diag_cap, 0x7fffffffu);
     const bool sorted =
-        nq < 65536
+        maxdiag < (1u << 20) - 1 && nq <= 4096
+            ? oi_mappings_sorted<OiKeyT32>(lane, qlen, nq, totalpositions, maxdiag, chrinit, diag_lookback, suffn,
+                                           npq, mpq, cum, table, pool, pbase, hist, evq, good, gcap, ngood, maxn)
+        : nq < 65536
             ? oi_mappings_sorted<OiKeyQT>(lane, qlen, nq, totalpositions, maxdiag, chrinit, diag_lookback, suffn,
                                            npq, mpq, cum, table, pool, pbase, hist, evq, good, gcap, ngood, maxn)
             : oi_mappings_sorted<OiKeyQ>(lane, qlen, nq, totalpositions, maxdiag, chrinit, diag_lookback, suffn,
