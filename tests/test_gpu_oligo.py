@@ -160,3 +160,35 @@ def test_gpu_oligo_wide_windows_match_oracle(engine):
     exp = [orc.oligo_mappings(p) for p in probs]
     d = _first_diff(got, exp)
     assert d is None, _msg(probs, d, "oracle")
+
+
+def test_gpu_oligo_event_key_formats(engine):
+    """oi_map_kernel's three event-key formats against the oracle: 32-bit (diagi << 12 | t) for queries of
+    <= 4 096 8-mer positions on windows below 2^20 (the bench's shape, covered above too), 64-bit with q and
+    t for longer queries or windows of 2^20 and more, 64-bit with q alone past 2^16 query positions (a
+    repetitive query: few distinct 8-mers).  Records carry querypos values recovered from t in the 32-bit
+    format (binary search over cum_nohits), from the key otherwise."""
+    rng = random.Random(8600)
+    g = _repeat_genome(rng, 1400000)
+    engine.set_genome(g)
+    orc = Oracle()
+    orc.set_genome(g)
+    probs = []
+    for i in range(24):
+        p = oligo_problem(rng, g, edge=(i % 5 == 0))
+        kind = i % 3
+        if kind == 0:  # a long query: 4 097+ positions
+            extra = bytes(g[p["chrstart"]:p["chrstart"] + 4200 + rng.randint(0, 1500)])
+            p["quc"] = extra + p["quc"]
+        elif kind == 1:  # a window past 2^20
+            span = rng.randint((1 << 20) + 10, (1 << 20) + 200000)
+            p["chrstart"] = max(0, min(p["chrstart"], len(g) - 2000 - span))
+            p["chrend"] = p["chrstart"] + span
+        else:  # past 2^16 query positions: a short unit repeated
+            unit = bytes(p["quc"][:rng.randint(300, 900)])
+            p["quc"] = unit * (66000 // len(unit) + 1)
+        probs.append(p)
+    got = engine.oligo_mappings_batch(probs)
+    exp = [orc.oligo_mappings(p) for p in probs]
+    d = _first_diff(got, exp)
+    assert d is None, _msg(probs, d, "oracle")
