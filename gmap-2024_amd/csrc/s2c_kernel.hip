@@ -2039,10 +2039,6 @@ __global__ __launch_bounds__(64) void s2a_kernel(
 #ifndef GMAPDP_S2B_WPE
 #define GMAPDP_S2B_WPE 4  // waves per SIMD the sweep's registers are budgeted for (variants: make variant DEFS=...)
 #endif
-// the sweeps launched first (the heaviest, by s2a's work estimate) issue ahead of the light waves that share
-// their SIMD: a heavy call's single-wave latency, not the grid's throughput, ends the launch
-__device__ int g_s2b_prio_n = 256;
-
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GMAPDP_S2B_WPE))) void s2b_kernel(
     const DevStage2Problem* __restrict__ probs, const uint32_t* __restrict__ blocks, uint64_t nwords,
     const char* __restrict__ qseq, const char* __restrict__ quc, const gmapdp_oligo_result* __restrict__ ores,
@@ -2083,7 +2079,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GMAPDP_S2B_W
   (void)diag_all; (void)counters; (void)scratch_cap; (void)paths_out; (void)path_cap; (void)pairs_out; (void)pair_cap;
   const gmapdp_stage2_result R0 = results[P.index];
   if (R0.status != kS2Chained) return;
-  if ((int)blockIdx.x < g_s2b_prio_n) __builtin_amdgcn_s_setprio(2);
   const int qstart = R0.diag_querystart, qend = R0.diag_queryend;
   S2_MARK(3);
 #ifdef GMAPDP_OI_TIMING
@@ -2683,17 +2678,7 @@ hipError_t launch_s2c(int nproblems, hipStream_t stream, const DevStage2Problem*
       const char* v = std::getenv("GMAPDP_S2B_LDS");
       return v ? (size_t)std::strtoull(v, nullptr, 10) : (size_t)0;
     }();
-    // GMAPDP_S2B_PRIO (experiments): how many of the first sweeps run at raised priority
-    static const int prio_n = [] {
-      const char* v = std::getenv("GMAPDP_S2B_PRIO");
-      return v ? std::atoi(v) : -1;
-    }();
-    static bool prio_set = false;
-    if (prio_n >= 0 && !prio_set) {
-      e = hipMemcpyToSymbol(HIP_SYMBOL(g_s2b_prio_n), &prio_n, sizeof(int));
-      prio_set = true;
-    }
-    if (e == hipSuccess && xlds > 64 * 1024)
+    if (xlds > 64 * 1024)
       e = hipFuncSetAttribute(reinterpret_cast<void*>(&s2b_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)xlds);
     if (e == hipSuccess)
