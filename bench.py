@@ -83,15 +83,18 @@ def algorithmic_bytes(rlength, glength, npairs, desc_bytes):
     return int((desc_bytes + 2 * r + 12 * ((g + 62) // 32) + 32).sum() + 16 * int(np.asarray(npairs).sum()))
 
 
-def genome_algorithmic_bytes(gp, npairs):
+def genome_algorithmic_bytes(gp, npairs, sprob_arena=False):
     """Dynprog_genome_gap with its splice-site MaxEnt (the fused operation gg_kernel runs): descriptor (96 B)
     + query and upper-cased query (2 x rlength) + the packed genome blocks of both segments + result (72 B)
     + one 16-B record per emitted pair.  The splice probabilities are computed in the kernel from the same
-    segments and the L2-resident model tables, so they are not counted (no probability arena exists)."""
+    segments and the L2-resident model tables, so they are not counted (no probability arena exists).
+    `sprob_arena`: the SIMD builds' uxg_kernel still reads the 8-B-per-column probability arena that its
+    me_gap_kernel prologue writes, so its classes count 8 x (glengthL + glengthR) more."""
     r = gp["rlength"].astype(np.int64)
     gL = gp["glengthL"].astype(np.int64)
     gR = gp["glengthR"].astype(np.int64)
-    return int((96 + 2 * r + 12 * ((gL + 62) // 32) + 12 * ((gR + 62) // 32) + 72).sum()
+    arena = 8 * (gL + gR) if sprob_arena else 0
+    return int((96 + 2 * r + 12 * ((gL + 62) // 32) + 12 * ((gR + 62) // 32) + 72 + arena).sum()
                + 16 * int(np.asarray(npairs).sum()))
 
 
@@ -665,7 +668,8 @@ def main():
                                    np.full(ne, gmapdp.END_PROBLEM_DTYPE.itemsize)])
             return algorithmic_bytes(rl[m], gl[m], npairs[m], desc[m]), None
         j = m - nprob
-        return genome_algorithmic_bytes(gp[j], gnp[j]), int(genome_cells(gp[j], g_fills[j]).sum())
+        return (genome_algorithmic_bytes(gp[j], gnp[j], sprob_arena=b["kinds"][li] == 5),
+                int(genome_cells(gp[j], g_fills[j]).sum()))
 
     def fetch_results(b):
         res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=gmapdp.RESULT_DTYPE)[:b["ngpu"]]

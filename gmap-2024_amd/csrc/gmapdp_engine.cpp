@@ -2550,6 +2550,16 @@ int gmapdp_oligo_mappings_batch(gmapdp_ctx* ctx, const gmapdp_oligo_problem* pro
     return GMAPDP_EINVAL;
   if (!ctx->d_genome) return GMAPDP_ENOGENOME;
   if (n == 0) return GMAPDP_OK;
+  {
+    // npositions / mappings are written per problem at its query slice [qoff, qoff + querylength), and the
+    // mappings turned absolute by adding that problem's table offset: two problems on overlapping slices
+    // would overwrite each other's outputs (and have the offset added twice), so they are refused.
+    std::vector<std::pair<int64_t, int64_t>> sl(n);
+    for (int i = 0; i < n; i++) sl[i] = {problems[i].qoff, (int64_t)problems[i].qoff + problems[i].querylength};
+    std::sort(sl.begin(), sl.end());
+    for (int i = 1; i < n; i++)
+      if (sl[i].first < sl[i - 1].second) return bad(ctx, "stage-2 seeding: two problems share query slots");
+  }
   gmapdp_oligo_plan* plan = nullptr;
   int rc = oligo_plan_build(ctx, problems, n, qseq_uc, qbytes, &plan, true);
   if (rc) return rc;

@@ -492,6 +492,27 @@ __device__ __forceinline__ void count_inc(CT* cnt, int u) {
   }
 }
 
+// A problem that outgrew its layout: no hits, oned_matrix_p -1 (Stage2_compute status -2), the event pool
+// slot marked empty, nothing written past the problem's slices.  Block-uniform: every thread calls it.
+__device__ void oi_report_overflow(const DevOligoProblem& P, int tid, int nthreads, int qlen, int32_t* npq,
+                                   int32_t* mpq, gmapdp_oligo_result* results, unsigned char* poolslot) {
+  for (int i = tid; i < qlen; i += nthreads) {
+    npq[i] = 0;
+    mpq[i] = -1;
+  }
+  if (tid == 0) {
+    gmapdp_oligo_result res;
+    res.totalpositions = 0;
+    res.maxnconsecutive = 0;
+    res.oned_matrix_p = -1;
+    res.ndiagonals = 0;
+    res.table_offset = P.table_offset;
+    res.diag_offset = P.diag_offset;
+    results[P.index] = res;
+    *reinterpret_cast<unsigned long long*>(poolslot) = ~0ull;
+  }
+}
+
 // Two waves per problem: both take half of the query's 8-mers and half of the window's pass-1 scan (the
 // long phase: ~200 steps on a 214-kb window) over the same LDS tables; the phases that carry a running
 // value in order (the id ranks, the table layout, pass 2's placement, the per-position mappings) stay
@@ -565,8 +586,16 @@ __global__ __launch_bounds__(64 * kOiWaves) void oi_kernel(
     if (wave == 0) wrank[base + lane] = (uint16_t)(run + incl - c);
     run += __builtin_amdgcn_readlane(incl, 63);
   }
-  const int U = run;  // <= umax (the host counted them)
+  const int U = run;
   OI_MARK(1);
+  unsigned char* base_s = scratch + P.scratch_offset;
+  const ScratchOi so = scratch_oi(qlen, P.chrend > P.chrstart ? P.chrend - P.chrstart : 0);
+  // More distinct 8-mers than the LDS bucket the plan gave the problem (a plan laid out from one query and
+  // run on another): cnt / offs would run past the dynamic LDS, so report overflow before writing them.
+  if (U > P.umax) {
+    oi_report_overflow(P, tid, 64 * kOiWaves, qlen, npq, mpq, results, base_s + so.poolbase);
+    return;
+  }
   for (int u = tid; u < U; u += 64 * kOiWaves) cnt[u] = 0;
   __syncthreads();
 
@@ -579,8 +608,6 @@ __global__ __launch_bounds__(64 * kOiWaves) void oi_kernel(
   // next); the next step's two loads are issued before this step's LDS work.  Every hit is appended
   // to the problem's hit list {window index, id} in ascending position, so pass 2 never re-reads the
   // window.
-  unsigned char* base_s = scratch + P.scratch_offset;
-  const ScratchOi so = scratch_oi(qlen, P.chrend > P.chrstart ? P.chrend - P.chrstart : 0);
   uint2* hitlist = reinterpret_cast<uint2*>(base_s + so.hits);
   int nhits = 0;
   if (npos > 0) {
@@ -691,21 +718,7 @@ __global__ __launch_bounds__(64 * kOiWaves) void oi_kernel(
   // then run on another query), or a 16-bit counter that could wrap: report overflow, as an exhausted
   // event pool does, with no hits and nothing written past the problem's slices.
   if ((uint32_t)nhits > P.hit_cap || tot > P.table_cap || (sizeof(CT) == 2 && nhits > 65535)) {
-    for (int i = tid; i < qlen; i += 64 * kOiWaves) {
-      npq[i] = 0;
-      mpq[i] = -1;
-    }
-    if (tid == 0) {
-      gmapdp_oligo_result res;
-      res.totalpositions = 0;
-      res.maxnconsecutive = 0;
-      res.oned_matrix_p = -1;
-      res.ndiagonals = 0;
-      res.table_offset = P.table_offset;
-      res.diag_offset = P.diag_offset;
-      results[P.index] = res;
-      *reinterpret_cast<unsigned long long*>(base_s + so.poolbase) = ~0ull;
-    }
+    oi_report_overflow(P, tid, 64 * kOiWaves, qlen, npq, mpq, results, base_s + so.poolbase);
     return;
   }
 

@@ -2332,6 +2332,7 @@ __wrap_Oligoindex_get_mappings (List_T diagonals, bool *coveredp, Chrpos_T **map
       GROW(r->dg, r->dgcap, 4 * dc + 4);
       shim_submit(r);
       shim_count(ST_OLIGO);
+      if (r->orr.oned_matrix_p < 0) shim_refuse("Oligoindex_get_mappings: the engine reported a layout overflow");
       this->table = NULL;
       if (r->tabn > 0) {
         this->table = (Chrpos_T *) MALLOC(r->tabn * sizeof(Chrpos_T));
@@ -2363,6 +2364,9 @@ __wrap_Oligoindex_get_mappings (List_T diagonals, bool *coveredp, Chrpos_T **map
   GROW(r->dg, r->dgcap, 4 * dc + 4);
   shim_submit(r);
   shim_count(ST_OLIGO);
+  /* oned_matrix_p -1: the engine's layout overflowed (nothing usable was written).  The request was sized
+     with the worst-case capacities, so this cannot happen; never hand GMAP an empty "valid" answer. */
+  if (r->orr.oned_matrix_p < 0) shim_refuse("Oligoindex_get_mappings: the engine reported a layout overflow");
   /* the table, owned by the oligoindex (freed by Oligoindex_untally) */
   this->table = NULL;
   if (r->tabn > 0) {

@@ -560,7 +560,9 @@ typedef struct {
   int64_t diag_offset;
 } gmapdp_oligo_result;
 
-/* npositions, mappings: qbytes entries each (indexed like the query arena). */
+/* npositions, mappings: qbytes entries each (indexed like the query arena); mappings are absolute
+ * indexes into `positions`.  Each problem writes its own query slice [qoff, qoff + querylength), so the
+ * problems' slices must be disjoint (GMAPDP_EINVAL otherwise). */
 int gmapdp_oligo_mappings_batch (gmapdp_ctx *ctx, const gmapdp_oligo_problem *problems, int n,
                                  const char *qseq_uc, size_t qbytes, gmapdp_oligo_result *results,
                                  int32_t *npositions, int32_t *mappings, uint32_t *positions,

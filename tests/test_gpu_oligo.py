@@ -94,6 +94,22 @@ def test_gpu_oligo_domain_check(engine):
         engine.oligo_mappings_batch([p])
 
 
+def test_gpu_oligo_batch_refuses_shared_query_slices(engine):
+    """the host-array API writes npositions / mappings per problem at its query slice and makes
+    the mappings absolute per problem; two problems on overlapping slices are refused (GMAPDP_EINVAL)."""
+    rng = random.Random(10)
+    g = random_genome(rng, 20000)
+    engine.set_genome(g)
+    q = bytes(g[3000:3400])
+    p = dict(quc=q, chrstart=100, chrend=8000, chroffset=0, chrhigh=20000, plusp=1, minor=0)
+    probs, qucbuf = gmapdp.Engine.build_oligo_batch([p, p])
+    probs[1]["qoff"] = 200  # overlaps problem 0's [0, 400)
+    with pytest.raises(gmapdp.GmapdpError):
+        engine.oligo_mappings_batch_raw(probs, qucbuf + bytes(200))
+    probs[1]["qoff"] = 400  # disjoint again: accepted
+    engine.oligo_mappings_batch_raw(probs, qucbuf)
+
+
 def _repeat_genome(rng, n):
     """A genome with tandem copies of short units: queries drawn over them put many diagonals past
     suffnconsecutive, which exercises the order of the good list."""

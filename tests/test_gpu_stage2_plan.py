@@ -120,3 +120,28 @@ def test_gpu_stage2_plan_other_query_reports_overflow(engine):
     keep = [i for i in range(len(calls)) if i not in grow]
     bad = stage2_mismatches(res[keep], paths, pairs, exp, index=keep)
     assert not bad, bad[:8]
+
+
+def test_gpu_stage2_plan_other_query_more_distinct_8mers(engine):
+    """a plan sized on reads whose first 1 400 nt are a 9-nt tandem unit (under 1 024 distinct
+    8-mers: the smallest LDS bucket), run on the ordinary reads of the same windows (~1 990 distinct 8-mers,
+    more than the bucket holds): those calls report status -2 (the seeding kernel checks the distinct
+    8-mers against its bucket before writing any per-8-mer counter), the unchanged calls equal the oracle."""
+    g, calls = _repeat_calls(seed=11, reps=(0, 0, 0, 0))
+    engine.set_genome(g)
+    probs, qb, qub = gmapdp.Engine.build_stage2_batch(calls)
+    rng = np.random.default_rng(3)
+    qa = bytearray(qub)
+    shrink = [0, 3, 5]
+    for k in shrink:
+        o = int(probs[k]["qoff"])
+        qa[o:o + 1400] = np.resize(_genome(rng, 9), 1400).tobytes()
+    qa = bytes(qa)
+    orc = Oracle()
+    orc.set_genome(g)
+    exp = oracle_stage2_batch(orc, probs, qub, qub)
+    res, paths, pairs, _ = engine.stage2_plan_raw(probs, qa, qa, run_qbuf=qub, run_qucbuf=qub)
+    assert [int(res[k]["status"]) for k in shrink] == [-2] * len(shrink)
+    keep = [i for i in range(len(calls)) if i not in shrink]
+    bad = stage2_mismatches(res[keep], paths, pairs, exp, index=keep)
+    assert not bad, bad[:8]
