@@ -1137,3 +1137,115 @@ def random_known_flags(rng, p, density=0.03):
 
     out = side(gL, True) + side(gR, False) + side(r + 1, True) + side(r + 1, False)
     return out
+
+
+# ---------------------------------------------------------------------------
+# Whole-batch DP oracle (oracle/dp_batch_oracle.c: orc_dp_batch) and the engine-side canonical form
+# ---------------------------------------------------------------------------
+DP_KINDS = {"single": 0, "end": 1, "genome": 2, "microexon": 3}
+
+
+def oracle_dp_batch(orc, fam, probs, qbuf, qucbuf, nthreads=None):
+    """orc_dp_batch over engine descriptors (gmapdp.PROBLEM_DTYPE / END_ / GENOME_ / MICROEXON_PROBLEM_DTYPE)
+    on the oracle's current genome, MaxEnt from the oracle's restatement (genome gaps, microexons), the
+    oracle's current semantics (orc_set_simd).  Returns (scal (n, 16) int32, dscal (n, 2) float64,
+    pairs (gmapdp.PAIR_DTYPE), pair_off (n + 1))."""
+    import numpy as np
+    import gmapdp
+    _orc_maxent(orc, 0, 0, 0)  # loads the MaxEnt tables once
+    orc._before_call()
+    n = len(probs)
+    r = probs["rlength"].astype(np.int64)
+    if fam in ("single", "end"):
+        cap = r + probs["glength"].astype(np.int64) + 16
+    elif fam == "genome":
+        cap = 2 * r + probs["glengthL"].astype(np.int64) + probs["glengthR"].astype(np.int64) + 16
+    else:
+        cap = r + 16
+    pair_off = np.zeros(n + 1, dtype=np.int64)
+    pair_off[1:] = np.cumsum(np.maximum(cap, 16))
+    scal = np.zeros((n, 16), dtype=np.int32)
+    dscal = np.zeros((n, 2), dtype=np.float64)
+    pairs = np.zeros(int(pair_off[-1]) + 1, dtype=gmapdp.PAIR_DTYPE)
+    f = orc.lib.orc_dp_batch
+    f.restype = C.c_int
+    pr = np.ascontiguousarray(probs)
+    nt = nthreads or min(16, os.cpu_count() or 4)
+    rc = f(C.c_int(DP_KINDS[fam]), C.c_int(n), C.c_void_p(pr.ctypes.data), C.c_char_p(qbuf), C.c_char_p(qucbuf),
+           C.c_void_p(scal.ctypes.data), C.c_void_p(dscal.ctypes.data), C.c_void_p(pairs.ctypes.data),
+           C.c_void_p(pair_off.ctypes.data), C.c_int(nt))
+    assert rc == 0
+    return scal, dscal, pairs, pair_off
+
+
+def _gather(pairs, offs, counts):
+    """records [offs[i], offs[i] + counts[i]) of every problem, concatenated in problem order, and each
+    record's problem index"""
+    import numpy as np
+    counts = np.maximum(counts.astype(np.int64), 0)
+    tot = int(counts.sum())
+    owner = np.repeat(np.arange(len(counts)), counts)
+    start = np.repeat(offs.astype(np.int64), counts)
+    first = np.repeat(np.cumsum(counts) - counts, counts)
+    return pairs[start + (np.arange(tot) - first)], owner
+
+
+def _canon_pairs(recs, keep_holder_comp):
+    """gap holders (querypos = genomepos = -1): only the jump (and, for microexons, comp '<' / '>') is part
+    of the reference's Pair_T the callers read; the other characters are zeroed on both sides"""
+    import numpy as np
+    v = recs.copy()
+    hold = (v["querypos"] == -1) & (v["genomepos"] == -1)
+    for k in ("cdna", "genome", "genomealt") + (() if keep_holder_comp else ("comp",)):
+        v[k][hold] = b"\0"
+    return v
+
+
+def dp_batch_mismatches(fam, res, pairs, orc_out):
+    """Problems whose engine outputs (plan / batch results in problem order; `pairs` the engine's pair
+    arena) differ from oracle_dp_batch's.  Returns [(problem, what)] (at most 64)."""
+    import numpy as np
+    scal, dscal, opairs, pair_off = orc_out
+    n = len(res)
+    bad = {}
+
+    def flag(mask, what):
+        for i in np.nonzero(mask)[0][:64]:
+            bad.setdefault(int(i), what)
+
+    flag(scal[:, 0] < -1, "oracle error")
+    flag(scal[:, 15] != 0, "oracle record the engine format cannot express")
+    onp = scal[:, 0].astype(np.int64)
+    if fam == "microexon":
+        enp = res["npairs"].astype(np.int64)
+        flag(enp != onp, "npairs")
+        flag(res["dynprogindex"] != scal[:, 1], "dynprogindex")
+        flag(res["microintrontype"] != scal[:, 2], "microintrontype")
+        flag(res["bestprob2"].view(np.int64) != dscal[:, 0].view(np.int64), "bestprob2")
+        flag(res["bestprob3"].view(np.int64) != dscal[:, 1].view(np.int64), "bestprob3")
+    else:
+        onp = np.maximum(onp, 0)  # the engine's NULL list is npairs 0
+        enp = res["npairs"].astype(np.int64)
+        flag(enp != onp, "npairs")
+        names = ["dynprogindex", "traceback_score", "nmatches", "nmismatches", "nopens", "nindels"]
+        if fam == "genome":
+            names += ["new_leftgenomepos", "new_rightgenomepos", "exonhead", "introntype"]
+        for k, nm in enumerate(names):
+            flag(res[nm] != scal[:, 1 + k], nm)
+        if fam == "genome":
+            live = enp > 0
+            flag(res["left_prob"].view(np.int64) != dscal[:, 0].view(np.int64), "left_prob")
+            flag(res["right_prob"].view(np.int64) != dscal[:, 1].view(np.int64), "right_prob")
+            # the intron gap holder's queryjump (every other holder has none)
+            flag(live & (scal[:, 14] > 1), "two holders with a queryjump")
+            eq = np.where(res["gap_index"] >= 0, res["gap_queryjump"], 0)
+            eg = np.where(eq != 0, res["gap_index"], -1)
+            flag(live & ((eg != scal[:, 12]) | (eq != scal[:, 13])), "gap holder queryjump")
+    same = enp == onp
+    cnt = np.where(same & (onp > 0), onp, 0)
+    e, owner = _gather(pairs, res["pair_offset"], cnt)
+    o, _ = _gather(opairs, pair_off[:-1], cnt)
+    hc = fam == "microexon"
+    diff = _canon_pairs(e, hc) != _canon_pairs(o, hc)
+    flag(np.bincount(owner[diff], minlength=n) > 0 if diff.any() else np.zeros(n, dtype=bool), "pair records")
+    return sorted(bad.items())[:64]

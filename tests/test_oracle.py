@@ -555,3 +555,62 @@ def test_oracle_splicejunction_vs_reference_random(oracle):
            for p in [splicejunction_problem(rng, g, edge=(i % 6 == 0))]
            if ref.end_splicejunction(p) != oracle.end_splicejunction(p)]
     assert bad == []
+
+
+@pytest.mark.parametrize("simd", [False, True])
+def test_oracle_dp_batch_matches_single_calls(simd):
+    """orc_dp_batch (the whole-block checker of tests/test_gpu_bench_workload.py: a thread pool over engine
+    descriptors, the engine's 16-B pair records, MaxEnt from the oracle's restatement) gives, call by call,
+    what the per-call oracle gives (dpbind's call_single / call_end / genome_gap with oracle_splice_probs /
+    microexon_int with microexon_probs), for every DP family."""
+    import numpy as np
+    import gmapdp
+    from dpbind import (call_end, call_single, end_gap_problem, genome_gap_problem, microexon_probs,
+                        microexon_problem, oracle_dp_batch, oracle_splice_probs, random_genome, single_gap_problem)
+    rng = random.Random(606)
+    orc = Oracle(simd=simd)
+    g = bytearray(random_genome(rng, 400000))
+    calls = {"single": [single_gap_problem(rng, bytes(g)) for _ in range(150)],
+             "end": [end_gap_problem(rng, bytes(g), edge=(i % 4 == 0)) for i in range(150)]}
+    calls["genome"] = [genome_gap_problem(rng, g, edge=(i % 4 == 0)) for i in range(120)]
+    at = [100]
+    calls["microexon"] = [microexon_problem(rng, g, edge=(i % 4 == 0), at=at) for i in range(80)]
+    g = bytes(g)
+    orc.set_genome(g)
+    exp = {"single": [call_single(orc, c) for c in calls["single"]],
+           "end": [call_end(orc, c) for c in calls["end"]],
+           "genome": [orc.genome_gap(c, *oracle_splice_probs(orc, c)) for c in calls["genome"]],
+           "microexon": [orc.microexon_int(c, microexon_probs(orc, orc.microexon_candidates(c) or [], c["chroffset"]))
+                         for c in calls["microexon"]]}
+    E = gmapdp.Engine
+    built = {"single": E.build_single_batch(calls["single"]), "end": E.build_end_batch(calls["end"]),
+             "genome": gmapdp.build_genome_batch(calls["genome"])[:3],
+             "microexon": E.build_microexon_batch(calls["microexon"])}
+    for fam, (probs, qb, qub) in built.items():
+        if simd and fam == "microexon":  # one semantics (no SIMD build variant)
+            continue
+        scal, dscal, pairs, off = oracle_dp_batch(orc, fam, probs, qb, qub, nthreads=4)
+        for i, e in enumerate(exp[fam]):
+            lst = e[-1]
+            n = max(int(scal[i, 0]), -1)  # (-3: a SIMD end gap outside the domain, None per call)
+            assert n == (-1 if lst is None else len(lst)), (fam, i)
+            if fam == "microexon":
+                assert tuple(scal[i, 1:3]) == tuple(e[0]) and tuple(dscal[i]) == tuple(e[1]), (fam, i)
+            else:
+                k = 6 if fam != "genome" else 10
+                assert tuple(int(x) for x in scal[i, 1:1 + k]) == tuple(e[0][:k]), (fam, i)
+                if fam == "genome":
+                    assert tuple(dscal[i]) == tuple(e[0][10:12]), (fam, i)
+            assert scal[i, 15] == 0, (fam, i)
+            for k, x in enumerate(lst or []):
+                r = pairs[int(off[i]) + k]
+                if x[9]:  # gap holder: the genomejump, and the queryjump of the intron's holder
+                    assert (int(r["querypos"]), int(r["genomepos"]), int(r["jump"])) == (-1, -1, x[3]), (fam, i, k)
+                    if x[2]:
+                        assert (int(scal[i, 12]), int(scal[i, 13])) == (k, x[2]), (fam, i, k)
+                    if fam == "microexon":
+                        assert r["comp"] == x[6], (fam, i, k)
+                else:
+                    got = (int(r["querypos"]), int(r["genomepos"]), 0, 0, x[4], r["cdna"], r["comp"], r["genome"],
+                           r["genomealt"], 0)
+                    assert got == x, (fam, i, k)
