@@ -4,11 +4,13 @@ Workload (gmap-2024_amd/gmapdp/workload.py):
   * configs[2] (default; "1M synthetic 2-kb cDNA (5 exons, 2 % mismatch) vs GRCh38, 1xMI355X, full stage2 +
     all Dynprog_* paths"): an i.i.d. ACGT genome laid out as GRCh38's 24 primary chromosomes (3.09 Gnt,
     universal coordinates past 2^31), generated directly as the reference's .genomecomp blocks and resident
-    in HBM (1.16 GB); per 2-kb read the calls GMAP's pipeline makes into the path: one
-    Stage2_compute call (gmap.c:1208: Oligoindex_hr_tally + Oligoindex_get_mappings over the read's
-    gregion, then the chaining -- Diag_compute_bounds, align_compute_lookback, convert_to_nucleotides,
-    Stage2_filter_unique) and 43.7 Dynprog_single_gap + 7.1 Dynprog_end5_gap + 6.5 Dynprog_end3_gap +
-    49.4 Dynprog_genome_gap + 25.6 Dynprog_microexon_int;
+    in HBM (1.16 GB); per 2-kb read the calls GMAP's own program makes into the path, measured with the
+    reference `gmap -d` over a gmap_build index (tools/callmix.py --index, profiles/r04_callmix/callmix_d.json;
+    workload.CDNA2K): 1.585 Stage2_compute calls (gmap.c:1208: Oligoindex_hr_tally + Oligoindex_get_mappings
+    over the read's locus +- 100 kb, gregion.c:899, then the chaining -- Diag_compute_bounds,
+    align_compute_lookback, convert_to_nucleotides, Stage2_filter_unique) and 21.1 Dynprog_single_gap +
+    6.78 Dynprog_end5_gap + 6.38 Dynprog_end3_gap + 49.7 Dynprog_genome_gap + 7.53 Dynprog_microexon_int
+    (`--mix appb`: SURVEY App. B's mix of rounds 1-3);
   * configs[4] (--config 4; gmapl, "500k 5-kb Iso-Seq-style reads vs 17-Gb wheat genome"): 5-kb reads of
     10 exons with 1 % substitutions + 1 % indels against a 17-Gnt wheat-layout genome (6.4 GB packed,
     universal coordinates past 2^32), the per-read call mix of that read shape (workload.ISOSEQ5K).

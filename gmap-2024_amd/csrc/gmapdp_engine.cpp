@@ -13,12 +13,14 @@
 #include <time.h>
 
 #include <algorithm>
+#include <climits>
 #include <cctype>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -98,6 +100,10 @@ hipError_t launch_oi(bool wide, int nproblems, size_t lds, hipStream_t stream, c
                      int32_t* npos, int32_t* map, uint32_t* table, int32_t* diags, uint64_t* pool,
                      unsigned long long* pool_counter, unsigned long long pool_cap, int32_t* nhits_out);
 size_t scratch_bytes_oi_hits(int querylength, size_t hitcap);
+hipError_t launch_oi_split(int nproblems, int umax, hipStream_t stream, const DevOligoProblem* probs,
+                           const uint32_t* blocks, const char* quc, unsigned char* scratch,
+                           gmapdp_oligo_result* results, int32_t* npos, int32_t* map, uint32_t* table, int32_t* diags,
+                           uint64_t* pool, unsigned long long* pool_counter, unsigned long long pool_cap);
 hipError_t launch_mx_search(int n, hipStream_t s, const gmapdp_microexon_problem* probs, const uint32_t* blocks,
                             uint64_t nwords, const char* qseq, const char* qseq_uc, gmapdp_microexon_result* results,
                             gmapdp_microexon_candidate* cands, unsigned long long cap, unsigned long long* counter,
@@ -837,9 +843,13 @@ static int convert_single(const gmapdp_ctx* ctx, const gmapdp_single_problem& p,
 }
 
 // Dynprog_end5_gap / Dynprog_end3_gap prologues (dynprog_end.c:1333-1411 / 1962-2027).
-static int convert_end(gmapdp_ctx* ctx, const gmapdp_end_problem& p, gmapdp_result& res, DevProblem& d,
-                       int* err) {
+static int convert_end(const gmapdp_ctx* ctx, const gmapdp_end_problem& p, gmapdp_result& res, DevProblem& d,
+                       int* err, const char** why) {
   *err = 0;
+  auto bad = [why](const gmapdp_ctx*, const char* msg) {
+    *why = msg;
+    return GMAPDP_EINVAL;
+  };
   const bool end3 = p.end3p != 0;
   const bool nogaps = p.endalign == kQueryendNogaps;
   if (p.endalign < 0 || p.endalign > 3) {
@@ -925,9 +935,13 @@ static int convert_end(gmapdp_ctx* ctx, const gmapdp_end_problem& p, gmapdp_resu
 }
 
 // Dynprog_genome_gap prologue (dynprog_genome.c:3351-3470): returns 1 if the problem runs on the GPU.
-static int convert_genome(gmapdp_ctx* ctx, const gmapdp_genome_problem& p, gmapdp_genome_result& res,
-                          DevGenomeProblem& d, int* err) {
+static int convert_genome(const gmapdp_ctx* ctx, const gmapdp_genome_problem& p, gmapdp_genome_result& res,
+                          DevGenomeProblem& d, int* err, const char** why) {
   *err = 0;
+  auto bad = [why](const gmapdp_ctx*, const char* msg) {
+    *why = msg;
+    return GMAPDP_EINVAL;
+  };
   res.npairs = 0;
   res.pair_offset = 0;
   res.nmatches = res.nmismatches = res.nopens = res.nindels = 0;
@@ -1016,126 +1030,285 @@ static int convert_genome(gmapdp_ctx* ctx, const gmapdp_genome_problem& p, gmapd
   return 1;
 }
 
+// GMAPDP_PLAN_TIMING=1: the plan builders print their phase times (ms) to stderr (tools, not the product)
+struct PlanTimer {
+  const char* what;
+  bool on;
+  struct timespec t0;
+  std::string line;
+  explicit PlanTimer(const char* w) : what(w), on(getenv("GMAPDP_PLAN_TIMING") != nullptr) {
+    if (on) clock_gettime(CLOCK_MONOTONIC, &t0);
+  }
+  void mark(const char* phase) {
+    if (!on) return;
+    struct timespec t1;
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    char b[96];
+    std::snprintf(b, sizeof(b), " %s=%.1f", phase, (t1.tv_sec - t0.tv_sec) * 1e3 + (t1.tv_nsec - t0.tv_nsec) * 1e-6);
+    line += b;
+    t0 = t1;
+  }
+  ~PlanTimer() {
+    if (on) std::fprintf(stderr, "[gmapdp plan timing] %s%s\n", what, line.c_str());
+  }
+};
+
+// ---- host threads of a plan build ----
+// A batch of kPlanParallelMin problems or more (bench.py's 10 000-read blocks: ~840 000) is planned on
+// GMAPDP_PLAN_THREADS host threads (default: min(16, hardware threads); a GPU-box job is given 16 cores);
+// smaller batches (the drop-in's dispatcher batches) on the calling thread.  The plan is the same either
+// way: per-problem work is independent, offsets are prefix sums taken in problem order, classes keep
+// their members in problem order and sort them stably.
+static const size_t kPlanParallelMin = 16384;
+static int plan_threads(size_t n) {
+  static const int v = [] {
+    const char* e = getenv("GMAPDP_PLAN_THREADS");
+    int t = e ? atoi(e) : 0;
+    if (t <= 0) t = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    return t;
+  }();
+  return n >= kPlanParallelMin ? v : 1;
+}
+// f(begin, end, t) over T contiguous chunks of [0, n), chunk 0 on the calling thread
+template <typename F>
+static void plan_parallel(size_t n, int T, F&& f) {
+  if (T <= 1 || n < 2) {
+    f((size_t)0, n, 0);
+    return;
+  }
+  const size_t per = (n + (size_t)T - 1) / (size_t)T;
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; t++) {
+    const size_t lo = (size_t)t * per, hi = std::min(n, lo + per);
+    if (lo < hi) th.emplace_back([&f, lo, hi, t] { f(lo, hi, t); });
+  }
+  f((size_t)0, std::min(n, per), 0);
+  for (auto& x : th) x.join();
+}
+// stable sort of ids by `before` (a strict weak order): T sorted runs, then pairwise stable merges
+template <typename C>
+static void plan_stable_sort(std::vector<int>& ids, int T, C before) {
+  if (T <= 1 || ids.size() < 65536) {
+    std::stable_sort(ids.begin(), ids.end(), before);
+    return;
+  }
+  const size_t n = ids.size(), per = (n + (size_t)T - 1) / (size_t)T;
+  std::vector<size_t> cut;
+  for (size_t x = 0; x < n; x += per) cut.push_back(x);
+  cut.push_back(n);
+  plan_parallel(cut.size() - 1, (int)cut.size() - 1, [&](size_t lo, size_t hi, int) {
+    for (size_t r = lo; r < hi; r++) std::stable_sort(ids.begin() + cut[r], ids.begin() + cut[r + 1], before);
+  });
+  std::vector<int> tmp(n);
+  while (cut.size() > 2) {
+    const size_t pairs = (cut.size() - 1) / 2;
+    std::vector<size_t> next;
+    plan_parallel(pairs, (int)pairs, [&](size_t lo, size_t hi, int) {
+      for (size_t q = lo; q < hi; q++)
+        std::merge(ids.begin() + cut[2 * q], ids.begin() + cut[2 * q + 1], ids.begin() + cut[2 * q + 1],
+                   ids.begin() + cut[2 * q + 2], tmp.begin() + cut[2 * q], before);
+    });
+    for (size_t q = 0; q < pairs; q++) {
+      std::copy(tmp.begin() + cut[2 * q], tmp.begin() + cut[2 * q + 2], ids.begin() + cut[2 * q]);
+      next.push_back(cut[2 * q]);
+    }
+    if ((cut.size() - 1) % 2) next.push_back(cut[cut.size() - 2]);
+    next.push_back(n);
+    cut.swap(next);
+  }
+}
+
+// a launch class key ordered as the tuple (kind, R, dirs in LDS, LDS bucket)
+static uint64_t class_key(int kind, int R, int dl, size_t bucket) {
+  return ((uint64_t)kind << 48) | ((uint64_t)R << 32) | ((uint64_t)(dl ? 1 : 0) << 31) | (uint64_t)bucket;
+}
+struct ClassOf {
+  uint64_t key = 0;
+  size_t need = 0;      // the problem's LDS bucket (a latency-mode class takes its largest member's)
+  size_t pair = 0;      // pair-arena records reserved
+  size_t gdirs = 0;     // bytes of the global direction scratch, 0: none
+  const char* err = nullptr;
+};
+
+// one single / end gap's launch class (classify's rules)
+static ClassOf classify_dev(DevProblem& d, bool latency) {
+  ClassOf c;
+  c.pair = (size_t)d.rlength + (size_t)d.glength + 2;
+  d.dirs_offset = 0;
+  const bool nofill = d.kind != kSingle && d.endalign == kQueryendNogaps;
+  if ((d.flags & kFSimd) && d.kind != kSingle) {
+    // Dynprog_end5/3_gap of the SIMD builds (dynprog_end.c:1406 / 2027): 8-bit triangles when
+    // either length is below use8p_size[ENDQ]
+    const int B = (d.rlength < kUse8pSize[kEndQ] || d.glength < kUse8pSize[kEndQ]) ? 32 : 16;
+    const size_t lds = lds_bytes_uxe(d.rlength, d.glength, B);
+    if (lds > 160 * 1024) { c.err = "problem exceeds the LDS of a CU"; return c; }
+    c.gdirs = (scratch_bytes_uxe(d.rlength, d.glength, d.lband, d.uband, B) + 255) & ~(size_t)255;
+    c.need = gg_lds_bucket(lds);
+    c.key = class_key((int)PlanCore::kUxe, B, 0, latency ? 0 : c.need);
+    return c;
+  }
+  if (d.flags & kFSimd) {
+    // Dynprog_single_gap of the SIMD builds (dynprog_single.c:593-631): 8-bit blocks of 32 rows when
+    // both lengths are below use8p_size (dynprog.c:1022-1025), else 16-bit blocks of 16 rows
+    static const int use8p[4] = {41, 63, 127, 24};
+    const int B = (d.rlength < use8p[d.mismatchtype] && d.glength < use8p[d.mismatchtype]) ? 32 : 16;
+    const size_t slot = gg_lds_bucket(lds_slot_sx(d.rlength, d.glength, B));
+    if (slot * (64 / B) > 160 * 1024) { c.err = "problem exceeds the LDS of a CU"; return c; }
+    c.need = slot;
+    c.key = class_key((int)PlanCore::kSx, B, 0, latency ? 0 : slot);
+    return c;
+  }
+  if (d.open > 0 && !nofill) { c.err = "positive gap-open penalty is not supported by the scan formulation"; return c; }
+  if (d.lband < 0 || d.uband < 0) { c.err = "negative band"; return c; }
+  const int W = d.lband + d.uband + 1;
+  if (!latency && (nofill || W <= 32)) {  // narrow band: pack 64/S problems per wave
+    const int S = (nofill || W <= 16) ? 16 : 32;
+    const size_t slot = slot_bucket(lds_slot_dpx(d.rlength, d.glength));
+    if (slot && slot * (64 / S) + lds_dirs_dpx(d.glength) <= kLdsBudget) {
+      c.need = slot;
+      c.key = class_key((int)PlanCore::kDpx, S, 1, slot);
+      return c;
+    }
+  }
+  int R = nofill ? 1 : pick_R(W);
+  if (R > kMaxR) { c.err = "band wider than 4096"; return c; }
+  // a band wider than the query: lanes over the query's rows cost fewer words per column
+  const int Rrows = pick_R(d.rlength + 1);
+  const bool rows = !nofill && Rrows < R && !rows_disabled();
+  if (rows) R = Rrows;
+  size_t lds = lds_bytes_dp(d.rlength, d.glength, R, !nofill);
+  const bool dirs_lds = !nofill && lds <= kLdsBudget;
+  if (!dirs_lds) {
+    lds = lds_bytes_dp(d.rlength, d.glength, R, false);
+    if (!nofill) c.gdirs = ((size_t)(d.glength + 1) * 4 * R * 8 + 255) & ~(size_t)255;
+  }
+  if (lds > 160 * 1024) { c.err = "problem exceeds the LDS of a CU"; return c; }
+  c.need = lds_bucket(lds);
+  c.key = class_key((int)(rows ? PlanCore::kDpRows : PlanCore::kDp), R, dirs_lds ? 1 : 0, latency ? 0 : c.need);
+  return c;
+}
+
+// one genome gap's launch class
+static ClassOf classify_gdev(DevGenomeProblem& d, bool latency, size_t lds_dirs_max) {
+  ClassOf c;
+  // traceback R (<= r + gR records) + gap holder + traceback L (<= r + gL records)
+  c.pair = 2 * (size_t)d.rlength + (size_t)d.glengthL + (size_t)d.glengthR + 4;
+  if (d.flags & kGSimd) {
+    // the SIMD builds' genome gap (dynprog_genome.c:3501-3507): 8-bit triangles when rlength, or
+    // both glengths, are below use8p_size
+    const int u = kUse8pSize[d.mismatchtype];
+    const int B = (d.rlength < u || (d.glengthL < u && d.glengthR < u)) ? 32 : 16;
+    const size_t lds = lds_bytes_uxg(d.rlength, d.glengthL, d.glengthR, B);
+    if (lds > 160 * 1024) { c.err = "problem exceeds the LDS of a CU"; return c; }
+    c.gdirs = (scratch_bytes_uxg(d.rlength, d.glengthL, d.glengthR, d.lbandL, B) + 255) & ~(size_t)255;
+    c.need = gg_lds_bucket(lds);
+    c.key = class_key((int)PlanCore::kUxg, B, 0, latency ? 0 : c.need);
+    return c;
+  }
+  if (d.open > 0) { c.err = "positive gap-open penalty is not supported by the scan formulation"; return c; }
+  const int WL = d.lbandL + d.ubandL + 1, WR = d.lbandL + d.ubandR + 1;
+  const int R = pick_R(std::max(WL, WR));
+  if (R > kMaxR) { c.err = "band wider than 4096"; return c; }
+  size_t lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, true, std::max(WL, WR));
+  const bool dirs_lds = lds <= lds_dirs_max;
+  if (!dirs_lds) lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, false, std::max(WL, WR));
+  // bridge candidates (+ direction planes) in global scratch
+  c.gdirs = (scratch_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, dirs_lds) + 255) & ~(size_t)255;
+  if (lds > 160 * 1024) { c.err = "problem exceeds the LDS of a CU"; return c; }
+  c.need = gg_lds_bucket(lds);
+  c.key = class_key((int)PlanCore::kGenomeGap, R, dirs_lds ? 1 : 0, latency ? 0 : c.need);
+  return c;
+}
+
 static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
   const size_t lds_dirs_max = gg_lds_dirs_max();  // read once per plan, not per genome-gap problem
-  std::map<std::tuple<int, int, int, size_t>, std::vector<int>> classes;  // (kind, R, dirs_lds, lds bucket)
-  size_t pair_off = 0, gdirs_off = 0;
+  const size_t nd = plan.dev.size(), ng = plan.gdev.size();
+  const int T = plan_threads(nd + ng);
   // Latency mode (small batches: the GMAP drop-in's dispatcher batches): one launch class per (kind, R,
   // direction placement) with the LDS of its largest member, and no packed narrow-band kernels, so a
   // batch is a few launches whose latencies do not add up class after class.
-  const bool latency = plan.dev.size() + plan.gdev.size() <= latency_batch();
-  std::vector<size_t> need(plan.dev.size(), 0), gneed(plan.gdev.size(), 0);
-  auto add = [&](int kind, int R, int dl, size_t bucket, size_t s) {
-    need[s] = bucket;
-    classes[std::make_tuple(kind, R, dl, latency ? (size_t)0 : bucket)].push_back((int)s);
-  };
-  auto gadd = [&](int kind, int R, int dl, size_t bucket, size_t s) {
-    gneed[s] = bucket;
-    classes[std::make_tuple(kind, R, dl, latency ? (size_t)0 : bucket)].push_back((int)s);
-  };
-  for (size_t s = 0; s < plan.dev.size(); s++) {
-    DevProblem& d = plan.dev[s];
-    d.pair_offset = (int32_t)pair_off;
-    pair_off += (size_t)d.rlength + (size_t)d.glength + 2;
-    const bool nofill = d.kind != kSingle && d.endalign == kQueryendNogaps;
-    if ((d.flags & kFSimd) && d.kind != kSingle) {
-      // Dynprog_end5/3_gap of the SIMD builds (dynprog_end.c:1406 / 2027): 8-bit triangles when
-      // either length is below use8p_size[ENDQ]
-      const int B = (d.rlength < kUse8pSize[kEndQ] || d.glength < kUse8pSize[kEndQ]) ? 32 : 16;
-      const size_t lds = lds_bytes_uxe(d.rlength, d.glength, B);
-      if (lds > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
-      d.dirs_offset = (int64_t)gdirs_off;
-      gdirs_off += (scratch_bytes_uxe(d.rlength, d.glength, d.lband, d.uband, B) + 255) & ~(size_t)255;
-      add((int)PlanCore::kUxe, B, 0, gg_lds_bucket(lds), s);
-      continue;
+  const bool latency = nd + ng <= latency_batch();
+  // per problem (threads): its class; slots 0..nd-1 single / end gaps, nd.. genome gaps
+  std::vector<ClassOf> cls(nd + ng);
+  plan_parallel(nd + ng, T, [&](size_t lo, size_t hi, int) {
+    for (size_t s = lo; s < hi; s++)
+      cls[s] = s < nd ? classify_dev(plan.dev[s], latency) : classify_gdev(plan.gdev[s - nd], latency, lds_dirs_max);
+  });
+  for (size_t s = 0; s < nd + ng; s++)  // the first problem in batch order that the engine rejects
+    if (cls[s].err) return bad(ctx, cls[s].err);
+  // pair-arena and direction-scratch offsets in problem order (single / end gaps, then genome gaps)
+  size_t pair_off = 0, gdirs_off = 0;
+  for (size_t s = 0; s < nd + ng; s++) {
+    const ClassOf& c = cls[s];
+    if (s < nd) {
+      plan.dev[s].pair_offset = (int32_t)pair_off;
+      if (c.gdirs) plan.dev[s].dirs_offset = (int64_t)gdirs_off;
+    } else {
+      plan.gdev[s - nd].pair_offset = (int32_t)pair_off;
+      plan.gdev[s - nd].dirs_offset = (int64_t)gdirs_off;
     }
-    if (d.flags & kFSimd) {
-      // Dynprog_single_gap of the SIMD builds (dynprog_single.c:593-631): 8-bit blocks of 32 rows when
-      // both lengths are below use8p_size (dynprog.c:1022-1025), else 16-bit blocks of 16 rows
-      static const int use8p[4] = {41, 63, 127, 24};
-      const int B = (d.rlength < use8p[d.mismatchtype] && d.glength < use8p[d.mismatchtype]) ? 32 : 16;
-      const size_t slot = gg_lds_bucket(lds_slot_sx(d.rlength, d.glength, B));
-      if (slot * (64 / B) > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
-      add((int)PlanCore::kSx, B, 0, slot, s);
-      continue;
-    }
-    if (d.open > 0 && !nofill) return bad(ctx, "positive gap-open penalty is not supported by the scan formulation");
-    if (d.lband < 0 || d.uband < 0) return bad(ctx, "negative band");
-    const int W = d.lband + d.uband + 1;
-    d.dirs_offset = 0;
-    if (!latency && (nofill || W <= 32)) {  // narrow band: pack 64/S problems per wave
-      const int S = (nofill || W <= 16) ? 16 : 32;
-      const size_t slot = slot_bucket(lds_slot_dpx(d.rlength, d.glength));
-      if (slot && slot * (64 / S) + lds_dirs_dpx(d.glength) <= kLdsBudget) {
-        add((int)PlanCore::kDpx, S, 1, slot, s);
-        continue;
-      }
-    }
-    int R = nofill ? 1 : pick_R(W);
-    if (R > kMaxR) return bad(ctx, "band wider than 4096");
-    // a band wider than the query: lanes over the query's rows cost fewer words per column
-    const int Rrows = pick_R(d.rlength + 1);
-    const bool rows = !nofill && Rrows < R && !rows_disabled();
-    if (rows) R = Rrows;
-    size_t lds = lds_bytes_dp(d.rlength, d.glength, R, !nofill);
-    bool dirs_lds = !nofill && lds <= kLdsBudget;
-    d.dirs_offset = 0;
-    if (!dirs_lds) {
-      lds = lds_bytes_dp(d.rlength, d.glength, R, false);
-      if (!nofill) {
-        d.dirs_offset = (int64_t)gdirs_off;
-        gdirs_off += ((size_t)(d.glength + 1) * 4 * R * 8 + 255) & ~(size_t)255;
-      }
-    }
-    if (lds > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
-    add((int)(rows ? PlanCore::kDpRows : PlanCore::kDp), R, dirs_lds ? 1 : 0, lds_bucket(lds), s);
+    pair_off += c.pair;
+    gdirs_off += c.gdirs;
   }
-  for (size_t s = 0; s < plan.gdev.size(); s++) {
-    DevGenomeProblem& d = plan.gdev[s];
-    d.pair_offset = (int32_t)pair_off;
-    // traceback R (<= r + gR records) + gap holder + traceback L (<= r + gL records)
-    pair_off += 2 * (size_t)d.rlength + (size_t)d.glengthL + (size_t)d.glengthR + 4;
-    if (d.flags & kGSimd) {
-      // the SIMD builds' genome gap (dynprog_genome.c:3501-3507): 8-bit triangles when rlength, or
-      // both glengths, are below use8p_size
-      const int u = kUse8pSize[d.mismatchtype];
-      const int B = (d.rlength < u || (d.glengthL < u && d.glengthR < u)) ? 32 : 16;
-      const size_t lds = lds_bytes_uxg(d.rlength, d.glengthL, d.glengthR, B);
-      if (lds > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
-      d.dirs_offset = (int64_t)gdirs_off;
-      gdirs_off += (scratch_bytes_uxg(d.rlength, d.glengthL, d.glengthR, d.lbandL, B) + 255) & ~(size_t)255;
-      gadd((int)PlanCore::kUxg, B, 0, gg_lds_bucket(lds), s);
-      continue;
-    }
-    if (d.open > 0) return bad(ctx, "positive gap-open penalty is not supported by the scan formulation");
-    const int WL = d.lbandL + d.ubandL + 1, WR = d.lbandL + d.ubandR + 1;
-    const int R = pick_R(std::max(WL, WR));
-    if (R > kMaxR) return bad(ctx, "band wider than 4096");
-    size_t lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, true, std::max(WL, WR));
-    const bool dirs_lds = lds <= lds_dirs_max;
-    if (!dirs_lds) lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, false, std::max(WL, WR));
-    d.dirs_offset = (int64_t)gdirs_off;  // bridge candidates (+ direction planes) in global scratch
-    gdirs_off += (scratch_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, dirs_lds) + 255) & ~(size_t)255;
-    if (lds > 160 * 1024) return bad(ctx, "problem exceeds the LDS of a CU");
-    gadd((int)PlanCore::kGenomeGap, R, dirs_lds ? 1 : 0, gg_lds_bucket(lds), s);
+  // members per class in problem order (the classes in key order, as the tuple map kept them)
+  std::vector<uint64_t> keys;
+  {
+    std::vector<std::vector<uint64_t>> tk(T);
+    plan_parallel(nd + ng, T, [&](size_t lo, size_t hi, int t) {
+      uint64_t last = ~0ull;
+      for (size_t s = lo; s < hi; s++)
+        if (cls[s].key != last) {
+          last = cls[s].key;
+          if (std::find(tk[t].begin(), tk[t].end(), last) == tk[t].end()) tk[t].push_back(last);
+        }
+    });
+    for (auto& v : tk) keys.insert(keys.end(), v.begin(), v.end());
+    std::sort(keys.begin(), keys.end());
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
   }
-  for (auto& kv : classes) {
+  const size_t K = keys.size();
+  auto class_index = [&](uint64_t k) { return (size_t)(std::lower_bound(keys.begin(), keys.end(), k) - keys.begin()); };
+  std::vector<std::vector<int>> members(K);
+  {
+    std::vector<std::vector<size_t>> cnt(T, std::vector<size_t>(K, 0));
+    std::vector<uint32_t> ci(nd + ng);
+    plan_parallel(nd + ng, T, [&](size_t lo, size_t hi, int t) {
+      for (size_t s = lo; s < hi; s++) {
+        ci[s] = (uint32_t)class_index(cls[s].key);
+        cnt[t][ci[s]]++;
+      }
+    });
+    std::vector<std::vector<size_t>> at(T, std::vector<size_t>(K, 0));
+    for (size_t k = 0; k < K; k++) {
+      size_t run = 0;
+      for (int t = 0; t < T; t++) {
+        at[t][k] = run;
+        run += cnt[t][k];
+      }
+      members[k].resize(run);
+    }
+    plan_parallel(nd + ng, T, [&](size_t lo, size_t hi, int t) {
+      for (size_t s = lo; s < hi; s++) members[ci[s]][at[t][ci[s]]++] = (int)(s < nd ? s : s - nd);
+    });
+  }
+  for (size_t k = 0; k < K; k++) {
     PlanCore::Launch L;
-    L.kind = std::get<0>(kv.first);
-    L.R = std::get<1>(kv.first);
-    L.dirs_lds = std::get<2>(kv.first) != 0;
-    L.lds = std::get<3>(kv.first);
-    L.count = (int)kv.second.size();
-    // longest problems first, so the tail of the launch is short work
-    std::vector<int> ids = kv.second;
+    const uint64_t key = keys[k];
+    L.kind = (int)(key >> 48);
+    L.R = (int)((key >> 32) & 0xFFFF);
+    L.dirs_lds = ((key >> 31) & 1) != 0;
+    L.lds = (size_t)(key & 0x7FFFFFFFull);
+    std::vector<int>& ids = members[k];
+    L.count = (int)ids.size();
+    const bool g = L.kind == PlanCore::kGenomeGap || L.kind == PlanCore::kUxg;
     if (latency) {  // the class's LDS: its largest member's
-      const bool g = L.kind == PlanCore::kGenomeGap || L.kind == PlanCore::kUxg;
       size_t m = 0;
-      for (int id : ids) m = std::max(m, g ? gneed[id] : need[id]);
+      for (int id : ids) m = std::max(m, cls[g ? nd + (size_t)id : (size_t)id].need);
       L.lds = m;
     }
-    if (L.kind != PlanCore::kGenomeGap && L.kind != PlanCore::kUxg) {
-      std::stable_sort(ids.begin(), ids.end(), [&](int a, int b) {
+    // longest problems first, so the tail of the launch is short work
+    if (!g) {
+      plan_stable_sort(ids, T, [&](int a, int b) {
         return (size_t)plan.dev[a].glength * (plan.dev[a].lband + plan.dev[a].uband + 1) >
                (size_t)plan.dev[b].glength * (plan.dev[b].lband + plan.dev[b].uband + 1);
       });
@@ -1146,7 +1319,7 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
         const DevGenomeProblem& d = plan.gdev[a];
         return (size_t)(d.glengthL + d.glengthR) * (size_t)(2 * d.lbandL + d.ubandL + d.ubandR + 2);
       };
-      std::stable_sort(ids.begin(), ids.end(), [&](int a, int b) { return work(a) > work(b); });
+      plan_stable_sort(ids, T, [&](int a, int b) { return work(a) > work(b); });
       L.first = (int)plan.gorder.size();
       plan.gorder.insert(plan.gorder.end(), ids.begin(), ids.end());
     }
@@ -1236,38 +1409,105 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
   return GMAPDP_OK;
 }
 
-// Results: singles first, then ends (host_results); genome-gap results separately.
+// Results: singles first, then ends (host_results); genome-gap results separately.  The per-problem
+// prologues (penalties, size guards, bands, segment bounds) run on plan_threads() host threads; the GPU
+// problems are then compacted in problem order.
 static int build_plan(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int nsingle,
                       const gmapdp_end_problem* ends, int nend, const gmapdp_genome_problem* genomes, int ngenome,
                       gmapdp_result* results, gmapdp_genome_result* gresults, PlanCore& plan) {
   plan = PlanCore();
+  PlanTimer tm("build_plan");
   const int n = nsingle + nend;
-  plan.dev_index.assign(n, -1);
-  for (int i = 0; i < n; i++) {
-    DevProblem d;
-    int gpu, err = 0;
-    if (i < nsingle) gpu = convert_single(ctx, singles[i], results[i], d);
-    else gpu = convert_end(ctx, ends[i - nsingle], results[i], d, &err);
-    if (err) return err;
-    results[i].pair_offset = 0;
-    if (!gpu) continue;
-    plan.dev_index[i] = (int)plan.dev.size();
-    plan.dev_problem.push_back(i);
-    plan.dev.push_back(d);
+  const int T = plan_threads((size_t)n + (size_t)ngenome);
+  std::vector<const char*> why(2 * T, nullptr);
+  std::vector<int> errat(2 * T, INT32_MAX), errcode(2 * T, 0);
+  // single and end gaps: convert in parallel, then the GPU ones compacted in order
+  {
+    std::vector<DevProblem> tmp(n);
+    std::vector<unsigned char> gpu(n, 0);
+    std::vector<size_t> cnt(T, 0);
+    plan_parallel((size_t)n, T, [&](size_t lo, size_t hi, int t) {
+      for (size_t i = lo; i < hi; i++) {
+        int err = 0;
+        const char* w = nullptr;
+        const int g = (int)i < nsingle ? convert_single(ctx, singles[i], results[i], tmp[i])
+                                       : convert_end(ctx, ends[i - nsingle], results[i], tmp[i], &err, &w);
+        if (err) {
+          errat[t] = (int)i;
+          errcode[t] = err;
+          why[t] = w;
+          return;
+        }
+        results[i].pair_offset = 0;
+        gpu[i] = (unsigned char)g;
+        cnt[t] += (size_t)g;
+      }
+    });
+    for (int t = 0; t < T; t++)
+      if (errat[t] != INT32_MAX) return why[t] ? bad(ctx, why[t]) : errcode[t];
+    size_t total = 0;
+    std::vector<size_t> at(T);
+    for (int t = 0; t < T; t++) {
+      at[t] = total;
+      total += cnt[t];
+    }
+    plan.dev_index.assign(n, -1);
+    plan.dev_problem.resize(total);
+    plan.dev.resize(total);
+    plan_parallel((size_t)n, T, [&](size_t lo, size_t hi, int t) {
+      size_t k = at[t];
+      for (size_t i = lo; i < hi; i++)
+        if (gpu[i]) {
+          plan.dev_index[i] = (int)k;
+          plan.dev_problem[k] = (int)i;
+          plan.dev[k++] = tmp[i];
+        }
+    });
   }
-  plan.gdev_index.assign(ngenome, -1);
-  for (int j = 0; j < ngenome; j++) {
-    DevGenomeProblem d;
-    int err = 0;
-    const int gpu = convert_genome(ctx, genomes[j], gresults[j], d, &err);
-    if (err) return err;
-    if (!gpu) continue;
-    plan.gdev_index[j] = (int)plan.gdev.size();
-    plan.gdev_problem.push_back(j);
-    plan.gdev.push_back(d);
+  {
+    std::vector<DevGenomeProblem> tmp(ngenome);
+    std::vector<unsigned char> gpu(ngenome, 0);
+    std::vector<size_t> cnt(T, 0);
+    plan_parallel((size_t)ngenome, T, [&](size_t lo, size_t hi, int t) {
+      for (size_t j = lo; j < hi; j++) {
+        int err = 0;
+        const char* w = nullptr;
+        const int g = convert_genome(ctx, genomes[j], gresults[j], tmp[j], &err, &w);
+        if (err) {
+          errat[T + t] = (int)j;
+          errcode[T + t] = err;
+          why[T + t] = w;
+          return;
+        }
+        gpu[j] = (unsigned char)g;
+        cnt[t] += (size_t)g;
+      }
+    });
+    for (int t = 0; t < T; t++)
+      if (errat[T + t] != INT32_MAX) return why[T + t] ? bad(ctx, why[T + t]) : errcode[T + t];
+    size_t total = 0;
+    std::vector<size_t> at(T);
+    for (int t = 0; t < T; t++) {
+      at[t] = total;
+      total += cnt[t];
+    }
+    plan.gdev_index.assign(ngenome, -1);
+    plan.gdev_problem.resize(total);
+    plan.gdev.resize(total);
+    plan_parallel((size_t)ngenome, T, [&](size_t lo, size_t hi, int t) {
+      size_t k = at[t];
+      for (size_t j = lo; j < hi; j++)
+        if (gpu[j]) {
+          plan.gdev_index[j] = (int)k;
+          plan.gdev_problem[k] = (int)j;
+          plan.gdev[k++] = tmp[j];
+        }
+    });
   }
+  tm.mark("convert");
   int rc = classify(ctx, plan);
   if (rc) return rc;
+  tm.mark("classify");
   for (size_t s = 0; s < plan.dev.size(); s++) results[plan.dev_problem[s]].pair_offset = plan.dev[s].pair_offset;
   for (size_t s = 0; s < plan.gdev.size(); s++) gresults[plan.gdev_problem[s]].pair_offset = plan.gdev[s].pair_offset;
   return GMAPDP_OK;
@@ -2043,10 +2283,12 @@ int gmapdp_plan_create_all(gmapdp_ctx* ctx, const gmapdp_single_problem* singles
   if ((nsingle + nend && !host_results) || (ngenome && !host_genome_results)) return GMAPDP_EINVAL;
   (void)hipSetDevice(ctx->device);
   gmapdp_plan* p = new gmapdp_plan();
+  PlanTimer tm("plan_create_all");
   p->nsingle = nsingle;
   p->nend = nend;
   p->ngenome = ngenome;
   int rc = build_plan(ctx, singles, nsingle, ends, nend, genomes, ngenome, host_results, host_genome_results, p->in);
+  tm.mark("build_plan");
   if (rc) {
     delete p;
     return rc;
@@ -2067,6 +2309,7 @@ int gmapdp_plan_create_all(gmapdp_ctx* ctx, const gmapdp_single_problem* singles
     e = hipMemcpy(p->d_gprobs, p->in.gdev.data(), sizeof(DevGenomeProblem) * ng, hipMemcpyHostToDevice);
   if (e == hipSuccess && ng) e = hipMemcpy(p->d_gorder, p->in.gorder.data(), sizeof(int) * ng, hipMemcpyHostToDevice);
   if (e == hipSuccess && p->in.gdirs_bytes) e = ctx->gdirs.ensure(p->in.gdirs_bytes);
+  tm.mark("upload");
   if (e != hipSuccess) {
     plan_free(p);
     return fail(ctx, GMAPDP_ENOMEM, "plan upload: %s", e);
@@ -2274,6 +2517,12 @@ struct gmapdp_oligo_plan {
   std::vector<int> keys;                      // per problem in launch order: its class key
   size_t table_cap = 0, diag_cap = 0, scratch_cap = 0;
   int32_t* d_nhits = nullptr;                 // sizing runs: each problem's hit-list length
+  // Two seeding paths with the same results.  Device-resident plans (a stage-2 plan's sizing run and its
+  // runs: bench.py's step, many calls beside the DP classes) take oi_kernel + oi_map_kernel, small-LDS
+  // kernels that share the CUs with the DP launches; the synchronous batch APIs (the drop-in's dispatcher
+  // batches: a few calls, latency-bound) take oi_scan_kernel + oi_build_kernel, four waves per call and
+  // the table and the event sort in LDS (measured: DESIGN.md §5.7).
+  bool split = false;
   // get_mappings' event pool (3 slots per hit, shared by a chunk through an atomic cursor; a problem that no
   // longer fits runs the sequential walk in its fallback region, or reports overflow when it has none)
   uint64_t* d_pool = nullptr;
@@ -2436,6 +2685,7 @@ static int oligo_plan_build(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problem
   gmapdp_oligo_plan* P = new gmapdp_oligo_plan();
   P->n = n;
   P->borrowed = borrow;
+  P->split = borrow;
   P->ord.reserve(n);
   for (auto& kv : classes)
     for (int i : kv.second) {
@@ -2533,10 +2783,15 @@ int gmapdp_oligo_plan_run(gmapdp_ctx* ctx, const gmapdp_oligo_plan* plan, const 
     if (hipMemsetAsync(plan->d_pool_counter, 0, sizeof(unsigned long long), s) != hipSuccess)
       return fail(ctx, GMAPDP_ELAUNCH, "oligo pool reset: %s", hipGetLastError());
     const int key = plan->umax[li];
-    const hipError_t e = launch_oi(key & 1, plan->launches[li].second, lds_bytes_oi(key >> 1, key & 1), s,
-                                   plan->d_probs + plan->launches[li].first, ctx->d_genome, d_qseq_uc,
-                                   plan->d_scratch, d_results, d_npositions, d_mappings, d_positions, d_diagonals,
-                                   plan->d_pool, plan->d_pool_counter, plan->pool_cap, plan->d_nhits);
+    const hipError_t e =
+        !plan->split
+            ? launch_oi(key & 1, plan->launches[li].second, lds_bytes_oi(key >> 1, key & 1), s,
+                        plan->d_probs + plan->launches[li].first, ctx->d_genome, d_qseq_uc, plan->d_scratch,
+                        d_results, d_npositions, d_mappings, d_positions, d_diagonals, plan->d_pool,
+                        plan->d_pool_counter, plan->pool_cap, plan->d_nhits)
+            : launch_oi_split(plan->launches[li].second, key >> 1, s, plan->d_probs + plan->launches[li].first,
+                              ctx->d_genome, d_qseq_uc, plan->d_scratch, d_results, d_npositions, d_mappings,
+                              d_positions, d_diagonals, plan->d_pool, plan->d_pool_counter, plan->pool_cap);
     if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "oligo launch: %s", e);
   }
   return GMAPDP_OK;
@@ -3329,9 +3584,11 @@ int gmapdp_stage2_plan_create(gmapdp_ctx* ctx, const gmapdp_stage2_problem* prob
     qsum += (size_t)p.querylength;
   }
   gmapdp_stage2_plan* P = new gmapdp_stage2_plan();
+  PlanTimer tm("stage2_plan_create");
   P->n = n;
   P->qbytes = qbytes;
   int rc = oligo_plan_build(ctx, op.data(), n, qseq_uc, qbytes, &P->oplan, false, /*sizing*/ true);
+  tm.mark("oligo_plan_build");
   if (rc) {
     delete P;
     return rc;
@@ -3352,6 +3609,7 @@ int gmapdp_stage2_plan_create(gmapdp_ctx* ctx, const gmapdp_stage2_problem* prob
     stage2_plan_free(P);
     return fail(ctx, GMAPDP_ENOMEM, "stage-2 plan: %s", e);
   }
+  tm.mark("buffers");
   // size the chaining scratch from one seeding run
   rc = stage2_plan_launch(ctx, P, nullptr, (const char*)ctx->qseq_uc.p, nullptr, ctx->stream, true, 0);
   std::vector<gmapdp_oligo_result> ores(n);
@@ -3367,6 +3625,7 @@ int gmapdp_stage2_plan_create(gmapdp_ctx* ctx, const gmapdp_stage2_problem* prob
     stage2_plan_free(P);
     return rc;
   }
+  tm.mark("sizing_run");
   // The seeding's arenas were sized from upper bounds (a window's worth of positions and 24 diagonals per
   // query position: 19 GB for 10 000 5-kb reads).  Re-lay them out from this run's measured use
   // (oligo_plan_relayout) so the plan keeps only what its runs write.
@@ -3377,6 +3636,7 @@ int gmapdp_stage2_plan_create(gmapdp_ctx* ctx, const gmapdp_stage2_problem* prob
   (void)hipFree(P->oplan->d_nhits);
   P->oplan->d_nhits = nullptr;
   e = oligo_plan_relayout(ctx, P->oplan, op.data(), ores.data(), nhits.data());
+  tm.mark("relayout");
   if (e == hipSuccess) e = hipMalloc(&P->d_table, sizeof(uint32_t) * std::max<size_t>(P->oplan->table_cap, 1));
   if (e == hipSuccess) e = hipMalloc(&P->d_diag, 4 * sizeof(int32_t) * std::max<size_t>(P->oplan->diag_cap, 1));
   if (e != hipSuccess) {
@@ -3393,6 +3653,7 @@ int gmapdp_stage2_plan_create(gmapdp_ctx* ctx, const gmapdp_stage2_problem* prob
   if (e == hipSuccess) e = hipMemcpy(P->d_probs, dp.data(), sizeof(DevStage2Problem) * n, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&P->d_paths, sizeof(gmapdp_path) * P->path_cap);
   if (e == hipSuccess) e = hipMalloc(&P->d_pairs, sizeof(gmapdp_path_pair) * P->pair_cap);
+  tm.mark("pools");
   if (e != hipSuccess) {
     stage2_plan_free(P);
     return fail(ctx, GMAPDP_ENOMEM, "stage-2 plan pools: %s", e);

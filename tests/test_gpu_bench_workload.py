@@ -23,8 +23,10 @@ import pytest
 
 import gmapdp
 from gmapdp import workload as W
-from dpbind import (S2B_PATHS, Oracle, call_end, call_single, microexon_probs, oracle_splice_probs,
-                    oracle_stage2_batch, stage2_mismatches)
+import ctypes as C
+
+from dpbind import (S2B_PATHS, Oracle, call_end, call_single, dp_batch_mismatches, microexon_probs,
+                    oracle_dp_batch, oracle_splice_probs, oracle_stage2_batch, stage2_mismatches)
 
 pytestmark = pytest.mark.gpu
 TAIL = 8192
@@ -240,3 +242,160 @@ def test_gpu_bench_configs4_block_sample():
     sizes, got = _run(lay, W.ISOSEQ5K, 2000, 1, chroms=small, frac=0.05)
     assert sizes["oligo"] >= 5 and sizes["genome"] > 100
     assert sum(1 for r in got["oligo"] if r[0] > 0) > 0.8 * sizes["oligo"]
+
+
+def _dp_plan_block(eng, d):
+    """bench.py's DP path over block d: gmapdp_plan_create_all (single, end and genome gaps), the device
+    MaxEnt bound (gmapdp_plan_bind_genome_maxent), gmapdp_plan_run; the microexon plan (search, device
+    MaxEnt, finish).  Returns {family: (results in problem order, the pair arena)}."""
+    lib = eng.lib
+    hip = gmapdp._hip()
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    bufs = []
+
+    def dbuf(nbytes, src=None):
+        ptr = C.c_void_p()
+        assert hip.hipMalloc(C.byref(ptr), max(int(nbytes), 16)) == 0
+        bufs.append(ptr)
+        if src is not None:
+            assert hip.hipMemcpy(ptr, src.ctypes.data, int(nbytes), 1) == 0
+        return ptr
+
+    def down(dst, ptr):
+        assert hip.hipMemcpy(dst.ctypes.data, ptr, dst.nbytes, 2) == 0
+        return dst
+
+    sp, ep, gp, mp = d["single"], d["end"], d["genome"], d["microexon"]
+    out = {}
+    try:
+        q = d["q"]
+        d_q = dbuf(len(q), q)
+        host_res = np.zeros(len(sp) + len(ep), dtype=gmapdp.RESULT_DTYPE)
+        host_gres = np.zeros(max(len(gp), 1), dtype=gmapdp.GENOME_RESULT_DTYPE)
+        plan = C.c_void_p()
+        eng._check(lib.gmapdp_plan_create_all(eng.h, sp.ctypes.data, len(sp), ep.ctypes.data, len(ep), gp.ctypes.data,
+                                              len(gp), host_res.ctypes.data, host_gres.ctypes.data, C.byref(plan)),
+                   "gmapdp_plan_create_all")
+        try:
+            ngpu, nggpu = lib.gmapdp_plan_gpu_problems(plan), lib.gmapdp_plan_genome_gpu_problems(plan)
+            cap = lib.gmapdp_plan_pair_capacity(plan)
+            d_res = dbuf(32 * max(ngpu, 1))
+            d_gres = dbuf(gmapdp.GENOME_RESULT_DTYPE.itemsize * max(nggpu, 1))
+            d_pairs = dbuf(16 * max(cap, 1))
+            m = int((gp["prob_offset"] + gp["glengthL"] + gp["glengthR"]).max()) if len(gp) else 1
+            d_sprob = dbuf(8 * max(m, 1))
+            eng._check(lib.gmapdp_plan_bind_genome_maxent(eng.h, plan, d_sprob, d_gres), "bind_genome_maxent")
+            eng._check(lib.gmapdp_plan_run(eng.h, plan, d_q, d_q, d_res, d_pairs, None), "gmapdp_plan_run")
+            assert hip.hipDeviceSynchronize() == 0
+            dres = down(np.zeros(max(ngpu, 1), dtype=gmapdp.RESULT_DTYPE), d_res)
+            dgres = down(np.zeros(max(nggpu, 1), dtype=gmapdp.GENOME_RESULT_DTYPE), d_gres)
+            pairs = down(np.zeros(max(cap, 1), dtype=gmapdp.PAIR_DTYPE), d_pairs)
+            res = host_res.copy()
+            di = np.array([lib.gmapdp_plan_dev_index(plan, i) for i in range(len(res))], dtype=np.int64)
+            res[di >= 0] = dres[di[di >= 0]]
+            gres = host_gres[:len(gp)].copy()
+            gi = np.array([lib.gmapdp_plan_genome_dev_index(plan, j) for j in range(len(gp))], dtype=np.int64)
+            gres[gi >= 0] = dgres[gi[gi >= 0]]
+            out["single"] = (res[:len(sp)], pairs)
+            out["end"] = (res[len(sp):], pairs)
+            out["genome"] = (gres, pairs)
+        finally:
+            lib.gmapdp_plan_destroy(plan)
+        if len(mp):
+            mplan = C.c_void_p()
+            eng._check(lib.gmapdp_microexon_plan_create(eng.h, mp.ctypes.data, len(mp), q.ctypes.data, q.ctypes.data,
+                                                        len(q), C.byref(mplan)), "gmapdp_microexon_plan_create")
+            try:
+                mcap = lib.gmapdp_microexon_plan_pair_capacity(mplan)
+                d_mres = dbuf(gmapdp.MICROEXON_RESULT_DTYPE.itemsize * len(mp))
+                d_mpairs = dbuf(16 * max(mcap, 1))
+                eng._check(lib.gmapdp_microexon_plan_run(eng.h, mplan, d_q, d_q, None, d_mres, d_mpairs, 3, None),
+                           "gmapdp_microexon_plan_run")
+                assert hip.hipDeviceSynchronize() == 0
+                out["microexon"] = (down(np.zeros(len(mp), dtype=gmapdp.MICROEXON_RESULT_DTYPE), d_mres),
+                                    down(np.zeros(max(mcap, 1), dtype=gmapdp.PAIR_DTYPE), d_mpairs))
+            finally:
+                lib.gmapdp_microexon_plan_destroy(mplan)
+    finally:
+        for b in bufs:
+            hip.hipFree(b)
+    return out
+
+
+def _oracle_dp_block(genome, d, fams, simd=False):
+    """orc_dp_batch over every call of the families, chromosome by chromosome (the oracle holds one
+    chromosome at chroffset 0; outputs are chromosome-relative): {family: (scal, dscal, pairs, pair_off)}
+    in problem order."""
+    orc = Oracle(simd=simd)
+    q = d["q"].tobytes()
+    out = {}
+    for fam in fams:
+        p = d[fam]
+        n = len(p)
+        scal = np.zeros((n, 16), dtype=np.int32)
+        dscal = np.zeros((n, 2), dtype=np.float64)
+        parts, pair_off, base = [], np.zeros(n + 1, dtype=np.int64), 0
+        order = np.zeros(n, dtype=np.int64)
+        for cho in sorted(set(int(x) for x in p["chroffset"])):
+            idx = np.nonzero(p["chroffset"] == cho)[0]
+            chh = int(p["chrhigh"][idx[0]])
+            orc.set_genome(genome.ascii(cho, min(genome.length, chh + TAIL)))
+            sub = p[idx].copy()
+            sub["chroffset"] = 0
+            sub["chrhigh"] = chh - cho
+            sc, ds, pr, po = oracle_dp_batch(orc, fam, sub, q, q)
+            scal[idx], dscal[idx] = sc, ds
+            pair_off[idx] = base + po[:-1]
+            parts.append(pr[:int(po[-1])])
+            base += int(po[-1])
+            order[idx] = 1
+        pair_off[n] = base
+        out[fam] = (scal, dscal, np.concatenate(parts) if parts else np.zeros(1, dtype=gmapdp.PAIR_DTYPE), pair_off)
+        _progress("oracle: every %s call (%d)" % (fam, n))
+    return out
+
+
+def _dp_every_call(genome, d, simd):
+    fams = ("single", "end", "genome") + (() if simd else ("microexon",))
+    if simd:
+        d = dict(d)
+        for fam in ("single", "end", "genome"):
+            d[fam] = d[fam].copy()
+            d[fam]["flags"] |= gmapdp.SIMD
+    eng = gmapdp.Engine(0)
+    eng.set_genome(blocks=genome.blocks, length=genome.length)
+    try:
+        got = _dp_plan_block(eng, d)
+    finally:
+        eng.close()
+    _progress("engine: the block's DP plan%s" % (" (SIMD semantics)" if simd else ""))
+    exp = _oracle_dp_block(genome, d, fams, simd=simd)
+    bad = {}
+    for fam in fams:
+        res, pairs = got[fam]
+        b = dp_batch_mismatches(fam, res, pairs, exp[fam])
+        if b:
+            bad[fam] = b[:8]
+    sizes = {fam: len(d[fam]) for fam in fams}
+    assert not bad, "bench block 0: calls differ from the oracle: %s of %s" % (bad, sizes)
+    return sizes, got
+
+
+def test_gpu_bench_configs2_dp_every_call(grch38_block0):
+    """Every Dynprog_single_gap, _end5/3_gap, _genome_gap and _microexon_int call of bench block 0 (configs[2],
+    GRCh38 coordinates; dynprog_single.c:429, dynprog_end.c:1294/1924, dynprog_genome.c:3288,
+    dynprog_single.c:900) through the plan path bench.py times (device MaxEnt), bit-exact against the
+    oracle's batch runner (orc_dp_batch, oracle MaxEnt) -- VERDICT r5 item 2: the whole block, not a sample."""
+    genome, d = grch38_block0
+    sizes, got = _dp_every_call(genome, d, simd=False)
+    assert sizes["single"] > 150000 and sizes["genome"] > 400000 and sizes["microexon"] > 50000
+    assert (got["genome"][0]["npairs"] > 0).mean() > 0.9
+
+
+def test_gpu_bench_configs2_simd_every_call(grch38_block0):
+    """`bench.py --simd` on bench block 0: every single, end and genome gap with the SIMD builds' semantics
+    (gmap.avx2: sx_kernel, uxe_kernel, uxg_kernel; dynprog_simd.c) at GRCh38 coordinates against the oracle's
+    S semantics (orc_set_simd 1)."""
+    genome, d = grch38_block0
+    sizes, got = _dp_every_call(genome, d, simd=True)
+    assert sizes["genome"] > 400000

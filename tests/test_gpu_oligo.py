@@ -139,7 +139,10 @@ def test_gpu_oligo_repeats_match_oracle(engine, seed):
 
 
 def test_gpu_oligo_pool_overflow_falls_back(engine, monkeypatch):
-    """A small event pool: the problems that no longer fit run the sequential walk; same results."""
+    """oi_build_kernel's fallbacks: the table image and the candidates kept out of LDS (GMAPDP_OI_LDS_TABLE 0:
+    scattered table stores, every event through the global pool; 512: tables past 512 entries and
+    candidate lists past 256 take the global paths, the rest stay in LDS), and a small event pool (the
+    problems that no longer fit run the sequential walk); same results every way."""
     rng = random.Random(8400)
     g = _repeat_genome(rng, 200000)
     engine.set_genome(g)
@@ -147,10 +150,18 @@ def test_gpu_oligo_pool_overflow_falls_back(engine, monkeypatch):
     orc.set_genome(g)
     probs = [oligo_problem(rng, g) for i in range(200)]
     exp = [orc.oligo_mappings(p) for p in probs]
-    for slots in ("0", "20000"):
-        monkeypatch.setenv("GMAPDP_OLIGO_POOL_SLOTS", slots)
-        d = _first_diff(engine.oligo_mappings_batch(probs), exp)
-        assert d is None, _msg(probs, d, "oracle (pool %s)" % slots)
+    for lds in ("0", "512", None):
+        if lds is None:
+            monkeypatch.delenv("GMAPDP_OI_LDS_TABLE", raising=False)
+        else:
+            monkeypatch.setenv("GMAPDP_OI_LDS_TABLE", lds)
+        for slots in ("0", "20000", None):
+            if slots is None:
+                monkeypatch.delenv("GMAPDP_OLIGO_POOL_SLOTS", raising=False)
+            else:
+                monkeypatch.setenv("GMAPDP_OLIGO_POOL_SLOTS", slots)
+            d = _first_diff(engine.oligo_mappings_batch(probs), exp)
+            assert d is None, _msg(probs, d, "oracle (LDS table %s, pool %s)" % (lds, slots))
 
 
 def test_gpu_oligo_wide_windows_match_oracle(engine):

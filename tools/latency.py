@@ -36,12 +36,13 @@ def main():
     rng = np.random.default_rng(5)
     sp, sq = W.make_single(genome, layout, 256, rng)
     gp, gq, gprob = W.make_genome_gaps(genome, layout, 256, rng)
-    op, oq = W.make_stage2(genome, layout, 64, rng)
+    # Stage2_compute over the windows `gmap -d` gives it (the read's locus +- ~100 kb, workload.CDNA2K)
+    op, oq = W.make_stage2(genome, layout, 64, rng, pad=W.CDNA2K.pad)
     s2calls = [dict(quc=oq[int(p["qoff"]):int(p["qoff"]) + int(p["querylength"])].tobytes(),
                     **{k: int(p[k]) for k in ("chrstart", "chrend", "chroffset", "chrhigh", "plusp")}) for p in op]
     out = {"reps": reps, "us_per_batch": {}}
     sqb, gqb = sq.tobytes(), gq.tobytes()
-    for k in (1, 8, 64):
+    for k in (1, 8, 16, 64):
         out["us_per_batch"]["single_gap_%d" % k] = _time(lambda: eng.single_gap_batch_raw(sp[:k], sqb, sqb), reps)
         out["us_per_batch"]["genome_gap_%d" % k] = _time(lambda: eng.genome_gap_batch_raw(gp[:k], gqb, gqb, gprob),
                                                          reps)

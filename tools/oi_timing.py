@@ -143,6 +143,15 @@ def main():
     torch.cuda.synchronize()
     lib.gmapdp_debug_oi_marks(marks.ctypes.data)
     t, c = marks[:16].astype(np.float64), marks[16:]
+    if int(c[10]):  # the split kernels (oi_scan_kernel 10 -> 11; oi_build_kernel 12, 2, 3, 4, 5, 13, 14, 15)
+        per = lambda a, b, w: round(float(t[b] - t[a]) / 1e2 / max(int(c[w]), 1), 1)  # noqa: E731
+        print(json.dumps({"waves": {k: int(c[k]) for k in (10, 11, 12, 2, 3, 4, 5, 13, 14, 15)},
+                          "us_per_wave": {"scan (set_inquery + pass 1)": per(10, 11, 10), "counts": per(12, 2, 12),
+                                          "layout": per(2, 3, 2), "placement + write-out": per(3, 4, 3),
+                                          "prelude": per(4, 5, 4), "slot counts": per(5, 13, 13),
+                                          "emit candidates": per(13, 14, 14), "sort + sweep": per(14, 15, 15)}}))
+        eng.close()
+        return
     # oi_kernel: marks 0..4; oi_map_kernel: 8 (start), 9 (pool allocated), 5, 6, 7
     spans = [(0, 1), (1, 2), (2, 3), (3, 4), (8, 9), (9, 5), (5, 6), (6, 7)]
     out = {"waves": [int(c[k]) for k in (0, 1, 2, 3, 4, 8, 9, 5, 6, 7)]}
