@@ -280,17 +280,25 @@ def latest_e2e(kind="e2e"):
             "outputs_identical": d.get("outputs_identical")}
 
 
-def like_for_like(out, pcie_ms, up, down):
+def like_for_like(out, pcie_ms, up, down, compact=None):
     """The headline next to what it leaves out: the step's own host-to-device and device-to-host copies and
     GMAP end to end through the drop-in.  MaxEnt is in the step (device), as it is in the CPU baseline's
-    reference objects."""
+    reference objects.  With the compact pair stream (`compact`), the down copy is the run-length stream
+    plus the results, and the compaction kernels are added; reads_per_s_incl_pcie takes the cheaper of the
+    two transports (the host's expansion back to records replaces reading the records, and is reported
+    beside it, not added: neither transport counts the consumer's own pass over the pairs)."""
     v = out["value"]
     ms = out["ms_per_step"]
     reads = out["config"]["reads_per_step_per_gpu"]
-    with_pcie = reads / ((ms + pcie_ms) * 1e-3) * out["n_gpus"]
+    raw = reads / ((ms + pcie_ms) * 1e-3) * out["n_gpus"]
+    with_pcie = raw
+    if compact and compact.get("expanded_equals_records"):
+        compact["reads_per_s_incl_pcie"] = reads / ((ms + compact["pcie_ms_per_step"]) * 1e-3) * out["n_gpus"]
+        with_pcie = max(raw, compact["reads_per_s_incl_pcie"])
     cb = out.get("cpu_baseline") or {}
     cpu = cb.get("value")
     return {"pcie_ms_per_step": pcie_ms, "pcie_bytes_up": up, "pcie_bytes_down": down,
+            "reads_per_s_incl_pcie_records": raw, "compact_pair_stream": compact,
             "reads_per_s_incl_pcie": with_pcie,
             "ratio_vs_cpu": v / cpu if cpu else None,
             "ratio_vs_cpu_incl_pcie": with_pcie / cpu if cpu else None,
@@ -910,7 +918,73 @@ def main():
             torch.cuda.synchronize()
             pcie_ms.append(e0.elapsed_time(e1))
     pcie_ms = float(np.median(pcie_ms[1:]))
+    up_ms = []
+    with torch.cuda.stream(stream):
+        for _ in range(4):
+            e0, e1 = mk()
+            e0.record(stream)
+            g_up.copy_(h_up, non_blocking=True)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            up_ms.append(e0.elapsed_time(e1))
+    up_ms = float(np.median(up_ms[1:]))
     del h_up, h_down, g_up, g_down
+
+    # ---- the compact pair stream: block b's DP pairs as run-length ops
+    # (gmapdp_plan_compact_pairs), copied down with the results and the stage-2 outputs, then expanded on the
+    # host (gmapdp_expand_pairs, 16 threads) and checked against the records themselves ----
+    compact = None
+    with torch.cuda.stream(stream):
+        step(b)
+        torch.cuda.synchronize()
+        nprob = b["ngpu"] + b["nggpu"]
+        d_off = torch.empty(nprob + 1, dtype=torch.int64, device=dev)
+        d_cmp = torch.empty(max(int(lib.gmapdp_plan_compact_bound(b["plan"])), 16), dtype=torch.uint8, device=dev)
+        cms = []
+        for _ in range(3):
+            e0, e1 = mk()
+            e0.record(stream)
+            eng._check(lib.gmapdp_plan_compact_pairs(eng.h, b["plan"], C.c_void_p(d_res.data_ptr()),
+                                                     C.c_void_p(d_pairs.data_ptr()), C.c_void_p(d_cmp.data_ptr()),
+                                                     C.c_void_p(d_off.data_ptr()), C.c_void_p(stream.cuda_stream)),
+                       "gmapdp_plan_compact_pairs")
+            e1.record(stream)
+            torch.cuda.synchronize()
+            cms.append(e0.elapsed_time(e1))
+        offs = d_off.cpu().numpy().view(np.uint64)
+        nbytes = int(offs[-1])
+        other = int(32 * b["ngpu"] + 72 * b["nggpu"] + 8 * (nprob + 1) + 32 * args.reads
+                    + 20 * checks["stage2_path_pairs"] / len(B))
+        cdown = nbytes + other
+        h_c = torch.empty(cdown, dtype=torch.uint8, pin_memory=True)
+        g_c = torch.empty(cdown, dtype=torch.uint8, device=dev)
+        dms = []
+        for _ in range(4):
+            e0, e1 = mk()
+            e0.record(stream)
+            h_c.copy_(g_c, non_blocking=True)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            dms.append(e0.elapsed_time(e1))
+        stream_host = d_cmp[:max(nbytes, 1)].cpu().numpy()
+        res_h, gres_h = fetch_results(b)
+        npc = np.concatenate([res_h["npairs"], gres_h["npairs"]]).astype(np.int32)
+        poff = np.concatenate([res_h["pair_offset"], gres_h["pair_offset"]]).astype(np.int64)
+        t0 = time.perf_counter()
+        exp = gmapdp.expand_pairs(stream_host, offs, npc, poff, b["cap"], nthreads=16)
+        expand_ms = (time.perf_counter() - t0) * 1e3
+        allp = np.frombuffer(d_pairs[:16 * b["cap"]].cpu().numpy().tobytes(), dtype=gmapdp.PAIR_DTYPE)
+        cnt = np.maximum(npc.astype(np.int64), 0)
+        idx = np.repeat(poff, cnt) + (np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt))
+        same = bool(np.array_equal(exp[idx], allp[idx]))
+        del h_c, g_c, d_cmp, allp, exp
+        compact = {"records": int(cnt.sum()), "stream_bytes": nbytes, "bytes_per_record": nbytes / max(int(cnt.sum()), 1),
+                   "compact_kernels_ms": float(np.median(cms[1:])), "pcie_bytes_down": cdown,
+                   "pcie_down_ms": float(np.median(dms[1:])), "pcie_up_ms": up_ms,
+                   "host_expand_ms_16_threads": expand_ms, "expanded_equals_records": same}
+        compact["pcie_ms_per_step"] = compact["pcie_up_ms"] + compact["compact_kernels_ms"] + compact["pcie_down_ms"]
+        progress("compact pair stream: %d records in %d bytes, expanded %s" % (compact["records"], nbytes,
+                                                                           "identically" if same else "DIFFERENTLY"))
 
     ms_step = elapsed / args.steps * 1e3
     reads_total = args.reads * world * args.steps
@@ -1024,7 +1098,7 @@ def main():
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:
-        out["like_for_like"] = like_for_like(out, pcie_ms, up, down)
+        out["like_for_like"] = like_for_like(out, pcie_ms, up, down, compact)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

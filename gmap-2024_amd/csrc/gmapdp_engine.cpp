@@ -23,6 +23,7 @@
 #include <thread>
 #include <string>
 #include <tuple>
+#include <utility>
 #include <vector>
 
 #include "gmapdp_internal.h"
@@ -100,6 +101,8 @@ hipError_t launch_oi(bool wide, int nproblems, size_t lds, hipStream_t stream, c
                      int32_t* npos, int32_t* map, uint32_t* table, int32_t* diags, uint64_t* pool,
                      unsigned long long* pool_counter, unsigned long long pool_cap, int32_t* nhits_out);
 size_t scratch_bytes_oi_hits(int querylength, size_t hitcap);
+hipError_t launch_pc(const unsigned char* r0, int n0, int s0, const unsigned char* r1, int n1, int s1,
+                     const gmapdp_pair* pairs, unsigned long long* offsets, unsigned char* out, hipStream_t stream);
 hipError_t launch_oi_split(int nproblems, int umax, hipStream_t stream, const DevOligoProblem* probs,
                            const uint32_t* blocks, const char* quc, unsigned char* scratch,
                            gmapdp_oligo_result* results, int32_t* npos, int32_t* map, uint32_t* table, int32_t* diags,
@@ -318,14 +321,37 @@ static hipError_t ctx_sync(gmapdp_ctx* ctx, hipStream_t s) {
   }
 }
 
+// Host arrays a plan build fills completely: resize() leaves them uninitialised (zero-filling ~200 MB of
+// descriptors for a 10 000-read block on one thread cost more than building them on 16).
+template <typename T>
+struct NoInitAlloc : std::allocator<T> {
+  template <typename U>
+  struct rebind {
+    using other = NoInitAlloc<U>;
+  };
+  NoInitAlloc() = default;
+  template <typename U>
+  NoInitAlloc(const NoInitAlloc<U>&) {}
+  template <typename U>
+  void construct(U* p) noexcept {
+    ::new ((void*)p) U;
+  }
+  template <typename U, typename... A>
+  void construct(U* p, A&&... a) {
+    ::new ((void*)p) U(std::forward<A>(a)...);
+  }
+};
+template <typename T>
+using HostArray = std::vector<T, NoInitAlloc<T>>;
+
 // A batch resolved on the host: GPU problems grouped into launch classes.
 struct PlanCore {
-  std::vector<DevProblem> dev;       // one per GPU problem (single / end)
-  std::vector<int> dev_index;        // problem index -> dev slot (-1: resolved on host)
-  std::vector<int> dev_problem;      // dev slot -> problem index
-  std::vector<DevGenomeProblem> gdev;  // Dynprog_genome_gap problems on the GPU
-  std::vector<int> gdev_index;       // genome problem index -> gdev slot (-1: resolved on host)
-  std::vector<int> gdev_problem;     // gdev slot -> genome problem index
+  HostArray<DevProblem> dev;         // one per GPU problem (single / end)
+  HostArray<int> dev_index;          // problem index -> dev slot (-1: resolved on host)
+  HostArray<int> dev_problem;        // dev slot -> problem index
+  HostArray<DevGenomeProblem> gdev;  // Dynprog_genome_gap problems on the GPU
+  HostArray<int> gdev_index;         // genome problem index -> gdev slot (-1: resolved on host)
+  HostArray<int> gdev_problem;       // gdev slot -> genome problem index
   // kDpx: 64/S narrow problems per wave, R = S; kSx: SIMD-build single gaps, 64/B problems per wave,
   // R = B; kUxe / kUxg: SIMD-build end / genome gaps (triangle fills), one wave per problem, R = B
   // kDpRows: dp_kernel's recurrence with lanes over query rows (dpr_kernel), R = row words
@@ -1085,37 +1111,49 @@ static void plan_parallel(size_t n, int T, F&& f) {
   f((size_t)0, std::min(n, per), 0);
   for (auto& x : th) x.join();
 }
-// stable sort of ids by `before` (a strict weak order): T sorted runs, then pairwise stable merges
-template <typename C>
-static void plan_stable_sort(std::vector<int>& ids, int T, C before) {
-  if (T <= 1 || ids.size() < 65536) {
-    std::stable_sort(ids.begin(), ids.end(), before);
-    return;
-  }
-  const size_t n = ids.size(), per = (n + (size_t)T - 1) / (size_t)T;
-  std::vector<size_t> cut;
-  for (size_t x = 0; x < n; x += per) cut.push_back(x);
-  cut.push_back(n);
-  plan_parallel(cut.size() - 1, (int)cut.size() - 1, [&](size_t lo, size_t hi, int) {
-    for (size_t r = lo; r < hi; r++) std::stable_sort(ids.begin() + cut[r], ids.begin() + cut[r + 1], before);
+// ids sorted by key(id) descending, ties in their current order (a stable sort).  The keys are taken
+// once, in the ids' order (a comparator reading the 88-128-B descriptors of two random problems per
+// comparison spent most of a 10 000-read plan on cache misses); T sorted runs of (key, position) pairs,
+// then pairwise merges.
+template <typename KF>
+static void plan_sort_desc(std::vector<int>& ids, int T, KF key) {
+  const size_t n = ids.size();
+  if (n < 2) return;
+  std::vector<std::pair<uint64_t, uint32_t>> kv(n);  // (~key, position): ascending = key descending, stable
+  plan_parallel(n, n >= 65536 ? T : 1, [&](size_t lo, size_t hi, int) {
+    for (size_t i = lo; i < hi; i++) kv[i] = {~(uint64_t)key(ids[i]), (uint32_t)i};
   });
-  std::vector<int> tmp(n);
-  while (cut.size() > 2) {
-    const size_t pairs = (cut.size() - 1) / 2;
-    std::vector<size_t> next;
-    plan_parallel(pairs, (int)pairs, [&](size_t lo, size_t hi, int) {
-      for (size_t q = lo; q < hi; q++)
-        std::merge(ids.begin() + cut[2 * q], ids.begin() + cut[2 * q + 1], ids.begin() + cut[2 * q + 1],
-                   ids.begin() + cut[2 * q + 2], tmp.begin() + cut[2 * q], before);
+  if (T <= 1 || n < 65536) {
+    std::sort(kv.begin(), kv.end());
+  } else {
+    const size_t per = (n + (size_t)T - 1) / (size_t)T;
+    std::vector<size_t> cut;
+    for (size_t x = 0; x < n; x += per) cut.push_back(x);
+    cut.push_back(n);
+    plan_parallel(cut.size() - 1, (int)cut.size() - 1, [&](size_t lo, size_t hi, int) {
+      for (size_t r = lo; r < hi; r++) std::sort(kv.begin() + cut[r], kv.begin() + cut[r + 1]);
     });
-    for (size_t q = 0; q < pairs; q++) {
-      std::copy(tmp.begin() + cut[2 * q], tmp.begin() + cut[2 * q + 2], ids.begin() + cut[2 * q]);
-      next.push_back(cut[2 * q]);
+    std::vector<std::pair<uint64_t, uint32_t>> tmp(n);
+    while (cut.size() > 2) {
+      const size_t pairs = (cut.size() - 1) / 2;
+      std::vector<size_t> next;
+      plan_parallel(pairs, (int)pairs, [&](size_t lo, size_t hi, int) {
+        for (size_t q = lo; q < hi; q++)
+          std::merge(kv.begin() + cut[2 * q], kv.begin() + cut[2 * q + 1], kv.begin() + cut[2 * q + 1],
+                     kv.begin() + cut[2 * q + 2], tmp.begin() + cut[2 * q]);
+      });
+      for (size_t q = 0; q < pairs; q++) {
+        std::copy(tmp.begin() + cut[2 * q], tmp.begin() + cut[2 * q + 2], kv.begin() + cut[2 * q]);
+        next.push_back(cut[2 * q]);
+      }
+      if ((cut.size() - 1) % 2) next.push_back(cut[cut.size() - 2]);
+      next.push_back(n);
+      cut.swap(next);
     }
-    if ((cut.size() - 1) % 2) next.push_back(cut[cut.size() - 2]);
-    next.push_back(n);
-    cut.swap(next);
   }
+  std::vector<int> out(n);
+  for (size_t i = 0; i < n; i++) out[i] = ids[kv[i].second];
+  ids.swap(out);
 }
 
 // a launch class key ordered as the tuple (kind, R, dirs in LDS, LDS bucket)
@@ -1228,12 +1266,14 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
   // direction placement) with the LDS of its largest member, and no packed narrow-band kernels, so a
   // batch is a few launches whose latencies do not add up class after class.
   const bool latency = nd + ng <= latency_batch();
+  PlanTimer tm("classify");
   // per problem (threads): its class; slots 0..nd-1 single / end gaps, nd.. genome gaps
   std::vector<ClassOf> cls(nd + ng);
   plan_parallel(nd + ng, T, [&](size_t lo, size_t hi, int) {
     for (size_t s = lo; s < hi; s++)
       cls[s] = s < nd ? classify_dev(plan.dev[s], latency) : classify_gdev(plan.gdev[s - nd], latency, lds_dirs_max);
   });
+  tm.mark("classes");
   for (size_t s = 0; s < nd + ng; s++)  // the first problem in batch order that the engine rejects
     if (cls[s].err) return bad(ctx, cls[s].err);
   // pair-arena and direction-scratch offsets in problem order (single / end gaps, then genome gaps)
@@ -1250,6 +1290,7 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     pair_off += c.pair;
     gdirs_off += c.gdirs;
   }
+  tm.mark("offsets");
   // members per class in problem order (the classes in key order, as the tuple map kept them)
   std::vector<uint64_t> keys;
   {
@@ -1291,6 +1332,7 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
       for (size_t s = lo; s < hi; s++) members[ci[s]][at[t][ci[s]]++] = (int)(s < nd ? s : s - nd);
     });
   }
+  tm.mark("members");
   for (size_t k = 0; k < K; k++) {
     PlanCore::Launch L;
     const uint64_t key = keys[k];
@@ -1306,76 +1348,96 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
       for (int id : ids) m = std::max(m, cls[g ? nd + (size_t)id : (size_t)id].need);
       L.lds = m;
     }
-    // longest problems first, so the tail of the launch is short work
-    if (!g) {
-      plan_stable_sort(ids, T, [&](int a, int b) {
-        return (size_t)plan.dev[a].glength * (plan.dev[a].lband + plan.dev[a].uband + 1) >
-               (size_t)plan.dev[b].glength * (plan.dev[b].lband + plan.dev[b].uband + 1);
-      });
-      L.first = (int)plan.order.size();
-      plan.order.insert(plan.order.end(), ids.begin(), ids.end());
-    } else {
-      auto work = [&](int a) {
-        const DevGenomeProblem& d = plan.gdev[a];
-        return (size_t)(d.glengthL + d.glengthR) * (size_t)(2 * d.lbandL + d.ubandL + d.ubandR + 2);
-      };
-      plan_stable_sort(ids, T, [&](int a, int b) { return work(a) > work(b); });
-      L.first = (int)plan.gorder.size();
-      plan.gorder.insert(plan.gorder.end(), ids.begin(), ids.end());
-    }
-    // work estimate: fill wave-columns (a packed wave fills 64/S problems at once)
+    // work estimate: fill wave-columns (a packed wave fills 64/S problems at once); the class's longest
+    // problem (span), and for the packed kernels the largest glength / fill steps -- one pass over the
+    // members in problem order (threads for the large classes; sums and maxima need no order)
     L.work = 0.0;
     L.span = 0.0;
     L.extra = 0;
     L.gdirs_offset = 0;
-    if (L.kind == PlanCore::kSx) {  // per wave: 4 direction words per fill step
-      int smax = 0;
-      for (int id : ids)
-        smax = std::max(smax, steps_sx(plan.dev[id].rlength, plan.dev[id].lband, plan.dev[id].uband, L.R));
-      L.extra = (size_t)smax * 32u;
-      L.dirs_lds = false;
-      L.gdirs_offset = gdirs_off;
-      const size_t nblocks = ((size_t)L.count + (64 / L.R) - 1) / (64 / L.R);
-      gdirs_off += (nblocks * L.extra + 255) & ~(size_t)255;
-    }
-    if (L.kind == PlanCore::kDpx) {
+    {
+      const int TT = ids.size() >= 65536 ? T : 1;
+      std::vector<double> tw(TT, 0.0), ts(TT, 0.0);
+      std::vector<int> tg(TT, 0);
+      const int kind = L.kind, R = L.R;
+      plan_parallel(ids.size(), TT, [&](size_t lo, size_t hi, int t) {
+        double w = 0.0, sp = 0.0;
+        int gm = 0;
+        for (size_t x = lo; x < hi; x++) {
+          const int id = ids[x];
+          double one;
+          if (kind == PlanCore::kGenomeGap) {
+            const DevGenomeProblem& d = plan.gdev[id];
+            one = (double)std::max(d.glengthL, d.glengthR) * R + d.rlength;
+          } else if (kind == PlanCore::kUxg) {
+            const DevGenomeProblem& d = plan.gdev[id];
+            one = (double)(d.glengthL + d.glengthR + 2 * d.rlength) + 4.0 * d.rlength;
+          } else if (kind == PlanCore::kUxe) {
+            const DevProblem& d = plan.dev[id];
+            one = (double)(d.rlength + d.glength) + 0.5 * d.rlength;
+          } else {
+            const DevProblem& d = plan.dev[id];
+            if (kind == PlanCore::kSx) {
+              const int st = steps_sx(d.rlength, d.lband, d.uband, R);
+              gm = std::max(gm, st);
+              one = (double)st * R / 64.0 + 0.25 * (d.rlength + d.glength);
+            } else {
+              gm = std::max(gm, (int)d.glength);
+              one = (double)d.glength * (kind == PlanCore::kDpx ? R / 64.0 : R) + 0.25 * (d.rlength + d.glength);
+            }
+          }
+          w += one;
+          // a packed wave's problems fill side by side: its latency is one problem's columns
+          sp = std::max(sp, (kind == PlanCore::kDpx || kind == PlanCore::kSx) ? one * 64.0 / R : one);
+        }
+        tw[t] = w;
+        ts[t] = sp;
+        tg[t] = gm;
+      });
       int gmax = 0;
-      for (int id : ids) gmax = std::max(gmax, (int)plan.dev[id].glength);
-      L.extra = lds_dirs_dpx(gmax);
-      // direction words in LDS while the workgroup stays small; beyond that they go to an
-      // L2-resident scratch so that more problems are resident per CU
-      L.dirs_lds = L.extra + L.lds * (64 / L.R) <= dpx_lds_dirs_max();
-      if (!L.dirs_lds) {
+      for (int t = 0; t < TT; t++) {
+        L.work += tw[t];
+        L.span = std::max(L.span, ts[t]);
+        gmax = std::max(gmax, tg[t]);
+      }
+      if (L.kind == PlanCore::kSx) {  // per wave: 4 direction words per fill step (gmax: the largest step count)
+        L.extra = (size_t)gmax * 32u;
+        L.dirs_lds = false;
         L.gdirs_offset = gdirs_off;
         const size_t nblocks = ((size_t)L.count + (64 / L.R) - 1) / (64 / L.R);
         gdirs_off += (nblocks * L.extra + 255) & ~(size_t)255;
       }
-    }
-    for (int id : ids) {
-      const double w0 = L.work;
-      if (L.kind == PlanCore::kGenomeGap) {
-        const DevGenomeProblem& d = plan.gdev[id];
-        L.work += (double)std::max(d.glengthL, d.glengthR) * L.R + d.rlength;
-      } else if (L.kind == PlanCore::kUxg) {
-        const DevGenomeProblem& d = plan.gdev[id];
-        L.work += (double)(d.glengthL + d.glengthR + 2 * d.rlength) + 4.0 * d.rlength;
-      } else if (L.kind == PlanCore::kUxe) {
-        const DevProblem& d = plan.dev[id];
-        L.work += (double)(d.rlength + d.glength) + 0.5 * d.rlength;
-      } else {
-        const DevProblem& d = plan.dev[id];
-        if (L.kind == PlanCore::kSx)
-          L.work += (double)steps_sx(d.rlength, d.lband, d.uband, L.R) * L.R / 64.0 + 0.25 * (d.rlength + d.glength);
-        else
-          L.work += (double)d.glength * (L.kind == PlanCore::kDpx ? L.R / 64.0 : L.R) + 0.25 * (d.rlength + d.glength);
+      if (L.kind == PlanCore::kDpx) {
+        L.extra = lds_dirs_dpx(gmax);
+        // direction words in LDS while the workgroup stays small; beyond that they go to an
+        // L2-resident scratch so that more problems are resident per CU
+        L.dirs_lds = L.extra + L.lds * (64 / L.R) <= dpx_lds_dirs_max();
+        if (!L.dirs_lds) {
+          L.gdirs_offset = gdirs_off;
+          const size_t nblocks = ((size_t)L.count + (64 / L.R) - 1) / (64 / L.R);
+          gdirs_off += (nblocks * L.extra + 255) & ~(size_t)255;
+        }
       }
-      // a packed wave's problems fill side by side: its latency is one problem's columns
-      const double one = (L.kind == PlanCore::kDpx || L.kind == PlanCore::kSx) ? (L.work - w0) * 64.0 / L.R : L.work - w0;
-      L.span = std::max(L.span, one);
+    }
+    // longest problems first, so the tail of the launch is short work
+    if (!g) {
+      plan_sort_desc(ids, T, [&](int a) {
+        return (uint64_t)plan.dev[a].glength * (uint64_t)(plan.dev[a].lband + plan.dev[a].uband + 1);
+      });
+      L.first = (int)plan.order.size();
+      plan.order.insert(plan.order.end(), ids.begin(), ids.end());
+    } else {
+      plan_sort_desc(ids, T, [&](int a) {
+        const DevGenomeProblem& d = plan.gdev[a];
+        return (uint64_t)(d.glengthL + d.glengthR) * (uint64_t)(2 * d.lbandL + d.ubandL + d.ubandR + 2);
+      });
+      L.first = (int)plan.gorder.size();
+      plan.gorder.insert(plan.gorder.end(), ids.begin(), ids.end());
     }
     L.stream = 0;
     plan.launches.push_back(L);
   }
+  tm.mark("launches");
   // Independent classes share the GPU: longest-processing-time-first over the caller's stream and
   // the three side streams, so that LDS-heavy and LDS-light classes are co-resident on the CUs and
   // no launch's drain leaves the chip idle.  Launches are then kept in issue order (per stream,
@@ -1421,91 +1483,77 @@ static int build_plan(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int
   const int T = plan_threads((size_t)n + (size_t)ngenome);
   std::vector<const char*> why(2 * T, nullptr);
   std::vector<int> errat(2 * T, INT32_MAX), errcode(2 * T, 0);
-  // single and end gaps: convert in parallel, then the GPU ones compacted in order
-  {
-    std::vector<DevProblem> tmp(n);
-    std::vector<unsigned char> gpu(n, 0);
+  // single and end gaps, then genome gaps: which run on the GPU (threads), the slots by a prefix count, then
+  // the descriptors converted again straight into their slots (threads)
+  auto compact = [&](int m, int err_base, auto&& conv, auto& dev, auto& dev_index, auto& dev_problem) -> int {
     std::vector<size_t> cnt(T, 0);
-    plan_parallel((size_t)n, T, [&](size_t lo, size_t hi, int t) {
+    HostArray<unsigned char> gpu(m);
+    plan_parallel((size_t)m, T, [&](size_t lo, size_t hi, int t) {
+      size_t c = 0;
       for (size_t i = lo; i < hi; i++) {
         int err = 0;
         const char* w = nullptr;
-        const int g = (int)i < nsingle ? convert_single(ctx, singles[i], results[i], tmp[i])
-                                       : convert_end(ctx, ends[i - nsingle], results[i], tmp[i], &err, &w);
+        const int g = conv(i, &err, &w, nullptr);
         if (err) {
-          errat[t] = (int)i;
-          errcode[t] = err;
-          why[t] = w;
+          errat[err_base + t] = (int)i;
+          errcode[err_base + t] = err;
+          why[err_base + t] = w;
           return;
         }
-        results[i].pair_offset = 0;
         gpu[i] = (unsigned char)g;
-        cnt[t] += (size_t)g;
+        c += (size_t)g;
       }
+      cnt[t] = c;
     });
     for (int t = 0; t < T; t++)
-      if (errat[t] != INT32_MAX) return why[t] ? bad(ctx, why[t]) : errcode[t];
-    size_t total = 0;
+      if (errat[err_base + t] != INT32_MAX) return why[err_base + t] ? bad(ctx, why[err_base + t]) : errcode[err_base + t];
     std::vector<size_t> at(T);
+    size_t total = 0;
     for (int t = 0; t < T; t++) {
       at[t] = total;
       total += cnt[t];
     }
-    plan.dev_index.assign(n, -1);
-    plan.dev_problem.resize(total);
-    plan.dev.resize(total);
-    plan_parallel((size_t)n, T, [&](size_t lo, size_t hi, int t) {
+    dev_index.resize(m);
+    dev_problem.resize(total);
+    dev.resize(total);
+    plan_parallel((size_t)m, T, [&](size_t lo, size_t hi, int t) {
       size_t k = at[t];
-      for (size_t i = lo; i < hi; i++)
-        if (gpu[i]) {
-          plan.dev_index[i] = (int)k;
-          plan.dev_problem[k] = (int)i;
-          plan.dev[k++] = tmp[i];
+      for (size_t i = lo; i < hi; i++) {
+        if (!gpu[i]) {
+          dev_index[i] = -1;
+          continue;
         }
-    });
-  }
-  {
-    std::vector<DevGenomeProblem> tmp(ngenome);
-    std::vector<unsigned char> gpu(ngenome, 0);
-    std::vector<size_t> cnt(T, 0);
-    plan_parallel((size_t)ngenome, T, [&](size_t lo, size_t hi, int t) {
-      for (size_t j = lo; j < hi; j++) {
         int err = 0;
         const char* w = nullptr;
-        const int g = convert_genome(ctx, genomes[j], gresults[j], tmp[j], &err, &w);
-        if (err) {
-          errat[T + t] = (int)j;
-          errcode[T + t] = err;
-          why[T + t] = w;
-          return;
-        }
-        gpu[j] = (unsigned char)g;
-        cnt[t] += (size_t)g;
+        conv(i, &err, &w, &dev[k]);
+        dev_index[i] = (int)k;
+        dev_problem[k++] = (int)i;
       }
     });
-    for (int t = 0; t < T; t++)
-      if (errat[T + t] != INT32_MAX) return why[T + t] ? bad(ctx, why[T + t]) : errcode[T + t];
-    size_t total = 0;
-    std::vector<size_t> at(T);
-    for (int t = 0; t < T; t++) {
-      at[t] = total;
-      total += cnt[t];
-    }
-    plan.gdev_index.assign(ngenome, -1);
-    plan.gdev_problem.resize(total);
-    plan.gdev.resize(total);
-    plan_parallel((size_t)ngenome, T, [&](size_t lo, size_t hi, int t) {
-      size_t k = at[t];
-      for (size_t j = lo; j < hi; j++)
-        if (gpu[j]) {
-          plan.gdev_index[j] = (int)k;
-          plan.gdev_problem[k] = (int)j;
-          plan.gdev[k++] = tmp[j];
-        }
-    });
-  }
+    return GMAPDP_OK;
+  };
+  int rc = compact(
+      n, 0,
+      [&](size_t i, int* err, const char** w, DevProblem* out) {
+        DevProblem scratch;
+        DevProblem& d = out ? *out : scratch;
+        const int g = (int)i < nsingle ? convert_single(ctx, singles[i], results[i], d)
+                                       : convert_end(ctx, ends[i - nsingle], results[i], d, err, w);
+        results[i].pair_offset = 0;
+        return g;
+      },
+      plan.dev, plan.dev_index, plan.dev_problem);
+  if (rc) return rc;
+  rc = compact(
+      ngenome, T,
+      [&](size_t j, int* err, const char** w, DevGenomeProblem* out) {
+        DevGenomeProblem scratch;
+        return convert_genome(ctx, genomes[j], gresults[j], out ? *out : scratch, err, w);
+      },
+      plan.gdev, plan.gdev_index, plan.gdev_problem);
+  if (rc) return rc;
   tm.mark("convert");
-  int rc = classify(ctx, plan);
+  rc = classify(ctx, plan);
   if (rc) return rc;
   tm.mark("classify");
   for (size_t s = 0; s < plan.dev.size(); s++) results[plan.dev_problem[s]].pair_offset = plan.dev[s].pair_offset;
@@ -2424,6 +2472,80 @@ int gmapdp_plan_run_launch(gmapdp_ctx* ctx, const gmapdp_plan* plan, int li, con
   return plan_run_launch(ctx, plan, li, d_qseq, d_qseq_uc, d_results, d_pairs, stream, true);
 }
 
+// Host side of the compact pair stream: problem i's ops at stream[offsets[i], offsets[i + 1]) back to its
+// npairs[i] records at out[pair_offsets[i]] (threads over the problems).  GMAPDP_EINVAL when a problem's
+// ops do not decode to exactly its records and bytes.
+int gmapdp_expand_pairs(const uint8_t* stream, const uint64_t* offsets, int n, const int32_t* npairs,
+                        const int64_t* pair_offsets, gmapdp_pair* out, int nthreads) {
+  if (n < 0 || (n && (!stream || !offsets || !npairs || !pair_offsets || !out))) return GMAPDP_EINVAL;
+  static const char nt[4] = {'A', 'C', 'G', 'T'}, cp[4] = {'*', '|', ' ', ':'};
+  const int T = nthreads > 0 ? nthreads : plan_threads((size_t)n * 64);
+  std::vector<int> bad_at(T, -1);
+  plan_parallel((size_t)n, T, [&](size_t lo, size_t hi, int t) {
+    for (size_t i = lo; i < hi; i++) {
+      const uint8_t* p = stream + offsets[i];
+      const uint8_t* end = stream + offsets[i + 1];
+      gmapdp_pair* o = out + pair_offsets[i];
+      int k = 0;
+      const int m = std::max(npairs[i], 0);
+      while (k < m && p < end) {
+        if (*p == 0x02) {
+          if (end - p < 17) break;
+          std::memcpy(&o[k++], p + 1, 16);
+          p += 17;
+          continue;
+        }
+        if (*p != 0x01 || end - p < 13) break;
+        int32_t q, g;
+        std::memcpy(&q, p + 1, 4);
+        std::memcpy(&g, p + 5, 4);
+        const int dq = (int8_t)p[9], dg = (int8_t)p[10];
+        const int len = p[11] | (p[12] << 8);
+        p += 13;
+        for (int r = 0; r < len && k < m && p < end; r++, k++) {
+          gmapdp_pair& x = o[k];
+          x.querypos = q + r * dq;
+          x.genomepos = g + r * dg;
+          x.jump = 0;
+          if (*p == 0xFF) {
+            std::memcpy(&x.cdna, p + 1, 4);
+            p += 5;
+          } else {
+            const uint8_t b = *p++;
+            x.cdna = nt[b & 3];
+            x.genome = x.genomealt = nt[(b >> 2) & 3];
+            x.comp = cp[(b >> 4) & 3];
+          }
+        }
+      }
+      if (k != m || p != end) {
+        bad_at[t] = (int)i;
+        return;
+      }
+    }
+  });
+  for (int t = 0; t < T; t++)
+    if (bad_at[t] >= 0) return GMAPDP_EINVAL;
+  return GMAPDP_OK;
+}
+
+// The compact pair stream (pc_kernel.hip): the plan's GPU problems in dev-slot order, then its genome gaps.
+size_t gmapdp_plan_compact_bound(const gmapdp_plan* plan) {
+  return plan ? 17 * plan->in.pair_capacity + 64 : 0;
+}
+int gmapdp_plan_compact_pairs(gmapdp_ctx* ctx, const gmapdp_plan* plan, const gmapdp_result* d_results,
+                              const gmapdp_pair* d_pairs, uint8_t* d_out, uint64_t* d_offsets, void* stream) {
+  if (!ctx || !plan || !d_offsets || (!plan->in.dev.empty() && !d_results)) return GMAPDP_EINVAL;
+  if (!plan->in.gdev.empty() && !plan->d_gresults) return bad(ctx, "genome-gap results not bound");
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  const hipError_t e = launch_pc((const unsigned char*)d_results, (int)plan->in.dev.size(), (int)sizeof(gmapdp_result),
+                                 (const unsigned char*)plan->d_gresults, (int)plan->in.gdev.size(),
+                                 (int)sizeof(gmapdp_genome_result), d_pairs, (unsigned long long*)d_offsets,
+                                 (unsigned char*)d_out, s);
+  return e == hipSuccess ? GMAPDP_OK : fail(ctx, GMAPDP_ELAUNCH, "pair compaction: %s", e);
+}
+
 int gmapdp_plan_run_launch_kernel(gmapdp_ctx* ctx, const gmapdp_plan* plan, int li, const char* d_qseq,
                                   const char* d_qseq_uc, gmapdp_result* d_results, gmapdp_pair* d_pairs, void* stream) {
   return plan_run_launch(ctx, plan, li, d_qseq, d_qseq_uc, d_results, d_pairs, stream, false);
@@ -2463,7 +2585,8 @@ static size_t oligo_diag_cap(const gmapdp_oligo_problem& p) {
 static int oligo_distinct(const char* q, int qlen, std::vector<uint32_t>& bm) {
   int n = 0, in_counter = 0;
   uint32_t oligo = 0;
-  std::vector<uint32_t> touched;
+  thread_local std::vector<uint32_t> touched;
+  touched.clear();
   for (int i = 0; i < qlen; i++) {
     in_counter++;
     switch (q[i]) {
@@ -2639,24 +2762,42 @@ static int oligo_plan_build(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problem
   *plan = nullptr;
   if (!ctx->d_genome) return GMAPDP_ENOGENOME;
   (void)hipSetDevice(ctx->device);
-  std::vector<uint32_t> bm(2048, 0u);
   std::vector<DevOligoProblem> dev(n);
   std::vector<size_t> slots(n), tcap(n), dcap(n);
   size_t toff = 0;
   static const int kBuckets[] = {1024, 2048, 4096, 8192, 16384};  // launch classes by LDS
   std::map<int, std::vector<int>> classes;
   const char* ev = std::getenv("GMAPDP_OLIGO_POOL_SLOTS");  // tests: a small pool forces the sequential walk
+  // each query's distinct 8-mers (plan_threads() host threads: the sweep over a 10 000-read block's 15 850
+  // queries was most of a stage-2 plan's host time), and the first problem the engine rejects
+  std::vector<int> distinct(n, 0);
+  std::vector<const char*> rej(n, nullptr);
+  const int T = plan_threads((size_t)n * 128);
+  plan_parallel((size_t)n, T, [&](size_t lo, size_t hi, int) {
+    std::vector<uint32_t> bm(2048, 0u);
+    for (size_t i = lo; i < hi; i++) {
+      const gmapdp_oligo_problem& p = problems[i];
+      if (p.querylength <= 8) {
+        rej[i] = "stage-2 seeding needs querylength > 8 (Oligoindex_set_inquery)";
+        continue;
+      }
+      if (p.qoff < 0 || (size_t)p.qoff + (size_t)p.querylength > qbytes) {
+        rej[i] = "query outside the arena";
+        continue;
+      }
+      distinct[i] = oligo_distinct(qseq_uc + p.qoff, p.querylength, bm);
+    }
+  });
   for (int i = 0; i < n; i++) {
     const gmapdp_oligo_problem& p = problems[i];
-    if (p.querylength <= 8) return bad(ctx, "stage-2 seeding needs querylength > 8 (Oligoindex_set_inquery)");
-    if (p.qoff < 0 || (size_t)p.qoff + (size_t)p.querylength > qbytes) return bad(ctx, "query outside the arena");
+    if (rej[i]) return bad(ctx, rej[i]);
     const uint64_t win = oligo_window(p);
     if (win > 0) {  // the last 8-mer start's half-word and the one after it (window8)
       const uint64_t lpl = (uint64_t)p.chroffset + p.chrend + (p.plusp ? 0 : 1) - 8;
       const uint64_t h = (lpl >> 4) + 1;
       if (3 * (h >> 1) + 1 >= ctx->genome_words) return bad(ctx, "stage-2 window past the genome");
     }
-    const int U = oligo_distinct(qseq_uc + p.qoff, p.querylength, bm);
+    const int U = distinct[i];
     if (U > kOligoMaxDistinct) return bad(ctx, "query with more than 16384 distinct 8-mers");
     int umax = kBuckets[0];
     for (int b : kBuckets)

@@ -293,6 +293,11 @@ def load_library(path=LIB_PATH):
         "gmapdp_mixed_batch": (C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p, C.c_size_t, P(Mixed)]),
         "gmapdp_maxent_available": (C.c_int, [C.c_char_p, C.c_size_t]),
         "gmapdp_plan_bind_genome_maxent": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+        "gmapdp_plan_compact_bound": (C.c_size_t, [C.c_void_p]),
+        "gmapdp_plan_compact_pairs": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                C.c_void_p, C.c_void_p]),
+        "gmapdp_expand_pairs": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                          C.c_int]),
         "gmapdp_maxent_sites": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
         "gmapdp_microexon_plan_create": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                                    C.c_size_t, P(C.c_void_p)]),
@@ -1046,3 +1051,19 @@ def decode_pairs(pairs, offset, n, dpi):
             lst.append((int(rec["querypos"]), int(rec["genomepos"]), 0, 0, dpi, rec["cdna"], rec["comp"],
                         rec["genome"], rec["genomealt"], 0))
     return lst
+
+
+def expand_pairs(stream, offsets, npairs, pair_offsets, capacity, nthreads=0):
+    """gmapdp_expand_pairs (host only): the compact pair stream back to gmapdp_pair records; a pair arena of
+    `capacity` records with problem i's npairs[i] records at pair_offsets[i]."""
+    lib = load_library()
+    out = np.zeros(max(int(capacity), 1), dtype=PAIR_DTYPE)
+    st = np.ascontiguousarray(stream, dtype=np.uint8)
+    of = np.ascontiguousarray(offsets, dtype=np.uint64)
+    npc = np.ascontiguousarray(npairs, dtype=np.int32)
+    po = np.ascontiguousarray(pair_offsets, dtype=np.int64)
+    rc = lib.gmapdp_expand_pairs(st.ctypes.data, of.ctypes.data, len(npc), npc.ctypes.data, po.ctypes.data,
+                                 out.ctypes.data, int(nthreads))
+    if rc != 0:
+        raise GmapdpError("gmapdp_expand_pairs: the stream does not decode to the records (%d)" % rc)
+    return out

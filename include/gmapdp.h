@@ -800,6 +800,20 @@ int gmapdp_plan_dev_index (const gmapdp_plan *plan, int i);
 int gmapdp_plan_nlaunches (const gmapdp_plan *plan);
 int gmapdp_plan_run (gmapdp_ctx *ctx, const gmapdp_plan *plan, const char *d_qseq, const char *d_qseq_uc,
                      gmapdp_result *d_results, gmapdp_pair *d_pairs, void *stream);
+/* The compact pair stream (run-length ops plus one character code per record; the host expands
+ * it into the same records -- Pair_T lists -- with gmapdp_expand_pairs).  After gmapdp_plan_run on `stream`:
+ * each GPU problem's list (dev slots 0..gmapdp_plan_gpu_problems - 1, then the genome gaps' slots) becomes a
+ * byte stream; d_offsets (gpu problems + genome gpu problems + 1 uint64, device) receives the exclusive
+ * offsets and the total.  d_out NULL: the offsets only (to size a copy); else at least
+ * gmapdp_plan_compact_bound bytes.  Stream format: pc_kernel.hip. */
+size_t gmapdp_plan_compact_bound (const gmapdp_plan *plan);
+int gmapdp_plan_compact_pairs (gmapdp_ctx *ctx, const gmapdp_plan *plan, const gmapdp_result *d_results,
+                               const gmapdp_pair *d_pairs, uint8_t *d_out, uint64_t *d_offsets, void *stream);
+/* Host: problem i's ops (stream[offsets[i], offsets[i + 1])) back to its npairs[i] records at
+ * out[pair_offsets[i]], on nthreads host threads (0: the plan builders' default).  GMAPDP_EINVAL when a
+ * problem's ops do not decode to exactly its records. */
+int gmapdp_expand_pairs (const uint8_t *stream, const uint64_t *offsets, int n, const int32_t *npairs,
+                         const int64_t *pair_offsets, gmapdp_pair *out, int nthreads);
 /* Per-launch-class access (one kernel launch per class; for profiling). */
 int gmapdp_plan_launch_info (const gmapdp_plan *plan, int li, int *R, int *dirs_lds, int *count, size_t *lds);
 /* Launch classes are spread over the caller's stream (0) and three side streams (1..3),

@@ -140,3 +140,24 @@ def test_genome_splice_sites_match_oracle():
         o = int(probs[i]["prob_offset"])
         got = list(zip(pos[o:o + len(sl) + len(sr)].tolist(), mod[o:o + len(sl) + len(sr)].tolist()))
         assert got == sl + sr
+
+
+def test_expand_pairs_decodes_the_stream_format():
+    """gmapdp_expand_pairs (host only, no GPU) on a hand-made stream of pc_kernel.hip's format: a diagonal RUN
+    with coded and escaped records, an indel RUN, a RAW gap holder; a truncated stream is refused."""
+    import struct
+    import numpy as np
+    import gmapdp
+    run = lambda q, g, dq, dg, n: struct.pack("<BiibbH", 1, q, g, dq, dg, n)  # noqa: E731
+    code = lambda c, g, m: bytes([("ACGT".index(c)) | ("ACGT".index(g) << 2) | ("*| :".index(m) << 4)])  # noqa: E731
+    s = run(10, 100, 1, 1, 3) + code("A", "A", "*") + code("C", "G", " ") + b"\xff" + b"n- N"
+    s += run(13, 103, 1, 0, 2) + b"\xff" + b"A- A" + b"\xff" + b"C- C"
+    s += b"\x02" + struct.pack("<iii", -1, -1, 250) + b" > ."
+    stream = np.frombuffer(s, dtype=np.uint8)
+    out = gmapdp.expand_pairs(stream, [0, len(s)], [6], [2], 8)
+    got = [(int(r["querypos"]), int(r["genomepos"]), int(r["jump"]), bytes(r["cdna"] + r["comp"] + r["genome"] +
+            r["genomealt"])) for r in out[2:8]]
+    assert got == [(10, 100, 0, b"A*AA"), (11, 101, 0, b"C GG"), (12, 102, 0, b"n- N"), (13, 103, 0, b"A- A"),
+                   (14, 103, 0, b"C- C"), (-1, -1, 250, b" > .")], got
+    with pytest.raises(gmapdp.GmapdpError):
+        gmapdp.expand_pairs(stream[:-3], [0, len(s) - 3], [6], [2], 8)

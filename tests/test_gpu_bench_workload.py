@@ -244,7 +244,7 @@ def test_gpu_bench_configs4_block_sample():
     assert sum(1 for r in got["oligo"] if r[0] > 0) > 0.8 * sizes["oligo"]
 
 
-def _dp_plan_block(eng, d):
+def _dp_plan_block(eng, d, compact=False):
     """bench.py's DP path over block d: gmapdp_plan_create_all (single, end and genome gaps), the device
     MaxEnt bound (gmapdp_plan_bind_genome_maxent), gmapdp_plan_run; the microexon plan (search, device
     MaxEnt, finish).  Returns {family: (results in problem order, the pair arena)}."""
@@ -299,6 +299,19 @@ def _dp_plan_block(eng, d):
             out["single"] = (res[:len(sp)], pairs)
             out["end"] = (res[len(sp):], pairs)
             out["genome"] = (gres, pairs)
+            if compact:  # the compact pair stream, expanded on the host (gmapdp_plan_compact_pairs / _expand)
+                nprob = ngpu + nggpu
+                d_off = dbuf(8 * (nprob + 1))
+                eng._check(lib.gmapdp_plan_compact_pairs(eng.h, plan, d_res, d_pairs, None, d_off, None), "compact")
+                assert hip.hipDeviceSynchronize() == 0
+                offs = down(np.zeros(nprob + 1, dtype=np.uint64), d_off)
+                d_out = dbuf(int(offs[-1]))
+                eng._check(lib.gmapdp_plan_compact_pairs(eng.h, plan, d_res, d_pairs, d_out, d_off, None), "compact")
+                assert hip.hipDeviceSynchronize() == 0
+                stream = down(np.zeros(max(int(offs[-1]), 1), dtype=np.uint8), d_out)
+                npc = np.concatenate([dres["npairs"][:ngpu], dgres["npairs"][:nggpu]])
+                poff = np.concatenate([dres["pair_offset"][:ngpu], dgres["pair_offset"][:nggpu]]).astype(np.int64)
+                out["compact"] = (gmapdp.expand_pairs(stream, offs, npc, poff, cap), npc, poff, int(offs[-1]))
         finally:
             lib.gmapdp_plan_destroy(plan)
         if len(mp):
@@ -365,10 +378,18 @@ def _dp_every_call(genome, d, simd):
     eng = gmapdp.Engine(0)
     eng.set_genome(blocks=genome.blocks, length=genome.length)
     try:
-        got = _dp_plan_block(eng, d)
+        got = _dp_plan_block(eng, d, compact=True)
     finally:
         eng.close()
     _progress("engine: the block's DP plan%s" % (" (SIMD semantics)" if simd else ""))
+    # the compact pair stream expands to exactly the records the kernels wrote (every GPU problem's range)
+    exp_pairs, npc, poff, nbytes = got["compact"]
+    pairs = got["single"][1]
+    cnt = np.maximum(npc.astype(np.int64), 0)
+    idx = np.repeat(poff, cnt) + (np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt))
+    assert np.array_equal(exp_pairs[idx], pairs[idx]), "the compact pair stream does not expand to the records"
+    _progress("compact stream: %d records in %d bytes (%.2f B per record)" % (len(idx), nbytes, nbytes / max(len(idx), 1)))
+    assert nbytes < 0.25 * 16 * len(idx)
     exp = _oracle_dp_block(genome, d, fams, simd=simd)
     bad = {}
     for fam in fams:
