@@ -484,6 +484,7 @@ def main():
     # ---- per block: device arenas and plans (host: bands, launch classes, offsets) ----
     B = []
     t_plan = t_oplan = 0.0
+    plan_ms, oplan_ms = [], []  # per block
     for bi, d in zip(mine, data):
         sp, ep, gp, op, mp = d["single"], d["end"], d["genome"], d["oligo"], d["microexon"]
         if args.simd:
@@ -504,6 +505,7 @@ def main():
                                               gp.ctypes.data, len(gp), blk["host_res"].ctypes.data,
                                               blk["host_gres"].ctypes.data, C.byref(plan)), "gmapdp_plan_create_all")
         t_plan += time.perf_counter() - t0
+        plan_ms.append((time.perf_counter() - t0) * 1e3)
         blk["plan"] = plan
         # Stage2_compute per read (gmap.c:1208): seeding + chaining, GMAP's defaults (splicing on,
         # maxintronlen 500000)
@@ -520,6 +522,7 @@ def main():
                                                      d["oq"].ctypes.data, len(d["oq"]), C.byref(oplan)),
                        "gmapdp_stage2_plan_create")
         t_oplan += time.perf_counter() - t0
+        oplan_ms.append((time.perf_counter() - t0) * 1e3)
         blk["oplan"] = oplan
         # Dynprog_microexon_int per read (stage3.c:9664) over genome-gap gaps: search + choice
         mplan = None
@@ -958,14 +961,14 @@ def main():
         cdown = nbytes + other
         h_c = torch.empty(cdown, dtype=torch.uint8, pin_memory=True)
         g_c = torch.empty(cdown, dtype=torch.uint8, device=dev)
-        dms = []
+        down_ms = []
         for _ in range(4):
             e0, e1 = mk()
             e0.record(stream)
             h_c.copy_(g_c, non_blocking=True)
             e1.record(stream)
             torch.cuda.synchronize()
-            dms.append(e0.elapsed_time(e1))
+            down_ms.append(e0.elapsed_time(e1))
         stream_host = d_cmp[:max(nbytes, 1)].cpu().numpy()
         res_h, gres_h = fetch_results(b)
         npc = np.concatenate([res_h["npairs"], gres_h["npairs"]]).astype(np.int32)
@@ -980,7 +983,7 @@ def main():
         del h_c, g_c, d_cmp, allp, exp
         compact = {"records": int(cnt.sum()), "stream_bytes": nbytes, "bytes_per_record": nbytes / max(int(cnt.sum()), 1),
                    "compact_kernels_ms": float(np.median(cms[1:])), "pcie_bytes_down": cdown,
-                   "pcie_down_ms": float(np.median(dms[1:])), "pcie_up_ms": up_ms,
+                   "pcie_down_ms": float(np.median(down_ms[1:])), "pcie_up_ms": up_ms,
                    "host_expand_ms_16_threads": expand_ms, "expanded_equals_records": same}
         compact["pcie_ms_per_step"] = compact["pcie_up_ms"] + compact["compact_kernels_ms"] + compact["pcie_down_ms"]
         progress("compact pair stream: %d records in %d bytes, expanded %s" % (compact["records"], nbytes,
@@ -1066,7 +1069,11 @@ def main():
                           "together": ms_step},
         "launch_classes": sorted(({"kernel": n, "dispatches": e[1], "ms_per_step": round(e[0] / args.steps, 4)}
                                   for n, e in per_kernel.items()), key=lambda x: -x["ms_per_step"]),
-        "host": {"plan_ms_per_block": t_plan * 1e3 / len(B), "stage2_plan_ms_per_block": t_oplan * 1e3 / len(B),
+        # the host's per-block planning (gmapdp_plan_create_all, gmapdp_stage2_plan_create: 16 host threads),
+        # the median block's (the first block also pays the process's first device allocations: listed apart)
+        "host": {"plan_ms_per_block": float(np.median(plan_ms)), "stage2_plan_ms_per_block": float(np.median(oplan_ms)),
+                 "plan_ms_first_block": plan_ms[0], "stage2_plan_ms_first_block": oplan_ms[0],
+                 "plan_threads": int(os.environ.get("GMAPDP_PLAN_THREADS", "16")),
                  "setup_s": t_gen},
         "checks": {"pairs_per_read": checks["pairs"] / checks["reads"],
                    "genome_gaps_bridged": checks["genome_gaps_bridged"],

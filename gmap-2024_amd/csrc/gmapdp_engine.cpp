@@ -219,7 +219,9 @@ static void build_tables(Tables& T, int mode) {
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
-  hipError_t ensure(size_t bytes) {
+  // tight: 1/8 headroom instead of doubling (the stage-2 plans' sizing arenas, tens of GB, about the same
+  // size for every block of a run)
+  hipError_t ensure(size_t bytes, bool tight = false) {
     if (bytes <= cap) return hipSuccess;
     if (p) (void)hipFree(p);
     p = nullptr;
@@ -227,7 +229,7 @@ struct DevBuf {
     // doubling: a hipFree waits for the whole device (every stream of every context), so a buffer
     // should grow a handful of times per process, not per batch
     size_t want = std::max(bytes, (size_t)4096);
-    want = want + want;
+    want = tight ? want + want / 8 : want + want;
     hipError_t e = hipMalloc(&p, want);
     if (e == hipSuccess) cap = want;
     return e;
@@ -294,6 +296,7 @@ struct gmapdp_ctx {
   DevBuf cprobs, corder, cresults, cscratch;  // Dynprog_cdna_gap batches
   DevBuf sjprobs, sjorder, sjresults, sjseq, sjdirs;  // Dynprog_end5/3_splicejunction batches
   DevBuf oprobs, oresults, oscratch, onpos, omap, otable, odiag, opool, opoolctr;  // stage-2 seeding batches
+  DevBuf onhits;  // stage-2 plans' sizing runs (with otable, odiag and the seeding scratch above)
   DevBuf s2probs, s2results, s2scratch, s2counters, s2paths, s2pairs, s2qseq;  // Stage2_compute batches
   DevBuf mxprobs, mxres, mxcands, mxcnt, mxdirect, mxprobs2, mxpairs;  // Dynprog_microexon_int batches
   std::string err;
@@ -1075,7 +1078,11 @@ struct PlanTimer {
     t0 = t1;
   }
   ~PlanTimer() {
-    if (on) std::fprintf(stderr, "[gmapdp plan timing] %s%s\n", what, line.c_str());
+    if (!on) return;
+    size_t fr = 0, tot = 0;
+    (void)hipMemGetInfo(&fr, &tot);
+    std::fprintf(stderr, "[gmapdp plan timing] %s%s (device free %.1f of %.1f GB)\n", what, line.c_str(), fr * 1e-9,
+                 tot * 1e-9);
   }
 };
 
@@ -1111,48 +1118,46 @@ static void plan_parallel(size_t n, int T, F&& f) {
   f((size_t)0, std::min(n, per), 0);
   for (auto& x : th) x.join();
 }
-// ids sorted by key(id) descending, ties in their current order (a stable sort).  The keys are taken
-// once, in the ids' order (a comparator reading the 88-128-B descriptors of two random problems per
-// comparison spent most of a 10 000-read plan on cache misses); T sorted runs of (key, position) pairs,
-// then pairwise merges.
+// ids ordered longest first by key(id): a stable counting sort on the key quantised to 16 steps per
+// doubling (1 024 buckets, descending), threads over contiguous chunks (per-chunk histograms, then each chunk
+// scatters its ids after the earlier chunks' of the same bucket).  The launch order only steers the tail of a
+// launch, so 6 % key steps are as good as an exact sort; a comparison sort reading two random descriptors
+// per comparison spent most of a 10 000-read plan on cache misses.
+static inline int plan_bucket(uint64_t key) {
+  if (key < 16) return (int)key;
+  const int lg = 63 - __builtin_clzll(key);  // >= 4
+  return std::min(1023, 16 * (lg - 3) + (int)((key >> (lg - 4)) & 15));
+}
 template <typename KF>
 static void plan_sort_desc(std::vector<int>& ids, int T, KF key) {
   const size_t n = ids.size();
   if (n < 2) return;
-  std::vector<std::pair<uint64_t, uint32_t>> kv(n);  // (~key, position): ascending = key descending, stable
-  plan_parallel(n, n >= 65536 ? T : 1, [&](size_t lo, size_t hi, int) {
-    for (size_t i = lo; i < hi; i++) kv[i] = {~(uint64_t)key(ids[i]), (uint32_t)i};
-  });
-  if (T <= 1 || n < 65536) {
-    std::sort(kv.begin(), kv.end());
-  } else {
-    const size_t per = (n + (size_t)T - 1) / (size_t)T;
-    std::vector<size_t> cut;
-    for (size_t x = 0; x < n; x += per) cut.push_back(x);
-    cut.push_back(n);
-    plan_parallel(cut.size() - 1, (int)cut.size() - 1, [&](size_t lo, size_t hi, int) {
-      for (size_t r = lo; r < hi; r++) std::sort(kv.begin() + cut[r], kv.begin() + cut[r + 1]);
-    });
-    std::vector<std::pair<uint64_t, uint32_t>> tmp(n);
-    while (cut.size() > 2) {
-      const size_t pairs = (cut.size() - 1) / 2;
-      std::vector<size_t> next;
-      plan_parallel(pairs, (int)pairs, [&](size_t lo, size_t hi, int) {
-        for (size_t q = lo; q < hi; q++)
-          std::merge(kv.begin() + cut[2 * q], kv.begin() + cut[2 * q + 1], kv.begin() + cut[2 * q + 1],
-                     kv.begin() + cut[2 * q + 2], tmp.begin() + cut[2 * q]);
-      });
-      for (size_t q = 0; q < pairs; q++) {
-        std::copy(tmp.begin() + cut[2 * q], tmp.begin() + cut[2 * q + 2], kv.begin() + cut[2 * q]);
-        next.push_back(cut[2 * q]);
-      }
-      if ((cut.size() - 1) % 2) next.push_back(cut[cut.size() - 2]);
-      next.push_back(n);
-      cut.swap(next);
+  constexpr int NB = 1024;
+  const int TT = n >= 65536 ? T : 1;
+  std::vector<uint16_t> bk(n);
+  std::vector<std::vector<uint32_t>> hist(TT, std::vector<uint32_t>(NB, 0));
+  const size_t per = (n + (size_t)TT - 1) / (size_t)TT;
+  plan_parallel(n, TT, [&](size_t lo, size_t hi, int t) {
+    std::vector<uint32_t>& h = hist[t];
+    for (size_t i = lo; i < hi; i++) {
+      const int b = NB - 1 - plan_bucket(key(ids[i]));  // descending keys
+      bk[i] = (uint16_t)b;
+      h[b]++;
     }
-  }
+  });
+  std::vector<std::vector<uint32_t>> at(TT, std::vector<uint32_t>(NB));
+  uint32_t run = 0;
+  for (int b = 0; b < NB; b++)
+    for (int t = 0; t < TT; t++) {
+      at[t][b] = run;
+      run += hist[t][b];
+    }
   std::vector<int> out(n);
-  for (size_t i = 0; i < n; i++) out[i] = ids[kv[i].second];
+  plan_parallel(n, TT, [&](size_t lo, size_t hi, int t) {
+    std::vector<uint32_t>& a = at[t];
+    for (size_t i = lo; i < hi; i++) out[a[bk[i]]++] = ids[i];
+  });
+  (void)per;
   ids.swap(out);
 }
 
@@ -1160,17 +1165,17 @@ static void plan_sort_desc(std::vector<int>& ids, int T, KF key) {
 static uint64_t class_key(int kind, int R, int dl, size_t bucket) {
   return ((uint64_t)kind << 48) | ((uint64_t)R << 32) | ((uint64_t)(dl ? 1 : 0) << 31) | (uint64_t)bucket;
 }
-struct ClassOf {
-  uint64_t key = 0;
-  size_t need = 0;      // the problem's LDS bucket (a latency-mode class takes its largest member's)
-  size_t pair = 0;      // pair-arena records reserved
-  size_t gdirs = 0;     // bytes of the global direction scratch, 0: none
-  const char* err = nullptr;
+struct ClassOf {  // (an aggregate: classify_dev / _gdev value-initialise it; arrays of it are left uninitialised)
+  uint64_t key;
+  size_t need;       // the problem's LDS bucket (a latency-mode class takes its largest member's)
+  size_t pair;       // pair-arena records reserved
+  size_t gdirs;      // bytes of the global direction scratch, 0: none
+  const char* err;
 };
 
 // one single / end gap's launch class (classify's rules)
 static ClassOf classify_dev(DevProblem& d, bool latency) {
-  ClassOf c;
+  ClassOf c{};
   c.pair = (size_t)d.rlength + (size_t)d.glength + 2;
   d.dirs_offset = 0;
   const bool nofill = d.kind != kSingle && d.endalign == kQueryendNogaps;
@@ -1228,7 +1233,7 @@ static ClassOf classify_dev(DevProblem& d, bool latency) {
 
 // one genome gap's launch class
 static ClassOf classify_gdev(DevGenomeProblem& d, bool latency, size_t lds_dirs_max) {
-  ClassOf c;
+  ClassOf c{};
   // traceback R (<= r + gR records) + gap holder + traceback L (<= r + gL records)
   c.pair = 2 * (size_t)d.rlength + (size_t)d.glengthL + (size_t)d.glengthR + 4;
   if (d.flags & kGSimd) {
@@ -1268,7 +1273,7 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
   const bool latency = nd + ng <= latency_batch();
   PlanTimer tm("classify");
   // per problem (threads): its class; slots 0..nd-1 single / end gaps, nd.. genome gaps
-  std::vector<ClassOf> cls(nd + ng);
+  HostArray<ClassOf> cls(nd + ng);
   plan_parallel(nd + ng, T, [&](size_t lo, size_t hi, int) {
     for (size_t s = lo; s < hi; s++)
       cls[s] = s < nd ? classify_dev(plan.dev[s], latency) : classify_gdev(plan.gdev[s - nd], latency, lds_dirs_max);
@@ -1276,19 +1281,42 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
   tm.mark("classes");
   for (size_t s = 0; s < nd + ng; s++)  // the first problem in batch order that the engine rejects
     if (cls[s].err) return bad(ctx, cls[s].err);
-  // pair-arena and direction-scratch offsets in problem order (single / end gaps, then genome gaps)
+  // pair-arena and direction-scratch offsets in problem order (single / end gaps, then genome gaps): each
+  // thread's chunk totals, then the chunk written from its prefix
   size_t pair_off = 0, gdirs_off = 0;
-  for (size_t s = 0; s < nd + ng; s++) {
-    const ClassOf& c = cls[s];
-    if (s < nd) {
-      plan.dev[s].pair_offset = (int32_t)pair_off;
-      if (c.gdirs) plan.dev[s].dirs_offset = (int64_t)gdirs_off;
-    } else {
-      plan.gdev[s - nd].pair_offset = (int32_t)pair_off;
-      plan.gdev[s - nd].dirs_offset = (int64_t)gdirs_off;
+  {
+    std::vector<size_t> tp(T, 0), tg(T, 0);
+    plan_parallel(nd + ng, T, [&](size_t lo, size_t hi, int t) {
+      size_t a = 0, b = 0;
+      for (size_t s = lo; s < hi; s++) {
+        a += cls[s].pair;
+        b += cls[s].gdirs;
+      }
+      tp[t] = a;
+      tg[t] = b;
+    });
+    std::vector<size_t> p0(T), g0(T);
+    for (int t = 0; t < T; t++) {
+      p0[t] = pair_off;
+      g0[t] = gdirs_off;
+      pair_off += tp[t];
+      gdirs_off += tg[t];
     }
-    pair_off += c.pair;
-    gdirs_off += c.gdirs;
+    plan_parallel(nd + ng, T, [&](size_t lo, size_t hi, int t) {
+      size_t a = p0[t], b = g0[t];
+      for (size_t s = lo; s < hi; s++) {
+        const ClassOf& c = cls[s];
+        if (s < nd) {
+          plan.dev[s].pair_offset = (int32_t)a;
+          if (c.gdirs) plan.dev[s].dirs_offset = (int64_t)b;
+        } else {
+          plan.gdev[s - nd].pair_offset = (int32_t)a;
+          plan.gdev[s - nd].dirs_offset = (int64_t)b;
+        }
+        a += c.pair;
+        b += c.gdirs;
+      }
+    });
   }
   tm.mark("offsets");
   // members per class in problem order (the classes in key order, as the tuple map kept them)
@@ -1309,29 +1337,85 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
   }
   const size_t K = keys.size();
   auto class_index = [&](uint64_t k) { return (size_t)(std::lower_bound(keys.begin(), keys.end(), k) - keys.begin()); };
-  std::vector<std::vector<int>> members(K);
-  {
-    std::vector<std::vector<size_t>> cnt(T, std::vector<size_t>(K, 0));
-    std::vector<uint32_t> ci(nd + ng);
-    plan_parallel(nd + ng, T, [&](size_t lo, size_t hi, int t) {
-      for (size_t s = lo; s < hi; s++) {
-        ci[s] = (uint32_t)class_index(cls[s].key);
-        cnt[t][ci[s]]++;
+  // One pass (threads over contiguous chunks of problems): each problem's class, its bin -- the class and its
+  // length quantised to 16 steps per doubling, longest first (plan_bucket: the launch order only steers the
+  // tail of a launch) -- and the classes' work estimates (sums and maxima need no order); then the bins'
+  // offsets (class-major; dev and genome classes into their own order arrays); then every problem scattered
+  // to its slot (in problem order within a bin).  A comparison sort reading two random descriptors per
+  // comparison spent most of a 10 000-read plan on cache misses.
+  constexpr int NB = 1024;
+  struct Acc {
+    double work = 0.0, span = 0.0;
+    int gm = 0;
+    size_t need = 0;
+  };
+  std::vector<std::vector<uint32_t>> hist(T, std::vector<uint32_t>(K * NB, 0));
+  std::vector<std::vector<Acc>> acc(T, std::vector<Acc>(K));
+  HostArray<uint32_t> bin(nd + ng);
+  plan_parallel(nd + ng, T, [&](size_t lo, size_t hi, int t) {
+    std::vector<uint32_t>& h = hist[t];
+    std::vector<Acc>& A = acc[t];
+    for (size_t s = lo; s < hi; s++) {
+      const uint64_t key = cls[s].key;
+      const size_t k = class_index(key);
+      const int kind = (int)(key >> 48), R = (int)((key >> 32) & 0xFFFF);
+      uint64_t len;
+      double one;
+      int gm = 0;
+      if (s >= nd) {
+        const DevGenomeProblem& d = plan.gdev[s - nd];
+        len = (uint64_t)(d.glengthL + d.glengthR) * (uint64_t)(2 * d.lbandL + d.ubandL + d.ubandR + 2);
+        one = kind == PlanCore::kGenomeGap ? (double)std::max(d.glengthL, d.glengthR) * R + d.rlength
+                                           : (double)(d.glengthL + d.glengthR + 2 * d.rlength) + 4.0 * d.rlength;
+      } else {
+        const DevProblem& d = plan.dev[s];
+        len = (uint64_t)d.glength * (uint64_t)(d.lband + d.uband + 1);
+        if (kind == PlanCore::kUxe) {
+          one = (double)(d.rlength + d.glength) + 0.5 * d.rlength;
+        } else if (kind == PlanCore::kSx) {
+          gm = steps_sx(d.rlength, d.lband, d.uband, R);
+          one = (double)gm * R / 64.0 + 0.25 * (d.rlength + d.glength);
+        } else {
+          gm = (int)d.glength;
+          one = (double)d.glength * (kind == PlanCore::kDpx ? R / 64.0 : R) + 0.25 * (d.rlength + d.glength);
+        }
       }
-    });
-    std::vector<std::vector<size_t>> at(T, std::vector<size_t>(K, 0));
-    for (size_t k = 0; k < K; k++) {
-      size_t run = 0;
-      for (int t = 0; t < T; t++) {
-        at[t][k] = run;
-        run += cnt[t][k];
-      }
-      members[k].resize(run);
+      const uint32_t bn = (uint32_t)(k * NB + (NB - 1 - plan_bucket(len)));
+      bin[s] = bn;
+      h[bn]++;
+      Acc& a = A[k];
+      a.work += one;
+      // a packed wave's problems fill side by side: its latency is one problem's columns
+      a.span = std::max(a.span, (kind == PlanCore::kDpx || kind == PlanCore::kSx) ? one * 64.0 / R : one);
+      a.gm = std::max(a.gm, gm);
+      a.need = std::max(a.need, cls[s].need);
     }
-    plan_parallel(nd + ng, T, [&](size_t lo, size_t hi, int t) {
-      for (size_t s = lo; s < hi; s++) members[ci[s]][at[t][ci[s]]++] = (int)(s < nd ? s : s - nd);
-    });
+  });
+  std::vector<std::vector<uint32_t>> at(T, std::vector<uint32_t>(K * NB));
+  std::vector<size_t> first(K), count(K);
+  {
+    size_t run[2] = {0, 0};  // dev order, genome order
+    for (size_t k = 0; k < K; k++) {
+      const int kind = (int)(keys[k] >> 48);
+      const int g = kind == PlanCore::kGenomeGap || kind == PlanCore::kUxg ? 1 : 0;
+      first[k] = run[g];
+      for (int b = 0; b < NB; b++)
+        for (int t = 0; t < T; t++) {
+          at[t][k * NB + b] = (uint32_t)run[g];
+          run[g] += hist[t][k * NB + b];
+        }
+      count[k] = run[g] - first[k];
+    }
+    plan.order.resize(run[0]);
+    plan.gorder.resize(run[1]);
   }
+  plan_parallel(nd + ng, T, [&](size_t lo, size_t hi, int t) {
+    std::vector<uint32_t>& a = at[t];
+    for (size_t s = lo; s < hi; s++) {
+      if (s < nd) plan.order[a[bin[s]]++] = (int)s;
+      else plan.gorder[a[bin[s]]++] = (int)(s - nd);
+    }
+  });
   tm.mark("members");
   for (size_t k = 0; k < K; k++) {
     PlanCore::Launch L;
@@ -1340,99 +1424,38 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
     L.R = (int)((key >> 32) & 0xFFFF);
     L.dirs_lds = ((key >> 31) & 1) != 0;
     L.lds = (size_t)(key & 0x7FFFFFFFull);
-    std::vector<int>& ids = members[k];
-    L.count = (int)ids.size();
-    const bool g = L.kind == PlanCore::kGenomeGap || L.kind == PlanCore::kUxg;
-    if (latency) {  // the class's LDS: its largest member's
-      size_t m = 0;
-      for (int id : ids) m = std::max(m, cls[g ? nd + (size_t)id : (size_t)id].need);
-      L.lds = m;
+    L.count = (int)count[k];
+    L.first = (int)first[k];
+    Acc a;
+    for (int t = 0; t < T; t++) {
+      const Acc& x = acc[t][k];
+      a.work += x.work;
+      a.span = std::max(a.span, x.span);
+      a.gm = std::max(a.gm, x.gm);
+      a.need = std::max(a.need, x.need);
     }
-    // work estimate: fill wave-columns (a packed wave fills 64/S problems at once); the class's longest
-    // problem (span), and for the packed kernels the largest glength / fill steps -- one pass over the
-    // members in problem order (threads for the large classes; sums and maxima need no order)
-    L.work = 0.0;
-    L.span = 0.0;
+    if (latency) L.lds = a.need;  // the class's LDS: its largest member's
+    L.work = a.work;
+    L.span = a.span;
     L.extra = 0;
     L.gdirs_offset = 0;
-    {
-      const int TT = ids.size() >= 65536 ? T : 1;
-      std::vector<double> tw(TT, 0.0), ts(TT, 0.0);
-      std::vector<int> tg(TT, 0);
-      const int kind = L.kind, R = L.R;
-      plan_parallel(ids.size(), TT, [&](size_t lo, size_t hi, int t) {
-        double w = 0.0, sp = 0.0;
-        int gm = 0;
-        for (size_t x = lo; x < hi; x++) {
-          const int id = ids[x];
-          double one;
-          if (kind == PlanCore::kGenomeGap) {
-            const DevGenomeProblem& d = plan.gdev[id];
-            one = (double)std::max(d.glengthL, d.glengthR) * R + d.rlength;
-          } else if (kind == PlanCore::kUxg) {
-            const DevGenomeProblem& d = plan.gdev[id];
-            one = (double)(d.glengthL + d.glengthR + 2 * d.rlength) + 4.0 * d.rlength;
-          } else if (kind == PlanCore::kUxe) {
-            const DevProblem& d = plan.dev[id];
-            one = (double)(d.rlength + d.glength) + 0.5 * d.rlength;
-          } else {
-            const DevProblem& d = plan.dev[id];
-            if (kind == PlanCore::kSx) {
-              const int st = steps_sx(d.rlength, d.lband, d.uband, R);
-              gm = std::max(gm, st);
-              one = (double)st * R / 64.0 + 0.25 * (d.rlength + d.glength);
-            } else {
-              gm = std::max(gm, (int)d.glength);
-              one = (double)d.glength * (kind == PlanCore::kDpx ? R / 64.0 : R) + 0.25 * (d.rlength + d.glength);
-            }
-          }
-          w += one;
-          // a packed wave's problems fill side by side: its latency is one problem's columns
-          sp = std::max(sp, (kind == PlanCore::kDpx || kind == PlanCore::kSx) ? one * 64.0 / R : one);
-        }
-        tw[t] = w;
-        ts[t] = sp;
-        tg[t] = gm;
-      });
-      int gmax = 0;
-      for (int t = 0; t < TT; t++) {
-        L.work += tw[t];
-        L.span = std::max(L.span, ts[t]);
-        gmax = std::max(gmax, tg[t]);
-      }
-      if (L.kind == PlanCore::kSx) {  // per wave: 4 direction words per fill step (gmax: the largest step count)
-        L.extra = (size_t)gmax * 32u;
-        L.dirs_lds = false;
+    if (L.kind == PlanCore::kSx) {  // per wave: 4 direction words per fill step (gm: the largest step count)
+      L.extra = (size_t)a.gm * 32u;
+      L.dirs_lds = false;
+      L.gdirs_offset = gdirs_off;
+      const size_t nblocks = ((size_t)L.count + (64 / L.R) - 1) / (64 / L.R);
+      gdirs_off += (nblocks * L.extra + 255) & ~(size_t)255;
+    }
+    if (L.kind == PlanCore::kDpx) {
+      L.extra = lds_dirs_dpx(a.gm);
+      // direction words in LDS while the workgroup stays small; beyond that they go to an
+      // L2-resident scratch so that more problems are resident per CU
+      L.dirs_lds = L.extra + L.lds * (64 / L.R) <= dpx_lds_dirs_max();
+      if (!L.dirs_lds) {
         L.gdirs_offset = gdirs_off;
         const size_t nblocks = ((size_t)L.count + (64 / L.R) - 1) / (64 / L.R);
         gdirs_off += (nblocks * L.extra + 255) & ~(size_t)255;
       }
-      if (L.kind == PlanCore::kDpx) {
-        L.extra = lds_dirs_dpx(gmax);
-        // direction words in LDS while the workgroup stays small; beyond that they go to an
-        // L2-resident scratch so that more problems are resident per CU
-        L.dirs_lds = L.extra + L.lds * (64 / L.R) <= dpx_lds_dirs_max();
-        if (!L.dirs_lds) {
-          L.gdirs_offset = gdirs_off;
-          const size_t nblocks = ((size_t)L.count + (64 / L.R) - 1) / (64 / L.R);
-          gdirs_off += (nblocks * L.extra + 255) & ~(size_t)255;
-        }
-      }
-    }
-    // longest problems first, so the tail of the launch is short work
-    if (!g) {
-      plan_sort_desc(ids, T, [&](int a) {
-        return (uint64_t)plan.dev[a].glength * (uint64_t)(plan.dev[a].lband + plan.dev[a].uband + 1);
-      });
-      L.first = (int)plan.order.size();
-      plan.order.insert(plan.order.end(), ids.begin(), ids.end());
-    } else {
-      plan_sort_desc(ids, T, [&](int a) {
-        const DevGenomeProblem& d = plan.gdev[a];
-        return (uint64_t)(d.glengthL + d.glengthR) * (uint64_t)(2 * d.lbandL + d.ubandL + d.ubandR + 2);
-      });
-      L.first = (int)plan.gorder.size();
-      plan.gorder.insert(plan.gorder.end(), ids.begin(), ids.end());
     }
     L.stream = 0;
     plan.launches.push_back(L);
@@ -1556,8 +1579,12 @@ static int build_plan(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int
   rc = classify(ctx, plan);
   if (rc) return rc;
   tm.mark("classify");
-  for (size_t s = 0; s < plan.dev.size(); s++) results[plan.dev_problem[s]].pair_offset = plan.dev[s].pair_offset;
-  for (size_t s = 0; s < plan.gdev.size(); s++) gresults[plan.gdev_problem[s]].pair_offset = plan.gdev[s].pair_offset;
+  plan_parallel(plan.dev.size() + plan.gdev.size(), T, [&](size_t lo, size_t hi, int) {
+    for (size_t s = lo; s < hi; s++) {
+      if (s < plan.dev.size()) results[plan.dev_problem[s]].pair_offset = plan.dev[s].pair_offset;
+      else gresults[plan.gdev_problem[s - plan.dev.size()]].pair_offset = plan.gdev[s - plan.dev.size()].pair_offset;
+    }
+  });
   return GMAPDP_OK;
 }
 
@@ -2654,12 +2681,19 @@ struct gmapdp_oligo_plan {
   // A plan made inside a synchronous batch call borrows the context's grow-only buffers: no
   // hipMalloc / hipFree per call (hipFree waits for the whole device, which would serialise the
   // shim's concurrent batches).  `ord` is the host image of d_probs, kept until the plan is freed.
-  bool borrowed = false;
+  // A stage-2 plan's sizing run borrows them as well (tight growth): its upper-bound arenas, tens of GB, are
+  // dropped right after the run, and a fresh hipMalloc of that size per plan took up to a second.
+  bool borrowed = false, sizing = false;
   std::vector<DevOligoProblem> ord;
 };
 
 static constexpr int kOligoChunkProblems = 16384;
+// scratch per launch chunk: 3 GB for the synchronous batches (a context keeps its grow-only scratch); a
+// stage-2 plan's sizing run (window-sized hit lists and walk states, ~7 MB per 214-kb call, freed right
+// after) takes 8 GB chunks: a 10 000-read block in a few launches instead of ~40 small ones (24 GB chunks
+// measured 10.7 ms against 26.5, but the process's first allocation of them took 4 s)
 static constexpr size_t kOligoChunkBytes = size_t(3) << 30;
+static constexpr size_t kOligoSizingChunkBytes = size_t(8) << 30;
 
 static void oligo_plan_free(gmapdp_oligo_plan* p) {
   if (!p) return;
@@ -2709,7 +2743,8 @@ static void oligo_layout(gmapdp_oligo_plan* P, const std::vector<size_t>& slots,
     const size_t mb = align_up(hcap ? scratch_bytes_oi_hits(d.querylength, (*hcap)[d.index])
                                     : scratch_bytes_oi(d.querylength, w), 256);
     const size_t fb = fallback ? align_up(scratch_bytes_oi_fallback(d.querylength, w), 256) : 0;
-    if (k > first && (P->keys[k] != P->keys[first] || k - first >= kOligoChunkProblems || cb + mb + fb > kOligoChunkBytes))
+    if (k > first && (P->keys[k] != P->keys[first] || k - first >= kOligoChunkProblems ||
+                      cb + mb + fb > (local ? kOligoSizingChunkBytes : kOligoChunkBytes)))
       close(k);
     d.scratch_offset = (int64_t)cb;
     d.fallback_offset = fallback ? (int64_t)(cb + mb) : -1;
@@ -2731,9 +2766,10 @@ static hipError_t oligo_buffers(gmapdp_ctx* ctx, gmapdp_oligo_plan* P) {
   const int n = P->n;
   hipError_t e = hipSuccess;
   if (P->borrowed) {
+    const bool t = P->sizing;
     e = ctx->oprobs.ensure(sizeof(DevOligoProblem) * std::max(n, 1));
-    if (e == hipSuccess) e = ctx->oscratch.ensure(std::max<size_t>(P->scratch_cap, 256));
-    if (e == hipSuccess) e = ctx->opool.ensure(sizeof(uint64_t) * std::max<size_t>(P->pool_cap, 1));
+    if (e == hipSuccess) e = ctx->oscratch.ensure(std::max<size_t>(P->scratch_cap, 256), t);
+    if (e == hipSuccess) e = ctx->opool.ensure(sizeof(uint64_t) * std::max<size_t>(P->pool_cap, 1), t);
     if (e == hipSuccess) e = ctx->opoolctr.ensure(sizeof(unsigned long long));
     P->d_probs = (DevOligoProblem*)ctx->oprobs.p;
     P->d_scratch = (unsigned char*)ctx->oscratch.p;
@@ -2825,8 +2861,9 @@ static int oligo_plan_build(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problem
   }
   gmapdp_oligo_plan* P = new gmapdp_oligo_plan();
   P->n = n;
-  P->borrowed = borrow;
   P->split = borrow;
+  P->borrowed = borrow || sizing;
+  P->sizing = sizing;
   P->ord.reserve(n);
   for (auto& kv : classes)
     for (int i : kv.second) {
@@ -2885,6 +2922,14 @@ static hipError_t oligo_plan_relayout(gmapdp_ctx* ctx, gmapdp_oligo_plan* P, con
   }
   // the hit lists sized as measured (a few % of a 214-kb window), so one launch holds most of a plan
   oligo_layout(P, slots, false, tcap, dcap, false, &hcap);
+  if (P->borrowed) {  // the sizing run's borrowed buffers stay the context's; the plan allocates its own
+    P->borrowed = P->sizing = false;
+    P->d_probs = nullptr;
+    P->d_scratch = nullptr;
+    P->d_pool = nullptr;
+    P->d_pool_counter = nullptr;
+    P->d_nhits = nullptr;
+  }
   return oligo_buffers(ctx, P);
 }
 
@@ -3739,14 +3784,24 @@ int gmapdp_stage2_plan_create(gmapdp_ctx* ctx, const gmapdp_stage2_problem* prob
   if (e == hipSuccess) e = hipMalloc(&P->d_ores, sizeof(gmapdp_oligo_result) * n);
   if (e == hipSuccess) e = hipMalloc(&P->d_npos, sizeof(int32_t) * qbytes);
   if (e == hipSuccess) e = hipMalloc(&P->d_map, sizeof(int32_t) * qbytes);
-  if (e == hipSuccess) e = hipMalloc(&P->d_table, sizeof(uint32_t) * std::max<size_t>(toff, 1));
-  if (e == hipSuccess) e = hipMalloc(&P->d_diag, 4 * sizeof(int32_t) * std::max<size_t>(doff, 1));
+  // the sizing run's upper-bound arenas: the context's grow-only buffers (see gmapdp_oligo_plan::borrowed)
+  auto drop_sizing = [&]() {
+    P->d_table = nullptr;
+    P->d_diag = nullptr;
+    P->oplan->d_nhits = nullptr;
+  };
+  if (e == hipSuccess) e = ctx->otable.ensure(sizeof(uint32_t) * std::max<size_t>(toff, 1), true);
+  if (e == hipSuccess) e = ctx->odiag.ensure(4 * sizeof(int32_t) * std::max<size_t>(doff, 1), true);
+  if (e == hipSuccess) e = ctx->onhits.ensure(sizeof(int32_t) * n);
+  P->d_table = (uint32_t*)ctx->otable.p;
+  P->d_diag = (int32_t*)ctx->odiag.p;
+  P->oplan->d_nhits = (int32_t*)ctx->onhits.p;
   if (e == hipSuccess) e = hipMalloc(&P->d_counters, s2_counters_bytes(n));
-  if (e == hipSuccess) e = hipMalloc(&P->oplan->d_nhits, sizeof(int32_t) * n);
   if (e == hipSuccess) e = hipMemcpy(P->d_probs, dp.data(), sizeof(DevStage2Problem) * n, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = ctx->qseq_uc.ensure(qbytes);
   if (e == hipSuccess) e = hipMemcpy(ctx->qseq_uc.p, qseq_uc, qbytes, hipMemcpyHostToDevice);
   if (e != hipSuccess) {
+    drop_sizing();
     stage2_plan_free(P);
     return fail(ctx, GMAPDP_ENOMEM, "stage-2 plan: %s", e);
   }
@@ -3762,6 +3817,7 @@ int gmapdp_stage2_plan_create(gmapdp_ctx* ctx, const gmapdp_stage2_problem* prob
     if (e == hipSuccess) e = ctx_sync(ctx, ctx->stream);
     if (e != hipSuccess) rc = fail(ctx, GMAPDP_ELAUNCH, "stage-2 plan seeding: %s", e);
   }
+  drop_sizing();
   if (rc) {
     stage2_plan_free(P);
     return rc;
@@ -3770,12 +3826,6 @@ int gmapdp_stage2_plan_create(gmapdp_ctx* ctx, const gmapdp_stage2_problem* prob
   // The seeding's arenas were sized from upper bounds (a window's worth of positions and 24 diagonals per
   // query position: 19 GB for 10 000 5-kb reads).  Re-lay them out from this run's measured use
   // (oligo_plan_relayout) so the plan keeps only what its runs write.
-  (void)hipFree(P->d_table);
-  (void)hipFree(P->d_diag);
-  P->d_table = nullptr;
-  P->d_diag = nullptr;
-  (void)hipFree(P->oplan->d_nhits);
-  P->oplan->d_nhits = nullptr;
   e = oligo_plan_relayout(ctx, P->oplan, op.data(), ores.data(), nhits.data());
   tm.mark("relayout");
   if (e == hipSuccess) e = hipMalloc(&P->d_table, sizeof(uint32_t) * std::max<size_t>(P->oplan->table_cap, 1));

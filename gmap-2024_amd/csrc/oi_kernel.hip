@@ -500,13 +500,23 @@ __device__ __forceinline__ int oi_sweep(int lane, const typename KT::K* S, int E
 
 // get_mappings over the shared global event pool.  Returns false (nothing written) when the pool could not
 // hold this problem's 3 E slots (`base` == ~0).
-template <typename KT>
+// With `slots` (kOimSlots 16-bit LDS counters) the events are first counted per diagonal slot (a hash of the
+// diagonal) and only those of slots holding at least suffn + 1 events are sorted and swept: a good diagonal
+// holds that many, so every event of every good diagonal is kept, and when some diagonal is good the good list
+// and maxnconsecutive are exactly the full event set's (oi_mappings_lds gives the argument).  On a 214-kb
+// window that is the read's locus, ~2 000 of ~8 300 events: a quarter of the keys written and scattered by
+// the radix passes.  With no good diagonal the full event set is sorted and swept after all.
+constexpr int kOimSlots = 1024;
+__device__ __forceinline__ uint32_t oim_slot(uint32_t di) { return (di * 2654435761u) >> 22; }
+
+template <typename KT, bool kSlots>
 __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t maxdiag, uint32_t chrinit,
                                    int lookback, int suffn, const int32_t* __restrict__ npq,
                                    const int32_t* __restrict__ mpq, const int* __restrict__ cum,
                                    const uint32_t* __restrict__ table_all, uint64_t* __restrict__ pool,
                                    unsigned long long base, uint32_t* hist,
-                                   int* evq, int32_t* __restrict__ good, int gcap, int& ngood_out, int& maxn_out) {
+                                   int* evq, int32_t* __restrict__ good, int gcap, int& ngood_out, int& maxn_out,
+                                   uint32_t* slots = nullptr) {
   OI_MARK(9);
   if (base == ~0ull) return false;
   using K = typename KT::K;
@@ -514,25 +524,54 @@ __device__ bool oi_mappings_sorted(int lane, int qlen, int nq, int E, uint32_t m
   K* evB = evA + E;                                 // radix-sort ping-pong
   int4* grec = reinterpret_cast<int4*>(pool + base + 2 * (size_t)E);  // good records (at most E / 2)
   const OiDigits D = oi_digits(maxdiag);
-  for (int i = lane; i < kOiHist; i += 64) hist[i] = 0u;
-  oi_wave_sync();
-  oi_for_events<KT>(lane, qlen, nq, chrinit, npq, mpq, cum, table_all, evq,
-                    [&](int e, bool v, uint32_t di, K key) {
-                      if (v) evA[e] = key;
-                      oi_hist_add(lane, v, di, D, hist);
-                    });
-  __threadfence_block();
-  oi_wave_sync();
-  OI_MARK(5);
-  const K* S = oi_radix<KT>(lane, evA, evB, E, D, hist);
-  OI_MARK(6);
   // the good diagonals' query-order keys: the free sort buffer (64-bit events), or the pool's second E words
   // (32-bit events: both sort buffers sit in the first)
-  uint64_t* gkey = sizeof(K) == 8 ? reinterpret_cast<uint64_t*>(S == evA ? evB : evA) : pool + base + E;
-  ngood_out = oi_sweep<KT>(lane, S, E, qlen, nq, lookback, suffn, cum, grec, gkey, good, gcap, maxn_out);
-  return true;
+  const uint32_t need = (uint32_t)suffn + 1u;
+  bool filtered = kSlots && E < 65536;
+  if (filtered) {
+    for (int i = lane; i < kOimSlots / 2; i += 64) slots[i] = 0u;
+    oi_wave_sync();
+    oi_for_events<KT>(lane, qlen, nq, chrinit, npq, mpq, cum, table_all, evq, [&](int, bool v, uint32_t di, K) {
+      if (v) {
+        const uint32_t h = oim_slot(di);
+        atomicAdd(&slots[h >> 1], 1u << (16 * (h & 1)));
+      }
+    });
+    oi_wave_sync();
+  }
+  for (;;) {
+    for (int i = lane; i < kOiHist; i += 64) hist[i] = 0u;
+    oi_wave_sync();
+    int C = 0;
+    oi_for_events<KT>(lane, qlen, nq, chrinit, npq, mpq, cum, table_all, evq,
+                      [&](int, bool v, uint32_t di, K key) {
+                        bool c = v;
+                        if (filtered) {
+                          const uint32_t h = oim_slot(di);
+                          c = v && ((slots[h >> 1] >> (16 * (h & 1))) & 0xFFFFu) >= need;
+                        }
+                        const uint64_t cm = ballot(c);
+                        if (c) evA[C + lanes_below(cm, lane)] = key;
+                        oi_hist_add(lane, c, di, D, hist);
+                        C += __popcll(cm);
+                      });
+    __threadfence_block();
+    oi_wave_sync();
+    OI_MARK(5);
+    const K* S = oi_radix<KT>(lane, evA, evB, C, D, hist);
+    OI_MARK(6);
+    uint64_t* gkey = sizeof(K) == 8 ? reinterpret_cast<uint64_t*>(S == evA ? evB : evA) : pool + base + E;
+    int maxn = 0;
+    const int ngood = oi_sweep<KT>(lane, S, C, qlen, nq, lookback, suffn, cum, grec, gkey, good, gcap, maxn);
+    if (filtered && ngood != -1 && (ngood == 0 || maxn < suffn)) {  // no good diagonal: the full event set
+      filtered = false;
+      continue;
+    }
+    ngood_out = ngood;
+    maxn_out = maxn;
+    return true;
+  }
 }
-
 
 // Per-id counters: 16-bit when the window has fewer than 65536 8-mer starts (no count or table
 // offset can reach 2^16, and the 28-KB LDS of a 2-kb read drops to 20 KB: 8 waves per CU, not 5),
@@ -574,12 +613,13 @@ __device__ void oi_report_overflow(const DevOligoProblem& P, int tid, int nthrea
 // the two lists meet only when the layout's capacity is exceeded, which is reported as overflow).
 constexpr int kOiWaves = 2;
 
+#define OI_PASS_ARGS                                                                                          \
+  const DevOligoProblem *__restrict__ probs, const uint32_t *__restrict__ blocks, const char *__restrict__ quc_all, \
+      unsigned char *__restrict__ scratch, gmapdp_oligo_result *__restrict__ results,                             \
+      int32_t *__restrict__ npos_out, int32_t *__restrict__ map_out, uint32_t *__restrict__ table_all,            \
+      unsigned long long *__restrict__ pool_counter, unsigned long long pool_cap, int32_t *__restrict__ nhits_out
 template <typename CT>
-__global__ __launch_bounds__(64 * kOiWaves) void oi_kernel(
-    const DevOligoProblem* __restrict__ probs, const uint32_t* __restrict__ blocks, const char* __restrict__ quc_all,
-    unsigned char* __restrict__ scratch, gmapdp_oligo_result* __restrict__ results, int32_t* __restrict__ npos_out,
-    int32_t* __restrict__ map_out, uint32_t* __restrict__ table_all, unsigned long long* __restrict__ pool_counter,
-    unsigned long long pool_cap, int32_t* __restrict__ nhits_out) {
+__device__ __forceinline__ void oi_pass(OI_PASS_ARGS) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int nh_wave[kOiWaves];  // each wave's pass-1 hits
   const int tid = threadIdx.x, lane = tid & 63;
@@ -663,6 +703,10 @@ __global__ __launch_bounds__(64 * kOiWaves) void oi_kernel(
   // to the problem's hit list {window index, id} in ascending position, so pass 2 never re-reads the
   // window.
   uint2* hitlist = reinterpret_cast<uint2*>(base_s + so.hits);
+  uint32_t* hitlist32 = reinterpret_cast<uint32_t*>(base_s + so.hits);
+  // hits as (window index << 14 | id) when the window has at most 2^18 starts (ids are below 2^14): half the
+  // bytes the list writes and pass 2 reads back
+  const bool compact = npos <= (1ull << 18);
   int nhits = 0;
   if (npos > 0) {
     // this wave's steps of 64 half-words: wave 0 the first half of the window's, wave 1 the rest
@@ -723,9 +767,12 @@ __global__ __launch_bounds__(64 * kOiWaves) void oi_kernel(
         const int id = oligo_id(bitmap, wrank, m, in);
         count_inc(cnt, id);
         // wave 0 from the start of the list, wave 1 from its end (its k-th hit at hit_cap - 1 - k)
-        if ((uint32_t)o < P.hit_cap)
-          hitlist[wave ? P.hit_cap - 1 - (uint32_t)o : (uint32_t)o] =
-              make_uint2((uint32_t)(16 * h + j - left), (uint32_t)id);
+        if ((uint32_t)o < P.hit_cap) {
+          const uint32_t at = wave ? P.hit_cap - 1 - (uint32_t)o : (uint32_t)o;
+          const uint32_t k = (uint32_t)(16 * h + j - left);
+          if (compact) hitlist32[at] = (k << 14) | (uint32_t)id;
+          else hitlist[at] = make_uint2(k, (uint32_t)id);
+        }
         o++;
       }
       nhits += __builtin_amdgcn_readlane(incl, 63);
@@ -788,9 +835,16 @@ __global__ __launch_bounds__(64 * kOiWaves) void oi_kernel(
     if (sl < nhits) {
       // ascending position: wave 0's list, then wave 1's from the list's end backwards
       const int a = P.plusp ? nhits - 1 - sl : sl;
-      const uint2 hv = hitlist[a < n0 ? (uint32_t)a : P.hit_cap - 1 - (uint32_t)(a - n0)];
-      k = hv.x;
-      id = (int)hv.y;
+      const uint32_t at = a < n0 ? (uint32_t)a : P.hit_cap - 1 - (uint32_t)(a - n0);
+      if (compact) {
+        const uint32_t e = hitlist32[at];
+        k = e >> 14;
+        id = (int)(e & 0x3FFFu);
+      } else {
+        const uint2 hv = hitlist[at];
+        k = hv.x;
+        id = (int)hv.y;
+      }
     }
     const uint64_t hits = ballot(id >= 0);
     // lane order = store order: a hit's rank among the chunk's hits of its oligo (ballot match on the
@@ -984,11 +1038,15 @@ __device__ bool oi_mappings_walk(int lane, const DevOligoProblem& P, unsigned ch
 
 // get_mappings over the global event pool (oi_mappings_sorted with the key format the problem's shape
 // allows), else the sequential walk; writes the result's maxnconsecutive / oned_matrix_p / ndiagonals.
+// kSlots: the slot filter over `slots` (oi_map_kernel; oi_build_kernel's fallback goes without, which keeps
+// that kernel's registers within its occupancy bound)
+template <bool kSlots>
 __device__ void oi_mappings_global(int lane, const DevOligoProblem& P, unsigned char* __restrict__ scratch, int qlen,
                                    int nq, int E, const int32_t* __restrict__ npq, const int32_t* __restrict__ mpq,
                                    const int* __restrict__ cum, const uint32_t* __restrict__ table,
                                    uint64_t* __restrict__ pool, unsigned long long pbase, uint32_t* hist, int* evq,
-                                   int32_t* __restrict__ good, gmapdp_oligo_result* __restrict__ results) {
+                                   int32_t* __restrict__ good, gmapdp_oligo_result* __restrict__ results,
+                                   uint32_t* slots = nullptr) {
   const int diag_lookback = P.minor ? 60 : 120, suffn = P.minor ? 10 : 20;
   const uint32_t chrinit = P.plusp ? P.chrstart : (P.chrhigh - P.chroffset) - P.chrend;
   int ngood = 0, maxn = 0;
@@ -996,13 +1054,13 @@ __device__ void oi_mappings_global(int lane, const DevOligoProblem& P, unsigned 
   const int gcap = (int)min(P.diag_cap, 0x7fffffffu);
   const bool sorted =
       maxdiag < (1u << 20) - 1 && nq <= 4096
-          ? oi_mappings_sorted<OiKeyT32>(lane, qlen, nq, E, maxdiag, chrinit, diag_lookback, suffn, npq, mpq, cum,
-                                         table, pool, pbase, hist, evq, good, gcap, ngood, maxn)
+          ? oi_mappings_sorted<OiKeyT32, kSlots>(lane, qlen, nq, E, maxdiag, chrinit, diag_lookback, suffn, npq, mpq, cum,
+                                         table, pool, pbase, hist, evq, good, gcap, ngood, maxn, slots)
       : nq < 65536
-          ? oi_mappings_sorted<OiKeyQT>(lane, qlen, nq, E, maxdiag, chrinit, diag_lookback, suffn, npq, mpq, cum,
-                                        table, pool, pbase, hist, evq, good, gcap, ngood, maxn)
-          : oi_mappings_sorted<OiKeyQ>(lane, qlen, nq, E, maxdiag, chrinit, diag_lookback, suffn, npq, mpq, cum,
-                                       table, pool, pbase, hist, evq, good, gcap, ngood, maxn);
+          ? oi_mappings_sorted<OiKeyQT, kSlots>(lane, qlen, nq, E, maxdiag, chrinit, diag_lookback, suffn, npq, mpq, cum,
+                                        table, pool, pbase, hist, evq, good, gcap, ngood, maxn, slots)
+          : oi_mappings_sorted<OiKeyQ, kSlots>(lane, qlen, nq, E, maxdiag, chrinit, diag_lookback, suffn, npq, mpq, cum,
+                                       table, pool, pbase, hist, evq, good, gcap, ngood, maxn, slots);
   if (!sorted && !oi_mappings_walk(lane, P, scratch, qlen, nq, npq, mpq, cum, table, chrinit, diag_lookback, suffn,
                                    good, ngood, maxn))
     ngood = -1;  // no pool slot and no fallback region: Stage2_compute answers GMAPDP overflow (status -2)
@@ -1013,16 +1071,31 @@ __device__ void oi_mappings_global(int lane, const DevOligoProblem& P, unsigned 
   }
 }
 
+// The plan runs' kernel, and the same code under another name for a stage-2 plan's sizing run (nhits_out
+// set), so that a profile of the bench tells the plan's one-time sizing dispatches from its step's.
+template <typename CT>
+__global__ __launch_bounds__(64 * kOiWaves) void oi_kernel(OI_PASS_ARGS) {
+  oi_pass<CT>(probs, blocks, quc_all, scratch, results, npos_out, map_out, table_all, pool_counter, pool_cap,
+              nhits_out);
+}
+template <typename CT>
+__global__ __launch_bounds__(64 * kOiWaves) void oi_size_kernel(OI_PASS_ARGS) {
+  oi_pass<CT>(probs, blocks, quc_all, scratch, results, npos_out, map_out, table_all, pool_counter, pool_cap,
+              nhits_out);
+}
+
 // ---- Oligoindex_get_mappings' diagonal state machine, one wave per problem, after oi_kernel ----
 // A kernel of its own: its only LDS is the radix histogram and the event step's offsets, so many more
 // waves share a CU and hide the L2 latency of the event passes than oi_kernel's query tables would allow.
-__global__ __launch_bounds__(64) void oi_map_kernel(
-    const DevOligoProblem* __restrict__ probs, unsigned char* __restrict__ scratch,
-    gmapdp_oligo_result* __restrict__ results, const int32_t* __restrict__ npos_out,
-    const int32_t* __restrict__ map_out, const uint32_t* __restrict__ table_all, int32_t* __restrict__ diag_all,
-    uint64_t* __restrict__ pool) {
+#define OI_MAP_ARGS                                                                                           \
+  const DevOligoProblem *__restrict__ probs, unsigned char *__restrict__ scratch,                                 \
+      gmapdp_oligo_result *__restrict__ results, const int32_t *__restrict__ npos_out,                            \
+      const int32_t *__restrict__ map_out, const uint32_t *__restrict__ table_all, int32_t *__restrict__ diag_all, \
+      uint64_t *__restrict__ pool
+__device__ __forceinline__ void oi_map_pass(OI_MAP_ARGS) {
   __shared__ uint32_t hist[kOiHist];
   __shared__ int evq[3 * 256];
+  __shared__ uint32_t slots[kOimSlots / 2];
   const int lane = threadIdx.x;
   const DevOligoProblem P = probs[blockIdx.x];
   if (P.chrend <= P.chrstart) return;  // oned_matrix_p stays 0 (oi_kernel wrote the record)
@@ -1036,10 +1109,10 @@ __global__ __launch_bounds__(64) void oi_map_kernel(
   unsigned char* base_s = scratch + P.scratch_offset;
   const ScratchOi so = scratch_oi(qlen, P.chrend - P.chrstart);
   const int totalpositions = results[P.index].totalpositions;
-  oi_mappings_global(lane, P, scratch, qlen, nq, totalpositions, npos_out + P.qoff, map_out + P.qoff,
+  oi_mappings_global<true>(lane, P, scratch, qlen, nq, totalpositions, npos_out + P.qoff, map_out + P.qoff,
                      reinterpret_cast<const int*>(base_s), table_all + P.table_offset, pool,
                      *reinterpret_cast<const unsigned long long*>(base_s + so.poolbase), hist, evq,
-                     diag_all + 4 * P.diag_offset, results);
+                     diag_all + 4 * P.diag_offset, results, slots);
   OI_MARK(7);
 #ifdef GMAPDP_OI_TIMING
   if (lane == 0 && P.index < 16384) {
@@ -1049,21 +1122,30 @@ __global__ __launch_bounds__(64) void oi_map_kernel(
 #endif
 }
 
+__global__ __launch_bounds__(64) void oi_map_kernel(OI_MAP_ARGS) {
+  oi_map_pass(probs, scratch, results, npos_out, map_out, table_all, diag_all, pool);
+}
+__global__ __launch_bounds__(64) void oi_size_map_kernel(OI_MAP_ARGS) {  // a sizing run's (see oi_size_kernel)
+  oi_map_pass(probs, scratch, results, npos_out, map_out, table_all, diag_all, pool);
+}
+
 // ---- the split seeding: oi_scan_kernel (the query's 8-mers, the window scan) + oi_build_kernel ----
 // oi_kernel above writes each table entry with a scattered 4-B store (pass 2) and oi_map_kernel radix-sorts
 // every event through the global pool (two scattered passes): partial cache lines, ~8x the seeding's
 // algorithmic write bytes.  The split path keeps both scatters in LDS:
 //   oi_scan_kernel (2 waves, 12 KB LDS: the bitmap and its ranks only) -- Oligoindex_set_inquery, each query
 //     position's 8-mer id, and pass 1's hit list (4 B per hit when the window has at most 2^18 starts);
-//   oi_build_kernel (1 wave) -- counts from the hit list, the table layout, pass 2's placement into an LDS
+//   oi_build_kernel (4 waves) -- counts from the hit list, the table layout, pass 2's placement into an LDS
 //     image of the table (written out coalesced), npositions / mappings / cum_nohits, then get_mappings:
-//     the events' diagonals marked in an LDS Bloom pair ("seen", "seen twice"); a diagonal with one event
-//     can neither start a run of two nor carry n > 0, so only the events whose diagonal was marked twice
-//     (every event of every repeated diagonal, plus a few single ones that share a slot) are candidates;
-//     they are emitted in query order into LDS, radix-sorted there and swept as oi_mappings_sorted does.
-//     A problem whose table or candidates do not fit its LDS falls back to the global paths above.
-// The plan's sizing run keeps oi_kernel + oi_map_kernel (same results), so profiles of the bench step see
-// only these two kernels.
+//     the events counted per diagonal slot (a hash of the diagonal) in LDS; a good diagonal has at least
+//     suffn + 1 events, so only the events of slots that reach that count are candidates (the answer is
+//     exact when the sweep finds a good diagonal with n >= suffn; otherwise the call is swept again over
+//     every event); they are emitted in query order into LDS, radix-sorted there and swept as
+//     oi_mappings_sorted does.  A problem whose table or candidates do not fit its LDS falls back to the
+//     global paths above.
+// The synchronous batch APIs take this path; the device-resident plans (bench.py's step) keep oi_kernel +
+// oi_map_kernel, which share the CUs with the DP launches better; oi_map_kernel applies the
+// same slot filter to its global event sort.
 
 // the query's 8-mers 256 positions at a time (one coalesced character load per lane and chunk, 5 chunks:
 // the last supplies the 7-character overlap; the 8-mer at i takes the codes of lanes i..i+7): f(i, ok, m)
@@ -1593,7 +1675,7 @@ __global__ __launch_bounds__(64 * kOibWaves, 3) void oi_build_kernel(
   oi_wave_sync();
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem);
   int* evq = reinterpret_cast<int*>(smem + 4 * kOiHist);
-  oi_mappings_global(lane, P, scratch, qlen, nq, E, npq, mpq, cum, table, pool, b, hist, evq, good, results);
+  oi_mappings_global<false>(lane, P, scratch, qlen, nq, E, npq, mpq, cum, table, pool, b, hist, evq, good, results);
 }
 
 size_t lds_bytes_oib(int umax, int* tcap) {
@@ -1658,7 +1740,11 @@ hipError_t launch_oi(bool wide, int nproblems, size_t lds, hipStream_t stream, c
                      const uint32_t* blocks, const char* quc, unsigned char* scratch, gmapdp_oligo_result* results,
                      int32_t* npos, int32_t* map, uint32_t* table, int32_t* diags, uint64_t* pool,
                      unsigned long long* pool_counter, unsigned long long pool_cap, int32_t* nhits_out) {
-  void* fn = wide ? reinterpret_cast<void*>(&oi_kernel<uint32_t>) : reinterpret_cast<void*>(&oi_kernel<uint16_t>);
+  const bool sizing = nhits_out != nullptr;  // a stage-2 plan's sizing run: the same code, its own names
+  void* fn = sizing ? (wide ? reinterpret_cast<void*>(&oi_size_kernel<uint32_t>)
+                            : reinterpret_cast<void*>(&oi_size_kernel<uint16_t>))
+                    : (wide ? reinterpret_cast<void*>(&oi_kernel<uint32_t>)
+                            : reinterpret_cast<void*>(&oi_kernel<uint16_t>));
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -1669,7 +1755,8 @@ hipError_t launch_oi(bool wide, int nproblems, size_t lds, hipStream_t stream, c
   if (e != hipSuccess) return e;
   void* margs[] = {(void*)&probs, (void*)&scratch, (void*)&results, (void*)&npos, (void*)&map, (void*)&table,
                    (void*)&diags, (void*)&pool};
-  return hipLaunchKernel(reinterpret_cast<void*>(&oi_map_kernel), dim3(nproblems), dim3(64), margs, 0, stream);
+  return hipLaunchKernel(sizing ? reinterpret_cast<void*>(&oi_size_map_kernel) : reinterpret_cast<void*>(&oi_map_kernel),
+                         dim3(nproblems), dim3(64), margs, 0, stream);
 }
 
 }  // namespace gmapdp
