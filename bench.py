@@ -211,6 +211,8 @@ def pmc_entry(key, workload):
         return None, None
     ks = d.get("kernels", {})
     rec = {}
+    # a stage-2 kernel: the profiled process's dispatch totals over its block runs (bench block_runs)
+    runs = (d.get("block_runs") or {}).get(key)
     parts = key.split("+")
     # a plain name (gmapdp::s2c_kernel) covers its template instances (s2c_kernel<false>, <true>)
     members = [[k for k in ks if k == p or (("<" not in p) and k.startswith(p + "<"))] for p in parts]
@@ -226,7 +228,7 @@ def pmc_entry(key, workload):
                     break
                 # per bench launch: a template instance dispatched on fewer blocks counts in proportion
                 disp = ks[k].get("dispatches") or 1
-                ref = max(ks[x].get("dispatches") or 1 for x in m)
+                ref = runs or max(ks[x].get("dispatches") or 1 for x in m)
                 tot += v * disp / ref
             if tot is None:
                 break
@@ -582,7 +584,16 @@ def main():
                      C.c_void_p(d_pairs.data_ptr()), C.c_void_p(s.cuda_stream)),
                    "gmapdp_plan_run_launch")
 
+    # how many times this process ran each stage-2 kernel over a block (every leg: warmup, timed steps, the
+    # outputs pass, the kernels alone, the PCIe legs), printed with the line so that tools/pmc_summary.py can
+    # turn a profile's dispatch totals into bytes per block (the seeding's launch chunks vary per block; the
+    # plans' sizing runs launch under other names and count nowhere)
+    block_runs = {k: 0 for k in S2_WHAT}
+
     def orun(b, s, what):
+        for k, w in S2_WHAT.items():
+            if what & w or (what & 2 and w > 1):
+                block_runs[k] += 1
         eng._check(lib.gmapdp_stage2_plan_run(eng.h, b["oplan"], C.c_void_p(b["d_oq"].data_ptr()),
                                               C.c_void_p(b["d_oq"].data_ptr()), C.c_void_p(d_s2res.data_ptr()),
                                               what, C.c_void_p(s.cuda_stream)), "gmapdp_stage2_plan_run")
@@ -904,7 +915,7 @@ def main():
     # (the splice and microexon probabilities are computed on the device: no probability crosses PCIe)
     up = d["q"].nbytes + d["oq"].nbytes + sum(d[k].nbytes for k in ("single", "end", "genome", "oligo", "microexon"))
     # the outputs as produced: results, the DP and microexon pairs, the stage-2 results and path pairs
-    down = int(32 * b["ngpu"] + 72 * b["nggpu"] + 16 * checks["pairs"] / len(B) + 32 * args.reads
+    down = int(32 * b["ngpu"] + 72 * b["nggpu"] + 16 * checks["pairs"] / len(B) + 32 * len(d["oligo"])
                + 20 * checks["stage2_path_pairs"] / len(B))
     h_up = torch.empty(up, dtype=torch.uint8, pin_memory=True)
     h_down = torch.empty(down, dtype=torch.uint8, pin_memory=True)
@@ -943,6 +954,13 @@ def main():
         nprob = b["ngpu"] + b["nggpu"]
         d_off = torch.empty(nprob + 1, dtype=torch.int64, device=dev)
         d_cmp = torch.empty(max(int(lib.gmapdp_plan_compact_bound(b["plan"])), 16), dtype=torch.uint8, device=dev)
+        # stage 2's path pairs too (gmapdp_stage2_plan_compact_pairs: one list per path record)
+        has_s2 = b["oplan"] is not None
+        if has_s2:
+            pcap = C.c_size_t()
+            s2bound = int(lib.gmapdp_stage2_plan_compact_bound(b["oplan"], C.byref(pcap)))
+            d_s2off = torch.empty(pcap.value + 1, dtype=torch.int64, device=dev)
+            d_s2cmp = torch.empty(max(s2bound, 16), dtype=torch.uint8, device=dev)
         cms = []
         for _ in range(3):
             e0, e1 = mk()
@@ -951,14 +969,49 @@ def main():
                                                      C.c_void_p(d_pairs.data_ptr()), C.c_void_p(d_cmp.data_ptr()),
                                                      C.c_void_p(d_off.data_ptr()), C.c_void_p(stream.cuda_stream)),
                        "gmapdp_plan_compact_pairs")
+            if has_s2:
+                eng._check(lib.gmapdp_stage2_plan_compact_pairs(eng.h, b["oplan"], C.c_void_p(d_s2cmp.data_ptr()),
+                                                                C.c_void_p(d_s2off.data_ptr()),
+                                                                C.c_void_p(stream.cuda_stream)),
+                           "gmapdp_stage2_plan_compact_pairs")
             e1.record(stream)
             torch.cuda.synchronize()
             cms.append(e0.elapsed_time(e1))
         offs = d_off.cpu().numpy().view(np.uint64)
         nbytes = int(offs[-1])
-        other = int(32 * b["ngpu"] + 72 * b["nggpu"] + 8 * (nprob + 1) + 32 * args.reads
-                    + 20 * checks["stage2_path_pairs"] / len(B))
-        cdown = nbytes + other
+        s2same, s2bytes, s2expand_ms, s2records, npaths = True, 0, 0.0, 0, 0
+        if has_s2:
+            s2r = np.zeros(len(b["d"]["oligo"]), dtype=gmapdp.STAGE2_RESULT_DTYPE)
+            pn, qn = C.c_size_t(), C.c_size_t()
+            rc = lib.gmapdp_stage2_plan_fetch(eng.h, b["oplan"], C.c_void_p(d_s2res.data_ptr()),
+                                              C.c_void_p(stream.cuda_stream), s2r.ctypes.data, None, 0, None, 0,
+                                              C.byref(pn), C.byref(qn))
+            if rc not in (0, -6):
+                eng._check(rc, "gmapdp_stage2_plan_fetch")
+            s2paths = np.zeros(max(pn.value, 1), dtype=gmapdp.PATH_DTYPE)
+            s2pairs = np.zeros(max(qn.value, 1), dtype=gmapdp.PATH_PAIR_DTYPE)
+            eng._check(lib.gmapdp_stage2_plan_fetch(eng.h, b["oplan"], C.c_void_p(d_s2res.data_ptr()),
+                                                    C.c_void_p(stream.cuda_stream), s2r.ctypes.data,
+                                                    s2paths.ctypes.data, len(s2paths), s2pairs.ctypes.data,
+                                                    len(s2pairs), C.byref(pn), C.byref(qn)), "gmapdp_stage2_plan_fetch")
+            npaths = int(pn.value)
+            s2offs = d_s2off[:npaths + 1].cpu().numpy().view(np.uint64)
+            s2bytes = int(s2offs[-1])
+            s2stream = d_s2cmp[:max(s2bytes, 1)].cpu().numpy()
+            t0 = time.perf_counter()
+            s2exp = gmapdp.expand_path_pairs(s2stream, s2offs, s2paths[:npaths], len(s2pairs), nthreads=16)
+            s2expand_ms = (time.perf_counter() - t0) * 1e3
+            pc = np.maximum(s2paths[:npaths]["npairs"].astype(np.int64), 0)
+            pidx = np.repeat(s2paths[:npaths]["pair_offset"], pc) + (np.arange(int(pc.sum()))
+                                                                      - np.repeat(np.cumsum(pc) - pc, pc))
+            s2same = bool(np.array_equal(s2exp[pidx], s2pairs[pidx]))
+            s2records = int(pc.sum())
+            del d_s2cmp, s2exp, s2pairs, s2stream
+        # the rest of the outputs as records: the DP results and stream offsets, the stage-2 results, path
+        # records and stream offsets
+        other = int(32 * b["ngpu"] + 72 * b["nggpu"] + 8 * (nprob + 1) + 32 * len(b["d"]["oligo"])
+                    + (16 * npaths + 8 * (npaths + 1) if has_s2 else 0))
+        cdown = nbytes + s2bytes + other
         h_c = torch.empty(cdown, dtype=torch.uint8, pin_memory=True)
         g_c = torch.empty(cdown, dtype=torch.uint8, device=dev)
         down_ms = []
@@ -979,15 +1032,18 @@ def main():
         allp = np.frombuffer(d_pairs[:16 * b["cap"]].cpu().numpy().tobytes(), dtype=gmapdp.PAIR_DTYPE)
         cnt = np.maximum(npc.astype(np.int64), 0)
         idx = np.repeat(poff, cnt) + (np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt))
-        same = bool(np.array_equal(exp[idx], allp[idx]))
+        same = bool(np.array_equal(exp[idx], allp[idx])) and s2same
         del h_c, g_c, d_cmp, allp, exp
         compact = {"records": int(cnt.sum()), "stream_bytes": nbytes, "bytes_per_record": nbytes / max(int(cnt.sum()), 1),
+                   "stage2_path_pair_records": s2records, "stage2_stream_bytes": s2bytes,
+                   "stage2_bytes_per_record": s2bytes / max(s2records, 1),
                    "compact_kernels_ms": float(np.median(cms[1:])), "pcie_bytes_down": cdown,
                    "pcie_down_ms": float(np.median(down_ms[1:])), "pcie_up_ms": up_ms,
-                   "host_expand_ms_16_threads": expand_ms, "expanded_equals_records": same}
+                   "host_expand_ms_16_threads": expand_ms, "stage2_host_expand_ms_16_threads": s2expand_ms,
+                   "expanded_equals_records": same}
         compact["pcie_ms_per_step"] = compact["pcie_up_ms"] + compact["compact_kernels_ms"] + compact["pcie_down_ms"]
-        progress("compact pair stream: %d records in %d bytes, expanded %s" % (compact["records"], nbytes,
-                                                                           "identically" if same else "DIFFERENTLY"))
+        progress("compact pair stream: %d DP records in %d bytes, %d stage-2 path pairs in %d bytes, expanded %s"
+                 % (compact["records"], nbytes, s2records, s2bytes, "identically" if same else "DIFFERENTLY"))
 
     ms_step = elapsed / args.steps * 1e3
     reads_total = args.reads * world * args.steps
@@ -1067,6 +1123,7 @@ def main():
                           "stage2_alone_seeding": s2_seed_ms,
                           "stage2_alone_chaining": s2_chain_ms, "dynprog_alone": el_dp / half * 1e3,
                           "together": ms_step},
+        "block_runs": dict(block_runs),
         "launch_classes": sorted(({"kernel": n, "dispatches": e[1], "ms_per_step": round(e[0] / args.steps, 4)}
                                   for n, e in per_kernel.items()), key=lambda x: -x["ms_per_step"]),
         # the host's per-block planning (gmapdp_plan_create_all, gmapdp_stage2_plan_create: 16 host threads),

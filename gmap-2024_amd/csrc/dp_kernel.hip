@@ -671,7 +671,10 @@ __host__ __device__ inline CarveGG carve_gg(int rlength, int glengthL, int gleng
   return cv;
 }
 
-__host__ __device__ inline ScratchGG scratch_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds) {
+// (direction planes in global scratch: packed as in LDS for one-word bands, W the wider side's band -- 20 B
+// per column for the bench's ~37-lane bands instead of 32, the largest share of gg_kernel's writes)
+__host__ __device__ inline ScratchGG scratch_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds,
+                                                int W = 64) {
   ScratchGG sv;
   size_t off = 0;
   sv.partB = off; off = align16(off + 16u * (size_t)(rlength + 1));
@@ -680,8 +683,8 @@ __host__ __device__ inline ScratchGG scratch_gg(int rlength, int glengthL, int g
   sv.diagR = off; off = align16(off + 4u * (size_t)(rlength + 1));
   sv.dirsL = sv.dirsR = off;
   if (!dirs_lds) {
-    sv.dirsL = off; off = align16(off + gg_dirs_bytes(glengthL, R));
-    sv.dirsR = off; off = align16(off + gg_dirs_bytes(glengthR, R));
+    sv.dirsL = off; off = align16(off + (R == 1 ? gg_dirs_bytes_packed(glengthL, W) : gg_dirs_bytes(glengthL, R)));
+    sv.dirsR = off; off = align16(off + (R == 1 ? gg_dirs_bytes_packed(glengthR, W) : gg_dirs_bytes(glengthR, R)));
   }
   sv.total = off;
   return sv;
@@ -717,9 +720,9 @@ __global__ __launch_bounds__(128) GGX_ATTR void gg_kernel(
   const int late = (flags & kFLate) ? 1 : 0;
   const int lband = P.lbandL, ubandL = P.ubandL, ubandR = P.ubandR;
   const int WL = lband + ubandL + 1, WR = lband + ubandR + 1;
-  constexpr bool DPK = DIRS_LDS && R == 1;  // packed LDS direction planes (PackedDirs)
+  constexpr bool DPK = R == 1;  // packed direction planes (PackedDirs), in LDS or global scratch
   const CarveGG cv = carve_gg(rlen, gL, gR, R, DIRS_LDS, WL > WR ? WL : WR);
-  const ScratchGG sv = scratch_gg(rlen, gL, gR, R, DIRS_LDS);
+  const ScratchGG sv = scratch_gg(rlen, gL, gR, R, DIRS_LDS, WL > WR ? WL : WR);
   unsigned char* gbase = gscratch + P.dirs_offset;
   double* pL = reinterpret_cast<double*>(smem + cv.pL);
   double* pR = reinterpret_cast<double*>(smem + cv.pR);
@@ -1166,8 +1169,8 @@ static void* gptr() { return reinterpret_cast<void*>(&gg_kernel<R, D>); }
 size_t lds_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds, int W) {
   return carve_gg(rlength, glengthL, glengthR, R, dirs_lds, W).total;
 }
-size_t scratch_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds) {
-  return scratch_gg(rlength, glengthL, glengthR, R, dirs_lds).total;
+size_t scratch_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds, int W) {
+  return scratch_gg(rlength, glengthL, glengthR, R, dirs_lds, W).total;
 }
 
 hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevGenomeProblem* probs,

@@ -49,7 +49,7 @@ hipError_t launch_dpx(int S, int nproblems, int slot, int dirs_bytes, unsigned c
                       const char* qseq, const char* qseq_uc, const int8_t* sctab, const uint8_t* constab,
                       gmapdp_result* results, gmapdp_pair* pairs);
 size_t lds_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds, int W);
-size_t scratch_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds);
+size_t scratch_bytes_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds, int W);
 hipError_t launch_gg(int R, bool dirs_lds, int nblocks, size_t lds, hipStream_t stream, const DevGenomeProblem* probs,
                      const int* order, const uint32_t* blocks, uint64_t nwords, const char* qseq,
                      const char* qseq_uc, const double* sprob, const int8_t* sctab, const uint8_t* constab,
@@ -103,6 +103,9 @@ hipError_t launch_oi(bool wide, int nproblems, size_t lds, hipStream_t stream, c
 size_t scratch_bytes_oi_hits(int querylength, size_t hitcap);
 hipError_t launch_pc(const unsigned char* r0, int n0, int s0, const unsigned char* r1, int n1, int s1,
                      const gmapdp_pair* pairs, unsigned long long* offsets, unsigned char* out, hipStream_t stream);
+hipError_t launch_pc_paths(const gmapdp_path* paths, const unsigned long long* npaths, int path_cap,
+                           const gmapdp_path_pair* pairs, unsigned long long pair_cap, unsigned long long* offsets,
+                           unsigned char* out, hipStream_t stream);
 hipError_t launch_oi_split(int nproblems, int umax, hipStream_t stream, const DevOligoProblem* probs,
                            const uint32_t* blocks, const char* quc, unsigned char* scratch,
                            gmapdp_oligo_result* results, int32_t* npos, int32_t* map, uint32_t* table, int32_t* diags,
@@ -1256,7 +1259,7 @@ static ClassOf classify_gdev(DevGenomeProblem& d, bool latency, size_t lds_dirs_
   const bool dirs_lds = lds <= lds_dirs_max;
   if (!dirs_lds) lds = lds_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, false, std::max(WL, WR));
   // bridge candidates (+ direction planes) in global scratch
-  c.gdirs = (scratch_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, dirs_lds) + 255) & ~(size_t)255;
+  c.gdirs = (scratch_bytes_gg(d.rlength, d.glengthL, d.glengthR, R, dirs_lds, std::max(WL, WR)) + 255) & ~(size_t)255;
   if (lds > 160 * 1024) { c.err = "problem exceeds the LDS of a CU"; return c; }
   c.need = gg_lds_bucket(lds);
   c.key = class_key((int)PlanCore::kGenomeGap, R, dirs_lds ? 1 : 0, latency ? 0 : c.need);
@@ -2502,24 +2505,29 @@ int gmapdp_plan_run_launch(gmapdp_ctx* ctx, const gmapdp_plan* plan, int li, con
 // Host side of the compact pair stream: problem i's ops at stream[offsets[i], offsets[i + 1]) back to its
 // npairs[i] records at out[pair_offsets[i]] (threads over the problems).  GMAPDP_EINVAL when a problem's
 // ops do not decode to exactly its records and bytes.
-int gmapdp_expand_pairs(const uint8_t* stream, const uint64_t* offsets, int n, const int32_t* npairs,
-                        const int64_t* pair_offsets, gmapdp_pair* out, int nthreads) {
-  if (n < 0 || (n && (!stream || !offsets || !npairs || !pair_offsets || !out))) return GMAPDP_EINVAL;
+}  // extern "C"
+
+// (Rec: gmapdp_pair, 17-B RAW ops, or gmapdp_path_pair, 21-B RAW ops; list i: npairs_of(i) records at
+// offset_of(i))
+template <typename Rec, typename NP, typename OF>
+static int expand_stream(const uint8_t* stream, const uint64_t* offsets, int n, NP&& npairs_of, OF&& offset_of,
+                         Rec* out, int nthreads) {
   static const char nt[4] = {'A', 'C', 'G', 'T'}, cp[4] = {'*', '|', ' ', ':'};
+  constexpr int kRaw = 1 + (int)sizeof(Rec);
   const int T = nthreads > 0 ? nthreads : plan_threads((size_t)n * 64);
   std::vector<int> bad_at(T, -1);
   plan_parallel((size_t)n, T, [&](size_t lo, size_t hi, int t) {
     for (size_t i = lo; i < hi; i++) {
       const uint8_t* p = stream + offsets[i];
       const uint8_t* end = stream + offsets[i + 1];
-      gmapdp_pair* o = out + pair_offsets[i];
+      const int m = std::max<int>(npairs_of(i), 0);
+      Rec* o = m ? out + offset_of(i) : out;
       int k = 0;
-      const int m = std::max(npairs[i], 0);
       while (k < m && p < end) {
         if (*p == 0x02) {
-          if (end - p < 17) break;
-          std::memcpy(&o[k++], p + 1, 16);
-          p += 17;
+          if (end - p < kRaw) break;
+          std::memcpy(&o[k++], p + 1, sizeof(Rec));
+          p += kRaw;
           continue;
         }
         if (*p != 0x01 || end - p < 13) break;
@@ -2530,10 +2538,15 @@ int gmapdp_expand_pairs(const uint8_t* stream, const uint64_t* offsets, int n, c
         const int len = p[11] | (p[12] << 8);
         p += 13;
         for (int r = 0; r < len && k < m && p < end; r++, k++) {
-          gmapdp_pair& x = o[k];
+          Rec& x = o[k];
           x.querypos = q + r * dq;
           x.genomepos = g + r * dg;
-          x.jump = 0;
+          if constexpr (sizeof(Rec) == sizeof(gmapdp_pair)) {
+            x.jump = 0;
+          } else {
+            x.queryjump = 0;
+            x.genomejump = 0;
+          }
           if (*p == 0xFF) {
             std::memcpy(&x.cdna, p + 1, 4);
             p += 5;
@@ -2554,6 +2567,22 @@ int gmapdp_expand_pairs(const uint8_t* stream, const uint64_t* offsets, int n, c
   for (int t = 0; t < T; t++)
     if (bad_at[t] >= 0) return GMAPDP_EINVAL;
   return GMAPDP_OK;
+}
+
+extern "C" {
+
+int gmapdp_expand_pairs(const uint8_t* stream, const uint64_t* offsets, int n, const int32_t* npairs,
+                        const int64_t* pair_offsets, gmapdp_pair* out, int nthreads) {
+  if (n < 0 || (n && (!stream || !offsets || !npairs || !pair_offsets || !out))) return GMAPDP_EINVAL;
+  return expand_stream(stream, offsets, n, [&](size_t i) { return npairs[i]; },
+                       [&](size_t i) { return pair_offsets[i]; }, out, nthreads);
+}
+
+int gmapdp_expand_path_pairs(const uint8_t* stream, const uint64_t* offsets, int npaths, const gmapdp_path* paths,
+                             gmapdp_path_pair* out, int nthreads) {
+  if (npaths < 0 || (npaths && (!stream || !offsets || !paths || !out))) return GMAPDP_EINVAL;
+  return expand_stream(stream, offsets, npaths, [&](size_t i) { return paths[i].npairs; },
+                       [&](size_t i) { return paths[i].pair_offset; }, out, nthreads);
 }
 
 // The compact pair stream (pc_kernel.hip): the plan's GPU problems in dev-slot order, then its genome gaps.
@@ -3908,6 +3937,22 @@ int gmapdp_stage2_plan_fetch(gmapdp_ctx* ctx, const gmapdp_stage2_plan* plan, co
   if (e == hipSuccess) e = ctx_sync(ctx, s);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "stage-2 plan fetch: %s", e);
   return GMAPDP_OK;
+}
+
+// The compact stream of the plan's path pairs (pc_kernel.hip), one list per path record of the pool
+size_t gmapdp_stage2_plan_compact_bound(const gmapdp_stage2_plan* plan, size_t* path_cap) {
+  if (path_cap) *path_cap = plan ? plan->path_cap : 0;
+  return plan ? 21 * plan->pair_cap + 64 : 0;
+}
+int gmapdp_stage2_plan_compact_pairs(gmapdp_ctx* ctx, const gmapdp_stage2_plan* plan, uint8_t* d_out,
+                                     uint64_t* d_offsets, void* stream) {
+  if (!ctx || !plan || !d_offsets) return GMAPDP_EINVAL;
+  if (plan->path_cap > (size_t)INT32_MAX) return bad(ctx, "stage-2 compaction: too many path records");
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  const hipError_t e = launch_pc_paths(plan->d_paths, plan->d_counters + 1, (int)plan->path_cap, plan->d_pairs,
+                                       plan->pair_cap, (unsigned long long*)d_offsets, (unsigned char*)d_out, s);
+  return e == hipSuccess ? GMAPDP_OK : fail(ctx, GMAPDP_ELAUNCH, "path pair compaction: %s", e);
 }
 
 int gmapdp_stage2_plan_seeding_classes(const gmapdp_stage2_plan* plan, int* n16, int* n32) {

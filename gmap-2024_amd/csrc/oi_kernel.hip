@@ -812,6 +812,15 @@ __device__ __forceinline__ void oi_pass(OI_PASS_ARGS) {
     }
     if (lane == 0) tot_s = tot;
   }
+  // each query position's 8-mer as its id (get_mappings' lookups), so that the bitmap and its ranks are free
+  // for pass 2's table staging
+  for (int i = tid; i < nq; i += 64 * kOiWaves) {
+    const int m = mpq[i];
+    if (m >= 0) {
+      bool in;
+      mpq[i] = oligo_id(bitmap, wrank, (uint32_t)m, in);
+    }
+  }
   __syncthreads();
   const uint32_t tot = tot_s;
   OI_MARK(2);
@@ -824,18 +833,23 @@ __device__ __forceinline__ void oi_pass(OI_PASS_ARGS) {
   }
 
   // ---- pass 2: store in descending chrpos (plus: right to left; minus: left to right) ----
+  // Compact lists: each hit's table slot goes beside its entry (the hit region's second half, unused by
+  // 4-B entries), then both waves place the hits into LDS images of the table, 3 072 slots at a time, each
+  // written out coalesced -- instead of one scattered 4-B store per hit (~8x the table's bytes
+  // in partial-line writes).
   uint32_t* table = table_all + P.table_offset;
+  uint32_t* slotarr = hitlist32 + P.hit_cap;
   const uint32_t chrpos0 = P.plusp ? P.chrstart : (P.chrhigh - P.chroffset) - P.chrend;
   const int idbits = U > 1 ? 32 - __clz(U - 1) : 1;
   __threadfence_block();
   for (int c = 0; wave == 0 && c < nhits; c += 64) {
     const int sl = c + lane;  // sl-th hit in store order: plus walks the list backwards
     int id = -1;
-    uint32_t k = 0;
+    uint32_t k = 0, at = 0;
     if (sl < nhits) {
       // ascending position: wave 0's list, then wave 1's from the list's end backwards
       const int a = P.plusp ? nhits - 1 - sl : sl;
-      const uint32_t at = a < n0 ? (uint32_t)a : P.hit_cap - 1 - (uint32_t)(a - n0);
+      at = a < n0 ? (uint32_t)a : P.hit_cap - 1 - (uint32_t)(a - n0);
       if (compact) {
         const uint32_t e = hitlist32[at];
         k = e >> 14;
@@ -858,12 +872,34 @@ __device__ __forceinline__ void oi_pass(OI_PASS_ARGS) {
       const int rank = lanes_below(eq, lane);
       const int same = __popcll(eq);
       const int r0 = (int)cnt[id];  // every lane reads before the first lane of each oligo writes
-      if (r0 - rank > 0)
-        table[offs[id] + r0 - rank - 1] = chrpos0 + (P.plusp ? k : (uint32_t)(npos - 1) - k);
+      const uint32_t slot = (uint32_t)offs[id] + (uint32_t)(r0 - rank - 1);
+      if (compact)
+        slotarr[at] = r0 - rank > 0 ? slot : 0xFFFFFFFFu;
+      else if (r0 - rank > 0)
+        table[slot] = chrpos0 + (P.plusp ? k : (uint32_t)(npos - 1) - k);
       if (rank == 0) cnt[id] = (CT)max(r0 - same, 0);
     }
   }
+  __threadfence_block();
   __syncthreads();
+  if (compact) {  // every slot of [0, tot) is some hit's (a wrapped count keeps its first count & 255 hits)
+    uint32_t* stage = reinterpret_cast<uint32_t*>(smem);  // the bitmap and ranks (12 KB)
+    constexpr uint32_t kStage = 6 * kOiWords / 4;
+    for (uint32_t b0 = 0; b0 < tot; b0 += kStage) {
+      for (int a = tid; a < nhits; a += 64 * kOiWaves) {
+        const uint32_t at = a < n0 ? (uint32_t)a : P.hit_cap - 1 - (uint32_t)(a - n0);
+        const uint32_t sd = slotarr[at] - b0;
+        if (sd < kStage) {
+          const uint32_t k = hitlist32[at] >> 14;
+          stage[sd] = chrpos0 + (P.plusp ? k : (uint32_t)(npos - 1) - k);
+        }
+      }
+      __syncthreads();
+      const uint32_t nb = min(kStage, tot - b0);
+      for (uint32_t j = tid; j < nb; j += 64 * kOiWaves) table[b0 + j] = stage[j];
+      __syncthreads();
+    }
+  }
   // the per-id counts again (nhits of lookup, :34074)
   OI_MARK(3);
   for (int u = tid; u < U; u += 64 * kOiWaves)
@@ -900,8 +936,7 @@ __device__ __forceinline__ void oi_pass(OI_PASS_ARGS) {
       if (i < nq) {
         int mo = -1;
         if (m >= 0) {
-          bool in;
-          const int u = oligo_id(bitmap, wrank, (uint32_t)m, in);
+          const int u = m;  // (the id, converted after pass 1)
           nh = (int)cnt[u];
           npq[i] = nh;
           if (nh > 0) mo = (int32_t)(uint32_t)offs[u];  // relative to the problem's table

@@ -9,6 +9,9 @@
 //          record: cdna | genome << 2 | comp << 4 (cdna, genome in ACGT, comp one of '*' '|' ' ' ':',
 //          genomealt = genome), or 0xFF and the record's four characters;
 //   RAW  : 0x02 and the 16-B record (gap holders, records with a jump or a negative position).
+// Stage 2's path pairs (gmapdp_path_pair, 20 B: querypos, genomepos, queryjump, genomejump, the four
+// characters; stage2.c convert_to_nucleotides) take the same ops with a 21-B RAW (any jump or negative
+// position); their lists are the plan's paths (gmapdp_path: pair_offset, npairs).
 // Record k of a RUN sits at (querypos + k dq, genomepos + k dg).  A 10 000-read bench block's 94 M records
 // (1.5 GB) take ~0.1 GB.  gmapdp_expand_pairs (gmapdp_engine.cpp) restores the records exactly.
 //
@@ -23,7 +26,7 @@
 namespace gmapdp {
 
 constexpr unsigned char kPcRun = 0x01, kPcRaw = 0x02, kPcEsc = 0xFF;
-constexpr int kPcHeader = 13, kPcRawBytes = 17;
+constexpr int kPcHeader = 13;
 
 __device__ __forceinline__ int pc_nt(char c) {
   return c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : c == 'T' ? 3 : -1;
@@ -31,38 +34,77 @@ __device__ __forceinline__ int pc_nt(char c) {
 __device__ __forceinline__ int pc_comp(char c) {
   return c == '*' ? 0 : c == '|' ? 1 : c == ' ' ? 2 : c == ':' ? 3 : -1;
 }
-// the record's one-byte code, or -1: escaped
-__device__ __forceinline__ int pc_code(int4 r) {
-  const uint32_t ch = (uint32_t)r.w;
+// the record's one-byte code from its four characters (cdna, comp, genome, genomealt), or -1: escaped
+__device__ __forceinline__ int pc_code(uint32_t ch) {
   const char cdna = (char)(ch & 0xFF), comp = (char)((ch >> 8) & 0xFF), gen = (char)((ch >> 16) & 0xFF),
              alt = (char)(ch >> 24);
   const int a = pc_nt(cdna), b = pc_nt(gen), c = pc_comp(comp);
   return (a < 0 || b < 0 || c < 0 || alt != gen) ? -1 : a | (b << 2) | (c << 4);
 }
 
-// the problem list: n0 records of stride s0 bytes then n1 of stride s1 (gmapdp_result / gmapdp_genome_result:
-// npairs at byte 0, pair_offset at byte 4)
+// the DP lists: n0 records of stride s0 bytes then n1 of stride s1 (gmapdp_result / gmapdp_genome_result:
+// npairs at byte 0, pair_offset at byte 4); 16-B gmapdp_pair records
 struct PcProblems {
   const unsigned char* r0;
   const unsigned char* r1;
   int n0, n1, s0, s1;
+  const int4* pairs;
+  static constexpr int kRaw = 17;
+  __device__ __forceinline__ void list(int i, int& npairs, long long& off) const {
+    const int* r = reinterpret_cast<const int*>(i < n0 ? r0 + (size_t)i * s0 : r1 + (size_t)(i - n0) * s1);
+    npairs = r[0];
+    off = r[1];
+  }
+  // record k of the list at `off`: positions, whether it must go RAW, its characters; raw bytes for RAW
+  __device__ __forceinline__ void rec(long long off, int k, int& q, int& g, bool& jump, uint32_t& ch) const {
+    const int4 r = pairs[off + k];
+    q = r.x;
+    g = r.y;
+    jump = r.z != 0;
+    ch = (uint32_t)r.w;
+  }
+  __device__ __forceinline__ const unsigned char* raw(long long off, int k) const {
+    return reinterpret_cast<const unsigned char*>(pairs + off + k);
+  }
 };
-__device__ __forceinline__ void pc_problem(const PcProblems& P, int i, int& npairs, int& off) {
-  const int* r = reinterpret_cast<const int*>(i < P.n0 ? P.r0 + (size_t)i * P.s0 : P.r1 + (size_t)(i - P.n0) * P.s1);
-  npairs = r[0];
-  off = r[1];
-}
+// stage 2's path lists: the plan's paths (count in *npaths, at most the launch's grid), 20-B gmapdp_path_pair
+struct PcPaths {
+  const gmapdp_path* paths;
+  const unsigned long long* npaths;
+  const gmapdp_path_pair* pairs;
+  unsigned long long pair_cap;
+  static constexpr int kRaw = 21;
+  __device__ __forceinline__ void list(int i, int& npairs, long long& off) const {
+    npairs = 0;
+    off = 0;
+    if ((unsigned long long)i >= *npaths) return;
+    const gmapdp_path p = paths[i];
+    // (a call that overflowed the pools reports status -2; its records need not be in the pool)
+    if (p.pair_offset < 0 || p.npairs < 0 || (unsigned long long)p.pair_offset + p.npairs > pair_cap) return;
+    npairs = p.npairs;
+    off = p.pair_offset;
+  }
+  __device__ __forceinline__ void rec(long long off, int k, int& q, int& g, bool& jump, uint32_t& ch) const {
+    const int* r = reinterpret_cast<const int*>(pairs + off + k);
+    q = r[0];
+    g = r[1];
+    jump = (r[2] | r[3]) != 0;
+    ch = (uint32_t)r[4];
+  }
+  __device__ __forceinline__ const unsigned char* raw(long long off, int k) const {
+    return reinterpret_cast<const unsigned char*>(pairs + off + k);
+  }
+};
 
-template <bool WRITE>
-__global__ __launch_bounds__(64) void pc_kernel(PcProblems P, const int4* __restrict__ pairs,
-                                               unsigned long long* __restrict__ sizes_or_offsets,
+template <bool WRITE, typename Src>
+__global__ __launch_bounds__(64) void pc_kernel(Src P, unsigned long long* __restrict__ sizes_or_offsets,
                                                unsigned char* __restrict__ out) {
   const int lane = threadIdx.x;
   const int i = blockIdx.x;
-  int npairs, off;
-  pc_problem(P, i, npairs, off);
+  int npairs;
+  long long off;
+  P.list(i, npairs, off);
   npairs = max(npairs, 0);
-  const int4* rec = pairs + off;
   unsigned char* o = WRITE ? out + sizes_or_offsets[i] : nullptr;
   unsigned long long pos = 0;  // bytes written so far
   // carries: the previous record (q, g, raw), the step into it (valid?), the open run's header position
@@ -72,9 +114,11 @@ __global__ __launch_bounds__(64) void pc_kernel(PcProblems P, const int4* __rest
   for (int c0 = 0; c0 < npairs; c0 += 64) {
     const int k = c0 + lane;
     const bool v = k < npairs;
-    const int4 r = v ? rec[k] : make_int4(0, 0, 0, 0);
-    const int q = r.x, g = r.y;
-    const bool raw = v && (r.z != 0 || q < 0 || g < 0);
+    int q = 0, g = 0;
+    bool jump = false;
+    uint32_t ch = 0;
+    if (v) P.rec(off, k, q, g, jump, ch);
+    const bool raw = v && (jump || q < 0 || g < 0);
     // the previous record (lane - 1, or the carry)
     int q1 = __shfl_up(q, 1, 64), g1 = __shfl_up(g, 1, 64);
     int raw1 = __shfl_up(raw ? 1 : 0, 1, 64);
@@ -94,8 +138,8 @@ __global__ __launch_bounds__(64) void pc_kernel(PcProblems P, const int4* __rest
     }
     const bool cont = stepok && (!s1v || (dq == s1q && dg == s1g));
     const bool start = v && !raw && !cont;
-    const int code = v && !raw ? pc_code(r) : 0;
-    const int bytes = !v ? 0 : raw ? kPcRawBytes : (start ? kPcHeader : 0) + (code < 0 ? 5 : 1);
+    const int code = v && !raw ? pc_code(ch) : 0;
+    const int bytes = !v ? 0 : raw ? Src::kRaw : (start ? kPcHeader : 0) + (code < 0 ? 5 : 1);
     const int incl = wave_scan_add(lane, bytes);
     const unsigned long long at = pos + (unsigned long long)(incl - bytes);
     // run ends: the open run (from an earlier step, or a lane below) closes at the first record that does not
@@ -104,8 +148,8 @@ __global__ __launch_bounds__(64) void pc_kernel(PcProblems P, const int4* __rest
     if (WRITE) {
       if (raw) {
         o[at] = kPcRaw;
-        const unsigned char* b = reinterpret_cast<const unsigned char*>(&r);
-        for (int x = 0; x < 16; x++) o[at + 1 + x] = b[x];
+        const unsigned char* b = P.raw(off, k);
+        for (int x = 0; x < Src::kRaw - 1; x++) o[at + 1 + x] = b[x];
       } else if (v) {
         unsigned long long p = at;
         if (start) {
@@ -120,8 +164,7 @@ __global__ __launch_bounds__(64) void pc_kernel(PcProblems P, const int4* __rest
         }
         if (code < 0) {
           o[p] = kPcEsc;
-          const unsigned char* b = reinterpret_cast<const unsigned char*>(&r.w);
-          for (int x = 0; x < 4; x++) o[p + 1 + x] = b[x];
+          for (int x = 0; x < 4; x++) o[p + 1 + x] = (unsigned char)(ch >> (8 * x));
         } else {
           o[p] = (unsigned char)code;
         }
@@ -232,13 +275,25 @@ __global__ __launch_bounds__(1024) void pc_scan_kernel(unsigned long long* __res
 
 hipError_t launch_pc(const unsigned char* r0, int n0, int s0, const unsigned char* r1, int n1, int s1,
                      const gmapdp_pair* pairs, unsigned long long* offsets, unsigned char* out, hipStream_t stream) {
-  PcProblems P{r0, r1, n0, n1, s0, s1};
+  PcProblems P{r0, r1, n0, n1, s0, s1, reinterpret_cast<const int4*>(pairs)};
   const int n = n0 + n1;
   if (n <= 0) return hipMemsetAsync(offsets, 0, sizeof(unsigned long long), stream);
-  const int4* pr = reinterpret_cast<const int4*>(pairs);
-  hipLaunchKernelGGL(pc_kernel<false>, dim3(n), dim3(64), 0, stream, P, pr, offsets, (unsigned char*)nullptr);
+  hipLaunchKernelGGL((pc_kernel<false, PcProblems>), dim3(n), dim3(64), 0, stream, P, offsets, (unsigned char*)nullptr);
   hipLaunchKernelGGL(pc_scan_kernel, dim3(1), dim3(1024), 0, stream, offsets, n);
-  if (out) hipLaunchKernelGGL(pc_kernel<true>, dim3(n), dim3(64), 0, stream, P, pr, offsets, out);
+  if (out) hipLaunchKernelGGL((pc_kernel<true, PcProblems>), dim3(n), dim3(64), 0, stream, P, offsets, out);
+  return hipGetLastError();
+}
+
+// stage 2: path_cap lists (those past *npaths are empty), offsets path_cap + 1 entries
+hipError_t launch_pc_paths(const gmapdp_path* paths, const unsigned long long* npaths, int path_cap,
+                           const gmapdp_path_pair* pairs, unsigned long long pair_cap, unsigned long long* offsets,
+                           unsigned char* out, hipStream_t stream) {
+  PcPaths P{paths, npaths, pairs, pair_cap};
+  if (path_cap <= 0) return hipMemsetAsync(offsets, 0, sizeof(unsigned long long), stream);
+  hipLaunchKernelGGL((pc_kernel<false, PcPaths>), dim3(path_cap), dim3(64), 0, stream, P, offsets,
+                     (unsigned char*)nullptr);
+  hipLaunchKernelGGL(pc_scan_kernel, dim3(1), dim3(1024), 0, stream, offsets, path_cap);
+  if (out) hipLaunchKernelGGL((pc_kernel<true, PcPaths>), dim3(path_cap), dim3(64), 0, stream, P, offsets, out);
   return hipGetLastError();
 }
 

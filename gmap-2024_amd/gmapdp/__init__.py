@@ -298,6 +298,9 @@ def load_library(path=LIB_PATH):
                                                 C.c_void_p, C.c_void_p]),
         "gmapdp_expand_pairs": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                           C.c_int]),
+        "gmapdp_stage2_plan_compact_bound": (C.c_size_t, [C.c_void_p, P(C.c_size_t)]),
+        "gmapdp_stage2_plan_compact_pairs": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+        "gmapdp_expand_path_pairs": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int]),
         "gmapdp_maxent_sites": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
         "gmapdp_microexon_plan_create": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                                    C.c_size_t, P(C.c_void_p)]),
@@ -799,12 +802,14 @@ class Engine:
             out.append((int(r["nresults"]), lists))
         return out
 
-    def stage2_plan_raw(self, probs, qbuf, qucbuf, run_qbuf=None, run_qucbuf=None):
+    def stage2_plan_raw(self, probs, qbuf, qucbuf, run_qbuf=None, run_qucbuf=None, compact_out=None):
         """The device-resident Stage2_compute plan (bench.py's path): gmapdp_stage2_plan_create on
         (probs, qbuf, qucbuf) -- its sizing run, the measured re-layout, the 16-bit seeding class --,
         gmapdp_stage2_plan_run(what = 3) against device copies of the query arenas (run_qbuf /
         run_qucbuf when given: another query of the same layout), gmapdp_stage2_plan_fetch.  Returns
-        (results, paths, pairs, (calls with 16-bit, with 32-bit seeding counters))."""
+        (results, paths, pairs, (calls with 16-bit, with 32-bit seeding counters)).  compact_out (a dict):
+        also the compact stream of the path pairs (gmapdp_stage2_plan_compact_pairs) expanded on the host
+        (gmapdp_expand_path_pairs): compact_out["pairs"] (an arena like `pairs`), ["bytes"]."""
         lib, n = self.lib, len(probs)
         hip = _hip()
         plan = C.c_void_p()
@@ -841,6 +846,21 @@ class Engine:
             self._check(lib.gmapdp_stage2_plan_fetch(self.h, plan, d_res, None, results.ctypes.data, paths.ctypes.data,
                                                      len(paths), pairs.ctypes.data, len(pairs), C.byref(pn),
                                                      C.byref(qn)), "gmapdp_stage2_plan_fetch")
+            if compact_out is not None:
+                pcap = C.c_size_t()
+                bound = lib.gmapdp_stage2_plan_compact_bound(plan, C.byref(pcap))
+                d_off, d_out = dbuf(8 * (pcap.value + 1)), dbuf(bound)
+                self._check(lib.gmapdp_stage2_plan_compact_pairs(self.h, plan, d_out, d_off, None), "compact")
+                if hip.hipDeviceSynchronize() != 0:
+                    raise GmapdpError("hipDeviceSynchronize failed")
+                offs = np.zeros(pn.value + 1, dtype=np.uint64)
+                if hip.hipMemcpy(offs.ctypes.data, d_off, offs.nbytes, 2) != 0:  # hipMemcpyDeviceToHost
+                    raise GmapdpError("hipMemcpy failed")
+                stream = np.zeros(max(int(offs[-1]), 1), dtype=np.uint8)
+                if hip.hipMemcpy(stream.ctypes.data, d_out, stream.nbytes, 2) != 0:
+                    raise GmapdpError("hipMemcpy failed")
+                compact_out["pairs"] = expand_path_pairs(stream, offs, paths[:pn.value], max(qn.value, 1))
+                compact_out["bytes"] = int(offs[-1])
             return results, paths[:pn.value], pairs[:qn.value], (n16.value, n32.value)
         finally:
             for b in bufs:
@@ -1066,4 +1086,20 @@ def expand_pairs(stream, offsets, npairs, pair_offsets, capacity, nthreads=0):
                                  out.ctypes.data, int(nthreads))
     if rc != 0:
         raise GmapdpError("gmapdp_expand_pairs: the stream does not decode to the records (%d)" % rc)
+    return out
+
+
+def expand_path_pairs(stream, offsets, paths, capacity, nthreads=0):
+    """gmapdp_expand_path_pairs (host only): a stage-2 plan's compact path-pair stream back to gmapdp_path_pair
+    records; a pair arena of `capacity` records with each path's npairs at its pair_offset (`paths`: the
+    plan's PATH_DTYPE records, one stream list each)."""
+    lib = load_library()
+    out = np.zeros(max(int(capacity), 1), dtype=PATH_PAIR_DTYPE)
+    st = np.ascontiguousarray(stream, dtype=np.uint8)
+    of = np.ascontiguousarray(offsets, dtype=np.uint64)
+    pa = np.ascontiguousarray(paths, dtype=PATH_DTYPE)
+    rc = lib.gmapdp_expand_path_pairs(st.ctypes.data, of.ctypes.data, len(pa), pa.ctypes.data, out.ctypes.data,
+                                      int(nthreads))
+    if rc != 0:
+        raise GmapdpError("gmapdp_expand_path_pairs: the stream does not decode to the records (%d)" % rc)
     return out

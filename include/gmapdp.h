@@ -682,6 +682,17 @@ int gmapdp_stage2_plan_seeding_results (gmapdp_ctx *ctx, const gmapdp_stage2_pla
 /* How many of the plan's calls seed with 16-bit and with 32-bit counters (after the plan's sizing run
  * moved every call with fewer than 2^16 hits to the 16-bit class). */
 int gmapdp_stage2_plan_seeding_classes (const gmapdp_stage2_plan *plan, int *n16, int *n32);
+/* The compact stream of a finished chaining run's path pairs (gmapdp_plan_compact_pairs' format, 21-B RAW
+ * ops: gmapdp_path_pair records with a jump or a negative position): one list per record of the plan's path
+ * pool (*path_cap of them; records past the pool's count are empty lists).  d_offsets: path_cap + 1 uint64
+ * (device), exclusive offsets and the total; d_out NULL sizes only, else at least
+ * gmapdp_stage2_plan_compact_bound bytes.  gmapdp_expand_path_pairs restores the records on the host, each
+ * path's npairs at its pair_offset (the path records as gmapdp_stage2_plan_fetch returns them). */
+size_t gmapdp_stage2_plan_compact_bound (const gmapdp_stage2_plan *plan, size_t *path_cap);
+int gmapdp_stage2_plan_compact_pairs (gmapdp_ctx *ctx, const gmapdp_stage2_plan *plan, uint8_t *d_out,
+                                      uint64_t *d_offsets, void *stream);
+int gmapdp_expand_path_pairs (const uint8_t *stream, const uint64_t *offsets, int npaths, const gmapdp_path *paths,
+                              gmapdp_path_pair *out, int nthreads);
 void gmapdp_stage2_plan_destroy (gmapdp_stage2_plan *plan);
 
 /* Create a context on HIP device `device`.  mode = Mode_T (mode.h:5;

@@ -161,3 +161,29 @@ def test_expand_pairs_decodes_the_stream_format():
                    (14, 103, 0, b"C- C"), (-1, -1, 250, b" > .")], got
     with pytest.raises(gmapdp.GmapdpError):
         gmapdp.expand_pairs(stream[:-3], [0, len(s) - 3], [6], [2], 8)
+
+
+def test_expand_path_pairs_decodes_the_stream_format():
+    """gmapdp_expand_path_pairs (host only, no GPU): the same ops over stage 2's 20-B path pairs -- a RUN of
+    matches, a 21-B RAW gap holder with both jumps -- two paths, the second at its own pair_offset; a stream
+    that ends early is refused."""
+    import struct
+    import numpy as np
+    import gmapdp
+    run = lambda q, g, dq, dg, n: struct.pack("<BiibbH", 1, q, g, dq, dg, n)  # noqa: E731
+    code = lambda c: bytes(["ACGT".index(c) | ("ACGT".index(c) << 2) | (1 << 4)])  # noqa: E731
+    a = run(0, 500, 1, 1, 3) + code("A") + code("C") + code("G")
+    a += b"\x02" + struct.pack("<iiii", -1, -1, 7, 130) + b" - ."
+    b = run(40, 900, 1, 1, 2) + code("T") + b"\xff" + b"n|N."
+    stream = np.frombuffer(a + b, dtype=np.uint8)
+    paths = np.zeros(2, dtype=gmapdp.PATH_DTYPE)
+    paths["pair_offset"] = [0, 6]
+    paths["npairs"] = [4, 2]
+    out = gmapdp.expand_path_pairs(stream, [0, len(a), len(a) + len(b)], paths, 8)
+    got = [(int(r["querypos"]), int(r["genomepos"]), int(r["queryjump"]), int(r["genomejump"]),
+            bytes(r["cdna"] + r["comp"] + r["genome"] + r["genomealt"])) for r in out]
+    assert got[:4] == [(0, 500, 0, 0, b"A|AA"), (1, 501, 0, 0, b"C|CC"), (2, 502, 0, 0, b"G|GG"),
+                       (-1, -1, 7, 130, b" - .")], got
+    assert got[6:8] == [(40, 900, 0, 0, b"T|TT"), (41, 901, 0, 0, b"n|N.")], got
+    with pytest.raises(gmapdp.GmapdpError):
+        gmapdp.expand_path_pairs(stream[:-2], [0, len(a), len(a) + len(b) - 2], paths, 8)

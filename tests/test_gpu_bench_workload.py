@@ -211,7 +211,9 @@ def test_gpu_bench_configs2_stage2_every_call(grch38_block0):
         13.6 GB of table for this block, past 2^31 entries -- the mappings are relative to each call's table);
       - the device-resident plan bench.py times (gmapdp_stage2_plan_create: the sizing run, the arenas
         re-laid out from it, the calls with fewer than 2^16 hits moved to the 16-bit seeding counters;
-        gmapdp_stage2_plan_run; gmapdp_stage2_plan_fetch)."""
+        gmapdp_stage2_plan_run; gmapdp_stage2_plan_fetch);
+    and the plan's compact path-pair stream (gmapdp_stage2_plan_compact_pairs) expands on the host to exactly
+    the records gmapdp_stage2_plan_fetch returns."""
     genome, d = grch38_block0
     s2p = _stage2_problems(d)
     q = d["oq"].tobytes()
@@ -224,10 +226,16 @@ def test_gpu_bench_configs2_stage2_every_call(grch38_block0):
         _progress("gmapdp_stage2_batch done")
         bad = stage2_mismatches(res, paths, pairs, exp)
         assert not bad, "gmapdp_stage2_batch differs from the oracle on %d of %d calls: %s" % (len(bad), len(s2p), bad[:8])
-        pres, ppaths, ppairs, (n16, n32) = eng.stage2_plan_raw(s2p, q, q)
+        cmp = {}
+        pres, ppaths, ppairs, (n16, n32) = eng.stage2_plan_raw(s2p, q, q, compact_out=cmp)
         _progress("stage-2 plan done (%d calls 16-bit, %d 32-bit)" % (n16, n32))
         bad = stage2_mismatches(pres, ppaths, ppairs, exp)
         assert not bad, "the stage-2 plan differs from the oracle on %d of %d calls: %s" % (len(bad), len(s2p), bad[:8])
+        cnt = np.maximum(ppaths["npairs"].astype(np.int64), 0)
+        idx = np.repeat(ppaths["pair_offset"], cnt) + (np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt))
+        assert len(idx) > 0 and np.array_equal(cmp["pairs"][idx], ppairs[idx]), \
+            "the compact path-pair stream does not expand to the records"
+        _progress("compact path-pair stream: %d records in %d bytes" % (len(idx), cmp["bytes"]))
     finally:
         eng.close()
     # the bench's configuration: 214-kb windows (>= 2^16 starts) seeded with 16-bit counters after the re-layout

@@ -56,6 +56,21 @@ def workload_of(src):
         return None
 
 
+def bench_block_runs(src):
+    """block_runs of the bench line the kernel-trace pass printed (stats.log), or None"""
+    try:
+        lines = open(os.path.join(src, "stats.log")).read().splitlines()
+    except OSError:
+        return None
+    for ln in reversed(lines):
+        if ln.startswith("{") and '"block_runs"' in ln:
+            try:
+                return json.loads(ln).get("block_runs")
+            except ValueError:
+                return None
+    return None
+
+
 def main(src, dst, iso=False):
     os.makedirs(dst, exist_ok=True)
     stats = find(src, "stats", "run_kernel_stats.csv")
@@ -103,6 +118,11 @@ def main(src, dst, iso=False):
                           "FETCH_SIZE counts half of wide reads)",
         "kernels": dict(sorted(kern.items(), key=lambda kv: -kv[1].get("total_ms", 0.0))),
     }
+    # the bench line's count of stage-2 kernel runs over a block in the profiled process (bench.py
+    # pmc_entry: dispatch totals / runs = bytes per block, whatever the seeding's launch chunks per block)
+    runs = bench_block_runs(src)
+    if runs:
+        summary["block_runs"] = runs
     with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     shutil.copy(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profile.sh"),
