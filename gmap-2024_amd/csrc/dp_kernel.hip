@@ -671,8 +671,15 @@ __host__ __device__ inline CarveGG carve_gg(int rlength, int glengthL, int gleng
   return cv;
 }
 
-// (direction planes in global scratch: packed as in LDS for one-word bands, W the wider side's band -- 20 B
-// per column for the bench's ~37-lane bands instead of 32, the largest share of gg_kernel's writes)
+// Direction planes in global scratch packed as in LDS for one-word bands (GMAPDP_GG_PACK_GLOBAL builds,
+// experiments): 20 B per column for the bench's ~37-lane bands instead of 32, but lane 0's packing sits on
+// the column loop's issue path and gg_kernel<1, 0> measured 2.04 ms per launch against 1.93 unpacked
+// (profiles/r06_seed), so the product stores the four 64-bit ballots.
+#ifdef GMAPDP_GG_PACK_GLOBAL
+constexpr bool kGgPackGlobal = true;
+#else
+constexpr bool kGgPackGlobal = false;
+#endif
 __host__ __device__ inline ScratchGG scratch_gg(int rlength, int glengthL, int glengthR, int R, bool dirs_lds,
                                                 int W = 64) {
   ScratchGG sv;
@@ -683,8 +690,9 @@ __host__ __device__ inline ScratchGG scratch_gg(int rlength, int glengthL, int g
   sv.diagR = off; off = align16(off + 4u * (size_t)(rlength + 1));
   sv.dirsL = sv.dirsR = off;
   if (!dirs_lds) {
-    sv.dirsL = off; off = align16(off + (R == 1 ? gg_dirs_bytes_packed(glengthL, W) : gg_dirs_bytes(glengthL, R)));
-    sv.dirsR = off; off = align16(off + (R == 1 ? gg_dirs_bytes_packed(glengthR, W) : gg_dirs_bytes(glengthR, R)));
+    const bool pk = R == 1 && kGgPackGlobal;
+    sv.dirsL = off; off = align16(off + (pk ? gg_dirs_bytes_packed(glengthL, W) : gg_dirs_bytes(glengthL, R)));
+    sv.dirsR = off; off = align16(off + (pk ? gg_dirs_bytes_packed(glengthR, W) : gg_dirs_bytes(glengthR, R)));
   }
   sv.total = off;
   return sv;
@@ -720,7 +728,7 @@ __global__ __launch_bounds__(128) GGX_ATTR void gg_kernel(
   const int late = (flags & kFLate) ? 1 : 0;
   const int lband = P.lbandL, ubandL = P.ubandL, ubandR = P.ubandR;
   const int WL = lband + ubandL + 1, WR = lband + ubandR + 1;
-  constexpr bool DPK = R == 1;  // packed direction planes (PackedDirs), in LDS or global scratch
+  constexpr bool DPK = R == 1 && (DIRS_LDS || kGgPackGlobal);  // packed direction planes (PackedDirs)
   const CarveGG cv = carve_gg(rlen, gL, gR, R, DIRS_LDS, WL > WR ? WL : WR);
   const ScratchGG sv = scratch_gg(rlen, gL, gR, R, DIRS_LDS, WL > WR ? WL : WR);
   unsigned char* gbase = gscratch + P.dirs_offset;

@@ -612,6 +612,14 @@ __device__ void oi_report_overflow(const DevOligoProblem& P, int tid, int nthrea
 // on wave 0 between workgroup barriers.  Wave 1 appends its hits from the far end of the hit list (so
 // the two lists meet only when the layout's capacity is exceeded, which is reported as overflow).
 constexpr int kOiWaves = 2;
+// Pass 2's table through LDS images (GMAPDP_OI_STAGE builds, experiments): ~5x fewer bytes written, but the
+// seeding measured 0.3 ms slower per 10 k-read block in the bench step (6.89 vs 6.61 ms alone,
+// profiles/r06_seed), so the product keeps the direct scattered stores.
+#ifdef GMAPDP_OI_STAGE
+constexpr bool kOiStage = true;
+#else
+constexpr bool kOiStage = false;
+#endif
 
 #define OI_PASS_ARGS                                                                                          \
   const DevOligoProblem *__restrict__ probs, const uint32_t *__restrict__ blocks, const char *__restrict__ quc_all, \
@@ -833,10 +841,9 @@ __device__ __forceinline__ void oi_pass(OI_PASS_ARGS) {
   }
 
   // ---- pass 2: store in descending chrpos (plus: right to left; minus: left to right) ----
-  // Compact lists: each hit's table slot goes beside its entry (the hit region's second half, unused by
-  // 4-B entries), then both waves place the hits into LDS images of the table, 3 072 slots at a time, each
-  // written out coalesced -- instead of one scattered 4-B store per hit (~8x the table's bytes
-  // in partial-line writes).
+  // kOiStage (compact lists): each hit's table slot goes beside its entry (the hit region's second half,
+  // unused by 4-B entries), then both waves place the hits into LDS images of the table, 3 072 slots at a
+  // time, each written out coalesced -- instead of one scattered 4-B store per hit.
   uint32_t* table = table_all + P.table_offset;
   uint32_t* slotarr = hitlist32 + P.hit_cap;
   const uint32_t chrpos0 = P.plusp ? P.chrstart : (P.chrhigh - P.chroffset) - P.chrend;
@@ -873,7 +880,7 @@ __device__ __forceinline__ void oi_pass(OI_PASS_ARGS) {
       const int same = __popcll(eq);
       const int r0 = (int)cnt[id];  // every lane reads before the first lane of each oligo writes
       const uint32_t slot = (uint32_t)offs[id] + (uint32_t)(r0 - rank - 1);
-      if (compact)
+      if (kOiStage && compact)
         slotarr[at] = r0 - rank > 0 ? slot : 0xFFFFFFFFu;
       else if (r0 - rank > 0)
         table[slot] = chrpos0 + (P.plusp ? k : (uint32_t)(npos - 1) - k);
@@ -882,7 +889,7 @@ __device__ __forceinline__ void oi_pass(OI_PASS_ARGS) {
   }
   __threadfence_block();
   __syncthreads();
-  if (compact) {  // every slot of [0, tot) is some hit's (a wrapped count keeps its first count & 255 hits)
+  if (kOiStage && compact) {  // every slot of [0, tot) is some hit's (a wrapped count keeps its first count & 255 hits)
     uint32_t* stage = reinterpret_cast<uint32_t*>(smem);  // the bitmap and ranks (12 KB)
     constexpr uint32_t kStage = 6 * kOiWords / 4;
     for (uint32_t b0 = 0; b0 < tot; b0 += kStage) {
