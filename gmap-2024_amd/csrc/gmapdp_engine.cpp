@@ -295,6 +295,7 @@ struct gmapdp_ctx {
   DevBuf probs, order, qseq, qseq_uc, results, pairs, gdirs;
   DevBuf din, dout;    // run_batch: all inputs / all outputs of one synchronous batch
   HostBuf hin, hout;   // their pinned host images
+  HostBuf hplan;       // a plan's descriptor upload (gmapdp_plan_create_all), staged pinned
   DevBuf gprobs, gorder, sprob, gresults;
   DevBuf cprobs, corder, cresults, cscratch;  // Dynprog_cdna_gap batches
   DevBuf sjprobs, sjorder, sjresults, sjseq, sjdirs;  // Dynprog_end5/3_splicejunction batches
@@ -1174,7 +1175,34 @@ struct ClassOf {  // (an aggregate: classify_dev / _gdev value-initialise it; ar
   size_t pair;       // pair-arena records reserved
   size_t gdirs;      // bytes of the global direction scratch, 0: none
   const char* err;
+  uint64_t len;      // the launch-order length (cells of the band) and work estimate (class_work)
+  double one;
+  int gm;
 };
+
+// A problem's launch-order length, work estimate and step count by its class (kind, R), filled in by the
+// classification pass while its descriptor is in cache.
+static void class_work(ClassOf& c, const DevProblem& d) {
+  const int kind = (int)(c.key >> 48), R = (int)((c.key >> 32) & 0xFFFF);
+  c.len = (uint64_t)d.glength * (uint64_t)(d.lband + d.uband + 1);
+  c.gm = 0;
+  if (kind == PlanCore::kUxe) {
+    c.one = (double)(d.rlength + d.glength) + 0.5 * d.rlength;
+  } else if (kind == PlanCore::kSx) {
+    c.gm = steps_sx(d.rlength, d.lband, d.uband, R);
+    c.one = (double)c.gm * R / 64.0 + 0.25 * (d.rlength + d.glength);
+  } else {
+    c.gm = (int)d.glength;
+    c.one = (double)d.glength * (kind == PlanCore::kDpx ? R / 64.0 : R) + 0.25 * (d.rlength + d.glength);
+  }
+}
+static void class_work(ClassOf& c, const DevGenomeProblem& d) {
+  const int kind = (int)(c.key >> 48), R = (int)((c.key >> 32) & 0xFFFF);
+  c.len = (uint64_t)(d.glengthL + d.glengthR) * (uint64_t)(2 * d.lbandL + d.ubandL + d.ubandR + 2);
+  c.one = kind == PlanCore::kGenomeGap ? (double)std::max(d.glengthL, d.glengthR) * R + d.rlength
+                                       : (double)(d.glengthL + d.glengthR + 2 * d.rlength) + 4.0 * d.rlength;
+  c.gm = 0;
+}
 
 // one single / end gap's launch class (classify's rules)
 static ClassOf classify_dev(DevProblem& d, bool latency) {
@@ -1277,13 +1305,23 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
   PlanTimer tm("classify");
   // per problem (threads): its class; slots 0..nd-1 single / end gaps, nd.. genome gaps
   HostArray<ClassOf> cls(nd + ng);
-  plan_parallel(nd + ng, T, [&](size_t lo, size_t hi, int) {
-    for (size_t s = lo; s < hi; s++)
-      cls[s] = s < nd ? classify_dev(plan.dev[s], latency) : classify_gdev(plan.gdev[s - nd], latency, lds_dirs_max);
+  std::vector<size_t> first_err(T, SIZE_MAX);  // per thread chunk: the first problem the engine rejects
+  plan_parallel(nd + ng, T, [&](size_t lo, size_t hi, int t) {
+    for (size_t s = lo; s < hi; s++) {
+      ClassOf& c = cls[s];
+      if (s < nd) {
+        c = classify_dev(plan.dev[s], latency);
+        if (!c.err) class_work(c, plan.dev[s]);
+      } else {
+        c = classify_gdev(plan.gdev[s - nd], latency, lds_dirs_max);
+        if (!c.err) class_work(c, plan.gdev[s - nd]);
+      }
+      if (c.err && first_err[t] == SIZE_MAX) first_err[t] = s;
+    }
   });
   tm.mark("classes");
-  for (size_t s = 0; s < nd + ng; s++)  // the first problem in batch order that the engine rejects
-    if (cls[s].err) return bad(ctx, cls[s].err);
+  for (int t = 0; t < T; t++)  // the first problem in batch order that the engine rejects (chunks in order)
+    if (first_err[t] != SIZE_MAX) return bad(ctx, cls[first_err[t]].err);
   // pair-arena and direction-scratch offsets in problem order (single / end gaps, then genome gaps): each
   // thread's chunk totals, then the chunk written from its prefix
   size_t pair_off = 0, gdirs_off = 0;
@@ -1358,32 +1396,18 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
   plan_parallel(nd + ng, T, [&](size_t lo, size_t hi, int t) {
     std::vector<uint32_t>& h = hist[t];
     std::vector<Acc>& A = acc[t];
+    size_t k = 0;
+    uint64_t kk = ~0ull;
     for (size_t s = lo; s < hi; s++) {
-      const uint64_t key = cls[s].key;
-      const size_t k = class_index(key);
-      const int kind = (int)(key >> 48), R = (int)((key >> 32) & 0xFFFF);
-      uint64_t len;
-      double one;
-      int gm = 0;
-      if (s >= nd) {
-        const DevGenomeProblem& d = plan.gdev[s - nd];
-        len = (uint64_t)(d.glengthL + d.glengthR) * (uint64_t)(2 * d.lbandL + d.ubandL + d.ubandR + 2);
-        one = kind == PlanCore::kGenomeGap ? (double)std::max(d.glengthL, d.glengthR) * R + d.rlength
-                                           : (double)(d.glengthL + d.glengthR + 2 * d.rlength) + 4.0 * d.rlength;
-      } else {
-        const DevProblem& d = plan.dev[s];
-        len = (uint64_t)d.glength * (uint64_t)(d.lband + d.uband + 1);
-        if (kind == PlanCore::kUxe) {
-          one = (double)(d.rlength + d.glength) + 0.5 * d.rlength;
-        } else if (kind == PlanCore::kSx) {
-          gm = steps_sx(d.rlength, d.lband, d.uband, R);
-          one = (double)gm * R / 64.0 + 0.25 * (d.rlength + d.glength);
-        } else {
-          gm = (int)d.glength;
-          one = (double)d.glength * (kind == PlanCore::kDpx ? R / 64.0 : R) + 0.25 * (d.rlength + d.glength);
-        }
+      const ClassOf& c = cls[s];
+      if (c.key != kk) {  // (runs of one class are common: a lookup per run)
+        kk = c.key;
+        k = class_index(kk);
       }
-      const uint32_t bn = (uint32_t)(k * NB + (NB - 1 - plan_bucket(len)));
+      const int kind = (int)(kk >> 48), R = (int)((kk >> 32) & 0xFFFF);
+      const double one = c.one;
+      const int gm = c.gm;
+      const uint32_t bn = (uint32_t)(k * NB + (NB - 1 - plan_bucket(c.len)));
       bin[s] = bn;
       h[bn]++;
       Acc& a = A[k];
@@ -1509,17 +1533,20 @@ static int build_plan(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int
   const int T = plan_threads((size_t)n + (size_t)ngenome);
   std::vector<const char*> why(2 * T, nullptr);
   std::vector<int> errat(2 * T, INT32_MAX), errcode(2 * T, 0);
-  // single and end gaps, then genome gaps: which run on the GPU (threads), the slots by a prefix count, then
-  // the descriptors converted again straight into their slots (threads)
+  // single and end gaps, then genome gaps: each descriptor converted once into a problem-order array
+  // (threads), the GPU problems' slots by a prefix count, then moved into their slots (threads; the array
+  // itself when every problem runs on the GPU)
   auto compact = [&](int m, int err_base, auto&& conv, auto& dev, auto& dev_index, auto& dev_problem) -> int {
+    using D = typename std::decay_t<decltype(dev)>::value_type;
     std::vector<size_t> cnt(T, 0);
     HostArray<unsigned char> gpu(m);
+    HostArray<D> tmp(m);
     plan_parallel((size_t)m, T, [&](size_t lo, size_t hi, int t) {
       size_t c = 0;
       for (size_t i = lo; i < hi; i++) {
         int err = 0;
         const char* w = nullptr;
-        const int g = conv(i, &err, &w, nullptr);
+        const int g = conv(i, &err, &w, &tmp[i]);
         if (err) {
           errat[err_base + t] = (int)i;
           errcode[err_base + t] = err;
@@ -1541,6 +1568,13 @@ static int build_plan(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int
     }
     dev_index.resize(m);
     dev_problem.resize(total);
+    if (total == (size_t)m) {
+      dev.swap(tmp);
+      plan_parallel((size_t)m, T, [&](size_t lo, size_t hi, int) {
+        for (size_t i = lo; i < hi; i++) dev_index[i] = dev_problem[i] = (int)i;
+      });
+      return GMAPDP_OK;
+    }
     dev.resize(total);
     plan_parallel((size_t)m, T, [&](size_t lo, size_t hi, int t) {
       size_t k = at[t];
@@ -1549,9 +1583,7 @@ static int build_plan(gmapdp_ctx* ctx, const gmapdp_single_problem* singles, int
           dev_index[i] = -1;
           continue;
         }
-        int err = 0;
-        const char* w = nullptr;
-        conv(i, &err, &w, &dev[k]);
+        dev[k] = tmp[i];
         dev_index[i] = (int)k;
         dev_problem[k++] = (int)i;
       }
@@ -2381,11 +2413,34 @@ int gmapdp_plan_create_all(gmapdp_ctx* ctx, const gmapdp_single_problem* singles
   if (e == hipSuccess) e = hipMalloc(&p->d_order, sizeof(int) * std::max<size_t>(nd, 1));
   if (e == hipSuccess) e = hipMalloc(&p->d_gprobs, sizeof(DevGenomeProblem) * std::max<size_t>(ng, 1));
   if (e == hipSuccess) e = hipMalloc(&p->d_gorder, sizeof(int) * std::max<size_t>(ng, 1));
-  if (e == hipSuccess && nd) e = hipMemcpy(p->d_probs, p->in.dev.data(), sizeof(DevProblem) * nd, hipMemcpyHostToDevice);
-  if (e == hipSuccess && nd) e = hipMemcpy(p->d_order, p->in.order.data(), sizeof(int) * nd, hipMemcpyHostToDevice);
-  if (e == hipSuccess && ng)
-    e = hipMemcpy(p->d_gprobs, p->in.gdev.data(), sizeof(DevGenomeProblem) * ng, hipMemcpyHostToDevice);
-  if (e == hipSuccess && ng) e = hipMemcpy(p->d_gorder, p->in.gorder.data(), sizeof(int) * ng, hipMemcpyHostToDevice);
+  // the four descriptor arrays (~115 MB for a 10 000-read block) copied into one pinned image on the plan's
+  // threads, then moved with asynchronous copies (a pageable hipMemcpy stages through the runtime's own
+  // buffers on one thread)
+  {
+    struct Part {
+      void* dst;
+      const void* src;
+      size_t n, at;
+    } parts[4] = {{p->d_probs, p->in.dev.data(), sizeof(DevProblem) * nd, 0},
+                  {p->d_order, p->in.order.data(), sizeof(int) * nd, 0},
+                  {p->d_gprobs, p->in.gdev.data(), sizeof(DevGenomeProblem) * ng, 0},
+                  {p->d_gorder, p->in.gorder.data(), sizeof(int) * ng, 0}};
+    size_t tot = 0;
+    for (Part& x : parts) {
+      x.at = tot;
+      tot = align_up(tot + x.n, 256);
+    }
+    if (e == hipSuccess) e = ctx->hplan.ensure(std::max<size_t>(tot, 256));
+    unsigned char* h = (unsigned char*)ctx->hplan.p;
+    for (Part& x : parts) {
+      if (e != hipSuccess || !x.n) continue;
+      plan_parallel(x.n, plan_threads(x.n / 64), [&](size_t lo, size_t hi, int) {
+        std::memcpy(h + x.at + lo, (const unsigned char*)x.src + lo, hi - lo);
+      });
+      e = hipMemcpyAsync(x.dst, h + x.at, x.n, hipMemcpyHostToDevice, ctx->stream);
+    }
+    if (e == hipSuccess) e = ctx_sync(ctx, ctx->stream);
+  }
   if (e == hipSuccess && p->in.gdirs_bytes) e = ctx->gdirs.ensure(p->in.gdirs_bytes);
   tm.mark("upload");
   if (e != hipSuccess) {
@@ -2643,15 +2698,26 @@ static int oligo_distinct(const char* q, int qlen, std::vector<uint32_t>& bm) {
   uint32_t oligo = 0;
   thread_local std::vector<uint32_t> touched;
   touched.clear();
-  for (int i = 0; i < qlen; i++) {
-    in_counter++;
-    switch (q[i]) {
-      case 'A': oligo = oligo << 2; break;
-      case 'C': oligo = (oligo << 2) | 1; break;
-      case 'G': oligo = (oligo << 2) | 2; break;
-      case 'T': oligo = (oligo << 2) | 3; break;
-      default: oligo = 0; in_counter = 0; break;
+  // (a table lookup per character: a four-way switch mispredicted on most characters)
+  static const struct Lut {
+    uint8_t v[256];
+    Lut() {
+      std::memset(v, 4, sizeof(v));
+      v['A'] = 0;
+      v['C'] = 1;
+      v['G'] = 2;
+      v['T'] = 3;
     }
+  } lut;
+  for (int i = 0; i < qlen; i++) {
+    const uint32_t c = lut.v[(unsigned char)q[i]];
+    if (c > 3) {
+      oligo = 0;
+      in_counter = 0;
+      continue;
+    }
+    in_counter++;
+    oligo = (oligo << 2) | c;
     if (in_counter == 8) {
       const uint32_t m = oligo & 0xFFFFu;
       if (!((bm[m >> 5] >> (m & 31)) & 1u)) {
