@@ -14,6 +14,8 @@
 #                  drop-in at -t 512 or the given list; configs as e2e_timing.py --configs)
 #   isot:<lib>     bench.py --iso-kernel $ISO_KERNEL (default gg_kernel<1, false>) with <lib>: HIP-event time per launch
 #   s2timing       tools/oi_timing.py s2 (the GMAPDP_OI_TIMING build: stage-2 sweep phases and counts)
+#   e2eidx:<b>:<n>[:<gpu threads>]  gmap -d over tools/e2e_index.py's index (e2e_pack/, unpacked on the box;
+#                  take ./e2e_pack off .gpurunignore for that call): unmodified vs drop-in
 set -o pipefail
 TAG=$1
 shift
@@ -38,10 +40,13 @@ for S in "$@"; do
     e2e:*) IFS=: read -r _ B N T C <<< "$S"; timeout -k 10 900 python tools/e2e_timing.py --build $B --reads $N --threads 16 --gpu-threads ${T:-512} ${C:+--configs "$C"} > $O/e2e_${B}_$N.json 2> $O/e2e_${B}_$N.err || exit 20 ;;
     isot:*) L=${S#isot:}; GMAPDP_LIB=$PWD/gmap-2024_amd/$L/libgmapdp.so timeout -k 10 300 python bench.py --iso-kernel "${ISO_KERNEL:-gmapdp::gg_kernel<1, false>}" --iso-reps ${ISO_REPS:-3} > $O/isot_$L.json 2> $O/isot_$L.err || exit 22 ;;
     oitiming) timeout -k 10 300 python tools/oi_timing.py 5000 > $O/oitiming.json 2> $O/oitiming.err || exit 24 ;;
+    ggtiming) timeout -k 10 300 python tools/oi_timing.py gg 10000 > $O/ggtiming.json 2> $O/ggtiming.err || exit 33 ;;
     e2eprof:*) IFS=: read -r _ B N T <<< "$S"; timeout -k 10 900 python tools/e2e_timing.py --build $B --reads $N --threads 16 --gpu-threads ${T:-2048} --prof $O/prof_$N > $O/e2eprof_${B}_$N.json 2> $O/e2eprof_${B}_$N.err || exit 26 ;;
     e2ecpu:*) IFS=: read -r _ B N T <<< "$S"; timeout -k 10 900 python tools/e2e_timing.py --build $B --reads $N --threads 16 --gpu-threads ${T:-2048} --thread-cpu > $O/e2ecpu_${B}_$N.json 2> $O/e2ecpu_${B}_$N.err || exit 25 ;;
     s2timing) timeout -k 10 300 python tools/oi_timing.py s2 5000 > $O/s2timing.json 2> $O/s2timing.err || exit 21 ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || exit 19 ;;
+    e2eidx:*) IFS=: read -r _ B N T <<< "$S"; mkdir -p e2e_idx && { [ -f e2e_idx/meta.json ] || { tar xzf e2e_pack/db.tgz -C e2e_idx && gunzip -c e2e_pack/r.fa.gz > e2e_idx/r.fa && cp e2e_pack/meta.json e2e_idx/; }; } || exit 31
+      timeout -k 10 900 python -u tools/e2e_timing.py --index e2e_idx --build $B --reads $N --threads 16 --gpu-threads ${T:-2048} > $O/e2eidx_${B}_$N.json 2> $O/e2eidx_${B}_$N.err || exit 32 ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
 done
