@@ -19,6 +19,10 @@ __device__ __forceinline__ int dpp_wave_shl1(int x, int fill) {
   // lane i <- lane i+1; lane 63 <- fill
   return __builtin_amdgcn_update_dpp(fill, x, 0x130, 0xf, 0xf, false);
 }
+// lane i <- lane i+1; lane 63 <- 0 (bound_ctrl: one DPP move, no default copied in first)
+__device__ __forceinline__ int dpp_wave_shl1_zero(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, 0x130, 0xf, 0xf, true);
+}
 __device__ __forceinline__ int dpp_wave_shr1(int x, int fill) {
   // lane i <- lane i-1; lane 0 <- fill
   return __builtin_amdgcn_update_dpp(fill, x, 0x138, 0xf, 0xf, false);
@@ -390,12 +394,13 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
   int kext[R];  // k*ext per element: r*ext = rtop*ext + k*ext without a per-column multiply
 #pragma unroll
   for (int i = 0; i < R; i++) kext[i] = (lk * R + i) * ext;
-  int cs[R], cc[R];  // carried bridge candidate per band row: score, column (-1: none), probability
+  // carried bridge candidate per band row: score, column + 1 (0: none), probability -- zero-filled shifts
+  int cs[R], cc[R];
   double cp[R];
 #pragma unroll
   for (int i = 0; i < R; i++) {
     cs[i] = 0;
-    cc[i] = -1;
+    cc[i] = 0;
     cp[i] = 0.0;
   }
   int rtop_ext = -uband * ext;  // (c - uband) * ext, advanced by ext per column
@@ -501,13 +506,13 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
       double icp[R];
 #pragma unroll
       for (int i = 0; i < R - 1; i++) { ics[i] = cs[i + 1]; icc[i] = cc[i + 1]; icp[i] = cp[i + 1]; }
-      ics[R - 1] = dpp_wave_shl1(cs[0], 0);
-      icc[R - 1] = dpp_wave_shl1(cc[0], -1);
+      ics[R - 1] = dpp_wave_shl1_zero(cs[0]);
+      icc[R - 1] = dpp_wave_shl1_zero(cc[0]);
       {
         const int2 v = *reinterpret_cast<const int2*>(&cp[0]);
         int2 w;
-        w.x = dpp_wave_shl1(v.x, 0);
-        w.y = dpp_wave_shl1(v.y, 0);
+        w.x = dpp_wave_shl1_zero(v.x);
+        w.y = dpp_wave_shl1_zero(v.y);
         icp[R - 1] = *reinterpret_cast<const double*>(&w);
       }
 #pragma unroll
@@ -524,14 +529,14 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
           s = B.isc[B.rowdi[other] & cdi] + Hc;
           p = B.rowp[other] + cpc;
         }
-        const bool take = cand & ((icc[i] < 0) | (s > ics[i]) | ((s == ics[i]) & (p > icp[i])));
+        const bool take = cand & ((icc[i] == 0) | (s > ics[i]) | ((s == ics[i]) & (p > icp[i])));
         cs[i] = take ? s : ics[i];
-        cc[i] = take ? c : icc[i];
+        cc[i] = take ? c + 1 : icc[i];
         cp[i] = take ? p : icp[i];
         if (inrow && k == uband) B.diag[r] = Hc;  // matrix[r][r]
         if (inrow && k == 0) {                    // the row leaves the band: its candidate is final
           B.part[r].s = cs[i];
-          B.part[r].c = cc[i];
+          B.part[r].c = cc[i] - 1;
           B.part[r].p = cp[i];
         }
       }
@@ -575,7 +580,7 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
       const int r = glen - uband + k;
       if (k < W && r >= 1 && r <= rlen - 1) {
         B.part[r].s = cs[i];
-        B.part[r].c = cc[i];
+        B.part[r].c = cc[i] - 1;
         B.part[r].p = cp[i];
       }
     }

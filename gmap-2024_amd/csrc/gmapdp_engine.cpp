@@ -21,6 +21,7 @@
 #include <map>
 #include <mutex>
 #include <thread>
+#include <sys/mman.h>
 #include <string>
 #include <tuple>
 #include <utility>
@@ -339,6 +340,23 @@ struct NoInitAlloc : std::allocator<T> {
   NoInitAlloc() = default;
   template <typename U>
   NoInitAlloc(const NoInitAlloc<U>&) {}
+  // Large arrays (a 10 000-read block's descriptors: tens of MB each) come from their own mapping with
+  // transparent huge pages requested, so that their first touch costs a fault per 2 MB rather than per
+  // 4 KB page (the plan builders' passes were fault-bound on the GPU box).
+  static constexpr size_t kHuge = size_t(4) << 20;
+  T* allocate(size_t n) {
+    const size_t b = n * sizeof(T);
+    if (b < kHuge) return std::allocator<T>::allocate(n);
+    void* p = mmap(nullptr, b, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p == MAP_FAILED) throw std::bad_alloc();
+    (void)madvise(p, b, MADV_HUGEPAGE);
+    return static_cast<T*>(p);
+  }
+  void deallocate(T* p, size_t n) {
+    const size_t b = n * sizeof(T);
+    if (b < kHuge) std::allocator<T>::deallocate(p, n);
+    else munmap(p, b);
+  }
   template <typename U>
   void construct(U* p) noexcept {
     ::new ((void*)p) U;
