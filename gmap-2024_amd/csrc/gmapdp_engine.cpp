@@ -2373,13 +2373,11 @@ struct gmapdp_plan {
   const double* d_sprob = nullptr;            // bound by gmapdp_plan_bind_genome
   gmapdp_genome_result* d_gresults = nullptr;
   const double* d_metab = nullptr;            // gmapdp_plan_bind_genome_maxent: each genome-gap class fills d_sprob
+  void* d_base = nullptr;                     // one allocation holding d_probs, d_order, d_gprobs, d_gorder
 };
 
 static void plan_free(gmapdp_plan* p) {
-  if (p->d_probs) (void)hipFree(p->d_probs);
-  if (p->d_order) (void)hipFree(p->d_order);
-  if (p->d_gprobs) (void)hipFree(p->d_gprobs);
-  if (p->d_gorder) (void)hipFree(p->d_gorder);
+  if (p->d_base) (void)hipFree(p->d_base);
   delete p;
 }
 
@@ -2427,10 +2425,19 @@ int gmapdp_plan_create_all(gmapdp_ctx* ctx, const gmapdp_single_problem* singles
       return bad(ctx, "GMAPDP_KNOWN_SITES genome gaps go through the synchronous batches, not plans");
     }
   const size_t nd = p->in.dev.size(), ng = p->in.gdev.size();
-  hipError_t e = hipMalloc(&p->d_probs, sizeof(DevProblem) * std::max<size_t>(nd, 1));
-  if (e == hipSuccess) e = hipMalloc(&p->d_order, sizeof(int) * std::max<size_t>(nd, 1));
-  if (e == hipSuccess) e = hipMalloc(&p->d_gprobs, sizeof(DevGenomeProblem) * std::max<size_t>(ng, 1));
-  if (e == hipSuccess) e = hipMalloc(&p->d_gorder, sizeof(int) * std::max<size_t>(ng, 1));
+  // the four descriptor arrays in one device allocation (one hipMalloc per plan, not four)
+  size_t o1 = align_up(sizeof(DevProblem) * std::max<size_t>(nd, 1), 256);
+  size_t o2 = o1 + align_up(sizeof(int) * std::max<size_t>(nd, 1), 256);
+  size_t o3 = o2 + align_up(sizeof(DevGenomeProblem) * std::max<size_t>(ng, 1), 256);
+  const size_t dtot = o3 + align_up(sizeof(int) * std::max<size_t>(ng, 1), 256);
+  hipError_t e = hipMalloc(&p->d_base, dtot);
+  if (e == hipSuccess) {
+    unsigned char* b = (unsigned char*)p->d_base;
+    p->d_probs = (DevProblem*)b;
+    p->d_order = (int*)(b + o1);
+    p->d_gprobs = (DevGenomeProblem*)(b + o2);
+    p->d_gorder = (int*)(b + o3);
+  }
   // the four descriptor arrays (~115 MB for a 10 000-read block) copied into one pinned image on the plan's
   // threads, then moved with asynchronous copies (a pageable hipMemcpy stages through the runtime's own
   // buffers on one thread)
@@ -2802,11 +2809,11 @@ struct gmapdp_oligo_plan {
 
 static constexpr int kOligoChunkProblems = 16384;
 // scratch per launch chunk: 3 GB for the synchronous batches (a context keeps its grow-only scratch); a
-// stage-2 plan's sizing run (window-sized hit lists and walk states, ~7 MB per 214-kb call, freed right
-// after) takes 8 GB chunks: a 10 000-read block in a few launches instead of ~40 small ones (24 GB chunks
-// measured 10.7 ms against 26.5, but the process's first allocation of them took 4 s)
+// stage-2 plan's sizing run (window-sized hit lists and walk states, ~7 MB per 214-kb call) takes 32 GB
+// chunks of the context's grow-only scratch: a 10 000-read block in 4 launches instead of 14 (a chunk of a
+// thousand calls leaves most of the GPU idle); the process pays the first allocation once
 static constexpr size_t kOligoChunkBytes = size_t(3) << 30;
-static constexpr size_t kOligoSizingChunkBytes = size_t(8) << 30;
+static constexpr size_t kOligoSizingChunkBytes = size_t(32) << 30;
 
 static void oligo_plan_free(gmapdp_oligo_plan* p) {
   if (!p) return;
