@@ -21,6 +21,7 @@
 #include <map>
 #include <mutex>
 #include <thread>
+#include <atomic>
 #include <sys/mman.h>
 #include <string>
 #include <tuple>
@@ -3464,6 +3465,30 @@ extern "C" int gmapdp_microexon_finish(gmapdp_ctx* ctx, const gmapdp_microexon_p
 // One copy up, the kernels, one copy down of the outputs, one wait.  A search that overflows the pool (a
 // result with cand_offset -2) or holds more candidates than its LDS (-1) is rerun by
 // gmapdp_microexon_search (a whole call then also by gmapdp_microexon_finish).
+// GMAPDP_BATCH_TIMING=1: the mixed batches' host phases summed over the process (every dispatcher thread),
+// printed at exit -- where a drop-in batch's wall time goes (tools, not the product)
+struct BatchTiming {
+  std::atomic<unsigned long long> n{0}, calls{0}, ns[5] = {};
+  bool on = getenv("GMAPDP_BATCH_TIMING") != nullptr;
+  BatchTiming() {
+    if (on) atexit([] { print(); });
+  }
+  static void print();
+  static unsigned long long now() {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (unsigned long long)t.tv_sec * 1000000000ull + (unsigned long long)t.tv_nsec;
+  }
+};
+static BatchTiming g_bt;
+void BatchTiming::print() {
+  static const char* names[5] = {"plan", "stage", "gpu (upload + kernels + download + wait)", "unpack", "reruns"};
+  const double n = (double)std::max<unsigned long long>(g_bt.n.load(), 1);
+  std::fprintf(stderr, "[gmapdp batch timing] batches=%llu calls=%llu", g_bt.n.load(), g_bt.calls.load());
+  for (int k = 0; k < 5; k++) std::fprintf(stderr, " %s=%.1fus", names[k], g_bt.ns[k].load() / n / 1e3);
+  std::fprintf(stderr, " (mean per batch)\n");
+}
+
 extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char* qseq_uc, size_t qbytes,
                                   gmapdp_mixed* m) {
   if (!ctx || !m) return GMAPDP_EINVAL;
@@ -3479,6 +3504,10 @@ extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char*
   if (nsingle + nend + ngenome + nxs + nxf + nxw == 0) return GMAPDP_OK;
   if (!qseq || !qseq_uc) return GMAPDP_EINVAL;
   (void)hipSetDevice(ctx->device);
+  unsigned long long bt[6] = {g_bt.on ? BatchTiming::now() : 0, 0, 0, 0, 0, 0};
+  auto mark = [&](int k) {
+    if (g_bt.on) bt[k] = BatchTiming::now();
+  };
   // ---- DP plan (as run_batch) ----
   PlanCore plan;
   size_t nsp = 0;
@@ -3542,6 +3571,7 @@ extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char*
   const double* metab = nullptr;
   if ((dev_me || fdev_me || nxw) && !(metab = me_tables(ctx))) return GMAPDP_EINVAL;
   const size_t nfc = nxf ? m->nfinish_candidates : 0;
+  mark(1);
   const size_t pool = nxs ? std::max<size_t>(4096, 16 * (size_t)nxs) : 0;   // search candidates
   const size_t wpool = nxw ? std::max<size_t>(4096, 16 * (size_t)nxw) : 0;  // whole calls' candidates
   // ---- one image: inputs, then outputs, then device-only scratch ----
@@ -3609,6 +3639,7 @@ extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char*
     std::memcpy(h + o_xwpoff, wpoff.data(), sizeof(int64_t) * nxw);
   }
   hipStream_t s = ctx->stream;
+  mark(2);
   e = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "upload: %s", e);
   if (ndev + ngdev) {
@@ -3652,6 +3683,7 @@ extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char*
   if (e == hipSuccess) e = hipMemcpyAsync(h + o_xfres, d + o_xfres, out_end - o_xfres, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = ctx_sync(ctx, s);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "mixed batch: %s", e);
+  mark(3);
   // ---- unpack ----
   const gmapdp_result* dres = (const gmapdp_result*)(h + r_res);
   const gmapdp_genome_result* gres = (const gmapdp_genome_result*)(h + r_gres);
@@ -3667,6 +3699,18 @@ extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char*
     std::memcpy(m->whole_pairs, h + r_xwpairs, sizeof(gmapdp_pair) * wpairs);
   }
   // (the buffers of the reruns below are the context's own; the image above is consumed)
+  mark(4);
+  struct BtDone {  // the reruns' time, and the sums (on every return below)
+    unsigned long long* bt;
+    int ncalls;
+    ~BtDone() {
+      if (!g_bt.on) return;
+      bt[5] = BatchTiming::now();
+      g_bt.n++;
+      g_bt.calls += (unsigned long long)ncalls;
+      for (int k = 0; k < 5; k++) g_bt.ns[k] += bt[k + 1] - bt[k];
+    }
+  } bt_done{bt, nsingle + nend + ngenome + nxs + nxf + nxw};
   int rc = GMAPDP_OK;
   if (nxs) {
     const gmapdp_microexon_result* xr = (const gmapdp_microexon_result*)(h + r_xsres);

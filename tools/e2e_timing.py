@@ -132,9 +132,12 @@ def main():
                 raise SystemExit("%s failed: %s" % (prog, r.stderr[-2000:]))
             sams[(prog, t, cname)] = r.stdout
             stats = [l for l in r.stderr.splitlines() if l.startswith("gmapdp shim calls")]
+            # GMAPDP_BATCH_TIMING=1 in a configuration: the engine's per-phase means of the mixed batches
+            bt = [l for l in r.stderr.splitlines() if l.startswith("[gmapdp batch timing]")]
             out["runs"].append({"program": prog, "threads": t, "config": cname, "env": cenv, "seconds": dt, "reads_per_s": a.reads / dt,
                                 "cpu_seconds": cpu, "cpu_cores_busy": cpu / dt,
-                                "shim_calls": stats[0] if stats else None, "thread_cpu_s": threads})
+                                "shim_calls": stats[0] if stats else None, "thread_cpu_s": threads,
+                                "batch_timing": bt[0] if bt else None})
             print(json.dumps(out["runs"][-1]), file=sys.stderr, flush=True)
     base = next(iter(sams.values())) if a.skip_cpu else next(v for k, v in sams.items() if k[0] == "gmap_%s%s" % (pv, a.build))
     out["outputs_identical"] = all(v == base for v in sams.values())
