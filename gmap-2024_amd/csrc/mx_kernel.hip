@@ -50,6 +50,25 @@ __device__ __forceinline__ bool mx_window(const uint32_t* __restrict__ blocks, u
   return true;
 }
 
+// mx_window without its early return: the flag and code words are loaded together (addresses clamped in
+// range), so the text scan below can have several steps' loads in flight instead of two dependent round
+// trips per step
+__device__ __forceinline__ bool mx_window_nb(const uint32_t* __restrict__ blocks, uint64_t nwords, uint64_t lo,
+                                             int ml, uint32_t& codes) {
+  const uint64_t hi = lo + (uint64_t)ml - 1u;
+  const uint64_t b0 = lo >> 5, b1 = hi >> 5;
+  const bool ok = 3 * b1 + 2 < nwords;
+  // (b1 == b0: the window's flag bits all lie in the first word; the second word's bits land above them)
+  const uint64_t f = (uint64_t)blocks[ok ? 3 * b0 + 2 : 2] | ((uint64_t)blocks[ok ? 3 * b1 + 2 : 2] << 32);
+  const uint64_t h = lo >> 4, h1 = h + 1u;  // half-words: even = low word (nt 0-15 of the block), odd = high
+  uint64_t i0 = 3 * (h >> 1) + ((h & 1u) ? 0 : 1), i1 = 3 * (h1 >> 1) + ((h1 & 1u) ? 0 : 1);
+  if (!ok) i0 = 0;
+  if (!ok || i1 >= nwords) i1 = 0;  // (only when the window does not reach half-word h1)
+  const uint64_t x = (uint64_t)blocks[i0] | ((uint64_t)blocks[i1] << 32);
+  codes = (uint32_t)(x >> (2u * (lo & 15u))) & ((1u << (2 * ml)) - 1u);
+  return ok && !((f >> (lo & 31u)) & ((1ull << ml) - 1ull));
+}
+
 // the second mismatch among n flags produced 64 at a time by `flag(i)`; n - 1 when there is none
 template <class F>
 __device__ __forceinline__ int mx_second_mismatch(int n, int lane, F flag) {
@@ -134,15 +153,26 @@ __global__ __launch_bounds__(64) void mx_search_kernel(const gmapdp_microexon_pr
           // genome[chroffset + textleft + i] (plus; '*' from chrhigh on) or the complement of
           // genome[chrhigh - textleft - i] (minus; '*' below chroffset)
           const int64_t base = watson ? (int64_t)P.chroffset + textleft : (int64_t)P.chrhigh - textleft;
-          for (int top = textlen - ml; top >= 0; top -= 64) {
-            const int j = top - lane;
-            bool hit = false;
-            if (j >= 0) {
+          // kMxU steps of 64 offsets at a time: their window loads all in flight, then the steps' ballots in
+          // order (descending j), so the candidates keep the reference's order
+          constexpr int kMxU = 4;
+          for (int top0 = textlen - ml; top0 >= 0; top0 -= 64 * kMxU) {
+            bool hu[kMxU];
+#pragma unroll
+            for (int u = 0; u < kMxU; u++) {
+              const int j = top0 - 64 * u - lane;
               const int64_t lo = watson ? base + j : base - j - (ml - 1);  // the window, ascending
-              const bool inb = watson ? lo + ml <= (int64_t)P.chrhigh : lo >= (int64_t)P.chroffset;
+              const bool inb = j >= 0 && (watson ? lo + ml <= (int64_t)P.chrhigh : lo >= (int64_t)P.chroffset);
               uint32_t codes;
-              hit = inb && mx_window(blocks, nwords, (uint64_t)lo, ml, codes) && codes == (watson ? pat : rcpat);
+              const bool w = mx_window_nb(blocks, nwords, inb ? (uint64_t)lo : 0u, ml, codes);
+              hu[u] = inb && w && codes == (watson ? pat : rcpat);
             }
+#pragma unroll
+            for (int u = 0; u < kMxU; u++) {
+            const int top = top0 - 64 * u;
+            if (top < 0) break;
+            const int j = top - lane;
+            bool hit = hu[u];
             const int cand = textleft + j;
             hit = hit && gnt(cand - 2) == i3 && gnt(cand - 1) == i4 && gnt(cand + ml) == i1 && gnt(cand + ml + 1) == i2;
             const uint64_t mh = ballot(hit);
@@ -168,6 +198,7 @@ __global__ __launch_bounds__(64) void mx_search_kernel(const gmapdp_microexon_pr
               else if (idx < kMxCap) lc[idx] = c;
             }
             ncand += __popcll(mh);
+            }
           }
         }
       }
