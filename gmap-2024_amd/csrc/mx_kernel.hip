@@ -153,31 +153,65 @@ __global__ __launch_bounds__(64) void mx_search_kernel(const gmapdp_microexon_pr
           // genome[chroffset + textleft + i] (plus; '*' from chrhigh on) or the complement of
           // genome[chrhigh - textleft - i] (minus; '*' below chroffset)
           const int64_t base = watson ? (int64_t)P.chroffset + textleft : (int64_t)P.chrhigh - textleft;
-          // kMxU steps of 64 offsets at a time: their window loads all in flight, then the steps' ballots in
-          // order (descending j), so the candidates keep the reference's order
-          constexpr int kMxU = 4;
-          for (int top0 = textlen - ml; top0 >= 0; top0 -= 64 * kMxU) {
-            bool hu[kMxU];
+          // 2 048 offsets per step: lane l takes the 32 offsets j = J0 - k (J0 = top - 32 l, k = 0..31), whose
+          // windows lie in 32 + ml - 1 genome positions from G0 -- decoded once from four half-words and three
+          // flag words -- and tests them from registers.  Descending j is lane order, then k: the candidates
+          // keep the reference's hit order (Intlist_push over descending j).  A lane whose positions run
+          // outside the genome's words (or below 0) tests its offsets one by one as mx_window does.
+          const uint32_t want = watson ? pat : rcpat;
+          const uint32_t cmask = (1u << (2 * ml)) - 1u, fmask = (1u << ml) - 1u;
+          for (int top = textlen - ml; top >= 0; top -= 64 * 32) {
+            const int J0 = top - 32 * lane;
+            uint32_t m = 0;  // bit k: offset J0 - k matches (window, N flags, chromosome bound)
+            if (J0 >= 0) {
+              const int kmax = min(31, J0);
+              const int64_t G0 = watson ? base + J0 - 31 : base - J0 - (ml - 1);
+              const uint64_t h0 = (uint64_t)G0 >> 4, b0 = (uint64_t)G0 >> 5;
+              const uint64_t hlast = h0 + 3, wlast = 3 * (hlast >> 1) + ((hlast & 1u) ? 0 : 1);
+              const bool fast = G0 >= 0 && wlast < nwords && 3 * (b0 + 2) + 2 < nwords;
+              if (fast) {
+                auto hw = [&](uint64_t h) { return (uint64_t)blocks[3 * (h >> 1) + ((h & 1u) ? 0 : 1)]; };
+                const uint64_t A = hw(h0) | (hw(h0 + 1) << 32), B = hw(h0 + 2) | (hw(h0 + 3) << 32);
+                const uint32_t sh = 2u * ((uint32_t)G0 & 15u);
+                const uint64_t lo = sh ? (A >> sh) | (B << (64 - sh)) : A, hi = B >> sh;
+                const uint64_t FA = (uint64_t)blocks[3 * b0 + 2] | ((uint64_t)blocks[3 * (b0 + 1) + 2] << 32);
+                const uint64_t FB = blocks[3 * (b0 + 2) + 2];
+                const uint32_t fs = (uint32_t)G0 & 31u;
+                const uint64_t fl = fs ? (FA >> fs) | (FB << (64 - fs)) : FA;
 #pragma unroll
-            for (int u = 0; u < kMxU; u++) {
-              const int j = top0 - 64 * u - lane;
-              const int64_t lo = watson ? base + j : base - j - (ml - 1);  // the window, ascending
-              const bool inb = j >= 0 && (watson ? lo + ml <= (int64_t)P.chrhigh : lo >= (int64_t)P.chroffset);
-              uint32_t codes;
-              const bool w = mx_window_nb(blocks, nwords, inb ? (uint64_t)lo : 0u, ml, codes);
-              hu[u] = inb && w && codes == (watson ? pat : rcpat);
+                for (int k = 0; k < 32; k++) {
+                  const int sidx = watson ? 31 - k : k;  // the window's first position, from G0
+                  const int64_t st = G0 + sidx;
+                  const bool inb = watson ? st + ml <= (int64_t)P.chrhigh : st >= (int64_t)P.chroffset;
+                  const uint64_t w = sidx ? (lo >> (2 * sidx)) | (hi << (64 - 2 * sidx)) : lo;
+                  const bool h = k <= kmax && inb && !((uint32_t)(fl >> sidx) & fmask) &&
+                                 ((uint32_t)w & cmask) == want;
+                  m |= (h ? 1u : 0u) << k;
+                }
+              } else {
+                for (int k = 0; k <= kmax; k++) {
+                  const int j = J0 - k;
+                  const int64_t st = watson ? base + j : base - j - (ml - 1);
+                  const bool inb = st >= 0 && (watson ? st + ml <= (int64_t)P.chrhigh : st >= (int64_t)P.chroffset);
+                  uint32_t codes;
+                  const bool w = mx_window_nb(blocks, nwords, inb ? (uint64_t)st : 0u, ml, codes);
+                  if (inb && w && codes == want) m |= 1u << k;
+                }
+              }
+              // the flanking dinucleotides of each match (rare: a few per call)
+              for (uint32_t r = m; r; r &= r - 1) {
+                const int k = __ffs(r) - 1;
+                const int cand = textleft + J0 - k;
+                if (!(gnt(cand - 2) == i3 && gnt(cand - 1) == i4 && gnt(cand + ml) == i1 && gnt(cand + ml + 1) == i2))
+                  m &= ~(1u << k);
+              }
             }
-#pragma unroll
-            for (int u = 0; u < kMxU; u++) {
-            const int top = top0 - 64 * u;
-            if (top < 0) break;
-            const int j = top - lane;
-            bool hit = hu[u];
-            const int cand = textleft + j;
-            hit = hit && gnt(cand - 2) == i3 && gnt(cand - 1) == i4 && gnt(cand + ml) == i1 && gnt(cand + ml + 1) == i2;
-            const uint64_t mh = ballot(hit);
-            if (hit) {
-              const int idx = ncand + lanes_below(mh, lane);
+            const int cnt = __popc(m);
+            const int incl = wave_scan_add(lane, cnt);
+            int idx = ncand + incl - cnt;
+            for (uint32_t r = m; r; r &= r - 1) {
+              const int k = __ffs(r) - 1;
+              const int cand = textleft + J0 - k;
               gmapdp_microexon_candidate c;
               c.cL = cL;
               c.cR = cR;
@@ -196,9 +230,9 @@ __global__ __launch_bounds__(64) void mx_search_kernel(const gmapdp_microexon_pr
               }
               if (dst >= 0) cands[dst + idx] = c;
               else if (idx < kMxCap) lc[idx] = c;
+              idx++;
             }
-            ncand += __popcll(mh);
-            }
+            ncand += __builtin_amdgcn_readlane(incl, 63);
           }
         }
       }
