@@ -1717,7 +1717,9 @@ static int run_plan(gmapdp_ctx* ctx, const PlanCore& plan, const RunArgs& a, hip
   // its assigned stream; join: `stream` waits for the side streams.  A small batch (the drop-in's
   // dispatcher batches) runs on `stream` alone: a process has few hardware queues (GPU_MAX_HW_QUEUES)
   // and several dispatcher contexts share them.
-  const bool one_stream = ctx->one_stream || plan.dev.size() + plan.gdev.size() < 2048;
+  // (GMAPDP_SMALL_BATCH_STREAMS=1, experiments: small batches spread over the side streams too)
+  static const bool small_streams = getenv("GMAPDP_SMALL_BATCH_STREAMS") != nullptr;
+  const bool one_stream = ctx->one_stream || (!small_streams && plan.dev.size() + plan.gdev.size() < 2048);
   hipError_t e = one_stream ? hipSuccess : hipEventRecord(ctx->ev_fork, stream);
   bool used[gmapdp_ctx::kAux] = {false, false, false};
   for (size_t li = 0; li < plan.launches.size() && e == hipSuccess; li++) {
@@ -3642,6 +3644,17 @@ extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char*
   mark(2);
   e = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "upload: %s", e);
+  // (GMAPDP_SMALL_BATCH_STREAMS with a multi-stream context, experiments: the microexon kernels on the last
+  // side stream, beside the DP classes)
+  static const bool small_streams = getenv("GMAPDP_SMALL_BATCH_STREAMS") != nullptr;
+  const bool mxside = small_streams && !ctx->one_stream && (nxs || nxf || nxw);
+  hipStream_t ms = s;
+  if (mxside) {
+    ms = ctx->aux[gmapdp_ctx::kAux - 1];
+    e = hipEventRecord(ctx->ev_fork, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ms, ctx->ev_fork, 0);
+    if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "mixed batch fork: %s", e);
+  }
   if (ndev + ngdev) {
     RunArgs a;
     a.d_probs = (const DevProblem*)(d + o_probs);
@@ -3661,25 +3674,29 @@ extern "C" int gmapdp_mixed_batch(gmapdp_ctx* ctx, const char* qseq, const char*
   }
   unsigned long long* cnt = (unsigned long long*)(d + o_xcnt);
   if (nxs)
-    e = launch_mx_search(nxs, s, (const gmapdp_microexon_problem*)(d + o_xs), ctx->d_genome, ctx->genome_words,
+    e = launch_mx_search(nxs, ms, (const gmapdp_microexon_problem*)(d + o_xs), ctx->d_genome, ctx->genome_words,
                          (const char*)(d + o_q), (const char*)(d + o_quc), (gmapdp_microexon_result*)(d + r_xsres),
                          (gmapdp_microexon_candidate*)(d + r_xcand), pool, cnt, nullptr);
   if (e == hipSuccess && nxf)
-    e = launch_mx_finish(nxf, s, (const gmapdp_microexon_problem*)(d + o_xf), ctx->d_genome, ctx->genome_words,
+    e = launch_mx_finish(nxf, ms, (const gmapdp_microexon_problem*)(d + o_xf), ctx->d_genome, ctx->genome_words,
                          (const char*)(d + o_q), (const char*)(d + o_quc), ctx->d_cs,
                          (const gmapdp_microexon_candidate*)(d + o_xfc), fdev_me ? nullptr : (const double*)(d + o_xfp),
                          fdev_me ? metab : nullptr, (gmapdp_microexon_result*)(d + o_xfres),
                          (gmapdp_pair*)(d + r_xfpairs), nullptr);
   if (e == hipSuccess && nxw)
-    e = launch_mx_search(nxw, s, (const gmapdp_microexon_problem*)(d + o_xw), ctx->d_genome, ctx->genome_words,
+    e = launch_mx_search(nxw, ms, (const gmapdp_microexon_problem*)(d + o_xw), ctx->d_genome, ctx->genome_words,
                          (const char*)(d + o_q), (const char*)(d + o_quc), (gmapdp_microexon_result*)(d + r_xwres),
                          (gmapdp_microexon_candidate*)(d + s_xwcand), wpool, cnt + 1, nullptr);
   if (e == hipSuccess && nxw)
-    e = launch_mx_finish(nxw, s, (const gmapdp_microexon_problem*)(d + o_xw), ctx->d_genome, ctx->genome_words,
+    e = launch_mx_finish(nxw, ms, (const gmapdp_microexon_problem*)(d + o_xw), ctx->d_genome, ctx->genome_words,
                          (const char*)(d + o_q), (const char*)(d + o_quc), ctx->d_cs,
                          (const gmapdp_microexon_candidate*)(d + s_xwcand), nullptr, metab,
                          (gmapdp_microexon_result*)(d + r_xwres), (gmapdp_pair*)(d + r_xwpairs),
                          (const int64_t*)(d + o_xwpoff));
+  if (e == hipSuccess && mxside) {
+    e = hipEventRecord(ctx->ev_join[gmapdp_ctx::kAux - 1], ms);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, ctx->ev_join[gmapdp_ctx::kAux - 1], 0);
+  }
   if (e == hipSuccess) e = hipMemcpyAsync(h + o_xfres, d + o_xfres, out_end - o_xfres, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = ctx_sync(ctx, s);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "mixed batch: %s", e);

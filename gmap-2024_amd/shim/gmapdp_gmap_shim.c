@@ -509,8 +509,12 @@ shim_context (Genome_T genome) {
     const char *blk = getenv("GMAPDP_SHIM_BLOCKING"), *poll = getenv("GMAPDP_SHIM_POLL");
     const int wait = blk != NULL && blk[0] == '1' ? GMAPDP_CTX_BLOCKING_SYNC
                      : (poll != NULL && poll[0] == '0' ? 0 : GMAPDP_CTX_POLL_SYNC);
+    /* GMAPDP_SHIM_MULTI_STREAM=1 (experiments): the short-call dispatchers' contexts keep their side streams,
+       so a batch's launch classes can run side by side (with GMAPDP_SMALL_BATCH_STREAMS=1 in the engine) */
+    const char *ms = getenv("GMAPDP_SHIM_MULTI_STREAM");
+    const int one = (ms != NULL && ms[0] == '1' && shim_qi == 0) ? 0 : GMAPDP_CTX_ONE_STREAM;
     shim_check(gmapdp_create_ex(&shim_ctx, shim_device(), shim_mode, shim_user_open, shim_user_extend,
-                                shim_user_dynprog_p, GMAPDP_CTX_ONE_STREAM | wait |
+                                shim_user_dynprog_p, one | wait |
                                     (shim_qi != 1 ? GMAPDP_CTX_PRIO_HIGH : GMAPDP_CTX_PRIO_LOW)),
                "gmapdp_create_ex");
   }
