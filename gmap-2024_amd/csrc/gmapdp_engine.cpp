@@ -1537,6 +1537,7 @@ static int classify(gmapdp_ctx* ctx, PlanCore& plan) {
   }
   plan.pair_capacity = pair_off;
   plan.gdirs_bytes = gdirs_off;
+  tm.mark("lpt");
   return GMAPDP_OK;
 }
 
@@ -2993,7 +2994,10 @@ static int oligo_plan_build(gmapdp_ctx* ctx, const gmapdp_oligo_problem* problem
       P->ord.push_back(dev[i]);
       P->keys.push_back(kv.first);
     }
-  oligo_layout(P, slots, true, tcap, dcap, sizing);
+  // (a sizing run keeps no sequential-walk region -- ~70 % of its scratch, the difference between one launch
+  // and four for a 10 000-read block; a call that exhausts its chunk's event pool there reports overflow, and
+  // the re-layout gives it the diagonal arena's upper bound instead of a measured count)
+  oligo_layout(P, slots, !sizing, tcap, dcap, sizing);
   // (the kernels' mappings are relative to each problem's table_offset: the arena may pass 2^31 entries;
   // the public seeding API, whose mappings are absolute 32-bit indexes, checks its own total)
   (void)toff;
@@ -3018,7 +3022,7 @@ static hipError_t oligo_plan_relayout(gmapdp_ctx* ctx, gmapdp_oligo_plan* P, con
   for (int i = 0; i < n; i++) {
     const size_t tp = (size_t)std::max(ores[i].totalpositions, 0);
     tcap[i] = std::min<size_t>(oligo_table_cap(problems[i]), tp);
-    dcap[i] = (size_t)std::max(ores[i].ndiagonals, 0);
+    dcap[i] = ores[i].oned_matrix_p < 0 ? oligo_diag_cap(problems[i]) : (size_t)std::max(ores[i].ndiagonals, 0);
     slots[i] = 3 * tp;
     hcap[i] = (size_t)std::max(nhits[i], 0);
   }
@@ -4017,7 +4021,10 @@ int gmapdp_stage2_plan_create(gmapdp_ctx* ctx, const gmapdp_stage2_problem* prob
   }
   for (int i = 0; i < n; i++) {
     dp[i].scratch_offset = (int64_t)P->scratch;
-    P->scratch += scratch_bytes_s2c(problems[i].querylength, ores[i].totalpositions, ores[i].ndiagonals);
+    // (a call whose sizing run overflowed its event pool measured no diagonals: its arena's upper bound)
+    const int nd = ores[i].oned_matrix_p < 0 ? (int)std::min<size_t>(oligo_diag_cap(op[i]), INT32_MAX)
+                                             : ores[i].ndiagonals;
+    P->scratch += scratch_bytes_s2c(problems[i].querylength, ores[i].totalpositions, nd);
   }
   P->path_cap = 16 + 4 * (size_t)n;
   P->pair_cap = 64 + 3 * qsum;

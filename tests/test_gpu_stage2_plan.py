@@ -145,3 +145,21 @@ def test_gpu_stage2_plan_other_query_more_distinct_8mers(engine):
     keep = [i for i in range(len(calls)) if i not in shrink]
     bad = stage2_mismatches(res[keep], paths, pairs, exp, index=keep)
     assert not bad, bad[:8]
+
+
+def test_gpu_stage2_plan_sizing_pool_overflow(engine, monkeypatch):
+    """A stage-2 plan's sizing run keeps no sequential-walk region; a call that exhausts its chunk's event pool
+    there (forced here with GMAPDP_OLIGO_POOL_SLOTS) reports overflow in the sizing run only: the re-layout
+    gives it the diagonal arena's upper bound and chaining scratch sized from it, the plan's own runs have an
+    exact pool, and every call equals the oracle."""
+    g, calls = _repeat_calls(seed=13, reps=(20000, 0, 30000, 0))
+    engine.set_genome(g)
+    orc = Oracle()
+    orc.set_genome(g)
+    probs, qb, qub = gmapdp.Engine.build_stage2_batch(calls)
+    exp = oracle_stage2_batch(orc, probs, qb, qub)
+    monkeypatch.setenv("GMAPDP_OLIGO_POOL_SLOTS", "30000")
+    res, paths, pairs, _ = engine.stage2_plan_raw(probs, qb, qub)
+    assert np.all(res["status"] >= 0), res["status"]
+    bad = stage2_mismatches(res, paths, pairs, exp)
+    assert not bad, bad[:8]
