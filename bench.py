@@ -1185,6 +1185,10 @@ def main():
                      "int_ops": {"cells_per_launch": kcells, "ops_per_cell": OPS_PER_CELL,
                                  "frac": OPS_PER_CELL * kcells / (INT_OPS_PEAK * kms * 1e-3) if kcells else None,
                                  "peak_ops_per_s": INT_OPS_PEAK,
+                                 # issued lanes (VALU wave-instructions x 64) per algorithmic
+                                 # int op of the launch -- the instruction overhead the issue fraction hides
+                                 "lane_slots_per_op": 64.0 * valu / (OPS_PER_CELL * kcells) if valu and kcells
+                                 else None,
                                  "note": "genome-gap fills counted only where genome_gap_simple did not answer"},
                      "note": "integer VALU/LDS/latency-bound DP and a serial stage-2 sweep (SURVEY §8d); the HBM "
                              "roofline is reported as required, the VALU issue fraction (and for DP fills the "
