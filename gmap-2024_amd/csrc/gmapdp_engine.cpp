@@ -11,6 +11,7 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <time.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <climits>
@@ -19,6 +20,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <condition_variable>
 #include <mutex>
 #include <thread>
 #include <atomic>
@@ -298,6 +300,7 @@ struct gmapdp_ctx {
   DevBuf din, dout;    // run_batch: all inputs / all outputs of one synchronous batch
   HostBuf hin, hout;   // their pinned host images
   HostBuf hplan;       // a plan's descriptor upload (gmapdp_plan_create_all), staged pinned
+  hipEvent_t ev_hplan = nullptr;  // the last upload from hplan (its copies may still be in flight)
   DevBuf gprobs, gorder, sprob, gresults;
   DevBuf cprobs, corder, cresults, cscratch;  // Dynprog_cdna_gap batches
   DevBuf sjprobs, sjorder, sjresults, sjseq, sjdirs;  // Dynprog_end5/3_splicejunction batches
@@ -330,6 +333,54 @@ static hipError_t ctx_sync(gmapdp_ctx* ctx, hipStream_t s) {
   }
 }
 
+// Large host mappings (transparent huge pages requested), recycled: get() hands out a free mapping of the
+// size rounded up to 2 MB (the smallest that fits, if within 2x), else maps a new one; put() keeps it while
+// the free ones total at most kKeep.  Process-wide, one mutex (a few calls per plan pass).
+struct HugeCache {
+  static constexpr size_t kKeep = size_t(2) << 30;
+  std::mutex m;
+  std::map<void*, size_t> live;              // mapping -> its size
+  std::multimap<size_t, void*> free_by_size;
+  size_t free_bytes = 0;
+  void* get(size_t b) {
+    b = (b + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
+    {
+      std::lock_guard<std::mutex> lk(m);
+      auto it = free_by_size.lower_bound(b);
+      if (it != free_by_size.end() && it->first <= 2 * b) {
+        void* p = it->second;
+        free_bytes -= it->first;
+        free_by_size.erase(it);
+        return p;
+      }
+    }
+    void* p = mmap(nullptr, b, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p == MAP_FAILED) throw std::bad_alloc();
+    (void)madvise(p, b, MADV_HUGEPAGE);
+    std::lock_guard<std::mutex> lk(m);
+    live[p] = b;
+    return p;
+  }
+  void put(void* p) {
+    std::unique_lock<std::mutex> lk(m);
+    auto it = live.find(p);
+    if (it == live.end()) return;
+    const size_t b = it->second;
+    if (free_bytes + b <= kKeep) {
+      free_by_size.emplace(b, p);
+      free_bytes += b;
+      return;
+    }
+    live.erase(it);
+    lk.unlock();
+    munmap(p, b);
+  }
+};
+static HugeCache& huge_cache() {
+  static HugeCache* c = new HugeCache();  // never destroyed: arrays may be freed at process exit
+  return *c;
+}
+
 // Host arrays a plan build fills completely: resize() leaves them uninitialised (zero-filling ~200 MB of
 // descriptors for a 10 000-read block on one thread cost more than building them on 16).
 template <typename T>
@@ -344,19 +395,19 @@ struct NoInitAlloc : std::allocator<T> {
   // Large arrays (a 10 000-read block's descriptors: tens of MB each) come from their own mapping with
   // transparent huge pages requested, so that their first touch costs a fault per 2 MB rather than per
   // 4 KB page (the plan builders' passes were fault-bound on the GPU box).
+  // A freed mapping is kept for the next plan's arrays (HugeCache): a block's plans free and re-create the
+  // same ~300 MB of temporaries, and unmapping them (page frees, TLB shoot-downs across the plan's threads)
+  // then faulting them in again cost milliseconds per plan.
   static constexpr size_t kHuge = size_t(4) << 20;
   T* allocate(size_t n) {
     const size_t b = n * sizeof(T);
     if (b < kHuge) return std::allocator<T>::allocate(n);
-    void* p = mmap(nullptr, b, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-    if (p == MAP_FAILED) throw std::bad_alloc();
-    (void)madvise(p, b, MADV_HUGEPAGE);
-    return static_cast<T*>(p);
+    return static_cast<T*>(huge_cache().get(b));
   }
   void deallocate(T* p, size_t n) {
     const size_t b = n * sizeof(T);
     if (b < kHuge) std::allocator<T>::deallocate(p, n);
-    else munmap(p, b);
+    else huge_cache().put(p);
   }
   template <typename U>
   void construct(U* p) noexcept {
@@ -502,6 +553,10 @@ void gmapdp_destroy(gmapdp_ctx* ctx) {
   }
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_block) (void)hipEventDestroy(ctx->ev_block);
+  if (ctx->ev_hplan) {
+    (void)hipEventSynchronize(ctx->ev_hplan);
+    (void)hipEventDestroy(ctx->ev_hplan);
+  }
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx->tables;
   delete ctx;
@@ -1103,7 +1158,8 @@ struct PlanTimer {
   ~PlanTimer() {
     if (!on) return;
     size_t fr = 0, tot = 0;
-    (void)hipMemGetInfo(&fr, &tot);
+    // (=2: with the device's free memory; hipMemGetInfo takes milliseconds, so phase times are without it)
+    if (std::atoi(getenv("GMAPDP_PLAN_TIMING")) >= 2) (void)hipMemGetInfo(&fr, &tot);
     std::fprintf(stderr, "[gmapdp plan timing] %s%s (device free %.1f of %.1f GB)\n", what, line.c_str(), fr * 1e-9,
                  tot * 1e-9);
   }
@@ -1125,6 +1181,69 @@ static int plan_threads(size_t n) {
   }();
   return n >= kPlanParallelMin ? v : 1;
 }
+// The plan's worker threads, started once per process: a block's plans run ~15 parallel passes, and
+// starting and joining 15 threads per pass cost milliseconds of a ~20-ms plan.  One caller at a time (a
+// second concurrent caller, or a forked child, starts its own threads as before); workers sleep on a
+// condition variable between passes.  Never destroyed: the threads end with the process.
+struct PlanPool {
+  std::mutex use;  // held by the pass being run
+  std::mutex m;
+  std::condition_variable cv;
+  uint64_t gen = 0;
+  int nchunks = 0;
+  void (*call)(void*, int) = nullptr;
+  void* arg = nullptr;
+  std::atomic<int> left{0};
+  int nthreads = 0;
+  pid_t pid = 0;
+  void start(int n) {
+    pid = getpid();
+    nthreads = n;
+    for (int i = 1; i <= n; i++)
+      std::thread([this, i] {
+        uint64_t seen = 0;
+        for (;;) {
+          std::unique_lock<std::mutex> lk(m);
+          cv.wait(lk, [&] { return gen != seen; });
+          seen = gen;
+          const bool mine = i < nchunks;
+          void (*c)(void*, int) = call;
+          void* a = arg;
+          lk.unlock();
+          if (mine) {
+            c(a, i);
+            left.fetch_sub(1, std::memory_order_acq_rel);
+          }
+        }
+      }).detach();
+  }
+  // chunks 1..T-1 on the workers, chunk 0 on the caller; false: pool unavailable (caller spawns threads)
+  template <typename G>
+  bool run(int T, G& g) {
+    if (T - 1 > nthreads || getpid() != pid || !use.try_lock()) return false;
+    {
+      std::lock_guard<std::mutex> lk(m);
+      nchunks = T;
+      call = [](void* a, int t) { (*static_cast<G*>(a))(t); };
+      arg = &g;
+      left.store(T - 1, std::memory_order_release);
+      gen++;
+    }
+    cv.notify_all();
+    g(0);
+    while (left.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+    use.unlock();
+    return true;
+  }
+};
+static PlanPool* plan_pool(int T) {
+  static PlanPool* p = [T] {
+    PlanPool* q = new PlanPool();
+    q->start(std::max(T, plan_threads(kPlanParallelMin)) - 1);
+    return q;
+  }();
+  return p;
+}
 // f(begin, end, t) over T contiguous chunks of [0, n), chunk 0 on the calling thread
 template <typename F>
 static void plan_parallel(size_t n, int T, F&& f) {
@@ -1133,12 +1252,14 @@ static void plan_parallel(size_t n, int T, F&& f) {
     return;
   }
   const size_t per = (n + (size_t)T - 1) / (size_t)T;
-  std::vector<std::thread> th;
-  for (int t = 1; t < T; t++) {
+  auto chunk = [&](int t) {
     const size_t lo = (size_t)t * per, hi = std::min(n, lo + per);
-    if (lo < hi) th.emplace_back([&f, lo, hi, t] { f(lo, hi, t); });
-  }
-  f((size_t)0, std::min(n, per), 0);
+    if (lo < hi) f(lo, hi, t);
+  };
+  if (plan_pool(T)->run(T, chunk)) return;
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; t++) th.emplace_back([&chunk, t] { chunk(t); });
+  chunk(0);
   for (auto& x : th) x.join();
 }
 // ids ordered longest first by key(id): a stable counting sort on the key quantised to 16 steps per
@@ -2378,11 +2499,27 @@ struct gmapdp_plan {
   gmapdp_genome_result* d_gresults = nullptr;
   const double* d_metab = nullptr;            // gmapdp_plan_bind_genome_maxent: each genome-gap class fills d_sprob
   void* d_base = nullptr;                     // one allocation holding d_probs, d_order, d_gprobs, d_gorder
+  // the descriptors' upload, left in flight by gmapdp_plan_create_all (it overlaps the caller's next host
+  // work: the stage-2 plan's build); the plan's first run waits for it
+  hipEvent_t ev_up = nullptr;
+  mutable std::atomic<bool> up_done{false};
 };
 
 static void plan_free(gmapdp_plan* p) {
+  if (p->ev_up) {
+    (void)hipEventSynchronize(p->ev_up);
+    (void)hipEventDestroy(p->ev_up);
+  }
   if (p->d_base) (void)hipFree(p->d_base);
   delete p;
+}
+
+// before a plan's descriptors are read on any stream
+static hipError_t plan_uploaded(const gmapdp_plan* p) {
+  if (!p->ev_up || p->up_done.load(std::memory_order_acquire)) return hipSuccess;
+  const hipError_t e = hipEventSynchronize(p->ev_up);
+  if (e == hipSuccess) p->up_done.store(true, std::memory_order_release);
+  return e;
 }
 
 static RunArgs plan_args(const gmapdp_plan* plan, const char* d_qseq, const char* d_qseq_uc, gmapdp_result* d_results,
@@ -2442,6 +2579,7 @@ int gmapdp_plan_create_all(gmapdp_ctx* ctx, const gmapdp_single_problem* singles
     p->d_gprobs = (DevGenomeProblem*)(b + o2);
     p->d_gorder = (int*)(b + o3);
   }
+  tm.mark("alloc");
   // the four descriptor arrays (~115 MB for a 10 000-read block) copied into one pinned image on the plan's
   // threads, then moved with asynchronous copies (a pageable hipMemcpy stages through the runtime's own
   // buffers on one thread)
@@ -2459,16 +2597,24 @@ int gmapdp_plan_create_all(gmapdp_ctx* ctx, const gmapdp_single_problem* singles
       x.at = tot;
       tot = align_up(tot + x.n, 256);
     }
+    // (the previous plan's copies out of hplan first)
+    if (e == hipSuccess && ctx->ev_hplan) e = hipEventSynchronize(ctx->ev_hplan);
     if (e == hipSuccess) e = ctx->hplan.ensure(std::max<size_t>(tot, 256));
     unsigned char* h = (unsigned char*)ctx->hplan.p;
-    for (Part& x : parts) {
-      if (e != hipSuccess || !x.n) continue;
-      plan_parallel(x.n, plan_threads(x.n / 64), [&](size_t lo, size_t hi, int) {
-        std::memcpy(h + x.at + lo, (const unsigned char*)x.src + lo, hi - lo);
-      });
-      e = hipMemcpyAsync(x.dst, h + x.at, x.n, hipMemcpyHostToDevice, ctx->stream);
-    }
-    if (e == hipSuccess) e = ctx_sync(ctx, ctx->stream);
+    // in 8-MB pieces, so that each piece's DMA runs while the threads fill the next
+    constexpr size_t kPiece = size_t(8) << 20;
+    for (Part& x : parts)
+      for (size_t o = 0; e == hipSuccess && o < x.n; o += kPiece) {
+        const size_t m = std::min(kPiece, x.n - o);
+        plan_parallel(m, plan_threads(m / 64), [&](size_t lo, size_t hi, int) {
+          std::memcpy(h + x.at + o + lo, (const unsigned char*)x.src + o + lo, hi - lo);
+        });
+        e = hipMemcpyAsync((unsigned char*)x.dst + o, h + x.at + o, m, hipMemcpyHostToDevice, ctx->stream);
+      }
+    if (e == hipSuccess && !ctx->ev_hplan) e = hipEventCreateWithFlags(&ctx->ev_hplan, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&p->ev_up, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(ctx->ev_hplan, ctx->stream);
+    if (e == hipSuccess) e = hipEventRecord(p->ev_up, ctx->stream);
   }
   if (e == hipSuccess && p->in.gdirs_bytes) e = ctx->gdirs.ensure(p->in.gdirs_bytes);
   tm.mark("upload");
@@ -2562,6 +2708,7 @@ int gmapdp_plan_run(gmapdp_ctx* ctx, const gmapdp_plan* plan, const char* d_qseq
   if (!ctx || !plan) return GMAPDP_EINVAL;
   if (!ctx->d_genome) return GMAPDP_ENOGENOME;
   if (!plan->in.gdev.empty() && (!plan->d_sprob || !plan->d_gresults)) return bad(ctx, "genome-gap buffers not bound");
+  if (const hipError_t eu = plan_uploaded(plan)) return fail(ctx, GMAPDP_ELAUNCH, "plan upload: %s", eu);
   return run_plan(ctx, plan->in, plan_args(plan, d_qseq, d_qseq_uc, d_results, d_pairs),
                   stream ? (hipStream_t)stream : ctx->stream);
 }
@@ -2575,6 +2722,7 @@ static int plan_run_launch(gmapdp_ctx* ctx, const gmapdp_plan* plan, int li, con
     hipError_t e = ctx->gdirs.ensure(plan->in.gdirs_bytes);
     if (e != hipSuccess) return fail(ctx, GMAPDP_ENOMEM, "direction scratch: %s", e);
   }
+  if (const hipError_t eu = plan_uploaded(plan)) return fail(ctx, GMAPDP_ELAUNCH, "plan upload: %s", eu);
   hipError_t e = launch_one(ctx, plan->in, li, plan_args(plan, d_qseq, d_qseq_uc, d_results, d_pairs),
                             stream ? (hipStream_t)stream : ctx->stream, prologue);
   if (e != hipSuccess) return fail(ctx, GMAPDP_ELAUNCH, "dp launch: %s", e);
