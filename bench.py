@@ -102,6 +102,7 @@ def genome_algorithmic_bytes(gp, npairs, sprob_arena=False):
 
 S2_SEED = "gmapdp::oi_kernel+gmapdp::oi_map_kernel"  # the seeding (Oligoindex_hr_tally + get_mappings)
 # stage-2 kernels timed alone: gmapdp_stage2_plan_run's `what` (1 seeding, 4 s2a, 8 s2b, 16 s2c)
+CHAIN_FUSED = "chaining_fused"  # s2a + s2b + s2c against the fused operation's bytes
 S2_WHAT = {S2_SEED: 1, "gmapdp::s2a_kernel": 4, "gmapdp::s2b_kernel": 8, "gmapdp::s2c_kernel": 16}
 
 
@@ -115,7 +116,10 @@ def stage2_algorithmic_bytes(op, ores, s2res):
       s2b:     per-position metadata 20 ql + the chrpos of every hit 4 T + one 36-B link per query position (the
                chain; a lower bound: the sweep scores every hit in the active ranges)
       s2c:     the score array 4 T + the kept paths' walk (32 B per pair) + 20-B pair records + 16-B path records
-               + the query twice 2 ql + result 32"""
+               + the query twice 2 ql + result 32
+      chaining (the three as one fused operation, no intermediates): what the seeding hands over (descriptor
+               48 + 32, npositions / mappings 8 ql, table 4 T, diagonals 16 nd) + the query twice 2 ql, and the
+               outputs (20-B pair records, 16-B path records, result 32)"""
     ql = op["querylength"].astype(np.int64)
     T = np.maximum(ores["totalpositions"].astype(np.int64), 0)
     nd = np.maximum(ores["ndiagonals"].astype(np.int64), 0)
@@ -124,7 +128,9 @@ def stage2_algorithmic_bytes(op, ores, s2res):
     return {S2_SEED: int((48 + ql + 12 * ((W + 16 + 31) // 32) + 8 * ql + 4 * T + 32 + 16 * nd).sum()),
             "gmapdp::s2a_kernel": int((80 + 8 * ql + 16 * nd + 4 * T + 8 * T + 24 * ql + 32).sum()),
             "gmapdp::s2b_kernel": int((20 * ql + 4 * T + 36 * ql).sum()),
-            "gmapdp::s2c_kernel": int((4 * T + 2 * ql + 32).sum()) + 52 * npairs + 16 * int(s2res["nresults"].sum())}
+            "gmapdp::s2c_kernel": int((4 * T + 2 * ql + 32).sum()) + 52 * npairs + 16 * int(s2res["nresults"].sum()),
+            CHAIN_FUSED: int((80 + 8 * ql + 4 * T + 16 * nd + 2 * ql + 32).sum()) + 20 * npairs
+            + 16 * int(s2res["nresults"].sum())}
 
 
 def workload_id(args):
@@ -587,6 +593,18 @@ def main():
     # (=2: only the seeding launch on a high-priority stream, the chaining back on a normal one)
     ostream = torch.cuda.Stream(dev, priority=-1) if s2prio == 1 else torch.cuda.Stream(dev)
     sstream = torch.cuda.Stream(dev, priority=-1) if s2prio == 2 else ostream
+    # The timed steps as a deployment streams blocks (GMAPDP_BENCH_PIPE, default 3): the stage-2 chains (on
+    # their stream) and the DP classes (forked from and joined into `stream`) run as two pipelines over the
+    # blocks -- a block's chain starts when the previous block's chain ends, not when its DP classes end, and
+    # the next block's DP classes do not wait for this block's sweep tail.  The two share no buffer (plans,
+    # result and pair arenas are per pipeline), every block's work completes inside the timed region, and the
+    # line reports the serialised step beside it (step_split_ms.together_serial).  0 = serialised steps (each
+    # joins its chain); 1 = chains not joined but still forked from `stream`; 2 = 1 with consecutive chains on
+    # two streams (measured slower: DESIGN.md §7).
+    pipe = int(os.environ.get("GMAPDP_BENCH_PIPE", "3"))
+    ostream2 = torch.cuda.Stream(dev) if pipe == 2 else None
+    d_s2res2 = torch.zeros(args.reads * 32, dtype=torch.uint8, device=dev) if pipe == 2 else None
+    nstep = [0]
     side_of = lambda k: min(k, len(sides))  # noqa: E731  plan stream k >= 1 -> side index + 1
 
     def launch(b, li, s, kernel_only=False):
@@ -602,12 +620,13 @@ def main():
     # plans' sizing runs launch under other names and count nowhere)
     block_runs = {k: 0 for k in S2_WHAT}
 
-    def orun(b, s, what):
+    def orun(b, s, what, res=None):
         for k, w in S2_WHAT.items():
             if what & w or (what & 2 and w > 1):
                 block_runs[k] += 1
+        res = d_s2res if res is None else res
         eng._check(lib.gmapdp_stage2_plan_run(eng.h, b["oplan"], C.c_void_p(b["d_oq"].data_ptr()),
-                                              C.c_void_p(b["d_oq"].data_ptr()), C.c_void_p(d_s2res.data_ptr()),
+                                              C.c_void_p(b["d_oq"].data_ptr()), C.c_void_p(res.data_ptr()),
                                               what, C.c_void_p(s.cuda_stream)), "gmapdp_stage2_plan_run")
 
     def mrun(b, s, what):
@@ -616,30 +635,34 @@ def main():
                                                  C.c_void_p(d_mres.data_ptr()), C.c_void_p(d_mpairs.data_ptr()),
                                                  what, C.c_void_p(s.cuda_stream)), "gmapdp_microexon_plan_run")
 
-    def step(b, do_oligo=True, do_dp=True, ev=None):
+    def step(b, do_oligo=True, do_dp=True, ev=None, piped=False):
         do_oligo = do_oligo and b["oplan"] is not None
         fork = torch.cuda.Event()
         fork.record(stream)
         used = set()
+        alt = piped and pipe == 2 and nstep[0] % 2 == 1
+        nstep[0] += 1
+        os_, ss_, res = (ostream2, ostream2, d_s2res2) if alt else (ostream, sstream, None)
         if do_oligo:
-            sstream.wait_event(fork)
+            if not (piped and pipe == 3):
+                ss_.wait_event(fork)
             if ev is not None:
-                ev["oligo"][0].record(sstream)
-            orun(b, sstream, 1)
+                ev["oligo"][0].record(ss_)
+            orun(b, ss_, 1, res)
             if ev is not None:
-                ev["oligo"][1].record(sstream)
-            if sstream is not ostream:
-                ostream.wait_stream(sstream)
+                ev["oligo"][1].record(ss_)
+            if ss_ is not os_:
+                os_.wait_stream(ss_)
             # the chaining as its three kernels (what 4 / 8 / 16: s2a, the s2b sweep, s2c), events between
-            orun(b, ostream, 4)
+            orun(b, os_, 4, res)
             if ev is not None:
-                ev["s2a"].record(ostream)
-            orun(b, ostream, 8)
+                ev["s2a"].record(os_)
+            orun(b, os_, 8, res)
             if ev is not None:
-                ev["s2b"].record(ostream)
-            orun(b, ostream, 16)
+                ev["s2b"].record(os_)
+            orun(b, os_, 16, res)
             if ev is not None:
-                ev["chain"][1].record(ostream)
+                ev["chain"][1].record(os_)
         if do_dp:
             for li in range(len(b["names"])):
                 k = side_of(b["lstream"][li])
@@ -664,7 +687,7 @@ def main():
                 ev["mx"][1].record(ms)
         for k in used:
             stream.wait_stream(sides[k - 1])
-        if do_oligo:
+        if do_oligo and not (piped and pipe):
             stream.wait_stream(ostream)
 
     mk = lambda: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))  # noqa: E731
@@ -754,6 +777,8 @@ def main():
 
 
     def timed(steps, warmup, **kw):
+        if not kw:  # the whole step (not a leg alone): GMAPDP_BENCH_PIPE applies
+            kw = {"piped": True}
         with torch.cuda.stream(stream):
             for k in range(warmup):
                 step(B[k % len(B)], **kw)
@@ -818,6 +843,7 @@ def main():
     progress("timing %d steps over %d blocks" % (args.steps, len(B)))
     elapsed, evs = timed(args.steps, args.warmup)
     progress("headline %.2f ms per step" % (elapsed / args.steps * 1e3))
+    el_serial, _ = timed(args.steps, 1, piped=False)
     half = max(2, args.steps // 4)
     el_dp, _ = timed(half, 1, do_oligo=False)
     has_s2 = all(b["oplan"] is not None for b in B)
@@ -920,6 +946,19 @@ def main():
                                               key=lambda n: per_kernel[n][0], default=None)]
               if n and n != dominant and n in per_kernel]
     roofline_others = [kernel_roofline(n, 1) for n in others]
+    # the chaining as one operation: its three kernels' traffic and time against the bytes
+    # a fused chaining would move (no s2a -> s2b -> s2c intermediates)
+    chain = {r["kernel"]: r for r in roofline_others if r["kernel"] in ("gmapdp::s2a_kernel", "gmapdp::s2b_kernel",
+                                                                      "gmapdp::s2c_kernel")}
+    chaining_fused = None
+    if len(chain) == 3 and all("s2bytes" in bb for bb in B):
+        fb = float(np.mean([bb["s2bytes"][CHAIN_FUSED] for bb in B]))
+        tr = [r["traffic"] for r in chain.values()]
+        ms3 = sum(r["ms_per_launch"] for r in chain.values())
+        chaining_fused = {"kernels": sorted(chain), "ms_alone_per_block": ms3, "fused_algorithmic_bytes_per_block": fb,
+                          "traffic_per_block": sum(tr) if all(t is not None for t in tr) else None,
+                          "traffic_over_fused": sum(tr) / fb if all(t is not None for t in tr) and fb else None,
+                          "achieved_fused": fb / (ms3 * 1e-3) / 1e9, "frac_fused": fb / (ms3 * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
     # ---- PCIe: one block's inputs up and outputs down through pinned host memory (outside the step) ----
     b = B[0]
@@ -1200,11 +1239,13 @@ def main():
                              "roofline is reported as required, the VALU issue fraction (and for DP fills the "
                              "algorithmic int-op fraction) are the binding bounds (BASELINE.md §3(i))"},
         "roofline_other_kernels": roofline_others,
+        "chaining_fused": chaining_fused,
         "gcups": cells_total / len(B) * world * args.steps / elapsed / 1e9,
         "step_split_ms": {"stage2_alone": el_o / half * 1e3 if el_o is not None else None,
                           "stage2_alone_seeding": s2_seed_ms,
                           "stage2_alone_chaining": s2_chain_ms, "dynprog_alone": el_dp / half * 1e3,
-                          "together": ms_step},
+                          "together": ms_step, "together_serial": el_serial / args.steps * 1e3,
+                          "pipelined_blocks": pipe},
         "block_runs": dict(block_runs),
         "launch_classes": sorted(({"kernel": n, "dispatches": e[1], "ms_per_step": round(e[0] / args.steps, 4)}
                                   for n, e in per_kernel.items()), key=lambda x: -x["ms_per_step"]),
