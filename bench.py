@@ -22,7 +22,9 @@ Read stream: blocks of --reads reads, each generated from its own seeds; rank r 
 b % N == r (GMAP's --part=r/N rule, inbuffer.c:283, per block) and cycles through --batches of them, so
 consecutive steps process different reads and genomic windows (a stream, not one warm replay).  One step
 = one pass of the engine over every call of one block (Stage2_compute on its own stream, the DP launch
-classes on three more, joined at the end of the step).  Inputs (descriptors, query arenas, splice
+classes on three more).  The timed steps stream the blocks as two pipelines, the stage-2 chains and the DP
+classes, each block's work complete inside the timed region (GMAPDP_BENCH_PIPE=0: each step joined at its
+end; its time is reported beside the headline as step_split_ms.together_serial).  Inputs (descriptors, query arenas, splice
 probabilities) are resident in HBM before the timed region (the contract's `value`); the host plans
 (bands, launch classes) are made once per block and their cost is reported as plan_ms.
 
