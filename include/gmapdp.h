@@ -771,8 +771,10 @@ size_t gmapdp_end_pair_capacity (const gmapdp_end_problem *problems, int n);
 /* Device-resident path for pipelined callers and throughput measurement.
  * gmapdp_plan_single resolves penalties, bands and launch classes once on
  * the host (problems resolved on the host -- the size guard -- are written
- * to host_results immediately) and uploads the descriptors.
- * gmapdp_plan_run then launches asynchronously on `stream` (a hipStream_t;
+ * to host_results immediately) and uploads the descriptors.  The upload
+ * may still be in flight when the create call returns (the host goes on to
+ * its next work); the plan's first run waits for it, so nothing changes for
+ * the caller.  gmapdp_plan_run then launches asynchronously on `stream` (a hipStream_t;
  * NULL = the context's stream) against device-resident query arenas; GPU
  * results land in d_results[gmapdp_plan_dev_index(plan, i)] and pairs in
  * d_pairs (capacity gmapdp_plan_pair_capacity). */
