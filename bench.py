@@ -593,8 +593,10 @@ def main():
     # stage 2 (the step's longest chain) may take the high-priority queue: GMAPDP_BENCH_S2_PRIORITY=1
     s2prio = int(os.environ.get("GMAPDP_BENCH_S2_PRIORITY", "0"))
     # (=2: only the seeding launch on a high-priority stream, the chaining back on a normal one)
-    ostream = torch.cuda.Stream(dev, priority=-1) if s2prio == 1 else torch.cuda.Stream(dev)
-    sstream = torch.cuda.Stream(dev, priority=-1) if s2prio == 2 else ostream
+    # (=3: the chaining kernels there, the seeding on a normal-priority stream of its own)
+    ostream = torch.cuda.Stream(dev, priority=-1) if s2prio in (1, 3) else torch.cuda.Stream(dev)
+    sstream = torch.cuda.Stream(dev, priority=-1) if s2prio == 2 else (torch.cuda.Stream(dev) if s2prio == 3
+                                                                       else ostream)
     # The timed steps as a deployment streams blocks (GMAPDP_BENCH_PIPE, default 3): the stage-2 chains (on
     # their stream) and the DP classes (forked from and joined into `stream`) run as two pipelines over the
     # blocks -- a block's chain starts when the previous block's chain ends, not when its DP classes end, and
