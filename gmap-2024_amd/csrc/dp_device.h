@@ -27,6 +27,10 @@ __device__ __forceinline__ int dpp_wave_shr1(int x, int fill) {
   // lane i <- lane i-1; lane 0 <- fill
   return __builtin_amdgcn_update_dpp(fill, x, 0x138, 0xf, 0xf, false);
 }
+// lane i <- lane i-1; lane 0 <- 0 (for values lane 0 never reads)
+__device__ __forceinline__ int dpp_wave_shr1_zero(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, 0x138, 0xf, 0xf, true);
+}
 
 // Inclusive max-scan over the 64 lanes (lane order).  Lanes without a source
 // read the identity INT_MIN, so the DPP move folds into v_max_i32_dpp.
@@ -364,7 +368,9 @@ struct PackedDirs {
   }
 };
 
-template <int R, bool CARRY, int S = 64, bool PK = (S < 64), bool STORE = false, bool DPK = false>
+// NB (whole-wave fills only): the band is narrower than the wave's 64 R elements, so the last lane's last
+// element is never a valid cell and the E / H values shifted into it need no -infinity default.
+template <int R, bool CARRY, int S = 64, bool PK = (S < 64), bool STORE = false, bool DPK = false, bool NB = false>
 __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lband, int uband, int open, int ext,
                                           int late, int track, const int8_t* sc, int srow, const uint8_t* gcl,
                                           uint64_t* dirs, const BridgeCarry* bc_, int& bestr, int& bestc,
@@ -372,6 +378,7 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
   static_assert(S == 64 || (R == 1 && !CARRY), "segmented fills are single-word, no bridge carry");
   static_assert(!STORE || S == 64, "score matrices are stored by whole-wave fills only");
   static_assert(!DPK || (R == 1 && S == 64), "packed direction words: one-word bands");
+  static_assert(!NB || S == 64, "narrow-band shifts: whole-wave fills");
   const int lk = (S == 64) ? lane : (lane & (S - 1));  // lane within the segment
   const int cend = (S == 64) ? glen : gmax;
   const int sat = kNegInf32;
@@ -403,6 +410,14 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
     cc[i] = 0;
     cp[i] = 0.0;
   }
+  // The genome-gap fills (CARRY: packed score rows in LDS) keep the row clamp and the table's LDS address in
+  // VGPRs: as scalars they were among the kernel's spilled SGPRs, reloaded by v_readlane every column.
+  int rlen1 = rlen + 1;
+  uint32_t scb = 0;
+  if constexpr (CARRY && PK) {
+    scb = (uint32_t)(size_t)(const __attribute__((address_space(3))) int32_t*)reinterpret_cast<const int32_t*>(sc);
+    asm volatile("" : "+v"(rlen1), "+v"(scb));
+  }
   int rtop_ext = -uband * ext;  // (c - uband) * ext, advanced by ext per column
   int oce = open;               // open + c * ext
   int gi_next = (S == 64) ? 0 : gcl[min(1, glen)];
@@ -431,8 +446,13 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
     int Ein[R], Hin[R];
 #pragma unroll
     for (int i = 0; i < R - 1; i++) { Ein[i] = E[i + 1]; Hin[i] = Hs[i + 1]; }
-    Ein[R - 1] = seg_shl1<S>(E[0], kNegInf32, lk);
-    Hin[R - 1] = seg_shl1<S>(Hs[0], kNegInf32, lk);
+    if constexpr (NB) {  // (lane 63's element R-1 lies outside the band: whatever arrives there is unread)
+      Ein[R - 1] = dpp_wave_shl1_zero(E[0]);
+      Hin[R - 1] = dpp_wave_shl1_zero(Hs[0]);
+    } else {
+      Ein[R - 1] = seg_shl1<S>(E[0], kNegInf32, lk);
+      Hin[R - 1] = seg_shl1<S>(Hs[0], kNegInf32, lk);
+    }
 
     int Hp[R], En[R], A[R];
     bool valid[R], eb[R], hb[R];
@@ -441,9 +461,13 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
       const int k = lk * R + i;
       const int r = rtop + k;
       valid[i] = (k < W) & (r >= rlo) & (r <= rhigh) & colact;
-      const int rr = min(max(r, 0), rlen + 1);
+      // (rows outside [0, rlen + 1] are invalid cells: unsigned, a negative row clamps to rlen + 1)
+      const int rr = (int)min((unsigned)r, (unsigned)rlen1);
       int s;
       if constexpr (!PK) s = scg[rr];
+      else if constexpr (CARRY)
+        s = __builtin_amdgcn_sbfe(*(const __attribute__((address_space(3))) int32_t*)(size_t)(scb + 4u * (uint32_t)rr),
+                                  gi4, 4);
       else s = __builtin_amdgcn_sbfe(reinterpret_cast<const int32_t*>(sc)[rr], gi4, 4);
       // Egap (dynprog.c:1518-1524)
       const int es = Hin[i] + open;
@@ -470,9 +494,17 @@ __device__ __forceinline__ void fill_band(int lane, int rlen, int glen, int lban
       vb[i] = F[i] > Hp[i] - late;
       Hun[i] = max(F[i], Hp[i]);
     }
-    // Fgap direction needs F(r-1), H(r-1) of this column (dynprog.c:1486-1492)
-    const int Fup = seg_shr1<S>(F[R - 1], kNegInf32, lk);
-    const int Hup = seg_shr1<S>(Hun[R - 1], kNegInf32, lk);
+    // Fgap direction needs F(r-1), H(r-1) of this column (dynprog.c:1486-1492).  Lane 0's element 0 reads
+    // them only when valid, and then it is the column's top row (r = rtop = rlo), which takes the constants
+    // below instead: a whole-wave fill shifts in zeros there (one DPP move, no default copied in first).
+    int Fup, Hup;
+    if constexpr (S == 64) {
+      Fup = dpp_wave_shr1_zero(F[R - 1]);
+      Hup = dpp_wave_shr1_zero(Hun[R - 1]);
+    } else {
+      Fup = seg_shr1<S>(F[R - 1], kNegInf32, lk);
+      Hup = seg_shr1<S>(Hun[R - 1], kNegInf32, lk);
+    }
     uint64_t mH[R], mV[R], mE[R], mF[R];
 #pragma unroll
     for (int i = 0; i < R; i++) {

@@ -891,14 +891,26 @@ __global__ __launch_bounds__(128) GGX_ATTR void gg_kernel(
   const int rdist = P.rev_goffsetR - P.goffsetL;  // "cR < rightoffset - leftoffset - cL"
   {
     int br, bc;
+    // (a band narrower than the wave's 64 R elements -- every bench genome gap: 37 -- takes the narrow-band
+    // shifts; a wave-uniform choice per fill)
     if (wave == 0) {
       const BridgeCarry B{ldi, rdi, pL, pR, isc, rdist, partB, diagR};
-      fill_band<R, true, 64, true, false, DPK>(lane, rlen, gR, lband, ubandR, P.open, P.extend, 1 - late, 0,
-                                               reinterpret_cast<const int8_t*>(scR), 0, gclR, dirsR, &B, br, bc);
+      if (WR < 64 * R)
+        fill_band<R, true, 64, true, false, DPK, true>(lane, rlen, gR, lband, ubandR, P.open, P.extend, 1 - late, 0,
+                                                       reinterpret_cast<const int8_t*>(scR), 0, gclR, dirsR, &B, br,
+                                                       bc);
+      else
+        fill_band<R, true, 64, true, false, DPK>(lane, rlen, gR, lband, ubandR, P.open, P.extend, 1 - late, 0,
+                                                 reinterpret_cast<const int8_t*>(scR), 0, gclR, dirsR, &B, br, bc);
     } else {
       const BridgeCarry B{rdi, ldi, pR, pL, isc, rdist, partC, diagL};
-      fill_band<R, true, 64, true, false, DPK>(lane, rlen, gL, lband, ubandL, P.open, P.extend, late, 0,
-                                               reinterpret_cast<const int8_t*>(scL), 0, gclL, dirsL, &B, br, bc);
+      if (WL < 64 * R)
+        fill_band<R, true, 64, true, false, DPK, true>(lane, rlen, gL, lband, ubandL, P.open, P.extend, late, 0,
+                                                       reinterpret_cast<const int8_t*>(scL), 0, gclL, dirsL, &B, br,
+                                                       bc);
+      else
+        fill_band<R, true, 64, true, false, DPK>(lane, rlen, gL, lband, ubandL, P.open, P.extend, late, 0,
+                                                 reinterpret_cast<const int8_t*>(scL), 0, gclL, dirsL, &B, br, bc);
     }
   }
   __threadfence_block();
